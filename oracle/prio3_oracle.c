@@ -1,0 +1,1063 @@
+/*
+ * prio3_oracle.c -- CPU restatement of prio 0.16.2 Prio3 (VDAF draft-08) for the
+ * Janus helper preparation path.  TEST INFRASTRUCTURE ONLY: used by tests/, by
+ * __graft_entry__.smoke() as the checker and by bench.py's cpu_baseline leg.
+ * Parity with prio bytes is UNPINNED (see prio3_oracle.h); pinned sub-results are
+ * listed there and in DESIGN.md.
+ *
+ * Section references "[VDAF-08 §x]" are to draft-irtf-cfrg-vdaf-08; "[prio]" marks
+ * an implementation detail of prio 0.16.2 that is mirrored for cost fidelity
+ * (e.g. DFT-based wire interpolation in FlpGeneric::query, the measurement-share
+ * re-expansion in Prio3::prepare_next).
+ */
+#include "prio3_oracle.h"
+
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef unsigned __int128 u128;
+
+/* ------------------------------------------------------------------------------------ */
+/* Keccak-p[1600, n_r] and TurboSHAKE128 (RFC 9861)                                     */
+/* ------------------------------------------------------------------------------------ */
+static const uint64_t KRC[24] = {
+    0x0000000000000001ULL, 0x0000000000008082ULL, 0x800000000000808AULL,
+    0x8000000080008000ULL, 0x000000000000808BULL, 0x0000000080000001ULL,
+    0x8000000080008081ULL, 0x8000000000008009ULL, 0x000000000000008AULL,
+    0x0000000000000088ULL, 0x0000000080008009ULL, 0x000000008000000AULL,
+    0x000000008000808BULL, 0x800000000000008BULL, 0x8000000000008089ULL,
+    0x8000000000008003ULL, 0x8000000000008002ULL, 0x8000000000000080ULL,
+    0x000000000000800AULL, 0x800000008000000AULL, 0x8000000080008081ULL,
+    0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
+
+static inline uint64_t rol64(uint64_t x, int n) {
+  return (x << (n & 63)) | (x >> ((64 - n) & 63));
+}
+
+/* Lane-complementing-free reference-style loop, fully unrolled by the compiler
+ * (pi lane walk + rho offsets from the Keccak reference). */
+static const int PI_LANE[24] = {10, 7,  11, 17, 18, 3, 5,  16, 8,  21, 24, 4,
+                                15, 23, 19, 13, 12, 2, 20, 14, 22, 9,  6,  1};
+static const int RHO_OFF[24] = {1,  3,  6,  10, 15, 21, 28, 36, 45, 55, 2,  14,
+                                27, 41, 56, 8,  25, 43, 62, 18, 39, 61, 20, 44};
+
+void orc_keccak_p1600(uint64_t st[25], int rounds) {
+  uint64_t bc[5], t;
+  for (int ir = 24 - rounds; ir < 24; ir++) {
+#pragma GCC unroll 5
+    for (int i = 0; i < 5; i++) bc[i] = st[i] ^ st[i + 5] ^ st[i + 10] ^ st[i + 15] ^ st[i + 20];
+#pragma GCC unroll 5
+    for (int i = 0; i < 5; i++) {
+      t = bc[(i + 4) % 5] ^ rol64(bc[(i + 1) % 5], 1);
+#pragma GCC unroll 5
+      for (int j = 0; j < 25; j += 5) st[j + i] ^= t;
+    }
+    t = st[1];
+#pragma GCC unroll 24
+    for (int i = 0; i < 24; i++) {
+      int j = PI_LANE[i];
+      bc[0] = st[j];
+      st[j] = rol64(t, RHO_OFF[i]);
+      t = bc[0];
+    }
+#pragma GCC unroll 5
+    for (int j = 0; j < 25; j += 5) {
+#pragma GCC unroll 5
+      for (int i = 0; i < 5; i++) bc[i] = st[j + i];
+#pragma GCC unroll 5
+      for (int i = 0; i < 5; i++) st[j + i] ^= (~bc[(i + 1) % 5]) & bc[(i + 2) % 5];
+    }
+    st[0] ^= KRC[ir];
+  }
+}
+
+#define TS_RATE 168
+typedef struct {
+  uint64_t s[25];
+  uint32_t pos;
+  int rounds;
+} sponge;
+
+static void sp_init(sponge* t, int rounds) {
+  memset(t->s, 0, sizeof t->s);
+  t->pos = 0;
+  t->rounds = rounds;
+}
+static inline uint8_t* sp_bytes(sponge* t) { return (uint8_t*)t->s; } /* little-endian host */
+static void sp_absorb(sponge* t, const uint8_t* d, size_t n) {
+  uint8_t* b = sp_bytes(t);
+  while (n--) {
+    b[t->pos++] ^= *d++;
+    if (t->pos == TS_RATE) {
+      orc_keccak_p1600(t->s, t->rounds);
+      t->pos = 0;
+    }
+  }
+}
+static void sp_finalize(sponge* t, uint8_t domain) {
+  uint8_t* b = sp_bytes(t);
+  b[t->pos] ^= domain;
+  b[TS_RATE - 1] ^= 0x80;
+  orc_keccak_p1600(t->s, t->rounds);
+  t->pos = 0;
+}
+static void sp_squeeze(sponge* t, uint8_t* out, size_t n) {
+  uint8_t* b = sp_bytes(t);
+  while (n--) {
+    if (t->pos == TS_RATE) {
+      orc_keccak_p1600(t->s, t->rounds);
+      t->pos = 0;
+    }
+    *out++ = b[t->pos++];
+  }
+}
+
+void orc_turboshake128(const uint8_t* msg, size_t len, uint8_t domain, uint8_t* out,
+                       size_t out_len) {
+  sponge t;
+  sp_init(&t, 12);
+  sp_absorb(&t, msg, len);
+  sp_finalize(&t, domain);
+  sp_squeeze(&t, out, out_len);
+}
+void orc_shake128(const uint8_t* msg, size_t len, uint8_t* out, size_t out_len) {
+  sponge t;
+  sp_init(&t, 24);
+  sp_absorb(&t, msg, len);
+  sp_finalize(&t, 0x1F);
+  sp_squeeze(&t, out, out_len);
+}
+
+/* XofTurboShake128(seed, dst, binder) = TurboSHAKE128(len(dst) || dst || seed || binder, D=1)
+ * [VDAF-08 §6.2.1; prio vdaf/xof.rs XofTurboShake128::init]. */
+static void xof_init(sponge* t, const uint8_t seed[16], const uint8_t* dst, size_t dst_len) {
+  sp_init(t, 12);
+  uint8_t l = (uint8_t)dst_len;
+  sp_absorb(t, &l, 1);
+  sp_absorb(t, dst, dst_len);
+  sp_absorb(t, seed, 16);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Fields [VDAF-08 §6.1.2]: Field64 p = 2^64 - 2^32 + 1, Field128 p = 2^128 - 28*2^64 + 1  */
+/* Elements are canonical integers in [0, p) held in a u128 for both fields.             */
+/* ------------------------------------------------------------------------------------ */
+typedef u128 fe;
+#define P64 0xffffffff00000001ULL
+static const u128 P128 = (((u128)0xffffffffffffffe4ULL) << 64) | 1;
+static const u128 C1_128 = (((u128)27) << 64) | 0xffffffffffffffffULL; /* 2^128 mod p = 28*2^64-1 */
+
+typedef struct {
+  int is128;
+  u128 p;
+} fld;
+
+static inline fe f_add(const fld* F, fe a, fe b) {
+  if (F->is128) {
+    u128 s = a + b;
+    if (s < a || s >= P128) s -= P128;
+    return s;
+  }
+  u128 s = a + b;
+  return s >= P64 ? s - P64 : s;
+}
+static inline fe f_sub(const fld* F, fe a, fe b) {
+  if (a >= b) return a - b;
+  return a + (F->p - b);
+}
+static inline fe f_neg(const fld* F, fe a) { return a ? F->p - a : 0; }
+
+static inline uint64_t f64_reduce128(u128 x) {
+  uint64_t lo = (uint64_t)x, hi = (uint64_t)(x >> 64);
+  uint64_t hh = hi >> 32, hl = hi & 0xffffffffULL;
+  uint64_t t0 = lo - hh;
+  if (lo < hh) t0 -= 0xffffffffULL;
+  uint64_t t1 = hl * 0xffffffffULL;
+  uint64_t r = t0 + t1;
+  if (r < t0) r += 0xffffffffULL;
+  if (r >= P64) r -= P64;
+  return r;
+}
+
+static inline u128 f128_mul(u128 a, u128 b) {
+  uint64_t a0 = (uint64_t)a, a1 = (uint64_t)(a >> 64);
+  uint64_t b0 = (uint64_t)b, b1 = (uint64_t)(b >> 64);
+  u128 p00 = (u128)a0 * b0, p01 = (u128)a0 * b1, p10 = (u128)a1 * b0, p11 = (u128)a1 * b1;
+  u128 mid = p01 + p10;
+  uint64_t cmid = mid < p01;
+  u128 lo = p00 + (mid << 64);
+  uint64_t clo = lo < p00;
+  u128 hi = p11 + (mid >> 64) + ((u128)cmid << 64) + clo;
+  /* X = hi*2^128 + lo;  2^128 = 28*2^64 - 1,  2^192 = 783*2^64 - 28  (mod p) */
+  uint64_t h0 = (uint64_t)hi, h1 = (uint64_t)(hi >> 64);
+  u128 T = (u128)h0 * 28 + (u128)h1 * 783;
+  uint64_t tlo = (uint64_t)T, t2 = (uint64_t)(T >> 64);
+  u128 U = (u128)tlo + (u128)t2 * 28;
+  int carry = (int)(U >> 64);
+  u128 acc = lo, add = U << 64;
+  acc += add;
+  if (acc < add) carry++;
+  u128 sub = (u128)h0 + (u128)h1 * 28 + t2;
+  if (acc < sub) carry--;
+  acc -= sub;
+  while (carry > 0) {
+    u128 c = (u128)(unsigned)carry * C1_128;
+    carry = 0;
+    acc += c;
+    if (acc < c) carry = 1;
+  }
+  while (carry < 0) {
+    carry++;
+    if (acc < C1_128) carry--;
+    acc -= C1_128;
+  }
+  while (acc >= P128) acc -= P128;
+  return acc;
+}
+
+static inline fe f_mul(const fld* F, fe a, fe b) {
+  if (F->is128) return f128_mul(a, b);
+  return f64_reduce128((u128)(uint64_t)a * (uint64_t)b);
+}
+static fe f_pow(const fld* F, fe a, u128 e) {
+  fe r = 1;
+  while (e) {
+    if (e & 1) r = f_mul(F, r, a);
+    a = f_mul(F, a, a);
+    e >>= 1;
+  }
+  return r;
+}
+static fe f_inv(const fld* F, fe a) { return f_pow(F, a, F->p - 2); }
+static fe f_from_u64(const fld* F, uint64_t x) { return F->is128 ? (fe)x : (fe)(x % P64); }
+
+/* Generator of the 2^num_roots subgroup [prio fp.rs FP64/FP128 `g`; VDAF-08 §6.1.2]. */
+/* roots[l] = g^(2^(num_roots - l)), the principal 2^l-th root (prio FieldParameters::roots). */
+#define MAX_ROOTS 20
+static fe ROOTS64[MAX_ROOTS + 1], ROOTS128[MAX_ROOTS + 1];
+static pthread_once_t roots_once = PTHREAD_ONCE_INIT;
+static void roots_init(void) {
+  fld F64 = {0, (u128)P64}, F128 = {1, 0};
+  F128.p = P128;
+  fe g128 = 0;
+  for (const char* c = "145091266659756586618791329697897684742"; *c; c++)
+    g128 = g128 * 10 + (u128)(*c - '0');
+  fe g64 = 1753635133440165772ULL;
+  for (int l = 0; l <= MAX_ROOTS; l++) {
+    fe r = g128;
+    for (int i = 0; i < 66 - l; i++) r = f_mul(&F128, r, r);
+    ROOTS128[l] = r;
+    r = g64;
+    for (int i = 0; i < 32 - l; i++) r = f_mul(&F64, r, r);
+    ROOTS64[l] = r;
+  }
+}
+static fe f_root(const fld* F, int l) {
+  pthread_once(&roots_once, roots_init);
+  return F->is128 ? ROOTS128[l] : ROOTS64[l];
+}
+
+static void enc_fe(const fld* F, fe x, uint8_t* out) {
+  int n = F->is128 ? 16 : 8;
+  for (int i = 0; i < n; i++) out[i] = (uint8_t)(x >> (8 * i));
+}
+static int dec_fe(const fld* F, const uint8_t* in, fe* x) {
+  int n = F->is128 ? 16 : 8;
+  u128 v = 0;
+  for (int i = n - 1; i >= 0; i--) v = (v << 8) | in[i];
+  if (v >= F->p) return -1;
+  *x = v;
+  return 0;
+}
+
+/* Xof.expand_into_vec with rejection sampling [VDAF-08 §6.2; prio Prng::get]. */
+static void xof_expand(const fld* F, sponge* t, fe* out, uint32_t n) {
+  int es = F->is128 ? 16 : 8;
+  uint8_t buf[16];
+  for (uint32_t i = 0; i < n;) {
+    sp_squeeze(t, buf, es);
+    u128 v = 0;
+    for (int k = es - 1; k >= 0; k--) v = (v << 8) | buf[k];
+    if (v < F->p) out[i++] = v;
+  }
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Polynomials / DFT -- mirrors prio fft.rs discrete_fourier_transform (bit-reversed      */
+/* input, iterative butterflies with roots(l)), discrete_fourier_transform_inv_finish     */
+/* and polynomial.rs poly_eval.                                                           */
+/* ------------------------------------------------------------------------------------ */
+static uint32_t log2u(uint32_t n) {
+  uint32_t d = 0;
+  while ((1u << d) < n) d++;
+  return d;
+}
+static uint32_t bitrev(uint32_t d, uint32_t x) {
+  uint32_t y = 0;
+  for (uint32_t i = 0; i < d; i++) {
+    y = (y << 1) | (x & 1);
+    x >>= 1;
+  }
+  return y;
+}
+static void dft(const fld* F, fe* outp, const fe* inp, uint32_t inp_len, uint32_t size) {
+  uint32_t d = log2u(size);
+  for (uint32_t i = 0; i < size; i++) {
+    uint32_t j = bitrev(d, i);
+    outp[i] = j < inp_len ? inp[j] : 0;
+  }
+  for (uint32_t l = 1; l <= d; l++) {
+    fe w = 1, r = f_root(F, (int)l);
+    uint32_t y = 1u << (l - 1), chunk = (size / y) >> 1;
+    for (uint32_t i = 0; i < y; i++) {
+      for (uint32_t j = 0; j < chunk; j++) {
+        uint32_t x = j << l;
+        fe u = outp[i + x], v = f_mul(F, w, outp[i + x + y]);
+        outp[i + x] = f_add(F, u, v);
+        outp[i + x + y] = f_sub(F, u, v);
+      }
+      w = f_mul(F, w, r);
+    }
+  }
+}
+static void dft_inv_finish(const fld* F, fe* outp, uint32_t size, fe size_inv) {
+  outp[0] = f_mul(F, outp[0], size_inv);
+  outp[size >> 1] = f_mul(F, outp[size >> 1], size_inv);
+  for (uint32_t i = 1; i < (size >> 1); i++) {
+    fe tmp = f_mul(F, outp[i], size_inv);
+    outp[i] = f_mul(F, outp[size - i], size_inv);
+    outp[size - i] = tmp;
+  }
+}
+static fe poly_eval(const fld* F, const fe* poly, uint32_t len, fe x) {
+  fe r = 0;
+  for (uint32_t i = len; i-- > 0;) r = f_add(F, f_mul(F, r, x), poly[i]);
+  return r;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Parameters [VDAF-08 §7.4 (Prio3Count/Sum/SumVec/Histogram); core/src/vdaf.rs:198-300] */
+/* ------------------------------------------------------------------------------------ */
+static uint32_t next_pow2(uint32_t n) {
+  uint32_t p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+int orc_params_init(orc_params* p, int type, uint32_t bits, uint32_t length,
+                    uint32_t chunk_length, uint32_t num_proofs) {
+  memset(p, 0, sizeof *p);
+  p->type = type;
+  p->bits = bits;
+  p->length = length;
+  p->chunk_length = chunk_length;
+  p->num_proofs = num_proofs ? num_proofs : 1;
+  if (p->num_proofs > 255) return -1;
+  p->qr_len = 1;
+  p->degree = 2;
+  switch (type) {
+    case ORC_COUNT: /* Prio3::new_count(2): Count<Field64>, Mul gadget, 1 call */
+      p->algorithm_id = 0;
+      p->field_bits = 64;
+      p->meas_len = 1;
+      p->out_len = 1;
+      p->jr_len = 0;
+      p->arity = 2;
+      p->calls = 1;
+      break;
+    case ORC_SUM: /* Prio3::new_sum(2, bits): Sum<Field128>, PolyEval(x^2-x) x bits */
+      if (bits == 0 || bits > 64) return -1;
+      p->algorithm_id = 1;
+      p->field_bits = 128;
+      p->meas_len = bits;
+      p->out_len = 1;
+      p->jr_len = 1;
+      p->arity = 1;
+      p->calls = bits;
+      break;
+    case ORC_SUMVEC: /* SumVec<Field128, ParallelSum<Mul>> */
+      if (bits == 0 || bits > 64 || length == 0 || chunk_length == 0) return -1;
+      p->algorithm_id = 2;
+      p->field_bits = 128;
+      p->meas_len = bits * length;
+      p->out_len = length;
+      p->jr_len = 1;
+      p->arity = 2 * chunk_length;
+      p->calls = (p->meas_len + chunk_length - 1) / chunk_length;
+      break;
+    case ORC_HISTOGRAM: /* Histogram<Field128, ParallelSum<Mul>> */
+      if (length == 0 || chunk_length == 0) return -1;
+      p->algorithm_id = 3;
+      p->field_bits = 128;
+      p->meas_len = length;
+      p->out_len = length;
+      p->jr_len = 2;
+      p->arity = 2 * chunk_length;
+      p->calls = (length + chunk_length - 1) / chunk_length;
+      break;
+    default:
+      return -1;
+  }
+  p->es = p->field_bits / 8;
+  p->prove_rand_len = p->arity;
+  p->wire_len = next_pow2(1 + p->calls);
+  p->proof_len = p->arity + p->degree * (p->wire_len - 1) + 1;
+  p->verifier_len = 1 + p->arity + 1;
+  p->helper_share_len = 16 * (p->jr_len ? 3 : 2);
+  p->public_share_len = p->jr_len ? 32 : 0;
+  p->leader_share_len =
+      (p->meas_len + p->proof_len * p->num_proofs) * p->es + (p->jr_len ? 16 : 0);
+  p->prep_share_len = p->verifier_len * p->num_proofs * p->es + (p->jr_len ? 16 : 0);
+  p->prep_msg_len = p->jr_len ? 16 : 0;
+  p->out_share_bytes = p->out_len * p->es;
+  return 0;
+}
+
+static fld mkfld(const orc_params* p) {
+  fld F;
+  F.is128 = p->field_bits == 128;
+  F.p = F.is128 ? P128 : (u128)P64;
+  return F;
+}
+
+/* format_dst(algo_class=0, algo, usage) [VDAF-08 §7.2.1 / prio Prio3::domain_separation_tag] */
+static void mkdst(const orc_params* p, uint16_t usage, uint8_t dst[8]) {
+  dst[0] = 8; /* VERSION */
+  dst[1] = 0; /* algorithm class: VDAF */
+  dst[2] = (uint8_t)(p->algorithm_id >> 24);
+  dst[3] = (uint8_t)(p->algorithm_id >> 16);
+  dst[4] = (uint8_t)(p->algorithm_id >> 8);
+  dst[5] = (uint8_t)(p->algorithm_id);
+  dst[6] = (uint8_t)(usage >> 8);
+  dst[7] = (uint8_t)usage;
+}
+enum {
+  U_MEAS_SHARE = 1,
+  U_PROOF_SHARE = 2,
+  U_JOINT_RANDOMNESS = 3,
+  U_PROVE_RANDOMNESS = 4,
+  U_QUERY_RANDOMNESS = 5,
+  U_JOINT_RAND_SEED = 6,
+  U_JOINT_RAND_PART = 7
+};
+
+static void xof_for(const orc_params* p, sponge* t, const uint8_t seed[16], uint16_t usage) {
+  uint8_t dst[8];
+  mkdst(p, usage, dst);
+  xof_init(t, seed, dst, 8);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* FLP (FlpBBCGGI19, [VDAF-08 §7.3]; prio flp.rs FlpGeneric) with shim gadgets           */
+/* ------------------------------------------------------------------------------------ */
+typedef struct {
+  const fld* F;
+  const orc_params* p;
+  int prove; /* 1: ProveShimGadget (evaluate inner), 0: QueryShimGadget */
+  uint32_t ct;
+  fe* f_vals;  /* arity x wire_len (row = wire), zero-padded */
+  fe* p_vals;  /* query: gadget polynomial at the 2P-th roots */
+  uint32_t step;
+} shim;
+
+static fe gadget_eval(const fld* F, const orc_params* p, const fe* x) {
+  switch (p->type) {
+    case ORC_COUNT:
+      return f_mul(F, x[0], x[1]); /* Mul */
+    case ORC_SUM:
+      return f_sub(F, f_mul(F, x[0], x[0]), x[0]); /* PolyEval([0,-1,1]) */
+    default: {                                     /* ParallelSum(Mul, chunk) */
+      fe s = 0;
+      for (uint32_t j = 0; j < p->chunk_length; j++)
+        s = f_add(F, s, f_mul(F, x[2 * j], x[2 * j + 1]));
+      return s;
+    }
+  }
+}
+
+static fe shim_call(shim* s, const fe* x) {
+  const orc_params* p = s->p;
+  for (uint32_t w = 0; w < p->arity; w++) s->f_vals[w * p->wire_len + s->ct] = x[w];
+  fe y = s->prove ? gadget_eval(s->F, p, x) : s->p_vals[s->ct * s->step];
+  s->ct++;
+  return y;
+}
+
+/* parallel_sum_range_checks [prio flp/types.rs; VDAF-08 §7.4.3/7.4.4 valid()] */
+static fe range_checks(shim* s, const fe* in, uint32_t n, fe r, fe shares_inv, fe* args) {
+  const fld* F = s->F;
+  uint32_t c = s->p->chunk_length;
+  fe out = 0, rp = r;
+  for (uint32_t base = 0; base < n; base += c) {
+    for (uint32_t j = 0; j < c; j++) {
+      uint32_t i = base + j;
+      fe m = i < n ? in[i] : 0; /* padding: measurement element 0 */
+      args[2 * j] = f_mul(F, rp, m);
+      args[2 * j + 1] = f_sub(F, m, shares_inv);
+      rp = f_mul(F, rp, r);
+    }
+    out = f_add(F, out, shim_call(s, args));
+  }
+  return out;
+}
+
+static fe valid(shim* s, const fe* in, const fe* jr, uint32_t num_shares) {
+  const fld* F = s->F;
+  const orc_params* p = s->p;
+  fe shares_inv = f_inv(F, f_from_u64(F, num_shares));
+  switch (p->type) {
+    case ORC_COUNT: { /* Count::valid: g(m, m) - m */
+      fe x[2] = {in[0], in[0]};
+      return f_sub(F, shim_call(s, x), in[0]);
+    }
+    case ORC_SUM: { /* Sum::valid: sum_i r^(i+1) * g(m_i) */
+      fe out = 0, r = jr[0];
+      for (uint32_t i = 0; i < p->meas_len; i++) {
+        out = f_add(F, out, f_mul(F, r, shim_call(s, &in[i])));
+        r = f_mul(F, r, jr[0]);
+      }
+      return out;
+    }
+    case ORC_SUMVEC: {
+      fe* args = (fe*)malloc(sizeof(fe) * p->arity);
+      fe out = range_checks(s, in, p->meas_len, jr[0], shares_inv, args);
+      free(args);
+      return out;
+    }
+    case ORC_HISTOGRAM: {
+      fe* args = (fe*)malloc(sizeof(fe) * p->arity);
+      fe rc = range_checks(s, in, p->meas_len, jr[0], shares_inv, args);
+      free(args);
+      fe sc = f_neg(F, shares_inv);
+      for (uint32_t i = 0; i < p->meas_len; i++) sc = f_add(F, sc, in[i]);
+      return f_add(F, f_mul(F, jr[1], rc), f_mul(F, f_mul(F, jr[1], jr[1]), sc));
+    }
+  }
+  return 0;
+}
+
+/* FlpGeneric::query -> verifier (verifier_len elements). Returns -1 if t is a P-th root. */
+static int flp_query(const fld* F, const orc_params* p, const fe* meas, const fe* proof,
+                     const fe* qr, const fe* jr, fe* verifier) {
+  uint32_t P = p->wire_len, size = next_pow2(P * p->degree);
+  fe t = qr[0];
+  if (f_pow(F, t, P) == 1) return -1;
+  uint32_t glen = p->degree * (P - 1) + 1;
+  shim s;
+  s.F = F;
+  s.p = p;
+  s.prove = 0;
+  s.ct = 1;
+  s.f_vals = (fe*)calloc((size_t)p->arity * P, sizeof(fe));
+  s.p_vals = (fe*)malloc(sizeof(fe) * size);
+  s.step = size / P;
+  dft(F, s.p_vals, proof + p->arity, glen, size);
+  fe p_at_r = poly_eval(F, proof + p->arity, glen, t);
+  for (uint32_t w = 0; w < p->arity; w++) s.f_vals[w * P] = proof[w];
+  verifier[0] = valid(&s, meas, jr, 2);
+  fe* f = (fe*)malloc(sizeof(fe) * P);
+  fe m_inv = f_inv(F, P);
+  for (uint32_t w = 0; w < p->arity; w++) {
+    dft(F, f, s.f_vals + (size_t)w * P, 1 + p->calls, P);
+    dft_inv_finish(F, f, P, m_inv);
+    verifier[1 + w] = poly_eval(F, f, P, t);
+  }
+  verifier[1 + p->arity] = p_at_r;
+  free(f);
+  free(s.f_vals);
+  free(s.p_vals);
+  return 0;
+}
+
+/* FlpGeneric::decide */
+static int flp_decide(const fld* F, const orc_params* p, const fe* v) {
+  if (v[0] != 0) return 0;
+  return gadget_eval(F, p, v + 1) == v[1 + p->arity];
+}
+
+/* FlpGeneric::prove (client side; used only to synthesise honest reports). */
+static void flp_prove(const fld* F, const orc_params* p, const fe* meas, const fe* prove_rand,
+                      const fe* jr, fe* proof) {
+  uint32_t P = p->wire_len, size = next_pow2(P * p->degree);
+  uint32_t glen = p->degree * (P - 1) + 1;
+  shim s;
+  s.F = F;
+  s.p = p;
+  s.prove = 1;
+  s.ct = 1;
+  s.f_vals = (fe*)calloc((size_t)p->arity * P, sizeof(fe));
+  s.p_vals = NULL;
+  s.step = 0;
+  for (uint32_t w = 0; w < p->arity; w++) s.f_vals[w * P] = prove_rand[w];
+  (void)valid(&s, meas, jr, 1);
+  fe m_inv = f_inv(F, P), size_inv = f_inv(F, size);
+  fe* coef = (fe*)malloc(sizeof(fe) * P);
+  fe* evals = (fe*)malloc(sizeof(fe) * (size_t)p->arity * size);
+  for (uint32_t w = 0; w < p->arity; w++) {
+    dft(F, coef, s.f_vals + (size_t)w * P, 1 + p->calls, P);
+    dft_inv_finish(F, coef, P, m_inv);
+    proof[w] = s.f_vals[(size_t)w * P];
+    dft(F, evals + (size_t)w * size, coef, P, size); /* wire poly at 2P-th roots */
+  }
+  fe* g = (fe*)malloc(sizeof(fe) * size);
+  fe* x = (fe*)malloc(sizeof(fe) * p->arity);
+  for (uint32_t k = 0; k < size; k++) {
+    for (uint32_t w = 0; w < p->arity; w++) x[w] = evals[(size_t)w * size + k];
+    g[k] = gadget_eval(F, p, x);
+  }
+  fe* gc = (fe*)malloc(sizeof(fe) * size);
+  dft(F, gc, g, size, size);
+  dft_inv_finish(F, gc, size, size_inv);
+  for (uint32_t k = 0; k < glen; k++) proof[p->arity + k] = gc[k];
+  free(coef);
+  free(evals);
+  free(g);
+  free(x);
+  free(gc);
+  free(s.f_vals);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Prio3 [VDAF-08 §7.2]                                                                  */
+/* ------------------------------------------------------------------------------------ */
+static void expand_seed(const orc_params* p, const fld* F, const uint8_t seed[16], uint16_t usage,
+                        const uint8_t* binder, size_t blen, fe* out, uint32_t n) {
+  sponge t;
+  xof_for(p, &t, seed, usage);
+  sp_absorb(&t, binder, blen);
+  sp_finalize(&t, 1);
+  xof_expand(F, &t, out, n);
+}
+static void derive_seed(const orc_params* p, const uint8_t seed[16], uint16_t usage,
+                        const uint8_t* binder, size_t blen, uint8_t out[16]) {
+  sponge t;
+  xof_for(p, &t, seed, usage);
+  sp_absorb(&t, binder, blen);
+  sp_finalize(&t, 1);
+  sp_squeeze(&t, out, 16);
+}
+static void helper_meas_share(const orc_params* p, const fld* F, const uint8_t k[16], uint8_t agg,
+                              fe* out) {
+  expand_seed(p, F, k, U_MEAS_SHARE, &agg, 1, out, p->meas_len);
+}
+static void helper_proofs_share(const orc_params* p, const fld* F, const uint8_t k[16],
+                                uint8_t agg, fe* out) {
+  uint8_t b[2] = {(uint8_t)p->num_proofs, agg};
+  expand_seed(p, F, k, U_PROOF_SHARE, b, 2, out, p->proof_len * p->num_proofs);
+}
+static void joint_rand_part(const orc_params* p, const fld* F, const uint8_t blind[16], uint8_t agg,
+                            const uint8_t nonce[16], const fe* meas, uint8_t out[16]) {
+  sponge t;
+  xof_for(p, &t, blind, U_JOINT_RAND_PART);
+  sp_absorb(&t, &agg, 1);
+  sp_absorb(&t, nonce, 16);
+  uint8_t buf[16];
+  for (uint32_t i = 0; i < p->meas_len; i++) {
+    enc_fe(F, meas[i], buf);
+    sp_absorb(&t, buf, p->es);
+  }
+  sp_finalize(&t, 1);
+  sp_squeeze(&t, out, 16);
+}
+static void joint_rand_seed(const orc_params* p, const uint8_t part0[16], const uint8_t part1[16],
+                            uint8_t out[16]) {
+  static const uint8_t zero[16] = {0};
+  uint8_t b[32];
+  memcpy(b, part0, 16);
+  memcpy(b + 16, part1, 16);
+  derive_seed(p, zero, U_JOINT_RAND_SEED, b, 32, out);
+}
+static void joint_rands(const orc_params* p, const fld* F, const uint8_t seed[16], fe* out) {
+  uint8_t b = (uint8_t)p->num_proofs;
+  expand_seed(p, F, seed, U_JOINT_RANDOMNESS, &b, 1, out, p->jr_len * p->num_proofs);
+}
+static void query_rands(const orc_params* p, const fld* F, const uint8_t vk[16],
+                        const uint8_t nonce[16], fe* out) {
+  uint8_t b[17];
+  b[0] = (uint8_t)p->num_proofs;
+  memcpy(b + 1, nonce, 16);
+  expand_seed(p, F, vk, U_QUERY_RANDOMNESS, b, 17, out, p->qr_len * p->num_proofs);
+}
+
+static int encode_measurement(const orc_params* p, const fld* F, const uint64_t* m, fe* out) {
+  switch (p->type) {
+    case ORC_COUNT:
+      if (m[0] > 1) return -1;
+      out[0] = m[0];
+      return 0;
+    case ORC_SUM:
+      if (p->bits < 64 && (m[0] >> p->bits)) return -1;
+      for (uint32_t i = 0; i < p->bits; i++) out[i] = (m[0] >> i) & 1;
+      return 0;
+    case ORC_SUMVEC:
+      for (uint32_t e = 0; e < p->length; e++) {
+        if (p->bits < 64 && (m[e] >> p->bits)) return -1;
+        for (uint32_t b = 0; b < p->bits; b++) out[e * p->bits + b] = (m[e] >> b) & 1;
+      }
+      return 0;
+    case ORC_HISTOGRAM:
+      if (m[0] >= p->length) return -1;
+      for (uint32_t i = 0; i < p->length; i++) out[i] = i == m[0];
+      return 0;
+  }
+  (void)F;
+  return -1;
+}
+
+static void truncate_share(const orc_params* p, const fld* F, const fe* meas, fe* out) {
+  switch (p->type) {
+    case ORC_COUNT:
+    case ORC_HISTOGRAM:
+      memcpy(out, meas, sizeof(fe) * p->meas_len);
+      return;
+    case ORC_SUM: {
+      fe acc = 0, pw = 1;
+      for (uint32_t i = 0; i < p->bits; i++) {
+        acc = f_add(F, acc, f_mul(F, pw, meas[i]));
+        pw = f_add(F, pw, pw);
+      }
+      out[0] = acc;
+      return;
+    }
+    case ORC_SUMVEC:
+      for (uint32_t e = 0; e < p->length; e++) {
+        fe acc = 0, pw = 1;
+        for (uint32_t b = 0; b < p->bits; b++) {
+          acc = f_add(F, acc, f_mul(F, pw, meas[e * p->bits + b]));
+          pw = f_add(F, pw, pw);
+        }
+        out[e] = acc;
+      }
+      return;
+  }
+}
+
+int orc_shard(const orc_params* p, const uint64_t* meas, const uint8_t nonce[16],
+              const uint8_t* rand, uint8_t* public_share, uint8_t* leader_share,
+              uint8_t* helper_share) {
+  fld F = mkfld(p);
+  uint32_t np = p->num_proofs;
+  fe* enc = (fe*)malloc(sizeof(fe) * p->meas_len);
+  fe* hm = (fe*)malloc(sizeof(fe) * p->meas_len);
+  fe* lm = (fe*)malloc(sizeof(fe) * p->meas_len);
+  fe* proofs = (fe*)malloc(sizeof(fe) * p->proof_len * np);
+  fe* hp = (fe*)malloc(sizeof(fe) * p->proof_len * np);
+  fe* prove_rand = (fe*)malloc(sizeof(fe) * p->prove_rand_len * np);
+  fe jr[64];
+  int rc = encode_measurement(p, &F, meas, enc);
+  if (rc) goto out;
+  const uint8_t* k_hmeas = rand;
+  const uint8_t* k_hproof = rand + 16;
+  const uint8_t* k_hblind = p->jr_len ? rand + 32 : NULL;
+  const uint8_t* k_lblind = p->jr_len ? rand + 48 : NULL;
+  const uint8_t* k_prove = p->jr_len ? rand + 64 : rand + 32;
+  helper_meas_share(p, &F, k_hmeas, 1, hm);
+  for (uint32_t i = 0; i < p->meas_len; i++) lm[i] = f_sub(&F, enc[i], hm[i]);
+  if (p->jr_len) {
+    uint8_t part0[16], part1[16], seed[16];
+    joint_rand_part(p, &F, k_hblind, 1, nonce, hm, part1);
+    joint_rand_part(p, &F, k_lblind, 0, nonce, lm, part0);
+    memcpy(public_share, part0, 16);
+    memcpy(public_share + 16, part1, 16);
+    joint_rand_seed(p, part0, part1, seed);
+    joint_rands(p, &F, seed, jr);
+  }
+  {
+    uint8_t b = (uint8_t)np;
+    expand_seed(p, &F, k_prove, U_PROVE_RANDOMNESS, &b, 1, prove_rand, p->prove_rand_len * np);
+  }
+  for (uint32_t k = 0; k < np; k++)
+    flp_prove(&F, p, enc, prove_rand + k * p->prove_rand_len, jr + k * p->jr_len,
+              proofs + k * p->proof_len);
+  helper_proofs_share(p, &F, k_hproof, 1, hp);
+  for (uint32_t i = 0; i < p->proof_len * np; i++) proofs[i] = f_sub(&F, proofs[i], hp[i]);
+  /* leader share: enc(meas) || enc(proofs) || [blind] */
+  uint8_t* o = leader_share;
+  for (uint32_t i = 0; i < p->meas_len; i++, o += p->es) enc_fe(&F, lm[i], o);
+  for (uint32_t i = 0; i < p->proof_len * np; i++, o += p->es) enc_fe(&F, proofs[i], o);
+  if (p->jr_len) memcpy(o, k_lblind, 16);
+  memcpy(helper_share, k_hmeas, 16);
+  memcpy(helper_share + 16, k_hproof, 16);
+  if (p->jr_len) memcpy(helper_share + 32, k_hblind, 16);
+out:
+  free(enc);
+  free(hm);
+  free(lm);
+  free(proofs);
+  free(hp);
+  free(prove_rand);
+  return rc;
+}
+
+/* Core of prepare_init; optionally exports intermediates. */
+static int prepare_init_core(const orc_params* p, const fld* F, const uint8_t vk[16], int agg_id,
+                             const uint8_t nonce[16], const uint8_t* public_share,
+                             const uint8_t* input_share, fe* meas, fe* proofs, uint8_t part[16],
+                             uint8_t corrected[16], fe* jr, fe* qr, fe* verifiers) {
+  uint32_t np = p->num_proofs;
+  if (agg_id == 0) {
+    const uint8_t* in = input_share;
+    for (uint32_t i = 0; i < p->meas_len; i++, in += p->es)
+      if (dec_fe(F, in, &meas[i])) return ORC_ERR_PREP_INIT;
+    for (uint32_t i = 0; i < p->proof_len * np; i++, in += p->es)
+      if (dec_fe(F, in, &proofs[i])) return ORC_ERR_PREP_INIT;
+  } else {
+    helper_meas_share(p, F, input_share, (uint8_t)agg_id, meas);
+    helper_proofs_share(p, F, input_share + 16, (uint8_t)agg_id, proofs);
+  }
+  if (p->jr_len) {
+    const uint8_t* blind = agg_id == 0
+                               ? input_share + (p->meas_len + p->proof_len * np) * p->es
+                               : input_share + 32;
+    joint_rand_part(p, F, blind, (uint8_t)agg_id, nonce, meas, part);
+    if (agg_id == 0)
+      joint_rand_seed(p, part, public_share + 16, corrected);
+    else
+      joint_rand_seed(p, public_share, part, corrected);
+    joint_rands(p, F, corrected, jr);
+  }
+  query_rands(p, F, vk, nonce, qr);
+  for (uint32_t k = 0; k < np; k++)
+    if (flp_query(F, p, meas, proofs + k * p->proof_len, qr + k * p->qr_len, jr + k * p->jr_len,
+                  verifiers + k * p->verifier_len))
+      return ORC_ERR_PREP_INIT;
+  return ORC_OK;
+}
+
+int orc_prepare_init(const orc_params* p, const uint8_t vk[16], int agg_id,
+                     const uint8_t nonce[16], const uint8_t* public_share,
+                     const uint8_t* input_share, uint8_t* state_out, uint8_t* prep_share_out) {
+  fld F = mkfld(p);
+  uint32_t np = p->num_proofs;
+  fe* meas = (fe*)malloc(sizeof(fe) * p->meas_len);
+  fe* proofs = (fe*)malloc(sizeof(fe) * p->proof_len * np);
+  fe* ver = (fe*)malloc(sizeof(fe) * p->verifier_len * np);
+  fe jr[64], qr[64];
+  uint8_t part[16], corrected[16];
+  int rc = prepare_init_core(p, &F, vk, agg_id, nonce, public_share, input_share, meas, proofs,
+                             part, corrected, jr, qr, ver);
+  if (rc == ORC_OK) {
+    uint8_t* o = state_out;
+    for (uint32_t i = 0; i < p->meas_len; i++, o += p->es) enc_fe(&F, meas[i], o);
+    if (p->jr_len) memcpy(o, corrected, 16);
+    o = prep_share_out;
+    for (uint32_t i = 0; i < p->verifier_len * np; i++, o += p->es) enc_fe(&F, ver[i], o);
+    if (p->jr_len) memcpy(o, part, 16);
+  }
+  free(meas);
+  free(proofs);
+  free(ver);
+  return rc;
+}
+
+int orc_helper_trace(const orc_params* p, const uint8_t vk[16], const uint8_t nonce[16],
+                     const uint8_t* public_share, const uint8_t* helper_share,
+                     uint8_t* meas_out, uint8_t* proofs_out, uint8_t* part_out,
+                     uint8_t* corrected_out, uint8_t* jr_out, uint8_t* qr_out,
+                     uint8_t* verifier_out) {
+  fld F = mkfld(p);
+  uint32_t np = p->num_proofs;
+  fe* meas = (fe*)malloc(sizeof(fe) * p->meas_len);
+  fe* proofs = (fe*)malloc(sizeof(fe) * p->proof_len * np);
+  fe* ver = (fe*)malloc(sizeof(fe) * p->verifier_len * np);
+  fe jr[64] = {0}, qr[64] = {0};
+  uint8_t part[16] = {0}, corrected[16] = {0};
+  int rc = prepare_init_core(p, &F, vk, 1, nonce, public_share, helper_share, meas, proofs, part,
+                             corrected, jr, qr, ver);
+  for (uint32_t i = 0; i < p->meas_len; i++) enc_fe(&F, meas[i], meas_out + i * p->es);
+  for (uint32_t i = 0; i < p->proof_len * np; i++) enc_fe(&F, proofs[i], proofs_out + i * p->es);
+  memcpy(part_out, part, 16);
+  memcpy(corrected_out, corrected, 16);
+  for (uint32_t i = 0; i < p->jr_len * np; i++) enc_fe(&F, jr[i], jr_out + i * p->es);
+  for (uint32_t i = 0; i < p->qr_len * np; i++) enc_fe(&F, qr[i], qr_out + i * p->es);
+  if (rc == ORC_OK)
+    for (uint32_t i = 0; i < p->verifier_len * np; i++)
+      enc_fe(&F, ver[i], verifier_out + i * p->es);
+  free(meas);
+  free(proofs);
+  free(ver);
+  return rc;
+}
+
+/* prepare_shares_to_prepare_message: shares = [leader, helper]. */
+static int prep_msg_core(const orc_params* p, const fld* F, const uint8_t* lps, const uint8_t* hps,
+                         uint8_t* msg) {
+  uint32_t nv = p->verifier_len * p->num_proofs;
+  fe* v = (fe*)malloc(sizeof(fe) * nv);
+  int rc = ORC_OK;
+  for (uint32_t i = 0; i < nv; i++) {
+    fe a, b;
+    if (dec_fe(F, lps + i * p->es, &a) || dec_fe(F, hps + i * p->es, &b)) {
+      rc = ORC_ERR_PREP_SHARE_DECODE;
+      goto out;
+    }
+    v[i] = f_add(F, a, b);
+  }
+  for (uint32_t k = 0; k < p->num_proofs; k++)
+    if (!flp_decide(F, p, v + k * p->verifier_len)) {
+      rc = ORC_ERR_DECIDE;
+      goto out;
+    }
+  if (p->jr_len) joint_rand_seed(p, lps + nv * p->es, hps + nv * p->es, msg);
+out:
+  free(v);
+  return rc;
+}
+
+int orc_prep_shares_to_prep_msg(const orc_params* p, const uint8_t* leader_prep_share,
+                                const uint8_t* helper_prep_share, uint8_t* prep_msg_out) {
+  fld F = mkfld(p);
+  return prep_msg_core(p, &F, leader_prep_share, helper_prep_share, prep_msg_out);
+}
+
+int orc_prepare_next(const orc_params* p, const uint8_t* state, const uint8_t* prep_msg,
+                     uint8_t* out_share_out) {
+  fld F = mkfld(p);
+  if (p->jr_len && memcmp(state + p->meas_len * p->es, prep_msg, 16) != 0)
+    return ORC_ERR_PREP_NEXT;
+  fe* meas = (fe*)malloc(sizeof(fe) * p->meas_len);
+  fe* out = (fe*)malloc(sizeof(fe) * p->out_len);
+  for (uint32_t i = 0; i < p->meas_len; i++) dec_fe(&F, state + i * p->es, &meas[i]);
+  truncate_share(p, &F, meas, out);
+  for (uint32_t i = 0; i < p->out_len; i++) enc_fe(&F, out[i], out_share_out + i * p->es);
+  free(meas);
+  free(out);
+  return ORC_OK;
+}
+
+void orc_agg_merge(const orc_params* p, uint8_t* acc, const uint8_t* other) {
+  fld F = mkfld(p);
+  for (uint32_t i = 0; i < p->out_len; i++) {
+    fe a = 0, b = 0;
+    dec_fe(&F, acc + i * p->es, &a);
+    dec_fe(&F, other + i * p->es, &b);
+    enc_fe(&F, f_add(&F, a, b), acc + i * p->es);
+  }
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Batched helper path with Janus's job structure (CPU baseline + batch oracle).         */
+/* ------------------------------------------------------------------------------------ */
+typedef struct {
+  const orc_params* p;
+  const uint8_t* vk;
+  uint32_t n;
+  const uint8_t *nonces, *publics, *helpers, *leader_ps;
+  const uint32_t* seg;
+  const uint8_t* accept;
+  uint32_t n_segments;
+  uint8_t* msgs;
+  uint8_t* status;
+  int job_size;
+  atomic_uint next_job;
+  pthread_mutex_t mu;
+  fe* agg;          /* n_segments x out_len */
+  uint64_t* count;
+} batch_ctx;
+
+static void* batch_worker(void* arg) {
+  batch_ctx* c = (batch_ctx*)arg;
+  const orc_params* p = c->p;
+  fld F = mkfld(p);
+  uint32_t np = p->num_proofs;
+  fe* meas = (fe*)malloc(sizeof(fe) * p->meas_len);
+  fe* proofs = (fe*)malloc(sizeof(fe) * p->proof_len * np);
+  fe* ver = (fe*)malloc(sizeof(fe) * p->verifier_len * np);
+  fe* out = (fe*)malloc(sizeof(fe) * p->out_len);
+  uint8_t* hps = (uint8_t*)malloc(p->prep_share_len);
+  fe* lagg = (fe*)calloc((size_t)c->n_segments * p->out_len, sizeof(fe));
+  uint64_t* lcnt = (uint64_t*)calloc(c->n_segments, sizeof(uint64_t));
+  fe jr[64], qr[64];
+  uint8_t part[16], corrected[16], msg[16];
+  for (;;) {
+    uint32_t job = atomic_fetch_add(&c->next_job, 1);
+    uint64_t lo = (uint64_t)job * c->job_size;
+    if (lo >= c->n) break;
+    uint64_t hi = lo + c->job_size;
+    if (hi > c->n) hi = c->n;
+    for (uint64_t i = lo; i < hi; i++) {
+      const uint8_t* pub = c->publics ? c->publics + i * p->public_share_len : NULL;
+      int rc = prepare_init_core(p, &F, c->vk, 1, c->nonces + i * 16, pub,
+                                 c->helpers + i * p->helper_share_len, meas, proofs, part,
+                                 corrected, jr, qr, ver);
+      if (rc == ORC_OK) {
+        uint8_t* o = hps;
+        for (uint32_t k = 0; k < p->verifier_len * np; k++, o += p->es) enc_fe(&F, ver[k], o);
+        if (p->jr_len) memcpy(o, part, 16);
+        rc = prep_msg_core(p, &F, c->leader_ps + i * p->prep_share_len, hps, msg);
+      }
+      if (rc == ORC_OK && p->jr_len && memcmp(corrected, msg, 16) != 0) rc = ORC_ERR_PREP_NEXT;
+      c->status[i] = (uint8_t)rc;
+      if (p->prep_msg_len) {
+        if (rc == ORC_OK)
+          memcpy(c->msgs + i * 16, msg, 16);
+        else
+          memset(c->msgs + i * 16, 0, 16);
+      }
+      if (rc != ORC_OK || (c->accept && !c->accept[i])) continue;
+      /* prepare_next re-derives the helper measurement share from its seed [prio]. */
+      helper_meas_share(p, &F, c->helpers + i * p->helper_share_len, 1, meas);
+      truncate_share(p, &F, meas, out);
+      uint32_t s = c->seg ? c->seg[i] : 0;
+      if (s >= c->n_segments) continue;
+      fe* a = lagg + (size_t)s * p->out_len;
+      for (uint32_t k = 0; k < p->out_len; k++) a[k] = f_add(&F, a[k], out[k]);
+      lcnt[s]++;
+    }
+  }
+  pthread_mutex_lock(&c->mu);
+  for (size_t k = 0; k < (size_t)c->n_segments * p->out_len; k++)
+    c->agg[k] = f_add(&F, c->agg[k], lagg[k]);
+  for (uint32_t s = 0; s < c->n_segments; s++) c->count[s] += lcnt[s];
+  pthread_mutex_unlock(&c->mu);
+  free(meas);
+  free(proofs);
+  free(ver);
+  free(out);
+  free(hps);
+  free(lagg);
+  free(lcnt);
+  return NULL;
+}
+
+int orc_helper_batch(const orc_params* p, const uint8_t vk[16], uint32_t n,
+                     const uint8_t* nonces, const uint8_t* public_shares,
+                     const uint8_t* helper_shares, const uint8_t* leader_prep_shares,
+                     const uint32_t* segment_ids, const uint8_t* accept_mask,
+                     uint32_t n_segments, uint8_t* prep_msgs_out, uint8_t* status_out,
+                     uint8_t* agg_out, uint64_t* count_out, int n_threads, int job_size) {
+  if (n_threads < 1) n_threads = 1;
+  if (job_size < 1) job_size = 500;
+  if (n_segments < 1) n_segments = 1;
+  batch_ctx c;
+  c.p = p;
+  c.vk = vk;
+  c.n = n;
+  c.nonces = nonces;
+  c.publics = public_shares;
+  c.helpers = helper_shares;
+  c.leader_ps = leader_prep_shares;
+  c.seg = segment_ids;
+  c.accept = accept_mask;
+  c.n_segments = n_segments;
+  c.msgs = prep_msgs_out;
+  c.status = status_out;
+  c.job_size = job_size;
+  atomic_init(&c.next_job, 0);
+  pthread_mutex_init(&c.mu, NULL);
+  c.agg = (fe*)calloc((size_t)n_segments * p->out_len, sizeof(fe));
+  c.count = count_out;
+  memset(count_out, 0, sizeof(uint64_t) * n_segments);
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * n_threads);
+  for (int t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, batch_worker, &c);
+  for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+  fld F = mkfld(p);
+  for (size_t k = 0; k < (size_t)n_segments * p->out_len; k++)
+    enc_fe(&F, c.agg[k], agg_out + k * p->es);
+  free(th);
+  free(c.agg);
+  pthread_mutex_destroy(&c.mu);
+  return 0;
+}
