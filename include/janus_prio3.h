@@ -1,0 +1,149 @@
+/*
+ * janus_prio3.h -- C ABI of the MI355X (gfx950) batched Prio3 helper prepare+aggregate
+ * engine.  This is the drop-in boundary a Janus FFI crate binds.
+ *
+ * It replaces, for a whole aggregation-job batch in one device call:
+ *   - the VDAF part of the helper's per-report loop in
+ *     VdafOps::handle_aggregate_init_generic, /root/reference/aggregator/src/aggregator.rs:2020-2042
+ *     (prio `helper_initialized(verify_key, agg_param, nonce, public_share, input_share,
+ *      inbound)` followed by `PingPongTransition::evaluate`, i.e. prio 0.16.2 Prio3
+ *      prepare_init(agg_id=1) -> decode leader PrepareShare ->
+ *      prepare_shares_to_prepare_message([leader, helper]) -> prepare_next);
+ *   - the per-report accumulate in AggregationJobWriter::
+ *     update_batch_aggregations_from_report_aggregations,
+ *     /root/reference/aggregator/src/aggregator/aggregation_job_writer.rs:591-695
+ *     (BatchAggregation::merged_with -> AggregateShare::merge,
+ *      /root/reference/aggregator_core/src/datastore/models.rs:1318-1372).
+ * The instance it is created for corresponds to one arm of `vdaf_dispatch!`
+ * (/root/reference/core/src/vdaf.rs:198-300): Prio3Count, Prio3Sum{bits},
+ * Prio3SumVec{bits,length,chunk_length}, Prio3Histogram{length,chunk_length}.
+ *
+ * Conventions: plain pointers and sizes, caller-owned buffers, no callbacks.  All
+ * per-report byte strings are fixed-length for a given instance (see prio3_sizes).
+ * A per-report failure never aborts the batch; it is reported in status_out.
+ */
+#ifndef JANUS_PRIO3_H
+#define JANUS_PRIO3_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* VDAF kinds (VdafInstance variants, core/src/vdaf.rs:65-108). */
+enum {
+  PRIO3_COUNT = 0,     /* Prio3::new_count(2)                         (vdaf.rs:201-208) */
+  PRIO3_SUM = 1,       /* Prio3::new_sum(2, bits)                     (vdaf.rs:210-217) */
+  PRIO3_SUMVEC = 2,    /* Prio3::new_sum_vec_multithreaded(2, ...)    (vdaf.rs:219-235) */
+  PRIO3_HISTOGRAM = 3, /* Prio3::new_histogram(2, length, chunk)      (vdaf.rs:257-266) */
+};
+
+/* Per-report status; each maps 1:1 to the PingPongError variant prio returns and to the
+ * metric label Janus records in handle_ping_pong_error
+ * (/root/reference/aggregator/src/aggregator/error.rs:365-428). */
+enum {
+  PRIO3_STATUS_FINISHED = 0,          /* PingPongState::Finished + PingPongMessage::Finish */
+  PRIO3_STATUS_PREP_INIT = 1,         /* VdafPrepareInit -> "prepare_init_failure" */
+  PRIO3_STATUS_PREP_SHARE_DECODE = 2, /* CodecPrepShare -> "leader_prep_share_decode_failure" */
+  PRIO3_STATUS_PREP_MSG = 3,          /* VdafPrepareSharesToPrepareMessage (decide failed) */
+  PRIO3_STATUS_PREP_NEXT = 4,         /* VdafPrepareNext (joint randomness mismatch) */
+  PRIO3_STATUS_PEER_MISMATCH = 5,     /* PeerMessageMismatch (set by the host framing layer) */
+};
+
+/* Whole-call return codes. */
+enum {
+  PRIO3_OK = 0,
+  PRIO3_EINVAL = -1,   /* bad parameters / sizes */
+  PRIO3_EDEVICE = -2,  /* HIP error (device lost, OOM): caller falls back to its CPU path */
+  PRIO3_EUNSUPPORTED = -3,
+};
+
+typedef struct {
+  uint32_t kind;         /* PRIO3_* */
+  uint32_t bits;         /* Sum, SumVec */
+  uint32_t length;       /* SumVec, Histogram */
+  uint32_t chunk_length; /* SumVec, Histogram */
+  uint32_t num_proofs;   /* 1 for every standard Prio3 instance */
+} prio3_params;
+
+typedef struct {
+  uint32_t field_bytes;       /* 8 (Field64) or 16 (Field128) */
+  uint32_t meas_len, out_len, proof_len, verifier_len, joint_rand_len;
+  uint32_t nonce_len;         /* 16 (report ID) */
+  uint32_t public_share_len;  /* 32 with joint randomness, else 0 */
+  uint32_t helper_share_len;  /* 48 with joint randomness, else 32 */
+  uint32_t prep_share_len;    /* leader PrepareShare bytes (verifiers || jr part) */
+  uint32_t prep_msg_len;      /* 16 with joint randomness, else 0 */
+  uint32_t agg_share_len;     /* out_len * field_bytes */
+} prio3_sizes_t;
+
+typedef struct prio3_engine prio3_engine;
+typedef struct prio3_batch prio3_batch;
+
+int prio3_sizes(const prio3_params* params, prio3_sizes_t* out);
+
+/* Created where Janus builds VdafOps for a task (aggregator.rs:880-988): one engine per
+ * (VDAF instance, verify key), bound to one GPU. */
+int prio3_engine_create(const prio3_params* params, const uint8_t verify_key[16], int device,
+                        prio3_engine** out);
+void prio3_engine_destroy(prio3_engine* engine);
+
+/* ---- Host-buffer entry points (what the Rust FFI calls from inside rayon::spawn) ---- */
+
+/* Prepares n reports.  Inputs are packed per report:
+ *   nonces[n][16]  (report IDs), public_shares[n][public_share_len],
+ *   helper_shares[n][helper_share_len], leader_prep_shares[n][prep_share_len]
+ *   (the prep_share of each PingPongMessage::Initialize, framing already removed).
+ * Outputs: prep_msgs_out[n][prep_msg_len] (the Finish message payload) and status_out[n].
+ * The output shares stay on the device inside *batch_out until prio3_accumulate. */
+int prio3_helper_prepare_batch(prio3_engine* engine, uint32_t n, const uint8_t* nonces,
+                               const uint8_t* public_shares, const uint8_t* helper_shares,
+                               const uint8_t* leader_prep_shares, uint8_t* prep_msgs_out,
+                               uint8_t* status_out, prio3_batch** batch_out);
+
+/* Accumulates the finished reports whose accept_mask byte is non-zero (NULL = all) into
+ * per-segment aggregate shares (segment = batch identifier, query_type.rs:72-82).
+ * agg_shares_out[n_segments][agg_share_len] (LE field elements, mod-p sums), counts_out. */
+int prio3_accumulate(prio3_batch* batch, const uint32_t* segment_ids, const uint8_t* accept_mask,
+                     uint32_t n_segments, uint8_t* agg_shares_out, uint64_t* counts_out);
+
+/* Parity-only: copies the n output shares (n x agg_share_len). */
+int prio3_debug_output_shares(prio3_batch* batch, uint8_t* out);
+void prio3_batch_free(prio3_batch* batch);
+
+/* ---- Device-resident entry points (buffers already in HBM; stream-ordered) ---- */
+/* d_* are device pointers with the same packed layouts; stream is a hipStream_t (NULL =
+ * the engine's own stream).  Output shares remain in the engine workspace until the next
+ * prio3_device_prepare on this engine. */
+int prio3_device_prepare(prio3_engine* engine, uint32_t n, const uint8_t* d_nonces,
+                         const uint8_t* d_public_shares, const uint8_t* d_helper_shares,
+                         const uint8_t* d_leader_prep_shares, uint8_t* d_prep_msgs,
+                         uint8_t* d_status, void* stream);
+int prio3_device_accumulate(prio3_engine* engine, uint32_t n, const uint8_t* d_status,
+                            const uint32_t* d_segment_ids, const uint8_t* d_accept_mask,
+                            uint32_t n_segments, uint8_t* d_agg_shares, uint64_t* d_counts,
+                            void* stream);
+/* Copies the output shares of the last device prepare (n x agg_share_len) to host. */
+int prio3_device_output_shares(prio3_engine* engine, uint32_t n, uint8_t* out);
+
+/* Mod-p element-wise sum of k partial aggregate shares (the multi-GPU combine after an
+ * RCCL all-gather; RCCL's integer sum is mod 2^64, not mod p).  d_in[k][n_segments*agg_len],
+ * d_counts_in[k][n_segments] -> d_out[n_segments*agg_len], d_counts_out[n_segments]. */
+int prio3_device_combine(prio3_engine* engine, uint32_t k, uint32_t n_segments,
+                         const uint8_t* d_in, const uint64_t* d_counts_in, uint8_t* d_out,
+                         uint64_t* d_counts_out, void* stream);
+
+/* ---- Test / measurement knobs ---- */
+/* force_slow_path=1 routes every report through the general rejection-sampling kernel. */
+int prio3_engine_set_option(prio3_engine* engine, const char* key, int64_t value);
+/* Per-kernel device time (ms) accumulated since the last reset, measured with HIP events
+ * on the launch stream when option "timing" is 1.  names: comma-separated kernel names. */
+int prio3_engine_timing(prio3_engine* engine, char* names, size_t names_cap, double* ms,
+                        uint64_t* launches, int cap);
+void prio3_engine_timing_reset(prio3_engine* engine);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

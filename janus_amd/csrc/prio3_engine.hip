@@ -1,0 +1,1316 @@
+// prio3_engine.hip -- MI355X (gfx950) batched Prio3 helper prepare+aggregate engine and its
+// C ABI (include/janus_prio3.h).
+//
+// Pipeline for one device call over n reports (one work-item = one report; SoA scratch
+// [element][report] so that every wave-wide load/store is 64 x 16 B contiguous):
+//   k_xof      helper XOF work: query randomness, measurement-share expansion fused with
+//              the joint-randomness-part absorb (one Keccak state squeezes while a second
+//              absorbs the same bytes, 16-bit funnel shifted), proofs-share expansion,
+//              corrected joint-rand seed and joint randomness.  Any rejection-sampling hit
+//              flags the report.                 [prio Prio3::prepare_init, VDAF-08 7.2.2]
+//   k_xof_slow general byte-level sponge with rejection sampling, run only for flagged
+//              reports (probability ~2^-59 per Field128 element, ~2^-32 per Field64 one).
+//   k_query    FLP query (wire polynomials evaluated at t with the Lagrange basis obtained
+//              from one size-P DFT of t-powers, gadget polynomial at the P-th roots from one
+//              folded size-P DFT), decode+add the leader verifier share, decide, prepare
+//              message, joint-rand check, truncate.  [prio FlpGeneric::query/decide,
+//              Prio3::prepare_shares_to_prepare_message, prepare_next]
+//   k_mask/k_acc_partial/k_acc_final  masked, segmented mod-p reduction of the output
+//              shares into per-batch aggregate shares [aggregation_job_writer.rs:591-695].
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/janus_prio3.h"
+#include "prio3_device.h"
+
+#define MAX_ROOTS 20
+
+struct DevParams {
+  uint32_t kind, es, meas_len, out_len, jr_len, arity, calls, P, logP, glen, proof_len,
+      verifier_len, chunk, bits, prep_share_len, helper_share_len, public_share_len;
+  uint32_t n, ld, force_slow;
+  uint32_t vk[4];
+  uint32_t dst[8][2];
+  uint32_t roots128[MAX_ROOTS + 1][4];
+  uint64_t roots64[MAX_ROOTS + 1];
+  uint32_t invP128[4], half128[4];
+  uint64_t invP64, half64;
+};
+
+struct InPtrs {
+  const uint8_t* nonces;
+  const uint8_t* pub;
+  const uint8_t* helper;
+  const uint8_t* leader;
+};
+
+struct Scratch {
+  void* meas;
+  void* proofs;
+  void* jr;
+  void* qr;
+  uint4* part;
+  uint4* corrected;
+  uint8_t* flag;
+  void* Lbuf;
+  void* PVbuf;
+  void* acc;
+  void* out;
+};
+
+struct OutPtrs {
+  uint8_t* prep_msgs;
+  uint8_t* status;
+};
+
+template <class F>
+struct FC;  // per-field constants from DevParams
+template <>
+struct FC<Fp128> {
+  static DEV f128 root(const DevParams& p, int l) { return Fp128::from_words(p.roots128[l]); }
+  static DEV f128 invP(const DevParams& p) { return Fp128::from_words(p.invP128); }
+  static DEV f128 half(const DevParams& p) { return Fp128::from_words(p.half128); }
+};
+template <>
+struct FC<Fp64> {
+  static DEV uint64_t root(const DevParams& p, int l) { return p.roots64[l]; }
+  static DEV uint64_t invP(const DevParams& p) { return p.invP64; }
+  static DEV uint64_t half(const DevParams& p) { return p.half64; }
+};
+
+DEV void load16(const uint8_t* p, uint32_t* w) {
+  uint4 v = *(const uint4*)p;
+  w[0] = v.x;
+  w[1] = v.y;
+  w[2] = v.z;
+  w[3] = v.w;
+}
+
+// ------------------------------------------------------------------------------------
+// k_xof: fast path (no rejection)
+// ------------------------------------------------------------------------------------
+template <class F>
+DEV void put_elem(const DevParams& p, void* base, uint32_t idx, uint32_t r, const uint32_t* w,
+                  uint32_t& flag) {
+  typename F::T x = F::from_words(w);
+  if (!F::lt_p(x)) flag = 1;
+  F::store(base, (size_t)idx * p.ld + r, x);
+}
+
+// Elements contained in squeeze block b of an XOF stream (no rejection).
+template <class F>
+DEV void squeeze_block(const DevParams& p, const KState& s, uint32_t b, uint32_t n_elems,
+                       uint32_t& pend0, uint32_t& pend1, void* base, uint32_t r,
+                       uint32_t& flag) {
+  if constexpr (F::ES == 16) {
+    uint32_t e0 = 21 * (b >> 1);
+    if ((b & 1) == 0) {
+#pragma unroll
+      for (int t = 0; t < 10; t++) {
+        uint32_t w[4] = {kword(s, 4 * t), kword(s, 4 * t + 1), kword(s, 4 * t + 2),
+                         kword(s, 4 * t + 3)};
+        if (e0 + t < n_elems) put_elem<F>(p, base, e0 + t, r, w, flag);
+      }
+      pend0 = kword(s, 40);
+      pend1 = kword(s, 41);
+    } else {
+      {
+        uint32_t w[4] = {pend0, pend1, kword(s, 0), kword(s, 1)};
+        if (e0 + 10 < n_elems) put_elem<F>(p, base, e0 + 10, r, w, flag);
+      }
+#pragma unroll
+      for (int t = 0; t < 10; t++) {
+        uint32_t w[4] = {kword(s, 2 + 4 * t), kword(s, 3 + 4 * t), kword(s, 4 + 4 * t),
+                         kword(s, 5 + 4 * t)};
+        if (e0 + 11 + t < n_elems) put_elem<F>(p, base, e0 + 11 + t, r, w, flag);
+      }
+    }
+  } else {
+    uint32_t e0 = 21 * b;
+#pragma unroll
+    for (int t = 0; t < 21; t++) {
+      uint32_t w[2] = {kword(s, 2 * t), kword(s, 2 * t + 1)};
+      if (e0 + t < n_elems) put_elem<F>(p, base, e0 + t, r, w, flag);
+    }
+  }
+}
+
+template <class F>
+__global__ __launch_bounds__(256) void k_xof(DevParams p, InPtrs in, Scratch sc) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= p.n) return;
+  constexpr uint32_t ES = F::ES;
+  uint32_t flag = p.force_slow;
+  uint32_t nonce[4], km[4], kp[4], kb[4] = {0, 0, 0, 0};
+  load16(in.nonces + 16 * (size_t)r, nonce);
+  const uint8_t* hs = in.helper + (size_t)r * p.helper_share_len;
+  load16(hs, km);
+  load16(hs + 16, kp);
+  const bool JR = p.jr_len > 0;
+  if (JR) load16(hs + 32, kb);
+
+  // 1. query randomness: XOF(vk, dst(5), [PROOFS] || nonce), one element
+  {
+    KState s;
+    kzero(s);
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[5]);
+    msg_bytes16(m, 9, p.vk);
+    msg_byte(m, 25, 1);
+    msg_bytes16(m, 26, nonce);
+    msg_absorb_final(s, m, 42);
+    uint32_t w[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
+    put_elem<F>(p, sc.qr, 0, r, w, flag);
+  }
+
+  // 2. measurement share XOF(k_meas, dst(1), [1]) fused with the joint-rand part
+  //    XOF(k_blind, dst(7), [1] || nonce || enc(meas)).
+  KState ms;
+  kzero(ms);
+  {
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[1]);
+    msg_bytes16(m, 9, km);
+    msg_byte(m, 25, 1);
+    msg_absorb_final(ms, m, 26);
+  }
+  const uint32_t M = p.meas_len;
+  const uint32_t mbytes = M * ES;
+  const uint32_t K = (mbytes + 167) / 168;
+  const uint32_t L = 42 + mbytes;
+  const uint32_t B = L / 168, rem = L % 168;
+  KState js;
+  uint32_t pre[11], tail[11];
+  uint32_t part[4] = {0, 0, 0, 0};
+  if (JR) {
+    kzero(js);
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[7]);
+    msg_bytes16(m, 9, kb);
+    msg_byte(m, 25, 1);
+    msg_bytes16(m, 26, nonce);
+#pragma unroll
+    for (int j = 0; j < 11; j++) pre[j] = m.w[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 11; j++) tail[j] = 0;
+  uint32_t pend0 = 0, pend1 = 0;
+  const uint32_t nb = JR ? B + 1 : K;
+  for (uint32_t b = 0; b < nb; b++) {
+    const bool hasW = b < K;
+    if (hasW) squeeze_block<F>(p, ms, b, M, pend0, pend1, sc.meas, r, flag);
+    if (JR) {
+      uint32_t x[42];
+#pragma unroll
+      for (int j = 0; j < 10; j++)
+        x[j] = b == 0 ? pre[j] : __builtin_amdgcn_alignbit(tail[j + 1], tail[j], 16);
+      uint32_t w0 = hasW ? kword(ms, 0) : 0u;
+      x[10] = b == 0 ? ((pre[10] & 0xffffu) | (w0 << 16))
+                     : __builtin_amdgcn_alignbit(w0, tail[10], 16);
+#pragma unroll
+      for (int j = 11; j < 42; j++)
+        x[j] = hasW ? __builtin_amdgcn_alignbit(kword(ms, j - 10), kword(ms, j - 11), 16) : 0u;
+      if (b < B) {
+#pragma unroll
+        for (int j = 0; j < 42; j++) kxor_word(js, j, x[j]);
+        keccak_p12(js);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 42; j++) {
+          const uint32_t lo = 4 * j;
+          uint32_t mask = (lo + 4 <= rem) ? 0xffffffffu
+                                          : (lo >= rem ? 0u : ((1u << (8 * (rem - lo))) - 1u));
+          x[j] &= mask;
+          if ((uint32_t)j == (rem >> 2)) x[j] ^= 1u << (8 * (rem & 3));
+        }
+        x[41] ^= 0x80000000u;
+#pragma unroll
+        for (int j = 0; j < 42; j++) kxor_word(js, j, x[j]);
+        keccak_p12(js);
+        part[0] = kword(js, 0);
+        part[1] = kword(js, 1);
+        part[2] = kword(js, 2);
+        part[3] = kword(js, 3);
+      }
+    }
+    if (hasW) {
+#pragma unroll
+      for (int t = 0; t < 11; t++) tail[t] = kword(ms, 31 + t);
+    }
+    if (b + 1 < K) keccak_p12(ms);
+  }
+
+  // 3. proofs share XOF(k_proofs, dst(2), [PROOFS, 1])
+  {
+    KState s;
+    kzero(s);
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[2]);
+    msg_bytes16(m, 9, kp);
+    msg_byte(m, 25, 1);
+    msg_byte(m, 26, 1);
+    msg_absorb_final(s, m, 27);
+    const uint32_t PL = p.proof_len;
+    const uint32_t Kp = (PL * ES + 167) / 168;
+    uint32_t q0 = 0, q1 = 0;
+    for (uint32_t b = 0; b < Kp; b++) {
+      squeeze_block<F>(p, s, b, PL, q0, q1, sc.proofs, r, flag);
+      if (b + 1 < Kp) keccak_p12(s);
+    }
+  }
+
+  // 4. corrected joint-rand seed and joint randomness
+  if (JR) {
+    uint32_t pub0[4];
+    load16(in.pub + (size_t)r * p.public_share_len, pub0);
+    KState s;
+    kzero(s);
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[6]);
+    msg_bytes16(m, 25, pub0);
+    msg_bytes16(m, 41, part);
+    msg_absorb_final(s, m, 57);
+    uint32_t cor[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
+    KState t;
+    kzero(t);
+    Msg m2;
+    msg_zero(m2);
+    msg_dst(m2, p.dst[3]);
+    msg_bytes16(m2, 9, cor);
+    msg_byte(m2, 25, 1);
+    msg_absorb_final(t, m2, 26);
+    uint32_t q0 = 0, q1 = 0;
+    squeeze_block<F>(p, t, 0, p.jr_len, q0, q1, sc.jr, r, flag);
+    sc.part[r] = make_uint4(part[0], part[1], part[2], part[3]);
+    sc.corrected[r] = make_uint4(cor[0], cor[1], cor[2], cor[3]);
+  }
+  sc.flag[r] = (uint8_t)flag;
+}
+
+// ------------------------------------------------------------------------------------
+// k_xof_slow: general byte-level sponge with rejection sampling (flagged reports only)
+// ------------------------------------------------------------------------------------
+struct BX {
+  KState s;
+  uint8_t buf[168];
+  uint32_t pos;
+};
+DEV void bx_xor_block(BX& x) {
+#pragma unroll
+  for (int w = 0; w < 42; w++) {
+    uint32_t v = (uint32_t)x.buf[4 * w] | ((uint32_t)x.buf[4 * w + 1] << 8) |
+                 ((uint32_t)x.buf[4 * w + 2] << 16) | ((uint32_t)x.buf[4 * w + 3] << 24);
+    kxor_word(x.s, w, v);
+  }
+  keccak_p12(x.s);
+}
+DEV void bx_fill(BX& x) {
+#pragma unroll
+  for (int w = 0; w < 42; w++) {
+    uint32_t v = kword(x.s, w);
+    x.buf[4 * w] = v;
+    x.buf[4 * w + 1] = v >> 8;
+    x.buf[4 * w + 2] = v >> 16;
+    x.buf[4 * w + 3] = v >> 24;
+  }
+  x.pos = 0;
+}
+DEV void bx_absorb(BX& x, uint8_t b) {
+  x.buf[x.pos++] = b;
+  if (x.pos == 168) {
+    bx_xor_block(x);
+    x.pos = 0;
+  }
+}
+DEV void bx_absorb_w(BX& x, const uint32_t* w, int nbytes) {
+  for (int i = 0; i < nbytes; i++) bx_absorb(x, (uint8_t)(w[i >> 2] >> (8 * (i & 3))));
+}
+DEV void bx_init(BX& x, const uint32_t* dst2, const uint32_t* seed) {
+  kzero(x.s);
+  x.pos = 0;
+  bx_absorb(x, 8);
+  bx_absorb_w(x, dst2, 8);
+  bx_absorb_w(x, seed, 16);
+}
+DEV void bx_finalize(BX& x) {
+  for (uint32_t i = x.pos; i < 168; i++) x.buf[i] = 0;
+  x.buf[x.pos] ^= 0x01;
+  x.buf[167] ^= 0x80;
+  bx_xor_block(x);
+  bx_fill(x);
+}
+DEV uint8_t bx_squeeze(BX& x) {
+  if (x.pos == 168) {
+    keccak_p12(x.s);
+    bx_fill(x);
+  }
+  return x.buf[x.pos++];
+}
+// next accepted element (rejection sampling); writes ES/4 words
+template <class F>
+DEV void bx_next_elem(BX& x, uint32_t* w) {
+  for (;;) {
+    for (int k = 0; k < F::ES / 4; k++) {
+      uint32_t v = 0;
+      for (int b = 0; b < 4; b++) v |= (uint32_t)bx_squeeze(x) << (8 * b);
+      w[k] = v;
+    }
+    if (F::lt_p(F::from_words(w))) return;
+  }
+}
+
+template <class F>
+__global__ __launch_bounds__(64) void k_xof_slow(DevParams p, InPtrs in, Scratch sc) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= p.n || sc.flag[r] == 0) return;
+  uint32_t nonce[4], km[4], kp[4], kb[4] = {0, 0, 0, 0};
+  load16(in.nonces + 16 * (size_t)r, nonce);
+  const uint8_t* hs = in.helper + (size_t)r * p.helper_share_len;
+  load16(hs, km);
+  load16(hs + 16, kp);
+  const bool JR = p.jr_len > 0;
+  if (JR) load16(hs + 32, kb);
+  uint32_t w[4];
+  BX x, y;
+  // query rand
+  bx_init(x, p.dst[5], p.vk);
+  bx_absorb(x, 1);
+  bx_absorb_w(x, nonce, 16);
+  bx_finalize(x);
+  bx_next_elem<F>(x, w);
+  F::store(sc.qr, r, F::from_words(w));
+  // meas + jr part
+  bx_init(x, p.dst[1], km);
+  bx_absorb(x, 1);
+  bx_finalize(x);
+  if (JR) {
+    bx_init(y, p.dst[7], kb);
+    bx_absorb(y, 1);
+    bx_absorb_w(y, nonce, 16);
+  }
+  for (uint32_t i = 0; i < p.meas_len; i++) {
+    bx_next_elem<F>(x, w);
+    F::store(sc.meas, (size_t)i * p.ld + r, F::from_words(w));
+    if (JR) bx_absorb_w(y, w, F::ES);
+  }
+  uint32_t part[4] = {0, 0, 0, 0};
+  if (JR) {
+    bx_finalize(y);
+    for (int k = 0; k < 4; k++) {
+      uint32_t v = 0;
+      for (int b = 0; b < 4; b++) v |= (uint32_t)bx_squeeze(y) << (8 * b);
+      part[k] = v;
+    }
+  }
+  // proofs
+  bx_init(x, p.dst[2], kp);
+  bx_absorb(x, 1);
+  bx_absorb(x, 1);
+  bx_finalize(x);
+  for (uint32_t i = 0; i < p.proof_len; i++) {
+    bx_next_elem<F>(x, w);
+    F::store(sc.proofs, (size_t)i * p.ld + r, F::from_words(w));
+  }
+  if (JR) {
+    uint32_t pub0[4], zero[4] = {0, 0, 0, 0}, cor[4];
+    load16(in.pub + (size_t)r * p.public_share_len, pub0);
+    bx_init(x, p.dst[6], zero);
+    bx_absorb_w(x, pub0, 16);
+    bx_absorb_w(x, part, 16);
+    bx_finalize(x);
+    for (int k = 0; k < 4; k++) {
+      uint32_t v = 0;
+      for (int b = 0; b < 4; b++) v |= (uint32_t)bx_squeeze(x) << (8 * b);
+      cor[k] = v;
+    }
+    bx_init(y, p.dst[3], cor);
+    bx_absorb(y, 1);
+    bx_finalize(y);
+    for (uint32_t i = 0; i < p.jr_len; i++) {
+      bx_next_elem<F>(y, w);
+      F::store(sc.jr, (size_t)i * p.ld + r, F::from_words(w));
+    }
+    sc.part[r] = make_uint4(part[0], part[1], part[2], part[3]);
+    sc.corrected[r] = make_uint4(cor[0], cor[1], cor[2], cor[3]);
+  }
+  sc.flag[r] = 0;
+}
+
+// ------------------------------------------------------------------------------------
+// k_query: FLP query + decide + prepare message + prepare_next + truncate
+// ------------------------------------------------------------------------------------
+DEV uint32_t bitrev(uint32_t x, uint32_t d) { return __builtin_bitreverse32(x) >> (32 - d); }
+
+template <class F>
+DEV void dft_lane(const DevParams& p, void* buf, uint32_t r) {
+  typedef typename F::T T;
+  const size_t ld = p.ld;
+  for (uint32_t l = 1; l <= p.logP; l++) {
+    const uint32_t half = 1u << (l - 1);
+    const T wl = FC<F>::root(p, l);
+    T w = F::one();
+    for (uint32_t i = 0; i < half; i++) {
+      for (uint32_t j = i; j < p.P; j += 2 * half) {
+        T u = F::load(buf, (size_t)j * ld + r);
+        T v = F::mul(w, F::load(buf, (size_t)(j + half) * ld + r));
+        F::store(buf, (size_t)j * ld + r, F::add(u, v));
+        F::store(buf, (size_t)(j + half) * ld + r, F::sub(u, v));
+      }
+      w = F::mul(w, wl);
+    }
+  }
+}
+
+template <class F>
+DEV typename F::T ldf(const void* base, uint32_t e, size_t ld, uint32_t r) {
+  return F::load(base, (size_t)e * ld + r);
+}
+
+template <class F>
+__global__ __launch_bounds__(256) void k_query(DevParams p, InPtrs in, Scratch sc, OutPtrs out) {
+  typedef typename F::T T;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= p.n) return;
+  const size_t ld = p.ld;
+  const uint32_t P = p.P, A = p.arity;
+  uint8_t status = PRIO3_STATUS_FINISHED;
+  const T t = ldf<F>(sc.qr, 0, ld, r);
+  T tp = t;
+  for (uint32_t l = 0; l < p.logP; l++) tp = F::mul(tp, tp);
+  if (F::eq(tp, F::one())) {
+    status = PRIO3_STATUS_PREP_INIT;
+  }
+  // Lagrange basis at t: L_c = (1/P) sum_e t^e alpha^(-ce) = DFT(t^e / P)[(P - c) mod P]
+  {
+    T pw = FC<F>::invP(p);
+    for (uint32_t e = 0; e < P; e++) {
+      F::store(sc.Lbuf, (size_t)bitrev(e, p.logP) * ld + r, pw);
+      pw = F::mul(pw, t);
+    }
+    dft_lane<F>(p, sc.Lbuf, r);
+  }
+  // gadget polynomial at the P-th roots: fold coefficients mod x^P - 1, DFT
+  for (uint32_t e = 0; e < P; e++) {
+    T q = ldf<F>(sc.proofs, A + e, ld, r);
+    if (e + P < p.glen) q = F::add(q, ldf<F>(sc.proofs, A + e + P, ld, r));
+    F::store(sc.PVbuf, (size_t)bitrev(e, p.logP) * ld + r, q);
+  }
+  dft_lane<F>(p, sc.PVbuf, r);
+  // p(t)
+  T pt = F::zero();
+  for (uint32_t e = p.glen; e-- > 0;) pt = F::add(F::mul(pt, t), ldf<F>(sc.proofs, A + e, ld, r));
+  auto Lc = [&](uint32_t c) { return ldf<F>(sc.Lbuf, (P - c) & (P - 1), ld, r); };
+  // wire accumulators start from the proof's wire seeds
+  {
+    const T L0 = Lc(0);
+    for (uint32_t w = 0; w < A; w++)
+      F::store(sc.acc, (size_t)w * ld + r, F::mul(ldf<F>(sc.proofs, w, ld, r), L0));
+  }
+  auto acc_add = [&](uint32_t w, const T& v) {
+    size_t idx = (size_t)w * ld + r;
+    F::store(sc.acc, idx, F::add(F::load(sc.acc, idx), v));
+  };
+  T v = F::zero();
+  if (p.kind == PRIO3_COUNT) {
+    const T m = ldf<F>(sc.meas, 0, ld, r);
+    const T x = F::mul(m, Lc(1));
+    acc_add(0, x);
+    acc_add(1, x);
+    v = F::sub(ldf<F>(sc.PVbuf, 1, ld, r), m);
+  } else if (p.kind == PRIO3_SUM) {
+    const T r0 = ldf<F>(sc.jr, 0, ld, r);
+    T rp = r0;
+    for (uint32_t i = 0; i < p.meas_len; i++) {
+      acc_add(0, F::mul(ldf<F>(sc.meas, i, ld, r), Lc(i + 1)));
+      v = F::add(v, F::mul(rp, ldf<F>(sc.PVbuf, i + 1, ld, r)));
+      rp = F::mul(rp, r0);
+    }
+  } else {
+    const T r0 = ldf<F>(sc.jr, 0, ld, r);
+    const T half = FC<F>::half(p);
+    T rp = r0, range = F::zero(), sum = F::zero();
+    for (uint32_t k = 0; k < p.calls; k++) {
+      const T L = Lc(k + 1);
+      for (uint32_t j = 0; j < p.chunk; j++) {
+        const uint32_t i = k * p.chunk + j;
+        const T m = i < p.meas_len ? ldf<F>(sc.meas, i, ld, r) : F::zero();
+        acc_add(2 * j, F::mul(F::mul(rp, m), L));
+        acc_add(2 * j + 1, F::mul(F::sub(m, half), L));
+        rp = F::mul(rp, r0);
+        sum = F::add(sum, m);
+      }
+      range = F::add(range, ldf<F>(sc.PVbuf, k + 1, ld, r));
+    }
+    if (p.kind == PRIO3_SUMVEC) {
+      v = range;
+    } else {
+      const T r1 = ldf<F>(sc.jr, 1, ld, r);
+      v = F::add(F::mul(r1, range), F::mul(F::mul(r1, r1), F::sub(sum, half)));
+    }
+  }
+  // combine with the leader's verifier share and decide
+  const uint8_t* lps = in.leader + (size_t)r * p.prep_share_len;
+  bool decode_ok = true;
+  auto lv = [&](uint32_t e) {
+    T x = F::load(lps, e);
+    if (!F::lt_p(x)) decode_ok = false;
+    return x;
+  };
+  const T V0 = F::add(lv(0), v);
+  T G = F::zero();
+  if (p.kind == PRIO3_COUNT) {
+    T a = F::add(lv(1), F::load(sc.acc, 0 * ld + r));
+    T b = F::add(lv(2), F::load(sc.acc, 1 * ld + r));
+    G = F::mul(a, b);
+  } else if (p.kind == PRIO3_SUM) {
+    T a = F::add(lv(1), F::load(sc.acc, r));
+    G = F::sub(F::mul(a, a), a);
+  } else {
+    for (uint32_t j = 0; j < p.chunk; j++) {
+      T a = F::add(lv(1 + 2 * j), F::load(sc.acc, (size_t)(2 * j) * ld + r));
+      T b = F::add(lv(2 + 2 * j), F::load(sc.acc, (size_t)(2 * j + 1) * ld + r));
+      G = F::add(G, F::mul(a, b));
+    }
+  }
+  const T PT = F::add(lv(A + 1), pt);
+  if (status == PRIO3_STATUS_FINISHED) {
+    if (!decode_ok)
+      status = PRIO3_STATUS_PREP_SHARE_DECODE;
+    else if (!F::is_zero(V0) || !F::eq(G, PT))
+      status = PRIO3_STATUS_PREP_MSG;
+  }
+  uint32_t msg[4] = {0, 0, 0, 0};
+  if (p.jr_len > 0) {
+    uint32_t lpart[4], hpart[4];
+    load16(lps + (size_t)p.verifier_len * F::ES, lpart);
+    uint4 hp = sc.part[r];
+    hpart[0] = hp.x;
+    hpart[1] = hp.y;
+    hpart[2] = hp.z;
+    hpart[3] = hp.w;
+    KState s;
+    kzero(s);
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[6]);
+    msg_bytes16(m, 25, lpart);
+    msg_bytes16(m, 41, hpart);
+    msg_absorb_final(s, m, 57);
+    uint4 cor = sc.corrected[r];
+    msg[0] = kword(s, 0);
+    msg[1] = kword(s, 1);
+    msg[2] = kword(s, 2);
+    msg[3] = kword(s, 3);
+    if (status == PRIO3_STATUS_FINISHED &&
+        (msg[0] != cor.x || msg[1] != cor.y || msg[2] != cor.z || msg[3] != cor.w))
+      status = PRIO3_STATUS_PREP_NEXT;
+    if (status != PRIO3_STATUS_FINISHED) msg[0] = msg[1] = msg[2] = msg[3] = 0;
+    ((uint4*)out.prep_msgs)[r] = make_uint4(msg[0], msg[1], msg[2], msg[3]);
+  }
+  out.status[r] = status;
+  // truncate (Count/Histogram: identity, read straight from the meas scratch)
+  if (p.kind == PRIO3_SUM) {
+    T acc = F::zero(), pw = F::one();
+    for (uint32_t i = 0; i < p.meas_len; i++) {
+      acc = F::add(acc, F::mul(pw, ldf<F>(sc.meas, i, ld, r)));
+      pw = F::add(pw, pw);
+    }
+    F::store(sc.out, r, acc);
+  } else if (p.kind == PRIO3_SUMVEC) {
+    for (uint32_t e = 0; e < p.out_len; e++) {
+      T acc = F::zero(), pw = F::one();
+      for (uint32_t b = 0; b < p.bits; b++) {
+        acc = F::add(acc, F::mul(pw, ldf<F>(sc.meas, e * p.bits + b, ld, r)));
+        pw = F::add(pw, pw);
+      }
+      F::store(sc.out, (size_t)e * ld + r, acc);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Accumulate: masked segmented mod-p reduction of output shares
+// ------------------------------------------------------------------------------------
+__global__ void k_mask(uint32_t n, const uint8_t* status, const uint32_t* seg,
+                       const uint8_t* accept, uint32_t s, uint8_t* mask) {
+  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  bool ok = status[r] == PRIO3_STATUS_FINISHED;
+  if (seg) ok = ok && seg[r] == s;
+  if (accept) ok = ok && accept[r] != 0;
+  mask[r] = ok ? 1 : 0;
+}
+
+// grid: x = output element, y = report chunk.  Block of 256 sums its chunk of the row.
+template <class F>
+__global__ __launch_bounds__(256) void k_acc_partial(uint32_t n, size_t ld, uint32_t chunk,
+                                                     uint32_t out_len, const void* src,
+                                                     const uint8_t* mask, void* partial,
+                                                     uint64_t* pcount) {
+  typedef typename F::T T;
+  __shared__ T red[256];
+  __shared__ uint32_t cred[256];
+  const uint32_t e = blockIdx.x, c = blockIdx.y;
+  const uint32_t lo = c * chunk, hi = min(n, lo + chunk);
+  T acc = F::zero();
+  uint32_t cnt = 0;
+  for (uint32_t r = lo + threadIdx.x; r < hi; r += 256) {
+    if (mask[r]) {
+      acc = F::add(acc, F::load(src, (size_t)e * ld + r));
+      cnt++;
+    }
+  }
+  red[threadIdx.x] = acc;
+  cred[threadIdx.x] = cnt;
+  __syncthreads();
+  for (uint32_t s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      red[threadIdx.x] = F::add(red[threadIdx.x], red[threadIdx.x + s]);
+      cred[threadIdx.x] += cred[threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    F::store(partial, (size_t)c * out_len + e, red[0]);
+    if (e == 0) pcount[c] = cred[0];
+  }
+}
+
+template <class F>
+__global__ void k_acc_final(uint32_t nchunks, uint32_t out_len, const void* partial,
+                            const uint64_t* pcount, uint8_t* agg, uint64_t* count) {
+  typedef typename F::T T;
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < out_len) {
+    T acc = F::zero();
+    for (uint32_t c = 0; c < nchunks; c++)
+      acc = F::add(acc, F::load(partial, (size_t)c * out_len + e));
+    F::store(agg, e, acc);
+  }
+  if (e == 0) {
+    uint64_t s = 0;
+    for (uint32_t c = 0; c < nchunks; c++) s += pcount[c];
+    *count = s;
+  }
+}
+
+// sum of k partial aggregates (multi-GPU combine)
+template <class F>
+__global__ void k_combine(uint32_t k, uint32_t len, uint32_t n_segments, const uint8_t* in,
+                          const uint64_t* cin, uint8_t* out, uint64_t* cout) {
+  typedef typename F::T T;
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < len) {
+    T acc = F::zero();
+    for (uint32_t i = 0; i < k; i++) acc = F::add(acc, F::load(in, (size_t)i * len + e));
+    F::store(out, e, acc);
+  }
+  if (e < n_segments) {
+    uint64_t s = 0;
+    for (uint32_t i = 0; i < k; i++) s += cin[(size_t)i * n_segments + e];
+    cout[e] = s;
+  }
+}
+
+// ====================================================================================
+// Host side
+// ====================================================================================
+namespace {
+
+typedef unsigned __int128 u128;
+const u128 HP128 = (((u128)0xffffffffffffffe4ULL) << 64) | 1;
+const uint64_t HP64 = 0xffffffff00000001ULL;
+
+u128 hmul(u128 a, u128 b, u128 p) {  // slow but simple: double-and-add
+  u128 r = 0;
+  a %= p;
+  while (b) {
+    if (b & 1) {
+      r += a;
+      if (r < a || r >= p) r -= p;
+    }
+    u128 a2 = a + a;
+    if (a2 < a || a2 >= p) a2 -= p;
+    a = a2;
+    b >>= 1;
+  }
+  return r;
+}
+u128 hpow(u128 a, u128 e, u128 p) {
+  u128 r = 1;
+  while (e) {
+    if (e & 1) r = hmul(r, a, p);
+    a = hmul(a, a, p);
+    e >>= 1;
+  }
+  return r;
+}
+
+struct KTime {
+  std::string name;
+  double ms = 0;
+  uint64_t launches = 0;
+};
+
+}  // namespace
+
+struct prio3_engine {
+  prio3_params params;
+  prio3_sizes_t sz;
+  DevParams dp;
+  int device;
+  hipStream_t stream;
+  uint32_t cap = 0;  // scratch capacity (reports)
+  Scratch sc{};
+  void* d_prep_partial = nullptr;
+  size_t partial_cap = 0;
+  uint64_t* d_pcount = nullptr;
+  uint8_t* d_mask = nullptr;
+  // host-API staging
+  uint32_t io_cap = 0;
+  uint8_t *d_nonces = nullptr, *d_pub = nullptr, *d_helper = nullptr, *d_leader = nullptr,
+          *d_msgs = nullptr, *d_status = nullptr;
+  int force_slow = 0;
+  int timing = 0;
+  std::vector<KTime> times;
+  std::vector<hipEvent_t> ev_pool;
+  std::mutex mu;
+};
+
+struct prio3_batch {
+  prio3_engine* e;
+  uint32_t n;
+};
+
+static uint32_t next_pow2(uint32_t n) {
+  uint32_t p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+static int fill_sizes(const prio3_params* pp, prio3_sizes_t* s, DevParams* dp) {
+  if (!pp) return PRIO3_EINVAL;
+  uint32_t proofs = pp->num_proofs ? pp->num_proofs : 1;
+  if (proofs != 1) return PRIO3_EUNSUPPORTED;
+  DevParams d;
+  memset(&d, 0, sizeof d);
+  d.kind = pp->kind;
+  d.bits = pp->bits;
+  d.chunk = pp->chunk_length;
+  uint32_t algo;
+  switch (pp->kind) {
+    case PRIO3_COUNT:
+      algo = 0;
+      d.es = 8;
+      d.meas_len = 1;
+      d.out_len = 1;
+      d.jr_len = 0;
+      d.arity = 2;
+      d.calls = 1;
+      break;
+    case PRIO3_SUM:
+      if (pp->bits == 0 || pp->bits > 64) return PRIO3_EINVAL;
+      algo = 1;
+      d.es = 16;
+      d.meas_len = pp->bits;
+      d.out_len = 1;
+      d.jr_len = 1;
+      d.arity = 1;
+      d.calls = pp->bits;
+      break;
+    case PRIO3_SUMVEC:
+      if (pp->bits == 0 || pp->bits > 64 || pp->length == 0 || pp->chunk_length == 0)
+        return PRIO3_EINVAL;
+      algo = 2;
+      d.es = 16;
+      d.meas_len = pp->bits * pp->length;
+      d.out_len = pp->length;
+      d.jr_len = 1;
+      d.arity = 2 * pp->chunk_length;
+      d.calls = (d.meas_len + pp->chunk_length - 1) / pp->chunk_length;
+      break;
+    case PRIO3_HISTOGRAM:
+      if (pp->length == 0 || pp->chunk_length == 0) return PRIO3_EINVAL;
+      algo = 3;
+      d.es = 16;
+      d.meas_len = pp->length;
+      d.out_len = pp->length;
+      d.jr_len = 2;
+      d.arity = 2 * pp->chunk_length;
+      d.calls = (pp->length + pp->chunk_length - 1) / pp->chunk_length;
+      break;
+    default:
+      return PRIO3_EINVAL;
+  }
+  d.P = next_pow2(1 + d.calls);
+  d.logP = 0;
+  while ((1u << d.logP) < d.P) d.logP++;
+  if (d.logP > MAX_ROOTS) return PRIO3_EUNSUPPORTED;
+  d.glen = 2 * (d.P - 1) + 1;
+  d.proof_len = d.arity + d.glen;
+  d.verifier_len = d.arity + 2;
+  d.helper_share_len = d.jr_len ? 48 : 32;
+  d.public_share_len = d.jr_len ? 32 : 0;
+  d.prep_share_len = d.verifier_len * d.es + (d.jr_len ? 16 : 0);
+  for (uint32_t u = 1; u <= 7; u++) {
+    uint8_t b[8] = {8, 0, (uint8_t)(algo >> 24), (uint8_t)(algo >> 16), (uint8_t)(algo >> 8),
+                    (uint8_t)algo, 0, (uint8_t)u};
+    memcpy(d.dst[u], b, 8);
+  }
+  // roots and constants
+  {
+    u128 g128 = 0;
+    for (const char* c = "145091266659756586618791329697897684742"; *c; c++)
+      g128 = g128 * 10 + (u128)(*c - '0');
+    uint64_t g64 = 1753635133440165772ULL;
+    for (int l = 0; l <= MAX_ROOTS; l++) {
+      u128 r = g128;
+      for (int i = 0; i < 66 - l; i++) r = hmul(r, r, HP128);
+      for (int k = 0; k < 4; k++) d.roots128[l][k] = (uint32_t)(r >> (32 * k));
+      u128 r64 = g64;
+      for (int i = 0; i < 32 - l; i++) r64 = hmul(r64, r64, HP64);
+      d.roots64[l] = (uint64_t)r64;
+    }
+    u128 ip = hpow(d.P, HP128 - 2, HP128), h = hpow(2, HP128 - 2, HP128);
+    for (int k = 0; k < 4; k++) {
+      d.invP128[k] = (uint32_t)(ip >> (32 * k));
+      d.half128[k] = (uint32_t)(h >> (32 * k));
+    }
+    d.invP64 = (uint64_t)hpow(d.P, HP64 - 2, HP64);
+    d.half64 = (uint64_t)hpow(2, HP64 - 2, HP64);
+  }
+  if (s) {
+    s->field_bytes = d.es;
+    s->meas_len = d.meas_len;
+    s->out_len = d.out_len;
+    s->proof_len = d.proof_len;
+    s->verifier_len = d.verifier_len;
+    s->joint_rand_len = d.jr_len;
+    s->nonce_len = 16;
+    s->public_share_len = d.public_share_len;
+    s->helper_share_len = d.helper_share_len;
+    s->prep_share_len = d.prep_share_len;
+    s->prep_msg_len = d.jr_len ? 16 : 0;
+    s->agg_share_len = d.out_len * d.es;
+  }
+  if (dp) *dp = d;
+  return PRIO3_OK;
+}
+
+#define HIPCHK(x)                                                                   \
+  do {                                                                              \
+    hipError_t _e = (x);                                                            \
+    if (_e != hipSuccess) {                                                         \
+      fprintf(stderr, "janus_prio3: HIP error %s at %s:%d\n", hipGetErrorString(_e), \
+              __FILE__, __LINE__);                                                  \
+      return PRIO3_EDEVICE;                                                         \
+    }                                                                               \
+  } while (0)
+
+static int ensure_scratch(prio3_engine* e, uint32_t n) {
+  if (n <= e->cap) return PRIO3_OK;
+  uint32_t ld = (n + 63) & ~63u;
+  const DevParams& d = e->dp;
+  size_t es = d.es;
+  void** bufs[] = {&e->sc.meas, &e->sc.proofs, &e->sc.jr, &e->sc.qr, (void**)&e->sc.part,
+                   (void**)&e->sc.corrected, (void**)&e->sc.flag, &e->sc.Lbuf, &e->sc.PVbuf,
+                   &e->sc.acc, &e->sc.out, (void**)&e->d_mask};
+  for (auto b : bufs)
+    if (*b) {
+      (void)hipFree(*b);
+      *b = nullptr;
+    }
+  size_t sizes[] = {es * d.meas_len * ld, es * d.proof_len * ld, es * (d.jr_len ? d.jr_len : 1) * ld,
+                    es * ld, 16 * (size_t)ld, 16 * (size_t)ld, (size_t)ld, es * d.P * ld,
+                    es * d.P * ld, es * d.arity * ld,
+                    (d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC) ? es * d.out_len * ld : 16,
+                    (size_t)ld};
+  for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]); i++) HIPCHK(hipMalloc(bufs[i], sizes[i]));
+  e->cap = ld;
+  e->dp.ld = ld;
+  return PRIO3_OK;
+}
+
+static hipEvent_t get_event(prio3_engine* e) {
+  hipEvent_t ev;
+  (void)hipEventCreate(&ev);
+  e->ev_pool.push_back(ev);
+  return ev;
+}
+
+// launch wrapper that optionally brackets the kernel with events
+struct Pending {
+  size_t idx;
+  hipEvent_t a, b;
+};
+static std::vector<Pending>& pending(prio3_engine* e) {
+  static thread_local std::vector<Pending> v;
+  (void)e;
+  return v;
+}
+static size_t time_slot(prio3_engine* e, const char* name) {
+  for (size_t i = 0; i < e->times.size(); i++)
+    if (e->times[i].name == name) return i;
+  e->times.push_back(KTime{name, 0, 0});
+  return e->times.size() - 1;
+}
+#define TIMED(e, st, name, launch)                            \
+  do {                                                        \
+    hipEvent_t _a = nullptr, _b = nullptr;                    \
+    if ((e)->timing) {                                        \
+      _a = get_event(e);                                      \
+      _b = get_event(e);                                      \
+      (void)hipEventRecord(_a, st);                           \
+    }                                                         \
+    launch;                                                   \
+    HIPCHK(hipGetLastError());                                \
+    if ((e)->timing) {                                        \
+      (void)hipEventRecord(_b, st);                           \
+      pending(e).push_back(Pending{time_slot(e, name), _a, _b}); \
+    }                                                         \
+  } while (0)
+
+static void collect_times(prio3_engine* e) {
+  auto& v = pending(e);
+  for (auto& pd : v) {
+    float ms = 0;
+    (void)hipEventSynchronize(pd.b);
+    (void)hipEventElapsedTime(&ms, pd.a, pd.b);
+    e->times[pd.idx].ms += ms;
+    e->times[pd.idx].launches += 1;
+  }
+  v.clear();
+  for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
+  e->ev_pool.clear();
+}
+
+extern "C" {
+
+int prio3_sizes(const prio3_params* params, prio3_sizes_t* out) {
+  return fill_sizes(params, out, nullptr);
+}
+
+int prio3_engine_create(const prio3_params* params, const uint8_t verify_key[16], int device,
+                        prio3_engine** out) {
+  if (!params || !verify_key || !out) return PRIO3_EINVAL;
+  prio3_engine* e = new prio3_engine();
+  int rc = fill_sizes(params, &e->sz, &e->dp);
+  if (rc) {
+    delete e;
+    return rc;
+  }
+  e->params = *params;
+  memcpy(e->dp.vk, verify_key, 16);
+  e->device = device;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete e;
+    return PRIO3_EDEVICE;
+  }
+  *out = e;
+  return PRIO3_OK;
+}
+
+void prio3_engine_destroy(prio3_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  (void)hipStreamSynchronize(e->stream);
+  void* bufs[] = {e->sc.meas, e->sc.proofs, e->sc.jr, e->sc.qr, e->sc.part, e->sc.corrected,
+                  e->sc.flag, e->sc.Lbuf, e->sc.PVbuf, e->sc.acc, e->sc.out, e->d_mask,
+                  e->d_prep_partial, e->d_pcount, e->d_nonces, e->d_pub, e->d_helper,
+                  e->d_leader, e->d_msgs, e->d_status};
+  for (auto b : bufs)
+    if (b) (void)hipFree(b);
+  for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
+  (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
+  if (!e || !key) return PRIO3_EINVAL;
+  if (!strcmp(key, "force_slow_path")) {
+    e->force_slow = (int)value;
+    return PRIO3_OK;
+  }
+  if (!strcmp(key, "timing")) {
+    e->timing = (int)value;
+    return PRIO3_OK;
+  }
+  return PRIO3_EINVAL;
+}
+
+int prio3_device_prepare(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
+                         const uint8_t* d_public_shares, const uint8_t* d_helper_shares,
+                         const uint8_t* d_leader_prep_shares, uint8_t* d_prep_msgs,
+                         uint8_t* d_status, void* stream) {
+  if (!e) return PRIO3_EINVAL;
+  if (n == 0) return PRIO3_OK;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIPCHK(hipSetDevice(e->device));
+  int rc = ensure_scratch(e, n);
+  if (rc) return rc;
+  hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+  DevParams dp = e->dp;
+  dp.n = n;
+  dp.force_slow = (uint32_t)e->force_slow;
+  InPtrs in{d_nonces, d_public_shares, d_helper_shares, d_leader_prep_shares};
+  OutPtrs out{d_prep_msgs, d_status};
+  const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
+  if (dp.es == 16) {
+    TIMED(e, st, "k_xof", (k_xof<Fp128><<<blocks, 256, 0, st>>>(dp, in, e->sc)));
+    TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp128><<<blocks64, 64, 0, st>>>(dp, in, e->sc)));
+    TIMED(e, st, "k_query", (k_query<Fp128><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
+  } else {
+    TIMED(e, st, "k_xof", (k_xof<Fp64><<<blocks, 256, 0, st>>>(dp, in, e->sc)));
+    TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp64><<<blocks64, 64, 0, st>>>(dp, in, e->sc)));
+    TIMED(e, st, "k_query", (k_query<Fp64><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
+  }
+  return PRIO3_OK;
+}
+
+int prio3_device_accumulate(prio3_engine* e, uint32_t n, const uint8_t* d_status,
+                            const uint32_t* d_segment_ids, const uint8_t* d_accept_mask,
+                            uint32_t n_segments, uint8_t* d_agg_shares, uint64_t* d_counts,
+                            void* stream) {
+  if (!e || n_segments == 0) return PRIO3_EINVAL;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+  const DevParams& d = e->dp;
+  const size_t agg_len = (size_t)d.out_len * d.es;
+  if (n == 0) {
+    HIPCHK(hipMemsetAsync(d_agg_shares, 0, agg_len * n_segments, st));
+    HIPCHK(hipMemsetAsync(d_counts, 0, 8 * n_segments, st));
+    return PRIO3_OK;
+  }
+  if (n > e->cap) return PRIO3_EINVAL;
+  const uint32_t chunk = 8192;
+  const uint32_t nchunks = (n + chunk - 1) / chunk;
+  size_t need = (size_t)nchunks * agg_len;
+  if (need > e->partial_cap) {
+    if (e->d_prep_partial) (void)hipFree(e->d_prep_partial);
+    if (e->d_pcount) (void)hipFree(e->d_pcount);
+    HIPCHK(hipMalloc(&e->d_prep_partial, need));
+    HIPCHK(hipMalloc((void**)&e->d_pcount, 8 * (size_t)nchunks));
+    e->partial_cap = need;
+  }
+  const void* src = (d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC) ? e->sc.out : e->sc.meas;
+  for (uint32_t s = 0; s < n_segments; s++) {
+    TIMED(e, st, "k_mask",
+          (k_mask<<<(n + 255) / 256, 256, 0, st>>>(n, d_status, d_segment_ids, d_accept_mask, s,
+                                                  e->d_mask)));
+    dim3 grid(d.out_len, nchunks);
+    if (d.es == 16) {
+      TIMED(e, st, "k_acc_partial",
+            (k_acc_partial<Fp128><<<grid, 256, 0, st>>>(n, d.ld, chunk, d.out_len, src, e->d_mask,
+                                                        e->d_prep_partial, e->d_pcount)));
+      TIMED(e, st, "k_acc_final",
+            (k_acc_final<Fp128><<<(d.out_len + 255) / 256, 256, 0, st>>>(
+                nchunks, d.out_len, e->d_prep_partial, e->d_pcount, d_agg_shares + s * agg_len,
+                d_counts + s)));
+    } else {
+      TIMED(e, st, "k_acc_partial",
+            (k_acc_partial<Fp64><<<grid, 256, 0, st>>>(n, d.ld, chunk, d.out_len, src, e->d_mask,
+                                                       e->d_prep_partial, e->d_pcount)));
+      TIMED(e, st, "k_acc_final",
+            (k_acc_final<Fp64><<<(d.out_len + 255) / 256, 256, 0, st>>>(
+                nchunks, d.out_len, e->d_prep_partial, e->d_pcount, d_agg_shares + s * agg_len,
+                d_counts + s)));
+    }
+  }
+  return PRIO3_OK;
+}
+
+int prio3_device_combine(prio3_engine* e, uint32_t k, uint32_t n_segments, const uint8_t* d_in,
+                         const uint64_t* d_counts_in, uint8_t* d_out, uint64_t* d_counts_out,
+                         void* stream) {
+  if (!e || k == 0) return PRIO3_EINVAL;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+  const DevParams& d = e->dp;
+  uint32_t len = d.out_len * n_segments;
+  uint32_t threads = len > n_segments ? len : n_segments;
+  if (d.es == 16)
+    TIMED(e, st, "k_combine",
+          (k_combine<Fp128><<<(threads + 255) / 256, 256, 0, st>>>(k, len, n_segments, d_in,
+                                                                  d_counts_in, d_out,
+                                                                  d_counts_out)));
+  else
+    TIMED(e, st, "k_combine",
+          (k_combine<Fp64><<<(threads + 255) / 256, 256, 0, st>>>(k, len, n_segments, d_in,
+                                                                 d_counts_in, d_out,
+                                                                 d_counts_out)));
+  return PRIO3_OK;
+}
+
+int prio3_device_output_shares(prio3_engine* e, uint32_t n, uint8_t* out) {
+  if (!e || !out || n > e->cap) return PRIO3_EINVAL;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIPCHK(hipSetDevice(e->device));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  HIPCHK(hipDeviceSynchronize());
+  const DevParams& d = e->dp;
+  const void* src = (d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC) ? e->sc.out : e->sc.meas;
+  std::vector<uint8_t> soa((size_t)d.out_len * d.ld * d.es);
+  HIPCHK(hipMemcpy(soa.data(), src, soa.size(), hipMemcpyDeviceToHost));
+  for (uint32_t r = 0; r < n; r++)
+    for (uint32_t i = 0; i < d.out_len; i++)
+      memcpy(out + ((size_t)r * d.out_len + i) * d.es, soa.data() + ((size_t)i * d.ld + r) * d.es,
+             d.es);
+  return PRIO3_OK;
+}
+
+static int ensure_io(prio3_engine* e, uint32_t n) {
+  if (n <= e->io_cap) return PRIO3_OK;
+  uint8_t** bufs[] = {&e->d_nonces, &e->d_pub, &e->d_helper, &e->d_leader, &e->d_msgs, &e->d_status};
+  for (auto b : bufs)
+    if (*b) {
+      (void)hipFree(*b);
+      *b = nullptr;
+    }
+  const DevParams& d = e->dp;
+  size_t sizes[] = {16 * (size_t)n, (size_t)(d.public_share_len ? d.public_share_len : 16) * n,
+                    (size_t)d.helper_share_len * n, (size_t)d.prep_share_len * n,
+                    16 * (size_t)n, (size_t)n};
+  for (size_t i = 0; i < 6; i++) HIPCHK(hipMalloc((void**)bufs[i], sizes[i]));
+  e->io_cap = n;
+  return PRIO3_OK;
+}
+
+int prio3_helper_prepare_batch(prio3_engine* e, uint32_t n, const uint8_t* nonces,
+                               const uint8_t* public_shares, const uint8_t* helper_shares,
+                               const uint8_t* leader_prep_shares, uint8_t* prep_msgs_out,
+                               uint8_t* status_out, prio3_batch** batch_out) {
+  if (!e || (n && (!nonces || !helper_shares || !leader_prep_shares || !status_out)))
+    return PRIO3_EINVAL;
+  const DevParams& d = e->dp;
+  if (n && d.jr_len && (!public_shares || !prep_msgs_out)) return PRIO3_EINVAL;
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIPCHK(hipSetDevice(e->device));
+    int rc = ensure_io(e, n ? n : 1);
+    if (rc) return rc;
+    hipStream_t st = e->stream;
+    if (n) {
+      HIPCHK(hipMemcpyAsync(e->d_nonces, nonces, 16 * (size_t)n, hipMemcpyHostToDevice, st));
+      if (d.jr_len)
+        HIPCHK(hipMemcpyAsync(e->d_pub, public_shares, (size_t)d.public_share_len * n,
+                              hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(e->d_helper, helper_shares, (size_t)d.helper_share_len * n,
+                            hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(e->d_leader, leader_prep_shares, (size_t)d.prep_share_len * n,
+                            hipMemcpyHostToDevice, st));
+    }
+  }
+  int rc = prio3_device_prepare(e, n, e->d_nonces, e->d_pub, e->d_helper, e->d_leader, e->d_msgs,
+                                e->d_status, nullptr);
+  if (rc) return rc;
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    hipStream_t st = e->stream;
+    if (n) {
+      HIPCHK(hipMemcpyAsync(status_out, e->d_status, n, hipMemcpyDeviceToHost, st));
+      if (d.jr_len)
+        HIPCHK(hipMemcpyAsync(prep_msgs_out, e->d_msgs, 16 * (size_t)n, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    if (e->timing) collect_times(e);
+  }
+  if (batch_out) {
+    prio3_batch* b = new prio3_batch{e, n};
+    *batch_out = b;
+  }
+  return PRIO3_OK;
+}
+
+int prio3_accumulate(prio3_batch* b, const uint32_t* segment_ids, const uint8_t* accept_mask,
+                     uint32_t n_segments, uint8_t* agg_shares_out, uint64_t* counts_out) {
+  if (!b || !agg_shares_out || !counts_out || n_segments == 0) return PRIO3_EINVAL;
+  prio3_engine* e = b->e;
+  const DevParams& d = e->dp;
+  const uint32_t n = b->n;
+  uint32_t* d_seg = nullptr;
+  uint8_t *d_acc = nullptr, *d_agg = nullptr;
+  uint64_t* d_cnt = nullptr;
+  const size_t agg_len = (size_t)d.out_len * d.es;
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = e->stream;
+  if (n && segment_ids) {
+    HIPCHK(hipMalloc((void**)&d_seg, 4 * (size_t)n));
+    HIPCHK(hipMemcpyAsync(d_seg, segment_ids, 4 * (size_t)n, hipMemcpyHostToDevice, st));
+  }
+  if (n && accept_mask) {
+    HIPCHK(hipMalloc((void**)&d_acc, n));
+    HIPCHK(hipMemcpyAsync(d_acc, accept_mask, n, hipMemcpyHostToDevice, st));
+  }
+  HIPCHK(hipMalloc((void**)&d_agg, agg_len * n_segments));
+  HIPCHK(hipMalloc((void**)&d_cnt, 8 * (size_t)n_segments));
+  int rc = prio3_device_accumulate(e, n, e->d_status, d_seg, d_acc, n_segments, d_agg, d_cnt,
+                                   nullptr);
+  if (rc == PRIO3_OK) {
+    HIPCHK(hipMemcpyAsync(agg_shares_out, d_agg, agg_len * n_segments, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(counts_out, d_cnt, 8 * (size_t)n_segments, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (e->timing) collect_times(e);
+  }
+  if (d_seg) (void)hipFree(d_seg);
+  if (d_acc) (void)hipFree(d_acc);
+  (void)hipFree(d_agg);
+  (void)hipFree(d_cnt);
+  return rc;
+}
+
+int prio3_debug_output_shares(prio3_batch* b, uint8_t* out) {
+  if (!b) return PRIO3_EINVAL;
+  return prio3_device_output_shares(b->e, b->n, out);
+}
+
+void prio3_batch_free(prio3_batch* b) { delete b; }
+
+int prio3_engine_timing(prio3_engine* e, char* names, size_t cap_names, double* ms,
+                        uint64_t* launches, int cap) {
+  if (!e) return PRIO3_EINVAL;
+  std::lock_guard<std::mutex> lk(e->mu);
+  (void)hipSetDevice(e->device);
+  collect_times(e);
+  std::string all;
+  int k = 0;
+  for (auto& t : e->times) {
+    if (k < cap) {
+      if (ms) ms[k] = t.ms;
+      if (launches) launches[k] = t.launches;
+    }
+    if (!all.empty()) all += ",";
+    all += t.name;
+    k++;
+  }
+  if (names && cap_names) {
+    strncpy(names, all.c_str(), cap_names - 1);
+    names[cap_names - 1] = 0;
+  }
+  return k;
+}
+
+void prio3_engine_timing_reset(prio3_engine* e) {
+  if (!e) return;
+  std::lock_guard<std::mutex> lk(e->mu);
+  collect_times(e);
+  for (auto& t : e->times) {
+    t.ms = 0;
+    t.launches = 0;
+  }
+}
+
+}  // extern "C"

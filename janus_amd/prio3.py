@@ -1,0 +1,300 @@
+"""Host-side mirror of the prio 0.16.2 ``Prio3`` aggregator surface that Janus uses on the
+helper's aggregate-init hot path, backed by the gfx950 HIP engine (``libjanus_prio3.so``).
+
+Reference surface being mirrored:
+  * instance constructors ``Prio3::new_count / new_sum / new_sum_vec_multithreaded /
+    new_histogram`` as dispatched by ``vdaf_dispatch!`` (/root/reference/core/src/vdaf.rs:198-300);
+  * the per-report ``helper_initialized(..) + evaluate(..)`` call inside
+    ``handle_aggregate_init_generic`` (/root/reference/aggregator/src/aggregator.rs:2020-2042),
+    here batched over the whole job;
+  * ``AggregateShare::merge`` accumulation performed by ``AggregationJobWriter``
+    (/root/reference/aggregator/src/aggregator/aggregation_job_writer.rs:591-695).
+
+There is no CPU fallback: if the HIP library is missing or no GPU is present, engine
+creation raises.  (The CPU restatement under ``oracle/`` is test infrastructure only.)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libjanus_prio3.so")
+
+PRIO3_COUNT, PRIO3_SUM, PRIO3_SUMVEC, PRIO3_HISTOGRAM = 0, 1, 2, 3
+
+STATUS_FINISHED = 0
+STATUS_PREP_INIT = 1
+STATUS_PREP_SHARE_DECODE = 2
+STATUS_PREP_MSG = 3
+STATUS_PREP_NEXT = 4
+STATUS_PEER_MISMATCH = 5
+
+#: prio ``PingPongError`` variant for each status (error.rs:365-428 maps these to labels).
+STATUS_PINGPONG_ERROR = {
+    STATUS_PREP_INIT: "VdafPrepareInit",
+    STATUS_PREP_SHARE_DECODE: "CodecPrepShare",
+    STATUS_PREP_MSG: "VdafPrepareSharesToPrepareMessage",
+    STATUS_PREP_NEXT: "VdafPrepareNext",
+    STATUS_PEER_MISMATCH: "PeerMessageMismatch",
+}
+
+#: ``janus_step_failures{type=...}`` metric label per status, helper role
+#: (handle_ping_pong_error, /root/reference/aggregator/src/aggregator/error.rs:379-411).
+STATUS_METRIC_LABEL = {
+    STATUS_PREP_INIT: "prepare_init_failure",
+    STATUS_PREP_SHARE_DECODE: "leader_prep_share_decode_failure",
+    STATUS_PREP_MSG: "prepare_message_failure",
+    STATUS_PREP_NEXT: "prepare_next_failure",
+    STATUS_PEER_MISMATCH: "leader_ping_pong_message_mismatch",
+}
+
+
+class Prio3Params(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("bits", C.c_uint32), ("length", C.c_uint32),
+                ("chunk_length", C.c_uint32), ("num_proofs", C.c_uint32)]
+
+
+class Prio3Sizes(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in (
+        "field_bytes", "meas_len", "out_len", "proof_len", "verifier_len", "joint_rand_len",
+        "nonce_len", "public_share_len", "helper_share_len", "prep_share_len", "prep_msg_len",
+        "agg_share_len")]
+
+
+#: Every symbol include/janus_prio3.h declares.
+EXPORTED_SYMBOLS = (
+    "prio3_sizes", "prio3_engine_create", "prio3_engine_destroy", "prio3_helper_prepare_batch",
+    "prio3_accumulate", "prio3_debug_output_shares", "prio3_batch_free", "prio3_device_prepare",
+    "prio3_device_accumulate", "prio3_device_output_shares", "prio3_device_combine",
+    "prio3_engine_set_option", "prio3_engine_timing", "prio3_engine_timing_reset",
+)
+
+_lib = None
+
+
+def load_library() -> C.CDLL:
+    """Load the in-tree HIP engine; raise loudly if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"janus_amd HIP engine not built: {LIB_PATH} is missing "
+                          "(run `make -C janus_amd` or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    P, u8p, vp = C.POINTER, C.POINTER(C.c_uint8), C.c_void_p
+    L.prio3_sizes.argtypes = [P(Prio3Params), P(Prio3Sizes)]
+    L.prio3_engine_create.argtypes = [P(Prio3Params), u8p, C.c_int, P(vp)]
+    L.prio3_engine_destroy.argtypes = [vp]
+    L.prio3_engine_destroy.restype = None
+    L.prio3_helper_prepare_batch.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, vp, vp, P(vp)]
+    L.prio3_accumulate.argtypes = [vp, vp, vp, C.c_uint32, vp, vp]
+    L.prio3_debug_output_shares.argtypes = [vp, vp]
+    L.prio3_batch_free.argtypes = [vp]
+    L.prio3_batch_free.restype = None
+    L.prio3_device_prepare.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, vp, vp, vp]
+    L.prio3_device_accumulate.argtypes = [vp, C.c_uint32, vp, vp, vp, C.c_uint32, vp, vp, vp]
+    L.prio3_device_output_shares.argtypes = [vp, C.c_uint32, vp]
+    L.prio3_device_combine.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp]
+    L.prio3_engine_set_option.argtypes = [vp, C.c_char_p, C.c_int64]
+    L.prio3_engine_timing.argtypes = [vp, C.c_char_p, C.c_size_t, P(C.c_double),
+                                      P(C.c_uint64), C.c_int]
+    L.prio3_engine_timing_reset.argtypes = [vp]
+    L.prio3_engine_timing_reset.restype = None
+    _lib = L
+    return L
+
+
+# ------------------------------------------------------------------------------------
+# VDAF instances (mirrors of prio's constructors; names follow core/src/vdaf.rs)
+# ------------------------------------------------------------------------------------
+@dataclass(frozen=True)
+class Prio3:
+    kind: int
+    bits: int = 0
+    length: int = 0
+    chunk_length: int = 0
+    num_proofs: int = 1
+
+    def params(self) -> Prio3Params:
+        return Prio3Params(self.kind, self.bits, self.length, self.chunk_length, self.num_proofs)
+
+    def sizes(self) -> Prio3Sizes:
+        s = Prio3Sizes()
+        rc = load_library().prio3_sizes(C.byref(self.params()), C.byref(s))
+        if rc:
+            raise ValueError(f"unsupported Prio3 parameters (rc={rc})")
+        return s
+
+
+def Prio3Count() -> Prio3:
+    return Prio3(PRIO3_COUNT)
+
+
+def Prio3Sum(bits: int) -> Prio3:
+    return Prio3(PRIO3_SUM, bits=bits)
+
+
+def Prio3SumVec(bits: int, length: int, chunk_length: int) -> Prio3:
+    return Prio3(PRIO3_SUMVEC, bits=bits, length=length, chunk_length=chunk_length)
+
+
+def Prio3Histogram(length: int, chunk_length: int) -> Prio3:
+    return Prio3(PRIO3_HISTOGRAM, length=length, chunk_length=chunk_length)
+
+
+def _np_ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _tptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+class PreparedBatch:
+    """Device-resident output shares of one ``prepare_batch`` call (prio3_batch*)."""
+
+    def __init__(self, engine: "HelperEngine", handle: C.c_void_p, n: int):
+        self.engine, self.handle, self.n = engine, handle, n
+
+    def accumulate(self, segment_ids=None, accept_mask=None, n_segments: int = 1):
+        sz = self.engine.sz
+        agg = np.zeros((n_segments, sz.agg_share_len), np.uint8)
+        cnt = np.zeros(n_segments, np.uint64)
+        seg = None if segment_ids is None else np.ascontiguousarray(segment_ids, np.uint32)
+        acc = None if accept_mask is None else np.ascontiguousarray(accept_mask, np.uint8)
+        rc = load_library().prio3_accumulate(self.handle, _np_ptr(seg), _np_ptr(acc), n_segments,
+                                             _np_ptr(agg), _np_ptr(cnt))
+        if rc:
+            raise RuntimeError(f"prio3_accumulate failed (rc={rc})")
+        return agg, cnt
+
+    def output_shares(self) -> np.ndarray:
+        out = np.zeros((self.n, self.engine.sz.agg_share_len), np.uint8)
+        rc = load_library().prio3_debug_output_shares(self.handle, _np_ptr(out))
+        if rc:
+            raise RuntimeError(f"prio3_debug_output_shares failed (rc={rc})")
+        return out
+
+    def free(self):
+        if self.handle:
+            load_library().prio3_batch_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class HelperEngine:
+    """One engine per (Prio3 instance, verify key, GPU) -- created where Janus builds
+    ``VdafOps`` for a task (aggregator.rs:880-988)."""
+
+    def __init__(self, vdaf: Prio3, verify_key: bytes, device: int = 0):
+        if len(verify_key) != 16:
+            raise ValueError("verify key must be 16 bytes (VERIFY_KEY_LENGTH, core/src/vdaf.rs:16)")
+        L = load_library()
+        self.vdaf, self.device = vdaf, device
+        self.sz = vdaf.sizes()
+        h = C.c_void_p()
+        vk = (C.c_uint8 * 16).from_buffer_copy(verify_key)
+        rc = L.prio3_engine_create(C.byref(vdaf.params()), vk, device, C.byref(h))
+        if rc:
+            raise RuntimeError(f"prio3_engine_create failed (rc={rc}); a GPU is required")
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None):
+            load_library().prio3_engine_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_option(self, key: str, value: int):
+        rc = load_library().prio3_engine_set_option(self.handle, key.encode(), int(value))
+        if rc:
+            raise ValueError(f"unknown option {key}")
+
+    # ---- host-buffer path -----------------------------------------------------------
+    def prepare_batch(self, nonces, public_shares, helper_shares, leader_prep_shares):
+        """Batched helper prepare_init -> prepare_shares_to_prepare_message -> prepare_next.
+
+        Arrays are uint8 [n, len].  Returns (prep_msgs [n, prep_msg_len], status [n], batch).
+        """
+        sz = self.sz
+        nonces = np.ascontiguousarray(nonces, np.uint8)
+        n = nonces.shape[0]
+        helper_shares = np.ascontiguousarray(helper_shares, np.uint8)
+        leader_prep_shares = np.ascontiguousarray(leader_prep_shares, np.uint8)
+        if helper_shares.shape != (n, sz.helper_share_len) or \
+                leader_prep_shares.shape != (n, sz.prep_share_len):
+            raise ValueError("input share shapes do not match the VDAF instance")
+        pub = None
+        if sz.public_share_len:
+            pub = np.ascontiguousarray(public_shares, np.uint8)
+            if pub.shape != (n, sz.public_share_len):
+                raise ValueError("public share shape does not match the VDAF instance")
+        msgs = np.zeros((n, max(sz.prep_msg_len, 1)), np.uint8)
+        status = np.zeros(n, np.uint8)
+        bh = C.c_void_p()
+        rc = load_library().prio3_helper_prepare_batch(
+            self.handle, n, _np_ptr(nonces), _np_ptr(pub), _np_ptr(helper_shares),
+            _np_ptr(leader_prep_shares), _np_ptr(msgs), _np_ptr(status), C.byref(bh))
+        if rc:
+            raise RuntimeError(f"prio3_helper_prepare_batch failed (rc={rc})")
+        return msgs[:, :sz.prep_msg_len], status, PreparedBatch(self, bh, n)
+
+    # ---- device-resident path (torch tensors on this engine's GPU) ------------------
+    def prepare_device(self, nonces, public_shares, helper_shares, leader_prep_shares,
+                       prep_msgs, status, stream=None) -> None:
+        rc = load_library().prio3_device_prepare(
+            self.handle, nonces.shape[0], _tptr(nonces), _tptr(public_shares),
+            _tptr(helper_shares), _tptr(leader_prep_shares), _tptr(prep_msgs), _tptr(status),
+            C.c_void_p(stream) if stream else None)
+        if rc:
+            raise RuntimeError(f"prio3_device_prepare failed (rc={rc})")
+
+    def accumulate_device(self, n, status, segment_ids, accept_mask, n_segments, agg, counts,
+                          stream=None) -> None:
+        rc = load_library().prio3_device_accumulate(
+            self.handle, n, _tptr(status), _tptr(segment_ids), _tptr(accept_mask), n_segments,
+            _tptr(agg), _tptr(counts), C.c_void_p(stream) if stream else None)
+        if rc:
+            raise RuntimeError(f"prio3_device_accumulate failed (rc={rc})")
+
+    def combine_device(self, k, n_segments, parts, part_counts, out, out_counts,
+                       stream=None) -> None:
+        rc = load_library().prio3_device_combine(
+            self.handle, k, n_segments, _tptr(parts), _tptr(part_counts), _tptr(out),
+            _tptr(out_counts), C.c_void_p(stream) if stream else None)
+        if rc:
+            raise RuntimeError(f"prio3_device_combine failed (rc={rc})")
+
+    def device_output_shares(self, n: int) -> np.ndarray:
+        out = np.zeros((n, self.sz.agg_share_len), np.uint8)
+        rc = load_library().prio3_device_output_shares(self.handle, n, _np_ptr(out))
+        if rc:
+            raise RuntimeError("prio3_device_output_shares failed")
+        return out
+
+    # ---- measurement ----------------------------------------------------------------
+    def timing(self) -> dict:
+        names = C.create_string_buffer(4096)
+        ms = (C.c_double * 64)()
+        launches = (C.c_uint64 * 64)()
+        k = load_library().prio3_engine_timing(self.handle, names, 4096, ms, launches, 64)
+        keys = names.value.decode().split(",") if k else []
+        return {keys[i]: (ms[i], int(launches[i])) for i in range(min(k, 64))}
+
+    def timing_reset(self):
+        load_library().prio3_engine_timing_reset(self.handle)

@@ -59,6 +59,8 @@ def lib():
                                        P(C.c_uint32), u8p, C.c_uint32, u8p, u8p, u8p,
                                        P(C.c_uint64), C.c_int, C.c_int]
         L.orc_agg_merge.argtypes = [P(OrcParams), u8p, u8p]
+        L.orc_gen_reports.argtypes = [P(OrcParams), u8p, C.c_uint32, C.c_uint64, C.c_int,
+                                      u8p, u8p, u8p, u8p, P(C.c_uint64), u8p]
         _lib = L
     return _lib
 
@@ -177,3 +179,45 @@ class Oracle:
                                _ptr(status), _ptr(agg), _ptr(cnt, C.c_uint64), n_threads,
                                job_size)
         return msgs[:, :p.prep_msg_len], status, agg, cnt
+
+    def gen_reports(self, vk: bytes, n: int, seed: int = 1, n_threads: int = 8):
+        """Deterministic honest reports: dict of uint8 arrays + measurements + leader out shares."""
+        p = self.p
+        mstride = p.length if self.kind == "sumvec" else 1
+        d = dict(nonces=np.zeros((n, 16), np.uint8),
+                 public_shares=np.zeros((n, max(p.public_share_len, 1)), np.uint8),
+                 helper_shares=np.zeros((n, p.helper_share_len), np.uint8),
+                 leader_prep_shares=np.zeros((n, p.prep_share_len), np.uint8),
+                 measurements=np.zeros((n, mstride), np.uint64),
+                 leader_out_shares=np.zeros((n, p.out_share_bytes), np.uint8))
+        lib().orc_gen_reports(C.byref(p), _buf(vk), n, seed, n_threads, _ptr(d["nonces"]),
+                              _ptr(d["public_shares"]), _ptr(d["helper_shares"]),
+                              _ptr(d["leader_prep_shares"]), _ptr(d["measurements"], C.c_uint64),
+                              _ptr(d["leader_out_shares"]))
+        if p.public_share_len == 0:
+            d["public_shares"] = np.zeros((n, 0), np.uint8)
+        return d
+
+
+def field_modulus(kind: str) -> int:
+    return 2**64 - 2**32 + 1 if kind == "count" else 2**128 - 28 * 2**64 + 1
+
+
+def decode_elems(buf: np.ndarray, es: int) -> list:
+    """uint8 array (..., k*es) -> python ints, LE."""
+    b = np.ascontiguousarray(buf, np.uint8).reshape(-1, es)
+    return [int.from_bytes(row.tobytes(), "little") for row in b]
+
+
+def sum_mod(rows: np.ndarray, es: int, p: int) -> list:
+    """Element-wise mod-p sum over axis 0 of a [n, out_len*es] uint8 array."""
+    n = rows.shape[0]
+    k = rows.shape[1] // es
+    v = np.ascontiguousarray(rows, np.uint8).reshape(n, k, es)
+    acc = [0] * k
+    limbs = [v[:, :, 4 * j:4 * j + 4].copy().view(np.uint32).reshape(n, k).astype(np.uint64)
+             for j in range(es // 4)]
+    sums = [l.sum(axis=0, dtype=np.uint64) for l in limbs]  # n < 2^32 so no overflow
+    for e in range(k):
+        acc[e] = sum(int(sums[j][e]) << (32 * j) for j in range(es // 4)) % p
+    return acc

@@ -1061,3 +1061,97 @@ int orc_helper_batch(const orc_params* p, const uint8_t vk[16], uint32_t n,
   pthread_mutex_destroy(&c.mu);
   return 0;
 }
+
+/* ------------------------------------------------------------------------------------ */
+/* Deterministic synthetic report generator (client shard + leader prepare_init), for   */
+/* tests only.  Per report i: stream = TurboSHAKE128("janus-amd-gen" || seed || i, D=1).  */
+/* ------------------------------------------------------------------------------------ */
+typedef struct {
+  const orc_params* p;
+  const uint8_t* vk;
+  uint32_t n;
+  uint64_t seed;
+  uint8_t *nonces, *publics, *helpers, *leader_ps, *leader_out;
+  uint64_t* meas;
+  atomic_uint next;
+} gen_ctx;
+
+static void* gen_worker(void* arg) {
+  gen_ctx* g = (gen_ctx*)arg;
+  const orc_params* p = g->p;
+  fld F = mkfld(p);
+  uint32_t mstride = p->type == ORC_SUMVEC ? p->length : 1;
+  uint8_t* ls = (uint8_t*)malloc(p->leader_share_len);
+  uint8_t* st = (uint8_t*)malloc(p->meas_len * p->es + 16);
+  uint8_t* ps = (uint8_t*)malloc(p->prep_share_len);
+  uint64_t* m = (uint64_t*)malloc(sizeof(uint64_t) * mstride);
+  fe* lm = (fe*)malloc(sizeof(fe) * p->meas_len);
+  fe* lo = (fe*)malloc(sizeof(fe) * p->out_len);
+  size_t slen = 16 + 80 + 8 * (size_t)mstride;
+  uint8_t* stream = (uint8_t*)malloc(slen);
+  uint8_t pub[32];
+  for (;;) {
+    uint32_t i = atomic_fetch_add(&g->next, 1);
+    if (i >= g->n) break;
+    uint8_t in[29];
+    memcpy(in, "janus-amd-gen", 13);
+    for (int k = 0; k < 8; k++) in[13 + k] = (uint8_t)(g->seed >> (8 * k));
+    for (int k = 0; k < 8; k++) in[21 + k] = (uint8_t)((uint64_t)i >> (8 * k));
+    orc_turboshake128(in, sizeof in, 0x01, stream, slen);
+    for (uint32_t e = 0; e < mstride; e++) {
+      uint64_t v = 0;
+      for (int k = 0; k < 8; k++) v |= (uint64_t)stream[96 + 8 * e + k] << (8 * k);
+      switch (p->type) {
+        case ORC_COUNT: v &= 1; break;
+        case ORC_SUM:
+        case ORC_SUMVEC: if (p->bits < 64) v &= ((uint64_t)1 << p->bits) - 1; break;
+        case ORC_HISTOGRAM: v %= p->length; break;
+      }
+      m[e] = v;
+    }
+    const uint8_t* nonce = stream;
+    orc_shard(p, m, nonce, stream + 16, pub, ls, g->helpers + (size_t)i * p->helper_share_len);
+    orc_prepare_init(p, g->vk, 0, nonce, pub, ls, st, ps);
+    memcpy(g->nonces + (size_t)i * 16, nonce, 16);
+    if (p->public_share_len) memcpy(g->publics + (size_t)i * p->public_share_len, pub, 32);
+    memcpy(g->leader_ps + (size_t)i * p->prep_share_len, ps, p->prep_share_len);
+    if (g->meas) memcpy(g->meas + (size_t)i * mstride, m, sizeof(uint64_t) * mstride);
+    if (g->leader_out) {
+      for (uint32_t k = 0; k < p->meas_len; k++) dec_fe(&F, st + k * p->es, &lm[k]);
+      truncate_share(p, &F, lm, lo);
+      for (uint32_t k = 0; k < p->out_len; k++)
+        enc_fe(&F, lo[k], g->leader_out + ((size_t)i * p->out_len + k) * p->es);
+    }
+  }
+  free(ls);
+  free(st);
+  free(ps);
+  free(m);
+  free(lm);
+  free(lo);
+  free(stream);
+  return NULL;
+}
+
+int orc_gen_reports(const orc_params* p, const uint8_t vk[16], uint32_t n, uint64_t seed,
+                    int n_threads, uint8_t* nonces, uint8_t* publics, uint8_t* helpers,
+                    uint8_t* leader_ps, uint64_t* meas_out, uint8_t* leader_out_shares) {
+  gen_ctx g;
+  g.p = p;
+  g.vk = vk;
+  g.n = n;
+  g.seed = seed;
+  g.nonces = nonces;
+  g.publics = publics;
+  g.helpers = helpers;
+  g.leader_ps = leader_ps;
+  g.leader_out = leader_out_shares;
+  g.meas = meas_out;
+  atomic_init(&g.next, 0);
+  if (n_threads < 1) n_threads = 1;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * n_threads);
+  for (int t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, gen_worker, &g);
+  for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+  free(th);
+  return 0;
+}

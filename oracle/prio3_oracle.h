@@ -104,6 +104,12 @@ int orc_helper_batch(const orc_params* p, const uint8_t vk[16], uint32_t n,
                      uint32_t n_segments, uint8_t* prep_msgs_out, uint8_t* status_out,
                      uint8_t* agg_out, uint64_t* count_out, int n_threads, int job_size);
 
+/* Deterministic synthetic reports (client shard + leader prepare_init), multithreaded.
+ * meas_out: n x (SumVec: length, else 1) u64; leader_out_shares: n x out_len*es (nullable). */
+int orc_gen_reports(const orc_params* p, const uint8_t vk[16], uint32_t n, uint64_t seed,
+                    int n_threads, uint8_t* nonces, uint8_t* publics, uint8_t* helpers,
+                    uint8_t* leader_ps, uint64_t* meas_out, uint8_t* leader_out_shares);
+
 /* Mod-p element-wise sum of agg shares (AggregateShare::merge). */
 void orc_agg_merge(const orc_params* p, uint8_t* acc, const uint8_t* other);
 

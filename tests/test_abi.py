@@ -1,0 +1,72 @@
+"""CPU tests of the drop-in boundary: the C-ABI library loads, exports every symbol
+include/janus_prio3.h declares, reports the right per-instance sizes, and fails loudly
+(no CPU fallback) when no GPU is available."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from tests.conftest import CONFIGS, ROOT
+
+HEADER = os.path.join(ROOT, "include", "janus_prio3.h")
+
+
+def _declared_symbols():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^(?:int|void)\s+(prio3_\w+)\s*\(", src, re.M)))
+
+
+def test_header_declares_the_exported_set():
+    from janus_amd import prio3 as J
+    assert _declared_symbols() == sorted(J.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    from janus_amd import prio3 as J
+    L = J.load_library()
+    for name in _declared_symbols():
+        assert hasattr(L, name), name
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_sizes_match_oracle(name, oracle_lib):
+    from janus_amd import prio3 as J
+    cfg = CONFIGS[name]
+    o = oracle_lib.Oracle(**cfg)
+    v = J.Prio3({"count": 0, "sum": 1, "sumvec": 2, "histogram": 3}[cfg["kind"]],
+                cfg.get("bits", 0), cfg.get("length", 0), cfg.get("chunk_length", 0))
+    s = v.sizes()
+    assert s.field_bytes == o.es
+    assert s.meas_len == o.meas_len and s.out_len == o.out_len
+    assert s.proof_len == o.proof_len and s.verifier_len == o.verifier_len
+    assert s.public_share_len == o.public_share_len
+    assert s.helper_share_len == o.helper_share_len
+    assert s.prep_share_len == o.prep_share_len
+    assert s.prep_msg_len == o.prep_msg_len
+    assert s.agg_share_len == o.out_share_bytes
+
+
+def test_histogram_256_sizes_match_survey():
+    """PROOF_LEN 95, VERIFIER_LEN 34, leader prep 560 B."""
+    from janus_amd import prio3 as J
+    s = J.Prio3Histogram(256, 16).sizes()
+    assert (s.proof_len, s.verifier_len, s.prep_share_len, s.helper_share_len) == (95, 34, 560, 48)
+
+
+def test_invalid_parameters_rejected():
+    from janus_amd import prio3 as J
+    for v in (J.Prio3Sum(0), J.Prio3Histogram(0, 1), J.Prio3SumVec(8, 10, 0), J.Prio3(9)):
+        with pytest.raises(ValueError):
+            v.sizes()
+    with pytest.raises(ValueError):
+        J.Prio3(J.PRIO3_COUNT, num_proofs=2).sizes()
+
+
+def test_engine_requires_gpu_or_fails_loudly():
+    import torch
+    from janus_amd import prio3 as J
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError):
+        J.HelperEngine(J.Prio3Count(), bytes(16), device=0)

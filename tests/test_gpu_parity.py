@@ -1,0 +1,153 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the CPU restatement (oracle/).
+
+Mirrors the reference's transcript pattern (core/src/test_util/mod.rs:86-232, used by
+taskprov_tests.rs:1268-1369): every helper output -- prepare message, per-report status,
+output share and aggregate share -- must equal the oracle's bit-for-bit.  Error paths use
+tampered inputs, mirroring FakeFailsPrepInit/FakeFailsPrepStep (core/src/vdaf.rs:354-385).
+"""
+import numpy as np
+import pytest
+
+from tests.conftest import CONFIGS
+
+pytestmark = pytest.mark.gpu
+
+VK = bytes(range(0x40, 0x50))
+
+
+def _engine(cfg):
+    from janus_amd import prio3 as J
+    kind = cfg["kind"]
+    if kind == "count":
+        v = J.Prio3Count()
+    elif kind == "sum":
+        v = J.Prio3Sum(cfg["bits"])
+    elif kind == "sumvec":
+        v = J.Prio3SumVec(cfg["bits"], cfg["length"], cfg["chunk_length"])
+    else:
+        v = J.Prio3Histogram(cfg["length"], cfg["chunk_length"])
+    return J.HelperEngine(v, VK, device=0)
+
+
+def _oracle(cfg):
+    from oracle.oracle import Oracle
+    return Oracle(**cfg)
+
+
+def _tamper(o, d, rng):
+    """Corrupt a few reports to hit each status code; returns the modified copy."""
+    d = {k: v.copy() for k, v in d.items()}
+    n = d["nonces"].shape[0]
+    es = o.es
+    # decide failure: flip a bit in the leader verifier share (element 1)
+    for i in range(1, n, 17):
+        d["leader_prep_shares"][i, es] ^= 0x01
+    # decode failure: leader verifier element 0 set to 0xff.. (>= p)
+    for i in range(3, n, 29):
+        d["leader_prep_shares"][i, :es] = 0xFF
+    if o.jr_len:
+        # joint-rand mismatch: corrupt the leader's joint-rand part in its prep share
+        for i in range(5, n, 23):
+            d["leader_prep_shares"][i, -1] ^= 0x80
+        # wrong public share (helper's corrected seed differs)
+        for i in range(7, n, 31):
+            d["public_shares"][i, 3] ^= 0x10
+    # corrupt a helper seed (share no longer matches the proof)
+    for i in range(11, n, 37):
+        d["helper_shares"][i, 0] ^= 0x01
+    return d
+
+
+def _check_against_oracle(cfg, n, seed, tamper=True, force_slow=False, n_segments=1):
+    from oracle.oracle import decode_elems
+    o = _oracle(cfg)
+    eng = _engine(cfg)
+    if force_slow:
+        eng.set_option("force_slow_path", 1)
+    d = o.gen_reports(VK, n, seed=seed, n_threads=8)
+    rng = np.random.default_rng(seed)
+    if tamper:
+        d = _tamper(o, d, rng)
+    seg = rng.integers(0, n_segments, n).astype(np.uint32)
+    accept = (rng.random(n) > 0.1).astype(np.uint8)
+    ref_msgs, ref_status, ref_agg, ref_cnt = o.helper_batch(
+        VK, d["nonces"], d["public_shares"], d["helper_shares"], d["leader_prep_shares"],
+        segment_ids=seg, accept_mask=accept, n_segments=n_segments, n_threads=8)
+    msgs, status, batch = eng.prepare_batch(d["nonces"], d["public_shares"], d["helper_shares"],
+                                            d["leader_prep_shares"])
+    np.testing.assert_array_equal(status, ref_status)
+    np.testing.assert_array_equal(msgs, ref_msgs)
+    agg, cnt = batch.accumulate(seg, accept, n_segments)
+    np.testing.assert_array_equal(cnt, ref_cnt)
+    np.testing.assert_array_equal(agg, ref_agg)
+    if tamper:
+        assert set(np.unique(status)) >= {0, 3}
+    return o, d, status, batch
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_parity_vs_oracle(name):
+    cfg = CONFIGS[name]
+    n = 64 if "1000" in name else 700
+    _check_against_oracle(cfg, n, seed=11)
+
+
+@pytest.mark.parametrize("name", ["count", "sum8", "sumvec_8x10_c9", "hist_256_c16"])
+def test_slow_path_parity(name):
+    """The general rejection-sampling kernel must give the same bytes as the fast path."""
+    _check_against_oracle(CONFIGS[name], 130, seed=5, force_slow=True)
+
+
+@pytest.mark.parametrize("name", ["count", "hist_256_c16", "sumvec_8x10_c9"])
+def test_segments_and_accept_mask(name):
+    _check_against_oracle(CONFIGS[name], 900, seed=3, n_segments=5)
+
+
+@pytest.mark.parametrize("name", ["count", "sum8", "sumvec_8x10_c9", "hist_10_c3"])
+def test_output_shares_match_prepare_next(name):
+    """Per-report output shares equal the oracle's prepare_next (truncate) output."""
+    from oracle.oracle import Oracle
+    cfg = CONFIGS[name]
+    o, d, status, batch = _check_against_oracle(cfg, 40, seed=9, tamper=False)
+    outs = batch.output_shares()
+    for i in range(0, 40, 7):
+        rc, st, ps = o.prepare_init(VK, 1, d["nonces"][i].tobytes(), d["public_shares"][i].tobytes(),
+                                    d["helper_shares"][i].tobytes())
+        assert rc == 0
+        rc, msg = o.prep_shares_to_prep_msg(d["leader_prep_shares"][i].tobytes(), ps)
+        assert rc == 0
+        rc, out = o.prepare_next(st, msg)
+        assert rc == 0 and out == outs[i].tobytes()
+
+
+def test_empty_batch():
+    eng = _engine(CONFIGS["hist_10_c3"])
+    z = lambda k: np.zeros((0, k), np.uint8)
+    sz = eng.sz
+    msgs, status, batch = eng.prepare_batch(z(16), z(sz.public_share_len), z(sz.helper_share_len),
+                                            z(sz.prep_share_len))
+    assert status.shape == (0,)
+    agg, cnt = batch.accumulate(None, None, 2)
+    assert cnt.tolist() == [0, 0] and not agg.any()
+
+
+def test_unshard_equals_plaintext_histogram():
+    """Semantic known answer (integration_tests/.../common.rs:513-526): leader + helper
+    aggregate shares unshard to the plaintext histogram."""
+    from oracle.oracle import Oracle, sum_mod, decode_elems, field_modulus
+    cfg = CONFIGS["hist_256_c16"]
+    o = Oracle(**cfg)
+    eng = _engine(cfg)
+    n = 5000
+    d = o.gen_reports(VK, n, seed=21, n_threads=8)
+    msgs, status, batch = eng.prepare_batch(d["nonces"], d["public_shares"], d["helper_shares"],
+                                            d["leader_prep_shares"])
+    assert not status.any()
+    agg, cnt = batch.accumulate()
+    p = field_modulus("histogram")
+    la = sum_mod(d["leader_out_shares"], 16, p)
+    ha = decode_elems(agg[0], 16)
+    tot = [(a + b) % p for a, b in zip(la, ha)]
+    exp = np.bincount(d["measurements"][:, 0].astype(np.int64), minlength=256)
+    assert tot == [int(x) for x in exp]
+    assert int(cnt[0]) == n
