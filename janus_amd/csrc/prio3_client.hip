@@ -1,0 +1,354 @@
+// prio3_client.hip -- on-device synthetic report generator: the client's Prio3 shard
+// (VDAF-08 7.2.1, prio Prio3::shard) followed by the leader's prepare_init (agg_id 0), so
+// that benchmarks and full-size tests get honest, distinct reports at HBM speed without a
+// CPU in the loop.  Report i is derived from (seed, i) exactly like the oracle's
+// orc_gen_reports: stream = TurboSHAKE128("janus-amd-gen" || seed || i, D=1) gives the
+// nonce (16 B), the shard randomness (5 or 3 seeds) and the measurement (8 B per entry).
+//
+// Prover path per lane: record the validity circuit's wire values (num_shares = 1), turn each
+// wire into coefficients with a size-P inverse DFT, evaluate on the 2P-th roots with a
+// size-2P DFT, apply the gadget pointwise, inverse-DFT back: the gadget polynomial
+// (prio FlpGeneric::prove, ProveShimGadget).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "prio3_common.h"
+
+struct GenScratch {
+  void *meas, *hm, *lm, *wires, *evals, *g, *tmp, *proof, *hp, *prand, *jr, *qr, *L, *PV, *acc;
+};
+struct GenOut {
+  uint8_t *nonces, *pub, *helper, *leader_ps, *leader_out;
+  uint64_t* meas;
+  uint8_t* flags;
+};
+
+// XOF(seed, dst, binder).expand_into_vec(n) into an SoA column set (no rejection: flagged)
+template <class F>
+DEV void expand_to(const DevParams& p, const uint32_t* dst2, const uint32_t* seed,
+                   const uint8_t* binder, int blen, uint32_t n, void* base, uint32_t r,
+                   uint32_t& flag) {
+  KState s;
+  kzero(s);
+  Msg m;
+  msg_zero(m);
+  msg_dst(m, dst2);
+  msg_bytes16(m, 9, seed);
+  for (int i = 0; i < blen; i++) msg_byte(m, 25 + i, binder[i]);
+  msg_absorb_final(s, m, 25 + blen);
+  const uint32_t K = (n * F::ES + 167) / 168;
+  uint32_t q0 = 0, q1 = 0;
+  for (uint32_t b = 0; b < K; b++) {
+    squeeze_block<F>(p, s, b, n, q0, q1, base, r, flag);
+    if (b + 1 < K) keccak_p12(s);
+  }
+}
+
+// joint_rand_part = XOF(blind, dst(7), [agg_id] || nonce || enc(share)) -> 16 bytes, with the
+// share read back from an SoA scratch column set.
+template <class F>
+DEV void jr_part_scratch(const DevParams& p, const uint32_t* blind, uint32_t agg_id,
+                         const uint32_t* nonce, const void* src, uint32_t r, uint32_t* part) {
+  constexpr uint32_t WPE = F::ES / 4;  // words per element
+  const uint32_t nwords = p.meas_len * WPE;
+  auto Sw = [&](uint32_t u) -> uint32_t {
+    if (u >= nwords) return 0u;
+    const uint32_t e = u / WPE, k = u % WPE;
+    return ((const uint32_t*)src)[((size_t)e * p.ld + r) * WPE + k];
+  };
+  Msg pm;
+  msg_zero(pm);
+  msg_dst(pm, p.dst[7]);
+  msg_bytes16(pm, 9, blind);
+  msg_byte(pm, 25, agg_id);
+  msg_bytes16(pm, 26, nonce);
+  const uint32_t L = 42 + p.meas_len * F::ES;
+  const uint32_t B = L / 168, rem = L % 168;
+  KState s;
+  kzero(s);
+  for (uint32_t b = 0; b <= B; b++) {
+    uint32_t x[42];
+#pragma unroll
+    for (int j = 0; j < 42; j++) {
+      uint32_t v;
+      if (b == 0 && j < 10) {
+        v = pm.w[j];
+      } else if (b == 0 && j == 10) {
+        v = (pm.w[10] & 0xffffu) | (Sw(0) << 16);
+      } else {
+        const uint32_t u = 42 * b + j - 11;
+        v = __builtin_amdgcn_alignbit(Sw(u + 1), Sw(u), 16);
+      }
+      if (b == B) {
+        const uint32_t lo = 4 * j;
+        uint32_t mask = (lo + 4 <= rem) ? 0xffffffffu
+                                        : (lo >= rem ? 0u : ((1u << (8 * (rem - lo))) - 1u));
+        v &= mask;
+        if ((uint32_t)j == (rem >> 2)) v ^= 1u << (8 * (rem & 3));
+        if (j == 41) v ^= 0x80000000u;
+      }
+      x[j] = v;
+    }
+#pragma unroll
+    for (int j = 0; j < 42; j++) kxor_word(s, j, x[j]);
+    keccak_p12(s);
+  }
+  for (int k = 0; k < 4; k++) part[k] = kword(s, k);
+}
+
+template <class F>
+DEV void seed_of(const DevParams& p, uint32_t usage, const uint32_t* seed16, const uint32_t* a,
+                 const uint32_t* b, uint32_t* out) {  // derive_seed(seed, dst(usage), a || b)
+  KState s;
+  kzero(s);
+  Msg m;
+  msg_zero(m);
+  msg_dst(m, p.dst[usage]);
+  msg_bytes16(m, 9, seed16);
+  msg_bytes16(m, 25, a);
+  msg_bytes16(m, 41, b);
+  msg_absorb_final(s, m, 57);
+  for (int k = 0; k < 4; k++) out[k] = kword(s, k);
+}
+
+// out[c] = IDFT_n(in)[c] (natural order in and out; tmp is scratch)
+template <class F>
+DEV void idft_lane(const DevParams& p, const void* in, uint32_t in_len, void* out, uint32_t n,
+                   uint32_t logn, uint32_t r, typename F::T n_inv) {
+  typedef typename F::T T;
+  const size_t ld = p.ld;
+  for (uint32_t e = 0; e < n; e++)
+    F::store(out, (size_t)bitrev(e, logn) * ld + r,
+             e < in_len ? F::load(in, (size_t)e * ld + r) : F::zero());
+  dft_lane<F>(p, out, r, n, logn);
+  // out[c] <- out[(n - c) % n] / n
+  F::store(out, r, F::mul(F::load(out, r), n_inv));
+  F::store(out, (size_t)(n / 2) * ld + r, F::mul(F::load(out, (size_t)(n / 2) * ld + r), n_inv));
+  for (uint32_t c = 1; c < n / 2; c++) {
+    T a = F::load(out, (size_t)c * ld + r), b = F::load(out, (size_t)(n - c) * ld + r);
+    F::store(out, (size_t)c * ld + r, F::mul(b, n_inv));
+    F::store(out, (size_t)(n - c) * ld + r, F::mul(a, n_inv));
+  }
+}
+
+template <class F>
+DEV typename F::T gadget_eval_lane(const DevParams& p, const void* ev, uint32_t k, uint32_t n2,
+                                   uint32_t r) {
+  typedef typename F::T T;
+  const size_t ld = p.ld;
+  auto E = [&](uint32_t w) { return F::load(ev, ((size_t)w * n2 + k) * ld + r); };
+  if (p.kind == PRIO3_COUNT) return F::mul(E(0), E(1));
+  if (p.kind == PRIO3_SUM) {
+    T x = E(0);
+    return F::sub(F::mul(x, x), x);
+  }
+  T s = F::zero();
+  for (uint32_t j = 0; j < p.chunk; j++) s = F::add(s, F::mul(E(2 * j), E(2 * j + 1)));
+  return s;
+}
+
+template <class F>
+__global__ __launch_bounds__(64) void k_gen(DevParams p, uint64_t seed, uint64_t first,
+                                            GenScratch gs, GenOut go, typename F::T invP,
+                                            typename F::T inv2P) {
+  typedef typename F::T T;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= p.n) return;
+  const size_t ld = p.ld;
+  const uint64_t idx = first + r;
+  const uint32_t M = p.meas_len, A = p.arity, P = p.P, P2 = 2 * P, PL = p.proof_len;
+  const bool JR = p.jr_len > 0;
+  const uint32_t mstride = p.kind == PRIO3_SUMVEC ? p.length_or_zero : 1;
+  uint32_t flag = 0;
+  // ---- per-report stream: nonce || rand || measurement bytes ----
+  KState st;
+  kzero(st);
+  {
+    Msg m;
+    msg_zero(m);
+    const char tag[13] = {'j', 'a', 'n', 'u', 's', '-', 'a', 'm', 'd', '-', 'g', 'e', 'n'};
+    for (int i = 0; i < 13; i++) msg_byte(m, i, (uint8_t)tag[i]);
+    for (int i = 0; i < 8; i++) msg_byte(m, 13 + i, (uint32_t)(seed >> (8 * i)));
+    for (int i = 0; i < 8; i++) msg_byte(m, 21 + i, (uint32_t)(idx >> (8 * i)));
+    msg_absorb_final(st, m, 29);
+  }
+  uint32_t nonce[4], k_hm[4], k_hp[4], k_hb[4] = {0, 0, 0, 0}, k_lb[4] = {0, 0, 0, 0}, k_pr[4];
+  for (int k = 0; k < 4; k++) {
+    nonce[k] = kword(st, k);
+    k_hm[k] = kword(st, 4 + k);
+    k_hp[k] = kword(st, 8 + k);
+  }
+  if (JR) {
+    for (int k = 0; k < 4; k++) {
+      k_hb[k] = kword(st, 12 + k);
+      k_lb[k] = kword(st, 16 + k);
+      k_pr[k] = kword(st, 20 + k);
+    }
+  } else {
+    for (int k = 0; k < 4; k++) k_pr[k] = kword(st, 12 + k);
+  }
+  // measurement bytes start at stream byte 96 (word 24); 168-byte blocks
+  uint32_t blk = 0;
+  auto stream_word = [&](uint32_t wi) -> uint32_t {  // wi: absolute word index, non-decreasing
+    while (wi >= 42 * (blk + 1)) {
+      keccak_p12(st);
+      blk++;
+    }
+    uint32_t w = wi - 42 * blk;
+    uint32_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 42; q++)
+      if ((uint32_t)q == w) v = kword(st, q);
+    return v;
+  };
+  // encode measurement into gs.meas and record it
+  for (uint32_t e = 0; e < M; e++) Fp128Or64Store<F>::zero(gs.meas, (size_t)e * ld + r);
+  for (uint32_t e = 0; e < mstride; e++) {
+    uint64_t v = (uint64_t)stream_word(24 + 2 * e) | ((uint64_t)stream_word(25 + 2 * e) << 32);
+    switch (p.kind) {
+      case PRIO3_COUNT:
+        v &= 1;
+        break;
+      case PRIO3_SUM:
+      case PRIO3_SUMVEC:
+        if (p.bits < 64) v &= (1ull << p.bits) - 1;
+        break;
+      default:
+        v %= p.length_or_zero;
+        break;
+    }
+    if (go.meas) go.meas[(size_t)idx * 0 + (size_t)r * mstride + e] = v;
+    if (p.kind == PRIO3_HISTOGRAM) {
+      F::store(gs.meas, (size_t)v * ld + r, F::one());
+    } else if (p.kind == PRIO3_COUNT) {
+      F::store(gs.meas, r, F::from_u32((uint32_t)v));
+    } else {
+      for (uint32_t b = 0; b < p.bits; b++)
+        F::store(gs.meas, (size_t)(e * p.bits + b) * ld + r, F::from_u32((uint32_t)((v >> b) & 1)));
+    }
+  }
+  // ---- shard ----
+  const uint8_t b_hm[1] = {1};
+  expand_to<F>(p, p.dst[1], k_hm, b_hm, 1, M, gs.hm, r, flag);
+  for (uint32_t e = 0; e < M; e++)
+    F::store(gs.lm, (size_t)e * ld + r,
+             F::sub(F::load(gs.meas, (size_t)e * ld + r), F::load(gs.hm, (size_t)e * ld + r)));
+  uint32_t part0[4] = {0, 0, 0, 0}, part1[4] = {0, 0, 0, 0}, jseed[4];
+  if (JR) {
+    jr_part_scratch<F>(p, k_hb, 1, nonce, gs.hm, r, part1);
+    jr_part_scratch<F>(p, k_lb, 0, nonce, gs.lm, r, part0);
+    const uint32_t zero[4] = {0, 0, 0, 0};
+    seed_of<F>(p, 6, zero, part0, part1, jseed);
+    const uint8_t b1[1] = {1};
+    expand_to<F>(p, p.dst[3], jseed, b1, 1, p.jr_len, gs.jr, r, flag);
+  }
+  {
+    const uint8_t b1[1] = {1};
+    expand_to<F>(p, p.dst[4], k_pr, b1, 1, A, gs.prand, r, flag);
+  }
+  // ---- prove: record wires (num_shares = 1) ----
+  for (uint32_t w = 0; w < A; w++) {
+    F::store(gs.wires, ((size_t)w * P) * ld + r, F::load(gs.prand, (size_t)w * ld + r));
+    for (uint32_t c = 1; c < P; c++) F::store(gs.wires, ((size_t)w * P + c) * ld + r, F::zero());
+  }
+  auto wset = [&](uint32_t w, uint32_t c, const T& x) {
+    F::store(gs.wires, ((size_t)w * P + c) * ld + r, x);
+  };
+  if (p.kind == PRIO3_COUNT) {
+    T m = F::load(gs.meas, r);
+    wset(0, 1, m);
+    wset(1, 1, m);
+  } else if (p.kind == PRIO3_SUM) {
+    for (uint32_t i = 0; i < M; i++) wset(0, i + 1, F::load(gs.meas, (size_t)i * ld + r));
+  } else {
+    const T r0 = F::load(gs.jr, r);
+    T rp = r0;
+    for (uint32_t k = 0; k < p.calls; k++)
+      for (uint32_t j = 0; j < p.chunk; j++) {
+        const uint32_t i = k * p.chunk + j;
+        const T m = i < M ? F::load(gs.meas, (size_t)i * ld + r) : F::zero();
+        wset(2 * j, k + 1, F::mul(rp, m));
+        wset(2 * j + 1, k + 1, F::sub(m, F::one()));
+        rp = F::mul(rp, r0);
+      }
+  }
+  // ---- wire polys -> evaluations on the 2P-th roots ----
+  for (uint32_t w = 0; w < A; w++) {
+    void* wcol = (uint8_t*)gs.wires + (size_t)w * P * ld * F::ES;
+    idft_lane<F>(p, wcol, P, gs.tmp, P, p.logP, r, invP);  // coefficients in tmp[0..P)
+    void* ecol = (uint8_t*)gs.evals + (size_t)w * P2 * ld * F::ES;
+    for (uint32_t e = 0; e < P2; e++)
+      F::store(ecol, (size_t)bitrev(e, p.logP + 1) * ld + r,
+               e < P ? F::load(gs.tmp, (size_t)e * ld + r) : F::zero());
+    dft_lane<F>(p, ecol, r, P2, p.logP + 1);
+  }
+  for (uint32_t k = 0; k < P2; k++)
+    F::store(gs.g, (size_t)k * ld + r, gadget_eval_lane<F>(p, gs.evals, k, P2, r));
+  idft_lane<F>(p, gs.g, P2, gs.tmp, P2, p.logP + 1, r, inv2P);  // gadget poly coefficients
+  // proof = prove_rand || coeffs[0..glen)
+  for (uint32_t w = 0; w < A; w++) F::store(gs.proof, (size_t)w * ld + r, F::load(gs.prand, (size_t)w * ld + r));
+  for (uint32_t e = 0; e < p.glen; e++)
+    F::store(gs.proof, (size_t)(A + e) * ld + r, F::load(gs.tmp, (size_t)e * ld + r));
+  // leader proofs share = proof - helper proofs share
+  {
+    const uint8_t b2[2] = {1, 1};
+    expand_to<F>(p, p.dst[2], k_hp, b2, 2, PL, gs.hp, r, flag);
+    for (uint32_t e = 0; e < PL; e++)
+      F::store(gs.hp, (size_t)e * ld + r,
+               F::sub(F::load(gs.proof, (size_t)e * ld + r), F::load(gs.hp, (size_t)e * ld + r)));
+  }
+  // ---- leader prepare_init (agg_id 0): query on (lm, leader proofs share) ----
+  {
+    KState s;
+    kzero(s);
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[5]);
+    msg_bytes16(m, 9, p.vk);
+    msg_byte(m, 25, 1);
+    msg_bytes16(m, 26, nonce);
+    msg_absorb_final(s, m, 42);
+    uint32_t w[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
+    put_elem<F>(p, gs.qr, 0, r, w, flag);
+  }
+  const T t = F::load(gs.qr, r);
+  T v, pt;
+  if (!flp_query_lane<F>(p, gs.lm, gs.hp, gs.jr, t, gs.L, gs.PV, gs.acc, r, v, pt)) flag = 1;
+  uint8_t* lps = go.leader_ps + (size_t)r * p.prep_share_len;
+  F::store(lps, 0, v);
+  for (uint32_t w = 0; w < A; w++) F::store(lps, 1 + w, F::load(gs.acc, (size_t)w * ld + r));
+  F::store(lps, A + 1, pt);
+  if (JR) *(uint4*)(lps + (size_t)p.verifier_len * F::ES) = make_uint4(part0[0], part0[1], part0[2], part0[3]);
+  // ---- public outputs ----
+  *(uint4*)(go.nonces + 16 * (size_t)r) = make_uint4(nonce[0], nonce[1], nonce[2], nonce[3]);
+  uint8_t* hs = go.helper + (size_t)r * p.helper_share_len;
+  *(uint4*)hs = make_uint4(k_hm[0], k_hm[1], k_hm[2], k_hm[3]);
+  *(uint4*)(hs + 16) = make_uint4(k_hp[0], k_hp[1], k_hp[2], k_hp[3]);
+  if (JR) {
+    *(uint4*)(hs + 32) = make_uint4(k_hb[0], k_hb[1], k_hb[2], k_hb[3]);
+    uint8_t* pb = go.pub + (size_t)r * p.public_share_len;
+    *(uint4*)pb = make_uint4(part0[0], part0[1], part0[2], part0[3]);
+    *(uint4*)(pb + 16) = make_uint4(part1[0], part1[1], part1[2], part1[3]);
+  }
+  // leader output share = truncate(leader meas share)
+  if (go.leader_out) {
+    uint8_t* lo = go.leader_out + (size_t)r * p.out_len * F::ES;
+    if (p.kind == PRIO3_SUM || p.kind == PRIO3_SUMVEC) {
+      const uint32_t outs = p.kind == PRIO3_SUM ? 1 : p.out_len;
+      for (uint32_t e = 0; e < outs; e++) {
+        T acc = F::zero(), pw = F::one();
+        for (uint32_t b = 0; b < p.bits; b++) {
+          acc = F::add(acc, F::mul(pw, F::load(gs.lm, (size_t)(e * p.bits + b) * ld + r)));
+          pw = F::add(pw, pw);
+        }
+        F::store(lo, e, acc);
+      }
+    } else {
+      for (uint32_t e = 0; e < M; e++) F::store(lo, e, F::load(gs.lm, (size_t)e * ld + r));
+    }
+  }
+  if (go.flags) go.flags[r] = (uint8_t)flag;
+}

@@ -1,0 +1,233 @@
+// prio3_common.h -- kernel-side structures and per-lane building blocks shared by the
+// helper engine (prio3_engine.hip) and the synthetic client (prio3_client.hip).
+#pragma once
+#include "../../include/janus_prio3.h"
+#include "prio3_device.h"
+
+#define MAX_ROOTS 20
+
+struct DevParams {
+  uint32_t kind, es, meas_len, out_len, jr_len, arity, calls, P, logP, glen, proof_len,
+      verifier_len, chunk, bits, prep_share_len, helper_share_len, public_share_len;
+  uint32_t n, ld, force_slow;
+  uint32_t vk[4];
+  uint32_t dst[8][2];
+  uint32_t roots128[MAX_ROOTS + 1][4];
+  uint64_t roots64[MAX_ROOTS + 1];
+  uint32_t invP128[4], half128[4];
+  uint64_t invP64, half64;
+};
+
+struct InPtrs {
+  const uint8_t* nonces;
+  const uint8_t* pub;
+  const uint8_t* helper;
+  const uint8_t* leader;
+};
+
+struct Scratch {
+  void* meas;
+  void* proofs;
+  void* jr;
+  void* qr;
+  uint4* part;
+  uint4* corrected;
+  uint8_t* flag;
+  void* Lbuf;
+  void* PVbuf;
+  void* acc;
+  void* out;
+};
+
+struct OutPtrs {
+  uint8_t* prep_msgs;
+  uint8_t* status;
+};
+
+template <class F>
+struct FC;  // per-field constants from DevParams
+template <>
+struct FC<Fp128> {
+  static DEV f128 root(const DevParams& p, int l) { return Fp128::from_words(p.roots128[l]); }
+  static DEV f128 invP(const DevParams& p) { return Fp128::from_words(p.invP128); }
+  static DEV f128 half(const DevParams& p) { return Fp128::from_words(p.half128); }
+};
+template <>
+struct FC<Fp64> {
+  static DEV uint64_t root(const DevParams& p, int l) { return p.roots64[l]; }
+  static DEV uint64_t invP(const DevParams& p) { return p.invP64; }
+  static DEV uint64_t half(const DevParams& p) { return p.half64; }
+};
+
+DEV void load16(const uint8_t* p, uint32_t* w) {
+  uint4 v = *(const uint4*)p;
+  w[0] = v.x;
+  w[1] = v.y;
+  w[2] = v.z;
+  w[3] = v.w;
+}
+
+// ------------------------------------------------------------------------------------
+// k_xof: fast path (no rejection)
+// ------------------------------------------------------------------------------------
+template <class F>
+DEV void put_elem(const DevParams& p, void* base, uint32_t idx, uint32_t r, const uint32_t* w,
+                  uint32_t& flag) {
+  typename F::T x = F::from_words(w);
+  if (!F::lt_p(x)) flag = 1;
+  F::store(base, (size_t)idx * p.ld + r, x);
+}
+
+// Elements contained in squeeze block b of an XOF stream (no rejection).
+template <class F>
+DEV void squeeze_block(const DevParams& p, const KState& s, uint32_t b, uint32_t n_elems,
+                       uint32_t& pend0, uint32_t& pend1, void* base, uint32_t r,
+                       uint32_t& flag) {
+  if constexpr (F::ES == 16) {
+    uint32_t e0 = 21 * (b >> 1);
+    if ((b & 1) == 0) {
+#pragma unroll
+      for (int t = 0; t < 10; t++) {
+        uint32_t w[4] = {kword(s, 4 * t), kword(s, 4 * t + 1), kword(s, 4 * t + 2),
+                         kword(s, 4 * t + 3)};
+        if (e0 + t < n_elems) put_elem<F>(p, base, e0 + t, r, w, flag);
+      }
+      pend0 = kword(s, 40);
+      pend1 = kword(s, 41);
+    } else {
+      {
+        uint32_t w[4] = {pend0, pend1, kword(s, 0), kword(s, 1)};
+        if (e0 + 10 < n_elems) put_elem<F>(p, base, e0 + 10, r, w, flag);
+      }
+#pragma unroll
+      for (int t = 0; t < 10; t++) {
+        uint32_t w[4] = {kword(s, 2 + 4 * t), kword(s, 3 + 4 * t), kword(s, 4 + 4 * t),
+                         kword(s, 5 + 4 * t)};
+        if (e0 + 11 + t < n_elems) put_elem<F>(p, base, e0 + 11 + t, r, w, flag);
+      }
+    }
+  } else {
+    uint32_t e0 = 21 * b;
+#pragma unroll
+    for (int t = 0; t < 21; t++) {
+      uint32_t w[2] = {kword(s, 2 * t), kword(s, 2 * t + 1)};
+      if (e0 + t < n_elems) put_elem<F>(p, base, e0 + t, r, w, flag);
+    }
+  }
+}
+
+
+DEV uint32_t bitrev(uint32_t x, uint32_t d) { return __builtin_bitreverse32(x) >> (32 - d); }
+
+// In-place radix-2 DIT DFT of one lane's n-element SoA column (input in bit-reversed
+// order), twiddles from the field's principal 2^l-th roots -- the same butterfly order as
+// prio fft.rs discrete_fourier_transform.
+template <class F>
+DEV void dft_lane(const DevParams& p, void* buf, uint32_t r, uint32_t n, uint32_t logn) {
+  typedef typename F::T T;
+  const size_t ld = p.ld;
+  for (uint32_t l = 1; l <= logn; l++) {
+    const uint32_t half = 1u << (l - 1);
+    const T wl = FC<F>::root(p, l);
+    T w = F::one();
+    for (uint32_t i = 0; i < half; i++) {
+      for (uint32_t j = i; j < n; j += 2 * half) {
+        T u = F::load(buf, (size_t)j * ld + r);
+        T v = F::mul(w, F::load(buf, (size_t)(j + half) * ld + r));
+        F::store(buf, (size_t)j * ld + r, F::add(u, v));
+        F::store(buf, (size_t)(j + half) * ld + r, F::sub(u, v));
+      }
+      w = F::mul(w, wl);
+    }
+  }
+}
+
+template <class F>
+DEV typename F::T ldf(const void* base, uint32_t e, size_t ld, uint32_t r) {
+  return F::load(base, (size_t)e * ld + r);
+}
+
+
+// FlpGeneric::query for one report (one lane), num_shares = 2.  Writes the wire-polynomial
+// values at t into acc[0..arity) and returns v (circuit output share) and pt = p(t).
+// Returns false if t is a P-th root of unity (prio FlpError -> VdafPrepareInit).
+template <class F>
+DEV bool flp_query_lane(const DevParams& p, const void* meas, const void* proofs, const void* jr,
+                        typename F::T t, void* Lbuf, void* PVbuf, void* acc, uint32_t r,
+                        typename F::T& v, typename F::T& pt) {
+  typedef typename F::T T;
+  const size_t ld = p.ld;
+  const uint32_t P = p.P, A = p.arity;
+  T tp = t;
+  for (uint32_t l = 0; l < p.logP; l++) tp = F::mul(tp, tp);
+  const bool t_ok = !F::eq(tp, F::one());
+  // Lagrange basis at t: L_c = (1/P) sum_e t^e alpha^(-ce) = DFT(t^e / P)[(P - c) mod P]
+  {
+    T pw = FC<F>::invP(p);
+    for (uint32_t e = 0; e < P; e++) {
+      F::store(Lbuf, (size_t)bitrev(e, p.logP) * ld + r, pw);
+      pw = F::mul(pw, t);
+    }
+    dft_lane<F>(p, Lbuf, r, p.P, p.logP);
+  }
+  // gadget polynomial at the P-th roots: fold coefficients mod x^P - 1, DFT
+  for (uint32_t e = 0; e < P; e++) {
+    T q = ldf<F>(proofs, A + e, ld, r);
+    if (e + P < p.glen) q = F::add(q, ldf<F>(proofs, A + e + P, ld, r));
+    F::store(PVbuf, (size_t)bitrev(e, p.logP) * ld + r, q);
+  }
+  dft_lane<F>(p, PVbuf, r, p.P, p.logP);
+  // p(t)
+  pt = F::zero();
+  for (uint32_t e = p.glen; e-- > 0;) pt = F::add(F::mul(pt, t), ldf<F>(proofs, A + e, ld, r));
+  auto Lc = [&](uint32_t c) { return ldf<F>(Lbuf, (P - c) & (P - 1), ld, r); };
+  // wire accumulators start from the proof's wire seeds
+  {
+    const T L0 = Lc(0);
+    for (uint32_t w = 0; w < A; w++)
+      F::store(acc, (size_t)w * ld + r, F::mul(ldf<F>(proofs, w, ld, r), L0));
+  }
+  auto acc_add = [&](uint32_t w, const T& v) {
+    size_t idx = (size_t)w * ld + r;
+    F::store(acc, idx, F::add(F::load(acc, idx), v));
+  };
+  v = F::zero();
+  if (p.kind == PRIO3_COUNT) {
+    const T m = ldf<F>(meas, 0, ld, r);
+    const T x = F::mul(m, Lc(1));
+    acc_add(0, x);
+    acc_add(1, x);
+    v = F::sub(ldf<F>(PVbuf, 1, ld, r), m);
+  } else if (p.kind == PRIO3_SUM) {
+    const T r0 = ldf<F>(jr, 0, ld, r);
+    T rp = r0;
+    for (uint32_t i = 0; i < p.meas_len; i++) {
+      acc_add(0, F::mul(ldf<F>(meas, i, ld, r), Lc(i + 1)));
+      v = F::add(v, F::mul(rp, ldf<F>(PVbuf, i + 1, ld, r)));
+      rp = F::mul(rp, r0);
+    }
+  } else {
+    const T r0 = ldf<F>(jr, 0, ld, r);
+    const T half = FC<F>::half(p);
+    T rp = r0, range = F::zero(), sum = F::zero();
+    for (uint32_t k = 0; k < p.calls; k++) {
+      const T L = Lc(k + 1);
+      for (uint32_t j = 0; j < p.chunk; j++) {
+        const uint32_t i = k * p.chunk + j;
+        const T m = i < p.meas_len ? ldf<F>(meas, i, ld, r) : F::zero();
+        acc_add(2 * j, F::mul(F::mul(rp, m), L));
+        acc_add(2 * j + 1, F::mul(F::sub(m, half), L));
+        rp = F::mul(rp, r0);
+        sum = F::add(sum, m);
+      }
+      range = F::add(range, ldf<F>(PVbuf, k + 1, ld, r));
+    }
+    if (p.kind == PRIO3_SUMVEC) {
+      v = range;
+    } else {
+      const T r1 = ldf<F>(jr, 1, ld, r);
+      v = F::add(F::mul(r1, range), F::mul(F::mul(r1, r1), F::sub(sum, half)));
+    }
+  }
+  return t_ok;
+}
