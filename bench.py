@@ -1,0 +1,204 @@
+"""Benchmark: helper-side Prio3Histogram(length=256, chunk_length=16) prepare+aggregate on
+MI355X (BASELINE.json metric; configs[1]: 1M reports per GPU).
+
+One step = one device call over the whole resident batch: k_xof -> k_xof_slow (flagged
+reports only) -> k_query (FLP query, decide, prepare message, joint-rand check) -> masked
+segmented mod-p accumulate into the aggregate share; with N>1 ranks the per-GPU partial
+aggregate shares are RCCL-all-gathered over xGMI and summed mod p on every rank (RCCL's
+integer sum is mod 2^64, not mod p).  Reports are distinct, honest, seed-derived and
+generated on the device before timing (inputs resident in HBM when the timed region starts).
+
+Usage: python bench.py [--gpus N --steps K --warmup W]  (N>1 via torch.distributed.run)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from janus_amd import prio3 as J  # noqa: E402
+
+METRIC = "reports prepared+aggregated/sec (helper, Prio3Histogram len=256) at 1/2/4/8 GPUs"
+VK = bytes.fromhex("4a414e55532d414d442d42454e434821")
+
+# --- cost model (DESIGN.md "Roofline"): 32-bit VALU instructions per unit, counted from the
+# gfx950 code object: Keccak-p[1600,12] = 12 x 190 (v_bitop3/v_xor/v_alignbit), Field128
+# multiply = 110 (23 v_mad_u64_u32 + carries/selects), Field128 add = 15.
+OPS_PERM, OPS_MUL, OPS_ADD = 12 * 190, 110, 15
+# Per-report algorithmic work of Prio3Histogram(256,16) helper prep (SURVEY 8(d) counts):
+#   k_xof:   63 permutations (1 query rand + 25 meas + 25 joint-rand part + 10 proofs + 2)
+#   k_query: 1 permutation (prepare message) + 1331 F128 mul + ~1600 F128 add
+KERNEL_OPS = {
+    "k_xof": 63 * OPS_PERM,
+    "k_query": 1 * OPS_PERM + 1331 * OPS_MUL + 1600 * OPS_ADD,
+}
+# per-report HBM bytes the kernels must move at minimum (inputs + outputs; scratch excluded)
+KERNEL_BYTES = {"k_xof": 16 + 32 + 48, "k_query": 560 + 16 + 1,
+                "k_acc_partial": 256 * 16 + 1}
+PEAK_VALU_OPS = 256 * 4 * 32 * 2.4e9  # 78.6e12 lane-ops/s (MI355X_MICROARCH.md chip table)
+PEAK_HBM = 8.0e12
+
+
+def cpu_threads() -> int:
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(aff, int(env))) if env else aff
+
+
+def cpu_baseline(eng, data, n_gpu_sample: int, target_s: float = 10.0):
+    """The oracle (CPU restatement of prio 0.16.2, Janus job structure) timed on this host on a
+    bounded sample of the same (GPU-generated) reports; also cross-checks the GPU results."""
+    from oracle.oracle import Oracle, build
+    build()
+    o = Oracle("histogram", length=256, chunk_length=16)
+    th = cpu_threads()
+    host = {k: data[k][:n_gpu_sample].cpu().numpy() for k in
+            ("nonces", "public_shares", "helper_shares", "leader_prep_shares")}
+
+    def run(m):
+        t0 = time.perf_counter()
+        r = o.helper_batch(VK, host["nonces"][:m], host["public_shares"][:m],
+                           host["helper_shares"][:m], host["leader_prep_shares"][:m],
+                           n_threads=th, job_size=500)
+        return time.perf_counter() - t0, r
+
+    probe = min(n_gpu_sample, 500 * th)
+    dt, _ = run(probe)
+    m = int(min(n_gpu_sample, max(probe, probe * target_s / max(dt, 1e-6))))
+    dt, (msgs, status, agg, cnt) = run(m)
+    return dict(value=m / dt, unit="reports/s", cores=th, kind="port",
+                sample=f"{m} of the benchmark's GPU-generated reports, jobs of 500 reports, "
+                       f"one job per worker thread (aggregator.rs:1794,2100), {dt:.1f}s wall",
+                seconds=dt, n=m), (msgs, status, agg, cnt)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--reports", type=int, default=1 << 20, help="reports per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    n = args.reports
+
+    eng = J.HelperEngine(J.Prio3Histogram(256, 16), VK, device=local)
+    sz = eng.sz
+    data = eng.generate_reports_device(n, seed=0x4A414E5553000001, first_index=rank * n,
+                                       with_checks=True)
+    torch.cuda.synchronize()
+    flags = int(data["flags"].sum().item())
+    prep_msgs = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    seg = torch.zeros(n, dtype=torch.int32, device=dev)
+    agg = torch.zeros((1, sz.agg_share_len), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    if world > 1:
+        g_agg = torch.empty((world, sz.agg_share_len), dtype=torch.uint8, device=dev)
+        g_cnt = torch.empty((world,), dtype=torch.int64, device=dev)
+        fin_agg = torch.empty((1, sz.agg_share_len), dtype=torch.uint8, device=dev)
+        fin_cnt = torch.empty(1, dtype=torch.int64, device=dev)
+
+    def step():
+        s = torch.cuda.current_stream().cuda_stream
+        eng.prepare_device(data["nonces"], data["public_shares"], data["helper_shares"],
+                           data["leader_prep_shares"], prep_msgs, status, stream=s)
+        eng.accumulate_device(n, status, seg, None, 1, agg, cnt, stream=s)
+        if world > 1:
+            dist.all_gather_into_tensor(g_agg, agg)
+            dist.all_gather_into_tensor(g_cnt, cnt)
+            eng.combine_device(world, 1, g_agg, g_cnt, fin_agg, fin_cnt, stream=s)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    eng.set_option("timing", 1)
+    eng.timing_reset()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    times = eng.timing()
+    eng.set_option("timing", 0)
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ok = int((status == 0).sum().item())
+    final_cnt = int((fin_cnt if world > 1 else cnt)[0].item())
+    value = world * n * args.steps / elapsed
+
+    # roofline of the dominant kernel, from the live HIP-event times on the launch stream
+    per_kernel = {k: dict(ms_total=v[0], launches=v[1], ms_avg=v[0] / max(v[1], 1))
+                  for k, v in times.items()}
+    dom = max((k for k in per_kernel if k in KERNEL_OPS), key=lambda k: per_kernel[k]["ms_total"])
+    avg_s = per_kernel[dom]["ms_avg"] / 1e3
+    achieved = KERNEL_OPS[dom] * n / avg_s
+    roofline = dict(bound="valu", achieved=achieved / 1e12, peak=PEAK_VALU_OPS / 1e12,
+                    unit="Tops/s (32-bit VALU lane-ops)", frac=achieved / PEAK_VALU_OPS,
+                    traffic=None, kernel=dom, ms_avg=per_kernel[dom]["ms_avg"],
+                    ops_per_report=KERNEL_OPS[dom],
+                    hbm_algorithmic_GBps=KERNEL_BYTES[dom] * n / avg_s / 1e9,
+                    hbm_peak_GBps=PEAK_HBM / 1e9)
+
+    out = dict(metric=METRIC, value=value, unit="reports/s", n_gpus=world, steps=args.steps,
+               warmup=args.warmup, ms_per_step=elapsed / args.steps * 1e3,
+               higher_is_better=True, scaling="weak", vs_baseline=None,
+               dtype="u32 limbs (Field128 mod-p integer arithmetic)",
+               data="synthetic: distinct honest reports generated on-device from a seed "
+                    "(client shard + leader prepare_init); verify key fixed",
+               config=dict(workload="Prio3Histogram length=256 chunk_length=16 helper "
+                                    "prepare_init+prepare_shares_to_prepare_message+prepare_next"
+                                    "+aggregate, 1 segment",
+                           reports_per_gpu=n, global_batch=world * n,
+                           parallelism=f"dp{world} (report shards; RCCL all-gather + mod-p combine)"),
+               roofline=roofline, kernels=per_kernel,
+               checks=dict(finished=ok, generator_flags=flags, agg_count=final_cnt))
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb, (msgs, cst, cagg, ccnt) = cpu_baseline(eng, data, min(n, 1 << 20), args.cpu_seconds)
+        m = cb.pop("n")
+        gm = prep_msgs[:m].cpu().numpy()
+        gs = status[:m].cpu().numpy()
+        out["checks"]["cpu_gpu_parity_on_sample"] = bool(np.array_equal(gs, cst) and
+                                                         np.array_equal(gm, msgs))
+        out["cpu_baseline"] = cb
+        out["speedup_vs_cpu"] = value / cb["value"]
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

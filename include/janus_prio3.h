@@ -134,6 +134,20 @@ int prio3_device_combine(prio3_engine* engine, uint32_t k, uint32_t n_segments,
                          const uint8_t* d_in, const uint64_t* d_counts_in, uint8_t* d_out,
                          uint64_t* d_counts_out, void* stream);
 
+/* ---- Synthetic client (benchmarks and tests) ---- */
+/* Generates n honest reports on the device: the client's shard (prio Prio3::shard,
+ * client/src/lib.rs:339-341) and the leader's prepare_init (agg_id 0,
+ * aggregation_job_driver.rs:397-415), for the engine's instance and verify key.  Report i is
+ * derived from (seed, first_index + i) exactly like the oracle's generator.
+ * d_measurements: n x (SumVec: length, else 1) u64 (nullable); d_leader_out_shares:
+ * n x agg_share_len (nullable); d_flags: n bytes, non-zero if a rejection-sampling event made
+ * the report unusable (nullable). */
+int prio3_client_generate_device(prio3_engine* engine, uint32_t n, uint64_t seed,
+                                 uint64_t first_index, uint8_t* d_nonces,
+                                 uint8_t* d_public_shares, uint8_t* d_helper_shares,
+                                 uint8_t* d_leader_prep_shares, uint64_t* d_measurements,
+                                 uint8_t* d_leader_out_shares, uint8_t* d_flags, void* stream);
+
 /* ---- Test / measurement knobs ---- */
 /* force_slow_path=1 routes every report through the general rejection-sampling kernel. */
 int prio3_engine_set_option(prio3_engine* engine, const char* key, int64_t value);

@@ -161,7 +161,7 @@ __global__ __launch_bounds__(64) void k_gen(DevParams p, uint64_t seed, uint64_t
   const uint64_t idx = first + r;
   const uint32_t M = p.meas_len, A = p.arity, P = p.P, P2 = 2 * P, PL = p.proof_len;
   const bool JR = p.jr_len > 0;
-  const uint32_t mstride = p.kind == PRIO3_SUMVEC ? p.length_or_zero : 1;
+  const uint32_t mstride = p.kind == PRIO3_SUMVEC ? p.length : 1;
   uint32_t flag = 0;
   // ---- per-report stream: nonce || rand || measurement bytes ----
   KState st;
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(64) void k_gen(DevParams p, uint64_t seed, uint64_t
     return v;
   };
   // encode measurement into gs.meas and record it
-  for (uint32_t e = 0; e < M; e++) Fp128Or64Store<F>::zero(gs.meas, (size_t)e * ld + r);
+  for (uint32_t e = 0; e < M; e++) F::store(gs.meas, (size_t)e * ld + r, F::zero());
   for (uint32_t e = 0; e < mstride; e++) {
     uint64_t v = (uint64_t)stream_word(24 + 2 * e) | ((uint64_t)stream_word(25 + 2 * e) << 32);
     switch (p.kind) {
@@ -217,10 +217,10 @@ __global__ __launch_bounds__(64) void k_gen(DevParams p, uint64_t seed, uint64_t
         if (p.bits < 64) v &= (1ull << p.bits) - 1;
         break;
       default:
-        v %= p.length_or_zero;
+        v %= p.length;
         break;
     }
-    if (go.meas) go.meas[(size_t)idx * 0 + (size_t)r * mstride + e] = v;
+    if (go.meas) go.meas[(size_t)r * mstride + e] = v;
     if (p.kind == PRIO3_HISTOGRAM) {
       F::store(gs.meas, (size_t)v * ld + r, F::one());
     } else if (p.kind == PRIO3_COUNT) {
@@ -351,4 +351,94 @@ __global__ __launch_bounds__(64) void k_gen(DevParams p, uint64_t seed, uint64_t
     }
   }
   if (go.flags) go.flags[r] = (uint8_t)flag;
+}
+
+// ====================================================================================
+// Host ABI
+// ====================================================================================
+#define GCHK(x)                                                                       \
+  do {                                                                                \
+    hipError_t _e = (x);                                                              \
+    if (_e != hipSuccess) {                                                           \
+      fprintf(stderr, "janus_prio3: HIP error %s at %s:%d\n", hipGetErrorString(_e),  \
+              __FILE__, __LINE__);                                                    \
+      rc = PRIO3_EDEVICE;                                                             \
+      goto done;                                                                      \
+    }                                                                                 \
+  } while (0)
+
+static f128 h128(const uint32_t* w) {
+  f128 r;
+  for (int k = 0; k < 4; k++) r.w[k] = w[k];
+  return r;
+}
+
+extern "C" int prio3_client_generate_device(prio3_engine* e, uint32_t n, uint64_t seed,
+                                            uint64_t first_index, uint8_t* d_nonces,
+                                            uint8_t* d_public_shares, uint8_t* d_helper_shares,
+                                            uint8_t* d_leader_prep_shares,
+                                            uint64_t* d_measurements,
+                                            uint8_t* d_leader_out_shares, uint8_t* d_flags,
+                                            void* stream) {
+  if (!e || !d_nonces || !d_helper_shares || !d_leader_prep_shares) return PRIO3_EINVAL;
+  if (n == 0) return PRIO3_OK;
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (hipSetDevice(e->device) != hipSuccess) return PRIO3_EDEVICE;
+  hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+  DevParams p = e->dp;
+  const size_t es = p.es;
+  const uint32_t A = p.arity, P = p.P;
+  // per-report scratch elements
+  const size_t per = 3 * (size_t)p.meas_len + (size_t)A * P + (size_t)A * 2 * P + 4 * (size_t)P +
+                     2 * (size_t)p.proof_len + A + p.jr_len + 1 + 2 * P + A;
+  size_t chunk = ((size_t)2 << 30) / (per * es);  // <= 2 GiB of scratch
+  if (chunk > 65536) chunk = 65536;
+  chunk = chunk < 64 ? 64 : (chunk & ~(size_t)63);
+  std::vector<void*> bufs;
+  int rc = PRIO3_OK;
+  GenScratch gs;
+  void** slots[] = {&gs.meas, &gs.hm, &gs.lm, &gs.wires, &gs.evals, &gs.g, &gs.tmp, &gs.proof,
+                    &gs.hp, &gs.prand, &gs.jr, &gs.qr, &gs.L, &gs.PV, &gs.acc};
+  size_t counts[] = {p.meas_len, p.meas_len, p.meas_len, (size_t)A * P, (size_t)A * 2 * P,
+                     2 * (size_t)P, 2 * (size_t)P, p.proof_len, p.proof_len, A,
+                     p.jr_len ? p.jr_len : 1, 1, P, P, A};
+  for (size_t i = 0; i < sizeof(counts) / sizeof(counts[0]); i++) {
+    void* b = nullptr;
+    GCHK(hipMalloc(&b, counts[i] * chunk * es));
+    bufs.push_back(b);
+    *slots[i] = b;
+  }
+  {
+    u128 ip = hpow(p.P, HP128 - 2, HP128), i2 = hpow(2 * p.P, HP128 - 2, HP128);
+    uint32_t w1[4], w2[4];
+    for (int k = 0; k < 4; k++) {
+      w1[k] = (uint32_t)(ip >> (32 * k));
+      w2[k] = (uint32_t)(i2 >> (32 * k));
+    }
+    uint64_t ip64 = (uint64_t)hpow(p.P, HP64 - 2, HP64), i264 = (uint64_t)hpow(2 * p.P, HP64 - 2, HP64);
+    const uint32_t mstride = p.kind == PRIO3_SUMVEC ? p.length : 1;
+    for (uint64_t off = 0; off < n; off += chunk) {
+      const uint32_t m = (uint32_t)std::min<uint64_t>(chunk, n - off);
+      p.n = m;
+      p.ld = (uint32_t)chunk;
+      GenOut go;
+      go.nonces = d_nonces + 16 * off;
+      go.pub = d_public_shares ? d_public_shares + p.public_share_len * off : nullptr;
+      go.helper = d_helper_shares + p.helper_share_len * off;
+      go.leader_ps = d_leader_prep_shares + p.prep_share_len * off;
+      go.leader_out = d_leader_out_shares ? d_leader_out_shares + (size_t)p.out_len * es * off : nullptr;
+      go.meas = d_measurements ? d_measurements + (size_t)mstride * off : nullptr;
+      go.flags = d_flags ? d_flags + off : nullptr;
+      if (es == 16)
+        k_gen<Fp128><<<(m + 63) / 64, 64, 0, st>>>(p, seed, first_index + off, gs, go, h128(w1),
+                                                   h128(w2));
+      else
+        k_gen<Fp64><<<(m + 63) / 64, 64, 0, st>>>(p, seed, first_index + off, gs, go, ip64, i264);
+      GCHK(hipGetLastError());
+    }
+  }
+  GCHK(hipStreamSynchronize(st));
+done:
+  for (auto b : bufs) (void)hipFree(b);
+  return rc;
 }

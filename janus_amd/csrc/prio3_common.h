@@ -1,6 +1,9 @@
 // prio3_common.h -- kernel-side structures and per-lane building blocks shared by the
 // helper engine (prio3_engine.hip) and the synthetic client (prio3_client.hip).
 #pragma once
+#include <mutex>
+#include <string>
+#include <vector>
 #include "../../include/janus_prio3.h"
 #include "prio3_device.h"
 
@@ -8,7 +11,7 @@
 
 struct DevParams {
   uint32_t kind, es, meas_len, out_len, jr_len, arity, calls, P, logP, glen, proof_len,
-      verifier_len, chunk, bits, prep_share_len, helper_share_len, public_share_len;
+      verifier_len, chunk, bits, length, prep_share_len, helper_share_len, public_share_len;
   uint32_t n, ld, force_slow;
   uint32_t vk[4];
   uint32_t dst[8][2];
@@ -231,3 +234,70 @@ DEV bool flp_query_lane(const DevParams& p, const void* meas, const void* proofs
   }
   return t_ok;
 }
+
+// host-side field helpers (parameter setup only)
+namespace {
+
+typedef unsigned __int128 u128;
+const u128 HP128 = (((u128)0xffffffffffffffe4ULL) << 64) | 1;
+const uint64_t HP64 = 0xffffffff00000001ULL;
+
+u128 hmul(u128 a, u128 b, u128 p) {  // slow but simple: double-and-add
+  u128 r = 0;
+  a %= p;
+  while (b) {
+    if (b & 1) {
+      r += a;
+      if (r < a || r >= p) r -= p;
+    }
+    u128 a2 = a + a;
+    if (a2 < a || a2 >= p) a2 -= p;
+    a = a2;
+    b >>= 1;
+  }
+  return r;
+}
+u128 hpow(u128 a, u128 e, u128 p) {
+  u128 r = 1;
+  while (e) {
+    if (e & 1) r = hmul(r, a, p);
+    a = hmul(a, a, p);
+    e >>= 1;
+  }
+  return r;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------
+// Host-side engine object (shared by both translation units)
+// ------------------------------------------------------------------------------------
+struct KTime {
+  std::string name;
+  double ms = 0;
+  uint64_t launches = 0;
+};
+
+struct prio3_engine {
+  prio3_params params;
+  prio3_sizes_t sz;
+  DevParams dp;
+  int device;
+  hipStream_t stream;
+  uint32_t cap = 0;  // scratch capacity (reports)
+  Scratch sc{};
+  void* d_prep_partial = nullptr;
+  size_t partial_cap = 0;
+  uint64_t* d_pcount = nullptr;
+  uint8_t* d_mask = nullptr;
+  // host-API staging
+  uint32_t io_cap = 0;
+  uint8_t *d_nonces = nullptr, *d_pub = nullptr, *d_helper = nullptr, *d_leader = nullptr,
+          *d_msgs = nullptr, *d_status = nullptr;
+  int force_slow = 0;
+  int timing = 0;
+  std::vector<KTime> times;
+  std::vector<hipEvent_t> ev_pool;
+  std::mutex mu;
+};
+

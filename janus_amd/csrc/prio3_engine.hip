@@ -519,67 +519,7 @@ __global__ void k_combine(uint32_t k, uint32_t len, uint32_t n_segments, const u
 // ====================================================================================
 // Host side
 // ====================================================================================
-namespace {
 
-typedef unsigned __int128 u128;
-const u128 HP128 = (((u128)0xffffffffffffffe4ULL) << 64) | 1;
-const uint64_t HP64 = 0xffffffff00000001ULL;
-
-u128 hmul(u128 a, u128 b, u128 p) {  // slow but simple: double-and-add
-  u128 r = 0;
-  a %= p;
-  while (b) {
-    if (b & 1) {
-      r += a;
-      if (r < a || r >= p) r -= p;
-    }
-    u128 a2 = a + a;
-    if (a2 < a || a2 >= p) a2 -= p;
-    a = a2;
-    b >>= 1;
-  }
-  return r;
-}
-u128 hpow(u128 a, u128 e, u128 p) {
-  u128 r = 1;
-  while (e) {
-    if (e & 1) r = hmul(r, a, p);
-    a = hmul(a, a, p);
-    e >>= 1;
-  }
-  return r;
-}
-
-struct KTime {
-  std::string name;
-  double ms = 0;
-  uint64_t launches = 0;
-};
-
-}  // namespace
-
-struct prio3_engine {
-  prio3_params params;
-  prio3_sizes_t sz;
-  DevParams dp;
-  int device;
-  hipStream_t stream;
-  uint32_t cap = 0;  // scratch capacity (reports)
-  Scratch sc{};
-  void* d_prep_partial = nullptr;
-  size_t partial_cap = 0;
-  uint64_t* d_pcount = nullptr;
-  uint8_t* d_mask = nullptr;
-  // host-API staging
-  uint32_t io_cap = 0;
-  uint8_t *d_nonces = nullptr, *d_pub = nullptr, *d_helper = nullptr, *d_leader = nullptr,
-          *d_msgs = nullptr, *d_status = nullptr;
-  int force_slow = 0;
-  int timing = 0;
-  std::vector<KTime> times;
-  std::vector<hipEvent_t> ev_pool;
-  std::mutex mu;
-};
 
 struct prio3_batch {
   prio3_engine* e;
@@ -600,6 +540,7 @@ static int fill_sizes(const prio3_params* pp, prio3_sizes_t* s, DevParams* dp) {
   memset(&d, 0, sizeof d);
   d.kind = pp->kind;
   d.bits = pp->bits;
+  d.length = pp->length;
   d.chunk = pp->chunk_length;
   uint32_t algo;
   switch (pp->kind) {

@@ -72,6 +72,7 @@ EXPORTED_SYMBOLS = (
     "prio3_accumulate", "prio3_debug_output_shares", "prio3_batch_free", "prio3_device_prepare",
     "prio3_device_accumulate", "prio3_device_output_shares", "prio3_device_combine",
     "prio3_engine_set_option", "prio3_engine_timing", "prio3_engine_timing_reset",
+    "prio3_client_generate_device",
 )
 
 _lib = None
@@ -85,6 +86,14 @@ def load_library() -> C.CDLL:
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"janus_amd HIP engine not built: {LIB_PATH} is missing "
                           "(run `make -C janus_amd` or __graft_entry__.build())")
+    # One HIP runtime per process: when PyTorch-ROCm is present its bundled libamdhip64
+    # (SONAME libamdhip64.so.7) must be the copy our NEEDED entry binds to, otherwise two HSA
+    # runtimes coexist and the second one sees no GPU.  Importing torch first makes the
+    # dynamic linker reuse torch's runtime for libjanus_prio3.so.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     P, u8p, vp = C.POINTER, C.POINTER(C.c_uint8), C.c_void_p
     L.prio3_sizes.argtypes = [P(Prio3Params), P(Prio3Sizes)]
@@ -100,6 +109,8 @@ def load_library() -> C.CDLL:
     L.prio3_device_accumulate.argtypes = [vp, C.c_uint32, vp, vp, vp, C.c_uint32, vp, vp, vp]
     L.prio3_device_output_shares.argtypes = [vp, C.c_uint32, vp]
     L.prio3_device_combine.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp]
+    L.prio3_client_generate_device.argtypes = [vp, C.c_uint32, C.c_uint64, C.c_uint64, vp, vp,
+                                               vp, vp, vp, vp, vp, vp]
     L.prio3_engine_set_option.argtypes = [vp, C.c_char_p, C.c_int64]
     L.prio3_engine_timing.argtypes = [vp, C.c_char_p, C.c_size_t, P(C.c_double),
                                       P(C.c_uint64), C.c_int]
@@ -285,6 +296,38 @@ class HelperEngine:
         rc = load_library().prio3_device_output_shares(self.handle, n, _np_ptr(out))
         if rc:
             raise RuntimeError("prio3_device_output_shares failed")
+        return out
+
+    # ---- synthetic client ------------------------------------------------------------
+    def generate_reports_device(self, n: int, seed: int = 1, first_index: int = 0,
+                                with_checks: bool = False, stream=None) -> dict:
+        """Honest synthetic reports generated on the GPU (shard + leader prepare_init).
+
+        Returns torch uint8 tensors on this engine's device (plus measurements / leader
+        output shares / flags when ``with_checks``)."""
+        import torch
+        sz = self.sz
+        dev = torch.device("cuda", self.device)
+        u8 = dict(dtype=torch.uint8, device=dev)
+        out = dict(nonces=torch.empty((n, 16), **u8),
+                   public_shares=torch.empty((n, max(sz.public_share_len, 1)), **u8),
+                   helper_shares=torch.empty((n, sz.helper_share_len), **u8),
+                   leader_prep_shares=torch.empty((n, sz.prep_share_len), **u8))
+        if with_checks:
+            mstride = self.vdaf.length if self.vdaf.kind == PRIO3_SUMVEC else 1
+            out["measurements"] = torch.empty((n, mstride), dtype=torch.int64, device=dev)
+            out["leader_out_shares"] = torch.empty((n, sz.agg_share_len), **u8)
+            out["flags"] = torch.zeros(n, **u8)
+        rc = load_library().prio3_client_generate_device(
+            self.handle, n, seed, first_index, _tptr(out["nonces"]),
+            _tptr(out["public_shares"]) if sz.public_share_len else None,
+            _tptr(out["helper_shares"]), _tptr(out["leader_prep_shares"]),
+            _tptr(out.get("measurements")), _tptr(out.get("leader_out_shares")),
+            _tptr(out.get("flags")), C.c_void_p(stream) if stream else None)
+        if rc:
+            raise RuntimeError(f"prio3_client_generate_device failed (rc={rc})")
+        if not sz.public_share_len:
+            out["public_shares"] = out["public_shares"][:, :0]
         return out
 
     # ---- measurement ----------------------------------------------------------------

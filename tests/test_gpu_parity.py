@@ -151,3 +151,56 @@ def test_unshard_equals_plaintext_histogram():
     exp = np.bincount(d["measurements"][:, 0].astype(np.int64), minlength=256)
     assert tot == [int(x) for x in exp]
     assert int(cnt[0]) == n
+
+
+GEN_CASES = ["count", "sum8", "sum32", "sumvec_8x10_c9", "sumvec_1x1_c1", "hist_256_c16",
+             "hist_10_c3", "hist_1_c1"]
+
+
+@pytest.mark.parametrize("name", GEN_CASES)
+def test_device_generator_matches_oracle_generator(name):
+    """The on-device client (shard + leader prepare_init) is bit-exact with the oracle's."""
+    cfg = CONFIGS[name]
+    eng = _engine(cfg)
+    o = _oracle(cfg)
+    first, n = 5, 70
+    d = eng.generate_reports_device(n, seed=99, first_index=first, with_checks=True)
+    ref = o.gen_reports(VK, first + n, seed=99, n_threads=8)
+    assert not d["flags"].any()
+    for k in ("nonces", "public_shares", "helper_shares", "leader_prep_shares",
+              "leader_out_shares"):
+        np.testing.assert_array_equal(d[k].cpu().numpy(), ref[k][first:], err_msg=k)
+    np.testing.assert_array_equal(d["measurements"].cpu().numpy().astype(np.uint64),
+                                  ref["measurements"][first:])
+
+
+def test_full_size_histogram_unshard_property():
+    """BASELINE configs[1] size (1M reports): leader agg (from the generator's leader output
+    shares) + helper agg (engine) unshards to the plaintext histogram; every report finishes."""
+    import torch
+    from oracle.oracle import sum_mod, decode_elems, field_modulus
+    from janus_amd import prio3 as J
+    eng = J.HelperEngine(J.Prio3Histogram(256, 16), VK, device=0)
+    n = 1 << 20
+    d = eng.generate_reports_device(n, seed=2024, with_checks=True)
+    assert int(d["flags"].sum()) == 0
+    dev = d["nonces"].device
+    msgs = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    agg = torch.zeros((1, 4096), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    eng.prepare_device(d["nonces"], d["public_shares"], d["helper_shares"],
+                       d["leader_prep_shares"], msgs, status)
+    eng.accumulate_device(n, status, None, None, 1, agg, cnt)
+    torch.cuda.synchronize()
+    assert int((status != 0).sum()) == 0 and int(cnt[0]) == n
+    p = field_modulus("histogram")
+    la = [0] * 256
+    step = 1 << 16
+    for i in range(0, n, step):
+        part = sum_mod(d["leader_out_shares"][i:i + step].cpu().numpy(), 16, p)
+        la = [(a + b) % p for a, b in zip(la, part)]
+    ha = decode_elems(agg[0].cpu().numpy(), 16)
+    tot = [(a + b) % p for a, b in zip(la, ha)]
+    exp = torch.bincount(d["measurements"][:, 0], minlength=256).cpu().tolist()
+    assert tot == exp
