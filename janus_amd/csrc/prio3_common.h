@@ -18,6 +18,9 @@ struct DevParams {
   uint32_t roots128[MAX_ROOTS + 1][4];
   uint64_t roots64[MAX_ROOTS + 1];
   uint32_t invP128[4], half128[4];
+  // P <= 32 only: sigma_e = sum_{c=1..calls} alpha^(ce) and twiddles alpha_P^i (i < P/2)
+  uint32_t sigma128[32][4];
+  uint32_t tw128[16][4];
   uint64_t invP64, half64;
 };
 
@@ -40,6 +43,7 @@ struct Scratch {
   void* PVbuf;
   void* acc;
   void* out;
+  void* beta;
 };
 
 struct OutPtrs {

@@ -30,6 +30,10 @@ DEV f128 mk128(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   return r;
 }
 DEV f128 zero128() { return mk128(0, 0, 0, 0); }
+// element-wise select (a struct-valued ?: can be lowered through private memory)
+DEV f128 sel128(bool c, const f128& a, const f128& b) {
+  return mk128(c ? a.w[0] : b.w[0], c ? a.w[1] : b.w[1], c ? a.w[2] : b.w[2], c ? a.w[3] : b.w[3]);
+}
 DEV f128 one128() { return mk128(1, 0, 0, 0); }
 DEV bool is_zero128(const f128& a) { return (a.w[0] | a.w[1] | a.w[2] | a.w[3]) == 0; }
 DEV bool eq128(const f128& a, const f128& b) {
@@ -66,7 +70,7 @@ DEV f128 canon128(const f128& x) {
   d.w[1] = subb(x.w[1], P128_1, b0, &b1);
   d.w[2] = subb(x.w[2], P128_2, b1, &b2);
   d.w[3] = subb(x.w[3], P128_3, b2, &b3);
-  return b3 ? x : d;
+  return sel128(b3 != 0, x, d);
 }
 
 DEV f128 add128(const f128& a, const f128& b) {
@@ -81,7 +85,7 @@ DEV f128 add128(const f128& a, const f128& b) {
   d.w[2] = subb(s.w[2], P128_2, b1, &b2);
   d.w[3] = subb(s.w[3], P128_3, b2, &b3);
   bool use_d = c3 | (b3 ^ 1u);
-  return use_d ? d : s;
+  return sel128(use_d, d, s);
 }
 
 DEV f128 sub128(const f128& a, const f128& b) {
@@ -197,6 +201,7 @@ struct Fp128 {
   static DEV bool eq(const T& a, const T& b) { return eq128(a, b); }
   static DEV bool is_zero(const T& a) { return is_zero128(a); }
   static DEV bool lt_p(const T& a) { return !ge_p128(a); }
+  static DEV T sel(bool c, const T& a, const T& b) { return sel128(c, a, b); }
   static DEV T from_words(const uint32_t* w) { return mk128(w[0], w[1], w[2], w[3]); }
   static DEV T from_u32(uint32_t x) { return mk128(x, 0, 0, 0); }
   static DEV T load(const void* base, size_t idx) {
@@ -219,6 +224,7 @@ struct Fp64 {
   static DEV bool eq(T a, T b) { return a == b; }
   static DEV bool is_zero(T a) { return a == 0; }
   static DEV bool lt_p(T a) { return a < P64; }
+  static DEV T sel(bool c, T a, T b) { return c ? a : b; }
   static DEV T from_words(const uint32_t* w) { return (uint64_t)w[1] << 32 | w[0]; }
   static DEV T from_u32(uint32_t x) { return x; }
   static DEV T load(const void* base, size_t idx) { return ((const uint64_t*)base)[idx]; }

@@ -433,6 +433,374 @@ __global__ __launch_bounds__(256) void k_query(DevParams p, InPtrs in, Scratch s
 }
 
 // ------------------------------------------------------------------------------------
+// k_query_ps: FLP query + decide for the ParallelSum(Mul, C) circuits (Histogram, SumVec).
+//
+// Wire 2j of gadget call k carries r^(Ck+j+1) m_(Ck+j), wire 2j+1 carries m_(Ck+j) - 1/2, so
+// with beta_k = L_(k+1)(t) r^(Ck):
+//   f_2j(t)   = seed_2j L_0 + r^(j+1) sum_k beta_k m_(Ck+j)
+//   f_2j+1(t) = seed_2j+1 L_0 + sum_k L_(k+1) m_(Ck+j) - (1/2) sum_k L_(k+1)
+// The 2C wire accumulators are swept GS wires-pairs at a time in registers (each measurement
+// element is read exactly once from HBM), two Field128 multiplies per element.
+// ------------------------------------------------------------------------------------
+template <int GS>
+__global__ __launch_bounds__(256) void k_query_ps(DevParams p, InPtrs in, Scratch sc,
+                                                  OutPtrs out) {
+  typedef Fp128 F;
+  typedef f128 T;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= p.n) return;
+  const size_t ld = p.ld;
+  const uint32_t P = p.P, A = p.arity, C = p.chunk, M = p.meas_len, K = p.calls;
+  uint8_t status = PRIO3_STATUS_FINISHED;
+  const T t = ldf<F>(sc.qr, 0, ld, r);
+  {
+    T tp = t;
+    for (uint32_t l = 0; l < p.logP; l++) tp = F::mul(tp, tp);
+    if (F::eq(tp, F::one())) status = PRIO3_STATUS_PREP_INIT;
+  }
+  // Lagrange basis at t (one size-P DFT of t^e/P) and gadget polynomial at the P-th roots
+  {
+    T pw = FC<F>::invP(p);
+    for (uint32_t e = 0; e < P; e++) {
+      F::store(sc.Lbuf, (size_t)bitrev(e, p.logP) * ld + r, pw);
+      pw = F::mul(pw, t);
+    }
+    dft_lane<F>(p, sc.Lbuf, r, P, p.logP);
+    for (uint32_t e = 0; e < P; e++) {
+      T q = ldf<F>(sc.proofs, A + e, ld, r);
+      if (e + P < p.glen) q = F::add(q, ldf<F>(sc.proofs, A + e + P, ld, r));
+      F::store(sc.PVbuf, (size_t)bitrev(e, p.logP) * ld + r, q);
+    }
+    dft_lane<F>(p, sc.PVbuf, r, P, p.logP);
+  }
+  auto Lc = [&](uint32_t c) { return ldf<F>(sc.Lbuf, (P - c) & (P - 1), ld, r); };
+  T pt = F::zero();
+  for (uint32_t e = p.glen; e-- > 0;) pt = F::add(F::mul(pt, t), ldf<F>(sc.proofs, A + e, ld, r));
+  // beta_k, sum of L_(k+1), sum of p(alpha^(k+1))
+  const T r0 = ldf<F>(sc.jr, 0, ld, r);
+  T rC = F::one();
+  for (uint32_t j = 0; j < C; j++) rC = F::mul(rC, r0);
+  T sumL = F::zero(), range = F::zero();
+  {
+    T rk = F::one();
+    for (uint32_t k = 0; k < K; k++) {
+      const T L = Lc(k + 1);
+      sumL = F::add(sumL, L);
+      range = F::add(range, ldf<F>(sc.PVbuf, k + 1, ld, r));
+      F::store(sc.beta, (size_t)k * ld + r, F::mul(L, rk));
+      rk = F::mul(rk, rC);
+    }
+  }
+  const T L0 = Lc(0);
+  const T half = FC<F>::half(p);
+  const T halfL = F::mul(half, sumL);
+  const uint8_t* lps = in.leader + (size_t)r * p.prep_share_len;
+  bool decode_ok = true;
+  auto lv = [&](uint32_t e) {
+    T x = F::load(lps, e);
+    if (!F::lt_p(x)) decode_ok = false;
+    return x;
+  };
+  T S = F::zero(), G = F::zero(), rj = r0;
+  const T Z = F::zero();
+  for (uint32_t jg = 0; jg < C; jg += GS) {
+    T Aa[GS], Bb[GS];
+#pragma unroll
+    for (int q = 0; q < GS; q++) Aa[q] = Bb[q] = Z;
+#pragma unroll 1
+    for (uint32_t k = 0; k < K; k++) {
+      const T be = ldf<F>(sc.beta, k, ld, r);
+      const T L = Lc(k + 1);
+      const uint32_t base = k * C + jg;
+#pragma unroll
+      for (int q = 0; q < GS; q++) {
+        const uint32_t i = base + q;
+        const bool valid = (jg + q < C) && (i < M);
+        T m = ldf<F>(sc.meas, valid ? i : 0, ld, r);
+        m = F::sel(valid, m, Z);
+        Aa[q] = F::add(Aa[q], F::mul(be, m));
+        Bb[q] = F::add(Bb[q], F::mul(L, m));
+        S = F::add(S, m);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < GS; q++) {
+      const uint32_t j = jg + q;
+      const bool valid = j < C;
+      const uint32_t jj = valid ? j : 0;
+      const T f0 = F::add(F::mul(ldf<F>(sc.proofs, 2 * jj, ld, r), L0), F::mul(rj, Aa[q]));
+      const T f1 = F::sub(F::add(F::mul(ldf<F>(sc.proofs, 2 * jj + 1, ld, r), L0), Bb[q]), halfL);
+      const T prod = F::mul(F::add(lv(1 + 2 * jj), f0), F::add(lv(2 + 2 * jj), f1));
+      G = F::add(G, F::sel(valid, prod, Z));
+      rj = F::sel(valid, F::mul(rj, r0), rj);
+    }
+  }
+  T v;
+  if (p.kind == PRIO3_SUMVEC) {
+    v = range;
+  } else {
+    const T r1 = ldf<F>(sc.jr, 1, ld, r);
+    v = F::add(F::mul(r1, range), F::mul(F::mul(r1, r1), F::sub(S, half)));
+  }
+  const T V0 = F::add(lv(0), v);
+  const T PT = F::add(lv(A + 1), pt);
+  if (status == PRIO3_STATUS_FINISHED) {
+    if (!decode_ok)
+      status = PRIO3_STATUS_PREP_SHARE_DECODE;
+    else if (!F::is_zero(V0) || !F::eq(G, PT))
+      status = PRIO3_STATUS_PREP_MSG;
+  }
+  uint32_t lpart[4], hpart[4];
+  load16(lps + (size_t)p.verifier_len * F::ES, lpart);
+  {
+    uint4 hp = sc.part[r];
+    hpart[0] = hp.x;
+    hpart[1] = hp.y;
+    hpart[2] = hp.z;
+    hpart[3] = hp.w;
+  }
+  KState s;
+  kzero(s);
+  Msg mm;
+  msg_zero(mm);
+  msg_dst(mm, p.dst[6]);
+  msg_bytes16(mm, 25, lpart);
+  msg_bytes16(mm, 41, hpart);
+  msg_absorb_final(s, mm, 57);
+  uint4 cor = sc.corrected[r];
+  uint32_t msg[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
+  if (status == PRIO3_STATUS_FINISHED &&
+      (msg[0] != cor.x || msg[1] != cor.y || msg[2] != cor.z || msg[3] != cor.w))
+    status = PRIO3_STATUS_PREP_NEXT;
+  if (status != PRIO3_STATUS_FINISHED) msg[0] = msg[1] = msg[2] = msg[3] = 0;
+  ((uint4*)out.prep_msgs)[r] = make_uint4(msg[0], msg[1], msg[2], msg[3]);
+  out.status[r] = status;
+  if (p.kind == PRIO3_SUMVEC) {
+    for (uint32_t e = 0; e < p.out_len; e++) {
+      T acc = F::zero(), pw = F::one();
+      for (uint32_t b = 0; b < p.bits; b++) {
+        acc = F::add(acc, F::mul(pw, ldf<F>(sc.meas, e * p.bits + b, ld, r)));
+        pw = F::add(pw, pw);
+      }
+      F::store(sc.out, (size_t)e * ld + r, acc);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// k_query_h<GS, PP>: k_query_ps specialised for a compile-time wire-polynomial length
+// PP <= 32 (Prio3Histogram(256,16) has PP = 32).  The Lagrange basis comes from an
+// in-register PP-point DFT of (t^e / P) -- no scratch round trips -- and the circuit only
+// needs sum_c p(alpha^c) = sum_e coef_e * sigma_(e mod P) (sigma precomputed on the host),
+// so the gadget polynomial is never evaluated on the roots.  The measurement loads of the
+// next gadget call are issued before the current call's arithmetic (register double buffer).
+// ------------------------------------------------------------------------------------
+// In-register radix-2 DFT of N (<= 16) Field128 values given in bit-reversed order; twiddle
+// w_N^i = p.tw128[i * stride * (32 / 2 / (N/2)) ...] is taken from the P-th root table.
+template <int N, int LOGN>
+DEV void dft_reg(const DevParams& p, f128 (&x)[N], int stride) {
+  typedef Fp128 F;
+#pragma unroll
+  for (int l = 1; l <= LOGN; l++) {
+    const int half = 1 << (l - 1);
+#pragma unroll
+    for (int i = 0; i < half; i++) {
+      // w_(2^l)^i = w_(N*stride)^(i * stride * N / 2^l)
+      const f128 w = F::from_words(p.tw128[i * stride * (N >> l)]);
+#pragma unroll
+      for (int j = i; j < N; j += 2 * half) {
+        const f128 u = x[j];
+        const f128 v = (i == 0) ? x[j + half] : F::mul(w, x[j + half]);
+        x[j] = F::add(u, v);
+        x[j + half] = F::sub(u, v);
+      }
+    }
+  }
+}
+
+template <int GS, int PP>
+__global__ __launch_bounds__(256, 2) void k_query_h(DevParams p, InPtrs in, Scratch sc,
+                                                    OutPtrs out) {
+  typedef Fp128 F;
+  typedef f128 T;
+  constexpr int LOGP = PP <= 2 ? 1 : PP <= 4 ? 2 : PP <= 8 ? 3 : PP <= 16 ? 4 : 5;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= p.n) return;
+  const size_t ld = p.ld;
+  const uint32_t A = p.arity, C = p.chunk, M = p.meas_len, K = p.calls;
+  uint8_t status = PRIO3_STATUS_FINISHED;
+  const T t = ldf<F>(sc.qr, 0, ld, r);
+  T L0, sumL = F::zero();
+  // u_e = t^e / P.  PP <= 16: one in-register DFT.  PP == 32: decimation in frequency,
+  // X[2k] = DFT16(u_e + u_(e+16)), X[2k+1] = DFT16((u_e - u_(e+16)) w32^e), each a geometric
+  // sequence, so only 16 values (64 VGPRs) are live at a time.
+  auto store_L = [&](int idx, const T& val) {  // X[idx] = L_c with c = (P - idx) mod P
+    const uint32_t c = (uint32_t)((PP - idx) & (PP - 1));
+    if (c == 0) {
+      L0 = val;
+    } else if (c <= K) {
+      F::store(sc.Lbuf, (size_t)c * ld + r, val);
+      sumL = F::add(sumL, val);
+    }
+  };
+  if constexpr (PP <= 16) {
+    T x[PP];
+    T pw = FC<F>::invP(p);
+#pragma unroll
+    for (int e = 0; e < PP; e++) {
+      x[__builtin_bitreverse32(e) >> (32 - LOGP)] = pw;
+      pw = F::mul(pw, t);
+    }
+    if (F::eq(pw, FC<F>::invP(p))) status = PRIO3_STATUS_PREP_INIT;  // t^P == 1
+    dft_reg<PP, LOGP>(p, x, 1);
+#pragma unroll
+    for (int k = 0; k < PP; k++) store_L(k, x[k]);
+  } else {
+    static_assert(PP == 32, "PP must be <= 32");
+    T t16 = t;
+#pragma unroll
+    for (int i = 0; i < 4; i++) t16 = F::mul(t16, t16);
+    const T t32 = F::mul(t16, t16);
+    if (F::eq(t32, F::one())) status = PRIO3_STATUS_PREP_INIT;
+    const T ip = FC<F>::invP(p);
+    const T gy = F::mul(ip, F::add(F::one(), t16)), gz = F::mul(ip, F::sub(F::one(), t16));
+    const T tw = F::mul(t, F::from_words(p.tw128[1]));  // t * w32
+#pragma unroll
+    for (int ph = 0; ph < 2; ph++) {
+      T x[16];
+      T pw = F::sel(ph == 0, gy, gz);
+      const T ratio = F::sel(ph == 0, t, tw);
+#pragma unroll
+      for (int e = 0; e < 16; e++) {
+        x[__builtin_bitreverse32(e) >> 28] = pw;
+        pw = F::mul(pw, ratio);
+      }
+      dft_reg<16, 4>(p, x, 2);
+#pragma unroll
+      for (int k = 0; k < 16; k++) store_L(2 * k + ph, x[k]);
+    }
+  }
+  // p(t) (Horner) and range = sum_c p(alpha^c) = sum_e coef_e sigma_(e mod P)
+  T pt = F::zero(), range = F::zero();
+  for (uint32_t e = p.glen; e-- > 0;) {
+    const T ce = ldf<F>(sc.proofs, A + e, ld, r);
+    pt = F::add(F::mul(pt, t), ce);
+    range = F::add(range, F::mul(ce, F::from_words(p.sigma128[e & (PP - 1)])));
+  }
+  const T r0 = ldf<F>(sc.jr, 0, ld, r);
+  {
+    T rC = F::one();
+    for (uint32_t j = 0; j < C; j++) rC = F::mul(rC, r0);
+    T rk = F::one();
+    for (uint32_t k = 0; k < K; k++) {
+      F::store(sc.beta, (size_t)k * ld + r, F::mul(ldf<F>(sc.Lbuf, k + 1, ld, r), rk));
+      rk = F::mul(rk, rC);
+    }
+  }
+  const T half = FC<F>::half(p);
+  const T halfL = F::mul(half, sumL);
+  const uint8_t* lps = in.leader + (size_t)r * p.prep_share_len;
+  bool decode_ok = true;
+  auto lv = [&](uint32_t e) {
+    T x = F::load(lps, e);
+    if (!F::lt_p(x)) decode_ok = false;
+    return x;
+  };
+  T S = F::zero(), G = F::zero(), rj = r0;
+  const T Z = F::zero();
+  for (uint32_t jg = 0; jg < C; jg += GS) {
+    T Aa[GS], Bb[GS], mc[GS];
+#pragma unroll
+    for (int q = 0; q < GS; q++) Aa[q] = Bb[q] = Z;
+    auto fetch = [&](uint32_t k, T* dst) {
+#pragma unroll
+      for (int q = 0; q < GS; q++) {
+        const uint32_t i = k * C + jg + q;
+        const bool valid = (k < K) && (jg + q < C) && (i < M);
+        dst[q] = F::sel(valid, ldf<F>(sc.meas, valid ? i : 0, ld, r), Z);
+      }
+    };
+    fetch(0, mc);
+#pragma unroll 1
+    for (uint32_t k = 0; k < K; k++) {
+      T mn[GS];
+      fetch(k + 1, mn);
+      const T be = ldf<F>(sc.beta, k, ld, r);
+      const T L = ldf<F>(sc.Lbuf, k + 1, ld, r);
+#pragma unroll
+      for (int q = 0; q < GS; q++) {
+        Aa[q] = F::add(Aa[q], F::mul(be, mc[q]));
+        Bb[q] = F::add(Bb[q], F::mul(L, mc[q]));
+        S = F::add(S, mc[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < GS; q++) mc[q] = mn[q];
+    }
+#pragma unroll
+    for (int q = 0; q < GS; q++) {
+      const uint32_t j = jg + q;
+      const bool valid = j < C;
+      const uint32_t jj = valid ? j : 0;
+      const T f0 = F::add(F::mul(ldf<F>(sc.proofs, 2 * jj, ld, r), L0), F::mul(rj, Aa[q]));
+      const T f1 = F::sub(F::add(F::mul(ldf<F>(sc.proofs, 2 * jj + 1, ld, r), L0), Bb[q]), halfL);
+      const T prod = F::mul(F::add(lv(1 + 2 * jj), f0), F::add(lv(2 + 2 * jj), f1));
+      G = F::add(G, F::sel(valid, prod, Z));
+      rj = F::sel(valid, F::mul(rj, r0), rj);
+    }
+  }
+  T v;
+  if (p.kind == PRIO3_SUMVEC) {
+    v = range;
+  } else {
+    const T r1 = ldf<F>(sc.jr, 1, ld, r);
+    v = F::add(F::mul(r1, range), F::mul(F::mul(r1, r1), F::sub(S, half)));
+  }
+  const T V0 = F::add(lv(0), v);
+  const T PT = F::add(lv(A + 1), pt);
+  if (status == PRIO3_STATUS_FINISHED) {
+    if (!decode_ok)
+      status = PRIO3_STATUS_PREP_SHARE_DECODE;
+    else if (!F::is_zero(V0) || !F::eq(G, PT))
+      status = PRIO3_STATUS_PREP_MSG;
+  }
+  uint32_t lpart[4], hpart[4];
+  load16(lps + (size_t)p.verifier_len * F::ES, lpart);
+  {
+    uint4 hp = sc.part[r];
+    hpart[0] = hp.x;
+    hpart[1] = hp.y;
+    hpart[2] = hp.z;
+    hpart[3] = hp.w;
+  }
+  KState s;
+  kzero(s);
+  Msg mm;
+  msg_zero(mm);
+  msg_dst(mm, p.dst[6]);
+  msg_bytes16(mm, 25, lpart);
+  msg_bytes16(mm, 41, hpart);
+  msg_absorb_final(s, mm, 57);
+  uint4 cor = sc.corrected[r];
+  uint32_t msg[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
+  if (status == PRIO3_STATUS_FINISHED &&
+      (msg[0] != cor.x || msg[1] != cor.y || msg[2] != cor.z || msg[3] != cor.w))
+    status = PRIO3_STATUS_PREP_NEXT;
+  if (status != PRIO3_STATUS_FINISHED) msg[0] = msg[1] = msg[2] = msg[3] = 0;
+  ((uint4*)out.prep_msgs)[r] = make_uint4(msg[0], msg[1], msg[2], msg[3]);
+  out.status[r] = status;
+  if (p.kind == PRIO3_SUMVEC) {
+    for (uint32_t e = 0; e < p.out_len; e++) {
+      T acc = F::zero(), pw = F::one();
+      for (uint32_t b = 0; b < p.bits; b++) {
+        acc = F::add(acc, F::mul(pw, ldf<F>(sc.meas, e * p.bits + b, ld, r)));
+        pw = F::add(pw, pw);
+      }
+      F::store(sc.out, (size_t)e * ld + r, acc);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // Accumulate: masked segmented mod-p reduction of output shares
 // ------------------------------------------------------------------------------------
 __global__ void k_mask(uint32_t n, const uint8_t* status, const uint32_t* seg,
@@ -622,6 +990,23 @@ static int fill_sizes(const prio3_params* pp, prio3_sizes_t* s, DevParams* dp) {
       d.half128[k] = (uint32_t)(h >> (32 * k));
     }
     d.invP64 = (uint64_t)hpow(d.P, HP64 - 2, HP64);
+    if (d.P <= 32) {
+      u128 alpha = 0;
+      for (int k = 0; k < 4; k++) alpha |= (u128)d.roots128[d.logP][k] << (32 * k);
+      for (uint32_t e2 = 0; e2 < d.P; e2++) {
+        u128 ae = hpow(alpha, e2, HP128), s = 0, x = 1;
+        for (uint32_t cc = 1; cc <= d.calls; cc++) {
+          x = hmul(x, ae, HP128);
+          s += x;
+          if (s < x || s >= HP128) s -= HP128;
+        }
+        for (int k = 0; k < 4; k++) d.sigma128[e2][k] = (uint32_t)(s >> (32 * k));
+      }
+      for (uint32_t i = 0; i < d.P / 2; i++) {
+        u128 w = hpow(alpha, i, HP128);
+        for (int k = 0; k < 4; k++) d.tw128[i][k] = (uint32_t)(w >> (32 * k));
+      }
+    }
     d.half64 = (uint64_t)hpow(2, HP64 - 2, HP64);
   }
   if (s) {
@@ -659,7 +1044,7 @@ static int ensure_scratch(prio3_engine* e, uint32_t n) {
   size_t es = d.es;
   void** bufs[] = {&e->sc.meas, &e->sc.proofs, &e->sc.jr, &e->sc.qr, (void**)&e->sc.part,
                    (void**)&e->sc.corrected, (void**)&e->sc.flag, &e->sc.Lbuf, &e->sc.PVbuf,
-                   &e->sc.acc, &e->sc.out, (void**)&e->d_mask};
+                   &e->sc.acc, &e->sc.out, &e->sc.beta, (void**)&e->d_mask};
   for (auto b : bufs)
     if (*b) {
       (void)hipFree(*b);
@@ -669,7 +1054,7 @@ static int ensure_scratch(prio3_engine* e, uint32_t n) {
                     es * ld, 16 * (size_t)ld, 16 * (size_t)ld, (size_t)ld, es * d.P * ld,
                     es * d.P * ld, es * d.arity * ld,
                     (d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC) ? es * d.out_len * ld : 16,
-                    (size_t)ld};
+                    es * d.calls * ld, (size_t)ld};
   for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]); i++) HIPCHK(hipMalloc(bufs[i], sizes[i]));
   e->cap = ld;
   e->dp.ld = ld;
@@ -761,7 +1146,7 @@ void prio3_engine_destroy(prio3_engine* e) {
   (void)hipSetDevice(e->device);
   (void)hipStreamSynchronize(e->stream);
   void* bufs[] = {e->sc.meas, e->sc.proofs, e->sc.jr, e->sc.qr, e->sc.part, e->sc.corrected,
-                  e->sc.flag, e->sc.Lbuf, e->sc.PVbuf, e->sc.acc, e->sc.out, e->d_mask,
+                  e->sc.flag, e->sc.Lbuf, e->sc.PVbuf, e->sc.acc, e->sc.out, e->sc.beta, e->d_mask,
                   e->d_prep_partial, e->d_pcount, e->d_nonces, e->d_pub, e->d_helper,
                   e->d_leader, e->d_msgs, e->d_status};
   for (auto b : bufs)
@@ -804,7 +1189,17 @@ int prio3_device_prepare(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
   if (dp.es == 16) {
     TIMED(e, st, "k_xof", (k_xof<Fp128><<<blocks, 256, 0, st>>>(dp, in, e->sc)));
     TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp128><<<blocks64, 64, 0, st>>>(dp, in, e->sc)));
-    TIMED(e, st, "k_query", (k_query<Fp128><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
+    const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
+    if (ps && dp.P == 32)
+      TIMED(e, st, "k_query", (k_query_h<4, 32><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
+    else if (ps && dp.P == 16)
+      TIMED(e, st, "k_query", (k_query_h<4, 16><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
+    else if (ps && dp.P == 8)
+      TIMED(e, st, "k_query", (k_query_h<4, 8><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
+    else if (ps)
+      TIMED(e, st, "k_query", (k_query_ps<4><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
+    else
+      TIMED(e, st, "k_query", (k_query<Fp128><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
   } else {
     TIMED(e, st, "k_xof", (k_xof<Fp64><<<blocks, 256, 0, st>>>(dp, in, e->sc)));
     TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp64><<<blocks64, 64, 0, st>>>(dp, in, e->sc)));
