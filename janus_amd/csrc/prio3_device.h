@@ -162,6 +162,77 @@ DEV f128 mul128(const f128& a, const f128& b) {
 }
 
 // -------------------------------------------------------------------------------------
+// Lazily reduced multiply-accumulate: sum of Field128 products kept as 7 product-scanning
+// columns (column k = c[k] + h[k]*2^64, weight 2^(32k)); each 32x32 limb product is ONE
+// v_mad_u64_u32 (carry-out to VCC) plus ONE v_addc into the column's top word -- no per-product
+// modular reduction.  Up to 2^31 products fit; mac_reduce() folds the result once.
+// -------------------------------------------------------------------------------------
+struct mac128 {
+  uint64_t c[7];
+  uint32_t h[7];
+};
+DEV void mac_zero(mac128& a) {
+#pragma unroll
+  for (int k = 0; k < 7; k++) {
+    a.c[k] = 0;
+    a.h[k] = 0;
+  }
+}
+DEV void mac_add(mac128& a, const f128& x, const f128& y) {
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"
+          : "+v"(a.c[i + j]), "+v"(a.h[i + j])
+          : "v"(x.w[i]), "v"(y.w[j])
+          : "vcc");
+}
+// 2^128 mod p and 2^256 mod p
+DEV f128 mac_reduce(const mac128& a) {
+  // normalise columns into 10 words: word n = lo32(c_n) + hi32(c_(n-1)) + h_(n-2) + carry
+  uint32_t w[10];
+  uint64_t carry = 0;
+#pragma unroll
+  for (int n = 0; n < 10; n++) {
+    uint64_t s = carry;
+    if (n < 7) s += (uint32_t)a.c[n];
+    if (n >= 1 && n - 1 < 7) s += (uint32_t)(a.c[n - 1] >> 32);
+    if (n >= 2 && n - 2 < 7) s += a.h[n - 2];
+    w[n] = (uint32_t)s;
+    carry = s >> 32;
+  }
+  // X = L + H*2^128 + T*2^256,  2^128 = 28*2^64 - 1,  2^256 = (2^128)^2 (mod p)
+  const f128 L = canon128(mk128(w[0], w[1], w[2], w[3]));
+  const f128 H = mk128(w[4], w[5], w[6], w[7]);
+  const f128 T = mk128(w[8], w[9], 0, 0);
+  const f128 c128 = mk128(0xffffffffu, 0xffffffffu, 27u, 0u);
+  const f128 c256 = mul128(c128, c128);
+  return add128(add128(L, mul128(canon128(H), c128)), mul128(T, c256));
+}
+// lazily reduced sum of Field128 values (128-bit sum + 32-bit carry word)
+struct sum128 {
+  uint32_t w[5];
+};
+DEV void sum_zero(sum128& s) {
+#pragma unroll
+  for (int k = 0; k < 5; k++) s.w[k] = 0;
+}
+DEV void sum_add(sum128& s, const f128& x) {
+  uint32_t c0, c1, c2, c3;
+  s.w[0] = addc(s.w[0], x.w[0], 0, &c0);
+  s.w[1] = addc(s.w[1], x.w[1], c0, &c1);
+  s.w[2] = addc(s.w[2], x.w[2], c1, &c2);
+  s.w[3] = addc(s.w[3], x.w[3], c2, &c3);
+  s.w[4] += c3;
+}
+DEV f128 sum_reduce(const sum128& s) {
+  const f128 c128 = mk128(0xffffffffu, 0xffffffffu, 27u, 0u);
+  return add128(canon128(mk128(s.w[0], s.w[1], s.w[2], s.w[3])),
+                mul128(mk128(s.w[4], 0, 0, 0), c128));
+}
+
+// -------------------------------------------------------------------------------------
 // Field64 (Goldilocks)
 // -------------------------------------------------------------------------------------
 #define P64 0xffffffff00000001ull

@@ -619,7 +619,7 @@ DEV void dft_reg(const DevParams& p, f128 (&x)[N], int stride) {
 }
 
 template <int GS, int PP>
-__global__ __launch_bounds__(256, 2) void k_query_h(DevParams p, InPtrs in, Scratch sc,
+__global__ __launch_bounds__(256, 3) void k_query_h(DevParams p, InPtrs in, Scratch sc,
                                                     OutPtrs out) {
   typedef Fp128 F;
   typedef f128 T;
@@ -706,12 +706,18 @@ __global__ __launch_bounds__(256, 2) void k_query_h(DevParams p, InPtrs in, Scra
     if (!F::lt_p(x)) decode_ok = false;
     return x;
   };
-  T S = F::zero(), G = F::zero(), rj = r0;
+  sum128 Ssum;
+  sum_zero(Ssum);
+  T G = F::zero(), rj = r0;
   const T Z = F::zero();
   for (uint32_t jg = 0; jg < C; jg += GS) {
-    T Aa[GS], Bb[GS], mc[GS];
+    mac128 Aa[GS], Bb[GS];
+    T mc[GS];
 #pragma unroll
-    for (int q = 0; q < GS; q++) Aa[q] = Bb[q] = Z;
+    for (int q = 0; q < GS; q++) {
+      mac_zero(Aa[q]);
+      mac_zero(Bb[q]);
+    }
     auto fetch = [&](uint32_t k, T* dst) {
 #pragma unroll
       for (int q = 0; q < GS; q++) {
@@ -729,9 +735,9 @@ __global__ __launch_bounds__(256, 2) void k_query_h(DevParams p, InPtrs in, Scra
       const T L = ldf<F>(sc.Lbuf, k + 1, ld, r);
 #pragma unroll
       for (int q = 0; q < GS; q++) {
-        Aa[q] = F::add(Aa[q], F::mul(be, mc[q]));
-        Bb[q] = F::add(Bb[q], F::mul(L, mc[q]));
-        S = F::add(S, mc[q]);
+        mac_add(Aa[q], be, mc[q]);
+        mac_add(Bb[q], L, mc[q]);
+        sum_add(Ssum, mc[q]);
       }
 #pragma unroll
       for (int q = 0; q < GS; q++) mc[q] = mn[q];
@@ -741,13 +747,15 @@ __global__ __launch_bounds__(256, 2) void k_query_h(DevParams p, InPtrs in, Scra
       const uint32_t j = jg + q;
       const bool valid = j < C;
       const uint32_t jj = valid ? j : 0;
-      const T f0 = F::add(F::mul(ldf<F>(sc.proofs, 2 * jj, ld, r), L0), F::mul(rj, Aa[q]));
-      const T f1 = F::sub(F::add(F::mul(ldf<F>(sc.proofs, 2 * jj + 1, ld, r), L0), Bb[q]), halfL);
+      const T Aq = mac_reduce(Aa[q]), Bq = mac_reduce(Bb[q]);
+      const T f0 = F::add(F::mul(ldf<F>(sc.proofs, 2 * jj, ld, r), L0), F::mul(rj, Aq));
+      const T f1 = F::sub(F::add(F::mul(ldf<F>(sc.proofs, 2 * jj + 1, ld, r), L0), Bq), halfL);
       const T prod = F::mul(F::add(lv(1 + 2 * jj), f0), F::add(lv(2 + 2 * jj), f1));
       G = F::add(G, F::sel(valid, prod, Z));
       rj = F::sel(valid, F::mul(rj, r0), rj);
     }
   }
+  const T S = sum_reduce(Ssum);
   T v;
   if (p.kind == PRIO3_SUMVEC) {
     v = range;
@@ -1191,11 +1199,11 @@ int prio3_device_prepare(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
     TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp128><<<blocks64, 64, 0, st>>>(dp, in, e->sc)));
     const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
     if (ps && dp.P == 32)
-      TIMED(e, st, "k_query", (k_query_h<4, 32><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
+      TIMED(e, st, "k_query", (k_query_h<2, 32><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
     else if (ps && dp.P == 16)
-      TIMED(e, st, "k_query", (k_query_h<4, 16><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
+      TIMED(e, st, "k_query", (k_query_h<2, 16><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
     else if (ps && dp.P == 8)
-      TIMED(e, st, "k_query", (k_query_h<4, 8><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
+      TIMED(e, st, "k_query", (k_query_h<2, 8><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
     else if (ps)
       TIMED(e, st, "k_query", (k_query_ps<4><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
     else
