@@ -91,6 +91,8 @@ def main():
     ap.add_argument("--reports", type=int, default=1 << 20, help="reports per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--opt", action="append", default=[],
+                    help="engine option key=value (e.g. split_xof=0), for A/B runs")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -108,6 +110,9 @@ def main():
 
     eng = J.HelperEngine(J.Prio3Histogram(256, 16), VK, device=local)
     sz = eng.sz
+    for kv in args.opt:
+        k, v = kv.split("=")
+        eng.set_option(k, int(v))
     data = eng.generate_reports_device(n, seed=0x4A414E5553000001, first_index=rank * n,
                                        with_checks=True)
     torch.cuda.synchronize()

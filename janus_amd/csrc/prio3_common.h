@@ -299,6 +299,7 @@ struct prio3_engine {
   uint8_t *d_nonces = nullptr, *d_pub = nullptr, *d_helper = nullptr, *d_leader = nullptr,
           *d_msgs = nullptr, *d_status = nullptr;
   int force_slow = 0;
+  int split_xof = 1;
   int timing = 0;
   std::vector<KTime> times;
   std::vector<hipEvent_t> ev_pool;

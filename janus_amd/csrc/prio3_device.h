@@ -400,15 +400,19 @@ DEV void keccak_round(KState& a, uint32_t rc_lo, uint32_t rc_hi) {
     clo[x] = xor3(xor3(a.lo[x], a.lo[x + 5], a.lo[x + 10]), a.lo[x + 15], a.lo[x + 20]);
     chi[x] = xor3(xor3(a.hi[x], a.hi[x + 5], a.hi[x + 10]), a.hi[x + 15], a.hi[x + 20]);
   }
+  // theta: A[x,y] ^= C[x-1] ^ rot1(C[x+1]) as one v_bitop3 xor3 per half-lane
+  uint32_t rlo[5], rhi[5];
 #pragma unroll
   for (int x = 0; x < 5; x++) {
-    uint32_t l = clo[(x + 1) % 5], h = chi[(x + 1) % 5];
-    uint32_t dlo = clo[(x + 4) % 5] ^ __builtin_amdgcn_alignbit(l, h, 31);
-    uint32_t dhi = chi[(x + 4) % 5] ^ __builtin_amdgcn_alignbit(h, l, 31);
+    rlo[x] = __builtin_amdgcn_alignbit(clo[x], chi[x], 31);
+    rhi[x] = __builtin_amdgcn_alignbit(chi[x], clo[x], 31);
+  }
+#pragma unroll
+  for (int x = 0; x < 5; x++) {
 #pragma unroll
     for (int y = 0; y < 25; y += 5) {
-      a.lo[x + y] ^= dlo;
-      a.hi[x + y] ^= dhi;
+      a.lo[x + y] = xor3(a.lo[x + y], clo[(x + 4) % 5], rlo[(x + 1) % 5]);
+      a.hi[x + y] = xor3(a.hi[x + y], chi[(x + 4) % 5], rhi[(x + 1) % 5]);
     }
   }
   uint32_t blo[25], bhi[25];

@@ -189,6 +189,184 @@ __global__ __launch_bounds__(256) void k_xof(DevParams p, InPtrs in, Scratch sc)
 }
 
 // ------------------------------------------------------------------------------------
+// Split XOF path (one Keccak state live per kernel, for occupancy):
+//   k_xof_a   query randomness, measurement share and proofs share squeezed to scratch
+//   k_jrpart  joint-rand part absorbed from the measurement share in scratch, corrected
+//             seed, joint randomness.  The 42-byte prefix leaves every message word a 16-bit
+//             funnel shift of two share words whose element/word offsets are compile-time
+//             constants relative to 21*(b/2) (b = block index), so each 168-byte block is 11-12
+//             coalesced 16-byte loads + 42 v_alignbit.
+// ------------------------------------------------------------------------------------
+template <class F>
+__global__ __launch_bounds__(256, 4) void k_xof_a(DevParams p, InPtrs in, Scratch sc) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= p.n) return;
+  constexpr uint32_t ES = F::ES;
+  uint32_t flag = p.force_slow;
+  uint32_t nonce[4], km[4], kp[4];
+  load16(in.nonces + 16 * (size_t)r, nonce);
+  const uint8_t* hs = in.helper + (size_t)r * p.helper_share_len;
+  load16(hs, km);
+  load16(hs + 16, kp);
+  {
+    KState s;
+    kzero(s);
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[5]);
+    msg_bytes16(m, 9, p.vk);
+    msg_byte(m, 25, 1);
+    msg_bytes16(m, 26, nonce);
+    msg_absorb_final(s, m, 42);
+    uint32_t w[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
+    put_elem<F>(p, sc.qr, 0, r, w, flag);
+  }
+  {
+    KState s;
+    kzero(s);
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[1]);
+    msg_bytes16(m, 9, km);
+    msg_byte(m, 25, 1);
+    msg_absorb_final(s, m, 26);
+    const uint32_t M = p.meas_len, K = (M * ES + 167) / 168;
+    uint32_t q0 = 0, q1 = 0;
+    for (uint32_t b = 0; b < K; b++) {
+      squeeze_block<F>(p, s, b, M, q0, q1, sc.meas, r, flag);
+      if (b + 1 < K) keccak_p12(s);
+    }
+  }
+  {
+    KState s;
+    kzero(s);
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[2]);
+    msg_bytes16(m, 9, kp);
+    msg_byte(m, 25, 1);
+    msg_byte(m, 26, 1);
+    msg_absorb_final(s, m, 27);
+    const uint32_t PL = p.proof_len, Kp = (PL * ES + 167) / 168;
+    uint32_t q0 = 0, q1 = 0;
+    for (uint32_t b = 0; b < Kp; b++) {
+      squeeze_block<F>(p, s, b, PL, q0, q1, sc.proofs, r, flag);
+      if (b + 1 < Kp) keccak_p12(s);
+    }
+  }
+  sc.flag[r] = (uint8_t)flag;
+}
+
+// Field128 only (every joint-randomness Prio3 instance uses Field128).
+__global__ __launch_bounds__(256, 4) void k_jrpart(DevParams p, InPtrs in, Scratch sc) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= p.n) return;
+  const size_t ld = p.ld;
+  const int M = (int)p.meas_len;
+  uint32_t nonce[4], kb[4];
+  load16(in.nonces + 16 * (size_t)r, nonce);
+  load16(in.helper + (size_t)r * p.helper_share_len + 32, kb);
+  uint32_t pre[11];
+  {
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[7]);
+    msg_bytes16(m, 9, kb);
+    msg_byte(m, 25, 1);
+    msg_bytes16(m, 26, nonce);
+#pragma unroll
+    for (int j = 0; j < 11; j++) pre[j] = m.w[j];
+  }
+  const uint4* meas = (const uint4*)sc.meas;
+  auto ldel = [&](int e) -> uint4 {
+    const bool ok = e >= 0 && e < M;
+    uint4 v = meas[(size_t)(ok ? e : 0) * ld + r];
+    return ok ? v : make_uint4(0, 0, 0, 0);
+  };
+  auto wsel = [](const uint4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; };
+  const uint32_t L = 42 + (uint32_t)M * 16;
+  const uint32_t B = L / 168, rem = L % 168;
+  KState s;
+  kzero(s);
+  for (uint32_t b = 0; b <= B; b++) {
+    uint32_t x[42];
+    const int q21 = 21 * (int)(b >> 1);
+    if ((b & 1) == 0) {
+      // u = 84q + j - 11: element 21q + floor((j-11)/4), word (j-11) mod 4; window 21q-3..21q+7
+      uint4 E[11];
+#pragma unroll
+      for (int t = 0; t < 11; t++) E[t] = ldel(q21 - 3 + t);
+#pragma unroll
+      for (int j = 0; j < 42; j++) {
+        const int u0 = j - 11 + 12, u1 = j - 10 + 12;  // +12 keeps the offsets non-negative
+        const uint32_t w0 = wsel(E[u0 >> 2], u0 & 3), w1 = wsel(E[u1 >> 2], u1 & 3);
+        x[j] = __builtin_amdgcn_alignbit(w1, w0, 16);
+      }
+      if (b == 0) {
+#pragma unroll
+        for (int j = 0; j < 10; j++) x[j] = pre[j];
+        x[10] = (pre[10] & 0xffffu) | (wsel(E[3], 0) << 16);
+      }
+    } else {
+      // u = 84q + 31 + j: element 21q + 7 + floor((j+3)/4), word (j+3) mod 4; window 21q+7..21q+18
+      uint4 E[12];
+#pragma unroll
+      for (int t = 0; t < 12; t++) E[t] = ldel(q21 + 7 + t);
+#pragma unroll
+      for (int j = 0; j < 42; j++) {
+        const int u0 = j + 3, u1 = j + 4;
+        const uint32_t w0 = wsel(E[u0 >> 2], u0 & 3), w1 = wsel(E[u1 >> 2], u1 & 3);
+        x[j] = __builtin_amdgcn_alignbit(w1, w0, 16);
+      }
+    }
+    if (b == B) {
+#pragma unroll
+      for (int j = 0; j < 42; j++) {
+        const uint32_t lo = 4 * j;
+        uint32_t mask = (lo + 4 <= rem) ? 0xffffffffu
+                                        : (lo >= rem ? 0u : ((1u << (8 * (rem - lo))) - 1u));
+        x[j] &= mask;
+        if ((uint32_t)j == (rem >> 2)) x[j] ^= 1u << (8 * (rem & 3));
+      }
+      x[41] ^= 0x80000000u;
+    }
+#pragma unroll
+    for (int j = 0; j < 42; j++) kxor_word(s, j, x[j]);
+    keccak_p12(s);
+  }
+  uint32_t part[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
+  uint32_t flag = sc.flag[r];
+  uint32_t pub0[4];
+  load16(in.pub + (size_t)r * p.public_share_len, pub0);
+  KState c;
+  kzero(c);
+  {
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[6]);
+    msg_bytes16(m, 25, pub0);
+    msg_bytes16(m, 41, part);
+    msg_absorb_final(c, m, 57);
+  }
+  uint32_t cor[4] = {kword(c, 0), kword(c, 1), kword(c, 2), kword(c, 3)};
+  {
+    KState t;
+    kzero(t);
+    Msg m2;
+    msg_zero(m2);
+    msg_dst(m2, p.dst[3]);
+    msg_bytes16(m2, 9, cor);
+    msg_byte(m2, 25, 1);
+    msg_absorb_final(t, m2, 26);
+    uint32_t q0 = 0, q1 = 0;
+    squeeze_block<Fp128>(p, t, 0, p.jr_len, q0, q1, sc.jr, r, flag);
+  }
+  sc.part[r] = make_uint4(part[0], part[1], part[2], part[3]);
+  sc.corrected[r] = make_uint4(cor[0], cor[1], cor[2], cor[3]);
+  sc.flag[r] = (uint8_t)flag;
+}
+
+// ------------------------------------------------------------------------------------
 // k_xof_slow: general byte-level sponge with rejection sampling (flagged reports only)
 // ------------------------------------------------------------------------------------
 struct BX {
@@ -1170,6 +1348,10 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
     e->force_slow = (int)value;
     return PRIO3_OK;
   }
+  if (!strcmp(key, "split_xof")) {
+    e->split_xof = (int)value;
+    return PRIO3_OK;
+  }
   if (!strcmp(key, "timing")) {
     e->timing = (int)value;
     return PRIO3_OK;
@@ -1195,7 +1377,12 @@ int prio3_device_prepare(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
   OutPtrs out{d_prep_msgs, d_status};
   const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
   if (dp.es == 16) {
-    TIMED(e, st, "k_xof", (k_xof<Fp128><<<blocks, 256, 0, st>>>(dp, in, e->sc)));
+    if (dp.jr_len && e->split_xof) {
+      TIMED(e, st, "k_xof_a", (k_xof_a<Fp128><<<blocks, 256, 0, st>>>(dp, in, e->sc)));
+      TIMED(e, st, "k_jrpart", (k_jrpart<<<blocks, 256, 0, st>>>(dp, in, e->sc)));
+    } else {
+      TIMED(e, st, "k_xof", (k_xof<Fp128><<<blocks, 256, 0, st>>>(dp, in, e->sc)));
+    }
     TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp128><<<blocks64, 64, 0, st>>>(dp, in, e->sc)));
     const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
     if (ps && dp.P == 32)
