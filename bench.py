@@ -29,21 +29,18 @@ from janus_amd import prio3 as J  # noqa: E402
 METRIC = "reports prepared+aggregated/sec (helper, Prio3Histogram len=256) at 1/2/4/8 GPUs"
 VK = bytes.fromhex("4a414e55532d414d442d42454e434821")
 
-# --- cost model (DESIGN.md "Roofline"): 32-bit VALU instructions per unit, counted from the
-# gfx950 code object: Keccak-p[1600,12] = 12 x 190 (v_bitop3/v_xor/v_alignbit), Field128
-# multiply = 110 (23 v_mad_u64_u32 + carries/selects), Field128 add = 15.
-OPS_PERM, OPS_MUL, OPS_ADD = 12 * 190, 110, 15
-# Per-report algorithmic work of Prio3Histogram(256,16) helper prep (SURVEY 8(d) counts):
-#   k_xof:   63 permutations (1 query rand + 25 meas + 25 joint-rand part + 10 proofs + 2)
-#   k_query: 1 permutation (prepare message) + 1331 F128 mul + ~1600 F128 add
-KERNEL_OPS = {
-    "k_xof": 63 * OPS_PERM,
-    "k_query": 1 * OPS_PERM + 1331 * OPS_MUL + 1600 * OPS_ADD,
-}
-# per-report HBM bytes the kernels must move at minimum (inputs + outputs; scratch excluded)
-KERNEL_BYTES = {"k_xof": 16 + 32 + 48, "k_query": 560 + 16 + 1,
+# --- roofline inputs.  Per kernel, profiles/kernel_counts.json (written by
+# tools/summarize_profiles.py from the committed rocprofv3 passes) holds the dynamic VALU
+# instructions per report (SQ_INSTS_VALU / SQ_WAVES, one report per lane), the mix-weighted VALU
+# ceiling of its hot loop (tools/isa_mix.py: full-rate ops 2 cycles, half-rate 4, from the
+# measured tools/ubench_valu rates) and its PMC HBM bytes per launch.
+COUNTS_PATH = os.path.join(ROOT, "profiles", "kernel_counts.json")
+# per-report HBM bytes each kernel must move at minimum (algorithmic; Histogram(256,16))
+KERNEL_BYTES = {"k_xof_a": 16 + 16 + 16 + 256 * 16 + 95 * 16,  # nonce, k_meas, k_proofs in; shares out
+                "k_jrpart": 16 + 16 + 32 + 256 * 16 + 2 * 16 + 16,
+                "k_query_h": 256 * 16 + 95 * 16 + 560 + 2 * 16 + 16 + 16 + 17,
                 "k_acc_partial": 256 * 16 + 1}
-PEAK_VALU_OPS = 256 * 4 * 32 * 2.4e9  # 78.6e12 lane-ops/s (MI355X_MICROARCH.md chip table)
+PEAK_VALU_NOMINAL = 256 * 4 * 32 * 2.4e9  # 78.6e12 lane-instr/s, full-rate VALU at 2.4 GHz
 PEAK_HBM = 8.0e12
 
 
@@ -167,15 +164,25 @@ def main():
     # roofline of the dominant kernel, from the live HIP-event times on the launch stream
     per_kernel = {k: dict(ms_total=v[0], launches=v[1], ms_avg=v[0] / max(v[1], 1))
                   for k, v in times.items()}
-    dom = max((k for k in per_kernel if k in KERNEL_OPS), key=lambda k: per_kernel[k]["ms_total"])
-    avg_s = per_kernel[dom]["ms_avg"] / 1e3
-    achieved = KERNEL_OPS[dom] * n / avg_s
-    roofline = dict(bound="valu", achieved=achieved / 1e12, peak=PEAK_VALU_OPS / 1e12,
-                    unit="Tops/s (32-bit VALU lane-ops)", frac=achieved / PEAK_VALU_OPS,
-                    traffic=None, kernel=dom, ms_avg=per_kernel[dom]["ms_avg"],
-                    ops_per_report=KERNEL_OPS[dom],
-                    hbm_algorithmic_GBps=KERNEL_BYTES[dom] * n / avg_s / 1e9,
-                    hbm_peak_GBps=PEAK_HBM / 1e9)
+    counts = json.load(open(COUNTS_PATH)) if os.path.exists(COUNTS_PATH) else dict(kernels={})
+    kc = counts["kernels"]
+    for k, v in per_kernel.items():
+        if k in kc and "valu_instr_per_item" in kc[k] and k != "k_acc_partial":
+            v["valu_T"] = kc[k]["valu_instr_per_item"] * n / (v["ms_avg"] / 1e3) / 1e12
+            v["valu_frac"] = v["valu_T"] / kc[k]["valu_ceiling_T"]
+        if k in KERNEL_BYTES:
+            v["hbm_algorithmic_GBps"] = KERNEL_BYTES[k] * n / (v["ms_avg"] / 1e3) / 1e9
+    dom = max((k for k in per_kernel if "valu_T" in per_kernel[k]),
+              key=lambda k: per_kernel[k]["ms_total"])
+    d = per_kernel[dom]
+    roofline = dict(bound="valu", achieved=d["valu_T"], peak=kc[dom]["valu_ceiling_T"],
+                    unit="T lane-instr/s (32-bit VALU, mix-weighted ceiling)",
+                    frac=d["valu_frac"], traffic=kc[dom].get("bytes"),
+                    traffic_source=f"{counts.get('source')} (PMC FETCH_SIZE*2+WRITE_SIZE, bytes/launch)",
+                    kernel=dom, ms_avg=d["ms_avg"],
+                    valu_instr_per_report=kc[dom]["valu_instr_per_item"],
+                    hbm_algorithmic_GBps=d.get("hbm_algorithmic_GBps"), hbm_peak_GBps=PEAK_HBM / 1e9,
+                    valu_nominal_peak_T=PEAK_VALU_NOMINAL / 1e12)
 
     out = dict(metric=METRIC, value=value, unit="reports/s", n_gpus=world, steps=args.steps,
                warmup=args.warmup, ms_per_step=elapsed / args.steps * 1e3,

@@ -1386,13 +1386,13 @@ int prio3_device_prepare(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
     TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp128><<<blocks64, 64, 0, st>>>(dp, in, e->sc)));
     const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
     if (ps && dp.P == 32)
-      TIMED(e, st, "k_query", (k_query_h<2, 32><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
+      TIMED(e, st, "k_query_h", (k_query_h<2, 32><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
     else if (ps && dp.P == 16)
-      TIMED(e, st, "k_query", (k_query_h<2, 16><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
+      TIMED(e, st, "k_query_h", (k_query_h<2, 16><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
     else if (ps && dp.P == 8)
-      TIMED(e, st, "k_query", (k_query_h<2, 8><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
+      TIMED(e, st, "k_query_h", (k_query_h<2, 8><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
     else if (ps)
-      TIMED(e, st, "k_query", (k_query_ps<4><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
+      TIMED(e, st, "k_query_ps", (k_query_ps<4><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
     else
       TIMED(e, st, "k_query", (k_query<Fp128><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
   } else {

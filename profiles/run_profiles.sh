@@ -18,4 +18,7 @@ timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format cs
 # 3) VALU / wave occupancy counters
 timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $OUT/pmc_sq -o run -- \
   python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > /dev/null
-find $OUT -name "*.csv" | head -50
+# 4) where the wave cycles go (WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~= WAVE_CYCLES)
+timeout -s KILL 200 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32 --kernel-trace --output-format csv -d $OUT/pmc_stall -o run -- \
+  python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > /dev/null
+ls $OUT
