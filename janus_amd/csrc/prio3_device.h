@@ -178,15 +178,49 @@ DEV void mac_zero(mac128& a) {
     a.h[k] = 0;
   }
 }
+// One asm statement for all 16 limb products: the compiler's hazard recogniser treats every
+// inline-asm boundary that writes VCC conservatively and pads it with s_nop, so splitting the
+// products into 16 statements cost ~1 s_nop per product (seen in the gfx950 assembly).
 DEV void mac_add(mac128& a, const f128& x, const f128& y) {
-#pragma unroll
-  for (int i = 0; i < 4; i++)
-#pragma unroll
-    for (int j = 0; j < 4; j++)
-      asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"
-          : "+v"(a.c[i + j]), "+v"(a.h[i + j])
-          : "v"(x.w[i]), "v"(y.w[j])
-          : "vcc");
+  asm(
+      "v_mad_u64_u32 %0, vcc, %14, %18, %0\n\t"
+      "v_addc_co_u32 %7, vcc, 0, %7, vcc\n\t"
+      "v_mad_u64_u32 %1, vcc, %14, %19, %1\n\t"
+      "v_addc_co_u32 %8, vcc, 0, %8, vcc\n\t"
+      "v_mad_u64_u32 %2, vcc, %14, %20, %2\n\t"
+      "v_addc_co_u32 %9, vcc, 0, %9, vcc\n\t"
+      "v_mad_u64_u32 %3, vcc, %14, %21, %3\n\t"
+      "v_addc_co_u32 %10, vcc, 0, %10, vcc\n\t"
+      "v_mad_u64_u32 %1, vcc, %15, %18, %1\n\t"
+      "v_addc_co_u32 %8, vcc, 0, %8, vcc\n\t"
+      "v_mad_u64_u32 %2, vcc, %15, %19, %2\n\t"
+      "v_addc_co_u32 %9, vcc, 0, %9, vcc\n\t"
+      "v_mad_u64_u32 %3, vcc, %15, %20, %3\n\t"
+      "v_addc_co_u32 %10, vcc, 0, %10, vcc\n\t"
+      "v_mad_u64_u32 %4, vcc, %15, %21, %4\n\t"
+      "v_addc_co_u32 %11, vcc, 0, %11, vcc\n\t"
+      "v_mad_u64_u32 %2, vcc, %16, %18, %2\n\t"
+      "v_addc_co_u32 %9, vcc, 0, %9, vcc\n\t"
+      "v_mad_u64_u32 %3, vcc, %16, %19, %3\n\t"
+      "v_addc_co_u32 %10, vcc, 0, %10, vcc\n\t"
+      "v_mad_u64_u32 %4, vcc, %16, %20, %4\n\t"
+      "v_addc_co_u32 %11, vcc, 0, %11, vcc\n\t"
+      "v_mad_u64_u32 %5, vcc, %16, %21, %5\n\t"
+      "v_addc_co_u32 %12, vcc, 0, %12, vcc\n\t"
+      "v_mad_u64_u32 %3, vcc, %17, %18, %3\n\t"
+      "v_addc_co_u32 %10, vcc, 0, %10, vcc\n\t"
+      "v_mad_u64_u32 %4, vcc, %17, %19, %4\n\t"
+      "v_addc_co_u32 %11, vcc, 0, %11, vcc\n\t"
+      "v_mad_u64_u32 %5, vcc, %17, %20, %5\n\t"
+      "v_addc_co_u32 %12, vcc, 0, %12, vcc\n\t"
+      "v_mad_u64_u32 %6, vcc, %17, %21, %6\n\t"
+      "v_addc_co_u32 %13, vcc, 0, %13, vcc\n\t"
+      : "+v"(a.c[0]), "+v"(a.c[1]), "+v"(a.c[2]), "+v"(a.c[3]), "+v"(a.c[4]), "+v"(a.c[5]),
+        "+v"(a.c[6]), "+v"(a.h[0]), "+v"(a.h[1]), "+v"(a.h[2]), "+v"(a.h[3]), "+v"(a.h[4]),
+        "+v"(a.h[5]), "+v"(a.h[6])
+      : "v"(x.w[0]), "v"(x.w[1]), "v"(x.w[2]), "v"(x.w[3]), "v"(y.w[0]), "v"(y.w[1]),
+        "v"(y.w[2]), "v"(y.w[3])
+      : "vcc");
 }
 // 2^128 mod p and 2^256 mod p
 DEV f128 mac_reduce(const mac128& a) {

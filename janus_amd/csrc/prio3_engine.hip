@@ -796,8 +796,8 @@ DEV void dft_reg(const DevParams& p, f128 (&x)[N], int stride) {
   }
 }
 
-template <int GS, int PP>
-__global__ __launch_bounds__(256, 3) void k_query_h(DevParams p, InPtrs in, Scratch sc,
+template <int GS, int PP, int PF = 1, int OCC = 3>
+__global__ __launch_bounds__(256, OCC) void k_query_h(DevParams p, InPtrs in, Scratch sc,
                                                     OutPtrs out) {
   typedef Fp128 F;
   typedef f128 T;
@@ -896,29 +896,49 @@ __global__ __launch_bounds__(256, 3) void k_query_h(DevParams p, InPtrs in, Scra
       mac_zero(Aa[q]);
       mac_zero(Bb[q]);
     }
+    // One dwordx4 load per element from a clamped (always in-bounds) address; padding
+    // elements are zeroed with a wave-uniform mask (a select on the loaded value made the
+    // compiler split the load into four branch-guarded dword loads).
     auto fetch = [&](uint32_t k, T* dst) {
 #pragma unroll
       for (int q = 0; q < GS; q++) {
         const uint32_t i = k * C + jg + q;
         const bool valid = (k < K) && (jg + q < C) && (i < M);
-        dst[q] = F::sel(valid, ldf<F>(sc.meas, valid ? i : 0, ld, r), Z);
+        const uint32_t msk = valid ? 0xffffffffu : 0u;
+        const uint4 v = ((const uint4*)sc.meas)[(size_t)(valid ? i : 0) * ld + r];
+        dst[q] = mk128(v.x & msk, v.y & msk, v.z & msk, v.w & msk);
       }
     };
     fetch(0, mc);
+    // PF=1: the per-call coefficients beta_k, L_(k+1) of the next call are loaded together
+    // with its measurement elements, one iteration ahead (they come from L2/MALL, and
+    // loading them at their use left the waves parked on s_waitcnt).
+    T be = ldf<F>(sc.beta, 0, ld, r), Lk = ldf<F>(sc.Lbuf, 1, ld, r);
 #pragma unroll 1
     for (uint32_t k = 0; k < K; k++) {
       T mn[GS];
       fetch(k + 1, mn);
-      const T be = ldf<F>(sc.beta, k, ld, r);
-      const T L = ldf<F>(sc.Lbuf, k + 1, ld, r);
+      T be_n, L_n;
+      const uint32_t kn = k + 1 < K ? k + 1 : k;
+      if constexpr (PF) {
+        be_n = ldf<F>(sc.beta, kn, ld, r);
+        L_n = ldf<F>(sc.Lbuf, kn + 1, ld, r);
+      } else {
+        be = ldf<F>(sc.beta, k, ld, r);
+        Lk = ldf<F>(sc.Lbuf, k + 1, ld, r);
+      }
 #pragma unroll
       for (int q = 0; q < GS; q++) {
         mac_add(Aa[q], be, mc[q]);
-        mac_add(Bb[q], L, mc[q]);
+        mac_add(Bb[q], Lk, mc[q]);
         sum_add(Ssum, mc[q]);
       }
 #pragma unroll
       for (int q = 0; q < GS; q++) mc[q] = mn[q];
+      if constexpr (PF) {
+        be = be_n;
+        Lk = L_n;
+      }
     }
 #pragma unroll
     for (int q = 0; q < GS; q++) {
@@ -1348,6 +1368,14 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
     e->force_slow = (int)value;
     return PRIO3_OK;
   }
+  if (!strcmp(key, "qh_occ")) {
+    e->qh_occ = (int)value;
+    return PRIO3_OK;
+  }
+  if (!strcmp(key, "qh_prefetch")) {
+    e->qh_prefetch = (int)value;
+    return PRIO3_OK;
+  }
   if (!strcmp(key, "split_xof")) {
     e->split_xof = (int)value;
     return PRIO3_OK;
@@ -1386,7 +1414,12 @@ int prio3_device_prepare(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
     TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp128><<<blocks64, 64, 0, st>>>(dp, in, e->sc)));
     const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
     if (ps && dp.P == 32)
-      TIMED(e, st, "k_query_h", (k_query_h<2, 32><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
+      switch (e->qh_prefetch * 10 + e->qh_occ) {
+        case 2: TIMED(e, st, "k_query_h", (k_query_h<2, 32, 0, 2><<<blocks, 256, 0, st>>>(dp, in, e->sc, out))); break;
+        case 3: TIMED(e, st, "k_query_h", (k_query_h<2, 32, 0, 3><<<blocks, 256, 0, st>>>(dp, in, e->sc, out))); break;
+        case 12: TIMED(e, st, "k_query_h", (k_query_h<2, 32, 1, 2><<<blocks, 256, 0, st>>>(dp, in, e->sc, out))); break;
+        default: TIMED(e, st, "k_query_h", (k_query_h<2, 32, 1, 3><<<blocks, 256, 0, st>>>(dp, in, e->sc, out))); break;
+      }
     else if (ps && dp.P == 16)
       TIMED(e, st, "k_query_h", (k_query_h<2, 16><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
     else if (ps && dp.P == 8)

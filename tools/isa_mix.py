@@ -27,7 +27,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HALF_RATE = re.compile(
     r"^v_(alignbit|mad_u64_u32|mad_i64_i32|lshl_add_u64|mul_lo_u32|mul_hi_u32|perm_b32|"
     r"lshl_or_b32|add_co_u32|addc_co_u32|sub_co_u32|subb_co_u32|subrev_co_u32|subbrev_co_u32|"
-    r"cmp_\w+_u64|cmp_\w+_i64|mov_b64|lshlrev_b64|lshrrev_b64|add_u64|sub_u64)")
+    r"cmp_\w+_u64|cmp_\w+_i64|mov_b64|lshlrev_b64|lshrrev_b64|add_u64|sub_u64|add3_u32|"
+    r"lshl_add_u32|add_lshl_u32|xad_u32|mad_u32_u24|mad_u32_u16)")
 PEAK_FULL_T = 64.5
 PEAK_HALF_T = 37.0
 

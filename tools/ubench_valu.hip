@@ -42,7 +42,6 @@ KERN(k_perm_8, 8, "v_perm_b32 %0, %0, %1, %2", "+v"(x[2 * i]), )
 KERN(k_lshlor_8, 8, "v_lshl_or_b32 %0, %0, 7, %1", "+v"(x[2 * i]), )
 KERN(k_addc_8, 8, "v_addc_co_u32 %0, vcc, %0, %1, vcc", "+v"(x[2 * i]), : "vcc")
 KERN(k_subb_8, 8, "v_subb_co_u32 %0, vcc, %0, %1, vcc", "+v"(x[2 * i]), : "vcc")
-KERN(k_cndmask_8, 8, "v_cndmask_b32 %0, %0, %1, vcc", "+v"(x[2 * i]), : "vcc")
 KERN(k_cmp64_8, 8, "v_cmp_lt_u64 vcc, %0, %0", "+v"(v), : "vcc")
 KERN(k_mov64_8, 8, "v_mov_b64 %0, %0", "+v"(v), )
 KERN(k_add3_8, 8, "v_add3_u32 %0, %0, %1, %2", "+v"(x[2 * i]), )
@@ -90,7 +89,6 @@ int main() {
     run("lshl_or x8", k_lshlor_8, o, blocks, threads, 8);
     run("addc x8", k_addc_8, o, blocks, threads, 8);
     run("subb x8", k_subb_8, o, blocks, threads, 8);
-    run("cndmask x8", k_cndmask_8, o, blocks, threads, 8);
     run("cmp_lt_u64 x8", k_cmp64_8, o, blocks, threads, 8);
     run("mov_b64 x8", k_mov64_8, o, blocks, threads, 8);
     run("add3 x8", k_add3_8, o, blocks, threads, 8);
