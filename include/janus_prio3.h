@@ -157,6 +157,12 @@ int prio3_engine_timing(prio3_engine* engine, char* names, size_t names_cap, dou
                         uint64_t* launches, int cap);
 void prio3_engine_timing_reset(prio3_engine* engine);
 
+/* Test-only: runs one Field128 primitive of the device library over n host-supplied operand
+ * pairs (16-byte LE elements) -- op 0/1: a*b (compiler / hand-scheduled), 2: a+b, 3: a-b,
+ * 4/5: sum of 16 products per output through the lazily reduced MAC (a, b hold 16 n elements).
+ * Lets tests pin the hand-written asm arithmetic against Python integers directly. */
+int prio3_selftest_field(int op, uint32_t n, const uint8_t* a, const uint8_t* b, uint8_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -300,8 +300,9 @@ struct prio3_engine {
           *d_msgs = nullptr, *d_status = nullptr;
   int force_slow = 0;
   int split_xof = 1;
-  int qh_prefetch = 0;
+  int qh_prefetch = 1;
   int qh_occ = 3;
+  int qh_regs = 0;
   int timing = 0;
   std::vector<KTime> times;
   std::vector<hipEvent_t> ev_pool;

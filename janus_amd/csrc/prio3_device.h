@@ -13,6 +13,10 @@
 #include <stdint.h>
 
 #define DEV __device__ __forceinline__
+// 1: Field128 multiply and MAC reduction use the hand-scheduled asm blocks below.
+#ifndef F128_ASM
+#define F128_ASM 1
+#endif
 
 // -------------------------------------------------------------------------------------
 // Field128
@@ -105,26 +109,12 @@ DEV f128 sub128(const f128& a, const f128& b) {
 
 DEV f128 neg128(const f128& a) { return sub128(zero128(), a); }
 
-// a*b mod p.  Product by schoolbook v_mad_u64_u32; reduction uses
-//   2^128 == 28*2^64 - 1,  2^192 == 783*2^64 - 28  (mod p).
-DEV f128 mul128(const f128& a, const f128& b) {
-  uint32_t r[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++) r[k] = 0;
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    uint64_t carry = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      uint64_t t = (uint64_t)a.w[i] * b.w[j] + (uint64_t)r[i + j] + carry;
-      r[i + j] = (uint32_t)t;
-      carry = t >> 32;
-    }
-    r[i + 4] = (uint32_t)carry;
-  }
-  // X = x3*2^192 + x2*2^128 + x1*2^64 + x0  (x_k = 64-bit words)
-  // S = x1 + 28*x2 + 783*x3 = s1*2^64 + (s_1:s_0)
-  uint64_t t0 = (uint64_t)r[2] + (uint64_t)r[4] * 28u + (uint64_t)r[6] * 783u;
+// Reduce X = r[0..7] + t * 2^256 (32-bit words; t < 2^32) mod p.  With 64-bit digits x_i:
+//   2^128 == 28*2^64 - 1,  2^192 == 783*2^64 - 28,  2^256 == 21896*2^64 - 783  (mod p), so
+//   X == (x0 - x2 - 28 x3 - 783 t) + 2^64 (x1 + 28 x2 + 783 x3 + 21896 t).
+DEV f128 red288(const uint32_t* r, uint32_t t) {
+  // S = x1 + 28*x2 + 783*x3 + 21896*t = s1*2^64 + (s_1:s_0)
+  uint64_t t0 = (uint64_t)r[2] + (uint64_t)r[4] * 28u + (uint64_t)r[6] * 783u + (uint64_t)t * 21896u;
   uint32_t s_0 = (uint32_t)t0;
   uint64_t t1 = (uint64_t)r[3] + (uint64_t)r[5] * 28u + (uint64_t)r[7] * 783u + (t0 >> 32);
   uint32_t s_1 = (uint32_t)t1;
@@ -132,8 +122,8 @@ DEV f128 mul128(const f128& a, const f128& b) {
   // u = (s_1:s_0) + 28*s1, carry c into 2^128
   uint64_t u = ((uint64_t)s_1 << 32 | s_0) + (uint64_t)s1 * 28u;
   uint32_t c = u < (uint64_t)s1 * 28u ? 1u : 0u;
-  // N = x2 + 28*x3 + s1  (< 2^70)
-  uint64_t n0 = (uint64_t)r[4] + (uint64_t)r[6] * 28u + s1;
+  // N = x2 + 28*x3 + 783*t + s1  (< 2^70)
+  uint64_t n0 = (uint64_t)r[4] + (uint64_t)r[6] * 28u + (uint64_t)t * 783u + s1;
   uint64_t n1 = (uint64_t)r[5] + (uint64_t)r[7] * 28u + (n0 >> 32);
   // A = x0 + u*2^64 + c*(28*2^64 - 1)
   uint32_t m = 0u - c, c0, c1, c2, c3;
@@ -159,6 +149,157 @@ DEV f128 mul128(const f128& a, const f128& b) {
   A.w[2] = addc(A.w[2], P128_2 & m, c1, &c2);
   A.w[3] = addc(A.w[3], P128_3 & m, c2, &c3);
   return canon128(A);
+}
+
+// a*b mod p.  Product by schoolbook v_mad_u64_u32, then red288.
+DEV f128 mul128(const f128& a, const f128& b) {
+  uint32_t r[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) r[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      uint64_t t = (uint64_t)a.w[i] * b.w[j] + (uint64_t)r[i + j] + carry;
+      r[i + j] = (uint32_t)t;
+      carry = t >> 32;
+    }
+    r[i + 4] = (uint32_t)carry;
+  }
+  return red288(r, 0);
+}
+
+
+// ---- hand-scheduled Field128 multiply / MAC reduction (gfx950 asm) ----------------------
+// The compiler pads every VCC/SGPR-carry chain it emits on gfx94x/gfx950 with s_nop (about one
+// per two VALU in mul128); these blocks are written as single asm statements whose VCC carry
+// chains are back to back.  Scratch lives in fixed registers v40-v68 (declared clobbered);
+// w0..w8 of the 288-bit value to reduce sit in v60-v68 so that every 64-bit operand
+// (x0 = v[60:61], x1 = v[62:63], x2 = v[64:65], x3 = v[66:67]) is an even-aligned pair.
+// Word-level model with every carry bound checked: tools/red288_model.py.
+#define F128_RED288_ASM                                                              \
+  /* S = x1 + 28 x2 + 783 x3 + 21896 t  ->  Y = v[40:41] (low 64), S2 = v44 */     \
+  "s_movk_i32 %[k783], 0x30f\n\t"                                                   \
+  "s_movk_i32 %[k21896], 0x5588\n\t"                                                \
+  "v_mad_u64_u32 v[40:41], vcc, v64, 28, v[62:63]\n\t"                              \
+  "v_cndmask_b32_e64 v44, 0, 1, vcc\n\t"                                            \
+  "v_mad_u64_u32 v[40:41], vcc, v66, %[k783], v[40:41]\n\t"                         \
+  "v_addc_co_u32_e32 v44, vcc, 0, v44, vcc\n\t"                                     \
+  "v_mad_u64_u32 v[40:41], vcc, v68, %[k21896], v[40:41]\n\t"                       \
+  "v_addc_co_u32_e32 v44, vcc, 0, v44, vcc\n\t"                                     \
+  "v_mad_u64_u32 v[42:43], vcc, v65, 28, 0\n\t"                                     \
+  "v_mad_u64_u32 v[42:43], vcc, v67, %[k783], v[42:43]\n\t"                         \
+  "v_add_co_u32_e32 v41, vcc, v41, v42\n\t"                                         \
+  "v_addc_co_u32_e32 v44, vcc, v43, v44, vcc\n\t"                                   \
+  /* N = x2 + 28 x3 + 783 t + S2  ->  Nn = v[46:47], N2 = v45 */                   \
+  "v_mad_u64_u32 v[46:47], vcc, v66, 28, v[64:65]\n\t"                              \
+  "v_cndmask_b32_e64 v45, 0, 1, vcc\n\t"                                            \
+  "v_mad_u64_u32 v[46:47], vcc, v68, %[k783], v[46:47]\n\t"                         \
+  "v_addc_co_u32_e32 v45, vcc, 0, v45, vcc\n\t"                                     \
+  "v_mad_u64_u32 v[46:47], vcc, v44, 1, v[46:47]\n\t"                               \
+  "v_addc_co_u32_e32 v45, vcc, 0, v45, vcc\n\t"                                     \
+  "v_mad_u64_u32 v[42:43], vcc, v67, 28, 0\n\t"                                     \
+  "v_add_co_u32_e32 v47, vcc, v47, v42\n\t"                                         \
+  "v_addc_co_u32_e32 v45, vcc, v43, v45, vcc\n\t"                                   \
+  /* U = Y + 28 S2 (carry c), A = (w0, w1, U) + c (28 2^64 - 1), folded twice */   \
+  "v_mad_u64_u32 v[40:41], vcc, v44, 28, v[40:41]\n\t"                              \
+  "v_cndmask_b32_e64 v48, 0, -1, vcc\n\t"                                           \
+  "v_add_co_u32_e32 v60, vcc, v60, v48\n\t"                                         \
+  "v_addc_co_u32_e32 v61, vcc, v61, v48, vcc\n\t"                                   \
+  "v_and_b32_e32 v49, 27, v48\n\t"                                                  \
+  "v_addc_co_u32_e32 v40, vcc, v40, v49, vcc\n\t"                                   \
+  "v_addc_co_u32_e32 v41, vcc, 0, v41, vcc\n\t"                                     \
+  "v_cndmask_b32_e64 v48, 0, -1, vcc\n\t"                                           \
+  "v_add_co_u32_e32 v60, vcc, v60, v48\n\t"                                         \
+  "v_addc_co_u32_e32 v61, vcc, v61, v48, vcc\n\t"                                   \
+  "v_and_b32_e32 v49, 27, v48\n\t"                                                  \
+  "v_addc_co_u32_e32 v40, vcc, v40, v49, vcc\n\t"                                   \
+  "v_addc_co_u32_e32 v41, vcc, 0, v41, vcc\n\t"                                     \
+  /* A - N, + p on borrow */                                                        \
+  "v_sub_co_u32_e32 v60, vcc, v60, v46\n\t"                                         \
+  "v_subb_co_u32_e32 v61, vcc, v61, v47, vcc\n\t"                                   \
+  "v_subb_co_u32_e32 v40, vcc, v40, v45, vcc\n\t"                                   \
+  "v_subbrev_co_u32_e32 v41, vcc, 0, v41, vcc\n\t"                                  \
+  "v_cndmask_b32_e64 v48, 0, -1, vcc\n\t"                                           \
+  "v_and_b32_e32 v49, 1, v48\n\t"                                                   \
+  "v_add_co_u32_e32 v60, vcc, v60, v49\n\t"                                         \
+  "v_addc_co_u32_e32 v61, vcc, 0, v61, vcc\n\t"                                     \
+  "v_and_b32_e32 v49, 0xffffffe4, v48\n\t"                                          \
+  "v_addc_co_u32_e32 v40, vcc, v40, v49, vcc\n\t"                                   \
+  "v_addc_co_u32_e32 v41, vcc, v41, v48, vcc\n\t"                                   \
+  /* canonical: A >= p  <=>  A + (2^128 - p) carries; 2^128 - p = (-1, -1, 27, 0) */ \
+  "v_add_co_u32_e32 v62, vcc, -1, v60\n\t"                                          \
+  "v_addc_co_u32_e32 v63, vcc, -1, v61, vcc\n\t"                                    \
+  "v_addc_co_u32_e32 v64, vcc, 27, v40, vcc\n\t"                                    \
+  "v_addc_co_u32_e32 v65, vcc, 0, v41, vcc\n\t"                                     \
+  "v_cndmask_b32_e32 %[r0], v60, v62, vcc\n\t"                                      \
+  "v_cndmask_b32_e32 %[r1], v61, v63, vcc\n\t"                                      \
+  "v_cndmask_b32_e32 %[r2], v40, v64, vcc\n\t"                                      \
+  "v_cndmask_b32_e32 %[r3], v41, v65, vcc\n\t"
+
+// reduction scratch: v40-v49 and w0..w8 = v60-v68
+#define F128_RED_CLOBBERS                                                                \
+  "vcc", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v60", "v61", \
+      "v62", "v63", "v64", "v65", "v66", "v67", "v68"
+// mul128_asm additionally holds the product columns in v40-v53 and h1..h5 in v54-v58
+#define F128_MUL_CLOBBERS                                                                 \
+  F128_RED_CLOBBERS, "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58"
+
+// a*b mod p: 16 v_mad_u64_u32 into even/odd product columns c_k = v[40+2k : 41+2k] with
+// overflow words h1..h5 = v54..v58 (first overflow of a column by v_cndmask), column
+// normalisation into w0..w8 = v60..v68, then the shared reduction.
+DEV f128 mul128_asm(const f128& a, const f128& b) {
+  f128 r;
+  uint32_t k783, k21896;
+  asm volatile(
+      "v_mad_u64_u32 v[40:41], vcc, %[a0], %[b0], 0\n\t"
+      "v_mad_u64_u32 v[42:43], vcc, %[a0], %[b1], 0\n\t"
+      "v_mad_u64_u32 v[42:43], vcc, %[a1], %[b0], v[42:43]\n\t"
+      "v_cndmask_b32_e64 v54, 0, 1, vcc\n\t"
+      "v_mad_u64_u32 v[44:45], vcc, %[a0], %[b2], 0\n\t"
+      "v_mad_u64_u32 v[44:45], vcc, %[a1], %[b1], v[44:45]\n\t"
+      "v_cndmask_b32_e64 v55, 0, 1, vcc\n\t"
+      "v_mad_u64_u32 v[44:45], vcc, %[a2], %[b0], v[44:45]\n\t"
+      "v_addc_co_u32_e32 v55, vcc, 0, v55, vcc\n\t"
+      "v_mad_u64_u32 v[46:47], vcc, %[a0], %[b3], 0\n\t"
+      "v_mad_u64_u32 v[46:47], vcc, %[a1], %[b2], v[46:47]\n\t"
+      "v_cndmask_b32_e64 v56, 0, 1, vcc\n\t"
+      "v_mad_u64_u32 v[46:47], vcc, %[a2], %[b1], v[46:47]\n\t"
+      "v_addc_co_u32_e32 v56, vcc, 0, v56, vcc\n\t"
+      "v_mad_u64_u32 v[46:47], vcc, %[a3], %[b0], v[46:47]\n\t"
+      "v_addc_co_u32_e32 v56, vcc, 0, v56, vcc\n\t"
+      "v_mad_u64_u32 v[48:49], vcc, %[a1], %[b3], 0\n\t"
+      "v_mad_u64_u32 v[48:49], vcc, %[a2], %[b2], v[48:49]\n\t"
+      "v_cndmask_b32_e64 v57, 0, 1, vcc\n\t"
+      "v_mad_u64_u32 v[48:49], vcc, %[a3], %[b1], v[48:49]\n\t"
+      "v_addc_co_u32_e32 v57, vcc, 0, v57, vcc\n\t"
+      "v_mad_u64_u32 v[50:51], vcc, %[a2], %[b3], 0\n\t"
+      "v_mad_u64_u32 v[50:51], vcc, %[a3], %[b2], v[50:51]\n\t"
+      "v_cndmask_b32_e64 v58, 0, 1, vcc\n\t"
+      "v_mad_u64_u32 v[52:53], vcc, %[a3], %[b3], 0\n\t"
+      /* X = E + O + H: E = c0 c2 c4 c6 (words 0-7), O = c1 c3 c5 (words 1-6), h_k at word k+2 */
+      "v_mov_b32_e32 v60, v40\n\t"
+      "v_add_co_u32_e32 v61, vcc, v41, v42\n\t"
+      "v_addc_co_u32_e32 v62, vcc, v44, v43, vcc\n\t"
+      "v_addc_co_u32_e32 v63, vcc, v45, v46, vcc\n\t"
+      "v_addc_co_u32_e32 v64, vcc, v48, v47, vcc\n\t"
+      "v_addc_co_u32_e32 v65, vcc, v49, v50, vcc\n\t"
+      "v_addc_co_u32_e32 v66, vcc, v52, v51, vcc\n\t"
+      "v_addc_co_u32_e32 v67, vcc, 0, v53, vcc\n\t"
+      "v_add_co_u32_e32 v63, vcc, v63, v54\n\t"
+      "v_addc_co_u32_e32 v64, vcc, v64, v55, vcc\n\t"
+      "v_addc_co_u32_e32 v65, vcc, v65, v56, vcc\n\t"
+      "v_addc_co_u32_e32 v66, vcc, v66, v57, vcc\n\t"
+      "v_addc_co_u32_e32 v67, vcc, v67, v58, vcc\n\t"
+      "v_mov_b32_e32 v68, 0\n\t"
+      F128_RED288_ASM
+      : [r0] "=&v"(r.w[0]), [r1] "=&v"(r.w[1]), [r2] "=&v"(r.w[2]), [r3] "=&v"(r.w[3]),
+        [k783] "=&s"(k783), [k21896] "=&s"(k21896)
+      : [a0] "v"(a.w[0]), [a1] "v"(a.w[1]), [a2] "v"(a.w[2]), [a3] "v"(a.w[3]),
+        [b0] "v"(b.w[0]), [b1] "v"(b.w[1]), [b2] "v"(b.w[2]), [b3] "v"(b.w[3])
+      : F128_MUL_CLOBBERS);
+  return r;
 }
 
 // -------------------------------------------------------------------------------------
@@ -222,28 +363,72 @@ DEV void mac_add(mac128& a, const f128& x, const f128& y) {
         "v"(y.w[2]), "v"(y.w[3])
       : "vcc");
 }
-// 2^128 mod p and 2^256 mod p
+// Column normalisation (X = E + O + H: even columns, odd columns, overflow words -- each a
+// plain concatenation) into 9 words, then one red288.  Valid for < 2^31 accumulated products.
 DEV f128 mac_reduce(const mac128& a) {
-  // normalise columns into 10 words: word n = lo32(c_n) + hi32(c_(n-1)) + h_(n-2) + carry
-  uint32_t w[10];
-  uint64_t carry = 0;
-#pragma unroll
-  for (int n = 0; n < 10; n++) {
-    uint64_t s = carry;
-    if (n < 7) s += (uint32_t)a.c[n];
-    if (n >= 1 && n - 1 < 7) s += (uint32_t)(a.c[n - 1] >> 32);
-    if (n >= 2 && n - 2 < 7) s += a.h[n - 2];
-    w[n] = (uint32_t)s;
-    carry = s >> 32;
-  }
-  // X = L + H*2^128 + T*2^256,  2^128 = 28*2^64 - 1,  2^256 = (2^128)^2 (mod p)
-  const f128 L = canon128(mk128(w[0], w[1], w[2], w[3]));
-  const f128 H = mk128(w[4], w[5], w[6], w[7]);
-  const f128 T = mk128(w[8], w[9], 0, 0);
-  const f128 c128 = mk128(0xffffffffu, 0xffffffffu, 27u, 0u);
-  const f128 c256 = mul128(c128, c128);
-  return add128(add128(L, mul128(canon128(H), c128)), mul128(T, c256));
+  uint32_t w[9], cy;
+  w[0] = (uint32_t)a.c[0];
+  w[1] = addc((uint32_t)(a.c[0] >> 32), (uint32_t)a.c[1], 0, &cy);
+  w[2] = addc((uint32_t)a.c[2], (uint32_t)(a.c[1] >> 32), cy, &cy);
+  w[3] = addc((uint32_t)(a.c[2] >> 32), (uint32_t)a.c[3], cy, &cy);
+  w[4] = addc((uint32_t)a.c[4], (uint32_t)(a.c[3] >> 32), cy, &cy);
+  w[5] = addc((uint32_t)(a.c[4] >> 32), (uint32_t)a.c[5], cy, &cy);
+  w[6] = addc((uint32_t)a.c[6], (uint32_t)(a.c[5] >> 32), cy, &cy);
+  w[7] = addc((uint32_t)(a.c[6] >> 32), 0, cy, &cy);
+  w[8] = cy;
+  w[2] = addc(w[2], a.h[0], 0, &cy);
+  w[3] = addc(w[3], a.h[1], cy, &cy);
+  w[4] = addc(w[4], a.h[2], cy, &cy);
+  w[5] = addc(w[5], a.h[3], cy, &cy);
+  w[6] = addc(w[6], a.h[4], cy, &cy);
+  w[7] = addc(w[7], a.h[5], cy, &cy);
+  w[8] = w[8] + a.h[6] + cy;
+  return red288(w, w[8]);
 }
+
+// mac_reduce in asm: X = E + O + H over the accumulator columns, then the shared reduction.
+DEV f128 mac_reduce_asm(const mac128& a) {
+  f128 r;
+  uint32_t k783, k21896;
+  asm volatile(
+      "v_mov_b32_e32 v60, %[c0l]\n\t"
+      "v_add_co_u32_e32 v61, vcc, %[c0h], %[c1l]\n\t"
+      "v_addc_co_u32_e32 v62, vcc, %[c2l], %[c1h], vcc\n\t"
+      "v_addc_co_u32_e32 v63, vcc, %[c2h], %[c3l], vcc\n\t"
+      "v_addc_co_u32_e32 v64, vcc, %[c4l], %[c3h], vcc\n\t"
+      "v_addc_co_u32_e32 v65, vcc, %[c4h], %[c5l], vcc\n\t"
+      "v_addc_co_u32_e32 v66, vcc, %[c6l], %[c5h], vcc\n\t"
+      "v_addc_co_u32_e32 v67, vcc, 0, %[c6h], vcc\n\t"
+      "v_cndmask_b32_e64 v68, 0, 1, vcc\n\t"
+      "v_add_co_u32_e32 v62, vcc, v62, %[h0]\n\t"
+      "v_addc_co_u32_e32 v63, vcc, v63, %[h1], vcc\n\t"
+      "v_addc_co_u32_e32 v64, vcc, v64, %[h2], vcc\n\t"
+      "v_addc_co_u32_e32 v65, vcc, v65, %[h3], vcc\n\t"
+      "v_addc_co_u32_e32 v66, vcc, v66, %[h4], vcc\n\t"
+      "v_addc_co_u32_e32 v67, vcc, v67, %[h5], vcc\n\t"
+      "v_addc_co_u32_e32 v68, vcc, v68, %[h6], vcc\n\t"
+      F128_RED288_ASM
+      : [r0] "=&v"(r.w[0]), [r1] "=&v"(r.w[1]), [r2] "=&v"(r.w[2]), [r3] "=&v"(r.w[3]),
+        [k783] "=&s"(k783), [k21896] "=&s"(k21896)
+      : [c0l] "v"((uint32_t)a.c[0]), [c0h] "v"((uint32_t)(a.c[0] >> 32)),
+        [c1l] "v"((uint32_t)a.c[1]), [c1h] "v"((uint32_t)(a.c[1] >> 32)),
+        [c2l] "v"((uint32_t)a.c[2]), [c2h] "v"((uint32_t)(a.c[2] >> 32)),
+        [c3l] "v"((uint32_t)a.c[3]), [c3h] "v"((uint32_t)(a.c[3] >> 32)),
+        [c4l] "v"((uint32_t)a.c[4]), [c4h] "v"((uint32_t)(a.c[4] >> 32)),
+        [c5l] "v"((uint32_t)a.c[5]), [c5h] "v"((uint32_t)(a.c[5] >> 32)),
+        [c6l] "v"((uint32_t)a.c[6]), [c6h] "v"((uint32_t)(a.c[6] >> 32)), [h0] "v"(a.h[0]),
+        [h1] "v"(a.h[1]), [h2] "v"(a.h[2]), [h3] "v"(a.h[3]), [h4] "v"(a.h[4]), [h5] "v"(a.h[5]),
+        [h6] "v"(a.h[6])
+      : F128_RED_CLOBBERS);
+  return r;
+}
+
+#if F128_ASM
+DEV f128 mac_reduce_f(const mac128& a) { return mac_reduce_asm(a); }
+#else
+DEV f128 mac_reduce_f(const mac128& a) { return mac_reduce(a); }
+#endif
+
 // lazily reduced sum of Field128 values (128-bit sum + 32-bit carry word)
 struct sum128 {
   uint32_t w[5];
@@ -302,7 +487,11 @@ struct Fp128 {
   static DEV T one() { return one128(); }
   static DEV T add(const T& a, const T& b) { return add128(a, b); }
   static DEV T sub(const T& a, const T& b) { return sub128(a, b); }
+#if F128_ASM
+  static DEV T mul(const T& a, const T& b) { return mul128_asm(a, b); }
+#else
   static DEV T mul(const T& a, const T& b) { return mul128(a, b); }
+#endif
   static DEV bool eq(const T& a, const T& b) { return eq128(a, b); }
   static DEV bool is_zero(const T& a) { return is_zero128(a); }
   static DEV bool lt_p(const T& a) { return !ge_p128(a); }

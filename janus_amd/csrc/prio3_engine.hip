@@ -859,20 +859,59 @@ __global__ __launch_bounds__(256, OCC) void k_query_h(DevParams p, InPtrs in, Sc
     }
   }
   // p(t) (Horner) and range = sum_c p(alpha^c) = sum_e coef_e sigma_(e mod P)
-  T pt = F::zero(), range = F::zero();
-  for (uint32_t e = p.glen; e-- > 0;) {
-    const T ce = ldf<F>(sc.proofs, A + e, ld, r);
-    pt = F::add(F::mul(pt, t), ce);
-    range = F::add(range, F::mul(ce, F::from_words(p.sigma128[e & (PP - 1)])));
+  // p(t) by Horner; the range sum is a lazily reduced dot product with the (uniform) sigma.
+  T pt = F::zero(), range;
+  {
+    mac128 R;
+    mac_zero(R);
+    // glen = 2 (PP - 1) + 1 for the degree-2 ParallelSum(Mul) gadget; the coefficients are
+    // loaded HD ahead (one exposed load latency per coefficient otherwise).
+    constexpr int GLEN = 2 * (PP - 1) + 1, HD = 4;
+    auto ldc = [&](int q) {  // coefficient e = GLEN-1-q (clamped; unused past the end)
+      const int e = GLEN - 1 - q;
+      return ldf<F>(sc.proofs, A + (e >= 0 ? e : 0), ld, r);
+    };
+    T cb[HD];
+#pragma unroll
+    for (int q = 0; q < HD; q++) cb[q] = ldc(q);
+#pragma unroll 1
+    for (int q0 = 0; q0 < GLEN; q0 += HD) {
+      T cn[HD];
+#pragma unroll
+      for (int q = 0; q < HD; q++) cn[q] = ldc(q0 + HD + q);
+#pragma unroll
+      for (int q = 0; q < HD; q++) {
+        const int e = GLEN - 1 - (q0 + q);
+        if (e >= 0) {
+          pt = F::add(F::mul(pt, t), cb[q]);
+          mac_add(R, cb[q], F::from_words(p.sigma128[e & (PP - 1)]));
+        }
+        cb[q] = cn[q];
+      }
+    }
+    range = mac_reduce_f(R);
   }
   const T r0 = ldf<F>(sc.jr, 0, ld, r);
   {
-    T rC = F::one();
-    for (uint32_t j = 0; j < C; j++) rC = F::mul(rC, r0);
+    // r0^C by square-and-multiply over the (uniform) bits of C
+    T rC = F::one(), sq = r0;
+    for (uint32_t e = C; e; e >>= 1) {
+      if (e & 1) rC = F::mul(rC, sq);
+      if (e > 1) sq = F::mul(sq, sq);
+    }
+    // beta_k = L_(k+1) r^(Ck), eight L values loaded at a time
     T rk = F::one();
-    for (uint32_t k = 0; k < K; k++) {
-      F::store(sc.beta, (size_t)k * ld + r, F::mul(ldf<F>(sc.Lbuf, k + 1, ld, r), rk));
-      rk = F::mul(rk, rC);
+    for (uint32_t k0 = 0; k0 < K; k0 += 8) {
+      T lb[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) lb[q] = ldf<F>(sc.Lbuf, k0 + q < K ? k0 + q + 1 : 1, ld, r);
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        if (k0 + q < K) {
+          F::store(sc.beta, (size_t)(k0 + q) * ld + r, F::mul(lb[q], rk));
+          rk = F::mul(rk, rC);
+        }
+      }
     }
   }
   const T half = FC<F>::half(p);
@@ -940,19 +979,246 @@ __global__ __launch_bounds__(256, OCC) void k_query_h(DevParams p, InPtrs in, Sc
         Lk = L_n;
       }
     }
+    // Wire values at t, lazily reduced: f1 = seed_(2j+1) L0 + B_j - L/2 folds the seed term into
+    // B's accumulator, f0 = seed_2j L0 + r^(j+1) A_j is one two-product MAC, and the gadget
+    // products of the group are summed in one MAC before a single reduction.
+    mac128 Gq;
+    mac_zero(Gq);
 #pragma unroll
     for (int q = 0; q < GS; q++) {
       const uint32_t j = jg + q;
-      const bool valid = j < C;
-      const uint32_t jj = valid ? j : 0;
-      const T Aq = mac_reduce(Aa[q]), Bq = mac_reduce(Bb[q]);
-      const T f0 = F::add(F::mul(ldf<F>(sc.proofs, 2 * jj, ld, r), L0), F::mul(rj, Aq));
-      const T f1 = F::sub(F::add(F::mul(ldf<F>(sc.proofs, 2 * jj + 1, ld, r), L0), Bq), halfL);
-      const T prod = F::mul(F::add(lv(1 + 2 * jj), f0), F::add(lv(2 + 2 * jj), f1));
-      G = F::add(G, F::sel(valid, prod, Z));
-      rj = F::sel(valid, F::mul(rj, r0), rj);
+      if (j < C) {  // wave-uniform
+        mac_add(Bb[q], ldf<F>(sc.proofs, 2 * j + 1, ld, r), L0);
+        const T f1 = F::sub(mac_reduce_f(Bb[q]), halfL);
+        const T Aq = mac_reduce_f(Aa[q]);
+        mac128 F0;
+        mac_zero(F0);
+        mac_add(F0, ldf<F>(sc.proofs, 2 * j, ld, r), L0);
+        mac_add(F0, rj, Aq);
+        const T f0 = mac_reduce_f(F0);
+        mac_add(Gq, F::add(lv(1 + 2 * j), f0), F::add(lv(2 + 2 * j), f1));
+        rj = F::mul(rj, r0);
+      }
+    }
+    G = F::add(G, mac_reduce_f(Gq));
+  }
+  const T S = sum_reduce(Ssum);
+  T v;
+  if (p.kind == PRIO3_SUMVEC) {
+    v = range;
+  } else {
+    const T r1 = ldf<F>(sc.jr, 1, ld, r);
+    v = F::add(F::mul(r1, range), F::mul(F::mul(r1, r1), F::sub(S, half)));
+  }
+  const T V0 = F::add(lv(0), v);
+  const T PT = F::add(lv(A + 1), pt);
+  if (status == PRIO3_STATUS_FINISHED) {
+    if (!decode_ok)
+      status = PRIO3_STATUS_PREP_SHARE_DECODE;
+    else if (!F::is_zero(V0) || !F::eq(G, PT))
+      status = PRIO3_STATUS_PREP_MSG;
+  }
+  uint32_t lpart[4], hpart[4];
+  load16(lps + (size_t)p.verifier_len * F::ES, lpart);
+  {
+    uint4 hp = sc.part[r];
+    hpart[0] = hp.x;
+    hpart[1] = hp.y;
+    hpart[2] = hp.z;
+    hpart[3] = hp.w;
+  }
+  KState s;
+  kzero(s);
+  Msg mm;
+  msg_zero(mm);
+  msg_dst(mm, p.dst[6]);
+  msg_bytes16(mm, 25, lpart);
+  msg_bytes16(mm, 41, hpart);
+  msg_absorb_final(s, mm, 57);
+  uint4 cor = sc.corrected[r];
+  uint32_t msg[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
+  if (status == PRIO3_STATUS_FINISHED &&
+      (msg[0] != cor.x || msg[1] != cor.y || msg[2] != cor.z || msg[3] != cor.w))
+    status = PRIO3_STATUS_PREP_NEXT;
+  if (status != PRIO3_STATUS_FINISHED) msg[0] = msg[1] = msg[2] = msg[3] = 0;
+  ((uint4*)out.prep_msgs)[r] = make_uint4(msg[0], msg[1], msg[2], msg[3]);
+  out.status[r] = status;
+  if (p.kind == PRIO3_SUMVEC) {
+    for (uint32_t e = 0; e < p.out_len; e++) {
+      T acc = F::zero(), pw = F::one();
+      for (uint32_t b = 0; b < p.bits; b++) {
+        acc = F::add(acc, F::mul(pw, ldf<F>(sc.meas, e * p.bits + b, ld, r)));
+        pw = F::add(pw, pw);
+      }
+      F::store(sc.out, (size_t)e * ld + r, acc);
     }
   }
+}
+
+
+// ------------------------------------------------------------------------------------
+// k_query_r<C, K>: the P = 32 ParallelSum(Mul, C) query (Prio3Histogram(256,16): C = K = 16)
+// with every per-call coefficient register-resident.  The Lagrange values L_1..L_K and
+// beta_k = L_(k+1) r^(Ck) never leave VGPRs (k_query_h re-read them from scratch on each of its
+// C/GS wire sweeps, ~4 KiB per report of L2-missing traffic); the sweep is wire-outer
+// (j = 0..C-1), call-inner (k unrolled), so each measurement element is loaded exactly once
+// with a rolling prefetch of QD elements.  2 waves/SIMD (256-VGPR budget).
+// ------------------------------------------------------------------------------------
+template <int C, int K, int QD = 4>
+__global__ __launch_bounds__(256, 2) void k_query_r(DevParams p, InPtrs in, Scratch sc,
+                                                   OutPtrs out) {
+  typedef Fp128 F;
+  typedef f128 T;
+  constexpr int PP = 32, GLEN = 2 * (PP - 1) + 1, A = 2 * C;
+  static_assert(K + 1 <= PP && K >= QD, "shape");
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= p.n) return;
+  const size_t ld = p.ld;
+  const uint32_t M = p.meas_len;
+  uint8_t status = PRIO3_STATUS_FINISHED;
+  const T t = ldf<F>(sc.qr, 0, ld, r);
+  // ---- Lagrange basis at t: X[idx] = L_c with c = (32 - idx) mod 32, X[2k + ph] from the
+  // ph-th decimation-in-frequency half (see k_query_h); L_c for c = 1..K is X[32 - c].
+  T L[K], L0;
+  {
+    T t16 = t;
+#pragma unroll
+    for (int i = 0; i < 4; i++) t16 = F::mul(t16, t16);
+    if (F::eq(F::mul(t16, t16), F::one())) status = PRIO3_STATUS_PREP_INIT;
+    const T ip = FC<F>::invP(p);
+    const T gy = F::mul(ip, F::add(F::one(), t16)), gz = F::mul(ip, F::sub(F::one(), t16));
+    const T tw = F::mul(t, F::from_words(p.tw128[1]));
+#pragma unroll
+    for (int ph = 0; ph < 2; ph++) {
+      T x[16];
+      T pw = ph == 0 ? gy : gz;
+      const T ratio = ph == 0 ? t : tw;
+#pragma unroll
+      for (int e = 0; e < 16; e++) {
+        x[__builtin_bitreverse32(e) >> 28] = pw;
+        if (e < 15) pw = F::mul(pw, ratio);
+      }
+      dft_reg<16, 4>(p, x, 2);
+      if (ph == 0) L0 = x[0];
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        const int c = (32 - (2 * k + ph)) & 31;
+        if (c >= 1 && c <= K) L[c - 1] = x[k];
+      }
+    }
+  }
+  T sumL = L[0];
+#pragma unroll
+  for (int c = 1; c < K; c++) sumL = F::add(sumL, L[c]);
+  // L_1..L_K go to LDS ([k][thread], conflict-free 16-byte rows; 64 KiB per 256-thread block,
+  // two blocks per CU), beta stays in VGPRs.
+  __shared__ uint4 Ls[K][256];
+#pragma unroll
+  for (int k = 0; k < K; k++) Ls[k][threadIdx.x] = make_uint4(L[k].w[0], L[k].w[1], L[k].w[2], L[k].w[3]);
+  // ---- p(t) (Horner) and range = sum_e coef_e sigma_(e mod 32) (lazy MAC)
+  T pt = F::zero(), range;
+  {
+    mac128 R;
+    mac_zero(R);
+    constexpr int HD = 4;  // rolling prefetch of the coefficients, highest first
+    T cb[HD];
+#pragma unroll
+    for (int q = 0; q < HD; q++) cb[q] = ldf<F>(sc.proofs, A + GLEN - 1 - q, ld, r);
+#pragma unroll
+    for (int q = 0; q < GLEN; q++) {
+      const int e = GLEN - 1 - q;
+      const T ce = cb[q % HD];
+      if (q + HD < GLEN) cb[q % HD] = ldf<F>(sc.proofs, A + e - HD, ld, r);
+      pt = F::add(F::mul(pt, t), ce);
+      mac_add(R, ce, F::from_words(p.sigma128[e & (PP - 1)]));
+    }
+    range = mac_reduce_f(R);
+  }
+  // ---- beta_k = L_(k+1) r0^(Ck)
+  const T r0 = ldf<F>(sc.jr, 0, ld, r);
+  T beta[K];
+  {
+    T rC = F::one(), sq = r0;
+#pragma unroll
+    for (int e = C; e; e >>= 1) {
+      if (e & 1) rC = F::mul(rC, sq);
+      if (e > 1) sq = F::mul(sq, sq);
+    }
+    beta[0] = L[0];
+    T rk = rC;
+#pragma unroll
+    for (int k = 1; k < K; k++) {
+      beta[k] = F::mul(L[k], rk);
+      if (k + 1 < K) rk = F::mul(rk, rC);
+    }
+  }
+  const T half = FC<F>::half(p);
+  const T halfL = F::mul(half, sumL);
+  const uint8_t* lps = in.leader + (size_t)r * p.prep_share_len;
+  bool decode_ok = true;
+  auto lv = [&](uint32_t e) {
+    T x = F::load(lps, e);
+    if (!F::lt_p(x)) decode_ok = false;
+    return x;
+  };
+  // ---- wire sweep: element i = k*C + j, rolling prefetch of QD elements
+  auto ldm = [&](int j, int k) {
+    const uint32_t i = (uint32_t)(k * C + j);
+    const bool valid = j < C && i < M;
+    const uint32_t msk = valid ? 0xffffffffu : 0u;
+    const uint4 v = ((const uint4*)sc.meas)[(size_t)(valid ? i : 0) * ld + r];
+    return mk128(v.x & msk, v.y & msk, v.z & msk, v.w & msk);
+  };
+  T mb[QD];
+#pragma unroll
+  for (int q = 0; q < QD; q++) mb[q] = ldm(0, q);
+  sum128 Ssum;
+  sum_zero(Ssum);
+  mac128 Gacc;
+  mac_zero(Gacc);
+  T rj = r0;
+  // per-wire operands of the next wire (seeds, leader verifier entries), one wire ahead
+  auto ldw = [&](int j, T* w) {
+    const int jj = j < C ? j : C - 1;
+    w[0] = ldf<F>(sc.proofs, 2 * jj, ld, r);
+    w[1] = ldf<F>(sc.proofs, 2 * jj + 1, ld, r);
+    w[2] = F::load(lps, 1 + 2 * jj);
+    w[3] = F::load(lps, 2 + 2 * jj);
+  };
+  T wn[4];
+  ldw(0, wn);
+#pragma unroll 1
+  for (int j = 0; j < C; j++) {
+    T wc[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) wc[q] = wn[q];
+    ldw(j + 1, wn);
+    mac128 Aa, Bb;
+    mac_zero(Aa);
+    mac_zero(Bb);
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const T m = mb[k % QD];
+      // refill with element (j, k + QD) or, past the last call, (j + 1, k + QD - K)
+      mb[k % QD] = (k + QD < K) ? ldm(j, k + QD) : ldm(j + 1, k + QD - K);
+      mac_add(Aa, beta[k], m);
+      const uint4 lk = Ls[k][threadIdx.x];
+      mac_add(Bb, mk128(lk.x, lk.y, lk.z, lk.w), m);
+      sum_add(Ssum, m);
+    }
+    mac_add(Bb, wc[1], L0);
+    const T f1 = F::sub(mac_reduce_f(Bb), halfL);
+    const T Aq = mac_reduce_f(Aa);
+    mac128 F0;
+    mac_zero(F0);
+    mac_add(F0, wc[0], L0);
+    mac_add(F0, rj, Aq);
+    const T f0 = mac_reduce_f(F0);
+    if (!F::lt_p(wc[2]) || !F::lt_p(wc[3])) decode_ok = false;
+    mac_add(Gacc, F::add(wc[2], f0), F::add(wc[3], f1));
+    rj = F::mul(rj, r0);
+  }
+  const T G = mac_reduce_f(Gacc);
   const T S = sum_reduce(Ssum);
   T v;
   if (p.kind == PRIO3_SUMVEC) {
@@ -1088,6 +1354,34 @@ __global__ void k_combine(uint32_t k, uint32_t len, uint32_t n_segments, const u
     for (uint32_t i = 0; i < k; i++) s += cin[(size_t)i * n_segments + e];
     cout[e] = s;
   }
+}
+
+
+// ------------------------------------------------------------------------------------
+// Field self-test (parity of the hand-scheduled Field128 blocks against Python bigints)
+// ------------------------------------------------------------------------------------
+// op 0: mul128 (compiler code), 1: mul128_asm, 2: add128, 3: sub128,
+// op 4: sum_{i<16} a_(16x+i) b_(16x+i) via mac_add + mac_reduce (compiler code),
+// op 5: the same with mac_reduce_asm.   a, b, out: [n][16 B] (ops 4/5: a, b [16 n][16 B]).
+__global__ void k_selftest_f128(int op, uint32_t n, const uint4* a, const uint4* b, uint4* out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  auto ld = [](const uint4* p, size_t k) {
+    const uint4 v = p[k];
+    return mk128(v.x, v.y, v.z, v.w);
+  };
+  f128 z;
+  if (op == 0) z = mul128(ld(a, i), ld(b, i));
+  else if (op == 1) z = mul128_asm(ld(a, i), ld(b, i));
+  else if (op == 2) z = add128(ld(a, i), ld(b, i));
+  else if (op == 3) z = sub128(ld(a, i), ld(b, i));
+  else {
+    mac128 m;
+    mac_zero(m);
+    for (int k = 0; k < 16; k++) mac_add(m, ld(a, (size_t)i * 16 + k), ld(b, (size_t)i * 16 + k));
+    z = op == 4 ? mac_reduce(m) : mac_reduce_asm(m);
+  }
+  out[i] = make_uint4(z.w[0], z.w[1], z.w[2], z.w[3]);
 }
 
 // ====================================================================================
@@ -1368,6 +1662,10 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
     e->force_slow = (int)value;
     return PRIO3_OK;
   }
+  if (!strcmp(key, "qh_regs")) {
+    e->qh_regs = (int)value;
+    return PRIO3_OK;
+  }
   if (!strcmp(key, "qh_occ")) {
     e->qh_occ = (int)value;
     return PRIO3_OK;
@@ -1413,7 +1711,9 @@ int prio3_device_prepare(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
     }
     TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp128><<<blocks64, 64, 0, st>>>(dp, in, e->sc)));
     const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
-    if (ps && dp.P == 32)
+    if (ps && dp.P == 32 && dp.chunk == 16 && dp.calls == 16 && e->qh_regs)
+      TIMED(e, st, "k_query_r", (k_query_r<16, 16><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
+    else if (ps && dp.P == 32)
       switch (e->qh_prefetch * 10 + e->qh_occ) {
         case 2: TIMED(e, st, "k_query_h", (k_query_h<2, 32, 0, 2><<<blocks, 256, 0, st>>>(dp, in, e->sc, out))); break;
         case 3: TIMED(e, st, "k_query_h", (k_query_h<2, 32, 0, 3><<<blocks, 256, 0, st>>>(dp, in, e->sc, out))); break;
@@ -1668,6 +1968,29 @@ void prio3_engine_timing_reset(prio3_engine* e) {
     t.ms = 0;
     t.launches = 0;
   }
+}
+
+int prio3_selftest_field(int op, uint32_t n, const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  if (op < 0 || op > 5) return PRIO3_EINVAL;
+  if (n == 0) return PRIO3_OK;
+  const size_t m = (op >= 4 ? 16 : 1) * (size_t)n * 16;
+  void *da = nullptr, *db = nullptr, *dout = nullptr;
+  int rc = PRIO3_OK;
+  if (hipMalloc(&da, m) != hipSuccess || hipMalloc(&db, m) != hipSuccess ||
+      hipMalloc(&dout, (size_t)n * 16) != hipSuccess ||
+      hipMemcpy(da, a, m, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(db, b, m, hipMemcpyHostToDevice) != hipSuccess) {
+    rc = PRIO3_EDEVICE;
+  } else {
+    k_selftest_f128<<<(n + 255) / 256, 256>>>(op, n, (const uint4*)da, (const uint4*)db, (uint4*)dout);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpy(out, dout, (size_t)n * 16, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = PRIO3_EDEVICE;
+  }
+  hipFree(da);
+  hipFree(db);
+  hipFree(dout);
+  return rc;
 }
 
 }  // extern "C"

@@ -72,7 +72,7 @@ EXPORTED_SYMBOLS = (
     "prio3_accumulate", "prio3_debug_output_shares", "prio3_batch_free", "prio3_device_prepare",
     "prio3_device_accumulate", "prio3_device_output_shares", "prio3_device_combine",
     "prio3_engine_set_option", "prio3_engine_timing", "prio3_engine_timing_reset",
-    "prio3_client_generate_device",
+    "prio3_client_generate_device", "prio3_selftest_field",
 )
 
 _lib = None
@@ -116,8 +116,21 @@ def load_library() -> C.CDLL:
                                       P(C.c_uint64), C.c_int]
     L.prio3_engine_timing_reset.argtypes = [vp]
     L.prio3_engine_timing_reset.restype = None
+    L.prio3_selftest_field.argtypes = [C.c_int, C.c_uint32, vp, vp, vp]
     _lib = L
     return L
+
+
+def selftest_field(op: int, a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """Test hook: device Field128 primitive ``op`` over uint8 [m, 16] operands (see header)."""
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    n = a.shape[0] // (16 if op >= 4 else 1)
+    out = np.zeros((n, 16), np.uint8)
+    rc = load_library().prio3_selftest_field(op, n, _np_ptr(a), _np_ptr(b), _np_ptr(out))
+    if rc:
+        raise RuntimeError(f"prio3_selftest_field failed (rc={rc})")
+    return out
 
 
 # ------------------------------------------------------------------------------------
