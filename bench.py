@@ -127,9 +127,10 @@ def main():
 
     def step():
         s = torch.cuda.current_stream().cuda_stream
-        eng.prepare_device(data["nonces"], data["public_shares"], data["helper_shares"],
-                           data["leader_prep_shares"], prep_msgs, status, stream=s)
-        eng.accumulate_device(n, status, seg, None, 1, agg, cnt, stream=s)
+        eng.prepare_aggregate_device(data["nonces"], data["public_shares"], data["helper_shares"],
+                                     data["leader_prep_shares"], seg, 1, prep_msgs, status,
+                                     stream=s)
+        eng.aggregate_finish_device(status, None, agg, cnt, stream=s)
         if world > 1:
             dist.all_gather_into_tensor(g_agg, agg)
             dist.all_gather_into_tensor(g_cnt, cnt)

@@ -113,8 +113,9 @@ int prio3_debug_output_shares(prio3_batch* batch, uint8_t* out);
 void prio3_batch_free(prio3_batch* batch);
 
 /* ---- Device-resident entry points (buffers already in HBM; stream-ordered) ---- */
-/* d_* are device pointers with the same packed layouts; stream is a hipStream_t (NULL =
- * the engine's own stream).  Output shares remain in the engine workspace until the next
+/* d_* are device pointers with the same packed layouts; stream is a hipStream_t, ordered like
+ * any HIP call on it (NULL = the null stream, as in HIP itself -- so a caller whose inputs were
+ * produced on the null stream needs no extra synchronisation).  Output shares remain in the engine workspace until the next
  * prio3_device_prepare on this engine. */
 int prio3_device_prepare(prio3_engine* engine, uint32_t n, const uint8_t* d_nonces,
                          const uint8_t* d_public_shares, const uint8_t* d_helper_shares,
@@ -124,6 +125,22 @@ int prio3_device_accumulate(prio3_engine* engine, uint32_t n, const uint8_t* d_s
                             const uint32_t* d_segment_ids, const uint8_t* d_accept_mask,
                             uint32_t n_segments, uint8_t* d_agg_shares, uint64_t* d_counts,
                             void* stream);
+/* Prepare + aggregate in one pass.  Same as prio3_device_prepare, and additionally the output
+ * shares of the batch are summed per segment (d_segment_ids[n], NULL = all in segment 0;
+ * segment = batch identifier) while the measurement shares stream through the device
+ * (Histogram: fused into the joint-randomness kernel; other instances: deferred to the
+ * finish call).  prio3_device_aggregate_finish then applies the verdicts in d_status and
+ * the host's accept mask (reports Janus drops after preparation -- replays, collected
+ * batches: aggregation_job_writer.rs:540-588) and writes d_agg_shares[n_segments][agg_len]
+ * and d_counts[n_segments].  Equivalent to prio3_device_prepare + prio3_device_accumulate. */
+int prio3_device_prepare_aggregate(prio3_engine* engine, uint32_t n, const uint8_t* d_nonces,
+                                   const uint8_t* d_public_shares, const uint8_t* d_helper_shares,
+                                   const uint8_t* d_leader_prep_shares,
+                                   const uint32_t* d_segment_ids, uint32_t n_segments,
+                                   uint8_t* d_prep_msgs, uint8_t* d_status, void* stream);
+int prio3_device_aggregate_finish(prio3_engine* engine, const uint8_t* d_status,
+                                  const uint8_t* d_accept_mask, uint8_t* d_agg_shares,
+                                  uint64_t* d_counts, void* stream);
 /* Copies the output shares of the last device prepare (n x agg_share_len) to host. */
 int prio3_device_output_shares(prio3_engine* engine, uint32_t n, uint8_t* out);
 

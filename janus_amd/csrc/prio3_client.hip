@@ -384,7 +384,7 @@ extern "C" int prio3_client_generate_device(prio3_engine* e, uint32_t n, uint64_
   if (n == 0) return PRIO3_OK;
   std::lock_guard<std::mutex> lk(e->mu);
   if (hipSetDevice(e->device) != hipSuccess) return PRIO3_EDEVICE;
-  hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+  hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
   DevParams p = e->dp;
   const size_t es = p.es;
   const uint32_t A = p.arity, P = p.P;

@@ -44,6 +44,11 @@ struct Scratch {
   void* acc;
   void* out;
   void* beta;
+  // fused accumulate (prio3_device_prepare_aggregate): per-report segment ids (nullable),
+  // per-wave half-limb partial sums [wave][meas_len][8] and per-wave segment (~0 = not fused)
+  const uint32_t* seg;
+  uint32_t* wpart;
+  uint32_t* wseg;
 };
 
 struct OutPtrs {
@@ -294,6 +299,20 @@ struct prio3_engine {
   size_t partial_cap = 0;
   uint64_t* d_pcount = nullptr;
   uint8_t* d_mask = nullptr;
+  // fused accumulate state
+  uint32_t* d_wpart = nullptr;
+  uint32_t* d_wseg = nullptr;
+  size_t wpart_cap = 0;  // waves
+  unsigned long long* d_agg64 = nullptr;
+  unsigned long long* d_cpart = nullptr;  // per wave-chunk partials
+  uint32_t* d_cseg = nullptr;
+  size_t agg64_cap = 0;
+  uint32_t* d_fix = nullptr;  // [0] = count, then entries
+  size_t fix_cap = 0;
+  uint32_t fused_n = 0, fused_segments = 0;
+  int fused_on = 0;  // last prepare_aggregate used the fused kernels
+  const uint32_t* fused_seg_ptr = nullptr;
+  int fuse_acc = 1;  // option: fused accumulate on/off (A/B)
   // host-API staging
   uint32_t io_cap = 0;
   uint8_t *d_nonces = nullptr, *d_pub = nullptr, *d_helper = nullptr, *d_leader = nullptr,

@@ -689,3 +689,41 @@ DEV void msg_absorb_final(KState& s, Msg& m, int len) {
   for (int i = 0; i < 42; i++) kxor_word(s, i, m.w[i]);
   keccak_p12(s);
 }
+
+// -------------------------------------------------------------------------------------
+// Cross-lane aggregation for the fused accumulate: the 64 lanes' copies of two Field128
+// elements, split into 16-bit half-limbs (16 values per lane), are reduce-scattered over the
+// wave with a 4-stage DPP butterfly inside each row of 16 (row_mirror = xor 15,
+// row_half_mirror = xor 7, quad_perm xor 2, xor 1 -- each stage keeps the half of the vector
+// selected by one lane-id bit and adds the partner's matching half) and two cross-row adds
+// (ds_swizzle xor 16, ds_bpermute xor 32).  Lane l returns the wave total of slot l & 15:
+// element (l >> 3) & 1, half-limb l & 7 (weight 2^(16 (l & 7))); each total is < 2^22.
+// -------------------------------------------------------------------------------------
+template <int N, int CTRL, int BIT>
+DEV void halfsum_stage(uint32_t (&v)[16], uint32_t lane) {
+  const bool sel = (lane >> BIT) & 1;
+#pragma unroll
+  for (int i = 0; i < N / 2; i++) {
+    const uint32_t lo = v[i], hi = v[i + N / 2];
+    const uint32_t send = sel ? lo : hi, keep = sel ? hi : lo;
+    v[i] = keep + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)send, CTRL, 0xf, 0xf, false);
+  }
+}
+DEV uint32_t wave_halfsum2(const f128& x0, const f128& x1, uint32_t lane) {
+  uint32_t v[16];
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    v[2 * w] = x0.w[w] & 0xffffu;
+    v[2 * w + 1] = x0.w[w] >> 16;
+    v[8 + 2 * w] = x1.w[w] & 0xffffu;
+    v[8 + 2 * w + 1] = x1.w[w] >> 16;
+  }
+  halfsum_stage<16, 0x140, 3>(v, lane);  // row_mirror
+  halfsum_stage<8, 0x141, 2>(v, lane);   // row_half_mirror
+  halfsum_stage<4, 0x4E, 1>(v, lane);    // quad_perm [2,3,0,1]
+  halfsum_stage<2, 0xB1, 0>(v, lane);    // quad_perm [1,0,3,2]
+  uint32_t x = v[0];
+  x += (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);                 // xor 16
+  x += (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane ^ 32u) << 2), (int)x);  // xor 32
+  return x;
+}

@@ -258,8 +258,26 @@ __global__ __launch_bounds__(256, 4) void k_xof_a(DevParams p, InPtrs in, Scratc
 }
 
 // Field128 only (every joint-randomness Prio3 instance uses Field128).
+// FUSE: the measurement share streams through here anyway, so the (optimistic) per-segment
+// aggregate is accumulated on the way: every element of the share is summed over the wave's 64
+// reports by wave_halfsum2 and the wave's half-limb partials go to sc.wpart.  Only waves whose
+// 64 reports are all present and in one segment are fused (sc.wseg records which); the rest,
+// and every report the verdict or the host mask excludes, are fixed up in aggregate_finish.
+template <bool FUSE>
 __global__ __launch_bounds__(256, 4) void k_jrpart(DevParams p, InPtrs in, Scratch sc) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  bool fuse = false;
+  if constexpr (FUSE) {
+    const bool valid = r < p.n;
+    const uint32_t sg = valid ? (sc.seg ? sc.seg[r] : 0u) : 0xffffffffu;
+    const uint32_t s0 = (uint32_t)__shfl((int)sg, 0);
+    // a report flagged for the rejection-sampling slow path gets its share rewritten later:
+    // its wave is left to the fix-up pass
+    const bool flagged = valid && sc.flag[r];
+    fuse = __all(valid && sg == s0 && !flagged);
+    if (lane == 0 && (r - lane) < p.n) sc.wseg[r >> 6] = fuse ? s0 : 0xffffffffu;
+  }
   if (r >= p.n) return;
   const size_t ld = p.ld;
   const int M = (int)p.meas_len;
@@ -284,6 +302,14 @@ __global__ __launch_bounds__(256, 4) void k_jrpart(DevParams p, InPtrs in, Scrat
     return ok ? v : make_uint4(0, 0, 0, 0);
   };
   auto wsel = [](const uint4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; };
+  // wave totals of elements e0, e0+1 (zero outside [0, M)); lanes 0..15 store slot lane
+  auto fused_pair = [&](int e0, const uint4& a, const uint4& b) {
+    if (e0 + 1 < 0 || e0 >= M) return;  // wave-uniform
+    const uint32_t tot = wave_halfsum2(mk128(a.x, a.y, a.z, a.w), mk128(b.x, b.y, b.z, b.w), lane);
+    const int e = e0 + (int)((lane >> 3) & 1u);
+    if (lane < 16 && e >= 0 && e < M)
+      sc.wpart[((size_t)(r >> 6) * (uint32_t)M + (uint32_t)e) * 8u + (lane & 7u)] = tot;
+  };
   const uint32_t L = 42 + (uint32_t)M * 16;
   const uint32_t B = L / 168, rem = L % 168;
   KState s;
@@ -296,6 +322,10 @@ __global__ __launch_bounds__(256, 4) void k_jrpart(DevParams p, InPtrs in, Scrat
       uint4 E[11];
 #pragma unroll
       for (int t = 0; t < 11; t++) E[t] = ldel(q21 - 3 + t);
+      if (FUSE && fuse) {  // this window accounts for elements q21-2 .. q21+7 (E[1..10])
+#pragma unroll
+        for (int t = 1; t < 11; t += 2) fused_pair(q21 - 3 + t, E[t], E[t + 1]);
+      }
 #pragma unroll
       for (int j = 0; j < 42; j++) {
         const int u0 = j - 11 + 12, u1 = j - 10 + 12;  // +12 keeps the offsets non-negative
@@ -312,6 +342,11 @@ __global__ __launch_bounds__(256, 4) void k_jrpart(DevParams p, InPtrs in, Scrat
       uint4 E[12];
 #pragma unroll
       for (int t = 0; t < 12; t++) E[t] = ldel(q21 + 7 + t);
+      if (FUSE && fuse) {  // elements q21+8 .. q21+18 (E[1..11])
+#pragma unroll
+        for (int t = 1; t < 12; t += 2)
+          fused_pair(q21 + 7 + t, E[t], t + 1 < 12 ? E[t + 1] : make_uint4(0, 0, 0, 0));
+      }
 #pragma unroll
       for (int j = 0; j < 42; j++) {
         const int u0 = j + 3, u1 = j + 4;
@@ -1338,6 +1373,169 @@ __global__ void k_acc_final(uint32_t nchunks, uint32_t out_len, const void* part
   }
 }
 
+
+// ------------------------------------------------------------------------------------
+// Fused accumulate, second half: combine the per-wave half-limb partials per segment,
+// then fix up exclusions / non-fused reports and reduce mod p.
+// ------------------------------------------------------------------------------------
+// Level 1: grid (ceil(M*8/256), chunks of WCH waves): thread = slot (element, half).  A chunk
+// whose fused waves all carry one segment writes a 64-bit chunk partial (cseg[chunk] = its
+// segment); a chunk mixing segments adds each run with a 64-bit atomic into agg64 directly
+// (cseg = ~0, as for a chunk with no fused wave).
+constexpr uint32_t WCH = 32;
+__global__ __launch_bounds__(256) void k_agg_waves(uint32_t nwaves, uint32_t M,
+                                                   const uint32_t* wpart, const uint32_t* wseg,
+                                                   unsigned long long* cpart, uint32_t* cseg,
+                                                   unsigned long long* agg64) {
+  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x, c = blockIdx.y;
+  const uint32_t w0 = c * WCH, w1 = min(nwaves, w0 + WCH);
+  uint32_t s0 = 0xffffffffu;
+  bool mixed = false;
+  for (uint32_t w = w0; w < w1; w++) {  // uniform across the block (wseg is per wave)
+    const uint32_t sg = wseg[w];
+    if (sg == 0xffffffffu) continue;
+    if (s0 == 0xffffffffu) s0 = sg;
+    else if (sg != s0) mixed = true;
+  }
+  if (slot == 0 && blockIdx.x == 0) cseg[c] = mixed ? 0xffffffffu : s0;
+  if (slot >= M * 8 || s0 == 0xffffffffu) return;
+  if (!mixed) {
+    unsigned long long acc = 0;
+#pragma unroll 8
+    for (uint32_t w = w0; w < w1; w++)
+      if (wseg[w] != 0xffffffffu) acc += wpart[(size_t)w * M * 8 + slot];
+    cpart[(size_t)c * M * 8 + slot] = acc;
+    return;
+  }
+  unsigned long long acc = 0;
+  uint32_t cur = 0xffffffffu;
+  for (uint32_t w = w0; w < w1; w++) {
+    const uint32_t sg = wseg[w];
+    if (sg == 0xffffffffu) continue;
+    if (sg != cur) {
+      if (cur != 0xffffffffu && acc) atomicAdd(&agg64[(size_t)cur * M * 8 + slot], acc);
+      cur = sg;
+      acc = 0;
+    }
+    acc += wpart[(size_t)w * M * 8 + slot];
+  }
+  if (cur != 0xffffffffu && acc) atomicAdd(&agg64[(size_t)cur * M * 8 + slot], acc);
+}
+
+// Counts the reports the aggregate must contain (status FINISHED and accepted by the host
+// mask) per segment and lists every report whose fused inclusion differs (entry = r, or
+// r | 0x80000000 when it must be subtracted).  A block covers FIX_R consecutive reports and
+// keeps its counts in a small LDS table keyed by segment, flushed with one atomic per entry.
+constexpr uint32_t FIX_R = 4096, FIX_T = 64;
+__global__ __launch_bounds__(256) void k_agg_fix(uint32_t n, const uint8_t* status,
+                                                 const uint32_t* seg, const uint8_t* accept,
+                                                 const uint32_t* wseg, uint32_t* fix,
+                                                 uint32_t fix_cap, unsigned long long* counts) {
+  __shared__ uint32_t tseg[FIX_T];
+  __shared__ unsigned int tcnt[FIX_T];
+  if (threadIdx.x < FIX_T) {
+    tseg[threadIdx.x] = 0xffffffffu;
+    tcnt[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  const uint32_t lo = blockIdx.x * FIX_R, hi = min(n, lo + FIX_R);
+  for (uint32_t base = lo; base < hi; base += 256) {
+    const uint32_t r = base + threadIdx.x;
+    const bool valid = r < hi;
+    const uint32_t sg = valid ? (seg ? seg[r] : 0u) : 0xffffffffu;
+    const bool inc = valid && status[r] == PRIO3_STATUS_FINISHED && (!accept || accept[r]);
+    const bool fused = valid && wseg[r >> 6] != 0xffffffffu;
+    const uint32_t s0 = (uint32_t)__shfl((int)sg, 0);
+    const bool uni = __all(!valid || sg == s0);
+    const unsigned long long b = __ballot(inc);
+    auto add = [&](uint32_t s, unsigned int k) {
+      const uint32_t h = s % FIX_T;
+      const uint32_t old = atomicCAS(&tseg[h], 0xffffffffu, s);
+      if (old == 0xffffffffu || old == s) atomicAdd(&tcnt[h], k);
+      else atomicAdd(&counts[s], (unsigned long long)k);  // table collision
+    };
+    if (uni) {
+      if ((threadIdx.x & 63u) == 0 && b) add(s0, (unsigned int)__popcll(b));
+    } else if (inc) {
+      add(sg, 1u);
+    }
+    if (valid && fused != inc) {
+      const uint32_t i = atomicAdd(&fix[0], 1u);
+      if (i < fix_cap) fix[1 + i] = r | (inc ? 0u : 0x80000000u);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < FIX_T && tseg[threadIdx.x] != 0xffffffffu && tcnt[threadIdx.x])
+    atomicAdd(&counts[tseg[threadIdx.x]], (unsigned long long)tcnt[threadIdx.x]);
+}
+
+// One block per (segment, element): thread (half h = tid & 7, lane cl = tid >> 3) sums the chunk
+// partials of its segment for chunks cl, cl+32, ...; then the fix-up list is applied by all
+// 256 threads (lazily reduced signed sums), reduced through LDS, and thread 0 folds the
+// half-limb totals X = sum_h H_h 2^(16h) (H_h < 2^48) mod p.
+__global__ __launch_bounds__(256) void k_agg_final(uint32_t M, size_t ld,
+                                                   const unsigned long long* agg64,
+                                                   uint32_t nchunks,
+                                                   const unsigned long long* cpart,
+                                                   const uint32_t* cseg, const uint32_t* fix,
+                                                   const uint32_t* seg, const void* meas,
+                                                   uint8_t* agg) {
+  const uint32_t idx = blockIdx.x, s = idx / M, e = idx % M;
+  const uint32_t tid = threadIdx.x, h = tid & 7u, cl = tid >> 3;
+  __shared__ unsigned long long red[256];
+  __shared__ f128 fadd[256], fsub[256];
+  unsigned long long acc = 0;
+  for (uint32_t c = cl; c < nchunks; c += 32)
+    if (cseg[c] == s) acc += cpart[((size_t)c * M + e) * 8 + h];
+  red[tid] = acc;
+  // fix-up entries, strided over the block
+  f128 ad = zero128(), sb = zero128();
+  const uint32_t nfix = fix[0];
+  for (uint32_t i = tid; i < nfix; i += 256) {
+    const uint32_t ent = fix[1 + i], r = ent & 0x7fffffffu;
+    if ((seg ? seg[r] : 0u) != s) continue;
+    const f128 x = Fp128::load(meas, (size_t)e * ld + r);
+    if (ent & 0x80000000u) sb = add128(sb, x);
+    else ad = add128(ad, x);
+  }
+  fadd[tid] = ad;
+  fsub[tid] = sb;
+  __syncthreads();
+  for (uint32_t st = 128; st >= 8; st >>= 1) {
+    if (tid < st) red[tid] += red[tid + st];
+    __syncthreads();
+  }
+  for (uint32_t st = 128; st >= 1; st >>= 1) {
+    if (tid < st) {
+      fadd[tid] = add128(fadd[tid], fadd[tid + st]);
+      fsub[tid] = add128(fsub[tid], fsub[tid + st]);
+    }
+    __syncthreads();
+  }
+  if (tid != 0) return;
+  uint32_t w[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int hh = 0; hh < 8; hh++) {
+    const unsigned long long H = red[hh] + agg64[(size_t)idx * 8 + hh];
+    const int sh = 16 * hh, wi = sh >> 5, bi = sh & 31;
+    const unsigned long long lo = bi ? (H << 16) & 0xffffffffull : H & 0xffffffffull;
+    const unsigned long long mid = bi ? (H >> 16) & 0xffffffffull : H >> 32;
+    const unsigned long long hi = bi ? H >> 48 : 0ull;
+    unsigned long long c = (unsigned long long)w[wi] + lo;
+    w[wi] = (uint32_t)c;
+    c = (unsigned long long)w[wi + 1] + mid + (c >> 32);
+    w[wi + 1] = (uint32_t)c;
+    c = (unsigned long long)w[wi + 2] + hi + (c >> 32);
+    w[wi + 2] = (uint32_t)c;
+    for (int k = wi + 3; k < 9 && (c >> 32); k++) {
+      c = (unsigned long long)w[k] + (c >> 32);
+      w[k] = (uint32_t)c;
+    }
+  }
+  f128 v = red288(w, w[8]);
+  v = sub128(add128(v, fadd[0]), fsub[0]);
+  Fp128::store(agg, idx, v);
+}
+
 // sum of k partial aggregates (multi-GPU combine)
 template <class F>
 __global__ void k_combine(uint32_t k, uint32_t len, uint32_t n_segments, const uint8_t* in,
@@ -1648,7 +1846,8 @@ void prio3_engine_destroy(prio3_engine* e) {
   void* bufs[] = {e->sc.meas, e->sc.proofs, e->sc.jr, e->sc.qr, e->sc.part, e->sc.corrected,
                   e->sc.flag, e->sc.Lbuf, e->sc.PVbuf, e->sc.acc, e->sc.out, e->sc.beta, e->d_mask,
                   e->d_prep_partial, e->d_pcount, e->d_nonces, e->d_pub, e->d_helper,
-                  e->d_leader, e->d_msgs, e->d_status};
+                  e->d_leader, e->d_msgs, e->d_status, e->d_wpart, e->d_wseg, e->d_agg64,
+                  e->d_fix, e->d_cpart, e->d_cseg};
   for (auto b : bufs)
     if (b) (void)hipFree(b);
   for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
@@ -1660,6 +1859,10 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
   if (!e || !key) return PRIO3_EINVAL;
   if (!strcmp(key, "force_slow_path")) {
     e->force_slow = (int)value;
+    return PRIO3_OK;
+  }
+  if (!strcmp(key, "fuse_acc")) {
+    e->fuse_acc = (int)value;
     return PRIO3_OK;
   }
   if (!strcmp(key, "qh_regs")) {
@@ -1685,17 +1888,53 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
   return PRIO3_EINVAL;
 }
 
-int prio3_device_prepare(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
-                         const uint8_t* d_public_shares, const uint8_t* d_helper_shares,
-                         const uint8_t* d_leader_prep_shares, uint8_t* d_prep_msgs,
-                         uint8_t* d_status, void* stream) {
-  if (!e) return PRIO3_EINVAL;
-  if (n == 0) return PRIO3_OK;
-  std::lock_guard<std::mutex> lk(e->mu);
-  HIPCHK(hipSetDevice(e->device));
+// The fused accumulate applies where the output share is the measurement share (Histogram;
+// truncate is the identity) and the joint-rand kernel streams that share.
+static bool fusable(const prio3_engine* e) {
+  return e->fuse_acc && e->dp.kind == PRIO3_HISTOGRAM && e->dp.jr_len && e->split_xof;
+}
+
+static int ensure_fused(prio3_engine* e, uint32_t n, uint32_t n_segments) {
+  const size_t waves = (n + 63) / 64, M = e->dp.meas_len;
+  if (waves > e->wpart_cap) {
+    if (e->d_wpart) (void)hipFree(e->d_wpart);
+    if (e->d_wseg) (void)hipFree(e->d_wseg);
+    e->d_wpart = nullptr;
+    e->d_wseg = nullptr;
+    HIPCHK(hipMalloc((void**)&e->d_wpart, waves * M * 8 * sizeof(uint32_t)));
+    HIPCHK(hipMalloc((void**)&e->d_wseg, waves * sizeof(uint32_t)));
+    const size_t chunks = (waves + WCH - 1) / WCH;
+    if (e->d_cpart) (void)hipFree(e->d_cpart);
+    if (e->d_cseg) (void)hipFree(e->d_cseg);
+    HIPCHK(hipMalloc((void**)&e->d_cpart, chunks * M * 8 * 8));
+    HIPCHK(hipMalloc((void**)&e->d_cseg, chunks * sizeof(uint32_t)));
+    e->wpart_cap = waves;
+  }
+  if ((size_t)n_segments * M * 8 > e->agg64_cap) {
+    if (e->d_agg64) (void)hipFree(e->d_agg64);
+    e->d_agg64 = nullptr;
+    HIPCHK(hipMalloc((void**)&e->d_agg64, (size_t)n_segments * M * 8 * 8));
+    e->agg64_cap = (size_t)n_segments * M * 8;
+  }
+  if ((size_t)n + 1 > e->fix_cap) {
+    if (e->d_fix) (void)hipFree(e->d_fix);
+    e->d_fix = nullptr;
+    HIPCHK(hipMalloc((void**)&e->d_fix, ((size_t)n + 1) * sizeof(uint32_t)));
+    e->fix_cap = (size_t)n + 1;
+  }
+  return PRIO3_OK;
+}
+
+static int prepare_impl(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
+                        const uint8_t* d_public_shares, const uint8_t* d_helper_shares,
+                        const uint8_t* d_leader_prep_shares, uint8_t* d_prep_msgs,
+                        uint8_t* d_status, hipStream_t st, const uint32_t* d_seg, bool fuse) {
   int rc = ensure_scratch(e, n);
   if (rc) return rc;
-  hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+  Scratch sc = e->sc;
+  sc.seg = d_seg;
+  sc.wpart = e->d_wpart;
+  sc.wseg = e->d_wseg;
   DevParams dp = e->dp;
   dp.n = n;
   dp.force_slow = (uint32_t)e->force_slow;
@@ -1705,7 +1944,10 @@ int prio3_device_prepare(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
   if (dp.es == 16) {
     if (dp.jr_len && e->split_xof) {
       TIMED(e, st, "k_xof_a", (k_xof_a<Fp128><<<blocks, 256, 0, st>>>(dp, in, e->sc)));
-      TIMED(e, st, "k_jrpart", (k_jrpart<<<blocks, 256, 0, st>>>(dp, in, e->sc)));
+      if (fuse)
+        TIMED(e, st, "k_jrpart", (k_jrpart<true><<<blocks, 256, 0, st>>>(dp, in, sc)));
+      else
+        TIMED(e, st, "k_jrpart", (k_jrpart<false><<<blocks, 256, 0, st>>>(dp, in, sc)));
     } else {
       TIMED(e, st, "k_xof", (k_xof<Fp128><<<blocks, 256, 0, st>>>(dp, in, e->sc)));
     }
@@ -1736,6 +1978,82 @@ int prio3_device_prepare(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
   return PRIO3_OK;
 }
 
+int prio3_device_prepare(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
+                         const uint8_t* d_public_shares, const uint8_t* d_helper_shares,
+                         const uint8_t* d_leader_prep_shares, uint8_t* d_prep_msgs,
+                         uint8_t* d_status, void* stream) {
+  if (!e) return PRIO3_EINVAL;
+  if (n == 0) return PRIO3_OK;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
+  e->fused_on = 0;
+  return prepare_impl(e, n, d_nonces, d_public_shares, d_helper_shares, d_leader_prep_shares,
+                      d_prep_msgs, d_status, st, nullptr, false);
+}
+
+int prio3_device_prepare_aggregate(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
+                                   const uint8_t* d_public_shares, const uint8_t* d_helper_shares,
+                                   const uint8_t* d_leader_prep_shares,
+                                   const uint32_t* d_segment_ids, uint32_t n_segments,
+                                   uint8_t* d_prep_msgs, uint8_t* d_status, void* stream) {
+  if (!e || n_segments == 0) return PRIO3_EINVAL;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
+  e->fused_n = n;
+  e->fused_segments = n_segments;
+  e->fused_seg_ptr = d_segment_ids;
+  e->fused_on = 0;
+  if (n == 0) return PRIO3_OK;
+  const bool fuse = fusable(e);
+  if (fuse) {
+    int rc = ensure_fused(e, n, n_segments);
+    if (rc) return rc;
+  }
+  int rc = prepare_impl(e, n, d_nonces, d_public_shares, d_helper_shares, d_leader_prep_shares,
+                        d_prep_msgs, d_status, st, d_segment_ids, fuse);
+  if (rc == PRIO3_OK) e->fused_on = fuse;
+  return rc;
+}
+
+int prio3_device_accumulate(prio3_engine* e, uint32_t n, const uint8_t* d_status,
+                            const uint32_t* d_segment_ids, const uint8_t* d_accept_mask,
+                            uint32_t n_segments, uint8_t* d_agg_shares, uint64_t* d_counts,
+                            void* stream);
+
+int prio3_device_aggregate_finish(prio3_engine* e, const uint8_t* d_status,
+                                  const uint8_t* d_accept_mask, uint8_t* d_agg_shares,
+                                  uint64_t* d_counts, void* stream) {
+  if (!e) return PRIO3_EINVAL;
+  if (!e->fused_on)  // not fusable (or nothing prepared): the classic masked reduction
+    return prio3_device_accumulate(e, e->fused_n, d_status, e->fused_seg_ptr, d_accept_mask,
+                                   e->fused_segments, d_agg_shares, d_counts, stream);
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
+  const uint32_t n = e->fused_n, S = e->fused_segments, M = e->dp.meas_len;
+  const uint32_t nwaves = (n + 63) / 64;
+  HIPCHK(hipMemsetAsync(e->d_agg64, 0, (size_t)S * M * 8 * 8, st));
+  HIPCHK(hipMemsetAsync(e->d_fix, 0, sizeof(uint32_t), st));
+  HIPCHK(hipMemsetAsync(d_counts, 0, 8 * (size_t)S, st));
+  const uint32_t nchunks = (nwaves + WCH - 1) / WCH;
+  dim3 g1((M * 8 + 255) / 256, nchunks);
+  TIMED(e, st, "k_agg_waves",
+        (k_agg_waves<<<g1, 256, 0, st>>>(nwaves, M, e->d_wpart, e->d_wseg, e->d_cpart, e->d_cseg,
+                                         e->d_agg64)));
+  TIMED(e, st, "k_agg_fix",
+        (k_agg_fix<<<(n + FIX_R - 1) / FIX_R, 256, 0, st>>>(
+            n, d_status, e->fused_seg_ptr, d_accept_mask, e->d_wseg, e->d_fix,
+            (uint32_t)(e->fix_cap - 1), (unsigned long long*)d_counts)));
+  TIMED(e, st, "k_agg_final",
+        (k_agg_final<<<S * M, 256, 0, st>>>(M, e->dp.ld, e->d_agg64, nchunks,
+                                                          e->d_cpart, e->d_cseg, e->d_fix,
+                                                          e->fused_seg_ptr, e->sc.meas,
+                                                          d_agg_shares)));
+  return PRIO3_OK;
+}
+
 int prio3_device_accumulate(prio3_engine* e, uint32_t n, const uint8_t* d_status,
                             const uint32_t* d_segment_ids, const uint8_t* d_accept_mask,
                             uint32_t n_segments, uint8_t* d_agg_shares, uint64_t* d_counts,
@@ -1743,7 +2061,7 @@ int prio3_device_accumulate(prio3_engine* e, uint32_t n, const uint8_t* d_status
   if (!e || n_segments == 0) return PRIO3_EINVAL;
   std::lock_guard<std::mutex> lk(e->mu);
   HIPCHK(hipSetDevice(e->device));
-  hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+  hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
   const DevParams& d = e->dp;
   const size_t agg_len = (size_t)d.out_len * d.es;
   if (n == 0) {
@@ -1795,7 +2113,7 @@ int prio3_device_combine(prio3_engine* e, uint32_t k, uint32_t n_segments, const
   if (!e || k == 0) return PRIO3_EINVAL;
   std::lock_guard<std::mutex> lk(e->mu);
   HIPCHK(hipSetDevice(e->device));
-  hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+  hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
   const DevParams& d = e->dp;
   uint32_t len = d.out_len * n_segments;
   uint32_t threads = len > n_segments ? len : n_segments;
@@ -1872,7 +2190,7 @@ int prio3_helper_prepare_batch(prio3_engine* e, uint32_t n, const uint8_t* nonce
     }
   }
   int rc = prio3_device_prepare(e, n, e->d_nonces, e->d_pub, e->d_helper, e->d_leader, e->d_msgs,
-                                e->d_status, nullptr);
+                                e->d_status, e->stream);
   if (rc) return rc;
   {
     std::lock_guard<std::mutex> lk(e->mu);
@@ -1915,7 +2233,7 @@ int prio3_accumulate(prio3_batch* b, const uint32_t* segment_ids, const uint8_t*
   HIPCHK(hipMalloc((void**)&d_agg, agg_len * n_segments));
   HIPCHK(hipMalloc((void**)&d_cnt, 8 * (size_t)n_segments));
   int rc = prio3_device_accumulate(e, n, e->d_status, d_seg, d_acc, n_segments, d_agg, d_cnt,
-                                   nullptr);
+                                   e->stream);
   if (rc == PRIO3_OK) {
     HIPCHK(hipMemcpyAsync(agg_shares_out, d_agg, agg_len * n_segments, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(counts_out, d_cnt, 8 * (size_t)n_segments, hipMemcpyDeviceToHost, st));

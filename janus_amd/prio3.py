@@ -72,7 +72,8 @@ EXPORTED_SYMBOLS = (
     "prio3_accumulate", "prio3_debug_output_shares", "prio3_batch_free", "prio3_device_prepare",
     "prio3_device_accumulate", "prio3_device_output_shares", "prio3_device_combine",
     "prio3_engine_set_option", "prio3_engine_timing", "prio3_engine_timing_reset",
-    "prio3_client_generate_device", "prio3_selftest_field",
+    "prio3_client_generate_device", "prio3_selftest_field", "prio3_device_prepare_aggregate",
+    "prio3_device_aggregate_finish",
 )
 
 _lib = None
@@ -117,6 +118,9 @@ def load_library() -> C.CDLL:
     L.prio3_engine_timing_reset.argtypes = [vp]
     L.prio3_engine_timing_reset.restype = None
     L.prio3_selftest_field.argtypes = [C.c_int, C.c_uint32, vp, vp, vp]
+    L.prio3_device_prepare_aggregate.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, vp, C.c_uint32,
+                                                 vp, vp, vp]
+    L.prio3_device_aggregate_finish.argtypes = [vp, vp, vp, vp, vp, vp]
     _lib = L
     return L
 
@@ -177,6 +181,16 @@ def _np_ptr(a: Optional[np.ndarray]):
 
 def _tptr(t):
     return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream(stream, device):
+    """Device-resident calls default to torch's current stream on the engine's device, so they
+    are ordered after the torch ops that produced their inputs (a handle of 0 is HIP's null
+    stream, which the C-ABI takes as such)."""
+    if stream:
+        return C.c_void_p(stream)
+    import torch
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream or None)
 
 
 class PreparedBatch:
@@ -284,15 +298,32 @@ class HelperEngine:
         rc = load_library().prio3_device_prepare(
             self.handle, nonces.shape[0], _tptr(nonces), _tptr(public_shares),
             _tptr(helper_shares), _tptr(leader_prep_shares), _tptr(prep_msgs), _tptr(status),
-            C.c_void_p(stream) if stream else None)
+            _stream(stream, self.device))
         if rc:
             raise RuntimeError(f"prio3_device_prepare failed (rc={rc})")
+
+    def prepare_aggregate_device(self, nonces, public_shares, helper_shares, leader_prep_shares,
+                                 segment_ids, n_segments, prep_msgs, status, stream=None) -> None:
+        """Prepare and aggregate in one pass (torch tensors on this engine's GPU)."""
+        rc = load_library().prio3_device_prepare_aggregate(
+            self.handle, nonces.shape[0], _tptr(nonces), _tptr(public_shares),
+            _tptr(helper_shares), _tptr(leader_prep_shares), _tptr(segment_ids), n_segments,
+            _tptr(prep_msgs), _tptr(status), _stream(stream, self.device))
+        if rc:
+            raise RuntimeError(f"prio3_device_prepare_aggregate failed (rc={rc})")
+
+    def aggregate_finish_device(self, status, accept_mask, agg, counts, stream=None) -> None:
+        rc = load_library().prio3_device_aggregate_finish(
+            self.handle, _tptr(status), _tptr(accept_mask), _tptr(agg), _tptr(counts),
+            _stream(stream, self.device))
+        if rc:
+            raise RuntimeError(f"prio3_device_aggregate_finish failed (rc={rc})")
 
     def accumulate_device(self, n, status, segment_ids, accept_mask, n_segments, agg, counts,
                           stream=None) -> None:
         rc = load_library().prio3_device_accumulate(
             self.handle, n, _tptr(status), _tptr(segment_ids), _tptr(accept_mask), n_segments,
-            _tptr(agg), _tptr(counts), C.c_void_p(stream) if stream else None)
+            _tptr(agg), _tptr(counts), _stream(stream, self.device))
         if rc:
             raise RuntimeError(f"prio3_device_accumulate failed (rc={rc})")
 
@@ -300,7 +331,7 @@ class HelperEngine:
                        stream=None) -> None:
         rc = load_library().prio3_device_combine(
             self.handle, k, n_segments, _tptr(parts), _tptr(part_counts), _tptr(out),
-            _tptr(out_counts), C.c_void_p(stream) if stream else None)
+            _tptr(out_counts), _stream(stream, self.device))
         if rc:
             raise RuntimeError(f"prio3_device_combine failed (rc={rc})")
 
@@ -336,7 +367,7 @@ class HelperEngine:
             _tptr(out["public_shares"]) if sz.public_share_len else None,
             _tptr(out["helper_shares"]), _tptr(out["leader_prep_shares"]),
             _tptr(out.get("measurements")), _tptr(out.get("leader_out_shares")),
-            _tptr(out.get("flags")), C.c_void_p(stream) if stream else None)
+            _tptr(out.get("flags")), _stream(stream, self.device))
         if rc:
             raise RuntimeError(f"prio3_client_generate_device failed (rc={rc})")
         if not sz.public_share_len:

@@ -1,0 +1,95 @@
+"""GPU parity of the one-pass prepare + aggregate entry points
+(prio3_device_prepare_aggregate / prio3_device_aggregate_finish) against the CPU restatement.
+
+The Histogram path sums the output shares inside the joint-randomness kernel, one wave of 64
+reports at a time, and then fixes up every report it must not have counted (decide failures,
+host-rejected reports, flagged slow-path reports) and every report it could not fuse (waves
+spanning two segments, the ragged last wave).  These cases are exercised here; the expected
+aggregate is the oracle's Janus-structured batch aggregate (aggregation_job_writer.rs:591-695).
+"""
+import numpy as np
+import pytest
+
+from tests.conftest import CONFIGS
+from tests.test_gpu_parity import VK, _engine, _oracle, _tamper
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(cfg, n, seed, n_segments=1, seg_mode="runs", tamper=True, accept_frac=0.9,
+         force_slow=False, fuse=True):
+    import torch
+    o = _oracle(cfg)
+    eng = _engine(cfg)
+    eng.set_option("fuse_acc", int(fuse))
+    if force_slow:
+        eng.set_option("force_slow_path", 1)
+    d = o.gen_reports(VK, n, seed=seed, n_threads=8)
+    rng = np.random.default_rng(seed)
+    if tamper:
+        d = _tamper(o, d, rng)
+    if seg_mode == "runs":  # contiguous batches whose boundaries fall inside waves
+        cuts = np.sort(rng.choice(np.arange(1, n), n_segments - 1, replace=False)) if n_segments > 1 else []
+        seg = np.zeros(n, np.uint32)
+        for c in cuts:
+            seg[c:] += 1
+    else:
+        seg = rng.integers(0, n_segments, n).astype(np.uint32)
+    accept = (rng.random(n) < accept_frac).astype(np.uint8)
+    ref_msgs, ref_status, ref_agg, ref_cnt = o.helper_batch(
+        VK, d["nonces"], d["public_shares"], d["helper_shares"], d["leader_prep_shares"],
+        segment_ids=seg, accept_mask=accept, n_segments=n_segments, n_threads=8)
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    sz = eng.sz
+    msgs = torch.zeros((n, max(sz.prep_msg_len, 1)), dtype=torch.uint8, device=dev)
+    status = torch.zeros(n, dtype=torch.uint8, device=dev)
+    agg = torch.zeros((n_segments, sz.agg_share_len), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(n_segments, dtype=torch.int64, device=dev)
+    pub = t(d["public_shares"]) if sz.public_share_len else None
+    eng.prepare_aggregate_device(t(d["nonces"]), pub, t(d["helper_shares"]),
+                                 t(d["leader_prep_shares"]), t(seg), n_segments, msgs, status)
+    eng.aggregate_finish_device(status, t(accept), agg, cnt)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(status.cpu().numpy(), ref_status)
+    np.testing.assert_array_equal(msgs.cpu().numpy()[:, :sz.prep_msg_len], ref_msgs)
+    np.testing.assert_array_equal(cnt.cpu().numpy().astype(np.uint64), ref_cnt)
+    np.testing.assert_array_equal(agg.cpu().numpy(), ref_agg)
+    return ref_status
+
+
+def test_fused_single_segment_all_accepted():
+    _run(CONFIGS["hist_256_c16"], 1024, seed=1, tamper=False, accept_frac=1.0)
+
+
+def test_fused_tampered_and_masked():
+    st = _run(CONFIGS["hist_256_c16"], 1000, seed=2)
+    assert (st != 0).any()
+
+
+def test_fused_segment_runs_inside_waves():
+    _run(CONFIGS["hist_256_c16"], 1500, seed=3, n_segments=7, seg_mode="runs")
+
+
+def test_fused_random_segments():
+    """Every wave spans several segments: nothing fuses, all goes through the fix-up pass."""
+    _run(CONFIGS["hist_256_c16"], 600, seed=4, n_segments=4, seg_mode="random")
+
+
+def test_fused_ragged_tail_and_small_histogram():
+    _run(CONFIGS["hist_10_c3"], 200, seed=5, n_segments=2)
+    _run(CONFIGS["hist_100_c10"], 131, seed=6)
+
+
+def test_fused_slow_path_flags():
+    _run(CONFIGS["hist_256_c16"], 192, seed=7, force_slow=True)
+
+
+@pytest.mark.parametrize("name", ["count", "sum8", "sumvec_8x10_c9"])
+def test_prepare_aggregate_other_instances(name):
+    """Instances without the fused kernel take the deferred masked reduction."""
+    _run(CONFIGS[name], 700, seed=8, n_segments=3)
+
+
+def test_fused_off_matches():
+    _run(CONFIGS["hist_256_c16"], 700, seed=9, n_segments=2, fuse=False)

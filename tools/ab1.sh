@@ -1,7 +1,7 @@
 # GPU A/B helper: field self-test + parity suite, then bench variants given as arguments
 # (each argument is one space-separated list of --opt key=value settings; "" = defaults).
 set -e
-timeout -k 10 300 python -u -m pytest tests/test_field_asm.py tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ab1_tests.log 2>&1 || { tail -30 gpurun_out/ab1_tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_field_asm.py tests/test_gpu_fused.py tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ab1_tests.log 2>&1 || { tail -30 gpurun_out/ab1_tests.log; exit 1; }
 tail -2 gpurun_out/ab1_tests.log
 for v in "$@"; do
   opts=""; for kv in $v; do opts="$opts --opt $kv"; done
