@@ -119,11 +119,13 @@ def main():
     seg = torch.zeros(n, dtype=torch.int32, device=dev)
     agg = torch.zeros((1, sz.agg_share_len), dtype=torch.uint8, device=dev)
     cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    combiner = None
     if world > 1:
-        g_agg = torch.empty((world, sz.agg_share_len), dtype=torch.uint8, device=dev)
-        g_cnt = torch.empty((world,), dtype=torch.int64, device=dev)
-        fin_agg = torch.empty((1, sz.agg_share_len), dtype=torch.uint8, device=dev)
-        fin_cnt = torch.empty(1, dtype=torch.int64, device=dev)
+        from janus_amd.dist import AggregateCombiner
+        combiner = AggregateCombiner(
+            dist, agg, cnt,
+            lambda k, ga, gc, oa, oc: eng.combine_device(k, 1, ga, gc, oa, oc,
+                                                         stream=torch.cuda.current_stream().cuda_stream))
 
     def step():
         s = torch.cuda.current_stream().cuda_stream
@@ -131,10 +133,8 @@ def main():
                                      data["leader_prep_shares"], seg, 1, prep_msgs, status,
                                      stream=s)
         eng.aggregate_finish_device(status, None, agg, cnt, stream=s)
-        if world > 1:
-            dist.all_gather_into_tensor(g_agg, agg)
-            dist.all_gather_into_tensor(g_cnt, cnt)
-            eng.combine_device(world, 1, g_agg, g_cnt, fin_agg, fin_cnt, stream=s)
+        if combiner is not None:
+            combiner(agg, cnt)
 
     for _ in range(args.warmup):
         step()
@@ -159,7 +159,7 @@ def main():
         elapsed = float(t.item())
 
     ok = int((status == 0).sum().item())
-    final_cnt = int((fin_cnt if world > 1 else cnt)[0].item())
+    final_cnt = int((combiner.out_cnt if combiner is not None else cnt)[0].item())
     value = world * n * args.steps / elapsed
 
     # roofline of the dominant kernel, from the live HIP-event times on the launch stream
