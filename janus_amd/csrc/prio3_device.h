@@ -652,8 +652,11 @@ DEV void keccak_round(KState& a, uint32_t rc_lo, uint32_t rc_hi) {
   a.hi[0] ^= rc_hi;
 }
 
+#ifndef KECCAK_UNROLL
+#define KECCAK_UNROLL 2
+#endif
 DEV void keccak_p12(KState& a) {
-#pragma unroll 2
+#pragma unroll KECCAK_UNROLL
   for (int r = 0; r < 12; r++) keccak_round(a, KRC_LO[r], KRC_HI[r]);
 }
 

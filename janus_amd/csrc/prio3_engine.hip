@@ -198,7 +198,13 @@ __global__ __launch_bounds__(256) void k_xof(DevParams p, InPtrs in, Scratch sc)
 //             coalesced 16-byte loads + 42 v_alignbit.
 // ------------------------------------------------------------------------------------
 template <class F>
-__global__ __launch_bounds__(256, 4) void k_xof_a(DevParams p, InPtrs in, Scratch sc) {
+#ifndef XOF_OCC
+#define XOF_OCC 4
+#endif
+#ifndef JR_OCC
+#define JR_OCC 4
+#endif
+__global__ __launch_bounds__(256, XOF_OCC) void k_xof_a(DevParams p, InPtrs in, Scratch sc) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= p.n) return;
   constexpr uint32_t ES = F::ES;
@@ -264,7 +270,7 @@ __global__ __launch_bounds__(256, 4) void k_xof_a(DevParams p, InPtrs in, Scratc
 // 64 reports are all present and in one segment are fused (sc.wseg records which); the rest,
 // and every report the verdict or the host mask excludes, are fixed up in aggregate_finish.
 template <bool FUSE>
-__global__ __launch_bounds__(256, 4) void k_jrpart(DevParams p, InPtrs in, Scratch sc) {
+__global__ __launch_bounds__(256, JR_OCC) void k_jrpart(DevParams p, InPtrs in, Scratch sc) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
   bool fuse = false;

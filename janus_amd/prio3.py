@@ -23,7 +23,9 @@ from typing import Optional
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libjanus_prio3.so")
+# JANUS_PRIO3_LIB selects an alternative build of the same sources (A/B experiments,
+# tools/build_variant.sh); the default is the in-tree library built by `make -C janus_amd`.
+LIB_PATH = os.environ.get("JANUS_PRIO3_LIB") or os.path.join(_HERE, "libjanus_prio3.so")
 
 PRIO3_COUNT, PRIO3_SUM, PRIO3_SUMVEC, PRIO3_HISTOGRAM = 0, 1, 2, 3
 

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Builds an A/B variant of the engine with extra compile-time definitions, e.g.
+#   bash tools/build_variant.sh ku4 -DKECCAK_UNROLL=4
+# -> janus_amd/variants/libjanus_prio3_ku4.so (select with JANUS_PRIO3_LIB=...).
+set -e
+TAG=$1; shift
+R=$(cd "$(dirname "$0")/.." && pwd)
+OUT=$R/janus_amd/variants/$TAG
+mkdir -p $OUT
+for f in prio3_engine prio3_client; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function "$@" \
+    -c -o $OUT/$f.o $R/janus_amd/csrc/$f.hip &
+done
+wait
+/opt/rocm/bin/hipcc -O3 -fPIC --offload-arch=gfx950 -shared -o $R/janus_amd/variants/libjanus_prio3_$TAG.so $OUT/prio3_engine.o $OUT/prio3_client.o
+rm -rf $OUT
+echo built janus_amd/variants/libjanus_prio3_$TAG.so

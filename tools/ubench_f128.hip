@@ -64,6 +64,36 @@ __global__ void k_redasm(uint32_t* out, uint32_t s) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
 }
 
+// Keccak-p[1600,12]: PERMS permutations per work-item, no memory traffic
+#define PERMS 16
+__global__ __launch_bounds__(256) void k_keccak(uint32_t* out, uint32_t s) {
+  KState st;
+  for (int i = 0; i < 25; i++) {
+    st.lo[i] = s * (i + 1) ^ threadIdx.x;
+    st.hi[i] = s + i;
+  }
+  for (int it = 0; it < PERMS; it++) keccak_p12(st);
+  uint32_t acc = 0;
+  for (int i = 0; i < 25; i++) acc ^= st.lo[i] ^ st.hi[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+__global__ __launch_bounds__(256) void k_keccak2(uint32_t* out, uint32_t s) {  // 2 states / lane
+  KState a, b;
+  for (int i = 0; i < 25; i++) {
+    a.lo[i] = s * (i + 1) ^ threadIdx.x;
+    a.hi[i] = s + i;
+    b.lo[i] = s * (i + 3) ^ threadIdx.x;
+    b.hi[i] = s + 2 * i;
+  }
+  for (int it = 0; it < PERMS / 2; it++) {
+    keccak_p12(a);
+    keccak_p12(b);
+  }
+  uint32_t acc = 0;
+  for (int i = 0; i < 25; i++) acc ^= a.lo[i] ^ a.hi[i] ^ b.lo[i] ^ b.hi[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
 template <typename K>
 void run(const char* name, K kern, uint32_t* buf, int w, double ops_per_thread, double valu_per_op) {
   int threads = 256, blocks = 256 * w;
@@ -92,6 +122,8 @@ int main() {
     run("mul128_asm", k_mula, buf, w, ITER / 4, 80);
     run("mul128_asm (2 chains)", k_mula2, buf, w, ITER / 4, 80);
     run("mac_reduce_f", k_redasm, buf, w, ITER / 4, 70);
+    run("keccak_p12", k_keccak, buf, w, PERMS, 12 * 190);
+    run("keccak_p12 (2 states)", k_keccak2, buf, w, PERMS, 12 * 190);
   }
   return 0;
 }
