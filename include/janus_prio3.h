@@ -49,6 +49,8 @@ enum {
   PRIO3_STATUS_PREP_MSG = 3,          /* VdafPrepareSharesToPrepareMessage (decide failed) */
   PRIO3_STATUS_PREP_NEXT = 4,         /* VdafPrepareNext (joint randomness mismatch) */
   PRIO3_STATUS_PEER_MISMATCH = 5,     /* PeerMessageMismatch (set by the host framing layer) */
+  PRIO3_STATUS_INPUT_SHARE_DECODE = 6, /* leader: input share not canonical -> PrepareError::
+                                          InvalidMessage (aggregation_job_driver.rs:397-415) */
 };
 
 /* Whole-call return codes. */
@@ -76,6 +78,7 @@ typedef struct {
   uint32_t prep_share_len;    /* leader PrepareShare bytes (verifiers || jr part) */
   uint32_t prep_msg_len;      /* 16 with joint randomness, else 0 */
   uint32_t agg_share_len;     /* out_len * field_bytes */
+  uint32_t leader_input_share_len; /* enc(meas share) || enc(proofs share) [|| k_blind] */
 } prio3_sizes_t;
 
 typedef struct prio3_engine prio3_engine;
@@ -150,6 +153,29 @@ int prio3_device_output_shares(prio3_engine* engine, uint32_t n, uint8_t* out);
 int prio3_device_combine(prio3_engine* engine, uint32_t k, uint32_t n_segments,
                          const uint8_t* d_in, const uint64_t* d_counts_in, uint8_t* d_out,
                          uint64_t* d_counts_out, void* stream);
+
+/* ---- Leader side ---- */
+/* The leader's half of the same VDAF on the same engine: prio Prio3::prepare_init with
+ * agg_id 0 on the explicit leader input shares (what PingPongTopology::leader_initialized
+ * runs for each report in AggregationJobDriver::step_aggregation_job_aggregate_init,
+ * /root/reference/aggregator/src/aggregator/aggregation_job_driver.rs:397-415), producing the
+ * leader prepare shares that go into PingPongMessage::Initialize; then prepare_next on the
+ * helper's prepare messages (leader_continued in process_response_from_helper, :677-691):
+ * status becomes PREP_NEXT when the message is not the leader's joint-rand seed, and the
+ * output shares stay on the device for prio3_accumulate / prio3_device_accumulate.
+ * leader_input_shares[n][leader_input_share_len]; prep_shares_out[n][prep_share_len]. */
+int prio3_leader_prepare_init_batch(prio3_engine* engine, uint32_t n, const uint8_t* nonces,
+                                    const uint8_t* public_shares,
+                                    const uint8_t* leader_input_shares, uint8_t* prep_shares_out,
+                                    uint8_t* status_out, prio3_batch** batch_out);
+int prio3_leader_prepare_next_batch(prio3_batch* batch, const uint8_t* prep_msgs,
+                                    uint8_t* status_inout);
+int prio3_device_leader_prepare_init(prio3_engine* engine, uint32_t n, const uint8_t* d_nonces,
+                                     const uint8_t* d_public_shares,
+                                     const uint8_t* d_leader_input_shares, uint8_t* d_prep_shares,
+                                     uint8_t* d_status, void* stream);
+int prio3_device_leader_prepare_next(prio3_engine* engine, uint32_t n, const uint8_t* d_prep_msgs,
+                                     uint8_t* d_status, void* stream);
 
 /* ---- Synthetic client (benchmarks and tests) ---- */
 /* Generates n honest reports on the device: the client's shard (prio Prio3::shard,

@@ -1,4 +1,5 @@
-// prio3_client.hip -- on-device synthetic report generator: the client's Prio3 shard
+// prio3_client.hip -- leader-side preparation (k_leader_init / k_leader_next, below) and the
+// on-device synthetic report generator: the client's Prio3 shard
 // (VDAF-08 7.2.1, prio Prio3::shard) followed by the leader's prepare_init (agg_id 0), so
 // that benchmarks and full-size tests get honest, distinct reports at HBM speed without a
 // CPU in the loop.  Report i is derived from (seed, i) exactly like the oracle's
@@ -366,6 +367,151 @@ __global__ __launch_bounds__(64) void k_gen(DevParams p, uint64_t seed, uint64_t
       goto done;                                                                      \
     }                                                                                 \
   } while (0)
+
+
+// ------------------------------------------------------------------------------------
+// Leader-side preparation: prio Prio3::prepare_init with agg_id 0 on the
+// explicit leader input share, as Janus's leader calls it through
+// PingPongTopology::leader_initialized (aggregation_job_driver.rs:397-415), and prepare_next on
+// the helper's prepare message (leader_continued, aggregation_job_driver.rs:677-691).
+// One report per lane with the generic lane helpers (the leader's own input share is in
+// HBM, so the share XOF of the helper path does not exist here).
+// ------------------------------------------------------------------------------------
+template <class F>
+__global__ __launch_bounds__(64) void k_leader_init(DevParams p, const uint8_t* nonces,
+                                                    const uint8_t* pub, const uint8_t* lshares,
+                                                    Scratch sc, uint8_t* prep_shares,
+                                                    uint8_t* status) {
+  typedef typename F::T T;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= p.n) return;
+  const size_t ld = p.ld;
+  const uint32_t M = p.meas_len, PL = p.proof_len, A = p.arity;
+  const bool JR = p.jr_len > 0;
+  uint8_t st = PRIO3_STATUS_FINISHED;
+  uint32_t flag = p.force_slow;
+  // decode the explicit shares into SoA scratch (canonical elements only)
+  const uint8_t* ls = lshares + (size_t)r * p.leader_share_len;
+  bool ok = true;
+  for (uint32_t e = 0; e < M; e++) {
+    const T x = F::load(ls, e);
+    ok = ok && F::lt_p(x);
+    F::store(sc.meas, (size_t)e * ld + r, x);
+  }
+  for (uint32_t e = 0; e < PL; e++) {
+    const T x = F::load(ls + (size_t)M * F::ES, e);
+    ok = ok && F::lt_p(x);
+    F::store(sc.proofs, (size_t)e * ld + r, x);
+  }
+  if (!ok) st = PRIO3_STATUS_INPUT_SHARE_DECODE;
+  uint32_t nonce[4];
+  load16(nonces + 16 * (size_t)r, nonce);
+  // query randomness
+  {
+    const uint8_t b1[1] = {1};
+    uint32_t vk[4] = {p.vk[0], p.vk[1], p.vk[2], p.vk[3]};
+    KState s;
+    kzero(s);
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[5]);
+    msg_bytes16(m, 9, vk);
+    msg_byte(m, 25, b1[0]);
+    msg_bytes16(m, 26, nonce);
+    msg_absorb_final(s, m, 42);
+    uint32_t w[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
+    put_elem<F>(p, sc.qr, 0, r, w, flag);
+  }
+  uint32_t part0[4] = {0, 0, 0, 0};
+  if (JR) {
+    uint32_t kb[4], part1[4], cor[4];
+    load16(ls + (size_t)(M + PL) * F::ES, kb);
+    jr_part_scratch<F>(p, kb, 0, nonce, sc.meas, r, part0);
+    load16(pub + (size_t)r * p.public_share_len + 16, part1);
+    const uint32_t zero[4] = {0, 0, 0, 0};
+    seed_of<F>(p, 6, zero, part0, part1, cor);
+    const uint8_t b1[1] = {1};
+    expand_to<F>(p, p.dst[3], cor, b1, 1, p.jr_len, sc.jr, r, flag);
+    sc.corrected[r] = make_uint4(cor[0], cor[1], cor[2], cor[3]);
+  }
+  if (flag) {  // a rejection-sampling event: redo the expansions with the byte-level sponge
+    uint32_t vk[4] = {p.vk[0], p.vk[1], p.vk[2], p.vk[3]};
+    uint8_t b[17];
+    b[0] = 1;
+    for (int i = 0; i < 16; i++) b[1 + i] = (uint8_t)(nonce[i >> 2] >> (8 * (i & 3)));
+    bx_expand<F>(p.dst[5], vk, b, 17, 1, sc.qr, ld, r);
+    if (JR) {
+      const uint4 c = sc.corrected[r];
+      const uint32_t cor[4] = {c.x, c.y, c.z, c.w};
+      bx_expand<F>(p.dst[3], cor, b, 1, p.jr_len, sc.jr, ld, r);
+    }
+  }
+  const T t = F::load(sc.qr, r);
+  T v, pt;
+  if (!flp_query_lane<F>(p, sc.meas, sc.proofs, sc.jr, t, sc.Lbuf, sc.PVbuf, sc.acc, r, v, pt) &&
+      st == PRIO3_STATUS_FINISHED)
+    st = PRIO3_STATUS_PREP_INIT;
+  uint8_t* ps = prep_shares + (size_t)r * p.prep_share_len;
+  F::store(ps, 0, v);
+  for (uint32_t w = 0; w < A; w++) F::store(ps, 1 + w, F::load(sc.acc, (size_t)w * ld + r));
+  F::store(ps, A + 1, pt);
+  if (JR) *(uint4*)(ps + (size_t)p.verifier_len * F::ES) = make_uint4(part0[0], part0[1], part0[2], part0[3]);
+  sc.flag[r] = (uint8_t)flag;
+  status[r] = st;
+}
+
+// prepare_next: the helper's prepare message must equal the leader's corrected joint-rand
+// seed (else VdafPrepareNext); the output share is truncate(meas share).
+template <class F>
+__global__ __launch_bounds__(256) void k_leader_next(DevParams p, const uint8_t* prep_msgs,
+                                                     Scratch sc, uint8_t* status) {
+  typedef typename F::T T;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= p.n) return;
+  const size_t ld = p.ld;
+  uint8_t st = status[r];
+  if (st == PRIO3_STATUS_FINISHED && p.jr_len) {
+    uint32_t m[4];
+    load16(prep_msgs + 16 * (size_t)r, m);
+    const uint4 c = sc.corrected[r];
+    if (m[0] != c.x || m[1] != c.y || m[2] != c.z || m[3] != c.w) st = PRIO3_STATUS_PREP_NEXT;
+  }
+  status[r] = st;
+  if (p.kind == PRIO3_SUM || p.kind == PRIO3_SUMVEC) {
+    const uint32_t outs = p.kind == PRIO3_SUM ? 1 : p.out_len;
+    for (uint32_t e = 0; e < outs; e++) {
+      T acc = F::zero(), pw = F::one();
+      for (uint32_t b = 0; b < p.bits; b++) {
+        acc = F::add(acc, F::mul(pw, F::load(sc.meas, (size_t)(e * p.bits + b) * ld + r)));
+        pw = F::add(pw, pw);
+      }
+      F::store(sc.out, (size_t)e * ld + r, acc);
+    }
+  }
+}
+
+extern "C" int launch_leader_init(const DevParams& dp, const uint8_t* d_nonces, const uint8_t* d_pub,
+                       const uint8_t* d_lshares, const Scratch& sc, uint8_t* d_prep_shares,
+                       uint8_t* d_status, hipStream_t st) {
+  const uint32_t blocks = (dp.n + 63) / 64;
+  if (dp.es == 16)
+    k_leader_init<Fp128><<<blocks, 64, 0, st>>>(dp, d_nonces, d_pub, d_lshares, sc,
+                                                d_prep_shares, d_status);
+  else
+    k_leader_init<Fp64><<<blocks, 64, 0, st>>>(dp, d_nonces, d_pub, d_lshares, sc,
+                                               d_prep_shares, d_status);
+  return hipGetLastError() == hipSuccess ? PRIO3_OK : PRIO3_EDEVICE;
+}
+
+extern "C" int launch_leader_next(const DevParams& dp, const uint8_t* d_prep_msgs, const Scratch& sc,
+                       uint8_t* d_status, hipStream_t st) {
+  const uint32_t blocks = (dp.n + 255) / 256;
+  if (dp.es == 16)
+    k_leader_next<Fp128><<<blocks, 256, 0, st>>>(dp, d_prep_msgs, sc, d_status);
+  else
+    k_leader_next<Fp64><<<blocks, 256, 0, st>>>(dp, d_prep_msgs, sc, d_status);
+  return hipGetLastError() == hipSuccess ? PRIO3_OK : PRIO3_EDEVICE;
+}
 
 static f128 h128(const uint32_t* w) {
   f128 r;

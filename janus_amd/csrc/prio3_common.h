@@ -11,7 +11,8 @@
 
 struct DevParams {
   uint32_t kind, es, meas_len, out_len, jr_len, arity, calls, P, logP, glen, proof_len,
-      verifier_len, chunk, bits, length, prep_share_len, helper_share_len, public_share_len;
+      verifier_len, chunk, bits, length, prep_share_len, helper_share_len, public_share_len,
+      leader_share_len;
   uint32_t n, ld, force_slow;
   uint32_t vk[4];
   uint32_t dst[8][2];
@@ -77,6 +78,93 @@ DEV void load16(const uint8_t* p, uint32_t* w) {
   w[1] = v.y;
   w[2] = v.z;
   w[3] = v.w;
+}
+
+// ------------------------------------------------------------------------------------
+// Byte-level sponge with rejection sampling (the slow path for flagged reports)
+// ------------------------------------------------------------------------------------
+struct BX {
+  KState s;
+  uint8_t buf[168];
+  uint32_t pos;
+};
+DEV void bx_xor_block(BX& x) {
+#pragma unroll
+  for (int w = 0; w < 42; w++) {
+    uint32_t v = (uint32_t)x.buf[4 * w] | ((uint32_t)x.buf[4 * w + 1] << 8) |
+                 ((uint32_t)x.buf[4 * w + 2] << 16) | ((uint32_t)x.buf[4 * w + 3] << 24);
+    kxor_word(x.s, w, v);
+  }
+  keccak_p12(x.s);
+}
+DEV void bx_fill(BX& x) {
+#pragma unroll
+  for (int w = 0; w < 42; w++) {
+    uint32_t v = kword(x.s, w);
+    x.buf[4 * w] = v;
+    x.buf[4 * w + 1] = v >> 8;
+    x.buf[4 * w + 2] = v >> 16;
+    x.buf[4 * w + 3] = v >> 24;
+  }
+  x.pos = 0;
+}
+DEV void bx_absorb(BX& x, uint8_t b) {
+  x.buf[x.pos++] = b;
+  if (x.pos == 168) {
+    bx_xor_block(x);
+    x.pos = 0;
+  }
+}
+DEV void bx_absorb_w(BX& x, const uint32_t* w, int nbytes) {
+  for (int i = 0; i < nbytes; i++) bx_absorb(x, (uint8_t)(w[i >> 2] >> (8 * (i & 3))));
+}
+DEV void bx_init(BX& x, const uint32_t* dst2, const uint32_t* seed) {
+  kzero(x.s);
+  x.pos = 0;
+  bx_absorb(x, 8);
+  bx_absorb_w(x, dst2, 8);
+  bx_absorb_w(x, seed, 16);
+}
+DEV void bx_finalize(BX& x) {
+  for (uint32_t i = x.pos; i < 168; i++) x.buf[i] = 0;
+  x.buf[x.pos] ^= 0x01;
+  x.buf[167] ^= 0x80;
+  bx_xor_block(x);
+  bx_fill(x);
+}
+DEV uint8_t bx_squeeze(BX& x) {
+  if (x.pos == 168) {
+    keccak_p12(x.s);
+    bx_fill(x);
+  }
+  return x.buf[x.pos++];
+}
+// next accepted element (rejection sampling); writes ES/4 words
+template <class F>
+DEV void bx_next_elem(BX& x, uint32_t* w) {
+  for (;;) {
+    for (int k = 0; k < F::ES / 4; k++) {
+      uint32_t v = 0;
+      for (int b = 0; b < 4; b++) v |= (uint32_t)bx_squeeze(x) << (8 * b);
+      w[k] = v;
+    }
+    if (F::lt_p(F::from_words(w))) return;
+  }
+}
+
+// XOF(seed, dst, binder).expand_into_vec(n) with rejection sampling, into SoA columns
+template <class F>
+DEV void bx_expand(const uint32_t* dst2, const uint32_t* seed, const uint8_t* binder, int blen,
+                   uint32_t n, void* base, size_t ld, uint32_t r) {
+  BX x;
+  bx_init(x, dst2, seed);
+  for (int i = 0; i < blen; i++) bx_absorb(x, binder[i]);
+  bx_finalize(x);
+  for (uint32_t i = 0; i < n; i++) {
+    uint32_t w[4];
+    bx_next_elem<F>(x, w);
+    F::store(base, (size_t)i * ld + r, F::from_words(w));
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -317,6 +405,9 @@ struct prio3_engine {
   uint32_t io_cap = 0;
   uint8_t *d_nonces = nullptr, *d_pub = nullptr, *d_helper = nullptr, *d_leader = nullptr,
           *d_msgs = nullptr, *d_status = nullptr;
+  uint8_t* d_linput = nullptr;  // leader input shares (host leader API)
+  uint32_t linput_cap = 0;
+  uint32_t leader_n = 0;
   int force_slow = 0;
   int split_xof = 1;
   int qh_prefetch = 1;

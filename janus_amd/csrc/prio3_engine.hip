@@ -410,75 +410,7 @@ __global__ __launch_bounds__(256, JR_OCC) void k_jrpart(DevParams p, InPtrs in, 
 // ------------------------------------------------------------------------------------
 // k_xof_slow: general byte-level sponge with rejection sampling (flagged reports only)
 // ------------------------------------------------------------------------------------
-struct BX {
-  KState s;
-  uint8_t buf[168];
-  uint32_t pos;
-};
-DEV void bx_xor_block(BX& x) {
-#pragma unroll
-  for (int w = 0; w < 42; w++) {
-    uint32_t v = (uint32_t)x.buf[4 * w] | ((uint32_t)x.buf[4 * w + 1] << 8) |
-                 ((uint32_t)x.buf[4 * w + 2] << 16) | ((uint32_t)x.buf[4 * w + 3] << 24);
-    kxor_word(x.s, w, v);
-  }
-  keccak_p12(x.s);
-}
-DEV void bx_fill(BX& x) {
-#pragma unroll
-  for (int w = 0; w < 42; w++) {
-    uint32_t v = kword(x.s, w);
-    x.buf[4 * w] = v;
-    x.buf[4 * w + 1] = v >> 8;
-    x.buf[4 * w + 2] = v >> 16;
-    x.buf[4 * w + 3] = v >> 24;
-  }
-  x.pos = 0;
-}
-DEV void bx_absorb(BX& x, uint8_t b) {
-  x.buf[x.pos++] = b;
-  if (x.pos == 168) {
-    bx_xor_block(x);
-    x.pos = 0;
-  }
-}
-DEV void bx_absorb_w(BX& x, const uint32_t* w, int nbytes) {
-  for (int i = 0; i < nbytes; i++) bx_absorb(x, (uint8_t)(w[i >> 2] >> (8 * (i & 3))));
-}
-DEV void bx_init(BX& x, const uint32_t* dst2, const uint32_t* seed) {
-  kzero(x.s);
-  x.pos = 0;
-  bx_absorb(x, 8);
-  bx_absorb_w(x, dst2, 8);
-  bx_absorb_w(x, seed, 16);
-}
-DEV void bx_finalize(BX& x) {
-  for (uint32_t i = x.pos; i < 168; i++) x.buf[i] = 0;
-  x.buf[x.pos] ^= 0x01;
-  x.buf[167] ^= 0x80;
-  bx_xor_block(x);
-  bx_fill(x);
-}
-DEV uint8_t bx_squeeze(BX& x) {
-  if (x.pos == 168) {
-    keccak_p12(x.s);
-    bx_fill(x);
-  }
-  return x.buf[x.pos++];
-}
-// next accepted element (rejection sampling); writes ES/4 words
-template <class F>
-DEV void bx_next_elem(BX& x, uint32_t* w) {
-  for (;;) {
-    for (int k = 0; k < F::ES / 4; k++) {
-      uint32_t v = 0;
-      for (int b = 0; b < 4; b++) v |= (uint32_t)bx_squeeze(x) << (8 * b);
-      w[k] = v;
-    }
-    if (F::lt_p(F::from_words(w))) return;
-  }
-}
-
+// (byte-level sponge helpers BX / bx_* live in prio3_common.h)
 template <class F>
 __global__ __launch_bounds__(64) void k_xof_slow(DevParams p, InPtrs in, Scratch sc) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1669,6 +1601,7 @@ static int fill_sizes(const prio3_params* pp, prio3_sizes_t* s, DevParams* dp) {
   d.helper_share_len = d.jr_len ? 48 : 32;
   d.public_share_len = d.jr_len ? 32 : 0;
   d.prep_share_len = d.verifier_len * d.es + (d.jr_len ? 16 : 0);
+  d.leader_share_len = (d.meas_len + d.proof_len) * d.es + (d.jr_len ? 16 : 0);
   for (uint32_t u = 1; u <= 7; u++) {
     uint8_t b[8] = {8, 0, (uint8_t)(algo >> 24), (uint8_t)(algo >> 16), (uint8_t)(algo >> 8),
                     (uint8_t)algo, 0, (uint8_t)u};
@@ -1726,6 +1659,7 @@ static int fill_sizes(const prio3_params* pp, prio3_sizes_t* s, DevParams* dp) {
     s->prep_share_len = d.prep_share_len;
     s->prep_msg_len = d.jr_len ? 16 : 0;
     s->agg_share_len = d.out_len * d.es;
+    s->leader_input_share_len = d.leader_share_len;
   }
   if (dp) *dp = d;
   return PRIO3_OK;
@@ -1853,7 +1787,7 @@ void prio3_engine_destroy(prio3_engine* e) {
                   e->sc.flag, e->sc.Lbuf, e->sc.PVbuf, e->sc.acc, e->sc.out, e->sc.beta, e->d_mask,
                   e->d_prep_partial, e->d_pcount, e->d_nonces, e->d_pub, e->d_helper,
                   e->d_leader, e->d_msgs, e->d_status, e->d_wpart, e->d_wseg, e->d_agg64,
-                  e->d_fix, e->d_cpart, e->d_cseg};
+                  e->d_fix, e->d_cpart, e->d_cseg, e->d_linput};
   for (auto b : bufs)
     if (b) (void)hipFree(b);
   for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
@@ -2292,6 +2226,117 @@ void prio3_engine_timing_reset(prio3_engine* e) {
     t.ms = 0;
     t.launches = 0;
   }
+}
+
+// ---- leader side ----
+int launch_leader_init(const DevParams& dp, const uint8_t* d_nonces, const uint8_t* d_pub,
+                       const uint8_t* d_lshares, const Scratch& sc, uint8_t* d_prep_shares,
+                       uint8_t* d_status, hipStream_t st);
+int launch_leader_next(const DevParams& dp, const uint8_t* d_prep_msgs, const Scratch& sc,
+                       uint8_t* d_status, hipStream_t st);
+
+int prio3_device_leader_prepare_init(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
+                                     const uint8_t* d_public_shares,
+                                     const uint8_t* d_leader_input_shares, uint8_t* d_prep_shares,
+                                     uint8_t* d_status, void* stream) {
+  if (!e) return PRIO3_EINVAL;
+  if (n == 0) return PRIO3_OK;
+  if (!d_nonces || !d_leader_input_shares || !d_prep_shares || !d_status ||
+      (e->dp.jr_len && !d_public_shares))
+    return PRIO3_EINVAL;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIPCHK(hipSetDevice(e->device));
+  int rc = ensure_scratch(e, n);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  DevParams dp = e->dp;
+  dp.n = n;
+  dp.force_slow = (uint32_t)e->force_slow;
+  e->leader_n = n;
+  return launch_leader_init(dp, d_nonces, d_public_shares, d_leader_input_shares, e->sc,
+                            d_prep_shares, d_status, st);
+}
+
+int prio3_device_leader_prepare_next(prio3_engine* e, uint32_t n, const uint8_t* d_prep_msgs,
+                                     uint8_t* d_status, void* stream) {
+  if (!e || n > e->cap) return PRIO3_EINVAL;
+  if (n == 0) return PRIO3_OK;
+  if (!d_status || (e->dp.jr_len && !d_prep_msgs)) return PRIO3_EINVAL;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIPCHK(hipSetDevice(e->device));
+  DevParams dp = e->dp;
+  dp.n = n;
+  return launch_leader_next(dp, d_prep_msgs, e->sc, d_status, (hipStream_t)stream);
+}
+
+int prio3_leader_prepare_init_batch(prio3_engine* e, uint32_t n, const uint8_t* nonces,
+                                    const uint8_t* public_shares,
+                                    const uint8_t* leader_input_shares, uint8_t* prep_shares_out,
+                                    uint8_t* status_out, prio3_batch** batch_out) {
+  if (!e || (n && (!nonces || !leader_input_shares || !prep_shares_out || !status_out)))
+    return PRIO3_EINVAL;
+  const DevParams& d = e->dp;
+  if (n && d.jr_len && !public_shares) return PRIO3_EINVAL;
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIPCHK(hipSetDevice(e->device));
+    int rc = ensure_io(e, n ? n : 1);
+    if (rc) return rc;
+    if (n > e->linput_cap) {
+      if (e->d_linput) (void)hipFree(e->d_linput);
+      e->d_linput = nullptr;
+      HIPCHK(hipMalloc((void**)&e->d_linput, (size_t)d.leader_share_len * n));
+      e->linput_cap = n;
+    }
+    hipStream_t st = e->stream;
+    if (n) {
+      HIPCHK(hipMemcpyAsync(e->d_nonces, nonces, 16 * (size_t)n, hipMemcpyHostToDevice, st));
+      if (d.jr_len)
+        HIPCHK(hipMemcpyAsync(e->d_pub, public_shares, (size_t)d.public_share_len * n,
+                              hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(e->d_linput, leader_input_shares, (size_t)d.leader_share_len * n,
+                            hipMemcpyHostToDevice, st));
+    }
+  }
+  int rc = prio3_device_leader_prepare_init(e, n, e->d_nonces, e->d_pub, e->d_linput, e->d_leader,
+                                            e->d_status, e->stream);
+  if (rc) return rc;
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    hipStream_t st = e->stream;
+    if (n) {
+      HIPCHK(hipMemcpyAsync(status_out, e->d_status, n, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(prep_shares_out, e->d_leader, (size_t)d.prep_share_len * n,
+                            hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  if (batch_out) *batch_out = new prio3_batch{e, n};
+  return PRIO3_OK;
+}
+
+int prio3_leader_prepare_next_batch(prio3_batch* b, const uint8_t* prep_msgs,
+                                    uint8_t* status_inout) {
+  if (!b || !status_inout) return PRIO3_EINVAL;
+  prio3_engine* e = b->e;
+  const uint32_t n = b->n;
+  const DevParams& d = e->dp;
+  if (n == 0) return PRIO3_OK;
+  if (d.jr_len && !prep_msgs) return PRIO3_EINVAL;
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIPCHK(hipSetDevice(e->device));
+    hipStream_t st = e->stream;
+    if (d.jr_len)
+      HIPCHK(hipMemcpyAsync(e->d_msgs, prep_msgs, 16 * (size_t)n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(e->d_status, status_inout, n, hipMemcpyHostToDevice, st));
+  }
+  int rc = prio3_device_leader_prepare_next(e, n, e->d_msgs, e->d_status, e->stream);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIPCHK(hipMemcpyAsync(status_inout, e->d_status, n, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return PRIO3_OK;
 }
 
 int prio3_selftest_field(int op, uint32_t n, const uint8_t* a, const uint8_t* b, uint8_t* out) {

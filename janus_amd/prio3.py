@@ -35,6 +35,7 @@ STATUS_PREP_SHARE_DECODE = 2
 STATUS_PREP_MSG = 3
 STATUS_PREP_NEXT = 4
 STATUS_PEER_MISMATCH = 5
+STATUS_INPUT_SHARE_DECODE = 6
 
 #: prio ``PingPongError`` variant for each status (error.rs:365-428 maps these to labels).
 STATUS_PINGPONG_ERROR = {
@@ -43,6 +44,7 @@ STATUS_PINGPONG_ERROR = {
     STATUS_PREP_MSG: "VdafPrepareSharesToPrepareMessage",
     STATUS_PREP_NEXT: "VdafPrepareNext",
     STATUS_PEER_MISMATCH: "PeerMessageMismatch",
+    STATUS_INPUT_SHARE_DECODE: "InvalidMessage",
 }
 
 #: ``janus_step_failures{type=...}`` metric label per status, helper role
@@ -65,7 +67,7 @@ class Prio3Sizes(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in (
         "field_bytes", "meas_len", "out_len", "proof_len", "verifier_len", "joint_rand_len",
         "nonce_len", "public_share_len", "helper_share_len", "prep_share_len", "prep_msg_len",
-        "agg_share_len")]
+        "agg_share_len", "leader_input_share_len")]
 
 
 #: Every symbol include/janus_prio3.h declares.
@@ -75,7 +77,9 @@ EXPORTED_SYMBOLS = (
     "prio3_device_accumulate", "prio3_device_output_shares", "prio3_device_combine",
     "prio3_engine_set_option", "prio3_engine_timing", "prio3_engine_timing_reset",
     "prio3_client_generate_device", "prio3_selftest_field", "prio3_device_prepare_aggregate",
-    "prio3_device_aggregate_finish",
+    "prio3_device_aggregate_finish", "prio3_leader_prepare_init_batch",
+    "prio3_leader_prepare_next_batch", "prio3_device_leader_prepare_init",
+    "prio3_device_leader_prepare_next",
 )
 
 _lib = None
@@ -123,6 +127,10 @@ def load_library() -> C.CDLL:
     L.prio3_device_prepare_aggregate.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, vp, C.c_uint32,
                                                  vp, vp, vp]
     L.prio3_device_aggregate_finish.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.prio3_leader_prepare_init_batch.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, vp, P(vp)]
+    L.prio3_leader_prepare_next_batch.argtypes = [vp, vp, vp]
+    L.prio3_device_leader_prepare_init.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, vp, vp]
+    L.prio3_device_leader_prepare_next.argtypes = [vp, C.c_uint32, vp, vp, vp]
     _lib = L
     return L
 
@@ -213,6 +221,21 @@ class PreparedBatch:
             raise RuntimeError(f"prio3_accumulate failed (rc={rc})")
         return agg, cnt
 
+    def leader_prepare_next(self, prep_msgs, status) -> np.ndarray:
+        """Leader ``prepare_next`` on the helper's prepare messages (leader_continued,
+        aggregation_job_driver.rs:677-691); returns the updated per-report status."""
+        st = np.array(status, np.uint8, copy=True)
+        msgs = None
+        if self.engine.sz.prep_msg_len:
+            msgs = np.ascontiguousarray(prep_msgs, np.uint8)
+            if msgs.shape != (self.n, self.engine.sz.prep_msg_len):
+                raise ValueError("prepare message shape does not match the VDAF instance")
+        rc = load_library().prio3_leader_prepare_next_batch(self.handle, _np_ptr(msgs),
+                                                            _np_ptr(st))
+        if rc:
+            raise RuntimeError(f"prio3_leader_prepare_next_batch failed (rc={rc})")
+        return st
+
     def output_shares(self) -> np.ndarray:
         out = np.zeros((self.n, self.engine.sz.agg_share_len), np.uint8)
         rc = load_library().prio3_debug_output_shares(self.handle, _np_ptr(out))
@@ -293,6 +316,48 @@ class HelperEngine:
         if rc:
             raise RuntimeError(f"prio3_helper_prepare_batch failed (rc={rc})")
         return msgs[:, :sz.prep_msg_len], status, PreparedBatch(self, bh, n)
+
+    # ---- leader side (same instance, agg_id 0) -----------------------------------
+    def leader_prepare_init_batch(self, nonces, public_shares, leader_input_shares):
+        """Batched leader prepare_init (leader_initialized, aggregation_job_driver.rs:397-415).
+
+        Returns (prep_shares [n, prep_share_len], status [n], batch); the batch's
+        ``leader_prepare_next`` then takes the helper's prepare messages."""
+        sz = self.sz
+        nonces = np.ascontiguousarray(nonces, np.uint8)
+        n = nonces.shape[0]
+        ls = np.ascontiguousarray(leader_input_shares, np.uint8)
+        if ls.shape != (n, sz.leader_input_share_len):
+            raise ValueError("leader input share shape does not match the VDAF instance")
+        pub = None
+        if sz.public_share_len:
+            pub = np.ascontiguousarray(public_shares, np.uint8)
+            if pub.shape != (n, sz.public_share_len):
+                raise ValueError("public share shape does not match the VDAF instance")
+        ps = np.zeros((n, sz.prep_share_len), np.uint8)
+        status = np.zeros(n, np.uint8)
+        bh = C.c_void_p()
+        rc = load_library().prio3_leader_prepare_init_batch(
+            self.handle, n, _np_ptr(nonces), _np_ptr(pub), _np_ptr(ls), _np_ptr(ps),
+            _np_ptr(status), C.byref(bh))
+        if rc:
+            raise RuntimeError(f"prio3_leader_prepare_init_batch failed (rc={rc})")
+        return ps, status, PreparedBatch(self, bh, n)
+
+    def leader_prepare_init_device(self, nonces, public_shares, leader_input_shares, prep_shares,
+                                   status, stream=None) -> None:
+        rc = load_library().prio3_device_leader_prepare_init(
+            self.handle, nonces.shape[0], _tptr(nonces), _tptr(public_shares),
+            _tptr(leader_input_shares), _tptr(prep_shares), _tptr(status),
+            _stream(stream, self.device))
+        if rc:
+            raise RuntimeError(f"prio3_device_leader_prepare_init failed (rc={rc})")
+
+    def leader_prepare_next_device(self, n, prep_msgs, status, stream=None) -> None:
+        rc = load_library().prio3_device_leader_prepare_next(
+            self.handle, n, _tptr(prep_msgs), _tptr(status), _stream(stream, self.device))
+        if rc:
+            raise RuntimeError(f"prio3_device_leader_prepare_next failed (rc={rc})")
 
     # ---- device-resident path (torch tensors on this engine's GPU) ------------------
     def prepare_device(self, nonces, public_shares, helper_shares, leader_prep_shares,

@@ -45,6 +45,7 @@ def test_sizes_match_oracle(name, oracle_lib):
     assert s.prep_share_len == o.prep_share_len
     assert s.prep_msg_len == o.prep_msg_len
     assert s.agg_share_len == o.out_share_bytes
+    assert s.leader_input_share_len == o.leader_share_len
 
 
 def test_histogram_256_sizes_match_survey():
