@@ -35,7 +35,7 @@ def _reports(o, cfg, n, seed):
         nonce = rng.bytes(16)
         pub, l, h = o.shard(m, nonce, rng.bytes(o.rand_size))
         nonces.append(nonce), pubs.append(pub), ls.append(l), hs.append(h), meas.append(m)
-    arr = lambda xs: np.frombuffer(b"".join(xs), np.uint8).reshape(n, -1) if xs[0] else \
+    arr = lambda xs: np.frombuffer(b"".join(xs), np.uint8).reshape(n, -1).copy() if xs[0] else \
         np.zeros((n, 0), np.uint8)
     return dict(nonces=arr(nonces), public_shares=arr(pubs), leader_shares=arr(ls),
                 helper_shares=arr(hs), measurements=meas)
