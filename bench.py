@@ -88,9 +88,13 @@ def main():
     ap.add_argument("--reports", type=int, default=1 << 20, help="reports per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--role", choices=["helper", "leader"], default="helper",
+                    help="helper (the BASELINE metric) or the leader side (SURVEY 8(f) row 1)")
     ap.add_argument("--opt", action="append", default=[],
                     help="engine option key=value (e.g. split_xof=0), for A/B runs")
     args = ap.parse_args()
+    if args.role == "leader":
+        return leader_main(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -211,6 +215,65 @@ def main():
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def leader_main(args):
+    """Leader-side line (not the BASELINE metric): one step = leader prepare_init (agg_id 0) on
+    the explicit input shares + prepare_next on the helper's prepare messages + accumulate,
+    for the same Histogram(256,16) batch.  The prepare messages are the helper engine's own
+    output on the same reports, computed once before timing."""
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    n = args.reports
+    eng = J.HelperEngine(J.Prio3Histogram(256, 16), VK, device=0)
+    sz = eng.sz
+    data = eng.generate_reports_device(n, seed=0x4A414E5553000002, with_checks=True,
+                                       with_leader_inputs=True)
+    u8 = dict(dtype=torch.uint8, device=dev)
+    msgs = torch.empty((n, 16), **u8)
+    status = torch.empty(n, **u8)
+    eng.prepare_device(data["nonces"], data["public_shares"], data["helper_shares"],
+                       data["leader_prep_shares"], msgs, status)
+    torch.cuda.synchronize()
+    helper_ok = int((status == 0).sum().item())
+    prep = torch.empty((n, sz.prep_share_len), **u8)
+    lstatus = torch.empty(n, **u8)
+    agg = torch.zeros((1, sz.agg_share_len), **u8)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def step():
+        eng.leader_prepare_init_device(data["nonces"], data["public_shares"],
+                                       data["leader_input_shares"], prep, lstatus)
+        eng.leader_prepare_next_device(n, msgs, lstatus)
+        eng.accumulate_device(n, lstatus, None, None, 1, agg, cnt)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    eng.set_option("timing", 1)
+    eng.timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    times = eng.timing()
+    per_kernel = {k: dict(ms_total=v[0], launches=v[1], ms_avg=v[0] / max(v[1], 1))
+                  for k, v in times.items()}
+    same = bool(torch.equal(prep, data["leader_prep_shares"]))
+    out = dict(metric="reports prepared+aggregated/sec (leader, Prio3Histogram len=256)",
+               value=n * args.steps / elapsed, unit="reports/s", n_gpus=1, steps=args.steps,
+               warmup=args.warmup, ms_per_step=elapsed / args.steps * 1e3,
+               higher_is_better=True, scaling="weak", vs_baseline=None,
+               dtype="u32 limbs (Field128 mod-p integer arithmetic)",
+               data="synthetic: on-device client reports (leader input shares explicit)",
+               config=dict(workload="Prio3Histogram length=256 chunk_length=16 leader "
+                                    "prepare_init+prepare_next+aggregate", reports_per_gpu=n),
+               kernels=per_kernel,
+               checks=dict(helper_finished=helper_ok,
+                           leader_finished=int((lstatus == 0).sum().item()),
+                           leader_prep_shares_equal_generator=same, agg_count=int(cnt[0].item())))
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

@@ -184,12 +184,14 @@ int prio3_device_leader_prepare_next(prio3_engine* engine, uint32_t n, const uin
  * derived from (seed, first_index + i) exactly like the oracle's generator.
  * d_measurements: n x (SumVec: length, else 1) u64 (nullable); d_leader_out_shares:
  * n x agg_share_len (nullable); d_flags: n bytes, non-zero if a rejection-sampling event made
- * the report unusable (nullable). */
+ * the report unusable (nullable); d_leader_input_shares: n x leader_input_share_len, the
+ * leader's input shares for the leader-side entry points (nullable). */
 int prio3_client_generate_device(prio3_engine* engine, uint32_t n, uint64_t seed,
                                  uint64_t first_index, uint8_t* d_nonces,
                                  uint8_t* d_public_shares, uint8_t* d_helper_shares,
                                  uint8_t* d_leader_prep_shares, uint64_t* d_measurements,
-                                 uint8_t* d_leader_out_shares, uint8_t* d_flags, void* stream);
+                                 uint8_t* d_leader_out_shares, uint8_t* d_flags,
+                                 uint8_t* d_leader_input_shares, void* stream);
 
 /* ---- Test / measurement knobs ---- */
 /* force_slow_path=1 routes every report through the general rejection-sampling kernel. */

@@ -22,7 +22,7 @@ struct GenScratch {
   void *meas, *hm, *lm, *wires, *evals, *g, *tmp, *proof, *hp, *prand, *jr, *qr, *L, *PV, *acc;
 };
 struct GenOut {
-  uint8_t *nonces, *pub, *helper, *leader_ps, *leader_out;
+  uint8_t *nonces, *pub, *helper, *leader_ps, *leader_out, *leader_in;
   uint64_t* meas;
   uint8_t* flags;
 };
@@ -323,6 +323,14 @@ __global__ __launch_bounds__(64) void k_gen(DevParams p, uint64_t seed, uint64_t
   for (uint32_t w = 0; w < A; w++) F::store(lps, 1 + w, F::load(gs.acc, (size_t)w * ld + r));
   F::store(lps, A + 1, pt);
   if (JR) *(uint4*)(lps + (size_t)p.verifier_len * F::ES) = make_uint4(part0[0], part0[1], part0[2], part0[3]);
+  // leader input share = enc(meas share) || enc(proofs share) [|| k_blind]
+  if (go.leader_in) {
+    uint8_t* li = go.leader_in + (size_t)r * p.leader_share_len;
+    for (uint32_t e = 0; e < M; e++) F::store(li, e, F::load(gs.lm, (size_t)e * ld + r));
+    for (uint32_t e = 0; e < PL; e++)
+      F::store(li + (size_t)M * F::ES, e, F::load(gs.hp, (size_t)e * ld + r));
+    if (JR) *(uint4*)(li + (size_t)(M + PL) * F::ES) = make_uint4(k_lb[0], k_lb[1], k_lb[2], k_lb[3]);
+  }
   // ---- public outputs ----
   *(uint4*)(go.nonces + 16 * (size_t)r) = make_uint4(nonce[0], nonce[1], nonce[2], nonce[3]);
   uint8_t* hs = go.helper + (size_t)r * p.helper_share_len;
@@ -525,7 +533,7 @@ extern "C" int prio3_client_generate_device(prio3_engine* e, uint32_t n, uint64_
                                             uint8_t* d_leader_prep_shares,
                                             uint64_t* d_measurements,
                                             uint8_t* d_leader_out_shares, uint8_t* d_flags,
-                                            void* stream) {
+                                            uint8_t* d_leader_input_shares, void* stream) {
   if (!e || !d_nonces || !d_helper_shares || !d_leader_prep_shares) return PRIO3_EINVAL;
   if (n == 0) return PRIO3_OK;
   std::lock_guard<std::mutex> lk(e->mu);
@@ -575,6 +583,8 @@ extern "C" int prio3_client_generate_device(prio3_engine* e, uint32_t n, uint64_
       go.leader_out = d_leader_out_shares ? d_leader_out_shares + (size_t)p.out_len * es * off : nullptr;
       go.meas = d_measurements ? d_measurements + (size_t)mstride * off : nullptr;
       go.flags = d_flags ? d_flags + off : nullptr;
+      go.leader_in = d_leader_input_shares ? d_leader_input_shares + (size_t)p.leader_share_len * off
+                                           : nullptr;
       if (es == 16)
         k_gen<Fp128><<<(m + 63) / 64, 64, 0, st>>>(p, seed, first_index + off, gs, go, h128(w1),
                                                    h128(w2));

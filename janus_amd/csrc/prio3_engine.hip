@@ -2253,8 +2253,11 @@ int prio3_device_leader_prepare_init(prio3_engine* e, uint32_t n, const uint8_t*
   dp.n = n;
   dp.force_slow = (uint32_t)e->force_slow;
   e->leader_n = n;
-  return launch_leader_init(dp, d_nonces, d_public_shares, d_leader_input_shares, e->sc,
-                            d_prep_shares, d_status, st);
+  int rc2 = PRIO3_OK;
+  TIMED(e, st, "k_leader_init",
+        rc2 = launch_leader_init(dp, d_nonces, d_public_shares, d_leader_input_shares, e->sc,
+                                 d_prep_shares, d_status, st));
+  return rc2;
 }
 
 int prio3_device_leader_prepare_next(prio3_engine* e, uint32_t n, const uint8_t* d_prep_msgs,
@@ -2266,7 +2269,10 @@ int prio3_device_leader_prepare_next(prio3_engine* e, uint32_t n, const uint8_t*
   HIPCHK(hipSetDevice(e->device));
   DevParams dp = e->dp;
   dp.n = n;
-  return launch_leader_next(dp, d_prep_msgs, e->sc, d_status, (hipStream_t)stream);
+  hipStream_t st = (hipStream_t)stream;
+  int rc2 = PRIO3_OK;
+  TIMED(e, st, "k_leader_next", rc2 = launch_leader_next(dp, d_prep_msgs, e->sc, d_status, st));
+  return rc2;
 }
 
 int prio3_leader_prepare_init_batch(prio3_engine* e, uint32_t n, const uint8_t* nonces,

@@ -117,7 +117,7 @@ def load_library() -> C.CDLL:
     L.prio3_device_output_shares.argtypes = [vp, C.c_uint32, vp]
     L.prio3_device_combine.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp]
     L.prio3_client_generate_device.argtypes = [vp, C.c_uint32, C.c_uint64, C.c_uint64, vp, vp,
-                                               vp, vp, vp, vp, vp, vp]
+                                               vp, vp, vp, vp, vp, vp, vp]
     L.prio3_engine_set_option.argtypes = [vp, C.c_char_p, C.c_int64]
     L.prio3_engine_timing.argtypes = [vp, C.c_char_p, C.c_size_t, P(C.c_double),
                                       P(C.c_uint64), C.c_int]
@@ -411,7 +411,8 @@ class HelperEngine:
 
     # ---- synthetic client ------------------------------------------------------------
     def generate_reports_device(self, n: int, seed: int = 1, first_index: int = 0,
-                                with_checks: bool = False, stream=None) -> dict:
+                                with_checks: bool = False, with_leader_inputs: bool = False,
+                                stream=None) -> dict:
         """Honest synthetic reports generated on the GPU (shard + leader prepare_init).
 
         Returns torch uint8 tensors on this engine's device (plus measurements / leader
@@ -429,12 +430,15 @@ class HelperEngine:
             out["measurements"] = torch.empty((n, mstride), dtype=torch.int64, device=dev)
             out["leader_out_shares"] = torch.empty((n, sz.agg_share_len), **u8)
             out["flags"] = torch.zeros(n, **u8)
+        if with_leader_inputs:
+            out["leader_input_shares"] = torch.empty((n, sz.leader_input_share_len), **u8)
         rc = load_library().prio3_client_generate_device(
             self.handle, n, seed, first_index, _tptr(out["nonces"]),
             _tptr(out["public_shares"]) if sz.public_share_len else None,
             _tptr(out["helper_shares"]), _tptr(out["leader_prep_shares"]),
             _tptr(out.get("measurements")), _tptr(out.get("leader_out_shares")),
-            _tptr(out.get("flags")), _stream(stream, self.device))
+            _tptr(out.get("flags")), _tptr(out.get("leader_input_shares")),
+            _stream(stream, self.device))
         if rc:
             raise RuntimeError(f"prio3_client_generate_device failed (rc={rc})")
         if not sz.public_share_len:
