@@ -400,7 +400,8 @@ struct prio3_engine {
   uint32_t fused_n = 0, fused_segments = 0;
   int fused_on = 0;  // last prepare_aggregate used the fused kernels
   const uint32_t* fused_seg_ptr = nullptr;
-  int fuse_acc = 1;  // option: fused accumulate on/off (A/B)
+  int fuse_acc = 1;
+  int leader_fast = 1;  // option: leader role on the helper kernels (Histogram / SumVec, P <= 32)  // option: fused accumulate on/off (A/B)
   // host-API staging
   uint32_t io_cap = 0;
   uint8_t *d_nonces = nullptr, *d_pub = nullptr, *d_helper = nullptr, *d_leader = nullptr,

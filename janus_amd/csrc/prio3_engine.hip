@@ -269,7 +269,10 @@ __global__ __launch_bounds__(256, XOF_OCC) void k_xof_a(DevParams p, InPtrs in, 
 // reports by wave_halfsum2 and the wave's half-limb partials go to sc.wpart.  Only waves whose
 // 64 reports are all present and in one segment are fused (sc.wseg records which); the rest,
 // and every report the verdict or the host mask excludes, are fixed up in aggregate_finish.
-template <bool FUSE>
+// LEADER: agg_id 0 -- the blind is the last 16 bytes of the explicit leader input share
+// (in.helper then points at the leader input shares), the binder byte is 0, and the corrected
+// seed is derive_seed(own part || public part 1) (leader part first).
+template <bool FUSE, bool LEADER = false>
 __global__ __launch_bounds__(256, JR_OCC) void k_jrpart(DevParams p, InPtrs in, Scratch sc) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
@@ -289,14 +292,17 @@ __global__ __launch_bounds__(256, JR_OCC) void k_jrpart(DevParams p, InPtrs in, 
   const int M = (int)p.meas_len;
   uint32_t nonce[4], kb[4];
   load16(in.nonces + 16 * (size_t)r, nonce);
-  load16(in.helper + (size_t)r * p.helper_share_len + 32, kb);
+  if constexpr (LEADER)
+    load16(in.helper + (size_t)r * p.leader_share_len + (size_t)(p.meas_len + p.proof_len) * 16, kb);
+  else
+    load16(in.helper + (size_t)r * p.helper_share_len + 32, kb);
   uint32_t pre[11];
   {
     Msg m;
     msg_zero(m);
     msg_dst(m, p.dst[7]);
     msg_bytes16(m, 9, kb);
-    msg_byte(m, 25, 1);
+    msg_byte(m, 25, LEADER ? 0 : 1);
     msg_bytes16(m, 26, nonce);
 #pragma unroll
     for (int j = 0; j < 11; j++) pre[j] = m.w[j];
@@ -378,15 +384,15 @@ __global__ __launch_bounds__(256, JR_OCC) void k_jrpart(DevParams p, InPtrs in, 
   uint32_t part[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
   uint32_t flag = sc.flag[r];
   uint32_t pub0[4];
-  load16(in.pub + (size_t)r * p.public_share_len, pub0);
+  load16(in.pub + (size_t)r * p.public_share_len + (LEADER ? 16 : 0), pub0);
   KState c;
   kzero(c);
   {
     Msg m;
     msg_zero(m);
     msg_dst(m, p.dst[6]);
-    msg_bytes16(m, 25, pub0);
-    msg_bytes16(m, 41, part);
+    msg_bytes16(m, 25, LEADER ? part : pub0);
+    msg_bytes16(m, 41, LEADER ? pub0 : part);
     msg_absorb_final(c, m, 57);
   }
   uint32_t cor[4] = {kword(c, 0), kword(c, 1), kword(c, 2), kword(c, 3)};
@@ -405,6 +411,89 @@ __global__ __launch_bounds__(256, JR_OCC) void k_jrpart(DevParams p, InPtrs in, 
   sc.part[r] = make_uint4(part[0], part[1], part[2], part[3]);
   sc.corrected[r] = make_uint4(cor[0], cor[1], cor[2], cor[3]);
   sc.flag[r] = (uint8_t)flag;
+}
+
+
+// ------------------------------------------------------------------------------------
+// k_leader_unpack: the leader's explicit input share (AoS, leader_input_share_len bytes per
+// report) into the SoA measurement / proofs scratch with the canonical-encoding check, plus the
+// query randomness (1 permutation) -- the leader analogue of k_xof_a.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_leader_unpack(DevParams p, InPtrs in, Scratch sc,
+                                                       uint8_t* status) {
+  // block = 64 reports; the explicit shares are transposed through LDS in chunks of 32
+  // elements (rows read 512 B contiguous per report, columns written 1 KiB contiguous per
+  // element) -- per-lane row streaming of the 5.6 KiB rows ran at a fraction of HBM speed.
+  typedef Fp128 F;
+  constexpr int RB = 64, CE = 32;
+  __shared__ uint4 tile[RB][CE + 1];
+  __shared__ uint32_t bad[RB];
+  const uint32_t tid = threadIdx.x, r0 = blockIdx.x * RB;
+  const size_t ld = p.ld;
+  const uint32_t M = p.meas_len, PL = p.proof_len, E = M + PL;
+  const uint32_t nrep = min((uint32_t)RB, p.n - r0);
+  if (tid < RB) bad[tid] = 0;
+  for (uint32_t c0 = 0; c0 < E; c0 += CE) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < RB * CE / 256; i++) {
+      const uint32_t idx = tid + 256 * i, rr = idx / CE, e = c0 + idx % CE;
+      if (rr < nrep && e < E) {
+        const uint4 v =
+            ((const uint4*)(in.helper + (size_t)(r0 + rr) * p.leader_share_len))[e];
+        if (!F::lt_p(mk128(v.x, v.y, v.z, v.w))) atomicOr(&bad[rr], 1u);
+        tile[rr][idx % CE] = v;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < RB * CE / 256; i++) {
+      const uint32_t idx = tid + 256 * i, rr = idx % RB, el = idx / RB, e = c0 + el;
+      if (rr < nrep && e < E) {
+        if (e < M)
+          ((uint4*)sc.meas)[(size_t)e * ld + r0 + rr] = tile[rr][el];
+        else
+          ((uint4*)sc.proofs)[(size_t)(e - M) * ld + r0 + rr] = tile[rr][el];
+      }
+    }
+  }
+  __syncthreads();
+  if (tid >= nrep) return;
+  const uint32_t r = r0 + tid;
+  uint32_t flag = p.force_slow;
+  uint32_t nonce[4];
+  load16(in.nonces + 16 * (size_t)r, nonce);
+  KState s;
+  kzero(s);
+  Msg m;
+  msg_zero(m);
+  msg_dst(m, p.dst[5]);
+  msg_bytes16(m, 9, p.vk);
+  msg_byte(m, 25, 1);
+  msg_bytes16(m, 26, nonce);
+  msg_absorb_final(s, m, 42);
+  uint32_t w[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
+  put_elem<F>(p, sc.qr, 0, r, w, flag);
+  sc.flag[r] = (uint8_t)flag;
+  status[r] = bad[tid] ? PRIO3_STATUS_INPUT_SHARE_DECODE : PRIO3_STATUS_FINISHED;
+}
+
+// Leader slow path: reports whose query or joint-rand expansion hit a rejection-sampling
+// event (flagged by k_leader_unpack / k_jrpart) get both redone by the byte-level sponge.
+__global__ __launch_bounds__(64) void k_leader_slowfix(DevParams p, InPtrs in, Scratch sc) {
+  typedef Fp128 F;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= p.n || !sc.flag[r]) return;
+  uint32_t nonce[4];
+  load16(in.nonces + 16 * (size_t)r, nonce);
+  uint8_t b[17];
+  b[0] = 1;
+  for (int i = 0; i < 16; i++) b[1 + i] = (uint8_t)(nonce[i >> 2] >> (8 * (i & 3)));
+  uint32_t vk[4] = {p.vk[0], p.vk[1], p.vk[2], p.vk[3]};
+  bx_expand<F>(p.dst[5], vk, b, 17, 1, sc.qr, p.ld, r);
+  const uint4 c = sc.corrected[r];
+  const uint32_t cor[4] = {c.x, c.y, c.z, c.w};
+  bx_expand<F>(p.dst[3], cor, b, 1, p.jr_len, sc.jr, p.ld, r);
 }
 
 // ------------------------------------------------------------------------------------
@@ -769,7 +858,10 @@ DEV void dft_reg(const DevParams& p, f128 (&x)[N], int stride) {
   }
 }
 
-template <int GS, int PP, int PF = 1, int OCC = 3>
+// LEADER = 1: the leader's prepare_init (agg_id 0) on the same data flow -- the wire values
+// f_j(t), v and p(t) are written as the leader prepare share (out.prep_msgs is the prepare
+// share buffer, stride prep_share_len) instead of being decided against a peer's share.
+template <int GS, int PP, int PF = 1, int OCC = 3, int LEADER = 0>
 __global__ __launch_bounds__(256, OCC) void k_query_h(DevParams p, InPtrs in, Scratch sc,
                                                     OutPtrs out) {
   typedef Fp128 F;
@@ -779,7 +871,8 @@ __global__ __launch_bounds__(256, OCC) void k_query_h(DevParams p, InPtrs in, Sc
   if (r >= p.n) return;
   const size_t ld = p.ld;
   const uint32_t A = p.arity, C = p.chunk, M = p.meas_len, K = p.calls;
-  uint8_t status = PRIO3_STATUS_FINISHED;
+  uint8_t status = LEADER ? out.status[r] : PRIO3_STATUS_FINISHED;  // leader: unpack verdict
+  uint8_t* lout = LEADER ? out.prep_msgs + (size_t)r * p.prep_share_len : nullptr;
   const T t = ldf<F>(sc.qr, 0, ld, r);
   T L0, sumL = F::zero();
   // u_e = t^e / P.  PP <= 16: one in-register DFT.  PP == 32: decimation in frequency,
@@ -969,11 +1062,16 @@ __global__ __launch_bounds__(256, OCC) void k_query_h(DevParams p, InPtrs in, Sc
         mac_add(F0, ldf<F>(sc.proofs, 2 * j, ld, r), L0);
         mac_add(F0, rj, Aq);
         const T f0 = mac_reduce_f(F0);
-        mac_add(Gq, F::add(lv(1 + 2 * j), f0), F::add(lv(2 + 2 * j), f1));
+        if constexpr (LEADER) {
+          F::store(lout, 1 + 2 * j, f0);
+          F::store(lout, 2 + 2 * j, f1);
+        } else {
+          mac_add(Gq, F::add(lv(1 + 2 * j), f0), F::add(lv(2 + 2 * j), f1));
+        }
         rj = F::mul(rj, r0);
       }
     }
-    G = F::add(G, mac_reduce_f(Gq));
+    if constexpr (!LEADER) G = F::add(G, mac_reduce_f(Gq));
   }
   const T S = sum_reduce(Ssum);
   T v;
@@ -983,6 +1081,12 @@ __global__ __launch_bounds__(256, OCC) void k_query_h(DevParams p, InPtrs in, Sc
     const T r1 = ldf<F>(sc.jr, 1, ld, r);
     v = F::add(F::mul(r1, range), F::mul(F::mul(r1, r1), F::sub(S, half)));
   }
+  if constexpr (LEADER) {
+    F::store(lout, 0, v);
+    F::store(lout, A + 1, pt);
+    *(uint4*)(lout + (size_t)p.verifier_len * F::ES) = sc.part[r];
+    out.status[r] = status;
+  } else {
   const T V0 = F::add(lv(0), v);
   const T PT = F::add(lv(A + 1), pt);
   if (status == PRIO3_STATUS_FINISHED) {
@@ -1016,6 +1120,7 @@ __global__ __launch_bounds__(256, OCC) void k_query_h(DevParams p, InPtrs in, Sc
   if (status != PRIO3_STATUS_FINISHED) msg[0] = msg[1] = msg[2] = msg[3] = 0;
   ((uint4*)out.prep_msgs)[r] = make_uint4(msg[0], msg[1], msg[2], msg[3]);
   out.status[r] = status;
+  }
   if (p.kind == PRIO3_SUMVEC) {
     for (uint32_t e = 0; e < p.out_len; e++) {
       T acc = F::zero(), pw = F::one();
@@ -1801,6 +1906,10 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
     e->force_slow = (int)value;
     return PRIO3_OK;
   }
+  if (!strcmp(key, "leader_fast")) {
+    e->leader_fast = (int)value;
+    return PRIO3_OK;
+  }
   if (!strcmp(key, "fuse_acc")) {
     e->fuse_acc = (int)value;
     return PRIO3_OK;
@@ -2253,6 +2362,28 @@ int prio3_device_leader_prepare_init(prio3_engine* e, uint32_t n, const uint8_t*
   dp.n = n;
   dp.force_slow = (uint32_t)e->force_slow;
   e->leader_n = n;
+  const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
+  if (ps && dp.jr_len && (dp.P == 32 || dp.P == 16 || dp.P == 8) && e->leader_fast) {
+    // the helper kernels in their leader role
+    InPtrs in{d_nonces, d_public_shares, d_leader_input_shares, nullptr};
+    OutPtrs out{d_prep_shares, d_status};
+    const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
+    TIMED(e, st, "k_leader_unpack",
+          (k_leader_unpack<<<(n + 63) / 64, 256, 0, st>>>(dp, in, e->sc, d_status)));
+    TIMED(e, st, "k_jrpart", (k_jrpart<false, true><<<blocks, 256, 0, st>>>(dp, in, e->sc)));
+    TIMED(e, st, "k_leader_slowfix",
+          (k_leader_slowfix<<<blocks64, 64, 0, st>>>(dp, in, e->sc)));
+    if (dp.P == 32)
+      TIMED(e, st, "k_query_h",
+            (k_query_h<2, 32, 1, 3, 1><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
+    else if (dp.P == 16)
+      TIMED(e, st, "k_query_h",
+            (k_query_h<2, 16, 1, 3, 1><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
+    else
+      TIMED(e, st, "k_query_h",
+            (k_query_h<2, 8, 1, 3, 1><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
+    return PRIO3_OK;
+  }
   int rc2 = PRIO3_OK;
   TIMED(e, st, "k_leader_init",
         rc2 = launch_leader_init(dp, d_nonces, d_public_shares, d_leader_input_shares, e->sc,

@@ -41,10 +41,13 @@ def _reports(o, cfg, n, seed):
                 helper_shares=arr(hs), measurements=meas)
 
 
-@pytest.mark.parametrize("name", ["count", "sum8", "sumvec_8x10_c9", "hist_256_c16", "hist_10_c3"])
-def test_leader_parity_vs_oracle(name):
+@pytest.mark.parametrize("fast", [1, 0])
+@pytest.mark.parametrize("name", ["count", "sum8", "sumvec_8x10_c9", "hist_256_c16", "hist_10_c3",
+                                  "hist_100_c10"])
+def test_leader_parity_vs_oracle(name, fast):
     cfg = CONFIGS[name]
     o, eng = _oracle(cfg), _engine(cfg)
+    eng.set_option("leader_fast", fast)
     n = 150
     d = _reports(o, cfg, n, seed=31)
     # corrupt: a non-canonical leader measurement-share element in one report
@@ -106,8 +109,9 @@ def test_leader_parity_vs_oracle(name):
         assert agg[s].tobytes() == b"".join(v.to_bytes(es, "little") for v in tot)
 
 
-def test_leader_slow_path():
-    cfg = CONFIGS["hist_10_c3"]
+@pytest.mark.parametrize("name", ["hist_10_c3", "hist_256_c16"])
+def test_leader_slow_path(name):
+    cfg = CONFIGS[name]
     o, eng = _oracle(cfg), _engine(cfg)
     eng.set_option("force_slow_path", 1)
     d = _reports(o, cfg, 70, seed=5)
