@@ -401,7 +401,11 @@ struct prio3_engine {
   int fused_on = 0;  // last prepare_aggregate used the fused kernels
   const uint32_t* fused_seg_ptr = nullptr;
   int fuse_acc = 1;
-  int leader_fast = 1;  // option: leader role on the helper kernels (Histogram / SumVec, P <= 32)  // option: fused accumulate on/off (A/B)
+  int leader_fast = 1;
+  int chunks = 1;                  // option: prepare in this many stream-overlapped chunks
+  std::vector<hipStream_t> side;   // side streams for chunked prepare
+  std::vector<hipEvent_t> side_ev;
+  hipEvent_t fork_ev = nullptr;  // option: leader role on the helper kernels (Histogram / SumVec, P <= 32)  // option: fused accumulate on/off (A/B)
   // host-API staging
   uint32_t io_cap = 0;
   uint8_t *d_nonces = nullptr, *d_pub = nullptr, *d_helper = nullptr, *d_leader = nullptr,
@@ -410,7 +414,7 @@ struct prio3_engine {
   uint32_t linput_cap = 0;
   uint32_t leader_n = 0;
   int force_slow = 0;
-  int split_xof = 1;
+  int split_xof = 2;  // 2: dual-state k_xofd, 1: k_xof_a + k_jrpart, 0: generic fused k_xof
   int qh_prefetch = 1;
   int qh_occ = 3;
   int qh_regs = 0;

@@ -31,8 +31,11 @@
 
 #include "prio3_common.h"
 
+#ifndef XOFD_OCC
+#define XOFD_OCC 3
+#endif
 template <class F>
-__global__ __launch_bounds__(256) void k_xof(DevParams p, InPtrs in, Scratch sc) {
+__global__ __launch_bounds__(256, XOFD_OCC) void k_xof(DevParams p, InPtrs in, Scratch sc) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= p.n) return;
   constexpr uint32_t ES = F::ES;
@@ -98,7 +101,19 @@ __global__ __launch_bounds__(256) void k_xof(DevParams p, InPtrs in, Scratch sc)
   for (uint32_t b = 0; b < nb; b++) {
     const bool hasW = b < K;
     if (hasW) squeeze_block<F>(p, ms, b, M, pend0, pend1, sc.meas, r, flag);
-    if (JR) {
+    if (JR && b < B) {  // full block: each message word goes straight into the state
+      const uint32_t w0 = hasW ? kword(ms, 0) : 0u;
+#pragma unroll
+      for (int j = 0; j < 10; j++)
+        kxor_word(js, j, b == 0 ? pre[j] : __builtin_amdgcn_alignbit(tail[j + 1], tail[j], 16));
+      kxor_word(js, 10, b == 0 ? ((pre[10] & 0xffffu) | (w0 << 16))
+                               : __builtin_amdgcn_alignbit(w0, tail[10], 16));
+#pragma unroll
+      for (int j = 11; j < 42; j++)
+        kxor_word(js, j, hasW ? __builtin_amdgcn_alignbit(kword(ms, j - 10), kword(ms, j - 11), 16)
+                              : 0u);
+      keccak_p12(js);
+    } else if (JR) {
       uint32_t x[42];
 #pragma unroll
       for (int j = 0; j < 10; j++)
@@ -109,11 +124,7 @@ __global__ __launch_bounds__(256) void k_xof(DevParams p, InPtrs in, Scratch sc)
 #pragma unroll
       for (int j = 11; j < 42; j++)
         x[j] = hasW ? __builtin_amdgcn_alignbit(kword(ms, j - 10), kword(ms, j - 11), 16) : 0u;
-      if (b < B) {
-#pragma unroll
-        for (int j = 0; j < 42; j++) kxor_word(js, j, x[j]);
-        keccak_p12(js);
-      } else {
+      {
 #pragma unroll
         for (int j = 0; j < 42; j++) {
           const uint32_t lo = 4 * j;
@@ -186,6 +197,219 @@ __global__ __launch_bounds__(256) void k_xof(DevParams p, InPtrs in, Scratch sc)
     sc.corrected[r] = make_uint4(cor[0], cor[1], cor[2], cor[3]);
   }
   sc.flag[r] = (uint8_t)flag;
+}
+
+
+// ------------------------------------------------------------------------------------
+// k_xofd: k_xof_a + k_jrpart in one pass with two live Keccak states -- each squeezed
+// measurement-share block is absorbed into the joint-rand-part sponge while still in
+// registers (no 4 KiB re-read), the two permutation streams give each wave 2x the ILP.
+// Field128 joint-randomness instances with at least three joint-rand blocks; peeled first and
+// last blocks keep the steady-state loop free of the prefix / padding code.
+// ------------------------------------------------------------------------------------
+// FUSE: the optimistic per-segment aggregate of the fused path (see k_jrpart<true>) is taken
+// here, from the squeezed elements while they are in registers; a wave in which any report got
+// flagged for the slow path is un-fused at the end (its partials are ignored, its reports go
+// through the fix-up list with their corrected shares).
+template <bool FUSE>
+__global__ __launch_bounds__(256, XOFD_OCC) void k_xofd(DevParams p, InPtrs in, Scratch sc) {
+  typedef Fp128 F;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  bool fuse = false;
+  uint32_t s0 = 0;
+  if constexpr (FUSE) {
+    const bool valid = r < p.n;
+    const uint32_t sg = valid ? (sc.seg ? sc.seg[r] : 0u) : 0xffffffffu;
+    s0 = (uint32_t)__shfl((int)sg, 0);
+    fuse = __all(valid && sg == s0);
+    if (lane == 0 && (r - lane) < p.n && !fuse) sc.wseg[r >> 6] = 0xffffffffu;
+  }
+  if (r >= p.n) return;
+  uint32_t flag = p.force_slow;
+  uint32_t nonce[4], km[4], kp[4], kb[4];
+  load16(in.nonces + 16 * (size_t)r, nonce);
+  const uint8_t* hs = in.helper + (size_t)r * p.helper_share_len;
+  load16(hs, km);
+  load16(hs + 16, kp);
+  load16(hs + 32, kb);
+  {  // query randomness
+    KState s;
+    kzero(s);
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[5]);
+    msg_bytes16(m, 9, p.vk);
+    msg_byte(m, 25, 1);
+    msg_bytes16(m, 26, nonce);
+    msg_absorb_final(s, m, 42);
+    uint32_t w[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
+    put_elem<F>(p, sc.qr, 0, r, w, flag);
+  }
+  const uint32_t M = p.meas_len, K = (M * 16 + 167) / 168;
+  const uint32_t L = 42 + M * 16, B = L / 168, rem = L % 168;  // B >= 2 (checked on the host)
+  KState ms, js;
+  kzero(ms);
+  kzero(js);
+  {
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[1]);
+    msg_bytes16(m, 9, km);
+    msg_byte(m, 25, 1);
+    msg_absorb_final(ms, m, 26);
+  }
+  uint32_t tail[11];
+  uint32_t pend0 = 0, pend1 = 0;
+  const int Mi = (int)M;
+  // wave totals of share elements e0, e0+1 (zero outside [0, M)), slot lane of lanes 0..15
+  auto fused_pair = [&](int e0, const f128& a, const f128& b2) __attribute__((always_inline)) {
+    if (e0 >= Mi) return;  // wave-uniform
+    const uint32_t tot = wave_halfsum2(a, b2, lane);
+    const int e = e0 + (int)((lane >> 3) & 1u);
+    if (lane < 16 && e < Mi)
+      sc.wpart[((size_t)(r >> 6) * M + (uint32_t)e) * 8u + (lane & 7u)] = tot;
+  };
+  // the elements squeezed from share block b (state ms, pend = carried half element)
+  auto fuse_block = [&](uint32_t b, uint32_t q0, uint32_t q1) __attribute__((always_inline)) {
+    const int e0 = 21 * (int)(b >> 1);
+    const f128 z = zero128();
+    if ((b & 1) == 0) {
+#pragma unroll
+      for (int t = 0; t < 10; t += 2)
+        fused_pair(e0 + t, mk128(kword(ms, 4 * t), kword(ms, 4 * t + 1), kword(ms, 4 * t + 2),
+                                 kword(ms, 4 * t + 3)),
+                   mk128(kword(ms, 4 * t + 4), kword(ms, 4 * t + 5), kword(ms, 4 * t + 6),
+                         kword(ms, 4 * t + 7)));
+    } else {
+      fused_pair(e0 + 10, mk128(q0, q1, kword(ms, 0), kword(ms, 1)),
+                 mk128(kword(ms, 2), kword(ms, 3), kword(ms, 4), kword(ms, 5)));
+#pragma unroll
+      for (int t = 1; t < 10; t += 2)
+        fused_pair(e0 + 11 + t,
+                   mk128(kword(ms, 2 + 4 * t), kword(ms, 3 + 4 * t), kword(ms, 4 + 4 * t),
+                         kword(ms, 5 + 4 * t)),
+                   t + 1 < 10 ? mk128(kword(ms, 6 + 4 * t), kword(ms, 7 + 4 * t),
+                                      kword(ms, 8 + 4 * t), kword(ms, 9 + 4 * t))
+                              : z);
+    }
+  };
+  // block 0: prefix (42 bytes) + the first 126 bytes of the share
+  {
+    if (FUSE && fuse) fuse_block(0, 0, 0);
+    squeeze_block<F>(p, ms, 0, M, pend0, pend1, sc.meas, r, flag);
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[7]);
+    msg_bytes16(m, 9, kb);
+    msg_byte(m, 25, 1);
+    msg_bytes16(m, 26, nonce);
+#pragma unroll
+    for (int j = 0; j < 10; j++) kxor_word(js, j, m.w[j]);
+    kxor_word(js, 10, (m.w[10] & 0xffffu) | (kword(ms, 0) << 16));
+#pragma unroll
+    for (int j = 11; j < 42; j++)
+      kxor_word(js, j, __builtin_amdgcn_alignbit(kword(ms, j - 10), kword(ms, j - 11), 16));
+#pragma unroll
+    for (int t = 0; t < 11; t++) tail[t] = kword(ms, 31 + t);
+    keccak_p12(js);
+    keccak_p12(ms);
+  }
+  // full joint-rand blocks 1 .. B-1 (share blocks b-1 tail + block b head)
+#pragma unroll 1
+  for (uint32_t b = 1; b < B; b++) {
+    const bool hasW = b < K;  // wave-uniform
+    if (FUSE && fuse && hasW) fuse_block(b, pend0, pend1);
+    if (hasW) squeeze_block<F>(p, ms, b, M, pend0, pend1, sc.meas, r, flag);
+#pragma unroll
+    for (int j = 0; j < 10; j++)
+      kxor_word(js, j, __builtin_amdgcn_alignbit(tail[j + 1], tail[j], 16));
+    kxor_word(js, 10, __builtin_amdgcn_alignbit(hasW ? kword(ms, 0) : 0u, tail[10], 16));
+    if (hasW) {
+#pragma unroll
+      for (int j = 11; j < 42; j++)
+        kxor_word(js, j, __builtin_amdgcn_alignbit(kword(ms, j - 10), kword(ms, j - 11), 16));
+#pragma unroll
+      for (int t = 0; t < 11; t++) tail[t] = kword(ms, 31 + t);
+    }
+    keccak_p12(js);
+    if (b + 1 < K) keccak_p12(ms);
+  }
+  // final joint-rand block B: remaining share bytes, padding
+  uint32_t part[4];
+  {
+    const bool hasW = B < K;
+    if (FUSE && fuse && hasW) fuse_block(B, pend0, pend1);
+    if (hasW) squeeze_block<F>(p, ms, B, M, pend0, pend1, sc.meas, r, flag);
+#pragma unroll
+    for (int j = 0; j < 42; j++) {
+      uint32_t x;
+      if (j < 10) x = __builtin_amdgcn_alignbit(tail[j + 1], tail[j], 16);
+      else if (j == 10) x = __builtin_amdgcn_alignbit(hasW ? kword(ms, 0) : 0u, tail[10], 16);
+      else x = hasW ? __builtin_amdgcn_alignbit(kword(ms, j - 10), kword(ms, j - 11), 16) : 0u;
+      const uint32_t lo = 4 * j;
+      const uint32_t mask = (lo + 4 <= rem) ? 0xffffffffu
+                                            : (lo >= rem ? 0u : ((1u << (8 * (rem - lo))) - 1u));
+      x &= mask;
+      if ((uint32_t)j == (rem >> 2)) x ^= 1u << (8 * (rem & 3));
+      if (j == 41) x ^= 0x80000000u;
+      kxor_word(js, j, x);
+    }
+    keccak_p12(js);
+    part[0] = kword(js, 0);
+    part[1] = kword(js, 1);
+    part[2] = kword(js, 2);
+    part[3] = kword(js, 3);
+  }
+  {  // proofs share
+    KState s;
+    kzero(s);
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[2]);
+    msg_bytes16(m, 9, kp);
+    msg_byte(m, 25, 1);
+    msg_byte(m, 26, 1);
+    msg_absorb_final(s, m, 27);
+    const uint32_t PL = p.proof_len, Kp = (PL * 16 + 167) / 168;
+    uint32_t q0 = 0, q1 = 0;
+    for (uint32_t b = 0; b < Kp; b++) {
+      squeeze_block<F>(p, s, b, PL, q0, q1, sc.proofs, r, flag);
+      if (b + 1 < Kp) keccak_p12(s);
+    }
+  }
+  {  // corrected seed, joint randomness
+    uint32_t pub0[4];
+    load16(in.pub + (size_t)r * p.public_share_len, pub0);
+    KState s;
+    kzero(s);
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[6]);
+    msg_bytes16(m, 25, pub0);
+    msg_bytes16(m, 41, part);
+    msg_absorb_final(s, m, 57);
+    uint32_t cor[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
+    KState t;
+    kzero(t);
+    Msg m2;
+    msg_zero(m2);
+    msg_dst(m2, p.dst[3]);
+    msg_bytes16(m2, 9, cor);
+    msg_byte(m2, 25, 1);
+    msg_absorb_final(t, m2, 26);
+    uint32_t q0 = 0, q1 = 0;
+    squeeze_block<F>(p, t, 0, p.jr_len, q0, q1, sc.jr, r, flag);
+    sc.part[r] = make_uint4(part[0], part[1], part[2], part[3]);
+    sc.corrected[r] = make_uint4(cor[0], cor[1], cor[2], cor[3]);
+  }
+  sc.flag[r] = (uint8_t)flag;
+  if constexpr (FUSE) {
+    if (fuse) {  // all 64 lanes are live here
+      const bool anyflag = __any(flag != 0);
+      if (lane == 0) sc.wseg[r >> 6] = anyflag ? 0xffffffffu : s0;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -1896,6 +2120,10 @@ void prio3_engine_destroy(prio3_engine* e) {
   for (auto b : bufs)
     if (b) (void)hipFree(b);
   for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
+  for (auto s2 : e->side) (void)hipStreamDestroy(s2);
+  for (auto j : e->side_ev) (void)hipEventDestroy(j);
+  if (e->fork_ev) (void)hipEventDestroy(e->fork_ev);
+  for (auto s2 : e->side) (void)hipStreamDestroy(s2);
   (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -1904,6 +2132,10 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
   if (!e || !key) return PRIO3_EINVAL;
   if (!strcmp(key, "force_slow_path")) {
     e->force_slow = (int)value;
+    return PRIO3_OK;
+  }
+  if (!strcmp(key, "chunks")) {
+    e->chunks = (int)value;
     return PRIO3_OK;
   }
   if (!strcmp(key, "leader_fast")) {
@@ -1940,7 +2172,8 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
 // The fused accumulate applies where the output share is the measurement share (Histogram;
 // truncate is the identity) and the joint-rand kernel streams that share.
 static bool fusable(const prio3_engine* e) {
-  return e->fuse_acc && e->dp.kind == PRIO3_HISTOGRAM && e->dp.jr_len && e->split_xof;
+  return e->fuse_acc && e->dp.kind == PRIO3_HISTOGRAM && e->dp.jr_len &&
+         (e->split_xof == 1 || (e->split_xof == 2 && (42 + e->dp.meas_len * 16) / 168 >= 2));
 }
 
 static int ensure_fused(prio3_engine* e, uint32_t n, uint32_t n_segments) {
@@ -1974,6 +2207,74 @@ static int ensure_fused(prio3_engine* e, uint32_t n, uint32_t n_segments) {
   return PRIO3_OK;
 }
 
+// The kernel sequence for reports [c0, c0 + n) of the batch: every pointer is shifted to the
+// chunk (SoA scratch keeps the batch's leading dimension, so a chunk is a column range).
+static int launch_prepare(prio3_engine* e, uint32_t c0, uint32_t n, InPtrs in, OutPtrs out,
+                          Scratch sc, hipStream_t st, bool fuse) {
+  DevParams dp = e->dp;
+  dp.n = n;
+  dp.force_slow = (uint32_t)e->force_slow;
+  const size_t es = dp.es;
+  in.nonces += 16 * (size_t)c0;
+  if (in.pub) in.pub += (size_t)dp.public_share_len * c0;
+  in.helper += (size_t)dp.helper_share_len * c0;
+  in.leader += (size_t)dp.prep_share_len * c0;
+  out.prep_msgs += 16 * (size_t)c0;
+  out.status += c0;
+  void** soa[] = {&sc.meas, &sc.proofs, &sc.jr, &sc.qr, &sc.Lbuf, &sc.PVbuf, &sc.acc, &sc.out,
+                  &sc.beta};
+  for (auto q : soa)
+    if (*q) *q = (uint8_t*)*q + es * c0;
+  sc.part += c0;
+  sc.corrected += c0;
+  sc.flag += c0;
+  if (sc.seg) sc.seg += c0;
+  if (sc.wseg) sc.wseg += c0 / 64;
+  if (sc.wpart) sc.wpart += (size_t)(c0 / 64) * dp.meas_len * 8;
+  const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
+  if (dp.es == 16) {
+    if (dp.jr_len && e->split_xof == 2 && (42 + dp.meas_len * 16) / 168 >= 2) {
+      if (fuse)
+        TIMED(e, st, "k_xofd", (k_xofd<true><<<blocks, 256, 0, st>>>(dp, in, sc)));
+      else
+        TIMED(e, st, "k_xofd", (k_xofd<false><<<blocks, 256, 0, st>>>(dp, in, sc)));
+    } else if (dp.jr_len && e->split_xof) {
+      TIMED(e, st, "k_xof_a", (k_xof_a<Fp128><<<blocks, 256, 0, st>>>(dp, in, sc)));
+      if (fuse)
+        TIMED(e, st, "k_jrpart", (k_jrpart<true><<<blocks, 256, 0, st>>>(dp, in, sc)));
+      else
+        TIMED(e, st, "k_jrpart", (k_jrpart<false><<<blocks, 256, 0, st>>>(dp, in, sc)));
+    } else {
+      TIMED(e, st, "k_xof", (k_xof<Fp128><<<blocks, 256, 0, st>>>(dp, in, sc)));
+    }
+    TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp128><<<blocks64, 64, 0, st>>>(dp, in, sc)));
+    const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
+    if (ps && dp.P == 32 && dp.chunk == 16 && dp.calls == 16 && e->qh_regs)
+      TIMED(e, st, "k_query_r", (k_query_r<16, 16><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+    else if (ps && dp.P == 32)
+      switch (e->qh_prefetch * 10 + e->qh_occ) {
+        case 2: TIMED(e, st, "k_query_h", (k_query_h<2, 32, 0, 2><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
+        case 3: TIMED(e, st, "k_query_h", (k_query_h<2, 32, 0, 3><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
+        case 12: TIMED(e, st, "k_query_h", (k_query_h<2, 32, 1, 2><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
+        default: TIMED(e, st, "k_query_h", (k_query_h<2, 32, 1, 3><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
+      }
+    else if (ps && dp.P == 16)
+      TIMED(e, st, "k_query_h", (k_query_h<2, 16><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+    else if (ps && dp.P == 8)
+      TIMED(e, st, "k_query_h", (k_query_h<2, 8><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+    else if (ps)
+      TIMED(e, st, "k_query_ps", (k_query_ps<4><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+    else
+      TIMED(e, st, "k_query", (k_query<Fp128><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+  } else {
+    TIMED(e, st, "k_xof", (k_xof<Fp64><<<blocks, 256, 0, st>>>(dp, in, sc)));
+    TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp64><<<blocks64, 64, 0, st>>>(dp, in, sc)));
+    TIMED(e, st, "k_query", (k_query<Fp64><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+  }
+  return PRIO3_OK;
+}
+
+
 static int prepare_impl(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
                         const uint8_t* d_public_shares, const uint8_t* d_helper_shares,
                         const uint8_t* d_leader_prep_shares, uint8_t* d_prep_msgs,
@@ -1984,45 +2285,33 @@ static int prepare_impl(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
   sc.seg = d_seg;
   sc.wpart = e->d_wpart;
   sc.wseg = e->d_wseg;
-  DevParams dp = e->dp;
-  dp.n = n;
-  dp.force_slow = (uint32_t)e->force_slow;
   InPtrs in{d_nonces, d_public_shares, d_helper_shares, d_leader_prep_shares};
   OutPtrs out{d_prep_msgs, d_status};
-  const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
-  if (dp.es == 16) {
-    if (dp.jr_len && e->split_xof) {
-      TIMED(e, st, "k_xof_a", (k_xof_a<Fp128><<<blocks, 256, 0, st>>>(dp, in, e->sc)));
-      if (fuse)
-        TIMED(e, st, "k_jrpart", (k_jrpart<true><<<blocks, 256, 0, st>>>(dp, in, sc)));
-      else
-        TIMED(e, st, "k_jrpart", (k_jrpart<false><<<blocks, 256, 0, st>>>(dp, in, sc)));
-    } else {
-      TIMED(e, st, "k_xof", (k_xof<Fp128><<<blocks, 256, 0, st>>>(dp, in, e->sc)));
-    }
-    TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp128><<<blocks64, 64, 0, st>>>(dp, in, e->sc)));
-    const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
-    if (ps && dp.P == 32 && dp.chunk == 16 && dp.calls == 16 && e->qh_regs)
-      TIMED(e, st, "k_query_r", (k_query_r<16, 16><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
-    else if (ps && dp.P == 32)
-      switch (e->qh_prefetch * 10 + e->qh_occ) {
-        case 2: TIMED(e, st, "k_query_h", (k_query_h<2, 32, 0, 2><<<blocks, 256, 0, st>>>(dp, in, e->sc, out))); break;
-        case 3: TIMED(e, st, "k_query_h", (k_query_h<2, 32, 0, 3><<<blocks, 256, 0, st>>>(dp, in, e->sc, out))); break;
-        case 12: TIMED(e, st, "k_query_h", (k_query_h<2, 32, 1, 2><<<blocks, 256, 0, st>>>(dp, in, e->sc, out))); break;
-        default: TIMED(e, st, "k_query_h", (k_query_h<2, 32, 1, 3><<<blocks, 256, 0, st>>>(dp, in, e->sc, out))); break;
-      }
-    else if (ps && dp.P == 16)
-      TIMED(e, st, "k_query_h", (k_query_h<2, 16><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
-    else if (ps && dp.P == 8)
-      TIMED(e, st, "k_query_h", (k_query_h<2, 8><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
-    else if (ps)
-      TIMED(e, st, "k_query_ps", (k_query_ps<4><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
-    else
-      TIMED(e, st, "k_query", (k_query<Fp128><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
-  } else {
-    TIMED(e, st, "k_xof", (k_xof<Fp64><<<blocks, 256, 0, st>>>(dp, in, e->sc)));
-    TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp64><<<blocks64, 64, 0, st>>>(dp, in, e->sc)));
-    TIMED(e, st, "k_query", (k_query<Fp64><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
+  // Option "chunks" > 1: the batch is cut into column ranges whose kernel chains run on the
+  // engine's side streams, so one chunk's memory-bound query overlaps the next chunk's
+  // VALU-bound Keccak (the caller's stream is joined before and after).
+  const uint32_t K = (uint32_t)std::max(1, e->chunks);
+  const uint32_t csz = ((n + K - 1) / K + 255) & ~255u;
+  if (K == 1 || n <= csz) return launch_prepare(e, 0, n, in, out, sc, st, fuse);
+  while (e->side.size() < 2) {  // side streams + their join events, created once per engine
+    hipStream_t s2;
+    hipEvent_t j;
+    HIPCHK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&j, hipEventDisableTiming));
+    e->side.push_back(s2);
+    e->side_ev.push_back(j);
+  }
+  if (!e->fork_ev) HIPCHK(hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(e->fork_ev, st));
+  for (auto s2 : e->side) HIPCHK(hipStreamWaitEvent(s2, e->fork_ev, 0));
+  uint32_t c = 0;
+  for (uint32_t c0 = 0; c0 < n; c0 += csz, c++) {
+    rc = launch_prepare(e, c0, std::min(csz, n - c0), in, out, sc, e->side[c % 2], fuse);
+    if (rc) return rc;
+  }
+  for (size_t i = 0; i < e->side.size(); i++) {
+    HIPCHK(hipEventRecord(e->side_ev[i], e->side[i]));
+    HIPCHK(hipStreamWaitEvent(st, e->side_ev[i], 0));
   }
   return PRIO3_OK;
 }
