@@ -38,6 +38,7 @@ COUNTS_PATH = os.path.join(ROOT, "profiles", "kernel_counts.json")
 # per-report HBM bytes each kernel must move at minimum (algorithmic; Histogram(256,16))
 KERNEL_BYTES = {"k_xof_a": 16 + 16 + 16 + 256 * 16 + 95 * 16,  # nonce, k_meas, k_proofs in; shares out
                 "k_jrpart": 16 + 16 + 32 + 256 * 16 + 2 * 16 + 16,
+                "k_xofd": 16 + 48 + 32 + 256 * 16 + 95 * 16 + 16 + 16 + 3 * 16,  # + jr/qr/part out
                 "k_query_h": 256 * 16 + 95 * 16 + 560 + 2 * 16 + 16 + 16 + 17,
                 "k_acc_partial": 256 * 16 + 1}
 PEAK_VALU_NOMINAL = 256 * 4 * 32 * 2.4e9  # 78.6e12 lane-instr/s, full-rate VALU at 2.4 GHz
@@ -111,9 +112,12 @@ def main():
 
     eng = J.HelperEngine(J.Prio3Histogram(256, 16), VK, device=local)
     sz = eng.sz
+    chunks_opt = 0  # engine default: auto
     for kv in args.opt:
         k, v = kv.split("=")
         eng.set_option(k, int(v))
+        if k == "chunks":
+            chunks_opt = int(v)
     data = eng.generate_reports_device(n, seed=0x4A414E5553000001, first_index=rank * n,
                                        with_checks=True)
     torch.cuda.synchronize()
@@ -155,12 +159,23 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    times = eng.timing()
-    eng.set_option("timing", 0)
+    step_times = eng.timing()
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # Roofline pass (after the timed region): the engine cuts a 1Mi batch into 8 chunks whose
+    # kernels overlap on two streams, so a launch's duration there includes its neighbour's
+    # share of the CU.  The per-kernel roofline is taken from whole-batch launches in isolation
+    # (option chunks=1), a few steps on the same stream and data.
+    eng.set_option("chunks", 1)
+    eng.timing_reset()
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    times = eng.timing()
+    eng.set_option("timing", 0)
+    eng.set_option("chunks", chunks_opt)
 
     ok = int((status == 0).sum().item())
     final_cnt = int((combiner.out_cnt if combiner is not None else cnt)[0].item())
@@ -201,6 +216,7 @@ def main():
                            reports_per_gpu=n, global_batch=world * n,
                            parallelism=f"dp{world} (report shards; RCCL all-gather + mod-p combine)"),
                roofline=roofline, kernels=per_kernel,
+               kernels_timed_region={k: dict(ms_total=v[0], launches=v[1]) for k, v in step_times.items()},
                checks=dict(finished=ok, generator_flags=flags, agg_count=final_cnt))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb, (msgs, cst, cagg, ccnt) = cpu_baseline(eng, data, min(n, 1 << 20), args.cpu_seconds)

@@ -402,7 +402,8 @@ struct prio3_engine {
   const uint32_t* fused_seg_ptr = nullptr;
   int fuse_acc = 1;
   int leader_fast = 1;
-  int chunks = 1;                  // option: prepare in this many stream-overlapped chunks
+  int chunks = 0;                  // option: prepare in this many stream-overlapped chunks
+                                   // (0 = auto: one chunk per 128Ki reports)
   std::vector<hipStream_t> side;   // side streams for chunked prepare
   std::vector<hipEvent_t> side_ev;
   hipEvent_t fork_ev = nullptr;  // option: leader role on the helper kernels (Histogram / SumVec, P <= 32)  // option: fused accumulate on/off (A/B)

@@ -17,13 +17,15 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(cfg, n, seed, n_segments=1, seg_mode="runs", tamper=True, accept_frac=0.9,
-         force_slow=False, fuse=True):
+         force_slow=False, fuse=True, chunks=None):
     import torch
     o = _oracle(cfg)
     eng = _engine(cfg)
     eng.set_option("fuse_acc", int(fuse))
     if force_slow:
         eng.set_option("force_slow_path", 1)
+    if chunks is not None:
+        eng.set_option("chunks", chunks)
     d = o.gen_reports(VK, n, seed=seed, n_threads=8)
     rng = np.random.default_rng(seed)
     if tamper:
@@ -93,3 +95,14 @@ def test_prepare_aggregate_other_instances(name):
 
 def test_fused_off_matches():
     _run(CONFIGS["hist_256_c16"], 700, seed=9, n_segments=2, fuse=False)
+
+
+@pytest.mark.parametrize("chunks", [2, 3, 5])
+def test_fused_stream_overlapped_chunks(chunks):
+    """The batch cut into column chunks on two side streams (the engine's default above 192Ki
+    reports): chunk boundaries fall inside segments and the wave partials stay aligned."""
+    _run(CONFIGS["hist_256_c16"], 1500, seed=10 + chunks, n_segments=5, chunks=chunks)
+
+
+def test_chunks_unfused_instance():
+    _run(CONFIGS["sumvec_8x10_c9"], 1100, seed=20, n_segments=2, chunks=3)
