@@ -127,22 +127,34 @@ def main():
     seg = torch.zeros(n, dtype=torch.int32, device=dev)
     agg = torch.zeros((1, sz.agg_share_len), dtype=torch.uint8, device=dev)
     cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    # report timestamps (seconds) inside one hour-long batch interval, seeded
+    g = torch.Generator(device=dev).manual_seed(0x4A414E55 + rank)
+    report_times = 1_700_000_000 + torch.randint(0, 3600, (n,), generator=g, device=dev,
+                                          dtype=torch.int64)
+    cks = torch.zeros((1, 32), dtype=torch.uint8, device=dev)
+    ivs = torch.zeros((1, 2), dtype=torch.int64, device=dev)
     combiner = None
     if world > 1:
         from janus_amd.dist import AggregateCombiner
+        cur = lambda: torch.cuda.current_stream().cuda_stream
         combiner = AggregateCombiner(
             dist, agg, cnt,
-            lambda k, ga, gc, oa, oc: eng.combine_device(k, 1, ga, gc, oa, oc,
-                                                         stream=torch.cuda.current_stream().cuda_stream))
+            lambda k, ga, gc, oa, oc: eng.combine_device(k, 1, ga, gc, oa, oc, stream=cur()),
+            cks, ivs,
+            lambda k, gk, gi, ok, oi: eng.combine_metadata_device(k, 1, gk, gi, ok, oi,
+                                                                  stream=cur()))
 
     def step():
+        # SURVEY 8(a) a3-a11 + a14: prepare, decide, prepare message, and the per-segment batch
+        # aggregation update (aggregate share, count, report-ID checksum, client interval)
         s = torch.cuda.current_stream().cuda_stream
         eng.prepare_aggregate_device(data["nonces"], data["public_shares"], data["helper_shares"],
                                      data["leader_prep_shares"], seg, 1, prep_msgs, status,
                                      stream=s)
         eng.aggregate_finish_device(status, None, agg, cnt, stream=s)
+        eng.batch_metadata_device(data["nonces"], report_times, status, None, seg, 1, cks, ivs, stream=s)
         if combiner is not None:
-            combiner(agg, cnt)
+            combiner(agg, cnt, cks, ivs)
 
     for _ in range(args.warmup):
         step()
@@ -225,6 +237,12 @@ def main():
         gs = status[:m].cpu().numpy()
         out["checks"]["cpu_gpu_parity_on_sample"] = bool(np.array_equal(gs, cst) and
                                                          np.array_equal(gm, msgs))
+        from oracle.oracle import batch_metadata
+        eck, eiv = batch_metadata(data["nonces"].cpu().numpy(), report_times.cpu().numpy(),
+                                  status.cpu().numpy(), None, None, 1)
+        out["checks"]["batch_metadata_parity"] = bool(
+            np.array_equal(cks.cpu().numpy(), eck) and
+            np.array_equal(ivs.cpu().numpy().view(np.uint64), eiv))
         out["cpu_baseline"] = cb
         out["speedup_vs_cpu"] = value / cb["value"]
     if rank == 0:

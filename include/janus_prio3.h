@@ -144,6 +144,34 @@ int prio3_device_prepare_aggregate(prio3_engine* engine, uint32_t n, const uint8
 int prio3_device_aggregate_finish(prio3_engine* engine, const uint8_t* d_status,
                                   const uint8_t* d_accept_mask, uint8_t* d_agg_shares,
                                   uint64_t* d_counts, void* stream);
+/* The rest of the per-segment BatchAggregation update (aggregation_job_writer.rs:637-690,
+ * models.rs:1318-1372), for the same batch and verdicts:
+ *   d_checksums[n_segments][32]  ReportIdChecksum = XOR of SHA-256(report_id) over the reports
+ *                                counted in d_counts (status FINISHED and accept mask non-zero;
+ *                                core/src/report_id.rs:18-42);
+ *   d_intervals[n_segments][2]   client-timestamp interval (start, duration) in seconds over
+ *                                every report of the segment, failed ones included
+ *                                (Interval::from_time + merge, core/src/time.rs:294-317);
+ *                                (0, 0) = Interval::EMPTY for a segment without reports.
+ * d_report_ids[n][16] are the report IDs (the VDAF nonces), d_times[n] the report timestamps
+ * (NULL: intervals not computed).  Either output may be NULL.  Both are overwritten; merging
+ * them into the batch aggregation already stored (XOR / Interval::merge) is the caller's. */
+int prio3_device_batch_metadata(prio3_engine* engine, uint32_t n, const uint8_t* d_report_ids,
+                                const uint64_t* d_times, const uint8_t* d_status,
+                                const uint8_t* d_accept_mask, const uint32_t* d_segment_ids,
+                                uint32_t n_segments, uint8_t* d_checksums, uint64_t* d_intervals,
+                                void* stream);
+/* Multi-GPU combine of k ranks' metadata after an all-gather: d_checksums_in[k][n_segments][32]
+ * XORed, d_intervals_in[k][n_segments][2] merged (Interval::merge, empty = identity). */
+int prio3_device_combine_metadata(prio3_engine* engine, uint32_t k, uint32_t n_segments,
+                                  const uint8_t* d_checksums_in, const uint64_t* d_intervals_in,
+                                  uint8_t* d_checksums_out, uint64_t* d_intervals_out,
+                                  void* stream);
+/* Host-buffer form of prio3_device_batch_metadata (blocking). */
+int prio3_batch_metadata(prio3_engine* engine, uint32_t n, const uint8_t* report_ids,
+                         const uint64_t* times, const uint8_t* status, const uint8_t* accept_mask,
+                         const uint32_t* segment_ids, uint32_t n_segments, uint8_t* checksums_out,
+                         uint64_t* intervals_out);
 /* Copies the output shares of the last device prepare (n x agg_share_len) to host. */
 int prio3_device_output_shares(prio3_engine* engine, uint32_t n, uint8_t* out);
 

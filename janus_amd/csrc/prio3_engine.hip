@@ -1821,6 +1821,193 @@ __global__ void k_combine(uint32_t k, uint32_t len, uint32_t n_segments, const u
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Batch metadata of the per-segment BatchAggregation: besides the
+// aggregate share and the count, every finished report XORs SHA-256(report_id) into the
+// segment's ReportIdChecksum (core/src/report_id.rs:18-42, called from
+// aggregation_job_writer.rs:650-656) and every report aggregation of the segment widens its
+// client-timestamp interval (Interval::from_time + merge, core/src/time.rs:294-317; merged for
+// failed reports too, aggregation_job_writer.rs:643-647).
+// One report per lane: one SHA-256 compression of the padded 16-byte ID, then a block-level
+// XOR / min / max reduction when the block's 256 reports share a segment (the common case:
+// contiguous batches) and per-report atomics on the segment otherwise.
+// ------------------------------------------------------------------------------------
+__constant__ uint32_t c_sha256_k[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u,
+    0xab1c5ed5u, 0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu,
+    0x9bdc06a7u, 0xc19bf174u, 0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu,
+    0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau, 0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u,
+    0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u, 0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu,
+    0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u, 0xa2bfe8a1u, 0xa81a664bu,
+    0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u, 0x19a4c116u,
+    0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u,
+    0xc67178f2u};
+
+DEV uint32_t rotr32(uint32_t x, uint32_t n) { return __builtin_amdgcn_alignbit(x, x, n); }
+
+// SHA-256 of the 16 bytes id[0..3] (little-endian words as loaded); the digest is returned as
+// 8 little-endian words of its byte string (so a byte-wise XOR is a word-wise XOR).
+DEV void sha256_id16(const uint32_t id[4], uint32_t out[8]) {
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 4; i++) w[i] = __builtin_bswap32(id[i]);
+  w[4] = 0x80000000u;
+#pragma unroll
+  for (int i = 5; i < 15; i++) w[i] = 0;
+  w[15] = 128;  // message length in bits
+  uint32_t a = 0x6a09e667u, b = 0xbb67ae85u, c = 0x3c6ef372u, d = 0xa54ff53au;
+  uint32_t e = 0x510e527fu, f = 0x9b05688cu, g = 0x1f83d9abu, h = 0x5be0cd19u;
+#pragma unroll
+  for (int t = 0; t < 64; t++) {
+    uint32_t wt;
+    if (t < 16) {
+      wt = w[t];
+    } else {  // rolling 16-word schedule
+      const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+      const uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
+      const uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+      wt = w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+    }
+    const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+    const uint32_t ch = (e & f) ^ (~e & g);
+    const uint32_t t1 = h + S1 + ch + c_sha256_k[t] + wt;
+    const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+    const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    h = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + S0 + mj;
+  }
+  const uint32_t H[8] = {a + 0x6a09e667u, b + 0xbb67ae85u, c + 0x3c6ef372u, d + 0xa54ff53au,
+                         e + 0x510e527fu, f + 0x9b05688cu, g + 0x1f83d9abu, h + 0x5be0cd19u};
+#pragma unroll
+  for (int i = 0; i < 8; i++) out[i] = __builtin_bswap32(H[i]);
+}
+
+// checksums[s][8 words] = 0, intervals[s] = (UINT64_MAX, 0) as a (min start, max end) pair
+__global__ void k_meta_init(uint32_t n_segments, uint32_t* ck, unsigned long long* iv) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_segments) return;
+  if (ck)
+    for (int i = 0; i < 8; i++) ck[8 * s + i] = 0;
+  if (iv) {
+    iv[2 * s] = ~0ull;
+    iv[2 * s + 1] = 0;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_meta(uint32_t n, const uint8_t* ids, const uint64_t* times,
+                                            const uint8_t* status, const uint8_t* mask,
+                                            const uint32_t* seg, uint32_t n_segments, uint32_t* ck,
+                                            unsigned long long* iv) {
+  __shared__ uint32_t s_seg0;
+  __shared__ uint32_t s_ck[4][8];
+  __shared__ unsigned long long s_lo[4], s_hi[4];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  const uint32_t r = blockIdx.x * blockDim.x + tid;
+  const bool valid = r < n;
+  const uint32_t sg = valid ? (seg ? seg[r] : 0u) : 0xffffffffu;
+  const bool in_range = valid && sg < n_segments;
+  const bool inc = in_range && status[r] == PRIO3_STATUS_FINISHED && (!mask || mask[r]);
+  uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (ck && inc) {
+    uint32_t id[4];
+    load16(ids + 16 * (size_t)r, id);
+    sha256_id16(id, h);
+  }
+  unsigned long long lo = ~0ull, hi = 0;
+  if (times && in_range) {
+    lo = times[r];
+    hi = lo + 1;  // Interval::from_time: [t, t + 1)
+  }
+  if (tid == 0) s_seg0 = sg;  // thread 0 of a launched block is always a valid report
+  __syncthreads();
+  const bool uniform = __syncthreads_and(!valid || sg == s_seg0) && s_seg0 < n_segments;
+  if (uniform) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) h[i] ^= (uint32_t)__shfl_xor((int)h[i], off);
+      const unsigned long long l2 = __shfl_xor(lo, off), h2 = __shfl_xor(hi, off);
+      lo = l2 < lo ? l2 : lo;
+      hi = h2 > hi ? h2 : hi;
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) s_ck[wv][i] = h[i];
+      s_lo[wv] = lo;
+      s_hi[wv] = hi;
+    }
+    __syncthreads();
+    const uint32_t nw = (blockDim.x + 63) / 64;
+    if (ck && tid < 8) {
+      uint32_t x = 0;
+      for (uint32_t q = 0; q < nw; q++) x ^= s_ck[q][tid];
+      if (x) atomicXor(ck + 8 * s_seg0 + tid, x);
+    }
+    if (iv && tid == 8) {
+      unsigned long long l = ~0ull, u = 0;
+      for (uint32_t q = 0; q < nw; q++) {
+        l = s_lo[q] < l ? s_lo[q] : l;
+        u = s_hi[q] > u ? s_hi[q] : u;
+      }
+      if (u) {
+        atomicMin(iv + 2 * s_seg0, l);
+        atomicMax(iv + 2 * s_seg0 + 1, u);
+      }
+    }
+  } else {
+    if (ck && inc)
+#pragma unroll
+      for (int i = 0; i < 8; i++) atomicXor(ck + 8 * sg + i, h[i]);
+    if (iv && times && in_range) {
+      atomicMin(iv + 2 * sg, lo);
+      atomicMax(iv + 2 * sg + 1, hi);
+    }
+  }
+}
+
+// multi-GPU combine of k per-rank metadata: checksums XOR, intervals Interval::merge
+// (an empty (.., 0) interval is the identity, core/src/time.rs:294-307)
+__global__ void k_combine_meta(uint32_t k, uint32_t n_segments, const uint32_t* ck_in,
+                               const unsigned long long* iv_in, uint32_t* ck_out,
+                               unsigned long long* iv_out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_segments * 8) return;
+  const uint32_t s = t >> 3, w = t & 7u;
+  if (ck_in && ck_out) {
+    uint32_t x = 0;
+    for (uint32_t i = 0; i < k; i++) x ^= ck_in[((size_t)i * n_segments + s) * 8 + w];
+    ck_out[(size_t)s * 8 + w] = x;
+  }
+  if (iv_in && iv_out && w == 0) {
+    unsigned long long lo = ~0ull, hi = 0;
+    for (uint32_t i = 0; i < k; i++) {
+      const unsigned long long a = iv_in[((size_t)i * n_segments + s) * 2];
+      const unsigned long long d = iv_in[((size_t)i * n_segments + s) * 2 + 1];
+      if (d == 0) continue;
+      lo = a < lo ? a : lo;
+      hi = a + d > hi ? a + d : hi;
+    }
+    iv_out[2 * s] = hi ? lo : 0;
+    iv_out[2 * s + 1] = hi ? hi - lo : 0;
+  }
+}
+
+// (min start, max end) -> (start, duration); a segment with no report -> Interval::EMPTY (0, 0)
+__global__ void k_meta_final(uint32_t n_segments, unsigned long long* iv) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_segments) return;
+  const unsigned long long lo = iv[2 * s], hi = iv[2 * s + 1];
+  iv[2 * s] = hi ? lo : 0;
+  iv[2 * s + 1] = hi ? hi - lo : 0;
+}
+
 
 // ------------------------------------------------------------------------------------
 // Field self-test (parity of the hand-scheduled Field128 blocks against Python bigints)
@@ -2469,6 +2656,92 @@ int prio3_device_combine(prio3_engine* e, uint32_t k, uint32_t n_segments, const
                                                                  d_counts_in, d_out,
                                                                  d_counts_out)));
   return PRIO3_OK;
+}
+
+int prio3_device_batch_metadata(prio3_engine* e, uint32_t n, const uint8_t* d_report_ids,
+                                const uint64_t* d_times, const uint8_t* d_status,
+                                const uint8_t* d_accept_mask, const uint32_t* d_segment_ids,
+                                uint32_t n_segments, uint8_t* d_checksums, uint64_t* d_intervals,
+                                void* stream) {
+  if (!e || n_segments == 0 || (n && (!d_status || (d_checksums && !d_report_ids))))
+    return PRIO3_EINVAL;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
+  uint32_t* ck = (uint32_t*)d_checksums;
+  unsigned long long* iv = (unsigned long long*)d_intervals;
+  const uint32_t sb = (n_segments + 255) / 256;
+  TIMED(e, st, "k_meta_init", (k_meta_init<<<sb, 256, 0, st>>>(n_segments, ck, iv)));
+  if (n)
+    TIMED(e, st, "k_meta",
+          (k_meta<<<(n + 255) / 256, 256, 0, st>>>(n, d_report_ids, d_times, d_status,
+                                                   d_accept_mask, d_segment_ids, n_segments, ck,
+                                                   d_times ? iv : nullptr)));
+  if (iv) TIMED(e, st, "k_meta_final", (k_meta_final<<<sb, 256, 0, st>>>(n_segments, iv)));
+  return PRIO3_OK;
+}
+
+int prio3_device_combine_metadata(prio3_engine* e, uint32_t k, uint32_t n_segments,
+                                  const uint8_t* d_checksums_in, const uint64_t* d_intervals_in,
+                                  uint8_t* d_checksums_out, uint64_t* d_intervals_out,
+                                  void* stream) {
+  if (!e || k == 0 || n_segments == 0) return PRIO3_EINVAL;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
+  TIMED(e, st, "k_combine_meta",
+        (k_combine_meta<<<(n_segments * 8 + 255) / 256, 256, 0, st>>>(
+            k, n_segments, (const uint32_t*)d_checksums_in,
+            (const unsigned long long*)d_intervals_in, (uint32_t*)d_checksums_out,
+            (unsigned long long*)d_intervals_out)));
+  return PRIO3_OK;
+}
+
+int prio3_batch_metadata(prio3_engine* e, uint32_t n, const uint8_t* report_ids,
+                         const uint64_t* times, const uint8_t* status, const uint8_t* accept_mask,
+                         const uint32_t* segment_ids, uint32_t n_segments, uint8_t* checksums_out,
+                         uint64_t* intervals_out) {
+  if (!e || n_segments == 0 || (n && (!status || !report_ids))) return PRIO3_EINVAL;
+  uint8_t *d_ids = nullptr, *d_st = nullptr, *d_mask = nullptr, *d_ck = nullptr;
+  uint64_t *d_t = nullptr, *d_iv = nullptr;
+  uint32_t* d_seg = nullptr;
+  int rc = PRIO3_OK;
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIPCHK(hipSetDevice(e->device));
+    const size_t N = n ? n : 1;
+    HIPCHK(hipMalloc((void**)&d_ids, 16 * N));
+    HIPCHK(hipMalloc((void**)&d_st, N));
+    HIPCHK(hipMalloc((void**)&d_ck, 32 * (size_t)n_segments));
+    HIPCHK(hipMalloc((void**)&d_iv, 16 * (size_t)n_segments));
+    if (times) HIPCHK(hipMalloc((void**)&d_t, 8 * N));
+    if (accept_mask) HIPCHK(hipMalloc((void**)&d_mask, N));
+    if (segment_ids) HIPCHK(hipMalloc((void**)&d_seg, 4 * N));
+    HIPCHK(hipMemcpyAsync(d_ids, report_ids, 16 * (size_t)n, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipMemcpyAsync(d_st, status, n, hipMemcpyHostToDevice, e->stream));
+    if (times) HIPCHK(hipMemcpyAsync(d_t, times, 8 * (size_t)n, hipMemcpyHostToDevice, e->stream));
+    if (accept_mask)
+      HIPCHK(hipMemcpyAsync(d_mask, accept_mask, n, hipMemcpyHostToDevice, e->stream));
+    if (segment_ids)
+      HIPCHK(hipMemcpyAsync(d_seg, segment_ids, 4 * (size_t)n, hipMemcpyHostToDevice, e->stream));
+  }
+  rc = prio3_device_batch_metadata(e, n, d_ids, d_t, d_st, d_mask, d_seg, n_segments,
+                                   checksums_out ? d_ck : nullptr, intervals_out ? d_iv : nullptr,
+                                   e->stream);
+  if (rc == PRIO3_OK) {
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (checksums_out)
+      HIPCHK(hipMemcpyAsync(checksums_out, d_ck, 32 * (size_t)n_segments, hipMemcpyDeviceToHost,
+                            e->stream));
+    if (intervals_out)
+      HIPCHK(hipMemcpyAsync(intervals_out, d_iv, 16 * (size_t)n_segments, hipMemcpyDeviceToHost,
+                            e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+  }
+  for (void* p : {(void*)d_ids, (void*)d_st, (void*)d_mask, (void*)d_ck, (void*)d_t, (void*)d_iv,
+                  (void*)d_seg})
+    if (p) (void)hipFree(p);
+  return rc;
 }
 
 int prio3_device_output_shares(prio3_engine* e, uint32_t n, uint8_t* out) {

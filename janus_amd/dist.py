@@ -3,8 +3,10 @@
 One process per GPU (``torch.distributed``; backend ``nccl`` is RCCL on ROCm).  Reports are
 independent, so each rank prepares a contiguous range of the batch with no collective on the
 data path.  The only exchange is the per-rank partial aggregate share
-(``n_segments x agg_share_len`` bytes plus ``u64`` counts per segment): it is all-gathered over
-xGMI and summed mod p by ``prio3_device_combine`` -- RCCL's integer reduction is mod 2^64, not
+(``n_segments x agg_share_len`` bytes plus ``u64`` counts, the 32-byte report-ID checksum and
+the client-timestamp interval per segment): it is all-gathered over xGMI in one packed
+collective and summed mod p by ``prio3_device_combine`` (checksums XORed, intervals merged by
+``prio3_device_combine_metadata``) -- RCCL's integer reduction is mod 2^64, not
 mod p, so an ``all_reduce(SUM)`` would be wrong.
 
 The analogue in Janus is merging per-shard ``batch_aggregations`` rows at collection time
@@ -16,7 +18,7 @@ CPU tensors, where the combine callable is the test's own mod-p sum.
 """
 from __future__ import annotations
 
-from typing import Callable, Tuple
+from typing import Callable, Optional, Tuple
 
 
 def shard_bounds(n_total: int, rank: int, world: int) -> Tuple[int, int]:
@@ -29,27 +31,59 @@ def shard_bounds(n_total: int, rank: int, world: int) -> Tuple[int, int]:
 
 
 class AggregateCombiner:
-    """Gathers every rank's partial aggregate share and reduces them mod p.
+    """Gathers every rank's partial batch aggregation and reduces it.
 
-    ``combine(k, gathered_agg, gathered_counts, out_agg, out_counts)`` does the mod-p sum of
-    the k gathered partials (on the GPU: ``HelperEngine.combine_device``).  Buffers are
-    preallocated once, so a step issues exactly two all-gathers and one combine launch.
+    The per-rank partials -- aggregate shares [S, agg_len] (uint8), counts [S] (int64) and,
+    optionally, the batch metadata (ReportIdChecksum [S, 32] uint8, interval [S, 2] int64) --
+    are packed into one byte row, so a step issues exactly ONE all-gather over xGMI (the
+    payload is a few KiB: latency-bound, so one collective instead of four).  Then
+    ``combine(k, gathered_agg, gathered_counts, out_agg, out_counts)`` does the mod-p sum
+    (on the GPU: ``HelperEngine.combine_device``) and ``combine_meta(k, gathered_checksums,
+    gathered_intervals, out_checksums, out_intervals)`` the XOR / Interval::merge
+    (``HelperEngine.combine_metadata_device``).  Buffers are preallocated once.
     """
 
-    def __init__(self, dist, agg, counts, combine: Callable):
+    def __init__(self, dist, agg, counts, combine: Callable, checksums=None, intervals=None,
+                 combine_meta: Optional[Callable] = None):
         import torch
         self.dist = dist
         self.world = dist.get_world_size()
         self.combine = combine
-        self.g_agg = torch.empty((self.world,) + tuple(agg.shape), dtype=agg.dtype,
-                                 device=agg.device)
-        self.g_cnt = torch.empty((self.world,) + tuple(counts.shape), dtype=counts.dtype,
-                                 device=counts.device)
-        self.out_agg = torch.empty_like(agg)
-        self.out_cnt = torch.empty_like(counts)
+        self.combine_meta = combine_meta
+        self.meta = checksums is not None
+        dev = agg.device
+        self.shapes = [tuple(agg.shape), tuple(counts.shape)]
+        self.dtypes = [agg.dtype, counts.dtype]
+        if self.meta:
+            self.shapes += [tuple(checksums.shape), tuple(intervals.shape)]
+            self.dtypes += [checksums.dtype, intervals.dtype]
+        self.nbytes = [int(torch.empty(sh, dtype=dt, device="meta").numel()) *
+                       torch.empty((), dtype=dt).element_size()
+                       for sh, dt in zip(self.shapes, self.dtypes)]
+        self.row = sum(self.nbytes)
+        self.send = torch.empty(self.row, dtype=torch.uint8, device=dev)
+        self.gathered = torch.empty((self.world, self.row), dtype=torch.uint8, device=dev)
+        self.outs = [torch.empty(sh, dtype=dt, device=dev)
+                     for sh, dt in zip(self.shapes, self.dtypes)]
+        self.out_agg, self.out_cnt = self.outs[0], self.outs[1]
+        if self.meta:
+            self.out_checksums, self.out_intervals = self.outs[2], self.outs[3]
 
-    def __call__(self, agg, counts):
-        self.dist.all_gather_into_tensor(self.g_agg.view(-1), agg.contiguous().view(-1))
-        self.dist.all_gather_into_tensor(self.g_cnt.view(-1), counts.contiguous().view(-1))
-        self.combine(self.world, self.g_agg, self.g_cnt, self.out_agg, self.out_cnt)
+    def _gathered(self, idx):
+        import torch
+        off = sum(self.nbytes[:idx])
+        g = self.gathered[:, off:off + self.nbytes[idx]].contiguous()
+        return g.view(self.dtypes[idx]).view((self.world,) + self.shapes[idx]) \
+            if self.dtypes[idx] != torch.uint8 else g.view((self.world,) + self.shapes[idx])
+
+    def __call__(self, agg, counts, checksums=None, intervals=None):
+        import torch
+        parts = [agg, counts] + ([checksums, intervals] if self.meta else [])
+        torch.cat([t.contiguous().view(-1).view(torch.uint8) for t in parts], out=self.send)
+        self.dist.all_gather_into_tensor(self.gathered.view(-1), self.send)
+        self.combine(self.world, self._gathered(0), self._gathered(1), self.out_agg, self.out_cnt)
+        if self.meta:
+            self.combine_meta(self.world, self._gathered(2), self._gathered(3),
+                              self.out_checksums, self.out_intervals)
+            return self.out_agg, self.out_cnt, self.out_checksums, self.out_intervals
         return self.out_agg, self.out_cnt

@@ -79,7 +79,8 @@ EXPORTED_SYMBOLS = (
     "prio3_client_generate_device", "prio3_selftest_field", "prio3_device_prepare_aggregate",
     "prio3_device_aggregate_finish", "prio3_leader_prepare_init_batch",
     "prio3_leader_prepare_next_batch", "prio3_device_leader_prepare_init",
-    "prio3_device_leader_prepare_next",
+    "prio3_device_leader_prepare_next", "prio3_device_batch_metadata", "prio3_batch_metadata",
+    "prio3_device_combine_metadata",
 )
 
 _lib = None
@@ -131,6 +132,10 @@ def load_library() -> C.CDLL:
     L.prio3_leader_prepare_next_batch.argtypes = [vp, vp, vp]
     L.prio3_device_leader_prepare_init.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, vp, vp]
     L.prio3_device_leader_prepare_next.argtypes = [vp, C.c_uint32, vp, vp, vp]
+    L.prio3_device_batch_metadata.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, vp, C.c_uint32, vp,
+                                              vp, vp]
+    L.prio3_batch_metadata.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, vp, C.c_uint32, vp, vp]
+    L.prio3_device_combine_metadata.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp]
     _lib = L
     return L
 
@@ -401,6 +406,45 @@ class HelperEngine:
             _tptr(out_counts), _stream(stream, self.device))
         if rc:
             raise RuntimeError(f"prio3_device_combine failed (rc={rc})")
+
+    def batch_metadata_device(self, report_ids, times, status, accept_mask, segment_ids,
+                              n_segments, checksums, intervals, stream=None) -> None:
+        """Per-segment ReportIdChecksum [n_segments, 32] (uint8) and client-timestamp interval
+        [n_segments, 2] (int64 start, duration) of the batch (torch tensors on this GPU)."""
+        rc = load_library().prio3_device_batch_metadata(
+            self.handle, status.shape[0], _tptr(report_ids), _tptr(times), _tptr(status),
+            _tptr(accept_mask), _tptr(segment_ids), n_segments, _tptr(checksums),
+            _tptr(intervals), _stream(stream, self.device))
+        if rc:
+            raise RuntimeError(f"prio3_device_batch_metadata failed (rc={rc})")
+
+    def combine_metadata_device(self, k, n_segments, checksums_in, intervals_in, checksums,
+                                intervals, stream=None) -> None:
+        rc = load_library().prio3_device_combine_metadata(
+            self.handle, k, n_segments, _tptr(checksums_in), _tptr(intervals_in),
+            _tptr(checksums), _tptr(intervals), _stream(stream, self.device))
+        if rc:
+            raise RuntimeError(f"prio3_device_combine_metadata failed (rc={rc})")
+
+    def batch_metadata(self, report_ids, times, status, accept_mask=None, segment_ids=None,
+                       n_segments: int = 1):
+        """Host-buffer form: returns (checksums uint8 [S, 32], intervals uint64 [S, 2])."""
+        ids = np.ascontiguousarray(report_ids, np.uint8)
+        n = ids.shape[0]
+        st = np.ascontiguousarray(status, np.uint8)
+        if ids.shape != (n, 16) or st.shape != (n,):
+            raise ValueError("report_ids must be [n, 16] and status [n]")
+        t = None if times is None else np.ascontiguousarray(times, np.uint64)
+        m = None if accept_mask is None else np.ascontiguousarray(accept_mask, np.uint8)
+        sg = None if segment_ids is None else np.ascontiguousarray(segment_ids, np.uint32)
+        ck = np.zeros((n_segments, 32), np.uint8)
+        iv = np.zeros((n_segments, 2), np.uint64)
+        rc = load_library().prio3_batch_metadata(
+            self.handle, n, _np_ptr(ids), _np_ptr(t), _np_ptr(st), _np_ptr(m), _np_ptr(sg),
+            n_segments, _np_ptr(ck), _np_ptr(iv))
+        if rc:
+            raise RuntimeError(f"prio3_batch_metadata failed (rc={rc})")
+        return ck, iv
 
     def device_output_shares(self, n: int) -> np.ndarray:
         out = np.zeros((n, self.sz.agg_share_len), np.uint8)

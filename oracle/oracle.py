@@ -221,3 +221,39 @@ def sum_mod(rows: np.ndarray, es: int, p: int) -> list:
     for e in range(k):
         acc[e] = sum(int(sums[j][e]) << (32 * j) for j in range(es // 4)) % p
     return acc
+
+
+def batch_metadata(report_ids: np.ndarray, times, status: np.ndarray, accept_mask=None,
+                   segment_ids=None, n_segments: int = 1):
+    """Per-segment ReportIdChecksum and client-timestamp interval of one batch (TEST ORACLE).
+
+    checksum[s] = XOR of SHA-256(report_id) over the reports counted in segment s (status 0 and
+    accept mask non-zero): ReportIdChecksum::for_report_id / combined_with,
+    /root/reference/core/src/report_id.rs:18-42, folded per report in
+    aggregator/src/aggregator/aggregation_job_writer.rs:637-690.  SHA-256 is ring's
+    digest::SHA256 in the reference (FIPS 180-4); hashlib computes the same function.
+    interval[s] = (start, duration): Interval::from_time(t) = [t, t + 1) merged over every report
+    aggregation of the segment (failed ones included), core/src/time.rs:294-317, starting from
+    Interval::EMPTY = (0, 0) (BatchAggregation::new, aggregation_job_writer.rs:606-611).
+    """
+    import hashlib
+    n = len(status)
+    ck = np.zeros((n_segments, 32), np.uint8)
+    lo = [None] * n_segments
+    hi = [None] * n_segments
+    for r in range(n):
+        s = 0 if segment_ids is None else int(segment_ids[r])
+        if s >= n_segments:
+            continue
+        if times is not None:
+            t = int(times[r])
+            lo[s] = t if lo[s] is None else min(lo[s], t)
+            hi[s] = t + 1 if hi[s] is None else max(hi[s], t + 1)
+        if status[r] == 0 and (accept_mask is None or accept_mask[r]):
+            d = hashlib.sha256(bytes(report_ids[r])).digest()
+            ck[s] ^= np.frombuffer(d, np.uint8)
+    iv = np.zeros((n_segments, 2), np.uint64)
+    for s in range(n_segments):
+        if lo[s] is not None:
+            iv[s] = (lo[s], hi[s] - lo[s])
+    return ck, iv

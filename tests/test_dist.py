@@ -55,11 +55,30 @@ def _modp_combine(p, es):
     return combine
 
 
+def _meta_combine(k, g_ck, g_iv, out_ck, out_iv):
+    """numpy stand-in for prio3_device_combine_metadata: XOR, Interval::merge."""
+    import torch
+    ck = np.bitwise_xor.reduce(g_ck.numpy(), axis=0)
+    iv = g_iv.numpy().view(np.uint64)
+    res = np.zeros(iv.shape[1:], np.uint64)
+    for s in range(iv.shape[1]):
+        spans = [(a, a + d) for a, d in iv[:, s] if d]
+        if spans:
+            lo, hi = min(a for a, _ in spans), max(b for _, b in spans)
+            res[s] = (lo, hi - lo)
+    out_ck.copy_(torch.from_numpy(ck))
+    out_iv.copy_(torch.from_numpy(res.view(np.int64)))
+
+
+def _times():
+    return (1_700_000_000 + (np.arange(N) * 7919) % 5000).astype(np.uint64)
+
+
 def _rank(rank, world, port, result_path):
     import torch
     import torch.distributed as dist
     from janus_amd.dist import AggregateCombiner
-    from oracle.oracle import Oracle, field_modulus
+    from oracle.oracle import Oracle, batch_metadata, field_modulus
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     o = Oracle(**CFG)
@@ -70,18 +89,25 @@ def _rank(rank, world, port, result_path):
     _, _, agg, cnt = o.helper_batch(VK, d["nonces"][sl], d["public_shares"][sl],
                                     d["helper_shares"][sl], d["leader_prep_shares"][sl],
                                     segment_ids=seg[sl], n_segments=NSEG, n_threads=2)
+    st = o.helper_batch(VK, d["nonces"][sl], d["public_shares"][sl], d["helper_shares"][sl],
+                        d["leader_prep_shares"][sl], n_threads=2)[1]
+    ck, iv = batch_metadata(d["nonces"][sl], _times()[sl], st, None, seg[sl], NSEG)
     agg_t = torch.from_numpy(agg.copy())
     cnt_t = torch.from_numpy(cnt.astype(np.int64))
-    comb = AggregateCombiner(dist, agg_t, cnt_t, _modp_combine(field_modulus("histogram"), 16))
-    out_agg, out_cnt = comb(agg_t, cnt_t)
+    ck_t = torch.from_numpy(ck)
+    iv_t = torch.from_numpy(iv.view(np.int64).copy())
+    comb = AggregateCombiner(dist, agg_t, cnt_t, _modp_combine(field_modulus("histogram"), 16),
+                             ck_t, iv_t, _meta_combine)
+    out_agg, out_cnt, out_ck, out_iv = comb(agg_t, cnt_t, ck_t, iv_t)
     if rank == 0:
-        np.savez(result_path, agg=out_agg.numpy(), cnt=out_cnt.numpy())
+        np.savez(result_path, agg=out_agg.numpy(), cnt=out_cnt.numpy(), ck=out_ck.numpy(),
+                 iv=out_iv.numpy())
     dist.destroy_process_group()
 
 
 def test_two_rank_combine_equals_single_process(tmp_path):
     import torch.multiprocessing as mp
-    from oracle.oracle import Oracle
+    from oracle.oracle import Oracle, batch_metadata
     res = str(tmp_path / "r.npz")
     mp.spawn(_rank, args=(2, _free_port(), res), nprocs=2, join=True)
     got = np.load(res)
@@ -93,3 +119,8 @@ def test_two_rank_combine_equals_single_process(tmp_path):
                                     n_threads=2)
     np.testing.assert_array_equal(got["agg"], agg)
     np.testing.assert_array_equal(got["cnt"].astype(np.uint64), cnt)
+    st = o.helper_batch(VK, d["nonces"], d["public_shares"], d["helper_shares"],
+                        d["leader_prep_shares"], n_threads=2)[1]
+    ck, iv = batch_metadata(d["nonces"], _times(), st, None, seg, NSEG)
+    np.testing.assert_array_equal(got["ck"], ck)
+    np.testing.assert_array_equal(got["iv"].view(np.uint64), iv)
