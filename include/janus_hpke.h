@@ -1,0 +1,108 @@
+/*
+ * janus_hpke.h -- C ABI of the batched HPKE opener for DAP input shares on MI355X (gfx950)
+ * (SURVEY.md 8(f) row 2).
+ *
+ * It replaces, for a whole aggregation-job batch in one device call, the per-report decryption
+ * in the helper's VdafOps::handle_aggregate_init_generic loop
+ * (/root/reference/aggregator/src/aggregator.rs:1796-1990): hpke::open(keypair,
+ * HpkeApplicationInfo(InputShare, Client, Helper), encrypted_input_share, InputShareAad)
+ * (/root/reference/core/src/hpke.rs:186-203), PlaintextInputShare::get_decoded, the
+ * duplicate / taskprov extension checks and the helper input share decode -- writing the decoded
+ * helper input shares straight into the layout prio3_device_prepare[_aggregate] reads.
+ *
+ * Suite: mode_base, DHKEM(X25519, HKDF-SHA256) (0x0020), HKDF-SHA256 (0x0001), AES-128-GCM
+ * (0x0001) -- the configuration Janus generates by default (hpke.rs:260-300).  Other suites
+ * return JANUS_HPKE_EUNSUPPORTED at creation; the host keeps its CPU path for them.
+ *
+ * Conventions as in janus_prio3.h: plain pointers and sizes, caller-owned buffers, device
+ * pointers (d_*) stream-ordered on a hipStream_t (NULL = the null stream), per-report failures
+ * reported in status, never aborting the batch.
+ */
+#ifndef JANUS_HPKE_H
+#define JANUS_HPKE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  JANUS_HPKE_KEM_X25519_HKDF_SHA256 = 0x0020,
+  JANUS_HPKE_KDF_HKDF_SHA256 = 0x0001,
+  JANUS_HPKE_AEAD_AES_128_GCM = 0x0001,
+};
+
+/* Per-report status: the DAP PrepareError code Janus records for the report
+ * (messages/src/lib.rs PrepareError; aggregator.rs:1880-1990). */
+enum {
+  JANUS_HPKE_OK = 0,
+  JANUS_HPKE_DECRYPT_ERROR = 4,    /* PrepareError::HpkeDecryptError */
+  JANUS_HPKE_INVALID_MESSAGE = 8,  /* PrepareError::InvalidMessage (plaintext decode, extensions,
+                                      input share length) */
+};
+
+/* Whole-call return codes (same values as janus_prio3.h). */
+enum {
+  JANUS_HPKE_SUCCESS = 0,
+  JANUS_HPKE_EINVAL = -1,
+  JANUS_HPKE_EDEVICE = -2,
+  JANUS_HPKE_EUNSUPPORTED = -3,
+};
+
+typedef struct janus_hpke_opener janus_hpke_opener;
+
+/* One opener per (HPKE keypair, application info), bound to one GPU: Janus's HpkeKeypair
+ * (hpke.rs:283-305) -- private_key is the 32-byte X25519 SerializePrivateKey, public_key the
+ * 32-byte pkRm -- and HpkeApplicationInfo (hpke.rs:70-85; for helper input shares
+ * "dap-09 input share" || 0x01 || 0x03). */
+int janus_hpke_opener_create(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id,
+                             const uint8_t* private_key, size_t private_key_len,
+                             const uint8_t* public_key, size_t public_key_len,
+                             const uint8_t* info, size_t info_len, int device,
+                             janus_hpke_opener** out);
+void janus_hpke_opener_destroy(janus_hpke_opener* opener);
+
+/* Helper input shares of one task.  Per report r:
+ *   d_enc[r][32]                      HpkeCiphertext.encapsulated_key
+ *   d_ct[r][ct_stride], d_ct_len[r]   HpkeCiphertext.payload (ciphertext || 16-byte tag)
+ *   d_report_ids[r][16], d_times[r]   ReportMetadata (report ID, time in seconds)
+ *   d_public_shares[r][public_share_len]
+ * The AAD is InputShareAad { task_id, metadata, public_share } (messages/src/lib.rs:1825-1872),
+ * built on the device.  Output: d_helper_shares[r][helper_share_len] (zeroed unless status OK)
+ * and d_status[r].  require_taskprov: the task is a taskprov task (aggregator.rs:1925-1958). */
+int janus_hpke_open_input_shares_device(janus_hpke_opener* opener, uint32_t n,
+                                        const uint8_t task_id[32], const uint8_t* d_enc,
+                                        const uint8_t* d_ct, const uint32_t* d_ct_len,
+                                        uint32_t ct_stride, const uint8_t* d_report_ids,
+                                        const uint64_t* d_times, const uint8_t* d_public_shares,
+                                        uint32_t public_share_len, uint32_t helper_share_len,
+                                        int require_taskprov, uint8_t* d_helper_shares,
+                                        uint8_t* d_status, void* stream);
+/* Host-buffer form (blocking). */
+int janus_hpke_open_input_shares(janus_hpke_opener* opener, uint32_t n, const uint8_t task_id[32],
+                                 const uint8_t* enc, const uint8_t* ct, const uint32_t* ct_len,
+                                 uint32_t ct_stride, const uint8_t* report_ids,
+                                 const uint64_t* times, const uint8_t* public_shares,
+                                 uint32_t public_share_len, uint32_t helper_share_len,
+                                 int require_taskprov, uint8_t* helper_shares, uint8_t* status);
+
+/* Generic single-shot open (sequence number 0) with explicit AAD: d_aad[r][aad_stride],
+ * d_aad_len[r]; plaintext to d_pt[r][ct_stride] (length d_ct_len[r] - 16), status OK or
+ * DECRYPT_ERROR.  Host-buffer form below. */
+int janus_hpke_open_device(janus_hpke_opener* opener, uint32_t n, const uint8_t* d_enc,
+                           const uint8_t* d_ct, const uint32_t* d_ct_len, uint32_t ct_stride,
+                           const uint8_t* d_aad, const uint32_t* d_aad_len, uint32_t aad_stride,
+                           uint8_t* d_pt, uint8_t* d_status, void* stream);
+int janus_hpke_open(janus_hpke_opener* opener, uint32_t n, const uint8_t* enc, const uint8_t* ct,
+                    const uint32_t* ct_len, uint32_t ct_stride, const uint8_t* aad,
+                    const uint32_t* aad_len, uint32_t aad_stride, uint8_t* pt, uint8_t* status);
+
+/* Per-kernel HIP-event timing of the opener's launches (as prio3_engine_timing). */
+int janus_hpke_set_timing(janus_hpke_opener* opener, int on);
+int janus_hpke_timing(janus_hpke_opener* opener, double* ms_total, uint32_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

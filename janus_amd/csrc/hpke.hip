@@ -1,0 +1,1291 @@
+// hpke.hip -- batched HPKE open of DAP input shares on MI355X (gfx950), SURVEY 8(f) row 2.
+//
+// One report per lane, the whole RFC 9180 base-mode open in one kernel:
+//   X25519 (RFC 7748 Montgomery ladder, GF(2^255-19) in 8 x 32-bit limbs: column-MAC products
+//   with v_mad_u64_u32 + carry-out words, like the Field128 MAC of prio3_device.h)
+//   -> DHKEM ExtractAndExpand and the key schedule (HMAC-SHA256, 19 compressions)
+//   -> AES-128-GCM (T-tables in LDS, bitwise GHASH) -> for DAP input shares the
+//   PlaintextInputShare decode and checks of aggregator.rs:1893-1990.
+// The server scalar is the same for every lane: its bits are wave-uniform (SGPR) and the
+// ladder's conditional swaps are v_cndmask on an SGPR mask, so every report runs the same
+// instruction stream (no key-dependent branch).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/janus_hpke.h"
+#include "prio3_device.h"
+#include "sha256_device.h"
+
+// -------------------------------------------------------------------------------------
+// GF(2^255 - 19), values in [0, 2^256) (loosely reduced), 8 little-endian 32-bit limbs
+// -------------------------------------------------------------------------------------
+struct fe {
+  uint32_t v[8];
+};
+
+DEV fe fe_set(uint32_t x) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = i ? 0u : x;
+  return r;
+}
+
+// r = lo + 38 * c (c small), folded twice so the result is < 2^256
+DEV void fe_fold(uint32_t r[8], uint32_t c) {
+  uint32_t cy;
+  r[0] = addc(r[0], c * 38u, 0, &cy);
+#pragma unroll
+  for (int i = 1; i < 8; i++) r[i] = addc(r[i], 0, cy, &cy);
+  r[0] = addc(r[0], cy * 38u, 0, &cy);  // second carry leaves r < 76: no further carry
+}
+
+DEV fe fe_add(const fe& a, const fe& b) {
+  fe r;
+  uint32_t cy;
+  r.v[0] = addc(a.v[0], b.v[0], 0, &cy);
+#pragma unroll
+  for (int i = 1; i < 8; i++) r.v[i] = addc(a.v[i], b.v[i], cy, &cy);
+  fe_fold(r.v, cy);
+  return r;
+}
+
+// a - b: a wrap adds 2^256 = 38 (mod p), compensated by subtracting 38 (twice at most)
+DEV fe fe_sub(const fe& a, const fe& b) {
+  fe r;
+  uint32_t bw;
+  r.v[0] = subb(a.v[0], b.v[0], 0, &bw);
+#pragma unroll
+  for (int i = 1; i < 8; i++) r.v[i] = subb(a.v[i], b.v[i], bw, &bw);
+#pragma unroll
+  for (int pass = 0; pass < 2; pass++) {
+    r.v[0] = subb(r.v[0], bw * 38u, 0, &bw);
+#pragma unroll
+    for (int i = 1; i < 8; i++) r.v[i] = subb(r.v[i], 0, bw, &bw);
+  }
+  return r;
+}
+
+// X = sum_k c[k] 2^(32k) + sum_k h[k] 2^(32(k+2)) -> 16 words, then reduce (2^256 = 38)
+DEV fe fe_reduce512(const uint32_t w[16]) {
+  fe r;
+  uint32_t cy = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t t = (uint64_t)w[8 + i] * 38u + w[i] + cy;
+    r.v[i] = (uint32_t)t;
+    cy = (uint32_t)(t >> 32);
+  }
+  fe_fold(r.v, cy);
+  return r;
+}
+
+DEV void fe_normalize(const uint64_t c[15], const uint32_t h[14], uint32_t w[16]) {
+  uint32_t cy;
+#pragma unroll
+  for (int k = 0; k < 15; k += 2) {  // even columns: a plain concatenation
+    w[k] = (uint32_t)c[k];
+    w[k + 1] = (uint32_t)(c[k] >> 32);
+  }
+  // + odd columns: c[k] (k odd) at words k, k+1
+  w[1] = addc(w[1], (uint32_t)c[1], 0, &cy);
+  w[2] = addc(w[2], (uint32_t)(c[1] >> 32), cy, &cy);
+#pragma unroll
+  for (int k = 3; k < 14; k += 2) {
+    w[k] = addc(w[k], (uint32_t)c[k], cy, &cy);
+    w[k + 1] = addc(w[k + 1], (uint32_t)(c[k] >> 32), cy, &cy);
+  }
+  w[15] = addc(w[15], 0, cy, &cy);
+  // + overflow words: h[k] at word k + 2
+  w[3] = addc(w[3], h[1], 0, &cy);
+#pragma unroll
+  for (int k = 2; k < 14; k++) w[k + 2] = addc(w[k + 2], h[k], cy, &cy);
+}
+
+DEV fe fe_mul(const fe& a, const fe& b) {
+  uint64_t c[15];
+  uint32_t h[14];
+#pragma unroll
+  for (int k = 0; k < 15; k++) c[k] = 0;
+#pragma unroll
+  for (int k = 0; k < 14; k++) h[k] = 0;
+  asm(
+            "v_mad_u64_u32 %0, vcc, %28, %36, %0\n\t"
+      "v_mad_u64_u32 %1, vcc, %28, %37, %1\n\t"
+      "v_addc_co_u32 %15, vcc, 0, %15, vcc\n\t"
+      "v_mad_u64_u32 %2, vcc, %28, %38, %2\n\t"
+      "v_addc_co_u32 %16, vcc, 0, %16, vcc\n\t"
+      "v_mad_u64_u32 %3, vcc, %28, %39, %3\n\t"
+      "v_addc_co_u32 %17, vcc, 0, %17, vcc\n\t"
+      "v_mad_u64_u32 %4, vcc, %28, %40, %4\n\t"
+      "v_addc_co_u32 %18, vcc, 0, %18, vcc\n\t"
+      "v_mad_u64_u32 %5, vcc, %28, %41, %5\n\t"
+      "v_addc_co_u32 %19, vcc, 0, %19, vcc\n\t"
+      "v_mad_u64_u32 %6, vcc, %28, %42, %6\n\t"
+      "v_addc_co_u32 %20, vcc, 0, %20, vcc\n\t"
+      "v_mad_u64_u32 %7, vcc, %28, %43, %7\n\t"
+      "v_addc_co_u32 %21, vcc, 0, %21, vcc\n\t"
+      "v_mad_u64_u32 %1, vcc, %29, %36, %1\n\t"
+      "v_addc_co_u32 %15, vcc, 0, %15, vcc\n\t"
+      "v_mad_u64_u32 %2, vcc, %29, %37, %2\n\t"
+      "v_addc_co_u32 %16, vcc, 0, %16, vcc\n\t"
+      "v_mad_u64_u32 %3, vcc, %29, %38, %3\n\t"
+      "v_addc_co_u32 %17, vcc, 0, %17, vcc\n\t"
+      "v_mad_u64_u32 %4, vcc, %29, %39, %4\n\t"
+      "v_addc_co_u32 %18, vcc, 0, %18, vcc\n\t"
+      "v_mad_u64_u32 %5, vcc, %29, %40, %5\n\t"
+      "v_addc_co_u32 %19, vcc, 0, %19, vcc\n\t"
+      "v_mad_u64_u32 %6, vcc, %29, %41, %6\n\t"
+      "v_addc_co_u32 %20, vcc, 0, %20, vcc\n\t"
+      "v_mad_u64_u32 %7, vcc, %29, %42, %7\n\t"
+      "v_addc_co_u32 %21, vcc, 0, %21, vcc\n\t"
+      "v_mad_u64_u32 %8, vcc, %29, %43, %8\n\t"
+      "v_addc_co_u32 %22, vcc, 0, %22, vcc\n\t"
+      "v_mad_u64_u32 %2, vcc, %30, %36, %2\n\t"
+      "v_addc_co_u32 %16, vcc, 0, %16, vcc\n\t"
+      "v_mad_u64_u32 %3, vcc, %30, %37, %3\n\t"
+      "v_addc_co_u32 %17, vcc, 0, %17, vcc\n\t"
+      "v_mad_u64_u32 %4, vcc, %30, %38, %4\n\t"
+      "v_addc_co_u32 %18, vcc, 0, %18, vcc\n\t"
+      "v_mad_u64_u32 %5, vcc, %30, %39, %5\n\t"
+      "v_addc_co_u32 %19, vcc, 0, %19, vcc\n\t"
+      "v_mad_u64_u32 %6, vcc, %30, %40, %6\n\t"
+      "v_addc_co_u32 %20, vcc, 0, %20, vcc\n\t"
+      "v_mad_u64_u32 %7, vcc, %30, %41, %7\n\t"
+      "v_addc_co_u32 %21, vcc, 0, %21, vcc\n\t"
+      "v_mad_u64_u32 %8, vcc, %30, %42, %8\n\t"
+      "v_addc_co_u32 %22, vcc, 0, %22, vcc\n\t"
+      "v_mad_u64_u32 %9, vcc, %30, %43, %9\n\t"
+      "v_addc_co_u32 %23, vcc, 0, %23, vcc\n\t"
+      "v_mad_u64_u32 %3, vcc, %31, %36, %3\n\t"
+      "v_addc_co_u32 %17, vcc, 0, %17, vcc\n\t"
+      "v_mad_u64_u32 %4, vcc, %31, %37, %4\n\t"
+      "v_addc_co_u32 %18, vcc, 0, %18, vcc\n\t"
+      "v_mad_u64_u32 %5, vcc, %31, %38, %5\n\t"
+      "v_addc_co_u32 %19, vcc, 0, %19, vcc\n\t"
+      "v_mad_u64_u32 %6, vcc, %31, %39, %6\n\t"
+      "v_addc_co_u32 %20, vcc, 0, %20, vcc\n\t"
+      "v_mad_u64_u32 %7, vcc, %31, %40, %7\n\t"
+      "v_addc_co_u32 %21, vcc, 0, %21, vcc\n\t"
+      "v_mad_u64_u32 %8, vcc, %31, %41, %8\n\t"
+      "v_addc_co_u32 %22, vcc, 0, %22, vcc\n\t"
+      "v_mad_u64_u32 %9, vcc, %31, %42, %9\n\t"
+      "v_addc_co_u32 %23, vcc, 0, %23, vcc\n\t"
+      "v_mad_u64_u32 %10, vcc, %31, %43, %10\n\t"
+      "v_addc_co_u32 %24, vcc, 0, %24, vcc\n\t"
+      "v_mad_u64_u32 %4, vcc, %32, %36, %4\n\t"
+      "v_addc_co_u32 %18, vcc, 0, %18, vcc\n\t"
+      "v_mad_u64_u32 %5, vcc, %32, %37, %5\n\t"
+      "v_addc_co_u32 %19, vcc, 0, %19, vcc\n\t"
+      "v_mad_u64_u32 %6, vcc, %32, %38, %6\n\t"
+      "v_addc_co_u32 %20, vcc, 0, %20, vcc\n\t"
+      "v_mad_u64_u32 %7, vcc, %32, %39, %7\n\t"
+      "v_addc_co_u32 %21, vcc, 0, %21, vcc\n\t"
+      "v_mad_u64_u32 %8, vcc, %32, %40, %8\n\t"
+      "v_addc_co_u32 %22, vcc, 0, %22, vcc\n\t"
+      "v_mad_u64_u32 %9, vcc, %32, %41, %9\n\t"
+      "v_addc_co_u32 %23, vcc, 0, %23, vcc\n\t"
+      "v_mad_u64_u32 %10, vcc, %32, %42, %10\n\t"
+      "v_addc_co_u32 %24, vcc, 0, %24, vcc\n\t"
+      "v_mad_u64_u32 %11, vcc, %32, %43, %11\n\t"
+      "v_addc_co_u32 %25, vcc, 0, %25, vcc\n\t"
+      "v_mad_u64_u32 %5, vcc, %33, %36, %5\n\t"
+      "v_addc_co_u32 %19, vcc, 0, %19, vcc\n\t"
+      "v_mad_u64_u32 %6, vcc, %33, %37, %6\n\t"
+      "v_addc_co_u32 %20, vcc, 0, %20, vcc\n\t"
+      "v_mad_u64_u32 %7, vcc, %33, %38, %7\n\t"
+      "v_addc_co_u32 %21, vcc, 0, %21, vcc\n\t"
+      "v_mad_u64_u32 %8, vcc, %33, %39, %8\n\t"
+      "v_addc_co_u32 %22, vcc, 0, %22, vcc\n\t"
+      "v_mad_u64_u32 %9, vcc, %33, %40, %9\n\t"
+      "v_addc_co_u32 %23, vcc, 0, %23, vcc\n\t"
+      "v_mad_u64_u32 %10, vcc, %33, %41, %10\n\t"
+      "v_addc_co_u32 %24, vcc, 0, %24, vcc\n\t"
+      "v_mad_u64_u32 %11, vcc, %33, %42, %11\n\t"
+      "v_addc_co_u32 %25, vcc, 0, %25, vcc\n\t"
+      "v_mad_u64_u32 %12, vcc, %33, %43, %12\n\t"
+      "v_addc_co_u32 %26, vcc, 0, %26, vcc\n\t"
+      "v_mad_u64_u32 %6, vcc, %34, %36, %6\n\t"
+      "v_addc_co_u32 %20, vcc, 0, %20, vcc\n\t"
+      "v_mad_u64_u32 %7, vcc, %34, %37, %7\n\t"
+      "v_addc_co_u32 %21, vcc, 0, %21, vcc\n\t"
+      "v_mad_u64_u32 %8, vcc, %34, %38, %8\n\t"
+      "v_addc_co_u32 %22, vcc, 0, %22, vcc\n\t"
+      "v_mad_u64_u32 %9, vcc, %34, %39, %9\n\t"
+      "v_addc_co_u32 %23, vcc, 0, %23, vcc\n\t"
+      "v_mad_u64_u32 %10, vcc, %34, %40, %10\n\t"
+      "v_addc_co_u32 %24, vcc, 0, %24, vcc\n\t"
+      "v_mad_u64_u32 %11, vcc, %34, %41, %11\n\t"
+      "v_addc_co_u32 %25, vcc, 0, %25, vcc\n\t"
+      "v_mad_u64_u32 %12, vcc, %34, %42, %12\n\t"
+      "v_addc_co_u32 %26, vcc, 0, %26, vcc\n\t"
+      "v_mad_u64_u32 %13, vcc, %34, %43, %13\n\t"
+      "v_addc_co_u32 %27, vcc, 0, %27, vcc\n\t"
+      "v_mad_u64_u32 %7, vcc, %35, %36, %7\n\t"
+      "v_addc_co_u32 %21, vcc, 0, %21, vcc\n\t"
+      "v_mad_u64_u32 %8, vcc, %35, %37, %8\n\t"
+      "v_addc_co_u32 %22, vcc, 0, %22, vcc\n\t"
+      "v_mad_u64_u32 %9, vcc, %35, %38, %9\n\t"
+      "v_addc_co_u32 %23, vcc, 0, %23, vcc\n\t"
+      "v_mad_u64_u32 %10, vcc, %35, %39, %10\n\t"
+      "v_addc_co_u32 %24, vcc, 0, %24, vcc\n\t"
+      "v_mad_u64_u32 %11, vcc, %35, %40, %11\n\t"
+      "v_addc_co_u32 %25, vcc, 0, %25, vcc\n\t"
+      "v_mad_u64_u32 %12, vcc, %35, %41, %12\n\t"
+      "v_addc_co_u32 %26, vcc, 0, %26, vcc\n\t"
+      "v_mad_u64_u32 %13, vcc, %35, %42, %13\n\t"
+      "v_addc_co_u32 %27, vcc, 0, %27, vcc\n\t"
+      "v_mad_u64_u32 %14, vcc, %35, %43, %14\n\t"
+      : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]),
+        "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11]), "+v"(c[12]), "+v"(c[13]),
+        "+v"(c[14]), "+v"(h[1]), "+v"(h[2]), "+v"(h[3]), "+v"(h[4]), "+v"(h[5]), "+v"(h[6]),
+        "+v"(h[7]), "+v"(h[8]), "+v"(h[9]), "+v"(h[10]), "+v"(h[11]), "+v"(h[12]), "+v"(h[13])
+      : "v"(a.v[0]), "v"(a.v[1]), "v"(a.v[2]), "v"(a.v[3]), "v"(a.v[4]), "v"(a.v[5]),
+        "v"(a.v[6]), "v"(a.v[7]), "v"(b.v[0]), "v"(b.v[1]), "v"(b.v[2]), "v"(b.v[3]),
+        "v"(b.v[4]), "v"(b.v[5]), "v"(b.v[6]), "v"(b.v[7])
+      : "vcc");
+  uint32_t w[16];
+  fe_normalize(c, h, w);
+  return fe_reduce512(w);
+}
+
+DEV fe fe_sqr(const fe& a) {
+  uint64_t c[15];
+  uint32_t h[14];
+#pragma unroll
+  for (int k = 0; k < 15; k++) c[k] = 0;
+#pragma unroll
+  for (int k = 0; k < 14; k++) h[k] = 0;
+  asm(
+            "v_mad_u64_u32 %1, vcc, %28, %29, %1\n\t"
+      "v_addc_co_u32 %15, vcc, 0, %15, vcc\n\t"
+      "v_mad_u64_u32 %2, vcc, %28, %30, %2\n\t"
+      "v_addc_co_u32 %16, vcc, 0, %16, vcc\n\t"
+      "v_mad_u64_u32 %3, vcc, %28, %31, %3\n\t"
+      "v_addc_co_u32 %17, vcc, 0, %17, vcc\n\t"
+      "v_mad_u64_u32 %4, vcc, %28, %32, %4\n\t"
+      "v_addc_co_u32 %18, vcc, 0, %18, vcc\n\t"
+      "v_mad_u64_u32 %5, vcc, %28, %33, %5\n\t"
+      "v_addc_co_u32 %19, vcc, 0, %19, vcc\n\t"
+      "v_mad_u64_u32 %6, vcc, %28, %34, %6\n\t"
+      "v_addc_co_u32 %20, vcc, 0, %20, vcc\n\t"
+      "v_mad_u64_u32 %7, vcc, %28, %35, %7\n\t"
+      "v_addc_co_u32 %21, vcc, 0, %21, vcc\n\t"
+      "v_mad_u64_u32 %3, vcc, %29, %30, %3\n\t"
+      "v_addc_co_u32 %17, vcc, 0, %17, vcc\n\t"
+      "v_mad_u64_u32 %4, vcc, %29, %31, %4\n\t"
+      "v_addc_co_u32 %18, vcc, 0, %18, vcc\n\t"
+      "v_mad_u64_u32 %5, vcc, %29, %32, %5\n\t"
+      "v_addc_co_u32 %19, vcc, 0, %19, vcc\n\t"
+      "v_mad_u64_u32 %6, vcc, %29, %33, %6\n\t"
+      "v_addc_co_u32 %20, vcc, 0, %20, vcc\n\t"
+      "v_mad_u64_u32 %7, vcc, %29, %34, %7\n\t"
+      "v_addc_co_u32 %21, vcc, 0, %21, vcc\n\t"
+      "v_mad_u64_u32 %8, vcc, %29, %35, %8\n\t"
+      "v_addc_co_u32 %22, vcc, 0, %22, vcc\n\t"
+      "v_mad_u64_u32 %5, vcc, %30, %31, %5\n\t"
+      "v_addc_co_u32 %19, vcc, 0, %19, vcc\n\t"
+      "v_mad_u64_u32 %6, vcc, %30, %32, %6\n\t"
+      "v_addc_co_u32 %20, vcc, 0, %20, vcc\n\t"
+      "v_mad_u64_u32 %7, vcc, %30, %33, %7\n\t"
+      "v_addc_co_u32 %21, vcc, 0, %21, vcc\n\t"
+      "v_mad_u64_u32 %8, vcc, %30, %34, %8\n\t"
+      "v_addc_co_u32 %22, vcc, 0, %22, vcc\n\t"
+      "v_mad_u64_u32 %9, vcc, %30, %35, %9\n\t"
+      "v_addc_co_u32 %23, vcc, 0, %23, vcc\n\t"
+      "v_mad_u64_u32 %7, vcc, %31, %32, %7\n\t"
+      "v_addc_co_u32 %21, vcc, 0, %21, vcc\n\t"
+      "v_mad_u64_u32 %8, vcc, %31, %33, %8\n\t"
+      "v_addc_co_u32 %22, vcc, 0, %22, vcc\n\t"
+      "v_mad_u64_u32 %9, vcc, %31, %34, %9\n\t"
+      "v_addc_co_u32 %23, vcc, 0, %23, vcc\n\t"
+      "v_mad_u64_u32 %10, vcc, %31, %35, %10\n\t"
+      "v_addc_co_u32 %24, vcc, 0, %24, vcc\n\t"
+      "v_mad_u64_u32 %9, vcc, %32, %33, %9\n\t"
+      "v_addc_co_u32 %23, vcc, 0, %23, vcc\n\t"
+      "v_mad_u64_u32 %10, vcc, %32, %34, %10\n\t"
+      "v_addc_co_u32 %24, vcc, 0, %24, vcc\n\t"
+      "v_mad_u64_u32 %11, vcc, %32, %35, %11\n\t"
+      "v_addc_co_u32 %25, vcc, 0, %25, vcc\n\t"
+      "v_mad_u64_u32 %11, vcc, %33, %34, %11\n\t"
+      "v_addc_co_u32 %25, vcc, 0, %25, vcc\n\t"
+      "v_mad_u64_u32 %12, vcc, %33, %35, %12\n\t"
+      "v_addc_co_u32 %26, vcc, 0, %26, vcc\n\t"
+      "v_mad_u64_u32 %13, vcc, %34, %35, %13\n\t"
+      "v_addc_co_u32 %27, vcc, 0, %27, vcc\n\t"
+
+      : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]),
+        "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11]), "+v"(c[12]), "+v"(c[13]),
+        "+v"(c[14]), "+v"(h[1]), "+v"(h[2]), "+v"(h[3]), "+v"(h[4]), "+v"(h[5]), "+v"(h[6]),
+        "+v"(h[7]), "+v"(h[8]), "+v"(h[9]), "+v"(h[10]), "+v"(h[11]), "+v"(h[12]), "+v"(h[13])
+      : "v"(a.v[0]), "v"(a.v[1]), "v"(a.v[2]), "v"(a.v[3]), "v"(a.v[4]), "v"(a.v[5]),
+        "v"(a.v[6]), "v"(a.v[7])
+      : "vcc");
+  uint32_t w[16], d[16];
+  fe_normalize(c, h, w);  // off-diagonal sum S
+  // 2S (S < 2^511) + D, D = sum a_i^2 2^(64 i) (non-overlapping 64-bit products)
+#pragma unroll
+  for (int i = 15; i > 0; i--) w[i] = __builtin_amdgcn_alignbit(w[i], w[i - 1], 31);
+  w[0] <<= 1;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t q = (uint64_t)a.v[i] * a.v[i];
+    d[2 * i] = (uint32_t)q;
+    d[2 * i + 1] = (uint32_t)(q >> 32);
+  }
+  uint32_t cy;
+  w[0] = addc(w[0], d[0], 0, &cy);
+#pragma unroll
+  for (int i = 1; i < 16; i++) w[i] = addc(w[i], d[i], cy, &cy);
+  return fe_reduce512(w);
+}
+
+DEV fe fe_sqr_n(fe a, int n) {
+#pragma unroll 1
+  for (int i = 0; i < n; i++) a = fe_sqr(a);
+  return a;
+}
+
+DEV fe fe_mul121665(const fe& a) {
+  fe r;
+  uint32_t cy = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t t = (uint64_t)a.v[i] * 121665u + cy;
+    r.v[i] = (uint32_t)t;
+    cy = (uint32_t)(t >> 32);
+  }
+  fe_fold(r.v, cy);
+  return r;
+}
+
+// z^(p - 2) (the ref10 addition chain: 254 squarings, 11 multiplications)
+DEV fe fe_inv(const fe& z) {
+  const fe z2 = fe_sqr(z);
+  const fe z9 = fe_mul(fe_sqr_n(z2, 2), z);
+  const fe z11 = fe_mul(z9, z2);
+  const fe z5_0 = fe_mul(fe_sqr(z11), z9);
+  const fe z10_0 = fe_mul(fe_sqr_n(z5_0, 5), z5_0);
+  const fe z20_0 = fe_mul(fe_sqr_n(z10_0, 10), z10_0);
+  const fe z40_0 = fe_mul(fe_sqr_n(z20_0, 20), z20_0);
+  const fe z50_0 = fe_mul(fe_sqr_n(z40_0, 10), z10_0);
+  const fe z100_0 = fe_mul(fe_sqr_n(z50_0, 50), z50_0);
+  const fe z200_0 = fe_mul(fe_sqr_n(z100_0, 100), z100_0);
+  const fe z250_0 = fe_mul(fe_sqr_n(z200_0, 50), z50_0);
+  return fe_mul(fe_sqr_n(z250_0, 5), z11);
+}
+
+// canonical representative in [0, p): at most two subtractions of p (values < 2^256 = 2p + 38)
+DEV fe fe_freeze(fe a) {
+#pragma unroll
+  for (int pass = 0; pass < 2; pass++) {
+    fe t;
+    uint32_t bw;
+    t.v[0] = subb(a.v[0], 0xffffffedu, 0, &bw);
+#pragma unroll
+    for (int i = 1; i < 7; i++) t.v[i] = subb(a.v[i], 0xffffffffu, bw, &bw);
+    t.v[7] = subb(a.v[7], 0x7fffffffu, bw, &bw);
+#pragma unroll
+    for (int i = 0; i < 8; i++) a.v[i] = bw ? a.v[i] : t.v[i];
+  }
+  return a;
+}
+
+DEV void fe_cswap(bool swap, fe& a, fe& b) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t x = a.v[i], y = b.v[i];
+    a.v[i] = swap ? y : x;
+    b.v[i] = swap ? x : y;
+  }
+}
+
+// X25519(k, u) (RFC 7748 section 5); k = the clamped scalar (LE words, wave-uniform)
+DEV fe x25519_ladder(const uint32_t* k, const fe& u) {
+  const fe x1 = u;
+  fe x2 = fe_set(1), z2 = fe_set(0), x3 = u, z3 = fe_set(1);
+  bool swap = false;
+#pragma unroll 1
+  for (int t = 254; t >= 0; t--) {
+    const bool kt = (k[t >> 5] >> (t & 31)) & 1u;
+    swap ^= kt;
+    fe_cswap(swap, x2, x3);
+    fe_cswap(swap, z2, z3);
+    swap = kt;
+    const fe A = fe_add(x2, z2), B = fe_sub(x2, z2);
+    const fe AA = fe_sqr(A), BB = fe_sqr(B);
+    const fe E = fe_sub(AA, BB);
+    const fe C = fe_add(x3, z3), D = fe_sub(x3, z3);
+    const fe DA = fe_mul(D, A), CB = fe_mul(C, B);
+    x3 = fe_sqr(fe_add(DA, CB));
+    z3 = fe_mul(x1, fe_sqr(fe_sub(DA, CB)));
+    x2 = fe_mul(AA, BB);
+    z2 = fe_mul(E, fe_add(AA, fe_mul121665(E)));
+  }
+  fe_cswap(swap, x2, x3);
+  fe_cswap(swap, z2, z3);
+  return fe_freeze(fe_mul(x2, fe_inv(z2)));
+}
+
+// -------------------------------------------------------------------------------------
+// SHA-256 message buffers (big-endian words) and HMAC
+// -------------------------------------------------------------------------------------
+template <int NW>
+struct Msg32 {
+  uint32_t w[NW];
+};
+template <int NW>
+DEV void mz(Msg32<NW>& m) {
+#pragma unroll
+  for (int i = 0; i < NW; i++) m.w[i] = 0;
+}
+template <int NW>
+DEV void mbyte(Msg32<NW>& m, int pos, uint32_t b) {
+  m.w[pos >> 2] |= (b & 0xffu) << (24 - 8 * (pos & 3));
+}
+template <int NW, int N>
+DEV void mstr(Msg32<NW>& m, int pos, const char (&s)[N]) {  // N - 1 bytes (no terminator)
+#pragma unroll
+  for (int i = 0; i < N - 1; i++) mbyte(m, pos + i, (uint8_t)s[i]);
+}
+// nbytes (multiple of 4) of big-endian words d at byte position pos
+template <int NW>
+DEV void mwords_be(Msg32<NW>& m, int pos, const uint32_t* d, int nwords) {
+  const int q = pos >> 2, o = pos & 3;
+  if (o == 0) {
+#pragma unroll
+    for (int i = 0; i < nwords; i++) m.w[q + i] |= d[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < nwords; i++) {
+      m.w[q + i] |= d[i] >> (8 * o);
+      m.w[q + i + 1] |= d[i] << (32 - 8 * o);
+    }
+  }
+}
+// little-endian packed bytes (as loaded from memory) at byte position pos
+template <int NW>
+DEV void mwords_le(Msg32<NW>& m, int pos, const uint32_t* d, int nwords) {
+  uint32_t be[16];
+#pragma unroll
+  for (int i = 0; i < nwords; i++) be[i] = __builtin_bswap32(d[i]);
+  mwords_be(m, pos, be, nwords);
+}
+// SHA-256 over the len message bytes of m after `prefix` bytes already compressed into st
+template <int NW>
+DEV void sha_final(uint32_t st[8], Msg32<NW>& m, int len, int prefix) {
+  mbyte(m, len, 0x80);
+  const int nblk = (len + 9 + 63) / 64;
+  m.w[nblk * 16 - 1] = (uint32_t)((prefix + len) * 8);
+#pragma unroll
+  for (int b = 0; b < nblk; b++) {
+    uint32_t blk[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) blk[i] = m.w[16 * b + i];
+    sha256d::compress(st, blk);
+  }
+}
+
+struct HmacKey {
+  uint32_t ist[8], ost[8];
+};
+// HMAC key of 32 bytes (big-endian words): the ipad / opad midstates
+DEV void hmac_key32(HmacKey& k, const uint32_t key[8]) {
+  uint32_t bi[16], bo[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const uint32_t x = i < 8 ? key[i] : 0u;
+    bi[i] = x ^ 0x36363636u;
+    bo[i] = x ^ 0x5c5c5c5cu;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) k.ist[i] = k.ost[i] = sha256d::IV[i];
+  sha256d::compress(k.ist, bi);
+  sha256d::compress(k.ost, bo);
+}
+template <int NW>
+DEV void hmac(const HmacKey& k, Msg32<NW>& m, int len, uint32_t out[8]) {
+  uint32_t st[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) st[i] = k.ist[i];
+  sha_final(st, m, len, 64);
+  Msg32<16> o;
+  mz(o);
+#pragma unroll
+  for (int i = 0; i < 8; i++) o.w[i] = st[i];
+#pragma unroll
+  for (int i = 0; i < 8; i++) out[i] = k.ost[i];
+  sha_final(out, o, 32, 64);
+}
+
+// -------------------------------------------------------------------------------------
+// AES-128 (FIPS 197) with little-endian packed column words and LDS T-tables
+// -------------------------------------------------------------------------------------
+__constant__ uint8_t c_sbox[256] = {
+    0x63, 0x7c, 0x77, 0x7b, 0xf2, 0x6b, 0x6f, 0xc5, 0x30, 0x01, 0x67, 0x2b, 0xfe, 0xd7, 0xab, 0x76,
+    0xca, 0x82, 0xc9, 0x7d, 0xfa, 0x59, 0x47, 0xf0, 0xad, 0xd4, 0xa2, 0xaf, 0x9c, 0xa4, 0x72, 0xc0,
+    0xb7, 0xfd, 0x93, 0x26, 0x36, 0x3f, 0xf7, 0xcc, 0x34, 0xa5, 0xe5, 0xf1, 0x71, 0xd8, 0x31, 0x15,
+    0x04, 0xc7, 0x23, 0xc3, 0x18, 0x96, 0x05, 0x9a, 0x07, 0x12, 0x80, 0xe2, 0xeb, 0x27, 0xb2, 0x75,
+    0x09, 0x83, 0x2c, 0x1a, 0x1b, 0x6e, 0x5a, 0xa0, 0x52, 0x3b, 0xd6, 0xb3, 0x29, 0xe3, 0x2f, 0x84,
+    0x53, 0xd1, 0x00, 0xed, 0x20, 0xfc, 0xb1, 0x5b, 0x6a, 0xcb, 0xbe, 0x39, 0x4a, 0x4c, 0x58, 0xcf,
+    0xd0, 0xef, 0xaa, 0xfb, 0x43, 0x4d, 0x33, 0x85, 0x45, 0xf9, 0x02, 0x7f, 0x50, 0x3c, 0x9f, 0xa8,
+    0x51, 0xa3, 0x40, 0x8f, 0x92, 0x9d, 0x38, 0xf5, 0xbc, 0xb6, 0xda, 0x21, 0x10, 0xff, 0xf3, 0xd2,
+    0xcd, 0x0c, 0x13, 0xec, 0x5f, 0x97, 0x44, 0x17, 0xc4, 0xa7, 0x7e, 0x3d, 0x64, 0x5d, 0x19, 0x73,
+    0x60, 0x81, 0x4f, 0xdc, 0x22, 0x2a, 0x90, 0x88, 0x46, 0xee, 0xb8, 0x14, 0xde, 0x5e, 0x0b, 0xdb,
+    0xe0, 0x32, 0x3a, 0x0a, 0x49, 0x06, 0x24, 0x5c, 0xc2, 0xd3, 0xac, 0x62, 0x91, 0x95, 0xe4, 0x79,
+    0xe7, 0xc8, 0x37, 0x6d, 0x8d, 0xd5, 0x4e, 0xa9, 0x6c, 0x56, 0xf4, 0xea, 0x65, 0x7a, 0xae, 0x08,
+    0xba, 0x78, 0x25, 0x2e, 0x1c, 0xa6, 0xb4, 0xc6, 0xe8, 0xdd, 0x74, 0x1f, 0x4b, 0xbd, 0x8b, 0x8a,
+    0x70, 0x3e, 0xb5, 0x66, 0x48, 0x03, 0xf6, 0x0e, 0x61, 0x35, 0x57, 0xb9, 0x86, 0xc1, 0x1d, 0x9e,
+    0xe1, 0xf8, 0x98, 0x11, 0x69, 0xd9, 0x8e, 0x94, 0x9b, 0x1e, 0x87, 0xe9, 0xce, 0x55, 0x28, 0xdf,
+    0x8c, 0xa1, 0x89, 0x0d, 0xbf, 0xe6, 0x42, 0x68, 0x41, 0x99, 0x2d, 0x0f, 0xb0, 0x54, 0xbb, 0x16};
+
+struct AesT {
+  uint32_t t[5][256];  // T0..T3 (MixColumns of the S-box output, row-rotated), T4 = S * 0x01010101
+};
+
+DEV void aes_tables_init(AesT& T) {
+  for (uint32_t x = threadIdx.x; x < 256; x += blockDim.x) {
+    const uint32_t s = c_sbox[x];
+    const uint32_t s2 = ((s << 1) ^ ((s >> 7) * 0x1bu)) & 0xffu, s3 = s2 ^ s;
+    const uint32_t t0 = s2 | (s << 8) | (s << 16) | (s3 << 24);
+    T.t[0][x] = t0;
+    T.t[1][x] = __builtin_amdgcn_alignbit(t0, t0, 24);  // rotl 8
+    T.t[2][x] = __builtin_amdgcn_alignbit(t0, t0, 16);
+    T.t[3][x] = __builtin_amdgcn_alignbit(t0, t0, 8);
+    T.t[4][x] = s * 0x01010101u;
+  }
+}
+
+DEV uint32_t b0(uint32_t x) { return x & 0xffu; }
+DEV uint32_t b1(uint32_t x) { return (x >> 8) & 0xffu; }
+DEV uint32_t b2(uint32_t x) { return (x >> 16) & 0xffu; }
+DEV uint32_t b3(uint32_t x) { return x >> 24; }
+
+DEV uint32_t sub_word(const AesT& T, uint32_t x) {
+  return (T.t[4][b0(x)] & 0xffu) | (T.t[4][b1(x)] & 0xff00u) | (T.t[4][b2(x)] & 0xff0000u) |
+         (T.t[4][b3(x)] & 0xff000000u);
+}
+
+DEV void aes128_expand(const AesT& T, const uint32_t key[4], uint32_t rk[44]) {
+  constexpr uint8_t RC[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1b, 0x36};
+#pragma unroll
+  for (int i = 0; i < 4; i++) rk[i] = key[i];
+#pragma unroll
+  for (int i = 4; i < 44; i++) {
+    uint32_t t = rk[i - 1];
+    if ((i & 3) == 0) t = sub_word(T, __builtin_amdgcn_alignbit(t, t, 8)) ^ RC[i / 4 - 1];
+    rk[i] = rk[i - 4] ^ t;
+  }
+}
+
+DEV void aes128_encrypt(const AesT& T, const uint32_t rk[44], const uint32_t in[4],
+                        uint32_t out[4]) {
+  uint32_t s0 = in[0] ^ rk[0], s1 = in[1] ^ rk[1], s2 = in[2] ^ rk[2], s3 = in[3] ^ rk[3];
+#pragma unroll
+  for (int r = 1; r < 10; r++) {
+    const uint32_t t0 = T.t[0][b0(s0)] ^ T.t[1][b1(s1)] ^ T.t[2][b2(s2)] ^ T.t[3][b3(s3)] ^ rk[4 * r];
+    const uint32_t t1 = T.t[0][b0(s1)] ^ T.t[1][b1(s2)] ^ T.t[2][b2(s3)] ^ T.t[3][b3(s0)] ^ rk[4 * r + 1];
+    const uint32_t t2 = T.t[0][b0(s2)] ^ T.t[1][b1(s3)] ^ T.t[2][b2(s0)] ^ T.t[3][b3(s1)] ^ rk[4 * r + 2];
+    const uint32_t t3 = T.t[0][b0(s3)] ^ T.t[1][b1(s0)] ^ T.t[2][b2(s1)] ^ T.t[3][b3(s2)] ^ rk[4 * r + 3];
+    s0 = t0;
+    s1 = t1;
+    s2 = t2;
+    s3 = t3;
+  }
+  out[0] = ((T.t[4][b0(s0)] & 0xffu) | (T.t[4][b1(s1)] & 0xff00u) | (T.t[4][b2(s2)] & 0xff0000u) |
+            (T.t[4][b3(s3)] & 0xff000000u)) ^ rk[40];
+  out[1] = ((T.t[4][b0(s1)] & 0xffu) | (T.t[4][b1(s2)] & 0xff00u) | (T.t[4][b2(s3)] & 0xff0000u) |
+            (T.t[4][b3(s0)] & 0xff000000u)) ^ rk[41];
+  out[2] = ((T.t[4][b0(s2)] & 0xffu) | (T.t[4][b1(s3)] & 0xff00u) | (T.t[4][b2(s0)] & 0xff0000u) |
+            (T.t[4][b3(s1)] & 0xff000000u)) ^ rk[42];
+  out[3] = ((T.t[4][b0(s3)] & 0xffu) | (T.t[4][b1(s0)] & 0xff00u) | (T.t[4][b2(s1)] & 0xff0000u) |
+            (T.t[4][b3(s2)] & 0xff000000u)) ^ rk[43];
+}
+
+// GHASH step (SP 800-38D Algorithm 1): y = (y ^ x) * H in GF(2^128), big-endian words
+DEV void ghash_block(uint32_t y[4], const uint32_t x[4], const uint32_t H[4]) {
+  uint32_t X[4] = {y[0] ^ x[0], y[1] ^ x[1], y[2] ^ x[2], y[3] ^ x[3]};
+  uint32_t Z[4] = {0, 0, 0, 0}, V[4] = {H[0], H[1], H[2], H[3]};
+#pragma unroll
+  for (int wi = 0; wi < 4; wi++) {
+#pragma unroll 8
+    for (int bit = 31; bit >= 0; bit--) {
+      const uint32_t m = 0u - ((X[wi] >> bit) & 1u);
+      Z[0] ^= V[0] & m;
+      Z[1] ^= V[1] & m;
+      Z[2] ^= V[2] & m;
+      Z[3] ^= V[3] & m;
+      const uint32_t lsb = 0u - (V[3] & 1u);
+      V[3] = __builtin_amdgcn_alignbit(V[2], V[3], 1);
+      V[2] = __builtin_amdgcn_alignbit(V[1], V[2], 1);
+      V[1] = __builtin_amdgcn_alignbit(V[0], V[1], 1);
+      V[0] = (V[0] >> 1) ^ (0xe1000000u & lsb);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) y[i] = Z[i];
+}
+
+// -------------------------------------------------------------------------------------
+// Kernel
+// -------------------------------------------------------------------------------------
+struct HpkeParams {
+  uint32_t sk[8];        // clamped X25519 scalar, LE words
+  uint32_t pk[8];        // pkRm bytes, LE-packed words
+  uint32_t ksc[17];      // key_schedule_context (65 bytes) as BE words, zero padded
+  uint32_t task[8];      // task ID (input-share AAD), BE words
+  uint32_t ipad0[8], opad0[8];  // HMAC midstates of the empty key
+};
+
+struct OpenArgs {
+  uint32_t n, ct_stride, aad_stride, share_len;
+  int require_taskprov;
+  const uint8_t *enc, *ct, *aad, *ids, *pubs;
+  const uint32_t *ct_len, *aad_len;
+  const uint64_t* times;
+  uint8_t *pt, *shares, *status;
+};
+
+DEV void load16(const uint8_t* p, uint32_t* w) {
+  const uint4 v = *(const uint4*)p;
+  w[0] = v.x;
+  w[1] = v.y;
+  w[2] = v.z;
+  w[3] = v.w;
+}
+
+DEV void load_words(const uint8_t* p, uint32_t* w, int n16) {
+#pragma unroll
+  for (int i = 0; i < n16; i++) load16(p + 16 * i, w + 4 * i);
+}
+
+// MODE 0: explicit AAD, plaintext out.  MODE 1: DAP helper input share with PUB bytes of
+// public share (InputShareAad built here), decoded helper share out.
+template <int MODE, int PUB>
+__global__ __launch_bounds__(256) void k_hpke_open(HpkeParams P, OpenArgs a) {
+  __shared__ AesT T;
+  aes_tables_init(T);
+  __syncthreads();
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= a.n) return;
+  // ---- DHKEM(X25519, HKDF-SHA256) Decap (RFC 9180 4.1) -------------------------------
+  uint32_t encw[8];
+  load_words(a.enc + 32 * (size_t)r, encw, 2);
+  fe u;
+#pragma unroll
+  for (int i = 0; i < 8; i++) u.v[i] = encw[i];
+  u.v[7] &= 0x7fffffffu;  // decodeUCoordinate masks bit 255
+  const fe dh = x25519_ladder(P.sk, u);
+  uint32_t nz = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) nz |= dh.v[i];
+  bool ok = nz != 0;  // all-zero shared secret: DeserializeError / ValidationError
+  uint32_t prk[8], ss[8], secret[8], keyw[8], noncew[8];
+  {  // eae_prk = LabeledExtract("", "eae_prk", dh)
+    Msg32<16> m;
+    mz(m);
+    mstr(m, 0, "HPKE-v1");
+    mstr(m, 7, "KEM");
+    mbyte(m, 10, 0x00);
+    mbyte(m, 11, 0x20);
+    mstr(m, 12, "eae_prk");
+    mwords_le(m, 19, dh.v, 8);
+    HmacKey k0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      k0.ist[i] = P.ipad0[i];
+      k0.ost[i] = P.opad0[i];
+    }
+    hmac(k0, m, 51, prk);
+  }
+  {  // shared_secret = LabeledExpand(eae_prk, "shared_secret", enc || pkRm, 32)
+    Msg32<32> m;
+    mz(m);
+    mbyte(m, 0, 0);
+    mbyte(m, 1, 32);
+    mstr(m, 2, "HPKE-v1");
+    mstr(m, 9, "KEM");
+    mbyte(m, 12, 0x00);
+    mbyte(m, 13, 0x20);
+    mstr(m, 14, "shared_secret");
+    mwords_le(m, 27, encw, 8);
+    mwords_le(m, 59, P.pk, 8);
+    mbyte(m, 91, 0x01);
+    HmacKey k;
+    hmac_key32(k, prk);
+    hmac(k, m, 92, ss);
+  }
+  {  // secret = LabeledExtract(shared_secret, "secret", "")
+    Msg32<16> m;
+    mz(m);
+    mstr(m, 0, "HPKE-v1");
+    mstr(m, 7, "HPKE");
+    mbyte(m, 11, 0x00);
+    mbyte(m, 12, 0x20);
+    mbyte(m, 13, 0x00);
+    mbyte(m, 14, 0x01);
+    mbyte(m, 15, 0x00);
+    mbyte(m, 16, 0x01);
+    mstr(m, 17, "secret");
+    HmacKey k;
+    hmac_key32(k, ss);
+    hmac(k, m, 23, secret);
+  }
+  {  // key / base_nonce = LabeledExpand(secret, "key" | "base_nonce", ksc, 16 | 12)
+    HmacKey k;
+    hmac_key32(k, secret);
+    Msg32<32> m;
+    mz(m);
+    mbyte(m, 0, 0);
+    mbyte(m, 1, 16);
+    mstr(m, 2, "HPKE-v1");
+    mstr(m, 9, "HPKE");
+    mbyte(m, 13, 0x00);
+    mbyte(m, 14, 0x20);
+    mbyte(m, 15, 0x00);
+    mbyte(m, 16, 0x01);
+    mbyte(m, 17, 0x00);
+    mbyte(m, 18, 0x01);
+    mstr(m, 19, "key");
+    mwords_be(m, 22, P.ksc, 17);  // 65 bytes + 3 zero padding bytes
+    mbyte(m, 87, 0x01);
+    hmac(k, m, 88, keyw);
+    Msg32<32> n2;
+    mz(n2);
+    mbyte(n2, 0, 0);
+    mbyte(n2, 1, 12);
+    mstr(n2, 2, "HPKE-v1");
+    mstr(n2, 9, "HPKE");
+    mbyte(n2, 13, 0x00);
+    mbyte(n2, 14, 0x20);
+    mbyte(n2, 15, 0x00);
+    mbyte(n2, 16, 0x01);
+    mbyte(n2, 17, 0x00);
+    mbyte(n2, 18, 0x01);
+    mstr(n2, 19, "base_nonce");
+    mwords_be(n2, 29, P.ksc, 17);
+    mbyte(n2, 94, 0x01);
+    hmac(k, n2, 95, noncew);
+  }
+  // ---- AES-128-GCM open, sequence number 0 (nonce = base_nonce) ----------------------
+  uint32_t kcol[4], rk[44];
+#pragma unroll
+  for (int i = 0; i < 4; i++) kcol[i] = __builtin_bswap32(keyw[i]);
+  aes128_expand(T, kcol, rk);
+  uint32_t H[4];
+  {
+    const uint32_t z[4] = {0, 0, 0, 0};
+    uint32_t hc[4];
+    aes128_encrypt(T, rk, z, hc);
+#pragma unroll
+    for (int i = 0; i < 4; i++) H[i] = __builtin_bswap32(hc[i]);
+  }
+  uint32_t y[4] = {0, 0, 0, 0};
+  uint32_t aad_len;
+  if constexpr (MODE == 1) {
+    // InputShareAad: task_id (32) || report_id (16) || time (u64 BE) || u32 BE len || public
+    constexpr int AW = (60 + PUB + 3) / 4;
+    uint32_t aw[((AW + 3) / 4) * 4];
+#pragma unroll
+    for (int i = 0; i < ((AW + 3) / 4) * 4; i++) aw[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) aw[i] = P.task[i];
+    uint32_t idw[4];
+    load16(a.ids + 16 * (size_t)r, idw);
+#pragma unroll
+    for (int i = 0; i < 4; i++) aw[8 + i] = __builtin_bswap32(idw[i]);
+    const uint64_t tm = a.times[r];
+    aw[12] = (uint32_t)(tm >> 32);
+    aw[13] = (uint32_t)tm;
+    aw[14] = PUB;
+    if constexpr (PUB > 0) {
+      uint32_t pw[PUB / 4];
+#pragma unroll
+      for (int i = 0; i < PUB / 16; i++) load16(a.pubs + (size_t)PUB * r + 16 * i, pw + 4 * i);
+#pragma unroll
+      for (int i = 0; i < PUB / 4; i++) aw[15 + i] = __builtin_bswap32(pw[i]);
+    }
+    aad_len = 60 + PUB;
+#pragma unroll
+    for (int b = 0; b < (AW + 3) / 4; b++) ghash_block(y, aw + 4 * b, H);
+  } else {
+    aad_len = a.aad_len[r];
+    const uint8_t* ap = a.aad + (size_t)a.aad_stride * r;
+    for (uint32_t off = 0; off < aad_len; off += 16) {
+      uint32_t xw[4];
+      load16(ap + off, xw);
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t lo = off + 4 * i;  // bytes past the end are zero
+        const uint32_t keep = lo + 4 <= aad_len ? 0xffffffffu
+                              : lo >= aad_len  ? 0u
+                                               : (1u << (8 * (aad_len - lo))) - 1u;
+        xw[i] = __builtin_bswap32(xw[i] & keep);
+      }
+      ghash_block(y, xw, H);
+    }
+  }
+  const uint32_t ct_len = a.ct_len[r];
+  const bool len_ok = ct_len >= 16 && ct_len <= a.ct_stride;
+  ok = ok && len_ok;
+  const uint32_t pt_len = len_ok ? ct_len - 16 : 0;
+  const uint8_t* cp = a.ct + (size_t)a.ct_stride * r;
+  uint8_t* pp = a.pt + (size_t)a.ct_stride * r;
+  uint32_t ctr[4];
+#pragma unroll
+  for (int i = 0; i < 3; i++) ctr[i] = __builtin_bswap32(noncew[i]);
+  for (uint32_t off = 0, blk = 2; off < pt_len; off += 16, blk++) {
+    uint32_t cw[4], ks[4];
+    load16(cp + off, cw);
+    ctr[3] = __builtin_bswap32(blk);
+    aes128_encrypt(T, rk, ctr, ks);
+    uint32_t xw[4], pw[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint32_t lo = off + 4 * i;
+      const uint32_t keep = lo + 4 <= pt_len ? 0xffffffffu
+                            : lo >= pt_len  ? 0u
+                                            : (1u << (8 * (pt_len - lo))) - 1u;
+      xw[i] = __builtin_bswap32(cw[i] & keep);
+      pw[i] = (cw[i] ^ ks[i]) & keep;
+    }
+    ghash_block(y, xw, H);
+    *(uint4*)(pp + off) = make_uint4(pw[0], pw[1], pw[2], pw[3]);
+  }
+  {  // lengths block, tag
+    const uint32_t lw[4] = {0, aad_len * 8, 0, pt_len * 8};
+    ghash_block(y, lw, H);
+    ctr[3] = __builtin_bswap32(1u);
+    uint32_t ek[4];
+    aes128_encrypt(T, rk, ctr, ek);
+    uint32_t diff = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint32_t t = __builtin_bswap32(y[i]) ^ ek[i];  // expected tag, LE-packed bytes
+      uint32_t got = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) got |= (uint32_t)cp[pt_len + 4 * i + j] << (8 * j);
+      diff |= t ^ got;
+    }
+    ok = ok && diff == 0;
+  }
+  if constexpr (MODE == 0) {
+    a.status[r] = ok ? JANUS_HPKE_OK : JANUS_HPKE_DECRYPT_ERROR;
+  } else {
+    // PlaintextInputShare::get_decoded + extension checks + helper share length
+    // (aggregator.rs:1893-1990): extensions (u16-prefixed list of {u16 type, u16-prefixed
+    // data}), payload (u32-prefixed) -- exact total length.
+    uint8_t st = ok ? JANUS_HPKE_OK : JANUS_HPKE_DECRYPT_ERROR;
+    uint32_t pay = 0;
+    if (ok) {
+      bool good = pt_len >= 2;
+      const uint32_t el = good ? ((uint32_t)pp[0] << 8 | pp[1]) : 0u;
+      good = good && 2 + el <= pt_len;
+      uint32_t q = 2;
+      bool taskprov_seen = false, taskprov_ok = false, tbd_seen = false;
+      while (good && q < 2 + el) {
+        if (q + 4 > 2 + el) {
+          good = false;
+          break;
+        }
+        const uint32_t ty = (uint32_t)pp[q] << 8 | pp[q + 1];
+        const uint32_t dl = (uint32_t)pp[q + 2] << 8 | pp[q + 3];
+        if (q + 4 + dl > 2 + el || (ty != 0 && ty != 0xFF00u)) {
+          good = false;
+          break;
+        }
+        // ExtensionType has two values, so a duplicate is a second Tbd or Taskprov
+        if (ty == 0) {
+          good = good && !tbd_seen;
+          tbd_seen = true;
+        } else {
+          good = good && !taskprov_seen;
+          taskprov_seen = true;
+          taskprov_ok = dl == 0;
+        }
+        q += 4 + dl;
+      }
+      q = 2 + el;
+      good = good && q + 4 <= pt_len;
+      const uint32_t pl = good ? ((uint32_t)pp[q] << 24 | (uint32_t)pp[q + 1] << 16 |
+                                  (uint32_t)pp[q + 2] << 8 | pp[q + 3])
+                               : 0u;
+      good = good && q + 4 + pl == pt_len;
+      good = good && (a.require_taskprov ? taskprov_ok : !taskprov_seen);
+      good = good && pl == a.share_len;
+      st = good ? JANUS_HPKE_OK : JANUS_HPKE_INVALID_MESSAGE;
+      pay = q + 4;
+    }
+    uint8_t* so = a.shares + (size_t)a.share_len * r;
+    for (uint32_t i = 0; i < a.share_len; i++) so[i] = st == JANUS_HPKE_OK ? pp[pay + i] : 0;
+    a.status[r] = st;
+  }
+}
+
+// -------------------------------------------------------------------------------------
+// Host side
+// -------------------------------------------------------------------------------------
+namespace {
+
+void sha256_compress_host(uint32_t st[8], const uint8_t blk[64]) {
+  static const uint32_t K[64] = {
+      0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u,
+      0xab1c5ed5u, 0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu,
+      0x9bdc06a7u, 0xc19bf174u, 0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu,
+      0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau, 0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u,
+      0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u, 0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu,
+      0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u, 0xa2bfe8a1u, 0xa81a664bu,
+      0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u, 0x19a4c116u,
+      0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+      0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u,
+      0xc67178f2u};
+  auto rotr = [](uint32_t x, int n) { return (x >> n) | (x << (32 - n)); };
+  uint32_t w[64];
+  for (int i = 0; i < 16; i++)
+    w[i] = (uint32_t)blk[4 * i] << 24 | (uint32_t)blk[4 * i + 1] << 16 |
+           (uint32_t)blk[4 * i + 2] << 8 | blk[4 * i + 3];
+  for (int i = 16; i < 64; i++)
+    w[i] = w[i - 16] + (rotr(w[i - 15], 7) ^ rotr(w[i - 15], 18) ^ (w[i - 15] >> 3)) + w[i - 7] +
+           (rotr(w[i - 2], 17) ^ rotr(w[i - 2], 19) ^ (w[i - 2] >> 10));
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6],
+           h = st[7];
+  for (int i = 0; i < 64; i++) {
+    const uint32_t t1 = h + (rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25)) + ((e & f) ^ (~e & g)) +
+                        K[i] + w[i];
+    const uint32_t t2 = (rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+    h = g, g = f, f = e, e = d + t1, d = c, c = b, b = a, a = t1 + t2;
+  }
+  st[0] += a, st[1] += b, st[2] += c, st[3] += d, st[4] += e, st[5] += f, st[6] += g, st[7] += h;
+}
+
+void sha256_host(const std::vector<uint8_t>& msg, uint8_t out[32]) {
+  uint32_t st[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                    0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  std::vector<uint8_t> m = msg;
+  const uint64_t bits = (uint64_t)msg.size() * 8;
+  m.push_back(0x80);
+  while (m.size() % 64 != 56) m.push_back(0);
+  for (int i = 7; i >= 0; i--) m.push_back((uint8_t)(bits >> (8 * i)));
+  for (size_t o = 0; o < m.size(); o += 64) sha256_compress_host(st, m.data() + o);
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j < 4; j++) out[4 * i + j] = (uint8_t)(st[i] >> (24 - 8 * j));
+}
+
+void hmac_host(const uint8_t* key, size_t klen, const std::vector<uint8_t>& msg, uint8_t out[32]) {
+  uint8_t k[64] = {0};
+  memcpy(k, key, klen);  // klen <= 64 here
+  std::vector<uint8_t> in(64), outer(64);
+  for (int i = 0; i < 64; i++) in[i] = k[i] ^ 0x36, outer[i] = k[i] ^ 0x5c;
+  in.insert(in.end(), msg.begin(), msg.end());
+  uint8_t ih[32];
+  sha256_host(in, ih);
+  outer.insert(outer.end(), ih, ih + 32);
+  sha256_host(outer, out);
+}
+
+std::vector<uint8_t> cat(std::initializer_list<std::vector<uint8_t>> parts) {
+  std::vector<uint8_t> r;
+  for (auto& p : parts) r.insert(r.end(), p.begin(), p.end());
+  return r;
+}
+std::vector<uint8_t> bytes(const char* s) { return std::vector<uint8_t>(s, s + strlen(s)); }
+
+const std::vector<uint8_t> kSuite = {'H', 'P', 'K', 'E', 0x00, 0x20, 0x00, 0x01, 0x00, 0x01};
+
+uint32_t be32(const uint8_t* p) {
+  return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3];
+}
+uint32_t le32(const uint8_t* p) {
+  return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+}
+
+}  // namespace
+
+struct janus_hpke_opener {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  HpkeParams P;
+  uint8_t* d_pt = nullptr;
+  size_t pt_cap = 0;
+  std::mutex mu;
+  int timing = 0;
+  double ms = 0;
+  uint32_t launches = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+};
+
+#define HCHK(x)                                                                       \
+  do {                                                                                \
+    hipError_t _e = (x);                                                              \
+    if (_e != hipSuccess) {                                                           \
+      fprintf(stderr, "janus_hpke: HIP error %s at %s:%d\n", hipGetErrorString(_e),   \
+              __FILE__, __LINE__);                                                    \
+      return JANUS_HPKE_EDEVICE;                                                      \
+    }                                                                                 \
+  } while (0)
+
+extern "C" {
+
+int janus_hpke_opener_create(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id,
+                             const uint8_t* private_key, size_t private_key_len,
+                             const uint8_t* public_key, size_t public_key_len,
+                             const uint8_t* info, size_t info_len, int device,
+                             janus_hpke_opener** out) {
+  if (!out || !private_key || !public_key || (info_len && !info)) return JANUS_HPKE_EINVAL;
+  *out = nullptr;
+  if (kem_id != JANUS_HPKE_KEM_X25519_HKDF_SHA256 || kdf_id != JANUS_HPKE_KDF_HKDF_SHA256 ||
+      aead_id != JANUS_HPKE_AEAD_AES_128_GCM)
+    return JANUS_HPKE_EUNSUPPORTED;
+  if (private_key_len != 32 || public_key_len != 32) return JANUS_HPKE_EINVAL;
+  auto* o = new janus_hpke_opener();
+  o->device = device;
+  memset(&o->P, 0, sizeof(o->P));
+  uint8_t k[32];
+  memcpy(k, private_key, 32);
+  k[0] &= 248;  // decodeScalar25519 (RFC 7748 section 5)
+  k[31] &= 127;
+  k[31] |= 64;
+  for (int i = 0; i < 8; i++) o->P.sk[i] = le32(k + 4 * i), o->P.pk[i] = le32(public_key + 4 * i);
+  // key_schedule_context = mode_base || LabeledExtract("", "psk_id_hash", "") ||
+  //                        LabeledExtract("", "info_hash", info)        (RFC 9180 5.1)
+  uint8_t ksc[68] = {0};
+  std::vector<uint8_t> inf(info, info + info_len);
+  hmac_host(nullptr, 0, cat({bytes("HPKE-v1"), kSuite, bytes("psk_id_hash")}), ksc + 1);
+  hmac_host(nullptr, 0, cat({bytes("HPKE-v1"), kSuite, bytes("info_hash"), inf}), ksc + 33);
+  for (int i = 0; i < 17; i++) o->P.ksc[i] = be32(ksc + 4 * i);
+  // HMAC midstates of the empty key (eae_prk extraction)
+  uint32_t iv[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                    0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  uint8_t b36[64], b5c[64];
+  memset(b36, 0x36, 64);
+  memset(b5c, 0x5c, 64);
+  memcpy(o->P.ipad0, iv, 32);
+  memcpy(o->P.opad0, iv, 32);
+  sha256_compress_host(o->P.ipad0, b36);
+  sha256_compress_host(o->P.opad0, b5c);
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&o->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete o;
+    return JANUS_HPKE_EDEVICE;
+  }
+  *out = o;
+  return JANUS_HPKE_SUCCESS;
+}
+
+void janus_hpke_opener_destroy(janus_hpke_opener* o) {
+  if (!o) return;
+  (void)hipSetDevice(o->device);
+  (void)hipStreamSynchronize(o->stream);
+  if (o->d_pt) (void)hipFree(o->d_pt);
+  for (auto& e : o->pending) {
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  (void)hipStreamDestroy(o->stream);
+  delete o;
+}
+
+int janus_hpke_set_timing(janus_hpke_opener* o, int on) {
+  if (!o) return JANUS_HPKE_EINVAL;
+  std::lock_guard<std::mutex> lk(o->mu);
+  o->timing = on;
+  o->ms = 0;
+  o->launches = 0;
+  return JANUS_HPKE_SUCCESS;
+}
+
+int janus_hpke_timing(janus_hpke_opener* o, double* ms_total, uint32_t* launches) {
+  if (!o) return JANUS_HPKE_EINVAL;
+  std::lock_guard<std::mutex> lk(o->mu);
+  for (auto& e : o->pending) {
+    float ms = 0;
+    HCHK(hipEventSynchronize(e.second));
+    HCHK(hipEventElapsedTime(&ms, e.first, e.second));
+    o->ms += ms;
+    o->launches++;
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  o->pending.clear();
+  if (ms_total) *ms_total = o->ms;
+  if (launches) *launches = o->launches;
+  return JANUS_HPKE_SUCCESS;
+}
+
+}  // extern "C"
+
+static int launch_open(janus_hpke_opener* o, int mode, int pub, const OpenArgs& a,
+                       hipStream_t st) {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (o->timing) {
+    HCHK(hipEventCreate(&e0));
+    HCHK(hipEventCreate(&e1));
+    HCHK(hipEventRecord(e0, st));
+  }
+  const uint32_t blocks = (a.n + 255) / 256;
+  if (mode == 0)
+    k_hpke_open<0, 0><<<blocks, 256, 0, st>>>(o->P, a);
+  else if (pub == 32)
+    k_hpke_open<1, 32><<<blocks, 256, 0, st>>>(o->P, a);
+  else
+    k_hpke_open<1, 0><<<blocks, 256, 0, st>>>(o->P, a);
+  HCHK(hipGetLastError());
+  if (o->timing) {
+    HCHK(hipEventRecord(e1, st));
+    o->pending.push_back({e0, e1});
+  }
+  return JANUS_HPKE_SUCCESS;
+}
+
+static int ensure_pt(janus_hpke_opener* o, size_t bytes) {
+  if (bytes <= o->pt_cap) return JANUS_HPKE_SUCCESS;
+  if (o->d_pt) HCHK(hipFree(o->d_pt));
+  o->d_pt = nullptr;
+  HCHK(hipMalloc((void**)&o->d_pt, bytes));
+  o->pt_cap = bytes;
+  return JANUS_HPKE_SUCCESS;
+}
+
+extern "C" {
+
+int janus_hpke_open_input_shares_device(janus_hpke_opener* o, uint32_t n,
+                                        const uint8_t task_id[32], const uint8_t* d_enc,
+                                        const uint8_t* d_ct, const uint32_t* d_ct_len,
+                                        uint32_t ct_stride, const uint8_t* d_report_ids,
+                                        const uint64_t* d_times, const uint8_t* d_public_shares,
+                                        uint32_t public_share_len, uint32_t helper_share_len,
+                                        int require_taskprov, uint8_t* d_helper_shares,
+                                        uint8_t* d_status, void* stream) {
+  if (!o || !task_id) return JANUS_HPKE_EINVAL;
+  if (n == 0) return JANUS_HPKE_SUCCESS;
+  if (!d_enc || !d_ct || !d_ct_len || !d_report_ids || !d_times || !d_helper_shares ||
+      !d_status || ct_stride == 0 || ct_stride % 16 != 0 ||
+      (public_share_len != 0 && public_share_len != 32) || (public_share_len && !d_public_shares))
+    return JANUS_HPKE_EINVAL;
+  std::lock_guard<std::mutex> lk(o->mu);
+  HCHK(hipSetDevice(o->device));
+  int rc = ensure_pt(o, (size_t)n * ct_stride);
+  if (rc) return rc;
+  for (int i = 0; i < 8; i++) o->P.task[i] = be32(task_id + 4 * i);
+  OpenArgs a{};
+  a.n = n;
+  a.ct_stride = ct_stride;
+  a.share_len = helper_share_len;
+  a.require_taskprov = require_taskprov;
+  a.enc = d_enc;
+  a.ct = d_ct;
+  a.ct_len = d_ct_len;
+  a.ids = d_report_ids;
+  a.times = d_times;
+  a.pubs = d_public_shares;
+  a.pt = o->d_pt;
+  a.shares = d_helper_shares;
+  a.status = d_status;
+  return launch_open(o, 1, (int)public_share_len, a, (hipStream_t)stream);
+}
+
+int janus_hpke_open_device(janus_hpke_opener* o, uint32_t n, const uint8_t* d_enc,
+                           const uint8_t* d_ct, const uint32_t* d_ct_len, uint32_t ct_stride,
+                           const uint8_t* d_aad, const uint32_t* d_aad_len, uint32_t aad_stride,
+                           uint8_t* d_pt, uint8_t* d_status, void* stream) {
+  if (!o) return JANUS_HPKE_EINVAL;
+  if (n == 0) return JANUS_HPKE_SUCCESS;
+  if (!d_enc || !d_ct || !d_ct_len || !d_pt || !d_status || ct_stride == 0 ||
+      ct_stride % 16 != 0 || aad_stride % 16 != 0 || (aad_stride && (!d_aad || !d_aad_len)))
+    return JANUS_HPKE_EINVAL;
+  std::lock_guard<std::mutex> lk(o->mu);
+  HCHK(hipSetDevice(o->device));
+  OpenArgs a{};
+  a.n = n;
+  a.ct_stride = ct_stride;
+  a.aad_stride = aad_stride;
+  a.enc = d_enc;
+  a.ct = d_ct;
+  a.ct_len = d_ct_len;
+  a.aad = d_aad;
+  a.aad_len = d_aad_len;
+  a.pt = d_pt;
+  a.status = d_status;
+  return launch_open(o, 0, 0, a, (hipStream_t)stream);
+}
+
+}  // extern "C"
+
+namespace {
+struct DevBuf {
+  void* p = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+int up(DevBuf& b, const void* h, size_t bytes, hipStream_t st) {
+  if (!h || !bytes) return JANUS_HPKE_SUCCESS;
+  HCHK(hipMalloc(&b.p, bytes));
+  HCHK(hipMemcpyAsync(b.p, h, bytes, hipMemcpyHostToDevice, st));
+  return JANUS_HPKE_SUCCESS;
+}
+}  // namespace
+
+extern "C" {
+
+int janus_hpke_open_input_shares(janus_hpke_opener* o, uint32_t n, const uint8_t task_id[32],
+                                 const uint8_t* enc, const uint8_t* ct, const uint32_t* ct_len,
+                                 uint32_t ct_stride, const uint8_t* report_ids,
+                                 const uint64_t* times, const uint8_t* public_shares,
+                                 uint32_t public_share_len, uint32_t helper_share_len,
+                                 int require_taskprov, uint8_t* helper_shares, uint8_t* status) {
+  if (!o) return JANUS_HPKE_EINVAL;
+  if (n == 0) return JANUS_HPKE_SUCCESS;
+  HCHK(hipSetDevice(o->device));
+  DevBuf de, dc, dl, di, dt, dp, ds, dst;
+  int rc;
+  if ((rc = up(de, enc, 32 * (size_t)n, o->stream)) || (rc = up(dc, ct, (size_t)ct_stride * n, o->stream)) ||
+      (rc = up(dl, ct_len, 4 * (size_t)n, o->stream)) ||
+      (rc = up(di, report_ids, 16 * (size_t)n, o->stream)) ||
+      (rc = up(dt, times, 8 * (size_t)n, o->stream)) ||
+      (rc = up(dp, public_shares, (size_t)public_share_len * n, o->stream)))
+    return rc;
+  HCHK(hipMalloc(&ds.p, (size_t)helper_share_len * n + 1));
+  HCHK(hipMalloc(&dst.p, n));
+  rc = janus_hpke_open_input_shares_device(
+      o, n, task_id, (const uint8_t*)de.p, (const uint8_t*)dc.p, (const uint32_t*)dl.p, ct_stride,
+      (const uint8_t*)di.p, (const uint64_t*)dt.p, (const uint8_t*)dp.p, public_share_len,
+      helper_share_len, require_taskprov, (uint8_t*)ds.p, (uint8_t*)dst.p, o->stream);
+  if (rc) return rc;
+  HCHK(hipMemcpyAsync(helper_shares, ds.p, (size_t)helper_share_len * n, hipMemcpyDeviceToHost,
+                      o->stream));
+  HCHK(hipMemcpyAsync(status, dst.p, n, hipMemcpyDeviceToHost, o->stream));
+  HCHK(hipStreamSynchronize(o->stream));
+  return JANUS_HPKE_SUCCESS;
+}
+
+int janus_hpke_open(janus_hpke_opener* o, uint32_t n, const uint8_t* enc, const uint8_t* ct,
+                    const uint32_t* ct_len, uint32_t ct_stride, const uint8_t* aad,
+                    const uint32_t* aad_len, uint32_t aad_stride, uint8_t* pt, uint8_t* status) {
+  if (!o) return JANUS_HPKE_EINVAL;
+  if (n == 0) return JANUS_HPKE_SUCCESS;
+  HCHK(hipSetDevice(o->device));
+  DevBuf de, dc, dl, da, dal, dpt, dst;
+  int rc;
+  if ((rc = up(de, enc, 32 * (size_t)n, o->stream)) || (rc = up(dc, ct, (size_t)ct_stride * n, o->stream)) ||
+      (rc = up(dl, ct_len, 4 * (size_t)n, o->stream)) ||
+      (rc = up(da, aad, (size_t)aad_stride * n, o->stream)) ||
+      (rc = up(dal, aad_len, aad_stride ? 4 * (size_t)n : 0, o->stream)))
+    return rc;
+  HCHK(hipMalloc(&dpt.p, (size_t)ct_stride * n));
+  HCHK(hipMalloc(&dst.p, n));
+  rc = janus_hpke_open_device(o, n, (const uint8_t*)de.p, (const uint8_t*)dc.p,
+                              (const uint32_t*)dl.p, ct_stride, (const uint8_t*)da.p,
+                              (const uint32_t*)dal.p, aad_stride, (uint8_t*)dpt.p,
+                              (uint8_t*)dst.p, o->stream);
+  if (rc) return rc;
+  HCHK(hipMemcpyAsync(pt, dpt.p, (size_t)ct_stride * n, hipMemcpyDeviceToHost, o->stream));
+  HCHK(hipMemcpyAsync(status, dst.p, n, hipMemcpyDeviceToHost, o->stream));
+  HCHK(hipStreamSynchronize(o->stream));
+  return JANUS_HPKE_SUCCESS;
+}
+
+}  // extern "C"

@@ -30,6 +30,7 @@
 #include "prio3_device.h"
 
 #include "prio3_common.h"
+#include "sha256_device.h"
 
 #ifndef XOFD_OCC
 #define XOFD_OCC 3
@@ -1832,20 +1833,6 @@ __global__ void k_combine(uint32_t k, uint32_t len, uint32_t n_segments, const u
 // XOR / min / max reduction when the block's 256 reports share a segment (the common case:
 // contiguous batches) and per-report atomics on the segment otherwise.
 // ------------------------------------------------------------------------------------
-__constant__ uint32_t c_sha256_k[64] = {
-    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u,
-    0xab1c5ed5u, 0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu,
-    0x9bdc06a7u, 0xc19bf174u, 0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu,
-    0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau, 0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u,
-    0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u, 0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu,
-    0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u, 0xa2bfe8a1u, 0xa81a664bu,
-    0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u, 0x19a4c116u,
-    0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
-    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u,
-    0xc67178f2u};
-
-DEV uint32_t rotr32(uint32_t x, uint32_t n) { return __builtin_amdgcn_alignbit(x, x, n); }
-
 // SHA-256 of the 16 bytes id[0..3] (little-endian words as loaded); the digest is returned as
 // 8 little-endian words of its byte string (so a byte-wise XOR is a word-wise XOR).
 DEV void sha256_id16(const uint32_t id[4], uint32_t out[8]) {
@@ -1856,37 +1843,12 @@ DEV void sha256_id16(const uint32_t id[4], uint32_t out[8]) {
 #pragma unroll
   for (int i = 5; i < 15; i++) w[i] = 0;
   w[15] = 128;  // message length in bits
-  uint32_t a = 0x6a09e667u, b = 0xbb67ae85u, c = 0x3c6ef372u, d = 0xa54ff53au;
-  uint32_t e = 0x510e527fu, f = 0x9b05688cu, g = 0x1f83d9abu, h = 0x5be0cd19u;
+  uint32_t st[8];
 #pragma unroll
-  for (int t = 0; t < 64; t++) {
-    uint32_t wt;
-    if (t < 16) {
-      wt = w[t];
-    } else {  // rolling 16-word schedule
-      const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
-      const uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
-      const uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
-      wt = w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
-    }
-    const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
-    const uint32_t ch = (e & f) ^ (~e & g);
-    const uint32_t t1 = h + S1 + ch + c_sha256_k[t] + wt;
-    const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
-    const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
-    h = g;
-    g = f;
-    f = e;
-    e = d + t1;
-    d = c;
-    c = b;
-    b = a;
-    a = t1 + S0 + mj;
-  }
-  const uint32_t H[8] = {a + 0x6a09e667u, b + 0xbb67ae85u, c + 0x3c6ef372u, d + 0xa54ff53au,
-                         e + 0x510e527fu, f + 0x9b05688cu, g + 0x1f83d9abu, h + 0x5be0cd19u};
+  for (int i = 0; i < 8; i++) st[i] = sha256d::IV[i];
+  sha256d::compress(st, w);
 #pragma unroll
-  for (int i = 0; i < 8; i++) out[i] = __builtin_bswap32(H[i]);
+  for (int i = 0; i < 8; i++) out[i] = __builtin_bswap32(st[i]);
 }
 
 // checksums[s][8 words] = 0, intervals[s] = (UINT64_MAX, 0) as a (min start, max end) pair

@@ -82,6 +82,12 @@ EXPORTED_SYMBOLS = (
     "prio3_device_leader_prepare_next", "prio3_device_batch_metadata", "prio3_batch_metadata",
     "prio3_device_combine_metadata",
 )
+# include/janus_hpke.h (the batched HPKE opener, janus_amd/hpke.py)
+HPKE_EXPORTED_SYMBOLS = (
+    "janus_hpke_opener_create", "janus_hpke_opener_destroy",
+    "janus_hpke_open_input_shares_device", "janus_hpke_open_input_shares",
+    "janus_hpke_open_device", "janus_hpke_open", "janus_hpke_set_timing", "janus_hpke_timing",
+)
 
 _lib = None
 

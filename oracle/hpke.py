@@ -1,0 +1,125 @@
+"""ctypes binding of oracle/hpke_oracle.c -- TEST INFRASTRUCTURE (checker + CPU baseline).
+
+HPKE base mode, DHKEM(X25519, HKDF-SHA256) / HKDF-SHA256 / AES-128-GCM (RFC 9180) composed over
+OpenSSL 3.0 primitives, plus Janus's helper input-share layer (aggregator.rs:1796-1990).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "build", "libhpke_oracle.so")
+INFO_INPUT_SHARE_HELPER = b"dap-09 input share" + bytes([1, 3])  # Role::Client, Role::Helper
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB) or \
+                os.path.getmtime(_LIB) < os.path.getmtime(os.path.join(_HERE, "hpke_oracle.c")):
+            subprocess.run(["make", "-s", "-C", _HERE], check=True)
+        _lib = C.CDLL(_LIB)
+        vp = C.c_void_p
+        _lib.hpke_open.argtypes = [vp, vp, vp, vp, C.c_size_t, vp, C.c_size_t, vp, C.c_size_t, vp]
+        _lib.hpke_seal.argtypes = [vp, vp, vp, C.c_size_t, vp, C.c_size_t, vp, C.c_size_t, vp, vp]
+        _lib.hpke_x25519_public.argtypes = [vp, vp]
+        _lib.hpke_input_share_aad.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint32, vp]
+        _lib.hpke_input_share_aad.restype = C.c_size_t
+        _lib.hpke_open_input_shares.argtypes = [vp, vp, vp, C.c_uint32, vp, vp, vp, C.c_uint32,
+                                                vp, vp, vp, C.c_uint32, C.c_uint32, C.c_int, vp,
+                                                vp, C.c_int]
+    return _lib
+
+
+def _p(b):
+    if b is None:
+        return None
+    if isinstance(b, np.ndarray):
+        return b.ctypes.data_as(C.c_void_p)
+    return C.cast(C.c_char_p(bytes(b)), C.c_void_p)
+
+
+def x25519_public(sk: bytes) -> bytes:
+    out = C.create_string_buffer(32)
+    assert lib().hpke_x25519_public(_p(sk), out) == 0
+    return out.raw
+
+
+def open_(skR: bytes, pkR: bytes, enc: bytes, info: bytes, aad: bytes, ct: bytes):
+    pt = C.create_string_buffer(max(len(ct), 1))
+    n = lib().hpke_open(_p(skR), _p(pkR), _p(enc), _p(info), len(info), _p(aad), len(aad),
+                        _p(ct), len(ct), pt)
+    return None if n < 0 else pt.raw[:n]
+
+
+def seal(pkR: bytes, skE: bytes, info: bytes, aad: bytes, pt: bytes):
+    enc = C.create_string_buffer(32)
+    ct = C.create_string_buffer(len(pt) + 16)
+    assert lib().hpke_seal(_p(pkR), _p(skE), _p(info), len(info), _p(aad), len(aad), _p(pt),
+                           len(pt), enc, ct) == 0
+    return enc.raw, ct.raw
+
+
+def input_share_aad(task_id: bytes, report_id: bytes, time: int, public_share: bytes) -> bytes:
+    out = C.create_string_buffer(64 + 4 + len(public_share))
+    n = lib().hpke_input_share_aad(_p(task_id), _p(report_id), time, _p(public_share),
+                                   len(public_share), out)
+    return out.raw[:n]
+
+
+def plaintext_input_share(payload: bytes, extensions=()) -> bytes:
+    """PlaintextInputShare encoding (messages/src/lib.rs:1326-1341)."""
+    ext = b"".join(t.to_bytes(2, "big") + len(d).to_bytes(2, "big") + d for t, d in extensions)
+    return len(ext).to_bytes(2, "big") + ext + len(payload).to_bytes(4, "big") + payload
+
+
+def open_input_shares(skR, pkR, task_id, enc, ct, ct_len, report_ids, times, pubs, share_len,
+                      require_taskprov=False, n_threads=8):
+    """Batched helper input-share open: (shares [n, share_len], status [n] in {0, 4, 8})."""
+    n = enc.shape[0]
+    enc = np.ascontiguousarray(enc, np.uint8)
+    ct = np.ascontiguousarray(ct, np.uint8)
+    ct_len = np.ascontiguousarray(ct_len, np.uint32)
+    ids = np.ascontiguousarray(report_ids, np.uint8)
+    times = np.ascontiguousarray(times, np.uint64)
+    publen = 0 if pubs is None else pubs.shape[1]
+    pubs = None if pubs is None else np.ascontiguousarray(pubs, np.uint8)
+    shares = np.zeros((n, share_len), np.uint8)
+    status = np.zeros(n, np.uint8)
+    lib().hpke_open_input_shares(_p(skR), _p(pkR), _p(task_id), n, _p(enc), _p(ct), _p(ct_len),
+                                 ct.shape[1], _p(ids), _p(times), _p(pubs), publen, share_len,
+                                 int(require_taskprov), _p(shares), _p(status), n_threads)
+    return shares, status
+
+
+def make_batch(n, share_len, pub_len, seed=1, skR=None, extensions=(), tamper=0.0):
+    """Synthetic Janus-shaped encrypted helper input shares (test/bench data), sealed by the
+    oracle with deterministic ephemeral keys.  Returns a dict of numpy arrays."""
+    rng = np.random.default_rng(seed)
+    skR = bytes(rng.integers(0, 256, 32, dtype=np.uint8)) if skR is None else skR
+    pkR = x25519_public(skR)
+    task_id = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+    ids = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    times = (1_700_000_000 + rng.integers(0, 3600, n)).astype(np.uint64)
+    pubs = rng.integers(0, 256, (n, pub_len), dtype=np.uint8) if pub_len else None
+    shares = rng.integers(0, 256, (n, share_len), dtype=np.uint8)
+    pt_len = len(plaintext_input_share(bytes(share_len), extensions))
+    stride = pt_len + 16
+    enc = np.zeros((n, 32), np.uint8)
+    ct = np.zeros((n, stride), np.uint8)
+    ct_len = np.full(n, stride, np.uint32)
+    for r in range(n):
+        aad = input_share_aad(task_id, ids[r].tobytes(), int(times[r]),
+                              b"" if pubs is None else pubs[r].tobytes())
+        skE = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+        e, c = seal(pkR, skE, INFO_INPUT_SHARE_HELPER, aad,
+                    plaintext_input_share(shares[r].tobytes(), extensions))
+        enc[r] = np.frombuffer(e, np.uint8)
+        ct[r] = np.frombuffer(c, np.uint8)
+    return dict(skR=skR, pkR=pkR, task_id=task_id, report_ids=ids, times=times, pubs=pubs,
+                shares=shares, enc=enc, ct=ct, ct_len=ct_len)

@@ -1,0 +1,268 @@
+/*
+ * hpke_oracle.c -- CPU restatement of the helper's input-share decryption.
+ * TEST INFRASTRUCTURE ONLY: the checker for tests/ and bench.py's cpu_baseline leg.
+ *
+ * HPKE base mode (RFC 9180 §5.1, §5.2) with DHKEM(X25519, HKDF-SHA256) (§4.1, §7.1),
+ * HKDF-SHA256 and AES-128-GCM -- the suite Janus generates by default
+ * (/root/reference/core/src/hpke.rs:260-280, generate_test_hpke_config_and_private_key), whose
+ * Rust implementation (hpke-dispatch -> hpke crate) is not in /root/reference.  The RFC 9180
+ * composition (labels, suite ids, key schedule) is restated here over OpenSSL 3.0 primitives
+ * (X25519, HMAC-SHA256, AES-128-GCM); it is pinned by the RFC 9180 test vector that Janus's
+ * own test reads (core/src/test-vectors.json, mode 0 / kem 0x20 / kdf 1 / aead 1,
+ * hpke.rs:480-560).
+ *
+ * The Janus layer around hpke::open follows aggregator.rs:1796-1990: application info
+ * "dap-09 input share" || Role::Client || Role::Helper (hpke.rs:55-85), AAD = InputShareAad
+ * { task_id, ReportMetadata { report_id, time }, public_share } (messages/src/lib.rs:1825-1872),
+ * then PlaintextInputShare::get_decoded (lib.rs:1301-1350), the duplicate-extension and
+ * taskprov-extension checks, and the exact-length helper input share decode.
+ */
+#define OPENSSL_SUPPRESS_DEPRECATED
+#include <openssl/evp.h>
+#include <openssl/hmac.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+enum { HPKE_OK = 0, HPKE_DECRYPT_ERROR = 4, HPKE_INVALID_MESSAGE = 8 };
+
+static const uint8_t KEM_SUITE[5] = {'K', 'E', 'M', 0x00, 0x20};
+static const uint8_t HPKE_SUITE[10] = {'H', 'P', 'K', 'E', 0x00, 0x20, 0x00, 0x01, 0x00, 0x01};
+
+static void hmac256(const uint8_t* key, size_t klen, const uint8_t* msg, size_t mlen,
+                    uint8_t out[32]) {
+  unsigned int ol = 32;
+  static const uint8_t zero = 0;
+  HMAC(EVP_sha256(), klen ? key : &zero, (int)klen, msg, mlen, out, &ol);
+}
+
+/* LabeledExtract(salt, label, ikm) = HKDF-Extract(salt, "HPKE-v1" || suite_id || label || ikm) */
+static void labeled_extract(const uint8_t* suite, size_t slen, const uint8_t* salt, size_t saltlen,
+                            const char* label, const uint8_t* ikm, size_t ikmlen, uint8_t out[32]) {
+  uint8_t buf[256];
+  size_t l = 0, ll = strlen(label);
+  memcpy(buf + l, "HPKE-v1", 7), l += 7;
+  memcpy(buf + l, suite, slen), l += slen;
+  memcpy(buf + l, label, ll), l += ll;
+  memcpy(buf + l, ikm, ikmlen), l += ikmlen;
+  hmac256(salt, saltlen, buf, l, out);
+}
+
+/* LabeledExpand(prk, label, info, L <= 32) = HKDF-Expand(prk, I2OSP(L, 2) || "HPKE-v1" ||
+ * suite_id || label || info, L): one HMAC block T(1) = HMAC(prk, labeled_info || 0x01) */
+static void labeled_expand(const uint8_t* suite, size_t slen, const uint8_t prk[32],
+                           const char* label, const uint8_t* info, size_t infolen, size_t L,
+                           uint8_t* out) {
+  uint8_t buf[256], t[32];
+  size_t l = 0, ll = strlen(label);
+  buf[l++] = (uint8_t)(L >> 8);
+  buf[l++] = (uint8_t)L;
+  memcpy(buf + l, "HPKE-v1", 7), l += 7;
+  memcpy(buf + l, suite, slen), l += slen;
+  memcpy(buf + l, label, ll), l += ll;
+  memcpy(buf + l, info, infolen), l += infolen;
+  buf[l++] = 0x01;
+  hmac256(prk, 32, buf, l, t);
+  memcpy(out, t, L);
+}
+
+static int x25519(const uint8_t sk[32], const uint8_t pk[32], uint8_t out[32]) {
+  EVP_PKEY* k = EVP_PKEY_new_raw_private_key(EVP_PKEY_X25519, NULL, sk, 32);
+  EVP_PKEY* p = EVP_PKEY_new_raw_public_key(EVP_PKEY_X25519, NULL, pk, 32);
+  EVP_PKEY_CTX* c = k ? EVP_PKEY_CTX_new(k, NULL) : NULL;
+  size_t ol = 32;
+  int ok = c && p && EVP_PKEY_derive_init(c) == 1 && EVP_PKEY_derive_set_peer(c, p) == 1 &&
+           EVP_PKEY_derive(c, out, &ol) == 1 && ol == 32;
+  EVP_PKEY_CTX_free(c);
+  EVP_PKEY_free(k);
+  EVP_PKEY_free(p);
+  return ok ? 0 : -1;
+}
+
+int hpke_x25519_public(const uint8_t sk[32], uint8_t pk[32]) {
+  EVP_PKEY* k = EVP_PKEY_new_raw_private_key(EVP_PKEY_X25519, NULL, sk, 32);
+  size_t ol = 32;
+  int ok = k && EVP_PKEY_get_raw_public_key(k, pk, &ol) == 1 && ol == 32;
+  EVP_PKEY_free(k);
+  return ok ? 0 : -1;
+}
+
+/* KeySchedule(mode_base, shared_secret, info) -> key (16), base_nonce (12)  [RFC 9180 §5.1] */
+static void key_schedule(const uint8_t ss[32], const uint8_t* info, size_t infolen,
+                         uint8_t key[16], uint8_t nonce[12]) {
+  uint8_t ksc[65], secret[32];
+  ksc[0] = 0x00;  /* mode_base */
+  labeled_extract(HPKE_SUITE, 10, NULL, 0, "psk_id_hash", NULL, 0, ksc + 1);
+  labeled_extract(HPKE_SUITE, 10, NULL, 0, "info_hash", info, infolen, ksc + 33);
+  labeled_extract(HPKE_SUITE, 10, ss, 32, "secret", NULL, 0, secret);
+  labeled_expand(HPKE_SUITE, 10, secret, "key", ksc, 65, 16, key);
+  labeled_expand(HPKE_SUITE, 10, secret, "base_nonce", ksc, 65, 12, nonce);
+}
+
+/* Decap (§4.1): dh = DH(skR, enc); shared_secret = ExtractAndExpand(dh, enc || pkRm) */
+static int decap(const uint8_t enc[32], const uint8_t skR[32], const uint8_t pkR[32],
+                 uint8_t ss[32]) {
+  uint8_t dh[32], prk[32], kc[64];
+  if (x25519(skR, enc, dh)) return -1;
+  static const uint8_t zero32[32];
+  if (!memcmp(dh, zero32, 32)) return -1; /* all-zero shared secret: ValidationError */
+  labeled_extract(KEM_SUITE, 5, NULL, 0, "eae_prk", dh, 32, prk);
+  memcpy(kc, enc, 32);
+  memcpy(kc + 32, pkR, 32);
+  labeled_expand(KEM_SUITE, 5, prk, "shared_secret", kc, 64, 32, ss);
+  return 0;
+}
+
+static int gcm(int decrypt, const uint8_t key[16], const uint8_t nonce[12], const uint8_t* aad,
+               size_t aadlen, const uint8_t* in, size_t inlen, uint8_t* out, uint8_t tag[16]) {
+  EVP_CIPHER_CTX* c = EVP_CIPHER_CTX_new();
+  int l = 0;
+  int ok = c && EVP_CipherInit_ex(c, EVP_aes_128_gcm(), NULL, NULL, NULL, !decrypt) == 1 &&
+                  EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_IVLEN, 12, NULL) == 1 &&
+                  EVP_CipherInit_ex(c, NULL, NULL, key, nonce, !decrypt) == 1;
+  if (ok && aadlen) ok = EVP_CipherUpdate(c, NULL, &l, aad, (int)aadlen) == 1;
+  if (ok && inlen) ok = EVP_CipherUpdate(c, out, &l, in, (int)inlen) == 1;
+  if (ok && decrypt) ok = EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_TAG, 16, tag) == 1;
+  int fl = 0;
+  if (ok) ok = EVP_CipherFinal_ex(c, out + l, &fl) == 1;
+  if (ok && !decrypt) ok = EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_GET_TAG, 16, tag) == 1;
+  EVP_CIPHER_CTX_free(c);
+  return ok ? 0 : -1;
+}
+
+/* base-mode single-shot open (sequence number 0); returns the plaintext length or -1 */
+int hpke_open(const uint8_t skR[32], const uint8_t pkR[32], const uint8_t enc[32],
+              const uint8_t* info, size_t infolen, const uint8_t* aad, size_t aadlen,
+              const uint8_t* ct, size_t ctlen, uint8_t* pt) {
+  uint8_t ss[32], key[16], nonce[12], tag[16];
+  if (ctlen < 16 || decap(enc, skR, pkR, ss)) return -1;
+  key_schedule(ss, info, infolen, key, nonce);
+  memcpy(tag, ct + ctlen - 16, 16);
+  if (gcm(1, key, nonce, aad, aadlen, ct, ctlen - 16, pt, tag)) return -1;
+  return (int)(ctlen - 16);
+}
+
+/* base-mode seal with the ephemeral key skE (Encap with a given ephemeral key, as the RFC 9180
+ * test vectors do); writes enc[32] and ct[ptlen + 16] */
+int hpke_seal(const uint8_t pkR[32], const uint8_t skE[32], const uint8_t* info, size_t infolen,
+              const uint8_t* aad, size_t aadlen, const uint8_t* pt, size_t ptlen, uint8_t enc[32],
+              uint8_t* ct) {
+  uint8_t dh[32], prk[32], kc[64], ss[32], key[16], nonce[12];
+  if (hpke_x25519_public(skE, enc) || x25519(skE, pkR, dh)) return -1;
+  labeled_extract(KEM_SUITE, 5, NULL, 0, "eae_prk", dh, 32, prk);
+  memcpy(kc, enc, 32);
+  memcpy(kc + 32, pkR, 32);
+  labeled_expand(KEM_SUITE, 5, prk, "shared_secret", kc, 64, 32, ss);
+  key_schedule(ss, info, infolen, key, nonce);
+  return gcm(0, key, nonce, aad, aadlen, pt, ptlen, ct, ct + ptlen);
+}
+
+/* ---- Janus helper layer ------------------------------------------------------------ */
+
+/* PlaintextInputShare::get_decoded + extension checks + helper input share length
+ * (aggregator.rs:1893-1990).  Returns HPKE_OK and copies the payload, or HPKE_INVALID_MESSAGE. */
+static int decode_plaintext(const uint8_t* pt, size_t len, uint32_t share_len,
+                            int require_taskprov, uint8_t* share_out) {
+  if (len < 2) return HPKE_INVALID_MESSAGE;
+  size_t el = ((size_t)pt[0] << 8) | pt[1], p = 2;
+  if (p + el > len) return HPKE_INVALID_MESSAGE;
+  uint16_t seen[64];
+  int ns = 0, taskprov_ok = 0, taskprov_seen = 0;
+  size_t q = p;
+  while (q < p + el) {
+    if (q + 4 > p + el) return HPKE_INVALID_MESSAGE;
+    uint16_t ty = (uint16_t)((pt[q] << 8) | pt[q + 1]);
+    size_t dl = ((size_t)pt[q + 2] << 8) | pt[q + 3];
+    if (q + 4 + dl > p + el) return HPKE_INVALID_MESSAGE;
+    if (ty != 0 && ty != 0xFF00) return HPKE_INVALID_MESSAGE; /* ExtensionType::try_from */
+    for (int i = 0; i < ns; i++)
+      if (seen[i] == ty) return HPKE_INVALID_MESSAGE; /* duplicate extension */
+    if (ns < 64) seen[ns++] = ty;
+    if (ty == 0xFF00) { /* ExtensionType::Taskprov */
+      taskprov_seen = 1;
+      taskprov_ok = dl == 0;
+    }
+    q += 4 + dl;
+  }
+  p += el;
+  if (p + 4 > len) return HPKE_INVALID_MESSAGE;
+  size_t pl = ((size_t)pt[p] << 24) | ((size_t)pt[p + 1] << 16) | ((size_t)pt[p + 2] << 8) | pt[p + 3];
+  p += 4;
+  if (p + pl != len) return HPKE_INVALID_MESSAGE; /* trailing or missing bytes */
+  if (require_taskprov ? !taskprov_ok : taskprov_seen) return HPKE_INVALID_MESSAGE;
+  if (pl != share_len) return HPKE_INVALID_MESSAGE;  /* Prio3 helper share: fixed seeds */
+  memcpy(share_out, pt + p, pl);
+  return HPKE_OK;
+}
+
+/* InputShareAad { task_id, ReportMetadata { report_id, time (u64 BE) }, public_share (u32
+ * length-prefixed) } (messages/src/lib.rs:1825-1872, 1257-1300) */
+size_t hpke_input_share_aad(const uint8_t task_id[32], const uint8_t report_id[16], uint64_t time,
+                            const uint8_t* pub, uint32_t publen, uint8_t* out) {
+  size_t l = 0;
+  memcpy(out, task_id, 32), l += 32;
+  memcpy(out + l, report_id, 16), l += 16;
+  for (int i = 7; i >= 0; i--) out[l++] = (uint8_t)(time >> (8 * i));
+  out[l++] = (uint8_t)(publen >> 24), out[l++] = (uint8_t)(publen >> 16);
+  out[l++] = (uint8_t)(publen >> 8), out[l++] = (uint8_t)publen;
+  if (publen) memcpy(out + l, pub, publen), l += publen;
+  return l;
+}
+
+typedef struct {
+  const uint8_t *skR, *pkR, *task_id, *enc, *ct, *report_ids, *pubs;
+  const uint32_t* ct_len;
+  const uint64_t* times;
+  uint32_t n, ct_stride, publen, share_len;
+  int require_taskprov;
+  uint8_t *shares, *status;
+  uint32_t lo, hi;
+} Job;
+
+static const uint8_t INFO[20] = {'d', 'a', 'p', '-', '0', '9', ' ', 'i', 'n', 'p',
+                                 'u', 't', ' ', 's', 'h', 'a', 'r', 'e', 1, 3};
+
+static void* run(void* arg) {
+  Job* j = (Job*)arg;
+  uint8_t aad[256], pt[4096];
+  for (uint32_t r = j->lo; r < j->hi; r++) {
+    size_t al = hpke_input_share_aad(j->task_id, j->report_ids + 16 * (size_t)r, j->times[r],
+                                     j->pubs ? j->pubs + (size_t)j->publen * r : NULL, j->publen,
+                                     aad);
+    uint32_t cl = j->ct_len[r];
+    int ptl = cl <= sizeof(pt) + 16
+                  ? hpke_open(j->skR, j->pkR, j->enc + 32 * (size_t)r, INFO, sizeof(INFO), aad, al,
+                              j->ct + (size_t)j->ct_stride * r, cl, pt)
+                  : -1;
+    uint8_t* so = j->shares + (size_t)j->share_len * r;
+    memset(so, 0, j->share_len);
+    j->status[r] = ptl < 0 ? HPKE_DECRYPT_ERROR
+                           : (uint8_t)decode_plaintext(pt, (size_t)ptl, j->share_len,
+                                                       j->require_taskprov, so);
+    if (j->status[r]) memset(so, 0, j->share_len);
+  }
+  return NULL;
+}
+
+/* Batched helper input-share open: status[r] = 0 (helper share written), 4 (HpkeDecryptError)
+ * or 8 (InvalidMessage), the PrepareError codes of messages/src/lib.rs. */
+int hpke_open_input_shares(const uint8_t skR[32], const uint8_t pkR[32], const uint8_t task_id[32],
+                           uint32_t n, const uint8_t* enc, const uint8_t* ct, const uint32_t* ct_len,
+                           uint32_t ct_stride, const uint8_t* report_ids, const uint64_t* times,
+                           const uint8_t* pubs, uint32_t publen, uint32_t share_len,
+                           int require_taskprov, uint8_t* shares, uint8_t* status, int n_threads) {
+  if (n_threads < 1) n_threads = 1;
+  pthread_t th[256];
+  Job jobs[256];
+  if (n_threads > 256) n_threads = 256;
+  for (int t = 0; t < n_threads; t++) {
+    jobs[t] = (Job){skR, pkR, task_id, enc, ct, report_ids, pubs, ct_len, times, n, ct_stride,
+                    publen, share_len, require_taskprov, shares, status,
+                    (uint32_t)((uint64_t)n * t / n_threads),
+                    (uint32_t)((uint64_t)n * (t + 1) / n_threads)};
+    pthread_create(&th[t], NULL, run, &jobs[t]);
+  }
+  for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+  return 0;
+}

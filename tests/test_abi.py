@@ -22,6 +22,26 @@ def test_header_declares_the_exported_set():
     assert _declared_symbols() == sorted(J.EXPORTED_SYMBOLS)
 
 
+def _declared_hpke_symbols():
+    src = open(os.path.join(ROOT, "include", "janus_hpke.h")).read()
+    return sorted(set(re.findall(r"^(?:int|void)\s+(janus_hpke_\w+)\s*\(", src, re.M)))
+
+
+def test_hpke_header_declares_the_exported_set():
+    from janus_amd import prio3 as J
+    assert _declared_hpke_symbols() == sorted(J.HPKE_EXPORTED_SYMBOLS)
+    L = J.load_library()
+    for name in _declared_hpke_symbols():
+        assert hasattr(L, name), name
+
+
+def test_hpke_unsupported_suite_is_refused():
+    """P-256 / other suites stay on the host path: creation says EUNSUPPORTED (no GPU call)."""
+    from janus_amd import hpke as H
+    with pytest.raises(NotImplementedError):
+        H.HpkeOpener(bytes(32), bytes(65), kem_id=0x0010)
+
+
 def test_library_exports_every_declared_symbol():
     from janus_amd import prio3 as J
     L = J.load_library()

@@ -1,0 +1,143 @@
+"""Batched HPKE open of DAP helper input shares.
+
+Pinned: the oracle (oracle/hpke_oracle.c: RFC 9180 composition over OpenSSL primitives) against
+the RFC 9180 test vector Janus's own HPKE test reads (core/src/test-vectors.json ->
+tests/golden/hpke_rfc9180_x25519.json); then the GPU opener against that vector and against the
+oracle on Janus-shaped batches (InputShareAad, PlaintextInputShare, extensions, tampering),
+following the error mapping of aggregator.rs:1796-1990.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import hpke as H
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "hpke_rfc9180_x25519.json")))
+b = bytes.fromhex
+
+
+def test_oracle_rfc9180_vector():
+    assert H.x25519_public(b(GOLD["skRm"])) == b(GOLD["pkRm"])
+    e = GOLD["encryptions"][0]
+    assert e["nonce"] == GOLD["base_nonce"]  # sequence number 0
+    pt = H.open_(b(GOLD["skRm"]), b(GOLD["pkRm"]), b(GOLD["enc"]), b(GOLD["info"]), b(e["aad"]),
+                 b(e["ct"]))
+    assert pt == b(e["pt"])
+    bad = bytearray(b(e["ct"]))
+    bad[0] ^= 1
+    assert H.open_(b(GOLD["skRm"]), b(GOLD["pkRm"]), b(GOLD["enc"]), b(GOLD["info"]),
+                   b(e["aad"]), bytes(bad)) is None
+
+
+def test_oracle_seal_open_round_trip_and_janus_layer():
+    d = H.make_batch(40, 48, 32, seed=5, extensions=[(0xFF00, b"")])
+    sh, st = H.open_input_shares(d["skR"], d["pkR"], d["task_id"], d["enc"], d["ct"], d["ct_len"],
+                                 d["report_ids"], d["times"], d["pubs"], 48, require_taskprov=True)
+    assert (st == 0).all() and (sh == d["shares"]).all()
+    # a non-taskprov task must reject the taskprov extension (aggregator.rs:1945-1958)
+    _, st2 = H.open_input_shares(d["skR"], d["pkR"], d["task_id"], d["enc"], d["ct"],
+                                 d["ct_len"], d["report_ids"], d["times"], d["pubs"], 48)
+    assert (st2 == H_INVALID).all()
+
+
+H_INVALID = 8
+
+
+def _tamper(d, rng):
+    """Janus-visible failure modes: wrong AAD (time / report id / public share), tag or
+    ciphertext bit flips, truncated ciphertext, wrong ephemeral key."""
+    n = d["enc"].shape[0]
+    d = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in d.items()}
+    exp = np.zeros(n, np.uint8)
+    for r in rng.choice(n, n // 4, replace=False):
+        kind = rng.integers(0, 6)
+        if kind == 0:
+            d["times"][r] += 1
+        elif kind == 1:
+            d["report_ids"][r, 3] ^= 0x10
+        elif kind == 2 and d["pubs"] is not None:
+            d["pubs"][r, 7] ^= 1
+        elif kind in (2, 3):
+            d["ct"][r, int(d["ct_len"][r]) - 1] ^= 0x80   # tag
+        elif kind == 4:
+            d["ct_len"][r] -= 1                          # truncated
+        else:
+            d["enc"][r, 5] ^= 4
+        exp[r] = 4
+    return d, exp
+
+
+@pytest.mark.gpu
+def test_gpu_rfc9180_vector():
+    from janus_amd import hpke as G
+    op = G.HpkeOpener(b(GOLD["skRm"]), b(GOLD["pkRm"]), info=b(GOLD["info"]))
+    e = GOLD["encryptions"][0]
+    bad = bytearray(b(e["ct"]))
+    bad[-1] ^= 1
+    got = op.open([b(GOLD["enc"])] * 3, [b(e["ct"]), bytes(bad), b(e["ct"])],
+                  [b(e["aad"]), b(e["aad"]), b"wrong aad"])
+    assert got[0] == b(e["pt"])
+    assert got[1] is None and got[2] is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,pub,share_len,ext,tamper", [
+    (1, 32, 48, (), False), (300, 32, 48, (), True), (257, 0, 32, (), True),
+    (200, 32, 48, ((0xFF00, b""),), False)])
+def test_gpu_input_shares_match_oracle(n, pub, share_len, ext, tamper):
+    from janus_amd import hpke as G
+    rng = np.random.default_rng(n + pub)
+    d = H.make_batch(n, share_len, pub, seed=n * 7 + pub, extensions=ext)
+    exp_status = None
+    if tamper:
+        d, exp_status = _tamper(d, rng)
+    taskprov = bool(ext)
+    ref_sh, ref_st = H.open_input_shares(d["skR"], d["pkR"], d["task_id"], d["enc"], d["ct"],
+                                         d["ct_len"], d["report_ids"], d["times"], d["pubs"],
+                                         share_len, require_taskprov=taskprov)
+    if exp_status is not None:
+        np.testing.assert_array_equal(ref_st, exp_status)
+    op = G.HpkeOpener(d["skR"], d["pkR"])
+    sh, st = op.open_input_shares(d["task_id"], d["enc"], d["ct"], d["ct_len"], d["report_ids"],
+                                  d["times"], d["pubs"], share_len, require_taskprov=taskprov)
+    np.testing.assert_array_equal(st, ref_st)
+    np.testing.assert_array_equal(sh, ref_sh)
+
+
+@pytest.mark.gpu
+def test_gpu_plaintext_decode_failures():
+    """Well-encrypted plaintexts that Janus rejects as InvalidMessage: unknown extension type,
+    duplicate extension, trailing bytes, wrong helper share length."""
+    from janus_amd import hpke as G
+    rng = np.random.default_rng(9)
+    skR = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+    pkR = H.x25519_public(skR)
+    task = bytes(range(32))
+    share = bytes(48)
+    pts = [H.plaintext_input_share(share, [(0x0001, b"")]),
+           H.plaintext_input_share(share, [(0, b""), (0, b"x")]),
+           H.plaintext_input_share(share) + b"\0",
+           H.plaintext_input_share(bytes(47)),
+           H.plaintext_input_share(share, [(0, b"ok")])]
+    want = [8, 8, 8, 8, 0]
+    n = len(pts)
+    stride = 96
+    enc = np.zeros((n, 32), np.uint8)
+    ct = np.zeros((n, stride), np.uint8)
+    cl = np.zeros(n, np.uint32)
+    ids = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    times = np.full(n, 1_700_000_000, np.uint64)
+    pubs = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    for i, pt in enumerate(pts):
+        aad = H.input_share_aad(task, ids[i].tobytes(), int(times[i]), pubs[i].tobytes())
+        e, c = H.seal(pkR, bytes([i + 1] * 32), H.INFO_INPUT_SHARE_HELPER, aad, pt)
+        enc[i] = np.frombuffer(e, np.uint8)
+        ct[i, :len(c)] = np.frombuffer(c, np.uint8)
+        cl[i] = len(c)
+    _, ref = H.open_input_shares(skR, pkR, task, enc, ct, cl, ids, times, pubs, 48)
+    assert ref.tolist() == want
+    op = G.HpkeOpener(skR, pkR)
+    _, st = op.open_input_shares(task, enc, ct, cl, ids, times, pubs, 48)
+    assert st.tolist() == want
