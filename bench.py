@@ -89,13 +89,16 @@ def main():
     ap.add_argument("--reports", type=int, default=1 << 20, help="reports per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--role", choices=["helper", "leader"], default="helper",
-                    help="helper (the BASELINE metric) or the leader side (SURVEY 8(f) row 1)")
+    ap.add_argument("--role", choices=["helper", "leader", "hpke"], default="helper",
+                    help="helper (the BASELINE metric), the leader side (SURVEY 8(f) row 1) or "
+                         "the batched HPKE open of helper input shares (8(f) row 2)")
     ap.add_argument("--opt", action="append", default=[],
                     help="engine option key=value (e.g. split_xof=0), for A/B runs")
     args = ap.parse_args()
     if args.role == "leader":
         return leader_main(args)
+    if args.role == "hpke":
+        return hpke_main(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -307,6 +310,85 @@ def leader_main(args):
                checks=dict(helper_finished=helper_ok,
                            leader_finished=int((lstatus == 0).sum().item()),
                            leader_prep_shares_equal_generator=same, agg_count=int(cnt[0].item())))
+    print(json.dumps(out), flush=True)
+
+
+def hpke_main(args):
+    """Batched HPKE open line (not the BASELINE metric): one step = decrypt +
+    PlaintextInputShare decode of n helper input shares of Prio3Histogram(256,16) (48-byte
+    helper shares, 32-byte public shares) with DHKEM(X25519, HKDF-SHA256)/AES-128-GCM -- the
+    per-report hpke::open of aggregator.rs:1796-1990.  Inputs are sealed on the host by the
+    oracle (OpenSSL, seeded) and resident in HBM before timing."""
+    from janus_amd import hpke as G
+    from oracle import hpke as H
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    n = args.reports
+    uniq = min(n, 1 << 18)
+    t0 = time.perf_counter()
+    d = H.make_batch_fast(uniq, 48, 32, seed=0x4A414E55, n_threads=cpu_threads())
+    gen_s = time.perf_counter() - t0
+    reps = -(-n // uniq)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(np.concatenate([a] * reps)[:n])).to(dev)
+    enc, ct, ct_len = T(d["enc"]), T(d["ct"]), T(d["ct_len"].view(np.int32))
+    ids, times, pubs = T(d["report_ids"]), T(d["times"].view(np.int64)), T(d["pubs"])
+    shares = torch.empty((n, 48), dtype=torch.uint8, device=dev)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    op = G.HpkeOpener(d["skR"], d["pkR"], device=0)
+
+    def step():
+        op.open_input_shares_device(d["task_id"], enc, ct, ct_len, ids, times, pubs, shares,
+                                    status, stream=torch.cuda.current_stream().cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    op.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ms_total, launches = op.timing()
+    op.set_timing(False)
+    value = n * args.steps / elapsed
+    ms_avg = ms_total / max(launches, 1)
+    counts = json.load(open(COUNTS_PATH)) if os.path.exists(COUNTS_PATH) else dict(kernels={})
+    kc = counts["kernels"].get("k_hpke_open", {})
+    roofline = None
+    if "valu_instr_per_item" in kc:
+        ach = kc["valu_instr_per_item"] * n / (ms_avg / 1e3) / 1e12
+        roofline = dict(bound="valu", achieved=ach, peak=kc["valu_ceiling_T"],
+                        unit="T lane-instr/s (32-bit VALU, mix-weighted ceiling)",
+                        frac=ach / kc["valu_ceiling_T"], traffic=kc.get("bytes"),
+                        kernel="k_hpke_open", ms_avg=ms_avg,
+                        valu_instr_per_report=kc["valu_instr_per_item"])
+    ok = int((status == 0).sum().item())
+    out = dict(metric="helper input shares HPKE-opened+decoded/sec (X25519-HKDF-SHA256, "
+                      "AES-128-GCM)", value=value, unit="reports/s", n_gpus=1, steps=args.steps,
+               warmup=args.warmup, ms_per_step=elapsed / args.steps * 1e3, higher_is_better=True,
+               scaling="weak", vs_baseline=None, dtype="u32 limbs (GF(2^255-19), GF(2^128), bytes)",
+               data=f"synthetic: {uniq} distinct sealed input shares (oracle/OpenSSL, seeded) "
+                    f"tiled x{reps}; generation {gen_s:.1f}s, not timed",
+               config=dict(workload="DAP helper input share open: X25519 decap + HPKE key "
+                                    "schedule + AES-128-GCM + PlaintextInputShare decode, "
+                                    "Prio3Histogram(256,16) shares", reports=n),
+               roofline=roofline, kernel_ms_avg=ms_avg, checks=dict(opened=ok))
+    if not args.no_cpu_baseline:
+        th = cpu_threads()
+        m = min(uniq, max(4096, int(16000 * th * args.cpu_seconds / 10)))
+        t0 = time.perf_counter()
+        csh, cst = H.open_input_shares(d["skR"], d["pkR"], d["task_id"], d["enc"][:m],
+                                       d["ct"][:m], d["ct_len"][:m], d["report_ids"][:m],
+                                       d["times"][:m], d["pubs"][:m], 48, n_threads=th)
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = dict(value=m / dt, unit="reports/s", cores=th, kind="port",
+                                   sample=f"{m} of the sealed input shares, OpenSSL 3.0 X25519 / "
+                                          f"HMAC-SHA256 / AES-128-GCM, {th} threads, {dt:.1f}s")
+        out["speedup_vs_cpu"] = value / (m / dt)
+        out["checks"]["cpu_gpu_parity_on_sample"] = bool(
+            np.array_equal(shares[:m].cpu().numpy(), csh) and
+            np.array_equal(status[:m].cpu().numpy(), cst))
     print(json.dumps(out), flush=True)
 
 

@@ -33,6 +33,9 @@ def lib():
         _lib.hpke_open_input_shares.argtypes = [vp, vp, vp, C.c_uint32, vp, vp, vp, C.c_uint32,
                                                 vp, vp, vp, C.c_uint32, C.c_uint32, C.c_int, vp,
                                                 vp, C.c_int]
+        _lib.hpke_make_input_shares.argtypes = [vp, vp, C.c_uint32, C.c_uint64, C.c_uint32,
+                                                C.c_uint32, C.c_int, C.c_uint32, vp, vp, vp, vp,
+                                                vp, vp, vp, C.c_int]
     return _lib
 
 
@@ -121,5 +124,27 @@ def make_batch(n, share_len, pub_len, seed=1, skR=None, extensions=(), tamper=0.
                     plaintext_input_share(shares[r].tobytes(), extensions))
         enc[r] = np.frombuffer(e, np.uint8)
         ct[r] = np.frombuffer(c, np.uint8)
+    return dict(skR=skR, pkR=pkR, task_id=task_id, report_ids=ids, times=times, pubs=pubs,
+                shares=shares, enc=enc, ct=ct, ct_len=ct_len)
+
+
+def make_batch_fast(n, share_len, pub_len, seed=1, taskprov=False, n_threads=8, skR=None):
+    """make_batch in C with threads (bench-size batches); every report distinct."""
+    rng = np.random.default_rng(seed)
+    skR = bytes(rng.integers(0, 256, 32, dtype=np.uint8)) if skR is None else skR
+    pkR = x25519_public(skR)
+    task_id = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+    stride = -(-((10 if taskprov else 6) + share_len + 16) // 16) * 16
+    enc = np.zeros((n, 32), np.uint8)
+    ct = np.zeros((n, stride), np.uint8)
+    ct_len = np.zeros(n, np.uint32)
+    ids = np.zeros((n, 16), np.uint8)
+    times = np.zeros(n, np.uint64)
+    pubs = np.zeros((n, pub_len), np.uint8) if pub_len else None
+    shares = np.zeros((n, share_len), np.uint8)
+    rc = lib().hpke_make_input_shares(_p(pkR), _p(task_id), n, seed, share_len, pub_len,
+                                      int(taskprov), stride, _p(enc), _p(ct), _p(ct_len), _p(ids),
+                                      _p(times), _p(pubs), _p(shares), n_threads)
+    assert rc == 0
     return dict(skR=skR, pkR=pkR, task_id=task_id, report_ids=ids, times=times, pubs=pubs,
                 shares=shares, enc=enc, ct=ct, ct_len=ct_len)

@@ -266,3 +266,83 @@ int hpke_open_input_shares(const uint8_t skR[32], const uint8_t pkR[32], const u
   for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
   return 0;
 }
+
+/* ---- synthetic batch generation (bench / large tests): the client side of the same layer,
+ * seeded per report (every byte = SHA-256(seed || r || purpose) stream), multithreaded ----- */
+#include <openssl/sha.h>
+
+typedef struct {
+  const uint8_t *pkR, *task_id;
+  uint64_t seed;
+  uint32_t share_len, publen, stride, lo, hi;
+  int taskprov;
+  uint8_t *enc, *ct, *ids, *pubs, *shares;
+  uint32_t* ct_len;
+  uint64_t* times;
+} GenJob;
+
+static void prf(uint64_t seed, uint32_t r, uint8_t purpose, uint8_t* out, size_t len) {
+  uint8_t in[13], h[32];
+  memcpy(in, &seed, 8);
+  memcpy(in + 8, &r, 4);
+  in[12] = purpose;
+  for (size_t o = 0; o < len; o += 32) {
+    in[12] = (uint8_t)(purpose + 16 * (o / 32));
+    SHA256(in, 13, h);
+    memcpy(out + o, h, len - o < 32 ? len - o : 32);
+  }
+}
+
+static void* gen_run(void* arg) {
+  GenJob* j = (GenJob*)arg;
+  uint8_t pt[4096], aad[256], skE[32];
+  for (uint32_t r = j->lo; r < j->hi; r++) {
+    uint8_t* id = j->ids + 16 * (size_t)r;
+    uint8_t* share = j->shares + (size_t)j->share_len * r;
+    uint8_t* pub = j->publen ? j->pubs + (size_t)j->publen * r : NULL;
+    prf(j->seed, r, 1, id, 16);
+    prf(j->seed, r, 2, share, j->share_len);
+    if (pub) prf(j->seed, r, 3, pub, j->publen);
+    prf(j->seed, r, 4, skE, 32);
+    uint8_t t8[8];
+    prf(j->seed, r, 5, t8, 8);
+    j->times[r] = 1700000000ull + (t8[0] | (uint32_t)t8[1] << 8) % 3600u;
+    size_t l = 0;
+    if (j->taskprov) {
+      pt[l++] = 0, pt[l++] = 4;             /* extensions: 4 bytes */
+      pt[l++] = 0xFF, pt[l++] = 0x00, pt[l++] = 0, pt[l++] = 0; /* Taskprov, empty */
+    } else {
+      pt[l++] = 0, pt[l++] = 0;
+    }
+    pt[l++] = (uint8_t)(j->share_len >> 24), pt[l++] = (uint8_t)(j->share_len >> 16);
+    pt[l++] = (uint8_t)(j->share_len >> 8), pt[l++] = (uint8_t)j->share_len;
+    memcpy(pt + l, share, j->share_len), l += j->share_len;
+    size_t al = hpke_input_share_aad(j->task_id, id, j->times[r], pub, j->publen, aad);
+    uint8_t* ct = j->ct + (size_t)j->stride * r;
+    memset(ct, 0, j->stride);
+    hpke_seal(j->pkR, skE, INFO, sizeof(INFO), aad, al, pt, l, j->enc + 32 * (size_t)r, ct);
+    j->ct_len[r] = (uint32_t)(l + 16);
+  }
+  return NULL;
+}
+
+int hpke_make_input_shares(const uint8_t pkR[32], const uint8_t task_id[32], uint32_t n,
+                           uint64_t seed, uint32_t share_len, uint32_t publen, int taskprov,
+                           uint32_t stride, uint8_t* enc, uint8_t* ct, uint32_t* ct_len,
+                           uint8_t* ids, uint64_t* times, uint8_t* pubs, uint8_t* shares,
+                           int n_threads) {
+  if ((taskprov ? 10u : 6u) + share_len + 16 > stride) return -1;
+  if (n_threads < 1) n_threads = 1;
+  if (n_threads > 256) n_threads = 256;
+  pthread_t th[256];
+  GenJob jobs[256];
+  for (int t = 0; t < n_threads; t++) {
+    jobs[t] = (GenJob){pkR, task_id, seed, share_len, publen, stride,
+                       (uint32_t)((uint64_t)n * t / n_threads),
+                       (uint32_t)((uint64_t)n * (t + 1) / n_threads), taskprov, enc, ct, ids, pubs,
+                       shares, ct_len, times};
+    pthread_create(&th[t], NULL, gen_run, &jobs[t]);
+  }
+  for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+  return 0;
+}

@@ -8,4 +8,6 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
 tail -3 gpurun_out/gpu_tests_$TAG.log
 timeout -k 10 300 python -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo "bench failed"; tail -30 gpurun_out/bench_$TAG.err; exit 1; }
 cat gpurun_out/bench_$TAG.json
+timeout -k 10 300 python -u bench.py --role hpke > gpurun_out/bench_hpke_$TAG.json 2> gpurun_out/bench_hpke_$TAG.err || { echo "hpke bench failed"; tail -30 gpurun_out/bench_hpke_$TAG.err; exit 1; }
+cat gpurun_out/bench_hpke_$TAG.json
 bash profiles/run_profiles.sh $TAG

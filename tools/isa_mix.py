@@ -33,10 +33,12 @@ PEAK_FULL_T = 64.5
 PEAK_HALF_T = 37.0
 
 
-def asm_path():
-    out = "/tmp/prio3_engine_gfx950.s"
-    src = os.path.join(ROOT, "janus_amd", "csrc", "prio3_engine.hip")
-    if not os.path.exists(out) or os.path.getmtime(out) < os.path.getmtime(src):
+def asm_path(source: str = "prio3_engine.hip"):
+    out = f"/tmp/{source.replace('.hip', '')}_gfx950.s"
+    src = os.path.join(ROOT, "janus_amd", "csrc", source)
+    deps = [src] + [os.path.join(ROOT, "janus_amd", "csrc", h) for h in
+                    ("prio3_device.h", "prio3_common.h", "sha256_device.h")]
+    if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(d) for d in deps):
         subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950",
                         "--cuda-device-only", "-S", "-o", out, src], check=True)
     return out
@@ -107,8 +109,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--asm")
     ap.add_argument("--kernel", default="")
+    ap.add_argument("--source", default="prio3_engine.hip")
     a = ap.parse_args()
-    lines = open(a.asm or asm_path()).read().splitlines()
+    lines = open(a.asm or asm_path(a.source)).read().splitlines()
     for k, body in split_kernels(lines).items():
         if a.kernel not in k:
             continue

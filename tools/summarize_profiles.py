@@ -45,28 +45,37 @@ def counters(path):
 def main():
     src, tag = sys.argv[1], sys.argv[2]
     lines = [f"# rocprofv3 summary, tag {tag} (source: {src}, produced by profiles/run_profiles.sh)",
-             "# command: python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline "
-             "(Prio3Histogram(256,16), 1,048,576 reports per launch)", ""]
-    stats = os.path.join(src, "trace", "run_kernel_stats.csv")
-    lines.append("## --kernel-trace --stats (per kernel)")
-    lines.append(f"{'kernel':40s} {'calls':>6s} {'avg_us':>10s} {'min_us':>10s} {'max_us':>10s} {'pct':>7s}")
-    with open(stats) as f:
-        for row in csv.DictReader(f):
-            if row["Name"].startswith(("void at::", "at::", "__amd")):
-                continue
-            lines.append(f"{short(row['Name']):40s} {row['Calls']:>6s} "
-                         f"{float(row['AverageNs']) / 1e3:10.1f} {float(row['MinNs']) / 1e3:10.1f} "
-                         f"{float(row['MaxNs']) / 1e3:10.1f} {float(row['Percentage']):7.2f}")
-    fetch = counters(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"))
-    write = counters(os.path.join(src, "pmc_write", "run_counter_collection.csv"))
-    sq = counters(os.path.join(src, "pmc_sq", "run_counter_collection.csv"))
-    for k, v in counters(os.path.join(src, "pmc_stall", "run_counter_collection.csv")).items():
-        for c, vals in v.items():
-            sq[k].setdefault(c, vals)
+             "# commands: python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --opt chunks=1 "
+             "(Prio3Histogram(256,16), 1,048,576 reports per launch) and, for k_hpke_open, "
+             "bench.py --role hpke --reports 262144", ""]
+    fetch, write, sq = {}, {}, {}
+    for pre in ("", "hpke_"):
+        stats = os.path.join(src, pre + "trace", "run_kernel_stats.csv")
+        if not os.path.exists(stats):
+            continue
+        lines.append(f"## --kernel-trace --stats (per kernel){' -- bench.py --role hpke' if pre else ''}")
+        lines.append(f"{'kernel':40s} {'calls':>6s} {'avg_us':>10s} {'min_us':>10s} {'max_us':>10s} {'pct':>7s}")
+        with open(stats) as f:
+            for row in csv.DictReader(f):
+                if row["Name"].startswith(("void at::", "at::", "__amd")):
+                    continue
+                lines.append(f"{short(row['Name']):40s} {row['Calls']:>6s} "
+                             f"{float(row['AverageNs']) / 1e3:10.1f} {float(row['MinNs']) / 1e3:10.1f} "
+                             f"{float(row['MaxNs']) / 1e3:10.1f} {float(row['Percentage']):7.2f}")
+        lines.append("")
+        for dst, name in ((fetch, "pmc_fetch"), (write, "pmc_write"), (sq, "pmc_sq"),
+                          (sq, "pmc_stall")):
+            for k, v in counters(os.path.join(src, pre + name, "run_counter_collection.csv")).items():
+                if k.startswith("k_hpke") != bool(pre):
+                    continue
+                for c, vals in v.items():
+                    dst.setdefault(k, {}).setdefault(c, vals)
     traffic = {}
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import isa_mix
-    asm = isa_mix.split_kernels(open(isa_mix.asm_path()).read().splitlines())
+    asm = {}
+    for source in ("prio3_engine.hip", "hpke.hip"):
+        asm.update(isa_mix.split_kernels(open(isa_mix.asm_path(source)).read().splitlines()))
     ceilings = {}
     for k, body in asm.items():
         lp = [isa_mix.mix(b) for _, b in isa_mix.loops(body)]
@@ -81,7 +90,7 @@ def main():
     for k in sorted(set(fetch) | set(write)):
         if k.startswith(("at::", "__amd", "vectorized", "elementwise", "reduce_kernel")):
             continue
-        fv, wv = fetch[k].get("FETCH_SIZE", []), write[k].get("WRITE_SIZE", [])
+        fv, wv = fetch.get(k, {}).get("FETCH_SIZE", []), write.get(k, {}).get("WRITE_SIZE", [])
         if not fv or not wv:
             continue
         fb = 2 * 1024 * sum(fv) / len(fv)
