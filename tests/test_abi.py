@@ -35,6 +35,17 @@ def test_hpke_header_declares_the_exported_set():
         assert hasattr(L, name), name
 
 
+def test_dap_header_declares_the_exported_set():
+    from janus_amd import dap as J
+    src = open(os.path.join(ROOT, "include", "janus_dap.h")).read()
+    declared = sorted(set(re.findall(r"^(?:int|void|int64_t|size_t)\s+(janus_dap_\w+)\s*\(",
+                                     src, re.M)))
+    assert declared == sorted(J.DAP_EXPORTED_SYMBOLS)
+    L = J._lib()
+    for name in declared:
+        assert hasattr(L, name), name
+
+
 def test_hpke_unsupported_suite_is_refused():
     """P-256 / other suites stay on the host path: creation says EUNSUPPORTED (no GPU call)."""
     from janus_amd import hpke as H
