@@ -89,7 +89,7 @@ def main():
     ap.add_argument("--reports", type=int, default=1 << 20, help="reports per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--role", choices=["helper", "leader", "hpke"], default="helper",
+    ap.add_argument("--role", choices=["helper", "leader", "hpke", "pipeline"], default="helper",
                     help="helper (the BASELINE metric), the leader side (SURVEY 8(f) row 1) or "
                          "the batched HPKE open of helper input shares (8(f) row 2)")
     ap.add_argument("--opt", action="append", default=[],
@@ -99,6 +99,8 @@ def main():
         return leader_main(args)
     if args.role == "hpke":
         return hpke_main(args)
+    if args.role == "pipeline":
+        return pipeline_main(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -389,6 +391,131 @@ def hpke_main(args):
         out["checks"]["cpu_gpu_parity_on_sample"] = bool(
             np.array_equal(shares[:m].cpu().numpy(), csh) and
             np.array_equal(status[:m].cpu().numpy(), cst))
+    print(json.dumps(out), flush=True)
+
+
+def pipeline_main(args):
+    """Whole helper aggregation-job init on the device, request bytes to response bytes (not
+    the BASELINE metric): janus_dap unpack of the AggregationJobInitializeReq body -> HPKE open
+    of the helper input shares -> prio3 prepare + aggregate + batch metadata -> AggregationJobResp
+    encode.  The request body (Prio3Histogram(256,16), X25519/AES-128-GCM, 738 B per report)
+    is resident in HBM before timing; aggregator.rs:1720-2096 per report in Janus."""
+    from janus_amd import dap as DJ
+    from janus_amd import hpke as G
+    from oracle import hpke as H
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    n = args.reports
+    th = cpu_threads()
+    eng = J.HelperEngine(J.Prio3Histogram(256, 16), VK, device=0)
+    t0 = time.perf_counter()
+    d = eng.generate_reports_device(n, seed=0x4A414E5553000002)
+    host = {k: d[k].cpu().numpy() for k in ("nonces", "public_shares", "helper_shares",
+                                             "leader_prep_shares")}
+    rng = np.random.default_rng(7)
+    skR = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+    pkR = H.x25519_public(skR)
+    task = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+    times = (1_700_000_000 + rng.integers(0, 3600, n)).astype(np.uint64)
+    enc, ct, ct_len, _ = H.seal_input_shares(pkR, task, host["nonces"], times,
+                                             host["public_shares"], host["helper_shares"],
+                                             seed=11, n_threads=th)
+    pl = int(ct_len[0])
+    L = host["leader_prep_shares"].shape[1]
+    rec = 16 + 8 + 4 + 32 + 1 + 2 + 32 + 4 + pl + 4 + 1 + 4 + L
+    R = np.zeros((n, rec), np.uint8)
+    be = lambda v, w: np.array([v], dtype=f">u{w}").view(np.uint8)
+    o = 0
+    for part in (host["nonces"], times.astype(">u8").view(np.uint8).reshape(n, 8),
+                 np.tile(be(32, 4), (n, 1)), host["public_shares"], np.full((n, 1), 1, np.uint8),
+                 np.tile(be(32, 2), (n, 1)), enc, np.tile(be(pl, 4), (n, 1)), ct[:, :pl],
+                 np.tile(be(5 + L, 4), (n, 1)), np.zeros((n, 1), np.uint8),
+                 np.tile(be(L, 4), (n, 1)), host["leader_prep_shares"]):
+        R[:, o:o + part.shape[1]] = part
+        o += part.shape[1]
+    body = (be(0, 4).tobytes() + b"\x01" + be(n * rec, 4).tobytes() + R.tobytes())
+    gen_s = time.perf_counter() - t0
+    lay = DJ.scan(body)
+    assert lay.uniform and lay.n == n
+    d_body = torch.zeros(len(body) + 8, dtype=torch.uint8, device=dev)
+    d_body[:len(body)] = torch.frombuffer(bytearray(body), dtype=torch.uint8).to(dev)
+    stride = DJ.ct_stride_for(lay)
+    op = G.HpkeOpener(skR, pkR, device=0)
+    shares = torch.empty((n, 48), dtype=torch.uint8, device=dev)
+    hs = torch.empty(n, dtype=torch.uint8, device=dev)
+    msgs = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    seg = torch.zeros(n, dtype=torch.int32, device=dev)
+    agg = torch.zeros((1, eng.sz.agg_share_len), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    cks = torch.zeros((1, 32), dtype=torch.uint8, device=dev)
+    ivs = torch.zeros((1, 2), dtype=torch.int64, device=dev)
+    res = {}
+
+    def step():
+        s = torch.cuda.current_stream().cuda_stream
+        u, mism = DJ.unpack_device(lay, d_body, stride, stream=s)
+        op.open_input_shares_device(task, u["enc"], u["ct"], u["ct_len"], u["report_ids"],
+                                    u["times"], u["public_shares"], shares, hs, stream=s)
+        eng.prepare_aggregate_device(u["report_ids"], u["public_shares"], shares,
+                                     u["prep_shares"], seg, 1, msgs, st, stream=s)
+        accept = ((hs == 0) & (u["msg_status"] == 0)).to(torch.uint8)
+        eng.aggregate_finish_device(st, accept, agg, cnt, stream=s)
+        st_all = st | u["msg_status"]
+        eng.batch_metadata_device(u["report_ids"], u["times"], st_all, accept, seg, 1, cks, ivs,
+                                  stream=s)
+        pe = torch.where(hs == 0, torch.full_like(hs, 0xFF), hs)
+        res["out"], res["len"] = DJ.encode_resp_device(u["report_ids"], pe, st_all, msgs, 16,
+                                                       stream=s)
+        res["mism"] = mism
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    value = n * args.steps / elapsed
+    resp_len = int(res["len"][0])
+    ok = int((st == 0).sum().item())
+    out = dict(metric="helper aggregation-job init reports/sec, request bytes to response bytes "
+                      "(DAP unpack + HPKE open + Prio3Histogram(256,16) prepare/aggregate + "
+                      "response encode)", value=value, unit="reports/s", n_gpus=1,
+               steps=args.steps, warmup=args.warmup, ms_per_step=elapsed / args.steps * 1e3,
+               higher_is_better=True, scaling="weak", vs_baseline=None,
+               dtype="u32 limbs / bytes",
+               data=f"synthetic: {n} distinct reports (device client + oracle HPKE seal), one "
+                    f"{len(body) / 1e6:.0f} MB request body resident in HBM; generation "
+                    f"{gen_s:.1f}s, not timed",
+               config=dict(workload="DAP-09 AggregationJobInitializeReq -> AggregationJobResp, "
+                                    "helper, Prio3Histogram(256,16), X25519-HKDF-SHA256/"
+                                    "AES-128-GCM", reports=n, request_bytes=len(body)),
+               checks=dict(finished=ok, unpack_mismatch=int(res["mism"][0]),
+                           response_bytes=resp_len,
+                           response_len_expected=4 + ok * 42 + (n - ok) * 18))
+    if not args.no_cpu_baseline:
+        from oracle.oracle import Oracle
+        m = min(n, max(2048, int(4000 * th * args.cpu_seconds / 10)))
+        t0 = time.perf_counter()
+        csh, cst = H.open_input_shares(skR, pkR, task, enc[:m], ct[:m], ct_len[:m],
+                                       host["nonces"][:m], times[:m], host["public_shares"][:m],
+                                       48, n_threads=th)
+        t1 = time.perf_counter()
+        o_ = Oracle("histogram", length=256, chunk_length=16)
+        cm, cs, _, _ = o_.helper_batch(VK, host["nonces"][:m], host["public_shares"][:m], csh,
+                                       host["leader_prep_shares"][:m], n_threads=th,
+                                       job_size=500)
+        t2 = time.perf_counter()
+        out["cpu_baseline"] = dict(value=m / (t2 - t0), unit="reports/s", cores=th, kind="port",
+                                   sample=f"{m} reports: OpenSSL HPKE open ({t1 - t0:.1f}s) then "
+                                          f"the C Prio3 restatement in 500-report jobs "
+                                          f"({t2 - t1:.1f}s), {th} threads; DAP codec excluded")
+        out["speedup_vs_cpu"] = value / out["cpu_baseline"]["value"]
+        out["checks"]["cpu_gpu_parity_on_sample"] = bool(
+            np.array_equal(st[:m].cpu().numpy(), cs) and
+            np.array_equal(msgs[:m].cpu().numpy(), cm))
     print(json.dumps(out), flush=True)
 
 

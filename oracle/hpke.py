@@ -36,6 +36,9 @@ def lib():
         _lib.hpke_make_input_shares.argtypes = [vp, vp, C.c_uint32, C.c_uint64, C.c_uint32,
                                                 C.c_uint32, C.c_int, C.c_uint32, vp, vp, vp, vp,
                                                 vp, vp, vp, C.c_int]
+        _lib.hpke_seal_input_shares.argtypes = [vp, vp, C.c_uint32, C.c_uint64, vp, vp, vp,
+                                                C.c_uint32, vp, C.c_uint32, C.c_uint32, vp, vp,
+                                                vp, C.c_int]
     return _lib
 
 
@@ -148,3 +151,21 @@ def make_batch_fast(n, share_len, pub_len, seed=1, taskprov=False, n_threads=8, 
     assert rc == 0
     return dict(skR=skR, pkR=pkR, task_id=task_id, report_ids=ids, times=times, pubs=pubs,
                 shares=shares, enc=enc, ct=ct, ct_len=ct_len)
+
+
+def seal_input_shares(pkR, task_id, ids, times, pubs, shares, seed=1, n_threads=8):
+    """Seals the given helper input shares (no extensions) -> (enc, ct, ct_len, stride)."""
+    n, share_len = shares.shape
+    stride = -(-(6 + share_len + 16) // 16) * 16
+    enc = np.zeros((n, 32), np.uint8)
+    ct = np.zeros((n, stride), np.uint8)
+    ct_len = np.zeros(n, np.uint32)
+    publen = 0 if pubs is None else pubs.shape[1]
+    rc = lib().hpke_seal_input_shares(
+        _p(pkR), _p(task_id), n, seed, _p(np.ascontiguousarray(ids, np.uint8)),
+        _p(np.ascontiguousarray(times, np.uint64)),
+        None if pubs is None else _p(np.ascontiguousarray(pubs, np.uint8)), publen,
+        _p(np.ascontiguousarray(shares, np.uint8)), share_len, stride, _p(enc), _p(ct),
+        _p(ct_len), n_threads)
+    assert rc == 0
+    return enc, ct, ct_len, stride
