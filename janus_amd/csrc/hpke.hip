@@ -34,6 +34,12 @@ DEV fe fe_set(uint32_t x) {
   return r;
 }
 
+#ifndef FE_ASM
+#define FE_ASM 1  // 1: the generated single-asm-statement field routines (fe25519_asm.h)
+#endif
+#if FE_ASM
+#include "fe25519_asm.h"
+#else
 // r = lo + 38 * c (c small), folded twice so the result is < 2^256
 DEV void fe_fold(uint32_t r[8], uint32_t c) {
   uint32_t cy;
@@ -343,12 +349,6 @@ DEV fe fe_sqr(const fe& a) {
   return fe_reduce512(w);
 }
 
-DEV fe fe_sqr_n(fe a, int n) {
-#pragma unroll 1
-  for (int i = 0; i < n; i++) a = fe_sqr(a);
-  return a;
-}
-
 DEV fe fe_mul121665(const fe& a) {
   fe r;
   uint32_t cy = 0;
@@ -360,6 +360,14 @@ DEV fe fe_mul121665(const fe& a) {
   }
   fe_fold(r.v, cy);
   return r;
+}
+
+#endif
+
+DEV fe fe_sqr_n(fe a, int n) {
+#pragma unroll 1
+  for (int i = 0; i < n; i++) a = fe_sqr(a);
+  return a;
 }
 
 // z^(p - 2) (the ref10 addition chain: 254 squarings, 11 multiplications)
