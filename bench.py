@@ -31,9 +31,8 @@ VK = bytes.fromhex("4a414e55532d414d442d42454e434821")
 
 # --- roofline inputs.  Per kernel, profiles/kernel_counts.json (written by
 # tools/summarize_profiles.py from the committed rocprofv3 passes) holds the dynamic VALU
-# instructions per report (SQ_INSTS_VALU / SQ_WAVES, one report per lane), the mix-weighted VALU
-# ceiling of its hot loop (tools/isa_mix.py: full-rate ops 2 cycles, half-rate 4, from the
-# measured tools/ubench_valu rates) and its PMC HBM bytes per launch.
+# instructions per report (SQ_INSTS_VALU / SQ_WAVES, one report per lane) and its PMC HBM bytes
+# per launch (plus the static half-rate fraction of its hot loop, tools/isa_mix.py, for reference).
 COUNTS_PATH = os.path.join(ROOT, "profiles", "kernel_counts.json")
 # per-report HBM bytes each kernel must move at minimum (algorithmic; Histogram(256,16))
 KERNEL_BYTES = {"k_xof_a": 16 + 16 + 16 + 256 * 16 + 95 * 16,  # nonce, k_meas, k_proofs in; shares out
@@ -41,7 +40,11 @@ KERNEL_BYTES = {"k_xof_a": 16 + 16 + 16 + 256 * 16 + 95 * 16,  # nonce, k_meas, 
                 "k_xofd": 16 + 48 + 32 + 256 * 16 + 95 * 16 + 16 + 16 + 3 * 16,  # + jr/qr/part out
                 "k_query_h": 256 * 16 + 95 * 16 + 560 + 2 * 16 + 16 + 16 + 17,
                 "k_acc_partial": 256 * 16 + 1}
-PEAK_VALU_NOMINAL = 256 * 4 * 32 * 2.4e9  # 78.6e12 lane-instr/s, full-rate VALU at 2.4 GHz
+# Peak: the guide's vector issue rate (MI355X_MICROARCH.md: 157.3 TFLOPS FP32 vector = 256 CU x
+# 4 SIMD x 32 lanes/clk x 2.4 GHz = 78.6 T lane-instructions/s); measured full-rate issue on
+# this chip is 64.5 T (profiles/r01_ubench_valu_gfx950.txt), reported beside it.
+PEAK_VALU_NOMINAL = 256 * 4 * 32 * 2.4e9  # 78.6e12 lane-instr/s
+MEASURED_ISSUE_T = 64.5
 PEAK_HBM = 8.0e12
 
 
@@ -206,14 +209,15 @@ def main():
     for k, v in per_kernel.items():
         if k in kc and "valu_instr_per_item" in kc[k] and k != "k_acc_partial":
             v["valu_T"] = kc[k]["valu_instr_per_item"] * n / (v["ms_avg"] / 1e3) / 1e12
-            v["valu_frac"] = v["valu_T"] / kc[k]["valu_ceiling_T"]
+            v["valu_frac"] = v["valu_T"] / (PEAK_VALU_NOMINAL / 1e12)
         if k in KERNEL_BYTES:
             v["hbm_algorithmic_GBps"] = KERNEL_BYTES[k] * n / (v["ms_avg"] / 1e3) / 1e9
     dom = max((k for k in per_kernel if "valu_T" in per_kernel[k]),
               key=lambda k: per_kernel[k]["ms_total"])
     d = per_kernel[dom]
-    roofline = dict(bound="valu", achieved=d["valu_T"], peak=kc[dom]["valu_ceiling_T"],
-                    unit="T lane-instr/s (32-bit VALU, mix-weighted ceiling)",
+    roofline = dict(bound="valu", achieved=d["valu_T"], peak=PEAK_VALU_NOMINAL / 1e12,
+                    unit="T lane-instr/s (32-bit VALU issue; peak = guide vector rate)",
+                    frac_of_measured_issue=d["valu_T"] / MEASURED_ISSUE_T,
                     frac=d["valu_frac"], traffic=kc[dom].get("bytes"),
                     traffic_source=f"{counts.get('source')} (PMC FETCH_SIZE*2+WRITE_SIZE, bytes/launch)",
                     kernel=dom, ms_avg=d["ms_avg"],
@@ -360,9 +364,10 @@ def hpke_main(args):
     roofline = None
     if "valu_instr_per_item" in kc:
         ach = kc["valu_instr_per_item"] * n / (ms_avg / 1e3) / 1e12
-        roofline = dict(bound="valu", achieved=ach, peak=kc["valu_ceiling_T"],
-                        unit="T lane-instr/s (32-bit VALU, mix-weighted ceiling)",
-                        frac=ach / kc["valu_ceiling_T"], traffic=kc.get("bytes"),
+        roofline = dict(bound="valu", achieved=ach, peak=PEAK_VALU_NOMINAL / 1e12,
+                        unit="T lane-instr/s (32-bit VALU issue; peak = guide vector rate)",
+                        frac=ach / (PEAK_VALU_NOMINAL / 1e12),
+                        frac_of_measured_issue=ach / MEASURED_ISSUE_T, traffic=kc.get("bytes"),
                         kernel="k_hpke_open", ms_avg=ms_avg,
                         valu_instr_per_report=kc["valu_instr_per_item"])
     ok = int((status == 0).sum().item())

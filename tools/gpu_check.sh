@@ -10,4 +10,6 @@ timeout -k 10 300 python -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/
 cat gpurun_out/bench_$TAG.json
 timeout -k 10 300 python -u bench.py --role hpke > gpurun_out/bench_hpke_$TAG.json 2> gpurun_out/bench_hpke_$TAG.err || { echo "hpke bench failed"; tail -30 gpurun_out/bench_hpke_$TAG.err; exit 1; }
 cat gpurun_out/bench_hpke_$TAG.json
+timeout -k 10 400 python -u bench.py --role pipeline > gpurun_out/bench_pipeline_$TAG.json 2> gpurun_out/bench_pipeline_$TAG.err || { echo "pipeline bench failed"; tail -30 gpurun_out/bench_pipeline_$TAG.err; exit 1; }
+cat gpurun_out/bench_pipeline_$TAG.json
 bash profiles/run_profiles.sh $TAG

@@ -46,6 +46,31 @@ KERN(k_cmp64_8, 8, "v_cmp_lt_u64 vcc, %0, %0", "+v"(v), : "vcc")
 KERN(k_mov64_8, 8, "v_mov_b64 %0, %0", "+v"(v), )
 KERN(k_add3_8, 8, "v_add3_u32 %0, %0, %1, %2", "+v"(x[2 * i]), )
 
+// Mixed pairs: one instruction of each class per chain step (independent registers), to see
+// whether a half-rate op and another op overlap in the issue pipeline (ops counted: 2 per step).
+#define KERN2(NAME, CH, ASM, CLOB)                                               \
+  __global__ void NAME(uint32_t* out, uint32_t a0) {                             \
+    uint32_t x[CH * 2], y[CH];                                                   \
+    for (int i = 0; i < CH * 2; i++) x[i] = a0 + i + threadIdx.x;               \
+    for (int i = 0; i < CH; i++) y[i] = a0 * 5 + i;                              \
+    uint32_t b = a0 * 3, c = a0 * 7;                                             \
+    for (int it = 0; it < ITER; it++) {                                          \
+      _Pragma("unroll") for (int i = 0; i < CH; i++) {                           \
+        uint64_t& v = *reinterpret_cast<uint64_t*>(&x[2 * i]);                   \
+        asm volatile(ASM : "+v"(v), "+v"(y[i]) : "v"(b), "v"(c) : CLOB);         \
+      }                                                                          \
+    }                                                                            \
+    uint32_t s = 0;                                                              \
+    for (int i = 0; i < CH * 2; i++) s ^= x[i];                                  \
+    for (int i = 0; i < CH; i++) s ^= y[i];                                      \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;                              \
+  }
+KERN2(k_mad_addc, 8, "v_mad_u64_u32 %0, s[20:21], %2, %3, %0\n\tv_addc_co_u32 %1, vcc, %1, %2, vcc", "vcc")
+KERN2(k_mad_xor, 8, "v_mad_u64_u32 %0, s[20:21], %2, %3, %0\n\tv_xor_b32 %1, %1, %2", "vcc")
+KERN2(k_addc_xor, 8, "v_addc_co_u32 %1, vcc, %1, %2, vcc\n\tv_xor_b32 %1, %1, %3", "vcc")
+KERN2(k_align_xor, 8, "v_alignbit_b32 %1, %1, %2, 7\n\tv_bitop3_b32 %1, %1, %2, %3 bitop3:0x96", "vcc")
+KERN2(k_mad_mad, 8, "v_mad_u64_u32 %0, s[20:21], %2, %3, %0\n\tv_mad_u64_u32 %0, s[22:23], %3, %2, %0", "vcc")
+
 template <typename K>
 void run(const char* name, K kern, uint32_t* buf, int blocks, int threads, int ch) {
   hipEvent_t a, b;
@@ -92,6 +117,11 @@ int main() {
     run("cmp_lt_u64 x8", k_cmp64_8, o, blocks, threads, 8);
     run("mov_b64 x8", k_mov64_8, o, blocks, threads, 8);
     run("add3 x8", k_add3_8, o, blocks, threads, 8);
+    run("mad64+addc", k_mad_addc, o, blocks, threads, 16);
+    run("mad64+xor", k_mad_xor, o, blocks, threads, 16);
+    run("addc+xor", k_addc_xor, o, blocks, threads, 16);
+    run("alignbit+bitop3", k_align_xor, o, blocks, threads, 16);
+    run("mad64+mad64", k_mad_mad, o, blocks, threads, 16);
   }
   return 0;
 }
