@@ -37,6 +37,10 @@ enum {
   PRIO3_SUM = 1,       /* Prio3::new_sum(2, bits)                     (vdaf.rs:210-217) */
   PRIO3_SUMVEC = 2,    /* Prio3::new_sum_vec_multithreaded(2, ...)    (vdaf.rs:219-235) */
   PRIO3_HISTOGRAM = 3, /* Prio3::new_histogram(2, length, chunk)      (vdaf.rs:257-266) */
+  /* Prio3SumVecField64MultiproofHmacSha256Aes128 (vdaf.rs:173-195, algorithm 0xFFFF1003):
+   * SumVec<Field64, ParallelSum<Mul>> with XofHmacSha256Aes128, 32-byte seeds and verify key,
+   * num_proofs >= 2.  Created with prio3_engine_create_ex (32-byte verify key); helper role. */
+  PRIO3_SUMVEC_F64_MP = 4,
 };
 
 /* Per-report status; each maps 1:1 to the PingPongError variant prio returns and to the
@@ -73,10 +77,10 @@ typedef struct {
   uint32_t field_bytes;       /* 8 (Field64) or 16 (Field128) */
   uint32_t meas_len, out_len, proof_len, verifier_len, joint_rand_len;
   uint32_t nonce_len;         /* 16 (report ID) */
-  uint32_t public_share_len;  /* 32 with joint randomness, else 0 */
-  uint32_t helper_share_len;  /* 48 with joint randomness, else 32 */
+  uint32_t public_share_len;  /* 2 seeds with joint randomness (32 B; 64 B for 32-byte seeds) */
+  uint32_t helper_share_len;  /* 3 seeds with joint randomness, else 2 (16- or 32-byte seeds) */
   uint32_t prep_share_len;    /* leader PrepareShare bytes (verifiers || jr part) */
-  uint32_t prep_msg_len;      /* 16 with joint randomness, else 0 */
+  uint32_t prep_msg_len;      /* one seed with joint randomness (16 or 32 B), else 0 */
   uint32_t agg_share_len;     /* out_len * field_bytes */
   uint32_t leader_input_share_len; /* enc(meas share) || enc(proofs share) [|| k_blind] */
 } prio3_sizes_t;
@@ -90,6 +94,10 @@ int prio3_sizes(const prio3_params* params, prio3_sizes_t* out);
  * (VDAF instance, verify key), bound to one GPU. */
 int prio3_engine_create(const prio3_params* params, const uint8_t verify_key[16], int device,
                         prio3_engine** out);
+/* As prio3_engine_create with a verify key of verify_key_len bytes: 16 for the TurboSHAKE
+ * instances, 32 for PRIO3_SUMVEC_F64_MP (VERIFY_KEY_LENGTH_HMACSHA256_AES128, vdaf.rs). */
+int prio3_engine_create_ex(const prio3_params* params, const uint8_t* verify_key,
+                           size_t verify_key_len, int device, prio3_engine** out);
 void prio3_engine_destroy(prio3_engine* engine);
 
 /* ---- Host-buffer entry points (what the Rust FFI calls from inside rayon::spawn) ---- */

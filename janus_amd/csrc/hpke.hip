@@ -19,6 +19,8 @@
 #include "../../include/janus_hpke.h"
 #include "prio3_device.h"
 #include "sha256_device.h"
+#include "aes_device.h"
+#include "sha256_host.h"
 
 // -------------------------------------------------------------------------------------
 // GF(2^255 - 19), values in [0, 2^256) (loosely reduced), 8 little-endian 32-bit limbs
@@ -438,181 +440,6 @@ DEV fe x25519_ladder(const uint32_t* k, const fe& u) {
   return fe_freeze(fe_mul(x2, fe_inv(z2)));
 }
 
-// -------------------------------------------------------------------------------------
-// SHA-256 message buffers (big-endian words) and HMAC
-// -------------------------------------------------------------------------------------
-template <int NW>
-struct Msg32 {
-  uint32_t w[NW];
-};
-template <int NW>
-DEV void mz(Msg32<NW>& m) {
-#pragma unroll
-  for (int i = 0; i < NW; i++) m.w[i] = 0;
-}
-template <int NW>
-DEV void mbyte(Msg32<NW>& m, int pos, uint32_t b) {
-  m.w[pos >> 2] |= (b & 0xffu) << (24 - 8 * (pos & 3));
-}
-template <int NW, int N>
-DEV void mstr(Msg32<NW>& m, int pos, const char (&s)[N]) {  // N - 1 bytes (no terminator)
-#pragma unroll
-  for (int i = 0; i < N - 1; i++) mbyte(m, pos + i, (uint8_t)s[i]);
-}
-// nbytes (multiple of 4) of big-endian words d at byte position pos
-template <int NW>
-DEV void mwords_be(Msg32<NW>& m, int pos, const uint32_t* d, int nwords) {
-  const int q = pos >> 2, o = pos & 3;
-  if (o == 0) {
-#pragma unroll
-    for (int i = 0; i < nwords; i++) m.w[q + i] |= d[i];
-  } else {
-#pragma unroll
-    for (int i = 0; i < nwords; i++) {
-      m.w[q + i] |= d[i] >> (8 * o);
-      m.w[q + i + 1] |= d[i] << (32 - 8 * o);
-    }
-  }
-}
-// little-endian packed bytes (as loaded from memory) at byte position pos
-template <int NW>
-DEV void mwords_le(Msg32<NW>& m, int pos, const uint32_t* d, int nwords) {
-  uint32_t be[16];
-#pragma unroll
-  for (int i = 0; i < nwords; i++) be[i] = __builtin_bswap32(d[i]);
-  mwords_be(m, pos, be, nwords);
-}
-// SHA-256 over the len message bytes of m after `prefix` bytes already compressed into st
-template <int NW>
-DEV void sha_final(uint32_t st[8], Msg32<NW>& m, int len, int prefix) {
-  mbyte(m, len, 0x80);
-  const int nblk = (len + 9 + 63) / 64;
-  m.w[nblk * 16 - 1] = (uint32_t)((prefix + len) * 8);
-#pragma unroll
-  for (int b = 0; b < nblk; b++) {
-    uint32_t blk[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) blk[i] = m.w[16 * b + i];
-    sha256d::compress(st, blk);
-  }
-}
-
-struct HmacKey {
-  uint32_t ist[8], ost[8];
-};
-// HMAC key of 32 bytes (big-endian words): the ipad / opad midstates
-DEV void hmac_key32(HmacKey& k, const uint32_t key[8]) {
-  uint32_t bi[16], bo[16];
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    const uint32_t x = i < 8 ? key[i] : 0u;
-    bi[i] = x ^ 0x36363636u;
-    bo[i] = x ^ 0x5c5c5c5cu;
-  }
-#pragma unroll
-  for (int i = 0; i < 8; i++) k.ist[i] = k.ost[i] = sha256d::IV[i];
-  sha256d::compress(k.ist, bi);
-  sha256d::compress(k.ost, bo);
-}
-template <int NW>
-DEV void hmac(const HmacKey& k, Msg32<NW>& m, int len, uint32_t out[8]) {
-  uint32_t st[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) st[i] = k.ist[i];
-  sha_final(st, m, len, 64);
-  Msg32<16> o;
-  mz(o);
-#pragma unroll
-  for (int i = 0; i < 8; i++) o.w[i] = st[i];
-#pragma unroll
-  for (int i = 0; i < 8; i++) out[i] = k.ost[i];
-  sha_final(out, o, 32, 64);
-}
-
-// -------------------------------------------------------------------------------------
-// AES-128 (FIPS 197) with little-endian packed column words and LDS T-tables
-// -------------------------------------------------------------------------------------
-__constant__ uint8_t c_sbox[256] = {
-    0x63, 0x7c, 0x77, 0x7b, 0xf2, 0x6b, 0x6f, 0xc5, 0x30, 0x01, 0x67, 0x2b, 0xfe, 0xd7, 0xab, 0x76,
-    0xca, 0x82, 0xc9, 0x7d, 0xfa, 0x59, 0x47, 0xf0, 0xad, 0xd4, 0xa2, 0xaf, 0x9c, 0xa4, 0x72, 0xc0,
-    0xb7, 0xfd, 0x93, 0x26, 0x36, 0x3f, 0xf7, 0xcc, 0x34, 0xa5, 0xe5, 0xf1, 0x71, 0xd8, 0x31, 0x15,
-    0x04, 0xc7, 0x23, 0xc3, 0x18, 0x96, 0x05, 0x9a, 0x07, 0x12, 0x80, 0xe2, 0xeb, 0x27, 0xb2, 0x75,
-    0x09, 0x83, 0x2c, 0x1a, 0x1b, 0x6e, 0x5a, 0xa0, 0x52, 0x3b, 0xd6, 0xb3, 0x29, 0xe3, 0x2f, 0x84,
-    0x53, 0xd1, 0x00, 0xed, 0x20, 0xfc, 0xb1, 0x5b, 0x6a, 0xcb, 0xbe, 0x39, 0x4a, 0x4c, 0x58, 0xcf,
-    0xd0, 0xef, 0xaa, 0xfb, 0x43, 0x4d, 0x33, 0x85, 0x45, 0xf9, 0x02, 0x7f, 0x50, 0x3c, 0x9f, 0xa8,
-    0x51, 0xa3, 0x40, 0x8f, 0x92, 0x9d, 0x38, 0xf5, 0xbc, 0xb6, 0xda, 0x21, 0x10, 0xff, 0xf3, 0xd2,
-    0xcd, 0x0c, 0x13, 0xec, 0x5f, 0x97, 0x44, 0x17, 0xc4, 0xa7, 0x7e, 0x3d, 0x64, 0x5d, 0x19, 0x73,
-    0x60, 0x81, 0x4f, 0xdc, 0x22, 0x2a, 0x90, 0x88, 0x46, 0xee, 0xb8, 0x14, 0xde, 0x5e, 0x0b, 0xdb,
-    0xe0, 0x32, 0x3a, 0x0a, 0x49, 0x06, 0x24, 0x5c, 0xc2, 0xd3, 0xac, 0x62, 0x91, 0x95, 0xe4, 0x79,
-    0xe7, 0xc8, 0x37, 0x6d, 0x8d, 0xd5, 0x4e, 0xa9, 0x6c, 0x56, 0xf4, 0xea, 0x65, 0x7a, 0xae, 0x08,
-    0xba, 0x78, 0x25, 0x2e, 0x1c, 0xa6, 0xb4, 0xc6, 0xe8, 0xdd, 0x74, 0x1f, 0x4b, 0xbd, 0x8b, 0x8a,
-    0x70, 0x3e, 0xb5, 0x66, 0x48, 0x03, 0xf6, 0x0e, 0x61, 0x35, 0x57, 0xb9, 0x86, 0xc1, 0x1d, 0x9e,
-    0xe1, 0xf8, 0x98, 0x11, 0x69, 0xd9, 0x8e, 0x94, 0x9b, 0x1e, 0x87, 0xe9, 0xce, 0x55, 0x28, 0xdf,
-    0x8c, 0xa1, 0x89, 0x0d, 0xbf, 0xe6, 0x42, 0x68, 0x41, 0x99, 0x2d, 0x0f, 0xb0, 0x54, 0xbb, 0x16};
-
-struct AesT {
-  uint32_t t[5][256];  // T0..T3 (MixColumns of the S-box output, row-rotated), T4 = S * 0x01010101
-};
-
-DEV void aes_tables_init(AesT& T) {
-  for (uint32_t x = threadIdx.x; x < 256; x += blockDim.x) {
-    const uint32_t s = c_sbox[x];
-    const uint32_t s2 = ((s << 1) ^ ((s >> 7) * 0x1bu)) & 0xffu, s3 = s2 ^ s;
-    const uint32_t t0 = s2 | (s << 8) | (s << 16) | (s3 << 24);
-    T.t[0][x] = t0;
-    T.t[1][x] = __builtin_amdgcn_alignbit(t0, t0, 24);  // rotl 8
-    T.t[2][x] = __builtin_amdgcn_alignbit(t0, t0, 16);
-    T.t[3][x] = __builtin_amdgcn_alignbit(t0, t0, 8);
-    T.t[4][x] = s * 0x01010101u;
-  }
-}
-
-DEV uint32_t b0(uint32_t x) { return x & 0xffu; }
-DEV uint32_t b1(uint32_t x) { return (x >> 8) & 0xffu; }
-DEV uint32_t b2(uint32_t x) { return (x >> 16) & 0xffu; }
-DEV uint32_t b3(uint32_t x) { return x >> 24; }
-
-DEV uint32_t sub_word(const AesT& T, uint32_t x) {
-  return (T.t[4][b0(x)] & 0xffu) | (T.t[4][b1(x)] & 0xff00u) | (T.t[4][b2(x)] & 0xff0000u) |
-         (T.t[4][b3(x)] & 0xff000000u);
-}
-
-DEV void aes128_expand(const AesT& T, const uint32_t key[4], uint32_t rk[44]) {
-  constexpr uint8_t RC[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1b, 0x36};
-#pragma unroll
-  for (int i = 0; i < 4; i++) rk[i] = key[i];
-#pragma unroll
-  for (int i = 4; i < 44; i++) {
-    uint32_t t = rk[i - 1];
-    if ((i & 3) == 0) t = sub_word(T, __builtin_amdgcn_alignbit(t, t, 8)) ^ RC[i / 4 - 1];
-    rk[i] = rk[i - 4] ^ t;
-  }
-}
-
-DEV void aes128_encrypt(const AesT& T, const uint32_t rk[44], const uint32_t in[4],
-                        uint32_t out[4]) {
-  uint32_t s0 = in[0] ^ rk[0], s1 = in[1] ^ rk[1], s2 = in[2] ^ rk[2], s3 = in[3] ^ rk[3];
-#pragma unroll
-  for (int r = 1; r < 10; r++) {
-    const uint32_t t0 = T.t[0][b0(s0)] ^ T.t[1][b1(s1)] ^ T.t[2][b2(s2)] ^ T.t[3][b3(s3)] ^ rk[4 * r];
-    const uint32_t t1 = T.t[0][b0(s1)] ^ T.t[1][b1(s2)] ^ T.t[2][b2(s3)] ^ T.t[3][b3(s0)] ^ rk[4 * r + 1];
-    const uint32_t t2 = T.t[0][b0(s2)] ^ T.t[1][b1(s3)] ^ T.t[2][b2(s0)] ^ T.t[3][b3(s1)] ^ rk[4 * r + 2];
-    const uint32_t t3 = T.t[0][b0(s3)] ^ T.t[1][b1(s0)] ^ T.t[2][b2(s1)] ^ T.t[3][b3(s2)] ^ rk[4 * r + 3];
-    s0 = t0;
-    s1 = t1;
-    s2 = t2;
-    s3 = t3;
-  }
-  out[0] = ((T.t[4][b0(s0)] & 0xffu) | (T.t[4][b1(s1)] & 0xff00u) | (T.t[4][b2(s2)] & 0xff0000u) |
-            (T.t[4][b3(s3)] & 0xff000000u)) ^ rk[40];
-  out[1] = ((T.t[4][b0(s1)] & 0xffu) | (T.t[4][b1(s2)] & 0xff00u) | (T.t[4][b2(s3)] & 0xff0000u) |
-            (T.t[4][b3(s0)] & 0xff000000u)) ^ rk[41];
-  out[2] = ((T.t[4][b0(s2)] & 0xffu) | (T.t[4][b1(s3)] & 0xff00u) | (T.t[4][b2(s0)] & 0xff0000u) |
-            (T.t[4][b3(s1)] & 0xff000000u)) ^ rk[42];
-  out[3] = ((T.t[4][b0(s3)] & 0xffu) | (T.t[4][b1(s0)] & 0xff00u) | (T.t[4][b2(s1)] & 0xff0000u) |
-            (T.t[4][b3(s2)] & 0xff000000u)) ^ rk[43];
-}
-
 // GHASH step (SP 800-38D Algorithm 1): y = (y ^ x) * H in GF(2^128), big-endian words
 DEV void ghash_block(uint32_t y[4], const uint32_t x[4], const uint32_t H[4]) {
   uint32_t X[4] = {y[0] ^ x[0], y[1] ^ x[1], y[2] ^ x[2], y[3] ^ x[3]};
@@ -937,37 +764,6 @@ __global__ __launch_bounds__(256) void k_hpke_open(HpkeParams P, OpenArgs a) {
 // Host side
 // -------------------------------------------------------------------------------------
 namespace {
-
-void sha256_compress_host(uint32_t st[8], const uint8_t blk[64]) {
-  static const uint32_t K[64] = {
-      0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u,
-      0xab1c5ed5u, 0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu,
-      0x9bdc06a7u, 0xc19bf174u, 0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu,
-      0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau, 0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u,
-      0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u, 0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu,
-      0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u, 0xa2bfe8a1u, 0xa81a664bu,
-      0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u, 0x19a4c116u,
-      0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
-      0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u,
-      0xc67178f2u};
-  auto rotr = [](uint32_t x, int n) { return (x >> n) | (x << (32 - n)); };
-  uint32_t w[64];
-  for (int i = 0; i < 16; i++)
-    w[i] = (uint32_t)blk[4 * i] << 24 | (uint32_t)blk[4 * i + 1] << 16 |
-           (uint32_t)blk[4 * i + 2] << 8 | blk[4 * i + 3];
-  for (int i = 16; i < 64; i++)
-    w[i] = w[i - 16] + (rotr(w[i - 15], 7) ^ rotr(w[i - 15], 18) ^ (w[i - 15] >> 3)) + w[i - 7] +
-           (rotr(w[i - 2], 17) ^ rotr(w[i - 2], 19) ^ (w[i - 2] >> 10));
-  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6],
-           h = st[7];
-  for (int i = 0; i < 64; i++) {
-    const uint32_t t1 = h + (rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25)) + ((e & f) ^ (~e & g)) +
-                        K[i] + w[i];
-    const uint32_t t2 = (rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
-    h = g, g = f, f = e, e = d + t1, d = c, c = b, b = a, a = t1 + t2;
-  }
-  st[0] += a, st[1] += b, st[2] += c, st[3] += d, st[4] += e, st[5] += f, st[6] += g, st[7] += h;
-}
 
 void sha256_host(const std::vector<uint8_t>& msg, uint8_t out[32]) {
   uint32_t st[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,

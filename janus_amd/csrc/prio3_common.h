@@ -375,6 +375,21 @@ struct KTime {
   uint64_t launches = 0;
 };
 
+// PRIO3_SUMVEC_F64_MP (prio3_mp64.hip): Field64 SumVec, XofHmacSha256Aes128, multiproof
+struct Mp64Params {
+  uint32_t meas_len, out_len, bits, chunk, calls, P, logP, glen, proof_len /* one proof */,
+      arity, vlen, np;
+  uint32_t dst[8][2];          // dst(usage) bytes, LE words
+  uint32_t vk_ist[8], vk_ost[8];    // HMAC midstates of the verify key (query randomness)
+  uint32_t z_ist[8], z_ost[8];      // HMAC midstates of the all-zero seed (joint-rand seeds)
+  uint64_t alpha, alpha_inv, invP, half;
+  const uint64_t* sigma;       // device [P]: sum_{k=1..calls} alpha^(k e)
+};
+
+struct prio3_engine;
+int launch_mp64(prio3_engine* e, uint32_t n, InPtrs in, OutPtrs out, Scratch sc,
+                hipStream_t st);
+
 struct prio3_engine {
   prio3_params params;
   prio3_sizes_t sz;
@@ -420,6 +435,8 @@ struct prio3_engine {
   int qh_occ = 3;
   int qh_regs = 0;
   int timing = 0;
+  Mp64Params mp{};          // PRIO3_SUMVEC_F64_MP only
+  uint64_t* d_sigma64 = nullptr;
   std::vector<KTime> times;
   std::vector<hipEvent_t> ev_pool;
   std::mutex mu;

@@ -31,6 +31,7 @@
 
 #include "prio3_common.h"
 #include "sha256_device.h"
+#include "sha256_host.h"
 
 #ifndef XOFD_OCC
 #define XOFD_OCC 3
@@ -2017,7 +2018,8 @@ static uint32_t next_pow2(uint32_t n) {
 static int fill_sizes(const prio3_params* pp, prio3_sizes_t* s, DevParams* dp) {
   if (!pp) return PRIO3_EINVAL;
   uint32_t proofs = pp->num_proofs ? pp->num_proofs : 1;
-  if (proofs != 1) return PRIO3_EUNSUPPORTED;
+  const bool mp = pp->kind == PRIO3_SUMVEC_F64_MP;
+  if (mp ? (proofs < 2 || proofs > 8) : proofs != 1) return mp ? PRIO3_EINVAL : PRIO3_EUNSUPPORTED;
   DevParams d;
   memset(&d, 0, sizeof d);
   d.kind = pp->kind;
@@ -2056,6 +2058,17 @@ static int fill_sizes(const prio3_params* pp, prio3_sizes_t* s, DevParams* dp) {
       d.arity = 2 * pp->chunk_length;
       d.calls = (d.meas_len + pp->chunk_length - 1) / pp->chunk_length;
       break;
+    case PRIO3_SUMVEC_F64_MP:  // SumVec<Field64, ParallelSum<Mul>> (vdaf.rs:173-195)
+      if (pp->bits == 0 || pp->bits > 64 || pp->length == 0 || pp->chunk_length == 0)
+        return PRIO3_EINVAL;
+      algo = 0xFFFF1003u;  // ALGORITHM_ID_PRIO3_SUM_VEC_FIELD64_MULTIPROOF_HMACSHA256_AES128
+      d.es = 8;
+      d.meas_len = pp->bits * pp->length;
+      d.out_len = pp->length;
+      d.jr_len = 1;
+      d.arity = 2 * pp->chunk_length;
+      d.calls = (d.meas_len + pp->chunk_length - 1) / pp->chunk_length;
+      break;
     case PRIO3_HISTOGRAM:
       if (pp->length == 0 || pp->chunk_length == 0) return PRIO3_EINVAL;
       algo = 3;
@@ -2076,10 +2089,11 @@ static int fill_sizes(const prio3_params* pp, prio3_sizes_t* s, DevParams* dp) {
   d.glen = 2 * (d.P - 1) + 1;
   d.proof_len = d.arity + d.glen;
   d.verifier_len = d.arity + 2;
-  d.helper_share_len = d.jr_len ? 48 : 32;
-  d.public_share_len = d.jr_len ? 32 : 0;
-  d.prep_share_len = d.verifier_len * d.es + (d.jr_len ? 16 : 0);
-  d.leader_share_len = (d.meas_len + d.proof_len) * d.es + (d.jr_len ? 16 : 0);
+  const uint32_t S = mp ? 32 : 16;  // seed size
+  d.helper_share_len = d.jr_len ? 3 * S : 2 * S;
+  d.public_share_len = d.jr_len ? 2 * S : 0;
+  d.prep_share_len = d.verifier_len * proofs * d.es + (d.jr_len ? S : 0);
+  d.leader_share_len = (d.meas_len + d.proof_len * proofs) * d.es + (d.jr_len ? S : 0);
   for (uint32_t u = 1; u <= 7; u++) {
     uint8_t b[8] = {8, 0, (uint8_t)(algo >> 24), (uint8_t)(algo >> 16), (uint8_t)(algo >> 8),
                     (uint8_t)algo, 0, (uint8_t)u};
@@ -2135,10 +2149,11 @@ static int fill_sizes(const prio3_params* pp, prio3_sizes_t* s, DevParams* dp) {
     s->public_share_len = d.public_share_len;
     s->helper_share_len = d.helper_share_len;
     s->prep_share_len = d.prep_share_len;
-    s->prep_msg_len = d.jr_len ? 16 : 0;
+    s->prep_msg_len = d.jr_len ? S : 0;
     s->agg_share_len = d.out_len * d.es;
     s->leader_input_share_len = d.leader_share_len;
   }
+  d.proof_len *= proofs;  // scratch holds every proof (prio3_sizes_t reports one)
   if (dp) *dp = d;
   return PRIO3_OK;
 }
@@ -2169,7 +2184,9 @@ static int ensure_scratch(prio3_engine* e, uint32_t n) {
   size_t sizes[] = {es * d.meas_len * ld, es * d.proof_len * ld, es * (d.jr_len ? d.jr_len : 1) * ld,
                     es * ld, 16 * (size_t)ld, 16 * (size_t)ld, (size_t)ld, es * d.P * ld,
                     es * d.P * ld, es * d.arity * ld,
-                    (d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC) ? es * d.out_len * ld : 16,
+                    (d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC || d.kind == PRIO3_SUMVEC_F64_MP)
+                        ? es * d.out_len * ld
+                        : 16,
                     es * d.calls * ld, (size_t)ld};
   for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]); i++) HIPCHK(hipMalloc(bufs[i], sizes[i]));
   e->cap = ld;
@@ -2236,9 +2253,11 @@ int prio3_sizes(const prio3_params* params, prio3_sizes_t* out) {
   return fill_sizes(params, out, nullptr);
 }
 
-int prio3_engine_create(const prio3_params* params, const uint8_t verify_key[16], int device,
-                        prio3_engine** out) {
+int prio3_engine_create_ex(const prio3_params* params, const uint8_t* verify_key,
+                           size_t verify_key_len, int device, prio3_engine** out) {
   if (!params || !verify_key || !out) return PRIO3_EINVAL;
+  const bool mp = params->kind == PRIO3_SUMVEC_F64_MP;
+  if (verify_key_len != (mp ? 32u : 16u)) return PRIO3_EINVAL;
   prio3_engine* e = new prio3_engine();
   int rc = fill_sizes(params, &e->sz, &e->dp);
   if (rc) {
@@ -2246,15 +2265,63 @@ int prio3_engine_create(const prio3_params* params, const uint8_t verify_key[16]
     return rc;
   }
   e->params = *params;
-  memcpy(e->dp.vk, verify_key, 16);
+  if (!mp) memcpy(e->dp.vk, verify_key, 16);
   e->device = device;
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     delete e;
     return PRIO3_EDEVICE;
   }
+  if (mp) {  // prio3_mp64.hip constants
+    const DevParams& d = e->dp;
+    Mp64Params& m = e->mp;
+    m.meas_len = d.meas_len;
+    m.out_len = d.out_len;
+    m.bits = params->bits;
+    m.chunk = params->chunk_length;
+    m.calls = d.calls;
+    m.P = d.P;
+    m.logP = d.logP;
+    m.glen = d.glen;
+    m.np = params->num_proofs;
+    m.proof_len = d.proof_len / m.np;
+    m.arity = d.arity;
+    m.vlen = d.verifier_len;
+    memcpy(m.dst, d.dst, sizeof m.dst);
+    hmac_midstates_host(verify_key, 32, m.vk_ist, m.vk_ost);
+    static const uint8_t zero32[32] = {0};
+    hmac_midstates_host(zero32, 32, m.z_ist, m.z_ost);
+    const u128 alpha = d.roots64[d.logP];
+    m.alpha = (uint64_t)alpha;
+    m.alpha_inv = (uint64_t)hpow(alpha, d.P - 1, HP64);
+    m.invP = d.invP64;
+    m.half = d.half64;
+    std::vector<uint64_t> sig(d.P);
+    for (uint32_t e2 = 0; e2 < d.P; e2++) {
+      const u128 ae = hpow(alpha, e2, HP64);
+      u128 sum = 0, x = 1;
+      for (uint32_t c = 1; c <= d.calls; c++) {
+        x = hmul(x, ae, HP64);
+        sum = (sum + x) % HP64;
+      }
+      sig[e2] = (uint64_t)sum;
+    }
+    if (hipMalloc((void**)&e->d_sigma64, 8 * (size_t)d.P) != hipSuccess ||
+        hipMemcpy(e->d_sigma64, sig.data(), 8 * (size_t)d.P, hipMemcpyHostToDevice) !=
+            hipSuccess) {
+      (void)hipStreamDestroy(e->stream);
+      delete e;
+      return PRIO3_EDEVICE;
+    }
+    m.sigma = e->d_sigma64;
+  }
   *out = e;
   return PRIO3_OK;
+}
+
+int prio3_engine_create(const prio3_params* params, const uint8_t verify_key[16], int device,
+                        prio3_engine** out) {
+  return prio3_engine_create_ex(params, verify_key, 16, device, out);
 }
 
 void prio3_engine_destroy(prio3_engine* e) {
@@ -2265,14 +2332,13 @@ void prio3_engine_destroy(prio3_engine* e) {
                   e->sc.flag, e->sc.Lbuf, e->sc.PVbuf, e->sc.acc, e->sc.out, e->sc.beta, e->d_mask,
                   e->d_prep_partial, e->d_pcount, e->d_nonces, e->d_pub, e->d_helper,
                   e->d_leader, e->d_msgs, e->d_status, e->d_wpart, e->d_wseg, e->d_agg64,
-                  e->d_fix, e->d_cpart, e->d_cseg, e->d_linput};
+                  e->d_fix, e->d_cpart, e->d_cseg, e->d_linput, e->d_sigma64};
   for (auto b : bufs)
     if (b) (void)hipFree(b);
   for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
   for (auto s2 : e->side) (void)hipStreamDestroy(s2);
   for (auto j : e->side_ev) (void)hipEventDestroy(j);
   if (e->fork_ev) (void)hipEventDestroy(e->fork_ev);
-  for (auto s2 : e->side) (void)hipStreamDestroy(s2);
   (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -2368,7 +2434,7 @@ static int launch_prepare(prio3_engine* e, uint32_t c0, uint32_t n, InPtrs in, O
   if (in.pub) in.pub += (size_t)dp.public_share_len * c0;
   in.helper += (size_t)dp.helper_share_len * c0;
   in.leader += (size_t)dp.prep_share_len * c0;
-  out.prep_msgs += 16 * (size_t)c0;
+  out.prep_msgs += (size_t)(dp.kind == PRIO3_SUMVEC_F64_MP ? 32 : 16) * c0;
   out.status += c0;
   void** soa[] = {&sc.meas, &sc.proofs, &sc.jr, &sc.qr, &sc.Lbuf, &sc.PVbuf, &sc.acc, &sc.out,
                   &sc.beta};
@@ -2381,6 +2447,11 @@ static int launch_prepare(prio3_engine* e, uint32_t c0, uint32_t n, InPtrs in, O
   if (sc.wseg) sc.wseg += c0 / 64;
   if (sc.wpart) sc.wpart += (size_t)(c0 / 64) * dp.meas_len * 8;
   const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
+  if (dp.kind == PRIO3_SUMVEC_F64_MP) {
+    int rc = PRIO3_OK;
+    TIMED(e, st, "k_mp64_prepare", (rc = launch_mp64(e, n, in, out, sc, st)));
+    return rc;
+  }
   if (dp.es == 16) {
     if (dp.jr_len && e->split_xof == 2 && (42 + dp.meas_len * 16) / 168 >= 2) {
       if (fuse)
@@ -2570,7 +2641,9 @@ int prio3_device_accumulate(prio3_engine* e, uint32_t n, const uint8_t* d_status
     HIPCHK(hipMalloc((void**)&e->d_pcount, 8 * (size_t)nchunks));
     e->partial_cap = need;
   }
-  const void* src = (d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC) ? e->sc.out : e->sc.meas;
+  const void* src = (d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC || d.kind == PRIO3_SUMVEC_F64_MP)
+                        ? e->sc.out
+                        : e->sc.meas;
   for (uint32_t s = 0; s < n_segments; s++) {
     TIMED(e, st, "k_mask",
           (k_mask<<<(n + 255) / 256, 256, 0, st>>>(n, d_status, d_segment_ids, d_accept_mask, s,
@@ -2713,7 +2786,9 @@ int prio3_device_output_shares(prio3_engine* e, uint32_t n, uint8_t* out) {
   HIPCHK(hipStreamSynchronize(e->stream));
   HIPCHK(hipDeviceSynchronize());
   const DevParams& d = e->dp;
-  const void* src = (d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC) ? e->sc.out : e->sc.meas;
+  const void* src = (d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC || d.kind == PRIO3_SUMVEC_F64_MP)
+                        ? e->sc.out
+                        : e->sc.meas;
   std::vector<uint8_t> soa((size_t)d.out_len * d.ld * d.es);
   HIPCHK(hipMemcpy(soa.data(), src, soa.size(), hipMemcpyDeviceToHost));
   for (uint32_t r = 0; r < n; r++)
@@ -2734,7 +2809,7 @@ static int ensure_io(prio3_engine* e, uint32_t n) {
   const DevParams& d = e->dp;
   size_t sizes[] = {16 * (size_t)n, (size_t)(d.public_share_len ? d.public_share_len : 16) * n,
                     (size_t)d.helper_share_len * n, (size_t)d.prep_share_len * n,
-                    16 * (size_t)n, (size_t)n};
+                    (size_t)(e->sz.prep_msg_len ? e->sz.prep_msg_len : 16) * n, (size_t)n};
   for (size_t i = 0; i < 6; i++) HIPCHK(hipMalloc((void**)bufs[i], sizes[i]));
   e->io_cap = n;
   return PRIO3_OK;
@@ -2774,7 +2849,8 @@ int prio3_helper_prepare_batch(prio3_engine* e, uint32_t n, const uint8_t* nonce
     if (n) {
       HIPCHK(hipMemcpyAsync(status_out, e->d_status, n, hipMemcpyDeviceToHost, st));
       if (d.jr_len)
-        HIPCHK(hipMemcpyAsync(prep_msgs_out, e->d_msgs, 16 * (size_t)n, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(prep_msgs_out, e->d_msgs, (size_t)e->sz.prep_msg_len * n,
+                              hipMemcpyDeviceToHost, st));
     }
     HIPCHK(hipStreamSynchronize(st));
     if (e->timing) collect_times(e);
@@ -2875,6 +2951,7 @@ int prio3_device_leader_prepare_init(prio3_engine* e, uint32_t n, const uint8_t*
                                      const uint8_t* d_public_shares,
                                      const uint8_t* d_leader_input_shares, uint8_t* d_prep_shares,
                                      uint8_t* d_status, void* stream) {
+  if (e && e->dp.kind == PRIO3_SUMVEC_F64_MP) return PRIO3_EUNSUPPORTED;  // helper role only
   if (!e) return PRIO3_EINVAL;
   if (n == 0) return PRIO3_OK;
   if (!d_nonces || !d_leader_input_shares || !d_prep_shares || !d_status ||
@@ -2920,6 +2997,7 @@ int prio3_device_leader_prepare_init(prio3_engine* e, uint32_t n, const uint8_t*
 
 int prio3_device_leader_prepare_next(prio3_engine* e, uint32_t n, const uint8_t* d_prep_msgs,
                                      uint8_t* d_status, void* stream) {
+  if (e && e->dp.kind == PRIO3_SUMVEC_F64_MP) return PRIO3_EUNSUPPORTED;  // helper role only
   if (!e || n > e->cap) return PRIO3_EINVAL;
   if (n == 0) return PRIO3_OK;
   if (!d_status || (e->dp.jr_len && !d_prep_msgs)) return PRIO3_EINVAL;
@@ -2937,6 +3015,7 @@ int prio3_leader_prepare_init_batch(prio3_engine* e, uint32_t n, const uint8_t* 
                                     const uint8_t* public_shares,
                                     const uint8_t* leader_input_shares, uint8_t* prep_shares_out,
                                     uint8_t* status_out, prio3_batch** batch_out) {
+  if (e && e->dp.kind == PRIO3_SUMVEC_F64_MP) return PRIO3_EUNSUPPORTED;  // helper role only
   if (!e || (n && (!nonces || !leader_input_shares || !prep_shares_out || !status_out)))
     return PRIO3_EINVAL;
   const DevParams& d = e->dp;
@@ -2992,7 +3071,8 @@ int prio3_leader_prepare_next_batch(prio3_batch* b, const uint8_t* prep_msgs,
     HIPCHK(hipSetDevice(e->device));
     hipStream_t st = e->stream;
     if (d.jr_len)
-      HIPCHK(hipMemcpyAsync(e->d_msgs, prep_msgs, 16 * (size_t)n, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(e->d_msgs, prep_msgs, (size_t)e->sz.prep_msg_len * n,
+                            hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(e->d_status, status_inout, n, hipMemcpyHostToDevice, st));
   }
   int rc = prio3_device_leader_prepare_next(e, n, e->d_msgs, e->d_status, e->stream);

@@ -67,3 +67,94 @@ DEV void compress(uint32_t st[8], uint32_t w[16]) {
 }
 
 }  // namespace sha256d
+
+// -------------------------------------------------------------------------------------
+// SHA-256 message buffers (big-endian words) and HMAC
+// -------------------------------------------------------------------------------------
+template <int NW>
+struct Msg32 {
+  uint32_t w[NW];
+};
+template <int NW>
+DEV void mz(Msg32<NW>& m) {
+#pragma unroll
+  for (int i = 0; i < NW; i++) m.w[i] = 0;
+}
+template <int NW>
+DEV void mbyte(Msg32<NW>& m, int pos, uint32_t b) {
+  m.w[pos >> 2] |= (b & 0xffu) << (24 - 8 * (pos & 3));
+}
+template <int NW, int N>
+DEV void mstr(Msg32<NW>& m, int pos, const char (&s)[N]) {  // N - 1 bytes (no terminator)
+#pragma unroll
+  for (int i = 0; i < N - 1; i++) mbyte(m, pos + i, (uint8_t)s[i]);
+}
+// nbytes (multiple of 4) of big-endian words d at byte position pos
+template <int NW>
+DEV void mwords_be(Msg32<NW>& m, int pos, const uint32_t* d, int nwords) {
+  const int q = pos >> 2, o = pos & 3;
+  if (o == 0) {
+#pragma unroll
+    for (int i = 0; i < nwords; i++) m.w[q + i] |= d[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < nwords; i++) {
+      m.w[q + i] |= d[i] >> (8 * o);
+      m.w[q + i + 1] |= d[i] << (32 - 8 * o);
+    }
+  }
+}
+// little-endian packed bytes (as loaded from memory) at byte position pos
+template <int NW>
+DEV void mwords_le(Msg32<NW>& m, int pos, const uint32_t* d, int nwords) {
+  uint32_t be[16];
+#pragma unroll
+  for (int i = 0; i < nwords; i++) be[i] = __builtin_bswap32(d[i]);
+  mwords_be(m, pos, be, nwords);
+}
+// SHA-256 over the len message bytes of m after `prefix` bytes already compressed into st
+template <int NW>
+DEV void sha_final(uint32_t st[8], Msg32<NW>& m, int len, int prefix) {
+  mbyte(m, len, 0x80);
+  const int nblk = (len + 9 + 63) / 64;
+  m.w[nblk * 16 - 1] = (uint32_t)((prefix + len) * 8);
+#pragma unroll
+  for (int b = 0; b < nblk; b++) {
+    uint32_t blk[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) blk[i] = m.w[16 * b + i];
+    sha256d::compress(st, blk);
+  }
+}
+
+struct HmacKey {
+  uint32_t ist[8], ost[8];
+};
+// HMAC key of 32 bytes (big-endian words): the ipad / opad midstates
+DEV void hmac_key32(HmacKey& k, const uint32_t key[8]) {
+  uint32_t bi[16], bo[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const uint32_t x = i < 8 ? key[i] : 0u;
+    bi[i] = x ^ 0x36363636u;
+    bo[i] = x ^ 0x5c5c5c5cu;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) k.ist[i] = k.ost[i] = sha256d::IV[i];
+  sha256d::compress(k.ist, bi);
+  sha256d::compress(k.ost, bo);
+}
+template <int NW>
+DEV void hmac(const HmacKey& k, Msg32<NW>& m, int len, uint32_t out[8]) {
+  uint32_t st[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) st[i] = k.ist[i];
+  sha_final(st, m, len, 64);
+  Msg32<16> o;
+  mz(o);
+#pragma unroll
+  for (int i = 0; i < 8; i++) o.w[i] = st[i];
+#pragma unroll
+  for (int i = 0; i < 8; i++) out[i] = k.ost[i];
+  sha_final(out, o, 32, 64);
+}

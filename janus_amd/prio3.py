@@ -27,7 +27,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # tools/build_variant.sh); the default is the in-tree library built by `make -C janus_amd`.
 LIB_PATH = os.environ.get("JANUS_PRIO3_LIB") or os.path.join(_HERE, "libjanus_prio3.so")
 
-PRIO3_COUNT, PRIO3_SUM, PRIO3_SUMVEC, PRIO3_HISTOGRAM = 0, 1, 2, 3
+PRIO3_COUNT, PRIO3_SUM, PRIO3_SUMVEC, PRIO3_HISTOGRAM, PRIO3_SUMVEC_F64_MP = 0, 1, 2, 3, 4
 
 STATUS_FINISHED = 0
 STATUS_PREP_INIT = 1
@@ -80,7 +80,7 @@ EXPORTED_SYMBOLS = (
     "prio3_device_aggregate_finish", "prio3_leader_prepare_init_batch",
     "prio3_leader_prepare_next_batch", "prio3_device_leader_prepare_init",
     "prio3_device_leader_prepare_next", "prio3_device_batch_metadata", "prio3_batch_metadata",
-    "prio3_device_combine_metadata",
+    "prio3_device_combine_metadata", "prio3_engine_create_ex",
 )
 # include/janus_hpke.h (the batched HPKE opener, janus_amd/hpke.py)
 HPKE_EXPORTED_SYMBOLS = (
@@ -112,6 +112,7 @@ def load_library() -> C.CDLL:
     P, u8p, vp = C.POINTER, C.POINTER(C.c_uint8), C.c_void_p
     L.prio3_sizes.argtypes = [P(Prio3Params), P(Prio3Sizes)]
     L.prio3_engine_create.argtypes = [P(Prio3Params), u8p, C.c_int, P(vp)]
+    L.prio3_engine_create_ex.argtypes = [P(Prio3Params), u8p, C.c_size_t, C.c_int, P(vp)]
     L.prio3_engine_destroy.argtypes = [vp]
     L.prio3_engine_destroy.restype = None
     L.prio3_helper_prepare_batch.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, vp, vp, P(vp)]
@@ -190,6 +191,15 @@ def Prio3Sum(bits: int) -> Prio3:
 
 def Prio3SumVec(bits: int, length: int, chunk_length: int) -> Prio3:
     return Prio3(PRIO3_SUMVEC, bits=bits, length=length, chunk_length=chunk_length)
+
+
+def Prio3SumVecField64MultiproofHmacSha256Aes128(proofs: int, bits: int, length: int,
+                                                 chunk_length: int) -> Prio3:
+    """janus_core::vdaf::new_prio3_sum_vec_field64_multiproof_hmacsha256_aes128
+    (core/src/vdaf.rs:173-195): 32-byte verify key and seeds, proofs >= 2."""
+    if proofs < 2:
+        raise ValueError("Must use at least two proofs with Field64")
+    return Prio3(PRIO3_SUMVEC_F64_MP, bits, length, chunk_length, proofs)
 
 
 def Prio3Histogram(length: int, chunk_length: int) -> Prio3:
@@ -271,14 +281,16 @@ class HelperEngine:
     ``VdafOps`` for a task (aggregator.rs:880-988)."""
 
     def __init__(self, vdaf: Prio3, verify_key: bytes, device: int = 0):
-        if len(verify_key) != 16:
-            raise ValueError("verify key must be 16 bytes (VERIFY_KEY_LENGTH, core/src/vdaf.rs:16)")
+        vk_len = 32 if vdaf.kind == PRIO3_SUMVEC_F64_MP else 16
+        if len(verify_key) != vk_len:
+            raise ValueError(f"verify key must be {vk_len} bytes (VERIFY_KEY_LENGTH[_HMACSHA256_"
+                             "AES128], core/src/vdaf.rs)")
         L = load_library()
         self.vdaf, self.device = vdaf, device
         self.sz = vdaf.sizes()
         h = C.c_void_p()
-        vk = (C.c_uint8 * 16).from_buffer_copy(verify_key)
-        rc = L.prio3_engine_create(C.byref(vdaf.params()), vk, device, C.byref(h))
+        vk = (C.c_uint8 * vk_len).from_buffer_copy(verify_key)
+        rc = L.prio3_engine_create_ex(C.byref(vdaf.params()), vk, vk_len, device, C.byref(h))
         if rc:
             raise RuntimeError(f"prio3_engine_create failed (rc={rc}); a GPU is required")
         self.handle = h

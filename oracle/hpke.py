@@ -39,6 +39,7 @@ def lib():
         _lib.hpke_seal_input_shares.argtypes = [vp, vp, C.c_uint32, C.c_uint64, vp, vp, vp,
                                                 C.c_uint32, vp, C.c_uint32, C.c_uint32, vp, vp,
                                                 vp, C.c_int]
+        _lib.aes128_ctr64_keystream.argtypes = [vp, vp, vp, C.c_size_t]
     return _lib
 
 
@@ -169,3 +170,10 @@ def seal_input_shares(pkR, task_id, ids, times, pubs, shares, seed=1, n_threads=
         _p(ct_len), n_threads)
     assert rc == 0
     return enc, ct, ct_len, stride
+
+
+def aes128_ctr64_keystream(key: bytes, iv: bytes, n: int) -> bytes:
+    """AES-128-CTR keystream, 64-bit BE counter in the IV's low half (prio SeedStreamAes128)."""
+    out = C.create_string_buffer(n)
+    assert lib().aes128_ctr64_keystream(_p(key), _p(iv), out, n) == 0
+    return out.raw

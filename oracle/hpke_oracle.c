@@ -398,3 +398,29 @@ int hpke_seal_input_shares(const uint8_t pkR[32], const uint8_t task_id[32], uin
   for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
   return 0;
 }
+
+/* AES-128 in CTR mode with a 64-bit big-endian counter in the low half of the IV (the
+ * `ctr::Ctr64BE<Aes128>` of prio's SeedStreamAes128, restated): keystream block i =
+ * AES(key, iv[0..8] || BE64(iv[8..16] + i)).  For XofHmacSha256Aes128 (oracle/prio3_py.py). */
+int aes128_ctr64_keystream(const uint8_t key[16], const uint8_t iv[16], uint8_t* out,
+                           size_t len) {
+  EVP_CIPHER_CTX* c = EVP_CIPHER_CTX_new();
+  if (!c || EVP_EncryptInit_ex(c, EVP_aes_128_ecb(), NULL, key, NULL) != 1) return -1;
+  EVP_CIPHER_CTX_set_padding(c, 0);
+  uint64_t lo = 0;
+  for (int i = 0; i < 8; i++) lo = lo << 8 | iv[8 + i];
+  uint8_t blk[16], ks[16];
+  for (size_t o = 0; o < len; o += 16) {
+    memcpy(blk, iv, 8);
+    const uint64_t ctr = lo + o / 16;
+    for (int i = 0; i < 8; i++) blk[8 + i] = (uint8_t)(ctr >> (56 - 8 * i));
+    int l = 0;
+    if (EVP_EncryptUpdate(c, ks, &l, blk, 16) != 1 || l != 16) {
+      EVP_CIPHER_CTX_free(c);
+      return -1;
+    }
+    memcpy(out + o, ks, len - o < 16 ? len - o : 16);
+  }
+  EVP_CIPHER_CTX_free(c);
+  return 0;
+}

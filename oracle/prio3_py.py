@@ -182,12 +182,38 @@ class Xof:
         return out
 
 
-def derive_seed(seed: bytes, dst: bytes, binder: bytes) -> bytes:
-    return Xof(seed, dst, binder).next(16)
+class XofHmacSha256Aes128:
+    """prio 0.16 XofHmacSha256Aes128 (SEED_SIZE 32), restated: HMAC-SHA256 keyed by the seed
+    over len(dst) || dst || binder; the 32-byte tag is split into an AES-128 key and IV for a
+    CTR keystream with a 64-bit big-endian counter (`Ctr64BE<Aes128>`, SeedStreamAes128).  The
+    janus custom VDAF using it: core/src/vdaf.rs:173-195.  Parity with prio UNPINNED."""
+
+    def __init__(self, seed: bytes, dst: bytes, binder: bytes):
+        import hashlib
+        import hmac
+        assert len(seed) == 32
+        tag = hmac.new(seed, bytes([len(dst)]) + dst + binder, hashlib.sha256).digest()
+        self.key, self.iv, self.pos, self.buf = tag[:16], tag[16:], 0, b""
+
+    def next(self, n: int) -> bytes:
+        from oracle.hpke import aes128_ctr64_keystream
+        need = self.pos + n
+        if len(self.buf) < need:
+            self.buf = aes128_ctr64_keystream(self.key, self.iv, -(-max(need, 2 * len(self.buf), 64) // 16) * 16)
+        out = self.buf[self.pos:need]
+        self.pos = need
+        return out
+
+    next_vec = Xof.next_vec
 
 
-def expand_into_vec(F: Field, seed: bytes, dst: bytes, binder: bytes, n: int) -> list[int]:
-    return Xof(seed, dst, binder).next_vec(F, n)
+def derive_seed(seed: bytes, dst: bytes, binder: bytes, xof=Xof) -> bytes:
+    return xof(seed, dst, binder).next(len(seed))
+
+
+def expand_into_vec(F: Field, seed: bytes, dst: bytes, binder: bytes, n: int,
+                    xof=Xof) -> list[int]:
+    return xof(seed, dst, binder).next_vec(F, n)
 
 
 # ------------------------------------------------------------------------------------
@@ -247,17 +273,29 @@ def next_pow2(n: int) -> int:
 
 @dataclass
 class Prio3Type:
-    kind: str  # "count" | "sum" | "sumvec" | "histogram"
+    kind: str  # "count" | "sum" | "sumvec" | "histogram" | "sumvec_f64_mp"
     bits: int = 0
     length: int = 0
     chunk_length: int = 0
     num_proofs: int = 1
     F: Field = dc_field(init=False)
     algo_id: int = dc_field(init=False)
+    seed_size: int = dc_field(init=False)
+    xof: object = dc_field(init=False)
 
     def __post_init__(self):
-        self.algo_id = {"count": 0, "sum": 1, "sumvec": 2, "histogram": 3}[self.kind]
-        self.F = Field64 if self.kind == "count" else Field128
+        # sumvec_f64_mp: Prio3SumVecField64MultiproofHmacSha256Aes128 (core/src/vdaf.rs:173-195:
+        # SumVec<Field64, ParallelSum<Mul>>, XofHmacSha256Aes128, SEED_SIZE 32, algorithm id
+        # 0xFFFF1003 (vdaf.rs:20), num_proofs >= 2)
+        self.algo_id = {"count": 0, "sum": 1, "sumvec": 2, "histogram": 3,
+                        "sumvec_f64_mp": 0xFFFF1003}[self.kind]
+        self.F = Field64 if self.kind in ("count", "sumvec_f64_mp") else Field128
+        self.seed_size = 32 if self.kind == "sumvec_f64_mp" else 16
+        self.xof = XofHmacSha256Aes128 if self.kind == "sumvec_f64_mp" else Xof
+        if self.kind == "sumvec_f64_mp":
+            if self.num_proofs < 2:
+                raise ValueError("Must use at least two proofs with Field64")
+            self.kind = "sumvec"  # the circuit is SumVec's
 
     # --- shapes ---
     @property
@@ -439,31 +477,38 @@ class Prio3:
     def np(self):
         return self.t.num_proofs
 
+    @property
+    def S(self):
+        return self.t.seed_size
+
     def helper_meas(self, agg_id, k):
-        return expand_into_vec(self.F, k, self.dst("meas"), bytes([agg_id]), self.t.meas_len)
+        return expand_into_vec(self.F, k, self.dst("meas"), bytes([agg_id]), self.t.meas_len,
+                               self.t.xof)
 
     def helper_proofs(self, agg_id, k):
         return expand_into_vec(self.F, k, self.dst("proof"), bytes([self.np, agg_id]),
-                               self.t.proof_len * self.np)
+                               self.t.proof_len * self.np, self.t.xof)
 
     def jr_part(self, agg_id, blind, meas, nonce):
         return derive_seed(blind, self.dst("jr_part"),
-                           bytes([agg_id]) + nonce + b"".join(self.F.enc(x) for x in meas))
+                           bytes([agg_id]) + nonce + b"".join(self.F.enc(x) for x in meas),
+                           self.t.xof)
 
     def jr_seed(self, parts):
-        return derive_seed(bytes(16), self.dst("jr_seed"), b"".join(parts))
+        return derive_seed(bytes(self.S), self.dst("jr_seed"), b"".join(parts), self.t.xof)
 
     def joint_rands(self, seed):
         return expand_into_vec(self.F, seed, self.dst("jr"), bytes([self.np]),
-                               self.t.jr_len * self.np)
+                               self.t.jr_len * self.np, self.t.xof)
 
     def query_rands(self, vk, nonce):
         return expand_into_vec(self.F, vk, self.dst("query"), bytes([self.np]) + nonce,
-                               1 * self.np)
+                               1 * self.np, self.t.xof)
 
     def shard(self, measurement, nonce: bytes, rand: bytes):
         t, F = self.t, self.F
-        seeds = [rand[i:i + 16] for i in range(0, len(rand), 16)]
+        S = self.S
+        seeds = [rand[i:i + S] for i in range(0, len(rand), S)]
         meas = t.encode(measurement)
         k_hm, k_hp = seeds[0], seeds[1]
         if t.jr_len:
@@ -479,7 +524,7 @@ class Prio3:
             public = parts[0] + parts[1]
             jr = self.joint_rands(self.jr_seed(parts))
         prove_rands = expand_into_vec(F, k_prove, self.dst("prove"), bytes([self.np]),
-                                      t.arity * self.np)
+                                      t.arity * self.np, t.xof)
         proofs = []
         for k in range(self.np):
             proofs += t.prove(meas, prove_rands[k * t.arity:(k + 1) * t.arity],
@@ -500,13 +545,14 @@ class Prio3:
             meas, proofs = vals[:t.meas_len], vals[t.meas_len:]
             blind = share[(t.meas_len + t.proof_len * self.np) * es:]
         else:
-            meas = self.helper_meas(agg_id, share[:16])
-            proofs = self.helper_proofs(agg_id, share[16:32])
-            blind = share[32:48]
+            S = self.S
+            meas = self.helper_meas(agg_id, share[:S])
+            proofs = self.helper_proofs(agg_id, share[S:2 * S])
+            blind = share[2 * S:3 * S]
         jr, part, corrected = [], b"", b""
         if t.jr_len:
             part = self.jr_part(agg_id, blind, meas, nonce)
-            parts = [public[0:16], public[16:32]]
+            parts = [public[0:self.S], public[self.S:2 * self.S]]
             parts[agg_id] = part
             corrected = self.jr_seed(parts)
             jr = self.joint_rands(corrected)
@@ -531,7 +577,8 @@ class Prio3:
             if not t.decide(v[k * t.verifier_len:(k + 1) * t.verifier_len]):
                 raise ValueError("decide failed")
         if t.jr_len:
-            return self.jr_seed([leader_ps[nv * es:nv * es + 16], helper_ps[nv * es:nv * es + 16]])
+            S = self.S
+            return self.jr_seed([leader_ps[nv * es:nv * es + S], helper_ps[nv * es:nv * es + S]])
         return b""
 
     def prepare_next(self, state, msg: bytes) -> list[int]:
