@@ -92,7 +92,8 @@ def main():
     ap.add_argument("--reports", type=int, default=1 << 20, help="reports per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--role", choices=["helper", "leader", "hpke", "pipeline"], default="helper",
+    ap.add_argument("--role", choices=["helper", "leader", "hpke", "pipeline", "mp64"],
+                    default="helper",
                     help="helper (the BASELINE metric), the leader side (SURVEY 8(f) row 1) or "
                          "the batched HPKE open of helper input shares (8(f) row 2)")
     ap.add_argument("--opt", action="append", default=[],
@@ -104,6 +105,8 @@ def main():
         return hpke_main(args)
     if args.role == "pipeline":
         return pipeline_main(args)
+    if args.role == "mp64":
+        return mp64_main(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -521,6 +524,82 @@ def pipeline_main(args):
         out["checks"]["cpu_gpu_parity_on_sample"] = bool(
             np.array_equal(st[:m].cpu().numpy(), cs) and
             np.array_equal(msgs[:m].cpu().numpy(), cm))
+    print(json.dumps(out), flush=True)
+
+
+def _mp64_reports(args):
+    from oracle import prio3_py as P
+    i, cfg, vk = args
+    v = P.Prio3(P.Prio3Type("sumvec_f64_mp", bits=cfg[1], length=cfg[2], chunk_length=cfg[3],
+                            num_proofs=cfg[0]))
+    rng = np.random.default_rng(1000 + i)
+    m = [int(x) for x in rng.integers(0, 2 ** cfg[1], cfg[2])]
+    nonce = bytes(rng.integers(0, 256, 16, dtype=np.uint8))
+    pub, leader, helper = v.shard(m, nonce, bytes(rng.integers(0, 256, 160, dtype=np.uint8)))
+    _, lps, _ = v.prepare_init(vk, 0, nonce, pub, leader)
+    return nonce, pub, helper, lps
+
+
+def mp64_main(args):
+    """Prio3SumVecField64MultiproofHmacSha256Aes128 helper prepare+aggregate line (not the
+    BASELINE metric) at the reference's own end-to-end configuration
+    (proofs 2, bits 16, length 15, chunk 16: integration_tests janus.rs:387-392).  Reports come
+    from the Python restatement (distinct ones tiled); no compiled CPU restatement of this VDAF
+    exists here, so no cpu_baseline is reported."""
+    import multiprocessing as mp_
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    cfg = (2, 16, 15, 16)
+    vk = bytes(range(0x40, 0x60))
+    n = args.reports
+    uniq = min(n, 2048)
+    t0 = time.perf_counter()
+    with mp_.get_context("spawn").Pool(min(16, cpu_threads())) as pool:
+        reps = pool.map(_mp64_reports, [(i, cfg, vk) for i in range(uniq)])
+    gen_s = time.perf_counter() - t0
+    reps_n = -(-n // uniq)
+    A = lambda k: torch.from_numpy(np.ascontiguousarray(np.tile(
+        np.array([list(r[k]) for r in reps], np.uint8), (reps_n, 1))[:n])).to(dev)
+    nonces, pub, helper, lps = A(0), A(1), A(2), A(3)
+    eng = J.HelperEngine(J.Prio3SumVecField64MultiproofHmacSha256Aes128(*cfg), vk, device=0)
+    msgs = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    seg = torch.zeros(n, dtype=torch.int32, device=dev)
+    agg = torch.zeros((1, eng.sz.agg_share_len), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def step():
+        s = torch.cuda.current_stream().cuda_stream
+        eng.prepare_aggregate_device(nonces, pub, helper, lps, seg, 1, msgs, status, stream=s)
+        eng.aggregate_finish_device(status, None, agg, cnt, stream=s)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    eng.set_option("timing", 1)
+    eng.timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    times = eng.timing()
+    eng.set_option("timing", 0)
+    value = n * args.steps / elapsed
+    out = dict(metric="reports prepared+aggregated/sec (helper, Prio3SumVecField64Multiproof"
+                      "HmacSha256Aes128 proofs=2 bits=16 length=15 chunk=16)", value=value,
+               unit="reports/s", n_gpus=1, steps=args.steps, warmup=args.warmup,
+               ms_per_step=elapsed / args.steps * 1e3, higher_is_better=True, scaling="weak",
+               vs_baseline=None, dtype="u64 (Field64), bytes",
+               data=f"synthetic: {uniq} distinct reports from the Python restatement tiled "
+                    f"x{reps_n}; generation {gen_s:.1f}s, not timed",
+               config=dict(workload="Prio3SumVecField64MultiproofHmacSha256Aes128 helper "
+                                    "prepare+aggregate", proofs=2, bits=16, length=15,
+                           chunk_length=16, reports=n),
+               kernels={k: dict(ms_total=v[0], launches=v[1], ms_avg=v[0] / max(v[1], 1))
+                        for k, v in times.items()},
+               checks=dict(finished=int((status == 0).sum().item()), agg_count=int(cnt[0])),
+               cpu_baseline=None)
     print(json.dumps(out), flush=True)
 
 

@@ -88,7 +88,10 @@ def _expected(v, reps):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("proofs,bits,length,chunk,n", [(2, 1, 10, 3, 70), (3, 2, 5, 3, 40),
-                                                        (2, 8, 20, 7, 33)])
+                                                        (2, 8, 20, 7, 33),
+                                                        # the reference's own end-to-end config
+                                                        # (integration janus.rs:387-392)
+                                                        (2, 16, 15, 16, 24)])
 def test_gpu_mp64_matches_oracle(proofs, bits, length, chunk, n):
     from janus_amd import prio3 as J
     v = _vdaf(proofs, bits, length, chunk)
