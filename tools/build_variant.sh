@@ -7,11 +7,12 @@ TAG=$1; shift
 R=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$R/janus_amd/variants/$TAG
 mkdir -p $OUT
-for f in prio3_engine prio3_client; do
+SRCS="prio3_engine prio3_client hpke dap_codec prio3_mp64"
+for f in $SRCS; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function "$@" \
     -c -o $OUT/$f.o $R/janus_amd/csrc/$f.hip &
 done
 wait
-/opt/rocm/bin/hipcc -O3 -fPIC --offload-arch=gfx950 -shared -o $R/janus_amd/variants/libjanus_prio3_$TAG.so $OUT/prio3_engine.o $OUT/prio3_client.o
+/opt/rocm/bin/hipcc -O3 -fPIC --offload-arch=gfx950 -shared -o $R/janus_amd/variants/libjanus_prio3_$TAG.so $(for f in $SRCS; do echo $OUT/$f.o; done)
 rm -rf $OUT
 echo built janus_amd/variants/libjanus_prio3_$TAG.so
