@@ -1,10 +1,12 @@
 // dap_codec.hip -- DAP-09 wire format <-> SoA marshaling for the helper's aggregation-job init
 // on MI355X (gfx950); SURVEY 8(f) row 3.  See include/janus_dap.h for the encodings.
 //
-//  k_unpack_init  one PrepareInit per lane at base + r * record_len (the speculative uniform
-//                 layout), every length field validated; fields scattered to the SoA buffers
-//                 the HPKE opener and the prio3 engine read.  Records start at arbitrary byte
-//                 offsets, so each lane reads aligned dwords and funnel-shifts them.
+//  k_unpack_check / k_unpack_gather
+//                 the speculative uniform layout (every PrepareInit has the first one's
+//                 length): one lane per record validates its length and type fields; then one
+//                 lane per OUTPUT DWORD gathers the byte fields (report ID, public share, enc,
+//                 payload, leader prep share) into the SoA buffers the HPKE opener and the
+//                 prio3 engine read -- coalesced reads of the body and coalesced writes.
 //  k_resp_count / k_resp_scan / k_resp_write
 //                 AggregationJobResp: per-block counts of the two PrepareResp sizes, an
 //                 exclusive scan of the block totals, then each lane writes its record at its
@@ -42,44 +44,36 @@ DEV uint32_t ld_le32(const uint8_t* base, uint64_t off) {
   const uint32_t hi = *(const uint32_t*)(base + a + 4);
   return __builtin_amdgcn_alignbit(hi, lo, 8 * sh);
 }
-// copy len bytes from an arbitrary source offset to a 4-byte-aligned destination
-DEV void copy_to_aligned(uint8_t* dst, const uint8_t* base, uint64_t off, uint32_t len) {
-  uint32_t i = 0;
-  for (; i + 4 <= len; i += 4) *(uint32_t*)(dst + i) = ld_le32(base, off + i);
-  for (; i < len; i++) dst[i] = base[off + i];
-}
-
 struct UnpackArgs {
   const uint8_t* body;
   uint64_t list_off;
-  uint32_t n, rec, psl, enc_len, pay_len, msg_len, ps_len, ct_stride;
-  uint8_t *ids, *pubs, *cfg, *enc, *ct, *ps, *msg_status;
+  uint32_t n, rec, psl, enc_len, pay_len, msg_len, ps_len;
+  uint8_t *cfg, *msg_status;
   uint64_t* times;
   uint32_t *ct_len, *mismatch;
 };
 
 // The body buffer must be readable up to a dword past its end (the host pads the copy).
-__global__ __launch_bounds__(256) void k_unpack_init(UnpackArgs a) {
+// k_unpack_check: one lane per record, only the length / type fields (a few scattered loads):
+// validates the record against the first record's shape and writes the small per-report
+// outputs (time, config id, payload length, message status).
+__global__ __launch_bounds__(256) void k_unpack_check(UnpackArgs a) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= a.n) return;
   const uint8_t* b = a.body;
   uint64_t o = a.list_off + (uint64_t)r * a.rec;
   const uint64_t end = o + a.rec;
-  // ReportMetadata
-  const uint64_t o_id = o, o_time = o + 16;
+  const uint64_t o_time = o + 16;
   o += 24;
   const uint32_t psl = ld_be32(b, o);
-  const uint64_t o_pub = o + 4;
-  o = o_pub + psl;
+  o += 4 + (uint64_t)psl;
   bool ok = psl == a.psl && o + 3 <= end;
   const uint32_t cfg = ok ? ld_u8(b, o) : 0u;
   const uint32_t encl = ok ? ld_be16(b, o + 1) : 0u;
-  const uint64_t o_enc = o + 3;
-  o = o_enc + encl;
+  o += 3 + (uint64_t)encl;
   ok = ok && encl == a.enc_len && o + 4 <= end;
   const uint32_t payl = ok ? ld_be32(b, o) : 0u;
-  const uint64_t o_pay = o + 4;
-  o = o_pay + payl;
+  o += 4 + (uint64_t)payl;
   ok = ok && payl == a.pay_len && o + 4 <= end;
   const uint32_t msgl = ok ? ld_be32(b, o) : 0u;
   const uint64_t o_msg = o + 4;
@@ -99,14 +93,49 @@ __global__ __launch_bounds__(256) void k_unpack_init(UnpackArgs a) {
   else if (psl2 != a.ps_len || msgl != 5 + psl2)
     st = 2;  // CodecPrepShare
   a.msg_status[r] = st;
-  copy_to_aligned(a.ids + 16 * (size_t)r, b, o_id, 16);
   a.times[r] = ((uint64_t)ld_be32(b, o_time) << 32) | ld_be32(b, o_time + 4);
-  if (a.psl) copy_to_aligned(a.pubs + (size_t)a.psl * r, b, o_pub, a.psl);
   a.cfg[r] = (uint8_t)cfg;
-  copy_to_aligned(a.enc + (size_t)a.enc_len * r, b, o_enc, a.enc_len);
-  copy_to_aligned(a.ct + (size_t)a.ct_stride * r, b, o_pay, a.pay_len);
   a.ct_len[r] = a.pay_len;
-  if (st == 0) copy_to_aligned(a.ps + (size_t)a.ps_len * r, b, o_msg + 5, a.ps_len);
+}
+
+// k_unpack_gather: the byte fields, one output dword per lane (grid.y = field): adjacent lanes
+// read adjacent source bytes of the uniform records and write adjacent output dwords, so both
+// sides are coalesced.  Output rows are `row` bytes, the field is `len` bytes at `off` within
+// each record; bytes past `len` in a row are zeroed.  Rows that are not a multiple of 4 bytes
+// (no Prio3 / X25519 field has one, but the ABI allows it) take a bytewise branch.
+struct GatherField {
+  uint8_t* dst;
+  uint32_t row, len, off;
+};
+struct GatherArgs {
+  const uint8_t* body;
+  uint64_t list_off;
+  uint32_t n, rec;
+  GatherField f[5];
+};
+__global__ __launch_bounds__(256) void k_unpack_gather(GatherArgs g) {
+  const GatherField F = g.f[blockIdx.y];
+  if (!F.dst) return;
+  const uint64_t total = (uint64_t)g.n * F.row;  // output bytes
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (4 * i >= total) return;
+  if ((F.row & 3u) == 0) {
+    const uint32_t wpr = F.row >> 2;
+    const uint32_t r = (uint32_t)(i / wpr), b = 4 * (uint32_t)(i - (uint64_t)r * wpr);
+    uint32_t v = 0;
+    if (b < F.len) {
+      v = ld_le32(g.body, g.list_off + (uint64_t)r * g.rec + F.off + b);
+      if (b + 4 > F.len) v &= (1u << (8 * (F.len - b))) - 1u;
+    }
+    ((uint32_t*)F.dst)[i] = v;
+    return;
+  }
+  for (uint32_t k = 0; k < 4; k++) {
+    const uint64_t j = 4 * i + k;
+    if (j >= total) break;
+    const uint32_t r = (uint32_t)(j / F.row), c = (uint32_t)(j - (uint64_t)r * F.row);
+    F.dst[j] = c < F.len ? g.body[g.list_off + (uint64_t)r * g.rec + F.off + c] : 0;
+  }
 }
 
 // ---- AggregationJobResp ----------------------------------------------------------------
@@ -334,18 +363,33 @@ int janus_dap_agg_init_unpack_device(const janus_dap_agg_init_layout* L, const u
   a.pay_len = L->payload_len;
   a.msg_len = L->message_len;
   a.ps_len = L->prep_share_len;
-  a.ct_stride = ct_stride;
-  a.ids = d_report_ids;
-  a.pubs = d_public_shares;
   a.cfg = d_config_ids;
-  a.enc = d_enc;
-  a.ct = d_ct;
-  a.ps = d_prep_shares;
   a.msg_status = d_msg_status;
   a.times = d_times;
   a.ct_len = d_ct_len;
   a.mismatch = d_mismatch;
-  k_unpack_init<<<(L->n + 255) / 256, 256, 0, st>>>(a);
+  k_unpack_check<<<(L->n + 255) / 256, 256, 0, st>>>(a);
+  DCHK(hipGetLastError());
+  // field offsets within a record of the first record's shape
+  const uint32_t o_pub = 28, o_enc = o_pub + L->public_share_len + 3,
+                 o_pay = o_enc + L->enc_len + 4, o_ps = o_pay + L->payload_len + 4 + 5;
+  GatherArgs g{};
+  g.body = d_body;
+  g.list_off = L->list_off;
+  g.n = L->n;
+  g.rec = L->record_len;
+  g.f[0] = GatherField{d_report_ids, 16, 16, 0};
+  g.f[1] = GatherField{L->public_share_len ? d_public_shares : nullptr, L->public_share_len,
+                       L->public_share_len, o_pub};
+  g.f[2] = GatherField{d_enc, L->enc_len, L->enc_len, o_enc};
+  g.f[3] = GatherField{d_ct, ct_stride, L->payload_len, o_pay};
+  g.f[4] = GatherField{L->prep_share_len ? d_prep_shares : nullptr, L->prep_share_len,
+                       L->prep_share_len, o_ps};
+  uint64_t maxw = 0;
+  for (auto& f : g.f)
+    if (f.dst && ((uint64_t)L->n * f.row + 3) / 4 > maxw) maxw = ((uint64_t)L->n * f.row + 3) / 4;
+  const uint64_t blocks = (maxw + 255) / 256;
+  k_unpack_gather<<<dim3((uint32_t)blocks, 5), 256, 0, st>>>(g);
   DCHK(hipGetLastError());
   return 0;
 }
