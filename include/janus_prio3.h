@@ -41,6 +41,11 @@ enum {
    * SumVec<Field64, ParallelSum<Mul>> with XofHmacSha256Aes128, 32-byte seeds and verify key,
    * num_proofs >= 2.  Created with prio3_engine_create_ex (32-byte verify key); helper role. */
   PRIO3_SUMVEC_F64_MP = 4,
+  /* Prio3FixedPointBoundedL2VecSum<FixedI16<U15> | FixedI32<U31>> (vdaf.rs:26-31, 292-335,
+   * algorithm 0xFFFF0000): bits = 16 or 32 (the BitSize), length = entries; chunk_length is
+   * ignored (both gadgets use optimal_chunk_length, as prio does).  Helper role.  The circuit
+   * is reconstructed (prio's fixedpoint_l2.rs is not in the reference): DESIGN.md section 10. */
+  PRIO3_FPVEC_BOUNDED_L2 = 5,
 };
 
 /* Per-report status; each maps 1:1 to the PingPongError variant prio returns and to the
@@ -67,8 +72,8 @@ enum {
 
 typedef struct {
   uint32_t kind;         /* PRIO3_* */
-  uint32_t bits;         /* Sum, SumVec */
-  uint32_t length;       /* SumVec, Histogram */
+  uint32_t bits;         /* Sum, SumVec; FPVec bit size (16 or 32) */
+  uint32_t length;       /* SumVec, Histogram, FPVec entries */
   uint32_t chunk_length; /* SumVec, Histogram */
   uint32_t num_proofs;   /* 1 for every standard Prio3 instance */
 } prio3_params;

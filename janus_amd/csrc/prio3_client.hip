@@ -534,7 +534,8 @@ extern "C" int prio3_client_generate_device(prio3_engine* e, uint32_t n, uint64_
                                             uint64_t* d_measurements,
                                             uint8_t* d_leader_out_shares, uint8_t* d_flags,
                                             uint8_t* d_leader_input_shares, void* stream) {
-  if (e && e->dp.kind == PRIO3_SUMVEC_F64_MP) return PRIO3_EUNSUPPORTED;  // TurboSHAKE client only
+  if (e && (e->dp.kind == PRIO3_SUMVEC_F64_MP || e->dp.kind == PRIO3_FPVEC_BOUNDED_L2))
+    return PRIO3_EUNSUPPORTED;  // TurboSHAKE single-gadget clients only
   if (!e || !d_nonces || !d_helper_shares || !d_leader_prep_shares) return PRIO3_EINVAL;
   if (n == 0) return PRIO3_OK;
   std::lock_guard<std::mutex> lk(e->mu);

@@ -14,6 +14,15 @@ struct DevParams {
       verifier_len, chunk, bits, length, prep_share_len, helper_share_len, public_share_len,
       leader_share_len;
   uint32_t n, ld, force_slow;
+  // query-randomness elements per proof (2 for the two-gadget FPVec circuit, else 1) and the
+  // leading dimension of the output-share scratch (FPVec runs the other scratch in sub-batches
+  // of ld columns; out keeps one column per report of the batch)
+  uint32_t qr_len, ld_out;
+  // FPVec gadget 1 (ParallelSum(PolyEval(y^2 - 2^n y), chunk1)): calls, domain, poly length;
+  // gadget 0 uses chunk / arity / calls / P / logP / glen.  invP1 = 1/P1, normc = entries *
+  // 2^(2n-2) / 2 (the norm's constant term, one share of it), twon = 2^n.
+  uint32_t chunk1, calls1, P1, logP1, glen1;
+  uint32_t invP1_128[4], normc128[4], twon128[4];
   uint32_t vk[4];
   uint32_t dst[8][2];
   uint32_t roots128[MAX_ROOTS + 1][4];
@@ -389,6 +398,8 @@ struct Mp64Params {
 struct prio3_engine;
 int launch_mp64(prio3_engine* e, uint32_t n, InPtrs in, OutPtrs out, Scratch sc,
                 hipStream_t st);
+// FPVec FLP query + decide + prepare message + truncate for p.n reports (prio3_fpvec.hip)
+void launch_fpvec_query(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st);
 
 struct prio3_engine {
   prio3_params params;
@@ -418,6 +429,7 @@ struct prio3_engine {
   int fuse_acc = 1;
   int leader_fast = 1;
   int chunks = 0;                  // option: prepare in this many stream-overlapped chunks
+  int64_t fp_sub_bytes = 48ll << 30;  // option: FPVec per-sub-batch scratch budget (bytes)
                                    // (0 = auto: one chunk per 128Ki reports)
   std::vector<hipStream_t> side;   // side streams for chunked prepare
   std::vector<hipEvent_t> side_ev;

@@ -50,7 +50,7 @@ __global__ __launch_bounds__(256, XOFD_OCC) void k_xof(DevParams p, InPtrs in, S
   const bool JR = p.jr_len > 0;
   if (JR) load16(hs + 32, kb);
 
-  // 1. query randomness: XOF(vk, dst(5), [PROOFS] || nonce), one element
+  // 1. query randomness: XOF(vk, dst(5), [PROOFS] || nonce), qr_len elements (<= 10)
   {
     KState s;
     kzero(s);
@@ -61,8 +61,8 @@ __global__ __launch_bounds__(256, XOFD_OCC) void k_xof(DevParams p, InPtrs in, S
     msg_byte(m, 25, 1);
     msg_bytes16(m, 26, nonce);
     msg_absorb_final(s, m, 42);
-    uint32_t w[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
-    put_elem<F>(p, sc.qr, 0, r, w, flag);
+    uint32_t q0 = 0, q1 = 0;
+    squeeze_block<F>(p, s, 0, p.qr_len, q0, q1, sc.qr, r, flag);
   }
 
   // 2. measurement share XOF(k_meas, dst(1), [1]) fused with the joint-rand part
@@ -744,8 +744,10 @@ __global__ __launch_bounds__(64) void k_xof_slow(DevParams p, InPtrs in, Scratch
   bx_absorb(x, 1);
   bx_absorb_w(x, nonce, 16);
   bx_finalize(x);
-  bx_next_elem<F>(x, w);
-  F::store(sc.qr, r, F::from_words(w));
+  for (uint32_t i = 0; i < p.qr_len; i++) {
+    bx_next_elem<F>(x, w);
+    F::store(sc.qr, (size_t)i * p.ld + r, F::from_words(w));
+  }
   // meas + jr part
   bx_init(x, p.dst[1], km);
   bx_absorb(x, 1);
@@ -2015,6 +2017,27 @@ static uint32_t next_pow2(uint32_t n) {
   return p;
 }
 
+// prio flp/gadgets.rs optimal_chunk_length: over calls = 2^k - 1, the chunk length minimising
+// the ParallelSum proof length 2 * chunk + 2 * ((1 + calls).next_power_of_two() - 1) + 1
+// (first minimum from the largest k, as min_by_key over the reversed range keeps)
+static uint32_t optimal_chunk_length(uint32_t m) {
+  if (m <= 1) return 1;
+  uint32_t max_log2 = 0;
+  while ((1u << max_log2) < m) max_log2++;
+  max_log2 += 1;
+  uint64_t best = UINT64_MAX;
+  uint32_t best_chunk = 1;
+  for (uint32_t l = max_log2; l >= 1; l--) {
+    const uint64_t calls = (1ull << l) - 1, chunk = (m + calls - 1) / calls;
+    const uint64_t cost = 2 * chunk + 2 * ((1ull << l) - 1) + 1;  // next_pow2(1 + calls) = 2^l
+    if (cost < best) {
+      best = cost;
+      best_chunk = (uint32_t)chunk;
+    }
+  }
+  return best_chunk;
+}
+
 static int fill_sizes(const prio3_params* pp, prio3_sizes_t* s, DevParams* dp) {
   if (!pp) return PRIO3_EINVAL;
   uint32_t proofs = pp->num_proofs ? pp->num_proofs : 1;
@@ -2069,6 +2092,21 @@ static int fill_sizes(const prio3_params* pp, prio3_sizes_t* s, DevParams* dp) {
       d.arity = 2 * pp->chunk_length;
       d.calls = (d.meas_len + pp->chunk_length - 1) / pp->chunk_length;
       break;
+    case PRIO3_FPVEC_BOUNDED_L2:  // Prio3FixedPointBoundedL2VecSum (vdaf.rs:292-335)
+      if ((pp->bits != 16 && pp->bits != 32) || pp->length == 0 || pp->length > (1u << 22))
+        return PRIO3_EINVAL;
+      algo = 0xFFFF0000u;
+      d.es = 16;
+      d.meas_len = pp->bits * pp->length + 2 * pp->bits - 2;
+      d.out_len = pp->length;
+      d.jr_len = 2;
+      d.qr_len = 2;
+      d.chunk = optimal_chunk_length(d.meas_len);
+      d.arity = 2 * d.chunk;
+      d.calls = (d.meas_len + d.chunk - 1) / d.chunk;
+      d.chunk1 = optimal_chunk_length(pp->length);
+      d.calls1 = (pp->length + d.chunk1 - 1) / d.chunk1;
+      break;
     case PRIO3_HISTOGRAM:
       if (pp->length == 0 || pp->chunk_length == 0) return PRIO3_EINVAL;
       algo = 3;
@@ -2089,6 +2127,15 @@ static int fill_sizes(const prio3_params* pp, prio3_sizes_t* s, DevParams* dp) {
   d.glen = 2 * (d.P - 1) + 1;
   d.proof_len = d.arity + d.glen;
   d.verifier_len = d.arity + 2;
+  if (!d.qr_len) d.qr_len = 1;
+  if (d.kind == PRIO3_FPVEC_BOUNDED_L2) {  // second gadget: seeds1 || coeffs1 follow
+    d.P1 = next_pow2(1 + d.calls1);
+    while ((1u << d.logP1) < d.P1) d.logP1++;
+    if (d.logP1 > MAX_ROOTS) return PRIO3_EUNSUPPORTED;
+    d.glen1 = 2 * (d.P1 - 1) + 1;
+    d.proof_len += d.chunk1 + d.glen1;
+    d.verifier_len = 1 + d.arity + 1 + d.chunk1 + 1;
+  }
   const uint32_t S = mp ? 32 : 16;  // seed size
   d.helper_share_len = d.jr_len ? 3 * S : 2 * S;
   d.public_share_len = d.jr_len ? 2 * S : 0;
@@ -2119,6 +2166,17 @@ static int fill_sizes(const prio3_params* pp, prio3_sizes_t* s, DevParams* dp) {
       d.half128[k] = (uint32_t)(h >> (32 * k));
     }
     d.invP64 = (uint64_t)hpow(d.P, HP64 - 2, HP64);
+    if (d.kind == PRIO3_FPVEC_BOUNDED_L2) {
+      const u128 ip1 = hpow(d.P1, HP128 - 2, HP128);
+      // entries * 2^(2n-2) / num_shares (2): < 2^22 * 2^62 / 2 < p
+      const u128 nc = ((u128)d.out_len << (2 * d.bits - 2)) >> 1;
+      const u128 tn = (u128)1 << d.bits;
+      for (int k = 0; k < 4; k++) {
+        d.invP1_128[k] = (uint32_t)(ip1 >> (32 * k));
+        d.normc128[k] = (uint32_t)(nc >> (32 * k));
+        d.twon128[k] = (uint32_t)(tn >> (32 * k));
+      }
+    }
     if (d.P <= 32) {
       u128 alpha = 0;
       for (int k = 0; k < 4; k++) alpha |= (u128)d.roots128[d.logP][k] << (32 * k);
@@ -2170,9 +2228,17 @@ static int fill_sizes(const prio3_params* pp, prio3_sizes_t* s, DevParams* dp) {
 
 static int ensure_scratch(prio3_engine* e, uint32_t n) {
   if (n <= e->cap) return PRIO3_OK;
-  uint32_t ld = (n + 63) & ~63u;
+  const uint32_t ld_out = (n + 63) & ~63u;
+  uint32_t ld = ld_out;
   const DevParams& d = e->dp;
   size_t es = d.es;
+  const bool fp = d.kind == PRIO3_FPVEC_BOUNDED_L2;
+  if (fp) {  // per-report scratch for one sub-batch (2.56 MB of meas share per report at 10^4)
+    const size_t per = es * ((size_t)d.meas_len + d.proof_len + d.P + d.P1 + d.P + d.P1 + d.calls);
+    uint64_t cols = (uint64_t)std::max<int64_t>(e->fp_sub_bytes, 1) / per;
+    cols = std::max<uint64_t>(256, cols & ~255ull);
+    ld = (uint32_t)std::min<uint64_t>(ld_out, cols);
+  }
   void** bufs[] = {&e->sc.meas, &e->sc.proofs, &e->sc.jr, &e->sc.qr, (void**)&e->sc.part,
                    (void**)&e->sc.corrected, (void**)&e->sc.flag, &e->sc.Lbuf, &e->sc.PVbuf,
                    &e->sc.acc, &e->sc.out, &e->sc.beta, (void**)&e->d_mask};
@@ -2182,15 +2248,17 @@ static int ensure_scratch(prio3_engine* e, uint32_t n) {
       *b = nullptr;
     }
   size_t sizes[] = {es * d.meas_len * ld, es * d.proof_len * ld, es * (d.jr_len ? d.jr_len : 1) * ld,
-                    es * ld, 16 * (size_t)ld, 16 * (size_t)ld, (size_t)ld, es * d.P * ld,
-                    es * d.P * ld, es * d.arity * ld,
-                    (d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC || d.kind == PRIO3_SUMVEC_F64_MP)
-                        ? es * d.out_len * ld
+                    es * d.qr_len * ld, 16 * (size_t)ld, 16 * (size_t)ld, (size_t)ld,
+                    es * (d.P + d.P1) * ld, es * (d.P + d.P1) * ld, fp ? 16 : es * d.arity * ld,
+                    (d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC ||
+                     d.kind == PRIO3_SUMVEC_F64_MP || fp)
+                        ? es * d.out_len * ld_out
                         : 16,
-                    es * d.calls * ld, (size_t)ld};
+                    es * d.calls * ld, (size_t)ld_out};
   for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]); i++) HIPCHK(hipMalloc(bufs[i], sizes[i]));
-  e->cap = ld;
+  e->cap = ld_out;
   e->dp.ld = ld;
+  e->dp.ld_out = ld_out;
   return PRIO3_OK;
 }
 
@@ -2353,6 +2421,12 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
     e->chunks = (int)value;
     return PRIO3_OK;
   }
+  if (!strcmp(key, "fp_sub_bytes")) {  // FPVec scratch budget per sub-batch (next allocation)
+    if (value <= 0) return PRIO3_EINVAL;
+    e->fp_sub_bytes = value;
+    e->cap = 0;  // re-size on the next call
+    return PRIO3_OK;
+  }
   if (!strcmp(key, "leader_fast")) {
     e->leader_fast = (int)value;
     return PRIO3_OK;
@@ -2452,6 +2526,31 @@ static int launch_prepare(prio3_engine* e, uint32_t c0, uint32_t n, InPtrs in, O
     TIMED(e, st, "k_mp64_prepare", (rc = launch_mp64(e, n, in, out, sc, st)));
     return rc;
   }
+  if (dp.kind == PRIO3_FPVEC_BOUNDED_L2) {
+    // Sub-batches of dp.ld reports through the per-report scratch (the whole batch's meas
+    // shares would not fit: 2.56 MB per report at 10^4 entries); output shares keep one
+    // column per report of the batch (ld_out), so accumulate runs once over all of them.
+    const uint32_t sub = dp.ld;
+    for (uint32_t s0 = 0; s0 < n; s0 += sub) {
+      DevParams q = dp;
+      q.n = std::min(sub, n - s0);
+      InPtrs qi = in;
+      qi.nonces += 16 * (size_t)s0;
+      qi.pub += (size_t)dp.public_share_len * s0;
+      qi.helper += (size_t)dp.helper_share_len * s0;
+      qi.leader += (size_t)dp.prep_share_len * s0;
+      OutPtrs qo = out;
+      qo.prep_msgs += 16 * (size_t)s0;
+      qo.status += s0;
+      Scratch qs = sc;
+      qs.out = (uint8_t*)sc.out + es * s0;
+      const uint32_t qb = (q.n + 255) / 256, qb64 = (q.n + 63) / 64;
+      TIMED(e, st, "k_xof", (k_xof<Fp128><<<qb, 256, 0, st>>>(q, qi, qs)));
+      TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp128><<<qb64, 64, 0, st>>>(q, qi, qs)));
+      TIMED(e, st, "k_query_fp", launch_fpvec_query(q, qi, qs, qo, st));
+    }
+    return PRIO3_OK;
+  }
   if (dp.es == 16) {
     if (dp.jr_len && e->split_xof == 2 && (42 + dp.meas_len * 16) / 168 >= 2) {
       if (fuse)
@@ -2515,7 +2614,8 @@ static int prepare_impl(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
   const uint32_t K = e->chunks > 0 ? (uint32_t)e->chunks
                                    : std::max(1u, (n + (1u << 16)) >> 17);
   const uint32_t csz = ((n + K - 1) / K + 255) & ~255u;
-  if (K == 1 || n <= csz) return launch_prepare(e, 0, n, in, out, sc, st, fuse);
+  if (K == 1 || n <= csz || e->dp.kind == PRIO3_FPVEC_BOUNDED_L2)
+    return launch_prepare(e, 0, n, in, out, sc, st, fuse);
   while (e->side.size() < 2) {  // side streams + their join events, created once per engine
     hipStream_t s2;
     hipEvent_t j;
@@ -2641,7 +2741,8 @@ int prio3_device_accumulate(prio3_engine* e, uint32_t n, const uint8_t* d_status
     HIPCHK(hipMalloc((void**)&e->d_pcount, 8 * (size_t)nchunks));
     e->partial_cap = need;
   }
-  const void* src = (d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC || d.kind == PRIO3_SUMVEC_F64_MP)
+  const void* src = (d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC ||
+                     d.kind == PRIO3_SUMVEC_F64_MP || d.kind == PRIO3_FPVEC_BOUNDED_L2)
                         ? e->sc.out
                         : e->sc.meas;
   for (uint32_t s = 0; s < n_segments; s++) {
@@ -2651,7 +2752,7 @@ int prio3_device_accumulate(prio3_engine* e, uint32_t n, const uint8_t* d_status
     dim3 grid(d.out_len, nchunks);
     if (d.es == 16) {
       TIMED(e, st, "k_acc_partial",
-            (k_acc_partial<Fp128><<<grid, 256, 0, st>>>(n, d.ld, chunk, d.out_len, src, e->d_mask,
+            (k_acc_partial<Fp128><<<grid, 256, 0, st>>>(n, d.ld_out, chunk, d.out_len, src, e->d_mask,
                                                         e->d_prep_partial, e->d_pcount)));
       TIMED(e, st, "k_acc_final",
             (k_acc_final<Fp128><<<(d.out_len + 255) / 256, 256, 0, st>>>(
@@ -2659,7 +2760,7 @@ int prio3_device_accumulate(prio3_engine* e, uint32_t n, const uint8_t* d_status
                 d_counts + s)));
     } else {
       TIMED(e, st, "k_acc_partial",
-            (k_acc_partial<Fp64><<<grid, 256, 0, st>>>(n, d.ld, chunk, d.out_len, src, e->d_mask,
+            (k_acc_partial<Fp64><<<grid, 256, 0, st>>>(n, d.ld_out, chunk, d.out_len, src, e->d_mask,
                                                        e->d_prep_partial, e->d_pcount)));
       TIMED(e, st, "k_acc_final",
             (k_acc_final<Fp64><<<(d.out_len + 255) / 256, 256, 0, st>>>(
@@ -2786,15 +2887,16 @@ int prio3_device_output_shares(prio3_engine* e, uint32_t n, uint8_t* out) {
   HIPCHK(hipStreamSynchronize(e->stream));
   HIPCHK(hipDeviceSynchronize());
   const DevParams& d = e->dp;
-  const void* src = (d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC || d.kind == PRIO3_SUMVEC_F64_MP)
+  const void* src = (d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC ||
+                     d.kind == PRIO3_SUMVEC_F64_MP || d.kind == PRIO3_FPVEC_BOUNDED_L2)
                         ? e->sc.out
                         : e->sc.meas;
-  std::vector<uint8_t> soa((size_t)d.out_len * d.ld * d.es);
+  std::vector<uint8_t> soa((size_t)d.out_len * d.ld_out * d.es);
   HIPCHK(hipMemcpy(soa.data(), src, soa.size(), hipMemcpyDeviceToHost));
   for (uint32_t r = 0; r < n; r++)
     for (uint32_t i = 0; i < d.out_len; i++)
-      memcpy(out + ((size_t)r * d.out_len + i) * d.es, soa.data() + ((size_t)i * d.ld + r) * d.es,
-             d.es);
+      memcpy(out + ((size_t)r * d.out_len + i) * d.es,
+             soa.data() + ((size_t)i * d.ld_out + r) * d.es, d.es);
   return PRIO3_OK;
 }
 
@@ -2951,7 +3053,8 @@ int prio3_device_leader_prepare_init(prio3_engine* e, uint32_t n, const uint8_t*
                                      const uint8_t* d_public_shares,
                                      const uint8_t* d_leader_input_shares, uint8_t* d_prep_shares,
                                      uint8_t* d_status, void* stream) {
-  if (e && e->dp.kind == PRIO3_SUMVEC_F64_MP) return PRIO3_EUNSUPPORTED;  // helper role only
+  if (e && (e->dp.kind == PRIO3_SUMVEC_F64_MP || e->dp.kind == PRIO3_FPVEC_BOUNDED_L2))
+    return PRIO3_EUNSUPPORTED;  // helper role only
   if (!e) return PRIO3_EINVAL;
   if (n == 0) return PRIO3_OK;
   if (!d_nonces || !d_leader_input_shares || !d_prep_shares || !d_status ||
@@ -2997,7 +3100,8 @@ int prio3_device_leader_prepare_init(prio3_engine* e, uint32_t n, const uint8_t*
 
 int prio3_device_leader_prepare_next(prio3_engine* e, uint32_t n, const uint8_t* d_prep_msgs,
                                      uint8_t* d_status, void* stream) {
-  if (e && e->dp.kind == PRIO3_SUMVEC_F64_MP) return PRIO3_EUNSUPPORTED;  // helper role only
+  if (e && (e->dp.kind == PRIO3_SUMVEC_F64_MP || e->dp.kind == PRIO3_FPVEC_BOUNDED_L2))
+    return PRIO3_EUNSUPPORTED;  // helper role only
   if (!e || n > e->cap) return PRIO3_EINVAL;
   if (n == 0) return PRIO3_OK;
   if (!d_status || (e->dp.jr_len && !d_prep_msgs)) return PRIO3_EINVAL;
@@ -3015,7 +3119,8 @@ int prio3_leader_prepare_init_batch(prio3_engine* e, uint32_t n, const uint8_t* 
                                     const uint8_t* public_shares,
                                     const uint8_t* leader_input_shares, uint8_t* prep_shares_out,
                                     uint8_t* status_out, prio3_batch** batch_out) {
-  if (e && e->dp.kind == PRIO3_SUMVEC_F64_MP) return PRIO3_EUNSUPPORTED;  // helper role only
+  if (e && (e->dp.kind == PRIO3_SUMVEC_F64_MP || e->dp.kind == PRIO3_FPVEC_BOUNDED_L2))
+    return PRIO3_EUNSUPPORTED;  // helper role only
   if (!e || (n && (!nonces || !leader_input_shares || !prep_shares_out || !status_out)))
     return PRIO3_EINVAL;
   const DevParams& d = e->dp;

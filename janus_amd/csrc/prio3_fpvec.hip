@@ -1,0 +1,226 @@
+// prio3_fpvec.hip -- helper FLP query + decide + prepare message + prepare_next + truncate for
+// Prio3FixedPointBoundedL2VecSum (Janus VdafInstance::Prio3FixedPointBoundedL2VecSum,
+// /root/reference/core/src/vdaf.rs:292-335; config C5 of BASELINE.json), MI355X (gfx950).
+//
+// The XOF half of prepare_init (measurement / proofs share expansion, joint-rand part over the
+// 2.56 MB measurement share, corrected seed, joint randomness, two query-randomness elements)
+// is the engine's generic k_xof; this file is the two-gadget query that follows it.  The
+// circuit is the reconstruction fixed in oracle/fpvec_py.py:
+//   gadget 0 = ParallelSum(Mul, C0): range checks of every bit (SumVec's construction, r0);
+//   gadget 1 = ParallelSum(PolyEval(y^2 - 2^n y), C1) over the decoded entries y_e;
+//   v = r1 * range + r1^2 * (sum gadget-1 outputs + entries 2^(2n-2)/2 - claimed norm).
+// One report per lane, SoA scratch [element][report] (sub-batch leading dimension p.ld);
+// output shares (the decoded entries) go to sc.out with leading dimension p.ld_out.
+//
+// Per report (10^4 entries, n = 16): the measurement share (160,030 elements) is read twice --
+// once by the gadget-0 sweep (2 Field128 multiplies per element) and once by the entry decode
+// of the gadget-1 sweep (doublings only) -- and 10^4 output elements are written.
+#include <hip/hip_runtime.h>
+
+#include "../../include/janus_prio3.h"
+#include "prio3_device.h"
+#include "prio3_common.h"
+
+namespace {
+
+typedef Fp128 F;
+typedef f128 T;
+
+// Lagrange basis on the P-th roots at t (scaled DFT of t^e / P, reversed as in k_query_ps) into
+// rows [0, P) of L, and the gadget polynomial's values at the P-th roots into rows [0, P) of PV.
+DEV void basis_and_roots(const DevParams& p, uint8_t* L, uint8_t* PV, const void* proofs,
+                         uint32_t coeff_off, uint32_t glen, uint32_t P, uint32_t logP, T invP,
+                         T t, uint32_t r) {
+  const size_t ld = p.ld;
+  T pw = invP;
+  for (uint32_t e = 0; e < P; e++) {
+    F::store(L, (size_t)bitrev(e, logP) * ld + r, pw);
+    pw = F::mul(pw, t);
+  }
+  dft_lane<F>(p, L, r, P, logP);
+  for (uint32_t e = 0; e < P; e++) {
+    T q = ldf<F>(proofs, coeff_off + e, ld, r);
+    for (uint32_t e2 = e + P; e2 < glen; e2 += P) q = F::add(q, ldf<F>(proofs, coeff_off + e2, ld, r));
+    F::store(PV, (size_t)bitrev(e, logP) * ld + r, q);
+  }
+  dft_lane<F>(p, PV, r, P, logP);
+}
+
+DEV T horner(const void* proofs, uint32_t off, uint32_t len, T t, size_t ld, uint32_t r) {
+  T acc = F::zero();
+  for (uint32_t e = len; e-- > 0;) acc = F::add(F::mul(acc, t), ldf<F>(proofs, off + e, ld, r));
+  return acc;
+}
+
+DEV bool root_of_unity(T t, uint32_t logP) {
+  for (uint32_t l = 0; l < logP; l++) t = F::mul(t, t);
+  return F::eq(t, F::one());
+}
+
+// y = sum_b 2^b m[base + b] (Field128::decode_bitvector), Horner from the top bit
+DEV T decode_bits(const void* meas, uint32_t base, uint32_t nbits, size_t ld, uint32_t r) {
+  T y = F::zero();
+  for (uint32_t b = nbits; b-- > 0;) y = F::add(F::add(y, y), ldf<F>(meas, base + b, ld, r));
+  return y;
+}
+
+template <int GS>
+__global__ __launch_bounds__(256) void k_query_fp(DevParams p, InPtrs in, Scratch sc, OutPtrs out) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= p.n) return;
+  const size_t ld = p.ld;
+  const uint32_t P0 = p.P, A0 = p.arity, C0 = p.chunk, M = p.meas_len, K0 = p.calls;
+  const uint32_t P1 = p.P1, C1 = p.chunk1, K1 = p.calls1, E = p.out_len, nb = p.bits;
+  const uint32_t off1 = A0 + p.glen;  // proof: seeds0 | coeffs0 | seeds1 | coeffs1
+  uint8_t status = PRIO3_STATUS_FINISHED;
+  const T t0 = ldf<F>(sc.qr, 0, ld, r), t1 = ldf<F>(sc.qr, 1, ld, r);
+  if (root_of_unity(t0, p.logP) || root_of_unity(t1, p.logP1)) status = PRIO3_STATUS_PREP_INIT;
+  uint8_t* L = (uint8_t*)sc.Lbuf;
+  uint8_t* PV = (uint8_t*)sc.PVbuf;
+  uint8_t* L1 = L + (size_t)F::ES * P0 * ld;
+  uint8_t* PV1 = PV + (size_t)F::ES * P0 * ld;
+  basis_and_roots(p, L, PV, sc.proofs, A0, p.glen, P0, p.logP, FC<F>::invP(p), t0, r);
+  basis_and_roots(p, L1, PV1, sc.proofs, off1 + C1, p.glen1, P1, p.logP1,
+                  F::from_words(p.invP1_128), t1, r);
+  auto Lc0 = [&](uint32_t c) { return ldf<F>(L, (P0 - c) & (P0 - 1), ld, r); };
+  auto Lc1 = [&](uint32_t c) { return ldf<F>(L1, (P1 - c) & (P1 - 1), ld, r); };
+  const T p0t = horner(sc.proofs, A0, p.glen, t0, ld, r);
+  const T p1t = horner(sc.proofs, off1 + C1, p.glen1, t1, ld, r);
+
+  // gadget 0: range checks (k_query_ps's sweep): beta_k = L_(k+1)(t0) r0^(C0 k)
+  const T r0 = ldf<F>(sc.jr, 0, ld, r), r1 = ldf<F>(sc.jr, 1, ld, r);
+  T rC = F::one();
+  for (uint32_t j = 0; j < C0; j++) rC = F::mul(rC, r0);
+  T sumL = F::zero(), range = F::zero(), normg = F::zero();
+  {
+    T rk = F::one();
+    for (uint32_t k = 0; k < K0; k++) {
+      const T Lk = Lc0(k + 1);
+      sumL = F::add(sumL, Lk);
+      range = F::add(range, ldf<F>(PV, k + 1, ld, r));
+      F::store(sc.beta, (size_t)k * ld + r, F::mul(Lk, rk));
+      rk = F::mul(rk, rC);
+    }
+    for (uint32_t k = 0; k < K1; k++) normg = F::add(normg, ldf<F>(PV1, k + 1, ld, r));
+  }
+  const T L00 = Lc0(0), L10 = Lc1(0);
+  const T halfL = F::mul(FC<F>::half(p), sumL);
+  const uint8_t* lps = in.leader + (size_t)r * p.prep_share_len;
+  bool decode_ok = true;
+  auto lv = [&](uint32_t e) {
+    T x = F::load(lps, e);
+    if (!F::lt_p(x)) decode_ok = false;
+    return x;
+  };
+  const T Z = F::zero();
+  T G0 = F::zero(), rj = r0;
+  for (uint32_t jg = 0; jg < C0; jg += GS) {
+    T Aa[GS], Bb[GS];
+#pragma unroll
+    for (int q = 0; q < GS; q++) Aa[q] = Bb[q] = Z;
+#pragma unroll 1
+    for (uint32_t k = 0; k < K0; k++) {
+      const T be = ldf<F>(sc.beta, k, ld, r);
+      const T Lk = Lc0(k + 1);
+      const uint32_t base = k * C0 + jg;
+#pragma unroll
+      for (int q = 0; q < GS; q++) {
+        const uint32_t i = base + q;
+        const bool valid = (jg + q < C0) && (i < M);
+        const T m = F::sel(valid, ldf<F>(sc.meas, valid ? i : 0, ld, r), Z);
+        Aa[q] = F::add(Aa[q], F::mul(be, m));
+        Bb[q] = F::add(Bb[q], F::mul(Lk, m));
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < GS; q++) {
+      const uint32_t j = jg + q;
+      const bool valid = j < C0;
+      const uint32_t jj = valid ? j : 0;
+      const T f0 = F::add(F::mul(ldf<F>(sc.proofs, 2 * jj, ld, r), L00), F::mul(rj, Aa[q]));
+      const T f1 = F::sub(F::add(F::mul(ldf<F>(sc.proofs, 2 * jj + 1, ld, r), L00), Bb[q]), halfL);
+      const T prod = F::mul(F::add(lv(1 + 2 * jj), f0), F::add(lv(2 + 2 * jj), f1));
+      G0 = F::add(G0, F::sel(valid, prod, Z));
+      rj = F::sel(valid, F::mul(rj, r0), rj);
+    }
+  }
+
+  // gadget 1: wires are the decoded entries y_(k C1 + j) (zero padded); each entry is decoded
+  // once here and written as the output share (truncate)
+  const T twon = F::from_words(p.twon128);
+  T G1 = F::zero();
+  for (uint32_t jg = 0; jg < C1; jg += GS) {
+    T Ac[GS];
+#pragma unroll
+    for (int q = 0; q < GS; q++) Ac[q] = Z;
+#pragma unroll 1
+    for (uint32_t k = 0; k < K1; k++) {
+      const T Lk = Lc1(k + 1);
+#pragma unroll
+      for (int q = 0; q < GS; q++) {
+        const uint32_t idx = k * C1 + jg + q;
+        if (jg + q < C1 && idx < E) {
+          const T y = decode_bits(sc.meas, nb * idx, nb, ld, r);
+          F::store(sc.out, (size_t)idx * p.ld_out + r, y);
+          Ac[q] = F::add(Ac[q], F::mul(Lk, y));
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < GS; q++) {
+      const uint32_t j = jg + q;
+      const bool valid = j < C1;
+      const uint32_t jj = valid ? j : 0;
+      const T f = F::add(F::mul(ldf<F>(sc.proofs, off1 + jj, ld, r), L10), Ac[q]);
+      const T a = F::add(lv(2 + A0 + jj), f);
+      const T qa = F::sub(F::mul(a, a), F::mul(twon, a));
+      G1 = F::add(G1, F::sel(valid, qa, Z));
+    }
+  }
+  const T claimed = decode_bits(sc.meas, nb * E, 2 * nb - 2, ld, r);
+  const T normd = F::sub(F::add(normg, F::from_words(p.normc128)), claimed);
+  const T v = F::add(F::mul(r1, range), F::mul(F::mul(r1, r1), normd));
+
+  const T V0 = F::add(lv(0), v);
+  const T PT0 = F::add(lv(1 + A0), p0t);
+  const T PT1 = F::add(lv(2 + A0 + C1), p1t);
+  if (status == PRIO3_STATUS_FINISHED) {
+    if (!decode_ok)
+      status = PRIO3_STATUS_PREP_SHARE_DECODE;
+    else if (!F::is_zero(V0) || !F::eq(G0, PT0) || !F::eq(G1, PT1))
+      status = PRIO3_STATUS_PREP_MSG;
+  }
+  // prepare message = joint-rand seed of (leader part, helper part); prepare_next checks it
+  // against the corrected seed
+  uint32_t lpart[4], hpart[4];
+  load16(lps + (size_t)p.verifier_len * F::ES, lpart);
+  {
+    const uint4 hp = sc.part[r];
+    hpart[0] = hp.x;
+    hpart[1] = hp.y;
+    hpart[2] = hp.z;
+    hpart[3] = hp.w;
+  }
+  KState s;
+  kzero(s);
+  Msg mm;
+  msg_zero(mm);
+  msg_dst(mm, p.dst[6]);
+  msg_bytes16(mm, 25, lpart);
+  msg_bytes16(mm, 41, hpart);
+  msg_absorb_final(s, mm, 57);
+  const uint4 cor = sc.corrected[r];
+  uint32_t msg[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
+  if (status == PRIO3_STATUS_FINISHED &&
+      (msg[0] != cor.x || msg[1] != cor.y || msg[2] != cor.z || msg[3] != cor.w))
+    status = PRIO3_STATUS_PREP_NEXT;
+  if (status != PRIO3_STATUS_FINISHED) msg[0] = msg[1] = msg[2] = msg[3] = 0;
+  ((uint4*)out.prep_msgs)[r] = make_uint4(msg[0], msg[1], msg[2], msg[3]);
+  out.status[r] = status;
+}
+
+}  // namespace
+
+void launch_fpvec_query(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st) {
+  k_query_fp<4><<<(p.n + 255) / 256, 256, 0, st>>>(p, in, sc, out);
+}

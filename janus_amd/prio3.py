@@ -28,6 +28,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("JANUS_PRIO3_LIB") or os.path.join(_HERE, "libjanus_prio3.so")
 
 PRIO3_COUNT, PRIO3_SUM, PRIO3_SUMVEC, PRIO3_HISTOGRAM, PRIO3_SUMVEC_F64_MP = 0, 1, 2, 3, 4
+PRIO3_FPVEC_BOUNDED_L2 = 5
 
 STATUS_FINISHED = 0
 STATUS_PREP_INIT = 1
@@ -204,6 +205,15 @@ def Prio3SumVecField64MultiproofHmacSha256Aes128(proofs: int, bits: int, length:
 
 def Prio3Histogram(length: int, chunk_length: int) -> Prio3:
     return Prio3(PRIO3_HISTOGRAM, length=length, chunk_length=chunk_length)
+
+
+def Prio3FixedPointBoundedL2VecSum(length: int, bitsize: int = 16) -> Prio3:
+    """Prio3::new_fixedpoint_boundedl2_vec_sum_multithreaded(2, length) with FixedI16<U15>
+    (bitsize 16) or FixedI32<U31> (bitsize 32) (core/src/vdaf.rs:292-335).  Helper role; the
+    circuit is the reconstruction in oracle/fpvec_py.py."""
+    if bitsize not in (16, 32):
+        raise ValueError("bitsize must be 16 or 32 (Prio3FixedPointBoundedL2VecSumBitSize)")
+    return Prio3(PRIO3_FPVEC_BOUNDED_L2, bits=bitsize, length=length)
 
 
 def _np_ptr(a: Optional[np.ndarray]):

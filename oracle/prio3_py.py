@@ -503,7 +503,7 @@ class Prio3:
 
     def query_rands(self, vk, nonce):
         return expand_into_vec(self.F, vk, self.dst("query"), bytes([self.np]) + nonce,
-                               1 * self.np, self.t.xof)
+                               getattr(self.t, "qr_len", 1) * self.np, self.t.xof)
 
     def shard(self, measurement, nonce: bytes, rand: bytes):
         t, F = self.t, self.F
@@ -557,10 +557,11 @@ class Prio3:
             corrected = self.jr_seed(parts)
             jr = self.joint_rands(corrected)
         qr = self.query_rands(vk, nonce)
+        ql = getattr(t, "qr_len", 1)
         verifiers = []
         for k in range(self.np):
             verifiers += t.query(meas, proofs[k * t.proof_len:(k + 1) * t.proof_len],
-                                 qr[k:k + 1], jr[k * t.jr_len:(k + 1) * t.jr_len])
+                                 qr[k * ql:(k + 1) * ql], jr[k * t.jr_len:(k + 1) * t.jr_len])
         ps = b"".join(F.enc(x) for x in verifiers) + part
         trace = dict(meas=meas, proofs=proofs, part=part, corrected=corrected, jr=jr, qr=qr,
                      verifiers=verifiers)

@@ -1,0 +1,244 @@
+"""Prio3FixedPointBoundedL2VecSum (BASELINE.json config C5; SURVEY 8(a) rows a3-a8 for the
+FixedPoint L2 circuit; core/src/vdaf.rs:292-335).
+
+prio's fixedpoint_l2.rs is not in the reference and SURVEY A.11(3) records its circuit as
+approximate, so the circuit is the reconstruction documented in oracle/fpvec_py.py: parity with
+prio is UNPINNED and the GPU is pinned to that restatement.
+
+CPU: the restatement is internally consistent -- shard, both aggregators' prepare, decide,
+unshard == the sum of the encoded entries; a vector of norm >= 1 cannot be encoded; a client
+that claims a wrong norm, a non-bit entry bit, or a tampered share is rejected -- and the C
+engine's sizes (prio3_sizes, host code) equal the restatement's.  GPU: k_xof + k_query_fp are
+bit-exact against the restatement (prepare messages, statuses, output shares, aggregate), with
+tampered reports, across sub-batches of the per-report scratch."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import prio3_py as P
+from oracle.fpvec_py import FpVecType, optimal_chunk_length
+
+VK = bytes(range(0x20, 0x30))
+
+
+def _vdaf(length, bits=16):
+    return P.Prio3(FpVecType(length, bits))
+
+
+def _vector(rng, length, bits):
+    """Random raw fixed-point entries with ||x||^2 < 1 (x_i = X_i / 2^(bits-1))."""
+    half = 1 << (bits - 1)
+    lim = max(1, int(half / np.sqrt(length)) - 1)
+    return [int(x) for x in rng.integers(-lim, lim, length)]
+
+
+def _prep_all(v, xs, nonce, rand):
+    pub, leader, helper = v.shard(xs, nonce, rand)
+    st0, lps, _ = v.prepare_init(VK, 0, nonce, pub, leader)
+    st1, hps, _ = v.prepare_init(VK, 1, nonce, pub, helper)
+    return pub, leader, helper, st0, lps, st1, hps
+
+
+def test_optimal_chunk_length_known_values():
+    # optimal_chunk_length(8000) = 63 (SumVec 8x1000); A.10 C5: ~314 / ~79
+    assert optimal_chunk_length(8000) == 63
+    assert optimal_chunk_length(160030) == 314
+    assert optimal_chunk_length(10000) == 79
+    assert optimal_chunk_length(1) == 1
+
+
+@pytest.mark.parametrize("length,bits", [(1, 16), (7, 16), (10000, 16), (3, 32), (1000, 32)])
+def test_engine_sizes_match_restatement(length, bits):
+    from janus_amd import prio3 as J
+    t = FpVecType(length, bits)
+    sz = J.Prio3FixedPointBoundedL2VecSum(length, bits).sizes()
+    assert (sz.field_bytes, sz.meas_len, sz.out_len, sz.proof_len, sz.verifier_len,
+            sz.joint_rand_len) == (16, t.meas_len, t.out_len, t.proof_len, t.verifier_len, 2)
+    assert sz.prep_share_len == 16 * t.verifier_len + 16
+    assert sz.helper_share_len == 48 and sz.public_share_len == 32 and sz.prep_msg_len == 16
+    assert sz.leader_input_share_len == 16 * (t.meas_len + t.proof_len) + 16
+
+
+def test_engine_rejects_bad_bitsize():
+    from janus_amd import prio3 as J
+    with pytest.raises(ValueError):
+        J.Prio3FixedPointBoundedL2VecSum(4, 8)
+    with pytest.raises(ValueError):
+        J.Prio3(J.PRIO3_FPVEC_BOUNDED_L2, bits=64, length=4).sizes()
+
+
+@pytest.mark.parametrize("length,bits", [(1, 16), (5, 16), (3, 32), (24, 16)])
+def test_oracle_unshard_equals_sum(length, bits):
+    v = _vdaf(length, bits)
+    rng = np.random.default_rng(length * bits)
+    half = 1 << (bits - 1)
+    agg = [[0] * length, [0] * length]
+    xs_all = []
+    for _ in range(4):
+        xs = _vector(rng, length, bits)
+        xs_all.append(xs)
+        _, _, _, st0, lps, st1, hps = _prep_all(v, xs, os.urandom(16), os.urandom(80))
+        msg = v.prep_shares_to_prep_msg(lps, hps)
+        for i, st in enumerate((st0, st1)):
+            agg[i] = [(a + b) % P.Field128.p for a, b in zip(agg[i], v.prepare_next(st, msg))]
+    tot = v.unshard(agg)
+    assert tot == [sum(x[e] + half for x in xs_all) for e in range(length)]
+    assert v.t.decode_result(tot, 4) == [sum(x[e] for x in xs_all) / half for e in range(length)]
+
+
+def test_oracle_norm_bound():
+    t = FpVecType(2, 16)
+    t.encode([23170, 23170])  # 2 * 23170^2 < 2^30
+    with pytest.raises(ValueError):
+        t.encode([23171, 23171])
+
+
+def test_oracle_rejects_dishonest_clients():
+    v = _vdaf(4)
+    t = v.t
+    xs = [1000, -2000, 300, 0]
+    good = t.encode(xs)
+    nb = t.bits * t.length
+    cases = []
+    wrong_norm = list(good)
+    wrong_norm[nb + 3] ^= 1  # claims another norm (still a bit vector)
+    cases.append(wrong_norm)
+    not_bit = list(good)
+    not_bit[5] = 2  # an entry "bit" of 2
+    cases.append(not_bit)
+    orig = t.encode
+    try:
+        for meas in cases:
+            t.encode = lambda _m, meas=meas: meas
+            nonce = os.urandom(16)
+            _, _, _, _, lps, _, hps = _prep_all(v, xs, nonce, os.urandom(80))
+            with pytest.raises(ValueError):
+                v.prep_shares_to_prep_msg(lps, hps)
+    finally:
+        t.encode = orig
+    # an honest report passes; a tampered wire value of either gadget fails
+    _, _, _, _, lps, _, hps = _prep_all(v, xs, os.urandom(16), os.urandom(80))
+    v.prep_shares_to_prep_msg(lps, hps)
+    for e in (1, 1 + t.A0 + 1):
+        bad = bytearray(lps)
+        bad[16 * e] ^= 1
+        with pytest.raises(ValueError):
+            v.prep_shares_to_prep_msg(bytes(bad), hps)
+
+
+# ------------------------------------------------------------------------------------
+# GPU
+# ------------------------------------------------------------------------------------
+def _reports(v, n, seed, distinct=None):
+    rng = np.random.default_rng(seed)
+    t = v.t
+    out = []
+    for i in range(n):
+        if distinct and i >= distinct:  # tile the first `distinct` reports
+            out.append(dict(out[i % distinct], lps=bytearray(out[i % distinct]["lps"])))
+            continue
+        xs = _vector(rng, t.length, t.bits)
+        nonce = bytes(rng.integers(0, 256, 16, dtype=np.uint8))
+        rand = bytes(rng.integers(0, 256, 80, dtype=np.uint8))
+        pub, leader, helper = v.shard(xs, nonce, rand)
+        _, lps, _ = v.prepare_init(VK, 0, nonce, pub, leader)
+        out.append(dict(nonce=nonce, pub=pub, helper=helper, lps=bytearray(lps)))
+    return out
+
+
+def _expected(v, reps):
+    msgs, status, outs = [], [], []
+    cache = {}
+    for r in reps:
+        key = (r["nonce"], r["helper"])
+        if key not in cache:
+            cache[key] = v.prepare_init(VK, 1, r["nonce"], r["pub"], r["helper"])
+        st1, hps, _ = cache[key]
+        try:
+            msg = v.prep_shares_to_prep_msg(bytes(r["lps"]), hps)
+        except ValueError as e:
+            code = 2 if "range" in str(e) else 3
+            msgs.append(bytes(16)), status.append(code), outs.append(None)
+            continue
+        try:
+            out = v.prepare_next(st1, msg)
+        except ValueError:
+            msgs.append(bytes(16)), status.append(4), outs.append(None)
+            continue
+        msgs.append(msg), status.append(0), outs.append(out)
+    return msgs, status, outs
+
+
+def _tamper(v, reps, frac, seed):
+    rng = np.random.default_rng(seed)
+    n, nv = len(reps), v.t.verifier_len
+    for i in rng.choice(n, max(1, int(n * frac)), replace=False):
+        kind = int(rng.integers(0, 4))
+        if kind == 0:
+            reps[i]["lps"][16 * int(rng.integers(0, nv))] ^= 1         # a verifier value
+        elif kind == 1:
+            reps[i]["lps"][16 * nv + 5] ^= 0x40                         # leader joint-rand part
+        elif kind == 2:
+            reps[i]["lps"][16 * int(rng.integers(0, nv)) + 15] = 0xff   # out of range: decode
+        else:
+            reps[i]["lps"][16 * (2 + v.t.A0)] ^= 2                      # a gadget-1 wire
+
+
+def _run(v, reps, sub_bytes=None):
+    from janus_amd import prio3 as J
+    t = v.t
+    eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(t.length, t.bits), VK)
+    if sub_bytes:
+        eng.set_option("fp_sub_bytes", sub_bytes)
+    A = lambda k: np.array([list(r[k]) for r in reps], np.uint8)
+    msgs, status, batch = eng.prepare_batch(A("nonce"), A("pub"), A("helper"), A("lps"))
+    outs = batch.output_shares()
+    agg, cnt = batch.accumulate()
+    return msgs, status, outs, agg, cnt
+
+
+def _check(v, reps, got):
+    msgs, status, outs, agg, cnt = got
+    exp_msgs, exp_st, exp_out = _expected(v, reps)
+    assert status.tolist() == exp_st
+    np.testing.assert_array_equal(msgs, np.array([list(m) for m in exp_msgs], np.uint8))
+    L = v.t.length
+    tot = [0] * L
+    for i, o in enumerate(exp_out):
+        if o is None:
+            continue
+        row = outs[i].reshape(L, 16)
+        assert [int.from_bytes(row[e].tobytes(), "little") for e in range(L)] == o
+        tot = [(a + b) % P.Field128.p for a, b in zip(tot, o)]
+    got_agg = [int.from_bytes(agg[0, 16 * e:16 * e + 16].tobytes(), "little") for e in range(L)]
+    assert got_agg == tot and int(cnt[0]) == sum(1 for s in exp_st if s == 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("length,bits,n", [(1, 16, 40), (5, 16, 70), (3, 32, 33), (24, 16, 65)])
+def test_gpu_fpvec_matches_oracle(length, bits, n):
+    v = _vdaf(length, bits)
+    reps = _reports(v, n, seed=length * 7 + bits)
+    _tamper(v, reps, 0.25, seed=length)
+    _check(v, reps, _run(v, reps))
+
+
+@pytest.mark.gpu
+def test_gpu_fpvec_sub_batches():
+    """A per-report scratch budget of one 256-report column block forces 3 sub-batches; the
+    output shares of every sub-batch land in their own columns and the aggregate covers all."""
+    v = _vdaf(6)
+    reps = _reports(v, 600, seed=11, distinct=150)
+    _tamper(v, reps, 0.05, seed=3)
+    _check(v, reps, _run(v, reps, sub_bytes=1))
+
+
+@pytest.mark.gpu
+def test_gpu_fpvec_1000_entries():
+    """1000 entries (MEAS_LEN 16,030; gadget 0: C0 127, P0 128; gadget 1: C1 33, P1 32): 3
+    distinct reports tiled to 130 lanes."""
+    v = _vdaf(1000)
+    reps = _reports(v, 130, seed=5, distinct=3)
+    reps[1]["lps"][16 * 7] ^= 1
+    _check(v, reps, _run(v, reps))
