@@ -92,7 +92,7 @@ def main():
     ap.add_argument("--reports", type=int, default=1 << 20, help="reports per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--role", choices=["helper", "leader", "hpke", "pipeline", "mp64"],
+    ap.add_argument("--role", choices=["helper", "leader", "hpke", "pipeline", "mp64", "fpvec"],
                     default="helper",
                     help="helper (the BASELINE metric), the leader side (SURVEY 8(f) row 1) or "
                          "the batched HPKE open of helper input shares (8(f) row 2)")
@@ -107,6 +107,8 @@ def main():
         return pipeline_main(args)
     if args.role == "mp64":
         return mp64_main(args)
+    if args.role == "fpvec":
+        return fpvec_main(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -600,6 +602,92 @@ def mp64_main(args):
                         for k, v in times.items()},
                checks=dict(finished=int((status == 0).sum().item()), agg_count=int(cnt[0])),
                cpu_baseline=None)
+    print(json.dumps(out), flush=True)
+
+def fpvec_main(args):
+    """Prio3FixedPointBoundedL2VecSum(length=10000, BitSize16) helper prepare+aggregate line
+    (BASELINE.json configs[4], C5: 100k reports; not the headline metric).  Inputs are the two
+    honest full-size reports of tests/golden/fpvec_l10000.npz (Python restatement,
+    tests/golden/gen_fpvec_l10000.py; ~35 s of CPU per report to generate) tiled to --reports
+    (default here 100k) and resident in HBM.  One step = prepare (k_xof, k_xof_slow, k_query_fp
+    per scratch sub-batch) + masked mod-p accumulate of the 10000-entry output shares.
+    cpu_baseline: the same restatement (pure Python, one core) on one report."""
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    g = np.load(os.path.join(ROOT, "tests", "golden", "fpvec_l10000.npz"))
+    vk = bytes(g["verify_key"])
+    n = args.reports if args.reports != 1 << 20 else 100_000
+    honest = np.flatnonzero(g["status"] == 0)
+    idx = honest[np.arange(n) % len(honest)]
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a[idx])).to(dev)
+    nonces, pub, helper, lps = T(g["nonce"]), T(g["pub"]), T(g["helper"]), T(g["lps"])
+    eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(10000, 16), vk, device=0)
+    for kv in args.opt:
+        k, v = kv.split("=")
+        eng.set_option(k, int(v))
+    msgs = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    seg = torch.zeros(n, dtype=torch.int32, device=dev)
+    agg = torch.zeros((1, eng.sz.agg_share_len), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def step():
+        s = torch.cuda.current_stream().cuda_stream
+        eng.prepare_device(nonces, pub, helper, lps, msgs, status, stream=s)
+        eng.accumulate_device(n, status, seg, None, 1, agg, cnt, stream=s)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    eng.set_option("timing", 1)
+    eng.timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    times = eng.timing()
+    eng.set_option("timing", 0)
+    # checks: prepare messages and every step's aggregate against the fixtures
+    P128 = (1 << 128) - 28 * (1 << 64) + 1
+    ok_msgs = bool(np.array_equal(msgs.cpu().numpy(), g["prep_msg"][idx]))
+    outs = [np.frombuffer(g["out_shares"][k].tobytes(), dtype="<u8").reshape(-1, 2) for k in honest]
+    cnts = [int((idx == k).sum()) for k in honest]  # accumulate overwrites: one step's sum
+    a = agg.cpu().numpy()[0].tobytes()
+    ok_agg = True
+    for e in range(0, 10000, 997):  # sampled entries (full check lives in tests/test_fpvec.py)
+        want = sum(c * (int(o[e, 0]) | int(o[e, 1]) << 64) for c, o in zip(cnts, outs)) % P128
+        ok_agg &= int.from_bytes(a[16 * e:16 * e + 16], "little") == want
+    cpu = None
+    if not args.no_cpu_baseline:
+        from oracle import prio3_py as P
+        from oracle.fpvec_py import FpVecType
+        v = P.Prio3(FpVecType(10000, 16))
+        k = int(honest[0])
+        t1 = time.perf_counter()
+        st1, hps, _ = v.prepare_init(vk, 1, bytes(g["nonce"][k]), bytes(g["pub"][k]),
+                                     bytes(g["helper"][k]))
+        v.prepare_next(st1, v.prep_shares_to_prep_msg(bytes(g["lps"][k]), hps))
+        dt = time.perf_counter() - t1
+        cpu = dict(value=1 / dt, unit="reports/s", cores=1, kind="port",
+                   sample=f"1 report through oracle/fpvec_py.py (pure Python, one core), {dt:.1f}s")
+    kern = {k: dict(ms_total=v[0], launches=v[1], ms_avg=v[0] / max(v[1], 1))
+            for k, v in times.items()}
+    value = n * args.steps / elapsed
+    out = dict(metric="reports prepared+aggregated/sec (helper, Prio3FixedPointBoundedL2VecSum "
+                      "length=10000)", value=value, unit="reports/s", n_gpus=1, steps=args.steps,
+               warmup=args.warmup, ms_per_step=elapsed / args.steps * 1e3, higher_is_better=True,
+               scaling="weak", vs_baseline=None, dtype="u32 limbs (Field128 mod-p integer arithmetic)",
+               data=f"synthetic: {len(honest)} honest full-size reports (tests/golden/"
+                    f"fpvec_l10000.npz) tiled to {n}",
+               config=dict(workload="Prio3FixedPointBoundedL2VecSum length=10000 BitSize16 helper "
+                                    "prepare+aggregate (configs[4], C5)", length=10000, bits=16,
+                           reports=n),
+               kernels=kern,
+               checks=dict(finished=int((status == 0).sum().item()), agg_count=int(cnt[0]),
+                           prep_msgs_match=ok_msgs, agg_sample_match=bool(ok_agg)),
+               cpu_baseline=cpu,
+               speedup_vs_cpu=(value / cpu["value"]) if cpu else None)
     print(json.dumps(out), flush=True)
 
 

@@ -429,7 +429,7 @@ struct prio3_engine {
   int fuse_acc = 1;
   int leader_fast = 1;
   int chunks = 0;                  // option: prepare in this many stream-overlapped chunks
-  int64_t fp_sub_bytes = 48ll << 30;  // option: FPVec per-sub-batch scratch budget (bytes)
+  int64_t fp_sub_bytes = 0;  // option: FPVec per-sub-batch scratch budget (bytes; 0 = auto)
                                    // (0 = auto: one chunk per 128Ki reports)
   std::vector<hipStream_t> side;   // side streams for chunked prepare
   std::vector<hipEvent_t> side_ev;

@@ -245,8 +245,13 @@ __global__ __launch_bounds__(256, XOFD_OCC) void k_xofd(DevParams p, InPtrs in, 
     msg_byte(m, 25, 1);
     msg_bytes16(m, 26, nonce);
     msg_absorb_final(s, m, 42);
-    uint32_t w[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
-    put_elem<F>(p, sc.qr, 0, r, w, flag);
+    if (p.qr_len == 1) {  // wave-uniform
+      uint32_t w[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
+      put_elem<F>(p, sc.qr, 0, r, w, flag);
+    } else {  // FPVec: one query point per gadget
+      uint32_t q0 = 0, q1 = 0;
+      squeeze_block<F>(p, s, 0, p.qr_len, q0, q1, sc.qr, r, flag);
+    }
   }
   const uint32_t M = p.meas_len, K = (M * 16 + 167) / 168;
   const uint32_t L = 42 + M * 16, B = L / 168, rem = L % 168;  // B >= 2 (checked on the host)
@@ -2233,12 +2238,6 @@ static int ensure_scratch(prio3_engine* e, uint32_t n) {
   const DevParams& d = e->dp;
   size_t es = d.es;
   const bool fp = d.kind == PRIO3_FPVEC_BOUNDED_L2;
-  if (fp) {  // per-report scratch for one sub-batch (2.56 MB of meas share per report at 10^4)
-    const size_t per = es * ((size_t)d.meas_len + d.proof_len + d.P + d.P1 + d.P + d.P1 + d.calls);
-    uint64_t cols = (uint64_t)std::max<int64_t>(e->fp_sub_bytes, 1) / per;
-    cols = std::max<uint64_t>(256, cols & ~255ull);
-    ld = (uint32_t)std::min<uint64_t>(ld_out, cols);
-  }
   void** bufs[] = {&e->sc.meas, &e->sc.proofs, &e->sc.jr, &e->sc.qr, (void**)&e->sc.part,
                    (void**)&e->sc.corrected, (void**)&e->sc.flag, &e->sc.Lbuf, &e->sc.PVbuf,
                    &e->sc.acc, &e->sc.out, &e->sc.beta, (void**)&e->d_mask};
@@ -2247,6 +2246,21 @@ static int ensure_scratch(prio3_engine* e, uint32_t n) {
       (void)hipFree(*b);
       *b = nullptr;
     }
+  if (fp) {  // per-report scratch for one sub-batch (2.56 MB of meas share per report at 10^4)
+    const size_t per = es * ((size_t)d.meas_len + d.proof_len + d.P + d.P1 + d.P + d.P1 + d.calls);
+    int64_t budget = e->fp_sub_bytes;
+    if (budget <= 0) {  // auto: 85% of free HBM after the batch's output shares (one column
+                        // per report); the kernels are latency-bound per lane, so the widest
+                        // sub-batch wins (MI355X, 100k x 10^4: 48 GB -> 43.7K/s, 180 GB -> 112K/s)
+      size_t fr = 0, tot = 0;
+      HIPCHK(hipMemGetInfo(&fr, &tot));
+      const int64_t outb = (int64_t)(es * d.out_len * ld_out + 64 * (size_t)ld_out);
+      budget = (int64_t)(0.85 * (double)fr) - outb;
+    }
+    uint64_t cols = (uint64_t)std::max<int64_t>(budget, 1) / per;
+    cols = std::max<uint64_t>(256, cols & ~255ull);
+    ld = (uint32_t)std::min<uint64_t>(ld_out, cols);
+  }
   size_t sizes[] = {es * d.meas_len * ld, es * d.proof_len * ld, es * (d.jr_len ? d.jr_len : 1) * ld,
                     es * d.qr_len * ld, 16 * (size_t)ld, 16 * (size_t)ld, (size_t)ld,
                     es * (d.P + d.P1) * ld, es * (d.P + d.P1) * ld, fp ? 16 : es * d.arity * ld,
@@ -2421,8 +2435,8 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
     e->chunks = (int)value;
     return PRIO3_OK;
   }
-  if (!strcmp(key, "fp_sub_bytes")) {  // FPVec scratch budget per sub-batch (next allocation)
-    if (value <= 0) return PRIO3_EINVAL;
+  if (!strcmp(key, "fp_sub_bytes")) {  // FPVec scratch budget per sub-batch (next allocation;
+    if (value < 0) return PRIO3_EINVAL;  // 0 = auto, sized from free HBM)
     e->fp_sub_bytes = value;
     e->cap = 0;  // re-size on the next call
     return PRIO3_OK;
@@ -2530,7 +2544,10 @@ static int launch_prepare(prio3_engine* e, uint32_t c0, uint32_t n, InPtrs in, O
     // Sub-batches of dp.ld reports through the per-report scratch (the whole batch's meas
     // shares would not fit: 2.56 MB per report at 10^4 entries); output shares keep one
     // column per report of the batch (ld_out), so accumulate runs once over all of them.
-    const uint32_t sub = dp.ld;
+    // equal sub-batches (columns rounded to 256): per-lane latency, not lane count, sets a
+    // launch's duration, so 2 x 50k beats 68k + 32k
+    const uint32_t nsub = (n + dp.ld - 1) / dp.ld;
+    const uint32_t sub = std::min(dp.ld, (((n + nsub - 1) / nsub) + 255) & ~255u);
     for (uint32_t s0 = 0; s0 < n; s0 += sub) {
       DevParams q = dp;
       q.n = std::min(sub, n - s0);
@@ -2545,7 +2562,11 @@ static int launch_prepare(prio3_engine* e, uint32_t c0, uint32_t n, InPtrs in, O
       Scratch qs = sc;
       qs.out = (uint8_t*)sc.out + es * s0;
       const uint32_t qb = (q.n + 255) / 256, qb64 = (q.n + 63) / 64;
-      TIMED(e, st, "k_xof", (k_xof<Fp128><<<qb, 256, 0, st>>>(q, qi, qs)));
+      // k_xofd (two live Keccak states: share squeeze + joint-rand absorb) unless A/B-ed off
+      if (e->split_xof == 2 && (42 + dp.meas_len * 16) / 168 >= 2)
+        TIMED(e, st, "k_xofd", (k_xofd<false><<<qb, 256, 0, st>>>(q, qi, qs)));
+      else
+        TIMED(e, st, "k_xof", (k_xof<Fp128><<<qb, 256, 0, st>>>(q, qi, qs)));
       TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp128><<<qb64, 64, 0, st>>>(q, qi, qs)));
       TIMED(e, st, "k_query_fp", launch_fpvec_query(q, qi, qs, qo, st));
     }

@@ -242,3 +242,45 @@ def test_gpu_fpvec_1000_entries():
     reps = _reports(v, 130, seed=5, distinct=3)
     reps[1]["lps"][16 * 7] ^= 1
     _check(v, reps, _run(v, reps))
+
+
+GOLDEN_C5 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fpvec_l10000.npz")
+
+
+def test_c5_fixture_shapes_match_engine_sizes():
+    """The full-size fixtures (gen_fpvec_l10000.py) have the wire sizes the engine expects."""
+    from janus_amd import prio3 as J
+    g = np.load(GOLDEN_C5)
+    sz = J.Prio3FixedPointBoundedL2VecSum(10000, 16).sizes()
+    assert g["helper"].shape[1] == sz.helper_share_len
+    assert g["lps"].shape[1] == sz.prep_share_len
+    assert g["pub"].shape[1] == sz.public_share_len
+    assert g["out_shares"].shape == (2, sz.agg_share_len)
+    assert g["status"].tolist() == [0, 0, 3]
+
+
+@pytest.mark.gpu
+def test_gpu_fpvec_c5_full_size():
+    """Config C5 at its full length (10000 entries, MEAS_LEN ~160k Field128 elements): two
+    honest reports and a tampered one, tiled to 384 lanes, against the committed fixtures --
+    statuses, prepare messages, sampled output shares and the whole aggregate share."""
+    from janus_amd import prio3 as J
+    g = np.load(GOLDEN_C5)
+    n = 384
+    idx = np.arange(n) % 3
+    eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(10000, 16), bytes(g["verify_key"]))
+    msgs, status, batch = eng.prepare_batch(g["nonce"][idx], g["pub"][idx], g["helper"][idx],
+                                            g["lps"][idx])
+    assert status.tolist() == g["status"][idx].tolist()
+    np.testing.assert_array_equal(msgs, g["prep_msg"][idx])
+    outs = batch.output_shares()
+    for r in (0, 1, 3, 4, n - 3, n - 2):
+        np.testing.assert_array_equal(outs[r].reshape(-1), g["out_shares"][idx[r]])
+    agg, cnt = batch.accumulate()
+    assert int(cnt[0]) == 2 * n // 3
+    o = [np.frombuffer(g["out_shares"][k].tobytes(), "<u8").reshape(-1, 2) for k in (0, 1)]
+    c = [int((idx == k).sum()) for k in (0, 1)]
+    want = b"".join(((c[0] * (int(o[0][e, 0]) | int(o[0][e, 1]) << 64) +
+                      c[1] * (int(o[1][e, 0]) | int(o[1][e, 1]) << 64)) % P.Field128.p)
+                    .to_bytes(16, "little") for e in range(10000))
+    assert agg[0].tobytes() == want
