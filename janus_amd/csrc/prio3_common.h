@@ -399,7 +399,8 @@ struct prio3_engine;
 int launch_mp64(prio3_engine* e, uint32_t n, InPtrs in, OutPtrs out, Scratch sc,
                 hipStream_t st);
 // FPVec FLP query + decide + prepare message + truncate for p.n reports (prio3_fpvec.hip)
-void launch_fpvec_query(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st);
+void launch_fpvec_query(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
+                        int gs);
 
 struct prio3_engine {
   prio3_params params;
@@ -443,6 +444,7 @@ struct prio3_engine {
   uint32_t leader_n = 0;
   int force_slow = 0;
   int split_xof = 2;  // 2: dual-state k_xofd, 1: k_xof_a + k_jrpart, 0: generic fused k_xof
+  int fp_gs = 8;      // option: FPVec query chunk-column group (loads in flight per lane): 4/8/16
   int qh_prefetch = 1;
   int qh_occ = 3;
   int qh_regs = 0;

@@ -2465,6 +2465,11 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
     e->split_xof = (int)value;
     return PRIO3_OK;
   }
+  if (!strcmp(key, "fp_gs")) {
+    if (value != 4 && value != 8 && value != 16) return PRIO3_EINVAL;
+    e->fp_gs = (int)value;
+    return PRIO3_OK;
+  }
   if (!strcmp(key, "timing")) {
     e->timing = (int)value;
     return PRIO3_OK;
@@ -2568,7 +2573,7 @@ static int launch_prepare(prio3_engine* e, uint32_t c0, uint32_t n, InPtrs in, O
       else
         TIMED(e, st, "k_xof", (k_xof<Fp128><<<qb, 256, 0, st>>>(q, qi, qs)));
       TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp128><<<qb64, 64, 0, st>>>(q, qi, qs)));
-      TIMED(e, st, "k_query_fp", launch_fpvec_query(q, qi, qs, qo, st));
+      TIMED(e, st, "k_query_fp", launch_fpvec_query(q, qi, qs, qo, st, e->fp_gs));
     }
     return PRIO3_OK;
   }

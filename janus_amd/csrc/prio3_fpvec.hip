@@ -221,6 +221,16 @@ __global__ __launch_bounds__(256) void k_query_fp(DevParams p, InPtrs in, Scratc
 
 }  // namespace
 
-void launch_fpvec_query(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st) {
-  k_query_fp<4><<<(p.n + 255) / 256, 256, 0, st>>>(p, in, sc, out);
+// GS = chunk columns per pass: each pass re-reads beta_k and L_(k+1) for all K0 calls, and
+// its GS independent meas loads are the lane's memory-level parallelism (one wave per SIMD at
+// 10^4 entries, so latency, not occupancy, is what GS buys back)
+void launch_fpvec_query(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
+                        int gs) {
+  const uint32_t b = (p.n + 255) / 256;
+  if (gs >= 16)
+    k_query_fp<16><<<b, 256, 0, st>>>(p, in, sc, out);
+  else if (gs >= 8)
+    k_query_fp<8><<<b, 256, 0, st>>>(p, in, sc, out);
+  else
+    k_query_fp<4><<<b, 256, 0, st>>>(p, in, sc, out);
 }
