@@ -4,7 +4,8 @@
 //
 // The XOF half of prepare_init (measurement / proofs share expansion, joint-rand part over the
 // 2.56 MB measurement share, corrected seed, joint randomness, two query-randomness elements)
-// is the engine's generic k_xof; this file is the two-gadget query that follows it.  The
+// is the engine's dual-state k_xofd (k_xof with split_xof=0); this file is the two-gadget
+// query that follows it.  The
 // circuit is the reconstruction fixed in oracle/fpvec_py.py:
 //   gadget 0 = ParallelSum(Mul, C0): range checks of every bit (SumVec's construction, r0);
 //   gadget 1 = ParallelSum(PolyEval(y^2 - 2^n y), C1) over the decoded entries y_e;
