@@ -444,6 +444,7 @@ struct prio3_engine {
   uint32_t leader_n = 0;
   int force_slow = 0;
   int split_xof = 2;  // 2: dual-state k_xofd, 1: k_xof_a + k_jrpart, 0: generic fused k_xof
+  int fp_overlap = 0;  // option: FPVec sub-batches alternate over two side streams (A/B: slower)
   int fp_gs = 8;      // option: FPVec query chunk-column group (loads in flight per lane): 4/8/16
   int qh_prefetch = 1;
   int qh_occ = 3;

@@ -2249,13 +2249,13 @@ static int ensure_scratch(prio3_engine* e, uint32_t n) {
   if (fp) {  // per-report scratch for one sub-batch (2.56 MB of meas share per report at 10^4)
     const size_t per = es * ((size_t)d.meas_len + d.proof_len + d.P + d.P1 + d.P + d.P1 + d.calls);
     int64_t budget = e->fp_sub_bytes;
-    if (budget <= 0) {  // auto: 85% of free HBM after the batch's output shares (one column
+    if (budget <= 0) {  // auto: 70% of free HBM after the batch's output shares (one column
                         // per report); the kernels are latency-bound per lane, so the widest
                         // sub-batch wins (MI355X, 100k x 10^4: 48 GB -> 43.7K/s, 180 GB -> 112K/s)
       size_t fr = 0, tot = 0;
       HIPCHK(hipMemGetInfo(&fr, &tot));
       const int64_t outb = (int64_t)(es * d.out_len * ld_out + 64 * (size_t)ld_out);
-      budget = (int64_t)(0.85 * (double)fr) - outb;
+      budget = (int64_t)(0.70 * (double)fr) - outb;
     }
     uint64_t cols = (uint64_t)std::max<int64_t>(budget, 1) / per;
     cols = std::max<uint64_t>(256, cols & ~255ull);
@@ -2465,6 +2465,10 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
     e->split_xof = (int)value;
     return PRIO3_OK;
   }
+  if (!strcmp(key, "fp_overlap")) {
+    e->fp_overlap = value ? 1 : 0;
+    return PRIO3_OK;
+  }
   if (!strcmp(key, "fp_gs")) {
     if (value != 4 && value != 8 && value != 16) return PRIO3_EINVAL;
     e->fp_gs = (int)value;
@@ -2517,6 +2521,20 @@ static int ensure_fused(prio3_engine* e, uint32_t n, uint32_t n_segments) {
 
 // The kernel sequence for reports [c0, c0 + n) of the batch: every pointer is shifted to the
 // chunk (SoA scratch keeps the batch's leading dimension, so a chunk is a column range).
+// side streams + their join events and the fork event, created once per engine
+static int ensure_side_streams(prio3_engine* e) {
+  while (e->side.size() < 2) {
+    hipStream_t s2;
+    hipEvent_t j;
+    HIPCHK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&j, hipEventDisableTiming));
+    e->side.push_back(s2);
+    e->side_ev.push_back(j);
+  }
+  if (!e->fork_ev) HIPCHK(hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming));
+  return PRIO3_OK;
+}
+
 static int launch_prepare(prio3_engine* e, uint32_t c0, uint32_t n, InPtrs in, OutPtrs out,
                           Scratch sc, hipStream_t st, bool fuse) {
   DevParams dp = e->dp;
@@ -2551,9 +2569,26 @@ static int launch_prepare(prio3_engine* e, uint32_t c0, uint32_t n, InPtrs in, O
     // column per report of the batch (ld_out), so accumulate runs once over all of them.
     // equal sub-batches (columns rounded to 256): per-lane latency, not lane count, sets a
     // launch's duration, so 2 x 50k beats 68k + 32k
-    const uint32_t nsub = (n + dp.ld - 1) / dp.ld;
-    const uint32_t sub = std::min(dp.ld, (((n + nsub - 1) / nsub) + 255) & ~255u);
-    for (uint32_t s0 = 0; s0 < n; s0 += sub) {
+    // Option fp_overlap: the scratch holds two column sets of half the width, and alternate
+    // sub-batches run on the two side streams, so one sub-batch's memory-latency-bound query
+    // shares the CUs with the next one's VALU-latency-bound Keccak (each alone holds < 1 wave
+    // per SIMD at 10^4 entries).
+    const uint32_t half = (dp.ld / 2) & ~255u;  // two column sets, each a multiple of 256
+    const bool two = e->fp_overlap && half > 0;
+    const uint32_t cap = two ? half : dp.ld;
+    const uint32_t nsub = (n + cap - 1) / cap;
+    const uint32_t sub = std::min(cap, (((n + nsub - 1) / nsub) + 255) & ~255u);
+    const bool ov = two && nsub > 1;  // set (si % 2) starts at column (si % 2) * cap < dp.ld
+    if (ov) {
+      int rc = ensure_side_streams(e);
+      if (rc) return rc;
+      HIPCHK(hipEventRecord(e->fork_ev, st));
+      for (auto s2 : e->side) HIPCHK(hipStreamWaitEvent(s2, e->fork_ev, 0));
+    }
+    uint32_t si = 0;
+    for (uint32_t s0 = 0; s0 < n; s0 += sub, si++) {
+      hipStream_t ss = ov ? e->side[si % 2] : st;
+      const size_t col = ov ? (size_t)(si % 2) * cap : 0;
       DevParams q = dp;
       q.n = std::min(sub, n - s0);
       InPtrs qi = in;
@@ -2565,16 +2600,26 @@ static int launch_prepare(prio3_engine* e, uint32_t c0, uint32_t n, InPtrs in, O
       qo.prep_msgs += 16 * (size_t)s0;
       qo.status += s0;
       Scratch qs = sc;
+      void** cols[] = {&qs.meas, &qs.proofs, &qs.jr, &qs.qr, &qs.Lbuf, &qs.PVbuf, &qs.beta};
+      for (auto c : cols) *c = (uint8_t*)*c + es * col;
+      qs.part += col;
+      qs.corrected += col;
+      qs.flag += col;
       qs.out = (uint8_t*)sc.out + es * s0;
       const uint32_t qb = (q.n + 255) / 256, qb64 = (q.n + 63) / 64;
       // k_xofd (two live Keccak states: share squeeze + joint-rand absorb) unless A/B-ed off
       if (e->split_xof == 2 && (42 + dp.meas_len * 16) / 168 >= 2)
-        TIMED(e, st, "k_xofd", (k_xofd<false><<<qb, 256, 0, st>>>(q, qi, qs)));
+        TIMED(e, ss, "k_xofd", (k_xofd<false><<<qb, 256, 0, ss>>>(q, qi, qs)));
       else
-        TIMED(e, st, "k_xof", (k_xof<Fp128><<<qb, 256, 0, st>>>(q, qi, qs)));
-      TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp128><<<qb64, 64, 0, st>>>(q, qi, qs)));
-      TIMED(e, st, "k_query_fp", launch_fpvec_query(q, qi, qs, qo, st, e->fp_gs));
+        TIMED(e, ss, "k_xof", (k_xof<Fp128><<<qb, 256, 0, ss>>>(q, qi, qs)));
+      TIMED(e, ss, "k_xof_slow", (k_xof_slow<Fp128><<<qb64, 64, 0, ss>>>(q, qi, qs)));
+      TIMED(e, ss, "k_query_fp", launch_fpvec_query(q, qi, qs, qo, ss, e->fp_gs));
     }
+    if (ov)
+      for (size_t i = 0; i < e->side.size(); i++) {
+        HIPCHK(hipEventRecord(e->side_ev[i], e->side[i]));
+        HIPCHK(hipStreamWaitEvent(st, e->side_ev[i], 0));
+      }
     return PRIO3_OK;
   }
   if (dp.es == 16) {
@@ -2642,15 +2687,8 @@ static int prepare_impl(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
   const uint32_t csz = ((n + K - 1) / K + 255) & ~255u;
   if (K == 1 || n <= csz || e->dp.kind == PRIO3_FPVEC_BOUNDED_L2)
     return launch_prepare(e, 0, n, in, out, sc, st, fuse);
-  while (e->side.size() < 2) {  // side streams + their join events, created once per engine
-    hipStream_t s2;
-    hipEvent_t j;
-    HIPCHK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&j, hipEventDisableTiming));
-    e->side.push_back(s2);
-    e->side_ev.push_back(j);
-  }
-  if (!e->fork_ev) HIPCHK(hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming));
+  rc = ensure_side_streams(e);
+  if (rc) return rc;
   HIPCHK(hipEventRecord(e->fork_ev, st));
   for (auto s2 : e->side) HIPCHK(hipStreamWaitEvent(s2, e->fork_ev, 0));
   uint32_t c = 0;

@@ -284,3 +284,23 @@ def test_gpu_fpvec_c5_full_size():
                       c[1] * (int(o[1][e, 0]) | int(o[1][e, 1]) << 64)) % P.Field128.p)
                     .to_bytes(16, "little") for e in range(10000))
     assert agg[0].tobytes() == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("overlap", [1, 0])
+def test_gpu_fpvec_stream_overlapped_sub_batches(overlap):
+    """1300 reports with the whole batch's scratch: fp_overlap splits it into two column sets
+    of 512 and runs sub-batches 512 + 512 + 276 on alternating side streams; every sub-batch's
+    shares, statuses and the aggregate must equal the restatement's either way."""
+    v = _vdaf(6)
+    reps = _reports(v, 1300, seed=21, distinct=130)
+    _tamper(v, reps, 0.05, seed=4)
+    from janus_amd import prio3 as J
+    t = v.t
+    eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(t.length, t.bits), VK)
+    eng.set_option("fp_overlap", overlap)
+    A = lambda k: np.array([list(r[k]) for r in reps], np.uint8)
+    msgs, status, batch = eng.prepare_batch(A("nonce"), A("pub"), A("helper"), A("lps"))
+    outs = batch.output_shares()
+    agg, cnt = batch.accumulate()
+    _check(v, reps, (msgs, status, outs, agg, cnt))
