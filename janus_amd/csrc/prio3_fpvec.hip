@@ -65,6 +65,20 @@ DEV T decode_bits(const void* meas, uint32_t base, uint32_t nbits, size_t ld, ui
   return y;
 }
 
+// the same for nbits a multiple of 16: each 16-bit group's loads are issued together (the
+// generic loop waits out one HBM latency per bit: 16 x 10^4 serialized misses per report)
+DEV T decode_bits16(const void* meas, uint32_t base, uint32_t nbits, size_t ld, uint32_t r) {
+  T y = F::zero();
+  for (uint32_t hi = nbits; hi > 0; hi -= 16) {
+    T m[16];
+#pragma unroll
+    for (int b = 0; b < 16; b++) m[b] = ldf<F>(meas, base + hi - 16 + b, ld, r);
+#pragma unroll
+    for (int b = 15; b >= 0; b--) y = F::add(F::add(y, y), m[b]);
+  }
+  return y;
+}
+
 template <int GS>
 __global__ __launch_bounds__(256) void k_query_fp(DevParams p, InPtrs in, Scratch sc, OutPtrs out) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -161,7 +175,7 @@ __global__ __launch_bounds__(256) void k_query_fp(DevParams p, InPtrs in, Scratc
       for (int q = 0; q < GS; q++) {
         const uint32_t idx = k * C1 + jg + q;
         if (jg + q < C1 && idx < E) {
-          const T y = decode_bits(sc.meas, nb * idx, nb, ld, r);
+          const T y = decode_bits16(sc.meas, nb * idx, nb, ld, r);  // nb is 16 or 32
           F::store(sc.out, (size_t)idx * p.ld_out + r, y);
           Ac[q] = F::add(Ac[q], F::mul(Lk, y));
         }
