@@ -133,16 +133,32 @@ __global__ __launch_bounds__(256) void k_query_fp(DevParams p, InPtrs in, Scratc
     T Aa[GS], Bb[GS];
 #pragma unroll
     for (int q = 0; q < GS; q++) Aa[q] = Bb[q] = Z;
+    // software-pipelined: call k+1's beta, L and meas loads are in flight while call k's
+    // products run (a lone wave per SIMD has nothing else to hide the HBM latency with);
+    // invalid slots load element 0 and are zeroed at use, so no select waits on a load early
+    auto ldm = [&](uint32_t k, int q) {
+      const uint32_t i = k * C0 + jg + (uint32_t)q;
+      return ldf<F>(sc.meas, (jg + q < C0 && i < M) ? i : 0, ld, r);
+    };
+    T be_n = ldf<F>(sc.beta, 0, ld, r), Lk_n = Lc0(1), mn[GS];
+#pragma unroll
+    for (int q = 0; q < GS; q++) mn[q] = ldm(0, q);
 #pragma unroll 1
     for (uint32_t k = 0; k < K0; k++) {
-      const T be = ldf<F>(sc.beta, k, ld, r);
-      const T Lk = Lc0(k + 1);
+      const T be = be_n, Lk = Lk_n;
+      T mc[GS];
+#pragma unroll
+      for (int q = 0; q < GS; q++) mc[q] = mn[q];
+      const uint32_t kn = k + 1 < K0 ? k + 1 : k;  // the last pass reloads its own call
+      be_n = ldf<F>(sc.beta, kn, ld, r);
+      Lk_n = Lc0(kn + 1);
+#pragma unroll
+      for (int q = 0; q < GS; q++) mn[q] = ldm(kn, q);
       const uint32_t base = k * C0 + jg;
 #pragma unroll
       for (int q = 0; q < GS; q++) {
-        const uint32_t i = base + q;
-        const bool valid = (jg + q < C0) && (i < M);
-        const T m = F::sel(valid, ldf<F>(sc.meas, valid ? i : 0, ld, r), Z);
+        const bool valid = (jg + q < C0) && (base + q < M);
+        const T m = F::sel(valid, mc[q], Z);
         Aa[q] = F::add(Aa[q], F::mul(be, m));
         Bb[q] = F::add(Bb[q], F::mul(Lk, m));
       }
