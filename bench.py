@@ -92,10 +92,13 @@ def main():
     ap.add_argument("--reports", type=int, default=1 << 20, help="reports per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--role", choices=["helper", "leader", "hpke", "pipeline", "mp64", "fpvec"],
+    ap.add_argument("--role", choices=["helper", "leader", "hpke", "pipeline", "mp64", "fpvec", "config"],
                     default="helper",
                     help="helper (the BASELINE metric), the leader side (SURVEY 8(f) row 1) or "
                          "the batched HPKE open of helper input shares (8(f) row 2)")
+    ap.add_argument("--vdaf", choices=["count", "sumvec", "sum32"], default="sumvec",
+                    help="--role config: C1 Prio3Count (100k), C3 Prio3SumVec 8x1000 chunk 63 "
+                         "(1M/8 per GPU), C4 Prio3Sum 32 (10M/8 per GPU)")
     ap.add_argument("--opt", action="append", default=[],
                     help="engine option key=value (e.g. split_xof=0), for A/B runs")
     args = ap.parse_args()
@@ -109,6 +112,8 @@ def main():
         return mp64_main(args)
     if args.role == "fpvec":
         return fpvec_main(args)
+    if args.role == "config":
+        return config_main(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -688,6 +693,98 @@ def fpvec_main(args):
                            prep_msgs_match=ok_msgs, agg_sample_match=bool(ok_agg)),
                cpu_baseline=cpu,
                speedup_vs_cpu=(value / cpu["value"]) if cpu else None)
+    print(json.dumps(out), flush=True)
+
+
+CONFIGS = {  # BASELINE.json configs[0], [2], [3]: (engine vdaf, oracle kwargs, reports per GPU)
+    "count": (lambda: J.Prio3Count(), dict(kind="count"), 100_000),
+    "sumvec": (lambda: J.Prio3SumVec(8, 1000, 63), dict(kind="sumvec", bits=8, length=1000,
+                                                         chunk_length=63), 1_000_000 // 8),
+    "sum32": (lambda: J.Prio3Sum(32), dict(kind="sum", bits=32), 10_000_000 // 8),
+}
+
+
+def config_main(args):
+    """Helper prepare+aggregate lines for the other BASELINE.json configs on one MI355X
+    (C1 Count 100k; C3 SumVec(8, 1000, chunk 63) and C4 Sum(32) at one GPU's 1/8 shard of
+    their 8-GPU totals).  Same step as the headline (prio3_device_prepare_aggregate +
+    aggregate_finish over resident device-generated reports); cpu_baseline = the C
+    restatement on a bounded sample of the same reports, Janus job structure."""
+    from oracle.oracle import Oracle, build
+    mk, okw, n_def = CONFIGS[args.vdaf]
+    n = args.reports if args.reports != 1 << 20 else n_def
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    eng = J.HelperEngine(mk(), VK, device=0)
+    for kv in args.opt:
+        k, v = kv.split("=")
+        eng.set_option(k, int(v))
+    sz = eng.sz
+    d = eng.generate_reports_device(n, seed=0x4A414E5553000001, with_checks=True)
+    torch.cuda.synchronize()
+    flags = int(d["flags"].sum().item())
+    msgs = torch.empty((n, max(sz.prep_msg_len, 1)), dtype=torch.uint8, device=dev)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    seg = torch.zeros(n, dtype=torch.int32, device=dev)
+    agg = torch.zeros((1, sz.agg_share_len), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    pub = d["public_shares"] if sz.public_share_len else None
+
+    def step():
+        s = torch.cuda.current_stream().cuda_stream
+        eng.prepare_aggregate_device(d["nonces"], pub, d["helper_shares"],
+                                     d["leader_prep_shares"], seg, 1, msgs, status, stream=s)
+        eng.aggregate_finish_device(status, None, agg, cnt, stream=s)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    eng.set_option("timing", 1)
+    eng.timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    times = eng.timing()
+    eng.set_option("timing", 0)
+    value = n * args.steps / elapsed
+    cpu, parity = None, None
+    if not args.no_cpu_baseline:
+        build()
+        o = Oracle(**okw)
+        th = cpu_threads()
+        host = {k: d[k].cpu().numpy() for k in
+                ("nonces", "public_shares", "helper_shares", "leader_prep_shares")}
+
+        def run(m):
+            t1 = time.perf_counter()
+            r = o.helper_batch(VK, host["nonces"][:m], host["public_shares"][:m],
+                               host["helper_shares"][:m], host["leader_prep_shares"][:m],
+                               n_threads=th, job_size=500)
+            return time.perf_counter() - t1, r
+
+        probe = min(n, 500 * th)
+        dt, _ = run(probe)
+        m = int(min(n, max(probe, probe * args.cpu_seconds / max(dt, 1e-6))))
+        dt, (cm, cs, _, _) = run(m)
+        parity = bool(np.array_equal(status[:m].cpu().numpy(), cs) and
+                      np.array_equal(msgs[:m, :cm.shape[1]].cpu().numpy(), cm))
+        cpu = dict(value=m / dt, unit="reports/s", cores=th, kind="port",
+                   sample=f"{m} of the benchmark's GPU-generated reports, jobs of 500 reports, "
+                          f"one job per worker thread (aggregator.rs:1794,2100), {dt:.1f}s wall")
+    out = dict(metric=f"reports prepared+aggregated/sec (helper, {args.vdaf})", value=value,
+               unit="reports/s", n_gpus=1, steps=args.steps, warmup=args.warmup,
+               ms_per_step=elapsed / args.steps * 1e3, higher_is_better=True, scaling="weak",
+               vs_baseline=None, dtype="u32 limbs (mod-p integer arithmetic)",
+               data="synthetic: distinct honest reports generated on-device from a seed",
+               config=dict(workload=f"{args.vdaf} helper prepare+aggregate, 1 segment",
+                           reports=n, **{k: v for k, v in okw.items() if k != "kind"}),
+               kernels={k: dict(ms_total=v[0], launches=v[1], ms_avg=v[0] / max(v[1], 1))
+                        for k, v in times.items()},
+               checks=dict(finished=int((status == 0).sum().item()), agg_count=int(cnt[0]),
+                           generator_flags=flags, cpu_gpu_parity_on_sample=parity),
+               cpu_baseline=cpu, speedup_vs_cpu=(value / cpu["value"]) if cpu else None)
     print(json.dumps(out), flush=True)
 
 
