@@ -980,17 +980,31 @@ __global__ __launch_bounds__(256) void k_query_ps(DevParams p, InPtrs in, Scratc
     T Aa[GS], Bb[GS];
 #pragma unroll
     for (int q = 0; q < GS; q++) Aa[q] = Bb[q] = Z;
+    // software-pipelined as in k_query_fp: call k+1's loads are in flight during call k's
+    // products; invalid slots load element 0 and are zeroed at use
+    auto ldm = [&](uint32_t k, int q) {
+      const uint32_t i = k * C + jg + (uint32_t)q;
+      return ldf<F>(sc.meas, (jg + q < C && i < M) ? i : 0, ld, r);
+    };
+    T be_n = ldf<F>(sc.beta, 0, ld, r), L_n = Lc(1), mn[GS];
+#pragma unroll
+    for (int q = 0; q < GS; q++) mn[q] = ldm(0, q);
 #pragma unroll 1
     for (uint32_t k = 0; k < K; k++) {
-      const T be = ldf<F>(sc.beta, k, ld, r);
-      const T L = Lc(k + 1);
+      const T be = be_n, L = L_n;
+      T mc[GS];
+#pragma unroll
+      for (int q = 0; q < GS; q++) mc[q] = mn[q];
+      const uint32_t kn = k + 1 < K ? k + 1 : k;
+      be_n = ldf<F>(sc.beta, kn, ld, r);
+      L_n = Lc(kn + 1);
+#pragma unroll
+      for (int q = 0; q < GS; q++) mn[q] = ldm(kn, q);
       const uint32_t base = k * C + jg;
 #pragma unroll
       for (int q = 0; q < GS; q++) {
-        const uint32_t i = base + q;
-        const bool valid = (jg + q < C) && (i < M);
-        T m = ldf<F>(sc.meas, valid ? i : 0, ld, r);
-        m = F::sel(valid, m, Z);
+        const bool valid = (jg + q < C) && (base + q < M);
+        const T m = F::sel(valid, mc[q], Z);
         Aa[q] = F::add(Aa[q], F::mul(be, m));
         Bb[q] = F::add(Bb[q], F::mul(L, m));
         S = F::add(S, m);
