@@ -9,11 +9,28 @@
 
 #define MAX_ROOTS 20
 
+// Debug build (make -C janus_amd DEVICE_CHECKS=1 -> libjanus_prio3_dbg.so): device-side bounds
+// assertions on the SoA scratch indexing (column < leading dimension, row < rows of the buffer)
+// that print the failing condition and trap.  Compiled out of the product library.
+#ifdef JANUS_DEVICE_CHECKS
+#define DCHECK(c)                                                                        \
+  do {                                                                                   \
+    if (!(c)) {                                                                          \
+      printf("janus device check failed: %s (%s:%d) block %u thread %u\n", #c, __FILE__, \
+             __LINE__, (unsigned)blockIdx.x, (unsigned)threadIdx.x);                     \
+      __builtin_trap();                                                                  \
+    }                                                                                    \
+  } while (0)
+#else
+#define DCHECK(c) ((void)0)
+#endif
+
 struct DevParams {
   uint32_t kind, es, meas_len, out_len, jr_len, arity, calls, P, logP, glen, proof_len,
       verifier_len, chunk, bits, length, prep_share_len, helper_share_len, public_share_len,
       leader_share_len;
   uint32_t n, ld, force_slow;
+  uint32_t nseg;  // fused accumulate: segment ids >= nseg are excluded from every aggregate
   // query-randomness elements per proof (2 for the two-gadget FPVec circuit, else 1) and the
   // leading dimension of the output-share scratch (FPVec runs the other scratch in sub-batches
   // of ld columns; out keeps one column per report of the batch)
@@ -184,6 +201,7 @@ DEV void put_elem(const DevParams& p, void* base, uint32_t idx, uint32_t r, cons
                   uint32_t& flag) {
   typename F::T x = F::from_words(w);
   if (!F::lt_p(x)) flag = 1;
+  DCHECK(r < p.ld);
   F::store(base, (size_t)idx * p.ld + r, x);
 }
 
@@ -235,6 +253,7 @@ template <class F>
 DEV void dft_lane(const DevParams& p, void* buf, uint32_t r, uint32_t n, uint32_t logn) {
   typedef typename F::T T;
   const size_t ld = p.ld;
+  DCHECK(r < ld);
   for (uint32_t l = 1; l <= logn; l++) {
     const uint32_t half = 1u << (l - 1);
     const T wl = FC<F>::root(p, l);
@@ -253,6 +272,7 @@ DEV void dft_lane(const DevParams& p, void* buf, uint32_t r, uint32_t n, uint32_
 
 template <class F>
 DEV typename F::T ldf(const void* base, uint32_t e, size_t ld, uint32_t r) {
+  DCHECK(r < ld);
   return F::load(base, (size_t)e * ld + r);
 }
 

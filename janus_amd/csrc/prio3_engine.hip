@@ -224,7 +224,8 @@ __global__ __launch_bounds__(256, XOFD_OCC) void k_xofd(DevParams p, InPtrs in, 
     const bool valid = r < p.n;
     const uint32_t sg = valid ? (sc.seg ? sc.seg[r] : 0u) : 0xffffffffu;
     s0 = (uint32_t)__shfl((int)sg, 0);
-    fuse = __all(valid && sg == s0);
+    // a segment id >= n_segments excludes the report from every aggregate (never fused)
+    fuse = __all(valid && sg == s0 && sg < p.nseg);
     if (lane == 0 && (r - lane) < p.n && !fuse) sc.wseg[r >> 6] = 0xffffffffu;
   }
   if (r >= p.n) return;
@@ -515,7 +516,7 @@ __global__ __launch_bounds__(256, JR_OCC) void k_jrpart(DevParams p, InPtrs in, 
     // a report flagged for the rejection-sampling slow path gets its share rewritten later:
     // its wave is left to the fix-up pass
     const bool flagged = valid && sc.flag[r];
-    fuse = __all(valid && sg == s0 && !flagged);
+    fuse = __all(valid && sg == s0 && sg < p.nseg && !flagged);
     if (lane == 0 && (r - lane) < p.n) sc.wseg[r >> 6] = fuse ? s0 : 0xffffffffu;
   }
   if (r >= p.n) return;
@@ -1720,7 +1721,8 @@ constexpr uint32_t FIX_R = 4096, FIX_T = 64;
 __global__ __launch_bounds__(256) void k_agg_fix(uint32_t n, const uint8_t* status,
                                                  const uint32_t* seg, const uint8_t* accept,
                                                  const uint32_t* wseg, uint32_t* fix,
-                                                 uint32_t fix_cap, unsigned long long* counts) {
+                                                 uint32_t fix_cap, uint32_t nseg,
+                                                 unsigned long long* counts) {
   __shared__ uint32_t tseg[FIX_T];
   __shared__ unsigned int tcnt[FIX_T];
   if (threadIdx.x < FIX_T) {
@@ -1733,7 +1735,9 @@ __global__ __launch_bounds__(256) void k_agg_fix(uint32_t n, const uint8_t* stat
     const uint32_t r = base + threadIdx.x;
     const bool valid = r < hi;
     const uint32_t sg = valid ? (seg ? seg[r] : 0u) : 0xffffffffu;
-    const bool inc = valid && status[r] == PRIO3_STATUS_FINISHED && (!accept || accept[r]);
+    // out-of-range segment ids are excluded everywhere (as k_mask and k_meta do)
+    const bool inc = valid && sg < nseg && status[r] == PRIO3_STATUS_FINISHED &&
+                     (!accept || accept[r]);
     const bool fused = valid && wseg[r >> 6] != 0xffffffffu;
     const uint32_t s0 = (uint32_t)__shfl((int)sg, 0);
     const bool uni = __all(!valid || sg == s0);
@@ -2245,13 +2249,10 @@ static int fill_sizes(const prio3_params* pp, prio3_sizes_t* s, DevParams* dp) {
     }                                                                               \
   } while (0)
 
-static int ensure_scratch(prio3_engine* e, uint32_t n) {
-  if (n <= e->cap) return PRIO3_OK;
-  const uint32_t ld_out = (n + 63) & ~63u;
-  uint32_t ld = ld_out;
-  const DevParams& d = e->dp;
-  size_t es = d.es;
-  const bool fp = d.kind == PRIO3_FPVEC_BOUNDED_L2;
+// Scratch for n reports.  All-or-nothing: on any allocation failure every buffer is freed and
+// the engine is left with cap = 0 (the next call re-sizes from scratch), so no later call can
+// launch on a stale capacity with null or short buffers.
+static void free_scratch(prio3_engine* e) {
   void** bufs[] = {&e->sc.meas, &e->sc.proofs, &e->sc.jr, &e->sc.qr, (void**)&e->sc.part,
                    (void**)&e->sc.corrected, (void**)&e->sc.flag, &e->sc.Lbuf, &e->sc.PVbuf,
                    &e->sc.acc, &e->sc.out, &e->sc.beta, (void**)&e->d_mask};
@@ -2260,30 +2261,68 @@ static int ensure_scratch(prio3_engine* e, uint32_t n) {
       (void)hipFree(*b);
       *b = nullptr;
     }
+  e->cap = 0;
+  e->dp.ld = e->dp.ld_out = 0;
+}
+
+// FPVec per-report scratch bytes of one sub-batch column: every buffer indexed [row][column]
+// with the sub-batch leading dimension ld (meas, proofs, jr, qr, part, corrected, flag, L, PV,
+// beta); the output shares and the accumulate mask have one column per report of the batch.
+static size_t fp_column_bytes(const DevParams& d) {
+  const size_t es = d.es;
+  return es * ((size_t)d.meas_len + d.proof_len + d.jr_len + d.qr_len + 2 * ((size_t)d.P + d.P1) +
+               d.calls) +
+         16 + 16 + 1;
+}
+
+static int ensure_scratch(prio3_engine* e, uint32_t n) {
+  if (n <= e->cap) return PRIO3_OK;
+  free_scratch(e);
+  const uint32_t ld_out = (n + 63) & ~63u;
+  uint32_t ld = ld_out;
+  const DevParams& d = e->dp;
+  size_t es = d.es;
+  const bool fp = d.kind == PRIO3_FPVEC_BOUNDED_L2;
   if (fp) {  // per-report scratch for one sub-batch (2.56 MB of meas share per report at 10^4)
-    const size_t per = es * ((size_t)d.meas_len + d.proof_len + d.P + d.P1 + d.P + d.P1 + d.calls);
+    const size_t per = fp_column_bytes(d);
     int64_t budget = e->fp_sub_bytes;
-    if (budget <= 0) {  // auto: 70% of free HBM after the batch's output shares (one column
-                        // per report); the kernels are latency-bound per lane, so the widest
-                        // sub-batch wins (MI355X, 100k x 10^4: 48 GB -> 43.7K/s, 180 GB -> 112K/s)
+    if (budget <= 0) {
+      // auto: free HBM minus the batch's output shares and mask (one column per report) and a
+      // fixed reserve for the runtime (kernel scratch / private segments, queues, the caller's
+      // allocator).  The kernels are latency-bound per lane, so the widest sub-batch wins
+      // (MI355X, 100k x 10^4: 48 GB -> 43.7K/s, 180 GB -> 112K/s).
       size_t fr = 0, tot = 0;
       HIPCHK(hipMemGetInfo(&fr, &tot));
       const int64_t outb = (int64_t)(es * d.out_len * ld_out + 64 * (size_t)ld_out);
-      budget = (int64_t)(0.70 * (double)fr) - outb;
+      const int64_t reserve = std::max<int64_t>((int64_t)8 << 30, (int64_t)(0.10 * (double)tot));
+      budget = (int64_t)fr - outb - reserve;
     }
     uint64_t cols = (uint64_t)std::max<int64_t>(budget, 1) / per;
     cols = std::max<uint64_t>(256, cols & ~255ull);
     ld = (uint32_t)std::min<uint64_t>(ld_out, cols);
   }
-  size_t sizes[] = {es * d.meas_len * ld, es * d.proof_len * ld, es * (d.jr_len ? d.jr_len : 1) * ld,
-                    es * d.qr_len * ld, 16 * (size_t)ld, 16 * (size_t)ld, (size_t)ld,
-                    es * (d.P + d.P1) * ld, es * (d.P + d.P1) * ld, fp ? 16 : es * d.arity * ld,
-                    (d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC ||
-                     d.kind == PRIO3_SUMVEC_F64_MP || fp)
-                        ? es * d.out_len * ld_out
-                        : 16,
-                    es * d.calls * ld, (size_t)ld_out};
-  for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]); i++) HIPCHK(hipMalloc(bufs[i], sizes[i]));
+  void** bufs[] = {&e->sc.meas, &e->sc.proofs, &e->sc.jr, &e->sc.qr, (void**)&e->sc.part,
+                   (void**)&e->sc.corrected, (void**)&e->sc.flag, &e->sc.Lbuf, &e->sc.PVbuf,
+                   &e->sc.acc, &e->sc.out, &e->sc.beta, (void**)&e->d_mask};
+  const bool own_out = d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC ||
+                       d.kind == PRIO3_SUMVEC_F64_MP || fp;
+  const size_t sizes[] = {es * d.meas_len * ld, es * d.proof_len * ld,
+                          es * (d.jr_len ? d.jr_len : 1) * ld, es * d.qr_len * ld, 16 * (size_t)ld,
+                          16 * (size_t)ld, (size_t)ld, es * (d.P + d.P1) * ld,
+                          es * (d.P + d.P1) * ld, fp ? 16 : es * d.arity * ld,
+                          own_out ? es * d.out_len * ld_out : 16, es * d.calls * ld,
+                          (size_t)ld_out};
+  static_assert(sizeof(sizes) / sizeof(sizes[0]) == sizeof(bufs) / sizeof(bufs[0]), "");
+  for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]); i++) {
+    const hipError_t err = hipMalloc(bufs[i], sizes[i]);
+    if (err != hipSuccess) {
+      fprintf(stderr, "janus_prio3: scratch allocation of %zu bytes failed (%s)\n", sizes[i],
+              hipGetErrorString(err));
+      (void)hipGetLastError();
+      free_scratch(e);
+      return PRIO3_EDEVICE;
+    }
+  }
   e->cap = ld_out;
   e->dp.ld = ld;
   e->dp.ld_out = ld_out;
@@ -2744,6 +2783,7 @@ int prio3_device_prepare_aggregate(prio3_engine* e, uint32_t n, const uint8_t* d
   e->fused_segments = n_segments;
   e->fused_seg_ptr = d_segment_ids;
   e->fused_on = 0;
+  e->dp.nseg = n_segments;
   if (n == 0) return PRIO3_OK;
   const bool fuse = fusable(e);
   if (fuse) {
@@ -2784,7 +2824,7 @@ int prio3_device_aggregate_finish(prio3_engine* e, const uint8_t* d_status,
   TIMED(e, st, "k_agg_fix",
         (k_agg_fix<<<(n + FIX_R - 1) / FIX_R, 256, 0, st>>>(
             n, d_status, e->fused_seg_ptr, d_accept_mask, e->d_wseg, e->d_fix,
-            (uint32_t)(e->fix_cap - 1), (unsigned long long*)d_counts)));
+            (uint32_t)(e->fix_cap - 1), S, (unsigned long long*)d_counts)));
   TIMED(e, st, "k_agg_final",
         (k_agg_final<<<S * M, 256, 0, st>>>(M, e->dp.ld, e->d_agg64, nchunks,
                                                           e->d_cpart, e->d_cseg, e->d_fix,

@@ -87,6 +87,8 @@ __global__ __launch_bounds__(256) void k_query_fp(DevParams p, InPtrs in, Scratc
   const uint32_t P0 = p.P, A0 = p.arity, C0 = p.chunk, M = p.meas_len, K0 = p.calls;
   const uint32_t P1 = p.P1, C1 = p.chunk1, K1 = p.calls1, E = p.out_len, nb = p.bits;
   const uint32_t off1 = A0 + p.glen;  // proof: seeds0 | coeffs0 | seeds1 | coeffs1
+  DCHECK(r < p.ld && off1 + C1 + p.glen1 <= p.proof_len && K0 * C0 >= M && K1 * C1 >= E);
+  DCHECK(p.ld_out >= p.n && nb * E + 2 * nb - 2 == M);
   uint8_t status = PRIO3_STATUS_FINISHED;
   const T t0 = ldf<F>(sc.qr, 0, ld, r), t1 = ldf<F>(sc.qr, 1, ld, r);
   if (root_of_unity(t0, p.logP) || root_of_unity(t1, p.logP1)) status = PRIO3_STATUS_PREP_INIT;
@@ -192,6 +194,7 @@ __global__ __launch_bounds__(256) void k_query_fp(DevParams p, InPtrs in, Scratc
         const uint32_t idx = k * C1 + jg + q;
         if (jg + q < C1 && idx < E) {
           const T y = decode_bits16(sc.meas, nb * idx, nb, ld, r);  // nb is 16 or 32
+          DCHECK(nb * idx + nb <= M);
           F::store(sc.out, (size_t)idx * p.ld_out + r, y);
           Ac[q] = F::add(Ac[q], F::mul(Lk, y));
         }

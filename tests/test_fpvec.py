@@ -304,3 +304,26 @@ def test_gpu_fpvec_stream_overlapped_sub_batches(overlap):
     outs = batch.output_shares()
     agg, cnt = batch.accumulate()
     _check(v, reps, (msgs, status, outs, agg, cnt))
+
+
+@pytest.mark.gpu
+def test_gpu_fpvec_scratch_wider_than_sub_batch():
+    """the r01u fault geometry -- the scratch leading dimension (ld) wider
+    than the equal sub-batches it is cut into, and both narrower than the output-share columns
+    (ld_out).  A budget of 768 scratch columns over 1000 reports gives ld 768, two sub-batches
+    of 512 + 488, ld_out 1024."""
+    from janus_amd import prio3 as J
+    v = _vdaf(6)
+    t = v.t
+    reps = _reports(v, 1000, seed=41, distinct=100)
+    _tamper(v, reps, 0.05, seed=5)
+    per = 16 * (t.meas_len + t.proof_len + 2 + 2 + 2 * (t.P0 + t.P1) + t.K0) + 33
+    eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(t.length, t.bits), VK)
+    eng.set_option("fp_sub_bytes", per * 768 + per // 2)
+    eng.set_option("timing", 1)
+    A = lambda k: np.array([list(r[k]) for r in reps], np.uint8)
+    msgs, status, batch = eng.prepare_batch(A("nonce"), A("pub"), A("helper"), A("lps"))
+    assert eng.timing()["k_query_fp"][1] == 2  # two sub-batches
+    outs = batch.output_shares()
+    agg, cnt = batch.accumulate()
+    _check(v, reps, (msgs, status, outs, agg, cnt))

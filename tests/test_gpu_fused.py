@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(cfg, n, seed, n_segments=1, seg_mode="runs", tamper=True, accept_frac=0.9,
-         force_slow=False, fuse=True, chunks=None):
+         force_slow=False, fuse=True, chunks=None, oob_frac=0.0):
     import torch
     o = _oracle(cfg)
     eng = _engine(cfg)
@@ -38,9 +38,16 @@ def _run(cfg, n, seed, n_segments=1, seg_mode="runs", tamper=True, accept_frac=0
     else:
         seg = rng.integers(0, n_segments, n).astype(np.uint32)
     accept = (rng.random(n) < accept_frac).astype(np.uint8)
+    # segment ids >= n_segments: the report is excluded from every aggregate and count, as if
+    # its accept-mask byte were 0 (include/janus_prio3.h); the oracle sees exactly that
+    oob = rng.random(n) < oob_frac
+    dev_seg = np.where(oob, n_segments + 5 + (np.arange(n) % 3), seg).astype(np.uint32)
+    ref_seg = np.where(oob, 0, seg).astype(np.uint32)
+    ref_accept = np.where(oob, 0, accept).astype(np.uint8)
     ref_msgs, ref_status, ref_agg, ref_cnt = o.helper_batch(
         VK, d["nonces"], d["public_shares"], d["helper_shares"], d["leader_prep_shares"],
-        segment_ids=seg, accept_mask=accept, n_segments=n_segments, n_threads=8)
+        segment_ids=ref_seg, accept_mask=ref_accept, n_segments=n_segments, n_threads=8)
+    seg = dev_seg
     dev = torch.device("cuda", 0)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     sz = eng.sz
@@ -106,3 +113,11 @@ def test_fused_stream_overlapped_chunks(chunks):
 
 def test_chunks_unfused_instance():
     _run(CONFIGS["sumvec_8x10_c9"], 1100, seed=20, n_segments=2, chunks=3)
+
+
+@pytest.mark.parametrize("name,fuse", [("hist_256_c16", True), ("hist_256_c16", False),
+                                       ("sum8", True)])
+def test_out_of_range_segment_ids_are_excluded(name, fuse):
+    """a segment id >= n_segments never reaches the aggregate or the counts (fused
+    Histogram path, its unfused fallback, and the deferred masked reduction alike)."""
+    _run(CONFIGS[name], 900, seed=31, n_segments=3, oob_frac=0.05, fuse=fuse)
