@@ -277,6 +277,29 @@ DEV typename F::T ldf(const void* base, uint32_t e, size_t ld, uint32_t r) {
 }
 
 
+// In-register radix-2 DFT of N (<= 16) Field128 values given in bit-reversed order; twiddle
+// w_N^i = p.tw128[i * stride * (32 / 2 / (N/2)) ...] is taken from the P-th root table.
+template <int N, int LOGN>
+DEV void dft_reg(const DevParams& p, f128 (&x)[N], int stride) {
+  typedef Fp128 F;
+#pragma unroll
+  for (int l = 1; l <= LOGN; l++) {
+    const int half = 1 << (l - 1);
+#pragma unroll
+    for (int i = 0; i < half; i++) {
+      // w_(2^l)^i = w_(N*stride)^(i * stride * N / 2^l)
+      const f128 w = F::from_words(p.tw128[i * stride * (N >> l)]);
+#pragma unroll
+      for (int j = i; j < N; j += 2 * half) {
+        const f128 u = x[j];
+        const f128 v = (i == 0) ? x[j + half] : F::mul(w, x[j + half]);
+        x[j] = F::add(u, v);
+        x[j + half] = F::sub(u, v);
+      }
+    }
+  }
+}
+
 // FlpGeneric::query for one report (one lane), num_shares = 2.  Writes the wire-polynomial
 // values at t into acc[0..arity) and returns v (circuit output share) and pt = p(t).
 // Returns false if t is a P-th root of unity (prio FlpError -> VdafPrepareInit).
@@ -418,6 +441,9 @@ struct Mp64Params {
 struct prio3_engine;
 int launch_mp64(prio3_engine* e, uint32_t n, InPtrs in, OutPtrs out, Scratch sc,
                 hipStream_t st);
+// P = 16 / 32 ParallelSum(Mul) helper query on lane pairs (prio3_query_pair.hip); false if the
+// instance is not one it takes
+bool launch_query_pair(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st);
 // FPVec FLP query + decide + prepare message + truncate for p.n reports (prio3_fpvec.hip)
 void launch_fpvec_query(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
                         int gs);
@@ -469,6 +495,7 @@ struct prio3_engine {
   int qh_prefetch = 1;
   int qh_occ = 3;
   int qh_regs = 0;
+  int qpair = 0;  // option: P = 16/32 query on lane pairs (k_query_pair; A/B: slower)
   int timing = 0;
   Mp64Params mp{};          // PRIO3_SUMVEC_F64_MP only
   uint64_t* d_sigma64 = nullptr;

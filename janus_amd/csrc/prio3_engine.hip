@@ -1083,29 +1083,6 @@ __global__ __launch_bounds__(256) void k_query_ps(DevParams p, InPtrs in, Scratc
 // so the gadget polynomial is never evaluated on the roots.  The measurement loads of the
 // next gadget call are issued before the current call's arithmetic (register double buffer).
 // ------------------------------------------------------------------------------------
-// In-register radix-2 DFT of N (<= 16) Field128 values given in bit-reversed order; twiddle
-// w_N^i = p.tw128[i * stride * (32 / 2 / (N/2)) ...] is taken from the P-th root table.
-template <int N, int LOGN>
-DEV void dft_reg(const DevParams& p, f128 (&x)[N], int stride) {
-  typedef Fp128 F;
-#pragma unroll
-  for (int l = 1; l <= LOGN; l++) {
-    const int half = 1 << (l - 1);
-#pragma unroll
-    for (int i = 0; i < half; i++) {
-      // w_(2^l)^i = w_(N*stride)^(i * stride * N / 2^l)
-      const f128 w = F::from_words(p.tw128[i * stride * (N >> l)]);
-#pragma unroll
-      for (int j = i; j < N; j += 2 * half) {
-        const f128 u = x[j];
-        const f128 v = (i == 0) ? x[j + half] : F::mul(w, x[j + half]);
-        x[j] = F::add(u, v);
-        x[j + half] = F::sub(u, v);
-      }
-    }
-  }
-}
-
 // LEADER = 1: the leader's prepare_init (agg_id 0) on the same data flow -- the wire values
 // f_j(t), v and p(t) are written as the leader prepare share (out.prep_msgs is the prepare
 // share buffer, stride prep_share_len) instead of being decided against a peer's share.
@@ -2502,6 +2479,10 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
     e->fuse_acc = (int)value;
     return PRIO3_OK;
   }
+  if (!strcmp(key, "qpair")) {
+    e->qpair = (int)value;
+    return PRIO3_OK;
+  }
   if (!strcmp(key, "qh_regs")) {
     e->qh_regs = (int)value;
     return PRIO3_OK;
@@ -2692,7 +2673,12 @@ static int launch_prepare(prio3_engine* e, uint32_t c0, uint32_t n, InPtrs in, O
     }
     TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp128><<<blocks64, 64, 0, st>>>(dp, in, sc)));
     const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
-    if (ps && dp.P == 32 && dp.chunk == 16 && dp.calls == 16 && e->qh_regs)
+    bool done = false;
+    if (ps && e->qpair && (dp.P == 32 || dp.P == 16)) {
+      TIMED(e, st, "k_query_pair", (done = launch_query_pair(dp, in, sc, out, st)));
+    }
+    if (done) {
+    } else if (ps && dp.P == 32 && dp.chunk == 16 && dp.calls == 16 && e->qh_regs)
       TIMED(e, st, "k_query_r", (k_query_r<16, 16><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
     else if (ps && dp.P == 32)
       switch (e->qh_prefetch * 10 + e->qh_occ) {
@@ -3323,9 +3309,9 @@ int prio3_selftest_field(int op, uint32_t n, const uint8_t* a, const uint8_t* b,
         hipMemcpy(out, dout, (size_t)n * 16, hipMemcpyDeviceToHost) != hipSuccess)
       rc = PRIO3_EDEVICE;
   }
-  hipFree(da);
-  hipFree(db);
-  hipFree(dout);
+  (void)hipFree(da);
+  (void)hipFree(db);
+  (void)hipFree(dout);
   return rc;
 }
 
