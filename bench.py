@@ -92,13 +92,20 @@ def main():
     ap.add_argument("--reports", type=int, default=1 << 20, help="reports per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--role", choices=["helper", "leader", "hpke", "pipeline", "mp64", "fpvec", "config"],
+    ap.add_argument("--role", choices=["helper", "leader", "hpke", "pipeline", "mp64", "fpvec", "config",
+                                       "jobs"],
                     default="helper",
                     help="helper (the BASELINE metric), the leader side (SURVEY 8(f) row 1) or "
                          "the batched HPKE open of helper input shares (8(f) row 2)")
     ap.add_argument("--vdaf", choices=["count", "sumvec", "sum32"], default="sumvec",
                     help="--role config: C1 Prio3Count (100k), C3 Prio3SumVec 8x1000 chunk 63 "
                          "(1M/8 per GPU), C4 Prio3Sum 32 (10M/8 per GPU)")
+    ap.add_argument("--threads", type=int, default=16,
+                    help="--role jobs: host worker threads (Janus's rayon pool)")
+    ap.add_argument("--job-size", type=int, default=500,
+                    help="--role jobs: reports per aggregation job (aggregation_job_creator.rs:63-64)")
+    ap.add_argument("--tasks", type=int, default=4,
+                    help="--role jobs: tasks (verify keys) of the VDAF instance the jobs rotate over")
     ap.add_argument("--opt", action="append", default=[],
                     help="engine option key=value (e.g. split_xof=0), for A/B runs")
     args = ap.parse_args()
@@ -114,6 +121,8 @@ def main():
         return fpvec_main(args)
     if args.role == "config":
         return config_main(args)
+    if args.role == "jobs":
+        return jobs_main(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -268,6 +277,125 @@ def main():
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def jobs_main(args):
+    """The production call shape: `--threads` host threads, each a Janus rayon
+    worker running whole aggregation jobs of `--job-size` reports (aggregator.rs:2100-2123;
+    aggregation_job_creator.rs:63-64) through the HOST-BUFFER C ABI -- prio3_helper_prepare_batch
+    (PCIe H2D of the job's shares, prepare, D2H of messages + statuses) then prio3_accumulate
+    and prio3_batch_free -- on `--tasks` engines (verify keys) of Prio3Histogram(256,16).
+    Concurrent jobs are coalesced by the engine's executor.  The harness is native
+    (janus_amd/libjanus_jobs.so, C++ threads), so Python is not on the timed path.  Reported
+    against the PCIe H2D roof and next to the CPU restatement's single-core latency."""
+    import ctypes as C
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    K, js, T = args.tasks, args.job_size, args.threads
+    n_jobs = max(K, (args.reports if args.reports != 1 << 20 else 1 << 21) // js)
+    pool = 1 << 16
+    vks = [bytes([0x51 + t]) * 16 for t in range(K)]
+    engines = [J.HelperEngine(J.Prio3Histogram(256, 16), vk, device=0) for vk in vks]
+    for kv in args.opt:
+        k, v = kv.split("=")
+        for e in engines:
+            e.set_option(k, int(v))
+    sz = engines[0].sz
+    parts = [e.generate_reports_device(pool, seed=0x4A414E5553000003 + t)
+             for t, e in enumerate(engines)]
+    torch.cuda.synchronize()
+    host = {k: np.ascontiguousarray(np.concatenate([p[k].cpu().numpy() for p in parts]))
+            for k in ("nonces", "public_shares", "helper_shares", "leader_prep_shares")}
+    lib = C.CDLL(os.path.join(ROOT, "janus_amd", "libjanus_jobs.so"))
+    lib.janus_jobs_run.restype = C.c_double
+    vp = C.c_void_p
+    lib.janus_jobs_run.argtypes = [C.POINTER(vp), C.c_int, vp, C.c_int, C.c_int, C.c_int,
+                                   C.c_uint32, vp, vp, vp, vp, vp, vp, vp]
+    eng_arr = (vp * K)(*[e.handle.value for e in engines])
+    status = np.zeros(n_jobs * js, np.uint8)
+    counts = np.zeros(n_jobs, np.uint64)
+    agg = np.zeros(sz.agg_share_len, np.uint8)
+    P = lambda a: a.ctypes.data_as(vp)
+
+    def run(jobs):
+        status[:] = 0xFF
+        return lib.janus_jobs_run(eng_arr, K, C.cast(C.pointer(sz), vp), T, jobs, js, pool,
+                                  P(host["nonces"]), P(host["public_shares"]),
+                                  P(host["helper_shares"]), P(host["leader_prep_shares"]),
+                                  P(status), P(counts), P(agg))
+
+    run(max(K, min(n_jobs, 8 * T)))  # warmup: pools, pinned staging, streams
+    for e in engines:
+        e.set_option("timing", 1)
+        e.timing_reset()
+    dt = run(n_jobs)
+    if dt < 0:
+        raise RuntimeError("janus_jobs_run: a C-ABI call failed")
+    launches = sum(e.timing().get("k_xofd", (0, 0))[1] for e in engines)
+    value = n_jobs * js / dt
+    # spot check: the last job's aggregate against the restatement
+    from oracle.oracle import Oracle
+    o = Oracle("histogram", length=256, chunk_length=16)
+    j = n_jobs - 1
+    t = j % K
+    r0 = t * pool + ((j // K) * js) % (pool - js + 1)
+    sl = slice(r0, r0 + js)
+    _, rst, ragg, rcnt = o.helper_batch(vks[t], host["nonces"][sl], host["public_shares"][sl],
+                                        host["helper_shares"][sl],
+                                        host["leader_prep_shares"][sl], n_threads=cpu_threads())
+    # the CPU reference path on this host: the restatement at the same job structure on all
+    # cores, and its single-core per-report latency
+    cores = cpu_threads()
+    cpu = None
+    if not args.no_cpu_baseline:
+        m = min(4000 * cores, len(host["nonces"]))
+        t0 = time.perf_counter()
+        o.helper_batch(vks[0], host["nonces"][:m], host["public_shares"][:m],
+                       host["helper_shares"][:m], host["leader_prep_shares"][:m],
+                       n_threads=cores, job_size=js)
+        dta = time.perf_counter() - t0
+        m1 = 2000
+        t0 = time.perf_counter()
+        o.helper_batch(vks[0], host["nonces"][:m1], host["public_shares"][:m1],
+                       host["helper_shares"][:m1], host["leader_prep_shares"][:m1],
+                       n_threads=1, job_size=js)
+        dt1 = time.perf_counter() - t0
+        cpu = dict(value=m / dta, unit="reports/s", cores=cores, kind="port",
+                   sample=f"{m} reports, jobs of {js}, one job per worker thread, {dta:.1f}s",
+                   single_core_us_per_report=dt1 / m1 * 1e6, cpu_model=cpu_model())
+    per_report_h2d = 16 + sz.public_share_len + sz.helper_share_len + sz.prep_share_len
+    out = dict(metric="reports prepared+aggregated/sec through the host-buffer C ABI "
+                      "(helper, Prio3Histogram len=256, concurrent aggregation jobs)",
+               value=value, unit="reports/s", n_gpus=1, steps=1, warmup=1,
+               ms_per_step=dt * 1e3, higher_is_better=True, scaling="weak", vs_baseline=None,
+               dtype="u32 limbs (Field128 mod-p integer arithmetic)",
+               data=f"synthetic: {K} x {pool} on-device client reports copied to host memory",
+               config=dict(workload="Prio3Histogram length=256 chunk_length=16 helper prepare + "
+                                    "accumulate per aggregation job, host buffers (PCIe included)",
+                           job_size=js, jobs=n_jobs, threads=T, tasks=K),
+               pcie=dict(h2d_bytes_per_report=per_report_h2d,
+                         h2d_GBps=value * per_report_h2d / 1e9,
+                         roof_reports_per_s=63e9 / per_report_h2d,
+                         roof_note="PCIe Gen5 x16 ~63 GB/s (MI355X_MICROARCH.md)"),
+               coalescing=dict(launches=launches, jobs=n_jobs,
+                               mean_reports_per_launch=n_jobs * js / max(launches, 1)),
+               checks=dict(all_finished=bool((status == 0).all()),
+                           counts_ok=bool((counts == js).all()),
+                           last_job_matches_cpu=bool(np.array_equal(agg, ragg[0]) and
+                                                     int(rcnt[0]) == js and not rst.any())),
+               cpu_baseline=cpu,
+               speedup_vs_cpu=(value / cpu["value"]) if cpu else None)
+    print(json.dumps(out), flush=True)
 
 
 def leader_main(args):
@@ -626,7 +754,8 @@ def fpvec_main(args):
     idx = honest[np.arange(n) % len(honest)]
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a[idx])).to(dev)
     nonces, pub, helper, lps = T(g["nonce"]), T(g["pub"]), T(g["helper"]), T(g["lps"])
-    eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(10000, 16), vk, device=0)
+    eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(10000, 16), vk, device=0,
+                         allow_unpinned=True)
     for kv in args.opt:
         k, v = kv.split("=")
         eng.set_option(k, int(v))

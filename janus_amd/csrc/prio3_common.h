@@ -1,6 +1,7 @@
 // prio3_common.h -- kernel-side structures and per-lane building blocks shared by the
 // helper engine (prio3_engine.hip) and the synthetic client (prio3_client.hip).
 #pragma once
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -56,7 +57,27 @@ struct InPtrs {
   const uint8_t* pub;
   const uint8_t* helper;
   const uint8_t* leader;
+  // coalesced launches of several tasks: per-report verify-key slot into vk_tab (nullable: the
+  // engine's own key, DevParams::vk)
+  const uint16_t* vk_slot = nullptr;
+  const uint4* vk_tab = nullptr;
 };
+
+// the verify key of report r (query randomness: XOF(vk, dst(5), [PROOFS] || nonce))
+DEV void load_vk(const DevParams& p, const InPtrs& in, uint32_t r, uint32_t vk[4]) {
+  if (in.vk_slot) {
+    const uint4 v = in.vk_tab[in.vk_slot[r]];
+    vk[0] = v.x;
+    vk[1] = v.y;
+    vk[2] = v.z;
+    vk[3] = v.w;
+  } else {
+    vk[0] = p.vk[0];
+    vk[1] = p.vk[1];
+    vk[2] = p.vk[2];
+    vk[3] = p.vk[3];
+  }
+}
 
 struct Scratch {
   void* meas;
@@ -439,7 +460,7 @@ struct Mp64Params {
 };
 
 struct prio3_engine;
-int launch_mp64(prio3_engine* e, uint32_t n, InPtrs in, OutPtrs out, Scratch sc,
+int launch_mp64(prio3_engine* e, uint32_t n, uint32_t ld, InPtrs in, OutPtrs out, Scratch sc,
                 hipStream_t st);
 // P = 16 / 32 ParallelSum(Mul) helper query on lane pairs (prio3_query_pair.hip); false if the
 // instance is not one it takes
@@ -448,59 +469,66 @@ bool launch_query_pair(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, h
 void launch_fpvec_query(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
                         int gs);
 
+struct Slab;
+// The device state of one prepare call (helper or leader) over n reports: the SoA scratch, the
+// device copies of host-buffer inputs/outputs and the fused-accumulate state, carved out of one
+// slab of the GPU's shared scratch pool (prio3_runtime.h).  Reference-counted: every batch handle
+// of the call holds one reference (host entry points), the engine holds one for its latest
+// device-resident call; the slab returns to the pool when the last reference goes.
+struct Run {
+  prio3_engine* e = nullptr;  // engine whose instance / options planned it
+  Slab* slab = nullptr;
+  int device = 0;
+  DevParams dp;    // instance parameters with n, ld, ld_out of this run
+  uint32_t n = 0;  // reports (columns)
+  Scratch sc{};
+  uint8_t *nonces = nullptr, *pub = nullptr, *helper = nullptr, *leader = nullptr,
+          *linput = nullptr, *msgs = nullptr, *status = nullptr;
+  uint16_t* vk_slot = nullptr;
+  uint4* vk_tab = nullptr;
+  // fused accumulate (prio3_device_prepare_aggregate)
+  uint32_t *wpart = nullptr, *wseg = nullptr, *cseg = nullptr, *fix = nullptr;
+  unsigned long long *cpart = nullptr, *agg64 = nullptr;
+  size_t fix_cap = 0;
+  bool fused = false;
+  bool aggregate = false;  // made by prio3_device_prepare_aggregate (finish may follow)
+  uint32_t nseg = 0;
+  const uint32_t* seg = nullptr;
+  std::atomic<int> refs{1};
+  hipStream_t last = nullptr;  // stream of the latest work on the run (its release point)
+};
+
 struct prio3_engine {
   prio3_params params;
   prio3_sizes_t sz;
   DevParams dp;
   int device;
-  hipStream_t stream;
-  uint32_t cap = 0;  // scratch capacity (reports)
-  Scratch sc{};
-  void* d_prep_partial = nullptr;
-  size_t partial_cap = 0;
-  uint64_t* d_pcount = nullptr;
-  uint8_t* d_mask = nullptr;
-  // fused accumulate state
-  uint32_t* d_wpart = nullptr;
-  uint32_t* d_wseg = nullptr;
-  size_t wpart_cap = 0;  // waves
-  unsigned long long* d_agg64 = nullptr;
-  unsigned long long* d_cpart = nullptr;  // per wave-chunk partials
-  uint32_t* d_cseg = nullptr;
-  size_t agg64_cap = 0;
-  uint32_t* d_fix = nullptr;  // [0] = count, then entries
-  size_t fix_cap = 0;
-  uint32_t fused_n = 0, fused_segments = 0;
-  int fused_on = 0;  // last prepare_aggregate used the fused kernels
-  const uint32_t* fused_seg_ptr = nullptr;
+  Run* cur = nullptr;  // the latest device-resident prepare (its output shares stay here)
   int fuse_acc = 1;
   int leader_fast = 1;
-  int chunks = 0;                  // option: prepare in this many stream-overlapped chunks
+  int chunks = 0;            // option: prepare in this many stream-overlapped chunks (0 = auto)
   int64_t fp_sub_bytes = 0;  // option: FPVec per-sub-batch scratch budget (bytes; 0 = auto)
-                                   // (0 = auto: one chunk per 128Ki reports)
-  std::vector<hipStream_t> side;   // side streams for chunked prepare
+  int coalesce = 1;          // option: host-buffer prepare through the coalescing executor
+  // option: PRIO3_FPVEC_BOUNDED_L2 prepares only after this explicit opt-in -- its circuit is a
+  // reconstruction (prio's fixedpoint_l2.rs is not in the reference; parity with prio unpinned)
+  int experimental_fpvec = 0;
+  std::vector<hipStream_t> side;  // side streams for chunked prepare
   std::vector<hipEvent_t> side_ev;
-  hipEvent_t fork_ev = nullptr;  // option: leader role on the helper kernels (Histogram / SumVec, P <= 32)  // option: fused accumulate on/off (A/B)
-  // host-API staging
-  uint32_t io_cap = 0;
-  uint8_t *d_nonces = nullptr, *d_pub = nullptr, *d_helper = nullptr, *d_leader = nullptr,
-          *d_msgs = nullptr, *d_status = nullptr;
-  uint8_t* d_linput = nullptr;  // leader input shares (host leader API)
-  uint32_t linput_cap = 0;
-  uint32_t leader_n = 0;
+  hipEvent_t fork_ev = nullptr;
   int force_slow = 0;
-  int split_xof = 2;  // 2: dual-state k_xofd, 1: k_xof_a + k_jrpart, 0: generic fused k_xof
+  int split_xof = 2;   // 2: dual-state k_xofd, 1: k_xof_a + k_jrpart, 0: generic fused k_xof
   int fp_overlap = 0;  // option: FPVec sub-batches alternate over two side streams (A/B: slower)
-  int fp_gs = 8;      // option: FPVec query chunk-column group (loads in flight per lane): 4/8/16
+  int fp_gs = 8;       // option: FPVec query chunk-column group (loads in flight per lane): 4/8/16
   int qh_prefetch = 1;
   int qh_occ = 3;
   int qh_regs = 0;
   int qpair = 0;  // option: P = 16/32 query on lane pairs (k_query_pair; A/B: slower)
   int timing = 0;
-  Mp64Params mp{};          // PRIO3_SUMVEC_F64_MP only
+  Mp64Params mp{};  // PRIO3_SUMVEC_F64_MP only
   uint64_t* d_sigma64 = nullptr;
   std::vector<KTime> times;
   std::vector<hipEvent_t> ev_pool;
-  std::mutex mu;
+  std::mutex tmu;  // timing bookkeeping (launches may come from several executor threads)
+  std::mutex mu;   // device-resident calls, `cur`, side streams
 };
 

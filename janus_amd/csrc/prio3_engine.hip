@@ -24,12 +24,14 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/janus_prio3.h"
 #include "prio3_device.h"
 
 #include "prio3_common.h"
+#include "prio3_runtime.h"
 #include "sha256_device.h"
 #include "sha256_host.h"
 
@@ -57,7 +59,11 @@ __global__ __launch_bounds__(256, XOFD_OCC) void k_xof(DevParams p, InPtrs in, S
     Msg m;
     msg_zero(m);
     msg_dst(m, p.dst[5]);
-    msg_bytes16(m, 9, p.vk);
+    {
+      uint32_t vk[4];
+      load_vk(p, in, r, vk);
+      msg_bytes16(m, 9, vk);
+    }
     msg_byte(m, 25, 1);
     msg_bytes16(m, 26, nonce);
     msg_absorb_final(s, m, 42);
@@ -242,7 +248,11 @@ __global__ __launch_bounds__(256, XOFD_OCC) void k_xofd(DevParams p, InPtrs in, 
     Msg m;
     msg_zero(m);
     msg_dst(m, p.dst[5]);
-    msg_bytes16(m, 9, p.vk);
+    {
+      uint32_t vk[4];
+      load_vk(p, in, r, vk);
+      msg_bytes16(m, 9, vk);
+    }
     msg_byte(m, 25, 1);
     msg_bytes16(m, 26, nonce);
     msg_absorb_final(s, m, 42);
@@ -452,7 +462,11 @@ __global__ __launch_bounds__(256, XOF_OCC) void k_xof_a(DevParams p, InPtrs in, 
     Msg m;
     msg_zero(m);
     msg_dst(m, p.dst[5]);
-    msg_bytes16(m, 9, p.vk);
+    {
+      uint32_t vk[4];
+      load_vk(p, in, r, vk);
+      msg_bytes16(m, 9, vk);
+    }
     msg_byte(m, 25, 1);
     msg_bytes16(m, 26, nonce);
     msg_absorb_final(s, m, 42);
@@ -746,7 +760,11 @@ __global__ __launch_bounds__(64) void k_xof_slow(DevParams p, InPtrs in, Scratch
   uint32_t w[4];
   BX x, y;
   // query rand
-  bx_init(x, p.dst[5], p.vk);
+  {
+    uint32_t vk[4];
+    load_vk(p, in, r, vk);
+    bx_init(x, p.dst[5], vk);
+  }
   bx_absorb(x, 1);
   bx_absorb_w(x, nonce, 16);
   bx_finalize(x);
@@ -1578,66 +1596,88 @@ __global__ __launch_bounds__(256, 2) void k_query_r(DevParams p, InPtrs in, Scra
 // ------------------------------------------------------------------------------------
 // Accumulate: masked segmented mod-p reduction of output shares
 // ------------------------------------------------------------------------------------
-__global__ void k_mask(uint32_t n, const uint8_t* status, const uint32_t* seg,
-                       const uint8_t* accept, uint32_t s, uint8_t* mask) {
-  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+// Per-report inclusion code: the report's segment if it is counted (status FINISHED, host mask
+// non-zero, segment id < n_segments), else ~0.  A segment id past n_segments excludes the report
+// from every aggregate and count, on every path (fused: k_agg_fix; metadata: k_meta).
+__global__ void k_code(uint32_t n, const uint8_t* status, const uint32_t* seg,
+                       const uint8_t* accept, uint32_t nseg, uint32_t* code) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
-  bool ok = status[r] == PRIO3_STATUS_FINISHED;
-  if (seg) ok = ok && seg[r] == s;
-  if (accept) ok = ok && accept[r] != 0;
-  mask[r] = ok ? 1 : 0;
+  const uint32_t s = seg ? seg[r] : 0u;
+  const bool ok = status[r] == PRIO3_STATUS_FINISHED && s < nseg && (!accept || accept[r]);
+  code[r] = ok ? s : 0xffffffffu;
 }
 
-// grid: x = output element, y = report chunk.  Block of 256 sums its chunk of the row.
-template <class F>
-__global__ __launch_bounds__(256) void k_acc_partial(uint32_t n, size_t ld, uint32_t chunk,
-                                                     uint32_t out_len, const void* src,
-                                                     const uint8_t* mask, void* partial,
-                                                     uint64_t* pcount) {
+// Segmented partial sums in one pass over the output shares.  grid: x = output element, y =
+// report chunk, z = group of SG segments; each thread keeps SG running sums (one per segment of
+// its group) and the block reduces them through LDS into partial[chunk][segment][element]
+// (counts into pcount[chunk][segment] from the element-0 blocks).
+template <class F, int SG>
+__global__ __launch_bounds__(256) void k_acc_seg(uint32_t n, size_t ld, uint32_t chunk,
+                                                 uint32_t out_len, uint32_t nseg, const void* src,
+                                                 const uint32_t* code, void* partial,
+                                                 uint64_t* pcount) {
   typedef typename F::T T;
   __shared__ T red[256];
   __shared__ uint32_t cred[256];
-  const uint32_t e = blockIdx.x, c = blockIdx.y;
+  const uint32_t e = blockIdx.x, c = blockIdx.y, s0 = blockIdx.z * SG;
   const uint32_t lo = c * chunk, hi = min(n, lo + chunk);
-  T acc = F::zero();
-  uint32_t cnt = 0;
+  T acc[SG];
+  uint32_t cnt[SG];
+#pragma unroll
+  for (int q = 0; q < SG; q++) {
+    acc[q] = F::zero();
+    cnt[q] = 0;
+  }
   for (uint32_t r = lo + threadIdx.x; r < hi; r += 256) {
-    if (mask[r]) {
-      acc = F::add(acc, F::load(src, (size_t)e * ld + r));
-      cnt++;
+    const uint32_t k = code[r] - s0;  // ~0 (excluded) wraps past SG
+    if (k < (uint32_t)SG) {
+      const T x = F::load(src, (size_t)e * ld + r);
+#pragma unroll
+      for (int q = 0; q < SG; q++)
+        if ((uint32_t)q == k) {
+          acc[q] = F::add(acc[q], x);
+          cnt[q]++;
+        }
     }
   }
-  red[threadIdx.x] = acc;
-  cred[threadIdx.x] = cnt;
-  __syncthreads();
-  for (uint32_t s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) {
-      red[threadIdx.x] = F::add(red[threadIdx.x], red[threadIdx.x + s]);
-      cred[threadIdx.x] += cred[threadIdx.x + s];
+#pragma unroll
+  for (int q = 0; q < SG; q++) {
+    if (s0 + q >= nseg) break;  // uniform
+    red[threadIdx.x] = acc[q];
+    cred[threadIdx.x] = cnt[q];
+    __syncthreads();
+    for (uint32_t st = 128; st > 0; st >>= 1) {
+      if (threadIdx.x < st) {
+        red[threadIdx.x] = F::add(red[threadIdx.x], red[threadIdx.x + st]);
+        cred[threadIdx.x] += cred[threadIdx.x + st];
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      F::store(partial, ((size_t)c * nseg + s0 + q) * out_len + e, red[0]);
+      if (e == 0) pcount[(size_t)c * nseg + s0 + q] = cred[0];
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    F::store(partial, (size_t)c * out_len + e, red[0]);
-    if (e == 0) pcount[c] = cred[0];
-  }
 }
 
+// grid (ceil(out_len / 256), nseg): per segment and element, the sum over the chunk partials
 template <class F>
-__global__ void k_acc_final(uint32_t nchunks, uint32_t out_len, const void* partial,
-                            const uint64_t* pcount, uint8_t* agg, uint64_t* count) {
+__global__ void k_acc_fin(uint32_t nchunks, uint32_t out_len, uint32_t nseg, const void* partial,
+                          const uint64_t* pcount, uint8_t* agg, uint64_t* count) {
   typedef typename F::T T;
-  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x, s = blockIdx.y;
   if (e < out_len) {
     T acc = F::zero();
     for (uint32_t c = 0; c < nchunks; c++)
-      acc = F::add(acc, F::load(partial, (size_t)c * out_len + e));
-    F::store(agg, e, acc);
+      acc = F::add(acc, F::load(partial, ((size_t)c * nseg + s) * out_len + e));
+    F::store(agg, (size_t)s * out_len + e, acc);
   }
   if (e == 0) {
-    uint64_t s = 0;
-    for (uint32_t c = 0; c < nchunks; c++) s += pcount[c];
-    *count = s;
+    uint64_t t = 0;
+    for (uint32_t c = 0; c < nchunks; c++) t += pcount[(size_t)c * nseg + s];
+    count[s] = t;
   }
 }
 
@@ -2006,9 +2046,18 @@ __global__ void k_selftest_f128(int op, uint32_t n, const uint4* a, const uint4*
 // ====================================================================================
 
 
+// ====================================================================================
+// Host side
+// ====================================================================================
+
+// A batch handle: one job's column range of a (possibly coalesced, shared) device run.  Every
+// handle owns its reference, so concurrent jobs of one engine never see each other's output
+// shares or verdicts (the run's slab stays out of the pool until the last handle is freed).
+// Handles must be freed before their engine is destroyed.
 struct prio3_batch {
   prio3_engine* e;
-  uint32_t n;
+  Run* run;  // nullptr for an empty batch
+  uint32_t c0, n;
 };
 
 static uint32_t next_pow2(uint32_t n) {
@@ -2226,25 +2275,73 @@ static int fill_sizes(const prio3_params* pp, prio3_sizes_t* s, DevParams* dp) {
     }                                                                               \
   } while (0)
 
-// Scratch for n reports.  All-or-nothing: on any allocation failure every buffer is freed and
-// the engine is left with cap = 0 (the next call re-sizes from scratch), so no later call can
-// launch on a stale capacity with null or short buffers.
-static void free_scratch(prio3_engine* e) {
-  void** bufs[] = {&e->sc.meas, &e->sc.proofs, &e->sc.jr, &e->sc.qr, (void**)&e->sc.part,
-                   (void**)&e->sc.corrected, (void**)&e->sc.flag, &e->sc.Lbuf, &e->sc.PVbuf,
-                   &e->sc.acc, &e->sc.out, &e->sc.beta, (void**)&e->d_mask};
-  for (auto b : bufs)
-    if (*b) {
-      (void)hipFree(*b);
-      *b = nullptr;
-    }
-  e->cap = 0;
-  e->dp.ld = e->dp.ld_out = 0;
+
+// ---- per-kernel timing (option "timing"): HIP events on the launch stream ----
+struct Pending {
+  prio3_engine* e;
+  size_t idx;
+  hipEvent_t a, b;
+};
+static std::vector<Pending>& pending() {
+  static thread_local std::vector<Pending> v;
+  return v;
 }
+static size_t time_slot(prio3_engine* e, const char* name) {
+  std::lock_guard<std::mutex> lk(e->tmu);
+  for (size_t i = 0; i < e->times.size(); i++)
+    if (e->times[i].name == name) return i;
+  e->times.push_back(KTime{name, 0, 0});
+  return e->times.size() - 1;
+}
+#define TIMED(e, st, name, launch)                                   \
+  do {                                                               \
+    hipEvent_t _a = nullptr, _b = nullptr;                           \
+    const bool _t = (e)->timing && hipEventCreate(&_a) == hipSuccess && \
+                    hipEventCreate(&_b) == hipSuccess;               \
+    if (_t) (void)hipEventRecord(_a, st);                            \
+    launch;                                                          \
+    HIPCHK(hipGetLastError());                                       \
+    if (_t) {                                                        \
+      (void)hipEventRecord(_b, st);                                  \
+      pending().push_back(Pending{(e), time_slot(e, name), _a, _b}); \
+    }                                                                \
+  } while (0)
+
+// folds this thread's finished timing events of engine e into e->times
+static void collect_times(prio3_engine* e) {
+  auto& v = pending();
+  std::vector<Pending> keep;
+  for (auto& pd : v) {
+    if (pd.e != e) {
+      keep.push_back(pd);
+      continue;
+    }
+    float ms = 0;
+    (void)hipEventSynchronize(pd.b);
+    (void)hipEventElapsedTime(&ms, pd.a, pd.b);
+    {
+      std::lock_guard<std::mutex> lk(e->tmu);
+      e->times[pd.idx].ms += ms;
+      e->times[pd.idx].launches += 1;
+    }
+    (void)hipEventDestroy(pd.a);
+    (void)hipEventDestroy(pd.b);
+  }
+  v.swap(keep);
+}
+
+// ---- runs: the device state of one prepare call, carved from one pooled slab ----
+enum : unsigned {
+  RUN_SCRATCH = 1,  // SoA prepare scratch
+  RUN_IO = 2,       // device copies of host inputs / outputs (host-buffer entry points)
+  RUN_VK = 4,       // per-report verify-key slots + key table (coalesced launches)
+  RUN_LINPUT = 8,   // leader input shares (host-buffer leader entry point)
+  RUN_FUSED = 16,   // fused-accumulate partials (prio3_device_prepare_aggregate, Histogram)
+};
 
 // FPVec per-report scratch bytes of one sub-batch column: every buffer indexed [row][column]
 // with the sub-batch leading dimension ld (meas, proofs, jr, qr, part, corrected, flag, L, PV,
-// beta); the output shares and the accumulate mask have one column per report of the batch.
+// beta); the output shares have one column per report of the batch (ld_out).
 static size_t fp_column_bytes(const DevParams& d) {
   const size_t es = d.es;
   return es * ((size_t)d.meas_len + d.proof_len + d.jr_len + d.qr_len + 2 * ((size_t)d.P + d.P1) +
@@ -2252,268 +2349,203 @@ static size_t fp_column_bytes(const DevParams& d) {
          16 + 16 + 1;
 }
 
-static int ensure_scratch(prio3_engine* e, uint32_t n) {
-  if (n <= e->cap) return PRIO3_OK;
-  free_scratch(e);
-  const uint32_t ld_out = (n + 63) & ~63u;
-  uint32_t ld = ld_out;
-  const DevParams& d = e->dp;
-  size_t es = d.es;
-  const bool fp = d.kind == PRIO3_FPVEC_BOUNDED_L2;
-  if (fp) {  // per-report scratch for one sub-batch (2.56 MB of meas share per report at 10^4)
-    const size_t per = fp_column_bytes(d);
-    int64_t budget = e->fp_sub_bytes;
-    if (budget <= 0) {
-      // auto: free HBM minus the batch's output shares and mask (one column per report) and a
-      // fixed reserve for the runtime (kernel scratch / private segments, queues, the caller's
-      // allocator).  The kernels are latency-bound per lane, so the widest sub-batch wins
-      // (MI355X, 100k x 10^4: 48 GB -> 43.7K/s, 180 GB -> 112K/s).
-      size_t fr = 0, tot = 0;
-      HIPCHK(hipMemGetInfo(&fr, &tot));
-      const int64_t outb = (int64_t)(es * d.out_len * ld_out + 64 * (size_t)ld_out);
-      const int64_t reserve = std::max<int64_t>((int64_t)8 << 30, (int64_t)(0.10 * (double)tot));
-      budget = (int64_t)fr - outb - reserve;
-    }
-    uint64_t cols = (uint64_t)std::max<int64_t>(budget, 1) / per;
-    cols = std::max<uint64_t>(256, cols & ~255ull);
-    ld = (uint32_t)std::min<uint64_t>(ld_out, cols);
-  }
-  void** bufs[] = {&e->sc.meas, &e->sc.proofs, &e->sc.jr, &e->sc.qr, (void**)&e->sc.part,
-                   (void**)&e->sc.corrected, (void**)&e->sc.flag, &e->sc.Lbuf, &e->sc.PVbuf,
-                   &e->sc.acc, &e->sc.out, &e->sc.beta, (void**)&e->d_mask};
-  const bool own_out = d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC ||
-                       d.kind == PRIO3_SUMVEC_F64_MP || fp;
-  const size_t sizes[] = {es * d.meas_len * ld, es * d.proof_len * ld,
-                          es * (d.jr_len ? d.jr_len : 1) * ld, es * d.qr_len * ld, 16 * (size_t)ld,
-                          16 * (size_t)ld, (size_t)ld, es * (d.P + d.P1) * ld,
-                          es * (d.P + d.P1) * ld, fp ? 16 : es * d.arity * ld,
-                          own_out ? es * d.out_len * ld_out : 16, es * d.calls * ld,
-                          (size_t)ld_out};
-  static_assert(sizeof(sizes) / sizeof(sizes[0]) == sizeof(bufs) / sizeof(bufs[0]), "");
-  for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]); i++) {
-    const hipError_t err = hipMalloc(bufs[i], sizes[i]);
-    if (err != hipSuccess) {
-      fprintf(stderr, "janus_prio3: scratch allocation of %zu bytes failed (%s)\n", sizes[i],
-              hipGetErrorString(err));
+// FPVec sub-batch width: the per-report scratch (2.6 MB at 10^4 entries) of a whole batch does
+// not fit, so the batch runs in equal sub-batches of ld columns.  Auto budget: free HBM plus the
+// pool's idle slabs, minus the batch's output shares and a fixed reserve for the runtime
+// (private segments, queues, the caller's allocator) -- the r01u hipErrorIllegalAddress came
+// with a budget of 85% of free HBM and did not recur with an explicit reserve.
+// The kernels are latency-bound per lane, so the widest sub-batch wins.
+static uint32_t fp_sub_ld(const prio3_engine* e, const DevParams& d, uint32_t ld_out) {
+  const size_t per = fp_column_bytes(d);
+  int64_t budget = e->fp_sub_bytes;
+  if (budget <= 0) {
+    size_t fr = 0, tot = 0, idle = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
       (void)hipGetLastError();
-      free_scratch(e);
-      return PRIO3_EDEVICE;
+      fr = tot = 0;
     }
+    (void)ws_pool_bytes(e->device, &idle);
+    const int64_t outb = (int64_t)(d.es * d.out_len * (size_t)ld_out + 64 * (size_t)ld_out);
+    const int64_t reserve = std::max<int64_t>((int64_t)8 << 30, (int64_t)(0.10 * (double)tot));
+    budget = (int64_t)(fr + idle) - outb - reserve;
   }
-  e->cap = ld_out;
-  e->dp.ld = ld;
-  e->dp.ld_out = ld_out;
+  uint64_t cols = (uint64_t)std::max<int64_t>(budget, 1) / per;
+  cols = std::max<uint64_t>(256, cols & ~255ull);
+  return (uint32_t)std::min<uint64_t>(ld_out, cols);
+}
+
+static bool own_out(const DevParams& d) {  // the output share is not the measurement share
+  return d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC || d.kind == PRIO3_SUMVEC_F64_MP ||
+         d.kind == PRIO3_FPVEC_BOUNDED_L2;
+}
+
+constexpr uint32_t WCH_HOST = 32;  // waves per fused-partial chunk (k_agg_waves WCH)
+
+// Lays the run's buffers out from `base` (nullptr: sizes only), 256-byte aligned.
+static size_t run_carve(Run* R, unsigned flags, uint32_t n_keys, uint8_t* base) {
+  const DevParams& d = R->dp;
+  const size_t es = d.es, ld = d.ld, ldo = d.ld_out, n = R->n ? R->n : 1;
+  size_t off = 0;
+  auto take = [&](auto** ptr, size_t bytes) {
+    *ptr = base ? (std::remove_pointer_t<decltype(ptr)>)(base + off) : nullptr;
+    off += (bytes + 255) & ~(size_t)255;
+  };
+  if (flags & RUN_SCRATCH) {
+    const bool fp = d.kind == PRIO3_FPVEC_BOUNDED_L2;
+    take(&R->sc.meas, es * d.meas_len * ld);
+    take(&R->sc.proofs, es * d.proof_len * ld);
+    take(&R->sc.jr, es * (d.jr_len ? d.jr_len : 1) * ld);
+    take(&R->sc.qr, es * d.qr_len * ld);
+    take(&R->sc.part, 16 * ld);
+    take(&R->sc.corrected, 16 * ld);
+    take(&R->sc.flag, ld);
+    take(&R->sc.Lbuf, es * ((size_t)d.P + d.P1) * ld);
+    take(&R->sc.PVbuf, es * ((size_t)d.P + d.P1) * ld);
+    take(&R->sc.acc, fp ? 16 : es * d.arity * ld);
+    take(&R->sc.out, own_out(d) ? es * d.out_len * ldo : 16);
+    take(&R->sc.beta, es * d.calls * ld);
+  }
+  if (flags & RUN_IO) {
+    const size_t ml = R->e->sz.prep_msg_len ? R->e->sz.prep_msg_len : 16;
+    take(&R->nonces, 16 * n);
+    take(&R->pub, (size_t)(d.public_share_len ? d.public_share_len : 16) * n);
+    take(&R->helper, (size_t)d.helper_share_len * n);
+    take(&R->leader, (size_t)d.prep_share_len * n);
+    take(&R->msgs, ml * n);
+    take(&R->status, n);
+  }
+  if (flags & RUN_LINPUT) take(&R->linput, (size_t)d.leader_share_len * n);
+  if (flags & RUN_VK) {
+    take(&R->vk_slot, 2 * n);
+    take(&R->vk_tab, 16 * (size_t)(n_keys ? n_keys : 1));
+  }
+  if (flags & RUN_FUSED) {
+    const size_t waves = (n + 63) / 64, M = d.meas_len, chunks = (waves + WCH_HOST - 1) / WCH_HOST;
+    take(&R->wpart, waves * M * 8 * sizeof(uint32_t));
+    take(&R->wseg, waves * sizeof(uint32_t));
+    take(&R->cpart, chunks * M * 8 * 8);
+    take(&R->cseg, chunks * sizeof(uint32_t));
+    take(&R->agg64, (size_t)(R->nseg ? R->nseg : 1) * M * 8 * 8);
+    take(&R->fix, (n + 1) * sizeof(uint32_t));
+  }
+  return off;
+}
+
+static Run* run_create(prio3_engine* e, uint32_t n, unsigned flags, uint32_t nseg,
+                       uint32_t n_keys, hipStream_t st, int* rc) {
+  Run* R = new Run();
+  R->e = e;
+  R->device = e->device;
+  R->n = n;
+  R->nseg = nseg;
+  R->dp = e->dp;
+  R->dp.n = n;
+  R->dp.nseg = nseg ? nseg : 1;
+  const uint32_t ld_out = ((n ? n : 1) + 63) & ~63u;
+  R->dp.ld_out = ld_out;
+  R->dp.ld = (flags & RUN_SCRATCH) && e->dp.kind == PRIO3_FPVEC_BOUNDED_L2
+                 ? fp_sub_ld(e, e->dp, ld_out)
+                 : ld_out;
+  const size_t bytes = run_carve(R, flags, n_keys, nullptr);
+  R->slab = ws_acquire(e->device, bytes, st, rc);
+  if (!R->slab) {
+    delete R;
+    return nullptr;
+  }
+  run_carve(R, flags, n_keys, R->slab->base);
+  R->fix_cap = (size_t)n + 1;
+  R->last = st;
+  return R;
+}
+
+// drops one reference; the last one returns the slab to the pool, ordered after `st` (or the
+// stream of the run's latest work)
+static void run_release(Run* R, hipStream_t st, bool use_st) {
+  if (!R) return;
+  if (R->refs.fetch_sub(1) != 1) return;
+  ws_release(R->slab, use_st ? st : R->last);
+  delete R;
+}
+
+// ---- one-pass segmented accumulate over columns [c0, c0 + n) of a run ----
+// d_status[n] (the run's verdicts for those columns), d_seg[n] (nullable: segment 0), d_accept[n]
+// (nullable: all accepted); d_agg[nseg][out_len * es], d_counts[nseg].
+static int run_accumulate(prio3_engine* e, Run* R, uint32_t c0, uint32_t n,
+                          const uint8_t* d_status, const uint32_t* d_seg, const uint8_t* d_accept,
+                          uint32_t nseg, uint8_t* d_agg, uint64_t* d_counts, hipStream_t st) {
+  const DevParams& d = R->dp;
+  const size_t es = d.es, agg_len = (size_t)d.out_len * es;
+  if (n == 0) {
+    HIPCHK(hipMemsetAsync(d_agg, 0, agg_len * nseg, st));
+    HIPCHK(hipMemsetAsync(d_counts, 0, 8 * (size_t)nseg, st));
+    return PRIO3_OK;
+  }
+  const uint32_t chunk = 8192, nchunks = (n + chunk - 1) / chunk;
+  const size_t code_b = ((size_t)4 * n + 255) & ~(size_t)255;
+  const size_t part_b = ((size_t)nchunks * nseg * agg_len + 255) & ~(size_t)255;
+  int rc = PRIO3_OK;
+  Slab* tmp = ws_acquire(R->device, code_b + part_b + 8 * (size_t)nchunks * nseg, st, &rc);
+  if (!tmp) return rc;
+  uint32_t* code = (uint32_t*)tmp->base;
+  void* partial = tmp->base + code_b;
+  uint64_t* pcount = (uint64_t*)(tmp->base + code_b + part_b);
+  const uint8_t* src = (const uint8_t*)(own_out(d) ? R->sc.out : R->sc.meas) + es * c0;
+  const size_t ld = d.ld_out;  // output shares: one column per report of the run
+  auto body = [&]() -> int {
+    TIMED(e, st, "k_code",
+          (k_code<<<(n + 255) / 256, 256, 0, st>>>(n, d_status, d_seg, d_accept, nseg, code)));
+    const int SG = nseg == 1 ? 1 : nseg <= 4 ? 4 : 8;
+    dim3 grid(d.out_len, nchunks, (nseg + SG - 1) / SG);
+    dim3 gfin((d.out_len + 255) / 256, nseg);
+    if (es == 16) {
+      if (SG == 1)
+        TIMED(e, st, "k_acc_seg", (k_acc_seg<Fp128, 1><<<grid, 256, 0, st>>>(n, ld, chunk, d.out_len, nseg, src, code, partial, pcount)));
+      else if (SG == 4)
+        TIMED(e, st, "k_acc_seg", (k_acc_seg<Fp128, 4><<<grid, 256, 0, st>>>(n, ld, chunk, d.out_len, nseg, src, code, partial, pcount)));
+      else
+        TIMED(e, st, "k_acc_seg", (k_acc_seg<Fp128, 8><<<grid, 256, 0, st>>>(n, ld, chunk, d.out_len, nseg, src, code, partial, pcount)));
+      TIMED(e, st, "k_acc_fin", (k_acc_fin<Fp128><<<gfin, 256, 0, st>>>(nchunks, d.out_len, nseg, partial, pcount, d_agg, d_counts)));
+    } else {
+      if (SG == 1)
+        TIMED(e, st, "k_acc_seg", (k_acc_seg<Fp64, 1><<<grid, 256, 0, st>>>(n, ld, chunk, d.out_len, nseg, src, code, partial, pcount)));
+      else if (SG == 4)
+        TIMED(e, st, "k_acc_seg", (k_acc_seg<Fp64, 4><<<grid, 256, 0, st>>>(n, ld, chunk, d.out_len, nseg, src, code, partial, pcount)));
+      else
+        TIMED(e, st, "k_acc_seg", (k_acc_seg<Fp64, 8><<<grid, 256, 0, st>>>(n, ld, chunk, d.out_len, nseg, src, code, partial, pcount)));
+      TIMED(e, st, "k_acc_fin", (k_acc_fin<Fp64><<<gfin, 256, 0, st>>>(nchunks, d.out_len, nseg, partial, pcount, d_agg, d_counts)));
+    }
+    return PRIO3_OK;
+  };
+  rc = body();
+  ws_release(tmp, st);
+  R->last = st;
+  return rc;
+}
+
+// columns [c0, c0 + n) of the run's output shares to host, per report (n x out_len x es)
+static int run_output_shares(Run* R, uint32_t c0, uint32_t n, uint8_t* out, hipStream_t st) {
+  const DevParams& d = R->dp;
+  const size_t es = d.es;
+  if (n == 0) return PRIO3_OK;
+  const uint8_t* src = (const uint8_t*)(own_out(d) ? R->sc.out : R->sc.meas) + es * c0;
+  std::vector<uint8_t> soa((size_t)d.out_len * n * es);
+  HIPCHK(hipMemcpy2DAsync(soa.data(), n * es, src, (size_t)d.ld_out * es, n * es, d.out_len,
+                          hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  for (uint32_t r = 0; r < n; r++)
+    for (uint32_t i = 0; i < d.out_len; i++)
+      memcpy(out + ((size_t)r * d.out_len + i) * es, soa.data() + ((size_t)i * n + r) * es, es);
   return PRIO3_OK;
 }
 
-static hipEvent_t get_event(prio3_engine* e) {
-  hipEvent_t ev;
-  (void)hipEventCreate(&ev);
-  e->ev_pool.push_back(ev);
-  return ev;
-}
-
-// launch wrapper that optionally brackets the kernel with events
-struct Pending {
-  size_t idx;
-  hipEvent_t a, b;
+// a pooled stream for one blocking host-buffer call
+struct PooledStream {
+  int device;
+  hipStream_t s;
+  explicit PooledStream(int dev) : device(dev), s(ws_stream_get(dev)) {}
+  ~PooledStream() { ws_stream_put(device, s); }
 };
-static std::vector<Pending>& pending(prio3_engine* e) {
-  static thread_local std::vector<Pending> v;
-  (void)e;
-  return v;
-}
-static size_t time_slot(prio3_engine* e, const char* name) {
-  for (size_t i = 0; i < e->times.size(); i++)
-    if (e->times[i].name == name) return i;
-  e->times.push_back(KTime{name, 0, 0});
-  return e->times.size() - 1;
-}
-#define TIMED(e, st, name, launch)                            \
-  do {                                                        \
-    hipEvent_t _a = nullptr, _b = nullptr;                    \
-    if ((e)->timing) {                                        \
-      _a = get_event(e);                                      \
-      _b = get_event(e);                                      \
-      (void)hipEventRecord(_a, st);                           \
-    }                                                         \
-    launch;                                                   \
-    HIPCHK(hipGetLastError());                                \
-    if ((e)->timing) {                                        \
-      (void)hipEventRecord(_b, st);                           \
-      pending(e).push_back(Pending{time_slot(e, name), _a, _b}); \
-    }                                                         \
-  } while (0)
 
-static void collect_times(prio3_engine* e) {
-  auto& v = pending(e);
-  for (auto& pd : v) {
-    float ms = 0;
-    (void)hipEventSynchronize(pd.b);
-    (void)hipEventElapsedTime(&ms, pd.a, pd.b);
-    e->times[pd.idx].ms += ms;
-    e->times[pd.idx].launches += 1;
-  }
-  v.clear();
-  for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
-  e->ev_pool.clear();
-}
-
-extern "C" {
-
-int prio3_sizes(const prio3_params* params, prio3_sizes_t* out) {
-  return fill_sizes(params, out, nullptr);
-}
-
-int prio3_engine_create_ex(const prio3_params* params, const uint8_t* verify_key,
-                           size_t verify_key_len, int device, prio3_engine** out) {
-  if (!params || !verify_key || !out) return PRIO3_EINVAL;
-  const bool mp = params->kind == PRIO3_SUMVEC_F64_MP;
-  if (verify_key_len != (mp ? 32u : 16u)) return PRIO3_EINVAL;
-  prio3_engine* e = new prio3_engine();
-  int rc = fill_sizes(params, &e->sz, &e->dp);
-  if (rc) {
-    delete e;
-    return rc;
-  }
-  e->params = *params;
-  if (!mp) memcpy(e->dp.vk, verify_key, 16);
-  e->device = device;
-  if (hipSetDevice(device) != hipSuccess ||
-      hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete e;
-    return PRIO3_EDEVICE;
-  }
-  if (mp) {  // prio3_mp64.hip constants
-    const DevParams& d = e->dp;
-    Mp64Params& m = e->mp;
-    m.meas_len = d.meas_len;
-    m.out_len = d.out_len;
-    m.bits = params->bits;
-    m.chunk = params->chunk_length;
-    m.calls = d.calls;
-    m.P = d.P;
-    m.logP = d.logP;
-    m.glen = d.glen;
-    m.np = params->num_proofs;
-    m.proof_len = d.proof_len / m.np;
-    m.arity = d.arity;
-    m.vlen = d.verifier_len;
-    memcpy(m.dst, d.dst, sizeof m.dst);
-    hmac_midstates_host(verify_key, 32, m.vk_ist, m.vk_ost);
-    static const uint8_t zero32[32] = {0};
-    hmac_midstates_host(zero32, 32, m.z_ist, m.z_ost);
-    const u128 alpha = d.roots64[d.logP];
-    m.alpha = (uint64_t)alpha;
-    m.alpha_inv = (uint64_t)hpow(alpha, d.P - 1, HP64);
-    m.invP = d.invP64;
-    m.half = d.half64;
-    std::vector<uint64_t> sig(d.P);
-    for (uint32_t e2 = 0; e2 < d.P; e2++) {
-      const u128 ae = hpow(alpha, e2, HP64);
-      u128 sum = 0, x = 1;
-      for (uint32_t c = 1; c <= d.calls; c++) {
-        x = hmul(x, ae, HP64);
-        sum = (sum + x) % HP64;
-      }
-      sig[e2] = (uint64_t)sum;
-    }
-    if (hipMalloc((void**)&e->d_sigma64, 8 * (size_t)d.P) != hipSuccess ||
-        hipMemcpy(e->d_sigma64, sig.data(), 8 * (size_t)d.P, hipMemcpyHostToDevice) !=
-            hipSuccess) {
-      (void)hipStreamDestroy(e->stream);
-      delete e;
-      return PRIO3_EDEVICE;
-    }
-    m.sigma = e->d_sigma64;
-  }
-  *out = e;
-  return PRIO3_OK;
-}
-
-int prio3_engine_create(const prio3_params* params, const uint8_t verify_key[16], int device,
-                        prio3_engine** out) {
-  return prio3_engine_create_ex(params, verify_key, 16, device, out);
-}
-
-void prio3_engine_destroy(prio3_engine* e) {
-  if (!e) return;
-  (void)hipSetDevice(e->device);
-  (void)hipStreamSynchronize(e->stream);
-  void* bufs[] = {e->sc.meas, e->sc.proofs, e->sc.jr, e->sc.qr, e->sc.part, e->sc.corrected,
-                  e->sc.flag, e->sc.Lbuf, e->sc.PVbuf, e->sc.acc, e->sc.out, e->sc.beta, e->d_mask,
-                  e->d_prep_partial, e->d_pcount, e->d_nonces, e->d_pub, e->d_helper,
-                  e->d_leader, e->d_msgs, e->d_status, e->d_wpart, e->d_wseg, e->d_agg64,
-                  e->d_fix, e->d_cpart, e->d_cseg, e->d_linput, e->d_sigma64};
-  for (auto b : bufs)
-    if (b) (void)hipFree(b);
-  for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
-  for (auto s2 : e->side) (void)hipStreamDestroy(s2);
-  for (auto j : e->side_ev) (void)hipEventDestroy(j);
-  if (e->fork_ev) (void)hipEventDestroy(e->fork_ev);
-  (void)hipStreamDestroy(e->stream);
-  delete e;
-}
-
-int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
-  if (!e || !key) return PRIO3_EINVAL;
-  if (!strcmp(key, "force_slow_path")) {
-    e->force_slow = (int)value;
-    return PRIO3_OK;
-  }
-  if (!strcmp(key, "chunks")) {
-    e->chunks = (int)value;
-    return PRIO3_OK;
-  }
-  if (!strcmp(key, "fp_sub_bytes")) {  // FPVec scratch budget per sub-batch (next allocation;
-    if (value < 0) return PRIO3_EINVAL;  // 0 = auto, sized from free HBM)
-    e->fp_sub_bytes = value;
-    e->cap = 0;  // re-size on the next call
-    return PRIO3_OK;
-  }
-  if (!strcmp(key, "leader_fast")) {
-    e->leader_fast = (int)value;
-    return PRIO3_OK;
-  }
-  if (!strcmp(key, "fuse_acc")) {
-    e->fuse_acc = (int)value;
-    return PRIO3_OK;
-  }
-  if (!strcmp(key, "qpair")) {
-    e->qpair = (int)value;
-    return PRIO3_OK;
-  }
-  if (!strcmp(key, "qh_regs")) {
-    e->qh_regs = (int)value;
-    return PRIO3_OK;
-  }
-  if (!strcmp(key, "qh_occ")) {
-    e->qh_occ = (int)value;
-    return PRIO3_OK;
-  }
-  if (!strcmp(key, "qh_prefetch")) {
-    e->qh_prefetch = (int)value;
-    return PRIO3_OK;
-  }
-  if (!strcmp(key, "split_xof")) {
-    e->split_xof = (int)value;
-    return PRIO3_OK;
-  }
-  if (!strcmp(key, "fp_overlap")) {
-    e->fp_overlap = value ? 1 : 0;
-    return PRIO3_OK;
-  }
-  if (!strcmp(key, "fp_gs")) {
-    if (value != 4 && value != 8 && value != 16) return PRIO3_EINVAL;
-    e->fp_gs = (int)value;
-    return PRIO3_OK;
-  }
-  if (!strcmp(key, "timing")) {
-    e->timing = (int)value;
-    return PRIO3_OK;
-  }
-  return PRIO3_EINVAL;
-}
 
 // The fused accumulate applies where the output share is the measurement share (Histogram;
 // truncate is the identity) and the joint-rand kernel streams that share.
@@ -2522,39 +2554,6 @@ static bool fusable(const prio3_engine* e) {
          (e->split_xof == 1 || (e->split_xof == 2 && (42 + e->dp.meas_len * 16) / 168 >= 2));
 }
 
-static int ensure_fused(prio3_engine* e, uint32_t n, uint32_t n_segments) {
-  const size_t waves = (n + 63) / 64, M = e->dp.meas_len;
-  if (waves > e->wpart_cap) {
-    if (e->d_wpart) (void)hipFree(e->d_wpart);
-    if (e->d_wseg) (void)hipFree(e->d_wseg);
-    e->d_wpart = nullptr;
-    e->d_wseg = nullptr;
-    HIPCHK(hipMalloc((void**)&e->d_wpart, waves * M * 8 * sizeof(uint32_t)));
-    HIPCHK(hipMalloc((void**)&e->d_wseg, waves * sizeof(uint32_t)));
-    const size_t chunks = (waves + WCH - 1) / WCH;
-    if (e->d_cpart) (void)hipFree(e->d_cpart);
-    if (e->d_cseg) (void)hipFree(e->d_cseg);
-    HIPCHK(hipMalloc((void**)&e->d_cpart, chunks * M * 8 * 8));
-    HIPCHK(hipMalloc((void**)&e->d_cseg, chunks * sizeof(uint32_t)));
-    e->wpart_cap = waves;
-  }
-  if ((size_t)n_segments * M * 8 > e->agg64_cap) {
-    if (e->d_agg64) (void)hipFree(e->d_agg64);
-    e->d_agg64 = nullptr;
-    HIPCHK(hipMalloc((void**)&e->d_agg64, (size_t)n_segments * M * 8 * 8));
-    e->agg64_cap = (size_t)n_segments * M * 8;
-  }
-  if ((size_t)n + 1 > e->fix_cap) {
-    if (e->d_fix) (void)hipFree(e->d_fix);
-    e->d_fix = nullptr;
-    HIPCHK(hipMalloc((void**)&e->d_fix, ((size_t)n + 1) * sizeof(uint32_t)));
-    e->fix_cap = (size_t)n + 1;
-  }
-  return PRIO3_OK;
-}
-
-// The kernel sequence for reports [c0, c0 + n) of the batch: every pointer is shifted to the
-// chunk (SoA scratch keeps the batch's leading dimension, so a chunk is a column range).
 // side streams + their join events and the fork event, created once per engine
 static int ensure_side_streams(prio3_engine* e) {
   while (e->side.size() < 2) {
@@ -2569,9 +2568,9 @@ static int ensure_side_streams(prio3_engine* e) {
   return PRIO3_OK;
 }
 
-static int launch_prepare(prio3_engine* e, uint32_t c0, uint32_t n, InPtrs in, OutPtrs out,
-                          Scratch sc, hipStream_t st, bool fuse) {
-  DevParams dp = e->dp;
+static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, uint32_t n,
+                          InPtrs in, OutPtrs out, Scratch sc, hipStream_t st, bool fuse) {
+  DevParams dp = base;
   dp.n = n;
   dp.force_slow = (uint32_t)e->force_slow;
   const size_t es = dp.es;
@@ -2579,6 +2578,7 @@ static int launch_prepare(prio3_engine* e, uint32_t c0, uint32_t n, InPtrs in, O
   if (in.pub) in.pub += (size_t)dp.public_share_len * c0;
   in.helper += (size_t)dp.helper_share_len * c0;
   in.leader += (size_t)dp.prep_share_len * c0;
+  if (in.vk_slot) in.vk_slot += c0;
   out.prep_msgs += (size_t)(dp.kind == PRIO3_SUMVEC_F64_MP ? 32 : 16) * c0;
   out.status += c0;
   void** soa[] = {&sc.meas, &sc.proofs, &sc.jr, &sc.qr, &sc.Lbuf, &sc.PVbuf, &sc.acc, &sc.out,
@@ -2594,7 +2594,7 @@ static int launch_prepare(prio3_engine* e, uint32_t c0, uint32_t n, InPtrs in, O
   const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
   if (dp.kind == PRIO3_SUMVEC_F64_MP) {
     int rc = PRIO3_OK;
-    TIMED(e, st, "k_mp64_prepare", (rc = launch_mp64(e, n, in, out, sc, st)));
+    TIMED(e, st, "k_mp64_prepare", (rc = launch_mp64(e, n, dp.ld, in, out, sc, st)));
     return rc;
   }
   if (dp.kind == PRIO3_FPVEC_BOUNDED_L2) {
@@ -2630,6 +2630,7 @@ static int launch_prepare(prio3_engine* e, uint32_t c0, uint32_t n, InPtrs in, O
       qi.pub += (size_t)dp.public_share_len * s0;
       qi.helper += (size_t)dp.helper_share_len * s0;
       qi.leader += (size_t)dp.prep_share_len * s0;
+      if (qi.vk_slot) qi.vk_slot += s0;
       OutPtrs qo = out;
       qo.prep_msgs += 16 * (size_t)s0;
       qo.status += s0;
@@ -2704,35 +2705,32 @@ static int launch_prepare(prio3_engine* e, uint32_t c0, uint32_t n, InPtrs in, O
 }
 
 
-static int prepare_impl(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
-                        const uint8_t* d_public_shares, const uint8_t* d_helper_shares,
-                        const uint8_t* d_leader_prep_shares, uint8_t* d_prep_msgs,
-                        uint8_t* d_status, hipStream_t st, const uint32_t* d_seg, bool fuse) {
-  int rc = ensure_scratch(e, n);
-  if (rc) return rc;
-  Scratch sc = e->sc;
-  sc.seg = d_seg;
-  sc.wpart = e->d_wpart;
-  sc.wseg = e->d_wseg;
-  InPtrs in{d_nonces, d_public_shares, d_helper_shares, d_leader_prep_shares};
-  OutPtrs out{d_prep_msgs, d_status};
-  // Option "chunks" > 1: the batch is cut into column ranges whose kernel chains run on the
-  // engine's side streams, so one chunk's memory-bound query overlaps the next chunk's
-  // VALU-bound Keccak (the caller's stream is joined before and after).
-  // Auto (0): one chunk per 128Ki reports (2 blocks per CU per kernel), measured best on
-  // MI355X at 1Mi reports (8 chunks: +4-5% over 1; 16: slower).
-  const uint32_t K = e->chunks > 0 ? (uint32_t)e->chunks
-                                   : std::max(1u, (n + (1u << 16)) >> 17);
+
+// The kernel chain over the whole run.  Option "chunks" > 1 (auto: one chunk per 128Ki reports,
+// measured best on MI355X at 1Mi reports: 8 chunks +4-5% over 1; 16: slower): the batch is cut
+// into column ranges whose chains alternate over the engine's two side streams (joined to `st`
+// before and after), so one chunk's memory-bound query overlaps the next chunk's VALU-bound
+// Keccak.  Side streams are per engine: callers that may overlap (the executor's concurrent
+// groups) pass allow_chunks = false.
+static int prepare_run(prio3_engine* e, Run* R, InPtrs in, OutPtrs out, hipStream_t st, bool fuse,
+                       bool allow_chunks) {
+  const uint32_t n = R->n;
+  Scratch sc = R->sc;
+  sc.seg = R->seg;
+  sc.wpart = R->wpart;
+  sc.wseg = R->wseg;
+  R->last = st;
+  const uint32_t K = e->chunks > 0 ? (uint32_t)e->chunks : std::max(1u, (n + (1u << 16)) >> 17);
   const uint32_t csz = ((n + K - 1) / K + 255) & ~255u;
-  if (K == 1 || n <= csz || e->dp.kind == PRIO3_FPVEC_BOUNDED_L2)
-    return launch_prepare(e, 0, n, in, out, sc, st, fuse);
-  rc = ensure_side_streams(e);
+  if (!allow_chunks || K == 1 || n <= csz || R->dp.kind == PRIO3_FPVEC_BOUNDED_L2)
+    return launch_prepare(e, R->dp, 0, n, in, out, sc, st, fuse);
+  int rc = ensure_side_streams(e);
   if (rc) return rc;
   HIPCHK(hipEventRecord(e->fork_ev, st));
   for (auto s2 : e->side) HIPCHK(hipStreamWaitEvent(s2, e->fork_ev, 0));
   uint32_t c = 0;
   for (uint32_t c0 = 0; c0 < n; c0 += csz, c++) {
-    rc = launch_prepare(e, c0, std::min(csz, n - c0), in, out, sc, e->side[c % 2], fuse);
+    rc = launch_prepare(e, R->dp, c0, std::min(csz, n - c0), in, out, sc, e->side[c % 2], fuse);
     if (rc) return rc;
   }
   for (size_t i = 0; i < e->side.size(); i++) {
@@ -2742,18 +2740,305 @@ static int prepare_impl(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
   return PRIO3_OK;
 }
 
+// the leader's prepare_init (agg_id 0) over the run
+extern "C" int launch_leader_init(const DevParams& dp, const uint8_t* d_nonces, const uint8_t* d_pub,
+                                  const uint8_t* d_lshares, const Scratch& sc,
+                                  uint8_t* d_prep_shares, uint8_t* d_status, hipStream_t st);
+extern "C" int launch_leader_next(const DevParams& dp, const uint8_t* d_prep_msgs, const Scratch& sc,
+                       uint8_t* d_status, hipStream_t st);
+
+static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
+                           const uint8_t* d_public_shares, const uint8_t* d_leader_input_shares,
+                           uint8_t* d_prep_shares, uint8_t* d_status, hipStream_t st) {
+  DevParams dp = R->dp;
+  dp.force_slow = (uint32_t)e->force_slow;
+  const uint32_t n = R->n;
+  R->last = st;
+  const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
+  if (ps && dp.jr_len && (dp.P == 32 || dp.P == 16 || dp.P == 8) && e->leader_fast) {
+    // the helper kernels in their leader role
+    InPtrs in{d_nonces, d_public_shares, d_leader_input_shares, nullptr};
+    OutPtrs out{d_prep_shares, d_status};
+    const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
+    TIMED(e, st, "k_leader_unpack",
+          (k_leader_unpack<<<(n + 63) / 64, 256, 0, st>>>(dp, in, R->sc, d_status)));
+    TIMED(e, st, "k_jrpart", (k_jrpart<false, true><<<blocks, 256, 0, st>>>(dp, in, R->sc)));
+    TIMED(e, st, "k_leader_slowfix",
+          (k_leader_slowfix<<<blocks64, 64, 0, st>>>(dp, in, R->sc)));
+    if (dp.P == 32)
+      TIMED(e, st, "k_query_h",
+            (k_query_h<2, 32, 1, 3, 1><<<blocks, 256, 0, st>>>(dp, in, R->sc, out)));
+    else if (dp.P == 16)
+      TIMED(e, st, "k_query_h",
+            (k_query_h<2, 16, 1, 3, 1><<<blocks, 256, 0, st>>>(dp, in, R->sc, out)));
+    else
+      TIMED(e, st, "k_query_h",
+            (k_query_h<2, 8, 1, 3, 1><<<blocks, 256, 0, st>>>(dp, in, R->sc, out)));
+    return PRIO3_OK;
+  }
+  int rc2 = PRIO3_OK;
+  TIMED(e, st, "k_leader_init",
+        rc2 = launch_leader_init(dp, d_nonces, d_public_shares, d_leader_input_shares, R->sc,
+                                 d_prep_shares, d_status, st));
+  return rc2;
+}
+
+// ---- executor hooks (prio3_runtime.h) ----
+int engine_device(const prio3_engine* e) { return e->device; }
+
+void engine_vk(const prio3_engine* e, uint8_t out[16]) { memcpy(out, e->dp.vk, 16); }
+
+static uint64_t fnv(uint64_t h, const void* p, size_t n) {
+  const uint8_t* b = (const uint8_t*)p;
+  for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
+  return h;
+}
+
+uint64_t engine_group_key(const prio3_engine* e) {
+  uint64_t h = 1469598103934665603ull;
+  h = fnv(h, &e->params, sizeof e->params);
+  h = fnv(h, &e->device, sizeof e->device);
+  const int opts[] = {e->force_slow, e->split_xof, e->fp_overlap, e->fp_gs, e->qh_prefetch,
+                      e->qh_occ,     e->qh_regs,   e->qpair};
+  h = fnv(h, opts, sizeof opts);
+  h = fnv(h, &e->fp_sub_bytes, sizeof e->fp_sub_bytes);
+  // XofHmacSha256Aes128 keys enter the kernels as HMAC midstates: one engine per launch; an
+  // engine with coalescing off gets a key of its own for every call
+  if (e->dp.kind == PRIO3_SUMVEC_F64_MP || !e->coalesce) {
+    static std::atomic<uint64_t> solo{0};
+    const uint64_t u[2] = {(uint64_t)(uintptr_t)e, e->coalesce ? 0 : ++solo};
+    h = fnv(h, u, sizeof u);
+  }
+  return h;
+}
+
+void engine_io_layout(const prio3_engine* e, uint32_t cap, IoLayout* L) {
+  const DevParams& d = e->dp;
+  L->len[0] = 16;
+  L->len[1] = d.public_share_len;
+  L->len[2] = d.helper_share_len;
+  L->len[3] = d.prep_share_len;
+  size_t off = 0;
+  for (int f = 0; f < 4; f++) {
+    L->off[f] = off;
+    off += (L->len[f] * cap + 15) & ~(size_t)15;
+  }
+  L->slot_off = off;
+  off += (2 * (size_t)cap + 15) & ~(size_t)15;
+  L->tab_off = off;
+  off += 16 * (size_t)exec_max_keys();
+  L->msg_len = e->sz.prep_msg_len;
+  L->msg_off = off;
+  off += L->msg_len * cap;
+  L->status_off = off;
+  off += cap;
+  L->bytes = off;
+}
+
+int engine_run_group(prio3_engine* lead, const GroupView& g, Run** run_out) {
+  *run_out = nullptr;
+  HIPCHK(hipSetDevice(lead->device));
+  PooledStream ps(lead->device);
+  hipStream_t st = ps.s;
+  if (!st) return PRIO3_EDEVICE;
+  const bool mp = lead->dp.kind == PRIO3_SUMVEC_F64_MP;
+  int rc = PRIO3_OK;
+  Run* R = run_create(lead, g.n, RUN_SCRATCH | RUN_IO | (mp ? 0u : (unsigned)RUN_VK), 0,
+                      g.n_keys, st, &rc);
+  if (!R) return rc;
+  IoLayout L;
+  engine_io_layout(lead, g.cap, &L);
+  uint8_t* dst[4] = {R->nonces, R->pub, R->helper, R->leader};
+  auto fail = [&](int code) {
+    run_release(R, st, true);
+    return code;
+  };
+  for (int f = 0; f < 4; f++)
+    if (L.len[f] &&
+        hipMemcpyAsync(dst[f], g.stg + L.off[f], L.len[f] * g.n, hipMemcpyHostToDevice, st) !=
+            hipSuccess)
+      return fail(PRIO3_EDEVICE);
+  InPtrs in{R->nonces, L.len[1] ? R->pub : nullptr, R->helper, R->leader};
+  if (!mp) {
+    if (hipMemcpyAsync(R->vk_slot, g.stg + L.slot_off, 2 * (size_t)g.n, hipMemcpyHostToDevice,
+                       st) != hipSuccess ||
+        hipMemcpyAsync(R->vk_tab, g.stg + L.tab_off, 16 * (size_t)g.n_keys,
+                       hipMemcpyHostToDevice, st) != hipSuccess)
+      return fail(PRIO3_EDEVICE);
+    in.vk_slot = R->vk_slot;
+    in.vk_tab = R->vk_tab;
+  }
+  OutPtrs out{R->msgs, R->status};
+  rc = prepare_run(lead, R, in, out, st, false, false);
+  if (rc) return fail(rc);
+  if ((L.msg_len && hipMemcpyAsync(g.stg + L.msg_off, R->msgs, L.msg_len * g.n,
+                                   hipMemcpyDeviceToHost, st) != hipSuccess) ||
+      hipMemcpyAsync(g.stg + L.status_off, R->status, g.n, hipMemcpyDeviceToHost, st) !=
+          hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return fail(PRIO3_EDEVICE);
+  if (lead->timing) collect_times(lead);
+  R->refs.store(g.jobs);
+  *run_out = R;
+  return PRIO3_OK;
+}
+
+extern "C" {
+
+int prio3_sizes(const prio3_params* params, prio3_sizes_t* out) {
+  return fill_sizes(params, out, nullptr);
+}
+
+int prio3_engine_create_ex(const prio3_params* params, const uint8_t* verify_key,
+                           size_t verify_key_len, int device, prio3_engine** out) {
+  if (!params || !verify_key || !out) return PRIO3_EINVAL;
+  const bool mp = params->kind == PRIO3_SUMVEC_F64_MP;
+  if (verify_key_len != (mp ? 32u : 16u)) return PRIO3_EINVAL;
+  prio3_engine* e = new prio3_engine();
+  int rc = fill_sizes(params, &e->sz, &e->dp);
+  if (rc) {
+    delete e;
+    return rc;
+  }
+  e->params = *params;
+  if (!mp) memcpy(e->dp.vk, verify_key, 16);
+  e->device = device;
+  hipStream_t probe = nullptr;  // a GPU must be present: the product path has no CPU fallback
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&probe, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    delete e;
+    return PRIO3_EDEVICE;
+  }
+  ws_stream_put(device, probe);  // the first member of the GPU's stream pool
+  if (mp) {  // prio3_mp64.hip constants
+    const DevParams& d = e->dp;
+    Mp64Params& m = e->mp;
+    m.meas_len = d.meas_len;
+    m.out_len = d.out_len;
+    m.bits = params->bits;
+    m.chunk = params->chunk_length;
+    m.calls = d.calls;
+    m.P = d.P;
+    m.logP = d.logP;
+    m.glen = d.glen;
+    m.np = params->num_proofs;
+    m.proof_len = d.proof_len / m.np;
+    m.arity = d.arity;
+    m.vlen = d.verifier_len;
+    memcpy(m.dst, d.dst, sizeof m.dst);
+    hmac_midstates_host(verify_key, 32, m.vk_ist, m.vk_ost);
+    static const uint8_t zero32[32] = {0};
+    hmac_midstates_host(zero32, 32, m.z_ist, m.z_ost);
+    const u128 alpha = d.roots64[d.logP];
+    m.alpha = (uint64_t)alpha;
+    m.alpha_inv = (uint64_t)hpow(alpha, d.P - 1, HP64);
+    m.invP = d.invP64;
+    m.half = d.half64;
+    std::vector<uint64_t> sig(d.P);
+    for (uint32_t e2 = 0; e2 < d.P; e2++) {
+      const u128 ae = hpow(alpha, e2, HP64);
+      u128 sum = 0, x = 1;
+      for (uint32_t c = 1; c <= d.calls; c++) {
+        x = hmul(x, ae, HP64);
+        sum = (sum + x) % HP64;
+      }
+      sig[e2] = (uint64_t)sum;
+    }
+    if (hipMalloc((void**)&e->d_sigma64, 8 * (size_t)d.P) != hipSuccess ||
+        hipMemcpy(e->d_sigma64, sig.data(), 8 * (size_t)d.P, hipMemcpyHostToDevice) !=
+            hipSuccess) {
+      delete e;
+      return PRIO3_EDEVICE;
+    }
+    m.sigma = e->d_sigma64;
+  }
+  *out = e;
+  return PRIO3_OK;
+}
+
+int prio3_engine_create(const prio3_params* params, const uint8_t verify_key[16], int device,
+                        prio3_engine** out) {
+  return prio3_engine_create_ex(params, verify_key, 16, device, out);
+}
+
+void prio3_engine_destroy(prio3_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  (void)hipDeviceSynchronize();
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (e->cur) run_release(e->cur, nullptr, true);
+    e->cur = nullptr;
+  }
+  collect_times(e);
+  if (e->d_sigma64) (void)hipFree(e->d_sigma64);
+  for (auto s2 : e->side) (void)hipStreamDestroy(s2);
+  for (auto j : e->side_ev) (void)hipEventDestroy(j);
+  if (e->fork_ev) (void)hipEventDestroy(e->fork_ev);
+  delete e;
+}
+
+int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
+  if (!e || !key) return PRIO3_EINVAL;
+  struct {
+    const char* name;
+    int* field;
+  } ints[] = {{"force_slow_path", &e->force_slow}, {"chunks", &e->chunks},
+              {"leader_fast", &e->leader_fast},    {"fuse_acc", &e->fuse_acc},
+              {"qh_regs", &e->qh_regs},            {"qh_occ", &e->qh_occ},
+              {"qh_prefetch", &e->qh_prefetch},    {"split_xof", &e->split_xof},
+              {"qpair", &e->qpair},                {"timing", &e->timing},
+              {"coalesce", &e->coalesce},          {"experimental_fpvec", &e->experimental_fpvec}};
+  for (auto& o : ints)
+    if (!strcmp(key, o.name)) {
+      *o.field = (int)value;
+      return PRIO3_OK;
+    }
+  if (!strcmp(key, "fp_sub_bytes")) {  // FPVec scratch budget per sub-batch (0 = auto)
+    if (value < 0) return PRIO3_EINVAL;
+    e->fp_sub_bytes = value;
+    return PRIO3_OK;
+  }
+  if (!strcmp(key, "fp_overlap")) {
+    e->fp_overlap = value ? 1 : 0;
+    return PRIO3_OK;
+  }
+  if (!strcmp(key, "fp_gs")) {
+    if (value != 4 && value != 8 && value != 16) return PRIO3_EINVAL;
+    e->fp_gs = (int)value;
+    return PRIO3_OK;
+  }
+  return PRIO3_EINVAL;
+}
+
+// ---- device-resident entry points ----
+// A device-resident prepare replaces the engine's current run: the previous one is released
+// (stream-ordered, so its slab can be reused by this very call) and this one stays until the
+// next device-resident prepare -- "output shares remain until the next prio3_device_prepare".
+static Run* device_run(prio3_engine* e, uint32_t n, unsigned flags, uint32_t nseg,
+                       hipStream_t st, int* rc) {
+  if (e->cur) run_release(e->cur, st, true);
+  e->cur = run_create(e, n, flags, nseg, 0, st, rc);
+  return e->cur;
+}
+
 int prio3_device_prepare(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
                          const uint8_t* d_public_shares, const uint8_t* d_helper_shares,
                          const uint8_t* d_leader_prep_shares, uint8_t* d_prep_msgs,
                          uint8_t* d_status, void* stream) {
   if (!e) return PRIO3_EINVAL;
+  if (e->dp.kind == PRIO3_FPVEC_BOUNDED_L2 && !e->experimental_fpvec)
+    return PRIO3_EUNSUPPORTED;  // unpinned reconstruction: explicit opt-in only
   if (n == 0) return PRIO3_OK;
   std::lock_guard<std::mutex> lk(e->mu);
   HIPCHK(hipSetDevice(e->device));
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
-  e->fused_on = 0;
-  return prepare_impl(e, n, d_nonces, d_public_shares, d_helper_shares, d_leader_prep_shares,
-                      d_prep_msgs, d_status, st, nullptr, false);
+  int rc = PRIO3_OK;
+  Run* R = device_run(e, n, RUN_SCRATCH, 0, st, &rc);
+  if (!R) return rc;
+  InPtrs in{d_nonces, d_public_shares, d_helper_shares, d_leader_prep_shares};
+  return prepare_run(e, R, in, OutPtrs{d_prep_msgs, d_status}, st, false, true);
 }
 
 int prio3_device_prepare_aggregate(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
@@ -2762,60 +3047,54 @@ int prio3_device_prepare_aggregate(prio3_engine* e, uint32_t n, const uint8_t* d
                                    const uint32_t* d_segment_ids, uint32_t n_segments,
                                    uint8_t* d_prep_msgs, uint8_t* d_status, void* stream) {
   if (!e || n_segments == 0) return PRIO3_EINVAL;
+  if (e->dp.kind == PRIO3_FPVEC_BOUNDED_L2 && !e->experimental_fpvec)
+    return PRIO3_EUNSUPPORTED;  // unpinned reconstruction: explicit opt-in only
   std::lock_guard<std::mutex> lk(e->mu);
   HIPCHK(hipSetDevice(e->device));
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
-  e->fused_n = n;
-  e->fused_segments = n_segments;
-  e->fused_seg_ptr = d_segment_ids;
-  e->fused_on = 0;
-  e->dp.nseg = n_segments;
+  const bool fuse = n > 0 && fusable(e);
+  int rc = PRIO3_OK;
+  Run* R = device_run(e, n, RUN_SCRATCH | (fuse ? (unsigned)RUN_FUSED : 0u), n_segments, st, &rc);
+  if (!R) return rc;
+  R->seg = d_segment_ids;
+  R->aggregate = true;
   if (n == 0) return PRIO3_OK;
-  const bool fuse = fusable(e);
-  if (fuse) {
-    int rc = ensure_fused(e, n, n_segments);
-    if (rc) return rc;
-  }
-  int rc = prepare_impl(e, n, d_nonces, d_public_shares, d_helper_shares, d_leader_prep_shares,
-                        d_prep_msgs, d_status, st, d_segment_ids, fuse);
-  if (rc == PRIO3_OK) e->fused_on = fuse;
+  InPtrs in{d_nonces, d_public_shares, d_helper_shares, d_leader_prep_shares};
+  rc = prepare_run(e, R, in, OutPtrs{d_prep_msgs, d_status}, st, fuse, true);
+  if (rc == PRIO3_OK) R->fused = fuse;
   return rc;
 }
-
-int prio3_device_accumulate(prio3_engine* e, uint32_t n, const uint8_t* d_status,
-                            const uint32_t* d_segment_ids, const uint8_t* d_accept_mask,
-                            uint32_t n_segments, uint8_t* d_agg_shares, uint64_t* d_counts,
-                            void* stream);
 
 int prio3_device_aggregate_finish(prio3_engine* e, const uint8_t* d_status,
                                   const uint8_t* d_accept_mask, uint8_t* d_agg_shares,
                                   uint64_t* d_counts, void* stream) {
   if (!e) return PRIO3_EINVAL;
-  if (!e->fused_on)  // not fusable (or nothing prepared): the classic masked reduction
-    return prio3_device_accumulate(e, e->fused_n, d_status, e->fused_seg_ptr, d_accept_mask,
-                                   e->fused_segments, d_agg_shares, d_counts, stream);
   std::lock_guard<std::mutex> lk(e->mu);
   HIPCHK(hipSetDevice(e->device));
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
-  const uint32_t n = e->fused_n, S = e->fused_segments, M = e->dp.meas_len;
+  Run* R = e->cur;
+  if (!R || !R->aggregate) return PRIO3_EINVAL;  // finish follows prio3_device_prepare_aggregate
+  R->last = st;
+  if (!R->fused)  // not fusable (or an empty batch): the one-pass segmented reduction
+    return run_accumulate(e, R, 0, R->n, d_status, R->seg, d_accept_mask, R->nseg, d_agg_shares,
+                          d_counts, st);
+  const uint32_t n = R->n, S = R->nseg, M = R->dp.meas_len;
   const uint32_t nwaves = (n + 63) / 64;
-  HIPCHK(hipMemsetAsync(e->d_agg64, 0, (size_t)S * M * 8 * 8, st));
-  HIPCHK(hipMemsetAsync(e->d_fix, 0, sizeof(uint32_t), st));
+  HIPCHK(hipMemsetAsync(R->agg64, 0, (size_t)S * M * 8 * 8, st));
+  HIPCHK(hipMemsetAsync(R->fix, 0, sizeof(uint32_t), st));
   HIPCHK(hipMemsetAsync(d_counts, 0, 8 * (size_t)S, st));
   const uint32_t nchunks = (nwaves + WCH - 1) / WCH;
   dim3 g1((M * 8 + 255) / 256, nchunks);
   TIMED(e, st, "k_agg_waves",
-        (k_agg_waves<<<g1, 256, 0, st>>>(nwaves, M, e->d_wpart, e->d_wseg, e->d_cpart, e->d_cseg,
-                                         e->d_agg64)));
+        (k_agg_waves<<<g1, 256, 0, st>>>(nwaves, M, R->wpart, R->wseg, R->cpart, R->cseg,
+                                         R->agg64)));
   TIMED(e, st, "k_agg_fix",
         (k_agg_fix<<<(n + FIX_R - 1) / FIX_R, 256, 0, st>>>(
-            n, d_status, e->fused_seg_ptr, d_accept_mask, e->d_wseg, e->d_fix,
-            (uint32_t)(e->fix_cap - 1), S, (unsigned long long*)d_counts)));
+            n, d_status, R->seg, d_accept_mask, R->wseg, R->fix, (uint32_t)(R->fix_cap - 1), S,
+            (unsigned long long*)d_counts)));
   TIMED(e, st, "k_agg_final",
-        (k_agg_final<<<S * M, 256, 0, st>>>(M, e->dp.ld, e->d_agg64, nchunks,
-                                                          e->d_cpart, e->d_cseg, e->d_fix,
-                                                          e->fused_seg_ptr, e->sc.meas,
-                                                          d_agg_shares)));
+        (k_agg_final<<<S * M, 256, 0, st>>>(M, R->dp.ld, R->agg64, nchunks, R->cpart, R->cseg,
+                                             R->fix, R->seg, R->sc.meas, d_agg_shares)));
   return PRIO3_OK;
 }
 
@@ -2827,59 +3106,22 @@ int prio3_device_accumulate(prio3_engine* e, uint32_t n, const uint8_t* d_status
   std::lock_guard<std::mutex> lk(e->mu);
   HIPCHK(hipSetDevice(e->device));
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
-  const DevParams& d = e->dp;
-  const size_t agg_len = (size_t)d.out_len * d.es;
+  const size_t agg_len = (size_t)e->dp.out_len * e->dp.es;
   if (n == 0) {
     HIPCHK(hipMemsetAsync(d_agg_shares, 0, agg_len * n_segments, st));
-    HIPCHK(hipMemsetAsync(d_counts, 0, 8 * n_segments, st));
+    HIPCHK(hipMemsetAsync(d_counts, 0, 8 * (size_t)n_segments, st));
     return PRIO3_OK;
   }
-  if (n > e->cap) return PRIO3_EINVAL;
-  const uint32_t chunk = 8192;
-  const uint32_t nchunks = (n + chunk - 1) / chunk;
-  size_t need = (size_t)nchunks * agg_len;
-  if (need > e->partial_cap) {
-    if (e->d_prep_partial) (void)hipFree(e->d_prep_partial);
-    if (e->d_pcount) (void)hipFree(e->d_pcount);
-    HIPCHK(hipMalloc(&e->d_prep_partial, need));
-    HIPCHK(hipMalloc((void**)&e->d_pcount, 8 * (size_t)nchunks));
-    e->partial_cap = need;
-  }
-  const void* src = (d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC ||
-                     d.kind == PRIO3_SUMVEC_F64_MP || d.kind == PRIO3_FPVEC_BOUNDED_L2)
-                        ? e->sc.out
-                        : e->sc.meas;
-  for (uint32_t s = 0; s < n_segments; s++) {
-    TIMED(e, st, "k_mask",
-          (k_mask<<<(n + 255) / 256, 256, 0, st>>>(n, d_status, d_segment_ids, d_accept_mask, s,
-                                                  e->d_mask)));
-    dim3 grid(d.out_len, nchunks);
-    if (d.es == 16) {
-      TIMED(e, st, "k_acc_partial",
-            (k_acc_partial<Fp128><<<grid, 256, 0, st>>>(n, d.ld_out, chunk, d.out_len, src, e->d_mask,
-                                                        e->d_prep_partial, e->d_pcount)));
-      TIMED(e, st, "k_acc_final",
-            (k_acc_final<Fp128><<<(d.out_len + 255) / 256, 256, 0, st>>>(
-                nchunks, d.out_len, e->d_prep_partial, e->d_pcount, d_agg_shares + s * agg_len,
-                d_counts + s)));
-    } else {
-      TIMED(e, st, "k_acc_partial",
-            (k_acc_partial<Fp64><<<grid, 256, 0, st>>>(n, d.ld_out, chunk, d.out_len, src, e->d_mask,
-                                                       e->d_prep_partial, e->d_pcount)));
-      TIMED(e, st, "k_acc_final",
-            (k_acc_final<Fp64><<<(d.out_len + 255) / 256, 256, 0, st>>>(
-                nchunks, d.out_len, e->d_prep_partial, e->d_pcount, d_agg_shares + s * agg_len,
-                d_counts + s)));
-    }
-  }
-  return PRIO3_OK;
+  Run* R = e->cur;
+  if (!R || n > R->n) return PRIO3_EINVAL;
+  return run_accumulate(e, R, 0, n, d_status, d_segment_ids, d_accept_mask, n_segments,
+                        d_agg_shares, d_counts, st);
 }
 
 int prio3_device_combine(prio3_engine* e, uint32_t k, uint32_t n_segments, const uint8_t* d_in,
                          const uint64_t* d_counts_in, uint8_t* d_out, uint64_t* d_counts_out,
                          void* stream) {
-  if (!e || k == 0) return PRIO3_EINVAL;
-  std::lock_guard<std::mutex> lk(e->mu);
+  if (!e || k == 0 || n_segments == 0) return PRIO3_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
   const DevParams& d = e->dp;
@@ -2905,7 +3147,6 @@ int prio3_device_batch_metadata(prio3_engine* e, uint32_t n, const uint8_t* d_re
                                 void* stream) {
   if (!e || n_segments == 0 || (n && (!d_status || (d_checksums && !d_report_ids))))
     return PRIO3_EINVAL;
-  std::lock_guard<std::mutex> lk(e->mu);
   HIPCHK(hipSetDevice(e->device));
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
   uint32_t* ck = (uint32_t*)d_checksums;
@@ -2926,7 +3167,6 @@ int prio3_device_combine_metadata(prio3_engine* e, uint32_t k, uint32_t n_segmen
                                   uint8_t* d_checksums_out, uint64_t* d_intervals_out,
                                   void* stream) {
   if (!e || k == 0 || n_segments == 0) return PRIO3_EINVAL;
-  std::lock_guard<std::mutex> lk(e->mu);
   HIPCHK(hipSetDevice(e->device));
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
   TIMED(e, st, "k_combine_meta",
@@ -2942,129 +3182,88 @@ int prio3_batch_metadata(prio3_engine* e, uint32_t n, const uint8_t* report_ids,
                          const uint32_t* segment_ids, uint32_t n_segments, uint8_t* checksums_out,
                          uint64_t* intervals_out) {
   if (!e || n_segments == 0 || (n && (!status || !report_ids))) return PRIO3_EINVAL;
-  uint8_t *d_ids = nullptr, *d_st = nullptr, *d_mask = nullptr, *d_ck = nullptr;
-  uint64_t *d_t = nullptr, *d_iv = nullptr;
-  uint32_t* d_seg = nullptr;
+  HIPCHK(hipSetDevice(e->device));
+  PooledStream ps(e->device);
+  hipStream_t st = ps.s;
+  if (!st) return PRIO3_EDEVICE;
+  const size_t N = n ? n : 1, S = n_segments;
+  const size_t al = 256;
+  auto up = [&](size_t b) { return (b + al - 1) / al * al; };
+  const size_t o_ids = 0, o_st = o_ids + up(16 * N), o_t = o_st + up(N), o_mask = o_t + up(8 * N),
+               o_seg = o_mask + up(N), o_ck = o_seg + up(4 * N), o_iv = o_ck + up(32 * S),
+               total = o_iv + up(16 * S);
   int rc = PRIO3_OK;
-  {
-    std::lock_guard<std::mutex> lk(e->mu);
-    HIPCHK(hipSetDevice(e->device));
-    const size_t N = n ? n : 1;
-    HIPCHK(hipMalloc((void**)&d_ids, 16 * N));
-    HIPCHK(hipMalloc((void**)&d_st, N));
-    HIPCHK(hipMalloc((void**)&d_ck, 32 * (size_t)n_segments));
-    HIPCHK(hipMalloc((void**)&d_iv, 16 * (size_t)n_segments));
-    if (times) HIPCHK(hipMalloc((void**)&d_t, 8 * N));
-    if (accept_mask) HIPCHK(hipMalloc((void**)&d_mask, N));
-    if (segment_ids) HIPCHK(hipMalloc((void**)&d_seg, 4 * N));
-    HIPCHK(hipMemcpyAsync(d_ids, report_ids, 16 * (size_t)n, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(hipMemcpyAsync(d_st, status, n, hipMemcpyHostToDevice, e->stream));
-    if (times) HIPCHK(hipMemcpyAsync(d_t, times, 8 * (size_t)n, hipMemcpyHostToDevice, e->stream));
-    if (accept_mask)
-      HIPCHK(hipMemcpyAsync(d_mask, accept_mask, n, hipMemcpyHostToDevice, e->stream));
-    if (segment_ids)
-      HIPCHK(hipMemcpyAsync(d_seg, segment_ids, 4 * (size_t)n, hipMemcpyHostToDevice, e->stream));
-  }
-  rc = prio3_device_batch_metadata(e, n, d_ids, d_t, d_st, d_mask, d_seg, n_segments,
-                                   checksums_out ? d_ck : nullptr, intervals_out ? d_iv : nullptr,
-                                   e->stream);
-  if (rc == PRIO3_OK) {
-    std::lock_guard<std::mutex> lk(e->mu);
-    if (checksums_out)
-      HIPCHK(hipMemcpyAsync(checksums_out, d_ck, 32 * (size_t)n_segments, hipMemcpyDeviceToHost,
-                            e->stream));
-    if (intervals_out)
-      HIPCHK(hipMemcpyAsync(intervals_out, d_iv, 16 * (size_t)n_segments, hipMemcpyDeviceToHost,
-                            e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
-  }
-  for (void* p : {(void*)d_ids, (void*)d_st, (void*)d_mask, (void*)d_ck, (void*)d_t, (void*)d_iv,
-                  (void*)d_seg})
-    if (p) (void)hipFree(p);
+  Slab* sl = ws_acquire(e->device, total, st, &rc);
+  if (!sl) return rc;
+  uint8_t* b = sl->base;
+  auto h2d = [&](size_t off, const void* src, size_t bytes) {
+    return !src || !bytes ||
+           hipMemcpyAsync(b + off, src, bytes, hipMemcpyHostToDevice, st) == hipSuccess;
+  };
+  if (!h2d(o_ids, report_ids, 16 * (size_t)n) || !h2d(o_st, status, n) ||
+      !h2d(o_t, times, 8 * (size_t)n) || !h2d(o_mask, accept_mask, n) ||
+      !h2d(o_seg, segment_ids, 4 * (size_t)n))
+    rc = PRIO3_EDEVICE;
+  if (rc == PRIO3_OK)
+    rc = prio3_device_batch_metadata(
+        e, n, b + o_ids, times ? (const uint64_t*)(b + o_t) : nullptr, b + o_st,
+        accept_mask ? b + o_mask : nullptr, segment_ids ? (const uint32_t*)(b + o_seg) : nullptr,
+        n_segments, checksums_out ? b + o_ck : nullptr,
+        intervals_out ? (uint64_t*)(b + o_iv) : nullptr, st);
+  if (rc == PRIO3_OK &&
+      ((checksums_out && hipMemcpyAsync(checksums_out, b + o_ck, 32 * S, hipMemcpyDeviceToHost,
+                                        st) != hipSuccess) ||
+       (intervals_out && hipMemcpyAsync(intervals_out, b + o_iv, 16 * S, hipMemcpyDeviceToHost,
+                                        st) != hipSuccess) ||
+       hipStreamSynchronize(st) != hipSuccess))
+    rc = PRIO3_EDEVICE;
+  if (e->timing) collect_times(e);
+  ws_release(sl, st);
   return rc;
 }
 
 int prio3_device_output_shares(prio3_engine* e, uint32_t n, uint8_t* out) {
-  if (!e || !out || n > e->cap) return PRIO3_EINVAL;
+  if (!e || !out) return PRIO3_EINVAL;
   std::lock_guard<std::mutex> lk(e->mu);
   HIPCHK(hipSetDevice(e->device));
-  HIPCHK(hipStreamSynchronize(e->stream));
-  HIPCHK(hipDeviceSynchronize());
-  const DevParams& d = e->dp;
-  const void* src = (d.kind == PRIO3_SUM || d.kind == PRIO3_SUMVEC ||
-                     d.kind == PRIO3_SUMVEC_F64_MP || d.kind == PRIO3_FPVEC_BOUNDED_L2)
-                        ? e->sc.out
-                        : e->sc.meas;
-  std::vector<uint8_t> soa((size_t)d.out_len * d.ld_out * d.es);
-  HIPCHK(hipMemcpy(soa.data(), src, soa.size(), hipMemcpyDeviceToHost));
-  for (uint32_t r = 0; r < n; r++)
-    for (uint32_t i = 0; i < d.out_len; i++)
-      memcpy(out + ((size_t)r * d.out_len + i) * d.es,
-             soa.data() + ((size_t)i * d.ld_out + r) * d.es, d.es);
-  return PRIO3_OK;
+  Run* R = e->cur;
+  if (!R || n > R->n) return PRIO3_EINVAL;
+  HIPCHK(hipDeviceSynchronize());  // the run's work may sit on any caller stream
+  PooledStream ps(e->device);
+  if (!ps.s) return PRIO3_EDEVICE;
+  return run_output_shares(R, 0, n, out, ps.s);
 }
 
-static int ensure_io(prio3_engine* e, uint32_t n) {
-  if (n <= e->io_cap) return PRIO3_OK;
-  uint8_t** bufs[] = {&e->d_nonces, &e->d_pub, &e->d_helper, &e->d_leader, &e->d_msgs, &e->d_status};
-  for (auto b : bufs)
-    if (*b) {
-      (void)hipFree(*b);
-      *b = nullptr;
-    }
-  const DevParams& d = e->dp;
-  size_t sizes[] = {16 * (size_t)n, (size_t)(d.public_share_len ? d.public_share_len : 16) * n,
-                    (size_t)d.helper_share_len * n, (size_t)d.prep_share_len * n,
-                    (size_t)(e->sz.prep_msg_len ? e->sz.prep_msg_len : 16) * n, (size_t)n};
-  for (size_t i = 0; i < 6; i++) HIPCHK(hipMalloc((void**)bufs[i], sizes[i]));
-  e->io_cap = n;
-  return PRIO3_OK;
-}
-
+// ---- host-buffer entry points (what the Rust FFI calls from inside rayon::spawn) ----
 int prio3_helper_prepare_batch(prio3_engine* e, uint32_t n, const uint8_t* nonces,
                                const uint8_t* public_shares, const uint8_t* helper_shares,
                                const uint8_t* leader_prep_shares, uint8_t* prep_msgs_out,
                                uint8_t* status_out, prio3_batch** batch_out) {
   if (!e || (n && (!nonces || !helper_shares || !leader_prep_shares || !status_out)))
     return PRIO3_EINVAL;
+  if (e->dp.kind == PRIO3_FPVEC_BOUNDED_L2 && !e->experimental_fpvec)
+    return PRIO3_EUNSUPPORTED;  // unpinned reconstruction: explicit opt-in only
   const DevParams& d = e->dp;
   if (n && d.jr_len && (!public_shares || !prep_msgs_out)) return PRIO3_EINVAL;
-  {
-    std::lock_guard<std::mutex> lk(e->mu);
-    HIPCHK(hipSetDevice(e->device));
-    int rc = ensure_io(e, n ? n : 1);
-    if (rc) return rc;
-    hipStream_t st = e->stream;
-    if (n) {
-      HIPCHK(hipMemcpyAsync(e->d_nonces, nonces, 16 * (size_t)n, hipMemcpyHostToDevice, st));
-      if (d.jr_len)
-        HIPCHK(hipMemcpyAsync(e->d_pub, public_shares, (size_t)d.public_share_len * n,
-                              hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(e->d_helper, helper_shares, (size_t)d.helper_share_len * n,
-                            hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(e->d_leader, leader_prep_shares, (size_t)d.prep_share_len * n,
-                            hipMemcpyHostToDevice, st));
-    }
+  if (n == 0) {
+    if (batch_out) *batch_out = new prio3_batch{e, nullptr, 0, 0};
+    return PRIO3_OK;
   }
-  int rc = prio3_device_prepare(e, n, e->d_nonces, e->d_pub, e->d_helper, e->d_leader, e->d_msgs,
-                                e->d_status, e->stream);
+  ExecJob job;
+  job.e = e;
+  job.n = n;
+  job.nonces = nonces;
+  job.pub = d.jr_len ? public_shares : nullptr;
+  job.helper = helper_shares;
+  job.leader = leader_prep_shares;
+  job.msgs_out = prep_msgs_out;
+  job.status_out = status_out;
+  const int rc = exec_submit(&job);
   if (rc) return rc;
-  {
-    std::lock_guard<std::mutex> lk(e->mu);
-    hipStream_t st = e->stream;
-    if (n) {
-      HIPCHK(hipMemcpyAsync(status_out, e->d_status, n, hipMemcpyDeviceToHost, st));
-      if (d.jr_len)
-        HIPCHK(hipMemcpyAsync(prep_msgs_out, e->d_msgs, (size_t)e->sz.prep_msg_len * n,
-                              hipMemcpyDeviceToHost, st));
-    }
-    HIPCHK(hipStreamSynchronize(st));
-    if (e->timing) collect_times(e);
-  }
-  if (batch_out) {
-    prio3_batch* b = new prio3_batch{e, n};
-    *batch_out = b;
-  }
+  if (batch_out)
+    *batch_out = new prio3_batch{e, job.run, job.c0, n};
+  else
+    run_release(job.run, nullptr, false);
   return PRIO3_OK;
 }
 
@@ -3072,52 +3271,68 @@ int prio3_accumulate(prio3_batch* b, const uint32_t* segment_ids, const uint8_t*
                      uint32_t n_segments, uint8_t* agg_shares_out, uint64_t* counts_out) {
   if (!b || !agg_shares_out || !counts_out || n_segments == 0) return PRIO3_EINVAL;
   prio3_engine* e = b->e;
-  const DevParams& d = e->dp;
+  const size_t agg_len = (size_t)e->dp.out_len * e->dp.es, S = n_segments;
+  if (!b->run || b->n == 0) {
+    memset(agg_shares_out, 0, agg_len * S);
+    memset(counts_out, 0, 8 * S);
+    return PRIO3_OK;
+  }
+  Run* R = b->run;
   const uint32_t n = b->n;
-  uint32_t* d_seg = nullptr;
-  uint8_t *d_acc = nullptr, *d_agg = nullptr;
-  uint64_t* d_cnt = nullptr;
-  const size_t agg_len = (size_t)d.out_len * d.es;
   HIPCHK(hipSetDevice(e->device));
-  hipStream_t st = e->stream;
-  if (n && segment_ids) {
-    HIPCHK(hipMalloc((void**)&d_seg, 4 * (size_t)n));
-    HIPCHK(hipMemcpyAsync(d_seg, segment_ids, 4 * (size_t)n, hipMemcpyHostToDevice, st));
-  }
-  if (n && accept_mask) {
-    HIPCHK(hipMalloc((void**)&d_acc, n));
-    HIPCHK(hipMemcpyAsync(d_acc, accept_mask, n, hipMemcpyHostToDevice, st));
-  }
-  HIPCHK(hipMalloc((void**)&d_agg, agg_len * n_segments));
-  HIPCHK(hipMalloc((void**)&d_cnt, 8 * (size_t)n_segments));
-  int rc = prio3_device_accumulate(e, n, e->d_status, d_seg, d_acc, n_segments, d_agg, d_cnt,
-                                   e->stream);
-  if (rc == PRIO3_OK) {
-    HIPCHK(hipMemcpyAsync(agg_shares_out, d_agg, agg_len * n_segments, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(counts_out, d_cnt, 8 * (size_t)n_segments, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    if (e->timing) collect_times(e);
-  }
-  if (d_seg) (void)hipFree(d_seg);
-  if (d_acc) (void)hipFree(d_acc);
-  (void)hipFree(d_agg);
-  (void)hipFree(d_cnt);
+  PooledStream ps(e->device);
+  hipStream_t st = ps.s;
+  if (!st) return PRIO3_EDEVICE;
+  auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_seg = 0, o_acc = up(4 * (size_t)n), o_agg = o_acc + up(n),
+               o_cnt = o_agg + up(agg_len * S), total = o_cnt + up(8 * S);
+  int rc = PRIO3_OK;
+  Slab* sl = ws_acquire(e->device, total, st, &rc);
+  if (!sl) return rc;
+  uint8_t* base = sl->base;
+  if ((segment_ids && hipMemcpyAsync(base + o_seg, segment_ids, 4 * (size_t)n,
+                                     hipMemcpyHostToDevice, st) != hipSuccess) ||
+      (accept_mask &&
+       hipMemcpyAsync(base + o_acc, accept_mask, n, hipMemcpyHostToDevice, st) != hipSuccess))
+    rc = PRIO3_EDEVICE;
+  if (rc == PRIO3_OK)
+    rc = run_accumulate(e, R, b->c0, n, R->status + b->c0,
+                        segment_ids ? (const uint32_t*)(base + o_seg) : nullptr,
+                        accept_mask ? base + o_acc : nullptr, n_segments, base + o_agg,
+                        (uint64_t*)(base + o_cnt), st);
+  if (rc == PRIO3_OK &&
+      (hipMemcpyAsync(agg_shares_out, base + o_agg, agg_len * S, hipMemcpyDeviceToHost, st) !=
+           hipSuccess ||
+       hipMemcpyAsync(counts_out, base + o_cnt, 8 * S, hipMemcpyDeviceToHost, st) !=
+           hipSuccess ||
+       hipStreamSynchronize(st) != hipSuccess))
+    rc = PRIO3_EDEVICE;
+  if (e->timing) collect_times(e);
+  ws_release(sl, st);
   return rc;
 }
 
 int prio3_debug_output_shares(prio3_batch* b, uint8_t* out) {
-  if (!b) return PRIO3_EINVAL;
-  return prio3_device_output_shares(b->e, b->n, out);
+  if (!b || !out) return PRIO3_EINVAL;
+  if (!b->run) return PRIO3_OK;
+  HIPCHK(hipSetDevice(b->e->device));
+  PooledStream ps(b->e->device);
+  if (!ps.s) return PRIO3_EDEVICE;
+  return run_output_shares(b->run, b->c0, b->n, out, ps.s);
 }
 
-void prio3_batch_free(prio3_batch* b) { delete b; }
+void prio3_batch_free(prio3_batch* b) {
+  if (!b) return;
+  if (b->run) run_release(b->run, nullptr, false);
+  delete b;
+}
 
 int prio3_engine_timing(prio3_engine* e, char* names, size_t cap_names, double* ms,
                         uint64_t* launches, int cap) {
   if (!e) return PRIO3_EINVAL;
-  std::lock_guard<std::mutex> lk(e->mu);
   (void)hipSetDevice(e->device);
   collect_times(e);
+  std::lock_guard<std::mutex> lk(e->tmu);
   std::string all;
   int k = 0;
   for (auto& t : e->times) {
@@ -3138,8 +3353,8 @@ int prio3_engine_timing(prio3_engine* e, char* names, size_t cap_names, double* 
 
 void prio3_engine_timing_reset(prio3_engine* e) {
   if (!e) return;
-  std::lock_guard<std::mutex> lk(e->mu);
   collect_times(e);
+  std::lock_guard<std::mutex> lk(e->tmu);
   for (auto& t : e->times) {
     t.ms = 0;
     t.launches = 0;
@@ -3147,12 +3362,6 @@ void prio3_engine_timing_reset(prio3_engine* e) {
 }
 
 // ---- leader side ----
-int launch_leader_init(const DevParams& dp, const uint8_t* d_nonces, const uint8_t* d_pub,
-                       const uint8_t* d_lshares, const Scratch& sc, uint8_t* d_prep_shares,
-                       uint8_t* d_status, hipStream_t st);
-int launch_leader_next(const DevParams& dp, const uint8_t* d_prep_msgs, const Scratch& sc,
-                       uint8_t* d_status, hipStream_t st);
-
 int prio3_device_leader_prepare_init(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
                                      const uint8_t* d_public_shares,
                                      const uint8_t* d_leader_input_shares, uint8_t* d_prep_shares,
@@ -3166,56 +3375,31 @@ int prio3_device_leader_prepare_init(prio3_engine* e, uint32_t n, const uint8_t*
     return PRIO3_EINVAL;
   std::lock_guard<std::mutex> lk(e->mu);
   HIPCHK(hipSetDevice(e->device));
-  int rc = ensure_scratch(e, n);
-  if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
-  DevParams dp = e->dp;
-  dp.n = n;
-  dp.force_slow = (uint32_t)e->force_slow;
-  e->leader_n = n;
-  const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
-  if (ps && dp.jr_len && (dp.P == 32 || dp.P == 16 || dp.P == 8) && e->leader_fast) {
-    // the helper kernels in their leader role
-    InPtrs in{d_nonces, d_public_shares, d_leader_input_shares, nullptr};
-    OutPtrs out{d_prep_shares, d_status};
-    const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
-    TIMED(e, st, "k_leader_unpack",
-          (k_leader_unpack<<<(n + 63) / 64, 256, 0, st>>>(dp, in, e->sc, d_status)));
-    TIMED(e, st, "k_jrpart", (k_jrpart<false, true><<<blocks, 256, 0, st>>>(dp, in, e->sc)));
-    TIMED(e, st, "k_leader_slowfix",
-          (k_leader_slowfix<<<blocks64, 64, 0, st>>>(dp, in, e->sc)));
-    if (dp.P == 32)
-      TIMED(e, st, "k_query_h",
-            (k_query_h<2, 32, 1, 3, 1><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
-    else if (dp.P == 16)
-      TIMED(e, st, "k_query_h",
-            (k_query_h<2, 16, 1, 3, 1><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
-    else
-      TIMED(e, st, "k_query_h",
-            (k_query_h<2, 8, 1, 3, 1><<<blocks, 256, 0, st>>>(dp, in, e->sc, out)));
-    return PRIO3_OK;
-  }
-  int rc2 = PRIO3_OK;
-  TIMED(e, st, "k_leader_init",
-        rc2 = launch_leader_init(dp, d_nonces, d_public_shares, d_leader_input_shares, e->sc,
-                                 d_prep_shares, d_status, st));
-  return rc2;
+  int rc = PRIO3_OK;
+  Run* R = device_run(e, n, RUN_SCRATCH, 0, st, &rc);
+  if (!R) return rc;
+  return leader_init_run(e, R, d_nonces, d_public_shares, d_leader_input_shares, d_prep_shares,
+                         d_status, st);
 }
 
 int prio3_device_leader_prepare_next(prio3_engine* e, uint32_t n, const uint8_t* d_prep_msgs,
                                      uint8_t* d_status, void* stream) {
   if (e && (e->dp.kind == PRIO3_SUMVEC_F64_MP || e->dp.kind == PRIO3_FPVEC_BOUNDED_L2))
     return PRIO3_EUNSUPPORTED;  // helper role only
-  if (!e || n > e->cap) return PRIO3_EINVAL;
+  if (!e) return PRIO3_EINVAL;
   if (n == 0) return PRIO3_OK;
   if (!d_status || (e->dp.jr_len && !d_prep_msgs)) return PRIO3_EINVAL;
   std::lock_guard<std::mutex> lk(e->mu);
   HIPCHK(hipSetDevice(e->device));
-  DevParams dp = e->dp;
+  Run* R = e->cur;
+  if (!R || n > R->n) return PRIO3_EINVAL;
+  DevParams dp = R->dp;
   dp.n = n;
   hipStream_t st = (hipStream_t)stream;
+  R->last = st;
   int rc2 = PRIO3_OK;
-  TIMED(e, st, "k_leader_next", rc2 = launch_leader_next(dp, d_prep_msgs, e->sc, d_status, st));
+  TIMED(e, st, "k_leader_next", rc2 = launch_leader_next(dp, d_prep_msgs, R->sc, d_status, st));
   return rc2;
 }
 
@@ -3229,41 +3413,41 @@ int prio3_leader_prepare_init_batch(prio3_engine* e, uint32_t n, const uint8_t* 
     return PRIO3_EINVAL;
   const DevParams& d = e->dp;
   if (n && d.jr_len && !public_shares) return PRIO3_EINVAL;
-  {
-    std::lock_guard<std::mutex> lk(e->mu);
-    HIPCHK(hipSetDevice(e->device));
-    int rc = ensure_io(e, n ? n : 1);
-    if (rc) return rc;
-    if (n > e->linput_cap) {
-      if (e->d_linput) (void)hipFree(e->d_linput);
-      e->d_linput = nullptr;
-      HIPCHK(hipMalloc((void**)&e->d_linput, (size_t)d.leader_share_len * n));
-      e->linput_cap = n;
-    }
-    hipStream_t st = e->stream;
-    if (n) {
-      HIPCHK(hipMemcpyAsync(e->d_nonces, nonces, 16 * (size_t)n, hipMemcpyHostToDevice, st));
-      if (d.jr_len)
-        HIPCHK(hipMemcpyAsync(e->d_pub, public_shares, (size_t)d.public_share_len * n,
-                              hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(e->d_linput, leader_input_shares, (size_t)d.leader_share_len * n,
-                            hipMemcpyHostToDevice, st));
-    }
+  if (n == 0) {
+    if (batch_out) *batch_out = new prio3_batch{e, nullptr, 0, 0};
+    return PRIO3_OK;
   }
-  int rc = prio3_device_leader_prepare_init(e, n, e->d_nonces, e->d_pub, e->d_linput, e->d_leader,
-                                            e->d_status, e->stream);
-  if (rc) return rc;
-  {
-    std::lock_guard<std::mutex> lk(e->mu);
-    hipStream_t st = e->stream;
-    if (n) {
-      HIPCHK(hipMemcpyAsync(status_out, e->d_status, n, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipMemcpyAsync(prep_shares_out, e->d_leader, (size_t)d.prep_share_len * n,
-                            hipMemcpyDeviceToHost, st));
-    }
-    HIPCHK(hipStreamSynchronize(st));
+  HIPCHK(hipSetDevice(e->device));
+  PooledStream ps(e->device);
+  hipStream_t st = ps.s;
+  if (!st) return PRIO3_EDEVICE;
+  int rc = PRIO3_OK;
+  Run* R = run_create(e, n, RUN_SCRATCH | RUN_IO | RUN_LINPUT, 0, 0, st, &rc);
+  if (!R) return rc;
+  if (hipMemcpyAsync(R->nonces, nonces, 16 * (size_t)n, hipMemcpyHostToDevice, st) != hipSuccess ||
+      (d.jr_len && hipMemcpyAsync(R->pub, public_shares, (size_t)d.public_share_len * n,
+                                  hipMemcpyHostToDevice, st) != hipSuccess) ||
+      hipMemcpyAsync(R->linput, leader_input_shares, (size_t)d.leader_share_len * n,
+                     hipMemcpyHostToDevice, st) != hipSuccess)
+    rc = PRIO3_EDEVICE;
+  if (rc == PRIO3_OK)
+    rc = leader_init_run(e, R, R->nonces, d.jr_len ? R->pub : nullptr, R->linput, R->leader,
+                         R->status, st);
+  if (rc == PRIO3_OK &&
+      (hipMemcpyAsync(status_out, R->status, n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+       hipMemcpyAsync(prep_shares_out, R->leader, (size_t)d.prep_share_len * n,
+                      hipMemcpyDeviceToHost, st) != hipSuccess ||
+       hipStreamSynchronize(st) != hipSuccess))
+    rc = PRIO3_EDEVICE;
+  if (e->timing) collect_times(e);
+  if (rc != PRIO3_OK) {
+    run_release(R, st, true);
+    return rc;
   }
-  if (batch_out) *batch_out = new prio3_batch{e, n};
+  if (batch_out)
+    *batch_out = new prio3_batch{e, R, 0, n};
+  else
+    run_release(R, st, true);
   return PRIO3_OK;
 }
 
@@ -3273,22 +3457,27 @@ int prio3_leader_prepare_next_batch(prio3_batch* b, const uint8_t* prep_msgs,
   prio3_engine* e = b->e;
   const uint32_t n = b->n;
   const DevParams& d = e->dp;
-  if (n == 0) return PRIO3_OK;
+  if (n == 0 || !b->run) return PRIO3_OK;
   if (d.jr_len && !prep_msgs) return PRIO3_EINVAL;
-  {
-    std::lock_guard<std::mutex> lk(e->mu);
-    HIPCHK(hipSetDevice(e->device));
-    hipStream_t st = e->stream;
-    if (d.jr_len)
-      HIPCHK(hipMemcpyAsync(e->d_msgs, prep_msgs, (size_t)e->sz.prep_msg_len * n,
-                            hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(e->d_status, status_inout, n, hipMemcpyHostToDevice, st));
-  }
-  int rc = prio3_device_leader_prepare_next(e, n, e->d_msgs, e->d_status, e->stream);
-  if (rc) return rc;
-  std::lock_guard<std::mutex> lk(e->mu);
-  HIPCHK(hipMemcpyAsync(status_inout, e->d_status, n, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(hipStreamSynchronize(e->stream));
+  Run* R = b->run;
+  if (!R->msgs || b->c0 != 0) return PRIO3_EINVAL;  // a leader batch (its own run)
+  HIPCHK(hipSetDevice(e->device));
+  PooledStream ps(e->device);
+  hipStream_t st = ps.s;
+  if (!st) return PRIO3_EDEVICE;
+  if (d.jr_len)
+    HIPCHK(hipMemcpyAsync(R->msgs, prep_msgs, (size_t)e->sz.prep_msg_len * n,
+                          hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(R->status, status_inout, n, hipMemcpyHostToDevice, st));
+  DevParams dp = R->dp;
+  dp.n = n;
+  R->last = st;
+  int rc2 = PRIO3_OK;
+  TIMED(e, st, "k_leader_next", rc2 = launch_leader_next(dp, R->msgs, R->sc, R->status, st));
+  if (rc2) return rc2;
+  HIPCHK(hipMemcpyAsync(status_inout, R->status, n, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (e->timing) collect_times(e);
   return PRIO3_OK;
 }
 

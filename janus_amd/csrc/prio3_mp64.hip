@@ -464,9 +464,9 @@ __global__ __launch_bounds__(256) void k_mp64_prepare(Mp64Params P, uint32_t n, 
   }
 }
 
-int launch_mp64(prio3_engine* e, uint32_t n, InPtrs in, OutPtrs out, Scratch sc,
+int launch_mp64(prio3_engine* e, uint32_t n, uint32_t ld, InPtrs in, OutPtrs out, Scratch sc,
                 hipStream_t st) {
-  k_mp64_prepare<<<(n + 255) / 256, 256, 0, st>>>(e->mp, n, e->dp.ld, in, sc, out,
+  k_mp64_prepare<<<(n + 255) / 256, 256, 0, st>>>(e->mp, n, ld, in, sc, out,
                                                   (uint32_t)e->force_slow);
   return hipGetLastError() == hipSuccess ? PRIO3_OK : PRIO3_EDEVICE;
 }

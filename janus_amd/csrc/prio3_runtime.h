@@ -1,0 +1,72 @@
+// prio3_runtime.h -- the host runtime under the C ABI: a per-GPU pool of device scratch slabs
+// shared by every engine on that GPU, a per-GPU pool of HIP streams for the blocking host-buffer
+// entry points, and the per-GPU executor that coalesces concurrent aggregation jobs into one
+// device launch (SURVEY.md 8(b) "Threading"; Janus runs one rayon::spawn per job,
+// /root/reference/aggregator/src/aggregator.rs:2100-2123, jobs of 100-500 reports,
+// /root/reference/aggregator/src/binaries/aggregation_job_creator.rs:63-64).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+// ---- device scratch slabs ----------------------------------------------------------------
+// A slab is one hipMalloc'ed byte range.  Released slabs return to the GPU's pool with an event
+// recorded on the releasing stream; the next acquirer's stream waits on that event, so reuse is
+// stream-ordered and no host synchronisation is needed.  Idle slabs beyond the pool's byte
+// budget are freed (oldest first).
+struct Slab {
+  uint8_t* base = nullptr;
+  size_t bytes = 0;
+  int device = 0;
+  hipEvent_t idle = nullptr;
+  bool pending = false;  // `idle` recorded and not yet known complete
+};
+// returns nullptr (rc = PRIO3_EDEVICE) when the device cannot provide `bytes`
+Slab* ws_acquire(int device, size_t bytes, hipStream_t st, int* rc);
+void ws_release(Slab* s, hipStream_t st);
+// bytes currently held by the GPU's pool (idle + in use), for tests
+size_t ws_pool_bytes(int device, size_t* idle_bytes);
+
+// ---- stream pool ---------------------------------------------------------------------------
+hipStream_t ws_stream_get(int device);  // nullptr on failure
+void ws_stream_put(int device, hipStream_t s);
+
+// ---- coalescing executor -------------------------------------------------------------------
+struct prio3_engine;
+struct Run;
+struct ExecJob {
+  prio3_engine* e;
+  uint32_t n;
+  const uint8_t *nonces, *pub, *helper, *leader;  // host inputs (packed per report)
+  uint8_t *msgs_out, *status_out;                 // host outputs
+  // results
+  int rc = 0;
+  Run* run = nullptr;  // holds one reference for this job
+  uint32_t c0 = 0;     // the job's first column in the run
+};
+// Blocks until the job's reports are prepared (alone or coalesced with concurrent jobs of
+// engines with the same VDAF instance on the same GPU).
+int exec_submit(ExecJob* job);
+
+// Engine hooks the executor calls (prio3_engine.hip).
+// Staging layout of a group with room for `cap` reports (pinned host buffer): the four input
+// fields [cap][len] (nonces, public shares, helper shares, leader prep shares), the per-report
+// verify-key slot (u16), the verify-key table [exec_max_keys()][16], then the outputs: prepare
+// messages [cap][msg_len] and statuses [cap].
+struct IoLayout {
+  size_t len[4], off[4];
+  size_t slot_off, tab_off, msg_off, status_off, msg_len, bytes;
+};
+void engine_io_layout(const prio3_engine* e, uint32_t cap, IoLayout* L);
+struct GroupView {
+  uint32_t n, cap;  // reports staged, staging capacity
+  uint8_t* stg;     // pinned staging (IoLayout for cap)
+  uint32_t n_keys;  // verify keys in the table
+  int jobs;         // references the run must carry (one per job)
+};
+int engine_device(const prio3_engine* e);
+uint64_t engine_group_key(const prio3_engine* e);  // equal keys may share one launch
+void engine_vk(const prio3_engine* e, uint8_t out[16]);
+int engine_run_group(prio3_engine* lead, const GroupView& g, Run** run_out);
+uint32_t exec_max_keys();

@@ -290,7 +290,10 @@ class HelperEngine:
     """One engine per (Prio3 instance, verify key, GPU) -- created where Janus builds
     ``VdafOps`` for a task (aggregator.rs:880-988)."""
 
-    def __init__(self, vdaf: Prio3, verify_key: bytes, device: int = 0):
+    def __init__(self, vdaf: Prio3, verify_key: bytes, device: int = 0,
+                 allow_unpinned: bool = False):
+        """allow_unpinned: required for Prio3FixedPointBoundedL2VecSum, whose circuit is a
+        reconstruction with parity against prio unpinned (engine option experimental_fpvec)."""
         vk_len = 32 if vdaf.kind == PRIO3_SUMVEC_F64_MP else 16
         if len(verify_key) != vk_len:
             raise ValueError(f"verify key must be {vk_len} bytes (VERIFY_KEY_LENGTH[_HMACSHA256_"
@@ -304,6 +307,8 @@ class HelperEngine:
         if rc:
             raise RuntimeError(f"prio3_engine_create failed (rc={rc}); a GPU is required")
         self.handle = h
+        if vdaf.kind == PRIO3_FPVEC_BOUNDED_L2 and allow_unpinned:
+            self.set_option("experimental_fpvec", 1)
 
     def close(self):
         if getattr(self, "handle", None):

@@ -188,7 +188,7 @@ def _tamper(v, reps, frac, seed):
 def _run(v, reps, sub_bytes=None):
     from janus_amd import prio3 as J
     t = v.t
-    eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(t.length, t.bits), VK)
+    eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(t.length, t.bits), VK, allow_unpinned=True)
     if sub_bytes:
         eng.set_option("fp_sub_bytes", sub_bytes)
     A = lambda k: np.array([list(r[k]) for r in reps], np.uint8)
@@ -268,7 +268,8 @@ def test_gpu_fpvec_c5_full_size():
     g = np.load(GOLDEN_C5)
     n = 384
     idx = np.arange(n) % 3
-    eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(10000, 16), bytes(g["verify_key"]))
+    eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(10000, 16), bytes(g["verify_key"]),
+                         allow_unpinned=True)
     msgs, status, batch = eng.prepare_batch(g["nonce"][idx], g["pub"][idx], g["helper"][idx],
                                             g["lps"][idx])
     assert status.tolist() == g["status"][idx].tolist()
@@ -297,7 +298,7 @@ def test_gpu_fpvec_stream_overlapped_sub_batches(overlap):
     _tamper(v, reps, 0.05, seed=4)
     from janus_amd import prio3 as J
     t = v.t
-    eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(t.length, t.bits), VK)
+    eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(t.length, t.bits), VK, allow_unpinned=True)
     eng.set_option("fp_overlap", overlap)
     A = lambda k: np.array([list(r[k]) for r in reps], np.uint8)
     msgs, status, batch = eng.prepare_batch(A("nonce"), A("pub"), A("helper"), A("lps"))
@@ -318,7 +319,7 @@ def test_gpu_fpvec_scratch_wider_than_sub_batch():
     reps = _reports(v, 1000, seed=41, distinct=100)
     _tamper(v, reps, 0.05, seed=5)
     per = 16 * (t.meas_len + t.proof_len + 2 + 2 + 2 * (t.P0 + t.P1) + t.K0) + 33
-    eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(t.length, t.bits), VK)
+    eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(t.length, t.bits), VK, allow_unpinned=True)
     eng.set_option("fp_sub_bytes", per * 768 + per // 2)
     eng.set_option("timing", 1)
     A = lambda k: np.array([list(r[k]) for r in reps], np.uint8)
@@ -327,3 +328,16 @@ def test_gpu_fpvec_scratch_wider_than_sub_batch():
     outs = batch.output_shares()
     agg, cnt = batch.accumulate()
     _check(v, reps, (msgs, status, outs, agg, cnt))
+
+
+@pytest.mark.gpu
+def test_gpu_fpvec_requires_explicit_opt_in():
+    """the reconstructed (parity-unpinned) FPVec circuit prepares only after the
+    experimental_fpvec opt-in; without it every prepare entry point returns EUNSUPPORTED."""
+    from janus_amd import prio3 as J
+    v = _vdaf(3)
+    reps = _reports(v, 4, seed=3)
+    eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(3, 16), VK)
+    A = lambda k: np.array([list(r[k]) for r in reps], np.uint8)
+    with pytest.raises(RuntimeError, match="rc=-3"):
+        eng.prepare_batch(A("nonce"), A("pub"), A("helper"), A("lps"))

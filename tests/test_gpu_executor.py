@@ -1,0 +1,145 @@
+"""The host runtime under the C ABI: per-batch device state and the coalescing executor.
+
+* Janus prepares concurrent aggregation jobs of one task on one VdafOps (one engine), each in
+  its own rayon::spawn (/root/reference/aggregator/src/aggregator.rs:2100-2123), and merges each
+  job's output shares later (aggregation_job_writer.rs:591-695).  A batch handle must therefore
+  keep its own output shares and verdicts however many other batches were prepared since
+  (ADVICE r1, high).
+* Concurrent jobs of engines with the same VDAF instance -- different tasks, different verify
+  keys -- are merged into one launch by the executor (per-report verify-key slots); every job
+  must still get exactly its own bytes back.
+Expected values come from the CPU restatement (oracle/), Janus job structure.
+"""
+import threading
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+from tests.conftest import CONFIGS
+from tests.test_gpu_parity import _tamper
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(cfg, vk):
+    from janus_amd import prio3 as J
+    k = cfg["kind"]
+    v = {"count": lambda: J.Prio3Count(), "sum": lambda: J.Prio3Sum(cfg["bits"]),
+         "sumvec": lambda: J.Prio3SumVec(cfg["bits"], cfg["length"], cfg["chunk_length"]),
+         "histogram": lambda: J.Prio3Histogram(cfg["length"], cfg["chunk_length"])}[k]()
+    return J.HelperEngine(v, vk, device=0)
+
+
+def _ref(o, vk, d, seg=None, accept=None, n_segments=1):
+    return o.helper_batch(vk, d["nonces"], d["public_shares"], d["helper_shares"],
+                          d["leader_prep_shares"], segment_ids=seg, accept_mask=accept,
+                          n_segments=n_segments, n_threads=4)
+
+
+def test_interleaved_batches_keep_their_own_outputs():
+    from oracle.oracle import Oracle
+    cfg = CONFIGS["hist_256_c16"]
+    vk = bytes(range(0x10, 0x20))
+    o = Oracle(**cfg)
+    eng = _engine(cfg, vk)
+    rng = np.random.default_rng(5)
+    dA = _tamper(o, o.gen_reports(vk, 300, seed=1, n_threads=4), rng)
+    dB = o.gen_reports(vk, 517, seed=2, n_threads=4)
+    mA, sA, bA = eng.prepare_batch(dA["nonces"], dA["public_shares"], dA["helper_shares"],
+                                   dA["leader_prep_shares"])
+    mB, sB, bB = eng.prepare_batch(dB["nonces"], dB["public_shares"], dB["helper_shares"],
+                                   dB["leader_prep_shares"])
+    # a leader batch on the same engine in between as well (the device client derives report i
+    # from (seed, i) exactly as the oracle's generator, so these are dB's leader input shares)
+    gB = eng.generate_reports_device(517, seed=2, with_leader_inputs=True)
+    ps, lst, lb = eng.leader_prepare_init_batch(dB["nonces"], dB["public_shares"],
+                                                gB["leader_input_shares"].cpu().numpy())
+    segA = rng.integers(0, 3, 300).astype(np.uint32)
+    accA = (rng.random(300) < 0.9).astype(np.uint8)
+    rm, rs, ra, rc = _ref(o, vk, dA, segA, accA, 3)
+    np.testing.assert_array_equal(sA, rs)
+    np.testing.assert_array_equal(mA, rm)
+    agg, cnt = bA.accumulate(segA, accA, 3)
+    np.testing.assert_array_equal(agg, ra)
+    np.testing.assert_array_equal(cnt, rc)
+    rm, rs, ra, rc = _ref(o, vk, dB)
+    agg, cnt = bB.accumulate()
+    np.testing.assert_array_equal(agg, ra)
+    assert int(cnt[0]) == 517
+    np.testing.assert_array_equal(ps, dB["leader_prep_shares"])
+    # output shares of A are still A's
+    outs = bA.output_shares()
+    assert outs.shape == (300, 4096)
+    fin = np.flatnonzero(sA == 0)
+    from oracle.oracle import sum_mod, decode_elems, field_modulus
+    p = field_modulus("histogram")
+    tot = sum_mod(outs[fin], 16, p)
+    ref_tot = decode_elems(_ref(o, vk, dA)[2][0], 16)
+    assert tot == ref_tot
+    for b in (bA, bB, lb):
+        b.free()
+
+
+@pytest.mark.parametrize("name", ["hist_256_c16", "sumvec_8x10_c9", "count"])
+def test_concurrent_jobs_of_several_tasks_are_coalesced(name):
+    """24 jobs of 100-500 reports for 4 tasks (verify keys) of one VDAF instance from 8 threads
+    at once: every job's prepare messages, statuses and aggregate equal the restatement's, and
+    the executor merged them into fewer launches than jobs."""
+    from oracle.oracle import Oracle
+    cfg = CONFIGS[name]
+    o = Oracle(**cfg)
+    vks = [bytes([k]) * 16 for k in (0x31, 0x32, 0x33, 0x34)]
+    engines = [_engine(cfg, vk) for vk in vks]
+    for e in engines:
+        e.set_option("timing", 1)
+        e.timing_reset()
+    rng = np.random.default_rng(9)
+    jobs = []
+    for j in range(24):
+        t = j % 4
+        n = int(rng.integers(100, 501))
+        d = o.gen_reports(vks[t], n, seed=100 + j, n_threads=4)
+        if j % 3 == 0:
+            d = _tamper(o, d, rng)
+        jobs.append((t, d))
+    start = threading.Barrier(8)
+
+    def run(j):
+        t, d = jobs[j]
+        if j < 8:
+            start.wait()
+        msgs, status, batch = engines[t].prepare_batch(d["nonces"], d["public_shares"],
+                                                       d["helper_shares"],
+                                                       d["leader_prep_shares"])
+        agg, cnt = batch.accumulate()
+        batch.free()
+        return msgs, status, agg, cnt
+
+    with ThreadPoolExecutor(8) as ex:
+        got = list(ex.map(run, range(24)))
+    for (t, d), (msgs, status, agg, cnt) in zip(jobs, got):
+        rm, rs, ra, rc = _ref(o, vks[t], d)
+        np.testing.assert_array_equal(status, rs)
+        np.testing.assert_array_equal(msgs, rm)
+        np.testing.assert_array_equal(agg, ra)
+        np.testing.assert_array_equal(cnt, rc)
+    kern = "k_xofd" if name != "count" else "k_xof"
+    launches = sum(e.timing().get(kern, (0, 0))[1] for e in engines)
+    assert 0 < launches < 24, launches
+
+
+def test_coalescing_off_matches():
+    from oracle.oracle import Oracle
+    cfg = CONFIGS["hist_10_c3"]
+    vk = bytes(range(16))
+    o = Oracle(**cfg)
+    eng = _engine(cfg, vk)
+    eng.set_option("coalesce", 0)
+    d = o.gen_reports(vk, 333, seed=4, n_threads=4)
+    msgs, status, batch = eng.prepare_batch(d["nonces"], d["public_shares"], d["helper_shares"],
+                                            d["leader_prep_shares"])
+    rm, rs, ra, rc = _ref(o, vk, d)
+    np.testing.assert_array_equal(msgs, rm)
+    agg, cnt = batch.accumulate()
+    np.testing.assert_array_equal(agg, ra)

@@ -101,7 +101,7 @@ def test_reference_e2e_on_device(name):
     t, meas = CASES[name]
     v = P.Prio3(t)
     reps = _shard_all(v, meas, seed=len(name))
-    eng = J.HelperEngine(_engine_vdaf(t), VK)
+    eng = J.HelperEngine(_engine_vdaf(t), VK, allow_unpinned=True)
     sz = eng.sz
     n = len(reps)
     A = lambda k, w: np.array([np.frombuffer(r[k], np.uint8) for r in reps], np.uint8).reshape(n, w)
