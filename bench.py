@@ -100,7 +100,7 @@ def main():
     ap.add_argument("--vdaf", choices=["count", "sumvec", "sum32"], default="sumvec",
                     help="--role config: C1 Prio3Count (100k), C3 Prio3SumVec 8x1000 chunk 63 "
                          "(1M/8 per GPU), C4 Prio3Sum 32 (10M/8 per GPU)")
-    ap.add_argument("--threads", type=int, default=16,
+    ap.add_argument("--threads", type=int, default=128,
                     help="--role jobs: host worker threads (Janus's rayon pool)")
     ap.add_argument("--job-size", type=int, default=500,
                     help="--role jobs: reports per aggregation job (aggregation_job_creator.rs:63-64)")

@@ -1682,6 +1682,71 @@ __global__ void k_acc_fin(uint32_t nchunks, uint32_t out_len, uint32_t nseg, con
 }
 
 
+// Accumulate of many small batches in one launch (the accumulate executor: concurrent
+// prio3_accumulate calls of Janus's aggregation jobs).  grid: x = output element, y = job; the
+// block sums its element over the job's reports (inclusion as k_code) into up to 8 segments at
+// a time and writes the job's aggregate share element and, from element 0, its counts.
+template <class F>
+__global__ __launch_bounds__(256) void k_acc_multi(const AccDesc* descs, uint8_t* base) {
+  typedef typename F::T T;
+  __shared__ T red[256];
+  __shared__ uint32_t cred[256];
+  const AccDesc d = descs[blockIdx.y];
+  const uint32_t e = blockIdx.x;
+  if (e >= d.out_len) return;  // uniform per block
+  const uint32_t* seg = (d.flags & 1) ? (const uint32_t*)(base + d.seg_off) : nullptr;
+  const uint8_t* acc = (d.flags & 2) ? base + d.acc_off : nullptr;
+  for (uint32_t s0 = 0; s0 < d.nseg; s0 += 8) {
+    T a[8];
+    uint32_t c[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      a[q] = F::zero();
+      c[q] = 0;
+    }
+    for (uint32_t r = threadIdx.x; r < d.n; r += 256) {
+      const uint32_t s = seg ? seg[r] : 0u;
+      const bool inc = d.status[r] == PRIO3_STATUS_FINISHED && s < d.nseg && (!acc || acc[r]);
+      const uint32_t k = s - s0;
+      if (inc && k < 8u) {
+        const T x = F::load(d.src, (size_t)e * d.ld + r);
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+          if ((uint32_t)q == k) {
+            a[q] = F::add(a[q], x);
+            c[q]++;
+          }
+      }
+    }
+    const uint32_t ns = min(8u, d.nseg - s0);
+    for (uint32_t q = 0; q < ns; q++) {
+      T v = F::zero();
+      uint32_t cv = 0;
+#pragma unroll
+      for (int q2 = 0; q2 < 8; q2++)
+        if ((uint32_t)q2 == q) {
+          v = a[q2];
+          cv = c[q2];
+        }
+      red[threadIdx.x] = v;
+      cred[threadIdx.x] = cv;
+      __syncthreads();
+      for (uint32_t st = 128; st > 0; st >>= 1) {
+        if (threadIdx.x < st) {
+          red[threadIdx.x] = F::add(red[threadIdx.x], red[threadIdx.x + st]);
+          cred[threadIdx.x] += cred[threadIdx.x + st];
+        }
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) {
+        F::store(base + d.agg_off, (size_t)(s0 + q) * d.out_len + e, red[0]);
+        if (e == 0) ((uint64_t*)(base + d.cnt_off))[s0 + q] = cred[0];
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // Fused accumulate, second half: combine the per-wave half-limb partials per segment,
 // then fix up exclusions / non-fused reports and reduce mod p.
@@ -2883,6 +2948,81 @@ int engine_run_group(prio3_engine* lead, const GroupView& g, Run** run_out) {
   return PRIO3_OK;
 }
 
+
+// ---- accumulate-executor hooks (prio3_runtime.h) ----
+uint32_t engine_acc_key(const AccJob* j) { return j->run->dp.es; }
+
+size_t engine_acc_out_bytes(const AccJob* j) {
+  const size_t agg = (size_t)j->run->dp.out_len * j->run->dp.es * j->nseg;
+  return ((agg + 7) & ~(size_t)7) + 8 * (size_t)j->nseg;
+}
+
+void engine_acc_stage(AccJob* j, uint8_t* stg, const AccLayout& L) {
+  const Run* R = j->run;
+  const DevParams& d = R->dp;
+  AccDesc& D = ((AccDesc*)(stg + L.desc_off))[j->slot];
+  D.src = (const uint8_t*)(own_out(d) ? R->sc.out : R->sc.meas) + (size_t)d.es * j->c0;
+  D.status = R->status + j->c0;
+  D.ld = d.ld_out;
+  D.n = j->n;
+  D.nseg = j->nseg;
+  D.out_len = d.out_len;
+  D.flags = (j->seg ? 1u : 0u) | (j->accept ? 2u : 0u);
+  D.seg_off = L.seg_off + 4 * (size_t)j->rep_off;
+  D.acc_off = L.acc_off + j->rep_off;
+  D.agg_off = L.out_off + j->out_off;
+  const size_t agg = (size_t)d.out_len * d.es * j->nseg;
+  D.cnt_off = D.agg_off + ((agg + 7) & ~(size_t)7);
+  if (j->seg) memcpy(stg + D.seg_off, j->seg, 4 * (size_t)j->n);
+  if (j->accept) memcpy(stg + D.acc_off, j->accept, j->n);
+}
+
+void engine_acc_unstage(AccJob* j, const uint8_t* stg, const AccLayout& L) {
+  const DevParams& d = j->run->dp;
+  const AccDesc& D = ((const AccDesc*)(stg + L.desc_off))[j->slot];
+  memcpy(j->agg_out, stg + D.agg_off, (size_t)d.out_len * d.es * j->nseg);
+  memcpy(j->counts_out, stg + D.cnt_off, 8 * (size_t)j->nseg);
+}
+
+int engine_acc_group(int device, int es, uint8_t* stg, const AccLayout& L, uint32_t n_jobs,
+                     size_t out_bytes) {
+  HIPCHK(hipSetDevice(device));
+  PooledStream ps(device);
+  hipStream_t st = ps.s;
+  if (!st) return PRIO3_EDEVICE;
+  int rc = PRIO3_OK;
+  Slab* sl = ws_acquire(device, L.bytes, st, &rc);
+  if (!sl) return rc;
+  const AccDesc* D = (const AccDesc*)(stg + L.desc_off);
+  uint32_t reps = 0, max_len = 0;
+  for (uint32_t i = 0; i < n_jobs; i++) {
+    reps = std::max(reps, (uint32_t)((D[i].acc_off - L.acc_off) + D[i].n));
+    max_len = std::max(max_len, D[i].out_len);
+  }
+  uint8_t* b = sl->base;
+  if (hipMemcpyAsync(b + L.desc_off, stg + L.desc_off, sizeof(AccDesc) * n_jobs,
+                     hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(b + L.seg_off, stg + L.seg_off, 4 * (size_t)reps, hipMemcpyHostToDevice,
+                     st) != hipSuccess ||
+      hipMemcpyAsync(b + L.acc_off, stg + L.acc_off, reps, hipMemcpyHostToDevice, st) !=
+          hipSuccess)
+    rc = PRIO3_EDEVICE;
+  if (rc == PRIO3_OK) {
+    dim3 grid(max_len, n_jobs);
+    if (es == 16)
+      k_acc_multi<Fp128><<<grid, 256, 0, st>>>((const AccDesc*)(b + L.desc_off), b);
+    else
+      k_acc_multi<Fp64><<<grid, 256, 0, st>>>((const AccDesc*)(b + L.desc_off), b);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(stg + L.out_off, b + L.out_off, out_bytes, hipMemcpyDeviceToHost, st) !=
+            hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      rc = PRIO3_EDEVICE;
+  }
+  ws_release(sl, st);
+  return rc;
+}
+
 extern "C" {
 
 int prio3_sizes(const prio3_params* params, prio3_sizes_t* out) {
@@ -3279,6 +3419,19 @@ int prio3_accumulate(prio3_batch* b, const uint32_t* segment_ids, const uint8_t*
   }
   Run* R = b->run;
   const uint32_t n = b->n;
+  if (n <= (1u << 14) && e->coalesce) {  // a job-sized batch: coalesced with concurrent ones
+    AccJob job;
+    job.device = e->device;
+    job.run = R;
+    job.c0 = b->c0;
+    job.n = n;
+    job.seg = segment_ids;
+    job.accept = accept_mask;
+    job.nseg = n_segments;
+    job.agg_out = agg_shares_out;
+    job.counts_out = counts_out;
+    if (engine_acc_out_bytes(&job) <= ((size_t)16 << 20)) return exec_accumulate(&job);
+  }
   HIPCHK(hipSetDevice(e->device));
   PooledStream ps(e->device);
   hipStream_t st = ps.s;

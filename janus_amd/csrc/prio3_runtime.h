@@ -44,6 +44,7 @@ struct ExecJob {
   int rc = 0;
   Run* run = nullptr;  // holds one reference for this job
   uint32_t c0 = 0;     // the job's first column in the run
+  uint32_t slot = 0;   // the job's verify-key slot in its group
 };
 // Blocks until the job's reports are prepared (alone or coalesced with concurrent jobs of
 // engines with the same VDAF instance on the same GPU).
@@ -70,3 +71,40 @@ uint64_t engine_group_key(const prio3_engine* e);  // equal keys may share one l
 void engine_vk(const prio3_engine* e, uint8_t out[16]);
 int engine_run_group(prio3_engine* lead, const GroupView& g, Run** run_out);
 uint32_t exec_max_keys();
+
+// ---- coalesced accumulate (prio3_accumulate of concurrent jobs) ----------------------------
+struct AccJob {
+  int device = 0;
+  Run* run = nullptr;
+  uint32_t c0 = 0, n = 0;       // the batch's columns
+  const uint32_t* seg = nullptr;  // host segment ids [n] (nullable)
+  const uint8_t* accept = nullptr;  // host accept mask [n] (nullable)
+  uint32_t nseg = 1;
+  uint8_t* agg_out = nullptr;    // host [nseg][agg_len]
+  uint64_t* counts_out = nullptr;  // host [nseg]
+  // placement in the group
+  uint32_t slot = 0, rep_off = 0;
+  size_t out_off = 0;
+};
+// one per job of an accumulate group (device-visible); *_off are byte offsets into the group's
+// device region
+struct AccDesc {
+  const uint8_t* src;     // output shares of the job's first column, SoA [element][ld]
+  const uint8_t* status;  // the job's verdicts [n]
+  uint64_t ld;
+  uint32_t n, nseg, out_len, flags;  // flags: 1 = segment ids, 2 = accept mask
+  uint64_t seg_off, acc_off, agg_off, cnt_off;
+};
+struct AccLayout {
+  uint32_t max_jobs, max_reps;
+  size_t out_cap, desc_off, seg_off, acc_off, out_off, bytes;
+};
+void acc_layout(uint32_t max_jobs, uint32_t max_reps, size_t out_cap, AccLayout* L);
+int exec_accumulate(AccJob* job);
+// engine hooks (prio3_engine.hip)
+uint32_t engine_acc_key(const AccJob* j);  // jobs with equal keys share a launch (field size)
+size_t engine_acc_out_bytes(const AccJob* j);
+void engine_acc_stage(AccJob* j, uint8_t* stg, const AccLayout& L);
+void engine_acc_unstage(AccJob* j, const uint8_t* stg, const AccLayout& L);
+int engine_acc_group(int device, int es, uint8_t* stg, const AccLayout& L, uint32_t n_jobs,
+                     size_t out_bytes);

@@ -29,6 +29,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/janus_prio3.h"
@@ -193,7 +194,12 @@ void ws_stream_put(int device, hipStream_t s) {
   sp.free.push_back(s);
 }
 
-// ---- executor -------------------------------------------------------------------------------
+// ---- executors -----------------------------------------------------------------------------
+// A generic group-commit executor, one per (GPU, work kind).  Callers reserve room in the open
+// group of their key and stage their inputs themselves (in parallel); `max_inflight` launcher
+// threads per executor take the oldest ready group -- or, when idle, the oldest open one -- wait
+// for its writers, launch it and wake exactly that group's callers.  An idle GPU therefore runs a
+// lone job at once, and under load jobs pile into the next group while launchers are busy.
 namespace {
 
 struct Staging {
@@ -201,34 +207,51 @@ struct Staging {
   size_t bytes = 0;
 };
 
-struct Group {
-  uint64_t key = 0;
-  prio3_engine* lead = nullptr;
-  std::vector<ExecJob*> jobs;
-  std::vector<const prio3_engine*> keys;  // verify-key table, slot = index
-  uint32_t n = 0, cap = 0;
-  size_t per_in = 0, per_out = 0;  // bytes per report (inputs incl. slot, outputs)
-  int writers = 0, readers = 0;
-  bool closed = false, flushing = false, done = false;
-  int rc = PRIO3_OK;
-  Staging stg;
-  size_t in_bytes = 0, out_bytes = 0, slot_off = 0, tab_off = 0;
-  Run* run = nullptr;
-};
+constexpr size_t STAGING_TARGET = (size_t)96 << 20;  // pinned bytes per group (grows to fit)
 
-struct Executor {
+struct StagingPool {
   std::mutex mu;
-  std::condition_variable cv;
-  std::map<uint64_t, Group*> open;
-  std::vector<Staging> staging;  // idle pinned buffers
-  int inflight = 0;
+  std::vector<Staging> idle;
 };
-Executor g_exec[MAX_DEVICES];
+StagingPool* g_staging = new StagingPool[MAX_DEVICES];  // never destroyed (see Exec)
+
+Staging staging_get(int dev, size_t bytes) {
+  {
+    std::lock_guard<std::mutex> lk(g_staging[dev].mu);
+    auto& v = g_staging[dev].idle;
+    for (size_t i = 0; i < v.size(); i++)
+      if (v[i].bytes >= bytes) {
+        Staging s = v[i];
+        v.erase(v.begin() + (long)i);
+        return s;
+      }
+  }
+  Staging s;
+  s.bytes = std::max(bytes, STAGING_TARGET);
+  if (hipSetDevice(dev) != hipSuccess ||
+      hipHostMalloc((void**)&s.p, s.bytes, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    s.p = nullptr;
+    s.bytes = 0;
+  }
+  return s;
+}
+
+void staging_put(int dev, Staging s) {
+  if (!s.p) return;
+  std::lock_guard<std::mutex> lk(g_staging[dev].mu);
+  auto& v = g_staging[dev].idle;
+  v.push_back(s);
+  if (v.size() > 8) {  // keep a few
+    (void)hipHostFree(v.front().p);
+    v.erase(v.begin());
+  }
+}
 
 int max_inflight() {
   static const int v = [] {
     const char* s = getenv("JANUS_PRIO3_MAX_INFLIGHT");
-    const int x = s ? atoi(s) : 2;
+    const int x = s ? atoi(s) : 1;
     return x < 1 ? 1 : x;
   }();
   return v;
@@ -241,154 +264,235 @@ uint32_t max_group_reports() {
   }();
   return v;
 }
-constexpr size_t STAGING_TARGET = (size_t)96 << 20;  // pinned bytes per group (grows to fit)
 
-Staging staging_get(Executor& X, size_t bytes) {  // caller holds X.mu
-  for (size_t i = 0; i < X.staging.size(); i++)
-    if (X.staging[i].bytes >= bytes) {
-      Staging s = X.staging[i];
-      X.staging.erase(X.staging.begin() + (long)i);
-      return s;
+template <class P>
+struct Exec {
+  struct Group {
+    uint64_t key = 0;
+    typename P::State st;
+    Staging stg;
+    int writers = 0, readers = 0;
+    bool closed = false, done = false;
+    int rc = PRIO3_OK;
+    std::condition_variable cv;
+  };
+  int device = 0;
+  std::mutex mu;
+  std::condition_variable cv;  // launchers
+  std::map<uint64_t, Group*> open;
+  std::deque<Group*> order;  // groups not yet taken by a launcher, oldest first
+  bool started = false;
+
+  void launcher() {
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      while (order.empty()) cv.wait(lk);
+      Group* g = order.front();
+      order.pop_front();
+      if (!g->closed) {  // take an open group: no later job joins it
+        g->closed = true;
+        auto it = open.find(g->key);
+        if (it != open.end() && it->second == g) open.erase(it);
+      }
+      while (g->writers > 0) g->cv.wait(lk);
+      lk.unlock();
+      const int rc = P::launch(device, g->st, g->stg);
+      lk.lock();
+      g->rc = rc;
+      g->done = true;
+      g->cv.notify_all();
     }
-  Staging s;
-  s.bytes = std::max(bytes, STAGING_TARGET);
-  if (hipHostMalloc((void**)&s.p, s.bytes, hipHostMallocDefault) != hipSuccess) {
-    (void)hipGetLastError();
-    s.p = nullptr;
-    s.bytes = 0;
   }
-  return s;
-}
 
-void staging_put(Executor& X, Staging s) {  // caller holds X.mu
-  if (!s.p) return;
-  X.staging.push_back(s);
-  if (X.staging.size() > 8) {  // keep a few
-    (void)hipHostFree(X.staging.front().p);
-    X.staging.erase(X.staging.begin());
+  int submit(typename P::Job* job) {
+    std::unique_lock<std::mutex> lk(mu);
+    if (!started) {
+      started = true;
+      for (int i = 0; i < max_inflight(); i++) std::thread([this] { launcher(); }).detach();
+    }
+    const uint64_t key = P::key(job);
+    Group* g = nullptr;
+    for (;;) {
+      auto it = open.find(key);
+      g = it == open.end() ? nullptr : it->second;
+      if (g && P::reserve(g->st, job)) break;
+      if (g) {  // full: it stays queued for a launcher as it is
+        g->closed = true;
+        open.erase(it);
+      }
+      g = new Group();
+      g->key = key;
+      size_t bytes = 0;
+      if (!P::create(g->st, job, &bytes)) {
+        delete g;
+        return PRIO3_EINVAL;
+      }
+      g->stg = staging_get(device, bytes);
+      if (!g->stg.p) {
+        delete g;
+        return PRIO3_EDEVICE;
+      }
+      open[key] = g;
+      order.push_back(g);
+      cv.notify_one();
+      if (!P::reserve(g->st, job)) return PRIO3_EINVAL;  // cannot happen: sized for the job
+      break;
+    }
+    g->writers++;
+    g->readers++;
+    lk.unlock();
+    P::stage(g->st, g->stg, job);
+    lk.lock();
+    if (--g->writers == 0) g->cv.notify_all();
+    while (!g->done) g->cv.wait(lk);
+    const int rc = g->rc;
+    lk.unlock();
+    if (rc == PRIO3_OK) P::unstage(g->st, g->stg, job);
+    lk.lock();
+    if (--g->readers == 0) {
+      staging_put(device, g->stg);
+      delete g;
+    }
+    return rc;
   }
-}
+};
+
+// ---- prepare groups ----
+struct PrepPolicy {
+  typedef ExecJob Job;
+  struct State {
+    prio3_engine* lead = nullptr;
+    std::vector<const prio3_engine*> keys;  // verify-key table, slot = index
+    uint32_t n = 0, cap = 0, jobs = 0;
+    IoLayout L;
+    Run* run = nullptr;
+  };
+  static uint64_t key(Job* j) { return engine_group_key(j->e); }
+  static bool create(State& s, Job* j, size_t* bytes) {
+    s.lead = j->e;
+    IoLayout l1, l2;
+    engine_io_layout(j->e, 1, &l1);
+    engine_io_layout(j->e, 2, &l2);
+    const size_t per = l2.bytes - l1.bytes + 1;
+    const uint32_t cap_b = (uint32_t)std::max<size_t>(1, STAGING_TARGET / per);
+    s.cap = std::max(j->n, std::min(max_group_reports(), cap_b));
+    engine_io_layout(j->e, s.cap, &s.L);
+    *bytes = s.L.bytes;
+    return true;
+  }
+  static bool reserve(State& s, Job* j) {
+    uint32_t k = 0;
+    while (k < s.keys.size() && s.keys[k] != j->e) k++;
+    if (k == s.keys.size() && s.keys.size() >= exec_max_keys()) return false;
+    if (s.n + j->n > s.cap) return false;
+    if (k == s.keys.size()) s.keys.push_back(j->e);
+    j->c0 = s.n;
+    j->slot = k;
+    s.n += j->n;
+    s.jobs++;
+    return true;
+  }
+  static void stage(State& s, Staging& g, Job* j) {
+    const IoLayout& L = s.L;
+    const uint8_t* src[4] = {j->nonces, j->pub, j->helper, j->leader};
+    for (int f = 0; f < 4; f++)
+      if (L.len[f] && src[f])
+        memcpy(g.p + L.off[f] + L.len[f] * j->c0, src[f], L.len[f] * j->n);
+    uint16_t* slots = (uint16_t*)(g.p + L.slot_off) + j->c0;
+    for (uint32_t i = 0; i < j->n; i++) slots[i] = (uint16_t)j->slot;
+    engine_vk(j->e, g.p + L.tab_off + 16 * (size_t)j->slot);
+  }
+  static int launch(int device, State& s, Staging& g) {
+    (void)device;
+    GroupView v;
+    v.n = s.n;
+    v.cap = s.cap;
+    v.stg = g.p;
+    v.n_keys = (uint32_t)s.keys.size();
+    v.jobs = (int)s.jobs;
+    return engine_run_group(s.lead, v, &s.run);
+  }
+  static void unstage(State& s, Staging& g, Job* j) {
+    const IoLayout& L = s.L;
+    if (L.msg_len && j->msgs_out)
+      memcpy(j->msgs_out, g.p + L.msg_off + L.msg_len * j->c0, L.msg_len * j->n);
+    if (j->status_out) memcpy(j->status_out, g.p + L.status_off + j->c0, j->n);
+    j->run = s.run;  // one reference per job (engine_run_group sets refs = jobs)
+  }
+};
+
+// ---- accumulate groups ----
+struct AccPolicy {
+  typedef AccJob Job;
+  static constexpr uint32_t MAX_JOBS = 1024, MAX_REPS = 1u << 17;
+  static constexpr size_t MAX_OUT = (size_t)32 << 20;
+  struct State {
+    AccLayout L;
+    uint32_t jobs = 0, reps = 0;
+    size_t out = 0;
+    int es = 16;
+  };
+  static uint64_t key(Job* j) { return (uint64_t)engine_acc_key(j); }
+  static bool create(State& s, Job* j, size_t* bytes) {
+    s.es = (int)engine_acc_key(j);
+    const uint32_t reps = std::max(MAX_REPS, j->n);
+    const size_t out = std::max(MAX_OUT, engine_acc_out_bytes(j));
+    acc_layout(MAX_JOBS, reps, out, &s.L);
+    *bytes = s.L.bytes;
+    return true;
+  }
+  static bool reserve(State& s, Job* j) {
+    const size_t ob = engine_acc_out_bytes(j);
+    if (s.jobs + 1 > s.L.max_jobs || s.reps + j->n > s.L.max_reps || s.out + ob > s.L.out_cap)
+      return false;
+    j->slot = s.jobs++;
+    j->rep_off = s.reps;
+    j->out_off = s.out;
+    s.reps += j->n;
+    s.out += ob;
+    return true;
+  }
+  static void stage(State& s, Staging& g, Job* j) { engine_acc_stage(j, g.p, s.L); }
+  static int launch(int device, State& s, Staging& g) {
+    return engine_acc_group(device, s.es, g.p, s.L, s.jobs, s.out);
+  }
+  static void unstage(State& s, Staging& g, Job* j) { engine_acc_unstage(j, g.p, s.L); }
+};
+
+Exec<PrepPolicy>* g_prep = [] {  // never destroyed: launcher threads may wait on them at exit
+  auto* x = new Exec<PrepPolicy>[MAX_DEVICES];
+  for (int d = 0; d < MAX_DEVICES; d++) x[d].device = d;
+  return x;
+}();
+Exec<AccPolicy>* g_acc = [] {
+  auto* x = new Exec<AccPolicy>[MAX_DEVICES];
+  for (int d = 0; d < MAX_DEVICES; d++) x[d].device = d;
+  return x;
+}();
 
 }  // namespace
 
 uint32_t exec_max_keys() { return 256; }
 
+void acc_layout(uint32_t max_jobs, uint32_t max_reps, size_t out_cap, AccLayout* L) {
+  auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  L->max_jobs = max_jobs;
+  L->max_reps = max_reps;
+  L->out_cap = out_cap;
+  L->desc_off = 0;
+  L->seg_off = up(sizeof(AccDesc) * (size_t)max_jobs);
+  L->acc_off = L->seg_off + up(4 * (size_t)max_reps);
+  L->out_off = L->acc_off + up((size_t)max_reps);
+  L->bytes = L->out_off + up(out_cap);
+}
+
 int exec_submit(ExecJob* job) {
-  prio3_engine* e = job->e;
-  const int device = engine_device(e);
+  const int device = engine_device(job->e);
   if (device < 0 || device >= MAX_DEVICES) return PRIO3_EINVAL;
-  Executor& X = g_exec[device];
-  const uint64_t key = engine_group_key(e);
-  std::unique_lock<std::mutex> lk(X.mu);
-  Group* g = nullptr;
-  uint32_t slot = 0;
-  for (;;) {
-    auto it = X.open.find(key);
-    g = it == X.open.end() ? nullptr : it->second;
-    if (g) {
-      uint32_t s = 0;
-      while (s < g->keys.size() && g->keys[s] != e) s++;
-      const bool key_ok = s < g->keys.size() || g->keys.size() < exec_max_keys();
-      if (key_ok && g->n + job->n <= g->cap) {
-        if (s == g->keys.size()) g->keys.push_back(e);
-        slot = s;
-        break;
-      }
-      g->closed = true;  // full: launch it as is, open another
-      X.open.erase(it);
-      X.cv.notify_all();
-      continue;
-    }
-    g = new Group();
-    g->key = key;
-    g->lead = e;
-    IoLayout l1, l2;
-    engine_io_layout(e, 1, &l1);
-    engine_io_layout(e, 2, &l2);
-    const size_t per = l2.bytes - l1.bytes + 1;
-    const uint32_t cap_b = (uint32_t)std::max<size_t>(1, STAGING_TARGET / per);
-    g->cap = std::max(job->n, std::min(max_group_reports(), cap_b));
-    IoLayout L;
-    engine_io_layout(e, g->cap, &L);
-    g->stg = staging_get(X, L.bytes);
-    if (!g->stg.p) {
-      delete g;
-      return PRIO3_EDEVICE;
-    }
-    g->keys.push_back(e);
-    slot = 0;
-    X.open[key] = g;
-    break;
-  }
-  job->c0 = g->n;
-  g->n += job->n;
-  g->jobs.push_back(job);
-  g->writers++;
-  g->readers++;
-  const uint32_t cap = g->cap;
-  lk.unlock();
+  return g_prep[device].submit(job);
+}
 
-  // ---- stage this job's inputs (parallel across the callers' threads) ----
-  IoLayout L;
-  engine_io_layout(e, cap, &L);
-  {
-    const uint8_t* src[4] = {job->nonces, job->pub, job->helper, job->leader};
-    for (int f = 0; f < 4; f++)
-      if (L.len[f] && src[f])
-        memcpy(g->stg.p + L.off[f] + L.len[f] * job->c0, src[f], L.len[f] * job->n);
-    uint16_t* slots = (uint16_t*)(g->stg.p + L.slot_off) + job->c0;
-    for (uint32_t i = 0; i < job->n; i++) slots[i] = (uint16_t)slot;
-    engine_vk(e, g->stg.p + L.tab_off + 16 * (size_t)slot);
-  }
-
-  lk.lock();
-  g->writers--;
-  X.cv.notify_all();
-  while (!g->done) {
-    if (!g->flushing && (g->closed || X.inflight < max_inflight())) {
-      g->flushing = true;
-      if (!g->closed) {
-        g->closed = true;
-        auto it = X.open.find(key);
-        if (it != X.open.end() && it->second == g) X.open.erase(it);
-      }
-      while (g->writers > 0) X.cv.wait(lk);
-      while (X.inflight >= max_inflight()) X.cv.wait(lk);
-      X.inflight++;
-      GroupView v;
-      v.n = g->n;
-      v.cap = g->cap;
-      v.stg = g->stg.p;
-      v.n_keys = (uint32_t)g->keys.size();
-      v.jobs = (int)g->jobs.size();
-      lk.unlock();
-      Run* run = nullptr;
-      const int rc = engine_run_group(g->lead, v, &run);
-      lk.lock();
-      X.inflight--;
-      g->rc = rc;
-      g->run = run;
-      g->done = true;
-      X.cv.notify_all();
-    } else {
-      X.cv.wait(lk);
-    }
-  }
-  const int rc = g->rc;
-  Run* run = g->run;
-  lk.unlock();
-
-  // ---- copy this job's outputs back ----
-  if (rc == PRIO3_OK) {
-    if (L.msg_len && job->msgs_out)
-      memcpy(job->msgs_out, g->stg.p + L.msg_off + L.msg_len * job->c0, L.msg_len * job->n);
-    if (job->status_out) memcpy(job->status_out, g->stg.p + L.status_off + job->c0, job->n);
-    job->run = run;  // one reference per job (engine_run_group sets refs = jobs)
-  }
-  lk.lock();
-  if (--g->readers == 0) {
-    staging_put(X, g->stg);
-    delete g;
-  }
-  return rc;
+int exec_accumulate(AccJob* job) {
+  if (job->device < 0 || job->device >= MAX_DEVICES) return PRIO3_EINVAL;
+  return g_acc[job->device].submit(job);
 }
