@@ -40,6 +40,63 @@ KERNEL_BYTES = {"k_xof_a": 16 + 16 + 16 + 256 * 16 + 95 * 16,  # nonce, k_meas, 
                 "k_xofd": 16 + 48 + 32 + 256 * 16 + 95 * 16 + 16 + 16 + 3 * 16,  # + jr/qr/part out
                 "k_query_h": 256 * 16 + 95 * 16 + 560 + 2 * 16 + 16 + 16 + 17,
                 "k_acc_partial": 256 * 16 + 1}
+# --- algorithmic VALU denominator ("The roofline denominator").  A frozen
+# table of gfx950 lane-instruction costs of the cheapest sequences known for each primitive,
+# times the algorithm's primitive counts per report.  No kernel can issue fewer instructions for
+# the same algorithm with these primitives, and no kernel can issue faster than the 78.6 T peak,
+# so model_instr x reports/s / 78.6 T is a roofline fraction <= 1; measured SQ_INSTS_VALU per
+# report / model_instr is the instruction-bloat ratio reported beside it.
+PRIM = dict(
+    keccak_round=190,  # 20 bitop3 (theta C) + 10 alignbit + 10 xor (theta D) + 50 xor (theta
+                       # apply) + 48 alignbit (rho; no lane rotates by a multiple of 32) +
+                       # 50 bitop3 (chi) + 2 (iota), 32-bit halves of the 64-bit lanes
+    f128_mul=90,       # 16 v_mad_u64_u32 schoolbook + carries, 2^128 = 28*2^64 - 1 fold (asm)
+    f128_mac=32,       # lazily reduced multiply-accumulate: 16 v_mad_u64_u32 + 16 carries
+    f128_reduce=67,    # lazy 288-bit accumulator -> canonical (asm)
+    f128_add=13,       # 4-limb add, conditional subtract of p
+    f128_sum_add=5,    # lazy sum of field elements (carry word)
+    lt_p=4,            # canonical-encoding check of one decoded / squeezed element
+    sha256_compress=1440,  # 64 rounds x 15 (bitop3 Ch/Maj, alignbit rotates, add3) + 48 x 10
+)
+
+
+def valu_model(kernel: str, length=256, chunk=16) -> float:
+    """Minimum lane-instructions per report of a Prio3Histogram(length, chunk) kernel."""
+    P = 1
+    calls = -(-length // chunk)
+    while P < calls + 1:
+        P *= 2
+    glen = 2 * (P - 1) + 1
+    perm = 12 * PRIM["keccak_round"]
+    if kernel in ("k_xofd", "k_xof"):
+        meas_blocks = -(-(16 * length) // 168)
+        jr_blocks = (42 + 16 * length) // 168 + 1
+        proof_len = 2 * chunk + glen
+        proofs_blocks = -(-(16 * proof_len) // 168)
+        perms = 1 + meas_blocks + jr_blocks + proofs_blocks + 1 + 1
+        squeezed = length + proof_len + 2 + 1
+        return perms * perm + squeezed * PRIM["lt_p"] + jr_blocks * 42  # + funnel shifts
+    if kernel in ("k_query_h", "k_query_pair"):
+        logP = P.bit_length() - 1
+        half = P // 2
+        # two DFTs of P/2 points (radix 2: (P/4) log2(P/2) butterflies, the w = 1 ones free)
+        bfly = (half // 2) * (logP - 1)
+        triv = sum(half // (1 << l) for l in range(1, logP))
+        muls = (logP + 4) + P + 2 * (bfly - triv)  # t powers, geometric sequences, twiddles
+        adds = 2 * 2 * bfly + calls
+        muls += (glen - 1) + chunk.bit_length() + 2 * calls  # Horner, r^C, beta
+        macs = (glen - 1) + 2 * length + 4 * chunk            # range, A/B sums, finalize
+        reduces = 1 + 3 * chunk + chunk // 2                 # range, A/B/f0 per wire, gadget groups
+        muls += chunk + 1 + 3 + 2                             # r^(j+1), L/2, v, sum fold
+        adds += (glen - 1) + 3 * chunk + 6
+        return (muls * PRIM["f128_mul"] + macs * PRIM["f128_mac"] +
+                reduces * PRIM["f128_reduce"] + adds * PRIM["f128_add"] +
+                length * PRIM["f128_sum_add"] + (2 * chunk + 2) * PRIM["lt_p"] + perm)
+    if kernel == "k_meta":
+        return PRIM["sha256_compress"]
+    return 0.0
+
+
 # Peak: the guide's vector issue rate (MI355X_MICROARCH.md: 157.3 TFLOPS FP32 vector = 256 CU x
 # 4 SIMD x 32 lanes/clk x 2.4 GHz = 78.6 T lane-instructions/s); measured full-rate issue on
 # this chip is 64.5 T (profiles/r01_ubench_valu_gfx950.txt), reported beside it.
@@ -220,29 +277,57 @@ def main():
     final_cnt = int((combiner.out_cnt if combiner is not None else cnt)[0].item())
     value = world * n * args.steps / elapsed
 
-    # roofline of the dominant kernel, from the live HIP-event times on the launch stream
+    # roofline of the dominant kernel, from the live HIP-event times on the launch stream:
+    # achieved = the frozen gfx950 VALU model (valu_model) x reports / duration;
+    # the measured instructions per report (PMC SQ_INSTS_VALU / SQ_WAVES, profiles/) give the
+    # issued rate and the bloat ratio beside it
     per_kernel = {k: dict(ms_total=v[0], launches=v[1], ms_avg=v[0] / max(v[1], 1))
                   for k, v in times.items()}
     counts = json.load(open(COUNTS_PATH)) if os.path.exists(COUNTS_PATH) else dict(kernels={})
     kc = counts["kernels"]
+    peak_T = PEAK_VALU_NOMINAL / 1e12
     for k, v in per_kernel.items():
-        if k in kc and "valu_instr_per_item" in kc[k] and k != "k_acc_partial":
-            v["valu_T"] = kc[k]["valu_instr_per_item"] * n / (v["ms_avg"] / 1e3) / 1e12
-            v["valu_frac"] = v["valu_T"] / (PEAK_VALU_NOMINAL / 1e12)
+        m = valu_model(k)
+        if m:
+            v["model_instr_per_report"] = m
+            v["model_T"] = m * n / (v["ms_avg"] / 1e3) / 1e12
+            v["frac"] = v["model_T"] / peak_T
+        if k in kc and "valu_instr_per_item" in kc[k]:
+            v["issued_instr_per_report"] = kc[k]["valu_instr_per_item"]
+            v["issued_T"] = kc[k]["valu_instr_per_item"] * n / (v["ms_avg"] / 1e3) / 1e12
+            if m:
+                v["issued_over_model"] = kc[k]["valu_instr_per_item"] / m
+        if k in kc and "bytes" in kc[k]:
+            v["hbm_pmc_TBps"] = kc[k]["bytes"] / (v["ms_avg"] / 1e3) / 1e12
+            v["hbm_frac"] = v["hbm_pmc_TBps"] * 1e12 / PEAK_HBM
         if k in KERNEL_BYTES:
             v["hbm_algorithmic_GBps"] = KERNEL_BYTES[k] * n / (v["ms_avg"] / 1e3) / 1e9
-    dom = max((k for k in per_kernel if "valu_T" in per_kernel[k]),
+    dom = max((k for k in per_kernel if "model_T" in per_kernel[k]),
               key=lambda k: per_kernel[k]["ms_total"])
     d = per_kernel[dom]
-    roofline = dict(bound="valu", achieved=d["valu_T"], peak=PEAK_VALU_NOMINAL / 1e12,
-                    unit="T lane-instr/s (32-bit VALU issue; peak = guide vector rate)",
-                    frac_of_measured_issue=d["valu_T"] / MEASURED_ISSUE_T,
-                    frac=d["valu_frac"], traffic=kc[dom].get("bytes"),
+    step_model = sum(valu_model(k) for k in per_kernel if valu_model(k))
+    roofline = dict(bound="valu", achieved=d["model_T"], peak=peak_T,
+                    unit="T lane-instr/s (32-bit VALU; achieved = frozen gfx950 minimum-"
+                         "instruction model x reports / kernel time; peak = guide vector rate)",
+                    frac=d["frac"], traffic=kc.get(dom, {}).get("bytes"),
                     traffic_source=f"{counts.get('source')} (PMC FETCH_SIZE*2+WRITE_SIZE, bytes/launch)",
                     kernel=dom, ms_avg=d["ms_avg"],
-                    valu_instr_per_report=kc[dom]["valu_instr_per_item"],
+                    model_instr_per_report=d["model_instr_per_report"],
+                    issued_instr_per_report=d.get("issued_instr_per_report"),
+                    issued_over_model=d.get("issued_over_model"),
+                    issued_frac=(d["issued_T"] / peak_T) if "issued_T" in d else None,
+                    frac_of_measured_issue=d["model_T"] / MEASURED_ISSUE_T,
                     hbm_algorithmic_GBps=d.get("hbm_algorithmic_GBps"), hbm_peak_GBps=PEAK_HBM / 1e9,
-                    valu_nominal_peak_T=PEAK_VALU_NOMINAL / 1e12)
+                    step=dict(model_instr_per_report=step_model,
+                              achieved=step_model * n * args.steps / elapsed / 1e12,
+                              frac=step_model * n * args.steps / elapsed / 1e12 / peak_T,
+                              note="whole timed step (all kernels, stream-overlapped chunks), "
+                                   "per GPU"))
+    qh = per_kernel.get("k_query_h") or per_kernel.get("k_query_pair")
+    if qh and "hbm_frac" in qh:
+        roofline["query_hbm"] = dict(kernel="k_query_h" if "k_query_h" in per_kernel else "k_query_pair",
+                                     achieved_TBps=qh["hbm_pmc_TBps"], peak_TBps=PEAK_HBM / 1e12,
+                                     frac=qh["hbm_frac"])
 
     out = dict(metric=METRIC, value=value, unit="reports/s", n_gpus=world, steps=args.steps,
                warmup=args.warmup, ms_per_step=elapsed / args.steps * 1e3,

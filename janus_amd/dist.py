@@ -13,8 +13,10 @@ The analogue in Janus is merging per-shard ``batch_aggregations`` rows at collec
 (``/root/reference/aggregator/src/aggregator/aggregate_share.rs:55-96``), which is also a
 mod-p element-wise sum of encoded aggregate shares.
 
-This module is the code bench.py runs for N > 1; tests/test_dist.py drives it with ``gloo`` on
-CPU tensors, where the combine callable is the test's own mod-p sum.
+This module is the code bench.py runs for N > 1.  tests/test_dist.py drives it with ``gloo`` on
+CPU tensors (the combine callable is the test's own mod-p sum); tests/test_gpu_dist.py runs two
+ranks whose partials come from the HIP engine and whose combine is the HIP kernel, with the
+collective staged through host memory for gloo.
 """
 from __future__ import annotations
 
@@ -44,7 +46,10 @@ class AggregateCombiner:
     """
 
     def __init__(self, dist, agg, counts, combine: Callable, checksums=None, intervals=None,
-                 combine_meta: Optional[Callable] = None):
+                 combine_meta: Optional[Callable] = None, stage_device=None):
+        """stage_device: where the collective's buffers live when it differs from the partials'
+        device (e.g. "cpu" for a gloo group whose partials come from a GPU engine); the gathered
+        rows are copied back to the partials' device for the combine kernels."""
         import torch
         self.dist = dist
         self.world = dist.get_world_size()
@@ -61,8 +66,12 @@ class AggregateCombiner:
                        torch.empty((), dtype=dt).element_size()
                        for sh, dt in zip(self.shapes, self.dtypes)]
         self.row = sum(self.nbytes)
-        self.send = torch.empty(self.row, dtype=torch.uint8, device=dev)
-        self.gathered = torch.empty((self.world, self.row), dtype=torch.uint8, device=dev)
+        self.dev = dev
+        cdev = torch.device(stage_device) if stage_device is not None else dev
+        self.send = torch.empty(self.row, dtype=torch.uint8, device=cdev)
+        self.gathered = torch.empty((self.world, self.row), dtype=torch.uint8, device=cdev)
+        self.gathered_dev = (self.gathered if cdev == dev else
+                             torch.empty((self.world, self.row), dtype=torch.uint8, device=dev))
         self.outs = [torch.empty(sh, dtype=dt, device=dev)
                      for sh, dt in zip(self.shapes, self.dtypes)]
         self.out_agg, self.out_cnt = self.outs[0], self.outs[1]
@@ -72,15 +81,21 @@ class AggregateCombiner:
     def _gathered(self, idx):
         import torch
         off = sum(self.nbytes[:idx])
-        g = self.gathered[:, off:off + self.nbytes[idx]].contiguous()
+        g = self.gathered_dev[:, off:off + self.nbytes[idx]].contiguous()
         return g.view(self.dtypes[idx]).view((self.world,) + self.shapes[idx]) \
             if self.dtypes[idx] != torch.uint8 else g.view((self.world,) + self.shapes[idx])
 
     def __call__(self, agg, counts, checksums=None, intervals=None):
         import torch
         parts = [agg, counts] + ([checksums, intervals] if self.meta else [])
-        torch.cat([t.contiguous().view(-1).view(torch.uint8) for t in parts], out=self.send)
+        flat = [t.contiguous().view(-1).view(torch.uint8) for t in parts]
+        if self.send.device == self.dev:
+            torch.cat(flat, out=self.send)
+        else:
+            self.send.copy_(torch.cat(flat))
         self.dist.all_gather_into_tensor(self.gathered.view(-1), self.send)
+        if self.gathered_dev is not self.gathered:
+            self.gathered_dev.copy_(self.gathered)
         self.combine(self.world, self._gathered(0), self._gathered(1), self.out_agg, self.out_cnt)
         if self.meta:
             self.combine_meta(self.world, self._gathered(2), self._gathered(3),

@@ -1,0 +1,172 @@
+"""Multi-rank path with the HIP engine behind it.
+
+* prio3_device_combine: k = 8 rank partials x several segments, Field128 and Field64, against a
+  Python mod-p sum (RCCL's integer sum would be mod 2^64: the reason the combine is a kernel).
+* prio3_device_combine_metadata: k = 8 ranks' ReportIdChecksums (XOR) and client-timestamp
+  intervals (Interval::merge, the empty interval the identity; core/src/time.rs:294-317).
+* world size 2 over gloo, one GPU: each rank prepares its shard of one batch on the HIP engine
+  (prepare_aggregate + finish + batch metadata), janus_amd.dist.AggregateCombiner all-gathers
+  the partials (staged through host memory for gloo) and combines them with the HIP kernels;
+  the result must equal the CPU restatement's aggregate of the whole batch
+  (aggregate_share.rs:55-96 merges per-shard batch aggregations the same way).
+The ranks are child processes started with subprocess (the pytest process may already hold the
+GPU; nothing is exec'ed in place).  8-GPU RCCL runs are the driver's (SCALE_rNN.json).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+VK = bytes(range(0x22, 0x32))
+N, NSEG = 2000, 3
+P128 = 2**128 - 28 * 2**64 + 1
+P64 = 2**64 - 2**32 + 1
+
+
+def _rand_elems(rng, shape, p, es):
+    vals = [int.from_bytes(rng.bytes(es), "little") % p for _ in range(int(np.prod(shape)))]
+    return np.frombuffer(b"".join(v.to_bytes(es, "little") for v in vals),
+                         np.uint8).reshape(shape[:-1] + (shape[-1] * es,)), vals
+
+
+@pytest.mark.parametrize("kind", ["histogram", "count"])
+def test_device_combine_eight_ranks(kind):
+    import torch
+    from janus_amd import prio3 as J
+    vdaf = J.Prio3Histogram(256, 16) if kind == "histogram" else J.Prio3Count()
+    p, es = (P128, 16) if kind == "histogram" else (P64, 8)
+    eng = J.HelperEngine(vdaf, VK)
+    k, S, L = 8, 5, eng.sz.out_len
+    rng = np.random.default_rng(3)
+    parts, vals = _rand_elems(rng, (k, S, L), p, es)
+    counts = rng.integers(0, 1 << 40, (k, S)).astype(np.int64)
+    dev = torch.device("cuda", 0)
+    out = torch.zeros((S, L * es), dtype=torch.uint8, device=dev)
+    oc = torch.zeros(S, dtype=torch.int64, device=dev)
+    eng.combine_device(k, S, torch.from_numpy(parts.copy()).to(dev),
+                       torch.from_numpy(counts).to(dev), out, oc)
+    torch.cuda.synchronize()
+    v = np.array(vals, dtype=object).reshape(k, S, L)
+    exp = [[sum(int(v[i, s, e]) for i in range(k)) % p for e in range(L)] for s in range(S)]
+    got = out.cpu().numpy().reshape(S, L, es)
+    assert [[int.from_bytes(got[s, e].tobytes(), "little") for e in range(L)]
+            for s in range(S)] == exp
+    np.testing.assert_array_equal(oc.cpu().numpy(), counts.sum(axis=0))
+
+
+def test_device_combine_metadata_eight_ranks():
+    import torch
+    from janus_amd import prio3 as J
+    eng = J.HelperEngine(J.Prio3Histogram(256, 16), VK)
+    k, S = 8, 6
+    rng = np.random.default_rng(4)
+    ck = rng.integers(0, 256, (k, S, 32), dtype=np.uint8)
+    iv = np.zeros((k, S, 2), np.uint64)
+    for i in range(k):
+        for s in range(S):
+            if s == 5 or (i + s) % 3 == 0:
+                continue  # Interval::EMPTY (0, 0) from ranks without reports in the segment
+            a = 1_700_000_000 + int(rng.integers(0, 100_000))
+            iv[i, s] = (a, int(rng.integers(1, 5000)))
+    dev = torch.device("cuda", 0)
+    oc = torch.zeros((S, 32), dtype=torch.uint8, device=dev)
+    oi = torch.zeros((S, 2), dtype=torch.int64, device=dev)
+    eng.combine_metadata_device(k, S, torch.from_numpy(ck).to(dev),
+                                torch.from_numpy(iv.view(np.int64)).to(dev), oc, oi)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(oc.cpu().numpy(), np.bitwise_xor.reduce(ck, axis=0))
+    got = oi.cpu().numpy().view(np.uint64)
+    for s in range(S):
+        spans = [(int(a), int(a) + int(d)) for a, d in iv[:, s] if d]
+        want = (min(x for x, _ in spans), max(y for _, y in spans) - min(x for x, _ in spans)) \
+            if spans else (0, 0)
+        assert tuple(int(x) for x in got[s]) == want, s
+
+
+def _batch():
+    from oracle.oracle import Oracle
+    o = Oracle("histogram", length=256, chunk_length=16)
+    d = o.gen_reports(VK, N, seed=91, n_threads=4)
+    for i in range(3, N, 41):  # some decide failures
+        d["leader_prep_shares"][i, 16] ^= 1
+    seg = (np.arange(N) * NSEG // N).astype(np.uint32)
+    times = (1_700_000_000 + (np.arange(N) * 7919) % 5000).astype(np.uint64)
+    return o, d, seg, times
+
+
+def _rank_main():
+    """One rank (child process): HIP partials of its shard, gloo all-gather, HIP combine."""
+    import torch
+    import torch.distributed as dist
+    from janus_amd import prio3 as J
+    from janus_amd.dist import AggregateCombiner, shard_bounds
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    o, d, seg, times = _batch()
+    lo, hi = shard_bounds(N, rank, world)
+    n = hi - lo
+    eng = J.HelperEngine(J.Prio3Histogram(256, 16), VK)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a[lo:hi])).to(dev)
+    msgs = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    agg = torch.zeros((NSEG, 4096), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(NSEG, dtype=torch.int64, device=dev)
+    ck = torch.zeros((NSEG, 32), dtype=torch.uint8, device=dev)
+    iv = torch.zeros((NSEG, 2), dtype=torch.int64, device=dev)
+    sg = T(seg)
+    eng.prepare_aggregate_device(T(d["nonces"]), T(d["public_shares"]), T(d["helper_shares"]),
+                                 T(d["leader_prep_shares"]), sg, NSEG, msgs, status)
+    eng.aggregate_finish_device(status, None, agg, cnt)
+    eng.batch_metadata_device(T(d["nonces"]), T(times.view(np.int64)), status, None, sg, NSEG,
+                              ck, iv)
+    cur = lambda: torch.cuda.current_stream().cuda_stream
+    comb = AggregateCombiner(
+        dist, agg, cnt, lambda k, ga, gc, oa, oc: eng.combine_device(k, NSEG, ga, gc, oa, oc,
+                                                                      stream=cur()),
+        ck, iv, lambda k, gk, gi, ok, oi: eng.combine_metadata_device(k, NSEG, gk, gi, ok, oi,
+                                                                       stream=cur()),
+        stage_device="cpu")
+    out_agg, out_cnt, out_ck, out_iv = comb(agg, cnt, ck, iv)
+    torch.cuda.synchronize()
+    if rank == 0:
+        np.savez(os.environ["RESULT"], agg=out_agg.cpu().numpy(), cnt=out_cnt.cpu().numpy(),
+                 ck=out_ck.cpu().numpy(), iv=out_iv.cpu().numpy())
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_partials_from_the_hip_engine(tmp_path):
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    res = str(tmp_path / "r.npz")
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), RESULT=res, PYTHONPATH=ROOT)
+        procs.append(subprocess.Popen(
+            [sys.executable, "-c", "from tests.test_gpu_dist import _rank_main; _rank_main()"],
+            cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    outs = [p.communicate(timeout=180)[0].decode(errors="replace") for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    got = np.load(res)
+    from oracle.oracle import batch_metadata
+    o, d, seg, times = _batch()
+    _, st, agg, cnt = o.helper_batch(VK, d["nonces"], d["public_shares"], d["helper_shares"],
+                                     d["leader_prep_shares"], segment_ids=seg, n_segments=NSEG,
+                                     n_threads=4)
+    np.testing.assert_array_equal(got["agg"], agg)
+    np.testing.assert_array_equal(got["cnt"].astype(np.uint64), cnt)
+    ck, iv = batch_metadata(d["nonces"], times, st, None, seg, NSEG)
+    np.testing.assert_array_equal(got["ck"], ck)
+    np.testing.assert_array_equal(got["iv"].view(np.uint64), iv)
+    assert int(cnt.sum()) < N  # the tampered reports are out
