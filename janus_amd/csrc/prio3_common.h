@@ -46,10 +46,13 @@ struct DevParams {
   uint32_t roots128[MAX_ROOTS + 1][4];
   uint64_t roots64[MAX_ROOTS + 1];
   uint32_t invP128[4], half128[4];
-  // P <= 32 only: sigma_e = sum_{c=1..calls} alpha^(ce) and twiddles alpha_P^i (i < P/2)
+  // P <= 32 only: sigma_e = sum_{c=1..calls} alpha^(ce) and twiddles alpha_P^i (i < P/2).
+  // P = 64 / 128 (k_query_w): tw128[k] = alpha_(P/8)^k (k < P/16), tw128[8 + i] = alpha_P^i
+  // (i < 8), and the sigma table of P entries in device memory (engine-owned; null if absent)
   uint32_t sigma128[32][4];
   uint32_t tw128[16][4];
   uint64_t invP64, half64;
+  const uint4* sigma_dev;
 };
 
 struct InPtrs {
@@ -465,6 +468,12 @@ int launch_mp64(prio3_engine* e, uint32_t n, uint32_t ld, InPtrs in, OutPtrs out
 // P = 16 / 32 ParallelSum(Mul) helper query on lane pairs (prio3_query_pair.hip); false if the
 // instance is not one it takes
 bool launch_query_pair(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st);
+// long-share helper XOF on lane pairs (prio3_xof_pair.hip); false if the instance is not one it takes
+bool launch_xof_pair(const DevParams& p, InPtrs in, Scratch sc, hipStream_t st);
+// P = 64 / 128 ParallelSum(Mul) helper query, eight lanes per report (prio3_query_wide.hip);
+// false if the instance is not one it takes
+bool launch_query_wide(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
+                       int gs);
 // FPVec FLP query + decide + prepare message + truncate for p.n reports (prio3_fpvec.hip)
 void launch_fpvec_query(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
                         int gs);
@@ -523,9 +532,16 @@ struct prio3_engine {
   int qh_occ = 3;
   int qh_regs = 0;
   int qpair = 0;  // option: P = 16/32 query on lane pairs (k_query_pair; A/B: slower)
+  // option: helper XOF on lane pairs (k_xof_pair): -1 auto (shares of >= 2048 elements), 0, 1
+  int xof_pair = -1;
+  // option: P = 64/128 query on eight lanes per report (k_query_w): 1 on, 0 off (k_query_ps);
+  // qw_gs: wire columns per lane and sweep (2, 3 or 4)
+  int qwide = 1;
+  int qw_gs = 3;
   int timing = 0;
   Mp64Params mp{};  // PRIO3_SUMVEC_F64_MP only
   uint64_t* d_sigma64 = nullptr;
+  uint4* d_sigma128 = nullptr;  // k_query_w's sigma table (DevParams::sigma_dev)
   std::vector<KTime> times;
   std::vector<hipEvent_t> ev_pool;
   std::mutex tmu;  // timing bookkeeping (launches may come from several executor threads)

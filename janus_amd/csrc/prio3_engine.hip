@@ -2307,6 +2307,18 @@ static int fill_sizes(const prio3_params* pp, prio3_sizes_t* s, DevParams* dp) {
         u128 w = hpow(alpha, i, HP128);
         for (int k = 0; k < 4; k++) d.tw128[i][k] = (uint32_t)(w >> (32 * k));
       }
+    } else if (d.P == 64 || d.P == 128) {  // k_query_w's four-step DFT
+      u128 alpha = 0;
+      for (int k = 0; k < 4; k++) alpha |= (u128)d.roots128[d.logP][k] << (32 * k);
+      const u128 aq = hpow(alpha, 8, HP128);  // alpha_(P/8)
+      for (uint32_t i = 0; i < d.P / 16; i++) {
+        const u128 w = hpow(aq, i, HP128);
+        for (int k = 0; k < 4; k++) d.tw128[i][k] = (uint32_t)(w >> (32 * k));
+      }
+      for (uint32_t i = 0; i < 8; i++) {
+        const u128 w = hpow(alpha, i, HP128);
+        for (int k = 0; k < 4; k++) d.tw128[8 + i][k] = (uint32_t)(w >> (32 * k));
+      }
     }
     d.half64 = (uint64_t)hpow(2, HP64 - 2, HP64);
   }
@@ -2708,7 +2720,11 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
       qs.out = (uint8_t*)sc.out + es * s0;
       const uint32_t qb = (q.n + 255) / 256, qb64 = (q.n + 63) / 64;
       // k_xofd (two live Keccak states: share squeeze + joint-rand absorb) unless A/B-ed off
-      if (e->split_xof == 2 && (42 + dp.meas_len * 16) / 168 >= 2)
+      bool paired = false;
+      if (e->xof_pair != 0 && e->split_xof == 2)
+        TIMED(e, ss, "k_xof_pair", (paired = launch_xof_pair(q, qi, qs, ss)));
+      if (paired) {
+      } else if (e->split_xof == 2 && (42 + dp.meas_len * 16) / 168 >= 2)
         TIMED(e, ss, "k_xofd", (k_xofd<false><<<qb, 256, 0, ss>>>(q, qi, qs)));
       else
         TIMED(e, ss, "k_xof", (k_xof<Fp128><<<qb, 256, 0, ss>>>(q, qi, qs)));
@@ -2723,7 +2739,13 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
     return PRIO3_OK;
   }
   if (dp.es == 16) {
-    if (dp.jr_len && e->split_xof == 2 && (42 + dp.meas_len * 16) / 168 >= 2) {
+    const bool pair_xof =
+        !fuse && e->xof_pair > 0;  // auto: off (SumVec 8x1000 A/B: 15.0 vs 12.8 ms, r02j)
+    bool paired = false;
+    if (dp.jr_len && e->split_xof == 2 && pair_xof)
+      TIMED(e, st, "k_xof_pair", (paired = launch_xof_pair(dp, in, sc, st)));
+    if (paired) {
+    } else if (dp.jr_len && e->split_xof == 2 && (42 + dp.meas_len * 16) / 168 >= 2) {
       if (fuse)
         TIMED(e, st, "k_xofd", (k_xofd<true><<<blocks, 256, 0, st>>>(dp, in, sc)));
       else
@@ -2743,6 +2765,9 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
     if (ps && e->qpair && (dp.P == 32 || dp.P == 16)) {
       TIMED(e, st, "k_query_pair", (done = launch_query_pair(dp, in, sc, out, st)));
     }
+    if (!done && ps && e->qwide && dp.sigma_dev && (dp.P == 64 || dp.P == 128) &&
+        (dp.kind != PRIO3_SUMVEC || dp.bits <= 32))
+      TIMED(e, st, "k_query_w", (done = launch_query_wide(dp, in, sc, out, st, e->qw_gs)));
     if (done) {
     } else if (ps && dp.P == 32 && dp.chunk == 16 && dp.calls == 16 && e->qh_regs)
       TIMED(e, st, "k_query_r", (k_query_r<16, 16><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
@@ -2864,7 +2889,7 @@ uint64_t engine_group_key(const prio3_engine* e) {
   h = fnv(h, &e->params, sizeof e->params);
   h = fnv(h, &e->device, sizeof e->device);
   const int opts[] = {e->force_slow, e->split_xof, e->fp_overlap, e->fp_gs, e->qh_prefetch,
-                      e->qh_occ,     e->qh_regs,   e->qpair};
+                      e->qh_occ,     e->qh_regs,   e->qpair,      e->xof_pair};
   h = fnv(h, opts, sizeof opts);
   h = fnv(h, &e->fp_sub_bytes, sizeof e->fp_sub_bytes);
   // XofHmacSha256Aes128 keys enter the kernels as HMAC midstates: one engine per launch; an
@@ -3051,6 +3076,32 @@ int prio3_engine_create_ex(const prio3_params* params, const uint8_t* verify_key
     return PRIO3_EDEVICE;
   }
   ws_stream_put(device, probe);  // the first member of the GPU's stream pool
+  if ((e->dp.kind == PRIO3_HISTOGRAM || e->dp.kind == PRIO3_SUMVEC) &&
+      (e->dp.P == 64 || e->dp.P == 128)) {
+    // k_query_w: sigma_e = sum_(c=1..calls) alpha^(ce), e < P (the range check's weights)
+    const DevParams& d = e->dp;
+    u128 alpha = 0;
+    for (int k = 0; k < 4; k++) alpha |= (u128)d.roots128[d.logP][k] << (32 * k);
+    std::vector<uint4> sig(d.P);
+    for (uint32_t e2 = 0; e2 < d.P; e2++) {
+      const u128 ae = hpow(alpha, e2, HP128);
+      u128 s = 0, x = 1;
+      for (uint32_t c = 1; c <= d.calls; c++) {
+        x = hmul(x, ae, HP128);
+        s += x;
+        if (s < x || s >= HP128) s -= HP128;
+      }
+      sig[e2] = make_uint4((uint32_t)s, (uint32_t)(s >> 32), (uint32_t)(s >> 64),
+                           (uint32_t)(s >> 96));
+    }
+    if (hipMalloc((void**)&e->d_sigma128, sizeof(uint4) * d.P) != hipSuccess ||
+        hipMemcpy(e->d_sigma128, sig.data(), sizeof(uint4) * d.P, hipMemcpyHostToDevice) !=
+            hipSuccess) {
+      delete e;
+      return PRIO3_EDEVICE;
+    }
+    e->dp.sigma_dev = e->d_sigma128;
+  }
   if (mp) {  // prio3_mp64.hip constants
     const DevParams& d = e->dp;
     Mp64Params& m = e->mp;
@@ -3113,6 +3164,7 @@ void prio3_engine_destroy(prio3_engine* e) {
   }
   collect_times(e);
   if (e->d_sigma64) (void)hipFree(e->d_sigma64);
+  if (e->d_sigma128) (void)hipFree(e->d_sigma128);
   for (auto s2 : e->side) (void)hipStreamDestroy(s2);
   for (auto j : e->side_ev) (void)hipEventDestroy(j);
   if (e->fork_ev) (void)hipEventDestroy(e->fork_ev);
@@ -3129,7 +3181,13 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
               {"qh_regs", &e->qh_regs},            {"qh_occ", &e->qh_occ},
               {"qh_prefetch", &e->qh_prefetch},    {"split_xof", &e->split_xof},
               {"qpair", &e->qpair},                {"timing", &e->timing},
-              {"coalesce", &e->coalesce},          {"experimental_fpvec", &e->experimental_fpvec}};
+              {"coalesce", &e->coalesce},          {"experimental_fpvec", &e->experimental_fpvec},
+              {"xof_pair", &e->xof_pair},          {"qwide", &e->qwide}};
+  if (!strcmp(key, "qw_gs")) {
+    if (value < 2 || value > 4) return PRIO3_EINVAL;
+    e->qw_gs = (int)value;
+    return PRIO3_OK;
+  }
   for (auto& o : ints)
     if (!strcmp(key, o.name)) {
       *o.field = (int)value;

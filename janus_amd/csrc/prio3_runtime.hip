@@ -61,9 +61,11 @@ void free_slab(Slab* s) {
   delete s;
 }
 
-// frees idle slabs (oldest first) until at most `keep` idle bytes remain; caller holds p.mu
-void trim_locked(Pool& p, size_t keep) {
-  while (!p.idle.empty() && p.idle_bytes > keep) {
+// frees idle slabs (oldest first) until at most `keep` idle bytes remain, never `spare` (the
+// slab just released: a device-resident caller re-acquires it on its next call -- an FPVec run
+// is ~225 GB, and re-allocating it per step cost seconds); caller holds p.mu
+void trim_locked(Pool& p, size_t keep, const Slab* spare = nullptr) {
+  while (!p.idle.empty() && p.idle_bytes > keep && p.idle.front() != spare) {
     Slab* s = p.idle.front();
     p.idle.pop_front();
     p.idle_bytes -= s->bytes;
@@ -158,7 +160,7 @@ void ws_release(Slab* s, hipStream_t st) {
   std::lock_guard<std::mutex> lk(p.mu);
   p.idle.push_back(s);
   p.idle_bytes += s->bytes;
-  trim_locked(p, p.budget);
+  trim_locked(p, p.budget, s);
 }
 
 size_t ws_pool_bytes(int device, size_t* idle_bytes) {

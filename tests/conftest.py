@@ -33,4 +33,9 @@ CONFIGS = {
     "hist_10_c3": dict(kind="histogram", length=10, chunk_length=3),
     "hist_1_c1": dict(kind="histogram", length=1, chunk_length=1),
     "hist_100_c10": dict(kind="histogram", length=100, chunk_length=10),
+    # 64- and 128-point wire domains (k_query_w, eight lanes per report)
+    "sumvec_4x100_c10": dict(kind="sumvec", bits=4, length=100, chunk_length=10),
+    "sumvec_32x20_c7": dict(kind="sumvec", bits=32, length=20, chunk_length=7),
+    "hist_500_c8": dict(kind="histogram", length=500, chunk_length=8),
+    "hist_1000_c10": dict(kind="histogram", length=1000, chunk_length=10),
 }

@@ -185,12 +185,14 @@ def _tamper(v, reps, frac, seed):
             reps[i]["lps"][16 * (2 + v.t.A0)] ^= 2                      # a gadget-1 wire
 
 
-def _run(v, reps, sub_bytes=None):
+def _run(v, reps, sub_bytes=None, opts=None):
     from janus_amd import prio3 as J
     t = v.t
     eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(t.length, t.bits), VK, allow_unpinned=True)
     if sub_bytes:
         eng.set_option("fp_sub_bytes", sub_bytes)
+    for k, val in (opts or {}).items():
+        eng.set_option(k, val)
     A = lambda k: np.array([list(r[k]) for r in reps], np.uint8)
     msgs, status, batch = eng.prepare_batch(A("nonce"), A("pub"), A("helper"), A("lps"))
     outs = batch.output_shares()
@@ -341,3 +343,16 @@ def test_gpu_fpvec_requires_explicit_opt_in():
     A = lambda k: np.array([list(r[k]) for r in reps], np.uint8)
     with pytest.raises(RuntimeError, match="rc=-3"):
         eng.prepare_batch(A("nonce"), A("pub"), A("helper"), A("lps"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("xof_pair", [0, 1])
+def test_gpu_fpvec_xof_lane_pairs(xof_pair):
+    """The FPVec share phase with and without the lane-pair XOF (auto: on from 2048 share
+    elements, so forced here at length 24), across two sub-batches."""
+    v = _vdaf(24)
+    reps = _reports(v, 300, seed=23, distinct=60)
+    _tamper(v, reps, 0.05, seed=6)
+    t = v.t
+    per = 16 * (t.meas_len + t.proof_len + 2 + 2 + 2 * (t.P0 + t.P1) + t.K0) + 33
+    _check(v, reps, _run(v, reps, sub_bytes=per * 256 + 1, opts={"xof_pair": xof_pair}))

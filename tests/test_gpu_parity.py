@@ -58,12 +58,14 @@ def _tamper(o, d, rng):
     return d
 
 
-def _check_against_oracle(cfg, n, seed, tamper=True, force_slow=False, n_segments=1):
+def _check_against_oracle(cfg, n, seed, tamper=True, force_slow=False, n_segments=1, opts=None):
     from oracle.oracle import decode_elems
     o = _oracle(cfg)
     eng = _engine(cfg)
     if force_slow:
         eng.set_option("force_slow_path", 1)
+    for k, v in (opts or {}).items():
+        eng.set_option(k, v)
     d = o.gen_reports(VK, n, seed=seed, n_threads=8)
     rng = np.random.default_rng(seed)
     if tamper:
@@ -204,3 +206,39 @@ def test_full_size_histogram_unshard_property():
     tot = [(a + b) % p for a, b in zip(la, ha)]
     exp = torch.bincount(d["measurements"][:, 0], minlength=256).cpu().tolist()
     assert tot == exp
+
+
+@pytest.mark.parametrize("name", ["sumvec_8x10_c9", "hist_256_c16", "sum32", "sumvec_8x1000_c63"])
+@pytest.mark.parametrize("force_slow", [False, True])
+def test_xof_pair_parity(name, force_slow):
+    """The two-lanes-per-report XOF (k_xof_pair: share squeeze and joint-rand-part absorb in the
+    two lanes of a pair, DPP-linked) forced on for short shares too, with ragged tails."""
+    n = 70 if "1000" in name else 301
+    _check_against_oracle(CONFIGS[name], n, seed=13, force_slow=force_slow, opts={"xof_pair": 1})
+
+
+@pytest.mark.parametrize("name", ["hist_256_c16", "hist_100_c10", "sumvec_8x10_c9"])
+def test_query_pair_parity(name):
+    """The lane-pair query (k_query_pair, option qpair) stays bit-exact (off by default)."""
+    _check_against_oracle(CONFIGS[name], 333, seed=17, opts={"qpair": 1})
+
+
+WIDE = ["sumvec_8x1000_c63", "sumvec_4x100_c10", "sumvec_32x20_c7", "hist_500_c8",
+        "hist_1000_c10"]
+
+
+@pytest.mark.parametrize("gs", [2, 3, 4])
+@pytest.mark.parametrize("name", WIDE)
+def test_query_wide_parity(name, gs):
+    """P = 64/128 ParallelSum query on eight lanes per report (k_query_w): every column-group
+    width, tampered reports, a batch that is not a multiple of the 32 reports of a block."""
+    n = 101 if "1000" in name else 333
+    _check_against_oracle(CONFIGS[name], n, seed=19 + gs, opts={"qwide": 1, "qw_gs": gs})
+
+
+@pytest.mark.parametrize("name", ["sumvec_8x1000_c63", "hist_500_c8"])
+def test_query_wide_off_and_slow_path(name):
+    """The one-lane k_query_ps stays selectable; the rejection-sampling XOF feeds k_query_w."""
+    n = 70 if "1000" in name else 200
+    _check_against_oracle(CONFIGS[name], n, seed=23, opts={"qwide": 0})
+    _check_against_oracle(CONFIGS[name], n, seed=29, force_slow=True)

@@ -9,9 +9,10 @@ vals = defaultdict(lambda: defaultdict(float))
 disp = defaultdict(set)
 for f in glob.glob(os.path.join(src, "pmc_*", "*counter_collection.csv")):
     for row in csv.DictReader(open(f)):
-        k = re.match(r"(?:void )?([A-Za-z_0-9]+)", row["Kernel_Name"]).group(1)
         if sub not in row["Kernel_Name"]:
             continue
+        m = re.search(r"(k_[A-Za-z_0-9]+)", row["Kernel_Name"])
+        k = m.group(1) if m else row["Kernel_Name"][:60]
         vals[k][row["Counter_Name"]] += float(row["Counter_Value"])
         disp[k, row["Counter_Name"]].add(row["Dispatch_Id"])
 for k, cs in vals.items():
