@@ -53,6 +53,9 @@ struct DevParams {
   uint32_t tw128[16][4];
   uint64_t invP64, half64;
   const uint4* sigma_dev;
+  // 1: the helper XOF kernel also truncates the measurement share into the output-share
+  // scratch (TruncSink); the query kernel then leaves sc.out alone
+  uint32_t trunc_xof;
 };
 
 struct InPtrs {
@@ -229,11 +232,11 @@ DEV void put_elem(const DevParams& p, void* base, uint32_t idx, uint32_t r, cons
   F::store(base, (size_t)idx * p.ld + r, x);
 }
 
-// Elements contained in squeeze block b of an XOF stream (no rejection).
-template <class F>
-DEV void squeeze_block(const DevParams& p, const KState& s, uint32_t b, uint32_t n_elems,
-                       uint32_t& pend0, uint32_t& pend1, void* base, uint32_t r,
-                       uint32_t& flag) {
+// Elements contained in squeeze block b of an XOF stream (no rejection), handed to put(idx, w)
+// in index order.
+template <class F, class Put>
+DEV void squeeze_block_with(const KState& s, uint32_t b, uint32_t n_elems, uint32_t& pend0,
+                            uint32_t& pend1, Put&& put) {
   if constexpr (F::ES == 16) {
     uint32_t e0 = 21 * (b >> 1);
     if ((b & 1) == 0) {
@@ -241,20 +244,20 @@ DEV void squeeze_block(const DevParams& p, const KState& s, uint32_t b, uint32_t
       for (int t = 0; t < 10; t++) {
         uint32_t w[4] = {kword(s, 4 * t), kword(s, 4 * t + 1), kword(s, 4 * t + 2),
                          kword(s, 4 * t + 3)};
-        if (e0 + t < n_elems) put_elem<F>(p, base, e0 + t, r, w, flag);
+        if (e0 + t < n_elems) put(e0 + t, w);
       }
       pend0 = kword(s, 40);
       pend1 = kword(s, 41);
     } else {
       {
         uint32_t w[4] = {pend0, pend1, kword(s, 0), kword(s, 1)};
-        if (e0 + 10 < n_elems) put_elem<F>(p, base, e0 + 10, r, w, flag);
+        if (e0 + 10 < n_elems) put(e0 + 10, w);
       }
 #pragma unroll
       for (int t = 0; t < 10; t++) {
         uint32_t w[4] = {kword(s, 2 + 4 * t), kword(s, 3 + 4 * t), kword(s, 4 + 4 * t),
                          kword(s, 5 + 4 * t)};
-        if (e0 + 11 + t < n_elems) put_elem<F>(p, base, e0 + 11 + t, r, w, flag);
+        if (e0 + 11 + t < n_elems) put(e0 + 11 + t, w);
       }
     }
   } else {
@@ -262,9 +265,75 @@ DEV void squeeze_block(const DevParams& p, const KState& s, uint32_t b, uint32_t
 #pragma unroll
     for (int t = 0; t < 21; t++) {
       uint32_t w[2] = {kword(s, 2 * t), kword(s, 2 * t + 1)};
-      if (e0 + t < n_elems) put_elem<F>(p, base, e0 + t, r, w, flag);
+      if (e0 + t < n_elems) put(e0 + t, w);
     }
   }
+}
+
+// Elements of squeeze block b stored to SoA column r of base (rejections flagged)
+template <class F>
+DEV void squeeze_block(const DevParams& p, const KState& s, uint32_t b, uint32_t n_elems,
+                       uint32_t& pend0, uint32_t& pend1, void* base, uint32_t r,
+                       uint32_t& flag) {
+  squeeze_block_with<F>(s, b, n_elems, pend0, pend1, [&](uint32_t i, const uint32_t* w) {
+    put_elem<F>(p, base, i, r, w, flag);
+  });
+}
+
+// a += m << s over a 160-bit accumulator, s < 32 (wave-uniform)
+DEV void shl_add160(sum128& a, const f128& m, uint32_t s) {
+  uint32_t w0 = m.w[0], w1 = m.w[1], w2 = m.w[2], w3 = m.w[3], w4 = 0;
+  if (s) {
+    const uint32_t rs = 32 - s;
+    w4 = m.w[3] >> rs;
+    w3 = __builtin_amdgcn_alignbit(m.w[3], m.w[2], rs);
+    w2 = __builtin_amdgcn_alignbit(m.w[2], m.w[1], rs);
+    w1 = __builtin_amdgcn_alignbit(m.w[1], m.w[0], rs);
+    w0 = m.w[0] << s;
+  }
+  uint32_t c;
+  a.w[0] = addc(a.w[0], w0, 0, &c);
+  a.w[1] = addc(a.w[1], w1, c, &c);
+  a.w[2] = addc(a.w[2], w2, c, &c);
+  a.w[3] = addc(a.w[3], w3, c, &c);
+  a.w[4] = a.w[4] + w4 + c;
+}
+
+// On-the-fly truncation of a Field128 measurement-share stream (SumVec truncate, FPVec entry
+// decode): entry e = sum_(b < nb) 2^b m_(e nb + b), accumulated over 160 bits as the elements
+// are squeezed and stored to out[e] (leading dimension ld_out), so the query kernel does not
+// re-read the share for it.  nb <= 32; elements arrive in index order from 0; elements past
+// the n_ent entries (FPVec's claimed-norm bits) are not entries.  DevParams::trunc_xof.
+struct TruncSink {
+  void* out;
+  size_t ld_out;
+  uint32_t r, nb, n_ent, e, bit;
+  sum128 acc;
+  DEV TruncSink(const DevParams& p, void* o, uint32_t rr)
+      : out(o), ld_out(p.ld_out), r(rr), nb(p.bits), n_ent(p.out_len), e(0), bit(0) {
+    sum_zero(acc);
+  }
+  DEV void put(const f128& m) {
+    if (e >= n_ent) return;  // wave-uniform
+    shl_add160(acc, m, bit);
+    if (++bit == nb) {
+      Fp128::store(out, (size_t)e * ld_out + r, sum_reduce(acc));
+      sum_zero(acc);
+      bit = 0;
+      e++;
+    }
+  }
+};
+
+// squeeze_block for the measurement share with the truncation sink (TR) or without
+template <bool TR>
+DEV void squeeze_meas(const DevParams& p, const KState& s, uint32_t b, uint32_t n_elems,
+                      uint32_t& pend0, uint32_t& pend1, void* base, uint32_t r, uint32_t& flag,
+                      TruncSink& ts) {
+  squeeze_block_with<Fp128>(s, b, n_elems, pend0, pend1, [&](uint32_t i, const uint32_t* w) {
+    put_elem<Fp128>(p, base, i, r, w, flag);
+    if constexpr (TR) ts.put(mk128(w[0], w[1], w[2], w[3]));
+  });
 }
 
 
@@ -474,6 +543,7 @@ bool launch_xof_pair(const DevParams& p, InPtrs in, Scratch sc, hipStream_t st);
 // false if the instance is not one it takes
 bool launch_query_wide(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
                        int gs);
+bool query_wide_takes(const DevParams& p);
 // FPVec FLP query + decide + prepare message + truncate for p.n reports (prio3_fpvec.hip)
 void launch_fpvec_query(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
                         int gs);
@@ -538,6 +608,9 @@ struct prio3_engine {
   // qw_gs: wire columns per lane and sweep (2, 3 or 4)
   int qwide = 1;
   int qw_gs = 3;
+  // option: the helper XOF truncates the measurement share on the fly (SumVec under k_query_w,
+  // FPVec entry decode) instead of the query re-reading it: 1 on, 0 off
+  int trunc_xof = 1;
   int timing = 0;
   Mp64Params mp{};  // PRIO3_SUMVEC_F64_MP only
   uint64_t* d_sigma64 = nullptr;

@@ -219,7 +219,8 @@ __global__ __launch_bounds__(256, XOFD_OCC) void k_xof(DevParams p, InPtrs in, S
 // here, from the squeezed elements while they are in registers; a wave in which any report got
 // flagged for the slow path is un-fused at the end (its partials are ignored, its reports go
 // through the fix-up list with their corrected shares).
-template <bool FUSE>
+// TR: the measurement share is also truncated into sc.out on the fly (DevParams::trunc_xof).
+template <bool FUSE, bool TR = false>
 __global__ __launch_bounds__(256, XOFD_OCC) void k_xofd(DevParams p, InPtrs in, Scratch sc) {
   typedef Fp128 F;
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -279,6 +280,7 @@ __global__ __launch_bounds__(256, XOFD_OCC) void k_xofd(DevParams p, InPtrs in, 
   }
   uint32_t tail[11];
   uint32_t pend0 = 0, pend1 = 0;
+  TruncSink ts(p, sc.out, r);
   const int Mi = (int)M;
   // wave totals of share elements e0, e0+1 (zero outside [0, M)), slot lane of lanes 0..15
   auto fused_pair = [&](int e0, const f128& a, const f128& b2) __attribute__((always_inline)) {
@@ -315,7 +317,7 @@ __global__ __launch_bounds__(256, XOFD_OCC) void k_xofd(DevParams p, InPtrs in, 
   // block 0: prefix (42 bytes) + the first 126 bytes of the share
   {
     if (FUSE && fuse) fuse_block(0, 0, 0);
-    squeeze_block<F>(p, ms, 0, M, pend0, pend1, sc.meas, r, flag);
+    squeeze_meas<TR>(p, ms, 0, M, pend0, pend1, sc.meas, r, flag, ts);
     Msg m;
     msg_zero(m);
     msg_dst(m, p.dst[7]);
@@ -338,7 +340,7 @@ __global__ __launch_bounds__(256, XOFD_OCC) void k_xofd(DevParams p, InPtrs in, 
   for (uint32_t b = 1; b < B; b++) {
     const bool hasW = b < K;  // wave-uniform
     if (FUSE && fuse && hasW) fuse_block(b, pend0, pend1);
-    if (hasW) squeeze_block<F>(p, ms, b, M, pend0, pend1, sc.meas, r, flag);
+    if (hasW) squeeze_meas<TR>(p, ms, b, M, pend0, pend1, sc.meas, r, flag, ts);
 #pragma unroll
     for (int j = 0; j < 10; j++)
       kxor_word(js, j, __builtin_amdgcn_alignbit(tail[j + 1], tail[j], 16));
@@ -358,7 +360,7 @@ __global__ __launch_bounds__(256, XOFD_OCC) void k_xofd(DevParams p, InPtrs in, 
   {
     const bool hasW = B < K;
     if (FUSE && fuse && hasW) fuse_block(B, pend0, pend1);
-    if (hasW) squeeze_block<F>(p, ms, B, M, pend0, pend1, sc.meas, r, flag);
+    if (hasW) squeeze_meas<TR>(p, ms, B, M, pend0, pend1, sc.meas, r, flag, ts);
 #pragma unroll
     for (int j = 0; j < 42; j++) {
       uint32_t x;
@@ -781,10 +783,20 @@ __global__ __launch_bounds__(64) void k_xof_slow(DevParams p, InPtrs in, Scratch
     bx_absorb(y, 1);
     bx_absorb_w(y, nonce, 16);
   }
-  for (uint32_t i = 0; i < p.meas_len; i++) {
-    bx_next_elem<F>(x, w);
-    F::store(sc.meas, (size_t)i * p.ld + r, F::from_words(w));
-    if (JR) bx_absorb_w(y, w, F::ES);
+  if constexpr (F::ES == 16) {
+    TruncSink ts(p, sc.out, r);
+    for (uint32_t i = 0; i < p.meas_len; i++) {
+      bx_next_elem<F>(x, w);
+      F::store(sc.meas, (size_t)i * p.ld + r, F::from_words(w));
+      if (p.trunc_xof) ts.put(mk128(w[0], w[1], w[2], w[3]));
+      if (JR) bx_absorb_w(y, w, F::ES);
+    }
+  } else {
+    for (uint32_t i = 0; i < p.meas_len; i++) {
+      bx_next_elem<F>(x, w);
+      F::store(sc.meas, (size_t)i * p.ld + r, F::from_words(w));
+      if (JR) bx_absorb_w(y, w, F::ES);
+    }
   }
   uint32_t part[4] = {0, 0, 0, 0};
   if (JR) {
@@ -2719,12 +2731,17 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
       qs.flag += col;
       qs.out = (uint8_t*)sc.out + es * s0;
       const uint32_t qb = (q.n + 255) / 256, qb64 = (q.n + 63) / 64;
-      // k_xofd (two live Keccak states: share squeeze + joint-rand absorb) unless A/B-ed off
+      // k_xofd (two live Keccak states: share squeeze + joint-rand absorb) unless A/B-ed off;
+      // both dual-sponge kernels decode the entries (the output share) as they squeeze
+      const bool dual = e->split_xof == 2 && (42 + dp.meas_len * 16) / 168 >= 2;
+      q.trunc_xof = dual && e->trunc_xof ? 1u : 0u;
       bool paired = false;
-      if (e->xof_pair != 0 && e->split_xof == 2)
+      if (e->xof_pair != 0 && dual)
         TIMED(e, ss, "k_xof_pair", (paired = launch_xof_pair(q, qi, qs, ss)));
       if (paired) {
-      } else if (e->split_xof == 2 && (42 + dp.meas_len * 16) / 168 >= 2)
+      } else if (dual && q.trunc_xof)
+        TIMED(e, ss, "k_xofd", (k_xofd<false, true><<<qb, 256, 0, ss>>>(q, qi, qs)));
+      else if (dual)
         TIMED(e, ss, "k_xofd", (k_xofd<false><<<qb, 256, 0, ss>>>(q, qi, qs)));
       else
         TIMED(e, ss, "k_xof", (k_xof<Fp128><<<qb, 256, 0, ss>>>(q, qi, qs)));
@@ -2739,15 +2756,24 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
     return PRIO3_OK;
   }
   if (dp.es == 16) {
+    const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
+    const bool wide = ps && e->qwide && !(e->qpair && (dp.P == 32 || dp.P == 16)) &&
+                      query_wide_takes(dp);
     const bool pair_xof =
         !fuse && e->xof_pair > 0;  // auto: off (SumVec 8x1000 A/B: 15.0 vs 12.8 ms, r02j)
+    const bool dual = dp.jr_len && e->split_xof == 2 && (42 + dp.meas_len * 16) / 168 >= 2;
+    // SumVec under k_query_w: the truncation rides on the XOF's squeeze (the query then reads
+    // the share once)
+    dp.trunc_xof = dp.kind == PRIO3_SUMVEC && wide && dual && !fuse && e->trunc_xof ? 1u : 0u;
     bool paired = false;
-    if (dp.jr_len && e->split_xof == 2 && pair_xof)
+    if (dual && pair_xof)
       TIMED(e, st, "k_xof_pair", (paired = launch_xof_pair(dp, in, sc, st)));
     if (paired) {
-    } else if (dp.jr_len && e->split_xof == 2 && (42 + dp.meas_len * 16) / 168 >= 2) {
+    } else if (dual) {
       if (fuse)
         TIMED(e, st, "k_xofd", (k_xofd<true><<<blocks, 256, 0, st>>>(dp, in, sc)));
+      else if (dp.trunc_xof)
+        TIMED(e, st, "k_xofd", (k_xofd<false, true><<<blocks, 256, 0, st>>>(dp, in, sc)));
       else
         TIMED(e, st, "k_xofd", (k_xofd<false><<<blocks, 256, 0, st>>>(dp, in, sc)));
     } else if (dp.jr_len && e->split_xof) {
@@ -2760,13 +2786,11 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
       TIMED(e, st, "k_xof", (k_xof<Fp128><<<blocks, 256, 0, st>>>(dp, in, sc)));
     }
     TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp128><<<blocks64, 64, 0, st>>>(dp, in, sc)));
-    const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
     bool done = false;
     if (ps && e->qpair && (dp.P == 32 || dp.P == 16)) {
       TIMED(e, st, "k_query_pair", (done = launch_query_pair(dp, in, sc, out, st)));
     }
-    if (!done && ps && e->qwide && dp.sigma_dev && (dp.P == 64 || dp.P == 128) &&
-        (dp.kind != PRIO3_SUMVEC || dp.bits <= 32))
+    if (!done && wide)
       TIMED(e, st, "k_query_w", (done = launch_query_wide(dp, in, sc, out, st, e->qw_gs)));
     if (done) {
     } else if (ps && dp.P == 32 && dp.chunk == 16 && dp.calls == 16 && e->qh_regs)
@@ -3182,7 +3206,8 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
               {"qh_prefetch", &e->qh_prefetch},    {"split_xof", &e->split_xof},
               {"qpair", &e->qpair},                {"timing", &e->timing},
               {"coalesce", &e->coalesce},          {"experimental_fpvec", &e->experimental_fpvec},
-              {"xof_pair", &e->xof_pair},          {"qwide", &e->qwide}};
+              {"xof_pair", &e->xof_pair},          {"qwide", &e->qwide},
+              {"trunc_xof", &e->trunc_xof}};
   if (!strcmp(key, "qw_gs")) {
     if (value < 2 || value > 4) return PRIO3_EINVAL;
     e->qw_gs = (int)value;

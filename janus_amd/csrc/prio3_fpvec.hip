@@ -193,9 +193,14 @@ __global__ __launch_bounds__(256) void k_query_fp(DevParams p, InPtrs in, Scratc
       for (int q = 0; q < GS; q++) {
         const uint32_t idx = k * C1 + jg + q;
         if (jg + q < C1 && idx < E) {
-          const T y = decode_bits16(sc.meas, nb * idx, nb, ld, r);  // nb is 16 or 32
-          DCHECK(nb * idx + nb <= M);
-          F::store(sc.out, (size_t)idx * p.ld_out + r, y);
+          T y;
+          if (p.trunc_xof) {  // decoded by the XOF kernel as it squeezed the share
+            y = F::load(sc.out, (size_t)idx * p.ld_out + r);
+          } else {
+            y = decode_bits16(sc.meas, nb * idx, nb, ld, r);  // nb is 16 or 32
+            DCHECK(nb * idx + nb <= M);
+            F::store(sc.out, (size_t)idx * p.ld_out + r, y);
+          }
           Ac[q] = F::add(Ac[q], F::mul(Lk, y));
         }
       }

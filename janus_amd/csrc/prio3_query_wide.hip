@@ -306,7 +306,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS == 2 ? 3
     out.status[r] = status;
   }
   // ---- truncate (SumVec): entry e = sum_b 2^b m_(e bits + b), entries e = l mod 8 per lane
-  if (p.kind == PRIO3_SUMVEC && live) {
+  if (p.kind == PRIO3_SUMVEC && live && !p.trunc_xof) {
     const uint32_t nb = p.bits;  // <= 32 (launcher)
     for (uint32_t e = l; e < p.out_len; e += 8) {
       sum128 a;
@@ -331,12 +331,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS == 2 ? 3
 
 // true if launched: ParallelSum(Mul) instances (Histogram, SumVec with bits <= 32) with P = 64 or
 // 128 and the engine's sigma table
-bool launch_query_wide(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
-                       int gs) {
-  if (p.es != 16 || !p.sigma_dev || p.n == 0) return false;
+bool query_wide_takes(const DevParams& p) {
+  if (p.es != 16 || !p.sigma_dev || (p.P != 64 && p.P != 128)) return false;
   if (p.kind != PRIO3_HISTOGRAM && p.kind != PRIO3_SUMVEC) return false;
   if (p.kind == PRIO3_SUMVEC && p.bits > 32) return false;
-  if (p.calls + 1 > p.P || p.glen != 2 * p.P - 1 || p.arity != 2 * p.chunk) return false;
+  return p.calls + 1 <= p.P && p.glen == 2 * p.P - 1 && p.arity == 2 * p.chunk;
+}
+
+bool launch_query_wide(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
+                       int gs) {
+  if (!query_wide_takes(p) || p.n == 0) return false;
   const uint32_t blocks = (p.n + 31) / 32;
   if (p.P == 128) {
     if (gs == 2)

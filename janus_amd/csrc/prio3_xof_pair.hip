@@ -85,7 +85,9 @@ DEV void absorb_share_block(KState& st, uint32_t h, bool hasW, uint32_t (&tail)[
   }
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) void k_xof_pair(
+// TR: the even lane also truncates the share into sc.out as it squeezes (DevParams::trunc_xof)
+template <bool TR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TR ? 4 : 5, TR ? 4 : 5))) void k_xof_pair(
     DevParams p, InPtrs in, Scratch sc) {
   const uint32_t tid = threadIdx.x, h = tid & 1u;
   const uint32_t r = blockIdx.x * 128 + (tid >> 1);
@@ -155,20 +157,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
 #pragma unroll
   for (int t = 0; t < 11; t++) tail[t] = 0;
   uint32_t pend0 = 0, pend1 = 0;
+  TruncSink ts(p, sc.out, rr);
   // block 0 (prefix), full blocks 1 .. B-1, the padded last block B (B >= 2: see the launcher)
-  if (h == 0 && live) squeeze_block<F>(p, st, 0, M, pend0, pend1, sc.meas, rr, flag);
+  if (h == 0 && live) squeeze_meas<TR>(p, st, 0, M, pend0, pend1, sc.meas, rr, flag, ts);
   absorb_share_block<true, false>(st, h, true, tail, pre, rem);
   keccak_p12(st);
 #pragma unroll 1
   for (uint32_t b = 1; b < B; b++) {
     const bool hasW = b < K;  // uniform
-    if (hasW && h == 0 && live) squeeze_block<F>(p, st, b, M, pend0, pend1, sc.meas, rr, flag);
+    if (hasW && h == 0 && live) squeeze_meas<TR>(p, st, b, M, pend0, pend1, sc.meas, rr, flag, ts);
     absorb_share_block<false, false>(st, h, hasW, tail, pre, rem);
     keccak_p12(st);  // even: next squeeze block; odd: absorb
   }
   {
     const bool hasW = B < K;
-    if (hasW && h == 0 && live) squeeze_block<F>(p, st, B, M, pend0, pend1, sc.meas, rr, flag);
+    if (hasW && h == 0 && live) squeeze_meas<TR>(p, st, B, M, pend0, pend1, sc.meas, rr, flag, ts);
     absorb_share_block<false, true>(st, h, hasW, tail, pre, rem);
     keccak_p12(st);
   }
@@ -224,6 +227,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
 // long-share joint-randomness instances (SumVec / FPVec): true if launched
 bool launch_xof_pair(const DevParams& p, InPtrs in, Scratch sc, hipStream_t st) {
   if (p.es != 16 || !p.jr_len || (42 + p.meas_len * 16) / 168 < 2) return false;
-  k_xof_pair<<<(p.n + 127) / 128, 256, 0, st>>>(p, in, sc);
+  if (p.trunc_xof)
+    k_xof_pair<true><<<(p.n + 127) / 128, 256, 0, st>>>(p, in, sc);
+  else
+    k_xof_pair<false><<<(p.n + 127) / 128, 256, 0, st>>>(p, in, sc);
   return true;
 }

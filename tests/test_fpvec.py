@@ -346,13 +346,27 @@ def test_gpu_fpvec_requires_explicit_opt_in():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("trunc_xof", [1, 0])
 @pytest.mark.parametrize("xof_pair", [0, 1])
-def test_gpu_fpvec_xof_lane_pairs(xof_pair):
-    """The FPVec share phase with and without the lane-pair XOF (auto: on from 2048 share
-    elements, so forced here at length 24), across two sub-batches."""
+def test_gpu_fpvec_xof_lane_pairs(xof_pair, trunc_xof):
+    """The FPVec share phase with and without the lane-pair XOF (the FPVec default), with the
+    entry decode (output share) done by the XOF as it squeezes or by the query, across two
+    sub-batches."""
     v = _vdaf(24)
     reps = _reports(v, 300, seed=23, distinct=60)
     _tamper(v, reps, 0.05, seed=6)
     t = v.t
     per = 16 * (t.meas_len + t.proof_len + 2 + 2 + 2 * (t.P0 + t.P1) + t.K0) + 33
-    _check(v, reps, _run(v, reps, sub_bytes=per * 256 + 1, opts={"xof_pair": xof_pair}))
+    _check(v, reps, _run(v, reps, sub_bytes=per * 256 + 1,
+                         opts={"xof_pair": xof_pair, "trunc_xof": trunc_xof}))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [16, 32])
+def test_gpu_fpvec_slow_path_decodes_entries(bits):
+    """Every report through the rejection-sampling XOF (force_slow_path): its entry decode must
+    give the same output shares as the fast kernels'."""
+    v = _vdaf(5, bits)
+    reps = _reports(v, 70, seed=31 + bits)
+    _tamper(v, reps, 0.1, seed=7)
+    _check(v, reps, _run(v, reps, opts={"force_slow_path": 1}))

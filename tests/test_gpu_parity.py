@@ -242,3 +242,13 @@ def test_query_wide_off_and_slow_path(name):
     n = 70 if "1000" in name else 200
     _check_against_oracle(CONFIGS[name], n, seed=23, opts={"qwide": 0})
     _check_against_oracle(CONFIGS[name], n, seed=29, force_slow=True)
+    _check_against_oracle(CONFIGS[name], n, seed=31, opts={"trunc_xof": 0})
+
+
+@pytest.mark.parametrize("name", ["sumvec_8x1000_c63", "sumvec_32x20_c7"])
+def test_truncate_in_xof_chunked_and_paired(name):
+    """SumVec under k_query_w truncates inside the XOF: over stream-overlapped chunks (the
+    output-share columns of every chunk) and on the lane-pair XOF."""
+    n = 600 if "1000" in name else 1500
+    _check_against_oracle(CONFIGS[name], n, seed=37, opts={"coalesce": 0, "chunks": 3})
+    _check_against_oracle(CONFIGS[name], n // 3, seed=41, opts={"xof_pair": 1})
