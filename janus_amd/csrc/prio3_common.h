@@ -545,8 +545,10 @@ bool launch_query_wide(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, h
                        int gs);
 bool query_wide_takes(const DevParams& p);
 // FPVec FLP query + decide + prepare message + truncate for p.n reports (prio3_fpvec.hip)
+// gs < 0: the eight-lane kernel k_query_fpw with column group -gs
 void launch_fpvec_query(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
                         int gs);
+bool fpvec_query_wide_takes(const DevParams& p);
 
 struct Slab;
 // The device state of one prepare call (helper or leader) over n reports: the SoA scratch, the
@@ -611,6 +613,10 @@ struct prio3_engine {
   // option: the helper XOF truncates the measurement share on the fly (SumVec under k_query_w,
   // FPVec entry decode) instead of the query re-reading it: 1 on, 0 off
   int trunc_xof = 1;
+  // option: FPVec query on eight lanes per report (k_query_fpw): 1 on, 0 off (k_query_fp);
+  // fp_wgs: its gadget-0 columns per lane and sweep (2, 3 or 4)
+  int fp_wide = 1;
+  int fp_wgs = 3;
   int timing = 0;
   Mp64Params mp{};  // PRIO3_SUMVEC_F64_MP only
   uint64_t* d_sigma64 = nullptr;

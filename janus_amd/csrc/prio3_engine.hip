@@ -2746,7 +2746,10 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
       else
         TIMED(e, ss, "k_xof", (k_xof<Fp128><<<qb, 256, 0, ss>>>(q, qi, qs)));
       TIMED(e, ss, "k_xof_slow", (k_xof_slow<Fp128><<<qb64, 64, 0, ss>>>(q, qi, qs)));
-      TIMED(e, ss, "k_query_fp", launch_fpvec_query(q, qi, qs, qo, ss, e->fp_gs));
+      if (e->fp_wide && fpvec_query_wide_takes(q))
+        TIMED(e, ss, "k_query_fpw", launch_fpvec_query(q, qi, qs, qo, ss, -e->fp_wgs));
+      else
+        TIMED(e, ss, "k_query_fp", launch_fpvec_query(q, qi, qs, qo, ss, e->fp_gs));
     }
     if (ov)
       for (size_t i = 0; i < e->side.size(); i++) {
@@ -3100,27 +3103,35 @@ int prio3_engine_create_ex(const prio3_params* params, const uint8_t* verify_key
     return PRIO3_EDEVICE;
   }
   ws_stream_put(device, probe);  // the first member of the GPU's stream pool
-  if ((e->dp.kind == PRIO3_HISTOGRAM || e->dp.kind == PRIO3_SUMVEC) &&
-      (e->dp.P == 64 || e->dp.P == 128)) {
-    // k_query_w: sigma_e = sum_(c=1..calls) alpha^(ce), e < P (the range check's weights)
+  const bool fpv = e->dp.kind == PRIO3_FPVEC_BOUNDED_L2;
+  if (((e->dp.kind == PRIO3_HISTOGRAM || e->dp.kind == PRIO3_SUMVEC) &&
+       (e->dp.P == 64 || e->dp.P == 128)) ||
+      (fpv && e->dp.logP <= 10 && e->dp.logP1 <= 10)) {
+    // k_query_w / k_query_fpw: sigma_e = sum_(c=1..calls) alpha_P^(ce), e < P -- the weights of
+    // sum_c p(alpha^c) over the polynomial's coefficients (FPVec: gadget 0's table, then gadget
+    // 1's)
     const DevParams& d = e->dp;
-    u128 alpha = 0;
-    for (int k = 0; k < 4; k++) alpha |= (u128)d.roots128[d.logP][k] << (32 * k);
-    std::vector<uint4> sig(d.P);
-    for (uint32_t e2 = 0; e2 < d.P; e2++) {
-      const u128 ae = hpow(alpha, e2, HP128);
-      u128 s = 0, x = 1;
-      for (uint32_t c = 1; c <= d.calls; c++) {
-        x = hmul(x, ae, HP128);
-        s += x;
-        if (s < x || s >= HP128) s -= HP128;
+    std::vector<uint4> sig;
+    auto table = [&](uint32_t logP, uint32_t calls) {
+      u128 alpha = 0;
+      for (int k = 0; k < 4; k++) alpha |= (u128)d.roots128[logP][k] << (32 * k);
+      for (uint32_t e2 = 0; e2 < (1u << logP); e2++) {
+        const u128 ae = hpow(alpha, e2, HP128);
+        u128 s = 0, x = 1;
+        for (uint32_t c = 1; c <= calls; c++) {
+          x = hmul(x, ae, HP128);
+          s += x;
+          if (s < x || s >= HP128) s -= HP128;
+        }
+        sig.push_back(make_uint4((uint32_t)s, (uint32_t)(s >> 32), (uint32_t)(s >> 64),
+                                 (uint32_t)(s >> 96)));
       }
-      sig[e2] = make_uint4((uint32_t)s, (uint32_t)(s >> 32), (uint32_t)(s >> 64),
-                           (uint32_t)(s >> 96));
-    }
-    if (hipMalloc((void**)&e->d_sigma128, sizeof(uint4) * d.P) != hipSuccess ||
-        hipMemcpy(e->d_sigma128, sig.data(), sizeof(uint4) * d.P, hipMemcpyHostToDevice) !=
-            hipSuccess) {
+    };
+    table(d.logP, d.calls);
+    if (fpv) table(d.logP1, d.calls1);
+    if (hipMalloc((void**)&e->d_sigma128, sizeof(uint4) * sig.size()) != hipSuccess ||
+        hipMemcpy(e->d_sigma128, sig.data(), sizeof(uint4) * sig.size(),
+                  hipMemcpyHostToDevice) != hipSuccess) {
       delete e;
       return PRIO3_EDEVICE;
     }
@@ -3207,7 +3218,12 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
               {"qpair", &e->qpair},                {"timing", &e->timing},
               {"coalesce", &e->coalesce},          {"experimental_fpvec", &e->experimental_fpvec},
               {"xof_pair", &e->xof_pair},          {"qwide", &e->qwide},
-              {"trunc_xof", &e->trunc_xof}};
+              {"trunc_xof", &e->trunc_xof},        {"fp_wide", &e->fp_wide}};
+  if (!strcmp(key, "fp_wgs")) {
+    if (value < 2 || value > 4) return PRIO3_EINVAL;
+    e->fp_wgs = (int)value;
+    return PRIO3_OK;
+  }
   if (!strcmp(key, "qw_gs")) {
     if (value < 2 || value > 4) return PRIO3_EINVAL;
     e->qw_gs = (int)value;

@@ -326,7 +326,8 @@ def test_gpu_fpvec_scratch_wider_than_sub_batch():
     eng.set_option("timing", 1)
     A = lambda k: np.array([list(r[k]) for r in reps], np.uint8)
     msgs, status, batch = eng.prepare_batch(A("nonce"), A("pub"), A("helper"), A("lps"))
-    assert eng.timing()["k_query_fp"][1] == 2  # two sub-batches
+    tm = eng.timing()
+    assert tm.get("k_query_fpw", tm.get("k_query_fp"))[1] == 2  # two sub-batches
     outs = batch.output_shares()
     agg, cnt = batch.accumulate()
     _check(v, reps, (msgs, status, outs, agg, cnt))
@@ -370,3 +371,19 @@ def test_gpu_fpvec_slow_path_decodes_entries(bits):
     reps = _reports(v, 70, seed=31 + bits)
     _tamper(v, reps, 0.1, seed=7)
     _check(v, reps, _run(v, reps, opts={"force_slow_path": 1}))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("length,opts", [
+    (24, {"fp_wide": 0}), (24, {"fp_wgs": 2}), (24, {"fp_wgs": 4}),
+    (24, {"fp_wgs": 3, "trunc_xof": 0}), (200, {"fp_wgs": 3}), (1000, {"fp_wgs": 4, "trunc_xof": 0}),
+])
+def test_gpu_fpvec_query_variants(length, opts):
+    """The eight-lane FPVec query (k_query_fpw, default) at each column-group width, with the
+    entries decoded by the XOF or by the query, against the one-lane k_query_fp (fp_wide=0) and
+    the restatement; 1000 entries exercises the two-level Lagrange split (P0 = 128 -> 8 x 16)."""
+    v = _vdaf(length)
+    n = 130 if length >= 1000 else 200
+    reps = _reports(v, n, seed=43 + length, distinct=5 if length >= 1000 else 40)
+    _tamper(v, reps, 0.1, seed=9)
+    _check(v, reps, _run(v, reps, opts=opts))
