@@ -348,8 +348,20 @@ def main():
         m = cb.pop("n")
         gm = prep_msgs[:m].cpu().numpy()
         gs = status[:m].cpu().numpy()
-        out["checks"]["cpu_gpu_parity_on_sample"] = bool(np.array_equal(gs, cst) and
-                                                         np.array_equal(gm, msgs))
+        # the GPU aggregate share and count of the same sample: the last step's device run
+        # finished again with an accept mask selecting its first m reports
+        accept = torch.zeros(n, dtype=torch.uint8, device=dev)
+        accept[:m] = 1
+        agg_s = torch.zeros_like(agg)
+        cnt_s = torch.zeros_like(cnt)
+        eng.aggregate_finish_device(status, accept, agg_s, cnt_s)
+        torch.cuda.synchronize()
+        out["checks"]["cpu_gpu_parity_on_sample"] = bool(
+            np.array_equal(gs, cst) and np.array_equal(gm, msgs) and
+            np.array_equal(agg_s.cpu().numpy().reshape(-1), np.asarray(cagg).reshape(-1)) and
+            int(cnt_s[0].item()) == int(np.asarray(ccnt).reshape(-1)[0]))
+        out["checks"]["cpu_gpu_parity_covers"] = (f"statuses, prepare messages, aggregate share "
+                                                  f"and count of {m} reports")
         from oracle.oracle import batch_metadata
         eck, eiv = batch_metadata(data["nonces"].cpu().numpy(), report_times.cpu().numpy(),
                                   status.cpu().numpy(), None, None, 1)
@@ -692,7 +704,7 @@ def pipeline_main(args):
         st_all = st | u["msg_status"]
         eng.batch_metadata_device(u["report_ids"], u["times"], st_all, accept, seg, 1, cks, ivs,
                                   stream=s)
-        pe = torch.where(hs == 0, torch.full_like(hs, 0xFF), hs)
+        pe = DJ.prepare_error(hs, u["msg_status"])
         res["out"], res["len"] = DJ.encode_resp_device(u["report_ids"], pe, st_all, msgs, 16,
                                                        stream=s)
         res["mism"] = mism

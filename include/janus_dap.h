@@ -37,7 +37,12 @@ enum { JANUS_DAP_QUERY_TIME_INTERVAL = 1, JANUS_DAP_QUERY_FIXED_SIZE = 2 };
 
 /* Per-report message status written by unpack (prio3 status codes, janus_prio3.h): 0 = the
  * message is PingPongMessage::Initialize with a prep_share of the expected length;
- * 2 = CodecPrepShare (wrong prep_share length); 5 = PeerMessageMismatch (not Initialize). */
+ * 2 = CodecPrepShare (wrong prep_share length); 5 = PeerMessageMismatch (Continue / Finish);
+ * 6 = the public share has another length than layout->public_share_len -- it does not decode:
+ * PrepareError::InvalidMessage (aggregator.rs:1985-1999), after any HPKE error of the report.
+ * A PingPongMessage that does not decode (unknown type, bad framing) rejects the whole request,
+ * as Janus's request decode does.  The caller checks layout->public_share_len against the
+ * VDAF's public share length (a body whose first record is off is malformed throughout). */
 
 typedef struct {
   /* filled by janus_dap_agg_init_scan */
@@ -73,8 +78,8 @@ int janus_dap_agg_init_unpack_device(const janus_dap_agg_init_layout* layout, co
                                      uint8_t* d_msg_status, uint32_t* d_mismatch, void* stream);
 
 /* Host (sequential) unpack of any well-formed body into host SoA buffers sized for `cap`
- * records: public shares and prep shares of another length than the first record's get
- * msg_status 2 (prep share) or are zero-filled (public share: the prio3 engine rejects them);
+ * records: prep shares / public shares of another length than the first record's get
+ * msg_status 2 / 6 (the public share row is zero-filled);
  * payloads longer than ct_stride give ct_len 0 (HPKE decrypt error).  Returns the number of
  * records, or -1 if the body does not decode (the whole request is rejected, as Janus does). */
 int64_t janus_dap_agg_init_unpack_host(const uint8_t* body, size_t len,

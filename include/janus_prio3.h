@@ -242,6 +242,11 @@ int prio3_engine_set_option(prio3_engine* engine, const char* key, int64_t value
 int prio3_engine_timing(prio3_engine* engine, char* names, size_t names_cap, double* ms,
                         uint64_t* launches, int cap);
 void prio3_engine_timing_reset(prio3_engine* engine);
+/* 1 if the entry points emit roctx ranges (environment JANUS_ROCTX=1 when the library was first
+ * used and a roctx library loadable): "handle_aggregate_init_generic threadpool task" around
+ * prio3_helper_prepare_batch, "VDAF preparation" around the device prepares, "batch aggregation"
+ * around the accumulates -- the spans of aggregator.rs:1786-1790, 2021. */
+int prio3_trace_enabled(void);
 
 /* Test-only: runs one Field128 primitive of the device library over n host-supplied operand
  * pairs (16-byte LE elements) -- op 0/1: a*b (compiler / hand-scheduled), 2: a+b, 3: a-b,

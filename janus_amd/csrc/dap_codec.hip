@@ -87,10 +87,21 @@ __global__ __launch_bounds__(256) void k_unpack_check(UnpackArgs a) {
   // messages/src/tests/aggregation.rs:201-209)
   const uint32_t ty = ld_u8(b, o_msg);
   const uint32_t psl2 = msgl >= 5 ? ld_be32(b, o_msg + 1) : 0xffffffffu;
+  // a message that does not decode rejects the whole request: leave it to the host parser
+  bool wf = msgl >= 5 && ty <= 2;
+  if (wf && ty != 1) wf = (uint64_t)msgl == 5 + (uint64_t)psl2;
+  if (wf && ty == 1)
+    wf = 9 + (uint64_t)psl2 <= msgl &&
+         (uint64_t)msgl == 9 + (uint64_t)psl2 + ld_be32(b, o_msg + 5 + psl2);
+  if (!wf) {
+    atomicAdd(a.mismatch, 1u);
+    a.msg_status[r] = 2;
+    return;
+  }
   uint8_t st = 0;
   if (ty != 0)
     st = 5;  // PeerMessageMismatch
-  else if (psl2 != a.ps_len || msgl != 5 + psl2)
+  else if (psl2 != a.ps_len)
     st = 2;  // CodecPrepShare
   a.msg_status[r] = st;
   a.times[r] = ((uint64_t)ld_be32(b, o_time) << 32) | ld_be32(b, o_time + 4);
@@ -262,6 +273,27 @@ struct RecShape {
   uint64_t time, end;
 };
 
+uint32_t be32(const uint8_t* p) {
+  return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3];
+}
+
+// PingPongMessage framing (ping_pong.rs; messages/src/tests/aggregation.rs:201-268):
+// 0 Initialize { prep_share<u32> }, 1 Continue { prep_msg<u32>, prep_share<u32> },
+// 2 Finish { prep_msg<u32> }; the message must use every byte of its u32-prefixed field
+bool pingpong_wellformed(const uint8_t* m, uint64_t len) {
+  if (len < 5) return false;
+  const uint64_t a = be32(m + 1);
+  switch (m[0]) {
+    case 0:
+    case 2:
+      return len == 5 + a;
+    case 1:
+      return 9 + a <= len && len == 9 + a + be32(m + 5 + a);
+    default:
+      return false;
+  }
+}
+
 bool parse_record(Cur& c, RecShape& s) {
   s.o_id = c.o;
   c.need(16);
@@ -430,16 +462,17 @@ int64_t janus_dap_agg_init_unpack_host(const uint8_t* body, size_t len,
     } else {
       ct_len[r] = 0;  // HPKE decrypt error for this report
     }
-    const uint32_t ty = s.msg_len ? body[s.o_msg] : 0xffu;
-    uint32_t psl2 = 0xffffffffu;
-    if (s.msg_len >= 5)
-      psl2 = (uint32_t)body[s.o_msg + 1] << 24 | (uint32_t)body[s.o_msg + 2] << 16 |
-             (uint32_t)body[s.o_msg + 3] << 8 | body[s.o_msg + 4];
+    // the PingPongMessage is decoded with the request: a malformed one rejects the request
+    if (!pingpong_wellformed(body + s.o_msg, s.msg_len)) return -1;
+    const uint32_t ty = body[s.o_msg];
+    const uint32_t psl2 = be32(body + s.o_msg + 1);
     uint8_t stt = 0;
-    if (ty != 0)
-      stt = 5;
-    else if (psl2 != L->prep_share_len || s.msg_len != 5 + psl2)
-      stt = 2;
+    if (s.psl != L->public_share_len)
+      stt = 6;  // public share does not decode: InvalidMessage (aggregator.rs:1985-1999)
+    else if (ty != 0)
+      stt = 5;  // PeerMessageMismatch: Continue / Finish where Initialize is due
+    else if (psl2 != L->prep_share_len)
+      stt = 2;  // CodecPrepShare
     msg_status[r] = stt;
     uint8_t* pd = prep_shares + (size_t)L->prep_share_len * r;
     if (stt == 0)

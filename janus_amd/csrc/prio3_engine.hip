@@ -3266,6 +3266,7 @@ int prio3_device_prepare(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
                          const uint8_t* d_public_shares, const uint8_t* d_helper_shares,
                          const uint8_t* d_leader_prep_shares, uint8_t* d_prep_msgs,
                          uint8_t* d_status, void* stream) {
+  TraceSpan span_("VDAF preparation");
   if (!e) return PRIO3_EINVAL;
   if (e->dp.kind == PRIO3_FPVEC_BOUNDED_L2 && !e->experimental_fpvec)
     return PRIO3_EUNSUPPORTED;  // unpinned reconstruction: explicit opt-in only
@@ -3285,6 +3286,7 @@ int prio3_device_prepare_aggregate(prio3_engine* e, uint32_t n, const uint8_t* d
                                    const uint8_t* d_leader_prep_shares,
                                    const uint32_t* d_segment_ids, uint32_t n_segments,
                                    uint8_t* d_prep_msgs, uint8_t* d_status, void* stream) {
+  TraceSpan span_("VDAF preparation + batch aggregation");
   if (!e || n_segments == 0) return PRIO3_EINVAL;
   if (e->dp.kind == PRIO3_FPVEC_BOUNDED_L2 && !e->experimental_fpvec)
     return PRIO3_EUNSUPPORTED;  // unpinned reconstruction: explicit opt-in only
@@ -3307,6 +3309,7 @@ int prio3_device_prepare_aggregate(prio3_engine* e, uint32_t n, const uint8_t* d
 int prio3_device_aggregate_finish(prio3_engine* e, const uint8_t* d_status,
                                   const uint8_t* d_accept_mask, uint8_t* d_agg_shares,
                                   uint64_t* d_counts, void* stream) {
+  TraceSpan span_("batch aggregation");
   if (!e) return PRIO3_EINVAL;
   std::lock_guard<std::mutex> lk(e->mu);
   HIPCHK(hipSetDevice(e->device));
@@ -3341,6 +3344,7 @@ int prio3_device_accumulate(prio3_engine* e, uint32_t n, const uint8_t* d_status
                             const uint32_t* d_segment_ids, const uint8_t* d_accept_mask,
                             uint32_t n_segments, uint8_t* d_agg_shares, uint64_t* d_counts,
                             void* stream) {
+  TraceSpan span_("batch aggregation");
   if (!e || n_segments == 0) return PRIO3_EINVAL;
   std::lock_guard<std::mutex> lk(e->mu);
   HIPCHK(hipSetDevice(e->device));
@@ -3360,6 +3364,7 @@ int prio3_device_accumulate(prio3_engine* e, uint32_t n, const uint8_t* d_status
 int prio3_device_combine(prio3_engine* e, uint32_t k, uint32_t n_segments, const uint8_t* d_in,
                          const uint64_t* d_counts_in, uint8_t* d_out, uint64_t* d_counts_out,
                          void* stream) {
+  TraceSpan span_("aggregate share combine");
   if (!e || k == 0 || n_segments == 0) return PRIO3_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
@@ -3384,6 +3389,7 @@ int prio3_device_batch_metadata(prio3_engine* e, uint32_t n, const uint8_t* d_re
                                 const uint8_t* d_accept_mask, const uint32_t* d_segment_ids,
                                 uint32_t n_segments, uint8_t* d_checksums, uint64_t* d_intervals,
                                 void* stream) {
+  TraceSpan span_("batch aggregation metadata");
   if (!e || n_segments == 0 || (n && (!d_status || (d_checksums && !d_report_ids))))
     return PRIO3_EINVAL;
   HIPCHK(hipSetDevice(e->device));
@@ -3478,6 +3484,7 @@ int prio3_helper_prepare_batch(prio3_engine* e, uint32_t n, const uint8_t* nonce
                                const uint8_t* public_shares, const uint8_t* helper_shares,
                                const uint8_t* leader_prep_shares, uint8_t* prep_msgs_out,
                                uint8_t* status_out, prio3_batch** batch_out) {
+  TraceSpan span_("handle_aggregate_init_generic threadpool task");
   if (!e || (n && (!nonces || !helper_shares || !leader_prep_shares || !status_out)))
     return PRIO3_EINVAL;
   if (e->dp.kind == PRIO3_FPVEC_BOUNDED_L2 && !e->experimental_fpvec)
@@ -3508,6 +3515,7 @@ int prio3_helper_prepare_batch(prio3_engine* e, uint32_t n, const uint8_t* nonce
 
 int prio3_accumulate(prio3_batch* b, const uint32_t* segment_ids, const uint8_t* accept_mask,
                      uint32_t n_segments, uint8_t* agg_shares_out, uint64_t* counts_out) {
+  TraceSpan span_("batch aggregation");
   if (!b || !agg_shares_out || !counts_out || n_segments == 0) return PRIO3_EINVAL;
   prio3_engine* e = b->e;
   const size_t agg_len = (size_t)e->dp.out_len * e->dp.es, S = n_segments;
@@ -3618,6 +3626,7 @@ int prio3_device_leader_prepare_init(prio3_engine* e, uint32_t n, const uint8_t*
                                      const uint8_t* d_public_shares,
                                      const uint8_t* d_leader_input_shares, uint8_t* d_prep_shares,
                                      uint8_t* d_status, void* stream) {
+  TraceSpan span_("leader VDAF preparation");
   if (e && (e->dp.kind == PRIO3_SUMVEC_F64_MP || e->dp.kind == PRIO3_FPVEC_BOUNDED_L2))
     return PRIO3_EUNSUPPORTED;  // helper role only
   if (!e) return PRIO3_EINVAL;
@@ -3637,6 +3646,7 @@ int prio3_device_leader_prepare_init(prio3_engine* e, uint32_t n, const uint8_t*
 
 int prio3_device_leader_prepare_next(prio3_engine* e, uint32_t n, const uint8_t* d_prep_msgs,
                                      uint8_t* d_status, void* stream) {
+  TraceSpan span_("leader VDAF preparation");
   if (e && (e->dp.kind == PRIO3_SUMVEC_F64_MP || e->dp.kind == PRIO3_FPVEC_BOUNDED_L2))
     return PRIO3_EUNSUPPORTED;  // helper role only
   if (!e) return PRIO3_EINVAL;
@@ -3659,6 +3669,7 @@ int prio3_leader_prepare_init_batch(prio3_engine* e, uint32_t n, const uint8_t* 
                                     const uint8_t* public_shares,
                                     const uint8_t* leader_input_shares, uint8_t* prep_shares_out,
                                     uint8_t* status_out, prio3_batch** batch_out) {
+  TraceSpan span_("leader VDAF preparation");
   if (e && (e->dp.kind == PRIO3_SUMVEC_F64_MP || e->dp.kind == PRIO3_FPVEC_BOUNDED_L2))
     return PRIO3_EUNSUPPORTED;  // helper role only
   if (!e || (n && (!nonces || !leader_input_shares || !prep_shares_out || !status_out)))
@@ -3705,6 +3716,7 @@ int prio3_leader_prepare_init_batch(prio3_engine* e, uint32_t n, const uint8_t* 
 
 int prio3_leader_prepare_next_batch(prio3_batch* b, const uint8_t* prep_msgs,
                                     uint8_t* status_inout) {
+  TraceSpan span_("leader VDAF preparation");
   if (!b || !status_inout) return PRIO3_EINVAL;
   prio3_engine* e = b->e;
   const uint32_t n = b->n;
@@ -3732,6 +3744,8 @@ int prio3_leader_prepare_next_batch(prio3_batch* b, const uint8_t* prep_msgs,
   if (e->timing) collect_times(e);
   return PRIO3_OK;
 }
+
+int prio3_trace_enabled(void) { return trace_enabled() ? 1 : 0; }
 
 int prio3_selftest_field(int op, uint32_t n, const uint8_t* a, const uint8_t* b, uint8_t* out) {
   if (op < 0 || op > 5) return PRIO3_EINVAL;

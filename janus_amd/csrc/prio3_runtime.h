@@ -28,6 +28,19 @@ void ws_release(Slab* s, hipStream_t st);
 // bytes currently held by the GPU's pool (idle + in use), for tests
 size_t ws_pool_bytes(int device, size_t* idle_bytes);
 
+// ---- tracing -------------------------------------------------------------------------------
+// roctx ranges around the C-ABI entry points, named after the Janus spans they stand in for
+// ("handle_aggregate_init_generic threadpool task", "VDAF preparation":
+// /root/reference/aggregator/src/aggregator.rs:1786-1790, 2021).  Off unless JANUS_ROCTX=1 at
+// the first call: the roctx library is then dlopen'ed (rocprofv3 --marker-trace shows the ranges
+// beside the kernels); no link-time dependency.
+struct TraceSpan {
+  explicit TraceSpan(const char* name);
+  ~TraceSpan();
+  bool on;
+};
+bool trace_enabled();
+
 // ---- stream pool ---------------------------------------------------------------------------
 hipStream_t ws_stream_get(int device);  // nullptr on failure
 void ws_stream_put(int device, hipStream_t s);

@@ -33,6 +33,8 @@
 #include <vector>
 
 #include "../../include/janus_prio3.h"
+#include <dlfcn.h>
+#include <cstdlib>
 
 namespace {
 
@@ -498,3 +500,39 @@ int exec_accumulate(AccJob* job) {
   if (job->device < 0 || job->device >= MAX_DEVICES) return PRIO3_EINVAL;
   return g_acc[job->device].submit(job);
 }
+
+// ---- tracing -------------------------------------------------------------------------------
+namespace {
+struct Roctx {
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+  bool on = false;
+  Roctx() {
+    const char* v = getenv("JANUS_ROCTX");
+    if (!v || strcmp(v, "1") != 0) return;
+    for (const char* lib : {"librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so",
+                            "libroctx64.so.4", "libroctx64.so"}) {
+      void* h = dlopen(lib, RTLD_NOW | RTLD_LOCAL);
+      if (!h) continue;
+      push = (int (*)(const char*))dlsym(h, "roctxRangePushA");
+      pop = (int (*)())dlsym(h, "roctxRangePop");
+      if (push && pop) {
+        on = true;
+        return;
+      }
+    }
+  }
+};
+Roctx& roctx() {
+  static Roctx r;
+  return r;
+}
+}  // namespace
+
+TraceSpan::TraceSpan(const char* name) : on(roctx().on) {
+  if (on) roctx().push(name);
+}
+TraceSpan::~TraceSpan() {
+  if (on) roctx().pop();
+}
+bool trace_enabled() { return roctx().on; }

@@ -58,6 +58,26 @@ def scan(body: bytes) -> Layout:
     return lay
 
 
+INVALID_MESSAGE = 8  # DAP PrepareError::InvalidMessage
+
+
+def prepare_error(hpke_status, msg_status):
+    """Per-report DAP PrepareError for the response encoder: the HPKE opener's error first, then
+    a public share that does not decode (msg_status 6 -> InvalidMessage, aggregator.rs:1985-1999),
+    else NO_ERROR (the prio3 status decides).  numpy arrays or torch tensors."""
+    try:
+        import torch
+        if isinstance(hpke_status, torch.Tensor):
+            pe = torch.where(msg_status == 6, torch.full_like(hpke_status, INVALID_MESSAGE),
+                             torch.full_like(hpke_status, NO_ERROR))
+            return torch.where(hpke_status != 0, hpke_status, pe)
+    except ImportError:
+        pass
+    hs = np.asarray(hpke_status, np.uint8)
+    pe = np.where(np.asarray(msg_status) == 6, INVALID_MESSAGE, NO_ERROR).astype(np.uint8)
+    return np.where(hs != 0, hs, pe).astype(np.uint8)
+
+
 def ct_stride_for(lay: Layout, slack: int = 0) -> int:
     return max(16, -(-(lay.payload_len + slack) // 16) * 16)
 

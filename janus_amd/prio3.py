@@ -77,7 +77,7 @@ EXPORTED_SYMBOLS = (
     "prio3_accumulate", "prio3_debug_output_shares", "prio3_batch_free", "prio3_device_prepare",
     "prio3_device_accumulate", "prio3_device_output_shares", "prio3_device_combine",
     "prio3_engine_set_option", "prio3_engine_timing", "prio3_engine_timing_reset",
-    "prio3_client_generate_device", "prio3_selftest_field", "prio3_device_prepare_aggregate",
+    "prio3_client_generate_device", "prio3_selftest_field", "prio3_trace_enabled", "prio3_device_prepare_aggregate",
     "prio3_device_aggregate_finish", "prio3_leader_prepare_init_batch",
     "prio3_leader_prepare_next_batch", "prio3_device_leader_prepare_init",
     "prio3_device_leader_prepare_next", "prio3_device_batch_metadata", "prio3_batch_metadata",
@@ -133,6 +133,7 @@ def load_library() -> C.CDLL:
     L.prio3_engine_timing_reset.argtypes = [vp]
     L.prio3_engine_timing_reset.restype = None
     L.prio3_selftest_field.argtypes = [C.c_int, C.c_uint32, vp, vp, vp]
+    L.prio3_trace_enabled.argtypes = []
     L.prio3_device_prepare_aggregate.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, vp, C.c_uint32,
                                                  vp, vp, vp]
     L.prio3_device_aggregate_finish.argtypes = [vp, vp, vp, vp, vp, vp]

@@ -64,9 +64,42 @@ def test_host_scan_and_unpack_match_the_fixture():
         assert out["ct"][0, :6].tobytes() == b"543210" and out["ct_len"][0] == 6
         assert out["ct_len"][1] == 0  # enc of another length than the first record's
         assert out["prep_shares"][0].tobytes() == b"012345"
-        assert out["msg_status"].tolist() == [0, 5]  # Finish where Initialize is due
+        # record 2: a public share of another length than the first record's does not decode
+        # (InvalidMessage, aggregator.rs:1985-1999) -- before its Finish message would matter
+        assert out["msg_status"].tolist() == [0, 6]
     with pytest.raises(ValueError):
         J.scan(bytes.fromhex(FX["agg_init_req_time_interval"]) + b"\0")  # trailing byte
+
+
+def _body(records):
+    return D.encode_agg_init_req(b"", 1, None, [
+        dict(report_id=bytes([i] * 16), time=1000 + i, public_share=ps, config_id=1,
+             enc=b"e" * 32, payload=b"p" * 40, message=msg)
+        for i, (ps, msg) in enumerate(records)])
+
+
+def test_host_unpack_message_and_public_share_errors():
+    """ADVICE r1 (dap_codec host unpack): per-report statuses follow Janus's order -- public
+    share decode (6 -> InvalidMessage) before the ping-pong message (5 PeerMessageMismatch,
+    2 CodecPrepShare); an unknown PingPongMessage type or bad framing rejects the request."""
+    from janus_amd import dap as J
+    init = lambda n: dict(type="initialize", prep_share=b"s" * n)
+    body = _body([(b"P" * 32, init(48)), (b"P" * 31, init(48)), (b"P" * 32, init(47)),
+                  (b"P" * 32, dict(type="continue", prep_msg=b"m", prep_share=b"s" * 48)),
+                  (b"P" * 32, dict(type="finish", prep_msg=b"m" * 16)), (b"", init(48))])
+    lay = J.scan(body)
+    out = J.unpack_host(body, lay, 8, J.ct_stride_for(lay))
+    assert out["msg_status"].tolist() == [0, 6, 2, 5, 5, 6]
+    assert not out["public_shares"][1].any() and out["public_shares"][0].tobytes() == b"P" * 32
+    hs = np.array([0, 0, 0, 0, 4, 4], np.uint8)  # HPKE errors win over the public share's
+    assert J.prepare_error(hs, out["msg_status"]).tolist() == [0xFF, 8, 0xFF, 0xFF, 4, 4]
+    good = bytearray(_body([(b"P" * 32, init(48))]))
+    for mutate in (lambda b: b.__setitem__(len(b) - 53, 3),   # message type 3: not a type
+                   lambda b: b.__setitem__(len(b) - 49, 40)):  # prep_share length 40 of 48 bytes
+        bad = bytearray(good)
+        mutate(bad)
+        with pytest.raises(ValueError):
+            J.unpack_host(bytes(bad), J.scan(bytes(bad)), 8, 64)
 
 
 def test_host_resp_encoder_matches_oracle():

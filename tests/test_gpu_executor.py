@@ -143,3 +143,32 @@ def test_coalescing_off_matches():
     np.testing.assert_array_equal(msgs, rm)
     agg, cnt = batch.accumulate()
     np.testing.assert_array_equal(agg, ra)
+
+
+def test_roctx_ranges_on_request(tmp_path):
+    """JANUS_ROCTX=1: the library loads roctx and wraps its entry points in ranges named after
+    Janus's spans; a prepare + accumulate still gives the oracle's bytes (child process: the
+    switch is read once per process)."""
+    import subprocess
+    import sys
+    code = (
+        "import numpy as np\n"
+        "from janus_amd import prio3 as J\n"
+        "from oracle.oracle import Oracle\n"
+        "assert J.load_library().prio3_trace_enabled() == 1\n"
+        "VK = bytes(range(16))\n"
+        "o = Oracle('histogram', length=256, chunk_length=16)\n"
+        "d = o.gen_reports(VK, 300, seed=3, n_threads=4)\n"
+        "m, s, a, c = o.helper_batch(VK, d['nonces'], d['public_shares'], d['helper_shares'],\n"
+        "                            d['leader_prep_shares'], n_threads=4)\n"
+        "e = J.HelperEngine(J.Prio3Histogram(256, 16), VK)\n"
+        "gm, gs, b = e.prepare_batch(d['nonces'], d['public_shares'], d['helper_shares'],\n"
+        "                            d['leader_prep_shares'])\n"
+        "ga, gc = b.accumulate()\n"
+        "assert (gm == m).all() and (gs == s).all() and (ga == a).all()\n"
+        "print('ok')\n")
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True,
+                       env=dict(os.environ, JANUS_ROCTX="1", PYTHONPATH=root), timeout=240)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr

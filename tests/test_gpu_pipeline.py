@@ -101,7 +101,7 @@ def test_device_helper_init_request_to_response(n):
     agg = torch.zeros((1, eng.sz.agg_share_len), dtype=torch.uint8, device=dev)
     cnt = torch.zeros(1, dtype=torch.int64, device=dev)
     eng.aggregate_finish_device(st, accept, agg, cnt)
-    pe = torch.where(hs == 0, torch.full_like(hs, 0xFF), hs)
+    pe = DJ.prepare_error(hs, u["msg_status"])
     out, ln = DJ.encode_resp_device(u["report_ids"], pe, st | u["msg_status"], msgs, 16)
     torch.cuda.synchronize()
     assert int(mism[0]) == 0
