@@ -776,8 +776,9 @@ def mp64_main(args):
     """Prio3SumVecField64MultiproofHmacSha256Aes128 helper prepare+aggregate line (not the
     BASELINE metric) at the reference's own end-to-end configuration
     (proofs 2, bits 16, length 15, chunk 16: integration_tests janus.rs:387-392).  Reports come
-    from the Python restatement (distinct ones tiled); no compiled CPU restatement of this VDAF
-    exists here, so no cpu_baseline is reported."""
+    from the Python restatement (distinct ones tiled).  cpu_baseline: the compiled C restatement
+    (oracle/prio3_oracle.c ORC_SUMVEC_F64_MP, OpenSSL SHA-256 / AES-128) in 500-report jobs on
+    every host thread, on a bounded sample of the same reports, cross-checking the GPU there."""
     import multiprocessing as mp_
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
@@ -832,6 +833,38 @@ def mp64_main(args):
                         for k, v in times.items()},
                checks=dict(finished=int((status == 0).sum().item()), agg_count=int(cnt[0])),
                cpu_baseline=None)
+    if not args.no_cpu_baseline:
+        from oracle.oracle import Oracle, build
+        build()
+        o = Oracle("sumvec_f64_mp", bits=cfg[1], length=cfg[2], chunk_length=cfg[3],
+                   num_proofs=cfg[0])
+        th = cpu_threads()
+        host = [t.cpu().numpy() for t in (nonces, pub, helper, lps)]
+
+        def crun(m):
+            t1 = time.perf_counter()
+            r = o.helper_batch(vk, *(h[:m] for h in host), n_threads=th, job_size=500)
+            return time.perf_counter() - t1, r
+
+        probe = min(n, 500 * th)
+        dt, _ = crun(probe)
+        m = int(min(n, max(probe, probe * args.cpu_seconds / max(dt, 1e-6))))
+        dt, (cm, cs, cagg, ccnt) = crun(m)
+        out["cpu_baseline"] = dict(value=m / dt, unit="reports/s", cores=th, kind="port",
+                                   sample=f"{m} of the same reports through the C restatement "
+                                          f"(oracle/prio3_oracle.c ORC_SUMVEC_F64_MP), jobs of "
+                                          f"500, {th} threads, {dt:.1f}s wall")
+        out["speedup_vs_cpu"] = value / out["cpu_baseline"]["value"]
+        accept = torch.zeros(n, dtype=torch.uint8, device=dev)
+        accept[:m] = 1
+        agg_s = torch.zeros_like(agg)
+        cnt_s = torch.zeros_like(cnt)
+        eng.aggregate_finish_device(status, accept, agg_s, cnt_s)
+        torch.cuda.synchronize()
+        out["checks"]["cpu_gpu_parity_on_sample"] = bool(
+            np.array_equal(status[:m].cpu().numpy(), cs) and
+            np.array_equal(msgs[:m].cpu().numpy(), cm) and
+            np.array_equal(agg_s.cpu().numpy(), cagg) and int(cnt_s[0].item()) == int(ccnt[0]))
     print(json.dumps(out), flush=True)
 
 def fpvec_main(args):
@@ -841,7 +874,8 @@ def fpvec_main(args):
     tests/golden/gen_fpvec_l10000.py; ~35 s of CPU per report to generate) tiled to --reports
     (default here 100k) and resident in HBM.  One step = prepare (k_xof, k_xof_slow, k_query_fp
     per scratch sub-batch) + masked mod-p accumulate of the 10000-entry output shares.
-    cpu_baseline: the same restatement (pure Python, one core) on one report."""
+    cpu_baseline: the compiled C restatement (oracle/prio3_oracle.c ORC_FPVEC) on a bounded
+    sample of the same reports, every host thread; it also cross-checks the GPU on the sample."""
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
     g = np.load(os.path.join(ROOT, "tests", "golden", "fpvec_l10000.npz"))
@@ -891,17 +925,38 @@ def fpvec_main(args):
         ok_agg &= int.from_bytes(a[16 * e:16 * e + 16], "little") == want
     cpu = None
     if not args.no_cpu_baseline:
-        from oracle import prio3_py as P
-        from oracle.fpvec_py import FpVecType
-        v = P.Prio3(FpVecType(10000, 16))
-        k = int(honest[0])
-        t1 = time.perf_counter()
-        st1, hps, _ = v.prepare_init(vk, 1, bytes(g["nonce"][k]), bytes(g["pub"][k]),
-                                     bytes(g["helper"][k]))
-        v.prepare_next(st1, v.prep_shares_to_prep_msg(bytes(g["lps"][k]), hps))
-        dt = time.perf_counter() - t1
-        cpu = dict(value=1 / dt, unit="reports/s", cores=1, kind="port",
-                   sample=f"1 report through oracle/fpvec_py.py (pure Python, one core), {dt:.1f}s")
+        # the compiled C restatement (oracle/prio3_oracle.c ORC_FPVEC, pinned to the Python one
+        # and to the fixtures by tests/test_fpvec.py) in 500-report jobs on every host thread,
+        # on a bounded sample of the same reports; cross-checks the GPU on that sample
+        from oracle.oracle import Oracle, build
+        build()
+        o = Oracle("fpvec", bits=16, length=10000)
+        th = cpu_threads()
+        hostd = {k: g[k][idx] for k in ("nonce", "pub", "helper", "lps")}
+
+        def crun(m):
+            t1 = time.perf_counter()
+            r = o.helper_batch(vk, hostd["nonce"][:m], hostd["pub"][:m], hostd["helper"][:m],
+                               hostd["lps"][:m], n_threads=th, job_size=500)
+            return time.perf_counter() - t1, r
+
+        probe = min(n, 2 * th)
+        dt, _ = crun(probe)
+        m = int(min(n, max(probe, probe * args.cpu_seconds / max(dt, 1e-6))))
+        dt, (cm, cs, cagg, ccnt) = crun(m)
+        cpu = dict(value=m / dt, unit="reports/s", cores=th, kind="port",
+                   sample=f"{m} of the tiled fixture reports through the C restatement "
+                          f"(oracle/prio3_oracle.c, ORC_FPVEC), {th} threads, {dt:.1f}s wall")
+        accept = torch.zeros(n, dtype=torch.uint8, device=dev)
+        accept[:m] = 1
+        agg_s = torch.zeros_like(agg)
+        cnt_s = torch.zeros_like(cnt)
+        eng.accumulate_device(n, status, seg, accept, 1, agg_s, cnt_s)
+        torch.cuda.synchronize()
+        cpu_parity = bool(np.array_equal(status[:m].cpu().numpy(), cs) and
+                          np.array_equal(msgs[:m].cpu().numpy(), cm) and
+                          np.array_equal(agg_s.cpu().numpy(), cagg) and
+                          int(cnt_s[0].item()) == int(ccnt[0]))
     kern = {k: dict(ms_total=v[0], launches=v[1], ms_avg=v[0] / max(v[1], 1))
             for k, v in times.items()}
     value = n * args.steps / elapsed
@@ -916,7 +971,8 @@ def fpvec_main(args):
                            reports=n),
                kernels=kern,
                checks=dict(finished=int((status == 0).sum().item()), agg_count=int(cnt[0]),
-                           prep_msgs_match=ok_msgs, agg_sample_match=bool(ok_agg)),
+                           prep_msgs_match=ok_msgs, agg_sample_match=bool(ok_agg),
+                           cpu_gpu_parity_on_sample=cpu_parity if cpu else None),
                cpu_baseline=cpu,
                speedup_vs_cpu=(value / cpu["value"]) if cpu else None)
     print(json.dumps(out), flush=True)

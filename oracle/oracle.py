@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "libprio3_oracle.so")
 
-KINDS = {"count": 0, "sum": 1, "sumvec": 2, "histogram": 3}
+KINDS = {"count": 0, "sum": 1, "sumvec": 2, "histogram": 3, "fpvec": 4, "sumvec_f64_mp": 5}
 
 
 class OrcParams(C.Structure):
@@ -24,7 +24,7 @@ class OrcParams(C.Structure):
         "field_bits", "es", "meas_len", "out_len", "jr_len", "qr_len", "prove_rand_len",
         "arity", "degree", "calls", "wire_len", "proof_len", "verifier_len",
         "helper_share_len", "public_share_len", "leader_share_len", "prep_share_len",
-        "prep_msg_len", "out_share_bytes"]]
+        "prep_msg_len", "out_share_bytes", "fp_C1", "fp_K1", "fp_P1", "seed_size", "xof_hm"]]
 
 
 def build(force: bool = False) -> str:

@@ -12,6 +12,7 @@
  */
 #include "prio3_oracle.h"
 
+#include <openssl/evp.h>
 #include <pthread.h>
 #include <stdatomic.h>
 #include <stdlib.h>
@@ -131,13 +132,95 @@ void orc_shake128(const uint8_t* msg, size_t len, uint8_t* out, size_t out_len) 
 }
 
 /* XofTurboShake128(seed, dst, binder) = TurboSHAKE128(len(dst) || dst || seed || binder, D=1)
- * [VDAF-08 §6.2.1; prio vdaf/xof.rs XofTurboShake128::init]. */
-static void xof_init(sponge* t, const uint8_t seed[16], const uint8_t* dst, size_t dst_len) {
-  sp_init(t, 12);
-  uint8_t l = (uint8_t)dst_len;
-  sp_absorb(t, &l, 1);
-  sp_absorb(t, dst, dst_len);
-  sp_absorb(t, seed, 16);
+ * [VDAF-08 §6.2.1; prio vdaf/xof.rs XofTurboShake128::init], and XofHmacSha256Aes128 (prio 0.16,
+ * SEED_SIZE 32; restated in oracle/prio3_py.py): tag = HMAC-SHA256(seed, len(dst) || dst ||
+ * binder), then an AES-128 keystream, key tag[0:16], IV tag[16:32] with a 64-bit big-endian
+ * counter in its low half (Ctr64BE). */
+typedef struct {
+  int hm;
+  sponge sp;
+  EVP_MD_CTX* md;
+  uint8_t okey[64];
+  EVP_CIPHER_CTX* aes;
+  uint8_t iv[16], ks[16];
+  uint64_t ctr;
+  uint32_t kpos;
+} xof_t;
+static void xf_init(xof_t* x, int hm, const uint8_t* seed, size_t seed_len, const uint8_t* dst,
+                    size_t dst_len) {
+  const uint8_t l = (uint8_t)dst_len;
+  x->hm = hm;
+  x->md = NULL;
+  x->aes = NULL;
+  if (!hm) {
+    sp_init(&x->sp, 12);
+    sp_absorb(&x->sp, &l, 1);
+    sp_absorb(&x->sp, dst, dst_len);
+    sp_absorb(&x->sp, seed, seed_len);
+    return;
+  }
+  uint8_t ikey[64];
+  memset(ikey, 0x36, 64);
+  memset(x->okey, 0x5c, 64);
+  for (size_t i = 0; i < seed_len; i++) {  /* seed_len <= 64: the key is used as is */
+    ikey[i] ^= seed[i];
+    x->okey[i] ^= seed[i];
+  }
+  x->md = EVP_MD_CTX_new();
+  EVP_DigestInit_ex(x->md, EVP_sha256(), NULL);
+  EVP_DigestUpdate(x->md, ikey, 64);
+  EVP_DigestUpdate(x->md, &l, 1);
+  EVP_DigestUpdate(x->md, dst, dst_len);
+}
+static void xf_absorb(xof_t* x, const uint8_t* d, size_t n) {
+  if (x->hm)
+    EVP_DigestUpdate(x->md, d, n);
+  else
+    sp_absorb(&x->sp, d, n);
+}
+static void xf_finalize(xof_t* x) {
+  if (!x->hm) {
+    sp_finalize(&x->sp, 1);
+    return;
+  }
+  uint8_t inner[32], tag[32];
+  unsigned int len = 0;
+  EVP_DigestFinal_ex(x->md, inner, &len);
+  EVP_DigestInit_ex(x->md, EVP_sha256(), NULL);
+  EVP_DigestUpdate(x->md, x->okey, 64);
+  EVP_DigestUpdate(x->md, inner, 32);
+  EVP_DigestFinal_ex(x->md, tag, &len);
+  x->aes = EVP_CIPHER_CTX_new();
+  EVP_EncryptInit_ex(x->aes, EVP_aes_128_ecb(), NULL, tag, NULL);
+  EVP_CIPHER_CTX_set_padding(x->aes, 0);
+  memcpy(x->iv, tag + 16, 16);
+  x->ctr = 0;
+  for (int i = 0; i < 8; i++) x->ctr = x->ctr << 8 | x->iv[8 + i];
+  x->kpos = 16;
+}
+static void xf_squeeze(xof_t* x, uint8_t* out, size_t n) {
+  if (!x->hm) {
+    sp_squeeze(&x->sp, out, n);
+    return;
+  }
+  while (n--) {
+    if (x->kpos == 16) {
+      uint8_t blk[16];
+      int l = 0;
+      memcpy(blk, x->iv, 8);
+      for (int i = 0; i < 8; i++) blk[8 + i] = (uint8_t)(x->ctr >> (56 - 8 * i));
+      x->ctr++;
+      EVP_EncryptUpdate(x->aes, x->ks, &l, blk, 16);
+      x->kpos = 0;
+    }
+    *out++ = x->ks[x->kpos++];
+  }
+}
+static void xf_free(xof_t* x) {
+  if (x->md) EVP_MD_CTX_free(x->md);
+  if (x->aes) EVP_CIPHER_CTX_free(x->aes);
+  x->md = NULL;
+  x->aes = NULL;
 }
 
 /* ------------------------------------------------------------------------------------ */
@@ -273,11 +356,11 @@ static int dec_fe(const fld* F, const uint8_t* in, fe* x) {
 }
 
 /* Xof.expand_into_vec with rejection sampling [VDAF-08 §6.2; prio Prng::get]. */
-static void xof_expand(const fld* F, sponge* t, fe* out, uint32_t n) {
+static void xof_expand(const fld* F, xof_t* t, fe* out, uint32_t n) {
   int es = F->is128 ? 16 : 8;
   uint8_t buf[16];
   for (uint32_t i = 0; i < n;) {
-    sp_squeeze(t, buf, es);
+    xf_squeeze(t, buf, es);
     u128 v = 0;
     for (int k = es - 1; k >= 0; k--) v = (v << 8) | buf[k];
     if (v < F->p) out[i++] = v;
@@ -346,6 +429,23 @@ static uint32_t next_pow2(uint32_t n) {
   return p;
 }
 
+/* prio flp/gadgets.rs optimal_chunk_length (restated as in oracle/fpvec_py.py): the chunk length
+ * minimising 2 chunk + 2 ((1 + calls).next_power_of_two() - 1) + 1 over calls = 2^k - 1, the
+ * first minimum from the largest k down */
+static uint32_t optimal_chunk_length(uint32_t meas_len) {
+  if (meas_len <= 1) return 1;
+  uint32_t max_log2 = log2u(next_pow2(meas_len)) + 1, best_cost = 0, best = 1;
+  for (uint32_t l2 = max_log2; l2 >= 1; l2--) {
+    const uint32_t calls = (1u << l2) - 1, chunk = (meas_len + calls - 1) / calls;
+    const uint32_t cost = 2 * chunk + 2 * (next_pow2(1 + calls) - 1) + 1;
+    if (l2 == max_log2 || cost < best_cost) {
+      best_cost = cost;
+      best = chunk;
+    }
+  }
+  return best;
+}
+
 int orc_params_init(orc_params* p, int type, uint32_t bits, uint32_t length,
                     uint32_t chunk_length, uint32_t num_proofs) {
   memset(p, 0, sizeof *p);
@@ -355,6 +455,7 @@ int orc_params_init(orc_params* p, int type, uint32_t bits, uint32_t length,
   p->chunk_length = chunk_length;
   p->num_proofs = num_proofs ? num_proofs : 1;
   if (p->num_proofs > 255) return -1;
+  p->seed_size = 16;
   p->qr_len = 1;
   p->degree = 2;
   switch (type) {
@@ -397,6 +498,35 @@ int orc_params_init(orc_params* p, int type, uint32_t bits, uint32_t length,
       p->arity = 2 * chunk_length;
       p->calls = (length + chunk_length - 1) / chunk_length;
       break;
+    case ORC_SUMVEC_F64_MP: /* SumVec<Field64, ParallelSum<Mul>>, XofHmacSha256Aes128,
+                               algorithm id 0xFFFF1003 (core/src/vdaf.rs:20, 173-195) */
+      if (bits == 0 || bits > 64 || length == 0 || chunk_length == 0 || p->num_proofs < 2)
+        return -1;
+      p->algorithm_id = 0xFFFF1003u;
+      p->field_bits = 64;
+      p->meas_len = bits * length;
+      p->out_len = length;
+      p->jr_len = 1;
+      p->arity = 2 * chunk_length;
+      p->calls = (p->meas_len + chunk_length - 1) / chunk_length;
+      p->seed_size = 32;
+      p->xof_hm = 1;
+      break;
+    case ORC_FPVEC: /* FixedPointBoundedL2VecSum (reconstruction, oracle/fpvec_py.py) */
+      if ((bits != 16 && bits != 32) || length == 0 || p->num_proofs != 1) return -1;
+      p->algorithm_id = 0xFFFF0000u;
+      p->field_bits = 128;
+      p->meas_len = bits * length + 2 * bits - 2;
+      p->out_len = length;
+      p->jr_len = 2;
+      p->qr_len = 2;
+      p->chunk_length = optimal_chunk_length(p->meas_len);
+      p->arity = 2 * p->chunk_length;
+      p->calls = (p->meas_len + p->chunk_length - 1) / p->chunk_length;
+      p->fp_C1 = optimal_chunk_length(length);
+      p->fp_K1 = (length + p->fp_C1 - 1) / p->fp_C1;
+      p->fp_P1 = next_pow2(1 + p->fp_K1);
+      break;
     default:
       return -1;
   }
@@ -405,12 +535,19 @@ int orc_params_init(orc_params* p, int type, uint32_t bits, uint32_t length,
   p->wire_len = next_pow2(1 + p->calls);
   p->proof_len = p->arity + p->degree * (p->wire_len - 1) + 1;
   p->verifier_len = 1 + p->arity + 1;
-  p->helper_share_len = 16 * (p->jr_len ? 3 : 2);
-  p->public_share_len = p->jr_len ? 32 : 0;
+  if (type == ORC_FPVEC) {  /* proof = seeds0 | coeffs0 | seeds1 | coeffs1 */
+    p->prove_rand_len = p->arity + p->fp_C1;
+    p->proof_len += p->fp_C1 + 2 * (p->fp_P1 - 1) + 1;
+    p->verifier_len += p->fp_C1 + 1;
+  }
+  const uint32_t S = p->seed_size;
+  if (p->jr_len * p->num_proofs > 64 || p->qr_len * p->num_proofs > 64) return -1;
+  p->helper_share_len = S * (p->jr_len ? 3 : 2);
+  p->public_share_len = p->jr_len ? 2 * S : 0;
   p->leader_share_len =
-      (p->meas_len + p->proof_len * p->num_proofs) * p->es + (p->jr_len ? 16 : 0);
-  p->prep_share_len = p->verifier_len * p->num_proofs * p->es + (p->jr_len ? 16 : 0);
-  p->prep_msg_len = p->jr_len ? 16 : 0;
+      (p->meas_len + p->proof_len * p->num_proofs) * p->es + (p->jr_len ? S : 0);
+  p->prep_share_len = p->verifier_len * p->num_proofs * p->es + (p->jr_len ? S : 0);
+  p->prep_msg_len = p->jr_len ? S : 0;
   p->out_share_bytes = p->out_len * p->es;
   return 0;
 }
@@ -443,10 +580,10 @@ enum {
   U_JOINT_RAND_PART = 7
 };
 
-static void xof_for(const orc_params* p, sponge* t, const uint8_t seed[16], uint16_t usage) {
+static void xof_for(const orc_params* p, xof_t* t, const uint8_t* seed, uint16_t usage) {
   uint8_t dst[8];
   mkdst(p, usage, dst);
-  xof_init(t, seed, dst, 8);
+  xf_init(t, (int)p->xof_hm, seed, p->seed_size, dst, 8);
 }
 
 /* ------------------------------------------------------------------------------------ */
@@ -520,7 +657,8 @@ static fe valid(shim* s, const fe* in, const fe* jr, uint32_t num_shares) {
       }
       return out;
     }
-    case ORC_SUMVEC: {
+    case ORC_SUMVEC:
+    case ORC_SUMVEC_F64_MP: {
       fe* args = (fe*)malloc(sizeof(fe) * p->arity);
       fe out = range_checks(s, in, p->meas_len, jr[0], shares_inv, args);
       free(args);
@@ -577,6 +715,102 @@ static int flp_decide(const fld* F, const orc_params* p, const fe* v) {
   return gadget_eval(F, p, v + 1) == v[1 + p->arity];
 }
 
+/* FixedPointBoundedL2VecSum query (oracle/fpvec_py.py FpVecType.query, the two-gadget FLP):
+ * verifier = [v, f0(t0) (A0 wires), p0(t0), f1(t1) (C1 wires), p1(t1)]. */
+static int fpvec_query(const fld* F, const orc_params* p, const fe* meas, const fe* proof,
+                       const fe* qr, const fe* jr, fe* ver) {
+  const uint32_t A0 = p->arity, C0 = p->chunk_length, K0 = p->calls, P0 = p->wire_len;
+  const uint32_t C1 = p->fp_C1, K1 = p->fp_K1, P1 = p->fp_P1, n = p->bits, E = p->length;
+  const uint32_t G0 = 2 * (P0 - 1) + 1, G1 = 2 * (P1 - 1) + 1, M = p->meas_len;
+  const fe *s0 = proof, *c0 = s0 + A0, *s1 = c0 + G0, *c1 = s1 + C1;
+  const fe t0 = qr[0], t1 = qr[1];
+  if (f_pow(F, t0, P0) == 1 || f_pow(F, t1, P1) == 1) return -1;
+  /* gadget polynomials at the P-th roots: coefficients folded mod x^P - 1, one DFT */
+  fe* fold = (fe*)calloc(P0 > P1 ? P0 : P1, sizeof(fe));
+  fe* pr0 = (fe*)malloc(sizeof(fe) * P0);
+  fe* pr1 = (fe*)malloc(sizeof(fe) * P1);
+  for (uint32_t i = 0; i < G0; i++) fold[i % P0] = f_add(F, fold[i % P0], c0[i]);
+  dft(F, pr0, fold, P0, P0);
+  memset(fold, 0, sizeof(fe) * (P0 > P1 ? P0 : P1));
+  for (uint32_t i = 0; i < G1; i++) fold[i % P1] = f_add(F, fold[i % P1], c1[i]);
+  dft(F, pr1, fold, P1, P1);
+  /* valid(): wire values of each call recorded (row 0 = the proof's seeds) */
+  fe* w0 = (fe*)calloc((size_t)A0 * (K0 + 1), sizeof(fe));
+  fe* w1 = (fe*)calloc((size_t)C1 * (K1 + 1), sizeof(fe));
+  for (uint32_t w = 0; w < A0; w++) w0[(size_t)w * (K0 + 1)] = s0[w];
+  for (uint32_t w = 0; w < C1; w++) w1[(size_t)w * (K1 + 1)] = s1[w];
+  const fe sinv = f_inv(F, 2);
+  fe rng = 0, rp = jr[0];
+  for (uint32_t k = 0; k < K0; k++) {
+    for (uint32_t j = 0; j < C0; j++) {
+      const uint32_t i = k * C0 + j;
+      const fe m = i < M ? meas[i] : 0;
+      w0[(size_t)(2 * j) * (K0 + 1) + k + 1] = f_mul(F, rp, m);
+      w0[(size_t)(2 * j + 1) * (K0 + 1) + k + 1] = f_sub(F, m, sinv);
+      rp = f_mul(F, rp, jr[0]);
+    }
+    rng = f_add(F, rng, pr0[k + 1]);
+  }
+  fe norm = 0;
+  for (uint32_t k = 0; k < K1; k++) {
+    for (uint32_t j = 0; j < C1; j++) {
+      const uint32_t e = k * C1 + j;
+      fe y = 0;
+      if (e < E)
+        for (uint32_t b = n; b-- > 0;) y = f_add(F, f_add(F, y, y), meas[n * e + b]);
+      w1[(size_t)j * (K1 + 1) + k + 1] = y;
+    }
+    norm = f_add(F, norm, pr1[k + 1]);
+  }
+  norm = f_add(F, norm, f_mul(F, f_mul(F, (fe)E, (fe)1 << (2 * n - 2)), sinv));
+  fe claimed = 0;
+  for (uint32_t b = 2 * n - 2; b-- > 0;) claimed = f_add(F, f_add(F, claimed, claimed), meas[n * E + b]);
+  ver[0] = f_add(F, f_mul(F, jr[1], rng),
+                 f_mul(F, f_mul(F, jr[1], jr[1]), f_sub(F, norm, claimed)));
+  /* wire polynomials at t: sum_c L_c(t) w[c], L_c(t) = alpha^c (t^P - 1) / (P (t - alpha^c)) */
+  for (int g = 0; g < 2; g++) {
+    const uint32_t P = g ? P1 : P0, K = g ? K1 : K0, A = g ? C1 : A0;
+    const fe t = g ? t1 : t0;
+    const fe* w = g ? w1 : w0;
+    fe* L = (fe*)malloc(sizeof(fe) * (K + 1));
+    const fe num = f_mul(F, f_sub(F, f_pow(F, t, P), 1), f_inv(F, P)), a = f_root(F, (int)log2u(P));
+    fe ac = 1;
+    for (uint32_t c = 0; c <= K; c++) {
+      L[c] = f_mul(F, f_mul(F, ac, f_inv(F, f_sub(F, t, ac))), num);
+      ac = f_mul(F, ac, a);
+    }
+    fe* out = ver + (g ? 2 + A0 : 1);
+    for (uint32_t x = 0; x < A; x++) {
+      fe acc = 0;
+      for (uint32_t c = 0; c <= K; c++) acc = f_add(F, acc, f_mul(F, L[c], w[(size_t)x * (K + 1) + c]));
+      out[x] = acc;
+    }
+    free(L);
+  }
+  ver[1 + A0] = poly_eval(F, c0, G0, t0);
+  ver[2 + A0 + C1] = poly_eval(F, c1, G1, t1);
+  free(fold);
+  free(pr0);
+  free(pr1);
+  free(w0);
+  free(w1);
+  return 0;
+}
+
+static int fpvec_decide(const fld* F, const orc_params* p, const fe* v) {
+  if (v[0] != 0) return 0;
+  const uint32_t A0 = p->arity, C1 = p->fp_C1;
+  fe g0 = 0, g1 = 0;
+  for (uint32_t j = 0; j < p->chunk_length; j++)
+    g0 = f_add(F, g0, f_mul(F, v[1 + 2 * j], v[2 + 2 * j]));
+  const fe twon = (fe)1 << p->bits;
+  for (uint32_t j = 0; j < C1; j++) {
+    const fe y = v[2 + A0 + j];
+    g1 = f_add(F, g1, f_sub(F, f_mul(F, y, y), f_mul(F, twon, y)));
+  }
+  return g0 == v[1 + A0] && g1 == v[2 + A0 + C1];
+}
+
 /* FlpGeneric::prove (client side; used only to synthesise honest reports). */
 static void flp_prove(const fld* F, const orc_params* p, const fe* meas, const fe* prove_rand,
                       const fe* jr, fe* proof) {
@@ -622,58 +856,67 @@ static void flp_prove(const fld* F, const orc_params* p, const fe* meas, const f
 /* ------------------------------------------------------------------------------------ */
 /* Prio3 [VDAF-08 §7.2]                                                                  */
 /* ------------------------------------------------------------------------------------ */
-static void expand_seed(const orc_params* p, const fld* F, const uint8_t seed[16], uint16_t usage,
+static void expand_seed(const orc_params* p, const fld* F, const uint8_t* seed, uint16_t usage,
                         const uint8_t* binder, size_t blen, fe* out, uint32_t n) {
-  sponge t;
+  xof_t t;
   xof_for(p, &t, seed, usage);
-  sp_absorb(&t, binder, blen);
-  sp_finalize(&t, 1);
+  xf_absorb(&t, binder, blen);
+  xf_finalize(&t);
   xof_expand(F, &t, out, n);
+  xf_free(&t);
 }
-static void derive_seed(const orc_params* p, const uint8_t seed[16], uint16_t usage,
-                        const uint8_t* binder, size_t blen, uint8_t out[16]) {
-  sponge t;
+static void derive_seed(const orc_params* p, const uint8_t* seed, uint16_t usage,
+                        const uint8_t* binder, size_t blen, uint8_t* out) {
+  xof_t t;
   xof_for(p, &t, seed, usage);
-  sp_absorb(&t, binder, blen);
-  sp_finalize(&t, 1);
-  sp_squeeze(&t, out, 16);
+  xf_absorb(&t, binder, blen);
+  xf_finalize(&t);
+  xf_squeeze(&t, out, p->seed_size);
+  xf_free(&t);
 }
-static void helper_meas_share(const orc_params* p, const fld* F, const uint8_t k[16], uint8_t agg,
+static void helper_meas_share(const orc_params* p, const fld* F, const uint8_t* k, uint8_t agg,
                               fe* out) {
   expand_seed(p, F, k, U_MEAS_SHARE, &agg, 1, out, p->meas_len);
 }
-static void helper_proofs_share(const orc_params* p, const fld* F, const uint8_t k[16],
+static void helper_proofs_share(const orc_params* p, const fld* F, const uint8_t* k,
                                 uint8_t agg, fe* out) {
   uint8_t b[2] = {(uint8_t)p->num_proofs, agg};
   expand_seed(p, F, k, U_PROOF_SHARE, b, 2, out, p->proof_len * p->num_proofs);
 }
-static void joint_rand_part(const orc_params* p, const fld* F, const uint8_t blind[16], uint8_t agg,
-                            const uint8_t nonce[16], const fe* meas, uint8_t out[16]) {
-  sponge t;
+static void joint_rand_part(const orc_params* p, const fld* F, const uint8_t* blind, uint8_t agg,
+                            const uint8_t nonce[16], const fe* meas, uint8_t* out) {
+  xof_t t;
   xof_for(p, &t, blind, U_JOINT_RAND_PART);
-  sp_absorb(&t, &agg, 1);
-  sp_absorb(&t, nonce, 16);
-  uint8_t buf[16];
-  for (uint32_t i = 0; i < p->meas_len; i++) {
-    enc_fe(F, meas[i], buf);
-    sp_absorb(&t, buf, p->es);
+  xf_absorb(&t, &agg, 1);
+  xf_absorb(&t, nonce, 16);
+  uint8_t buf[16 * 64];
+  uint32_t nb = 0;
+  for (uint32_t i = 0; i < p->meas_len; i++) {  /* absorbed 64 elements at a time */
+    enc_fe(F, meas[i], buf + nb * p->es);
+    if (++nb == 64) {
+      xf_absorb(&t, buf, nb * p->es);
+      nb = 0;
+    }
   }
-  sp_finalize(&t, 1);
-  sp_squeeze(&t, out, 16);
+  xf_absorb(&t, buf, nb * p->es);
+  xf_finalize(&t);
+  xf_squeeze(&t, out, p->seed_size);
+  xf_free(&t);
 }
-static void joint_rand_seed(const orc_params* p, const uint8_t part0[16], const uint8_t part1[16],
-                            uint8_t out[16]) {
-  static const uint8_t zero[16] = {0};
-  uint8_t b[32];
-  memcpy(b, part0, 16);
-  memcpy(b + 16, part1, 16);
-  derive_seed(p, zero, U_JOINT_RAND_SEED, b, 32, out);
+static void joint_rand_seed(const orc_params* p, const uint8_t* part0, const uint8_t* part1,
+                            uint8_t* out) {
+  static const uint8_t zero[32] = {0};
+  uint8_t b[64];
+  const uint32_t S = p->seed_size;
+  memcpy(b, part0, S);
+  memcpy(b + S, part1, S);
+  derive_seed(p, zero, U_JOINT_RAND_SEED, b, 2 * S, out);
 }
-static void joint_rands(const orc_params* p, const fld* F, const uint8_t seed[16], fe* out) {
+static void joint_rands(const orc_params* p, const fld* F, const uint8_t* seed, fe* out) {
   uint8_t b = (uint8_t)p->num_proofs;
   expand_seed(p, F, seed, U_JOINT_RANDOMNESS, &b, 1, out, p->jr_len * p->num_proofs);
 }
-static void query_rands(const orc_params* p, const fld* F, const uint8_t vk[16],
+static void query_rands(const orc_params* p, const fld* F, const uint8_t* vk,
                         const uint8_t nonce[16], fe* out) {
   uint8_t b[17];
   b[0] = (uint8_t)p->num_proofs;
@@ -722,6 +965,8 @@ static void truncate_share(const orc_params* p, const fld* F, const fe* meas, fe
       return;
     }
     case ORC_SUMVEC:
+    case ORC_SUMVEC_F64_MP:
+    case ORC_FPVEC: /* FPVec: the decoded entries (the claimed-norm bits are not output) */
       for (uint32_t e = 0; e < p->length; e++) {
         fe acc = 0, pw = 1;
         for (uint32_t b = 0; b < p->bits; b++) {
@@ -737,6 +982,7 @@ static void truncate_share(const orc_params* p, const fld* F, const fe* meas, fe
 int orc_shard(const orc_params* p, const uint64_t* meas, const uint8_t nonce[16],
               const uint8_t* rand, uint8_t* public_share, uint8_t* leader_share,
               uint8_t* helper_share) {
+  if (p->seed_size != 16 || p->type == ORC_FPVEC) return -1; /* client side: TurboSHAKE types */
   fld F = mkfld(p);
   uint32_t np = p->num_proofs;
   fe* enc = (fe*)malloc(sizeof(fe) * p->meas_len);
@@ -792,10 +1038,11 @@ out:
 }
 
 /* Core of prepare_init; optionally exports intermediates. */
-static int prepare_init_core(const orc_params* p, const fld* F, const uint8_t vk[16], int agg_id,
+static int prepare_init_core(const orc_params* p, const fld* F, const uint8_t* vk, int agg_id,
                              const uint8_t nonce[16], const uint8_t* public_share,
-                             const uint8_t* input_share, fe* meas, fe* proofs, uint8_t part[16],
-                             uint8_t corrected[16], fe* jr, fe* qr, fe* verifiers) {
+                             const uint8_t* input_share, fe* meas, fe* proofs, uint8_t* part,
+                             uint8_t* corrected, fe* jr, fe* qr, fe* verifiers) {
+  const uint32_t S = p->seed_size;
   uint32_t np = p->num_proofs;
   if (agg_id == 0) {
     const uint8_t* in = input_share;
@@ -805,28 +1052,29 @@ static int prepare_init_core(const orc_params* p, const fld* F, const uint8_t vk
       if (dec_fe(F, in, &proofs[i])) return ORC_ERR_PREP_INIT;
   } else {
     helper_meas_share(p, F, input_share, (uint8_t)agg_id, meas);
-    helper_proofs_share(p, F, input_share + 16, (uint8_t)agg_id, proofs);
+    helper_proofs_share(p, F, input_share + S, (uint8_t)agg_id, proofs);
   }
   if (p->jr_len) {
     const uint8_t* blind = agg_id == 0
                                ? input_share + (p->meas_len + p->proof_len * np) * p->es
-                               : input_share + 32;
+                               : input_share + 2 * S;
     joint_rand_part(p, F, blind, (uint8_t)agg_id, nonce, meas, part);
     if (agg_id == 0)
-      joint_rand_seed(p, part, public_share + 16, corrected);
+      joint_rand_seed(p, part, public_share + S, corrected);
     else
       joint_rand_seed(p, public_share, part, corrected);
     joint_rands(p, F, corrected, jr);
   }
   query_rands(p, F, vk, nonce, qr);
   for (uint32_t k = 0; k < np; k++)
-    if (flp_query(F, p, meas, proofs + k * p->proof_len, qr + k * p->qr_len, jr + k * p->jr_len,
-                  verifiers + k * p->verifier_len))
+    if ((p->type == ORC_FPVEC ? fpvec_query : flp_query)(
+            F, p, meas, proofs + k * p->proof_len, qr + k * p->qr_len, jr + k * p->jr_len,
+            verifiers + k * p->verifier_len))
       return ORC_ERR_PREP_INIT;
   return ORC_OK;
 }
 
-int orc_prepare_init(const orc_params* p, const uint8_t vk[16], int agg_id,
+int orc_prepare_init(const orc_params* p, const uint8_t* vk, int agg_id,
                      const uint8_t nonce[16], const uint8_t* public_share,
                      const uint8_t* input_share, uint8_t* state_out, uint8_t* prep_share_out) {
   fld F = mkfld(p);
@@ -835,16 +1083,16 @@ int orc_prepare_init(const orc_params* p, const uint8_t vk[16], int agg_id,
   fe* proofs = (fe*)malloc(sizeof(fe) * p->proof_len * np);
   fe* ver = (fe*)malloc(sizeof(fe) * p->verifier_len * np);
   fe jr[64], qr[64];
-  uint8_t part[16], corrected[16];
+  uint8_t part[32], corrected[32];
   int rc = prepare_init_core(p, &F, vk, agg_id, nonce, public_share, input_share, meas, proofs,
                              part, corrected, jr, qr, ver);
   if (rc == ORC_OK) {
     uint8_t* o = state_out;
     for (uint32_t i = 0; i < p->meas_len; i++, o += p->es) enc_fe(&F, meas[i], o);
-    if (p->jr_len) memcpy(o, corrected, 16);
+    if (p->jr_len) memcpy(o, corrected, p->seed_size);
     o = prep_share_out;
     for (uint32_t i = 0; i < p->verifier_len * np; i++, o += p->es) enc_fe(&F, ver[i], o);
-    if (p->jr_len) memcpy(o, part, 16);
+    if (p->jr_len) memcpy(o, part, p->seed_size);
   }
   free(meas);
   free(proofs);
@@ -852,7 +1100,7 @@ int orc_prepare_init(const orc_params* p, const uint8_t vk[16], int agg_id,
   return rc;
 }
 
-int orc_helper_trace(const orc_params* p, const uint8_t vk[16], const uint8_t nonce[16],
+int orc_helper_trace(const orc_params* p, const uint8_t* vk, const uint8_t nonce[16],
                      const uint8_t* public_share, const uint8_t* helper_share,
                      uint8_t* meas_out, uint8_t* proofs_out, uint8_t* part_out,
                      uint8_t* corrected_out, uint8_t* jr_out, uint8_t* qr_out,
@@ -863,13 +1111,13 @@ int orc_helper_trace(const orc_params* p, const uint8_t vk[16], const uint8_t no
   fe* proofs = (fe*)malloc(sizeof(fe) * p->proof_len * np);
   fe* ver = (fe*)malloc(sizeof(fe) * p->verifier_len * np);
   fe jr[64] = {0}, qr[64] = {0};
-  uint8_t part[16] = {0}, corrected[16] = {0};
+  uint8_t part[32] = {0}, corrected[32] = {0};
   int rc = prepare_init_core(p, &F, vk, 1, nonce, public_share, helper_share, meas, proofs, part,
                              corrected, jr, qr, ver);
   for (uint32_t i = 0; i < p->meas_len; i++) enc_fe(&F, meas[i], meas_out + i * p->es);
   for (uint32_t i = 0; i < p->proof_len * np; i++) enc_fe(&F, proofs[i], proofs_out + i * p->es);
-  memcpy(part_out, part, 16);
-  memcpy(corrected_out, corrected, 16);
+  memcpy(part_out, part, p->seed_size);
+  memcpy(corrected_out, corrected, p->seed_size);
   for (uint32_t i = 0; i < p->jr_len * np; i++) enc_fe(&F, jr[i], jr_out + i * p->es);
   for (uint32_t i = 0; i < p->qr_len * np; i++) enc_fe(&F, qr[i], qr_out + i * p->es);
   if (rc == ORC_OK)
@@ -896,7 +1144,7 @@ static int prep_msg_core(const orc_params* p, const fld* F, const uint8_t* lps, 
     v[i] = f_add(F, a, b);
   }
   for (uint32_t k = 0; k < p->num_proofs; k++)
-    if (!flp_decide(F, p, v + k * p->verifier_len)) {
+    if (!(p->type == ORC_FPVEC ? fpvec_decide : flp_decide)(F, p, v + k * p->verifier_len)) {
       rc = ORC_ERR_DECIDE;
       goto out;
     }
@@ -915,7 +1163,7 @@ int orc_prep_shares_to_prep_msg(const orc_params* p, const uint8_t* leader_prep_
 int orc_prepare_next(const orc_params* p, const uint8_t* state, const uint8_t* prep_msg,
                      uint8_t* out_share_out) {
   fld F = mkfld(p);
-  if (p->jr_len && memcmp(state + p->meas_len * p->es, prep_msg, 16) != 0)
+  if (p->jr_len && memcmp(state + p->meas_len * p->es, prep_msg, p->seed_size) != 0)
     return ORC_ERR_PREP_NEXT;
   fe* meas = (fe*)malloc(sizeof(fe) * p->meas_len);
   fe* out = (fe*)malloc(sizeof(fe) * p->out_len);
@@ -970,7 +1218,8 @@ static void* batch_worker(void* arg) {
   fe* lagg = (fe*)calloc((size_t)c->n_segments * p->out_len, sizeof(fe));
   uint64_t* lcnt = (uint64_t*)calloc(c->n_segments, sizeof(uint64_t));
   fe jr[64], qr[64];
-  uint8_t part[16], corrected[16], msg[16];
+  uint8_t part[32], corrected[32], msg[32];
+  const uint32_t S = p->seed_size;
   for (;;) {
     uint32_t job = atomic_fetch_add(&c->next_job, 1);
     uint64_t lo = (uint64_t)job * c->job_size;
@@ -985,16 +1234,16 @@ static void* batch_worker(void* arg) {
       if (rc == ORC_OK) {
         uint8_t* o = hps;
         for (uint32_t k = 0; k < p->verifier_len * np; k++, o += p->es) enc_fe(&F, ver[k], o);
-        if (p->jr_len) memcpy(o, part, 16);
+        if (p->jr_len) memcpy(o, part, S);
         rc = prep_msg_core(p, &F, c->leader_ps + i * p->prep_share_len, hps, msg);
       }
-      if (rc == ORC_OK && p->jr_len && memcmp(corrected, msg, 16) != 0) rc = ORC_ERR_PREP_NEXT;
+      if (rc == ORC_OK && p->jr_len && memcmp(corrected, msg, S) != 0) rc = ORC_ERR_PREP_NEXT;
       c->status[i] = (uint8_t)rc;
       if (p->prep_msg_len) {
         if (rc == ORC_OK)
-          memcpy(c->msgs + i * 16, msg, 16);
+          memcpy(c->msgs + i * S, msg, S);
         else
-          memset(c->msgs + i * 16, 0, 16);
+          memset(c->msgs + i * S, 0, S);
       }
       if (rc != ORC_OK || (c->accept && !c->accept[i])) continue;
       /* prepare_next re-derives the helper measurement share from its seed [prio]. */
@@ -1022,7 +1271,7 @@ static void* batch_worker(void* arg) {
   return NULL;
 }
 
-int orc_helper_batch(const orc_params* p, const uint8_t vk[16], uint32_t n,
+int orc_helper_batch(const orc_params* p, const uint8_t* vk, uint32_t n,
                      const uint8_t* nonces, const uint8_t* public_shares,
                      const uint8_t* helper_shares, const uint8_t* leader_prep_shares,
                      const uint32_t* segment_ids, const uint8_t* accept_mask,
@@ -1136,6 +1385,7 @@ static void* gen_worker(void* arg) {
 int orc_gen_reports(const orc_params* p, const uint8_t vk[16], uint32_t n, uint64_t seed,
                     int n_threads, uint8_t* nonces, uint8_t* publics, uint8_t* helpers,
                     uint8_t* leader_ps, uint64_t* meas_out, uint8_t* leader_out_shares) {
+  if (p->type == ORC_FPVEC || p->seed_size != 16) return -1;  /* helper side only */
   gen_ctx g;
   g.p = p;
   g.vk = vk;

@@ -29,7 +29,8 @@
 extern "C" {
 #endif
 
-enum { ORC_COUNT = 0, ORC_SUM = 1, ORC_SUMVEC = 2, ORC_HISTOGRAM = 3 };
+enum { ORC_COUNT = 0, ORC_SUM = 1, ORC_SUMVEC = 2, ORC_HISTOGRAM = 3, ORC_FPVEC = 4,
+       ORC_SUMVEC_F64_MP = 5 };
 
 /* Per-report status codes; identical to include/janus_prio3.h (PRIO3_STATUS_*). */
 enum {
@@ -53,6 +54,13 @@ typedef struct {
   uint32_t proof_len, verifier_len;
   uint32_t helper_share_len, public_share_len, leader_share_len;
   uint32_t prep_share_len, prep_msg_len, out_share_bytes;
+  /* ORC_FPVEC (Prio3FixedPointBoundedL2VecSum, the reconstruction fixed in oracle/fpvec_py.py;
+   * helper side only: shard / gen_reports return -1): gadget 0 uses chunk_length / arity /
+   * calls / wire_len; gadget 1 = ParallelSum(PolyEval(y^2 - 2^n y), fp_C1) over the entries. */
+  uint32_t fp_C1, fp_K1, fp_P1;
+  /* XOF: seed size (16: XofTurboShake128; 32: XofHmacSha256Aes128, ORC_SUMVEC_F64_MP =
+   * Prio3SumVecField64MultiproofHmacSha256Aes128, core/src/vdaf.rs:173-195, helper side only) */
+  uint32_t seed_size, xof_hm;
 } orc_params;
 
 int orc_params_init(orc_params* p, int type, uint32_t bits, uint32_t length,
@@ -73,7 +81,7 @@ int orc_shard(const orc_params* p, const uint64_t* meas, const uint8_t nonce[16]
 /* prepare_init for agg_id 0 (leader, explicit share) or 1 (helper, seeds).
  * state_out: meas share (meas_len*es bytes) || corrected joint-rand seed (16, if JR).
  * prep_share_out: prep_share_len bytes. */
-int orc_prepare_init(const orc_params* p, const uint8_t vk[16], int agg_id,
+int orc_prepare_init(const orc_params* p, const uint8_t* vk, int agg_id,
                      const uint8_t nonce[16], const uint8_t* public_share,
                      const uint8_t* input_share, uint8_t* state_out, uint8_t* prep_share_out);
 
@@ -85,7 +93,7 @@ int orc_prepare_next(const orc_params* p, const uint8_t* state, const uint8_t* p
                      uint8_t* out_share_out);
 
 /* Intermediate values of the helper's prepare_init, for golden fixtures. */
-int orc_helper_trace(const orc_params* p, const uint8_t vk[16], const uint8_t nonce[16],
+int orc_helper_trace(const orc_params* p, const uint8_t* vk, const uint8_t nonce[16],
                      const uint8_t* public_share, const uint8_t* helper_share,
                      uint8_t* meas_out, uint8_t* proofs_out, uint8_t* part_out,
                      uint8_t* corrected_out, uint8_t* jr_out, uint8_t* qr_out,
@@ -97,7 +105,7 @@ int orc_helper_trace(const orc_params* p, const uint8_t vk[16], const uint8_t no
  * merged per segment (aggregation_job_writer.rs:591-695).  The leader prep share is the
  * raw prep_share bytes (ping-pong framing is removed by the caller).
  * agg_out: n_segments * out_len * es bytes; count_out: n_segments. */
-int orc_helper_batch(const orc_params* p, const uint8_t vk[16], uint32_t n,
+int orc_helper_batch(const orc_params* p, const uint8_t* vk, uint32_t n,
                      const uint8_t* nonces, const uint8_t* public_shares,
                      const uint8_t* helper_shares, const uint8_t* leader_prep_shares,
                      const uint32_t* segment_ids, const uint8_t* accept_mask,

@@ -387,3 +387,48 @@ def test_gpu_fpvec_query_variants(length, opts):
     reps = _reports(v, n, seed=43 + length, distinct=5 if length >= 1000 else 40)
     _tamper(v, reps, 0.1, seed=9)
     _check(v, reps, _run(v, reps, opts=opts))
+
+
+def _c_oracle(length, bits):
+    from oracle.oracle import Oracle, build
+    build()
+    return Oracle("fpvec", bits=bits, length=length)
+
+
+@pytest.mark.parametrize("length,bits", [(1, 16), (3, 32), (24, 16), (200, 16)])
+def test_c_restatement_matches_python(length, bits):
+    """The compiled C restatement of the FPVec helper path (oracle/prio3_oracle.c ORC_FPVEC: the
+    CPU baseline of bench.py --role fpvec) against the Python restatement, tampered reports
+    included: statuses, prepare messages, aggregate share and count."""
+    v = _vdaf(length, bits)
+    reps = _reports(v, 12, seed=51 + length)
+    _tamper(v, reps, 0.3, seed=13)
+    exp_msgs, exp_st, exp_out = _expected(v, reps)
+    o = _c_oracle(length, bits)
+    A = lambda k: np.array([list(r[k]) for r in reps], np.uint8)
+    msgs, st, agg, cnt = o.helper_batch(VK, A("nonce"), A("pub"), A("helper"), A("lps"),
+                                        n_threads=4)
+    assert st.tolist() == exp_st
+    np.testing.assert_array_equal(msgs, np.array([list(m) for m in exp_msgs], np.uint8))
+    tot = [0] * length
+    for o_ in exp_out:
+        if o_ is not None:
+            tot = [(a + b) % P.Field128.p for a, b in zip(tot, o_)]
+    assert [int.from_bytes(agg[0, 16 * e:16 * e + 16].tobytes(), "little")
+            for e in range(length)] == tot
+    assert int(cnt[0]) == exp_st.count(0)
+
+
+def test_c_restatement_reproduces_c5_fixture():
+    """Full size (10^4 entries, 160,030-element shares): the C restatement reproduces the
+    committed fixtures the Python restatement generated (tests/golden/fpvec_l10000.npz)."""
+    g = np.load(GOLDEN_C5)
+    o = _c_oracle(10000, 16)
+    msgs, st, agg, cnt = o.helper_batch(bytes(g["verify_key"]), g["nonce"], g["pub"], g["helper"],
+                                        g["lps"], n_threads=3)
+    assert st.tolist() == g["status"].tolist()
+    np.testing.assert_array_equal(msgs, g["prep_msg"])
+    want = b"".join(((int.from_bytes(g["out_shares"][0][16 * e:16 * e + 16].tobytes(), "little") +
+                      int.from_bytes(g["out_shares"][1][16 * e:16 * e + 16].tobytes(), "little"))
+                     % P.Field128.p).to_bytes(16, "little") for e in range(10000))
+    assert agg[0].tobytes() == want and int(cnt[0]) == 2

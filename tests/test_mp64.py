@@ -120,3 +120,30 @@ def test_gpu_mp64_matches_oracle(proofs, bits, length, chunk, n):
             tot = [(a + b) % P.Field64.p for a, b in zip(tot, o)]
     got = [int.from_bytes(agg[0, 8 * e:8 * e + 8].tobytes(), "little") for e in range(length)]
     assert got == tot and int(cnt[0]) == sum(1 for s in exp_st if s == 0)
+
+
+@pytest.mark.parametrize("proofs,bits,length,chunk", [(2, 16, 15, 16), (3, 2, 5, 3), (2, 1, 10, 3)])
+def test_c_restatement_matches_python(proofs, bits, length, chunk):
+    """The compiled C restatement (oracle/prio3_oracle.c ORC_SUMVEC_F64_MP: XofHmacSha256Aes128
+    on OpenSSL's SHA-256 / AES-128, 32-byte seeds; the CPU baseline of bench.py --role mp64)
+    against the Python restatement, tampered reports included."""
+    from oracle.oracle import Oracle, build
+    build()
+    v = _vdaf(proofs, bits, length, chunk)
+    reps = _reports(v, 9, seed=proofs * 10 + bits)
+    reps[2]["lps"][8] ^= 1                                  # a wire value: decide fails
+    reps[5]["lps"][-1] ^= 0x40                              # leader joint-rand part
+    reps[7]["lps"][0:8] = b"\xff" * 8                       # verifier element >= p
+    exp_msgs, exp_st, exp_out = _expected(v, reps)
+    o = Oracle("sumvec_f64_mp", bits=bits, length=length, chunk_length=chunk, num_proofs=proofs)
+    A = lambda k: np.array([list(r[k]) for r in reps], np.uint8)
+    msgs, st, agg, cnt = o.helper_batch(VK, A("nonce"), A("pub"), A("helper"), A("lps"),
+                                        n_threads=3)
+    assert st.tolist() == exp_st
+    np.testing.assert_array_equal(msgs, np.array([list(m) for m in exp_msgs], np.uint8))
+    tot = [0] * length
+    for o_ in exp_out:
+        if o_ is not None:
+            tot = [(a + b) % P.Field64.p for a, b in zip(tot, o_)]
+    assert [int.from_bytes(agg[0, 8 * e:8 * e + 8].tobytes(), "little") for e in range(length)] == tot
+    assert int(cnt[0]) == exp_st.count(0)
