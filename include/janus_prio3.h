@@ -112,14 +112,21 @@ void prio3_engine_destroy(prio3_engine* engine);
  *   helper_shares[n][helper_share_len], leader_prep_shares[n][prep_share_len]
  *   (the prep_share of each PingPongMessage::Initialize, framing already removed).
  * Outputs: prep_msgs_out[n][prep_msg_len] (the Finish message payload) and status_out[n].
- * The output shares stay on the device inside *batch_out until prio3_accumulate. */
+ * The output shares stay on the device inside *batch_out until prio3_accumulate.
+ * Thread-safe: concurrent calls (from any engines of the same VDAF instance on the same GPU,
+ * whatever their verify keys) are coalesced by the GPU's executor into shared launches.
+ * Each batch owns the device state of its own call: batches of one engine may be accumulated
+ * in any order, also after later prepares (free each with prio3_batch_free).
+ * PRIO3_FPVEC_BOUNDED_L2 returns PRIO3_EUNSUPPORTED unless option "experimental_fpvec" is 1
+ * (its circuit is a reconstruction; parity with prio unpinned). */
 int prio3_helper_prepare_batch(prio3_engine* engine, uint32_t n, const uint8_t* nonces,
                                const uint8_t* public_shares, const uint8_t* helper_shares,
                                const uint8_t* leader_prep_shares, uint8_t* prep_msgs_out,
                                uint8_t* status_out, prio3_batch** batch_out);
 
 /* Accumulates the finished reports whose accept_mask byte is non-zero (NULL = all) into
- * per-segment aggregate shares (segment = batch identifier, query_type.rs:72-82).
+ * per-segment aggregate shares (segment = batch identifier, query_type.rs:72-82).  A segment id
+ * >= n_segments excludes the report from every aggregate and count (all accumulate paths).
  * agg_shares_out[n_segments][agg_share_len] (LE field elements, mod-p sums), counts_out. */
 int prio3_accumulate(prio3_batch* batch, const uint32_t* segment_ids, const uint8_t* accept_mask,
                      uint32_t n_segments, uint8_t* agg_shares_out, uint64_t* counts_out);
@@ -131,8 +138,10 @@ void prio3_batch_free(prio3_batch* batch);
 /* ---- Device-resident entry points (buffers already in HBM; stream-ordered) ---- */
 /* d_* are device pointers with the same packed layouts; stream is a hipStream_t, ordered like
  * any HIP call on it (NULL = the null stream, as in HIP itself -- so a caller whose inputs were
- * produced on the null stream needs no extra synchronisation).  Output shares remain in the engine workspace until the next
- * prio3_device_prepare on this engine. */
+ * produced on the null stream needs no extra synchronisation).  The output shares of the
+ * latest device-resident prepare of an engine stay on the device (its "current run") until the
+ * next device-resident prepare of that engine replaces it; the accumulate / finish / output-share
+ * calls act on that run. */
 int prio3_device_prepare(prio3_engine* engine, uint32_t n, const uint8_t* d_nonces,
                          const uint8_t* d_public_shares, const uint8_t* d_helper_shares,
                          const uint8_t* d_leader_prep_shares, uint8_t* d_prep_msgs,
