@@ -569,6 +569,7 @@ struct Run {
   uint4* vk_tab = nullptr;
   // fused accumulate (prio3_device_prepare_aggregate)
   uint32_t *wpart = nullptr, *wseg = nullptr, *cseg = nullptr, *fix = nullptr;
+  uint4* corr_all = nullptr;  // FPVec: corrected joint-rand seeds of all n reports (leader)
   unsigned long long *cpart = nullptr, *agg64 = nullptr;
   size_t fix_cap = 0;
   bool fused = false;

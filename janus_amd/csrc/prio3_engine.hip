@@ -722,6 +722,10 @@ __global__ __launch_bounds__(256) void k_leader_unpack(DevParams p, InPtrs in, S
   msg_absorb_final(s, m, 42);
   uint32_t w[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
   put_elem<F>(p, sc.qr, 0, r, w, flag);
+  if (p.qr_len > 1) {  // FPVec: one query point per gadget, from the same squeeze block
+    uint32_t w1[4] = {kword(s, 4), kword(s, 5), kword(s, 6), kword(s, 7)};
+    put_elem<F>(p, sc.qr, 1, r, w1, flag);
+  }
   sc.flag[r] = (uint8_t)flag;
   status[r] = bad[tid] ? PRIO3_STATUS_INPUT_SHARE_DECODE : PRIO3_STATUS_FINISHED;
 }
@@ -738,7 +742,7 @@ __global__ __launch_bounds__(64) void k_leader_slowfix(DevParams p, InPtrs in, S
   b[0] = 1;
   for (int i = 0; i < 16; i++) b[1 + i] = (uint8_t)(nonce[i >> 2] >> (8 * (i & 3)));
   uint32_t vk[4] = {p.vk[0], p.vk[1], p.vk[2], p.vk[3]};
-  bx_expand<F>(p.dst[5], vk, b, 17, 1, sc.qr, p.ld, r);
+  bx_expand<F>(p.dst[5], vk, b, 17, p.qr_len, sc.qr, p.ld, r);
   const uint4 c = sc.corrected[r];
   const uint32_t cor[4] = {c.x, c.y, c.z, c.w};
   bx_expand<F>(p.dst[3], cor, b, 1, p.jr_len, sc.jr, p.ld, r);
@@ -2444,7 +2448,8 @@ static size_t fp_column_bytes(const DevParams& d) {
 // (private segments, queues, the caller's allocator) -- the r01u hipErrorIllegalAddress came
 // with a budget of 85% of free HBM and did not recur with an explicit reserve.
 // The kernels are latency-bound per lane, so the widest sub-batch wins.
-static uint32_t fp_sub_ld(const prio3_engine* e, const DevParams& d, uint32_t ld_out) {
+static uint32_t fp_sub_ld(const prio3_engine* e, const DevParams& d, uint32_t ld_out,
+                          size_t other_bytes) {
   const size_t per = fp_column_bytes(d);
   int64_t budget = e->fp_sub_bytes;
   if (budget <= 0) {
@@ -2456,7 +2461,7 @@ static uint32_t fp_sub_ld(const prio3_engine* e, const DevParams& d, uint32_t ld
     (void)ws_pool_bytes(e->device, &idle);
     const int64_t outb = (int64_t)(d.es * d.out_len * (size_t)ld_out + 64 * (size_t)ld_out);
     const int64_t reserve = std::max<int64_t>((int64_t)8 << 30, (int64_t)(0.10 * (double)tot));
-    budget = (int64_t)(fr + idle) - outb - reserve;
+    budget = (int64_t)(fr + idle) - outb - reserve - (int64_t)other_bytes;
   }
   uint64_t cols = (uint64_t)std::max<int64_t>(budget, 1) / per;
   cols = std::max<uint64_t>(256, cols & ~255ull);
@@ -2493,6 +2498,9 @@ static size_t run_carve(Run* R, unsigned flags, uint32_t n_keys, uint8_t* base) 
     take(&R->sc.acc, fp ? 16 : es * d.arity * ld);
     take(&R->sc.out, own_out(d) ? es * d.out_len * ldo : 16);
     take(&R->sc.beta, es * d.calls * ld);
+    // FPVec runs in sub-batches of ld columns: the leader's corrected seeds of every report
+    // outlive their sub-batch's scratch (prepare_next reads them)
+    if (fp) take(&R->corr_all, 16 * n);
   }
   if (flags & RUN_IO) {
     const size_t ml = R->e->sz.prep_msg_len ? R->e->sz.prep_msg_len : 16;
@@ -2532,9 +2540,13 @@ static Run* run_create(prio3_engine* e, uint32_t n, unsigned flags, uint32_t nse
   R->dp.nseg = nseg ? nseg : 1;
   const uint32_t ld_out = ((n ? n : 1) + 63) & ~63u;
   R->dp.ld_out = ld_out;
-  R->dp.ld = (flags & RUN_SCRATCH) && e->dp.kind == PRIO3_FPVEC_BOUNDED_L2
-                 ? fp_sub_ld(e, e->dp, ld_out)
-                 : ld_out;
+  R->dp.ld = ld_out;
+  if ((flags & RUN_SCRATCH) && e->dp.kind == PRIO3_FPVEC_BOUNDED_L2) {
+    // the rest of the run (I/O copies, the leader's explicit input shares: 2.6 MB per report at
+    // 10^4 entries) comes out of the same budget as the scratch sub-batch
+    const size_t other = run_carve(R, flags & ~RUN_SCRATCH, n_keys, nullptr);
+    R->dp.ld = fp_sub_ld(e, e->dp, ld_out, other);
+  }
   const size_t bytes = run_carve(R, flags, n_keys, nullptr);
   R->slab = ws_acquire(e->device, bytes, st, rc);
   if (!R->slab) {
@@ -2864,6 +2876,43 @@ extern "C" int launch_leader_init(const DevParams& dp, const uint8_t* d_nonces, 
 extern "C" int launch_leader_next(const DevParams& dp, const uint8_t* d_prep_msgs, const Scratch& sc,
                        uint8_t* d_status, hipStream_t st);
 
+// FPVec leader (agg_id 0): sub-batches of the run's ld columns, each through the helper's
+// kernels in their leader role -- k_leader_unpack (explicit share -> SoA, canonical check, both
+// query points), k_jrpart<false, true> (the leader's joint-rand part over its 2.56 MB share,
+// corrected seed, joint randomness), k_leader_slowfix, k_query_fpw<GS, LEADER> (verifier share,
+// the decoded entries as output shares) -- and the corrected seeds saved for prepare_next.
+static int leader_init_fpvec(prio3_engine* e, Run* R, const uint8_t* d_nonces,
+                             const uint8_t* d_pub, const uint8_t* d_lin, uint8_t* d_prep_shares,
+                             uint8_t* d_status, hipStream_t st) {
+  DevParams dp = R->dp;
+  dp.force_slow = (uint32_t)e->force_slow;
+  dp.trunc_xof = 0;
+  if (!fpvec_query_wide_takes(dp) || !R->corr_all) return PRIO3_EUNSUPPORTED;
+  const uint32_t n = R->n, cap = dp.ld;
+  const uint32_t nsub = (n + cap - 1) / cap;
+  const uint32_t sub = std::min(cap, (((n + nsub - 1) / nsub) + 255) & ~255u);
+  const size_t es = dp.es;
+  for (uint32_t s0 = 0; s0 < n; s0 += sub) {
+    DevParams q = dp;
+    q.n = std::min(sub, n - s0);
+    InPtrs qi{d_nonces + 16 * (size_t)s0,
+              d_pub ? d_pub + (size_t)dp.public_share_len * s0 : nullptr,
+              d_lin + (size_t)dp.leader_share_len * s0, nullptr};
+    OutPtrs qo{d_prep_shares + (size_t)dp.prep_share_len * s0, d_status + s0};
+    Scratch qs = R->sc;
+    qs.out = (uint8_t*)R->sc.out + es * s0;
+    const uint32_t blocks = (q.n + 255) / 256, blocks64 = (q.n + 63) / 64;
+    TIMED(e, st, "k_leader_unpack",
+          (k_leader_unpack<<<(q.n + 63) / 64, 256, 0, st>>>(q, qi, qs, qo.status)));
+    TIMED(e, st, "k_jrpart", (k_jrpart<false, true><<<blocks, 256, 0, st>>>(q, qi, qs)));
+    TIMED(e, st, "k_leader_slowfix", (k_leader_slowfix<<<blocks64, 64, 0, st>>>(q, qi, qs)));
+    TIMED(e, st, "k_query_fpw", launch_fpvec_query(q, qi, qs, qo, st, -10 - e->fp_wgs));
+    HIPCHK(hipMemcpyAsync(R->corr_all + s0, qs.corrected, 16 * (size_t)q.n,
+                          hipMemcpyDeviceToDevice, st));
+  }
+  return PRIO3_OK;
+}
+
 static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
                            const uint8_t* d_public_shares, const uint8_t* d_leader_input_shares,
                            uint8_t* d_prep_shares, uint8_t* d_status, hipStream_t st) {
@@ -2871,6 +2920,9 @@ static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
   dp.force_slow = (uint32_t)e->force_slow;
   const uint32_t n = R->n;
   R->last = st;
+  if (dp.kind == PRIO3_FPVEC_BOUNDED_L2)
+    return leader_init_fpvec(e, R, d_nonces, d_public_shares, d_leader_input_shares,
+                             d_prep_shares, d_status, st);
   const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
   if (ps && dp.jr_len && (dp.P == 32 || dp.P == 16 || dp.P == 8) && e->leader_fast) {
     // the helper kernels in their leader role
@@ -3627,8 +3679,9 @@ int prio3_device_leader_prepare_init(prio3_engine* e, uint32_t n, const uint8_t*
                                      const uint8_t* d_leader_input_shares, uint8_t* d_prep_shares,
                                      uint8_t* d_status, void* stream) {
   TraceSpan span_("leader VDAF preparation");
-  if (e && (e->dp.kind == PRIO3_SUMVEC_F64_MP || e->dp.kind == PRIO3_FPVEC_BOUNDED_L2))
-    return PRIO3_EUNSUPPORTED;  // helper role only
+  if (e && (e->dp.kind == PRIO3_SUMVEC_F64_MP ||
+            (e->dp.kind == PRIO3_FPVEC_BOUNDED_L2 && !e->experimental_fpvec)))
+    return PRIO3_EUNSUPPORTED;  // mp64: helper role only; FPVec: explicit opt-in
   if (!e) return PRIO3_EINVAL;
   if (n == 0) return PRIO3_OK;
   if (!d_nonces || !d_leader_input_shares || !d_prep_shares || !d_status ||
@@ -3647,8 +3700,9 @@ int prio3_device_leader_prepare_init(prio3_engine* e, uint32_t n, const uint8_t*
 int prio3_device_leader_prepare_next(prio3_engine* e, uint32_t n, const uint8_t* d_prep_msgs,
                                      uint8_t* d_status, void* stream) {
   TraceSpan span_("leader VDAF preparation");
-  if (e && (e->dp.kind == PRIO3_SUMVEC_F64_MP || e->dp.kind == PRIO3_FPVEC_BOUNDED_L2))
-    return PRIO3_EUNSUPPORTED;  // helper role only
+  if (e && (e->dp.kind == PRIO3_SUMVEC_F64_MP ||
+            (e->dp.kind == PRIO3_FPVEC_BOUNDED_L2 && !e->experimental_fpvec)))
+    return PRIO3_EUNSUPPORTED;  // mp64: helper role only; FPVec: explicit opt-in
   if (!e) return PRIO3_EINVAL;
   if (n == 0) return PRIO3_OK;
   if (!d_status || (e->dp.jr_len && !d_prep_msgs)) return PRIO3_EINVAL;
@@ -3660,8 +3714,10 @@ int prio3_device_leader_prepare_next(prio3_engine* e, uint32_t n, const uint8_t*
   dp.n = n;
   hipStream_t st = (hipStream_t)stream;
   R->last = st;
+  Scratch sc = R->sc;
+  if (R->corr_all) sc.corrected = R->corr_all;  // FPVec: seeds of every sub-batch
   int rc2 = PRIO3_OK;
-  TIMED(e, st, "k_leader_next", rc2 = launch_leader_next(dp, d_prep_msgs, R->sc, d_status, st));
+  TIMED(e, st, "k_leader_next", rc2 = launch_leader_next(dp, d_prep_msgs, sc, d_status, st));
   return rc2;
 }
 
@@ -3670,8 +3726,9 @@ int prio3_leader_prepare_init_batch(prio3_engine* e, uint32_t n, const uint8_t* 
                                     const uint8_t* leader_input_shares, uint8_t* prep_shares_out,
                                     uint8_t* status_out, prio3_batch** batch_out) {
   TraceSpan span_("leader VDAF preparation");
-  if (e && (e->dp.kind == PRIO3_SUMVEC_F64_MP || e->dp.kind == PRIO3_FPVEC_BOUNDED_L2))
-    return PRIO3_EUNSUPPORTED;  // helper role only
+  if (e && (e->dp.kind == PRIO3_SUMVEC_F64_MP ||
+            (e->dp.kind == PRIO3_FPVEC_BOUNDED_L2 && !e->experimental_fpvec)))
+    return PRIO3_EUNSUPPORTED;  // mp64: helper role only; FPVec: explicit opt-in
   if (!e || (n && (!nonces || !leader_input_shares || !prep_shares_out || !status_out)))
     return PRIO3_EINVAL;
   const DevParams& d = e->dp;
@@ -3736,8 +3793,10 @@ int prio3_leader_prepare_next_batch(prio3_batch* b, const uint8_t* prep_msgs,
   DevParams dp = R->dp;
   dp.n = n;
   R->last = st;
+  Scratch sc = R->sc;
+  if (R->corr_all) sc.corrected = R->corr_all;  // FPVec: seeds of every sub-batch
   int rc2 = PRIO3_OK;
-  TIMED(e, st, "k_leader_next", rc2 = launch_leader_next(dp, R->msgs, R->sc, R->status, st));
+  TIMED(e, st, "k_leader_next", rc2 = launch_leader_next(dp, R->msgs, sc, R->status, st));
   if (rc2) return rc2;
   HIPCHK(hipMemcpyAsync(status_inout, R->status, n, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));

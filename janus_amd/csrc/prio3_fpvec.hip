@@ -272,7 +272,11 @@ __global__ __launch_bounds__(256) void k_query_fp(DevParams p, InPtrs in, Scratc
 //     lane and sweep (beta_k, L_(k+1) loads shared by the group);
 //   * gadget-1 wires from the entries the XOF decoded (trunc_xof) or decoded here.
 // ------------------------------------------------------------------------------------
-template <int GS>
+// LEADER = 1: the leader's prepare_init (agg_id 0) on the same data flow -- the verifier share
+// [v, f0 wires, p0(t0), f1 wires, p1(t1)] || joint-rand part goes to out.prep_msgs (stride
+// prep_share_len) instead of being decided against a peer's share; out.status holds the unpack
+// verdict on entry; the entries (output share) are decoded here (trunc_xof = 0).
+template <int GS, int LEADER = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_query_fpw(
     DevParams p, InPtrs in, Scratch sc, OutPtrs out) {
   using namespace wide;
@@ -289,6 +293,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   DCHECK(p.ld_out >= p.n && nb * E + 2 * nb - 2 == M);
   const T one = F::one(), Z = F::zero();
   uint8_t status = PRIO3_STATUS_FINISHED;
+  if (LEADER && live) status = out.status[r];
+  uint8_t* lout = LEADER ? out.prep_msgs + (size_t)rr * p.prep_share_len : nullptr;
   uint8_t* L = (uint8_t*)sc.Lbuf;                   // rows [0, P0): L_c(t0)
   uint8_t* L1 = L + (size_t)F::ES * P0 * ld;        // rows [0, P1): L_c(t1)
   // ---- Lagrange bases: L_c for c = 1..K to scratch rows c, L_0 and the sum of L0_1..L0_K0
@@ -400,7 +406,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           mac_add(F0, ldf<F>(sc.proofs, 2 * j, ld, rr), L00);
           mac_add(F0, rj, Aq);
           const T f0 = mac_reduce(F0);
-          G0 = F::add(G0, mul128(F::add(lv(1 + 2 * j), f0), F::add(lv(2 + 2 * j), f1)));
+          if constexpr (LEADER) {
+            if (live) {
+              F::store(lout, 1 + 2 * j, f0);
+              F::store(lout, 2 + 2 * j, f1);
+            }
+          } else {
+            G0 = F::add(G0, mul128(F::add(lv(1 + 2 * j), f0), F::add(lv(2 + 2 * j), f1)));
+          }
         }
         rj = F::mul(rj, r08);
       }
@@ -447,8 +460,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         const uint32_t j = (s * GS1 + (uint32_t)q) * 8u + l;
         if (j < C1) {
           mac_add(Ac[q], ldf<F>(sc.proofs, off1 + j, ld, rr), L10);
-          const T a = F::add(lv(2 + A0 + j), mac_reduce(Ac[q]));
-          G1 = F::add(G1, F::sub(mul128(a, a), mul128(twon, a)));
+          if constexpr (LEADER) {
+            if (live) F::store(lout, 2 + A0 + j, mac_reduce(Ac[q]));
+          } else {
+            const T a = F::add(lv(2 + A0 + j), mac_reduce(Ac[q]));
+            G1 = F::add(G1, F::sub(mul128(a, a), mul128(twon, a)));
+          }
         }
       }
     }
@@ -495,6 +512,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const T r1 = ldf<F>(sc.jr, 1, ld, rr);
   const T normd = F::sub(F::add(normg, F::from_words(p.normc128)), claimed);
   const T v = F::add(F::mul(r1, range), F::mul(F::mul(r1, r1), normd));
+  if constexpr (LEADER) {
+    if (l == 0 && live) {
+      F::store(lout, 0, v);
+      F::store(lout, 1 + A0, p0t);
+      F::store(lout, 2 + A0 + C1, p1t);
+      *(uint4*)(lout + (size_t)p.verifier_len * F::ES) = sc.part[r];
+      out.status[r] = status;
+    }
+    return;
+  }
   const T V0 = F::add(lv(0), v);
   const T PT0 = F::add(lv(1 + A0), p0t);
   const T PT1 = F::add(lv(2 + A0 + C1), p1t);
@@ -546,6 +573,16 @@ bool fpvec_query_wide_takes(const DevParams& p) {
 // 10^4 entries, so latency, not occupancy, is what GS buys back)
 void launch_fpvec_query(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
                         int gs) {
+  if (gs < -10) {  // the eight-lane kernel in its leader role: -12, -13, -14
+    const uint32_t b = (p.n + 31) / 32;
+    if (gs == -14)
+      k_query_fpw<4, 1><<<b, 256, 0, st>>>(p, in, sc, out);
+    else if (gs == -12)
+      k_query_fpw<2, 1><<<b, 256, 0, st>>>(p, in, sc, out);
+    else
+      k_query_fpw<3, 1><<<b, 256, 0, st>>>(p, in, sc, out);
+    return;
+  }
   if (gs < 0) {  // the eight-lane kernel: -2, -3, -4 = its column group width
     const uint32_t b = (p.n + 31) / 32;
     if (gs == -4)

@@ -432,3 +432,57 @@ def test_c_restatement_reproduces_c5_fixture():
                       int.from_bytes(g["out_shares"][1][16 * e:16 * e + 16].tobytes(), "little"))
                      % P.Field128.p).to_bytes(16, "little") for e in range(10000))
     assert agg[0].tobytes() == want and int(cnt[0]) == 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("length,bits,n,sub", [(5, 16, 70, None), (24, 32, 90, None),
+                                               (1000, 16, 40, None), (24, 16, 600, 256)])
+def test_gpu_fpvec_leader_role(length, bits, n, sub):
+    """the FPVec leader (prepare_init agg_id 0 + prepare_next) on the device.
+    The leader prep shares must equal the restatement's; both roles on the device then decide,
+    and the two aggregate shares unshard to the sum of the encoded entries.  A non-canonical
+    element in one leader input share gives status 6; `sub` forces scratch sub-batches."""
+    from janus_amd import prio3 as J
+    v = _vdaf(length, bits)
+    t = v.t
+    rng = np.random.default_rng(61 + length)
+    reps, leaders, xs_all = [], [], []
+    for i in range(n):
+        if i >= 8:  # tile 8 distinct reports
+            reps.append(reps[i % 8]), leaders.append(leaders[i % 8]), xs_all.append(xs_all[i % 8])
+            continue
+        xs = _vector(rng, length, bits)
+        nonce = bytes(rng.integers(0, 256, 16, dtype=np.uint8))
+        pub, leader, helper = v.shard(xs, nonce, bytes(rng.integers(0, 256, 80, dtype=np.uint8)))
+        _, lps, _ = v.prepare_init(VK, 0, nonce, pub, leader)
+        reps.append(dict(nonce=nonce, pub=pub, helper=helper, lps=lps))
+        leaders.append(bytearray(leader))
+        xs_all.append(xs)
+    leaders = [bytearray(x) for x in leaders]
+    leaders[3][16 * 2:16 * 3] = b"\xff" * 16  # a non-canonical measurement-share element
+    eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(length, bits), VK, allow_unpinned=True)
+    if sub:
+        per = 16 * (t.meas_len + t.proof_len + 2 + 2 + 2 * (t.P0 + t.P1) + t.K0) + 33
+        eng.set_option("fp_sub_bytes", per * sub + 1)
+    A = lambda k: np.array([list(r[k]) for r in reps], np.uint8)
+    lps, lst, lbatch = eng.leader_prepare_init_batch(
+        A("nonce"), A("pub"), np.array([list(x) for x in leaders], np.uint8))
+    want = [0] * n
+    want[3] = 6
+    assert lst.tolist() == want
+    for i in range(n):
+        if i != 3:
+            assert lps[i].tobytes() == bytes(reps[i]["lps"]), i
+    msgs, hst, hbatch = eng.prepare_batch(A("nonce"), A("pub"), A("helper"), lps)
+    assert [int(x) for x in hst if x] == [3]  # the decode-failed leader share: decide fails
+    st = lbatch.leader_prepare_next(msgs, lst.copy())
+    assert st.tolist() == want
+    lagg, lcnt = lbatch.accumulate()
+    hagg, hcnt = hbatch.accumulate()
+    assert int(lcnt[0]) == int(hcnt[0]) == n - 1
+    tot = [(int.from_bytes(lagg[0, 16 * e:16 * e + 16].tobytes(), "little") +
+            int.from_bytes(hagg[0, 16 * e:16 * e + 16].tobytes(), "little")) % P.Field128.p
+           for e in range(length)]
+    half = 1 << (bits - 1)
+    expect = [sum(xs_all[i][e] + half for i in range(n) if i != 3) for e in range(length)]
+    assert tot == expect

@@ -95,8 +95,8 @@ def _engine_vdaf(t):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", list(CASES))
 def test_reference_e2e_on_device(name):
-    """GPU: both aggregators' prepare on the HIP engine (leader from the restatement where the
-    device leader role is not built), aggregate shares from the engine, unshard, decode."""
+    """GPU: both aggregators' prepare on the HIP engine (the leader's prep shares also checked
+    against the restatement's), aggregate shares from the engine, unshard, decode."""
     from janus_amd import prio3 as J
     t, meas = CASES[name]
     v = P.Prio3(t)
@@ -107,29 +107,20 @@ def test_reference_e2e_on_device(name):
     A = lambda k, w: np.array([np.frombuffer(r[k], np.uint8) for r in reps], np.uint8).reshape(n, w)
     nonces = A("nonce", 16)
     pub = A("pub", sz.public_share_len) if sz.public_share_len else None
-    try:
-        lps, lst, lbatch = eng.leader_prepare_init_batch(nonces, pub,
-                                                         A("leader", sz.leader_input_share_len))
-        assert not lst.any()
-    except RuntimeError:  # leader role not on the device for this instance: restatement
-        lbatch = None
-        lps = np.array([np.frombuffer(v.prepare_init(VK, 0, r["nonce"], r["pub"], r["leader"])[1],
-                                      np.uint8) for r in reps], np.uint8)
+    # every instance here has its leader role on the device (FPVec since round 2)
+    lps, lst, lbatch = eng.leader_prepare_init_batch(nonces, pub,
+                                                     A("leader", sz.leader_input_share_len))
+    assert not lst.any()
+    assert lps.tobytes() == b"".join(
+        v.prepare_init(VK, 0, r["nonce"], r["pub"], r["leader"])[1] for r in reps)
     msgs, status, hbatch = eng.prepare_batch(nonces, pub, A("helper", sz.helper_share_len), lps)
     assert not status.any()
     hagg, hcnt = hbatch.accumulate()
-    if lbatch is not None:
-        st = lbatch.leader_prepare_next(msgs if sz.prep_msg_len else None, np.zeros(n, np.uint8))
-        assert not st.any()
-        lagg, _ = lbatch.accumulate()
-        leader_agg = [int.from_bytes(lagg[0, i:i + sz.field_bytes].tobytes(), "little")
-                      for i in range(0, sz.agg_share_len, sz.field_bytes)]
-    else:
-        leader_agg = [0] * t.out_len
-        for r, m in zip(reps, msgs):
-            st0, _, _ = v.prepare_init(VK, 0, r["nonce"], r["pub"], r["leader"])
-            out = v.prepare_next(st0, m.tobytes())
-            leader_agg = [(a + b) % v.F.p for a, b in zip(leader_agg, out)]
+    st = lbatch.leader_prepare_next(msgs if sz.prep_msg_len else None, np.zeros(n, np.uint8))
+    assert not st.any()
+    lagg, _ = lbatch.accumulate()
+    leader_agg = [int.from_bytes(lagg[0, i:i + sz.field_bytes].tobytes(), "little")
+                  for i in range(0, sz.agg_share_len, sz.field_bytes)]
     helper_agg = [int.from_bytes(hagg[0, i:i + sz.field_bytes].tobytes(), "little")
                   for i in range(0, sz.agg_share_len, sz.field_bytes)]
     assert int(hcnt[0]) == n
