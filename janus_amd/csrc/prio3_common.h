@@ -534,6 +534,10 @@ struct Mp64Params {
 struct prio3_engine;
 int launch_mp64(prio3_engine* e, uint32_t n, uint32_t ld, InPtrs in, OutPtrs out, Scratch sc,
                 hipStream_t st);
+int launch_mp64_leader(prio3_engine* e, uint32_t n, uint32_t ld, InPtrs in, OutPtrs out,
+                       Scratch sc, hipStream_t st);
+int launch_mp64_leader_next(uint32_t n, const uint8_t* d_prep_msgs, Scratch sc, uint8_t* d_status,
+                            hipStream_t st);
 // P = 16 / 32 ParallelSum(Mul) helper query on lane pairs (prio3_query_pair.hip); false if the
 // instance is not one it takes
 bool launch_query_pair(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st);

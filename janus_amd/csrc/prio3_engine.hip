@@ -2923,6 +2923,14 @@ static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
   if (dp.kind == PRIO3_FPVEC_BOUNDED_L2)
     return leader_init_fpvec(e, R, d_nonces, d_public_shares, d_leader_input_shares,
                              d_prep_shares, d_status, st);
+  if (dp.kind == PRIO3_SUMVEC_F64_MP) {
+    int rc = PRIO3_OK;
+    TIMED(e, st, "k_mp64_prepare",
+          (rc = launch_mp64_leader(e, n, dp.ld, InPtrs{d_nonces, d_public_shares,
+                                                       d_leader_input_shares, nullptr},
+                                   OutPtrs{d_prep_shares, d_status}, R->sc, st)));
+    return rc;
+  }
   const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
   if (ps && dp.jr_len && (dp.P == 32 || dp.P == 16 || dp.P == 8) && e->leader_fast) {
     // the helper kernels in their leader role
@@ -3679,9 +3687,8 @@ int prio3_device_leader_prepare_init(prio3_engine* e, uint32_t n, const uint8_t*
                                      const uint8_t* d_leader_input_shares, uint8_t* d_prep_shares,
                                      uint8_t* d_status, void* stream) {
   TraceSpan span_("leader VDAF preparation");
-  if (e && (e->dp.kind == PRIO3_SUMVEC_F64_MP ||
-            (e->dp.kind == PRIO3_FPVEC_BOUNDED_L2 && !e->experimental_fpvec)))
-    return PRIO3_EUNSUPPORTED;  // mp64: helper role only; FPVec: explicit opt-in
+  if (e && e->dp.kind == PRIO3_FPVEC_BOUNDED_L2 && !e->experimental_fpvec)
+    return PRIO3_EUNSUPPORTED;  // FPVec: explicit opt-in
   if (!e) return PRIO3_EINVAL;
   if (n == 0) return PRIO3_OK;
   if (!d_nonces || !d_leader_input_shares || !d_prep_shares || !d_status ||
@@ -3700,9 +3707,8 @@ int prio3_device_leader_prepare_init(prio3_engine* e, uint32_t n, const uint8_t*
 int prio3_device_leader_prepare_next(prio3_engine* e, uint32_t n, const uint8_t* d_prep_msgs,
                                      uint8_t* d_status, void* stream) {
   TraceSpan span_("leader VDAF preparation");
-  if (e && (e->dp.kind == PRIO3_SUMVEC_F64_MP ||
-            (e->dp.kind == PRIO3_FPVEC_BOUNDED_L2 && !e->experimental_fpvec)))
-    return PRIO3_EUNSUPPORTED;  // mp64: helper role only; FPVec: explicit opt-in
+  if (e && e->dp.kind == PRIO3_FPVEC_BOUNDED_L2 && !e->experimental_fpvec)
+    return PRIO3_EUNSUPPORTED;  // FPVec: explicit opt-in
   if (!e) return PRIO3_EINVAL;
   if (n == 0) return PRIO3_OK;
   if (!d_status || (e->dp.jr_len && !d_prep_msgs)) return PRIO3_EINVAL;
@@ -3717,7 +3723,10 @@ int prio3_device_leader_prepare_next(prio3_engine* e, uint32_t n, const uint8_t*
   Scratch sc = R->sc;
   if (R->corr_all) sc.corrected = R->corr_all;  // FPVec: seeds of every sub-batch
   int rc2 = PRIO3_OK;
-  TIMED(e, st, "k_leader_next", rc2 = launch_leader_next(dp, d_prep_msgs, sc, d_status, st));
+  if (dp.kind == PRIO3_SUMVEC_F64_MP)
+    TIMED(e, st, "k_leader_next", rc2 = launch_mp64_leader_next(n, d_prep_msgs, sc, d_status, st));
+  else
+    TIMED(e, st, "k_leader_next", rc2 = launch_leader_next(dp, d_prep_msgs, sc, d_status, st));
   return rc2;
 }
 
@@ -3726,9 +3735,8 @@ int prio3_leader_prepare_init_batch(prio3_engine* e, uint32_t n, const uint8_t* 
                                     const uint8_t* leader_input_shares, uint8_t* prep_shares_out,
                                     uint8_t* status_out, prio3_batch** batch_out) {
   TraceSpan span_("leader VDAF preparation");
-  if (e && (e->dp.kind == PRIO3_SUMVEC_F64_MP ||
-            (e->dp.kind == PRIO3_FPVEC_BOUNDED_L2 && !e->experimental_fpvec)))
-    return PRIO3_EUNSUPPORTED;  // mp64: helper role only; FPVec: explicit opt-in
+  if (e && e->dp.kind == PRIO3_FPVEC_BOUNDED_L2 && !e->experimental_fpvec)
+    return PRIO3_EUNSUPPORTED;  // FPVec: explicit opt-in
   if (!e || (n && (!nonces || !leader_input_shares || !prep_shares_out || !status_out)))
     return PRIO3_EINVAL;
   const DevParams& d = e->dp;
@@ -3796,7 +3804,10 @@ int prio3_leader_prepare_next_batch(prio3_batch* b, const uint8_t* prep_msgs,
   Scratch sc = R->sc;
   if (R->corr_all) sc.corrected = R->corr_all;  // FPVec: seeds of every sub-batch
   int rc2 = PRIO3_OK;
-  TIMED(e, st, "k_leader_next", rc2 = launch_leader_next(dp, R->msgs, sc, R->status, st));
+  if (dp.kind == PRIO3_SUMVEC_F64_MP)
+    TIMED(e, st, "k_leader_next", rc2 = launch_mp64_leader_next(n, R->msgs, sc, R->status, st));
+  else
+    TIMED(e, st, "k_leader_next", rc2 = launch_leader_next(dp, R->msgs, sc, R->status, st));
   if (rc2) return rc2;
   HIPCHK(hipMemcpyAsync(status_inout, R->status, n, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));

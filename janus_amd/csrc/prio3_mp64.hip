@@ -205,6 +205,12 @@ NI uint32_t jr_word(uint32_t t, const uint32_t pre[7], const uint64_t* meas, siz
 
 }  // namespace
 
+// LEADER = 1: the leader's prepare_init (agg_id 0, aggregation_job_driver.rs:397-415) on its
+// explicit input share (in.helper = the leader input shares: enc(meas) || enc(proofs) ||
+// k_blind): the shares are decoded (non-canonical -> INPUT_SHARE_DECODE) instead of expanded,
+// the verifier share || joint-rand part is written to out.prep_msgs (stride prep_share_len), and
+// the corrected seed is kept for prepare_next (words 0-3 in sc.corrected, 4-7 in sc.part).
+template <int LEADER>
 __global__ __launch_bounds__(256) void k_mp64_prepare(Mp64Params P, uint32_t n, size_t ld,
                                                       InPtrs in, Scratch sc, OutPtrs out,
                                                       uint32_t force_slow) {
@@ -219,26 +225,49 @@ __global__ __launch_bounds__(256) void k_mp64_prepare(Mp64Params P, uint32_t n, 
   uint64_t* Lb = (uint64_t*)sc.Lbuf;
   uint8_t status = PRIO3_STATUS_FINISHED;
   uint32_t nonce[4], kmeas[8], kproofs[8], kblind[8], pub0[8];
+  const uint32_t M = P.meas_len, np = P.np, PL = P.proof_len;
+  const size_t lshare_len = (size_t)(M + PL * np) * 8 + 32;
   {
     const uint4 v = *(const uint4*)(in.nonces + 16 * (size_t)r);
     nonce[0] = v.x, nonce[1] = v.y, nonce[2] = v.z, nonce[3] = v.w;
-    const uint4* hs = (const uint4*)(in.helper + 96 * (size_t)r);
-    const uint4* ps = (const uint4*)(in.pub + 64 * (size_t)r);
+    // helper: k_meas || k_proofs || k_blind and the leader's part (public share bytes 0..31);
+    // leader: k_blind at the end of its explicit share and the helper's part (bytes 32..63)
+    const uint4* hs = (const uint4*)(in.helper + (LEADER ? lshare_len : 96) * (size_t)r);
+    const uint4* kb = LEADER ? (const uint4*)((const uint8_t*)hs + lshare_len - 32) : hs + 4;
+    const uint4* ps = (const uint4*)(in.pub + 64 * (size_t)r) + (LEADER ? 2 : 0);
 #pragma unroll
     for (int i = 0; i < 2; i++) {
-      const uint4 a = hs[i], b = hs[2 + i], c = hs[4 + i], d = ps[i];
-      kmeas[4 * i] = a.x, kmeas[4 * i + 1] = a.y, kmeas[4 * i + 2] = a.z, kmeas[4 * i + 3] = a.w;
-      kproofs[4 * i] = b.x, kproofs[4 * i + 1] = b.y, kproofs[4 * i + 2] = b.z,
-      kproofs[4 * i + 3] = b.w;
+      const uint4 c = kb[i], d = ps[i];
+      if (!LEADER) {
+        const uint4 a = hs[i], b = hs[2 + i];
+        kmeas[4 * i] = a.x, kmeas[4 * i + 1] = a.y, kmeas[4 * i + 2] = a.z,
+        kmeas[4 * i + 3] = a.w;
+        kproofs[4 * i] = b.x, kproofs[4 * i + 1] = b.y, kproofs[4 * i + 2] = b.z,
+        kproofs[4 * i + 3] = b.w;
+      }
       kblind[4 * i] = c.x, kblind[4 * i + 1] = c.y, kblind[4 * i + 2] = c.z,
       kblind[4 * i + 3] = c.w;
       pub0[4 * i] = d.x, pub0[4 * i + 1] = d.y, pub0[4 * i + 2] = d.z, pub0[4 * i + 3] = d.w;
     }
   }
-  const uint32_t M = P.meas_len, np = P.np, PL = P.proof_len;
   uint32_t rej = 0;
+  if (LEADER) {  // the explicit shares into SoA scratch, canonical encodings only
+    const uint64_t* ls = (const uint64_t*)(in.helper + lshare_len * (size_t)r);
+    bool ok = true;
+    for (uint32_t e = 0; e < M; e++) {
+      const uint64_t x = ls[e];
+      ok = ok && x < P64;
+      meas[(size_t)e * ld + r] = x;
+    }
+    for (uint32_t e = 0; e < PL * np; e++) {
+      const uint64_t x = ls[M + e];
+      ok = ok && x < P64;
+      proofs[(size_t)e * ld + r] = x;
+    }
+    if (!ok) status = PRIO3_STATUS_INPUT_SHARE_DECODE;
+  }
   // 1. measurement share: XOF(k_meas, dst(1), [1])
-  {
+  if (!LEADER) {
     Msg32<16> m;
     mz(m);
     msg_dst(m, P, 1);
@@ -250,7 +279,7 @@ __global__ __launch_bounds__(256) void k_mp64_prepare(Mp64Params P, uint32_t n, 
     rej += expand_soa(A, s, meas, ld, r, M);
   }
   // 2. proofs share: XOF(k_proofs, dst(2), [np, 1])
-  {
+  if (!LEADER) {
     Msg32<16> m;
     mz(m);
     msg_dst(m, P, 2);
@@ -270,7 +299,7 @@ __global__ __launch_bounds__(256) void k_mp64_prepare(Mp64Params P, uint32_t n, 
     Msg32<8> pm;  // the 26-byte prefix, big-endian words 0..6 (+2 bytes of word 6 free)
     mz(pm);
     msg_dst(pm, P, 7);
-    mbyte(pm, 9, 1);
+    mbyte(pm, 9, LEADER ? 0 : 1);
     mwords_le(pm, 10, nonce, 4);
     const uint32_t L = 26 + 8 * M;
     const uint32_t nblk = (L + 9 + 63) / 64;
@@ -294,14 +323,15 @@ __global__ __launch_bounds__(256) void k_mp64_prepare(Mp64Params P, uint32_t n, 
     stream_init(A, s, tag);
     derive32(A, s, part);
   }
-  // 4. corrected seed: XOF(0^32, dst(6), part_leader (public share) || part) -> 32 bytes
+  // 4. corrected seed: XOF(0^32, dst(6), leader part || helper part) -> 32 bytes (the other
+  //    party's part from the public share)
   uint32_t corrected[8];
   {
     Msg32<32> m;
     mz(m);
     msg_dst(m, P, 6);
-    mwords_le(m, 9, pub0, 8);
-    mwords_le(m, 41, part, 8);
+    mwords_le(m, 9, LEADER ? part : pub0, 8);
+    mwords_le(m, 41, LEADER ? pub0 : part, 8);
     uint32_t tag[8];
     hmac_ni(P.z_ist, P.z_ost, m.w, 73, tag);
     Stream s;
@@ -336,7 +366,8 @@ __global__ __launch_bounds__(256) void k_mp64_prepare(Mp64Params P, uint32_t n, 
     expand_regs<MAXP>(A, s, qr, np);
   }
   // 6. FLP query per proof + decide against the leader's verifier share
-  const uint8_t* lps = in.leader + (size_t)(P.vlen * np * 8 + 32) * r;
+  const uint8_t* lps = LEADER ? nullptr : in.leader + (size_t)(P.vlen * np * 8 + 32) * r;
+  uint8_t* lout = LEADER ? out.prep_msgs + (size_t)(P.vlen * np * 8 + 32) * r : nullptr;
   bool decode_ok = true, decide_ok = true;
   const T half = P.half;
   const uint32_t C = P.chunk, K = P.calls, PP = P.P;
@@ -380,7 +411,8 @@ __global__ __launch_bounds__(256) void k_mp64_prepare(Mp64Params P, uint32_t n, 
     T rC = 1;
     for (uint32_t i = 0; i < C; i++) rC = F::mul(rC, rr);
     T G = 0, rj = rr;
-    const uint8_t* lv = lps + (size_t)k * P.vlen * 8;
+    const uint8_t* lv = LEADER ? nullptr : lps + (size_t)k * P.vlen * 8;
+    T* vo = LEADER ? (T*)(lout + (size_t)k * P.vlen * 8) : nullptr;
     auto lvf = [&](uint32_t e) {
       const T x = *(const T*)(lv + 8 * e);
       if (x >= P64) decode_ok = false;
@@ -397,7 +429,12 @@ __global__ __launch_bounds__(256) void k_mp64_prepare(Mp64Params P, uint32_t n, 
         f1 = F::add(f1, F::mul(F::sub(m, half), Lk));
         rp = F::mul(rp, rC);
       }
-      G = F::add(G, F::mul(F::add(f0, lvf(1 + 2 * jj)), F::add(f1, lvf(2 + 2 * jj))));
+      if (LEADER) {
+        vo[1 + 2 * jj] = f0;
+        vo[2 + 2 * jj] = f1;
+      } else {
+        G = F::add(G, F::mul(F::add(f0, lvf(1 + 2 * jj)), F::add(f1, lvf(2 + 2 * jj))));
+      }
       rj = F::mul(rj, rr);
     }
     // p(t) by Horner; v = sum_calls p(alpha^(c+1)) = sum_e coef_e sigma_(e mod P)
@@ -408,9 +445,22 @@ __global__ __launch_bounds__(256) void k_mp64_prepare(Mp64Params P, uint32_t n, 
       pt = F::add(F::mul(pt, t), c);
       v = F::add(v, F::mul(c, P.sigma[e & (PP - 1)]));
     }
-    const T V0 = F::add(lvf(0), v), PT = F::add(lvf(P.arity + 1), pt);
-    if (V0 != 0 || G != PT) decide_ok = false;
+    if (LEADER) {
+      vo[0] = v;
+      vo[P.arity + 1] = pt;
+    } else {
+      const T V0 = F::add(lvf(0), v), PT = F::add(lvf(P.arity + 1), pt);
+      if (V0 != 0 || G != PT) decide_ok = false;
+    }
   }
+  if (LEADER) {  // joint-rand part after the verifiers; corrected seed kept for prepare_next
+    uint4* po = (uint4*)(lout + (size_t)P.vlen * np * 8);
+    po[0] = make_uint4(part[0], part[1], part[2], part[3]);
+    po[1] = make_uint4(part[4], part[5], part[6], part[7]);
+    sc.corrected[r] = make_uint4(corrected[0], corrected[1], corrected[2], corrected[3]);
+    sc.part[r] = make_uint4(corrected[4], corrected[5], corrected[6], corrected[7]);
+    out.status[r] = status;
+  } else {
   // 7. prepare message XOF(0^32, dst(6), leader part || helper part), joint-rand check
   uint32_t lpart[8];
   {
@@ -452,6 +502,7 @@ __global__ __launch_bounds__(256) void k_mp64_prepare(Mp64Params P, uint32_t n, 
   mo[0] = fin ? make_uint4(msg[0], msg[1], msg[2], msg[3]) : make_uint4(0, 0, 0, 0);
   mo[1] = fin ? make_uint4(msg[4], msg[5], msg[6], msg[7]) : make_uint4(0, 0, 0, 0);
   out.status[r] = status;
+  }
   // 8. output share: SumVec truncate (bit recomposition)
   uint64_t* o = (uint64_t*)sc.out;
   for (uint32_t e = 0; e < P.out_len; e++) {
@@ -466,7 +517,34 @@ __global__ __launch_bounds__(256) void k_mp64_prepare(Mp64Params P, uint32_t n, 
 
 int launch_mp64(prio3_engine* e, uint32_t n, uint32_t ld, InPtrs in, OutPtrs out, Scratch sc,
                 hipStream_t st) {
-  k_mp64_prepare<<<(n + 255) / 256, 256, 0, st>>>(e->mp, n, ld, in, sc, out,
-                                                  (uint32_t)e->force_slow);
+  k_mp64_prepare<0><<<(n + 255) / 256, 256, 0, st>>>(e->mp, n, ld, in, sc, out,
+                                                     (uint32_t)e->force_slow);
+  return hipGetLastError() == hipSuccess ? PRIO3_OK : PRIO3_EDEVICE;
+}
+
+// leader prepare_init (in.helper = the leader input shares, out.prep_msgs = prep shares)
+int launch_mp64_leader(prio3_engine* e, uint32_t n, uint32_t ld, InPtrs in, OutPtrs out,
+                       Scratch sc, hipStream_t st) {
+  k_mp64_prepare<1><<<(n + 255) / 256, 256, 0, st>>>(e->mp, n, ld, in, sc, out,
+                                                     (uint32_t)e->force_slow);
+  return hipGetLastError() == hipSuccess ? PRIO3_OK : PRIO3_EDEVICE;
+}
+
+// leader prepare_next: the helper's 32-byte prepare message must equal the corrected seed
+// (else VdafPrepareNext); the output share was written by the init kernel
+__global__ __launch_bounds__(256) void k_mp64_leader_next(uint32_t n, const uint8_t* prep_msgs,
+                                                          Scratch sc, uint8_t* status) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n || status[r] != PRIO3_STATUS_FINISHED) return;
+  const uint4* m = (const uint4*)(prep_msgs + 32 * (size_t)r);
+  const uint4 a = m[0], b = m[1], c = sc.corrected[r], d = sc.part[r];
+  const uint32_t diff = (a.x ^ c.x) | (a.y ^ c.y) | (a.z ^ c.z) | (a.w ^ c.w) | (b.x ^ d.x) |
+                        (b.y ^ d.y) | (b.z ^ d.z) | (b.w ^ d.w);
+  if (diff) status[r] = PRIO3_STATUS_PREP_NEXT;
+}
+
+int launch_mp64_leader_next(uint32_t n, const uint8_t* d_prep_msgs, Scratch sc, uint8_t* d_status,
+                            hipStream_t st) {
+  k_mp64_leader_next<<<(n + 255) / 256, 256, 0, st>>>(n, d_prep_msgs, sc, d_status);
   return hipGetLastError() == hipSuccess ? PRIO3_OK : PRIO3_EDEVICE;
 }

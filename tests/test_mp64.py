@@ -147,3 +147,59 @@ def test_c_restatement_matches_python(proofs, bits, length, chunk):
             tot = [(a + b) % P.Field64.p for a, b in zip(tot, o_)]
     assert [int.from_bytes(agg[0, 8 * e:8 * e + 8].tobytes(), "little") for e in range(length)] == tot
     assert int(cnt[0]) == exp_st.count(0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("proofs,bits,length,chunk,n", [(2, 16, 15, 16, 40), (3, 2, 5, 3, 300)])
+def test_gpu_mp64_leader_role(proofs, bits, length, chunk, n):
+    """the mp64 leader (prepare_init agg_id 0 + prepare_next) on the device.
+    The leader prep shares (verifier shares || joint-rand part) must equal the restatement's;
+    both roles on the device then decide, and the two aggregate shares unshard to the plaintext
+    sum.  A non-canonical element in one leader input share gives status 6 (the helper's decide
+    on that report then fails); a tampered prepare message gives VdafPrepareNext (4)."""
+    from janus_amd import prio3 as J
+    v = _vdaf(proofs, bits, length, chunk)
+    rng = np.random.default_rng(proofs * 7 + bits)
+    reps, leaders = [], []
+    for i in range(n):
+        if i >= 16:  # tile 16 distinct reports
+            reps.append(reps[i % 16]), leaders.append(bytearray(leaders[i % 16]))
+            continue
+        m = [int(x) for x in rng.integers(0, 2 ** bits, length)]
+        nonce = bytes(rng.integers(0, 256, 16, dtype=np.uint8))
+        pub, leader, helper = v.shard(m, nonce, bytes(rng.integers(0, 256, 160, dtype=np.uint8)))
+        _, lps, _ = v.prepare_init(VK, 0, nonce, pub, leader)
+        reps.append(dict(m=m, nonce=nonce, pub=pub, helper=helper, lps=lps))
+        leaders.append(bytearray(leader))
+    leaders[3][8 * 2:8 * 3] = b"\xff" * 8          # a non-canonical measurement-share element
+    ml = v.t.meas_len
+    leaders[5][8 * (ml + 1):8 * (ml + 2)] = b"\xff" * 8  # a non-canonical proof-share element
+    eng = J.HelperEngine(J.Prio3SumVecField64MultiproofHmacSha256Aes128(proofs, bits, length,
+                                                                         chunk), VK)
+    A = lambda k: np.array([list(r[k]) for r in reps], np.uint8)
+    lps, lst, lbatch = eng.leader_prepare_init_batch(
+        A("nonce"), A("pub"), np.array([list(x) for x in leaders], np.uint8))
+    bad = {3, 5}
+    assert [i for i in range(n) if lst[i]] == sorted(bad) and set(lst[list(bad)]) == {6}
+    for i in range(n):
+        if i not in bad:
+            assert lps[i].tobytes() == bytes(reps[i]["lps"]), i
+    msgs, hst, hbatch = eng.prepare_batch(A("nonce"), A("pub"), A("helper"), lps)
+    assert [i for i in range(n) if hst[i]] == sorted(bad)
+    sent = msgs.copy()
+    sent[7, 0] ^= 1                               # the leader must reject this prepare message
+    st = lbatch.leader_prepare_next(sent, lst.copy())
+    assert st[7] == 4 and [i for i in range(n) if st[i] and i != 7] == sorted(bad)
+    lagg, lcnt = lbatch.accumulate()
+    hagg, hcnt = hbatch.accumulate()
+    assert int(lcnt[0]) == n - 3 and int(hcnt[0]) == n - 2
+    tot = [(int.from_bytes(lagg[0, 8 * e:8 * e + 8].tobytes(), "little") +
+            int.from_bytes(hagg[0, 8 * e:8 * e + 8].tobytes(), "little")) % P.Field64.p
+           for e in range(length)]
+    # the helper aggregated report 7, which the leader rejected: the sum is every other good
+    # report's measurement plus the helper's own output share of report 7
+    st7, _, _ = v.prepare_init(VK, 1, reps[7]["nonce"], reps[7]["pub"], reps[7]["helper"])
+    h7 = v.prepare_next(st7, msgs[7].tobytes())
+    expect = [(sum(reps[i]["m"][e] for i in range(n) if i not in bad and i != 7) + h7[e])
+              % P.Field64.p for e in range(length)]
+    assert tot == expect

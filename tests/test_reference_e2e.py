@@ -9,6 +9,10 @@ These are the only known answers the reference holds for Prio3 aggregation seman
   e2e_prio3_fixed16vec     FixedPointBoundedL2VecSum BitSize16, length 3  -> ["0.5","0.5","0.6875"]
   e2e_prio3_fixed32vec     FixedPointBoundedL2VecSum BitSize32, length 3  -> ["0.5","0.5","0.6875"]
                                                                                (:688-764)
+  janus_in_process_customized_sum_vec
+                           Prio3SumVecField64MultiproofHmacSha256Aes128 proofs 2, bits 16,
+                           length 15, chunk 16, random 16-bit entries
+                           (integration_tests/tests/integration/janus.rs:378-400, common.rs:458-490)
 The reference asserts the fixed-point result literally and the others by type; here the
 others are checked against the plaintext sums they must decode to (the semantic known answer of
 integration_tests/tests/integration/common.rs:332-554).  The client shard is the Python
@@ -36,8 +40,16 @@ CASES = {
     "e2e_prio3_histogram": (P.Prio3Type("histogram", length=6, chunk_length=2), HIST),
     "e2e_prio3_fixed16vec": (FpVecType(3, 16), [[int(x * (1 << 15)) for x in v] for v in FIXED]),
     "e2e_prio3_fixed32vec": (FpVecType(3, 32), [[int(x * (1 << 31)) for x in v] for v in FIXED]),
+    "janus_in_process_customized_sum_vec": (
+        P.Prio3Type("sumvec_f64_mp", bits=16, length=15, chunk_length=16, num_proofs=2),
+        [[int(x) for x in row] for row in np.random.default_rng(458).integers(0, 1 << 16, (20, 15))]),
 }
-VK = bytes(range(0x70, 0x80))
+VK16 = bytes(range(0x70, 0x80))
+VK32 = bytes(range(0x70, 0x90))
+
+
+def _vk(t):
+    return VK32 if getattr(t, "seed_size", 16) == 32 else VK16
 
 
 def _expected(name, meas):
@@ -45,6 +57,8 @@ def _expected(name, meas):
         return sum(meas)
     if name == "e2e_prio3_sum_vec":
         return [sum(m[e] for m in meas) for e in range(4)]
+    if name == "janus_in_process_customized_sum_vec":
+        return [sum(m[e] for m in meas) for e in range(15)]
     if name == "e2e_prio3_histogram":
         return [meas.count(b) for b in range(6)]
     return ["0.5", "0.5", "0.6875"]  # end_to_end.rs:724, 763
@@ -72,6 +86,7 @@ def test_reference_e2e_restatement(name):
     """CPU: the restatement alone reproduces each reference end-to-end result."""
     t, meas = CASES[name]
     v = P.Prio3(t)
+    VK = _vk(t)
     aggs = [[0] * t.out_len, [0] * t.out_len]
     for r in _shard_all(v, meas, seed=len(name)):
         st0, lps, _ = v.prepare_init(VK, 0, r["nonce"], r["pub"], r["leader"])
@@ -89,7 +104,10 @@ def _engine_vdaf(t):
         return J.Prio3FixedPointBoundedL2VecSum(t.length, t.bits)
     return {"count": lambda: J.Prio3Count(), "sum": lambda: J.Prio3Sum(t.bits),
             "sumvec": lambda: J.Prio3SumVec(t.bits, t.length, t.chunk_length),
-            "histogram": lambda: J.Prio3Histogram(t.length, t.chunk_length)}[t.kind]()
+            "histogram": lambda: J.Prio3Histogram(t.length, t.chunk_length),
+            "sumvec_f64_mp": lambda: J.Prio3SumVecField64MultiproofHmacSha256Aes128(
+                t.num_proofs, t.bits, t.length, t.chunk_length)}[
+                "sumvec_f64_mp" if t.seed_size == 32 else t.kind]()
 
 
 @pytest.mark.gpu
@@ -101,13 +119,14 @@ def test_reference_e2e_on_device(name):
     t, meas = CASES[name]
     v = P.Prio3(t)
     reps = _shard_all(v, meas, seed=len(name))
+    VK = _vk(t)
     eng = J.HelperEngine(_engine_vdaf(t), VK, allow_unpinned=True)
     sz = eng.sz
     n = len(reps)
     A = lambda k, w: np.array([np.frombuffer(r[k], np.uint8) for r in reps], np.uint8).reshape(n, w)
     nonces = A("nonce", 16)
     pub = A("pub", sz.public_share_len) if sz.public_share_len else None
-    # every instance here has its leader role on the device (FPVec since round 2)
+    # every instance here has its leader role on the device (FPVec and mp64 since round 2)
     lps, lst, lbatch = eng.leader_prepare_init_batch(nonces, pub,
                                                      A("leader", sz.leader_input_share_len))
     assert not lst.any()
