@@ -550,7 +550,40 @@ def leader_main(args):
                kernels=per_kernel,
                checks=dict(helper_finished=helper_ok,
                            leader_finished=int((lstatus == 0).sum().item()),
-                           leader_prep_shares_equal_generator=same, agg_count=int(cnt[0].item())))
+                           leader_prep_shares_equal_generator=same, agg_count=int(cnt[0].item())),
+               cpu_baseline=None)
+    if not args.no_cpu_baseline:
+        # the C restatement's leader path (orc_leader_batch: prepare_init agg_id 0 +
+        # prepare_next + aggregate in Janus-sized jobs) on a bounded sample of the same reports
+        from oracle.oracle import Oracle, build
+        build()
+        o = Oracle("histogram", length=256, chunk_length=16)
+        th = cpu_threads()
+        host = [t.cpu().numpy() for t in (data["nonces"], data["public_shares"],
+                                          data["leader_input_shares"], msgs)]
+
+        def crun(m):
+            t1 = time.perf_counter()
+            r = o.leader_batch(VK, *(h[:m] for h in host), n_threads=th, job_size=500)
+            return time.perf_counter() - t1, r
+
+        probe = min(n, 500 * th)
+        dt, _ = crun(probe)
+        m = int(min(n, max(probe, probe * args.cpu_seconds / max(dt, 1e-6))))
+        dt, (cps, cst, cagg, ccnt) = crun(m)
+        out["cpu_baseline"] = dict(value=m / dt, unit="reports/s", cores=th, kind="port",
+                                   sample=f"{m} of the same reports through the C restatement's "
+                                          f"leader path (oracle/prio3_oracle.c orc_leader_batch), "
+                                          f"jobs of 500, {th} threads, {dt:.1f}s wall")
+        out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+        agg_s = torch.zeros_like(agg)
+        cnt_s = torch.zeros_like(cnt)
+        eng.accumulate_device(m, lstatus[:m], None, None, 1, agg_s, cnt_s)
+        torch.cuda.synchronize()
+        out["checks"]["cpu_gpu_parity_on_sample"] = bool(
+            np.array_equal(lstatus[:m].cpu().numpy(), cst) and
+            np.array_equal(prep[:m].cpu().numpy(), cps) and
+            np.array_equal(agg_s.cpu().numpy(), cagg) and int(cnt_s[0].item()) == int(ccnt[0]))
     print(json.dumps(out), flush=True)
 
 

@@ -1312,6 +1312,110 @@ int orc_helper_batch(const orc_params* p, const uint8_t* vk, uint32_t n,
 }
 
 /* ------------------------------------------------------------------------------------ */
+/* Batched leader path (CPU baseline of bench.py --role leader): per report prepare_init   */
+/* with agg_id 0 on the explicit share (aggregation_job_driver.rs:397-415), prepare_next   */
+/* on the helper's prepare message (:700-760: corrected-seed check), then the output share */
+/* merged per segment, in jobs of job_size on n_threads workers.                          */
+/* ------------------------------------------------------------------------------------ */
+typedef struct {
+  const orc_params* p;
+  const uint8_t* vk;
+  uint32_t n;
+  const uint8_t *nonces, *publics, *leaders, *msgs;
+  uint8_t *prep_out, *status;
+  int job_size;
+  atomic_uint next_job;
+  pthread_mutex_t mu;
+  fe* agg;
+  uint64_t* count;
+} leader_ctx;
+
+static void* leader_worker(void* arg) {
+  leader_ctx* c = (leader_ctx*)arg;
+  const orc_params* p = c->p;
+  fld F = mkfld(p);
+  const uint32_t np = p->num_proofs, S = p->seed_size;
+  fe* meas = (fe*)malloc(sizeof(fe) * p->meas_len);
+  fe* proofs = (fe*)malloc(sizeof(fe) * p->proof_len * np);
+  fe* ver = (fe*)malloc(sizeof(fe) * p->verifier_len * np);
+  fe* out = (fe*)malloc(sizeof(fe) * p->out_len);
+  fe* lagg = (fe*)calloc(p->out_len, sizeof(fe));
+  uint64_t lcnt = 0;
+  fe jr[64], qr[64];
+  uint8_t part[32], corrected[32];
+  for (;;) {
+    uint32_t job = atomic_fetch_add(&c->next_job, 1);
+    uint64_t lo = (uint64_t)job * c->job_size;
+    if (lo >= c->n) break;
+    uint64_t hi = lo + c->job_size;
+    if (hi > c->n) hi = c->n;
+    for (uint64_t i = lo; i < hi; i++) {
+      const uint8_t* pub = c->publics ? c->publics + i * p->public_share_len : NULL;
+      uint8_t* o = c->prep_out + i * p->prep_share_len;
+      int rc = prepare_init_core(p, &F, c->vk, 0, c->nonces + i * 16, pub,
+                                 c->leaders + i * p->leader_share_len, meas, proofs, part,
+                                 corrected, jr, qr, ver);
+      if (rc == ORC_OK) {
+        for (uint32_t k = 0; k < p->verifier_len * np; k++, o += p->es) enc_fe(&F, ver[k], o);
+        if (p->jr_len) memcpy(o, part, S);
+        if (p->jr_len && c->msgs && memcmp(corrected, c->msgs + i * S, S) != 0)
+          rc = ORC_ERR_PREP_NEXT;
+      } else {
+        memset(o, 0, p->prep_share_len);
+      }
+      c->status[i] = (uint8_t)rc;
+      if (rc != ORC_OK) continue;
+      truncate_share(p, &F, meas, out);
+      for (uint32_t k = 0; k < p->out_len; k++) lagg[k] = f_add(&F, lagg[k], out[k]);
+      lcnt++;
+    }
+  }
+  pthread_mutex_lock(&c->mu);
+  for (uint32_t k = 0; k < p->out_len; k++) c->agg[k] = f_add(&F, c->agg[k], lagg[k]);
+  *c->count += lcnt;
+  pthread_mutex_unlock(&c->mu);
+  free(meas);
+  free(proofs);
+  free(ver);
+  free(out);
+  free(lagg);
+  return NULL;
+}
+
+int orc_leader_batch(const orc_params* p, const uint8_t* vk, uint32_t n, const uint8_t* nonces,
+                     const uint8_t* public_shares, const uint8_t* leader_shares,
+                     const uint8_t* prep_msgs, uint8_t* prep_shares_out, uint8_t* status_out,
+                     uint8_t* agg_out, uint64_t* count_out, int n_threads, int job_size) {
+  if (n_threads < 1) n_threads = 1;
+  if (job_size < 1) job_size = 500;
+  leader_ctx c;
+  c.p = p;
+  c.vk = vk;
+  c.n = n;
+  c.nonces = nonces;
+  c.publics = public_shares;
+  c.leaders = leader_shares;
+  c.msgs = prep_msgs;
+  c.prep_out = prep_shares_out;
+  c.status = status_out;
+  c.job_size = job_size;
+  atomic_init(&c.next_job, 0);
+  pthread_mutex_init(&c.mu, NULL);
+  c.agg = (fe*)calloc(p->out_len, sizeof(fe));
+  c.count = count_out;
+  *count_out = 0;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * n_threads);
+  for (int t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, leader_worker, &c);
+  for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+  fld F = mkfld(p);
+  for (uint32_t k = 0; k < p->out_len; k++) enc_fe(&F, c.agg[k], agg_out + (size_t)k * p->es);
+  free(th);
+  free(c.agg);
+  pthread_mutex_destroy(&c.mu);
+  return 0;
+}
+
+/* ------------------------------------------------------------------------------------ */
 /* Deterministic synthetic report generator (client shard + leader prepare_init), for   */
 /* tests only.  Per report i: stream = TurboSHAKE128("janus-amd-gen" || seed || i, D=1).  */
 /* ------------------------------------------------------------------------------------ */

@@ -112,6 +112,15 @@ int orc_helper_batch(const orc_params* p, const uint8_t* vk, uint32_t n,
                      uint32_t n_segments, uint8_t* prep_msgs_out, uint8_t* status_out,
                      uint8_t* agg_out, uint64_t* count_out, int n_threads, int job_size);
 
+/* Batched leader prepare_init (agg_id 0) + prepare_next (prep_msgs: the helper's prepare
+ * messages, seed_size bytes each, nullable without joint randomness) + aggregate, one
+ * segment.  Status: 0 finished, ORC_ERR_PREP_INIT (non-canonical share element) or
+ * ORC_ERR_PREP_NEXT.  prep_shares_out: n x prep_share_len (zero on init failure). */
+int orc_leader_batch(const orc_params* p, const uint8_t* vk, uint32_t n, const uint8_t* nonces,
+                     const uint8_t* public_shares, const uint8_t* leader_shares,
+                     const uint8_t* prep_msgs, uint8_t* prep_shares_out, uint8_t* status_out,
+                     uint8_t* agg_out, uint64_t* count_out, int n_threads, int job_size);
+
 /* Deterministic synthetic reports (client shard + leader prepare_init), multithreaded.
  * meas_out: n x (SumVec: length, else 1) u64; leader_out_shares: n x out_len*es (nullable). */
 int orc_gen_reports(const orc_params* p, const uint8_t vk[16], uint32_t n, uint64_t seed,

@@ -152,6 +152,53 @@ def test_batch_unshard_equals_plaintext(oracle_lib, name):
     assert tot == exp
 
 
+@pytest.mark.parametrize("name", ["count", "sumvec_8x10_c9", "hist_256_c16"])
+def test_leader_batch_matches_python(oracle_lib, name):
+    """orc_leader_batch (the leader line's CPU baseline) against the Python restatement's
+    prepare_init(agg 0) / prepare_next: prep shares, statuses (non-canonical share element ->
+    1, tampered prepare message -> 4) and the leader aggregate share."""
+    from oracle import prio3_py as py
+    cfg = CONFIGS[name]
+    o = oracle_lib.Oracle(**cfg)
+    t = py.Prio3Type(cfg["kind"], **{k: v for k, v in cfg.items() if k != "kind"})
+    v = py.Prio3(t)
+    rnd = random.Random(name + "leader")
+    vk = bytes(range(16))
+    reps = []
+    for i in range(12):
+        m = _meas(rnd, cfg)
+        nonce = bytes(rnd.randrange(256) for _ in range(16))
+        pub, ls, hs = v.shard(m, nonce, bytes(rnd.randrange(256) for _ in range(o.rand_size)))
+        reps.append(dict(nonce=nonce, pub=pub, ls=bytearray(ls), hs=hs))
+    reps[2]["ls"][0:o.es] = b"\xff" * o.es                 # non-canonical element
+    exp_ps, exp_st, msgs, tot = [], [], [], [0] * t.out_len
+    for i, r in enumerate(reps):
+        try:
+            st0, ps0, _ = v.prepare_init(vk, 0, r["nonce"], r["pub"], bytes(r["ls"]))
+        except ValueError:
+            exp_ps.append(bytes(o.prep_share_len)), exp_st.append(1), msgs.append(bytes(16))
+            continue
+        st1, ps1, _ = v.prepare_init(vk, 1, r["nonce"], r["pub"], r["hs"])
+        msg = bytearray(v.prep_shares_to_prep_msg(ps0, ps1))
+        if i == 5 and msg:
+            msg[0] ^= 1
+        exp_ps.append(ps0), msgs.append(bytes(msg) or bytes(16))
+        if i == 5 and msg:
+            exp_st.append(4)
+            continue
+        exp_st.append(0)
+        tot = [(a + b) % t.F.p for a, b in zip(tot, v.prepare_next(st0, bytes(msg)))]
+    n = len(reps)
+    A = lambda k, w: np.array([np.frombuffer(bytes(r[k]), np.uint8) for r in reps]).reshape(n, w)
+    ps, st, agg, cnt = o.leader_batch(
+        vk, A("nonce", 16), A("pub", o.public_share_len) if o.public_share_len else None,
+        A("ls", o.leader_share_len), np.array([np.frombuffer(m, np.uint8) for m in msgs]),
+        n_threads=3, job_size=4)
+    assert st.tolist() == exp_st
+    assert [bytes(x) for x in ps] == exp_ps
+    assert oracle_lib.decode_elems(agg[0], o.es) == tot and int(cnt[0]) == exp_st.count(0)
+
+
 def test_invalid_measurements_rejected(oracle_lib):
     """Soundness smoke: a two-hot histogram and a bucket value of 2, proven honestly over the
     invalid encoding, fail decide (status 3)."""
