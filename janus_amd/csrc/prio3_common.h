@@ -608,6 +608,7 @@ struct prio3_engine {
   int qh_prefetch = 1;
   int qh_occ = 3;
   int qh_regs = 0;
+  int slow_rpl = 16;  // k_xof_slow reports per lane (16; 1 = the round-1 grid)
   int qpair = 0;  // option: P = 16/32 query on lane pairs (k_query_pair; A/B: slower)
   // option: helper XOF on lane pairs (k_xof_pair): -1 auto (shares of >= 2048 elements), 0, 1
   int xof_pair = -1;

@@ -753,9 +753,8 @@ __global__ __launch_bounds__(64) void k_leader_slowfix(DevParams p, InPtrs in, S
 // ------------------------------------------------------------------------------------
 // (byte-level sponge helpers BX / bx_* live in prio3_common.h)
 template <class F>
-__global__ __launch_bounds__(64) void k_xof_slow(DevParams p, InPtrs in, Scratch sc) {
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= p.n || sc.flag[r] == 0) return;
+__device__ __noinline__ void xof_slow_one(const DevParams& p, const InPtrs& in, const Scratch& sc,
+                                          uint32_t r) {
   uint32_t nonce[4], km[4], kp[4], kb[4] = {0, 0, 0, 0};
   load16(in.nonces + 16 * (size_t)r, nonce);
   const uint8_t* hs = in.helper + (size_t)r * p.helper_share_len;
@@ -844,6 +843,35 @@ __global__ __launch_bounds__(64) void k_xof_slow(DevParams p, InPtrs in, Scratch
   }
   sc.flag[r] = 0;
 }
+
+// The slow path's launch: each lane scans the flags of 16 reports with one 16-byte load and
+// re-runs the byte-level XOF only for flagged ones (a rejection has probability ~2^-59 per
+// Field128 element, so in practice every lane exits after its one load; the old one-lane-per-
+// report grid of 64-thread blocks cost a mean 15 us per launch).
+template <class F, int RPL = 16>
+__global__ __launch_bounds__(64) void k_xof_slow(DevParams p, InPtrs in, Scratch sc) {
+  const uint32_t r0 = (blockIdx.x * blockDim.x + threadIdx.x) * RPL;
+  if (r0 >= p.n) return;
+  const uint8_t* fl = sc.flag + r0;
+  uint32_t any = 0;
+  if (RPL == 16 && r0 + 16 <= p.n && ((uintptr_t)fl & 15) == 0) {
+    const uint4 v = *(const uint4*)fl;
+    any = v.x | v.y | v.z | v.w;
+  } else {
+    for (uint32_t i = 0; i < RPL && r0 + i < p.n; i++) any |= fl[i];
+  }
+  if (!any) return;
+  for (uint32_t i = 0; i < RPL && r0 + i < p.n; i++)
+    if (fl[i]) xof_slow_one<F>(p, in, sc, r0 + i);
+}
+
+// launch geometry of k_xof_slow: 16 reports per lane, one wave per block (a one-wave block
+// needs one SIMD with room for it, not four on one CU, beside the other streams' kernels)
+static inline uint32_t slow_blocks(uint32_t n) { return (n + 1023) / 1024; }
+// option slow_rpl=1: the round-1 geometry (one report per lane), kept for A/B
+template <class F>
+static void launch_xof_slow(const prio3_engine* e, const DevParams& p, const InPtrs& in,
+                            const Scratch& sc, hipStream_t st);
 
 // ------------------------------------------------------------------------------------
 // k_query: FLP query + decide + prepare message + prepare_next + truncate
@@ -1251,7 +1279,6 @@ __global__ __launch_bounds__(256, OCC) void k_query_h(DevParams p, InPtrs in, Sc
   sum128 Ssum;
   sum_zero(Ssum);
   T G = F::zero(), rj = r0;
-  const T Z = F::zero();
   for (uint32_t jg = 0; jg < C; jg += GS) {
     mac128 Aa[GS], Bb[GS];
     T mc[GS];
@@ -2475,6 +2502,15 @@ static bool own_out(const DevParams& d) {  // the output share is not the measur
 
 constexpr uint32_t WCH_HOST = 32;  // waves per fused-partial chunk (k_agg_waves WCH)
 
+template <class F>
+static void launch_xof_slow(const prio3_engine* e, const DevParams& p, const InPtrs& in,
+                            const Scratch& sc, hipStream_t st) {
+  if (e->slow_rpl == 1)
+    k_xof_slow<F, 1><<<(p.n + 63) / 64, 64, 0, st>>>(p, in, sc);
+  else
+    k_xof_slow<F, 16><<<slow_blocks(p.n), 64, 0, st>>>(p, in, sc);
+}
+
 // Lays the run's buffers out from `base` (nullptr: sizes only), 256-byte aligned.
 static size_t run_carve(Run* R, unsigned flags, uint32_t n_keys, uint8_t* base) {
   const DevParams& d = R->dp;
@@ -2692,7 +2728,7 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
   if (sc.seg) sc.seg += c0;
   if (sc.wseg) sc.wseg += c0 / 64;
   if (sc.wpart) sc.wpart += (size_t)(c0 / 64) * dp.meas_len * 8;
-  const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
+  const uint32_t blocks = (n + 255) / 256;
   if (dp.kind == PRIO3_SUMVEC_F64_MP) {
     int rc = PRIO3_OK;
     TIMED(e, st, "k_mp64_prepare", (rc = launch_mp64(e, n, dp.ld, in, out, sc, st)));
@@ -2742,7 +2778,7 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
       qs.corrected += col;
       qs.flag += col;
       qs.out = (uint8_t*)sc.out + es * s0;
-      const uint32_t qb = (q.n + 255) / 256, qb64 = (q.n + 63) / 64;
+      const uint32_t qb = (q.n + 255) / 256;
       // k_xofd (two live Keccak states: share squeeze + joint-rand absorb) unless A/B-ed off;
       // both dual-sponge kernels decode the entries (the output share) as they squeeze
       const bool dual = e->split_xof == 2 && (42 + dp.meas_len * 16) / 168 >= 2;
@@ -2757,7 +2793,7 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
         TIMED(e, ss, "k_xofd", (k_xofd<false><<<qb, 256, 0, ss>>>(q, qi, qs)));
       else
         TIMED(e, ss, "k_xof", (k_xof<Fp128><<<qb, 256, 0, ss>>>(q, qi, qs)));
-      TIMED(e, ss, "k_xof_slow", (k_xof_slow<Fp128><<<qb64, 64, 0, ss>>>(q, qi, qs)));
+      TIMED(e, ss, "k_xof_slow", launch_xof_slow<Fp128>(e, q, qi, qs, ss));
       if (e->fp_wide && fpvec_query_wide_takes(q))
         TIMED(e, ss, "k_query_fpw", launch_fpvec_query(q, qi, qs, qo, ss, -e->fp_wgs));
       else
@@ -2800,7 +2836,7 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
     } else {
       TIMED(e, st, "k_xof", (k_xof<Fp128><<<blocks, 256, 0, st>>>(dp, in, sc)));
     }
-    TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp128><<<blocks64, 64, 0, st>>>(dp, in, sc)));
+    TIMED(e, st, "k_xof_slow", launch_xof_slow<Fp128>(e, dp, in, sc, st));
     bool done = false;
     if (ps && e->qpair && (dp.P == 32 || dp.P == 16)) {
       TIMED(e, st, "k_query_pair", (done = launch_query_pair(dp, in, sc, out, st)));
@@ -2827,7 +2863,7 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
       TIMED(e, st, "k_query", (k_query<Fp128><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
   } else {
     TIMED(e, st, "k_xof", (k_xof<Fp64><<<blocks, 256, 0, st>>>(dp, in, sc)));
-    TIMED(e, st, "k_xof_slow", (k_xof_slow<Fp64><<<blocks64, 64, 0, st>>>(dp, in, sc)));
+    TIMED(e, st, "k_xof_slow", launch_xof_slow<Fp64>(e, dp, in, sc, st));
     TIMED(e, st, "k_query", (k_query<Fp64><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
   }
   return PRIO3_OK;
@@ -3274,6 +3310,7 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
   } ints[] = {{"force_slow_path", &e->force_slow}, {"chunks", &e->chunks},
               {"leader_fast", &e->leader_fast},    {"fuse_acc", &e->fuse_acc},
               {"qh_regs", &e->qh_regs},            {"qh_occ", &e->qh_occ},
+              {"slow_rpl", &e->slow_rpl},
               {"qh_prefetch", &e->qh_prefetch},    {"split_xof", &e->split_xof},
               {"qpair", &e->qpair},                {"timing", &e->timing},
               {"coalesce", &e->coalesce},          {"experimental_fpvec", &e->experimental_fpvec},
