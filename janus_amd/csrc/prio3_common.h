@@ -56,6 +56,8 @@ struct DevParams {
   // 1: the helper XOF kernel also truncates the measurement share into the output-share
   // scratch (TruncSink); the query kernel then leaves sc.out alone
   uint32_t trunc_xof;
+  // 1: the prepare message is not re-hashed (see prep_msg_check)
+  uint32_t msg_cmp;
 };
 
 struct InPtrs {
@@ -131,6 +133,40 @@ DEV void load16(const uint8_t* p, uint32_t* w) {
   w[1] = v.y;
   w[2] = v.z;
   w[3] = v.w;
+}
+
+// The helper's prepare message and its prepare_next check (prio Prio3:
+// prepare_shares_to_prepare_message hashes the two joint-rand parts of the prep shares into the
+// joint-rand seed; prepare_next requires it to equal the corrected seed, which the XOF kernel
+// derived from the leader part of the public share and the helper's own part).  Both hashes take
+// the same helper part, so with msg_cmp the message is the corrected seed when the leader's part
+// in its prep share equals the one in the public share, and the check fails otherwise -- the
+// hashed result except on a TurboSHAKE128 collision of 16-byte outputs.  Returns true if the
+// check passes; msg gets the message.
+DEV bool prep_msg_check(const DevParams& p, const InPtrs& in, const Scratch& sc, uint32_t r,
+                        const uint32_t lpart[4], uint32_t msg[4]) {
+  const uint4 cor = sc.corrected[r];
+  if (p.msg_cmp) {
+    uint32_t pl[4];
+    load16(in.pub + (size_t)r * p.public_share_len, pl);
+    msg[0] = cor.x, msg[1] = cor.y, msg[2] = cor.z, msg[3] = cor.w;
+    return ((lpart[0] ^ pl[0]) | (lpart[1] ^ pl[1]) | (lpart[2] ^ pl[2]) | (lpart[3] ^ pl[3])) == 0;
+  }
+  uint32_t hpart[4];
+  {
+    const uint4 hp = sc.part[r];
+    hpart[0] = hp.x, hpart[1] = hp.y, hpart[2] = hp.z, hpart[3] = hp.w;
+  }
+  KState s;
+  kzero(s);
+  Msg mm;
+  msg_zero(mm);
+  msg_dst(mm, p.dst[6]);
+  msg_bytes16(mm, 25, lpart);
+  msg_bytes16(mm, 41, hpart);
+  msg_absorb_final(s, mm, 57);
+  msg[0] = kword(s, 0), msg[1] = kword(s, 1), msg[2] = kword(s, 2), msg[3] = kword(s, 3);
+  return msg[0] == cor.x && msg[1] == cor.y && msg[2] == cor.z && msg[3] == cor.w;
 }
 
 // ------------------------------------------------------------------------------------
@@ -608,6 +644,8 @@ struct prio3_engine {
   int qh_prefetch = 1;
   int qh_occ = 3;
   int qh_regs = 0;
+  int msg_cmp = 0;   // prepare message by part comparison instead of a re-hash (prep_msg_check)
+  int qwide32 = 0;   // P = 32 (Histogram 256/16) on k_query_w instead of k_query_h
   int slow_rpl = 16;  // k_xof_slow reports per lane (16; 1 = the round-1 grid)
   int qpair = 0;  // option: P = 16/32 query on lane pairs (k_query_pair; A/B: slower)
   // option: helper XOF on lane pairs (k_xof_pair): -1 auto (shares of >= 2048 elements), 0, 1

@@ -1381,27 +1381,9 @@ __global__ __launch_bounds__(256, OCC) void k_query_h(DevParams p, InPtrs in, Sc
     else if (!F::is_zero(V0) || !F::eq(G, PT))
       status = PRIO3_STATUS_PREP_MSG;
   }
-  uint32_t lpart[4], hpart[4];
+  uint32_t lpart[4], msg[4];
   load16(lps + (size_t)p.verifier_len * F::ES, lpart);
-  {
-    uint4 hp = sc.part[r];
-    hpart[0] = hp.x;
-    hpart[1] = hp.y;
-    hpart[2] = hp.z;
-    hpart[3] = hp.w;
-  }
-  KState s;
-  kzero(s);
-  Msg mm;
-  msg_zero(mm);
-  msg_dst(mm, p.dst[6]);
-  msg_bytes16(mm, 25, lpart);
-  msg_bytes16(mm, 41, hpart);
-  msg_absorb_final(s, mm, 57);
-  uint4 cor = sc.corrected[r];
-  uint32_t msg[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
-  if (status == PRIO3_STATUS_FINISHED &&
-      (msg[0] != cor.x || msg[1] != cor.y || msg[2] != cor.z || msg[3] != cor.w))
+  if (!prep_msg_check(p, in, sc, r, lpart, msg) && status == PRIO3_STATUS_FINISHED)
     status = PRIO3_STATUS_PREP_NEXT;
   if (status != PRIO3_STATUS_FINISHED) msg[0] = msg[1] = msg[2] = msg[3] = 0;
   ((uint4*)out.prep_msgs)[r] = make_uint4(msg[0], msg[1], msg[2], msg[3]);
@@ -2809,13 +2791,14 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
   if (dp.es == 16) {
     const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
     const bool wide = ps && e->qwide && !(e->qpair && (dp.P == 32 || dp.P == 16)) &&
-                      query_wide_takes(dp);
+                      (dp.P != 32 || e->qwide32) && query_wide_takes(dp);
     const bool pair_xof =
         !fuse && e->xof_pair > 0;  // auto: off (SumVec 8x1000 A/B: 15.0 vs 12.8 ms, r02j)
     const bool dual = dp.jr_len && e->split_xof == 2 && (42 + dp.meas_len * 16) / 168 >= 2;
     // SumVec under k_query_w: the truncation rides on the XOF's squeeze (the query then reads
     // the share once)
     dp.trunc_xof = dp.kind == PRIO3_SUMVEC && wide && dual && !fuse && e->trunc_xof ? 1u : 0u;
+    dp.msg_cmp = e->msg_cmp ? 1u : 0u;
     bool paired = false;
     if (dual && pair_xof)
       TIMED(e, st, "k_xof_pair", (paired = launch_xof_pair(dp, in, sc, st)));
@@ -3201,7 +3184,7 @@ int prio3_engine_create_ex(const prio3_params* params, const uint8_t* verify_key
   ws_stream_put(device, probe);  // the first member of the GPU's stream pool
   const bool fpv = e->dp.kind == PRIO3_FPVEC_BOUNDED_L2;
   if (((e->dp.kind == PRIO3_HISTOGRAM || e->dp.kind == PRIO3_SUMVEC) &&
-       (e->dp.P == 64 || e->dp.P == 128)) ||
+       (e->dp.P == 32 || e->dp.P == 64 || e->dp.P == 128)) ||
       (fpv && e->dp.logP <= 10 && e->dp.logP1 <= 10)) {
     // k_query_w / k_query_fpw: sigma_e = sum_(c=1..calls) alpha_P^(ce), e < P -- the weights of
     // sum_c p(alpha^c) over the polynomial's coefficients (FPVec: gadget 0's table, then gadget
@@ -3310,7 +3293,8 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
   } ints[] = {{"force_slow_path", &e->force_slow}, {"chunks", &e->chunks},
               {"leader_fast", &e->leader_fast},    {"fuse_acc", &e->fuse_acc},
               {"qh_regs", &e->qh_regs},            {"qh_occ", &e->qh_occ},
-              {"slow_rpl", &e->slow_rpl},
+              {"slow_rpl", &e->slow_rpl},          {"qwide32", &e->qwide32},
+              {"msg_cmp", &e->msg_cmp},
               {"qh_prefetch", &e->qh_prefetch},    {"split_xof", &e->split_xof},
               {"qpair", &e->qpair},                {"timing", &e->timing},
               {"coalesce", &e->coalesce},          {"experimental_fpvec", &e->experimental_fpvec},

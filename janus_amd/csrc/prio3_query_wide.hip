@@ -1,6 +1,7 @@
 // prio3_query_wide.hip -- the helper FLP query + decide for ParallelSum(Mul, C) circuits with a
-// 64- or 128-point wire-polynomial domain (Prio3SumVec bits=8 length=1000 chunk 63: 127 gadget
-// calls, P = 128), EIGHT lanes per report (MI355X, gfx950).
+// 32-, 64- or 128-point wire-polynomial domain (Prio3SumVec bits=8 length=1000 chunk 63: 127 gadget
+// calls, P = 128; Prio3Histogram(256, 16): P = 32, option qwide32), EIGHT lanes per report
+// (MI355X, gfx950).
 //
 // prio 0.16.2 FlpGeneric::query + decide, helper side of
 // Prio3::prepare_init / prepare_shares_to_prepare_message; call site helper_initialized,
@@ -100,11 +101,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS == 2 ? 3
 #pragma unroll
     for (int i = 0; i < 3; i++) tP = F::mul(tP, tP);
     if (F::eq(tP, one)) status = PRIO3_STATUS_PREP_INIT;  // t is a P-th root of unity
-    // tw128[k] = alpha_PQ^k (k < PQ/2), tw128[8 + i] = alpha_P^i (i < 8); alpha_8 = alpha_PQ^(PQ/8)
-    const T w8l = lane_pow(F::from_words(p.tw128[PQ / 8]), F::from_words(p.tw128[PQ / 4]),
+    // P = 64 / 128: tw128[k] = alpha_PQ^k (k < PQ/2), tw128[8 + i] = alpha_P^i (i < 8), so
+    // alpha_8 = alpha_PQ^(PQ/8).  P = 32: tw128[i] = alpha_32^i (i < 16), alpha_8 = tw128[4].
+    constexpr int I8 = PQ == 4 ? 4 : PQ / 8, I4 = PQ == 4 ? 8 : PQ / 4;
+    constexpr int IP = PQ == 4 ? 0 : 8;  // alpha_P^i at tw128[IP + i]
+    const T w8l = lane_pow(F::from_words(p.tw128[I8]), F::from_words(p.tw128[I4]),
                            F::sub(Z, one), l);
-    const T wl = lane_pow(F::from_words(p.tw128[9]), F::from_words(p.tw128[10]),
-                          F::from_words(p.tw128[12]), l);
+    const T wl = lane_pow(F::from_words(p.tw128[IP + 1]), F::from_words(p.tw128[IP + 2]),
+                          F::from_words(p.tw128[IP + 4]), l);
     const T z = F::mul(tq, w8l);
     T g = F::add(z, one);
 #pragma unroll
@@ -116,7 +120,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS == 2 ? 3
       x[__builtin_bitreverse32(n2) >> (32 - LOGQ)] = y;
       if (n2 + 1 < PQ) y = F::mul(y, ratio);
     }
-    dft_reg<PQ, LOGQ>(p, x, 1);
+    dft_reg<PQ, LOGQ>(p, x, PQ == 4 ? 8 : 1);  // P = 32: alpha_4^i = alpha_32^(8i)
   }
   // x[m] = L_c, c = (P - 8m - l) mod P.  L_0 is lane 0's x[0].
   const T L0 = shfl128(x[0], (int)(threadIdx.x & 56u));
@@ -281,25 +285,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS == 2 ? 3
     }
     // prepare message: joint-rand seed of (leader part, helper part), checked against the
     // corrected seed (prepare_next)
-    uint32_t lpart[4], hpart[4];
+    uint32_t lpart[4], msg[4];
     load16(lps + (size_t)p.verifier_len * F::ES, lpart);
-    const uint4 hp = sc.part[r];
-    hpart[0] = hp.x;
-    hpart[1] = hp.y;
-    hpart[2] = hp.z;
-    hpart[3] = hp.w;
-    KState ks;
-    kzero(ks);
-    Msg mm;
-    msg_zero(mm);
-    msg_dst(mm, p.dst[6]);
-    msg_bytes16(mm, 25, lpart);
-    msg_bytes16(mm, 41, hpart);
-    msg_absorb_final(ks, mm, 57);
-    const uint4 cor = sc.corrected[r];
-    uint32_t msg[4] = {kword(ks, 0), kword(ks, 1), kword(ks, 2), kword(ks, 3)};
-    if (status == PRIO3_STATUS_FINISHED &&
-        (msg[0] != cor.x || msg[1] != cor.y || msg[2] != cor.z || msg[3] != cor.w))
+    if (!prep_msg_check(p, in, sc, r, lpart, msg) && status == PRIO3_STATUS_FINISHED)
       status = PRIO3_STATUS_PREP_NEXT;
     if (status != PRIO3_STATUS_FINISHED) msg[0] = msg[1] = msg[2] = msg[3] = 0;
     ((uint4*)out.prep_msgs)[r] = make_uint4(msg[0], msg[1], msg[2], msg[3]);
@@ -329,10 +317,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS == 2 ? 3
 
 }  // namespace
 
-// true if launched: ParallelSum(Mul) instances (Histogram, SumVec with bits <= 32) with P = 64 or
-// 128 and the engine's sigma table
+// true if launched: ParallelSum(Mul) instances (Histogram, SumVec with bits <= 32) with P = 32, 64
+// or 128 and the engine's sigma table
 bool query_wide_takes(const DevParams& p) {
-  if (p.es != 16 || !p.sigma_dev || (p.P != 64 && p.P != 128)) return false;
+  if (p.es != 16 || !p.sigma_dev || (p.P != 32 && p.P != 64 && p.P != 128)) return false;
   if (p.kind != PRIO3_HISTOGRAM && p.kind != PRIO3_SUMVEC) return false;
   if (p.kind == PRIO3_SUMVEC && p.bits > 32) return false;
   return p.calls + 1 <= p.P && p.glen == 2 * p.P - 1 && p.arity == 2 * p.chunk;
@@ -349,6 +337,10 @@ bool launch_query_wide(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, h
       k_query_w<16, 4, 3><<<blocks, 256, 0, st>>>(p, in, sc, out);
     else
       k_query_w<16, 4, 4><<<blocks, 256, 0, st>>>(p, in, sc, out);
+    return true;
+  }
+  if (p.P == 32) {  // Prio3Histogram(256, 16): two columns per lane, one sweep
+    k_query_w<4, 2, 2><<<blocks, 256, 0, st>>>(p, in, sc, out);
     return true;
   }
   if (p.P == 64) {

@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(cfg, n, seed, n_segments=1, seg_mode="runs", tamper=True, accept_frac=0.9,
-         force_slow=False, fuse=True, chunks=None, oob_frac=0.0):
+         force_slow=False, fuse=True, chunks=None, oob_frac=0.0, opts=None):
     import torch
     o = _oracle(cfg)
     eng = _engine(cfg)
@@ -26,6 +26,8 @@ def _run(cfg, n, seed, n_segments=1, seg_mode="runs", tamper=True, accept_frac=0
         eng.set_option("force_slow_path", 1)
     if chunks is not None:
         eng.set_option("chunks", chunks)
+    for k, v in (opts or {}).items():
+        eng.set_option(k, v)
     d = o.gen_reports(VK, n, seed=seed, n_threads=8)
     rng = np.random.default_rng(seed)
     if tamper:
@@ -102,6 +104,15 @@ def test_prepare_aggregate_other_instances(name):
 
 def test_fused_off_matches():
     _run(CONFIGS["hist_256_c16"], 700, seed=9, n_segments=2, fuse=False)
+
+
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_fused_wide_query_p32(chunks):
+    """The fused path with the eight-lane P = 32 query (option qwide32): tampered reports,
+    segment runs inside waves, stream-overlapped chunks, the slow path."""
+    _run(CONFIGS["hist_256_c16"], 1500, seed=60 + chunks, n_segments=5, chunks=chunks,
+         opts={"qwide32": 1})
+    _run(CONFIGS["hist_256_c16"], 192, seed=62, force_slow=True, opts={"qwide32": 1})
 
 
 @pytest.mark.parametrize("chunks", [2, 3, 5])

@@ -236,6 +236,26 @@ def test_query_wide_parity(name, gs):
     _check_against_oracle(CONFIGS[name], n, seed=19 + gs, opts={"qwide": 1, "qw_gs": gs})
 
 
+@pytest.mark.parametrize("opts", [{"msg_cmp": 1}, {"msg_cmp": 1, "qwide32": 1},
+                                  {"msg_cmp": 1, "chunks": 3, "coalesce": 0}])
+@pytest.mark.parametrize("name", ["hist_256_c16", "sumvec_8x1000_c63", "hist_500_c8"])
+def test_prepare_message_by_part_comparison(name, opts):
+    """Option msg_cmp: the prepare message is the corrected seed when the leader's joint-rand
+    part in its prep share equals the public share's (prep_msg_check), the same bytes and
+    statuses as re-hashing the parts, tampered parts and public shares included."""
+    n = 101 if "1000" in name else 700
+    _check_against_oracle(CONFIGS[name], n, seed=59, opts=opts)
+
+
+@pytest.mark.parametrize("name", ["hist_256_c16", "sumvec_2x100_c10", "hist_100_c4"])
+def test_query_wide_p32_parity(name):
+    """P = 32 on eight lanes (option qwide32, k_query_w<4, 2, 2>): two columns per lane in one
+    sweep; the headline Histogram(256, 16) instance, fused and unfused, with the slow path."""
+    _check_against_oracle(CONFIGS[name], 333, seed=43, opts={"qwide32": 1})
+    _check_against_oracle(CONFIGS[name], 97, seed=47, opts={"qwide32": 1}, force_slow=True)
+    _check_against_oracle(CONFIGS[name], 300, seed=53, opts={"qwide32": 1, "fuse_acc": 0})
+
+
 @pytest.mark.parametrize("name", ["sumvec_8x1000_c63", "hist_500_c8"])
 def test_query_wide_off_and_slow_path(name):
     """The one-lane k_query_ps stays selectable; the rejection-sampling XOF feeds k_query_w."""
