@@ -58,6 +58,9 @@ struct DevParams {
   uint32_t trunc_xof;
   // 1: the prepare message is not re-hashed (see prep_msg_check)
   uint32_t msg_cmp;
+  // Prio3Sum query (k_query_sum, P = 16 NPH): tws[j] = w16^j (j < 8), tws[8 + i] = alpha_P^i
+  // (i < 8), tws[16 + i] = alpha_P^(16 i) (i < 8)
+  uint32_t tws[24][4];
 };
 
 struct InPtrs {
@@ -568,6 +571,10 @@ struct Mp64Params {
 };
 
 struct prio3_engine;
+// prio3_query_sum.hip: true if launched (Prio3Sum with 16 <= P <= 128)
+bool query_sum_takes(const DevParams& p);
+bool launch_query_sum(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
+                      int occ);
 int launch_mp64(prio3_engine* e, uint32_t n, uint32_t ld, InPtrs in, OutPtrs out, Scratch sc,
                 hipStream_t st);
 int launch_mp64_leader(prio3_engine* e, uint32_t n, uint32_t ld, InPtrs in, OutPtrs out,
@@ -644,6 +651,8 @@ struct prio3_engine {
   int qh_prefetch = 1;
   int qh_occ = 3;
   int qh_regs = 0;
+  int qsum = 1;      // Prio3Sum on k_query_sum (0: the generic k_query)
+  int qsum_occ = 3;  // k_query_sum waves per SIMD (2 or 3)
   int msg_cmp = 0;   // prepare message by part comparison instead of a re-hash (prep_msg_check)
   int qwide32 = 0;   // P = 32 (Histogram 256/16) on k_query_w instead of k_query_h
   int slow_rpl = 16;  // k_xof_slow reports per lane (16; 1 = the round-1 grid)

@@ -2345,6 +2345,16 @@ static int fill_sizes(const prio3_params* pp, prio3_sizes_t* s, DevParams* dp) {
         for (int k = 0; k < 4; k++) d.tw128[8 + i][k] = (uint32_t)(w >> (32 * k));
       }
     }
+    if (d.P >= 16 && d.P <= 128) {  // k_query_sum's twiddles
+      u128 alpha = 0;
+      for (int k = 0; k < 4; k++) alpha |= (u128)d.roots128[d.logP][k] << (32 * k);
+      const u128 w16 = hpow(alpha, d.P / 16, HP128), a16 = hpow(alpha, 16, HP128);
+      for (uint32_t i = 0; i < 8; i++) {
+        const u128 v[3] = {hpow(w16, i, HP128), hpow(alpha, i, HP128), hpow(a16, i, HP128)};
+        for (int t = 0; t < 3; t++)
+          for (int k = 0; k < 4; k++) d.tws[8 * t + i][k] = (uint32_t)(v[t] >> (32 * k));
+      }
+    }
     d.half64 = (uint64_t)hpow(2, HP64 - 2, HP64);
   }
   if (s) {
@@ -2842,8 +2852,12 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
       TIMED(e, st, "k_query_h", (k_query_h<2, 8><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
     else if (ps)
       TIMED(e, st, "k_query_ps", (k_query_ps<4><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
-    else
-      TIMED(e, st, "k_query", (k_query<Fp128><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+    else {
+      bool qs = false;
+      if (e->qsum && query_sum_takes(dp))
+        TIMED(e, st, "k_query_sum", (qs = launch_query_sum(dp, in, sc, out, st, e->qsum_occ)));
+      if (!qs) TIMED(e, st, "k_query", (k_query<Fp128><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+    }
   } else {
     TIMED(e, st, "k_xof", (k_xof<Fp64><<<blocks, 256, 0, st>>>(dp, in, sc)));
     TIMED(e, st, "k_xof_slow", launch_xof_slow<Fp64>(e, dp, in, sc, st));
@@ -3294,7 +3308,8 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
               {"leader_fast", &e->leader_fast},    {"fuse_acc", &e->fuse_acc},
               {"qh_regs", &e->qh_regs},            {"qh_occ", &e->qh_occ},
               {"slow_rpl", &e->slow_rpl},          {"qwide32", &e->qwide32},
-              {"msg_cmp", &e->msg_cmp},
+              {"msg_cmp", &e->msg_cmp},            {"qsum", &e->qsum},
+              {"qsum_occ", &e->qsum_occ},
               {"qh_prefetch", &e->qh_prefetch},    {"split_xof", &e->split_xof},
               {"qpair", &e->qpair},                {"timing", &e->timing},
               {"coalesce", &e->coalesce},          {"experimental_fpvec", &e->experimental_fpvec},

@@ -26,6 +26,12 @@ CONFIGS = {
     "sum8": dict(kind="sum", bits=8),
     "sum32": dict(kind="sum", bits=32),
     "sum1": dict(kind="sum", bits=1),
+    # k_query_sum domains: P = 16 (b = 15), 32 (b = 1), 64 (b = 0 and 2), 128 (b = 0)
+    "sum15": dict(kind="sum", bits=15),
+    "sum17": dict(kind="sum", bits=17),
+    "sum32": dict(kind="sum", bits=32),
+    "sum50": dict(kind="sum", bits=50),
+    "sum64": dict(kind="sum", bits=64),
     "sumvec_8x10_c9": dict(kind="sumvec", bits=8, length=10, chunk_length=9),
     "sumvec_1x1_c1": dict(kind="sumvec", bits=1, length=1, chunk_length=1),
     "sumvec_8x1000_c63": dict(kind="sumvec", bits=8, length=1000, chunk_length=63),

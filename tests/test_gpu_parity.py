@@ -247,6 +247,18 @@ def test_prepare_message_by_part_comparison(name, opts):
     _check_against_oracle(CONFIGS[name], n, seed=59, opts=opts)
 
 
+@pytest.mark.parametrize("occ", [3, 2])
+@pytest.mark.parametrize("name", ["sum8", "sum15", "sum17", "sum32", "sum50", "sum64"])
+def test_query_sum_parity(name, occ):
+    """Prio3Sum on k_query_sum (P = 16..128 as NPH phases of an in-register DFT16; the
+    validity weights with 16 | bits applied per phase, else per element): tampered reports,
+    the slow path, and the generic k_query it replaces."""
+    _check_against_oracle(CONFIGS[name], 700, seed=61, opts={"qsum_occ": occ})
+    if occ == 3:
+        _check_against_oracle(CONFIGS[name], 130, seed=67, force_slow=True)
+        _check_against_oracle(CONFIGS[name], 300, seed=71, opts={"qsum": 0})
+
+
 @pytest.mark.parametrize("name", ["hist_256_c16", "sumvec_2x100_c10", "hist_100_c4"])
 def test_query_wide_p32_parity(name):
     """P = 32 on eight lanes (option qwide32, k_query_w<4, 2, 2>): two columns per lane in one
