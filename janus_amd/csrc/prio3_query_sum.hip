@@ -19,7 +19,8 @@
 //     s(n) = sum over i of (r^16 alpha^(16 ph))^i for 1 <= n + 16 i <= K -- three distinct
 //     values; when 16 | K (Sum(32), Sum(64)) s is constant for n >= 1 and is applied once per
 //     phase instead of per element;
-//   * p(t) by Horner; the truncation sum_b 2^b m_b by shift-and-add over a 160-bit accumulator.
+//   * p(t) as 16-coefficient blocks of lazy MACs against t^0..t^15, Horner in t^16 across the
+//     blocks; the truncation sum_b 2^b m_b by shift-and-add over a 160-bit accumulator.
 #include <hip/hip_runtime.h>
 
 #include "../../include/janus_prio3.h"
@@ -156,27 +157,24 @@ __global__ __launch_bounds__(256, OCC) void k_query_sum(DevParams p, InPtrs in, 
     }
   }
   f = F::add(f, F::mul(L0, ldf<F>(sc.proofs, 0, ld, r)));
-  // p(t) by Horner over the GL coefficients (proof elements 1 .. GL)
+  // p(t) = sum_j (t^16)^j sum_(n<16) coef_(16 j + n) t^n: the inner sums as lazy MACs against
+  // t^0..t^15, Horner in t^16 over the GL / 16 blocks (GL = 2P - 1: 2 NPH blocks)
   T pt = Z;
   {
-    constexpr int HD = 4;
-    auto ldc = [&](uint32_t q) {  // coefficient e = GL - 1 - q (clamped)
-      const uint32_t e = q < GL ? GL - 1 - q : 0;
-      return ldf<F>(sc.proofs, 1 + e, ld, r);
-    };
-    T cb[HD];
+    T pw[16];
+    pw[0] = one;
 #pragma unroll
-    for (int q = 0; q < HD; q++) cb[q] = ldc(q);
+    for (int n = 1; n < 16; n++) pw[n] = F::mul(pw[n - 1], t);
 #pragma unroll 1
-    for (uint32_t q0 = 0; q0 < GL; q0 += HD) {
-      T cn[HD];
+    for (uint32_t j = 2 * NPH; j-- > 0;) {
+      mac128 S;
+      mac_zero(S);
 #pragma unroll
-      for (int q = 0; q < HD; q++) cn[q] = ldc(q0 + HD + q);
-#pragma unroll
-      for (int q = 0; q < HD; q++) {
-        if (q0 + q < GL) pt = F::add(F::mul(pt, t), cb[q]);
-        cb[q] = cn[q];
+      for (int n = 0; n < 16; n++) {
+        const uint32_t e = 16 * j + (uint32_t)n;
+        if (e < GL) mac_add(S, ldf<F>(sc.proofs, 1 + e, ld, r), pw[n]);  // uniform
       }
+      pt = F::add(F::mul(pt, t16), mac_reduce_f(S));
     }
   }
   // decide against the leader's verifier share [v, f(t), p(t)]
