@@ -1148,13 +1148,29 @@ __global__ __launch_bounds__(256) void k_query_ps(DevParams p, InPtrs in, Scratc
 // LEADER = 1: the leader's prepare_init (agg_id 0) on the same data flow -- the wire values
 // f_j(t), v and p(t) are written as the leader prepare share (out.prep_msgs is the prepare
 // share buffer, stride prep_share_len) instead of being decided against a peer's share.
-template <int GS, int PP, int PF = 1, int OCC = 3, int LEADER = 0>
+// FUSE: the fused accumulate rides on the query instead of the XOF (option fuse_q): the sweeps
+// load every measurement-share element exactly once, after the slow path has run, so each wave
+// whose 64 reports share one segment reduces consecutive element pairs over its reports
+// (wave_halfsum2, as k_xofd<true> does) into sc.wpart and writes its segment to sc.wseg.  The
+// query waits on memory about half its cycles, where the XOF is issue-bound.
+template <int GS, int PP, int PF = 1, int OCC = 3, int LEADER = 0, bool FUSE = false>
 __global__ __launch_bounds__(256, OCC) void k_query_h(DevParams p, InPtrs in, Scratch sc,
                                                     OutPtrs out) {
   typedef Fp128 F;
   typedef f128 T;
   constexpr int LOGP = PP <= 2 ? 1 : PP <= 4 ? 2 : PP <= 8 ? 3 : PP <= 16 ? 4 : 5;
+  static_assert(!FUSE || (GS == 2 && !LEADER), "fused pairs need two columns per sweep");
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  bool fuse = false;
+  if constexpr (FUSE) {
+    const bool valid = r < p.n;
+    const uint32_t sg = valid ? (sc.seg ? sc.seg[r] : 0u) : 0xffffffffu;
+    const uint32_t s0 = (uint32_t)__shfl((int)sg, 0);
+    // a segment id >= n_segments excludes the report from every aggregate (never fused)
+    fuse = __all(valid && sg == s0 && sg < p.nseg);
+    if (lane == 0 && (r - lane) < p.n) sc.wseg[r >> 6] = fuse ? s0 : 0xffffffffu;
+  }
   if (r >= p.n) return;
   const size_t ld = p.ld;
   const uint32_t A = p.arity, C = p.chunk, M = p.meas_len, K = p.calls;
@@ -1323,6 +1339,14 @@ __global__ __launch_bounds__(256, OCC) void k_query_h(DevParams p, InPtrs in, Sc
         mac_add(Aa[q], be, mc[q]);
         mac_add(Bb[q], Lk, mc[q]);
         sum_add(Ssum, mc[q]);
+      }
+      if constexpr (FUSE) {
+        const uint32_t i0 = k * C + jg;  // elements i0, i0 + 1 (C even: one call)
+        if (fuse && i0 < M) {             // wave-uniform
+          const uint32_t tot = wave_halfsum2(mc[0], mc[1], lane);
+          const uint32_t e = i0 + ((lane >> 3) & 1u);
+          if (lane < 16 && e < M) sc.wpart[((size_t)(r >> 6) * M + e) * 8u + (lane & 7u)] = tot;
+        }
       }
 #pragma unroll
       for (int q = 0; q < GS; q++) mc[q] = mn[q];
@@ -2812,9 +2836,13 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
     bool paired = false;
     if (dual && pair_xof)
       TIMED(e, st, "k_xof_pair", (paired = launch_xof_pair(dp, in, sc, st)));
+    // option fuse_q: the fused accumulate in k_query_h (P = 32, two columns per sweep, even
+    // chunk) instead of k_xofd
+    const bool fuseq = fuse && e->fuse_q && dual && ps && !wide && dp.P == 32 &&
+                       (dp.chunk & 1u) == 0 && !e->qh_regs && !e->qpair;
     if (paired) {
     } else if (dual) {
-      if (fuse)
+      if (fuse && !fuseq)
         TIMED(e, st, "k_xofd", (k_xofd<true><<<blocks, 256, 0, st>>>(dp, in, sc)));
       else if (dp.trunc_xof)
         TIMED(e, st, "k_xofd", (k_xofd<false, true><<<blocks, 256, 0, st>>>(dp, in, sc)));
@@ -2839,6 +2867,8 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
     if (done) {
     } else if (ps && dp.P == 32 && dp.chunk == 16 && dp.calls == 16 && e->qh_regs)
       TIMED(e, st, "k_query_r", (k_query_r<16, 16><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+    else if (fuseq)
+      TIMED(e, st, "k_query_h", (k_query_h<2, 32, 1, 3, 0, true><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
     else if (ps && dp.P == 32)
       switch (e->qh_prefetch * 10 + e->qh_occ) {
         case 2: TIMED(e, st, "k_query_h", (k_query_h<2, 32, 0, 2><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
@@ -3309,7 +3339,7 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
               {"qh_regs", &e->qh_regs},            {"qh_occ", &e->qh_occ},
               {"slow_rpl", &e->slow_rpl},          {"qwide32", &e->qwide32},
               {"msg_cmp", &e->msg_cmp},            {"qsum", &e->qsum},
-              {"qsum_occ", &e->qsum_occ},
+              {"qsum_occ", &e->qsum_occ},          {"fuse_q", &e->fuse_q},
               {"qh_prefetch", &e->qh_prefetch},    {"split_xof", &e->split_xof},
               {"qpair", &e->qpair},                {"timing", &e->timing},
               {"coalesce", &e->coalesce},          {"experimental_fpvec", &e->experimental_fpvec},

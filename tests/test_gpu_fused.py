@@ -106,6 +106,25 @@ def test_fused_off_matches():
     _run(CONFIGS["hist_256_c16"], 700, seed=9, n_segments=2, fuse=False)
 
 
+@pytest.mark.parametrize("case", ["runs", "random", "slow", "chunks", "tampered_masked"])
+def test_fused_accumulate_in_query(case):
+    """Option fuse_q: the fused accumulate rides on k_query_h instead of k_xofd (wave pairs of
+    elements reduced as the sweeps load them) -- every fix-up path of the fused aggregate."""
+    o = {"fuse_q": 1}
+    cfg = CONFIGS["hist_256_c16"]
+    if case == "runs":
+        _run(cfg, 1500, seed=81, n_segments=7, seg_mode="runs", opts=o)
+    elif case == "random":
+        _run(cfg, 600, seed=82, n_segments=4, seg_mode="random", opts=o)
+    elif case == "slow":
+        _run(cfg, 192, seed=83, force_slow=True, opts=o)
+    elif case == "chunks":
+        _run(cfg, 1500, seed=84, n_segments=5, chunks=3, opts=o, oob_frac=0.02)
+    else:
+        st = _run(cfg, 1000, seed=85, accept_frac=0.8, opts=o)
+        assert (st != 0).any()
+
+
 @pytest.mark.parametrize("chunks", [1, 3])
 def test_fused_wide_query_p32(chunks):
     """The fused path with the eight-lane P = 32 query (option qwide32): tampered reports,
