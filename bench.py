@@ -157,6 +157,9 @@ def main():
     ap.add_argument("--vdaf", choices=["count", "sumvec", "sum32"], default="sumvec",
                     help="--role config: C1 Prio3Count (100k), C3 Prio3SumVec 8x1000 chunk 63 "
                          "(1M/8 per GPU), C4 Prio3Sum 32 (10M/8 per GPU)")
+    ap.add_argument("--leader-vdaf", choices=["hist", "sum32"], default="hist",
+                    help="--role leader: Prio3Histogram(256,16) at 1Mi (default) or Prio3Sum(32) "
+                         "at C4's 1.25M per GPU")
     ap.add_argument("--threads", type=int, default=128,
                     help="--role jobs: host worker threads (Janus's rayon pool)")
     ap.add_argument("--job-size", type=int, default=500,
@@ -498,12 +501,14 @@ def jobs_main(args):
 def leader_main(args):
     """Leader-side line (not the BASELINE metric): one step = leader prepare_init (agg_id 0) on
     the explicit input shares + prepare_next on the helper's prepare messages + accumulate,
-    for the same Histogram(256,16) batch.  The prepare messages are the helper engine's own
-    output on the same reports, computed once before timing."""
+    for a Histogram(256,16) batch (or Prio3Sum(32) at C4's per-GPU share with
+    --leader-vdaf sum32).  The prepare messages are the helper engine's own output on the same
+    reports, computed once before timing."""
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
-    n = args.reports
-    eng = J.HelperEngine(J.Prio3Histogram(256, 16), VK, device=0)
+    hist = args.leader_vdaf == "hist"
+    n = args.reports if (hist or args.reports != 1 << 20) else 10_000_000 // 8
+    eng = J.HelperEngine(J.Prio3Histogram(256, 16) if hist else J.Prio3Sum(32), VK, device=0)
     sz = eng.sz
     data = eng.generate_reports_device(n, seed=0x4A414E5553000002, with_checks=True,
                                        with_leader_inputs=True)
@@ -539,14 +544,16 @@ def leader_main(args):
     per_kernel = {k: dict(ms_total=v[0], launches=v[1], ms_avg=v[0] / max(v[1], 1))
                   for k, v in times.items()}
     same = bool(torch.equal(prep, data["leader_prep_shares"]))
-    out = dict(metric="reports prepared+aggregated/sec (leader, Prio3Histogram len=256)",
+    name = "Prio3Histogram len=256" if hist else "Prio3Sum bits=32"
+    out = dict(metric=f"reports prepared+aggregated/sec (leader, {name})",
                value=n * args.steps / elapsed, unit="reports/s", n_gpus=1, steps=args.steps,
                warmup=args.warmup, ms_per_step=elapsed / args.steps * 1e3,
                higher_is_better=True, scaling="weak", vs_baseline=None,
                dtype="u32 limbs (Field128 mod-p integer arithmetic)",
                data="synthetic: on-device client reports (leader input shares explicit)",
-               config=dict(workload="Prio3Histogram length=256 chunk_length=16 leader "
-                                    "prepare_init+prepare_next+aggregate", reports_per_gpu=n),
+               config=dict(workload=("Prio3Histogram length=256 chunk_length=16" if hist else
+                                     "Prio3Sum bits=32") + " leader prepare_init+prepare_next+"
+                                    "aggregate", reports_per_gpu=n),
                kernels=per_kernel,
                checks=dict(helper_finished=helper_ok,
                            leader_finished=int((lstatus == 0).sum().item()),
@@ -557,7 +564,8 @@ def leader_main(args):
         # prepare_next + aggregate in Janus-sized jobs) on a bounded sample of the same reports
         from oracle.oracle import Oracle, build
         build()
-        o = Oracle("histogram", length=256, chunk_length=16)
+        o = (Oracle("histogram", length=256, chunk_length=16) if hist else
+             Oracle("sum", bits=32))
         th = cpu_threads()
         host = [t.cpu().numpy() for t in (data["nonces"], data["public_shares"],
                                           data["leader_input_shares"], msgs)]

@@ -574,7 +574,7 @@ struct prio3_engine;
 // prio3_query_sum.hip: true if launched (Prio3Sum with 16 <= P <= 128)
 bool query_sum_takes(const DevParams& p);
 bool launch_query_sum(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
-                      int occ);
+                      int occ, bool leader = false);
 int launch_mp64(prio3_engine* e, uint32_t n, uint32_t ld, InPtrs in, OutPtrs out, Scratch sc,
                 hipStream_t st);
 int launch_mp64_leader(prio3_engine* e, uint32_t n, uint32_t ld, InPtrs in, OutPtrs out,

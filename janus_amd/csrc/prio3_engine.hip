@@ -3016,6 +3016,20 @@ static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
             (k_query_h<2, 8, 1, 3, 1><<<blocks, 256, 0, st>>>(dp, in, R->sc, out)));
     return PRIO3_OK;
   }
+  if (dp.kind == PRIO3_SUM && e->qsum && e->leader_fast && query_sum_takes(dp)) {
+    // Prio3Sum: the same unpack / joint-rand kernels, then k_query_sum in its leader role
+    InPtrs in{d_nonces, d_public_shares, d_leader_input_shares, nullptr};
+    OutPtrs out{d_prep_shares, d_status};
+    const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
+    TIMED(e, st, "k_leader_unpack",
+          (k_leader_unpack<<<(n + 63) / 64, 256, 0, st>>>(dp, in, R->sc, d_status)));
+    TIMED(e, st, "k_jrpart", (k_jrpart<false, true><<<blocks, 256, 0, st>>>(dp, in, R->sc)));
+    TIMED(e, st, "k_leader_slowfix",
+          (k_leader_slowfix<<<blocks64, 64, 0, st>>>(dp, in, R->sc)));
+    bool ok = false;
+    TIMED(e, st, "k_query_sum", (ok = launch_query_sum(dp, in, R->sc, out, st, 3, true)));
+    return ok ? PRIO3_OK : PRIO3_EDEVICE;
+  }
   int rc2 = PRIO3_OK;
   TIMED(e, st, "k_leader_init",
         rc2 = launch_leader_init(dp, d_nonces, d_public_shares, d_leader_input_shares, R->sc,

@@ -62,7 +62,11 @@ DEV void geo16(T (&x)[16], T s, const T& q) {
   }
 }
 
-template <int NPH, int OCC>
+// LEADER = 1: the leader's prepare_init (agg_id 0) on the same data flow (after k_leader_unpack
+// and the leader k_jrpart): the verifier share [v, f(t), p(t)] and the joint-rand part go to
+// out.prep_msgs (stride prep_share_len) instead of being decided against a peer's share;
+// out.status holds the unpack verdict on entry.
+template <int NPH, int OCC, int LEADER = 0>
 __global__ __launch_bounds__(256, OCC) void k_query_sum(DevParams p, InPtrs in, Scratch sc,
                                                       OutPtrs out) {
   constexpr uint32_t P = 16 * NPH;
@@ -71,7 +75,7 @@ __global__ __launch_bounds__(256, OCC) void k_query_sum(DevParams p, InPtrs in, 
   const size_t ld = p.ld;
   const uint32_t K = p.calls, GL = p.glen;
   const T one = F::one(), Z = F::zero();
-  uint8_t status = PRIO3_STATUS_FINISHED;
+  uint8_t status = LEADER ? out.status[r] : PRIO3_STATUS_FINISHED;
   const T t = ldf<F>(sc.qr, 0, ld, r);
   T t16 = F::mul(t, t);
   t16 = F::mul(t16, t16);
@@ -177,6 +181,14 @@ __global__ __launch_bounds__(256, OCC) void k_query_sum(DevParams p, InPtrs in, 
       pt = F::add(F::mul(pt, t16), mac_reduce_f(S));
     }
   }
+  if constexpr (LEADER) {
+    uint8_t* lout = out.prep_msgs + (size_t)r * p.prep_share_len;
+    F::store(lout, 0, v);
+    F::store(lout, 1, f);
+    F::store(lout, 2, pt);
+    *(uint4*)(lout + (size_t)p.verifier_len * F::ES) = sc.part[r];
+    out.status[r] = status;
+  } else {
   // decide against the leader's verifier share [v, f(t), p(t)]
   const uint8_t* lps = in.leader + (size_t)r * p.prep_share_len;
   bool decode_ok = true;
@@ -202,6 +214,7 @@ __global__ __launch_bounds__(256, OCC) void k_query_sum(DevParams p, InPtrs in, 
   if (status != PRIO3_STATUS_FINISHED) msg[0] = msg[1] = msg[2] = msg[3] = 0;
   ((uint4*)out.prep_msgs)[r] = make_uint4(msg[0], msg[1], msg[2], msg[3]);
   out.status[r] = status;
+  }
   // truncate: sum_b 2^b m_b
   if (K <= 32) {  // shift-and-add over 160 bits (< 2^160 for at most 32 steps)
     sum128 acc;
@@ -236,12 +249,14 @@ bool query_sum_takes(const DevParams& p) {
 }
 
 bool launch_query_sum(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
-                      int occ) {
+                      int occ, bool leader) {
   if (!query_sum_takes(p) || p.n == 0) return false;
   const uint32_t blocks = (p.n + 255) / 256;
 #define QS(N)                                                             \
   do {                                                                    \
-    if (occ == 2)                                                         \
+    if (leader)                                                           \
+      k_query_sum<N, 3, 1><<<blocks, 256, 0, st>>>(p, in, sc, out);       \
+    else if (occ == 2)                                                    \
       k_query_sum<N, 2><<<blocks, 256, 0, st>>>(p, in, sc, out);          \
     else                                                                  \
       k_query_sum<N, 3><<<blocks, 256, 0, st>>>(p, in, sc, out);          \

@@ -20,8 +20,8 @@ def _measurement(cfg, rng):
     k = cfg["kind"]
     if k == "count":
         return int(rng.integers(0, 2))
-    if k == "sum":
-        return int(rng.integers(0, 1 << cfg["bits"]))
+    if k == "sum":  # up to 64 bits (beyond numpy's int64 bounds)
+        return int.from_bytes(rng.bytes(8), "little") >> (64 - cfg["bits"])
     if k == "sumvec":
         return [int(x) for x in rng.integers(0, 1 << cfg["bits"], cfg["length"])]
     return int(rng.integers(0, cfg["length"]))
@@ -43,7 +43,7 @@ def _reports(o, cfg, n, seed):
 
 @pytest.mark.parametrize("fast", [1, 0])
 @pytest.mark.parametrize("name", ["count", "sum8", "sumvec_8x10_c9", "hist_256_c16", "hist_10_c3",
-                                  "hist_100_c10"])
+                                  "hist_100_c10", "sum15", "sum17", "sum32", "sum64"])
 def test_leader_parity_vs_oracle(name, fast):
     cfg = CONFIGS[name]
     o, eng = _oracle(cfg), _engine(cfg)
@@ -109,7 +109,7 @@ def test_leader_parity_vs_oracle(name, fast):
         assert agg[s].tobytes() == b"".join(v.to_bytes(es, "little") for v in tot)
 
 
-@pytest.mark.parametrize("name", ["hist_10_c3", "hist_256_c16"])
+@pytest.mark.parametrize("name", ["hist_10_c3", "hist_256_c16", "sum32"])
 def test_leader_slow_path(name):
     cfg = CONFIGS[name]
     o, eng = _oracle(cfg), _engine(cfg)
@@ -123,7 +123,7 @@ def test_leader_slow_path(name):
         assert rc == 0 and ps[i].tobytes() == lps
 
 
-@pytest.mark.parametrize("name", ["hist_256_c16", "sum8", "count"])
+@pytest.mark.parametrize("name", ["hist_256_c16", "sum8", "count", "sum32"])
 def test_full_job_both_roles_unshard(name):
     """Leader init (GPU) -> helper init+finish (GPU) -> leader continue (GPU) -> both
     aggregates unshard to the plaintext sum (integration_tests/.../common.rs:332-554)."""
