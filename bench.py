@@ -509,6 +509,9 @@ def leader_main(args):
     hist = args.leader_vdaf == "hist"
     n = args.reports if (hist or args.reports != 1 << 20) else 10_000_000 // 8
     eng = J.HelperEngine(J.Prio3Histogram(256, 16) if hist else J.Prio3Sum(32), VK, device=0)
+    for kv in args.opt:
+        k, v = kv.split("=")
+        eng.set_option(k, int(v))
     sz = eng.sz
     data = eng.generate_reports_device(n, seed=0x4A414E5553000002, with_checks=True,
                                        with_leader_inputs=True)

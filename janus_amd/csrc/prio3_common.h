@@ -651,6 +651,8 @@ struct prio3_engine {
   int qh_prefetch = 1;
   int qh_occ = 3;
   int qh_regs = 0;
+  int n_cu = 256;    // compute units of the engine's GPU
+  int fp_round = 1;  // FPVec sub-batches rounded to whole query rounds (fp_sub_sizes)
   int fuse_q = 0;    // fused accumulate in k_query_h instead of k_xofd (Histogram P = 32)
   int qsum = 1;      // Prio3Sum on k_query_sum (0: the generic k_query)
   int qsum_occ = 3;  // k_query_sum waves per SIMD (2 or 3)

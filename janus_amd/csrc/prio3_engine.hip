@@ -2491,6 +2491,24 @@ static size_t fp_column_bytes(const DevParams& d) {
 // (private segments, queues, the caller's allocator) -- the r01u hipErrorIllegalAddress came
 // with a budget of 85% of free HBM and did not recur with an explicit reserve.
 // The kernels are latency-bound per lane, so the widest sub-batch wins.
+// FPVec sub-batch sizes for n reports in scratch of cap columns: nsub equal sub-batches (columns
+// rounded to 256), except that under the eight-lane query (k_query_fpw, two waves per SIMD, eight
+// reports per wave) the first nsub - 1 are rounded down to whole query rounds -- n_cu x 4 SIMDs x
+// 2 waves x 8 reports (16,384 on MI355X) -- when the last still fits the scratch (option
+// fp_round).  The query's waves all take the same time, so a sub-batch of 3.05 rounds takes 4:
+// 2 x 50,000 run 8 rounds, 49,152 + 50,848 run 7, while the XOF of either size keeps at most two
+// waves per SIMD.
+static void fp_sub_sizes(const prio3_engine* e, uint32_t n, uint32_t cap, bool wide,
+                         uint32_t& nsub, uint32_t& sub) {
+  nsub = (n + cap - 1) / cap;
+  sub = std::min(cap, (((n + nsub - 1) / nsub) + 255) & ~255u);
+  if (wide && e->fp_round && nsub > 1) {
+    const uint32_t Q = (uint32_t)e->n_cu * 4u * 2u * 8u;
+    const uint32_t s2 = sub / Q * Q;
+    if (s2 > 0 && n - (nsub - 1) * s2 <= cap) sub = s2;
+  }
+}
+
 static uint32_t fp_sub_ld(const prio3_engine* e, const DevParams& d, uint32_t ld_out,
                           size_t other_bytes) {
   const size_t per = fp_column_bytes(d);
@@ -2763,8 +2781,8 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
     const uint32_t half = (dp.ld / 2) & ~255u;  // two column sets, each a multiple of 256
     const bool two = e->fp_overlap && half > 0;
     const uint32_t cap = two ? half : dp.ld;
-    const uint32_t nsub = (n + cap - 1) / cap;
-    const uint32_t sub = std::min(cap, (((n + nsub - 1) / nsub) + 255) & ~255u);
+    uint32_t nsub, sub;
+    fp_sub_sizes(e, n, cap, e->fp_wide && fpvec_query_wide_takes(dp), nsub, sub);
     const bool ov = two && nsub > 1;  // set (si % 2) starts at column (si % 2) * cap < dp.ld
     if (ov) {
       int rc = ensure_side_streams(e);
@@ -2772,12 +2790,12 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
       HIPCHK(hipEventRecord(e->fork_ev, st));
       for (auto s2 : e->side) HIPCHK(hipStreamWaitEvent(s2, e->fork_ev, 0));
     }
-    uint32_t si = 0;
-    for (uint32_t s0 = 0; s0 < n; s0 += sub, si++) {
+    for (uint32_t si = 0; si < nsub; si++) {
+      const uint32_t s0 = si * sub;
       hipStream_t ss = ov ? e->side[si % 2] : st;
       const size_t col = ov ? (size_t)(si % 2) * cap : 0;
       DevParams q = dp;
-      q.n = std::min(sub, n - s0);
+      q.n = si + 1 < nsub ? sub : n - s0;
       InPtrs qi = in;
       qi.nonces += 16 * (size_t)s0;
       qi.pub += (size_t)dp.public_share_len * s0;
@@ -2952,12 +2970,13 @@ static int leader_init_fpvec(prio3_engine* e, Run* R, const uint8_t* d_nonces,
   dp.trunc_xof = 0;
   if (!fpvec_query_wide_takes(dp) || !R->corr_all) return PRIO3_EUNSUPPORTED;
   const uint32_t n = R->n, cap = dp.ld;
-  const uint32_t nsub = (n + cap - 1) / cap;
-  const uint32_t sub = std::min(cap, (((n + nsub - 1) / nsub) + 255) & ~255u);
+  uint32_t nsub, sub;
+  fp_sub_sizes(e, n, cap, true, nsub, sub);
   const size_t es = dp.es;
-  for (uint32_t s0 = 0; s0 < n; s0 += sub) {
+  for (uint32_t si = 0; si < nsub; si++) {
+    const uint32_t s0 = si * sub;
     DevParams q = dp;
-    q.n = std::min(sub, n - s0);
+    q.n = si + 1 < nsub ? sub : n - s0;
     InPtrs qi{d_nonces + 16 * (size_t)s0,
               d_pub ? d_pub + (size_t)dp.public_share_len * s0 : nullptr,
               d_lin + (size_t)dp.leader_share_len * s0, nullptr};
@@ -3232,6 +3251,10 @@ int prio3_engine_create_ex(const prio3_params* params, const uint8_t* verify_key
   e->params = *params;
   if (!mp) memcpy(e->dp.vk, verify_key, 16);
   e->device = device;
+  if (hipDeviceGetAttribute(&e->n_cu, hipDeviceAttributeMultiprocessorCount, device) !=
+          hipSuccess ||
+      e->n_cu <= 0)
+    e->n_cu = 256;
   hipStream_t probe = nullptr;  // a GPU must be present: the product path has no CPU fallback
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&probe, hipStreamNonBlocking) != hipSuccess) {
@@ -3354,6 +3377,7 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
               {"slow_rpl", &e->slow_rpl},          {"qwide32", &e->qwide32},
               {"msg_cmp", &e->msg_cmp},            {"qsum", &e->qsum},
               {"qsum_occ", &e->qsum_occ},          {"fuse_q", &e->fuse_q},
+              {"fp_round", &e->fp_round},
               {"qh_prefetch", &e->qh_prefetch},    {"split_xof", &e->split_xof},
               {"qpair", &e->qpair},                {"timing", &e->timing},
               {"coalesce", &e->coalesce},          {"experimental_fpvec", &e->experimental_fpvec},

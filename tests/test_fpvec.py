@@ -237,6 +237,61 @@ def test_gpu_fpvec_sub_batches():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fp_round", [1, 0])
+def test_gpu_fpvec_sub_batches_rounded_to_query_rounds(fp_round):
+    """40,000 reports in scratch of 24,576 columns: two sub-batches, which fp_sub_sizes cuts at
+    whole eight-lane query rounds (16,384 + 23,616 on a 256-CU part) instead of 2 x 20,000.
+    Statuses, messages, output shares and the aggregate must not depend on the cut, for the
+    helper and for the leader."""
+    from janus_amd import prio3 as J
+    v = _vdaf(1)
+    t = v.t
+    n, distinct = 40000, 16
+    reps = _reports(v, n, seed=29, distinct=distinct)
+    reps[5]["lps"][16 * t.verifier_len + 5] ^= 0x40  # one tampered leader joint-rand part
+    per = 16 * (t.meas_len + t.proof_len + 2 + 2 + 2 * (t.P0 + t.P1) + t.K0) + 33
+    msgs, status, outs, agg, cnt = _run(v, reps, sub_bytes=per * 24576 + 1,
+                                        opts={"fp_round": fp_round})
+    # expectations of the distinct reports, plus a clean copy of the tampered one (its tiles
+    # keep the original prep share)
+    exp = _expected(v, reps[:distinct] + [reps[distinct + 5]])
+    src = lambda i: i if i < distinct else (distinct if i % distinct == 5 else i % distinct)
+    want_st = [exp[1][src(i)] for i in range(n)]
+    assert status.tolist() == want_st and want_st[5] != 0
+    tot = 0
+    for i in range(n):
+        assert msgs[i].tobytes() == exp[0][src(i)], i
+        o = exp[2][src(i)]
+        if o is not None:
+            assert int.from_bytes(outs[i].tobytes(), "little") == o[0], i
+            tot = (tot + o[0]) % P.Field128.p
+    assert int.from_bytes(agg[0, :16].tobytes(), "little") == tot
+    assert int(cnt[0]) == sum(1 for x in want_st if x == 0)
+    # the leader over the same cut
+    eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(t.length, t.bits), VK,
+                         allow_unpinned=True)
+    eng.set_option("fp_sub_bytes", per * 24576 + 1)
+    eng.set_option("fp_round", fp_round)
+    leaders = []
+    rng = np.random.default_rng(29)
+    for i in range(distinct):  # the leader shares of the same distinct reports
+        xs = _vector(rng, t.length, t.bits)
+        nonce = bytes(rng.integers(0, 256, 16, dtype=np.uint8))
+        rand = bytes(rng.integers(0, 256, 80, dtype=np.uint8))
+        _, leader, _ = v.shard(xs, nonce, rand)
+        assert nonce == reps[i]["nonce"]
+        leaders.append(list(leader))
+    A = lambda k: np.array([list(r[k]) for r in reps], np.uint8)
+    lps, lst, _ = eng.leader_prepare_init_batch(
+        A("nonce"), A("pub"), np.array([leaders[i % distinct] for i in range(n)], np.uint8))
+    assert not lst.any()
+    clean = [bytes(v.prepare_init(VK, 0, reps[i]["nonce"], reps[i]["pub"], bytes(leaders[i]))[1])
+             for i in range(distinct)]
+    for i in range(n):
+        assert lps[i].tobytes() == clean[i % distinct], i
+
+
+@pytest.mark.gpu
 def test_gpu_fpvec_1000_entries():
     """1000 entries (MEAS_LEN 16,030; gadget 0: C0 127, P0 128; gadget 1: C1 33, P1 32): 3
     distinct reports tiled to 130 lanes."""
