@@ -39,7 +39,10 @@ KERNEL_BYTES = {"k_xof_a": 16 + 16 + 16 + 256 * 16 + 95 * 16,  # nonce, k_meas, 
                 "k_jrpart": 16 + 16 + 32 + 256 * 16 + 2 * 16 + 16,
                 "k_xofd": 16 + 48 + 32 + 256 * 16 + 95 * 16 + 16 + 16 + 3 * 16,  # + jr/qr/part out
                 "k_query_h": 256 * 16 + 95 * 16 + 560 + 2 * 16 + 16 + 16 + 17,
+                "k_query_rows": 256 * 16 + 95 * 16 + 560 + 2 * 16 + 16 + 16 + 17,
                 "k_acc_partial": 256 * 16 + 1}
+# the fused XOF + query kernel moves both kernels' bytes (the share still round-trips through HBM)
+KERNEL_BYTES["k_prep_h"] = KERNEL_BYTES["k_xofd"] + KERNEL_BYTES["k_query_h"]
 # --- algorithmic VALU denominator ("The roofline denominator").  A frozen
 # table of gfx950 lane-instruction costs of the cheapest sequences known for each primitive,
 # times the algorithm's primitive counts per report.  No kernel can issue fewer instructions for
@@ -76,7 +79,7 @@ def valu_model(kernel: str, length=256, chunk=16) -> float:
         perms = 1 + meas_blocks + jr_blocks + proofs_blocks + 1 + 1
         squeezed = length + proof_len + 2 + 1
         return perms * perm + squeezed * PRIM["lt_p"] + jr_blocks * 42  # + funnel shifts
-    if kernel in ("k_query_h", "k_query_pair"):
+    if kernel in ("k_query_h", "k_query_pair", "k_query_rows"):
         logP = P.bit_length() - 1
         half = P // 2
         # two DFTs of P/2 points (radix 2: (P/4) log2(P/2) butterflies, the w = 1 ones free)
@@ -92,6 +95,8 @@ def valu_model(kernel: str, length=256, chunk=16) -> float:
         return (muls * PRIM["f128_mul"] + macs * PRIM["f128_mac"] +
                 reduces * PRIM["f128_reduce"] + adds * PRIM["f128_add"] +
                 length * PRIM["f128_sum_add"] + (2 * chunk + 2) * PRIM["lt_p"] + perm)
+    if kernel == "k_prep_h":  # dual-state XOF + P = 32 query in one launch
+        return valu_model("k_xofd", length, chunk) + valu_model("k_query_h", length, chunk)
     if kernel == "k_meta":
         return PRIM["sha256_compress"]
     return 0.0
@@ -326,9 +331,10 @@ def main():
                               frac=step_model * n * args.steps / elapsed / 1e12 / peak_T,
                               note="whole timed step (all kernels, stream-overlapped chunks), "
                                    "per GPU"))
-    qh = per_kernel.get("k_query_h") or per_kernel.get("k_query_pair")
+    qk = next((k for k in ("k_query_rows", "k_query_h", "k_query_pair") if k in per_kernel), None)
+    qh = per_kernel.get(qk) if qk else None
     if qh and "hbm_frac" in qh:
-        roofline["query_hbm"] = dict(kernel="k_query_h" if "k_query_h" in per_kernel else "k_query_pair",
+        roofline["query_hbm"] = dict(kernel=qk,
                                      achieved_TBps=qh["hbm_pmc_TBps"], peak_TBps=PEAK_HBM / 1e12,
                                      frac=qh["hbm_frac"])
 

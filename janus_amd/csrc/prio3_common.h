@@ -58,6 +58,11 @@ struct DevParams {
   uint32_t trunc_xof;
   // 1: the prepare message is not re-hashed (see prep_msg_check)
   uint32_t msg_cmp;
+  // 1: the query kernel skips reports the XOF flagged for the rejection-sampling slow path; the
+  // run ends with one k_xof_slow launch (which marks the redone reports 2) and a redo launch of
+  // the query (redo = 1) over exactly those reports, instead of a k_xof_slow launch per chunk
+  // between the XOF and the query
+  uint32_t slow_defer, redo;
   // Prio3Sum query (k_query_sum, P = 16 NPH): tws[j] = w16^j (j < 8), tws[8 + i] = alpha_P^i
   // (i < 8), tws[16 + i] = alpha_P^(16 i) (i < 8)
   uint32_t tws[24][4];
@@ -584,6 +589,9 @@ int launch_mp64_leader_next(uint32_t n, const uint8_t* d_prep_msgs, Scratch sc, 
 // P = 16 / 32 ParallelSum(Mul) helper query on lane pairs (prio3_query_pair.hip); false if the
 // instance is not one it takes
 bool launch_query_pair(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st);
+// prio3_query_rows.hip: Histogram K = 16, chunk 16 (P = 32) on row-split lane pairs
+bool launch_query_rows(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st);
+bool query_rows_takes(const DevParams& p);
 // long-share helper XOF on lane pairs (prio3_xof_pair.hip); false if the instance is not one it takes
 bool launch_xof_pair(const DevParams& p, InPtrs in, Scratch sc, hipStream_t st);
 // P = 64 / 128 ParallelSum(Mul) helper query, eight lanes per report (prio3_query_wide.hip);
@@ -659,6 +667,12 @@ struct prio3_engine {
   int msg_cmp = 0;   // prepare message by part comparison instead of a re-hash (prep_msg_check)
   int qwide32 = 0;   // P = 32 (Histogram 256/16) on k_query_w instead of k_query_h
   int slow_rpl = 16;  // k_xof_slow reports per lane (16; 1 = the round-1 grid)
+  int qrows = 0;      // Histogram K = 16 / chunk 16 query on row-split lane pairs (k_query_rows;
+                      // A/B: 2.86 vs 2.29 ms for k_query_h)
+  int slow_defer = 1; // Histogram P <= 32: slow path deferred to the end of the run
+                      // (VERDICT r1 item 11); 0: a k_xof_slow launch per chunk
+  int prep_fused = 1; // Histogram P = 32: XOF + query in one launch (k_prep_h); 0: two kernels
+  int prep_persist = 0;  // k_prep_h as a persistent grid with out-of-step waves (k_prep_hp)
   int qpair = 0;  // option: P = 16/32 query on lane pairs (k_query_pair; A/B: slower)
   // option: helper XOF on lane pairs (k_xof_pair): -1 auto (shares of >= 2048 elements), 0, 1
   int xof_pair = -1;

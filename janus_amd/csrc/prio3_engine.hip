@@ -221,9 +221,9 @@ __global__ __launch_bounds__(256, XOFD_OCC) void k_xof(DevParams p, InPtrs in, S
 // through the fix-up list with their corrected shares).
 // TR: the measurement share is also truncated into sc.out on the fly (DevParams::trunc_xof).
 template <bool FUSE, bool TR = false>
-__global__ __launch_bounds__(256, XOFD_OCC) void k_xofd(DevParams p, InPtrs in, Scratch sc) {
+__device__ __forceinline__ void xofd_body(const DevParams& p, const InPtrs& in, const Scratch& sc,
+                                          const uint32_t r) {  // r & 63 == this lane
   typedef Fp128 F;
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
   bool fuse = false;
   uint32_t s0 = 0;
@@ -430,6 +430,10 @@ __global__ __launch_bounds__(256, XOFD_OCC) void k_xofd(DevParams p, InPtrs in, 
       if (lane == 0) sc.wseg[r >> 6] = anyflag ? 0xffffffffu : s0;
     }
   }
+}
+template <bool FUSE, bool TR = false>
+__global__ __launch_bounds__(256, XOFD_OCC) void k_xofd(DevParams p, InPtrs in, Scratch sc) {
+  xofd_body<FUSE, TR>(p, in, sc, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // ------------------------------------------------------------------------------------
@@ -752,57 +756,67 @@ __global__ __launch_bounds__(64) void k_leader_slowfix(DevParams p, InPtrs in, S
 // k_xof_slow: general byte-level sponge with rejection sampling (flagged reports only)
 // ------------------------------------------------------------------------------------
 // (byte-level sponge helpers BX / bx_* live in prio3_common.h)
-template <class F>
+// The sponges run one at a time (one Keccak state live): the joint-rand-part sponge absorbs the
+// measurement share from the scratch rows this lane has just written, instead of beside the
+template <class F, int SITE = 0>
 __device__ __noinline__ void xof_slow_one(const DevParams& p, const InPtrs& in, const Scratch& sc,
                                           uint32_t r) {
-  uint32_t nonce[4], km[4], kp[4], kb[4] = {0, 0, 0, 0};
+  uint32_t nonce[4];
   load16(in.nonces + 16 * (size_t)r, nonce);
   const uint8_t* hs = in.helper + (size_t)r * p.helper_share_len;
-  load16(hs, km);
-  load16(hs + 16, kp);
   const bool JR = p.jr_len > 0;
-  if (JR) load16(hs + 32, kb);
   uint32_t w[4];
-  BX x, y;
-  // query rand
-  {
+  {  // query rand
+    BX x;
     uint32_t vk[4];
     load_vk(p, in, r, vk);
     bx_init(x, p.dst[5], vk);
-  }
-  bx_absorb(x, 1);
-  bx_absorb_w(x, nonce, 16);
-  bx_finalize(x);
-  for (uint32_t i = 0; i < p.qr_len; i++) {
-    bx_next_elem<F>(x, w);
-    F::store(sc.qr, (size_t)i * p.ld + r, F::from_words(w));
-  }
-  // meas + jr part
-  bx_init(x, p.dst[1], km);
-  bx_absorb(x, 1);
-  bx_finalize(x);
-  if (JR) {
-    bx_init(y, p.dst[7], kb);
-    bx_absorb(y, 1);
-    bx_absorb_w(y, nonce, 16);
-  }
-  if constexpr (F::ES == 16) {
-    TruncSink ts(p, sc.out, r);
-    for (uint32_t i = 0; i < p.meas_len; i++) {
+    bx_absorb(x, 1);
+    bx_absorb_w(x, nonce, 16);
+    bx_finalize(x);
+    for (uint32_t i = 0; i < p.qr_len; i++) {
       bx_next_elem<F>(x, w);
-      F::store(sc.meas, (size_t)i * p.ld + r, F::from_words(w));
-      if (p.trunc_xof) ts.put(mk128(w[0], w[1], w[2], w[3]));
-      if (JR) bx_absorb_w(y, w, F::ES);
+      F::store(sc.qr, (size_t)i * p.ld + r, F::from_words(w));
     }
-  } else {
-    for (uint32_t i = 0; i < p.meas_len; i++) {
-      bx_next_elem<F>(x, w);
-      F::store(sc.meas, (size_t)i * p.ld + r, F::from_words(w));
-      if (JR) bx_absorb_w(y, w, F::ES);
+  }
+  {  // measurement share
+    BX x;
+    uint32_t km[4];
+    load16(hs, km);
+    bx_init(x, p.dst[1], km);
+    bx_absorb(x, 1);
+    bx_finalize(x);
+    if constexpr (F::ES == 16) {
+      TruncSink ts(p, sc.out, r);
+      for (uint32_t i = 0; i < p.meas_len; i++) {
+        bx_next_elem<F>(x, w);
+        F::store(sc.meas, (size_t)i * p.ld + r, F::from_words(w));
+        if (p.trunc_xof) ts.put(mk128(w[0], w[1], w[2], w[3]));
+      }
+    } else {
+      for (uint32_t i = 0; i < p.meas_len; i++) {
+        bx_next_elem<F>(x, w);
+        F::store(sc.meas, (size_t)i * p.ld + r, F::from_words(w));
+      }
     }
   }
   uint32_t part[4] = {0, 0, 0, 0};
-  if (JR) {
+  if (JR) {  // joint-rand part over the encoded share, read back from this lane's rows
+    BX y;
+    uint32_t kb[4];
+    load16(hs + 32, kb);
+    bx_init(y, p.dst[7], kb);
+    bx_absorb(y, 1);
+    bx_absorb_w(y, nonce, 16);
+    for (uint32_t i = 0; i < p.meas_len; i++) {
+      const typename F::T v = F::load(sc.meas, (size_t)i * p.ld + r);
+      if constexpr (F::ES == 16) {
+        w[0] = v.w[0], w[1] = v.w[1], w[2] = v.w[2], w[3] = v.w[3];
+      } else {
+        w[0] = (uint32_t)v, w[1] = (uint32_t)(v >> 32);
+      }
+      bx_absorb_w(y, w, F::ES);
+    }
     bx_finalize(y);
     for (int k = 0; k < 4; k++) {
       uint32_t v = 0;
@@ -810,27 +824,36 @@ __device__ __noinline__ void xof_slow_one(const DevParams& p, const InPtrs& in, 
       part[k] = v;
     }
   }
-  // proofs
-  bx_init(x, p.dst[2], kp);
-  bx_absorb(x, 1);
-  bx_absorb(x, 1);
-  bx_finalize(x);
-  for (uint32_t i = 0; i < p.proof_len; i++) {
-    bx_next_elem<F>(x, w);
-    F::store(sc.proofs, (size_t)i * p.ld + r, F::from_words(w));
+  {  // proofs
+    BX x;
+    uint32_t kp[4];
+    load16(hs + 16, kp);
+    bx_init(x, p.dst[2], kp);
+    bx_absorb(x, 1);
+    bx_absorb(x, 1);
+    bx_finalize(x);
+    for (uint32_t i = 0; i < p.proof_len; i++) {
+      bx_next_elem<F>(x, w);
+      F::store(sc.proofs, (size_t)i * p.ld + r, F::from_words(w));
+    }
   }
   if (JR) {
-    uint32_t pub0[4], zero[4] = {0, 0, 0, 0}, cor[4];
-    load16(in.pub + (size_t)r * p.public_share_len, pub0);
-    bx_init(x, p.dst[6], zero);
-    bx_absorb_w(x, pub0, 16);
-    bx_absorb_w(x, part, 16);
-    bx_finalize(x);
-    for (int k = 0; k < 4; k++) {
-      uint32_t v = 0;
-      for (int b = 0; b < 4; b++) v |= (uint32_t)bx_squeeze(x) << (8 * b);
-      cor[k] = v;
+    uint32_t cor[4];
+    {
+      BX x;
+      uint32_t pub0[4], zero[4] = {0, 0, 0, 0};
+      load16(in.pub + (size_t)r * p.public_share_len, pub0);
+      bx_init(x, p.dst[6], zero);
+      bx_absorb_w(x, pub0, 16);
+      bx_absorb_w(x, part, 16);
+      bx_finalize(x);
+      for (int k = 0; k < 4; k++) {
+        uint32_t v = 0;
+        for (int b = 0; b < 4; b++) v |= (uint32_t)bx_squeeze(x) << (8 * b);
+        cor[k] = v;
+      }
     }
+    BX y;
     bx_init(y, p.dst[3], cor);
     bx_absorb(y, 1);
     bx_finalize(y);
@@ -841,7 +864,7 @@ __device__ __noinline__ void xof_slow_one(const DevParams& p, const InPtrs& in, 
     sc.part[r] = make_uint4(part[0], part[1], part[2], part[3]);
     sc.corrected[r] = make_uint4(cor[0], cor[1], cor[2], cor[3]);
   }
-  sc.flag[r] = 0;
+  sc.flag[r] = p.slow_defer ? 2u : 0u;
 }
 
 // The slow path's launch: each lane scans the flags of 16 reports with one 16-byte load and
@@ -1154,13 +1177,12 @@ __global__ __launch_bounds__(256) void k_query_ps(DevParams p, InPtrs in, Scratc
 // (wave_halfsum2, as k_xofd<true> does) into sc.wpart and writes its segment to sc.wseg.  The
 // query waits on memory about half its cycles, where the XOF is issue-bound.
 template <int GS, int PP, int PF = 1, int OCC = 3, int LEADER = 0, bool FUSE = false>
-__global__ __launch_bounds__(256, OCC) void k_query_h(DevParams p, InPtrs in, Scratch sc,
-                                                    OutPtrs out) {
+__device__ __forceinline__ void query_h_body(const DevParams& p, const InPtrs& in, const Scratch& sc,
+                                             const OutPtrs& out, const uint32_t r) {
   typedef Fp128 F;
   typedef f128 T;
   constexpr int LOGP = PP <= 2 ? 1 : PP <= 4 ? 2 : PP <= 8 ? 3 : PP <= 16 ? 4 : 5;
   static_assert(!FUSE || (GS == 2 && !LEADER), "fused pairs need two columns per sweep");
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
   bool fuse = false;
   if constexpr (FUSE) {
@@ -1172,6 +1194,16 @@ __global__ __launch_bounds__(256, OCC) void k_query_h(DevParams p, InPtrs in, Sc
     if (lane == 0 && (r - lane) < p.n) sc.wseg[r >> 6] = fuse ? s0 : 0xffffffffu;
   }
   if (r >= p.n) return;
+  // slow_defer: a report the XOF flagged (a rejected sample) is skipped here; after the whole
+  // run, k_xof_slow re-runs its XOF (flag := 2) and this kernel runs again with p.redo = 1 for
+  // exactly those reports -- no k_xof_slow launch between the XOF and the query of each chunk
+  if constexpr (!LEADER && !FUSE) {
+    if (p.redo) {
+      if (sc.flag[r] != 2) return;
+    } else if (p.slow_defer && sc.flag[r]) {
+      return;
+    }
+  }
   const size_t ld = p.ld;
   const uint32_t A = p.arity, C = p.chunk, M = p.meas_len, K = p.calls;
   uint8_t status = LEADER ? out.status[r] : PRIO3_STATUS_FINISHED;  // leader: unpack verdict
@@ -1422,6 +1454,50 @@ __global__ __launch_bounds__(256, OCC) void k_query_h(DevParams p, InPtrs in, Sc
       }
       F::store(sc.out, (size_t)e * ld + r, acc);
     }
+  }
+}
+template <int GS, int PP, int PF = 1, int OCC = 3, int LEADER = 0, bool FUSE = false>
+__global__ __launch_bounds__(256, OCC) void k_query_h(DevParams p, InPtrs in, Scratch sc,
+                                                    OutPtrs out) {
+  query_h_body<GS, PP, PF, OCC, LEADER, FUSE>(p, in, sc, out, blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// k_prep_h<FUSE>: the whole helper prepare of Prio3Histogram with P = 32 in one launch -- the
+// dual-state XOF (xofd_body) and then the query (query_h_body; flagged reports deferred to the
+// run's redo pass, slow_defer) of the same 64 reports on the same wave.  Both phases fit 3 waves per SIMD, and the waves of a
+// SIMD drift apart, so one wave's memory-bound query runs beside other waves' issue-bound Keccak
+// without a kernel boundary, a second stream or the k_xof_slow launch between them.  The query
+// reads the scratch rows its own lane has just written.
+template <bool FUSE>
+__global__ __launch_bounds__(256, 3) void k_prep_h(DevParams p, InPtrs in, Scratch sc,
+                                                   OutPtrs out) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  xofd_body<FUSE, false>(p, in, sc, r);
+  query_h_body<2, 32, 1, 3, 0, false>(p, in, sc, out, r);
+}
+
+// k_prep_hp<FUSE>: k_prep_h as a persistent grid (option prep_persist) -- one 64-report tile
+// per wave and iteration, waves striding over the tiles.  A wave of an odd block runs one tile
+// behind (XOF of tile i+1 before the query of tile i), so the waves sharing a SIMD drift out
+// of step: one wave's memory-bound query beside the others' issue-bound Keccak instead of every
+// wave of a launch round entering its query at the same time.
+template <bool FUSE>
+__global__ __launch_bounds__(256, 3) void k_prep_hp(DevParams p, InPtrs in, Scratch sc,
+                                                    OutPtrs out) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
+  const uint32_t ntiles = (p.n + 63) >> 6;
+  const uint32_t lag = blockIdx.x & 1u;  // tiles the query trails the XOF by
+  // one call site per body (each is inlined once): iteration i runs the XOF of tile w0 + i nw
+  // and the query of tile w0 + (i - lag) nw, while either exists (wave-uniform)
+  for (uint32_t i = 0;; i++) {
+    const uint32_t tx = w0 + i * nw;
+    const bool qv = i >= lag;
+    const uint32_t tq = qv ? w0 + (i - lag) * nw : 0u;
+    if (tx >= ntiles && (!qv || tq >= ntiles)) break;
+    if (tx < ntiles) xofd_body<FUSE, false>(p, in, sc, tx * 64u + lane);
+    if (qv && tq < ntiles) query_h_body<2, 32, 1, 3, 0, false>(p, in, sc, out, tq * 64u + lane);
   }
 }
 
@@ -2539,6 +2615,9 @@ constexpr uint32_t WCH_HOST = 32;  // waves per fused-partial chunk (k_agg_waves
 template <class F>
 static void launch_xof_slow(const prio3_engine* e, const DevParams& p, const InPtrs& in,
                             const Scratch& sc, hipStream_t st) {
+#ifdef JANUS_AB_SKIP_SLOW  // A/B build only (tools/build_variant.sh): the cost of the launch
+  return;
+#endif
   if (e->slow_rpl == 1)
     k_xof_slow<F, 1><<<(p.n + 63) / 64, 64, 0, st>>>(p, in, sc);
   else
@@ -2739,11 +2818,29 @@ static int ensure_side_streams(prio3_engine* e) {
   return PRIO3_OK;
 }
 
+// The helper chain of this instance is the fused k_prep_h (dual-state XOF + k_query_h<2, 32>
+// in one launch; the conditions under which launch_prepare would launch exactly those two).
+static bool prep_fused_takes(const prio3_engine* e, const DevParams& dp, bool fuse) {
+  const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
+  const bool dual = dp.es == 16 && dp.jr_len && e->split_xof == 2 &&
+                    (42 + dp.meas_len * 16) / 168 >= 2;
+  const bool wide = ps && e->qwide && !(e->qpair && (dp.P == 32 || dp.P == 16)) &&
+                    (dp.P != 32 || e->qwide32) && query_wide_takes(dp);
+  return e->prep_fused && e->slow_defer && dp.kind != PRIO3_FPVEC_BOUNDED_L2 && ps && dual &&
+         !wide && dp.P == 32 && !(fuse && e->fuse_q) && !(!fuse && e->xof_pair > 0) &&
+         !e->qh_regs && !e->qpair && !e->qrows && e->qh_prefetch == 1 && e->qh_occ == 3;
+}
+
+// *deferred: set when a query kernel of this chain skipped flagged reports (slow_defer); the
+// caller then ends the run with launch_slow_redo
 static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, uint32_t n,
-                          InPtrs in, OutPtrs out, Scratch sc, hipStream_t st, bool fuse) {
+                          InPtrs in, OutPtrs out, Scratch sc, hipStream_t st, bool fuse,
+                          bool* deferred) {
   DevParams dp = base;
   dp.n = n;
   dp.force_slow = (uint32_t)e->force_slow;
+  dp.slow_defer = 0;
+  dp.redo = 0;
   const size_t es = dp.es;
   in.nonces += 16 * (size_t)c0;
   if (in.pub) in.pub += (size_t)dp.public_share_len * c0;
@@ -2858,6 +2955,22 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
     // chunk) instead of k_xofd
     const bool fuseq = fuse && e->fuse_q && dual && ps && !wide && dp.P == 32 &&
                        (dp.chunk & 1u) == 0 && !e->qh_regs && !e->qpair;
+    // option prep_fused (default): XOF + query of Histogram P = 32 in one launch (k_prep_h)
+    if (!paired && prep_fused_takes(e, dp, fuse)) {
+      dp.slow_defer = 1u;
+      if (deferred) *deferred = true;
+      if (e->prep_persist) {
+        const uint32_t pb = std::min(blocks, (uint32_t)e->n_cu * 3u);  // 3 blocks per CU resident
+        if (fuse)
+          TIMED(e, st, "k_prep_h", (k_prep_hp<true><<<pb, 256, 0, st>>>(dp, in, sc, out)));
+        else
+          TIMED(e, st, "k_prep_h", (k_prep_hp<false><<<pb, 256, 0, st>>>(dp, in, sc, out)));
+      } else if (fuse)
+        TIMED(e, st, "k_prep_h", (k_prep_h<true><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+      else
+        TIMED(e, st, "k_prep_h", (k_prep_h<false><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+      return PRIO3_OK;
+    }
     if (paired) {
     } else if (dual) {
       if (fuse && !fuseq)
@@ -2875,13 +2988,23 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
     } else {
       TIMED(e, st, "k_xof", (k_xof<Fp128><<<blocks, 256, 0, st>>>(dp, in, sc)));
     }
-    TIMED(e, st, "k_xof_slow", launch_xof_slow<Fp128>(e, dp, in, sc, st));
+    // the query is k_query_h: flagged reports are deferred to the run's redo pass (slow_defer)
+    const bool rows = ps && e->qrows && !fuseq && !e->qh_regs && !e->qpair && !wide &&
+                      query_rows_takes(dp);
+    const bool qh_path = ps && !e->qpair && !wide && !rows &&
+                         (dp.P == 32 || dp.P == 16 || dp.P == 8) &&
+                         !(dp.P == 32 && dp.chunk == 16 && dp.calls == 16 && e->qh_regs);
+    dp.slow_defer = qh_path && !fuseq && e->slow_defer ? 1u : 0u;
+    if (dp.slow_defer && deferred) *deferred = true;
+    if (!dp.slow_defer) TIMED(e, st, "k_xof_slow", launch_xof_slow<Fp128>(e, dp, in, sc, st));
     bool done = false;
     if (ps && e->qpair && (dp.P == 32 || dp.P == 16)) {
       TIMED(e, st, "k_query_pair", (done = launch_query_pair(dp, in, sc, out, st)));
     }
     if (!done && wide)
       TIMED(e, st, "k_query_w", (done = launch_query_wide(dp, in, sc, out, st, e->qw_gs)));
+    if (!done && rows)
+      TIMED(e, st, "k_query_rows", (done = launch_query_rows(dp, in, sc, out, st)));
     if (done) {
     } else if (ps && dp.P == 32 && dp.chunk == 16 && dp.calls == 16 && e->qh_regs)
       TIMED(e, st, "k_query_r", (k_query_r<16, 16><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
@@ -2916,6 +3039,33 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
 
 
 
+// The deferred slow path of a run whose k_query_h launches skipped the reports the XOF flagged
+// (slow_defer): one k_xof_slow launch over the whole run redoes their XOF and marks them 2, then
+// k_query_h runs once more with redo = 1, for exactly those reports (every other lane leaves
+// after reading its flag).  Two launches per run instead of one k_xof_slow launch between the
+// XOF and the query of every chunk, where its one-wave blocks waited behind the other stream's
+// kernels (~0.2 ms per chunk in the r02 trace).
+static int launch_slow_redo(prio3_engine* e, const DevParams& base, uint32_t n, InPtrs in,
+                            OutPtrs out, Scratch sc, hipStream_t st) {
+  DevParams dp = base;
+  dp.n = n;
+  dp.force_slow = (uint32_t)e->force_slow;
+  dp.msg_cmp = e->msg_cmp ? 1u : 0u;
+  dp.trunc_xof = 0;
+  dp.slow_defer = 1;
+  dp.redo = 0;
+  TIMED(e, st, "k_xof_slow", launch_xof_slow<Fp128>(e, dp, in, sc, st));
+  dp.redo = 1;
+  const uint32_t blocks = (n + 255) / 256;
+  if (dp.P == 32)
+    TIMED(e, st, "k_query_redo", (k_query_h<2, 32><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+  else if (dp.P == 16)
+    TIMED(e, st, "k_query_redo", (k_query_h<2, 16><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+  else
+    TIMED(e, st, "k_query_redo", (k_query_h<2, 8><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+  return PRIO3_OK;
+}
+
 // The kernel chain over the whole run.  Option "chunks" > 1 (auto: one chunk per 128Ki reports,
 // measured best on MI355X at 1Mi reports: 8 chunks +4-5% over 1; 16: slower): the batch is cut
 // into column ranges whose chains alternate over the engine's two side streams (joined to `st`
@@ -2930,23 +3080,33 @@ static int prepare_run(prio3_engine* e, Run* R, InPtrs in, OutPtrs out, hipStrea
   sc.wpart = R->wpart;
   sc.wseg = R->wseg;
   R->last = st;
-  const uint32_t K = e->chunks > 0 ? (uint32_t)e->chunks : std::max(1u, (n + (1u << 16)) >> 17);
+  // auto: one chunk per 128Ki reports on the two-kernel chain; one launch for the fused k_prep_h
+  // (A/B on MI355X, 1 Mi reports: 169.9 M/s at 1 chunk vs 163.2 M/s at 8)
+  const uint32_t K = e->chunks > 0                       ? (uint32_t)e->chunks
+                     : prep_fused_takes(e, R->dp, fuse) ? 1u
+                                                        : std::max(1u, (n + (1u << 16)) >> 17);
   const uint32_t csz = ((n + K - 1) / K + 255) & ~255u;
-  if (!allow_chunks || K == 1 || n <= csz || R->dp.kind == PRIO3_FPVEC_BOUNDED_L2)
-    return launch_prepare(e, R->dp, 0, n, in, out, sc, st, fuse);
+  bool deferred = false;
+  if (!allow_chunks || K == 1 || n <= csz || R->dp.kind == PRIO3_FPVEC_BOUNDED_L2) {
+    const int rc = launch_prepare(e, R->dp, 0, n, in, out, sc, st, fuse, &deferred);
+    if (rc == PRIO3_OK && deferred) return launch_slow_redo(e, R->dp, n, in, out, sc, st);
+    return rc;
+  }
   int rc = ensure_side_streams(e);
   if (rc) return rc;
   HIPCHK(hipEventRecord(e->fork_ev, st));
   for (auto s2 : e->side) HIPCHK(hipStreamWaitEvent(s2, e->fork_ev, 0));
   uint32_t c = 0;
   for (uint32_t c0 = 0; c0 < n; c0 += csz, c++) {
-    rc = launch_prepare(e, R->dp, c0, std::min(csz, n - c0), in, out, sc, e->side[c % 2], fuse);
+    rc = launch_prepare(e, R->dp, c0, std::min(csz, n - c0), in, out, sc, e->side[c % 2], fuse,
+                        &deferred);
     if (rc) return rc;
   }
   for (size_t i = 0; i < e->side.size(); i++) {
     HIPCHK(hipEventRecord(e->side_ev[i], e->side[i]));
     HIPCHK(hipStreamWaitEvent(st, e->side_ev[i], 0));
   }
+  if (deferred) return launch_slow_redo(e, R->dp, n, in, out, sc, st);
   return PRIO3_OK;
 }
 
@@ -3377,7 +3537,9 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
               {"slow_rpl", &e->slow_rpl},          {"qwide32", &e->qwide32},
               {"msg_cmp", &e->msg_cmp},            {"qsum", &e->qsum},
               {"qsum_occ", &e->qsum_occ},          {"fuse_q", &e->fuse_q},
-              {"fp_round", &e->fp_round},
+              {"fp_round", &e->fp_round},          {"qrows", &e->qrows},
+              {"slow_defer", &e->slow_defer},      {"prep_fused", &e->prep_fused},
+              {"prep_persist", &e->prep_persist},
               {"qh_prefetch", &e->qh_prefetch},    {"split_xof", &e->split_xof},
               {"qpair", &e->qpair},                {"timing", &e->timing},
               {"coalesce", &e->coalesce},          {"experimental_fpvec", &e->experimental_fpvec},

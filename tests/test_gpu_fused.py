@@ -92,8 +92,16 @@ def test_fused_ragged_tail_and_small_histogram():
     _run(CONFIGS["hist_100_c10"], 131, seed=6)
 
 
-def test_fused_slow_path_flags():
-    _run(CONFIGS["hist_256_c16"], 192, seed=7, force_slow=True)
+@pytest.mark.parametrize("slow_defer", [1, 0])
+def test_fused_slow_path_flags(slow_defer):
+    """Every report flagged: the slow path deferred to the end of the run (slow_defer=1, the
+    default: the query skips flagged reports, k_xof_slow + a redo query after the last chunk) or
+    a k_xof_slow launch per chunk (slow_defer=0), with 2 chunks so both streams carry flags, on
+    the fused XOF + query kernel and on the two-kernel chain."""
+    for pf in (1, 0):
+        o = {"slow_defer": slow_defer, "prep_fused": pf}
+        _run(CONFIGS["hist_256_c16"], 192, seed=7, force_slow=True, opts=o)
+        _run(CONFIGS["hist_256_c16"], 700, seed=8, force_slow=True, chunks=2, opts=o)
 
 
 @pytest.mark.parametrize("name", ["count", "sum8", "sumvec_8x10_c9"])
@@ -151,3 +159,12 @@ def test_out_of_range_segment_ids_are_excluded(name, fuse):
     """a segment id >= n_segments never reaches the aggregate or the counts (fused
     Histogram path, its unfused fallback, and the deferred masked reduction alike)."""
     _run(CONFIGS[name], 900, seed=31, n_segments=3, oob_frac=0.05, fuse=fuse)
+
+
+@pytest.mark.parametrize("opts", [{"prep_persist": 1}, {"prep_persist": 1, "chunks": 3},
+                                  {"prep_fused": 0}])
+def test_fused_accumulate_on_fused_prepare_variants(opts):
+    """The fused accumulate (wave partials in the XOF) under the persistent out-of-step k_prep_hp
+    and the two-kernel chain, segment runs inside waves, tampered reports, the host mask."""
+    _run(CONFIGS["hist_256_c16"], 3000, seed=91, n_segments=4, opts=opts)
+    _run(CONFIGS["hist_256_c16"], 256, seed=92, force_slow=True, opts=opts)

@@ -100,6 +100,16 @@ def test_slow_path_parity(name):
     _check_against_oracle(CONFIGS[name], 130, seed=5, force_slow=True)
 
 
+@pytest.mark.parametrize("opts", [{"slow_defer": 0}, {"qrows": 1}, {"prep_fused": 0},
+                                  {"chunks": 3}])
+@pytest.mark.parametrize("name", ["hist_256_c16", "hist_10_c3"])
+def test_slow_path_launch_variants(name, opts):
+    """The slow path as a k_xof_slow launch between the XOF and the query (slow_defer=0, or under
+    k_query_rows), deferred after the two-kernel chain (prep_fused=0) or after stream-overlapped
+    chunks, besides the default (deferred after the fused XOF + query kernel)."""
+    _check_against_oracle(CONFIGS[name], 130, seed=6, force_slow=True, opts=opts)
+
+
 @pytest.mark.parametrize("name", ["count", "hist_256_c16", "sumvec_8x10_c9"])
 def test_segments_and_accept_mask(name):
     _check_against_oracle(CONFIGS[name], 900, seed=3, n_segments=5)
@@ -284,3 +294,45 @@ def test_truncate_in_xof_chunked_and_paired(name):
     n = 600 if "1000" in name else 1500
     _check_against_oracle(CONFIGS[name], n, seed=37, opts={"coalesce": 0, "chunks": 3})
     _check_against_oracle(CONFIGS[name], n // 3, seed=41, opts={"xof_pair": 1})
+
+
+HIST_ROWS = {"hist_256_c16": CONFIGS["hist_256_c16"],
+             "hist_250_c16": dict(kind="histogram", length=250, chunk_length=16),
+             "hist_241_c16": dict(kind="histogram", length=241, chunk_length=16)}
+
+
+@pytest.mark.parametrize("n", [1, 127, 700])
+@pytest.mark.parametrize("name", list(HIST_ROWS))
+def test_query_rows_parity(name, n):
+    """Histogram with 16 calls of chunk 16 (P = 32) on row-split lane pairs (k_query_rows, the
+    default): tampered reports (decide, decode, joint-rand and public-share failures), a share
+    shorter than K x C (masked rows), odd and sub-block batch sizes; then the same batch on the
+    one-lane k_query_h (qrows=0)."""
+    cfg = HIST_ROWS[name]
+    _check_against_oracle(cfg, n, seed=71 + n, tamper=n > 100, opts={"qrows": 1})
+    _check_against_oracle(cfg, n, seed=71 + n, tamper=n > 100, opts={"qrows": 0})
+
+
+@pytest.mark.parametrize("opts", [{"qrows": 1, "chunks": 3}, {"qrows": 1, "msg_cmp": 1}])
+def test_query_rows_with_options(opts):
+    """k_query_rows under stream-overlapped chunks and the prepare message by comparison."""
+    _check_against_oracle(CONFIGS["hist_256_c16"], 900, seed=77, opts=opts)
+
+
+@pytest.mark.parametrize("opts", [{"prep_fused": 1}, {"prep_fused": 1, "chunks": 3},
+                                  {"prep_fused": 0}, {"prep_fused": 0, "slow_defer": 0}])
+@pytest.mark.parametrize("name", ["hist_256_c16", "sumvec_2x100_c10", "hist_100_c4"])
+def test_fused_prepare_kernel_parity(name, opts):
+    """P = 32 ParallelSum(Mul) (Histogram with 16 and 25 calls, SumVec with 20): the XOF and the
+    query in one launch (k_prep_h, the default; one chunk or three stream-overlapped ones) and
+    the two-kernel chain with the slow path deferred or per chunk, on tampered ragged batches."""
+    _check_against_oracle(CONFIGS[name], 777, seed=83, opts=opts)
+
+
+@pytest.mark.parametrize("n", [1, 300, 5000])
+def test_fused_prepare_persistent_parity(n):
+    """Option prep_persist: k_prep_h as a persistent grid whose odd blocks run the query one tile
+    behind the XOF (k_prep_hp) -- ragged tiles, a batch smaller than one wave, and more tiles
+    than resident waves would need at a small grid are covered through the oracle."""
+    _check_against_oracle(CONFIGS["hist_256_c16"], n, seed=85 + n, tamper=n > 100,
+                          opts={"prep_persist": 1})

@@ -7,7 +7,7 @@ TAG=$1; shift
 R=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$R/janus_amd/variants/$TAG
 mkdir -p $OUT
-SRCS="prio3_engine prio3_client hpke dap_codec prio3_mp64"
+SRCS=$(cd $R/janus_amd/csrc && ls *.hip | sed "s/\.hip$//")
 for f in $SRCS; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function "$@" \
     -c -o $OUT/$f.o $R/janus_amd/csrc/$f.hip &
