@@ -268,10 +268,10 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    # Roofline pass (after the timed region): the engine cuts a 1Mi batch into 8 chunks whose
-    # kernels overlap on two streams, so a launch's duration there includes its neighbour's
-    # share of the CU.  The per-kernel roofline is taken from whole-batch launches in isolation
-    # (option chunks=1), a few steps on the same stream and data.
+    # Roofline pass (after the timed region): whole-batch launches (option chunks=1, which the
+    # fused k_prep_h default already uses; the two-kernel chain would cut a 1Mi batch into 8
+    # stream-overlapped chunks, where a launch's duration includes its neighbour's share of the
+    # CU), a few steps on the same stream and data.
     eng.set_option("chunks", 1)
     eng.timing_reset()
     for _ in range(3):
@@ -318,7 +318,8 @@ def main():
                     unit="T lane-instr/s (32-bit VALU; achieved = frozen gfx950 minimum-"
                          "instruction model x reports / kernel time; peak = guide vector rate)",
                     frac=d["frac"], traffic=kc.get(dom, {}).get("bytes"),
-                    traffic_source=f"{counts.get('source')} (PMC FETCH_SIZE*2+WRITE_SIZE, bytes/launch)",
+                    traffic_source=f"{kc.get(dom, {}).get('source', counts.get('source'))} "
+                                   "(PMC FETCH_SIZE*2+WRITE_SIZE, bytes/launch)",
                     kernel=dom, ms_avg=d["ms_avg"],
                     model_instr_per_report=d["model_instr_per_report"],
                     issued_instr_per_report=d.get("issued_instr_per_report"),
@@ -329,8 +330,7 @@ def main():
                     step=dict(model_instr_per_report=step_model,
                               achieved=step_model * n * args.steps / elapsed / 1e12,
                               frac=step_model * n * args.steps / elapsed / 1e12 / peak_T,
-                              note="whole timed step (all kernels, stream-overlapped chunks), "
-                                   "per GPU"))
+                              note="whole timed step (all kernels), per GPU"))
     qk = next((k for k in ("k_query_rows", "k_query_h", "k_query_pair") if k in per_kernel), None)
     qh = per_kernel.get(qk) if qk else None
     if qh and "hbm_frac" in qh:

@@ -672,7 +672,6 @@ struct prio3_engine {
   int slow_defer = 1; // Histogram P <= 32: slow path deferred to the end of the run
                       // (VERDICT r1 item 11); 0: a k_xof_slow launch per chunk
   int prep_fused = 1; // Histogram P = 32: XOF + query in one launch (k_prep_h); 0: two kernels
-  int prep_persist = 0;  // k_prep_h as a persistent grid with out-of-step waves (k_prep_hp)
   int qpair = 0;  // option: P = 16/32 query on lane pairs (k_query_pair; A/B: slower)
   // option: helper XOF on lane pairs (k_xof_pair): -1 auto (shares of >= 2048 elements), 0, 1
   int xof_pair = -1;

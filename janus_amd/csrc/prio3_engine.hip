@@ -1476,30 +1476,6 @@ __global__ __launch_bounds__(256, 3) void k_prep_h(DevParams p, InPtrs in, Scrat
   query_h_body<2, 32, 1, 3, 0, false>(p, in, sc, out, r);
 }
 
-// k_prep_hp<FUSE>: k_prep_h as a persistent grid (option prep_persist) -- one 64-report tile
-// per wave and iteration, waves striding over the tiles.  A wave of an odd block runs one tile
-// behind (XOF of tile i+1 before the query of tile i), so the waves sharing a SIMD drift out
-// of step: one wave's memory-bound query beside the others' issue-bound Keccak instead of every
-// wave of a launch round entering its query at the same time.
-template <bool FUSE>
-__global__ __launch_bounds__(256, 3) void k_prep_hp(DevParams p, InPtrs in, Scratch sc,
-                                                    OutPtrs out) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
-  const uint32_t ntiles = (p.n + 63) >> 6;
-  const uint32_t lag = blockIdx.x & 1u;  // tiles the query trails the XOF by
-  // one call site per body (each is inlined once): iteration i runs the XOF of tile w0 + i nw
-  // and the query of tile w0 + (i - lag) nw, while either exists (wave-uniform)
-  for (uint32_t i = 0;; i++) {
-    const uint32_t tx = w0 + i * nw;
-    const bool qv = i >= lag;
-    const uint32_t tq = qv ? w0 + (i - lag) * nw : 0u;
-    if (tx >= ntiles && (!qv || tq >= ntiles)) break;
-    if (tx < ntiles) xofd_body<FUSE, false>(p, in, sc, tx * 64u + lane);
-    if (qv && tq < ntiles) query_h_body<2, 32, 1, 3, 0, false>(p, in, sc, out, tq * 64u + lane);
-  }
-}
 
 
 // ------------------------------------------------------------------------------------
@@ -2959,13 +2935,7 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
     if (!paired && prep_fused_takes(e, dp, fuse)) {
       dp.slow_defer = 1u;
       if (deferred) *deferred = true;
-      if (e->prep_persist) {
-        const uint32_t pb = std::min(blocks, (uint32_t)e->n_cu * 3u);  // 3 blocks per CU resident
-        if (fuse)
-          TIMED(e, st, "k_prep_h", (k_prep_hp<true><<<pb, 256, 0, st>>>(dp, in, sc, out)));
-        else
-          TIMED(e, st, "k_prep_h", (k_prep_hp<false><<<pb, 256, 0, st>>>(dp, in, sc, out)));
-      } else if (fuse)
+      if (fuse)
         TIMED(e, st, "k_prep_h", (k_prep_h<true><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
       else
         TIMED(e, st, "k_prep_h", (k_prep_h<false><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
@@ -3539,7 +3509,6 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
               {"qsum_occ", &e->qsum_occ},          {"fuse_q", &e->fuse_q},
               {"fp_round", &e->fp_round},          {"qrows", &e->qrows},
               {"slow_defer", &e->slow_defer},      {"prep_fused", &e->prep_fused},
-              {"prep_persist", &e->prep_persist},
               {"qh_prefetch", &e->qh_prefetch},    {"split_xof", &e->split_xof},
               {"qpair", &e->qpair},                {"timing", &e->timing},
               {"coalesce", &e->coalesce},          {"experimental_fpvec", &e->experimental_fpvec},

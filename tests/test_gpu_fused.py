@@ -161,10 +161,10 @@ def test_out_of_range_segment_ids_are_excluded(name, fuse):
     _run(CONFIGS[name], 900, seed=31, n_segments=3, oob_frac=0.05, fuse=fuse)
 
 
-@pytest.mark.parametrize("opts", [{"prep_persist": 1}, {"prep_persist": 1, "chunks": 3},
-                                  {"prep_fused": 0}])
+@pytest.mark.parametrize("opts", [{}, {"chunks": 3}, {"prep_fused": 0}])
 def test_fused_accumulate_on_fused_prepare_variants(opts):
-    """The fused accumulate (wave partials in the XOF) under the persistent out-of-step k_prep_hp
-    and the two-kernel chain, segment runs inside waves, tampered reports, the host mask."""
+    """The fused accumulate (wave partials in the XOF) under the fused XOF + query kernel (one
+    launch or three stream-overlapped chunks) and the two-kernel chain: segment runs inside
+    waves, tampered reports, the host mask, every report on the deferred slow path."""
     _run(CONFIGS["hist_256_c16"], 3000, seed=91, n_segments=4, opts=opts)
     _run(CONFIGS["hist_256_c16"], 256, seed=92, force_slow=True, opts=opts)

@@ -328,11 +328,3 @@ def test_fused_prepare_kernel_parity(name, opts):
     the two-kernel chain with the slow path deferred or per chunk, on tampered ragged batches."""
     _check_against_oracle(CONFIGS[name], 777, seed=83, opts=opts)
 
-
-@pytest.mark.parametrize("n", [1, 300, 5000])
-def test_fused_prepare_persistent_parity(n):
-    """Option prep_persist: k_prep_h as a persistent grid whose odd blocks run the query one tile
-    behind the XOF (k_prep_hp) -- ragged tiles, a batch smaller than one wave, and more tiles
-    than resident waves would need at a small grid are covered through the oracle."""
-    _check_against_oracle(CONFIGS["hist_256_c16"], n, seed=85 + n, tamper=n > 100,
-                          opts={"prep_persist": 1})
