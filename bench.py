@@ -162,6 +162,8 @@ def main():
     ap.add_argument("--vdaf", choices=["count", "sumvec", "sum32"], default="sumvec",
                     help="--role config: C1 Prio3Count (100k), C3 Prio3SumVec 8x1000 chunk 63 "
                          "(1M/8 per GPU), C4 Prio3Sum 32 (10M/8 per GPU)")
+    ap.add_argument("--hpke-aead", type=int, choices=[1, 2, 3], default=1,
+                    help="--role hpke: AEAD id (1 AES-128-GCM, 2 AES-256-GCM, 3 ChaCha20Poly1305)")
     ap.add_argument("--leader-vdaf", choices=["hist", "sum32"], default="hist",
                     help="--role leader: Prio3Histogram(256,16) at 1Mi (default) or Prio3Sum(32) "
                          "at C4's 1.25M per GPU")
@@ -617,7 +619,9 @@ def hpke_main(args):
     n = args.reports
     uniq = min(n, 1 << 18)
     t0 = time.perf_counter()
-    d = H.make_batch_fast(uniq, 48, 32, seed=0x4A414E55, n_threads=cpu_threads())
+    aead = args.hpke_aead
+    aead_name = {1: "AES-128-GCM", 2: "AES-256-GCM", 3: "ChaCha20Poly1305"}[aead]
+    d = H.make_batch_fast(uniq, 48, 32, seed=0x4A414E55, n_threads=cpu_threads(), aead=aead)
     gen_s = time.perf_counter() - t0
     reps = -(-n // uniq)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(np.concatenate([a] * reps)[:n])).to(dev)
@@ -625,7 +629,7 @@ def hpke_main(args):
     ids, times, pubs = T(d["report_ids"]), T(d["times"].view(np.int64)), T(d["pubs"])
     shares = torch.empty((n, 48), dtype=torch.uint8, device=dev)
     status = torch.empty(n, dtype=torch.uint8, device=dev)
-    op = G.HpkeOpener(d["skR"], d["pkR"], device=0)
+    op = G.HpkeOpener(d["skR"], d["pkR"], device=0, aead_id=aead)
 
     def step():
         op.open_input_shares_device(d["task_id"], enc, ct, ct_len, ids, times, pubs, shares,
@@ -647,7 +651,7 @@ def hpke_main(args):
     counts = json.load(open(COUNTS_PATH)) if os.path.exists(COUNTS_PATH) else dict(kernels={})
     kc = counts["kernels"].get("k_hpke_open", {})
     roofline = None
-    if "valu_instr_per_item" in kc:
+    if "valu_instr_per_item" in kc and aead == 1:  # counts were taken on the AES-128-GCM kernel
         ach = kc["valu_instr_per_item"] * n / (ms_avg / 1e3) / 1e12
         roofline = dict(bound="valu", achieved=ach, peak=PEAK_VALU_NOMINAL / 1e12,
                         unit="T lane-instr/s (32-bit VALU issue; peak = guide vector rate)",
@@ -657,13 +661,13 @@ def hpke_main(args):
                         valu_instr_per_report=kc["valu_instr_per_item"])
     ok = int((status == 0).sum().item())
     out = dict(metric="helper input shares HPKE-opened+decoded/sec (X25519-HKDF-SHA256, "
-                      "AES-128-GCM)", value=value, unit="reports/s", n_gpus=1, steps=args.steps,
+                      f"{aead_name})", value=value, unit="reports/s", n_gpus=1, steps=args.steps,
                warmup=args.warmup, ms_per_step=elapsed / args.steps * 1e3, higher_is_better=True,
                scaling="weak", vs_baseline=None, dtype="u32 limbs (GF(2^255-19), GF(2^128), bytes)",
                data=f"synthetic: {uniq} distinct sealed input shares (oracle/OpenSSL, seeded) "
                     f"tiled x{reps}; generation {gen_s:.1f}s, not timed",
                config=dict(workload="DAP helper input share open: X25519 decap + HPKE key "
-                                    "schedule + AES-128-GCM + PlaintextInputShare decode, "
+                                    f"schedule + {aead_name} + PlaintextInputShare decode, "
                                     "Prio3Histogram(256,16) shares", reports=n),
                roofline=roofline, kernel_ms_avg=ms_avg, checks=dict(opened=ok))
     if not args.no_cpu_baseline:
@@ -672,11 +676,12 @@ def hpke_main(args):
         t0 = time.perf_counter()
         csh, cst = H.open_input_shares(d["skR"], d["pkR"], d["task_id"], d["enc"][:m],
                                        d["ct"][:m], d["ct_len"][:m], d["report_ids"][:m],
-                                       d["times"][:m], d["pubs"][:m], 48, n_threads=th)
+                                       d["times"][:m], d["pubs"][:m], 48, n_threads=th,
+                                       aead=aead)
         dt = time.perf_counter() - t0
         out["cpu_baseline"] = dict(value=m / dt, unit="reports/s", cores=th, kind="port",
                                    sample=f"{m} of the sealed input shares, OpenSSL 3.0 X25519 / "
-                                          f"HMAC-SHA256 / AES-128-GCM, {th} threads, {dt:.1f}s")
+                                          f"HMAC-SHA256 / {aead_name}, {th} threads, {dt:.1f}s")
         out["speedup_vs_cpu"] = value / (m / dt)
         out["checks"]["cpu_gpu_parity_on_sample"] = bool(
             np.array_equal(shares[:m].cpu().numpy(), csh) and

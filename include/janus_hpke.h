@@ -10,9 +10,12 @@
  * duplicate / taskprov extension checks and the helper input share decode -- writing the decoded
  * helper input shares straight into the layout prio3_device_prepare[_aggregate] reads.
  *
- * Suite: mode_base, DHKEM(X25519, HKDF-SHA256) (0x0020), HKDF-SHA256 (0x0001), AES-128-GCM
- * (0x0001) -- the configuration Janus generates by default (hpke.rs:260-300).  Other suites
- * return JANUS_HPKE_EUNSUPPORTED at creation; the host keeps its CPU path for them.
+ * Suites: mode_base, DHKEM(X25519, HKDF-SHA256) (0x0020), HKDF-SHA256 (0x0001), with any of the
+ * three AEADs of messages/src/lib.rs:844-853 (HpkeAeadId): AES-128-GCM (0x0001, the
+ * configuration Janus generates by default, hpke.rs:260-300), AES-256-GCM (0x0002) and
+ * ChaCha20Poly1305 (0x0003).  The other KEMs (P-256 0x0010, P-384, P-521, X448) and KDFs
+ * (HKDF-SHA384 / -SHA512) return JANUS_HPKE_EUNSUPPORTED at creation; the host keeps its CPU
+ * path for them.
  *
  * Conventions as in janus_prio3.h: plain pointers and sizes, caller-owned buffers, device
  * pointers (d_*) stream-ordered on a hipStream_t (NULL = the null stream), per-report failures
@@ -31,6 +34,8 @@ enum {
   JANUS_HPKE_KEM_X25519_HKDF_SHA256 = 0x0020,
   JANUS_HPKE_KDF_HKDF_SHA256 = 0x0001,
   JANUS_HPKE_AEAD_AES_128_GCM = 0x0001,
+  JANUS_HPKE_AEAD_AES_256_GCM = 0x0002,
+  JANUS_HPKE_AEAD_CHACHA20_POLY1305 = 0x0003,
 };
 
 /* Per-report status: the DAP PrepareError code Janus records for the report

@@ -4,7 +4,8 @@
 //   X25519 (RFC 7748 Montgomery ladder, GF(2^255-19) in 8 x 32-bit limbs: column-MAC products
 //   with v_mad_u64_u32 + carry-out words, like the Field128 MAC of prio3_device.h)
 //   -> DHKEM ExtractAndExpand and the key schedule (HMAC-SHA256, 19 compressions)
-//   -> AES-128-GCM (T-tables in LDS, bitwise GHASH) -> for DAP input shares the
+//   -> AES-128-GCM / AES-256-GCM (T-tables in LDS, bitwise GHASH) or ChaCha20Poly1305
+//   (RFC 8439: ARX keystream, Poly1305 in 26-bit limbs) -> for DAP input shares the
 //   PlaintextInputShare decode and checks of aggregator.rs:1893-1990.
 // The server scalar is the same for every lane: its bits are wave-uniform (SGPR) and the
 // ladder's conditional swaps are v_cndmask on an SGPR mask, so every report runs the same
@@ -465,6 +466,114 @@ DEV void ghash_block(uint32_t y[4], const uint32_t x[4], const uint32_t H[4]) {
 }
 
 // -------------------------------------------------------------------------------------
+// ChaCha20 (RFC 8439 2.3) and Poly1305 (2.5) for the ChaCha20Poly1305 AEAD (2.8)
+// -------------------------------------------------------------------------------------
+DEV uint32_t rotl32(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
+#define CHACHA_QR(a, b, c, d)                  \
+  a += b, d ^= a, d = rotl32(d, 16);           \
+  c += d, b ^= c, b = rotl32(b, 12);           \
+  a += b, d ^= a, d = rotl32(d, 8);            \
+  c += d, b ^= c, b = rotl32(b, 7)
+
+// one 64-byte keystream block as 16 little-endian words
+DEV void chacha20_block(const uint32_t key[8], uint32_t counter, const uint32_t nonce[3],
+                        uint32_t out[16]) {
+  uint32_t x[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key[0], key[1],
+                    key[2],      key[3],      key[4],      key[5],      key[6], key[7],
+                    counter,     nonce[0],    nonce[1],    nonce[2]};
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    CHACHA_QR(x[0], x[4], x[8], x[12]);
+    CHACHA_QR(x[1], x[5], x[9], x[13]);
+    CHACHA_QR(x[2], x[6], x[10], x[14]);
+    CHACHA_QR(x[3], x[7], x[11], x[15]);
+    CHACHA_QR(x[0], x[5], x[10], x[15]);
+    CHACHA_QR(x[1], x[6], x[11], x[12]);
+    CHACHA_QR(x[2], x[7], x[8], x[13]);
+    CHACHA_QR(x[3], x[4], x[9], x[14]);
+  }
+  const uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key[0], key[1],
+                          key[2],      key[3],      key[4],      key[5],      key[6], key[7],
+                          counter,     nonce[0],    nonce[1],    nonce[2]};
+#pragma unroll
+  for (int i = 0; i < 16; i++) out[i] = x[i] + s[i];
+}
+
+// Poly1305 over 16-byte blocks with the 2^128 pad bit (the AEAD's zero-padded data): h and r in
+// five 26-bit limbs, 32 x 32 -> 64-bit products (v_mad_u64_u32)
+struct Poly1305 {
+  uint32_t r0, r1, r2, r3, r4, h0, h1, h2, h3, h4, pad[4];
+};
+DEV void poly_init(Poly1305& P, const uint32_t otk[8]) {  // one-time key: r || s, LE words
+  P.r0 = otk[0] & 0x3ffffffu;
+  P.r1 = ((otk[0] >> 26) | (otk[1] << 6)) & 0x3ffff03u;
+  P.r2 = ((otk[1] >> 20) | (otk[2] << 12)) & 0x3ffc0ffu;
+  P.r3 = ((otk[2] >> 14) | (otk[3] << 18)) & 0x3f03fffu;
+  P.r4 = (otk[3] >> 8) & 0x00fffffu;
+  P.h0 = P.h1 = P.h2 = P.h3 = P.h4 = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) P.pad[i] = otk[4 + i];
+}
+DEV void poly_block(Poly1305& P, const uint32_t m[4]) {  // m: 16 bytes as LE words
+  constexpr uint32_t M26 = 0x3ffffffu;
+  P.h0 += m[0] & M26;
+  P.h1 += ((m[0] >> 26) | (m[1] << 6)) & M26;
+  P.h2 += ((m[1] >> 20) | (m[2] << 12)) & M26;
+  P.h3 += ((m[2] >> 14) | (m[3] << 18)) & M26;
+  P.h4 += (m[3] >> 8) | (1u << 24);
+  const uint32_t s1 = P.r1 * 5, s2 = P.r2 * 5, s3 = P.r3 * 5, s4 = P.r4 * 5;
+  typedef uint64_t u64;
+  u64 d0 = (u64)P.h0 * P.r0 + (u64)P.h1 * s4 + (u64)P.h2 * s3 + (u64)P.h3 * s2 + (u64)P.h4 * s1;
+  u64 d1 = (u64)P.h0 * P.r1 + (u64)P.h1 * P.r0 + (u64)P.h2 * s4 + (u64)P.h3 * s3 + (u64)P.h4 * s2;
+  u64 d2 = (u64)P.h0 * P.r2 + (u64)P.h1 * P.r1 + (u64)P.h2 * P.r0 + (u64)P.h3 * s4 + (u64)P.h4 * s3;
+  u64 d3 = (u64)P.h0 * P.r3 + (u64)P.h1 * P.r2 + (u64)P.h2 * P.r1 + (u64)P.h3 * P.r0 + (u64)P.h4 * s4;
+  u64 d4 = (u64)P.h0 * P.r4 + (u64)P.h1 * P.r3 + (u64)P.h2 * P.r2 + (u64)P.h3 * P.r1 + (u64)P.h4 * P.r0;
+  uint32_t c = (uint32_t)(d0 >> 26);
+  P.h0 = (uint32_t)d0 & M26;
+  d1 += c, c = (uint32_t)(d1 >> 26), P.h1 = (uint32_t)d1 & M26;
+  d2 += c, c = (uint32_t)(d2 >> 26), P.h2 = (uint32_t)d2 & M26;
+  d3 += c, c = (uint32_t)(d3 >> 26), P.h3 = (uint32_t)d3 & M26;
+  d4 += c, c = (uint32_t)(d4 >> 26), P.h4 = (uint32_t)d4 & M26;
+  P.h0 += c * 5, c = P.h0 >> 26, P.h0 &= M26;
+  P.h1 += c;
+}
+// tag = (h mod 2^130 - 5) + s mod 2^128, LE words
+DEV void poly_finish(Poly1305& P, uint32_t tag[4]) {
+  constexpr uint32_t M26 = 0x3ffffffu;
+  uint32_t h0 = P.h0, h1 = P.h1, h2 = P.h2, h3 = P.h3, h4 = P.h4, c;
+  c = h1 >> 26, h1 &= M26, h2 += c;
+  c = h2 >> 26, h2 &= M26, h3 += c;
+  c = h3 >> 26, h3 &= M26, h4 += c;
+  c = h4 >> 26, h4 &= M26, h0 += c * 5;
+  c = h0 >> 26, h0 &= M26, h1 += c;
+  uint32_t g0 = h0 + 5;  // h - p = h + 5 - 2^130
+  c = g0 >> 26, g0 &= M26;
+  uint32_t g1 = h1 + c;
+  c = g1 >> 26, g1 &= M26;
+  uint32_t g2 = h2 + c;
+  c = g2 >> 26, g2 &= M26;
+  uint32_t g3 = h3 + c;
+  c = g3 >> 26, g3 &= M26;
+  const uint32_t g4 = h4 + c - (1u << 26);
+  const uint32_t keep_g = (g4 >> 31) - 1u;  // all ones when h >= p
+  h0 = (h0 & ~keep_g) | (g0 & keep_g);
+  h1 = (h1 & ~keep_g) | (g1 & keep_g);
+  h2 = (h2 & ~keep_g) | (g2 & keep_g);
+  h3 = (h3 & ~keep_g) | (g3 & keep_g);
+  h4 = (h4 & ~keep_g) | (g4 & keep_g);
+  const uint32_t w0 = h0 | (h1 << 26), w1 = (h1 >> 6) | (h2 << 20), w2 = (h2 >> 12) | (h3 << 14),
+                 w3 = (h3 >> 18) | (h4 << 8);
+  uint64_t f = (uint64_t)w0 + P.pad[0];
+  tag[0] = (uint32_t)f;
+  f = (uint64_t)w1 + P.pad[1] + (f >> 32);
+  tag[1] = (uint32_t)f;
+  f = (uint64_t)w2 + P.pad[2] + (f >> 32);
+  tag[2] = (uint32_t)f;
+  f = (uint64_t)w3 + P.pad[3] + (f >> 32);
+  tag[3] = (uint32_t)f;
+}
+
+// -------------------------------------------------------------------------------------
 // Kernel
 // -------------------------------------------------------------------------------------
 struct HpkeParams {
@@ -473,6 +582,7 @@ struct HpkeParams {
   uint32_t ksc[17];      // key_schedule_context (65 bytes) as BE words, zero padded
   uint32_t task[8];      // task ID (input-share AAD), BE words
   uint32_t ipad0[8], opad0[8];  // HMAC midstates of the empty key
+  uint32_t aead;                // AEAD id (1, 2, 3): selects the kernel instance
 };
 
 struct OpenArgs {
@@ -499,8 +609,11 @@ DEV void load_words(const uint8_t* p, uint32_t* w, int n16) {
 
 // MODE 0: explicit AAD, plaintext out.  MODE 1: DAP helper input share with PUB bytes of
 // public share (InputShareAad built here), decoded helper share out.
-template <int MODE, int PUB>
+// AEAD: 1 AES-128-GCM, 2 AES-256-GCM, 3 ChaCha20Poly1305 (RFC 9180 7.3 ids)
+template <int MODE, int PUB, int AEAD>
 __global__ __launch_bounds__(256) void k_hpke_open(HpkeParams P, OpenArgs a) {
+  static_assert(AEAD >= 1 && AEAD <= 3, "AEAD id");
+  constexpr uint32_t NK = AEAD == 1 ? 16 : 32;  // Nk: AEAD key bytes
   __shared__ AesT T;
   aes_tables_init(T);
   __syncthreads();
@@ -563,19 +676,19 @@ __global__ __launch_bounds__(256) void k_hpke_open(HpkeParams P, OpenArgs a) {
     mbyte(m, 13, 0x00);
     mbyte(m, 14, 0x01);
     mbyte(m, 15, 0x00);
-    mbyte(m, 16, 0x01);
+    mbyte(m, 16, AEAD);
     mstr(m, 17, "secret");
     HmacKey k;
     hmac_key32(k, ss);
     hmac(k, m, 23, secret);
   }
-  {  // key / base_nonce = LabeledExpand(secret, "key" | "base_nonce", ksc, 16 | 12)
+  {  // key / base_nonce = LabeledExpand(secret, "key" | "base_nonce", ksc, Nk | 12)
     HmacKey k;
     hmac_key32(k, secret);
     Msg32<32> m;
     mz(m);
     mbyte(m, 0, 0);
-    mbyte(m, 1, 16);
+    mbyte(m, 1, NK);
     mstr(m, 2, "HPKE-v1");
     mstr(m, 9, "HPKE");
     mbyte(m, 13, 0x00);
@@ -583,7 +696,7 @@ __global__ __launch_bounds__(256) void k_hpke_open(HpkeParams P, OpenArgs a) {
     mbyte(m, 15, 0x00);
     mbyte(m, 16, 0x01);
     mbyte(m, 17, 0x00);
-    mbyte(m, 18, 0x01);
+    mbyte(m, 18, AEAD);
     mstr(m, 19, "key");
     mwords_be(m, 22, P.ksc, 17);  // 65 bytes + 3 zero padding bytes
     mbyte(m, 87, 0x01);
@@ -599,27 +712,132 @@ __global__ __launch_bounds__(256) void k_hpke_open(HpkeParams P, OpenArgs a) {
     mbyte(n2, 15, 0x00);
     mbyte(n2, 16, 0x01);
     mbyte(n2, 17, 0x00);
-    mbyte(n2, 18, 0x01);
+    mbyte(n2, 18, AEAD);
     mstr(n2, 19, "base_nonce");
     mwords_be(n2, 29, P.ksc, 17);
     mbyte(n2, 94, 0x01);
     hmac(k, n2, 95, noncew);
   }
-  // ---- AES-128-GCM open, sequence number 0 (nonce = base_nonce) ----------------------
-  uint32_t kcol[4], rk[44];
+  uint32_t aad_len, pt_len;
+  uint8_t* pp;
+  if constexpr (AEAD == 3) {
+  // ---- ChaCha20Poly1305 open (AEAD 3, RFC 8439 2.8), sequence number 0 -------------------
+  uint32_t ckey[8], cnon[3];
 #pragma unroll
-  for (int i = 0; i < 4; i++) kcol[i] = __builtin_bswap32(keyw[i]);
-  aes128_expand(T, kcol, rk);
+  for (int i = 0; i < 8; i++) ckey[i] = __builtin_bswap32(keyw[i]);  // key bytes as LE words
+#pragma unroll
+  for (int i = 0; i < 3; i++) cnon[i] = __builtin_bswap32(noncew[i]);
+  Poly1305 mac;
+  {
+    uint32_t b0[16];
+    chacha20_block(ckey, 0, cnon, b0);  // Poly1305 one-time key = first 32 bytes of block 0
+    poly_init(mac, b0);
+  }
+  if constexpr (MODE == 1) {
+    // InputShareAad (as the GCM path builds it), zero padded to 16 bytes, as LE words
+    constexpr int AW = (60 + PUB + 3) / 4;
+    uint32_t aw[((AW + 3) / 4) * 4];
+#pragma unroll
+    for (int i = 0; i < ((AW + 3) / 4) * 4; i++) aw[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) aw[i] = __builtin_bswap32(P.task[i]);
+    uint32_t idw[4];
+    load16(a.ids + 16 * (size_t)r, idw);
+#pragma unroll
+    for (int i = 0; i < 4; i++) aw[8 + i] = idw[i];
+    const uint64_t tm = a.times[r];
+    aw[12] = __builtin_bswap32((uint32_t)(tm >> 32));
+    aw[13] = __builtin_bswap32((uint32_t)tm);
+    aw[14] = __builtin_bswap32((uint32_t)PUB);
+    if constexpr (PUB > 0) {
+      uint32_t pw[PUB / 4];
+#pragma unroll
+      for (int i = 0; i < PUB / 16; i++) load16(a.pubs + (size_t)PUB * r + 16 * i, pw + 4 * i);
+#pragma unroll
+      for (int i = 0; i < PUB / 4; i++) aw[15 + i] = pw[i];
+    }
+    aad_len = 60 + PUB;
+#pragma unroll
+    for (int b = 0; b < (AW + 3) / 4; b++) poly_block(mac, aw + 4 * b);
+  } else {
+    aad_len = a.aad_len[r];
+    const uint8_t* ap = a.aad + (size_t)a.aad_stride * r;
+    for (uint32_t off = 0; off < aad_len; off += 16) {
+      uint32_t xw[4];
+      load16(ap + off, xw);
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t lo = off + 4 * i;  // bytes past the end are zero
+        const uint32_t keep = lo + 4 <= aad_len ? 0xffffffffu
+                              : lo >= aad_len  ? 0u
+                                               : (1u << (8 * (aad_len - lo))) - 1u;
+        xw[i] &= keep;
+      }
+      poly_block(mac, xw);
+    }
+  }
+  const uint32_t ct_len = a.ct_len[r];
+  const bool len_ok = ct_len >= 16 && ct_len <= a.ct_stride;
+  ok = ok && len_ok;
+  pt_len = len_ok ? ct_len - 16 : 0;
+  const uint8_t* cp = a.ct + (size_t)a.ct_stride * r;
+  pp = a.pt + (size_t)a.ct_stride * r;
+  for (uint32_t off0 = 0, blk = 1; off0 < pt_len; off0 += 64, blk++) {
+    uint32_t ks[16];
+    chacha20_block(ckey, blk, cnon, ks);
+#pragma unroll
+    for (int c4 = 0; c4 < 4; c4++) {
+      const uint32_t off = off0 + 16 * c4;
+      if (off >= pt_len) break;
+      uint32_t cw[4], xw[4], pw[4];
+      load16(cp + off, cw);
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t lo = off + 4 * i;
+        const uint32_t keep = lo + 4 <= pt_len ? 0xffffffffu
+                              : lo >= pt_len  ? 0u
+                                              : (1u << (8 * (pt_len - lo))) - 1u;
+        xw[i] = cw[i] & keep;
+        pw[i] = (cw[i] ^ ks[4 * c4 + i]) & keep;
+      }
+      poly_block(mac, xw);
+      *(uint4*)(pp + off) = make_uint4(pw[0], pw[1], pw[2], pw[3]);
+    }
+  }
+  {  // le64(aad_len) || le64(ct_len), tag
+    const uint32_t lw[4] = {aad_len, 0, pt_len, 0};
+    poly_block(mac, lw);
+    uint32_t tag[4];
+    poly_finish(mac, tag);
+    uint32_t diff = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      uint32_t got = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) got |= (uint32_t)cp[pt_len + 4 * i + j] << (8 * j);
+      diff |= tag[i] ^ got;
+    }
+    ok = ok && diff == 0;
+  }
+  } else {
+  // ---- AES-GCM open (AEAD 1, 2), sequence number 0 (nonce = base_nonce) --------------
+  constexpr int NR = AEAD == 1 ? 10 : 14;
+  uint32_t kcol[8], rk[4 * (NR + 1)];
+#pragma unroll
+  for (int i = 0; i < 8; i++) kcol[i] = __builtin_bswap32(keyw[i]);
+  if constexpr (AEAD == 1)
+    aes128_expand(T, kcol, rk);
+  else
+    aes256_expand(T, kcol, rk);
   uint32_t H[4];
   {
     const uint32_t z[4] = {0, 0, 0, 0};
     uint32_t hc[4];
-    aes128_encrypt(T, rk, z, hc);
+    aes_encrypt<NR>(T, rk, z, hc);
 #pragma unroll
     for (int i = 0; i < 4; i++) H[i] = __builtin_bswap32(hc[i]);
   }
   uint32_t y[4] = {0, 0, 0, 0};
-  uint32_t aad_len;
   if constexpr (MODE == 1) {
     // InputShareAad: task_id (32) || report_id (16) || time (u64 BE) || u32 BE len || public
     constexpr int AW = (60 + PUB + 3) / 4;
@@ -666,9 +884,9 @@ __global__ __launch_bounds__(256) void k_hpke_open(HpkeParams P, OpenArgs a) {
   const uint32_t ct_len = a.ct_len[r];
   const bool len_ok = ct_len >= 16 && ct_len <= a.ct_stride;
   ok = ok && len_ok;
-  const uint32_t pt_len = len_ok ? ct_len - 16 : 0;
+  pt_len = len_ok ? ct_len - 16 : 0;
   const uint8_t* cp = a.ct + (size_t)a.ct_stride * r;
-  uint8_t* pp = a.pt + (size_t)a.ct_stride * r;
+  pp = a.pt + (size_t)a.ct_stride * r;
   uint32_t ctr[4];
 #pragma unroll
   for (int i = 0; i < 3; i++) ctr[i] = __builtin_bswap32(noncew[i]);
@@ -676,7 +894,7 @@ __global__ __launch_bounds__(256) void k_hpke_open(HpkeParams P, OpenArgs a) {
     uint32_t cw[4], ks[4];
     load16(cp + off, cw);
     ctr[3] = __builtin_bswap32(blk);
-    aes128_encrypt(T, rk, ctr, ks);
+    aes_encrypt<NR>(T, rk, ctr, ks);
     uint32_t xw[4], pw[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -695,7 +913,7 @@ __global__ __launch_bounds__(256) void k_hpke_open(HpkeParams P, OpenArgs a) {
     ghash_block(y, lw, H);
     ctr[3] = __builtin_bswap32(1u);
     uint32_t ek[4];
-    aes128_encrypt(T, rk, ctr, ek);
+    aes_encrypt<NR>(T, rk, ctr, ek);
     uint32_t diff = 0;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -706,6 +924,7 @@ __global__ __launch_bounds__(256) void k_hpke_open(HpkeParams P, OpenArgs a) {
       diff |= t ^ got;
     }
     ok = ok && diff == 0;
+  }
   }
   if constexpr (MODE == 0) {
     a.status[r] = ok ? JANUS_HPKE_OK : JANUS_HPKE_DECRYPT_ERROR;
@@ -797,7 +1016,10 @@ std::vector<uint8_t> cat(std::initializer_list<std::vector<uint8_t>> parts) {
 }
 std::vector<uint8_t> bytes(const char* s) { return std::vector<uint8_t>(s, s + strlen(s)); }
 
-const std::vector<uint8_t> kSuite = {'H', 'P', 'K', 'E', 0x00, 0x20, 0x00, 0x01, 0x00, 0x01};
+// suite_id = "HPKE" || kem_id || kdf_id || aead_id (RFC 9180 5.1)
+std::vector<uint8_t> hpke_suite(uint16_t aead) {
+  return {'H', 'P', 'K', 'E', 0x00, 0x20, 0x00, 0x01, (uint8_t)(aead >> 8), (uint8_t)aead};
+}
 
 uint32_t be32(const uint8_t* p) {
   return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3];
@@ -841,7 +1063,8 @@ int janus_hpke_opener_create(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id,
   if (!out || !private_key || !public_key || (info_len && !info)) return JANUS_HPKE_EINVAL;
   *out = nullptr;
   if (kem_id != JANUS_HPKE_KEM_X25519_HKDF_SHA256 || kdf_id != JANUS_HPKE_KDF_HKDF_SHA256 ||
-      aead_id != JANUS_HPKE_AEAD_AES_128_GCM)
+      (aead_id != JANUS_HPKE_AEAD_AES_128_GCM && aead_id != JANUS_HPKE_AEAD_AES_256_GCM &&
+       aead_id != JANUS_HPKE_AEAD_CHACHA20_POLY1305))
     return JANUS_HPKE_EUNSUPPORTED;
   if (private_key_len != 32 || public_key_len != 32) return JANUS_HPKE_EINVAL;
   auto* o = new janus_hpke_opener();
@@ -857,8 +1080,10 @@ int janus_hpke_opener_create(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id,
   //                        LabeledExtract("", "info_hash", info)        (RFC 9180 5.1)
   uint8_t ksc[68] = {0};
   std::vector<uint8_t> inf(info, info + info_len);
-  hmac_host(nullptr, 0, cat({bytes("HPKE-v1"), kSuite, bytes("psk_id_hash")}), ksc + 1);
-  hmac_host(nullptr, 0, cat({bytes("HPKE-v1"), kSuite, bytes("info_hash"), inf}), ksc + 33);
+  const std::vector<uint8_t> suite = hpke_suite(aead_id);
+  hmac_host(nullptr, 0, cat({bytes("HPKE-v1"), suite, bytes("psk_id_hash")}), ksc + 1);
+  hmac_host(nullptr, 0, cat({bytes("HPKE-v1"), suite, bytes("info_hash"), inf}), ksc + 33);
+  o->P.aead = aead_id;
   for (int i = 0; i < 17; i++) o->P.ksc[i] = be32(ksc + 4 * i);
   // HMAC midstates of the empty key (eae_prk extraction)
   uint32_t iv[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
@@ -930,12 +1155,21 @@ static int launch_open(janus_hpke_opener* o, int mode, int pub, const OpenArgs& 
     HCHK(hipEventRecord(e0, st));
   }
   const uint32_t blocks = (a.n + 255) / 256;
-  if (mode == 0)
-    k_hpke_open<0, 0><<<blocks, 256, 0, st>>>(o->P, a);
-  else if (pub == 32)
-    k_hpke_open<1, 32><<<blocks, 256, 0, st>>>(o->P, a);
-  else
-    k_hpke_open<1, 0><<<blocks, 256, 0, st>>>(o->P, a);
+#define JANUS_HPKE_LAUNCH(AE)                                    \
+  if (mode == 0)                                                 \
+    k_hpke_open<0, 0, AE><<<blocks, 256, 0, st>>>(o->P, a);      \
+  else if (pub == 32)                                            \
+    k_hpke_open<1, 32, AE><<<blocks, 256, 0, st>>>(o->P, a);     \
+  else                                                           \
+    k_hpke_open<1, 0, AE><<<blocks, 256, 0, st>>>(o->P, a);
+  if (o->P.aead == JANUS_HPKE_AEAD_AES_256_GCM) {
+    JANUS_HPKE_LAUNCH(2)
+  } else if (o->P.aead == JANUS_HPKE_AEAD_CHACHA20_POLY1305) {
+    JANUS_HPKE_LAUNCH(3)
+  } else {
+    JANUS_HPKE_LAUNCH(1)
+  }
+#undef JANUS_HPKE_LAUNCH
   HCHK(hipGetLastError());
   if (o->timing) {
     HCHK(hipEventRecord(e1, st));

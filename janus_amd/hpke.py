@@ -17,6 +17,8 @@ from .prio3 import _np_ptr, _stream, _tptr, load_library
 KEM_X25519_HKDF_SHA256 = 0x0020
 KDF_HKDF_SHA256 = 0x0001
 AEAD_AES_128_GCM = 0x0001
+AEAD_AES_256_GCM = 0x0002
+AEAD_CHACHA20_POLY1305 = 0x0003
 OK, DECRYPT_ERROR, INVALID_MESSAGE = 0, 4, 8
 INFO_INPUT_SHARE_HELPER = b"dap-09 input share" + bytes([1, 3])  # Label::InputShare, Client->Helper
 

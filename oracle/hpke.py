@@ -1,6 +1,7 @@
 """ctypes binding of oracle/hpke_oracle.c -- TEST INFRASTRUCTURE (checker + CPU baseline).
 
-HPKE base mode, DHKEM(X25519, HKDF-SHA256) / HKDF-SHA256 / AES-128-GCM (RFC 9180) composed over
+HPKE base mode, DHKEM(X25519, HKDF-SHA256) / HKDF-SHA256 / AES-128-GCM, AES-256-GCM or
+ChaCha20Poly1305 (RFC 9180) composed over
 OpenSSL 3.0 primitives, plus Janus's helper input-share layer (aggregator.rs:1796-1990).
 """
 from __future__ import annotations
@@ -40,6 +41,12 @@ def lib():
                                                 C.c_uint32, vp, C.c_uint32, C.c_uint32, vp, vp,
                                                 vp, C.c_int]
         _lib.aes128_ctr64_keystream.argtypes = [vp, vp, vp, C.c_size_t]
+        # the AEAD-selecting forms (aead 1 AES-128-GCM, 2 AES-256-GCM, 3 ChaCha20Poly1305)
+        u16 = C.c_uint16
+        _lib.hpke_open_ex.argtypes = [u16] + _lib.hpke_open.argtypes
+        _lib.hpke_seal_ex.argtypes = [u16] + _lib.hpke_seal.argtypes
+        _lib.hpke_open_input_shares_ex.argtypes = [u16] + _lib.hpke_open_input_shares.argtypes
+        _lib.hpke_make_input_shares_ex.argtypes = [u16] + _lib.hpke_make_input_shares.argtypes
     return _lib
 
 
@@ -57,18 +64,18 @@ def x25519_public(sk: bytes) -> bytes:
     return out.raw
 
 
-def open_(skR: bytes, pkR: bytes, enc: bytes, info: bytes, aad: bytes, ct: bytes):
+def open_(skR: bytes, pkR: bytes, enc: bytes, info: bytes, aad: bytes, ct: bytes, aead=1):
     pt = C.create_string_buffer(max(len(ct), 1))
-    n = lib().hpke_open(_p(skR), _p(pkR), _p(enc), _p(info), len(info), _p(aad), len(aad),
-                        _p(ct), len(ct), pt)
+    n = lib().hpke_open_ex(aead, _p(skR), _p(pkR), _p(enc), _p(info), len(info), _p(aad),
+                           len(aad), _p(ct), len(ct), pt)
     return None if n < 0 else pt.raw[:n]
 
 
-def seal(pkR: bytes, skE: bytes, info: bytes, aad: bytes, pt: bytes):
+def seal(pkR: bytes, skE: bytes, info: bytes, aad: bytes, pt: bytes, aead=1):
     enc = C.create_string_buffer(32)
     ct = C.create_string_buffer(len(pt) + 16)
-    assert lib().hpke_seal(_p(pkR), _p(skE), _p(info), len(info), _p(aad), len(aad), _p(pt),
-                           len(pt), enc, ct) == 0
+    assert lib().hpke_seal_ex(aead, _p(pkR), _p(skE), _p(info), len(info), _p(aad), len(aad),
+                              _p(pt), len(pt), enc, ct) == 0
     return enc.raw, ct.raw
 
 
@@ -86,7 +93,7 @@ def plaintext_input_share(payload: bytes, extensions=()) -> bytes:
 
 
 def open_input_shares(skR, pkR, task_id, enc, ct, ct_len, report_ids, times, pubs, share_len,
-                      require_taskprov=False, n_threads=8):
+                      require_taskprov=False, n_threads=8, aead=1):
     """Batched helper input-share open: (shares [n, share_len], status [n] in {0, 4, 8})."""
     n = enc.shape[0]
     enc = np.ascontiguousarray(enc, np.uint8)
@@ -98,13 +105,14 @@ def open_input_shares(skR, pkR, task_id, enc, ct, ct_len, report_ids, times, pub
     pubs = None if pubs is None else np.ascontiguousarray(pubs, np.uint8)
     shares = np.zeros((n, share_len), np.uint8)
     status = np.zeros(n, np.uint8)
-    lib().hpke_open_input_shares(_p(skR), _p(pkR), _p(task_id), n, _p(enc), _p(ct), _p(ct_len),
-                                 ct.shape[1], _p(ids), _p(times), _p(pubs), publen, share_len,
-                                 int(require_taskprov), _p(shares), _p(status), n_threads)
+    lib().hpke_open_input_shares_ex(aead, _p(skR), _p(pkR), _p(task_id), n, _p(enc), _p(ct),
+                                    _p(ct_len), ct.shape[1], _p(ids), _p(times), _p(pubs),
+                                    publen, share_len, int(require_taskprov), _p(shares),
+                                    _p(status), n_threads)
     return shares, status
 
 
-def make_batch(n, share_len, pub_len, seed=1, skR=None, extensions=(), tamper=0.0):
+def make_batch(n, share_len, pub_len, seed=1, skR=None, extensions=(), tamper=0.0, aead=1):
     """Synthetic Janus-shaped encrypted helper input shares (test/bench data), sealed by the
     oracle with deterministic ephemeral keys.  Returns a dict of numpy arrays."""
     rng = np.random.default_rng(seed)
@@ -125,14 +133,14 @@ def make_batch(n, share_len, pub_len, seed=1, skR=None, extensions=(), tamper=0.
                               b"" if pubs is None else pubs[r].tobytes())
         skE = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
         e, c = seal(pkR, skE, INFO_INPUT_SHARE_HELPER, aad,
-                    plaintext_input_share(shares[r].tobytes(), extensions))
+                    plaintext_input_share(shares[r].tobytes(), extensions), aead=aead)
         enc[r] = np.frombuffer(e, np.uint8)
         ct[r] = np.frombuffer(c, np.uint8)
     return dict(skR=skR, pkR=pkR, task_id=task_id, report_ids=ids, times=times, pubs=pubs,
                 shares=shares, enc=enc, ct=ct, ct_len=ct_len)
 
 
-def make_batch_fast(n, share_len, pub_len, seed=1, taskprov=False, n_threads=8, skR=None):
+def make_batch_fast(n, share_len, pub_len, seed=1, taskprov=False, n_threads=8, skR=None, aead=1):
     """make_batch in C with threads (bench-size batches); every report distinct."""
     rng = np.random.default_rng(seed)
     skR = bytes(rng.integers(0, 256, 32, dtype=np.uint8)) if skR is None else skR
@@ -146,9 +154,10 @@ def make_batch_fast(n, share_len, pub_len, seed=1, taskprov=False, n_threads=8, 
     times = np.zeros(n, np.uint64)
     pubs = np.zeros((n, pub_len), np.uint8) if pub_len else None
     shares = np.zeros((n, share_len), np.uint8)
-    rc = lib().hpke_make_input_shares(_p(pkR), _p(task_id), n, seed, share_len, pub_len,
-                                      int(taskprov), stride, _p(enc), _p(ct), _p(ct_len), _p(ids),
-                                      _p(times), _p(pubs), _p(shares), n_threads)
+    rc = lib().hpke_make_input_shares_ex(aead, _p(pkR), _p(task_id), n, seed, share_len,
+                                         pub_len, int(taskprov), stride, _p(enc), _p(ct),
+                                         _p(ct_len), _p(ids), _p(times), _p(pubs), _p(shares),
+                                         n_threads)
     assert rc == 0
     return dict(skR=skR, pkR=pkR, task_id=task_id, report_ids=ids, times=times, pubs=pubs,
                 shares=shares, enc=enc, ct=ct, ct_len=ct_len)

@@ -3,7 +3,8 @@
  * TEST INFRASTRUCTURE ONLY: the checker for tests/ and bench.py's cpu_baseline leg.
  *
  * HPKE base mode (RFC 9180 §5.1, §5.2) with DHKEM(X25519, HKDF-SHA256) (§4.1, §7.1),
- * HKDF-SHA256 and AES-128-GCM -- the suite Janus generates by default
+ * HKDF-SHA256 and AES-128-GCM -- the suite Janus generates by default -- or AES-256-GCM /
+ * ChaCha20Poly1305 (pinned by the RFC 9180 vectors for kem 0x20 / kdf 1 / aead 2 and 3)
  * (/root/reference/core/src/hpke.rs:260-280, generate_test_hpke_config_and_private_key), whose
  * Rust implementation (hpke-dispatch -> hpke crate) is not in /root/reference.  The RFC 9180
  * composition (labels, suite ids, key schedule) is restated here over OpenSSL 3.0 primitives
@@ -28,7 +29,15 @@
 enum { HPKE_OK = 0, HPKE_DECRYPT_ERROR = 4, HPKE_INVALID_MESSAGE = 8 };
 
 static const uint8_t KEM_SUITE[5] = {'K', 'E', 'M', 0x00, 0x20};
-static const uint8_t HPKE_SUITE[10] = {'H', 'P', 'K', 'E', 0x00, 0x20, 0x00, 0x01, 0x00, 0x01};
+/* suite_id = "HPKE" || kem || kdf || aead (RFC 9180 5.1); aead 1 AES-128-GCM, 2 AES-256-GCM,
+ * 3 ChaCha20Poly1305 (messages/src/lib.rs:844-853) */
+static void hpke_suite(uint16_t aead, uint8_t s[10]) {
+  static const uint8_t base[8] = {'H', 'P', 'K', 'E', 0x00, 0x20, 0x00, 0x01};
+  memcpy(s, base, 8);
+  s[8] = (uint8_t)(aead >> 8);
+  s[9] = (uint8_t)aead;
+}
+static size_t aead_nk(uint16_t aead) { return aead == 1 ? 16 : 32; }
 
 static void hmac256(const uint8_t* key, size_t klen, const uint8_t* msg, size_t mlen,
                     uint8_t out[32]) {
@@ -88,16 +97,17 @@ int hpke_x25519_public(const uint8_t sk[32], uint8_t pk[32]) {
   return ok ? 0 : -1;
 }
 
-/* KeySchedule(mode_base, shared_secret, info) -> key (16), base_nonce (12)  [RFC 9180 §5.1] */
-static void key_schedule(const uint8_t ss[32], const uint8_t* info, size_t infolen,
-                         uint8_t key[16], uint8_t nonce[12]) {
-  uint8_t ksc[65], secret[32];
+/* KeySchedule(mode_base, shared_secret, info) -> key (Nk), base_nonce (12)  [RFC 9180 §5.1] */
+static void key_schedule(uint16_t aead, const uint8_t ss[32], const uint8_t* info,
+                         size_t infolen, uint8_t key[32], uint8_t nonce[12]) {
+  uint8_t ksc[65], secret[32], su[10];
+  hpke_suite(aead, su);
   ksc[0] = 0x00;  /* mode_base */
-  labeled_extract(HPKE_SUITE, 10, NULL, 0, "psk_id_hash", NULL, 0, ksc + 1);
-  labeled_extract(HPKE_SUITE, 10, NULL, 0, "info_hash", info, infolen, ksc + 33);
-  labeled_extract(HPKE_SUITE, 10, ss, 32, "secret", NULL, 0, secret);
-  labeled_expand(HPKE_SUITE, 10, secret, "key", ksc, 65, 16, key);
-  labeled_expand(HPKE_SUITE, 10, secret, "base_nonce", ksc, 65, 12, nonce);
+  labeled_extract(su, 10, NULL, 0, "psk_id_hash", NULL, 0, ksc + 1);
+  labeled_extract(su, 10, NULL, 0, "info_hash", info, infolen, ksc + 33);
+  labeled_extract(su, 10, ss, 32, "secret", NULL, 0, secret);
+  labeled_expand(su, 10, secret, "key", ksc, 65, aead_nk(aead), key);
+  labeled_expand(su, 10, secret, "base_nonce", ksc, 65, 12, nonce);
 }
 
 /* Decap (§4.1): dh = DH(skR, enc); shared_secret = ExtractAndExpand(dh, enc || pkRm) */
@@ -114,48 +124,66 @@ static int decap(const uint8_t enc[32], const uint8_t skR[32], const uint8_t pkR
   return 0;
 }
 
-static int gcm(int decrypt, const uint8_t key[16], const uint8_t nonce[12], const uint8_t* aad,
-               size_t aadlen, const uint8_t* in, size_t inlen, uint8_t* out, uint8_t tag[16]) {
+/* the AEAD of the suite through OpenSSL's EVP AEAD interface (16-byte tag, 12-byte nonce) */
+static int aead_crypt(uint16_t aead, int decrypt, const uint8_t* key, const uint8_t nonce[12],
+                      const uint8_t* aad, size_t aadlen, const uint8_t* in, size_t inlen,
+                      uint8_t* out, uint8_t tag[16]) {
+  const EVP_CIPHER* ci = aead == 1   ? EVP_aes_128_gcm()
+                         : aead == 2 ? EVP_aes_256_gcm()
+                         : aead == 3 ? EVP_chacha20_poly1305()
+                                     : NULL;
+  if (!ci) return -1;
   EVP_CIPHER_CTX* c = EVP_CIPHER_CTX_new();
   int l = 0;
-  int ok = c && EVP_CipherInit_ex(c, EVP_aes_128_gcm(), NULL, NULL, NULL, !decrypt) == 1 &&
-                  EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_IVLEN, 12, NULL) == 1 &&
+  int ok = c && EVP_CipherInit_ex(c, ci, NULL, NULL, NULL, !decrypt) == 1 &&
+                  EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_AEAD_SET_IVLEN, 12, NULL) == 1 &&
                   EVP_CipherInit_ex(c, NULL, NULL, key, nonce, !decrypt) == 1;
   if (ok && aadlen) ok = EVP_CipherUpdate(c, NULL, &l, aad, (int)aadlen) == 1;
+  l = 0;
   if (ok && inlen) ok = EVP_CipherUpdate(c, out, &l, in, (int)inlen) == 1;
-  if (ok && decrypt) ok = EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_TAG, 16, tag) == 1;
+  if (ok && decrypt) ok = EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_AEAD_SET_TAG, 16, tag) == 1;
   int fl = 0;
   if (ok) ok = EVP_CipherFinal_ex(c, out + l, &fl) == 1;
-  if (ok && !decrypt) ok = EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_GET_TAG, 16, tag) == 1;
+  if (ok && !decrypt) ok = EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_AEAD_GET_TAG, 16, tag) == 1;
   EVP_CIPHER_CTX_free(c);
   return ok ? 0 : -1;
 }
 
 /* base-mode single-shot open (sequence number 0); returns the plaintext length or -1 */
+int hpke_open_ex(uint16_t aead, const uint8_t skR[32], const uint8_t pkR[32],
+                 const uint8_t enc[32], const uint8_t* info, size_t infolen, const uint8_t* aad,
+                 size_t aadlen, const uint8_t* ct, size_t ctlen, uint8_t* pt) {
+  uint8_t ss[32], key[32], nonce[12], tag[16];
+  if (ctlen < 16 || decap(enc, skR, pkR, ss)) return -1;
+  key_schedule(aead, ss, info, infolen, key, nonce);
+  memcpy(tag, ct + ctlen - 16, 16);
+  if (aead_crypt(aead, 1, key, nonce, aad, aadlen, ct, ctlen - 16, pt, tag)) return -1;
+  return (int)(ctlen - 16);
+}
 int hpke_open(const uint8_t skR[32], const uint8_t pkR[32], const uint8_t enc[32],
               const uint8_t* info, size_t infolen, const uint8_t* aad, size_t aadlen,
               const uint8_t* ct, size_t ctlen, uint8_t* pt) {
-  uint8_t ss[32], key[16], nonce[12], tag[16];
-  if (ctlen < 16 || decap(enc, skR, pkR, ss)) return -1;
-  key_schedule(ss, info, infolen, key, nonce);
-  memcpy(tag, ct + ctlen - 16, 16);
-  if (gcm(1, key, nonce, aad, aadlen, ct, ctlen - 16, pt, tag)) return -1;
-  return (int)(ctlen - 16);
+  return hpke_open_ex(1, skR, pkR, enc, info, infolen, aad, aadlen, ct, ctlen, pt);
 }
 
 /* base-mode seal with the ephemeral key skE (Encap with a given ephemeral key, as the RFC 9180
  * test vectors do); writes enc[32] and ct[ptlen + 16] */
-int hpke_seal(const uint8_t pkR[32], const uint8_t skE[32], const uint8_t* info, size_t infolen,
-              const uint8_t* aad, size_t aadlen, const uint8_t* pt, size_t ptlen, uint8_t enc[32],
-              uint8_t* ct) {
-  uint8_t dh[32], prk[32], kc[64], ss[32], key[16], nonce[12];
+int hpke_seal_ex(uint16_t aead, const uint8_t pkR[32], const uint8_t skE[32],
+                 const uint8_t* info, size_t infolen, const uint8_t* aad, size_t aadlen,
+                 const uint8_t* pt, size_t ptlen, uint8_t enc[32], uint8_t* ct) {
+  uint8_t dh[32], prk[32], kc[64], ss[32], key[32], nonce[12];
   if (hpke_x25519_public(skE, enc) || x25519(skE, pkR, dh)) return -1;
   labeled_extract(KEM_SUITE, 5, NULL, 0, "eae_prk", dh, 32, prk);
   memcpy(kc, enc, 32);
   memcpy(kc + 32, pkR, 32);
   labeled_expand(KEM_SUITE, 5, prk, "shared_secret", kc, 64, 32, ss);
-  key_schedule(ss, info, infolen, key, nonce);
-  return gcm(0, key, nonce, aad, aadlen, pt, ptlen, ct, ct + ptlen);
+  key_schedule(aead, ss, info, infolen, key, nonce);
+  return aead_crypt(aead, 0, key, nonce, aad, aadlen, pt, ptlen, ct, ct + ptlen);
+}
+int hpke_seal(const uint8_t pkR[32], const uint8_t skE[32], const uint8_t* info, size_t infolen,
+              const uint8_t* aad, size_t aadlen, const uint8_t* pt, size_t ptlen, uint8_t enc[32],
+              uint8_t* ct) {
+  return hpke_seal_ex(1, pkR, skE, info, infolen, aad, aadlen, pt, ptlen, enc, ct);
 }
 
 /* ---- Janus helper layer ------------------------------------------------------------ */
@@ -218,6 +246,7 @@ typedef struct {
   int require_taskprov;
   uint8_t *shares, *status;
   uint32_t lo, hi;
+  uint16_t aead;
 } Job;
 
 static const uint8_t INFO[20] = {'d', 'a', 'p', '-', '0', '9', ' ', 'i', 'n', 'p',
@@ -232,8 +261,8 @@ static void* run(void* arg) {
                                      aad);
     uint32_t cl = j->ct_len[r];
     int ptl = cl <= sizeof(pt) + 16
-                  ? hpke_open(j->skR, j->pkR, j->enc + 32 * (size_t)r, INFO, sizeof(INFO), aad, al,
-                              j->ct + (size_t)j->ct_stride * r, cl, pt)
+                  ? hpke_open_ex(j->aead, j->skR, j->pkR, j->enc + 32 * (size_t)r, INFO,
+                                 sizeof(INFO), aad, al, j->ct + (size_t)j->ct_stride * r, cl, pt)
                   : -1;
     uint8_t* so = j->shares + (size_t)j->share_len * r;
     memset(so, 0, j->share_len);
@@ -247,11 +276,13 @@ static void* run(void* arg) {
 
 /* Batched helper input-share open: status[r] = 0 (helper share written), 4 (HpkeDecryptError)
  * or 8 (InvalidMessage), the PrepareError codes of messages/src/lib.rs. */
-int hpke_open_input_shares(const uint8_t skR[32], const uint8_t pkR[32], const uint8_t task_id[32],
-                           uint32_t n, const uint8_t* enc, const uint8_t* ct, const uint32_t* ct_len,
-                           uint32_t ct_stride, const uint8_t* report_ids, const uint64_t* times,
-                           const uint8_t* pubs, uint32_t publen, uint32_t share_len,
-                           int require_taskprov, uint8_t* shares, uint8_t* status, int n_threads) {
+int hpke_open_input_shares_ex(uint16_t aead, const uint8_t skR[32], const uint8_t pkR[32],
+                              const uint8_t task_id[32], uint32_t n, const uint8_t* enc,
+                              const uint8_t* ct, const uint32_t* ct_len, uint32_t ct_stride,
+                              const uint8_t* report_ids, const uint64_t* times,
+                              const uint8_t* pubs, uint32_t publen, uint32_t share_len,
+                              int require_taskprov, uint8_t* shares, uint8_t* status,
+                              int n_threads) {
   if (n_threads < 1) n_threads = 1;
   pthread_t th[256];
   Job jobs[256];
@@ -260,11 +291,20 @@ int hpke_open_input_shares(const uint8_t skR[32], const uint8_t pkR[32], const u
     jobs[t] = (Job){skR, pkR, task_id, enc, ct, report_ids, pubs, ct_len, times, n, ct_stride,
                     publen, share_len, require_taskprov, shares, status,
                     (uint32_t)((uint64_t)n * t / n_threads),
-                    (uint32_t)((uint64_t)n * (t + 1) / n_threads)};
+                    (uint32_t)((uint64_t)n * (t + 1) / n_threads), aead};
     pthread_create(&th[t], NULL, run, &jobs[t]);
   }
   for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
   return 0;
+}
+int hpke_open_input_shares(const uint8_t skR[32], const uint8_t pkR[32], const uint8_t task_id[32],
+                           uint32_t n, const uint8_t* enc, const uint8_t* ct, const uint32_t* ct_len,
+                           uint32_t ct_stride, const uint8_t* report_ids, const uint64_t* times,
+                           const uint8_t* pubs, uint32_t publen, uint32_t share_len,
+                           int require_taskprov, uint8_t* shares, uint8_t* status, int n_threads) {
+  return hpke_open_input_shares_ex(1, skR, pkR, task_id, n, enc, ct, ct_len, ct_stride,
+                                   report_ids, times, pubs, publen, share_len, require_taskprov,
+                                   shares, status, n_threads);
 }
 
 /* ---- synthetic batch generation (bench / large tests): the client side of the same layer,
@@ -279,6 +319,7 @@ typedef struct {
   uint8_t *enc, *ct, *ids, *pubs, *shares;
   uint32_t* ct_len;
   uint64_t* times;
+  uint16_t aead;
 } GenJob;
 
 static void prf(uint64_t seed, uint32_t r, uint8_t purpose, uint8_t* out, size_t len) {
@@ -320,17 +361,18 @@ static void* gen_run(void* arg) {
     size_t al = hpke_input_share_aad(j->task_id, id, j->times[r], pub, j->publen, aad);
     uint8_t* ct = j->ct + (size_t)j->stride * r;
     memset(ct, 0, j->stride);
-    hpke_seal(j->pkR, skE, INFO, sizeof(INFO), aad, al, pt, l, j->enc + 32 * (size_t)r, ct);
+    hpke_seal_ex(j->aead, j->pkR, skE, INFO, sizeof(INFO), aad, al, pt, l,
+                 j->enc + 32 * (size_t)r, ct);
     j->ct_len[r] = (uint32_t)(l + 16);
   }
   return NULL;
 }
 
-int hpke_make_input_shares(const uint8_t pkR[32], const uint8_t task_id[32], uint32_t n,
-                           uint64_t seed, uint32_t share_len, uint32_t publen, int taskprov,
-                           uint32_t stride, uint8_t* enc, uint8_t* ct, uint32_t* ct_len,
-                           uint8_t* ids, uint64_t* times, uint8_t* pubs, uint8_t* shares,
-                           int n_threads) {
+int hpke_make_input_shares_ex(uint16_t aead, const uint8_t pkR[32], const uint8_t task_id[32],
+                              uint32_t n, uint64_t seed, uint32_t share_len, uint32_t publen,
+                              int taskprov, uint32_t stride, uint8_t* enc, uint8_t* ct,
+                              uint32_t* ct_len, uint8_t* ids, uint64_t* times, uint8_t* pubs,
+                              uint8_t* shares, int n_threads) {
   if ((taskprov ? 10u : 6u) + share_len + 16 > stride) return -1;
   if (n_threads < 1) n_threads = 1;
   if (n_threads > 256) n_threads = 256;
@@ -340,11 +382,19 @@ int hpke_make_input_shares(const uint8_t pkR[32], const uint8_t task_id[32], uin
     jobs[t] = (GenJob){pkR, task_id, seed, share_len, publen, stride,
                        (uint32_t)((uint64_t)n * t / n_threads),
                        (uint32_t)((uint64_t)n * (t + 1) / n_threads), taskprov, enc, ct, ids, pubs,
-                       shares, ct_len, times};
+                       shares, ct_len, times, aead};
     pthread_create(&th[t], NULL, gen_run, &jobs[t]);
   }
   for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
   return 0;
+}
+int hpke_make_input_shares(const uint8_t pkR[32], const uint8_t task_id[32], uint32_t n,
+                           uint64_t seed, uint32_t share_len, uint32_t publen, int taskprov,
+                           uint32_t stride, uint8_t* enc, uint8_t* ct, uint32_t* ct_len,
+                           uint8_t* ids, uint64_t* times, uint8_t* pubs, uint8_t* shares,
+                           int n_threads) {
+  return hpke_make_input_shares_ex(1, pkR, task_id, n, seed, share_len, publen, taskprov, stride,
+                                   enc, ct, ct_len, ids, times, pubs, shares, n_threads);
 }
 
 /* Seal given helper input shares (bench data for the request->response pipeline): enc[n][32],

@@ -1,5 +1,6 @@
-"""Extracts the RFC 9180 test vector(s) of the HPKE suite the GPU opener implements
-(mode_base, DHKEM(X25519, HKDF-SHA256) 0x0020, HKDF-SHA256 0x0001, AES-128-GCM 0x0001) from the
+"""Extracts the RFC 9180 test vectors of the HPKE suites the GPU opener implements
+(mode_base, DHKEM(X25519, HKDF-SHA256) 0x0020, HKDF-SHA256 0x0001, with AES-128-GCM 0x0001,
+AES-256-GCM 0x0002 and ChaCha20Poly1305 0x0003) from the
 file Janus's own HPKE test reads (/root/reference/core/src/test-vectors.json, used by
 core/src/hpke.rs `decrypt_test_vectors`).  Run in the build container only; the output fixture is
 data (keys, ciphertexts, plaintexts), committed as tests/golden/hpke_rfc9180_x25519.json."""
@@ -11,18 +12,27 @@ SRC = "/root/reference/core/src/test-vectors.json"
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "hpke_rfc9180_x25519.json")
 
 
+# (aead id, output file): AES-128-GCM (the original fixture), AES-256-GCM, ChaCha20Poly1305
+OUTS = {1: OUT,
+        2: os.path.join(os.path.dirname(OUT), "hpke_rfc9180_x25519_aes256gcm.json"),
+        3: os.path.join(os.path.dirname(OUT), "hpke_rfc9180_x25519_chacha20poly1305.json")}
+
+
 def main():
     vecs = json.load(open(SRC))
-    keep = [v for v in vecs if (v["mode"], v["kem_id"], v["kdf_id"], v["aead_id"]) == (0, 32, 1, 1)]
-    if len(keep) != 1:
-        sys.exit("expected exactly one X25519/HKDF-SHA256/AES-128-GCM base-mode vector")
-    v = keep[0]
-    out = {k: v[k] for k in ("mode", "kem_id", "kdf_id", "aead_id", "info", "enc", "pkRm", "skRm",
-                             "base_nonce")}
-    out["encryptions"] = v["encryptions"][:4]
-    out["source"] = "RFC 9180 Appendix A.1.1 via core/src/test-vectors.json"
-    json.dump(out, open(OUT, "w"), indent=1)
-    print("wrote", OUT)
+    for aead, path in OUTS.items():
+        keep = [v for v in vecs
+                if (v["mode"], v["kem_id"], v["kdf_id"], v["aead_id"]) == (0, 32, 1, aead)]
+        if len(keep) != 1:
+            sys.exit(f"expected exactly one X25519/HKDF-SHA256/aead {aead} base-mode vector")
+        v = keep[0]
+        out = {k: v[k] for k in ("mode", "kem_id", "kdf_id", "aead_id", "info", "enc", "pkRm",
+                                 "skRm", "base_nonce")}
+        out["encryptions"] = v["encryptions"][:4]
+        out["source"] = ("RFC 9180 test-vector set, core/src/test-vectors.json (read by Janus's "
+                         "hpke.rs decrypt_test_vectors)")
+        json.dump(out, open(path, "w"), indent=1)
+        print("wrote", path)
 
 
 if __name__ == "__main__":
