@@ -1852,16 +1852,18 @@ __global__ __launch_bounds__(256) void k_acc_multi(const AccDesc* descs, uint8_t
 // Fused accumulate, second half: combine the per-wave half-limb partials per segment,
 // then fix up exclusions / non-fused reports and reduce mod p.
 // ------------------------------------------------------------------------------------
-// Level 1: grid (ceil(M*8/256), chunks of WCH waves): thread = slot (element, half).  A chunk
-// whose fused waves all carry one segment writes a 64-bit chunk partial (cseg[chunk] = its
-// segment); a chunk mixing segments adds each run with a 64-bit atomic into agg64 directly
-// (cseg = ~0, as for a chunk with no fused wave).
+// Level 1: grid (ceil(M*8/1024), chunks of WCH waves): thread = 4 consecutive slots (element,
+// half), read as one 16-byte load per wave (4x the bytes in flight of a slot per thread: the
+// 1-slot version moved the 134 MB of a 1 Mi batch's wave partials at 1.8 TB/s).  A chunk whose
+// fused waves all carry one segment writes 64-bit chunk partials (cseg[chunk] = its segment); a
+// chunk mixing segments adds each run with a 64-bit atomic into agg64 directly (cseg = ~0, as
+// for a chunk with no fused wave).
 constexpr uint32_t WCH = 32;
 __global__ __launch_bounds__(256) void k_agg_waves(uint32_t nwaves, uint32_t M,
                                                    const uint32_t* wpart, const uint32_t* wseg,
                                                    unsigned long long* cpart, uint32_t* cseg,
                                                    unsigned long long* agg64) {
-  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x, c = blockIdx.y;
+  const uint32_t slot = 4 * (blockIdx.x * blockDim.x + threadIdx.x), c = blockIdx.y;
   const uint32_t w0 = c * WCH, w1 = min(nwaves, w0 + WCH);
   uint32_t s0 = 0xffffffffu;
   bool mixed = false;
@@ -1872,28 +1874,35 @@ __global__ __launch_bounds__(256) void k_agg_waves(uint32_t nwaves, uint32_t M,
     else if (sg != s0) mixed = true;
   }
   if (slot == 0 && blockIdx.x == 0) cseg[c] = mixed ? 0xffffffffu : s0;
-  if (slot >= M * 8 || s0 == 0xffffffffu) return;
+  if (slot >= M * 8 || s0 == 0xffffffffu) return;  // M * 8 is a multiple of 4
+  const size_t row = (size_t)M * 8;
   if (!mixed) {
-    unsigned long long acc = 0;
-#pragma unroll 8
+    unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+#pragma unroll 16
     for (uint32_t w = w0; w < w1; w++)
-      if (wseg[w] != 0xffffffffu) acc += wpart[(size_t)w * M * 8 + slot];
-    cpart[(size_t)c * M * 8 + slot] = acc;
+      if (wseg[w] != 0xffffffffu) {
+        const uint4 v = *(const uint4*)(wpart + (size_t)w * row + slot);
+        a0 += v.x, a1 += v.y, a2 += v.z, a3 += v.w;
+      }
+    unsigned long long* o = cpart + (size_t)c * row + slot;
+    o[0] = a0, o[1] = a1, o[2] = a2, o[3] = a3;
     return;
   }
-  unsigned long long acc = 0;
-  uint32_t cur = 0xffffffffu;
-  for (uint32_t w = w0; w < w1; w++) {
-    const uint32_t sg = wseg[w];
-    if (sg == 0xffffffffu) continue;
-    if (sg != cur) {
-      if (cur != 0xffffffffu && acc) atomicAdd(&agg64[(size_t)cur * M * 8 + slot], acc);
-      cur = sg;
-      acc = 0;
+  for (uint32_t k = 0; k < 4; k++) {
+    unsigned long long acc = 0;
+    uint32_t cur = 0xffffffffu;
+    for (uint32_t w = w0; w < w1; w++) {
+      const uint32_t sg = wseg[w];
+      if (sg == 0xffffffffu) continue;
+      if (sg != cur) {
+        if (cur != 0xffffffffu && acc) atomicAdd(&agg64[(size_t)cur * row + slot + k], acc);
+        cur = sg;
+        acc = 0;
+      }
+      acc += wpart[(size_t)w * row + slot + k];
     }
-    acc += wpart[(size_t)w * M * 8 + slot];
+    if (cur != 0xffffffffu && acc) atomicAdd(&agg64[(size_t)cur * row + slot + k], acc);
   }
-  if (cur != 0xffffffffu && acc) atomicAdd(&agg64[(size_t)cur * M * 8 + slot], acc);
 }
 
 // Counts the reports the aggregate must contain (status FINISHED and accepted by the host
@@ -2039,7 +2048,7 @@ __global__ void k_combine(uint32_t k, uint32_t len, uint32_t n_segments, const u
 // client-timestamp interval (Interval::from_time + merge, core/src/time.rs:294-317; merged for
 // failed reports too, aggregation_job_writer.rs:643-647).
 // One report per lane: one SHA-256 compression of the padded 16-byte ID, then a block-level
-// XOR / min / max reduction when the block's 256 reports share a segment (the common case:
+// XOR / min / max reduction when a tile's 1024 reports share a segment (the common case:
 // contiguous batches) and per-report atomics on the segment otherwise.
 // ------------------------------------------------------------------------------------
 // SHA-256 of the 16 bytes id[0..3] (little-endian words as loaded); the digest is returned as
@@ -2072,75 +2081,99 @@ __global__ void k_meta_init(uint32_t n_segments, uint32_t* ck, unsigned long lon
   }
 }
 
-__global__ __launch_bounds__(256) void k_meta(uint32_t n, const uint8_t* ids, const uint64_t* times,
-                                            const uint8_t* status, const uint8_t* mask,
-                                            const uint32_t* seg, uint32_t n_segments, uint32_t* ck,
-                                            unsigned long long* iv) {
+// Grid-stride over tiles of 1024 reports (16 waves): a tile whose reports share one segment is
+// reduced in the block and folded into the block's running (segment, XOR, min, max) registers,
+// which go out with one atomic per word when the segment changes and at the end -- so a 1 Mi
+// batch of one segment issues ~5 k atomics on the segment's 10 words instead of ~41 k from
+// 256-report blocks, whose serialisation on those addresses had set the kernel's time (112 us).
+constexpr uint32_t META_T = 1024, META_W = META_T / 64, META_BLOCKS = 512;
+__global__ __launch_bounds__(1024) void k_meta(uint32_t n, const uint8_t* ids, const uint64_t* times,
+                                             const uint8_t* status, const uint8_t* mask,
+                                             const uint32_t* seg, uint32_t n_segments, uint32_t* ck,
+                                             unsigned long long* iv) {
   __shared__ uint32_t s_seg0;
-  __shared__ uint32_t s_ck[4][8];
-  __shared__ unsigned long long s_lo[4], s_hi[4];
+  __shared__ uint32_t s_ck[META_W][8];
+  __shared__ unsigned long long s_lo[META_W], s_hi[META_W];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-  const uint32_t r = blockIdx.x * blockDim.x + tid;
-  const bool valid = r < n;
-  const uint32_t sg = valid ? (seg ? seg[r] : 0u) : 0xffffffffu;
-  const bool in_range = valid && sg < n_segments;
-  const bool inc = in_range && status[r] == PRIO3_STATUS_FINISHED && (!mask || mask[r]);
-  uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (ck && inc) {
-    uint32_t id[4];
-    load16(ids + 16 * (size_t)r, id);
-    sha256_id16(id, h);
-  }
-  unsigned long long lo = ~0ull, hi = 0;
-  if (times && in_range) {
-    lo = times[r];
-    hi = lo + 1;  // Interval::from_time: [t, t + 1)
-  }
-  if (tid == 0) s_seg0 = sg;  // thread 0 of a launched block is always a valid report
-  __syncthreads();
-  const bool uniform = __syncthreads_and(!valid || sg == s_seg0) && s_seg0 < n_segments;
-  if (uniform) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-#pragma unroll
-      for (int i = 0; i < 8; i++) h[i] ^= (uint32_t)__shfl_xor((int)h[i], off);
-      const unsigned long long l2 = __shfl_xor(lo, off), h2 = __shfl_xor(hi, off);
-      lo = l2 < lo ? l2 : lo;
-      hi = h2 > hi ? h2 : hi;
+  // the block's running partial (block-uniform `cur`; word tid on threads 0..7, the interval on
+  // thread 8)
+  uint32_t cur = 0xffffffffu, acc_x = 0;
+  unsigned long long acc_lo = ~0ull, acc_hi = 0;
+  auto flush = [&]() {
+    if (cur != 0xffffffffu) {
+      if (ck && tid < 8 && acc_x) atomicXor(ck + 8 * cur + tid, acc_x);
+      if (iv && tid == 8 && acc_hi) {
+        atomicMin(iv + 2 * cur, acc_lo);
+        atomicMax(iv + 2 * cur + 1, acc_hi);
+      }
     }
-    if (lane == 0) {
-#pragma unroll
-      for (int i = 0; i < 8; i++) s_ck[wv][i] = h[i];
-      s_lo[wv] = lo;
-      s_hi[wv] = hi;
+    acc_x = 0;
+    acc_lo = ~0ull;
+    acc_hi = 0;
+  };
+  for (uint32_t base = blockIdx.x * META_T; base < n; base += gridDim.x * META_T) {
+    const uint32_t r = base + tid;
+    const bool valid = r < n;
+    const uint32_t sg = valid ? (seg ? seg[r] : 0u) : 0xffffffffu;
+    const bool in_range = valid && sg < n_segments;
+    const bool inc = in_range && status[r] == PRIO3_STATUS_FINISHED && (!mask || mask[r]);
+    uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (ck && inc) {
+      uint32_t id[4];
+      load16(ids + 16 * (size_t)r, id);
+      sha256_id16(id, h);
     }
+    unsigned long long lo = ~0ull, hi = 0;
+    if (times && in_range) {
+      lo = times[r];
+      hi = lo + 1;  // Interval::from_time: [t, t + 1)
+    }
+    if (tid == 0) s_seg0 = sg;  // thread 0 of a tile is always a valid report
     __syncthreads();
-    const uint32_t nw = (blockDim.x + 63) / 64;
-    if (ck && tid < 8) {
-      uint32_t x = 0;
-      for (uint32_t q = 0; q < nw; q++) x ^= s_ck[q][tid];
-      if (x) atomicXor(ck + 8 * s_seg0 + tid, x);
-    }
-    if (iv && tid == 8) {
-      unsigned long long l = ~0ull, u = 0;
-      for (uint32_t q = 0; q < nw; q++) {
-        l = s_lo[q] < l ? s_lo[q] : l;
-        u = s_hi[q] > u ? s_hi[q] : u;
-      }
-      if (u) {
-        atomicMin(iv + 2 * s_seg0, l);
-        atomicMax(iv + 2 * s_seg0 + 1, u);
-      }
-    }
-  } else {
-    if (ck && inc)
+    const bool uniform = __syncthreads_and(!valid || sg == s_seg0) && s_seg0 < n_segments;
+    if (uniform) {
 #pragma unroll
-      for (int i = 0; i < 8; i++) atomicXor(ck + 8 * sg + i, h[i]);
-    if (iv && times && in_range) {
-      atomicMin(iv + 2 * sg, lo);
-      atomicMax(iv + 2 * sg + 1, hi);
+      for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) h[i] ^= (uint32_t)__shfl_xor((int)h[i], off);
+        const unsigned long long l2 = __shfl_xor(lo, off), h2 = __shfl_xor(hi, off);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+      }
+      if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) s_ck[wv][i] = h[i];
+        s_lo[wv] = lo;
+        s_hi[wv] = hi;
+      }
+      __syncthreads();
+      if (s_seg0 != cur) {  // block-uniform
+        flush();
+        cur = s_seg0;
+      }
+      if (tid < 8) {
+        uint32_t x = 0;
+        for (uint32_t q = 0; q < META_W; q++) x ^= s_ck[q][tid];
+        acc_x ^= x;
+      }
+      if (tid == 8) {
+        for (uint32_t q = 0; q < META_W; q++) {
+          acc_lo = s_lo[q] < acc_lo ? s_lo[q] : acc_lo;
+          acc_hi = s_hi[q] > acc_hi ? s_hi[q] : acc_hi;
+        }
+      }
+    } else {
+      if (ck && inc)
+#pragma unroll
+        for (int i = 0; i < 8; i++) atomicXor(ck + 8 * sg + i, h[i]);
+      if (iv && times && in_range) {
+        atomicMin(iv + 2 * sg, lo);
+        atomicMax(iv + 2 * sg + 1, hi);
+      }
     }
+    __syncthreads();  // s_seg0 / s_ck of this tile are read before the next tile writes them
   }
+  flush();
 }
 
 // multi-GPU combine of k per-rank metadata: checksums XOR, intervals Interval::merge
@@ -3621,7 +3654,7 @@ int prio3_device_aggregate_finish(prio3_engine* e, const uint8_t* d_status,
   HIPCHK(hipMemsetAsync(R->fix, 0, sizeof(uint32_t), st));
   HIPCHK(hipMemsetAsync(d_counts, 0, 8 * (size_t)S, st));
   const uint32_t nchunks = (nwaves + WCH - 1) / WCH;
-  dim3 g1((M * 8 + 255) / 256, nchunks);
+  dim3 g1((M * 8 / 4 + 255) / 256, nchunks);  // 4 slots per thread (k_agg_waves)
   TIMED(e, st, "k_agg_waves",
         (k_agg_waves<<<g1, 256, 0, st>>>(nwaves, M, R->wpart, R->wseg, R->cpart, R->cseg,
                                          R->agg64)));
@@ -3695,7 +3728,8 @@ int prio3_device_batch_metadata(prio3_engine* e, uint32_t n, const uint8_t* d_re
   TIMED(e, st, "k_meta_init", (k_meta_init<<<sb, 256, 0, st>>>(n_segments, ck, iv)));
   if (n)
     TIMED(e, st, "k_meta",
-          (k_meta<<<(n + 255) / 256, 256, 0, st>>>(n, d_report_ids, d_times, d_status,
+          (k_meta<<<std::min((n + META_T - 1) / META_T, META_BLOCKS), META_T, 0, st>>>(
+              n, d_report_ids, d_times, d_status,
                                                    d_accept_mask, d_segment_ids, n_segments, ck,
                                                    d_times ? iv : nullptr)));
   if (iv) TIMED(e, st, "k_meta_final", (k_meta_final<<<sb, 256, 0, st>>>(n_segments, iv)));
