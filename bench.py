@@ -164,6 +164,8 @@ def main():
                          "(1M/8 per GPU), C4 Prio3Sum 32 (10M/8 per GPU)")
     ap.add_argument("--hpke-aead", type=int, choices=[1, 2, 3], default=1,
                     help="--role hpke: AEAD id (1 AES-128-GCM, 2 AES-256-GCM, 3 ChaCha20Poly1305)")
+    ap.add_argument("--hpke-kem", choices=["x25519", "p256"], default="x25519",
+                    help="--role hpke: DHKEM(X25519, HKDF-SHA256) or DHKEM(P-256, HKDF-SHA256)")
     ap.add_argument("--leader-vdaf", choices=["hist", "sum32"], default="hist",
                     help="--role leader: Prio3Histogram(256,16) at 1Mi (default) or Prio3Sum(32) "
                          "at C4's 1.25M per GPU")
@@ -621,7 +623,10 @@ def hpke_main(args):
     t0 = time.perf_counter()
     aead = args.hpke_aead
     aead_name = {1: "AES-128-GCM", 2: "AES-256-GCM", 3: "ChaCha20Poly1305"}[aead]
-    d = H.make_batch_fast(uniq, 48, 32, seed=0x4A414E55, n_threads=cpu_threads(), aead=aead)
+    kem = H.KEM_P256 if args.hpke_kem == "p256" else H.KEM_X25519
+    kem_name = "P256" if kem == H.KEM_P256 else "X25519"
+    d = H.make_batch_fast(uniq, 48, 32, seed=0x4A414E55, n_threads=cpu_threads(), aead=aead,
+                          kem=kem)
     gen_s = time.perf_counter() - t0
     reps = -(-n // uniq)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(np.concatenate([a] * reps)[:n])).to(dev)
@@ -629,7 +634,7 @@ def hpke_main(args):
     ids, times, pubs = T(d["report_ids"]), T(d["times"].view(np.int64)), T(d["pubs"])
     shares = torch.empty((n, 48), dtype=torch.uint8, device=dev)
     status = torch.empty(n, dtype=torch.uint8, device=dev)
-    op = G.HpkeOpener(d["skR"], d["pkR"], device=0, aead_id=aead)
+    op = G.HpkeOpener(d["skR"], d["pkR"], device=0, aead_id=aead, kem_id=kem)
 
     def step():
         op.open_input_shares_device(d["task_id"], enc, ct, ct_len, ids, times, pubs, shares,
@@ -651,7 +656,7 @@ def hpke_main(args):
     counts = json.load(open(COUNTS_PATH)) if os.path.exists(COUNTS_PATH) else dict(kernels={})
     kc = counts["kernels"].get("k_hpke_open", {})
     roofline = None
-    if "valu_instr_per_item" in kc and aead == 1:  # counts were taken on the AES-128-GCM kernel
+    if "valu_instr_per_item" in kc and aead == 1 and kem == H.KEM_X25519:  # counts: that kernel
         ach = kc["valu_instr_per_item"] * n / (ms_avg / 1e3) / 1e12
         roofline = dict(bound="valu", achieved=ach, peak=PEAK_VALU_NOMINAL / 1e12,
                         unit="T lane-instr/s (32-bit VALU issue; peak = guide vector rate)",
@@ -660,13 +665,13 @@ def hpke_main(args):
                         kernel="k_hpke_open", ms_avg=ms_avg,
                         valu_instr_per_report=kc["valu_instr_per_item"])
     ok = int((status == 0).sum().item())
-    out = dict(metric="helper input shares HPKE-opened+decoded/sec (X25519-HKDF-SHA256, "
+    out = dict(metric=f"helper input shares HPKE-opened+decoded/sec ({kem_name}-HKDF-SHA256, "
                       f"{aead_name})", value=value, unit="reports/s", n_gpus=1, steps=args.steps,
                warmup=args.warmup, ms_per_step=elapsed / args.steps * 1e3, higher_is_better=True,
                scaling="weak", vs_baseline=None, dtype="u32 limbs (GF(2^255-19), GF(2^128), bytes)",
                data=f"synthetic: {uniq} distinct sealed input shares (oracle/OpenSSL, seeded) "
                     f"tiled x{reps}; generation {gen_s:.1f}s, not timed",
-               config=dict(workload="DAP helper input share open: X25519 decap + HPKE key "
+               config=dict(workload=f"DAP helper input share open: {kem_name} decap + HPKE key "
                                     f"schedule + {aead_name} + PlaintextInputShare decode, "
                                     "Prio3Histogram(256,16) shares", reports=n),
                roofline=roofline, kernel_ms_avg=ms_avg, checks=dict(opened=ok))
@@ -677,10 +682,10 @@ def hpke_main(args):
         csh, cst = H.open_input_shares(d["skR"], d["pkR"], d["task_id"], d["enc"][:m],
                                        d["ct"][:m], d["ct_len"][:m], d["report_ids"][:m],
                                        d["times"][:m], d["pubs"][:m], 48, n_threads=th,
-                                       aead=aead)
+                                       aead=aead, kem=kem)
         dt = time.perf_counter() - t0
         out["cpu_baseline"] = dict(value=m / dt, unit="reports/s", cores=th, kind="port",
-                                   sample=f"{m} of the sealed input shares, OpenSSL 3.0 X25519 / "
+                                   sample=f"{m} of the sealed input shares, OpenSSL 3.0 {kem_name} / "
                                           f"HMAC-SHA256 / {aead_name}, {th} threads, {dt:.1f}s")
         out["speedup_vs_cpu"] = value / (m / dt)
         out["checks"]["cpu_gpu_parity_on_sample"] = bool(

@@ -10,12 +10,14 @@
  * duplicate / taskprov extension checks and the helper input share decode -- writing the decoded
  * helper input shares straight into the layout prio3_device_prepare[_aggregate] reads.
  *
- * Suites: mode_base, DHKEM(X25519, HKDF-SHA256) (0x0020), HKDF-SHA256 (0x0001), with any of the
- * three AEADs of messages/src/lib.rs:844-853 (HpkeAeadId): AES-128-GCM (0x0001, the
- * configuration Janus generates by default, hpke.rs:260-300), AES-256-GCM (0x0002) and
- * ChaCha20Poly1305 (0x0003).  The other KEMs (P-256 0x0010, P-384, P-521, X448) and KDFs
- * (HKDF-SHA384 / -SHA512) return JANUS_HPKE_EUNSUPPORTED at creation; the host keeps its CPU
- * path for them.
+ * Suites: mode_base, DHKEM(X25519, HKDF-SHA256) (0x0020) or DHKEM(P-256, HKDF-SHA256) (0x0010),
+ * HKDF-SHA256 (0x0001), with any of the three AEADs of messages/src/lib.rs:844-853 (HpkeAeadId):
+ * AES-128-GCM (0x0001; X25519 + AES-128-GCM is the configuration Janus generates by default,
+ * hpke.rs:260-300), AES-256-GCM (0x0002) and ChaCha20Poly1305 (0x0003).  Key and enc sizes
+ * follow the KEM: X25519 private / public key 32 / 32 bytes and enc[n][32]; P-256 private key
+ * 32 bytes (big-endian scalar, 1 <= sk < n), public key and enc[n][65] (uncompressed SEC1
+ * points).  The other KEMs (P-384, P-521, X448) and KDFs (HKDF-SHA384 / -SHA512) return
+ * JANUS_HPKE_EUNSUPPORTED at creation; the host keeps its CPU path for them.
  *
  * Conventions as in janus_prio3.h: plain pointers and sizes, caller-owned buffers, device
  * pointers (d_*) stream-ordered on a hipStream_t (NULL = the null stream), per-report failures
@@ -32,6 +34,7 @@ extern "C" {
 
 enum {
   JANUS_HPKE_KEM_X25519_HKDF_SHA256 = 0x0020,
+  JANUS_HPKE_KEM_P256_HKDF_SHA256 = 0x0010,
   JANUS_HPKE_KDF_HKDF_SHA256 = 0x0001,
   JANUS_HPKE_AEAD_AES_128_GCM = 0x0001,
   JANUS_HPKE_AEAD_AES_256_GCM = 0x0002,
@@ -69,7 +72,7 @@ int janus_hpke_opener_create(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id,
 void janus_hpke_opener_destroy(janus_hpke_opener* opener);
 
 /* Helper input shares of one task.  Per report r:
- *   d_enc[r][32]                      HpkeCiphertext.encapsulated_key
+ *   d_enc[r][Nenc]                    HpkeCiphertext.encapsulated_key (Nenc = 32 X25519, 65 P-256)
  *   d_ct[r][ct_stride], d_ct_len[r]   HpkeCiphertext.payload (ciphertext || 16-byte tag)
  *   d_report_ids[r][16], d_times[r]   ReportMetadata (report ID, time in seconds)
  *   d_public_shares[r][public_share_len]

@@ -2,7 +2,8 @@
 //
 // One report per lane, the whole RFC 9180 base-mode open in one kernel:
 //   X25519 (RFC 7748 Montgomery ladder, GF(2^255-19) in 8 x 32-bit limbs: column-MAC products
-//   with v_mad_u64_u32 + carry-out words, like the Field128 MAC of prio3_device.h)
+//   with v_mad_u64_u32 + carry-out words, like the Field128 MAC of prio3_device.h) or P-256
+//   ECDH (p256_device.h: validated uncompressed point, NIST fast reduction, Jacobian ladder)
 //   -> DHKEM ExtractAndExpand and the key schedule (HMAC-SHA256, 19 compressions)
 //   -> AES-128-GCM / AES-256-GCM (T-tables in LDS, bitwise GHASH) or ChaCha20Poly1305
 //   (RFC 8439: ARX keystream, Poly1305 in 26-bit limbs) -> for DAP input shares the
@@ -15,12 +16,14 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/janus_hpke.h"
 #include "prio3_device.h"
 #include "sha256_device.h"
 #include "aes_device.h"
+#include "p256_device.h"
 #include "sha256_host.h"
 
 // -------------------------------------------------------------------------------------
@@ -583,6 +586,8 @@ struct HpkeParams {
   uint32_t task[8];      // task ID (input-share AAD), BE words
   uint32_t ipad0[8], opad0[8];  // HMAC midstates of the empty key
   uint32_t aead;                // AEAD id (1, 2, 3): selects the kernel instance
+  uint32_t kem;                 // KEM id (0x20 X25519, 0x10 P-256)
+  uint8_t pk65[68];             // P-256: pkRm, the 65-byte uncompressed point (kem_context)
 };
 
 struct OpenArgs {
@@ -609,62 +614,103 @@ DEV void load_words(const uint8_t* p, uint32_t* w, int n16) {
 
 // MODE 0: explicit AAD, plaintext out.  MODE 1: DAP helper input share with PUB bytes of
 // public share (InputShareAad built here), decoded helper share out.
-// AEAD: 1 AES-128-GCM, 2 AES-256-GCM, 3 ChaCha20Poly1305 (RFC 9180 7.3 ids)
-template <int MODE, int PUB, int AEAD>
+// AEAD (P.aead): 1 AES-128-GCM, 2 AES-256-GCM, 3 ChaCha20Poly1305 (RFC 9180 7.3 ids).
+// KEM: 0x20 DHKEM(X25519, HKDF-SHA256) (enc: 32 bytes), 0x10 DHKEM(P-256, HKDF-SHA256) (enc: the
+// 65-byte uncompressed point)
+// The AEAD is a kernel argument (P.aead, wave-uniform): one instance per (MODE, PUB, KEM) keeps
+// the X25519 / P-256 ladders to six copies.
+template <int MODE, int PUB, int KEM>
 __global__ __launch_bounds__(256) void k_hpke_open(HpkeParams P, OpenArgs a) {
-  static_assert(AEAD >= 1 && AEAD <= 3, "AEAD id");
-  constexpr uint32_t NK = AEAD == 1 ? 16 : 32;  // Nk: AEAD key bytes
+  static_assert(KEM == 0x20 || KEM == 0x10, "KEM id");
+  const uint32_t AEAD = P.aead;
+  const uint32_t NK = AEAD == 1 ? 16 : 32;  // Nk: AEAD key bytes
   __shared__ AesT T;
   aes_tables_init(T);
   __syncthreads();
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= a.n) return;
-  // ---- DHKEM(X25519, HKDF-SHA256) Decap (RFC 9180 4.1) -------------------------------
-  uint32_t encw[8];
-  load_words(a.enc + 32 * (size_t)r, encw, 2);
-  fe u;
-#pragma unroll
-  for (int i = 0; i < 8; i++) u.v[i] = encw[i];
-  u.v[7] &= 0x7fffffffu;  // decodeUCoordinate masks bit 255
-  const fe dh = x25519_ladder(P.sk, u);
-  uint32_t nz = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) nz |= dh.v[i];
-  bool ok = nz != 0;  // all-zero shared secret: DeserializeError / ValidationError
+  // ---- DHKEM Decap (RFC 9180 4.1): dh, then ExtractAndExpand(dh, enc || pkRm) -------------
   uint32_t prk[8], ss[8], secret[8], keyw[8], noncew[8];
-  {  // eae_prk = LabeledExtract("", "eae_prk", dh)
-    Msg32<16> m;
-    mz(m);
-    mstr(m, 0, "HPKE-v1");
-    mstr(m, 7, "KEM");
-    mbyte(m, 10, 0x00);
-    mbyte(m, 11, 0x20);
-    mstr(m, 12, "eae_prk");
-    mwords_le(m, 19, dh.v, 8);
-    HmacKey k0;
+  bool ok;
+  HmacKey k0;  // the empty-key HMAC midstates (eae_prk extraction)
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      k0.ist[i] = P.ipad0[i];
-      k0.ost[i] = P.opad0[i];
-    }
-    hmac(k0, m, 51, prk);
+  for (int i = 0; i < 8; i++) {
+    k0.ist[i] = P.ipad0[i];
+    k0.ost[i] = P.opad0[i];
   }
-  {  // shared_secret = LabeledExpand(eae_prk, "shared_secret", enc || pkRm, 32)
-    Msg32<32> m;
-    mz(m);
-    mbyte(m, 0, 0);
-    mbyte(m, 1, 32);
-    mstr(m, 2, "HPKE-v1");
-    mstr(m, 9, "KEM");
-    mbyte(m, 12, 0x00);
-    mbyte(m, 13, 0x20);
-    mstr(m, 14, "shared_secret");
-    mwords_le(m, 27, encw, 8);
-    mwords_le(m, 59, P.pk, 8);
-    mbyte(m, 91, 0x01);
-    HmacKey k;
-    hmac_key32(k, prk);
-    hmac(k, m, 92, ss);
+  if constexpr (KEM == 0x20) {
+    uint32_t encw[8];
+    load_words(a.enc + 32 * (size_t)r, encw, 2);
+    fe u;
+#pragma unroll
+    for (int i = 0; i < 8; i++) u.v[i] = encw[i];
+    u.v[7] &= 0x7fffffffu;  // decodeUCoordinate masks bit 255
+    const fe dh = x25519_ladder(P.sk, u);
+    uint32_t nz = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) nz |= dh.v[i];
+    ok = nz != 0;  // all-zero shared secret: DeserializeError / ValidationError
+    {  // eae_prk = LabeledExtract("", "eae_prk", dh)
+      Msg32<16> m;
+      mz(m);
+      mstr(m, 0, "HPKE-v1");
+      mstr(m, 7, "KEM");
+      mbyte(m, 10, 0x00);
+      mbyte(m, 11, 0x20);
+      mstr(m, 12, "eae_prk");
+      mwords_le(m, 19, dh.v, 8);
+      hmac(k0, m, 51, prk);
+    }
+    {  // shared_secret = LabeledExpand(eae_prk, "shared_secret", enc || pkRm, 32)
+      Msg32<32> m;
+      mz(m);
+      mbyte(m, 0, 0);
+      mbyte(m, 1, 32);
+      mstr(m, 2, "HPKE-v1");
+      mstr(m, 9, "KEM");
+      mbyte(m, 12, 0x00);
+      mbyte(m, 13, 0x20);
+      mstr(m, 14, "shared_secret");
+      mwords_le(m, 27, encw, 8);
+      mwords_le(m, 59, P.pk, 8);
+      mbyte(m, 91, 0x01);
+      HmacKey k;
+      hmac_key32(k, prk);
+      hmac(k, m, 92, ss);
+    }
+  } else {
+    const uint8_t* ep = a.enc + 65 * (size_t)r;
+    uint32_t dh[8];  // x-coordinate, big-endian words
+    ok = p256::ecdh(P.sk, ep, dh);
+    {  // eae_prk = LabeledExtract("", "eae_prk", dh)
+      Msg32<16> m;
+      mz(m);
+      mstr(m, 0, "HPKE-v1");
+      mstr(m, 7, "KEM");
+      mbyte(m, 10, 0x00);
+      mbyte(m, 11, 0x10);
+      mstr(m, 12, "eae_prk");
+      mwords_be(m, 19, dh, 8);
+      hmac(k0, m, 51, prk);
+    }
+    {  // shared_secret = LabeledExpand(eae_prk, "shared_secret", enc || pkRm (130 B), 32)
+      Msg32<48> m;
+      mz(m);
+      mbyte(m, 0, 0);
+      mbyte(m, 1, 32);
+      mstr(m, 2, "HPKE-v1");
+      mstr(m, 9, "KEM");
+      mbyte(m, 12, 0x00);
+      mbyte(m, 13, 0x10);
+      mstr(m, 14, "shared_secret");
+      for (int i = 0; i < 65; i++) mbyte(m, 27 + i, ep[i]);
+#pragma unroll
+      for (int i = 0; i < 65; i++) mbyte(m, 92 + i, P.pk65[i]);
+      mbyte(m, 157, 0x01);
+      HmacKey k;
+      hmac_key32(k, prk);
+      hmac(k, m, 158, ss);
+    }
   }
   {  // secret = LabeledExtract(shared_secret, "secret", "")
     Msg32<16> m;
@@ -672,7 +718,7 @@ __global__ __launch_bounds__(256) void k_hpke_open(HpkeParams P, OpenArgs a) {
     mstr(m, 0, "HPKE-v1");
     mstr(m, 7, "HPKE");
     mbyte(m, 11, 0x00);
-    mbyte(m, 12, 0x20);
+    mbyte(m, 12, KEM);
     mbyte(m, 13, 0x00);
     mbyte(m, 14, 0x01);
     mbyte(m, 15, 0x00);
@@ -692,7 +738,7 @@ __global__ __launch_bounds__(256) void k_hpke_open(HpkeParams P, OpenArgs a) {
     mstr(m, 2, "HPKE-v1");
     mstr(m, 9, "HPKE");
     mbyte(m, 13, 0x00);
-    mbyte(m, 14, 0x20);
+    mbyte(m, 14, KEM);
     mbyte(m, 15, 0x00);
     mbyte(m, 16, 0x01);
     mbyte(m, 17, 0x00);
@@ -708,7 +754,7 @@ __global__ __launch_bounds__(256) void k_hpke_open(HpkeParams P, OpenArgs a) {
     mstr(n2, 2, "HPKE-v1");
     mstr(n2, 9, "HPKE");
     mbyte(n2, 13, 0x00);
-    mbyte(n2, 14, 0x20);
+    mbyte(n2, 14, KEM);
     mbyte(n2, 15, 0x00);
     mbyte(n2, 16, 0x01);
     mbyte(n2, 17, 0x00);
@@ -720,112 +766,13 @@ __global__ __launch_bounds__(256) void k_hpke_open(HpkeParams P, OpenArgs a) {
   }
   uint32_t aad_len, pt_len;
   uint8_t* pp;
-  if constexpr (AEAD == 3) {
-  // ---- ChaCha20Poly1305 open (AEAD 3, RFC 8439 2.8), sequence number 0 -------------------
-  uint32_t ckey[8], cnon[3];
-#pragma unroll
-  for (int i = 0; i < 8; i++) ckey[i] = __builtin_bswap32(keyw[i]);  // key bytes as LE words
-#pragma unroll
-  for (int i = 0; i < 3; i++) cnon[i] = __builtin_bswap32(noncew[i]);
-  Poly1305 mac;
-  {
-    uint32_t b0[16];
-    chacha20_block(ckey, 0, cnon, b0);  // Poly1305 one-time key = first 32 bytes of block 0
-    poly_init(mac, b0);
-  }
-  if constexpr (MODE == 1) {
-    // InputShareAad (as the GCM path builds it), zero padded to 16 bytes, as LE words
-    constexpr int AW = (60 + PUB + 3) / 4;
-    uint32_t aw[((AW + 3) / 4) * 4];
-#pragma unroll
-    for (int i = 0; i < ((AW + 3) / 4) * 4; i++) aw[i] = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) aw[i] = __builtin_bswap32(P.task[i]);
-    uint32_t idw[4];
-    load16(a.ids + 16 * (size_t)r, idw);
-#pragma unroll
-    for (int i = 0; i < 4; i++) aw[8 + i] = idw[i];
-    const uint64_t tm = a.times[r];
-    aw[12] = __builtin_bswap32((uint32_t)(tm >> 32));
-    aw[13] = __builtin_bswap32((uint32_t)tm);
-    aw[14] = __builtin_bswap32((uint32_t)PUB);
-    if constexpr (PUB > 0) {
-      uint32_t pw[PUB / 4];
-#pragma unroll
-      for (int i = 0; i < PUB / 16; i++) load16(a.pubs + (size_t)PUB * r + 16 * i, pw + 4 * i);
-#pragma unroll
-      for (int i = 0; i < PUB / 4; i++) aw[15 + i] = pw[i];
-    }
-    aad_len = 60 + PUB;
-#pragma unroll
-    for (int b = 0; b < (AW + 3) / 4; b++) poly_block(mac, aw + 4 * b);
-  } else {
-    aad_len = a.aad_len[r];
-    const uint8_t* ap = a.aad + (size_t)a.aad_stride * r;
-    for (uint32_t off = 0; off < aad_len; off += 16) {
-      uint32_t xw[4];
-      load16(ap + off, xw);
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const uint32_t lo = off + 4 * i;  // bytes past the end are zero
-        const uint32_t keep = lo + 4 <= aad_len ? 0xffffffffu
-                              : lo >= aad_len  ? 0u
-                                               : (1u << (8 * (aad_len - lo))) - 1u;
-        xw[i] &= keep;
-      }
-      poly_block(mac, xw);
-    }
-  }
-  const uint32_t ct_len = a.ct_len[r];
-  const bool len_ok = ct_len >= 16 && ct_len <= a.ct_stride;
-  ok = ok && len_ok;
-  pt_len = len_ok ? ct_len - 16 : 0;
-  const uint8_t* cp = a.ct + (size_t)a.ct_stride * r;
-  pp = a.pt + (size_t)a.ct_stride * r;
-  for (uint32_t off0 = 0, blk = 1; off0 < pt_len; off0 += 64, blk++) {
-    uint32_t ks[16];
-    chacha20_block(ckey, blk, cnon, ks);
-#pragma unroll
-    for (int c4 = 0; c4 < 4; c4++) {
-      const uint32_t off = off0 + 16 * c4;
-      if (off >= pt_len) break;
-      uint32_t cw[4], xw[4], pw[4];
-      load16(cp + off, cw);
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const uint32_t lo = off + 4 * i;
-        const uint32_t keep = lo + 4 <= pt_len ? 0xffffffffu
-                              : lo >= pt_len  ? 0u
-                                              : (1u << (8 * (pt_len - lo))) - 1u;
-        xw[i] = cw[i] & keep;
-        pw[i] = (cw[i] ^ ks[4 * c4 + i]) & keep;
-      }
-      poly_block(mac, xw);
-      *(uint4*)(pp + off) = make_uint4(pw[0], pw[1], pw[2], pw[3]);
-    }
-  }
-  {  // le64(aad_len) || le64(ct_len), tag
-    const uint32_t lw[4] = {aad_len, 0, pt_len, 0};
-    poly_block(mac, lw);
-    uint32_t tag[4];
-    poly_finish(mac, tag);
-    uint32_t diff = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      uint32_t got = 0;
-#pragma unroll
-      for (int j = 0; j < 4; j++) got |= (uint32_t)cp[pt_len + 4 * i + j] << (8 * j);
-      diff |= tag[i] ^ got;
-    }
-    ok = ok && diff == 0;
-  }
-  } else {
+  auto gcm_open = [&](auto nr_tag) {  // NR = 10 (AES-128-GCM) or 14 (AES-256-GCM)
+    constexpr int NR = decltype(nr_tag)::value;
   // ---- AES-GCM open (AEAD 1, 2), sequence number 0 (nonce = base_nonce) --------------
-  constexpr int NR = AEAD == 1 ? 10 : 14;
   uint32_t kcol[8], rk[4 * (NR + 1)];
 #pragma unroll
   for (int i = 0; i < 8; i++) kcol[i] = __builtin_bswap32(keyw[i]);
-  if constexpr (AEAD == 1)
+  if constexpr (NR == 10)
     aes128_expand(T, kcol, rk);
   else
     aes256_expand(T, kcol, rk);
@@ -925,6 +872,110 @@ __global__ __launch_bounds__(256) void k_hpke_open(HpkeParams P, OpenArgs a) {
     }
     ok = ok && diff == 0;
   }
+  };
+  if (AEAD == 3) {
+  // ---- ChaCha20Poly1305 open (AEAD 3, RFC 8439 2.8), sequence number 0 -------------------
+  uint32_t ckey[8], cnon[3];
+#pragma unroll
+  for (int i = 0; i < 8; i++) ckey[i] = __builtin_bswap32(keyw[i]);  // key bytes as LE words
+#pragma unroll
+  for (int i = 0; i < 3; i++) cnon[i] = __builtin_bswap32(noncew[i]);
+  Poly1305 mac;
+  {
+    uint32_t b0[16];
+    chacha20_block(ckey, 0, cnon, b0);  // Poly1305 one-time key = first 32 bytes of block 0
+    poly_init(mac, b0);
+  }
+  if constexpr (MODE == 1) {
+    // InputShareAad (as the GCM path builds it), zero padded to 16 bytes, as LE words
+    constexpr int AW = (60 + PUB + 3) / 4;
+    uint32_t aw[((AW + 3) / 4) * 4];
+#pragma unroll
+    for (int i = 0; i < ((AW + 3) / 4) * 4; i++) aw[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) aw[i] = __builtin_bswap32(P.task[i]);
+    uint32_t idw[4];
+    load16(a.ids + 16 * (size_t)r, idw);
+#pragma unroll
+    for (int i = 0; i < 4; i++) aw[8 + i] = idw[i];
+    const uint64_t tm = a.times[r];
+    aw[12] = __builtin_bswap32((uint32_t)(tm >> 32));
+    aw[13] = __builtin_bswap32((uint32_t)tm);
+    aw[14] = __builtin_bswap32((uint32_t)PUB);
+    if constexpr (PUB > 0) {
+      uint32_t pw[PUB / 4];
+#pragma unroll
+      for (int i = 0; i < PUB / 16; i++) load16(a.pubs + (size_t)PUB * r + 16 * i, pw + 4 * i);
+#pragma unroll
+      for (int i = 0; i < PUB / 4; i++) aw[15 + i] = pw[i];
+    }
+    aad_len = 60 + PUB;
+#pragma unroll
+    for (int b = 0; b < (AW + 3) / 4; b++) poly_block(mac, aw + 4 * b);
+  } else {
+    aad_len = a.aad_len[r];
+    const uint8_t* ap = a.aad + (size_t)a.aad_stride * r;
+    for (uint32_t off = 0; off < aad_len; off += 16) {
+      uint32_t xw[4];
+      load16(ap + off, xw);
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t lo = off + 4 * i;  // bytes past the end are zero
+        const uint32_t keep = lo + 4 <= aad_len ? 0xffffffffu
+                              : lo >= aad_len  ? 0u
+                                               : (1u << (8 * (aad_len - lo))) - 1u;
+        xw[i] &= keep;
+      }
+      poly_block(mac, xw);
+    }
+  }
+  const uint32_t ct_len = a.ct_len[r];
+  const bool len_ok = ct_len >= 16 && ct_len <= a.ct_stride;
+  ok = ok && len_ok;
+  pt_len = len_ok ? ct_len - 16 : 0;
+  const uint8_t* cp = a.ct + (size_t)a.ct_stride * r;
+  pp = a.pt + (size_t)a.ct_stride * r;
+  for (uint32_t off0 = 0, blk = 1; off0 < pt_len; off0 += 64, blk++) {
+    uint32_t ks[16];
+    chacha20_block(ckey, blk, cnon, ks);
+#pragma unroll
+    for (int c4 = 0; c4 < 4; c4++) {
+      const uint32_t off = off0 + 16 * c4;
+      if (off >= pt_len) break;
+      uint32_t cw[4], xw[4], pw[4];
+      load16(cp + off, cw);
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t lo = off + 4 * i;
+        const uint32_t keep = lo + 4 <= pt_len ? 0xffffffffu
+                              : lo >= pt_len  ? 0u
+                                              : (1u << (8 * (pt_len - lo))) - 1u;
+        xw[i] = cw[i] & keep;
+        pw[i] = (cw[i] ^ ks[4 * c4 + i]) & keep;
+      }
+      poly_block(mac, xw);
+      *(uint4*)(pp + off) = make_uint4(pw[0], pw[1], pw[2], pw[3]);
+    }
+  }
+  {  // le64(aad_len) || le64(ct_len), tag
+    const uint32_t lw[4] = {aad_len, 0, pt_len, 0};
+    poly_block(mac, lw);
+    uint32_t tag[4];
+    poly_finish(mac, tag);
+    uint32_t diff = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      uint32_t got = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) got |= (uint32_t)cp[pt_len + 4 * i + j] << (8 * j);
+      diff |= tag[i] ^ got;
+    }
+    ok = ok && diff == 0;
+  }
+  } else if (AEAD == 2) {
+    gcm_open(std::integral_constant<int, 14>{});
+  } else {
+    gcm_open(std::integral_constant<int, 10>{});
   }
   if constexpr (MODE == 0) {
     a.status[r] = ok ? JANUS_HPKE_OK : JANUS_HPKE_DECRYPT_ERROR;
@@ -1017,9 +1068,14 @@ std::vector<uint8_t> cat(std::initializer_list<std::vector<uint8_t>> parts) {
 std::vector<uint8_t> bytes(const char* s) { return std::vector<uint8_t>(s, s + strlen(s)); }
 
 // suite_id = "HPKE" || kem_id || kdf_id || aead_id (RFC 9180 5.1)
-std::vector<uint8_t> hpke_suite(uint16_t aead) {
-  return {'H', 'P', 'K', 'E', 0x00, 0x20, 0x00, 0x01, (uint8_t)(aead >> 8), (uint8_t)aead};
+std::vector<uint8_t> hpke_suite(uint16_t kem, uint16_t aead) {
+  return {'H',         'P',           'K',  'E', (uint8_t)(kem >> 8), (uint8_t)kem, 0x00, 0x01,
+          (uint8_t)(aead >> 8), (uint8_t)aead};
 }
+// P-256 group order n (SEC 2), big-endian
+const uint8_t kP256N[32] = {0xff, 0xff, 0xff, 0xff, 0x00, 0x00, 0x00, 0x00, 0xff, 0xff, 0xff,
+                            0xff, 0xff, 0xff, 0xff, 0xff, 0xbc, 0xe6, 0xfa, 0xad, 0xa7, 0x17,
+                            0x9e, 0x84, 0xf3, 0xb9, 0xca, 0xc2, 0xfc, 0x63, 0x25, 0x51};
 
 uint32_t be32(const uint8_t* p) {
   return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3];
@@ -1062,25 +1118,41 @@ int janus_hpke_opener_create(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id,
                              janus_hpke_opener** out) {
   if (!out || !private_key || !public_key || (info_len && !info)) return JANUS_HPKE_EINVAL;
   *out = nullptr;
-  if (kem_id != JANUS_HPKE_KEM_X25519_HKDF_SHA256 || kdf_id != JANUS_HPKE_KDF_HKDF_SHA256 ||
+  const bool x25519 = kem_id == JANUS_HPKE_KEM_X25519_HKDF_SHA256,
+             p256 = kem_id == JANUS_HPKE_KEM_P256_HKDF_SHA256;
+  if ((!x25519 && !p256) || kdf_id != JANUS_HPKE_KDF_HKDF_SHA256 ||
       (aead_id != JANUS_HPKE_AEAD_AES_128_GCM && aead_id != JANUS_HPKE_AEAD_AES_256_GCM &&
        aead_id != JANUS_HPKE_AEAD_CHACHA20_POLY1305))
     return JANUS_HPKE_EUNSUPPORTED;
-  if (private_key_len != 32 || public_key_len != 32) return JANUS_HPKE_EINVAL;
+  if (private_key_len != 32 || public_key_len != (x25519 ? 32u : 65u)) return JANUS_HPKE_EINVAL;
+  if (p256) {  // DeserializePrivateKey: 1 <= sk < n; pkRm an uncompressed point
+    bool zero = true, below = false, decided = false;
+    for (int i = 0; i < 32; i++) {
+      zero = zero && private_key[i] == 0;
+      if (!decided && private_key[i] != kP256N[i]) below = private_key[i] < kP256N[i], decided = true;
+    }
+    if (zero || !below || public_key[0] != 0x04) return JANUS_HPKE_EINVAL;
+  }
   auto* o = new janus_hpke_opener();
   o->device = device;
   memset(&o->P, 0, sizeof(o->P));
-  uint8_t k[32];
-  memcpy(k, private_key, 32);
-  k[0] &= 248;  // decodeScalar25519 (RFC 7748 section 5)
-  k[31] &= 127;
-  k[31] |= 64;
-  for (int i = 0; i < 8; i++) o->P.sk[i] = le32(k + 4 * i), o->P.pk[i] = le32(public_key + 4 * i);
+  o->P.kem = kem_id;
+  if (x25519) {
+    uint8_t k[32];
+    memcpy(k, private_key, 32);
+    k[0] &= 248;  // decodeScalar25519 (RFC 7748 section 5)
+    k[31] &= 127;
+    k[31] |= 64;
+    for (int i = 0; i < 8; i++) o->P.sk[i] = le32(k + 4 * i), o->P.pk[i] = le32(public_key + 4 * i);
+  } else {
+    for (int i = 0; i < 8; i++) o->P.sk[i] = be32(private_key + 4 * (7 - i));  // LE limbs
+    memcpy(o->P.pk65, public_key, 65);
+  }
   // key_schedule_context = mode_base || LabeledExtract("", "psk_id_hash", "") ||
   //                        LabeledExtract("", "info_hash", info)        (RFC 9180 5.1)
   uint8_t ksc[68] = {0};
   std::vector<uint8_t> inf(info, info + info_len);
-  const std::vector<uint8_t> suite = hpke_suite(aead_id);
+  const std::vector<uint8_t> suite = hpke_suite(kem_id, aead_id);
   hmac_host(nullptr, 0, cat({bytes("HPKE-v1"), suite, bytes("psk_id_hash")}), ksc + 1);
   hmac_host(nullptr, 0, cat({bytes("HPKE-v1"), suite, bytes("info_hash"), inf}), ksc + 33);
   o->P.aead = aead_id;
@@ -1155,19 +1227,17 @@ static int launch_open(janus_hpke_opener* o, int mode, int pub, const OpenArgs& 
     HCHK(hipEventRecord(e0, st));
   }
   const uint32_t blocks = (a.n + 255) / 256;
-#define JANUS_HPKE_LAUNCH(AE)                                    \
+#define JANUS_HPKE_LAUNCH(KE)                                    \
   if (mode == 0)                                                 \
-    k_hpke_open<0, 0, AE><<<blocks, 256, 0, st>>>(o->P, a);      \
+    k_hpke_open<0, 0, KE><<<blocks, 256, 0, st>>>(o->P, a);      \
   else if (pub == 32)                                            \
-    k_hpke_open<1, 32, AE><<<blocks, 256, 0, st>>>(o->P, a);     \
+    k_hpke_open<1, 32, KE><<<blocks, 256, 0, st>>>(o->P, a);     \
   else                                                           \
-    k_hpke_open<1, 0, AE><<<blocks, 256, 0, st>>>(o->P, a);
-  if (o->P.aead == JANUS_HPKE_AEAD_AES_256_GCM) {
-    JANUS_HPKE_LAUNCH(2)
-  } else if (o->P.aead == JANUS_HPKE_AEAD_CHACHA20_POLY1305) {
-    JANUS_HPKE_LAUNCH(3)
+    k_hpke_open<1, 0, KE><<<blocks, 256, 0, st>>>(o->P, a);
+  if (o->P.kem == JANUS_HPKE_KEM_P256_HKDF_SHA256) {
+    JANUS_HPKE_LAUNCH(0x10)
   } else {
-    JANUS_HPKE_LAUNCH(1)
+    JANUS_HPKE_LAUNCH(0x20)
   }
 #undef JANUS_HPKE_LAUNCH
   HCHK(hipGetLastError());
@@ -1280,7 +1350,8 @@ int janus_hpke_open_input_shares(janus_hpke_opener* o, uint32_t n, const uint8_t
   HCHK(hipSetDevice(o->device));
   DevBuf de, dc, dl, di, dt, dp, ds, dst;
   int rc;
-  if ((rc = up(de, enc, 32 * (size_t)n, o->stream)) || (rc = up(dc, ct, (size_t)ct_stride * n, o->stream)) ||
+  const size_t nenc = o->P.kem == JANUS_HPKE_KEM_P256_HKDF_SHA256 ? 65 : 32;
+  if ((rc = up(de, enc, nenc * n, o->stream)) || (rc = up(dc, ct, (size_t)ct_stride * n, o->stream)) ||
       (rc = up(dl, ct_len, 4 * (size_t)n, o->stream)) ||
       (rc = up(di, report_ids, 16 * (size_t)n, o->stream)) ||
       (rc = up(dt, times, 8 * (size_t)n, o->stream)) ||
@@ -1308,7 +1379,8 @@ int janus_hpke_open(janus_hpke_opener* o, uint32_t n, const uint8_t* enc, const 
   HCHK(hipSetDevice(o->device));
   DevBuf de, dc, dl, da, dal, dpt, dst;
   int rc;
-  if ((rc = up(de, enc, 32 * (size_t)n, o->stream)) || (rc = up(dc, ct, (size_t)ct_stride * n, o->stream)) ||
+  const size_t nenc = o->P.kem == JANUS_HPKE_KEM_P256_HKDF_SHA256 ? 65 : 32;
+  if ((rc = up(de, enc, nenc * n, o->stream)) || (rc = up(dc, ct, (size_t)ct_stride * n, o->stream)) ||
       (rc = up(dl, ct_len, 4 * (size_t)n, o->stream)) ||
       (rc = up(da, aad, (size_t)aad_stride * n, o->stream)) ||
       (rc = up(dal, aad_len, aad_stride ? 4 * (size_t)n : 0, o->stream)))

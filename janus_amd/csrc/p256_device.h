@@ -1,0 +1,221 @@
+// p256_device.h -- NIST P-256 (FIPS 186-4 D.1.2.3, SEC 2) ECDH for DHKEM(P-256, HKDF-SHA256)
+// (RFC 9180 7.1), one report per work-item on MI355X (gfx950).  Used by the HPKE opener
+// (hpke.hip, KEM 0x0010).
+//
+// GF(p), p = 2^256 - 2^224 + 2^192 + 2^96 - 1: 8 little-endian 32-bit limbs, values loosely
+// reduced in [0, 2^256).  A product is the 16-word schoolbook (v_mad_u64_u32) folded by the
+// NIST fast reduction (FIPS 186-4 D.2.3: s1 + 2 s2 + 2 s3 + s4 + s5 - s6 - s7 - s8 - s9) in
+// signed 64-bit word sums, whose carry out of 2^256 folds back as 2^256 = 2^224 - 2^192 - 2^96 + 1
+// (mod p); three carry passes always leave [0, 2^256).
+// The scalar is the server's private key, the same in every lane: a left-to-right ladder over
+// its (wave-uniform) bits that doubles and adds (mixed Jacobian, a = -3) every step and keeps
+// the sum only where the bit is set, so every key runs the same instruction stream.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifndef DEV
+#define DEV __device__ __forceinline__
+#endif
+
+namespace p256 {
+
+struct fp {
+  uint32_t v[8];
+};
+
+// carry-propagate signed word sums t[0..7] (each |t| < 2^40) into [0, 2^256), folding the
+// carry out of 2^256 twice (the second carry is in {-1, 0, 1}, the third always 0)
+DEV fp fold(int64_t t[8]) {
+#pragma unroll
+  for (int pass = 0; pass < 3; pass++) {
+    int64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      t[i] += c;
+      c = t[i] >> 32;  // arithmetic shift: floor division
+      t[i] &= 0xffffffffll;
+    }
+    if (pass < 2) {
+      t[0] += c;
+      t[3] -= c;
+      t[6] -= c;
+      t[7] += c;
+    }
+  }
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = (uint32_t)t[i];
+  return r;
+}
+
+DEV fp add(const fp& a, const fp& b) {
+  int64_t t[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = (int64_t)a.v[i] + b.v[i];
+  return fold(t);
+}
+DEV fp sub(const fp& a, const fp& b) {
+  int64_t t[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = (int64_t)a.v[i] - b.v[i];
+  return fold(t);
+}
+DEV fp mul_small(const fp& a, uint32_t k) {  // k <= 8
+  int64_t t[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = (int64_t)a.v[i] * k;
+  return fold(t);
+}
+
+// out of line: ~20 call sites in the point formulas (compile time, code size)
+__device__ __noinline__ fp mul(const fp& a, const fp& b) {
+  uint32_t c[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) c[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint64_t x = (uint64_t)a.v[i] * b.v[j] + c[i + j] + carry;
+      c[i + j] = (uint32_t)x;
+      carry = x >> 32;
+    }
+    c[i + 8] = (uint32_t)carry;
+  }
+  typedef int64_t s;
+  int64_t t[8];
+  t[0] = (s)c[0] + c[8] + c[9] - (s)c[11] - c[12] - c[13] - c[14];
+  t[1] = (s)c[1] + c[9] + c[10] - (s)c[12] - c[13] - c[14] - c[15];
+  t[2] = (s)c[2] + c[10] + c[11] - (s)c[13] - c[14] - c[15];
+  t[3] = (s)c[3] + 2 * (s)c[11] + 2 * (s)c[12] + c[13] - (s)c[15] - c[8] - c[9];
+  t[4] = (s)c[4] + 2 * (s)c[12] + 2 * (s)c[13] + c[14] - (s)c[9] - c[10];
+  t[5] = (s)c[5] + 2 * (s)c[13] + 2 * (s)c[14] + c[15] - (s)c[10] - c[11];
+  t[6] = (s)c[6] + 3 * (s)c[14] + 2 * (s)c[15] + c[13] - (s)c[8] - c[9];
+  t[7] = (s)c[7] + 3 * (s)c[15] + c[8] - (s)c[10] - c[11] - c[12] - c[13];
+  return fold(t);
+}
+DEV fp sqr(const fp& a) { return mul(a, a); }
+
+// canonical representative in [0, p)
+DEV fp freeze(const fp& a) {
+  constexpr uint32_t P[8] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u, 1u, 0xffffffffu};
+  fp d;
+  int64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int64_t x = (int64_t)a.v[i] - P[i] + br;
+    d.v[i] = (uint32_t)x;
+    br = x >> 32;  // 0 or -1
+  }
+  const bool ge = br == 0;  // a >= p
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = ge ? d.v[i] : a.v[i];
+  return r;
+}
+DEV bool eq(const fp& a, const fp& b) {
+  const fp x = freeze(a), y = freeze(b);
+  uint32_t d = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) d |= x.v[i] ^ y.v[i];
+  return d == 0;
+}
+DEV bool is_zero(const fp& a) {
+  const fp x = freeze(a);
+  uint32_t d = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) d |= x.v[i];
+  return d == 0;
+}
+
+// a^(p - 2): p - 2 = ffffffff 00000001 00000000 00000000 00000000 ffffffff ffffffff fffffffd
+DEV fp inv(const fp& a) {
+  constexpr uint32_t E[8] = {0xfffffffdu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u, 1u, 0xffffffffu};
+  fp r = a;  // the top bit of E is set
+#pragma unroll 1
+  for (int i = 254; i >= 0; i--) {
+    r = sqr(r);
+    if ((E[i >> 5] >> (i & 31)) & 1u) r = mul(r, a);
+  }
+  return r;
+}
+
+// 32 big-endian bytes -> limbs; false if the value is >= p (a non-canonical coordinate)
+DEV bool from_be(const uint8_t* b, fp& out) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint8_t* q = b + 4 * (7 - i);
+    out.v[i] = (uint32_t)q[0] << 24 | (uint32_t)q[1] << 16 | (uint32_t)q[2] << 8 | q[3];
+  }
+  const fp f = freeze(out);
+  uint32_t d = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) d |= f.v[i] ^ out.v[i];
+  return d == 0;
+}
+
+struct jac {
+  fp X, Y, Z;
+};
+
+// dbl-2001-b (a = -3): delta = Z^2, gamma = Y^2, beta = X gamma, alpha = 3 (X - delta)(X + delta)
+DEV jac dbl(const jac& P) {
+  const fp delta = sqr(P.Z), gamma = sqr(P.Y), beta = mul(P.X, gamma);
+  const fp alpha = mul_small(mul(sub(P.X, delta), add(P.X, delta)), 3);
+  jac R;
+  R.X = sub(sqr(alpha), mul_small(beta, 8));
+  R.Z = sub(sub(sqr(add(P.Y, P.Z)), gamma), delta);
+  R.Y = sub(mul(alpha, sub(mul_small(beta, 4), R.X)), mul_small(sqr(gamma), 8));
+  return R;
+}
+
+// madd-2007-bl: P (Jacobian) + (x2, y2) (affine), P != +-(x2, y2), P not at infinity
+DEV jac madd(const jac& P, const fp& x2, const fp& y2) {
+  const fp Z1Z1 = sqr(P.Z);
+  const fp U2 = mul(x2, Z1Z1), S2 = mul(y2, mul(P.Z, Z1Z1));
+  const fp H = sub(U2, P.X), HH = sqr(H);
+  const fp I = mul_small(HH, 4), J = mul(H, I);
+  const fp rr = mul_small(sub(S2, P.Y), 2), V = mul(P.X, I);
+  jac R;
+  R.X = sub(sub(sqr(rr), J), mul_small(V, 2));
+  R.Y = sub(mul(rr, sub(V, R.X)), mul_small(mul(P.Y, J), 2));
+  R.Z = sub(sub(sqr(add(P.Z, H)), Z1Z1), HH);
+  return R;
+}
+
+// DH(sk, pkE) for an uncompressed SEC1 point enc = 0x04 || X || Y (65 bytes): validates the
+// point (prefix, canonical coordinates, y^2 = x^3 - 3x + b) and writes the shared x-coordinate
+// as 8 big-endian words (its 32-byte encoding, RFC 9180 7.1.1).  sk: LE limbs, 1 <= sk < n.
+DEV bool ecdh(const uint32_t sk[8], const uint8_t* enc, uint32_t dh_be[8]) {
+  constexpr fp B = {{0x27d2604bu, 0x3bce3c3eu, 0xcc53b0f6u, 0x651d06b0u, 0x769886bcu, 0xb3ebbd55u,
+                     0xaa3a93e7u, 0x5ac635d8u}};
+  fp x, y;
+  bool ok = enc[0] == 0x04;
+  ok = from_be(enc + 1, x) && ok;
+  ok = from_be(enc + 33, y) && ok;
+  const fp rhs = add(sub(mul(sqr(x), x), mul_small(x, 3)), B);
+  ok = ok && eq(sqr(y), rhs);
+  // left-to-right: R = P at the top set bit, then double, add, keep the sum where the bit is 1
+  int top = 255;
+  while (top > 0 && !((sk[top >> 5] >> (top & 31)) & 1u)) top--;  // wave-uniform
+  jac R;
+  R.X = x;
+  R.Y = y;
+  R.Z = fp{{1u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}};
+#pragma unroll 1
+  for (int i = top - 1; i >= 0; i--) {
+    R = dbl(R);
+    const jac T = madd(R, x, y);
+    if ((sk[i >> 5] >> (i & 31)) & 1u) R = T;  // wave-uniform: every key bit costs the same
+  }
+  ok = ok && !is_zero(R.Z);
+  const fp zi = inv(R.Z);
+  const fp ax = freeze(mul(R.X, sqr(zi)));
+#pragma unroll
+  for (int i = 0; i < 8; i++) dh_be[i] = ax.v[7 - i];
+  return ok;
+}
+
+}  // namespace p256

@@ -15,6 +15,7 @@ import numpy as np
 from .prio3 import _np_ptr, _stream, _tptr, load_library
 
 KEM_X25519_HKDF_SHA256 = 0x0020
+KEM_P256_HKDF_SHA256 = 0x0010
 KDF_HKDF_SHA256 = 0x0001
 AEAD_AES_128_GCM = 0x0001
 AEAD_AES_256_GCM = 0x0002
@@ -55,6 +56,7 @@ class HpkeOpener:
                  device: int = 0, kem_id=KEM_X25519_HKDF_SHA256, kdf_id=KDF_HKDF_SHA256,
                  aead_id=AEAD_AES_128_GCM):
         self.device = device
+        self.nenc = 65 if kem_id == KEM_P256_HKDF_SHA256 else 32  # enc bytes per report
         self._keep = (bytes(private_key), bytes(public_key), bytes(info))
         h = C.c_void_p()
         rc = _lib().janus_hpke_opener_create(kem_id, kdf_id, aead_id, _b(private_key),
@@ -121,7 +123,7 @@ class HpkeOpener:
         n = len(ct_list)
         cs = max(16, -(-max(len(c) for c in ct_list) // 16) * 16)
         as_ = -(-max([len(a) for a in aad_list] + [1]) // 16) * 16
-        encs = np.zeros((n, 32), np.uint8)
+        encs = np.zeros((n, self.nenc), np.uint8)
         ct = np.zeros((n, cs), np.uint8)
         aad = np.zeros((n, as_), np.uint8)
         cl = np.zeros(n, np.uint32)

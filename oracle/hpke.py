@@ -47,6 +47,12 @@ def lib():
         _lib.hpke_seal_ex.argtypes = [u16] + _lib.hpke_seal.argtypes
         _lib.hpke_open_input_shares_ex.argtypes = [u16] + _lib.hpke_open_input_shares.argtypes
         _lib.hpke_make_input_shares_ex.argtypes = [u16] + _lib.hpke_make_input_shares.argtypes
+        # and the KEM-selecting forms (kem 0x20 X25519, 0x10 P-256)
+        _lib.hpke_p256_public.argtypes = [vp, vp]
+        _lib.hpke_open_kem.argtypes = [u16] + _lib.hpke_open_ex.argtypes
+        _lib.hpke_seal_kem.argtypes = [u16] + _lib.hpke_seal_ex.argtypes
+        _lib.hpke_open_input_shares_kem.argtypes = [u16] + _lib.hpke_open_input_shares_ex.argtypes
+        _lib.hpke_make_input_shares_kem.argtypes = [u16] + _lib.hpke_make_input_shares_ex.argtypes
     return _lib
 
 
@@ -58,24 +64,49 @@ def _p(b):
     return C.cast(C.c_char_p(bytes(b)), C.c_void_p)
 
 
+KEM_X25519, KEM_P256 = 0x20, 0x10
+
+
+def nenc(kem: int) -> int:
+    """Nenc = Npk: 32 (X25519) or 65 (P-256, uncompressed point)."""
+    return 65 if kem == KEM_P256 else 32
+
+
 def x25519_public(sk: bytes) -> bytes:
     out = C.create_string_buffer(32)
     assert lib().hpke_x25519_public(_p(sk), out) == 0
     return out.raw
 
 
-def open_(skR: bytes, pkR: bytes, enc: bytes, info: bytes, aad: bytes, ct: bytes, aead=1):
+def kem_public(sk: bytes, kem=KEM_X25519) -> bytes:
+    if kem == KEM_X25519:
+        return x25519_public(sk)
+    out = C.create_string_buffer(65)
+    assert lib().hpke_p256_public(_p(sk), out) == 0
+    return out.raw
+
+
+def kem_private(rng, kem=KEM_X25519) -> bytes:
+    """A random private key (P-256: below 2^255, hence below the group order)."""
+    sk = bytearray(rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+    if kem == KEM_P256:
+        sk[0] &= 0x7F
+    return bytes(sk)
+
+
+def open_(skR: bytes, pkR: bytes, enc: bytes, info: bytes, aad: bytes, ct: bytes, aead=1,
+          kem=KEM_X25519):
     pt = C.create_string_buffer(max(len(ct), 1))
-    n = lib().hpke_open_ex(aead, _p(skR), _p(pkR), _p(enc), _p(info), len(info), _p(aad),
-                           len(aad), _p(ct), len(ct), pt)
+    n = lib().hpke_open_kem(kem, aead, _p(skR), _p(pkR), _p(enc), _p(info), len(info), _p(aad),
+                            len(aad), _p(ct), len(ct), pt)
     return None if n < 0 else pt.raw[:n]
 
 
-def seal(pkR: bytes, skE: bytes, info: bytes, aad: bytes, pt: bytes, aead=1):
-    enc = C.create_string_buffer(32)
+def seal(pkR: bytes, skE: bytes, info: bytes, aad: bytes, pt: bytes, aead=1, kem=KEM_X25519):
+    enc = C.create_string_buffer(nenc(kem))
     ct = C.create_string_buffer(len(pt) + 16)
-    assert lib().hpke_seal_ex(aead, _p(pkR), _p(skE), _p(info), len(info), _p(aad), len(aad),
-                              _p(pt), len(pt), enc, ct) == 0
+    assert lib().hpke_seal_kem(kem, aead, _p(pkR), _p(skE), _p(info), len(info), _p(aad),
+                               len(aad), _p(pt), len(pt), enc, ct) == 0
     return enc.raw, ct.raw
 
 
@@ -93,7 +124,7 @@ def plaintext_input_share(payload: bytes, extensions=()) -> bytes:
 
 
 def open_input_shares(skR, pkR, task_id, enc, ct, ct_len, report_ids, times, pubs, share_len,
-                      require_taskprov=False, n_threads=8, aead=1):
+                      require_taskprov=False, n_threads=8, aead=1, kem=KEM_X25519):
     """Batched helper input-share open: (shares [n, share_len], status [n] in {0, 4, 8})."""
     n = enc.shape[0]
     enc = np.ascontiguousarray(enc, np.uint8)
@@ -105,19 +136,20 @@ def open_input_shares(skR, pkR, task_id, enc, ct, ct_len, report_ids, times, pub
     pubs = None if pubs is None else np.ascontiguousarray(pubs, np.uint8)
     shares = np.zeros((n, share_len), np.uint8)
     status = np.zeros(n, np.uint8)
-    lib().hpke_open_input_shares_ex(aead, _p(skR), _p(pkR), _p(task_id), n, _p(enc), _p(ct),
-                                    _p(ct_len), ct.shape[1], _p(ids), _p(times), _p(pubs),
-                                    publen, share_len, int(require_taskprov), _p(shares),
-                                    _p(status), n_threads)
+    lib().hpke_open_input_shares_kem(kem, aead, _p(skR), _p(pkR), _p(task_id), n, _p(enc),
+                                     _p(ct), _p(ct_len), ct.shape[1], _p(ids), _p(times),
+                                     _p(pubs), publen, share_len, int(require_taskprov),
+                                     _p(shares), _p(status), n_threads)
     return shares, status
 
 
-def make_batch(n, share_len, pub_len, seed=1, skR=None, extensions=(), tamper=0.0, aead=1):
+def make_batch(n, share_len, pub_len, seed=1, skR=None, extensions=(), tamper=0.0, aead=1,
+               kem=KEM_X25519):
     """Synthetic Janus-shaped encrypted helper input shares (test/bench data), sealed by the
     oracle with deterministic ephemeral keys.  Returns a dict of numpy arrays."""
     rng = np.random.default_rng(seed)
-    skR = bytes(rng.integers(0, 256, 32, dtype=np.uint8)) if skR is None else skR
-    pkR = x25519_public(skR)
+    skR = kem_private(rng, kem) if skR is None else skR
+    pkR = kem_public(skR, kem)
     task_id = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
     ids = rng.integers(0, 256, (n, 16), dtype=np.uint8)
     times = (1_700_000_000 + rng.integers(0, 3600, n)).astype(np.uint64)
@@ -125,39 +157,40 @@ def make_batch(n, share_len, pub_len, seed=1, skR=None, extensions=(), tamper=0.
     shares = rng.integers(0, 256, (n, share_len), dtype=np.uint8)
     pt_len = len(plaintext_input_share(bytes(share_len), extensions))
     stride = pt_len + 16
-    enc = np.zeros((n, 32), np.uint8)
+    enc = np.zeros((n, nenc(kem)), np.uint8)
     ct = np.zeros((n, stride), np.uint8)
     ct_len = np.full(n, stride, np.uint32)
     for r in range(n):
         aad = input_share_aad(task_id, ids[r].tobytes(), int(times[r]),
                               b"" if pubs is None else pubs[r].tobytes())
-        skE = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+        skE = kem_private(rng, kem)
         e, c = seal(pkR, skE, INFO_INPUT_SHARE_HELPER, aad,
-                    plaintext_input_share(shares[r].tobytes(), extensions), aead=aead)
+                    plaintext_input_share(shares[r].tobytes(), extensions), aead=aead, kem=kem)
         enc[r] = np.frombuffer(e, np.uint8)
         ct[r] = np.frombuffer(c, np.uint8)
     return dict(skR=skR, pkR=pkR, task_id=task_id, report_ids=ids, times=times, pubs=pubs,
                 shares=shares, enc=enc, ct=ct, ct_len=ct_len)
 
 
-def make_batch_fast(n, share_len, pub_len, seed=1, taskprov=False, n_threads=8, skR=None, aead=1):
+def make_batch_fast(n, share_len, pub_len, seed=1, taskprov=False, n_threads=8, skR=None, aead=1,
+                    kem=KEM_X25519):
     """make_batch in C with threads (bench-size batches); every report distinct."""
     rng = np.random.default_rng(seed)
-    skR = bytes(rng.integers(0, 256, 32, dtype=np.uint8)) if skR is None else skR
-    pkR = x25519_public(skR)
+    skR = kem_private(rng, kem) if skR is None else skR
+    pkR = kem_public(skR, kem)
     task_id = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
     stride = -(-((10 if taskprov else 6) + share_len + 16) // 16) * 16
-    enc = np.zeros((n, 32), np.uint8)
+    enc = np.zeros((n, nenc(kem)), np.uint8)
     ct = np.zeros((n, stride), np.uint8)
     ct_len = np.zeros(n, np.uint32)
     ids = np.zeros((n, 16), np.uint8)
     times = np.zeros(n, np.uint64)
     pubs = np.zeros((n, pub_len), np.uint8) if pub_len else None
     shares = np.zeros((n, share_len), np.uint8)
-    rc = lib().hpke_make_input_shares_ex(aead, _p(pkR), _p(task_id), n, seed, share_len,
-                                         pub_len, int(taskprov), stride, _p(enc), _p(ct),
-                                         _p(ct_len), _p(ids), _p(times), _p(pubs), _p(shares),
-                                         n_threads)
+    rc = lib().hpke_make_input_shares_kem(kem, aead, _p(pkR), _p(task_id), n, seed, share_len,
+                                          pub_len, int(taskprov), stride, _p(enc), _p(ct),
+                                          _p(ct_len), _p(ids), _p(times), _p(pubs), _p(shares),
+                                          n_threads)
     assert rc == 0
     return dict(skR=skR, pkR=pkR, task_id=task_id, report_ids=ids, times=times, pubs=pubs,
                 shares=shares, enc=enc, ct=ct, ct_len=ct_len)

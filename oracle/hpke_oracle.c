@@ -19,8 +19,12 @@
  * taskprov-extension checks, and the exact-length helper input share decode.
  */
 #define OPENSSL_SUPPRESS_DEPRECATED
+#include <openssl/bn.h>
+#include <openssl/ec.h>
+#include <openssl/ecdh.h>
 #include <openssl/evp.h>
 #include <openssl/hmac.h>
+#include <openssl/obj_mac.h>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -28,12 +32,17 @@
 
 enum { HPKE_OK = 0, HPKE_DECRYPT_ERROR = 4, HPKE_INVALID_MESSAGE = 8 };
 
-static const uint8_t KEM_SUITE[5] = {'K', 'E', 'M', 0x00, 0x20};
+/* KEM 0x0020 DHKEM(X25519, HKDF-SHA256) (Nenc = Npk = 32) or 0x0010 DHKEM(P-256, HKDF-SHA256)
+ * (Nenc = Npk = 65, uncompressed points) */
+static void kem_suite(uint16_t kem, uint8_t s[5]) {
+  s[0] = 'K', s[1] = 'E', s[2] = 'M', s[3] = (uint8_t)(kem >> 8), s[4] = (uint8_t)kem;
+}
+static size_t kem_nenc(uint16_t kem) { return kem == 0x10 ? 65 : 32; }
 /* suite_id = "HPKE" || kem || kdf || aead (RFC 9180 5.1); aead 1 AES-128-GCM, 2 AES-256-GCM,
  * 3 ChaCha20Poly1305 (messages/src/lib.rs:844-853) */
-static void hpke_suite(uint16_t aead, uint8_t s[10]) {
-  static const uint8_t base[8] = {'H', 'P', 'K', 'E', 0x00, 0x20, 0x00, 0x01};
-  memcpy(s, base, 8);
+static void hpke_suite(uint16_t kem, uint16_t aead, uint8_t s[10]) {
+  s[0] = 'H', s[1] = 'P', s[2] = 'K', s[3] = 'E';
+  s[4] = (uint8_t)(kem >> 8), s[5] = (uint8_t)kem, s[6] = 0x00, s[7] = 0x01;
   s[8] = (uint8_t)(aead >> 8);
   s[9] = (uint8_t)aead;
 }
@@ -89,6 +98,39 @@ static int x25519(const uint8_t sk[32], const uint8_t pk[32], uint8_t out[32]) {
   return ok ? 0 : -1;
 }
 
+/* P-256 ECDH (SEC 1): the x-coordinate of sk * pk, pk an uncompressed point (validated) */
+static int p256_dh(const uint8_t sk[32], const uint8_t pk[65], uint8_t out[32]) {
+  EC_KEY* k = EC_KEY_new_by_curve_name(NID_X9_62_prime256v1);
+  const EC_GROUP* g = k ? EC_KEY_get0_group(k) : NULL;
+  BIGNUM* d = BN_bin2bn(sk, 32, NULL);
+  EC_POINT* q = g ? EC_POINT_new(g) : NULL;
+  int ok = k && d && q && EC_KEY_set_private_key(k, d) == 1 &&
+           EC_POINT_oct2point(g, q, pk, 65, NULL) == 1 && EC_POINT_is_on_curve(g, q, NULL) == 1 &&
+           ECDH_compute_key(out, 32, q, k, NULL) == 32;
+  EC_POINT_free(q);
+  BN_free(d);
+  EC_KEY_free(k);
+  return ok ? 0 : -1;
+}
+
+int hpke_p256_public(const uint8_t sk[32], uint8_t pk[65]) {
+  EC_KEY* k = EC_KEY_new_by_curve_name(NID_X9_62_prime256v1);
+  const EC_GROUP* g = k ? EC_KEY_get0_group(k) : NULL;
+  BIGNUM* d = BN_bin2bn(sk, 32, NULL);
+  EC_POINT* q = g ? EC_POINT_new(g) : NULL;
+  int ok = k && d && q && EC_POINT_mul(g, q, d, NULL, NULL, NULL) == 1 &&
+           EC_POINT_point2oct(g, q, POINT_CONVERSION_UNCOMPRESSED, pk, 65, NULL) == 65;
+  EC_POINT_free(q);
+  BN_free(d);
+  EC_KEY_free(k);
+  return ok ? 0 : -1;
+}
+
+static int kem_dh(uint16_t kem, const uint8_t sk[32], const uint8_t* pk, uint8_t out[32]) {
+  return kem == 0x10 ? p256_dh(sk, pk, out) : x25519(sk, pk, out);
+}
+static int kem_public(uint16_t kem, const uint8_t sk[32], uint8_t* pk);
+
 int hpke_x25519_public(const uint8_t sk[32], uint8_t pk[32]) {
   EVP_PKEY* k = EVP_PKEY_new_raw_private_key(EVP_PKEY_X25519, NULL, sk, 32);
   size_t ol = 32;
@@ -96,12 +138,15 @@ int hpke_x25519_public(const uint8_t sk[32], uint8_t pk[32]) {
   EVP_PKEY_free(k);
   return ok ? 0 : -1;
 }
+static int kem_public(uint16_t kem, const uint8_t sk[32], uint8_t* pk) {
+  return kem == 0x10 ? hpke_p256_public(sk, pk) : hpke_x25519_public(sk, pk);
+}
 
 /* KeySchedule(mode_base, shared_secret, info) -> key (Nk), base_nonce (12)  [RFC 9180 §5.1] */
-static void key_schedule(uint16_t aead, const uint8_t ss[32], const uint8_t* info,
+static void key_schedule(uint16_t kem, uint16_t aead, const uint8_t ss[32], const uint8_t* info,
                          size_t infolen, uint8_t key[32], uint8_t nonce[12]) {
   uint8_t ksc[65], secret[32], su[10];
-  hpke_suite(aead, su);
+  hpke_suite(kem, aead, su);
   ksc[0] = 0x00;  /* mode_base */
   labeled_extract(su, 10, NULL, 0, "psk_id_hash", NULL, 0, ksc + 1);
   labeled_extract(su, 10, NULL, 0, "info_hash", info, infolen, ksc + 33);
@@ -111,16 +156,18 @@ static void key_schedule(uint16_t aead, const uint8_t ss[32], const uint8_t* inf
 }
 
 /* Decap (§4.1): dh = DH(skR, enc); shared_secret = ExtractAndExpand(dh, enc || pkRm) */
-static int decap(const uint8_t enc[32], const uint8_t skR[32], const uint8_t pkR[32],
+static int decap(uint16_t kem, const uint8_t* enc, const uint8_t skR[32], const uint8_t* pkR,
                  uint8_t ss[32]) {
-  uint8_t dh[32], prk[32], kc[64];
-  if (x25519(skR, enc, dh)) return -1;
+  uint8_t dh[32], prk[32], kc[130], ks[5];
+  const size_t ne = kem_nenc(kem);
+  if (kem_dh(kem, skR, enc, dh)) return -1;
   static const uint8_t zero32[32];
-  if (!memcmp(dh, zero32, 32)) return -1; /* all-zero shared secret: ValidationError */
-  labeled_extract(KEM_SUITE, 5, NULL, 0, "eae_prk", dh, 32, prk);
-  memcpy(kc, enc, 32);
-  memcpy(kc + 32, pkR, 32);
-  labeled_expand(KEM_SUITE, 5, prk, "shared_secret", kc, 64, 32, ss);
+  if (kem != 0x10 && !memcmp(dh, zero32, 32)) return -1; /* X25519 all-zero: ValidationError */
+  kem_suite(kem, ks);
+  labeled_extract(ks, 5, NULL, 0, "eae_prk", dh, 32, prk);
+  memcpy(kc, enc, ne);
+  memcpy(kc + ne, pkR, ne);
+  labeled_expand(ks, 5, prk, "shared_secret", kc, 2 * ne, 32, ss);
   return 0;
 }
 
@@ -150,15 +197,20 @@ static int aead_crypt(uint16_t aead, int decrypt, const uint8_t* key, const uint
 }
 
 /* base-mode single-shot open (sequence number 0); returns the plaintext length or -1 */
-int hpke_open_ex(uint16_t aead, const uint8_t skR[32], const uint8_t pkR[32],
-                 const uint8_t enc[32], const uint8_t* info, size_t infolen, const uint8_t* aad,
-                 size_t aadlen, const uint8_t* ct, size_t ctlen, uint8_t* pt) {
+int hpke_open_kem(uint16_t kem, uint16_t aead, const uint8_t skR[32], const uint8_t* pkR,
+                  const uint8_t* enc, const uint8_t* info, size_t infolen, const uint8_t* aad,
+                  size_t aadlen, const uint8_t* ct, size_t ctlen, uint8_t* pt) {
   uint8_t ss[32], key[32], nonce[12], tag[16];
-  if (ctlen < 16 || decap(enc, skR, pkR, ss)) return -1;
-  key_schedule(aead, ss, info, infolen, key, nonce);
+  if (ctlen < 16 || decap(kem, enc, skR, pkR, ss)) return -1;
+  key_schedule(kem, aead, ss, info, infolen, key, nonce);
   memcpy(tag, ct + ctlen - 16, 16);
   if (aead_crypt(aead, 1, key, nonce, aad, aadlen, ct, ctlen - 16, pt, tag)) return -1;
   return (int)(ctlen - 16);
+}
+int hpke_open_ex(uint16_t aead, const uint8_t skR[32], const uint8_t pkR[32],
+                 const uint8_t enc[32], const uint8_t* info, size_t infolen, const uint8_t* aad,
+                 size_t aadlen, const uint8_t* ct, size_t ctlen, uint8_t* pt) {
+  return hpke_open_kem(0x20, aead, skR, pkR, enc, info, infolen, aad, aadlen, ct, ctlen, pt);
 }
 int hpke_open(const uint8_t skR[32], const uint8_t pkR[32], const uint8_t enc[32],
               const uint8_t* info, size_t infolen, const uint8_t* aad, size_t aadlen,
@@ -168,17 +220,24 @@ int hpke_open(const uint8_t skR[32], const uint8_t pkR[32], const uint8_t enc[32
 
 /* base-mode seal with the ephemeral key skE (Encap with a given ephemeral key, as the RFC 9180
  * test vectors do); writes enc[32] and ct[ptlen + 16] */
+int hpke_seal_kem(uint16_t kem, uint16_t aead, const uint8_t* pkR, const uint8_t skE[32],
+                  const uint8_t* info, size_t infolen, const uint8_t* aad, size_t aadlen,
+                  const uint8_t* pt, size_t ptlen, uint8_t* enc, uint8_t* ct) {
+  uint8_t dh[32], prk[32], kc[130], ss[32], key[32], nonce[12], ks[5];
+  const size_t ne = kem_nenc(kem);
+  if (kem_public(kem, skE, enc) || kem_dh(kem, skE, pkR, dh)) return -1;
+  kem_suite(kem, ks);
+  labeled_extract(ks, 5, NULL, 0, "eae_prk", dh, 32, prk);
+  memcpy(kc, enc, ne);
+  memcpy(kc + ne, pkR, ne);
+  labeled_expand(ks, 5, prk, "shared_secret", kc, 2 * ne, 32, ss);
+  key_schedule(kem, aead, ss, info, infolen, key, nonce);
+  return aead_crypt(aead, 0, key, nonce, aad, aadlen, pt, ptlen, ct, ct + ptlen);
+}
 int hpke_seal_ex(uint16_t aead, const uint8_t pkR[32], const uint8_t skE[32],
                  const uint8_t* info, size_t infolen, const uint8_t* aad, size_t aadlen,
                  const uint8_t* pt, size_t ptlen, uint8_t enc[32], uint8_t* ct) {
-  uint8_t dh[32], prk[32], kc[64], ss[32], key[32], nonce[12];
-  if (hpke_x25519_public(skE, enc) || x25519(skE, pkR, dh)) return -1;
-  labeled_extract(KEM_SUITE, 5, NULL, 0, "eae_prk", dh, 32, prk);
-  memcpy(kc, enc, 32);
-  memcpy(kc + 32, pkR, 32);
-  labeled_expand(KEM_SUITE, 5, prk, "shared_secret", kc, 64, 32, ss);
-  key_schedule(aead, ss, info, infolen, key, nonce);
-  return aead_crypt(aead, 0, key, nonce, aad, aadlen, pt, ptlen, ct, ct + ptlen);
+  return hpke_seal_kem(0x20, aead, pkR, skE, info, infolen, aad, aadlen, pt, ptlen, enc, ct);
 }
 int hpke_seal(const uint8_t pkR[32], const uint8_t skE[32], const uint8_t* info, size_t infolen,
               const uint8_t* aad, size_t aadlen, const uint8_t* pt, size_t ptlen, uint8_t enc[32],
@@ -246,7 +305,7 @@ typedef struct {
   int require_taskprov;
   uint8_t *shares, *status;
   uint32_t lo, hi;
-  uint16_t aead;
+  uint16_t aead, kem;
 } Job;
 
 static const uint8_t INFO[20] = {'d', 'a', 'p', '-', '0', '9', ' ', 'i', 'n', 'p',
@@ -261,8 +320,9 @@ static void* run(void* arg) {
                                      aad);
     uint32_t cl = j->ct_len[r];
     int ptl = cl <= sizeof(pt) + 16
-                  ? hpke_open_ex(j->aead, j->skR, j->pkR, j->enc + 32 * (size_t)r, INFO,
-                                 sizeof(INFO), aad, al, j->ct + (size_t)j->ct_stride * r, cl, pt)
+                  ? hpke_open_kem(j->kem, j->aead, j->skR, j->pkR,
+                                  j->enc + kem_nenc(j->kem) * (size_t)r, INFO, sizeof(INFO), aad,
+                                  al, j->ct + (size_t)j->ct_stride * r, cl, pt)
                   : -1;
     uint8_t* so = j->shares + (size_t)j->share_len * r;
     memset(so, 0, j->share_len);
@@ -276,13 +336,20 @@ static void* run(void* arg) {
 
 /* Batched helper input-share open: status[r] = 0 (helper share written), 4 (HpkeDecryptError)
  * or 8 (InvalidMessage), the PrepareError codes of messages/src/lib.rs. */
-int hpke_open_input_shares_ex(uint16_t aead, const uint8_t skR[32], const uint8_t pkR[32],
-                              const uint8_t task_id[32], uint32_t n, const uint8_t* enc,
-                              const uint8_t* ct, const uint32_t* ct_len, uint32_t ct_stride,
-                              const uint8_t* report_ids, const uint64_t* times,
-                              const uint8_t* pubs, uint32_t publen, uint32_t share_len,
-                              int require_taskprov, uint8_t* shares, uint8_t* status,
-                              int n_threads) {
+int hpke_open_input_shares_kem(uint16_t kem, uint16_t aead, const uint8_t skR[32],
+                               const uint8_t* pkR, const uint8_t task_id[32], uint32_t n,
+                               const uint8_t* enc, const uint8_t* ct, const uint32_t* ct_len,
+                               uint32_t ct_stride, const uint8_t* report_ids,
+                               const uint64_t* times, const uint8_t* pubs, uint32_t publen,
+                               uint32_t share_len, int require_taskprov, uint8_t* shares,
+                               uint8_t* status, int n_threads);
+int hpke_open_input_shares_kem(uint16_t kem, uint16_t aead, const uint8_t skR[32],
+                               const uint8_t* pkR, const uint8_t task_id[32], uint32_t n,
+                               const uint8_t* enc, const uint8_t* ct, const uint32_t* ct_len,
+                               uint32_t ct_stride, const uint8_t* report_ids,
+                               const uint64_t* times, const uint8_t* pubs, uint32_t publen,
+                               uint32_t share_len, int require_taskprov, uint8_t* shares,
+                               uint8_t* status, int n_threads) {
   if (n_threads < 1) n_threads = 1;
   pthread_t th[256];
   Job jobs[256];
@@ -291,11 +358,22 @@ int hpke_open_input_shares_ex(uint16_t aead, const uint8_t skR[32], const uint8_
     jobs[t] = (Job){skR, pkR, task_id, enc, ct, report_ids, pubs, ct_len, times, n, ct_stride,
                     publen, share_len, require_taskprov, shares, status,
                     (uint32_t)((uint64_t)n * t / n_threads),
-                    (uint32_t)((uint64_t)n * (t + 1) / n_threads), aead};
+                    (uint32_t)((uint64_t)n * (t + 1) / n_threads), aead, kem};
     pthread_create(&th[t], NULL, run, &jobs[t]);
   }
   for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
   return 0;
+}
+int hpke_open_input_shares_ex(uint16_t aead, const uint8_t skR[32], const uint8_t pkR[32],
+                              const uint8_t task_id[32], uint32_t n, const uint8_t* enc,
+                              const uint8_t* ct, const uint32_t* ct_len, uint32_t ct_stride,
+                              const uint8_t* report_ids, const uint64_t* times,
+                              const uint8_t* pubs, uint32_t publen, uint32_t share_len,
+                              int require_taskprov, uint8_t* shares, uint8_t* status,
+                              int n_threads) {
+  return hpke_open_input_shares_kem(0x20, aead, skR, pkR, task_id, n, enc, ct, ct_len, ct_stride,
+                                    report_ids, times, pubs, publen, share_len, require_taskprov,
+                                    shares, status, n_threads);
 }
 int hpke_open_input_shares(const uint8_t skR[32], const uint8_t pkR[32], const uint8_t task_id[32],
                            uint32_t n, const uint8_t* enc, const uint8_t* ct, const uint32_t* ct_len,
@@ -319,7 +397,7 @@ typedef struct {
   uint8_t *enc, *ct, *ids, *pubs, *shares;
   uint32_t* ct_len;
   uint64_t* times;
-  uint16_t aead;
+  uint16_t aead, kem;
 } GenJob;
 
 static void prf(uint64_t seed, uint32_t r, uint8_t purpose, uint8_t* out, size_t len) {
@@ -361,18 +439,19 @@ static void* gen_run(void* arg) {
     size_t al = hpke_input_share_aad(j->task_id, id, j->times[r], pub, j->publen, aad);
     uint8_t* ct = j->ct + (size_t)j->stride * r;
     memset(ct, 0, j->stride);
-    hpke_seal_ex(j->aead, j->pkR, skE, INFO, sizeof(INFO), aad, al, pt, l,
-                 j->enc + 32 * (size_t)r, ct);
+    if (j->kem == 0x10) skE[0] &= 0x7f; /* a P-256 scalar below the group order */
+    hpke_seal_kem(j->kem, j->aead, j->pkR, skE, INFO, sizeof(INFO), aad, al, pt, l,
+                  j->enc + kem_nenc(j->kem) * (size_t)r, ct);
     j->ct_len[r] = (uint32_t)(l + 16);
   }
   return NULL;
 }
 
-int hpke_make_input_shares_ex(uint16_t aead, const uint8_t pkR[32], const uint8_t task_id[32],
-                              uint32_t n, uint64_t seed, uint32_t share_len, uint32_t publen,
-                              int taskprov, uint32_t stride, uint8_t* enc, uint8_t* ct,
-                              uint32_t* ct_len, uint8_t* ids, uint64_t* times, uint8_t* pubs,
-                              uint8_t* shares, int n_threads) {
+int hpke_make_input_shares_kem(uint16_t kem, uint16_t aead, const uint8_t* pkR,
+                               const uint8_t task_id[32], uint32_t n, uint64_t seed,
+                               uint32_t share_len, uint32_t publen, int taskprov, uint32_t stride,
+                               uint8_t* enc, uint8_t* ct, uint32_t* ct_len, uint8_t* ids,
+                               uint64_t* times, uint8_t* pubs, uint8_t* shares, int n_threads) {
   if ((taskprov ? 10u : 6u) + share_len + 16 > stride) return -1;
   if (n_threads < 1) n_threads = 1;
   if (n_threads > 256) n_threads = 256;
@@ -382,19 +461,28 @@ int hpke_make_input_shares_ex(uint16_t aead, const uint8_t pkR[32], const uint8_
     jobs[t] = (GenJob){pkR, task_id, seed, share_len, publen, stride,
                        (uint32_t)((uint64_t)n * t / n_threads),
                        (uint32_t)((uint64_t)n * (t + 1) / n_threads), taskprov, enc, ct, ids, pubs,
-                       shares, ct_len, times, aead};
+                       shares, ct_len, times, aead, kem};
     pthread_create(&th[t], NULL, gen_run, &jobs[t]);
   }
   for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
   return 0;
+}
+int hpke_make_input_shares_ex(uint16_t aead, const uint8_t pkR[32], const uint8_t task_id[32],
+                              uint32_t n, uint64_t seed, uint32_t share_len, uint32_t publen,
+                              int taskprov, uint32_t stride, uint8_t* enc, uint8_t* ct,
+                              uint32_t* ct_len, uint8_t* ids, uint64_t* times, uint8_t* pubs,
+                              uint8_t* shares, int n_threads) {
+  return hpke_make_input_shares_kem(0x20, aead, pkR, task_id, n, seed, share_len, publen,
+                                    taskprov, stride, enc, ct, ct_len, ids, times, pubs, shares,
+                                    n_threads);
 }
 int hpke_make_input_shares(const uint8_t pkR[32], const uint8_t task_id[32], uint32_t n,
                            uint64_t seed, uint32_t share_len, uint32_t publen, int taskprov,
                            uint32_t stride, uint8_t* enc, uint8_t* ct, uint32_t* ct_len,
                            uint8_t* ids, uint64_t* times, uint8_t* pubs, uint8_t* shares,
                            int n_threads) {
-  return hpke_make_input_shares_ex(1, pkR, task_id, n, seed, share_len, publen, taskprov, stride,
-                                   enc, ct, ct_len, ids, times, pubs, shares, n_threads);
+  return hpke_make_input_shares_kem(0x20, 1, pkR, task_id, n, seed, share_len, publen, taskprov,
+                                    stride, enc, ct, ct_len, ids, times, pubs, shares, n_threads);
 }
 
 /* Seal given helper input shares (bench data for the request->response pipeline): enc[n][32],

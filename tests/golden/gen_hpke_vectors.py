@@ -1,6 +1,6 @@
 """Extracts the RFC 9180 test vectors of the HPKE suites the GPU opener implements
-(mode_base, DHKEM(X25519, HKDF-SHA256) 0x0020, HKDF-SHA256 0x0001, with AES-128-GCM 0x0001,
-AES-256-GCM 0x0002 and ChaCha20Poly1305 0x0003) from the
+(mode_base, DHKEM(X25519, HKDF-SHA256) 0x0020 or DHKEM(P-256, HKDF-SHA256) 0x0010, HKDF-SHA256
+0x0001, with AES-128-GCM 0x0001, AES-256-GCM 0x0002 and ChaCha20Poly1305 0x0003) from the
 file Janus's own HPKE test reads (/root/reference/core/src/test-vectors.json, used by
 core/src/hpke.rs `decrypt_test_vectors`).  Run in the build container only; the output fixture is
 data (keys, ciphertexts, plaintexts), committed as tests/golden/hpke_rfc9180_x25519.json."""
@@ -13,18 +13,22 @@ OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "hpke_rfc9180_x25
 
 
 # (aead id, output file): AES-128-GCM (the original fixture), AES-256-GCM, ChaCha20Poly1305
-OUTS = {1: OUT,
-        2: os.path.join(os.path.dirname(OUT), "hpke_rfc9180_x25519_aes256gcm.json"),
-        3: os.path.join(os.path.dirname(OUT), "hpke_rfc9180_x25519_chacha20poly1305.json")}
+_D = os.path.dirname(OUT)
+OUTS = {(32, 1): OUT,
+        (32, 2): os.path.join(_D, "hpke_rfc9180_x25519_aes256gcm.json"),
+        (32, 3): os.path.join(_D, "hpke_rfc9180_x25519_chacha20poly1305.json"),
+        (16, 1): os.path.join(_D, "hpke_rfc9180_p256_aes128gcm.json"),
+        (16, 2): os.path.join(_D, "hpke_rfc9180_p256_aes256gcm.json"),
+        (16, 3): os.path.join(_D, "hpke_rfc9180_p256_chacha20poly1305.json")}
 
 
 def main():
     vecs = json.load(open(SRC))
-    for aead, path in OUTS.items():
+    for (kem, aead), path in OUTS.items():
         keep = [v for v in vecs
-                if (v["mode"], v["kem_id"], v["kdf_id"], v["aead_id"]) == (0, 32, 1, aead)]
+                if (v["mode"], v["kem_id"], v["kdf_id"], v["aead_id"]) == (0, kem, 1, aead)]
         if len(keep) != 1:
-            sys.exit(f"expected exactly one X25519/HKDF-SHA256/aead {aead} base-mode vector")
+            sys.exit(f"expected exactly one kem {kem} / HKDF-SHA256 / aead {aead} base-mode vector")
         v = keep[0]
         out = {k: v[k] for k in ("mode", "kem_id", "kdf_id", "aead_id", "info", "enc", "pkRm",
                                  "skRm", "base_nonce")}

@@ -216,3 +216,81 @@ def test_gpu_input_shares_match_oracle_every_aead(aead, n, pub, share_len, ext, 
                                   d["times"], d["pubs"], share_len, require_taskprov=taskprov)
     np.testing.assert_array_equal(st, ref_st)
     np.testing.assert_array_equal(sh, ref_sh)
+
+
+# ---- DHKEM(P-256, HKDF-SHA256) (0x0010), every AEAD -----------------------------------------
+GOLD_P256 = {a: json.load(open(os.path.join(_GDIR, f"hpke_rfc9180_p256_{n}.json")))
+             for a, n in ((1, "aes128gcm"), (2, "aes256gcm"), (3, "chacha20poly1305"))}
+
+
+@pytest.mark.parametrize("aead", [1, 2, 3])
+def test_oracle_p256_vectors(aead):
+    """The oracle's DHKEM(P-256): public key from the private scalar, Decap of the vector's enc
+    (kem_context = enc || pkRm, 130 bytes) and the key schedule with kem 0x0010 in the suite id,
+    pinned by the vectors of core/src/test-vectors.json for kem 0x10 / kdf 1."""
+    g = GOLD_P256[aead]
+    assert g["kem_id"] == 0x10 and g["kdf_id"] == 1 and g["aead_id"] == aead
+    assert H.kem_public(b(g["skRm"]), H.KEM_P256) == b(g["pkRm"])
+    e = g["encryptions"][0]
+    pt = H.open_(b(g["skRm"]), b(g["pkRm"]), b(g["enc"]), b(g["info"]), b(e["aad"]), b(e["ct"]),
+                 aead=aead, kem=H.KEM_P256)
+    assert pt == b(e["pt"])
+    bad_enc = bytearray(b(g["enc"]))
+    bad_enc[40] ^= 1  # off the curve
+    assert H.open_(b(g["skRm"]), b(g["pkRm"]), bytes(bad_enc), b(g["info"]), b(e["aad"]),
+                   b(e["ct"]), aead=aead, kem=H.KEM_P256) is None
+    # seal -> open round trip through the oracle's encap
+    rng = np.random.default_rng(aead)
+    skE = H.kem_private(rng, H.KEM_P256)
+    enc, ct = H.seal(b(g["pkRm"]), skE, b(g["info"]), b"aad", b"plaintext", aead=aead,
+                     kem=H.KEM_P256)
+    assert len(enc) == 65 and enc[0] == 4
+    assert H.open_(b(g["skRm"]), b(g["pkRm"]), enc, b(g["info"]), b"aad", ct, aead=aead,
+                   kem=H.KEM_P256) == b"plaintext"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("aead", [1, 2, 3])
+def test_gpu_p256_vectors(aead):
+    from janus_amd import hpke as G
+    g = GOLD_P256[aead]
+    op = G.HpkeOpener(b(g["skRm"]), b(g["pkRm"]), info=b(g["info"]),
+                      kem_id=G.KEM_P256_HKDF_SHA256, aead_id=aead)
+    e = g["encryptions"][0]
+    bad = bytearray(b(e["ct"]))
+    bad[-1] ^= 1
+    off_curve = bytearray(b(g["enc"]))
+    off_curve[40] ^= 1
+    not_canon = bytearray(b(g["enc"]))
+    not_canon[1:33] = b"\xff" * 32  # x >= p
+    got = op.open([b(g["enc"]), b(g["enc"]), b(g["enc"]), bytes(off_curve), bytes(not_canon)],
+                  [b(e["ct"]), bytes(bad), b(e["ct"]), b(e["ct"]), b(e["ct"])],
+                  [b(e["aad"]), b(e["aad"]), b"wrong aad", b(e["aad"]), b(e["aad"])])
+    assert got[0] == b(e["pt"])
+    assert got[1:] == [None] * 4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("aead", [1, 3])
+@pytest.mark.parametrize("n,pub,tamper", [(1, 32, False), (130, 32, True), (97, 0, True)])
+def test_gpu_p256_input_shares_match_oracle(aead, n, pub, tamper):
+    """DHKEM(P-256) helper input shares (65-byte enc): the GPU opener against the oracle with
+    the Janus-visible tampering, a wrong ephemeral point included."""
+    from janus_amd import hpke as G
+    rng = np.random.default_rng(n + pub + 1000 * aead)
+    d = H.make_batch(n, 48, pub, seed=n * 11 + pub + aead, aead=aead, kem=H.KEM_P256)
+    exp = None
+    if tamper:
+        d, exp = _tamper(d, rng)
+    ref_sh, ref_st = H.open_input_shares(d["skR"], d["pkR"], d["task_id"], d["enc"], d["ct"],
+                                         d["ct_len"], d["report_ids"], d["times"], d["pubs"], 48,
+                                         aead=aead, kem=H.KEM_P256)
+    if exp is not None:
+        np.testing.assert_array_equal(ref_st, exp)
+    else:
+        assert (ref_st == 0).all()
+    op = G.HpkeOpener(d["skR"], d["pkR"], kem_id=G.KEM_P256_HKDF_SHA256, aead_id=aead)
+    sh, st = op.open_input_shares(d["task_id"], d["enc"], d["ct"], d["ct_len"], d["report_ids"],
+                                  d["times"], d["pubs"], 48)
+    np.testing.assert_array_equal(st, ref_st)
+    np.testing.assert_array_equal(sh, ref_sh)
