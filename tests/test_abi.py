@@ -47,10 +47,19 @@ def test_dap_header_declares_the_exported_set():
 
 
 def test_hpke_unsupported_suite_is_refused():
-    """P-256 / other suites stay on the host path: creation says EUNSUPPORTED (no GPU call)."""
+    """P-384 / P-521 / X448 and HKDF-SHA384/512 stay on the host path: creation says
+    EUNSUPPORTED before any GPU call; a P-256 key outside [1, n) is EINVAL (no GPU call)."""
     from janus_amd import hpke as H
     with pytest.raises(NotImplementedError):
-        H.HpkeOpener(bytes(32), bytes(65), kem_id=0x0010)
+        H.HpkeOpener(bytes(48), bytes(97), kem_id=0x0011)   # P-384
+    with pytest.raises(NotImplementedError):
+        H.HpkeOpener(bytes(56), bytes(56), kem_id=0x0021)   # X448
+    with pytest.raises(NotImplementedError):
+        H.HpkeOpener(bytes(32), bytes(32), kdf_id=0x0003)   # HKDF-SHA512
+    with pytest.raises(RuntimeError, match="rc=-1"):
+        H.HpkeOpener(bytes(32), b"\x04" + bytes(64), kem_id=0x0010)  # sk = 0
+    with pytest.raises(RuntimeError, match="rc=-1"):
+        H.HpkeOpener(b"\xff" * 32, b"\x04" + bytes(64), kem_id=0x0010)  # sk >= n
 
 
 def test_library_exports_every_declared_symbol():
