@@ -1478,6 +1478,7 @@ __global__ __launch_bounds__(256, 3) void k_prep_h(DevParams p, InPtrs in, Scrat
 
 
 
+
 // ------------------------------------------------------------------------------------
 // k_query_r<C, K>: the P = 32 ParallelSum(Mul, C) query (Prio3Histogram(256,16): C = K = 16)
 // with every per-call coefficient register-resident.  The Lagrange values L_1..L_K and

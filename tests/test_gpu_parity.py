@@ -328,3 +328,4 @@ def test_fused_prepare_kernel_parity(name, opts):
     the two-kernel chain with the slow path deferred or per chunk, on tampered ragged batches."""
     _check_against_oracle(CONFIGS[name], 777, seed=83, opts=opts)
 
+
