@@ -3044,11 +3044,33 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
 
 
 // The deferred slow path of a run whose k_query_h launches skipped the reports the XOF flagged
-// (slow_defer): one k_xof_slow launch over the whole run redoes their XOF and marks them 2, then
-// k_query_h runs once more with redo = 1, for exactly those reports (every other lane leaves
-// after reading its flag).  Two launches per run instead of one k_xof_slow launch between the
-// XOF and the query of every chunk, where its one-wave blocks waited behind the other stream's
-// kernels (~0.2 ms per chunk in the r02 trace).
+// (slow_defer): one k_slow_redo launch over the whole run redoes their XOF (marking them 2) and
+// then their query (redo = 1), lane by lane.  One launch per run instead of one k_xof_slow
+// launch between the XOF and the query of every chunk, where its one-wave blocks waited behind
+// the other stream's kernels (~0.2 ms per chunk in the r02 trace).
+// k_slow_redo<PP>: both halves in one launch -- each lane scans the flags of 16 reports with one
+// 16-byte load (as k_xof_slow<F, 16>) and, for a flagged report, re-runs its XOF (flag := 2) and
+// then its query on the same lane.
+template <int PP>
+__global__ __launch_bounds__(64) void k_slow_redo(DevParams p, InPtrs in, Scratch sc, OutPtrs out) {
+  const uint32_t r0 = (blockIdx.x * blockDim.x + threadIdx.x) * 16u;
+  if (r0 >= p.n) return;
+  const uint8_t* fl = sc.flag + r0;
+  uint32_t any = 0;
+  if (r0 + 16 <= p.n && ((uintptr_t)fl & 15) == 0) {
+    const uint4 v = *(const uint4*)fl;
+    any = v.x | v.y | v.z | v.w;
+  } else {
+    for (uint32_t i = 0; i < 16 && r0 + i < p.n; i++) any |= fl[i];
+  }
+  if (!any) return;
+  for (uint32_t i = 0; i < 16 && r0 + i < p.n; i++)
+    if (fl[i]) {
+      xof_slow_one<Fp128>(p, in, sc, r0 + i);
+      query_h_body<2, PP, 1, 3, 0, false>(p, in, sc, out, r0 + i);
+    }
+}
+
 static int launch_slow_redo(prio3_engine* e, const DevParams& base, uint32_t n, InPtrs in,
                             OutPtrs out, Scratch sc, hipStream_t st) {
   DevParams dp = base;
@@ -3057,16 +3079,14 @@ static int launch_slow_redo(prio3_engine* e, const DevParams& base, uint32_t n, 
   dp.msg_cmp = e->msg_cmp ? 1u : 0u;
   dp.trunc_xof = 0;
   dp.slow_defer = 1;
-  dp.redo = 0;
-  TIMED(e, st, "k_xof_slow", launch_xof_slow<Fp128>(e, dp, in, sc, st));
   dp.redo = 1;
-  const uint32_t blocks = (n + 255) / 256;
+  const uint32_t g = slow_blocks(n);
   if (dp.P == 32)
-    TIMED(e, st, "k_query_redo", (k_query_h<2, 32><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+    TIMED(e, st, "k_slow_redo", (k_slow_redo<32><<<g, 64, 0, st>>>(dp, in, sc, out)));
   else if (dp.P == 16)
-    TIMED(e, st, "k_query_redo", (k_query_h<2, 16><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+    TIMED(e, st, "k_slow_redo", (k_slow_redo<16><<<g, 64, 0, st>>>(dp, in, sc, out)));
   else
-    TIMED(e, st, "k_query_redo", (k_query_h<2, 8><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+    TIMED(e, st, "k_slow_redo", (k_slow_redo<8><<<g, 64, 0, st>>>(dp, in, sc, out)));
   return PRIO3_OK;
 }
 
