@@ -31,6 +31,7 @@
 #include "prio3_device.h"
 
 #include "prio3_common.h"
+#include "prio3_query_sum.h"
 #include "prio3_runtime.h"
 #include "sha256_device.h"
 #include "sha256_host.h"
@@ -1476,6 +1477,16 @@ __global__ __launch_bounds__(256, 3) void k_prep_h(DevParams p, InPtrs in, Scrat
   query_h_body<2, 32, 1, 3, 0, false>(p, in, sc, out, r);
 }
 
+// k_prep_sum<NPH>: the same for Prio3Sum (P = 16 NPH): the dual-state XOF and k_query_sum's body
+// (prio3_query_sum.h) on the same wave, flagged reports deferred to the run's redo launch
+template <int NPH>
+__global__ __launch_bounds__(256, 3) void k_prep_sum(DevParams p, InPtrs in, Scratch sc,
+                                                     OutPtrs out) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  xofd_body<false, false>(p, in, sc, r);
+  qsum::query_sum_body<NPH, 0>(p, in, sc, out, r);
+}
+
 
 
 
@@ -2836,6 +2847,9 @@ static bool prep_fused_takes(const prio3_engine* e, const DevParams& dp, bool fu
                     (42 + dp.meas_len * 16) / 168 >= 2;
   const bool wide = ps && e->qwide && !(e->qpair && (dp.P == 32 || dp.P == 16)) &&
                     (dp.P != 32 || e->qwide32) && query_wide_takes(dp);
+  if (e->prep_fused && e->slow_defer && dp.kind == PRIO3_SUM && dual && !fuse &&
+      e->xof_pair <= 0 && e->qsum && e->qsum_occ == 3 && query_sum_takes(dp))
+    return true;  // k_prep_sum
   return e->prep_fused && e->slow_defer && dp.kind != PRIO3_FPVEC_BOUNDED_L2 && ps && dual &&
          !wide && dp.P == 32 && !(fuse && e->fuse_q) && !(!fuse && e->xof_pair > 0) &&
          !e->qh_regs && !e->qpair && !e->qrows && e->qh_prefetch == 1 && e->qh_occ == 3;
@@ -2965,7 +2979,19 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
     // chunk) instead of k_xofd
     const bool fuseq = fuse && e->fuse_q && dual && ps && !wide && dp.P == 32 &&
                        (dp.chunk & 1u) == 0 && !e->qh_regs && !e->qpair;
-    // option prep_fused (default): XOF + query of Histogram P = 32 in one launch (k_prep_h)
+    // option prep_fused (default): XOF + query in one launch -- Prio3Sum (k_prep_sum) and
+    // Histogram / SumVec with P = 32 (k_prep_h)
+    if (!paired && dp.kind == PRIO3_SUM && prep_fused_takes(e, dp, fuse)) {
+      dp.slow_defer = 1u;
+      if (deferred) *deferred = true;
+      switch (dp.P) {
+        case 16: TIMED(e, st, "k_prep_sum", (k_prep_sum<1><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
+        case 32: TIMED(e, st, "k_prep_sum", (k_prep_sum<2><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
+        case 64: TIMED(e, st, "k_prep_sum", (k_prep_sum<4><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
+        default: TIMED(e, st, "k_prep_sum", (k_prep_sum<8><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
+      }
+      return PRIO3_OK;
+    }
     if (!paired && prep_fused_takes(e, dp, fuse)) {
       dp.slow_defer = 1u;
       if (deferred) *deferred = true;
@@ -3071,6 +3097,27 @@ __global__ __launch_bounds__(64) void k_slow_redo(DevParams p, InPtrs in, Scratc
     }
 }
 
+template <int NPH>
+__global__ __launch_bounds__(64) void k_slow_redo_sum(DevParams p, InPtrs in, Scratch sc,
+                                                      OutPtrs out) {
+  const uint32_t r0 = (blockIdx.x * blockDim.x + threadIdx.x) * 16u;
+  if (r0 >= p.n) return;
+  const uint8_t* fl = sc.flag + r0;
+  uint32_t any = 0;
+  if (r0 + 16 <= p.n && ((uintptr_t)fl & 15) == 0) {
+    const uint4 v = *(const uint4*)fl;
+    any = v.x | v.y | v.z | v.w;
+  } else {
+    for (uint32_t i = 0; i < 16 && r0 + i < p.n; i++) any |= fl[i];
+  }
+  if (!any) return;
+  for (uint32_t i = 0; i < 16 && r0 + i < p.n; i++)
+    if (fl[i]) {
+      xof_slow_one<Fp128>(p, in, sc, r0 + i);
+      qsum::query_sum_body<NPH, 0>(p, in, sc, out, r0 + i);
+    }
+}
+
 static int launch_slow_redo(prio3_engine* e, const DevParams& base, uint32_t n, InPtrs in,
                             OutPtrs out, Scratch sc, hipStream_t st) {
   DevParams dp = base;
@@ -3081,7 +3128,14 @@ static int launch_slow_redo(prio3_engine* e, const DevParams& base, uint32_t n, 
   dp.slow_defer = 1;
   dp.redo = 1;
   const uint32_t g = slow_blocks(n);
-  if (dp.P == 32)
+  if (dp.kind == PRIO3_SUM) {
+    switch (dp.P) {
+      case 16: TIMED(e, st, "k_slow_redo", (k_slow_redo_sum<1><<<g, 64, 0, st>>>(dp, in, sc, out))); break;
+      case 32: TIMED(e, st, "k_slow_redo", (k_slow_redo_sum<2><<<g, 64, 0, st>>>(dp, in, sc, out))); break;
+      case 64: TIMED(e, st, "k_slow_redo", (k_slow_redo_sum<4><<<g, 64, 0, st>>>(dp, in, sc, out))); break;
+      default: TIMED(e, st, "k_slow_redo", (k_slow_redo_sum<8><<<g, 64, 0, st>>>(dp, in, sc, out))); break;
+    }
+  } else if (dp.P == 32)
     TIMED(e, st, "k_slow_redo", (k_slow_redo<32><<<g, 64, 0, st>>>(dp, in, sc, out)));
   else if (dp.P == 16)
     TIMED(e, st, "k_slow_redo", (k_slow_redo<16><<<g, 64, 0, st>>>(dp, in, sc, out)));

@@ -329,3 +329,13 @@ def test_fused_prepare_kernel_parity(name, opts):
     _check_against_oracle(CONFIGS[name], 777, seed=83, opts=opts)
 
 
+
+
+@pytest.mark.parametrize("opts", [{}, {"prep_fused": 0}, {"chunks": 3}])
+@pytest.mark.parametrize("name", ["sum8", "sum15", "sum32", "sum50", "sum64"])
+def test_fused_sum_prepare_parity(name, opts):
+    """Prio3Sum (P = 16..128) with the XOF and k_query_sum's body in one launch (k_prep_sum, the
+    default; one chunk or three), and the two-kernel chain, on tampered ragged batches; every
+    report through the deferred slow path (k_slow_redo_sum)."""
+    _check_against_oracle(CONFIGS[name], 555, seed=89, opts=opts)
+    _check_against_oracle(CONFIGS[name], 130, seed=90, force_slow=True, opts=opts)
