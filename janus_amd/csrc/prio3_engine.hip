@@ -2855,11 +2855,13 @@ static bool prep_fused_takes(const prio3_engine* e, const DevParams& dp, bool fu
          !e->qh_regs && !e->qpair && !e->qrows && e->qh_prefetch == 1 && e->qh_occ == 3;
 }
 
+// which query family deferred the slow path of its flagged reports (launch_slow_redo redoes them)
+enum : int { DEFER_NONE = 0, DEFER_QH = 1, DEFER_SUM = 2 };
 // *deferred: set when a query kernel of this chain skipped flagged reports (slow_defer); the
 // caller then ends the run with launch_slow_redo
 static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, uint32_t n,
                           InPtrs in, OutPtrs out, Scratch sc, hipStream_t st, bool fuse,
-                          bool* deferred) {
+                          int* deferred) {
   DevParams dp = base;
   dp.n = n;
   dp.force_slow = (uint32_t)e->force_slow;
@@ -2983,7 +2985,7 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
     // Histogram / SumVec with P = 32 (k_prep_h)
     if (!paired && dp.kind == PRIO3_SUM && prep_fused_takes(e, dp, fuse)) {
       dp.slow_defer = 1u;
-      if (deferred) *deferred = true;
+      if (deferred) *deferred = DEFER_SUM;
       switch (dp.P) {
         case 16: TIMED(e, st, "k_prep_sum", (k_prep_sum<1><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
         case 32: TIMED(e, st, "k_prep_sum", (k_prep_sum<2><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
@@ -2994,7 +2996,7 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
     }
     if (!paired && prep_fused_takes(e, dp, fuse)) {
       dp.slow_defer = 1u;
-      if (deferred) *deferred = true;
+      if (deferred) *deferred = DEFER_QH;
       if (fuse)
         TIMED(e, st, "k_prep_h", (k_prep_h<true><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
       else
@@ -3025,7 +3027,7 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
                          (dp.P == 32 || dp.P == 16 || dp.P == 8) &&
                          !(dp.P == 32 && dp.chunk == 16 && dp.calls == 16 && e->qh_regs);
     dp.slow_defer = qh_path && !fuseq && e->slow_defer ? 1u : 0u;
-    if (dp.slow_defer && deferred) *deferred = true;
+    if (dp.slow_defer && deferred) *deferred = DEFER_QH;
     if (!dp.slow_defer) TIMED(e, st, "k_xof_slow", launch_xof_slow<Fp128>(e, dp, in, sc, st));
     bool done = false;
     if (ps && e->qpair && (dp.P == 32 || dp.P == 16)) {
@@ -3119,7 +3121,7 @@ __global__ __launch_bounds__(64) void k_slow_redo_sum(DevParams p, InPtrs in, Sc
 }
 
 static int launch_slow_redo(prio3_engine* e, const DevParams& base, uint32_t n, InPtrs in,
-                            OutPtrs out, Scratch sc, hipStream_t st) {
+                            OutPtrs out, Scratch sc, hipStream_t st, int family) {
   DevParams dp = base;
   dp.n = n;
   dp.force_slow = (uint32_t)e->force_slow;
@@ -3128,7 +3130,7 @@ static int launch_slow_redo(prio3_engine* e, const DevParams& base, uint32_t n, 
   dp.slow_defer = 1;
   dp.redo = 1;
   const uint32_t g = slow_blocks(n);
-  if (dp.kind == PRIO3_SUM) {
+  if (family == DEFER_SUM) {
     switch (dp.P) {
       case 16: TIMED(e, st, "k_slow_redo", (k_slow_redo_sum<1><<<g, 64, 0, st>>>(dp, in, sc, out))); break;
       case 32: TIMED(e, st, "k_slow_redo", (k_slow_redo_sum<2><<<g, 64, 0, st>>>(dp, in, sc, out))); break;
@@ -3164,10 +3166,11 @@ static int prepare_run(prio3_engine* e, Run* R, InPtrs in, OutPtrs out, hipStrea
                      : prep_fused_takes(e, R->dp, fuse) ? 1u
                                                         : std::max(1u, (n + (1u << 16)) >> 17);
   const uint32_t csz = ((n + K - 1) / K + 255) & ~255u;
-  bool deferred = false;
+  int deferred = DEFER_NONE;
   if (!allow_chunks || K == 1 || n <= csz || R->dp.kind == PRIO3_FPVEC_BOUNDED_L2) {
     const int rc = launch_prepare(e, R->dp, 0, n, in, out, sc, st, fuse, &deferred);
-    if (rc == PRIO3_OK && deferred) return launch_slow_redo(e, R->dp, n, in, out, sc, st);
+    if (rc == PRIO3_OK && deferred)
+      return launch_slow_redo(e, R->dp, n, in, out, sc, st, deferred);
     return rc;
   }
   int rc = ensure_side_streams(e);
@@ -3184,7 +3187,7 @@ static int prepare_run(prio3_engine* e, Run* R, InPtrs in, OutPtrs out, hipStrea
     HIPCHK(hipEventRecord(e->side_ev[i], e->side[i]));
     HIPCHK(hipStreamWaitEvent(st, e->side_ev[i], 0));
   }
-  if (deferred) return launch_slow_redo(e, R->dp, n, in, out, sc, st);
+  if (deferred) return launch_slow_redo(e, R->dp, n, in, out, sc, st, deferred);
   return PRIO3_OK;
 }
 

@@ -339,3 +339,13 @@ def test_fused_sum_prepare_parity(name, opts):
     report through the deferred slow path (k_slow_redo_sum)."""
     _check_against_oracle(CONFIGS[name], 555, seed=89, opts=opts)
     _check_against_oracle(CONFIGS[name], 130, seed=90, force_slow=True, opts=opts)
+
+
+@pytest.mark.parametrize("opts", [{}, {"prep_fused": 0}, {"chunks": 3}])
+@pytest.mark.parametrize("name", ["sumvec_8x1000_c63", "sumvec_4x100_c10", "sumvec_32x20_c7"])
+def test_sumvec_wide_prepare_options_parity(name, opts):
+    """SumVec on the eight-lane query (P = 64 / 128): the two-kernel chain (its XOF truncating on
+    the fly), under every launch option, with every report through the slow path."""
+    n = 101 if "1000" in name else 333
+    _check_against_oracle(CONFIGS[name], n, seed=93, opts=opts)
+    _check_against_oracle(CONFIGS[name], 70, seed=94, force_slow=True, opts=opts)
