@@ -40,8 +40,9 @@
 #define XOFD_OCC 3
 #endif
 template <class F>
-__global__ __launch_bounds__(256, XOFD_OCC) void k_xof(DevParams p, InPtrs in, Scratch sc) {
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void xof_body(const DevParams& p, const InPtrs& in, const Scratch& sc,
+                                         const uint32_t r) {
+  // r: this lane's report
   if (r >= p.n) return;
   constexpr uint32_t ES = F::ES;
   uint32_t flag = p.force_slow;
@@ -206,6 +207,10 @@ __global__ __launch_bounds__(256, XOFD_OCC) void k_xof(DevParams p, InPtrs in, S
     sc.corrected[r] = make_uint4(cor[0], cor[1], cor[2], cor[3]);
   }
   sc.flag[r] = (uint8_t)flag;
+}
+template <class F>
+__global__ __launch_bounds__(256, XOFD_OCC) void k_xof(DevParams p, InPtrs in, Scratch sc) {
+  xof_body<F>(p, in, sc, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 
@@ -901,10 +906,16 @@ static void launch_xof_slow(const prio3_engine* e, const DevParams& p, const InP
 // k_query: FLP query + decide + prepare message + prepare_next + truncate
 // ------------------------------------------------------------------------------------
 template <class F>
-__global__ __launch_bounds__(256) void k_query(DevParams p, InPtrs in, Scratch sc, OutPtrs out) {
+__device__ __forceinline__ void query_body(const DevParams& p, const InPtrs& in, const Scratch& sc,
+                                           const OutPtrs& out, const uint32_t r) {
   typedef typename F::T T;
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  // r: this lane's report; slow_defer / redo (DevParams) as in query_h_body
   if (r >= p.n) return;
+  if (p.redo) {
+    if (sc.flag[r] != 2) return;
+  } else if (p.slow_defer && sc.flag[r]) {
+    return;
+  }
   const size_t ld = p.ld;
   const uint32_t A = p.arity;
   uint8_t status = PRIO3_STATUS_FINISHED;
@@ -990,6 +1001,19 @@ __global__ __launch_bounds__(256) void k_query(DevParams p, InPtrs in, Scratch s
       F::store(sc.out, (size_t)e * ld + r, acc);
     }
   }
+}
+template <class F>
+__global__ __launch_bounds__(256) void k_query(DevParams p, InPtrs in, Scratch sc, OutPtrs out) {
+  query_body<F>(p, in, sc, out, blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// k_prep_gen<F>: the generic XOF and query of one report on one lane in one launch (Prio3Count,
+// C1), the slow path deferred to the run's redo launch, as k_prep_h
+template <class F>
+__global__ __launch_bounds__(256) void k_prep_gen(DevParams p, InPtrs in, Scratch sc, OutPtrs out) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  xof_body<F>(p, in, sc, r);
+  query_body<F>(p, in, sc, out, r);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2856,7 +2880,7 @@ static bool prep_fused_takes(const prio3_engine* e, const DevParams& dp, bool fu
 }
 
 // which query family deferred the slow path of its flagged reports (launch_slow_redo redoes them)
-enum : int { DEFER_NONE = 0, DEFER_QH = 1, DEFER_SUM = 2 };
+enum : int { DEFER_NONE = 0, DEFER_QH = 1, DEFER_SUM = 2, DEFER_GEN64 = 3 };
 // *deferred: set when a query kernel of this chain skipped flagged reports (slow_defer); the
 // caller then ends the run with launch_slow_redo
 static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, uint32_t n,
@@ -3061,6 +3085,10 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
         TIMED(e, st, "k_query_sum", (qs = launch_query_sum(dp, in, sc, out, st, e->qsum_occ)));
       if (!qs) TIMED(e, st, "k_query", (k_query<Fp128><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
     }
+  } else if (e->prep_fused && e->slow_defer) {  // Field64 (Prio3Count): one launch
+    dp.slow_defer = 1u;
+    if (deferred) *deferred = DEFER_GEN64;
+    TIMED(e, st, "k_prep_gen", (k_prep_gen<Fp64><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
   } else {
     TIMED(e, st, "k_xof", (k_xof<Fp64><<<blocks, 256, 0, st>>>(dp, in, sc)));
     TIMED(e, st, "k_xof_slow", launch_xof_slow<Fp64>(e, dp, in, sc, st));
@@ -3130,7 +3158,13 @@ static int launch_slow_redo(prio3_engine* e, const DevParams& base, uint32_t n, 
   dp.slow_defer = 1;
   dp.redo = 1;
   const uint32_t g = slow_blocks(n);
-  if (family == DEFER_SUM) {
+  if (family == DEFER_GEN64) {  // k_prep_gen<Fp64>: XOF redo, then the generic query
+    dp.redo = 0;
+    TIMED(e, st, "k_slow_redo", launch_xof_slow<Fp64>(e, dp, in, sc, st));
+    dp.redo = 1;
+    TIMED(e, st, "k_slow_redo",
+          (k_query<Fp64><<<(n + 255) / 256, 256, 0, st>>>(dp, in, sc, out)));
+  } else if (family == DEFER_SUM) {
     switch (dp.P) {
       case 16: TIMED(e, st, "k_slow_redo", (k_slow_redo_sum<1><<<g, 64, 0, st>>>(dp, in, sc, out))); break;
       case 32: TIMED(e, st, "k_slow_redo", (k_slow_redo_sum<2><<<g, 64, 0, st>>>(dp, in, sc, out))); break;

@@ -124,8 +124,8 @@ def test_concurrent_jobs_of_several_tasks_are_coalesced(name):
         np.testing.assert_array_equal(msgs, rm)
         np.testing.assert_array_equal(agg, ra)
         np.testing.assert_array_equal(cnt, rc)
-    # Histogram(256, 16) (P = 32) runs its XOF and query in one launch (k_prep_h)
-    kern = {"count": "k_xof", "hist_256_c16": "k_prep_h"}.get(name, "k_xofd")
+    # Histogram(256, 16) (P = 32) and Count run their XOF and query in one launch
+    kern = {"count": "k_prep_gen", "hist_256_c16": "k_prep_h"}.get(name, "k_xofd")
     launches = sum(e.timing().get(kern, (0, 0))[1] for e in engines)
     assert 0 < launches < 24, launches
 

@@ -349,3 +349,11 @@ def test_sumvec_wide_prepare_options_parity(name, opts):
     n = 101 if "1000" in name else 333
     _check_against_oracle(CONFIGS[name], n, seed=93, opts=opts)
     _check_against_oracle(CONFIGS[name], 70, seed=94, force_slow=True, opts=opts)
+
+
+@pytest.mark.parametrize("opts", [{}, {"prep_fused": 0}, {"chunks": 3}])
+def test_fused_count_prepare_parity(opts):
+    """Prio3Count (Field64) with the generic XOF and query in one launch (k_prep_gen, the default)
+    and on two kernels, on a tampered ragged batch and with every report on the slow path."""
+    _check_against_oracle(CONFIGS["count"], 999, seed=95, opts=opts)
+    _check_against_oracle(CONFIGS["count"], 130, seed=96, force_slow=True, opts=opts)
