@@ -588,6 +588,7 @@ struct HpkeParams {
   uint32_t aead;                // AEAD id (1, 2, 3): selects the kernel instance
   uint32_t kem;                 // KEM id (0x20 X25519, 0x10 P-256)
   uint8_t pk65[68];             // P-256: pkRm, the 65-byte uncompressed point (kem_context)
+  int8_t p256_dig[88];          // P-256: signed window digits of the private key (p256_recode)
 };
 
 struct OpenArgs {
@@ -681,7 +682,7 @@ __global__ __launch_bounds__(256) void k_hpke_open(HpkeParams P, OpenArgs a) {
   } else {
     const uint8_t* ep = a.enc + 65 * (size_t)r;
     uint32_t dh[8];  // x-coordinate, big-endian words
-    ok = p256::ecdh(P.sk, ep, dh);
+    ok = p256::ecdh(P.p256_dig, ep, dh);
     {  // eae_prk = LabeledExtract("", "eae_prk", dh)
       Msg32<16> m;
       mz(m);
@@ -1086,6 +1087,36 @@ uint32_t le32(const uint8_t* p) {
 
 }  // namespace
 
+// Regular signed window recoding (w = 3) of a P-256 private key for p256::ecdh: k' = sk when sk
+// is odd, else n - sk (same x-coordinate of k'P), then 85 digits d = (k' mod 16) - 8 (odd, in
+// [-7, 7]) with k' <- (k' - d) / 8, which stays odd, and the remaining k' in {1, 3} on top.
+static void p256_recode(const uint32_t sk[8], int8_t dig[88]) {
+  uint32_t k[8];
+  memcpy(k, sk, sizeof(k));
+  if (!(k[0] & 1u)) {
+    int64_t br = 0;
+    for (int i = 0; i < 8; i++) {
+      const uint32_t ni = be32(kP256N + 4 * (7 - i));
+      const int64_t t = (int64_t)ni - k[i] + br;
+      k[i] = (uint32_t)t;
+      br = t >> 32;
+    }
+  }
+  for (int i = 0; i < 85; i++) {
+    const int d = (int)(k[0] & 15u) - 8;
+    dig[i] = (int8_t)d;
+    int64_t c = -(int64_t)d;  // k -= d
+    for (int j = 0; j < 8; j++) {
+      const int64_t t = (int64_t)k[j] + c;
+      k[j] = (uint32_t)t;
+      c = t >> 32;
+    }
+    for (int j = 0; j < 8; j++) k[j] = k[j] >> 3 | (j < 7 ? k[j + 1] << 29 : 0u);
+  }
+  dig[85] = (int8_t)k[0];
+  dig[86] = dig[87] = 0;
+}
+
 struct janus_hpke_opener {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -1147,6 +1178,7 @@ int janus_hpke_opener_create(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id,
   } else {
     for (int i = 0; i < 8; i++) o->P.sk[i] = be32(private_key + 4 * (7 - i));  // LE limbs
     memcpy(o->P.pk65, public_key, 65);
+    p256_recode(o->P.sk, o->P.p256_dig);
   }
   // key_schedule_context = mode_base || LabeledExtract("", "psk_id_hash", "") ||
   //                        LabeledExtract("", "info_hash", info)        (RFC 9180 5.1)

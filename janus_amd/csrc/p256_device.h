@@ -7,15 +7,20 @@
 // NIST fast reduction (FIPS 186-4 D.2.3: s1 + 2 s2 + 2 s3 + s4 + s5 - s6 - s7 - s8 - s9) in
 // signed 64-bit word sums, whose carry out of 2^256 folds back as 2^256 = 2^224 - 2^192 - 2^96 + 1
 // (mod p); three carry passes always leave [0, 2^256).
-// The scalar is the server's private key, the same in every lane: a left-to-right ladder over
-// its (wave-uniform) bits that doubles and adds (mixed Jacobian, a = -3) every step and keeps
-// the sum only where the bit is set, so every key runs the same instruction stream.
+// The scalar is the server's private key, the same in every lane: a fixed signed window (w = 3)
+// over its host-side recoding, so every key runs the same instruction stream (see ecdh).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #ifndef DEV
 #define DEV __device__ __forceinline__
+#endif
+#ifndef P256_ASM
+#define P256_ASM 1  // 1: the generated single-asm-statement products (p256_asm.h)
+#endif
+#if P256_ASM
+#include "p256_asm.h"  // mul512 / sqr512 (generated: tools/gen_p256_asm.py)
 #endif
 
 namespace p256 {
@@ -68,9 +73,27 @@ DEV fp mul_small(const fp& a, uint32_t k) {  // k <= 8
   return fold(t);
 }
 
+// NIST fast reduction of a 512-bit product c[0..15] (FIPS 186-4 D.2.3 as signed word sums)
+DEV fp reduce(const uint32_t c[16]) {
+  typedef int64_t s;
+  int64_t t[8];
+  t[0] = (s)c[0] + c[8] + c[9] - (s)c[11] - c[12] - c[13] - c[14];
+  t[1] = (s)c[1] + c[9] + c[10] - (s)c[12] - c[13] - c[14] - c[15];
+  t[2] = (s)c[2] + c[10] + c[11] - (s)c[13] - c[14] - c[15];
+  t[3] = (s)c[3] + 2 * (s)c[11] + 2 * (s)c[12] + c[13] - (s)c[15] - c[8] - c[9];
+  t[4] = (s)c[4] + 2 * (s)c[12] + 2 * (s)c[13] + c[14] - (s)c[9] - c[10];
+  t[5] = (s)c[5] + 2 * (s)c[13] + 2 * (s)c[14] + c[15] - (s)c[10] - c[11];
+  t[6] = (s)c[6] + 3 * (s)c[14] + 2 * (s)c[15] + c[13] - (s)c[8] - c[9];
+  t[7] = (s)c[7] + 3 * (s)c[15] + c[8] - (s)c[10] - c[11] - c[12] - c[13];
+  return fold(t);
+}
+
 // out of line: ~20 call sites in the point formulas (compile time, code size)
 __device__ __noinline__ fp mul(const fp& a, const fp& b) {
   uint32_t c[16];
+#if P256_ASM
+  mul512(a.v, b.v, c);
+#else
 #pragma unroll
   for (int i = 0; i < 16; i++) c[i] = 0;
 #pragma unroll
@@ -84,19 +107,47 @@ __device__ __noinline__ fp mul(const fp& a, const fp& b) {
     }
     c[i + 8] = (uint32_t)carry;
   }
-  typedef int64_t s;
-  int64_t t[8];
-  t[0] = (s)c[0] + c[8] + c[9] - (s)c[11] - c[12] - c[13] - c[14];
-  t[1] = (s)c[1] + c[9] + c[10] - (s)c[12] - c[13] - c[14] - c[15];
-  t[2] = (s)c[2] + c[10] + c[11] - (s)c[13] - c[14] - c[15];
-  t[3] = (s)c[3] + 2 * (s)c[11] + 2 * (s)c[12] + c[13] - (s)c[15] - c[8] - c[9];
-  t[4] = (s)c[4] + 2 * (s)c[12] + 2 * (s)c[13] + c[14] - (s)c[9] - c[10];
-  t[5] = (s)c[5] + 2 * (s)c[13] + 2 * (s)c[14] + c[15] - (s)c[10] - c[11];
-  t[6] = (s)c[6] + 3 * (s)c[14] + 2 * (s)c[15] + c[13] - (s)c[8] - c[9];
-  t[7] = (s)c[7] + 3 * (s)c[15] + c[8] - (s)c[10] - c[11] - c[12] - c[13];
-  return fold(t);
+#endif
+  return reduce(c);
 }
-DEV fp sqr(const fp& a) { return mul(a, a); }
+
+// a^2 with 36 word products instead of 64: the 28 cross products once, doubled by a one-bit
+// shift, plus the 8 squares on the diagonal
+__device__ __noinline__ fp sqr(const fp& a) {
+  uint32_t c[16];
+#if P256_ASM
+  sqr512(a.v, c);
+#else
+#pragma unroll
+  for (int i = 0; i < 16; i++) c[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 7; i++) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = i + 1; j < 8; j++) {
+      const uint64_t x = (uint64_t)a.v[i] * a.v[j] + c[i + j] + carry;
+      c[i + j] = (uint32_t)x;
+      carry = x >> 32;
+    }
+    c[i + 8] = (uint32_t)carry;
+  }
+  uint32_t top = 0;  // the bit shifted out of the previous word pair
+  uint64_t cy = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t e = c[2 * i], o = c[2 * i + 1];
+    const uint32_t d0 = e << 1 | top, d1 = o << 1 | e >> 31;
+    top = o >> 31;
+    const uint64_t sq = (uint64_t)a.v[i] * a.v[i];
+    const uint64_t t0 = (uint64_t)d0 + (uint32_t)sq + cy;
+    const uint64_t t1 = (uint64_t)d1 + (sq >> 32) + (t0 >> 32);
+    c[2 * i] = (uint32_t)t0;
+    c[2 * i + 1] = (uint32_t)t1;
+    cy = t1 >> 32;
+  }
+#endif
+  return reduce(c);
+}
 
 // canonical representative in [0, p)
 DEV fp freeze(const fp& a) {
@@ -185,30 +236,81 @@ DEV jac madd(const jac& P, const fp& x2, const fp& y2) {
   return R;
 }
 
+DEV fp neg(const fp& a) { return sub(fp{{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}}, a); }
+
+// Jacobian -> affine for three points with one inversion (Montgomery's trick)
+DEV void to_affine3(const jac& A, const jac& B, const jac& C, fp& ax, fp& ay, fp& bx, fp& by,
+                    fp& cx, fp& cy) {
+  const fp ab = mul(A.Z, B.Z), abc = mul(ab, C.Z), i = inv(abc);
+  const fp ic = mul(i, ab), iab = mul(i, C.Z), ia = mul(iab, B.Z), ib = mul(iab, A.Z);
+  const fp ia2 = sqr(ia), ib2 = sqr(ib), ic2 = sqr(ic);
+  ax = mul(A.X, ia2);
+  ay = mul(A.Y, mul(ia2, ia));
+  bx = mul(B.X, ib2);
+  by = mul(B.Y, mul(ib2, ib));
+  cx = mul(C.X, ic2);
+  cy = mul(C.Y, mul(ic2, ic));
+}
+
+// Digits of the regular signed window recoding (w = 3) of the private key, computed on the host
+// (hpke.hip p256_recode): k' = sk if sk is odd, else n - sk (x(k'P) = x(-sk P) = x(sk P)), and
+// k' = sum_i d_i 8^i with every d_i odd in [-7, 7], d_85 in {1, 3}.
+constexpr int kDigits = 86;
+
 // DH(sk, pkE) for an uncompressed SEC1 point enc = 0x04 || X || Y (65 bytes): validates the
 // point (prefix, canonical coordinates, y^2 = x^3 - 3x + b) and writes the shared x-coordinate
-// as 8 big-endian words (its 32-byte encoding, RFC 9180 7.1.1).  sk: LE limbs, 1 <= sk < n.
-DEV bool ecdh(const uint32_t sk[8], const uint8_t* enc, uint32_t dh_be[8]) {
+// as 8 big-endian words (its 32-byte encoding, RFC 9180 7.1.1).
+// Fixed window over the recoded key: a table of P, 3P, 5P, 7P (affine, one shared inversion),
+// then 85 x (three doublings + one mixed addition of +-table[|d|]).  The digits are the same in
+// every lane (one server key), and every key runs the same instruction stream: 85 windows, the
+// table entry picked by selects, not by an indexed load.
+// The additions never meet the doubling case R = +-T except, for k' in {n - 2, n - 6, n - 10,
+// n - 14}, at the last window (8 k_1 = k' - d_0 = d_0 mod n); there madd returns Z = 0 and the
+// doubled R, computed beside it for every key, is the sum.
+DEV bool ecdh(const int8_t* dig, const uint8_t* enc, uint32_t dh_be[8]) {
   constexpr fp B = {{0x27d2604bu, 0x3bce3c3eu, 0xcc53b0f6u, 0x651d06b0u, 0x769886bcu, 0xb3ebbd55u,
                      0xaa3a93e7u, 0x5ac635d8u}};
+  constexpr fp ONE = {{1u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}};
   fp x, y;
   bool ok = enc[0] == 0x04;
   ok = from_be(enc + 1, x) && ok;
   ok = from_be(enc + 33, y) && ok;
   const fp rhs = add(sub(mul(sqr(x), x), mul_small(x, 3)), B);
   ok = ok && eq(sqr(y), rhs);
-  // left-to-right: R = P at the top set bit, then double, add, keep the sum where the bit is 1
-  int top = 255;
-  while (top > 0 && !((sk[top >> 5] >> (top & 31)) & 1u)) top--;  // wave-uniform
+  // odd multiples: 3P = 2P + P, 5P = 4P + P, 7P = 8P - P
+  fp x3, y3, x5, y5, x7, y7;
+  {
+    const jac P2 = dbl(jac{x, y, ONE});
+    const jac P4 = dbl(P2);
+    to_affine3(madd(P2, x, y), madd(P4, x, y), madd(dbl(P4), x, neg(y)), x3, y3, x5, y5, x7, y7);
+  }
+  auto pick = [&](int d, fp& tx, fp& ty) {
+    const int a = d < 0 ? -d : d;
+#pragma unroll
+    for (int w = 0; w < 8; w++) {
+      tx.v[w] = a == 1 ? x.v[w] : a == 3 ? x3.v[w] : a == 5 ? x5.v[w] : x7.v[w];
+      ty.v[w] = a == 1 ? y.v[w] : a == 3 ? y3.v[w] : a == 5 ? y5.v[w] : y7.v[w];
+    }
+    const fp ny = neg(ty);
+    if (d < 0) ty = ny;
+  };
   jac R;
-  R.X = x;
-  R.Y = y;
-  R.Z = fp{{1u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}};
+  pick(dig[kDigits - 1], R.X, R.Y);
+  R.Z = ONE;
 #pragma unroll 1
-  for (int i = top - 1; i >= 0; i--) {
-    R = dbl(R);
-    const jac T = madd(R, x, y);
-    if ((sk[i >> 5] >> (i & 31)) & 1u) R = T;  // wave-uniform: every key bit costs the same
+  for (int i = kDigits - 2; i >= 1; i--) {
+    R = dbl(dbl(dbl(R)));
+    fp tx, ty;
+    pick(dig[i], tx, ty);
+    R = madd(R, tx, ty);
+  }
+  R = dbl(dbl(dbl(R)));
+  {
+    fp tx, ty;
+    pick(dig[0], tx, ty);
+    const jac D = dbl(R);
+    const jac S = madd(R, tx, ty);
+    R = is_zero(S.Z) ? D : S;
   }
   ok = ok && !is_zero(R.Z);
   const fp zi = inv(R.Z);

@@ -294,3 +294,27 @@ def test_gpu_p256_input_shares_match_oracle(aead, n, pub, tamper):
                                   d["times"], d["pubs"], 48)
     np.testing.assert_array_equal(st, ref_st)
     np.testing.assert_array_equal(sh, ref_sh)
+
+
+P256_N = 0xffffffff00000000ffffffffffffffffbce6faada7179e84f3b9cac2fc632551
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sk", [1, 2, 3, 6, 14, P256_N - 1, P256_N - 2, P256_N - 6, P256_N - 14,
+                                P256_N - 15, 2 ** 255, 0x1234567 << 200])
+def test_gpu_p256_edge_private_keys(sk):
+    """The fixed signed window (p256_device.h ecdh) over the host recoding of the server key:
+    even keys (run as n - sk), the keys whose last window meets the doubling case (n - 2, n - 6,
+    n - 10, n - 14 and the even 2, 6, 10, 14), tiny and near-n keys, against the OpenSSL oracle."""
+    from janus_amd import hpke as G
+    skR = sk.to_bytes(32, "big")
+    d = H.make_batch(8, 48, 32, seed=sk % 997, skR=skR, kem=H.KEM_P256)
+    ref_sh, ref_st = H.open_input_shares(d["skR"], d["pkR"], d["task_id"], d["enc"], d["ct"],
+                                         d["ct_len"], d["report_ids"], d["times"], d["pubs"], 48,
+                                         kem=H.KEM_P256)
+    assert (ref_st == 0).all()
+    op = G.HpkeOpener(d["skR"], d["pkR"], kem_id=G.KEM_P256_HKDF_SHA256)
+    sh, st = op.open_input_shares(d["task_id"], d["enc"], d["ct"], d["ct_len"], d["report_ids"],
+                                  d["times"], d["pubs"], 48)
+    np.testing.assert_array_equal(st, ref_st)
+    np.testing.assert_array_equal(sh, ref_sh)

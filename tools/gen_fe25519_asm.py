@@ -275,12 +275,15 @@ def gen_mul_small():
 """
 
 
-print("""// fe25519_asm.h -- GENERATED by tools/gen_fe25519_asm.py (see its docstring); do not edit.
+HEADER = """// fe25519_asm.h -- GENERATED by tools/gen_fe25519_asm.py (see its docstring); do not edit.
 // GF(2^255 - 19) in 8 x 32-bit limbs, loosely reduced in [0, 2^256), for hpke.hip.
 #pragma once
-""")
-print(gen_mul())
-print(gen_sqr())
-print(gen_add2())
-print(gen_sub())
-print(gen_mul_small())
+"""
+
+if __name__ == "__main__":
+    print(HEADER)
+    print(gen_mul())
+    print(gen_sqr())
+    print(gen_add2())
+    print(gen_sub())
+    print(gen_mul_small())
