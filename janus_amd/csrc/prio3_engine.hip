@@ -1016,6 +1016,30 @@ __global__ __launch_bounds__(256) void k_prep_gen(DevParams p, InPtrs in, Scratc
   query_body<F>(p, in, sc, out, r);
 }
 
+// k_slow_redo_gen<F>: k_prep_gen's deferred slow path in one launch (as k_slow_redo): each lane
+// scans the flags of 16 reports with one load and, for a flagged one, re-runs its XOF on the
+// byte-level sponge (flag := 2) and then its query (p.redo = 1)
+template <class F>
+__global__ __launch_bounds__(64) void k_slow_redo_gen(DevParams p, InPtrs in, Scratch sc,
+                                                      OutPtrs out) {
+  const uint32_t r0 = (blockIdx.x * blockDim.x + threadIdx.x) * 16u;
+  if (r0 >= p.n) return;
+  const uint8_t* fl = sc.flag + r0;
+  uint32_t any = 0;
+  if (r0 + 16 <= p.n && ((uintptr_t)fl & 15) == 0) {
+    const uint4 v = *(const uint4*)fl;
+    any = v.x | v.y | v.z | v.w;
+  } else {
+    for (uint32_t i = 0; i < 16 && r0 + i < p.n; i++) any |= fl[i];
+  }
+  if (!any) return;
+  for (uint32_t i = 0; i < 16 && r0 + i < p.n; i++)
+    if (fl[i]) {
+      xof_slow_one<F>(p, in, sc, r0 + i);
+      query_body<F>(p, in, sc, out, r0 + i);
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // k_query_ps: FLP query + decide for the ParallelSum(Mul, C) circuits (Histogram, SumVec).
 //
@@ -1733,26 +1757,21 @@ __global__ __launch_bounds__(256, 2) void k_query_r(DevParams p, InPtrs in, Scra
 // ------------------------------------------------------------------------------------
 // Accumulate: masked segmented mod-p reduction of output shares
 // ------------------------------------------------------------------------------------
-// Per-report inclusion code: the report's segment if it is counted (status FINISHED, host mask
-// non-zero, segment id < n_segments), else ~0.  A segment id past n_segments excludes the report
-// from every aggregate and count, on every path (fused: k_agg_fix; metadata: k_meta).
-__global__ void k_code(uint32_t n, const uint8_t* status, const uint32_t* seg,
-                       const uint8_t* accept, uint32_t nseg, uint32_t* code) {
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n) return;
-  const uint32_t s = seg ? seg[r] : 0u;
-  const bool ok = status[r] == PRIO3_STATUS_FINISHED && s < nseg && (!accept || accept[r]);
-  code[r] = ok ? s : 0xffffffffu;
-}
+// Per-report inclusion: a report counts in its segment if its status is FINISHED, the host mask
+// is non-zero and its segment id is < n_segments.  A segment id past n_segments excludes the
+// report from every aggregate and count, on every path (fused: k_agg_fix; metadata: k_meta).
 
 // Segmented partial sums in one pass over the output shares.  grid: x = output element, y =
 // report chunk, z = group of SG segments; each thread keeps SG running sums (one per segment of
 // its group) and the block reduces them through LDS into partial[chunk][segment][element]
 // (counts into pcount[chunk][segment] from the element-0 blocks).
+// Inclusion is decided inline (status, segment id, accept mask; no separate code pass), so the
+// accumulate is one launch plus k_acc_fin.
 template <class F, int SG>
 __global__ __launch_bounds__(256) void k_acc_seg(uint32_t n, size_t ld, uint32_t chunk,
                                                  uint32_t out_len, uint32_t nseg, const void* src,
-                                                 const uint32_t* code, void* partial,
+                                                 const uint8_t* status, const uint32_t* seg,
+                                                 const uint8_t* accept, void* partial,
                                                  uint64_t* pcount) {
   typedef typename F::T T;
   __shared__ T red[256];
@@ -1767,7 +1786,9 @@ __global__ __launch_bounds__(256) void k_acc_seg(uint32_t n, size_t ld, uint32_t
     cnt[q] = 0;
   }
   for (uint32_t r = lo + threadIdx.x; r < hi; r += 256) {
-    const uint32_t k = code[r] - s0;  // ~0 (excluded) wraps past SG
+    const uint32_t sr = seg ? seg[r] : 0u;
+    const bool ok = status[r] == PRIO3_STATUS_FINISHED && sr < nseg && (!accept || accept[r]);
+    const uint32_t k = (ok ? sr : 0xffffffffu) - s0;  // ~0 (excluded) wraps past SG
     if (k < (uint32_t)SG) {
       const T x = F::load(src, (size_t)e * ld + r);
 #pragma unroll
@@ -1819,9 +1840,40 @@ __global__ void k_acc_fin(uint32_t nchunks, uint32_t out_len, uint32_t nseg, con
 }
 
 
-// Accumulate of many small batches in one launch (the accumulate executor: concurrent
+// k_acc_fin for the short outputs (Count, Sum: 2048-report chunks, so hundreds of partials per
+// element): grid (out_len, nseg), the block's threads stride over the chunks and reduce in LDS
+template <class F>
+__global__ __launch_bounds__(256) void k_acc_fin_blk(uint32_t nchunks, uint32_t out_len,
+                                                     uint32_t nseg, const void* partial,
+                                                     const uint64_t* pcount, uint8_t* agg,
+                                                     uint64_t* count) {
+  typedef typename F::T T;
+  __shared__ T red[256];
+  __shared__ uint64_t cred[256];
+  const uint32_t e = blockIdx.x, s = blockIdx.y;
+  T acc = F::zero();
+  uint64_t t = 0;
+  for (uint32_t c = threadIdx.x; c < nchunks; c += 256) {
+    acc = F::add(acc, F::load(partial, ((size_t)c * nseg + s) * out_len + e));
+    if (e == 0) t += pcount[(size_t)c * nseg + s];
+  }
+  red[threadIdx.x] = acc;
+  cred[threadIdx.x] = t;
+  __syncthreads();
+  for (uint32_t st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st) {
+      red[threadIdx.x] = F::add(red[threadIdx.x], red[threadIdx.x + st]);
+      cred[threadIdx.x] += cred[threadIdx.x + st];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    F::store(agg, (size_t)s * out_len + e, red[0]);
+    if (e == 0) count[s] = cred[0];
+  }
+}// Accumulate of many small batches in one launch (the accumulate executor: concurrent
 // prio3_accumulate calls of Janus's aggregation jobs).  grid: x = output element, y = job; the
-// block sums its element over the job's reports (inclusion as k_code) into up to 8 segments at
+// block sums its element over the job's reports (inclusion as k_acc_seg) into up to 8 segments at
 // a time and writes the job's aggregate share element and, from element 0, its counts.
 template <class F>
 __global__ __launch_bounds__(256) void k_acc_multi(const AccDesc* descs, uint8_t* base) {
@@ -2775,39 +2827,44 @@ static int run_accumulate(prio3_engine* e, Run* R, uint32_t c0, uint32_t n,
     HIPCHK(hipMemsetAsync(d_counts, 0, 8 * (size_t)nseg, st));
     return PRIO3_OK;
   }
-  const uint32_t chunk = 8192, nchunks = (n + chunk - 1) / chunk;
-  const size_t code_b = ((size_t)4 * n + 255) & ~(size_t)255;
+  // reports per k_acc_seg block: 8192, or 2048 for the short outputs (Count, Sum) whose grid
+  // would otherwise be a few blocks wide
+  const bool short_out = d.out_len <= 4;
+  const uint32_t chunk = short_out ? 2048 : 8192, nchunks = (n + chunk - 1) / chunk;
   const size_t part_b = ((size_t)nchunks * nseg * agg_len + 255) & ~(size_t)255;
   int rc = PRIO3_OK;
-  Slab* tmp = ws_acquire(R->device, code_b + part_b + 8 * (size_t)nchunks * nseg, st, &rc);
+  Slab* tmp = ws_acquire(R->device, part_b + 8 * (size_t)nchunks * nseg, st, &rc);
   if (!tmp) return rc;
-  uint32_t* code = (uint32_t*)tmp->base;
-  void* partial = tmp->base + code_b;
-  uint64_t* pcount = (uint64_t*)(tmp->base + code_b + part_b);
+  void* partial = tmp->base;
+  uint64_t* pcount = (uint64_t*)(tmp->base + part_b);
   const uint8_t* src = (const uint8_t*)(own_out(d) ? R->sc.out : R->sc.meas) + es * c0;
   const size_t ld = d.ld_out;  // output shares: one column per report of the run
   auto body = [&]() -> int {
-    TIMED(e, st, "k_code",
-          (k_code<<<(n + 255) / 256, 256, 0, st>>>(n, d_status, d_seg, d_accept, nseg, code)));
     const int SG = nseg == 1 ? 1 : nseg <= 4 ? 4 : 8;
     dim3 grid(d.out_len, nchunks, (nseg + SG - 1) / SG);
     dim3 gfin((d.out_len + 255) / 256, nseg);
     if (es == 16) {
       if (SG == 1)
-        TIMED(e, st, "k_acc_seg", (k_acc_seg<Fp128, 1><<<grid, 256, 0, st>>>(n, ld, chunk, d.out_len, nseg, src, code, partial, pcount)));
+        TIMED(e, st, "k_acc_seg", (k_acc_seg<Fp128, 1><<<grid, 256, 0, st>>>(n, ld, chunk, d.out_len, nseg, src, d_status, d_seg, d_accept, partial, pcount)));
       else if (SG == 4)
-        TIMED(e, st, "k_acc_seg", (k_acc_seg<Fp128, 4><<<grid, 256, 0, st>>>(n, ld, chunk, d.out_len, nseg, src, code, partial, pcount)));
+        TIMED(e, st, "k_acc_seg", (k_acc_seg<Fp128, 4><<<grid, 256, 0, st>>>(n, ld, chunk, d.out_len, nseg, src, d_status, d_seg, d_accept, partial, pcount)));
       else
-        TIMED(e, st, "k_acc_seg", (k_acc_seg<Fp128, 8><<<grid, 256, 0, st>>>(n, ld, chunk, d.out_len, nseg, src, code, partial, pcount)));
-      TIMED(e, st, "k_acc_fin", (k_acc_fin<Fp128><<<gfin, 256, 0, st>>>(nchunks, d.out_len, nseg, partial, pcount, d_agg, d_counts)));
+        TIMED(e, st, "k_acc_seg", (k_acc_seg<Fp128, 8><<<grid, 256, 0, st>>>(n, ld, chunk, d.out_len, nseg, src, d_status, d_seg, d_accept, partial, pcount)));
+      if (short_out)
+        TIMED(e, st, "k_acc_fin", (k_acc_fin_blk<Fp128><<<dim3(d.out_len, nseg), 256, 0, st>>>(nchunks, d.out_len, nseg, partial, pcount, d_agg, d_counts)));
+      else
+        TIMED(e, st, "k_acc_fin", (k_acc_fin<Fp128><<<gfin, 256, 0, st>>>(nchunks, d.out_len, nseg, partial, pcount, d_agg, d_counts)));
     } else {
       if (SG == 1)
-        TIMED(e, st, "k_acc_seg", (k_acc_seg<Fp64, 1><<<grid, 256, 0, st>>>(n, ld, chunk, d.out_len, nseg, src, code, partial, pcount)));
+        TIMED(e, st, "k_acc_seg", (k_acc_seg<Fp64, 1><<<grid, 256, 0, st>>>(n, ld, chunk, d.out_len, nseg, src, d_status, d_seg, d_accept, partial, pcount)));
       else if (SG == 4)
-        TIMED(e, st, "k_acc_seg", (k_acc_seg<Fp64, 4><<<grid, 256, 0, st>>>(n, ld, chunk, d.out_len, nseg, src, code, partial, pcount)));
+        TIMED(e, st, "k_acc_seg", (k_acc_seg<Fp64, 4><<<grid, 256, 0, st>>>(n, ld, chunk, d.out_len, nseg, src, d_status, d_seg, d_accept, partial, pcount)));
       else
-        TIMED(e, st, "k_acc_seg", (k_acc_seg<Fp64, 8><<<grid, 256, 0, st>>>(n, ld, chunk, d.out_len, nseg, src, code, partial, pcount)));
-      TIMED(e, st, "k_acc_fin", (k_acc_fin<Fp64><<<gfin, 256, 0, st>>>(nchunks, d.out_len, nseg, partial, pcount, d_agg, d_counts)));
+        TIMED(e, st, "k_acc_seg", (k_acc_seg<Fp64, 8><<<grid, 256, 0, st>>>(n, ld, chunk, d.out_len, nseg, src, d_status, d_seg, d_accept, partial, pcount)));
+      if (short_out)
+        TIMED(e, st, "k_acc_fin", (k_acc_fin_blk<Fp64><<<dim3(d.out_len, nseg), 256, 0, st>>>(nchunks, d.out_len, nseg, partial, pcount, d_agg, d_counts)));
+      else
+        TIMED(e, st, "k_acc_fin", (k_acc_fin<Fp64><<<gfin, 256, 0, st>>>(nchunks, d.out_len, nseg, partial, pcount, d_agg, d_counts)));
     }
     return PRIO3_OK;
   };
@@ -3159,11 +3216,14 @@ static int launch_slow_redo(prio3_engine* e, const DevParams& base, uint32_t n, 
   dp.redo = 1;
   const uint32_t g = slow_blocks(n);
   if (family == DEFER_GEN64) {  // k_prep_gen<Fp64>: XOF redo, then the generic query
-    dp.redo = 0;
-    TIMED(e, st, "k_slow_redo", launch_xof_slow<Fp64>(e, dp, in, sc, st));
-    dp.redo = 1;
-    TIMED(e, st, "k_slow_redo",
-          (k_query<Fp64><<<(n + 255) / 256, 256, 0, st>>>(dp, in, sc, out)));
+    if (e->slow_rpl == 2) {  // A/B: the two-launch form (k_xof_slow, then k_query with redo)
+      dp.redo = 0;
+      TIMED(e, st, "k_slow_redo", launch_xof_slow<Fp64>(e, dp, in, sc, st));
+      dp.redo = 1;
+      TIMED(e, st, "k_slow_redo",
+            (k_query<Fp64><<<(n + 255) / 256, 256, 0, st>>>(dp, in, sc, out)));
+    } else
+      TIMED(e, st, "k_slow_redo", (k_slow_redo_gen<Fp64><<<g, 64, 0, st>>>(dp, in, sc, out)));
   } else if (family == DEFER_SUM) {
     switch (dp.P) {
       case 16: TIMED(e, st, "k_slow_redo", (k_slow_redo_sum<1><<<g, 64, 0, st>>>(dp, in, sc, out))); break;

@@ -351,9 +351,10 @@ def test_sumvec_wide_prepare_options_parity(name, opts):
     _check_against_oracle(CONFIGS[name], 70, seed=94, force_slow=True, opts=opts)
 
 
-@pytest.mark.parametrize("opts", [{}, {"prep_fused": 0}, {"chunks": 3}])
+@pytest.mark.parametrize("opts", [{}, {"prep_fused": 0}, {"chunks": 3}, {"slow_rpl": 2}])
 def test_fused_count_prepare_parity(opts):
     """Prio3Count (Field64) with the generic XOF and query in one launch (k_prep_gen, the default)
-    and on two kernels, on a tampered ragged batch and with every report on the slow path."""
+    and on two kernels, on a tampered ragged batch and with every report on the slow path (its
+    redo in one k_slow_redo_gen launch, or, slow_rpl = 2, as k_xof_slow + k_query)."""
     _check_against_oracle(CONFIGS["count"], 999, seed=95, opts=opts)
     _check_against_oracle(CONFIGS["count"], 130, seed=96, force_slow=True, opts=opts)
