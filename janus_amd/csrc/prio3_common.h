@@ -629,6 +629,7 @@ struct Run {
   size_t fix_cap = 0;
   bool fused = false;
   bool aggregate = false;  // made by prio3_device_prepare_aggregate (finish may follow)
+  bool lfused = false;     // leader init summed the wave partials (segment 0; leader_fuse_acc)
   uint32_t nseg = 0;
   const uint32_t* seg = nullptr;
   std::atomic<int> refs{1};
@@ -643,6 +644,7 @@ struct prio3_engine {
   Run* cur = nullptr;  // the latest device-resident prepare (its output shares stay here)
   int fuse_acc = 1;
   int leader_fast = 1;
+  int leader_fuse_acc = 1;  // option: device leader init accumulates wave partials (k_jrpart<true>)
   int chunks = 0;            // option: prepare in this many stream-overlapped chunks (0 = auto)
   int64_t fp_sub_bytes = 0;  // option: FPVec per-sub-batch scratch budget (bytes; 0 = auto)
   int coalesce = 1;          // option: host-buffer prepare through the coalescing executor

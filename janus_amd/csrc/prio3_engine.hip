@@ -3356,7 +3356,16 @@ static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
     const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
     TIMED(e, st, "k_leader_unpack",
           (k_leader_unpack<<<(n + 63) / 64, 256, 0, st>>>(dp, in, R->sc, d_status)));
-    TIMED(e, st, "k_jrpart", (k_jrpart<false, true><<<blocks, 256, 0, st>>>(dp, in, R->sc)));
+    if (R->lfused) {  // wave partials of the share for segment 0, fixed up at accumulate
+      DevParams q = dp;
+      q.nseg = 1;
+      Scratch qs = R->sc;
+      qs.seg = nullptr;
+      qs.wpart = R->wpart;
+      qs.wseg = R->wseg;
+      TIMED(e, st, "k_jrpart", (k_jrpart<true, true><<<blocks, 256, 0, st>>>(q, in, qs)));
+    } else
+      TIMED(e, st, "k_jrpart", (k_jrpart<false, true><<<blocks, 256, 0, st>>>(dp, in, R->sc)));
     TIMED(e, st, "k_leader_slowfix",
           (k_leader_slowfix<<<blocks64, 64, 0, st>>>(dp, in, R->sc)));
     if (dp.P == 32)
@@ -3718,7 +3727,8 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
               {"qpair", &e->qpair},                {"timing", &e->timing},
               {"coalesce", &e->coalesce},          {"experimental_fpvec", &e->experimental_fpvec},
               {"xof_pair", &e->xof_pair},          {"qwide", &e->qwide},
-              {"trunc_xof", &e->trunc_xof},        {"fp_wide", &e->fp_wide}};
+              {"trunc_xof", &e->trunc_xof},        {"fp_wide", &e->fp_wide},
+              {"leader_fuse_acc", &e->leader_fuse_acc}};
   if (!strcmp(key, "fp_wgs")) {
     if (value < 2 || value > 4) return PRIO3_EINVAL;
     e->fp_wgs = (int)value;
@@ -3781,6 +3791,43 @@ int prio3_device_prepare(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
   return prepare_run(e, R, in, OutPtrs{d_prep_msgs, d_status}, st, false, true);
 }
 
+// The aggregate from the run's wave partials: k_agg_waves (chunk partials), k_agg_fix (counts
+// and the reports whose fused inclusion differs from their verdict), k_agg_final.  seg: the
+// inclusion segment ids; fix_seg: the segment each fix-up entry applies to (nullptr: 0 -- the
+// leader's partials are all summed for segment 0, so with one segment every fix-up, an
+// out-of-range id included, is a correction of segment 0).
+static int fused_finish(prio3_engine* e, Run* R, const uint8_t* d_status, const uint32_t* seg,
+                        const uint32_t* fix_seg, const uint8_t* d_accept_mask, uint32_t S,
+                        uint8_t* d_agg_shares, uint64_t* d_counts, hipStream_t st) {
+  const uint32_t n = R->n, M = R->dp.meas_len;
+  const uint32_t nwaves = (n + 63) / 64;
+  HIPCHK(hipMemsetAsync(R->agg64, 0, (size_t)S * M * 8 * 8, st));
+  HIPCHK(hipMemsetAsync(R->fix, 0, sizeof(uint32_t), st));
+  HIPCHK(hipMemsetAsync(d_counts, 0, 8 * (size_t)S, st));
+  const uint32_t nchunks = (nwaves + WCH - 1) / WCH;
+  dim3 g1((M * 8 / 4 + 255) / 256, nchunks);  // 4 slots per thread (k_agg_waves)
+  TIMED(e, st, "k_agg_waves",
+        (k_agg_waves<<<g1, 256, 0, st>>>(nwaves, M, R->wpart, R->wseg, R->cpart, R->cseg,
+                                         R->agg64)));
+  TIMED(e, st, "k_agg_fix",
+        (k_agg_fix<<<(n + FIX_R - 1) / FIX_R, 256, 0, st>>>(
+            n, d_status, seg, d_accept_mask, R->wseg, R->fix, (uint32_t)(R->fix_cap - 1), S,
+            (unsigned long long*)d_counts)));
+  TIMED(e, st, "k_agg_final",
+        (k_agg_final<<<S * M, 256, 0, st>>>(M, R->dp.ld, R->agg64, nchunks, R->cpart, R->cseg,
+                                             R->fix, fix_seg, R->sc.meas, d_agg_shares)));
+  return PRIO3_OK;
+}
+
+// Device leader init with the accumulate fused into k_jrpart<true, true> (option
+// leader_fuse_acc): Histogram on the helper kernels' leader role, whose output share is the
+// measurement share that k_jrpart streams anyway.
+static bool leader_fuse_takes(const prio3_engine* e) {
+  const DevParams& d = e->dp;
+  return e->leader_fuse_acc && e->leader_fast && d.jr_len && d.kind == PRIO3_HISTOGRAM &&
+         (d.P == 32 || d.P == 16 || d.P == 8) && !own_out(d) && d.es == 16;
+}
+
 int prio3_device_prepare_aggregate(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
                                    const uint8_t* d_public_shares, const uint8_t* d_helper_shares,
                                    const uint8_t* d_leader_prep_shares,
@@ -3820,24 +3867,8 @@ int prio3_device_aggregate_finish(prio3_engine* e, const uint8_t* d_status,
   if (!R->fused)  // not fusable (or an empty batch): the one-pass segmented reduction
     return run_accumulate(e, R, 0, R->n, d_status, R->seg, d_accept_mask, R->nseg, d_agg_shares,
                           d_counts, st);
-  const uint32_t n = R->n, S = R->nseg, M = R->dp.meas_len;
-  const uint32_t nwaves = (n + 63) / 64;
-  HIPCHK(hipMemsetAsync(R->agg64, 0, (size_t)S * M * 8 * 8, st));
-  HIPCHK(hipMemsetAsync(R->fix, 0, sizeof(uint32_t), st));
-  HIPCHK(hipMemsetAsync(d_counts, 0, 8 * (size_t)S, st));
-  const uint32_t nchunks = (nwaves + WCH - 1) / WCH;
-  dim3 g1((M * 8 / 4 + 255) / 256, nchunks);  // 4 slots per thread (k_agg_waves)
-  TIMED(e, st, "k_agg_waves",
-        (k_agg_waves<<<g1, 256, 0, st>>>(nwaves, M, R->wpart, R->wseg, R->cpart, R->cseg,
-                                         R->agg64)));
-  TIMED(e, st, "k_agg_fix",
-        (k_agg_fix<<<(n + FIX_R - 1) / FIX_R, 256, 0, st>>>(
-            n, d_status, R->seg, d_accept_mask, R->wseg, R->fix, (uint32_t)(R->fix_cap - 1), S,
-            (unsigned long long*)d_counts)));
-  TIMED(e, st, "k_agg_final",
-        (k_agg_final<<<S * M, 256, 0, st>>>(M, R->dp.ld, R->agg64, nchunks, R->cpart, R->cseg,
-                                             R->fix, R->seg, R->sc.meas, d_agg_shares)));
-  return PRIO3_OK;
+  return fused_finish(e, R, d_status, R->seg, R->seg, d_accept_mask, R->nseg, d_agg_shares,
+                      d_counts, st);
 }
 
 int prio3_device_accumulate(prio3_engine* e, uint32_t n, const uint8_t* d_status,
@@ -3857,6 +3888,11 @@ int prio3_device_accumulate(prio3_engine* e, uint32_t n, const uint8_t* d_status
   }
   Run* R = e->cur;
   if (!R || n > R->n) return PRIO3_EINVAL;
+  if (R->lfused && n == R->n && n_segments == 1) {
+    R->last = st;
+    return fused_finish(e, R, d_status, d_segment_ids, nullptr, d_accept_mask, 1, d_agg_shares,
+                        d_counts, st);
+  }
   return run_accumulate(e, R, 0, n, d_status, d_segment_ids, d_accept_mask, n_segments,
                         d_agg_shares, d_counts, st);
 }
@@ -4139,8 +4175,11 @@ int prio3_device_leader_prepare_init(prio3_engine* e, uint32_t n, const uint8_t*
   HIPCHK(hipSetDevice(e->device));
   hipStream_t st = (hipStream_t)stream;
   int rc = PRIO3_OK;
-  Run* R = device_run(e, n, RUN_SCRATCH, 0, st, &rc);
+  const bool lfuse = leader_fuse_takes(e);
+  Run* R = device_run(e, n, RUN_SCRATCH | (lfuse ? (unsigned)RUN_FUSED : 0u), lfuse ? 1u : 0u, st,
+                      &rc);
   if (!R) return rc;
+  R->lfused = lfuse;
   return leader_init_run(e, R, d_nonces, d_public_shares, d_leader_input_shares, d_prep_shares,
                          d_status, st);
 }

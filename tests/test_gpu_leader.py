@@ -150,3 +150,54 @@ def test_full_job_both_roles_unshard(name):
     else:
         exp = [sum(d["measurements"])]
     assert tot == exp
+
+
+@pytest.mark.parametrize("fuse", [1, 0])
+@pytest.mark.parametrize("name", ["hist_256_c16", "hist_10_c3", "hist_100_c10"])
+def test_device_leader_fused_accumulate(name, fuse):
+    """The device-resident leader step (bench.py --role leader): init -> next -> accumulate, the
+    accumulate fused into k_jrpart's wave partials (option leader_fuse_acc = 1) or the separate
+    segmented pass, against the host-batch leader path (pinned to the oracle above).  A
+    non-canonical leader share, a tampered prepare message, a ragged batch, a host mask,
+    out-of-range segment ids with one segment (fused + fix-ups) and three segments (the
+    separate pass)."""
+    import torch
+    cfg = CONFIGS[name]
+    o = _oracle(cfg)
+    ref, helper, eng = _engine(cfg), _engine(cfg), _engine(cfg)
+    eng.set_option("leader_fuse_acc", fuse)
+    n = 300
+    d = _reports(o, cfg, n, seed=77)
+    d["leader_shares"][9, :o.es] = 0xFF
+    lps, lst, lbatch = ref.leader_prepare_init_batch(d["nonces"], d["public_shares"],
+                                                     d["leader_shares"])
+    msgs, _, _ = helper.prepare_batch(d["nonces"], d["public_shares"], d["helper_shares"], lps)
+    msgs = msgs.copy()
+    msgs[17, -1] ^= 1
+    lst2 = lbatch.leader_prepare_next(msgs, lst.copy())
+    assert lst[9] != 0 and lst2[17] != 0 and (lst2 == 0).sum() > n - 5
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to("cuda")
+    ps_d = torch.zeros(lps.shape, dtype=torch.uint8, device="cuda")
+    st_d = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    eng.leader_prepare_init_device(t(d["nonces"]), t(d["public_shares"]), t(d["leader_shares"]),
+                                   ps_d, st_d)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(st_d.cpu().numpy(), lst)
+    ok = lst == 0
+    np.testing.assert_array_equal(ps_d.cpu().numpy()[ok], lps[ok])
+    eng.leader_prepare_next_device(n, t(msgs), st_d)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(st_d.cpu().numpy(), lst2)
+    rng = np.random.default_rng(3)
+    accept = (rng.random(n) > 0.1).astype(np.uint8)
+    seg1 = np.where(rng.random(n) > 0.05, 0, 5).astype(np.uint32)
+    seg3 = rng.integers(0, 3, n).astype(np.uint32)
+    for seg, acc, S in [(None, None, 1), (seg1, accept, 1), (None, accept, 1), (seg3, accept, 3)]:
+        ra, rc = lbatch.accumulate(seg, acc, S)
+        agg = torch.zeros(ra.shape, dtype=torch.uint8, device="cuda")
+        cnt = torch.zeros(S, dtype=torch.int64, device="cuda")
+        eng.accumulate_device(n, st_d, None if seg is None else t(seg),
+                              None if acc is None else t(acc), S, agg, cnt)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(agg.cpu().numpy(), ra)
+        np.testing.assert_array_equal(cnt.cpu().numpy().astype(np.uint64), rc)
