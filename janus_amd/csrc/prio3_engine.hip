@@ -677,8 +677,14 @@ __global__ __launch_bounds__(256, JR_OCC) void k_jrpart(DevParams p, InPtrs in, 
 // report) into the SoA measurement / proofs scratch with the canonical-encoding check, plus the
 // query randomness (1 permutation) -- the leader analogue of k_xof_a.
 // ------------------------------------------------------------------------------------
+// wpart / wseg (non-null: the device leader's fused accumulate, leader_fuse_acc): while a chunk
+// sits in LDS, thread (element tid / 8, half-limb tid % 8) also sums that 16-bit half-limb over
+// the block's 64 reports -- the wave partials k_agg_waves reads (the layout of wave_halfsum2's)
+// -- and the block's wave is marked fused for segment 0 when all 64 reports are present and
+// canonical.
 __global__ __launch_bounds__(256) void k_leader_unpack(DevParams p, InPtrs in, Scratch sc,
-                                                       uint8_t* status) {
+                                                       uint8_t* status, uint32_t* wpart,
+                                                       uint32_t* wseg) {
   // block = 64 reports; the explicit shares are transposed through LDS in chunks of 32
   // elements (rows read 512 B contiguous per report, columns written 1 KiB contiguous per
   // element) -- per-lane row streaming of the 5.6 KiB rows ran at a fraction of HBM speed.
@@ -714,6 +720,18 @@ __global__ __launch_bounds__(256) void k_leader_unpack(DevParams p, InPtrs in, S
           ((uint4*)sc.proofs)[(size_t)(e - M) * ld + r0 + rr] = tile[rr][el];
       }
     }
+    if (wpart && nrep == RB && c0 < M) {  // uniform
+      const uint32_t el = tid >> 3, h = tid & 7u, e = c0 + el;
+      if (e < M) {
+        uint32_t sum = 0;
+#pragma unroll 8
+        for (uint32_t rr = 0; rr < RB; rr++) {
+          const uint32_t* w = (const uint32_t*)&tile[rr][el];
+          sum += (w[h >> 1] >> ((h & 1u) * 16u)) & 0xffffu;
+        }
+        wpart[((size_t)blockIdx.x * M + e) * 8u + h] = sum;
+      }
+    }
   }
   __syncthreads();
   if (tid >= nrep) return;
@@ -738,6 +756,10 @@ __global__ __launch_bounds__(256) void k_leader_unpack(DevParams p, InPtrs in, S
   }
   sc.flag[r] = (uint8_t)flag;
   status[r] = bad[tid] ? PRIO3_STATUS_INPUT_SHARE_DECODE : PRIO3_STATUS_FINISHED;
+  if (wseg) {
+    const bool fuse = nrep == RB && __all(!bad[tid]);  // nrep == RB: all 64 lanes are here
+    if (tid == 0) wseg[blockIdx.x] = fuse ? 0u : 0xffffffffu;
+  }
 }
 
 // Leader slow path: reports whose query or joint-rand expansion hit a rejection-sampling
@@ -3320,7 +3342,7 @@ static int leader_init_fpvec(prio3_engine* e, Run* R, const uint8_t* d_nonces,
     qs.out = (uint8_t*)R->sc.out + es * s0;
     const uint32_t blocks = (q.n + 255) / 256, blocks64 = (q.n + 63) / 64;
     TIMED(e, st, "k_leader_unpack",
-          (k_leader_unpack<<<(q.n + 63) / 64, 256, 0, st>>>(q, qi, qs, qo.status)));
+          (k_leader_unpack<<<(q.n + 63) / 64, 256, 0, st>>>(q, qi, qs, qo.status, nullptr, nullptr)));
     TIMED(e, st, "k_jrpart", (k_jrpart<false, true><<<blocks, 256, 0, st>>>(q, qi, qs)));
     TIMED(e, st, "k_leader_slowfix", (k_leader_slowfix<<<blocks64, 64, 0, st>>>(q, qi, qs)));
     TIMED(e, st, "k_query_fpw", launch_fpvec_query(q, qi, qs, qo, st, -10 - e->fp_wgs));
@@ -3354,18 +3376,12 @@ static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
     InPtrs in{d_nonces, d_public_shares, d_leader_input_shares, nullptr};
     OutPtrs out{d_prep_shares, d_status};
     const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
+    // R->lfused: the wave partials of the share for segment 0, fixed up at accumulate
     TIMED(e, st, "k_leader_unpack",
-          (k_leader_unpack<<<(n + 63) / 64, 256, 0, st>>>(dp, in, R->sc, d_status)));
-    if (R->lfused) {  // wave partials of the share for segment 0, fixed up at accumulate
-      DevParams q = dp;
-      q.nseg = 1;
-      Scratch qs = R->sc;
-      qs.seg = nullptr;
-      qs.wpart = R->wpart;
-      qs.wseg = R->wseg;
-      TIMED(e, st, "k_jrpart", (k_jrpart<true, true><<<blocks, 256, 0, st>>>(q, in, qs)));
-    } else
-      TIMED(e, st, "k_jrpart", (k_jrpart<false, true><<<blocks, 256, 0, st>>>(dp, in, R->sc)));
+          (k_leader_unpack<<<(n + 63) / 64, 256, 0, st>>>(dp, in, R->sc, d_status,
+                                                         R->lfused ? R->wpart : nullptr,
+                                                         R->lfused ? R->wseg : nullptr)));
+    TIMED(e, st, "k_jrpart", (k_jrpart<false, true><<<blocks, 256, 0, st>>>(dp, in, R->sc)));
     TIMED(e, st, "k_leader_slowfix",
           (k_leader_slowfix<<<blocks64, 64, 0, st>>>(dp, in, R->sc)));
     if (dp.P == 32)
@@ -3385,7 +3401,8 @@ static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
     OutPtrs out{d_prep_shares, d_status};
     const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
     TIMED(e, st, "k_leader_unpack",
-          (k_leader_unpack<<<(n + 63) / 64, 256, 0, st>>>(dp, in, R->sc, d_status)));
+          (k_leader_unpack<<<(n + 63) / 64, 256, 0, st>>>(dp, in, R->sc, d_status, nullptr,
+                                                         nullptr)));
     TIMED(e, st, "k_jrpart", (k_jrpart<false, true><<<blocks, 256, 0, st>>>(dp, in, R->sc)));
     TIMED(e, st, "k_leader_slowfix",
           (k_leader_slowfix<<<blocks64, 64, 0, st>>>(dp, in, R->sc)));
@@ -3819,9 +3836,9 @@ static int fused_finish(prio3_engine* e, Run* R, const uint8_t* d_status, const 
   return PRIO3_OK;
 }
 
-// Device leader init with the accumulate fused into k_jrpart<true, true> (option
-// leader_fuse_acc): Histogram on the helper kernels' leader role, whose output share is the
-// measurement share that k_jrpart streams anyway.
+// Device leader init with the accumulate fused into k_leader_unpack (option leader_fuse_acc):
+// Histogram on the helper kernels' leader role, whose output share is the measurement share
+// that the unpack stages through LDS anyway.
 static bool leader_fuse_takes(const prio3_engine* e) {
   const DevParams& d = e->dp;
   return e->leader_fuse_acc && e->leader_fast && d.jr_len && d.kind == PRIO3_HISTOGRAM &&
