@@ -226,6 +226,11 @@ int prio3_device_leader_prepare_init(prio3_engine* engine, uint32_t n, const uin
                                      uint8_t* d_status, void* stream);
 int prio3_device_leader_prepare_next(prio3_engine* engine, uint32_t n, const uint8_t* d_prep_msgs,
                                      uint8_t* d_status, void* stream);
+/* The device leader's output shares are summed by prio3_device_accumulate.  For Histogram the
+ * sum is started inside prio3_device_leader_prepare_init (wave partials while the explicit
+ * shares are unpacked; option leader_fuse_acc, default 1): an accumulate over the whole batch
+ * with n_segments == 1 finishes from them (the verdicts, the accept mask and out-of-range
+ * segment ids are applied as corrections), any other accumulate reads the output shares. */
 
 /* ---- Synthetic client (benchmarks and tests) ---- */
 /* Generates n honest reports on the device: the client's shard (prio Prio3::shard,
@@ -244,7 +249,9 @@ int prio3_client_generate_device(prio3_engine* engine, uint32_t n, uint64_t seed
                                  uint8_t* d_leader_input_shares, void* stream);
 
 /* ---- Test / measurement knobs ---- */
-/* force_slow_path=1 routes every report through the general rejection-sampling kernel. */
+/* force_slow_path=1 routes every report through the general rejection-sampling kernel;
+ * leader_fuse_acc=0 turns off the fused device-leader accumulate (A/B); the other keys are the
+ * launch variants prio3_engine.hip's prio3_engine_set_option lists. */
 int prio3_engine_set_option(prio3_engine* engine, const char* key, int64_t value);
 /* Per-kernel device time (ms) accumulated since the last reset, measured with HIP events
  * on the launch stream when option "timing" is 1.  names: comma-separated kernel names. */

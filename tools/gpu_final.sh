@@ -17,6 +17,7 @@ timeout -k 10 200 python3 bench.py --role leader > $O/leader.json
 timeout -k 10 200 python3 bench.py --role leader --leader-vdaf sum32 > $O/leader_sum32.json
 timeout -k 10 200 python3 bench.py --role jobs > $O/jobs128.json
 timeout -k 10 200 python3 bench.py --role hpke --reports 1048576 > $O/hpke.json
+timeout -k 10 200 python3 bench.py --role hpke --hpke-kem p256 --reports 262144 > $O/hpke_p256.json
 timeout -k 10 200 python3 bench.py --role pipeline --reports 1048576 > $O/pipeline.json
 timeout -k 10 200 python3 bench.py --role mp64 --reports 1000000 > $O/mp64.json
 python3 - <<'PY'
