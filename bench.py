@@ -451,7 +451,8 @@ def jobs_main(args):
     dt = run(n_jobs)
     if dt < 0:
         raise RuntimeError("janus_jobs_run: a C-ABI call failed")
-    launches = sum(e.timing().get("k_xofd", (0, 0))[1] for e in engines)
+    # the prepare launches: the fused XOF + query (k_prep_h) or, on the two-kernel chain, k_xofd
+    launches = sum(e.timing().get(k, (0, 0))[1] for e in engines for k in ("k_prep_h", "k_xofd"))
     value = n_jobs * js / dt
     # spot check: the last job's aggregate against the restatement
     from oracle.oracle import Oracle
