@@ -1973,27 +1973,28 @@ __global__ __launch_bounds__(256) void k_agg_waves(uint32_t nwaves, uint32_t M,
                                                    const uint32_t* wpart, const uint32_t* wseg,
                                                    unsigned long long* cpart, uint32_t* cseg,
                                                    unsigned long long* agg64) {
+  static_assert(WCH <= 64, "one chunk's wave segments are read by one wave");
   const uint32_t slot = 4 * (blockIdx.x * blockDim.x + threadIdx.x), c = blockIdx.y;
-  const uint32_t w0 = c * WCH, w1 = min(nwaves, w0 + WCH);
-  uint32_t s0 = 0xffffffffu;
-  bool mixed = false;
-  for (uint32_t w = w0; w < w1; w++) {  // uniform across the block (wseg is per wave)
-    const uint32_t sg = wseg[w];
-    if (sg == 0xffffffffu) continue;
-    if (s0 == 0xffffffffu) s0 = sg;
-    else if (sg != s0) mixed = true;
-  }
+  const uint32_t w0 = c * WCH, w1 = min(nwaves, w0 + WCH), lane = threadIdx.x & 63u;
+  // the chunk's wave segments in one load per lane (not a dependent scalar load per wave):
+  // bit i of `fused` = wave w0 + i was fused; s0 = the first fused wave's segment
+  const uint32_t my = w0 + lane < w1 ? wseg[w0 + lane] : 0xffffffffu;
+  const uint64_t fused = __ballot(my != 0xffffffffu);
+  const uint32_t s0 = fused ? (uint32_t)__shfl((int)my, __ffsll((long long)fused) - 1) : 0xffffffffu;
+  const bool mixed = __any(my != 0xffffffffu && my != s0);
   if (slot == 0 && blockIdx.x == 0) cseg[c] = mixed ? 0xffffffffu : s0;
   if (slot >= M * 8 || s0 == 0xffffffffu) return;  // M * 8 is a multiple of 4
   const size_t row = (size_t)M * 8;
   if (!mixed) {
+    // all WCH loads independent and unconditional (clamped to the last wave, masked by bit)
     unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-#pragma unroll 16
-    for (uint32_t w = w0; w < w1; w++)
-      if (wseg[w] != 0xffffffffu) {
-        const uint4 v = *(const uint4*)(wpart + (size_t)w * row + slot);
-        a0 += v.x, a1 += v.y, a2 += v.z, a3 += v.w;
-      }
+#pragma unroll
+    for (uint32_t i = 0; i < WCH; i++) {
+      const uint32_t w = min(w0 + i, w1 - 1);
+      const uint4 v = *(const uint4*)(wpart + (size_t)w * row + slot);
+      const uint32_t m = 0u - (uint32_t)((fused >> i) & 1u);
+      a0 += v.x & m, a1 += v.y & m, a2 += v.z & m, a3 += v.w & m;
+    }
     unsigned long long* o = cpart + (size_t)c * row + slot;
     o[0] = a0, o[1] = a1, o[2] = a2, o[3] = a3;
     return;
