@@ -919,6 +919,27 @@ __global__ __launch_bounds__(64) void k_xof_slow(DevParams p, InPtrs in, Scratch
 // launch geometry of k_xof_slow: 16 reports per lane, one wave per block (a one-wave block
 // needs one SIMD with room for it, not four on one CU, beside the other streams' kernels)
 static inline uint32_t slow_blocks(uint32_t n) { return (n + 1023) / 1024; }
+// the deferred slow path's redo launches (k_slow_redo*): REDO_RPL reports scanned per lane, so a
+// run without flagged reports costs few waves
+constexpr uint32_t REDO_RPL = 64;
+static inline uint32_t redo_blocks(uint32_t n) {
+  return (n + 64 * REDO_RPL - 1) / (64 * REDO_RPL);
+}
+// any flag among reports [r0, r0 + REDO_RPL) of the run
+__device__ __forceinline__ bool redo_any(const DevParams& p, const Scratch& sc, uint32_t r0) {
+  const uint8_t* fl = sc.flag + r0;
+  uint32_t any = 0;
+  if (r0 + REDO_RPL <= p.n && ((uintptr_t)fl & 15) == 0) {
+#pragma unroll
+    for (uint32_t k = 0; k < REDO_RPL / 16; k++) {
+      const uint4 v = ((const uint4*)fl)[k];
+      any |= v.x | v.y | v.z | v.w;
+    }
+  } else {
+    for (uint32_t i = 0; i < REDO_RPL && r0 + i < p.n; i++) any |= fl[i];
+  }
+  return any != 0;
+}
 // option slow_rpl=1: the round-1 geometry (one report per lane), kept for A/B
 template <class F>
 static void launch_xof_slow(const prio3_engine* e, const DevParams& p, const InPtrs& in,
@@ -1039,23 +1060,15 @@ __global__ __launch_bounds__(256) void k_prep_gen(DevParams p, InPtrs in, Scratc
 }
 
 // k_slow_redo_gen<F>: k_prep_gen's deferred slow path in one launch (as k_slow_redo): each lane
-// scans the flags of 16 reports with one load and, for a flagged one, re-runs its XOF on the
+// scans the flags of REDO_RPL reports and, for a flagged one, re-runs its XOF on the
 // byte-level sponge (flag := 2) and then its query (p.redo = 1)
 template <class F>
 __global__ __launch_bounds__(64) void k_slow_redo_gen(DevParams p, InPtrs in, Scratch sc,
                                                       OutPtrs out) {
-  const uint32_t r0 = (blockIdx.x * blockDim.x + threadIdx.x) * 16u;
-  if (r0 >= p.n) return;
+  const uint32_t r0 = (blockIdx.x * blockDim.x + threadIdx.x) * REDO_RPL;
+  if (r0 >= p.n || !redo_any(p, sc, r0)) return;
   const uint8_t* fl = sc.flag + r0;
-  uint32_t any = 0;
-  if (r0 + 16 <= p.n && ((uintptr_t)fl & 15) == 0) {
-    const uint4 v = *(const uint4*)fl;
-    any = v.x | v.y | v.z | v.w;
-  } else {
-    for (uint32_t i = 0; i < 16 && r0 + i < p.n; i++) any |= fl[i];
-  }
-  if (!any) return;
-  for (uint32_t i = 0; i < 16 && r0 + i < p.n; i++)
+  for (uint32_t i = 0; i < REDO_RPL && r0 + i < p.n; i++)
     if (fl[i]) {
       xof_slow_one<F>(p, in, sc, r0 + i);
       query_body<F>(p, in, sc, out, r0 + i);
@@ -3184,23 +3197,15 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
 // then their query (redo = 1), lane by lane.  One launch per run instead of one k_xof_slow
 // launch between the XOF and the query of every chunk, where its one-wave blocks waited behind
 // the other stream's kernels (~0.2 ms per chunk in the r02 trace).
-// k_slow_redo<PP>: both halves in one launch -- each lane scans the flags of 16 reports with one
-// 16-byte load (as k_xof_slow<F, 16>) and, for a flagged report, re-runs its XOF (flag := 2) and
-// then its query on the same lane.
+// k_slow_redo<PP>: both halves in one launch -- each lane scans the flags of REDO_RPL reports
+// (16-byte loads) and, for a flagged report, re-runs its XOF (flag := 2) and then its query on
+// the same lane.
 template <int PP>
 __global__ __launch_bounds__(64) void k_slow_redo(DevParams p, InPtrs in, Scratch sc, OutPtrs out) {
-  const uint32_t r0 = (blockIdx.x * blockDim.x + threadIdx.x) * 16u;
-  if (r0 >= p.n) return;
+  const uint32_t r0 = (blockIdx.x * blockDim.x + threadIdx.x) * REDO_RPL;
+  if (r0 >= p.n || !redo_any(p, sc, r0)) return;
   const uint8_t* fl = sc.flag + r0;
-  uint32_t any = 0;
-  if (r0 + 16 <= p.n && ((uintptr_t)fl & 15) == 0) {
-    const uint4 v = *(const uint4*)fl;
-    any = v.x | v.y | v.z | v.w;
-  } else {
-    for (uint32_t i = 0; i < 16 && r0 + i < p.n; i++) any |= fl[i];
-  }
-  if (!any) return;
-  for (uint32_t i = 0; i < 16 && r0 + i < p.n; i++)
+  for (uint32_t i = 0; i < REDO_RPL && r0 + i < p.n; i++)
     if (fl[i]) {
       xof_slow_one<Fp128>(p, in, sc, r0 + i);
       query_h_body<2, PP, 1, 3, 0, false>(p, in, sc, out, r0 + i);
@@ -3210,18 +3215,10 @@ __global__ __launch_bounds__(64) void k_slow_redo(DevParams p, InPtrs in, Scratc
 template <int NPH>
 __global__ __launch_bounds__(64) void k_slow_redo_sum(DevParams p, InPtrs in, Scratch sc,
                                                       OutPtrs out) {
-  const uint32_t r0 = (blockIdx.x * blockDim.x + threadIdx.x) * 16u;
-  if (r0 >= p.n) return;
+  const uint32_t r0 = (blockIdx.x * blockDim.x + threadIdx.x) * REDO_RPL;
+  if (r0 >= p.n || !redo_any(p, sc, r0)) return;
   const uint8_t* fl = sc.flag + r0;
-  uint32_t any = 0;
-  if (r0 + 16 <= p.n && ((uintptr_t)fl & 15) == 0) {
-    const uint4 v = *(const uint4*)fl;
-    any = v.x | v.y | v.z | v.w;
-  } else {
-    for (uint32_t i = 0; i < 16 && r0 + i < p.n; i++) any |= fl[i];
-  }
-  if (!any) return;
-  for (uint32_t i = 0; i < 16 && r0 + i < p.n; i++)
+  for (uint32_t i = 0; i < REDO_RPL && r0 + i < p.n; i++)
     if (fl[i]) {
       xof_slow_one<Fp128>(p, in, sc, r0 + i);
       qsum::query_sum_body<NPH, 0>(p, in, sc, out, r0 + i);
@@ -3237,7 +3234,7 @@ static int launch_slow_redo(prio3_engine* e, const DevParams& base, uint32_t n, 
   dp.trunc_xof = 0;
   dp.slow_defer = 1;
   dp.redo = 1;
-  const uint32_t g = slow_blocks(n);
+  const uint32_t g = redo_blocks(n);
   if (family == DEFER_GEN64) {  // k_prep_gen<Fp64>: XOF redo, then the generic query
     if (e->slow_rpl == 2) {  // A/B: the two-launch form (k_xof_slow, then k_query with redo)
       dp.redo = 0;
