@@ -41,8 +41,9 @@ enum { JANUS_DAP_QUERY_TIME_INTERVAL = 1, JANUS_DAP_QUERY_FIXED_SIZE = 2 };
  * 6 = the public share has another length than layout->public_share_len -- it does not decode:
  * PrepareError::InvalidMessage (aggregator.rs:1985-1999), after any HPKE error of the report.
  * A PingPongMessage that does not decode (unknown type, bad framing) rejects the whole request,
- * as Janus's request decode does.  The caller checks layout->public_share_len against the
- * VDAF's public share length (a body whose first record is off is malformed throughout). */
+ * as Janus's request decode does.  janus_dap_agg_init_scan_ex takes the lengths the task
+ * expects (VDAF public share, KEM Nenc, VDAF prep share), so a malformed first record fails
+ * alone; janus_dap_agg_init_scan takes them from the first record. */
 
 typedef struct {
   /* filled by janus_dap_agg_init_scan */
@@ -53,14 +54,26 @@ typedef struct {
   uint64_t agg_param_off, agg_param_len;
   uint64_t list_off, list_len;  /* byte range of the PrepareInit list */
   uint32_t record_len;          /* byte length of the first PrepareInit */
-  uint32_t public_share_len;    /* of the first record */
-  uint32_t enc_len, payload_len, message_len, prep_share_len;  /* of the first record */
+  uint32_t public_share_len;    /* expected (scan_ex) or of the first record */
+  uint32_t enc_len, payload_len, message_len, prep_share_len;  /* enc / prep share: as
+                                   public_share_len; payload, message: of the first record */
   int uniform;                  /* list_len is a multiple of record_len */
 } janus_dap_agg_init_layout;
 
 /* Parses the header and the first PrepareInit of an AggregationJobInitializeReq body (host
  * memory; O(1)).  Returns 0, or -1 if the header does not decode. */
 int janus_dap_agg_init_scan(const uint8_t* body, size_t len, janus_dap_agg_init_layout* out);
+
+/* As janus_dap_agg_init_scan, with the lengths every record must have: the VDAF's public share
+ * length, the HPKE KEM's Nenc and the VDAF's leader prep share length (JANUS_DAP_LEN_ANY: the
+ * first record's).  The layout carries the expected lengths; if the first record differs from
+ * them, layout->uniform is 0 and the caller unpacks on the host, where each record with another
+ * public share / prep share length gets msg_status 6 / 2 and another enc length ct_len 0 (HPKE
+ * decrypt error) -- the reference fails only that report (aggregator.rs:1967-1999). */
+#define JANUS_DAP_LEN_ANY 0xFFFFFFFFu
+int janus_dap_agg_init_scan_ex(const uint8_t* body, size_t len, uint32_t public_share_len,
+                               uint32_t enc_len, uint32_t prep_share_len,
+                               janus_dap_agg_init_layout* out);
 
 /* Device unpack of a body whose records all have layout->record_len bytes (layout->uniform).
  * d_body is the request body in device memory.  Outputs (device, n = list_len / record_len):

@@ -371,6 +371,27 @@ int janus_dap_agg_init_scan(const uint8_t* body, size_t len, janus_dap_agg_init_
   return 0;
 }
 
+int janus_dap_agg_init_scan_ex(const uint8_t* body, size_t len, uint32_t public_share_len,
+                               uint32_t enc_len, uint32_t prep_share_len,
+                               janus_dap_agg_init_layout* L) {
+  const int rc = janus_dap_agg_init_scan(body, len, L);
+  if (rc || L->list_len == 0) return rc;
+  // the task's expected lengths, not the first record's: a record whose public share, enc or
+  // prep share has another length fails alone, and a body whose first record is off
+  // is unpacked on the host, where every record is checked against these
+  const bool fits = (public_share_len == JANUS_DAP_LEN_ANY || L->public_share_len == public_share_len) &&
+                    (enc_len == JANUS_DAP_LEN_ANY || L->enc_len == enc_len) &&
+                    (prep_share_len == JANUS_DAP_LEN_ANY || L->prep_share_len == prep_share_len);
+  if (public_share_len != JANUS_DAP_LEN_ANY) L->public_share_len = public_share_len;
+  if (enc_len != JANUS_DAP_LEN_ANY) L->enc_len = enc_len;
+  if (prep_share_len != JANUS_DAP_LEN_ANY) L->prep_share_len = prep_share_len;
+  if (!fits) {
+    L->uniform = 0;
+    L->n = 0;
+  }
+  return 0;
+}
+
 int janus_dap_agg_init_unpack_device(const janus_dap_agg_init_layout* L, const uint8_t* d_body,
                                      uint8_t* d_report_ids, uint64_t* d_times,
                                      uint8_t* d_public_shares, uint8_t* d_config_ids,

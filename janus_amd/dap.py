@@ -10,7 +10,7 @@ import numpy as np
 from .prio3 import _np_ptr, _stream, _tptr, load_library
 
 DAP_EXPORTED_SYMBOLS = (
-    "janus_dap_agg_init_scan", "janus_dap_agg_init_unpack_device",
+    "janus_dap_agg_init_scan", "janus_dap_agg_init_scan_ex", "janus_dap_agg_init_unpack_device",
     "janus_dap_agg_init_unpack_host", "janus_dap_agg_job_resp_max_len",
     "janus_dap_agg_job_resp_encode_device", "janus_dap_agg_job_resp_encode_host",
 )
@@ -35,6 +35,7 @@ def _lib():
     if not _bound:
         vp, u32 = C.c_void_p, C.c_uint32
         L.janus_dap_agg_init_scan.argtypes = [vp, C.c_size_t, C.POINTER(Layout)]
+        L.janus_dap_agg_init_scan_ex.argtypes = [vp, C.c_size_t, u32, u32, u32, C.POINTER(Layout)]
         L.janus_dap_agg_init_unpack_device.argtypes = [C.POINTER(Layout), vp, vp, vp, vp, vp, vp,
                                                        vp, vp, u32, vp, vp, vp, vp]
         L.janus_dap_agg_init_unpack_host.argtypes = [vp, C.c_size_t, C.POINTER(Layout), u32, vp,
@@ -50,10 +51,23 @@ def _lib():
     return L
 
 
-def scan(body: bytes) -> Layout:
+LEN_ANY = 0xFFFFFFFF
+
+
+def scan(body: bytes, public_share_len=None, enc_len=None, prep_share_len=None) -> Layout:
+    """Layout of an AggregationJobInitializeReq body.  With the task's expected lengths (VDAF
+    public share, KEM Nenc, VDAF leader prep share) every record is checked against those, so a
+    malformed first record fails alone (janus_dap_agg_init_scan_ex); without them the first
+    record's lengths are taken."""
     lay = Layout()
     buf = np.frombuffer(body, np.uint8)
-    if _lib().janus_dap_agg_init_scan(_np_ptr(buf), len(body), C.byref(lay)):
+    if public_share_len is None and enc_len is None and prep_share_len is None:
+        rc = _lib().janus_dap_agg_init_scan(_np_ptr(buf), len(body), C.byref(lay))
+    else:
+        v = lambda x: LEN_ANY if x is None else int(x)
+        rc = _lib().janus_dap_agg_init_scan_ex(_np_ptr(buf), len(body), v(public_share_len),
+                                               v(enc_len), v(prep_share_len), C.byref(lay))
+    if rc:
         raise ValueError("AggregationJobInitializeReq does not decode")
     return lay
 

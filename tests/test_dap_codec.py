@@ -102,6 +102,40 @@ def test_host_unpack_message_and_public_share_errors():
             J.unpack_host(bytes(bad), J.scan(bytes(bad)), 8, 64)
 
 
+def test_scan_with_expected_lengths_fails_only_the_malformed_first_record():
+    """ADVICE r2 (dap_codec.hip scan): only record 0 has a public share of the wrong length (and,
+    in a second body, an enc of the wrong length and a short prep share).  With the task's
+    expected lengths (scan_ex) the layout keeps those lengths, the body goes to the host unpack,
+    and only record 0 fails -- the reference fails just the report whose share does not decode
+    (aggregator.rs:1967-1999); taking the first record's lengths would fail all the others."""
+    from janus_amd import dap as J
+    init = lambda n: dict(type="initialize", prep_share=b"s" * n)
+    body = _body([(b"P" * 31, init(48))] + [(b"P" * 32, init(48))] * 4)
+    naive = J.unpack_host(body, J.scan(body), 8, 64)
+    assert naive["msg_status"].tolist() == [0, 6, 6, 6, 6]  # what first-record lengths give
+    lay = J.scan(body, public_share_len=32, enc_len=32, prep_share_len=48)
+    assert (lay.public_share_len, lay.enc_len, lay.prep_share_len, lay.uniform) == (32, 32, 48, 0)
+    out = J.unpack_host(body, lay, 8, J.ct_stride_for(lay))
+    assert out["msg_status"].tolist() == [6, 0, 0, 0, 0]
+    assert not out["public_shares"][0].any() and out["public_shares"][1].tobytes() == b"P" * 32
+    assert out["ct_len"].tolist() == [40] * 5
+    # a wrong-length enc in record 0 is that report's HPKE decrypt error; a short prep share
+    # its CodecPrepShare
+    recs = [dict(report_id=bytes([i] * 16), time=1000 + i, public_share=b"P" * 32, config_id=1,
+                 enc=b"e" * (31 if i == 0 else 32), payload=b"p" * 40,
+                 message=init(47 if i == 0 else 48)) for i in range(4)]
+    body2 = D.encode_agg_init_req(b"", 1, None, recs)
+    lay2 = J.scan(body2, public_share_len=32, enc_len=32, prep_share_len=48)
+    assert not lay2.uniform
+    out2 = J.unpack_host(body2, lay2, 8, J.ct_stride_for(lay2))
+    assert out2["msg_status"].tolist() == [2, 0, 0, 0]
+    assert out2["ct_len"].tolist() == [0, 40, 40, 40]
+    # a uniform body with the expected lengths keeps the device path
+    ok = J.scan(_body([(b"P" * 32, init(48))] * 3), public_share_len=32, enc_len=32,
+                prep_share_len=48)
+    assert ok.uniform and ok.n == 3
+
+
 def test_host_resp_encoder_matches_oracle():
     from janus_amd import dap as J
     rng = np.random.default_rng(3)
