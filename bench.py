@@ -176,7 +176,7 @@ def main():
     ap.add_argument("--tasks", type=int, default=4,
                     help="--role jobs: tasks (verify keys) of the VDAF instance the jobs rotate over")
     ap.add_argument("--opt", action="append", default=[],
-                    help="engine option key=value (e.g. split_xof=0), for A/B runs")
+                    help="engine option key=value (e.g. chunks=3, force_generic_query=1), for A/B runs")
     args = ap.parse_args()
     if args.role == "leader":
         return leader_main(args)

@@ -56,8 +56,6 @@ struct DevParams {
   // 1: the helper XOF kernel also truncates the measurement share into the output-share
   // scratch (TruncSink); the query kernel then leaves sc.out alone
   uint32_t trunc_xof;
-  // 1: the prepare message is not re-hashed (see prep_msg_check)
-  uint32_t msg_cmp;
   // 1: the query kernel skips reports the XOF flagged for the rejection-sampling slow path; the
   // run ends with one k_xof_slow launch (which marks the redone reports 2) and a redo launch of
   // the query (redo = 1) over exactly those reports, instead of a k_xof_slow launch per chunk
@@ -146,20 +144,11 @@ DEV void load16(const uint8_t* p, uint32_t* w) {
 // The helper's prepare message and its prepare_next check (prio Prio3:
 // prepare_shares_to_prepare_message hashes the two joint-rand parts of the prep shares into the
 // joint-rand seed; prepare_next requires it to equal the corrected seed, which the XOF kernel
-// derived from the leader part of the public share and the helper's own part).  Both hashes take
-// the same helper part, so with msg_cmp the message is the corrected seed when the leader's part
-// in its prep share equals the one in the public share, and the check fails otherwise -- the
-// hashed result except on a TurboSHAKE128 collision of 16-byte outputs.  Returns true if the
-// check passes; msg gets the message.
+// derived from the leader part of the public share and the helper's own part).  The message is
+// re-hashed as prio does.  Returns true if the check passes; msg gets the message.
 DEV bool prep_msg_check(const DevParams& p, const InPtrs& in, const Scratch& sc, uint32_t r,
                         const uint32_t lpart[4], uint32_t msg[4]) {
   const uint4 cor = sc.corrected[r];
-  if (p.msg_cmp) {
-    uint32_t pl[4];
-    load16(in.pub + (size_t)r * p.public_share_len, pl);
-    msg[0] = cor.x, msg[1] = cor.y, msg[2] = cor.z, msg[3] = cor.w;
-    return ((lpart[0] ^ pl[0]) | (lpart[1] ^ pl[1]) | (lpart[2] ^ pl[2]) | (lpart[3] ^ pl[3])) == 0;
-  }
   uint32_t hpart[4];
   {
     const uint4 hp = sc.part[r];
@@ -579,30 +568,23 @@ struct prio3_engine;
 // prio3_query_sum.hip: true if launched (Prio3Sum with 16 <= P <= 128)
 bool query_sum_takes(const DevParams& p);
 bool launch_query_sum(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
-                      int occ, bool leader = false);
+                      bool leader = false);
 int launch_mp64(prio3_engine* e, uint32_t n, uint32_t ld, InPtrs in, OutPtrs out, Scratch sc,
                 hipStream_t st);
 int launch_mp64_leader(prio3_engine* e, uint32_t n, uint32_t ld, InPtrs in, OutPtrs out,
                        Scratch sc, hipStream_t st);
 int launch_mp64_leader_next(uint32_t n, const uint8_t* d_prep_msgs, Scratch sc, uint8_t* d_status,
                             hipStream_t st);
-// P = 16 / 32 ParallelSum(Mul) helper query on lane pairs (prio3_query_pair.hip); false if the
-// instance is not one it takes
-bool launch_query_pair(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st);
-// prio3_query_rows.hip: Histogram K = 16, chunk 16 (P = 32) on row-split lane pairs
-bool launch_query_rows(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st);
-bool query_rows_takes(const DevParams& p);
 // long-share helper XOF on lane pairs (prio3_xof_pair.hip); false if the instance is not one it takes
 bool launch_xof_pair(const DevParams& p, InPtrs in, Scratch sc, hipStream_t st);
 // P = 64 / 128 ParallelSum(Mul) helper query, eight lanes per report (prio3_query_wide.hip);
 // false if the instance is not one it takes
-bool launch_query_wide(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
-                       int gs);
+bool launch_query_wide(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st);
 bool query_wide_takes(const DevParams& p);
 // FPVec FLP query + decide + prepare message + truncate for p.n reports (prio3_fpvec.hip)
-// gs < 0: the eight-lane kernel k_query_fpw with column group -gs
+// wide: the eight-lane kernel k_query_fpw (fpvec_query_wide_takes); leader: its agg_id-0 role
 void launch_fpvec_query(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
-                        int gs);
+                        bool wide, bool leader);
 bool fpvec_query_wide_takes(const DevParams& p);
 
 struct Slab;
@@ -654,40 +636,11 @@ struct prio3_engine {
   std::vector<hipStream_t> side;  // side streams for chunked prepare
   std::vector<hipEvent_t> side_ev;
   hipEvent_t fork_ev = nullptr;
-  int force_slow = 0;
-  int split_xof = 2;   // 2: dual-state k_xofd, 1: k_xof_a + k_jrpart, 0: generic fused k_xof
-  int fp_overlap = 0;  // option: FPVec sub-batches alternate over two side streams (A/B: slower)
-  int fp_gs = 8;       // option: FPVec query chunk-column group (loads in flight per lane): 4/8/16
-  int qh_prefetch = 1;
-  int qh_occ = 3;
-  int qh_regs = 0;
+  int force_slow = 0;     // test hook: every report through the rejection-sampling slow path
+  int force_generic = 0;  // test hook: the one-lane fallback queries (k_query_ps, k_query,
+                          // k_query_fp) that take the shapes the specialised kernels do not
   int n_cu = 256;    // compute units of the engine's GPU
   int fp_round = 1;  // FPVec sub-batches rounded to whole query rounds (fp_sub_sizes)
-  int fuse_q = 0;    // fused accumulate in k_query_h instead of k_xofd (Histogram P = 32)
-  int qsum = 1;      // Prio3Sum on k_query_sum (0: the generic k_query)
-  int qsum_occ = 3;  // k_query_sum waves per SIMD (2 or 3)
-  int msg_cmp = 0;   // prepare message by part comparison instead of a re-hash (prep_msg_check)
-  int qwide32 = 0;   // P = 32 (Histogram 256/16) on k_query_w instead of k_query_h
-  int slow_rpl = 16;  // k_xof_slow reports per lane (16; 1 = the round-1 grid)
-  int qrows = 0;      // Histogram K = 16 / chunk 16 query on row-split lane pairs (k_query_rows;
-                      // A/B: 2.86 vs 2.29 ms for k_query_h)
-  int slow_defer = 1; // Histogram P <= 32: slow path deferred to the end of the run
-                      // (VERDICT r1 item 11); 0: a k_xof_slow launch per chunk
-  int prep_fused = 1; // Histogram P = 32: XOF + query in one launch (k_prep_h); 0: two kernels
-  int qpair = 0;  // option: P = 16/32 query on lane pairs (k_query_pair; A/B: slower)
-  // option: helper XOF on lane pairs (k_xof_pair): -1 auto (shares of >= 2048 elements), 0, 1
-  int xof_pair = -1;
-  // option: P = 64/128 query on eight lanes per report (k_query_w): 1 on, 0 off (k_query_ps);
-  // qw_gs: wire columns per lane and sweep (2, 3 or 4)
-  int qwide = 1;
-  int qw_gs = 3;
-  // option: the helper XOF truncates the measurement share on the fly (SumVec under k_query_w,
-  // FPVec entry decode) instead of the query re-reading it: 1 on, 0 off
-  int trunc_xof = 1;
-  // option: FPVec query on eight lanes per report (k_query_fpw): 1 on, 0 off (k_query_fp);
-  // fp_wgs: its gadget-0 columns per lane and sweep (2, 3 or 4)
-  int fp_wide = 1;
-  int fp_wgs = 3;
   int timing = 0;
   Mp64Params mp{};  // PRIO3_SUMVEC_F64_MP only
   uint64_t* d_sigma64 = nullptr;

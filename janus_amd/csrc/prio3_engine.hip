@@ -940,7 +940,6 @@ __device__ __forceinline__ bool redo_any(const DevParams& p, const Scratch& sc, 
   }
   return any != 0;
 }
-// option slow_rpl=1: the round-1 geometry (one report per lane), kept for A/B
 template <class F>
 static void launch_xof_slow(const prio3_engine* e, const DevParams& p, const InPtrs& in,
                             const Scratch& sc, hipStream_t st);
@@ -1255,33 +1254,17 @@ __global__ __launch_bounds__(256) void k_query_ps(DevParams p, InPtrs in, Scratc
 // LEADER = 1: the leader's prepare_init (agg_id 0) on the same data flow -- the wire values
 // f_j(t), v and p(t) are written as the leader prepare share (out.prep_msgs is the prepare
 // share buffer, stride prep_share_len) instead of being decided against a peer's share.
-// FUSE: the fused accumulate rides on the query instead of the XOF (option fuse_q): the sweeps
-// load every measurement-share element exactly once, after the slow path has run, so each wave
-// whose 64 reports share one segment reduces consecutive element pairs over its reports
-// (wave_halfsum2, as k_xofd<true> does) into sc.wpart and writes its segment to sc.wseg.  The
-// query waits on memory about half its cycles, where the XOF is issue-bound.
-template <int GS, int PP, int PF = 1, int OCC = 3, int LEADER = 0, bool FUSE = false>
+template <int GS, int PP, int LEADER = 0>
 __device__ __forceinline__ void query_h_body(const DevParams& p, const InPtrs& in, const Scratch& sc,
                                              const OutPtrs& out, const uint32_t r) {
   typedef Fp128 F;
   typedef f128 T;
   constexpr int LOGP = PP <= 2 ? 1 : PP <= 4 ? 2 : PP <= 8 ? 3 : PP <= 16 ? 4 : 5;
-  static_assert(!FUSE || (GS == 2 && !LEADER), "fused pairs need two columns per sweep");
-  const uint32_t lane = threadIdx.x & 63u;
-  bool fuse = false;
-  if constexpr (FUSE) {
-    const bool valid = r < p.n;
-    const uint32_t sg = valid ? (sc.seg ? sc.seg[r] : 0u) : 0xffffffffu;
-    const uint32_t s0 = (uint32_t)__shfl((int)sg, 0);
-    // a segment id >= n_segments excludes the report from every aggregate (never fused)
-    fuse = __all(valid && sg == s0 && sg < p.nseg);
-    if (lane == 0 && (r - lane) < p.n) sc.wseg[r >> 6] = fuse ? s0 : 0xffffffffu;
-  }
   if (r >= p.n) return;
   // slow_defer: a report the XOF flagged (a rejected sample) is skipped here; after the whole
   // run, k_xof_slow re-runs its XOF (flag := 2) and this kernel runs again with p.redo = 1 for
   // exactly those reports -- no k_xof_slow launch between the XOF and the query of each chunk
-  if constexpr (!LEADER && !FUSE) {
+  if constexpr (!LEADER) {
     if (p.redo) {
       if (sc.flag[r] != 2) return;
     } else if (p.slow_defer && sc.flag[r]) {
@@ -1433,43 +1416,26 @@ __device__ __forceinline__ void query_h_body(const DevParams& p, const InPtrs& i
       }
     };
     fetch(0, mc);
-    // PF=1: the per-call coefficients beta_k, L_(k+1) of the next call are loaded together
-    // with its measurement elements, one iteration ahead (they come from L2/MALL, and
-    // loading them at their use left the waves parked on s_waitcnt).
+    // The per-call coefficients beta_k, L_(k+1) of the next call are loaded together with its
+    // measurement elements, one iteration ahead (they come from L2/MALL, and loading them at
+    // their use left the waves parked on s_waitcnt).
     T be = ldf<F>(sc.beta, 0, ld, r), Lk = ldf<F>(sc.Lbuf, 1, ld, r);
 #pragma unroll 1
     for (uint32_t k = 0; k < K; k++) {
       T mn[GS];
       fetch(k + 1, mn);
-      T be_n, L_n;
       const uint32_t kn = k + 1 < K ? k + 1 : k;
-      if constexpr (PF) {
-        be_n = ldf<F>(sc.beta, kn, ld, r);
-        L_n = ldf<F>(sc.Lbuf, kn + 1, ld, r);
-      } else {
-        be = ldf<F>(sc.beta, k, ld, r);
-        Lk = ldf<F>(sc.Lbuf, k + 1, ld, r);
-      }
+      const T be_n = ldf<F>(sc.beta, kn, ld, r), L_n = ldf<F>(sc.Lbuf, kn + 1, ld, r);
 #pragma unroll
       for (int q = 0; q < GS; q++) {
         mac_add(Aa[q], be, mc[q]);
         mac_add(Bb[q], Lk, mc[q]);
         sum_add(Ssum, mc[q]);
       }
-      if constexpr (FUSE) {
-        const uint32_t i0 = k * C + jg;  // elements i0, i0 + 1 (C even: one call)
-        if (fuse && i0 < M) {             // wave-uniform
-          const uint32_t tot = wave_halfsum2(mc[0], mc[1], lane);
-          const uint32_t e = i0 + ((lane >> 3) & 1u);
-          if (lane < 16 && e < M) sc.wpart[((size_t)(r >> 6) * M + e) * 8u + (lane & 7u)] = tot;
-        }
-      }
 #pragma unroll
       for (int q = 0; q < GS; q++) mc[q] = mn[q];
-      if constexpr (PF) {
-        be = be_n;
-        Lk = L_n;
-      }
+      be = be_n;
+      Lk = L_n;
     }
     // Wire values at t, lazily reduced: f1 = seed_(2j+1) L0 + B_j - L/2 folds the seed term into
     // B's accumulator, f0 = seed_2j L0 + r^(j+1) A_j is one two-product MAC, and the gadget
@@ -1540,10 +1506,10 @@ __device__ __forceinline__ void query_h_body(const DevParams& p, const InPtrs& i
     }
   }
 }
-template <int GS, int PP, int PF = 1, int OCC = 3, int LEADER = 0, bool FUSE = false>
-__global__ __launch_bounds__(256, OCC) void k_query_h(DevParams p, InPtrs in, Scratch sc,
-                                                    OutPtrs out) {
-  query_h_body<GS, PP, PF, OCC, LEADER, FUSE>(p, in, sc, out, blockIdx.x * blockDim.x + threadIdx.x);
+template <int GS, int PP, int LEADER = 0>
+__global__ __launch_bounds__(256, 3) void k_query_h(DevParams p, InPtrs in, Scratch sc,
+                                                  OutPtrs out) {
+  query_h_body<GS, PP, LEADER>(p, in, sc, out, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // k_prep_h<FUSE>: the whole helper prepare of Prio3Histogram with P = 32 in one launch -- the
@@ -1557,7 +1523,7 @@ __global__ __launch_bounds__(256, 3) void k_prep_h(DevParams p, InPtrs in, Scrat
                                                    OutPtrs out) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   xofd_body<FUSE, false>(p, in, sc, r);
-  query_h_body<2, 32, 1, 3, 0, false>(p, in, sc, out, r);
+  query_h_body<2, 32>(p, in, sc, out, r);
 }
 
 // k_prep_sum<NPH>: the same for Prio3Sum (P = 16 NPH): the dual-state XOF and k_query_sum's body
@@ -1572,222 +1538,6 @@ __global__ __launch_bounds__(256, 3) void k_prep_sum(DevParams p, InPtrs in, Scr
 
 
 
-
-// ------------------------------------------------------------------------------------
-// k_query_r<C, K>: the P = 32 ParallelSum(Mul, C) query (Prio3Histogram(256,16): C = K = 16)
-// with every per-call coefficient register-resident.  The Lagrange values L_1..L_K and
-// beta_k = L_(k+1) r^(Ck) never leave VGPRs (k_query_h re-read them from scratch on each of its
-// C/GS wire sweeps, ~4 KiB per report of L2-missing traffic); the sweep is wire-outer
-// (j = 0..C-1), call-inner (k unrolled), so each measurement element is loaded exactly once
-// with a rolling prefetch of QD elements.  2 waves/SIMD (256-VGPR budget).
-// ------------------------------------------------------------------------------------
-template <int C, int K, int QD = 4>
-__global__ __launch_bounds__(256, 2) void k_query_r(DevParams p, InPtrs in, Scratch sc,
-                                                   OutPtrs out) {
-  typedef Fp128 F;
-  typedef f128 T;
-  constexpr int PP = 32, GLEN = 2 * (PP - 1) + 1, A = 2 * C;
-  static_assert(K + 1 <= PP && K >= QD, "shape");
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= p.n) return;
-  const size_t ld = p.ld;
-  const uint32_t M = p.meas_len;
-  uint8_t status = PRIO3_STATUS_FINISHED;
-  const T t = ldf<F>(sc.qr, 0, ld, r);
-  // ---- Lagrange basis at t: X[idx] = L_c with c = (32 - idx) mod 32, X[2k + ph] from the
-  // ph-th decimation-in-frequency half (see k_query_h); L_c for c = 1..K is X[32 - c].
-  T L[K], L0;
-  {
-    T t16 = t;
-#pragma unroll
-    for (int i = 0; i < 4; i++) t16 = F::mul(t16, t16);
-    if (F::eq(F::mul(t16, t16), F::one())) status = PRIO3_STATUS_PREP_INIT;
-    const T ip = FC<F>::invP(p);
-    const T gy = F::mul(ip, F::add(F::one(), t16)), gz = F::mul(ip, F::sub(F::one(), t16));
-    const T tw = F::mul(t, F::from_words(p.tw128[1]));
-#pragma unroll
-    for (int ph = 0; ph < 2; ph++) {
-      T x[16];
-      T pw = ph == 0 ? gy : gz;
-      const T ratio = ph == 0 ? t : tw;
-#pragma unroll
-      for (int e = 0; e < 16; e++) {
-        x[__builtin_bitreverse32(e) >> 28] = pw;
-        if (e < 15) pw = F::mul(pw, ratio);
-      }
-      dft_reg<16, 4>(p, x, 2);
-      if (ph == 0) L0 = x[0];
-#pragma unroll
-      for (int k = 0; k < 16; k++) {
-        const int c = (32 - (2 * k + ph)) & 31;
-        if (c >= 1 && c <= K) L[c - 1] = x[k];
-      }
-    }
-  }
-  T sumL = L[0];
-#pragma unroll
-  for (int c = 1; c < K; c++) sumL = F::add(sumL, L[c]);
-  // L_1..L_K go to LDS ([k][thread], conflict-free 16-byte rows; 64 KiB per 256-thread block,
-  // two blocks per CU), beta stays in VGPRs.
-  __shared__ uint4 Ls[K][256];
-#pragma unroll
-  for (int k = 0; k < K; k++) Ls[k][threadIdx.x] = make_uint4(L[k].w[0], L[k].w[1], L[k].w[2], L[k].w[3]);
-  // ---- p(t) (Horner) and range = sum_e coef_e sigma_(e mod 32) (lazy MAC)
-  T pt = F::zero(), range;
-  {
-    mac128 R;
-    mac_zero(R);
-    constexpr int HD = 4;  // rolling prefetch of the coefficients, highest first
-    T cb[HD];
-#pragma unroll
-    for (int q = 0; q < HD; q++) cb[q] = ldf<F>(sc.proofs, A + GLEN - 1 - q, ld, r);
-#pragma unroll
-    for (int q = 0; q < GLEN; q++) {
-      const int e = GLEN - 1 - q;
-      const T ce = cb[q % HD];
-      if (q + HD < GLEN) cb[q % HD] = ldf<F>(sc.proofs, A + e - HD, ld, r);
-      pt = F::add(F::mul(pt, t), ce);
-      mac_add(R, ce, F::from_words(p.sigma128[e & (PP - 1)]));
-    }
-    range = mac_reduce_f(R);
-  }
-  // ---- beta_k = L_(k+1) r0^(Ck)
-  const T r0 = ldf<F>(sc.jr, 0, ld, r);
-  T beta[K];
-  {
-    T rC = F::one(), sq = r0;
-#pragma unroll
-    for (int e = C; e; e >>= 1) {
-      if (e & 1) rC = F::mul(rC, sq);
-      if (e > 1) sq = F::mul(sq, sq);
-    }
-    beta[0] = L[0];
-    T rk = rC;
-#pragma unroll
-    for (int k = 1; k < K; k++) {
-      beta[k] = F::mul(L[k], rk);
-      if (k + 1 < K) rk = F::mul(rk, rC);
-    }
-  }
-  const T half = FC<F>::half(p);
-  const T halfL = F::mul(half, sumL);
-  const uint8_t* lps = in.leader + (size_t)r * p.prep_share_len;
-  bool decode_ok = true;
-  auto lv = [&](uint32_t e) {
-    T x = F::load(lps, e);
-    if (!F::lt_p(x)) decode_ok = false;
-    return x;
-  };
-  // ---- wire sweep: element i = k*C + j, rolling prefetch of QD elements
-  auto ldm = [&](int j, int k) {
-    const uint32_t i = (uint32_t)(k * C + j);
-    const bool valid = j < C && i < M;
-    const uint32_t msk = valid ? 0xffffffffu : 0u;
-    const uint4 v = ((const uint4*)sc.meas)[(size_t)(valid ? i : 0) * ld + r];
-    return mk128(v.x & msk, v.y & msk, v.z & msk, v.w & msk);
-  };
-  T mb[QD];
-#pragma unroll
-  for (int q = 0; q < QD; q++) mb[q] = ldm(0, q);
-  sum128 Ssum;
-  sum_zero(Ssum);
-  mac128 Gacc;
-  mac_zero(Gacc);
-  T rj = r0;
-  // per-wire operands of the next wire (seeds, leader verifier entries), one wire ahead
-  auto ldw = [&](int j, T* w) {
-    const int jj = j < C ? j : C - 1;
-    w[0] = ldf<F>(sc.proofs, 2 * jj, ld, r);
-    w[1] = ldf<F>(sc.proofs, 2 * jj + 1, ld, r);
-    w[2] = F::load(lps, 1 + 2 * jj);
-    w[3] = F::load(lps, 2 + 2 * jj);
-  };
-  T wn[4];
-  ldw(0, wn);
-#pragma unroll 1
-  for (int j = 0; j < C; j++) {
-    T wc[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) wc[q] = wn[q];
-    ldw(j + 1, wn);
-    mac128 Aa, Bb;
-    mac_zero(Aa);
-    mac_zero(Bb);
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-      const T m = mb[k % QD];
-      // refill with element (j, k + QD) or, past the last call, (j + 1, k + QD - K)
-      mb[k % QD] = (k + QD < K) ? ldm(j, k + QD) : ldm(j + 1, k + QD - K);
-      mac_add(Aa, beta[k], m);
-      const uint4 lk = Ls[k][threadIdx.x];
-      mac_add(Bb, mk128(lk.x, lk.y, lk.z, lk.w), m);
-      sum_add(Ssum, m);
-    }
-    mac_add(Bb, wc[1], L0);
-    const T f1 = F::sub(mac_reduce_f(Bb), halfL);
-    const T Aq = mac_reduce_f(Aa);
-    mac128 F0;
-    mac_zero(F0);
-    mac_add(F0, wc[0], L0);
-    mac_add(F0, rj, Aq);
-    const T f0 = mac_reduce_f(F0);
-    if (!F::lt_p(wc[2]) || !F::lt_p(wc[3])) decode_ok = false;
-    mac_add(Gacc, F::add(wc[2], f0), F::add(wc[3], f1));
-    rj = F::mul(rj, r0);
-  }
-  const T G = mac_reduce_f(Gacc);
-  const T S = sum_reduce(Ssum);
-  T v;
-  if (p.kind == PRIO3_SUMVEC) {
-    v = range;
-  } else {
-    const T r1 = ldf<F>(sc.jr, 1, ld, r);
-    v = F::add(F::mul(r1, range), F::mul(F::mul(r1, r1), F::sub(S, half)));
-  }
-  const T V0 = F::add(lv(0), v);
-  const T PT = F::add(lv(A + 1), pt);
-  if (status == PRIO3_STATUS_FINISHED) {
-    if (!decode_ok)
-      status = PRIO3_STATUS_PREP_SHARE_DECODE;
-    else if (!F::is_zero(V0) || !F::eq(G, PT))
-      status = PRIO3_STATUS_PREP_MSG;
-  }
-  uint32_t lpart[4], hpart[4];
-  load16(lps + (size_t)p.verifier_len * F::ES, lpart);
-  {
-    uint4 hp = sc.part[r];
-    hpart[0] = hp.x;
-    hpart[1] = hp.y;
-    hpart[2] = hp.z;
-    hpart[3] = hp.w;
-  }
-  KState s;
-  kzero(s);
-  Msg mm;
-  msg_zero(mm);
-  msg_dst(mm, p.dst[6]);
-  msg_bytes16(mm, 25, lpart);
-  msg_bytes16(mm, 41, hpart);
-  msg_absorb_final(s, mm, 57);
-  uint4 cor = sc.corrected[r];
-  uint32_t msg[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
-  if (status == PRIO3_STATUS_FINISHED &&
-      (msg[0] != cor.x || msg[1] != cor.y || msg[2] != cor.z || msg[3] != cor.w))
-    status = PRIO3_STATUS_PREP_NEXT;
-  if (status != PRIO3_STATUS_FINISHED) msg[0] = msg[1] = msg[2] = msg[3] = 0;
-  ((uint4*)out.prep_msgs)[r] = make_uint4(msg[0], msg[1], msg[2], msg[3]);
-  out.status[r] = status;
-  if (p.kind == PRIO3_SUMVEC) {
-    for (uint32_t e = 0; e < p.out_len; e++) {
-      T acc = F::zero(), pw = F::one();
-      for (uint32_t b = 0; b < p.bits; b++) {
-        acc = F::add(acc, F::mul(pw, ldf<F>(sc.meas, e * p.bits + b, ld, r)));
-        pw = F::add(pw, pw);
-      }
-      F::store(sc.out, (size_t)e * ld + r, acc);
-    }
-  }
-}
 
 // ------------------------------------------------------------------------------------
 // Accumulate: masked segmented mod-p reduction of output shares
@@ -2751,10 +2501,8 @@ static void launch_xof_slow(const prio3_engine* e, const DevParams& p, const InP
 #ifdef JANUS_AB_SKIP_SLOW  // A/B build only (tools/build_variant.sh): the cost of the launch
   return;
 #endif
-  if (e->slow_rpl == 1)
-    k_xof_slow<F, 1><<<(p.n + 63) / 64, 64, 0, st>>>(p, in, sc);
-  else
-    k_xof_slow<F, 16><<<slow_blocks(p.n), 64, 0, st>>>(p, in, sc);
+  (void)e;
+  k_xof_slow<F><<<slow_blocks(p.n), 64, 0, st>>>(p, in, sc);
 }
 
 // Lays the run's buffers out from `base` (nullptr: sizes only), 256-byte aligned.
@@ -2939,7 +2687,7 @@ struct PooledStream {
 // truncate is the identity) and the joint-rand kernel streams that share.
 static bool fusable(const prio3_engine* e) {
   return e->fuse_acc && e->dp.kind == PRIO3_HISTOGRAM && e->dp.jr_len &&
-         (e->split_xof == 1 || (e->split_xof == 2 && (42 + e->dp.meas_len * 16) / 168 >= 2));
+         (42 + e->dp.meas_len * 16) / 168 >= 2;
 }
 
 // side streams + their join events and the fork event, created once per engine
@@ -2959,17 +2707,11 @@ static int ensure_side_streams(prio3_engine* e) {
 // The helper chain of this instance is the fused k_prep_h (dual-state XOF + k_query_h<2, 32>
 // in one launch; the conditions under which launch_prepare would launch exactly those two).
 static bool prep_fused_takes(const prio3_engine* e, const DevParams& dp, bool fuse) {
+  if (e->force_generic) return false;
   const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
-  const bool dual = dp.es == 16 && dp.jr_len && e->split_xof == 2 &&
-                    (42 + dp.meas_len * 16) / 168 >= 2;
-  const bool wide = ps && e->qwide && !(e->qpair && (dp.P == 32 || dp.P == 16)) &&
-                    (dp.P != 32 || e->qwide32) && query_wide_takes(dp);
-  if (e->prep_fused && e->slow_defer && dp.kind == PRIO3_SUM && dual && !fuse &&
-      e->xof_pair <= 0 && e->qsum && e->qsum_occ == 3 && query_sum_takes(dp))
-    return true;  // k_prep_sum
-  return e->prep_fused && e->slow_defer && dp.kind != PRIO3_FPVEC_BOUNDED_L2 && ps && dual &&
-         !wide && dp.P == 32 && !(fuse && e->fuse_q) && !(!fuse && e->xof_pair > 0) &&
-         !e->qh_regs && !e->qpair && !e->qrows && e->qh_prefetch == 1 && e->qh_occ == 3;
+  const bool dual = dp.es == 16 && dp.jr_len && (42 + dp.meas_len * 16) / 168 >= 2;
+  if (dp.kind == PRIO3_SUM) return dual && !fuse && query_sum_takes(dp);  // k_prep_sum
+  return ps && dual && dp.P == 32;                                         // k_prep_h
 }
 
 // which query family deferred the slow path of its flagged reports (launch_slow_redo redoes them)
@@ -3012,28 +2754,13 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
     // Sub-batches of dp.ld reports through the per-report scratch (the whole batch's meas
     // shares would not fit: 2.56 MB per report at 10^4 entries); output shares keep one
     // column per report of the batch (ld_out), so accumulate runs once over all of them.
-    // equal sub-batches (columns rounded to 256): per-lane latency, not lane count, sets a
-    // launch's duration, so 2 x 50k beats 68k + 32k
-    // Option fp_overlap: the scratch holds two column sets of half the width, and alternate
-    // sub-batches run on the two side streams, so one sub-batch's memory-latency-bound query
-    // shares the CUs with the next one's VALU-latency-bound Keccak (each alone holds < 1 wave
-    // per SIMD at 10^4 entries).
-    const uint32_t half = (dp.ld / 2) & ~255u;  // two column sets, each a multiple of 256
-    const bool two = e->fp_overlap && half > 0;
-    const uint32_t cap = two ? half : dp.ld;
+    // Equal sub-batches, cut at whole query rounds (fp_sub_sizes): per-lane latency, not lane
+    // count, sets a launch's duration.
     uint32_t nsub, sub;
-    fp_sub_sizes(e, n, cap, e->fp_wide && fpvec_query_wide_takes(dp), nsub, sub);
-    const bool ov = two && nsub > 1;  // set (si % 2) starts at column (si % 2) * cap < dp.ld
-    if (ov) {
-      int rc = ensure_side_streams(e);
-      if (rc) return rc;
-      HIPCHK(hipEventRecord(e->fork_ev, st));
-      for (auto s2 : e->side) HIPCHK(hipStreamWaitEvent(s2, e->fork_ev, 0));
-    }
+    const bool qwide = !e->force_generic && fpvec_query_wide_takes(dp);
+    fp_sub_sizes(e, n, dp.ld, qwide, nsub, sub);
     for (uint32_t si = 0; si < nsub; si++) {
       const uint32_t s0 = si * sub;
-      hipStream_t ss = ov ? e->side[si % 2] : st;
-      const size_t col = ov ? (size_t)(si % 2) * cap : 0;
       DevParams q = dp;
       q.n = si + 1 < nsub ? sub : n - s0;
       InPtrs qi = in;
@@ -3046,146 +2773,96 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
       qo.prep_msgs += 16 * (size_t)s0;
       qo.status += s0;
       Scratch qs = sc;
-      void** cols[] = {&qs.meas, &qs.proofs, &qs.jr, &qs.qr, &qs.Lbuf, &qs.PVbuf, &qs.beta};
-      for (auto c : cols) *c = (uint8_t*)*c + es * col;
-      qs.part += col;
-      qs.corrected += col;
-      qs.flag += col;
       qs.out = (uint8_t*)sc.out + es * s0;
       const uint32_t qb = (q.n + 255) / 256;
-      // k_xofd (two live Keccak states: share squeeze + joint-rand absorb) unless A/B-ed off;
-      // both dual-sponge kernels decode the entries (the output share) as they squeeze
-      const bool dual = e->split_xof == 2 && (42 + dp.meas_len * 16) / 168 >= 2;
-      q.trunc_xof = dual && e->trunc_xof ? 1u : 0u;
+      // the lane-pair XOF (k_xof_pair, the entries decoded as the share is squeezed), else the
+      // dual-state k_xofd; both decode the entries (the output share) on the fly
+      const bool dual = (42 + dp.meas_len * 16) / 168 >= 2;
+      q.trunc_xof = dual ? 1u : 0u;
       bool paired = false;
-      if (e->xof_pair != 0 && dual)
-        TIMED(e, ss, "k_xof_pair", (paired = launch_xof_pair(q, qi, qs, ss)));
-      if (paired) {
-      } else if (dual && q.trunc_xof)
-        TIMED(e, ss, "k_xofd", (k_xofd<false, true><<<qb, 256, 0, ss>>>(q, qi, qs)));
-      else if (dual)
-        TIMED(e, ss, "k_xofd", (k_xofd<false><<<qb, 256, 0, ss>>>(q, qi, qs)));
+      if (dual) TIMED(e, st, "k_xof_pair", (paired = launch_xof_pair(q, qi, qs, st)));
+      if (!paired && dual)
+        TIMED(e, st, "k_xofd", (k_xofd<false, true><<<qb, 256, 0, st>>>(q, qi, qs)));
+      else if (!paired)
+        TIMED(e, st, "k_xof", (k_xof<Fp128><<<qb, 256, 0, st>>>(q, qi, qs)));
+      TIMED(e, st, "k_xof_slow", launch_xof_slow<Fp128>(e, q, qi, qs, st));
+      if (qwide)
+        TIMED(e, st, "k_query_fpw", launch_fpvec_query(q, qi, qs, qo, st, true, false));
       else
-        TIMED(e, ss, "k_xof", (k_xof<Fp128><<<qb, 256, 0, ss>>>(q, qi, qs)));
-      TIMED(e, ss, "k_xof_slow", launch_xof_slow<Fp128>(e, q, qi, qs, ss));
-      if (e->fp_wide && fpvec_query_wide_takes(q))
-        TIMED(e, ss, "k_query_fpw", launch_fpvec_query(q, qi, qs, qo, ss, -e->fp_wgs));
-      else
-        TIMED(e, ss, "k_query_fp", launch_fpvec_query(q, qi, qs, qo, ss, e->fp_gs));
+        TIMED(e, st, "k_query_fp", launch_fpvec_query(q, qi, qs, qo, st, false, false));
     }
-    if (ov)
-      for (size_t i = 0; i < e->side.size(); i++) {
-        HIPCHK(hipEventRecord(e->side_ev[i], e->side[i]));
-        HIPCHK(hipStreamWaitEvent(st, e->side_ev[i], 0));
-      }
     return PRIO3_OK;
   }
   if (dp.es == 16) {
     const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
-    const bool wide = ps && e->qwide && !(e->qpair && (dp.P == 32 || dp.P == 16)) &&
-                      (dp.P != 32 || e->qwide32) && query_wide_takes(dp);
-    const bool pair_xof =
-        !fuse && e->xof_pair > 0;  // auto: off (SumVec 8x1000 A/B: 15.0 vs 12.8 ms, r02j)
-    const bool dual = dp.jr_len && e->split_xof == 2 && (42 + dp.meas_len * 16) / 168 >= 2;
+    // P = 64 / 128 on eight lanes per report (k_query_w)
+    const bool wide = ps && !e->force_generic && dp.P != 32 && query_wide_takes(dp);
+    const bool dual = dp.jr_len && (42 + dp.meas_len * 16) / 168 >= 2;
     // SumVec under k_query_w: the truncation rides on the XOF's squeeze (the query then reads
     // the share once)
-    dp.trunc_xof = dp.kind == PRIO3_SUMVEC && wide && dual && !fuse && e->trunc_xof ? 1u : 0u;
-    dp.msg_cmp = e->msg_cmp ? 1u : 0u;
-    bool paired = false;
-    if (dual && pair_xof)
-      TIMED(e, st, "k_xof_pair", (paired = launch_xof_pair(dp, in, sc, st)));
-    // option fuse_q: the fused accumulate in k_query_h (P = 32, two columns per sweep, even
-    // chunk) instead of k_xofd
-    const bool fuseq = fuse && e->fuse_q && dual && ps && !wide && dp.P == 32 &&
-                       (dp.chunk & 1u) == 0 && !e->qh_regs && !e->qpair;
-    // option prep_fused (default): XOF + query in one launch -- Prio3Sum (k_prep_sum) and
-    // Histogram / SumVec with P = 32 (k_prep_h)
-    if (!paired && dp.kind == PRIO3_SUM && prep_fused_takes(e, dp, fuse)) {
+    dp.trunc_xof = dp.kind == PRIO3_SUMVEC && wide && dual && !fuse ? 1u : 0u;
+    // XOF + query in one launch: Prio3Sum (k_prep_sum) and Histogram / SumVec with P = 32
+    // (k_prep_h); the slow path of both is deferred to the run's redo launch
+    if (prep_fused_takes(e, dp, fuse)) {
       dp.slow_defer = 1u;
-      if (deferred) *deferred = DEFER_SUM;
-      switch (dp.P) {
-        case 16: TIMED(e, st, "k_prep_sum", (k_prep_sum<1><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
-        case 32: TIMED(e, st, "k_prep_sum", (k_prep_sum<2><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
-        case 64: TIMED(e, st, "k_prep_sum", (k_prep_sum<4><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
-        default: TIMED(e, st, "k_prep_sum", (k_prep_sum<8><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
+      if (dp.kind == PRIO3_SUM) {
+        if (deferred) *deferred = DEFER_SUM;
+        switch (dp.P) {
+          case 16: TIMED(e, st, "k_prep_sum", (k_prep_sum<1><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
+          case 32: TIMED(e, st, "k_prep_sum", (k_prep_sum<2><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
+          case 64: TIMED(e, st, "k_prep_sum", (k_prep_sum<4><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
+          default: TIMED(e, st, "k_prep_sum", (k_prep_sum<8><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
+        }
+      } else {
+        if (deferred) *deferred = DEFER_QH;
+        if (fuse)
+          TIMED(e, st, "k_prep_h", (k_prep_h<true><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+        else
+          TIMED(e, st, "k_prep_h", (k_prep_h<false><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
       }
       return PRIO3_OK;
     }
-    if (!paired && prep_fused_takes(e, dp, fuse)) {
-      dp.slow_defer = 1u;
-      if (deferred) *deferred = DEFER_QH;
+    // two kernels: the XOF (dual-state k_xofd when the share spans >= 2 joint-rand blocks, else
+    // k_xof_a + k_jrpart), then the query
+    if (dual) {
       if (fuse)
-        TIMED(e, st, "k_prep_h", (k_prep_h<true><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
-      else
-        TIMED(e, st, "k_prep_h", (k_prep_h<false><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
-      return PRIO3_OK;
-    }
-    if (paired) {
-    } else if (dual) {
-      if (fuse && !fuseq)
         TIMED(e, st, "k_xofd", (k_xofd<true><<<blocks, 256, 0, st>>>(dp, in, sc)));
       else if (dp.trunc_xof)
         TIMED(e, st, "k_xofd", (k_xofd<false, true><<<blocks, 256, 0, st>>>(dp, in, sc)));
       else
         TIMED(e, st, "k_xofd", (k_xofd<false><<<blocks, 256, 0, st>>>(dp, in, sc)));
-    } else if (dp.jr_len && e->split_xof) {
-      TIMED(e, st, "k_xof_a", (k_xof_a<Fp128><<<blocks, 256, 0, st>>>(dp, in, sc)));
-      if (fuse)
-        TIMED(e, st, "k_jrpart", (k_jrpart<true><<<blocks, 256, 0, st>>>(dp, in, sc)));
-      else
-        TIMED(e, st, "k_jrpart", (k_jrpart<false><<<blocks, 256, 0, st>>>(dp, in, sc)));
     } else {
-      TIMED(e, st, "k_xof", (k_xof<Fp128><<<blocks, 256, 0, st>>>(dp, in, sc)));
+      TIMED(e, st, "k_xof_a", (k_xof_a<Fp128><<<blocks, 256, 0, st>>>(dp, in, sc)));
+      TIMED(e, st, "k_jrpart", (k_jrpart<false><<<blocks, 256, 0, st>>>(dp, in, sc)));
     }
-    // the query is k_query_h: flagged reports are deferred to the run's redo pass (slow_defer)
-    const bool rows = ps && e->qrows && !fuseq && !e->qh_regs && !e->qpair && !wide &&
-                      query_rows_takes(dp);
-    const bool qh_path = ps && !e->qpair && !wide && !rows &&
-                         (dp.P == 32 || dp.P == 16 || dp.P == 8) &&
-                         !(dp.P == 32 && dp.chunk == 16 && dp.calls == 16 && e->qh_regs);
-    dp.slow_defer = qh_path && !fuseq && e->slow_defer ? 1u : 0u;
-    if (dp.slow_defer && deferred) *deferred = DEFER_QH;
-    if (!dp.slow_defer) TIMED(e, st, "k_xof_slow", launch_xof_slow<Fp128>(e, dp, in, sc, st));
+    // k_query_h defers flagged reports to the run's redo pass (slow_defer); the other queries
+    // read the shares the k_xof_slow launch rewrote
+    const bool qh_path =
+        ps && !e->force_generic && !wide && (dp.P == 32 || dp.P == 16 || dp.P == 8);
+    dp.slow_defer = qh_path ? 1u : 0u;
+    if (qh_path && deferred) *deferred = DEFER_QH;
+    if (!qh_path) TIMED(e, st, "k_xof_slow", launch_xof_slow<Fp128>(e, dp, in, sc, st));
     bool done = false;
-    if (ps && e->qpair && (dp.P == 32 || dp.P == 16)) {
-      TIMED(e, st, "k_query_pair", (done = launch_query_pair(dp, in, sc, out, st)));
-    }
-    if (!done && wide)
-      TIMED(e, st, "k_query_w", (done = launch_query_wide(dp, in, sc, out, st, e->qw_gs)));
-    if (!done && rows)
-      TIMED(e, st, "k_query_rows", (done = launch_query_rows(dp, in, sc, out, st)));
+    if (wide) TIMED(e, st, "k_query_w", (done = launch_query_wide(dp, in, sc, out, st)));
     if (done) {
-    } else if (ps && dp.P == 32 && dp.chunk == 16 && dp.calls == 16 && e->qh_regs)
-      TIMED(e, st, "k_query_r", (k_query_r<16, 16><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
-    else if (fuseq)
-      TIMED(e, st, "k_query_h", (k_query_h<2, 32, 1, 3, 0, true><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
-    else if (ps && dp.P == 32)
-      switch (e->qh_prefetch * 10 + e->qh_occ) {
-        case 2: TIMED(e, st, "k_query_h", (k_query_h<2, 32, 0, 2><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
-        case 3: TIMED(e, st, "k_query_h", (k_query_h<2, 32, 0, 3><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
-        case 12: TIMED(e, st, "k_query_h", (k_query_h<2, 32, 1, 2><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
-        default: TIMED(e, st, "k_query_h", (k_query_h<2, 32, 1, 3><<<blocks, 256, 0, st>>>(dp, in, sc, out))); break;
-      }
-    else if (ps && dp.P == 16)
+    } else if (qh_path && dp.P == 32)
+      TIMED(e, st, "k_query_h", (k_query_h<2, 32><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+    else if (qh_path && dp.P == 16)
       TIMED(e, st, "k_query_h", (k_query_h<2, 16><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
-    else if (ps && dp.P == 8)
+    else if (qh_path && dp.P == 8)
       TIMED(e, st, "k_query_h", (k_query_h<2, 8><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
     else if (ps)
       TIMED(e, st, "k_query_ps", (k_query_ps<4><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
     else {
       bool qs = false;
-      if (e->qsum && query_sum_takes(dp))
-        TIMED(e, st, "k_query_sum", (qs = launch_query_sum(dp, in, sc, out, st, e->qsum_occ)));
+      if (!e->force_generic && query_sum_takes(dp))
+        TIMED(e, st, "k_query_sum", (qs = launch_query_sum(dp, in, sc, out, st)));
       if (!qs) TIMED(e, st, "k_query", (k_query<Fp128><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
     }
-  } else if (e->prep_fused && e->slow_defer) {  // Field64 (Prio3Count): one launch
+  } else {  // Field64 (Prio3Count): XOF + query in one launch, the slow path deferred
     dp.slow_defer = 1u;
     if (deferred) *deferred = DEFER_GEN64;
     TIMED(e, st, "k_prep_gen", (k_prep_gen<Fp64><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
-  } else {
-    TIMED(e, st, "k_xof", (k_xof<Fp64><<<blocks, 256, 0, st>>>(dp, in, sc)));
-    TIMED(e, st, "k_xof_slow", launch_xof_slow<Fp64>(e, dp, in, sc, st));
-    TIMED(e, st, "k_query", (k_query<Fp64><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
   }
   return PRIO3_OK;
 }
@@ -3208,7 +2885,7 @@ __global__ __launch_bounds__(64) void k_slow_redo(DevParams p, InPtrs in, Scratc
   for (uint32_t i = 0; i < REDO_RPL && r0 + i < p.n; i++)
     if (fl[i]) {
       xof_slow_one<Fp128>(p, in, sc, r0 + i);
-      query_h_body<2, PP, 1, 3, 0, false>(p, in, sc, out, r0 + i);
+      query_h_body<2, PP>(p, in, sc, out, r0 + i);
     }
 }
 
@@ -3230,20 +2907,12 @@ static int launch_slow_redo(prio3_engine* e, const DevParams& base, uint32_t n, 
   DevParams dp = base;
   dp.n = n;
   dp.force_slow = (uint32_t)e->force_slow;
-  dp.msg_cmp = e->msg_cmp ? 1u : 0u;
   dp.trunc_xof = 0;
   dp.slow_defer = 1;
   dp.redo = 1;
   const uint32_t g = redo_blocks(n);
   if (family == DEFER_GEN64) {  // k_prep_gen<Fp64>: XOF redo, then the generic query
-    if (e->slow_rpl == 2) {  // A/B: the two-launch form (k_xof_slow, then k_query with redo)
-      dp.redo = 0;
-      TIMED(e, st, "k_slow_redo", launch_xof_slow<Fp64>(e, dp, in, sc, st));
-      dp.redo = 1;
-      TIMED(e, st, "k_slow_redo",
-            (k_query<Fp64><<<(n + 255) / 256, 256, 0, st>>>(dp, in, sc, out)));
-    } else
-      TIMED(e, st, "k_slow_redo", (k_slow_redo_gen<Fp64><<<g, 64, 0, st>>>(dp, in, sc, out)));
+    TIMED(e, st, "k_slow_redo", (k_slow_redo_gen<Fp64><<<g, 64, 0, st>>>(dp, in, sc, out)));
   } else if (family == DEFER_SUM) {
     switch (dp.P) {
       case 16: TIMED(e, st, "k_slow_redo", (k_slow_redo_sum<1><<<g, 64, 0, st>>>(dp, in, sc, out))); break;
@@ -3343,7 +3012,7 @@ static int leader_init_fpvec(prio3_engine* e, Run* R, const uint8_t* d_nonces,
           (k_leader_unpack<<<(q.n + 63) / 64, 256, 0, st>>>(q, qi, qs, qo.status, nullptr, nullptr)));
     TIMED(e, st, "k_jrpart", (k_jrpart<false, true><<<blocks, 256, 0, st>>>(q, qi, qs)));
     TIMED(e, st, "k_leader_slowfix", (k_leader_slowfix<<<blocks64, 64, 0, st>>>(q, qi, qs)));
-    TIMED(e, st, "k_query_fpw", launch_fpvec_query(q, qi, qs, qo, st, -10 - e->fp_wgs));
+    TIMED(e, st, "k_query_fpw", launch_fpvec_query(q, qi, qs, qo, st, true, true));
     HIPCHK(hipMemcpyAsync(R->corr_all + s0, qs.corrected, 16 * (size_t)q.n,
                           hipMemcpyDeviceToDevice, st));
   }
@@ -3383,17 +3052,14 @@ static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
     TIMED(e, st, "k_leader_slowfix",
           (k_leader_slowfix<<<blocks64, 64, 0, st>>>(dp, in, R->sc)));
     if (dp.P == 32)
-      TIMED(e, st, "k_query_h",
-            (k_query_h<2, 32, 1, 3, 1><<<blocks, 256, 0, st>>>(dp, in, R->sc, out)));
+      TIMED(e, st, "k_query_h", (k_query_h<2, 32, 1><<<blocks, 256, 0, st>>>(dp, in, R->sc, out)));
     else if (dp.P == 16)
-      TIMED(e, st, "k_query_h",
-            (k_query_h<2, 16, 1, 3, 1><<<blocks, 256, 0, st>>>(dp, in, R->sc, out)));
+      TIMED(e, st, "k_query_h", (k_query_h<2, 16, 1><<<blocks, 256, 0, st>>>(dp, in, R->sc, out)));
     else
-      TIMED(e, st, "k_query_h",
-            (k_query_h<2, 8, 1, 3, 1><<<blocks, 256, 0, st>>>(dp, in, R->sc, out)));
+      TIMED(e, st, "k_query_h", (k_query_h<2, 8, 1><<<blocks, 256, 0, st>>>(dp, in, R->sc, out)));
     return PRIO3_OK;
   }
-  if (dp.kind == PRIO3_SUM && e->qsum && e->leader_fast && query_sum_takes(dp)) {
+  if (dp.kind == PRIO3_SUM && e->leader_fast && query_sum_takes(dp)) {
     // Prio3Sum: the same unpack / joint-rand kernels, then k_query_sum in its leader role
     InPtrs in{d_nonces, d_public_shares, d_leader_input_shares, nullptr};
     OutPtrs out{d_prep_shares, d_status};
@@ -3405,7 +3071,7 @@ static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
     TIMED(e, st, "k_leader_slowfix",
           (k_leader_slowfix<<<blocks64, 64, 0, st>>>(dp, in, R->sc)));
     bool ok = false;
-    TIMED(e, st, "k_query_sum", (ok = launch_query_sum(dp, in, R->sc, out, st, 3, true)));
+    TIMED(e, st, "k_query_sum", (ok = launch_query_sum(dp, in, R->sc, out, st, true)));
     return ok ? PRIO3_OK : PRIO3_EDEVICE;
   }
   int rc2 = PRIO3_OK;
@@ -3430,8 +3096,11 @@ uint64_t engine_group_key(const prio3_engine* e) {
   uint64_t h = 1469598103934665603ull;
   h = fnv(h, &e->params, sizeof e->params);
   h = fnv(h, &e->device, sizeof e->device);
-  const int opts[] = {e->force_slow, e->split_xof, e->fp_overlap, e->fp_gs, e->qh_prefetch,
-                      e->qh_occ,     e->qh_regs,   e->qpair,      e->xof_pair};
+  // every option that changes what a launch computes or records (an A/B set on one
+  // engine must not silently run with the lead engine's options)
+  const int opts[] = {e->force_slow, e->chunks, e->fuse_acc,           e->leader_fast,
+                      e->leader_fuse_acc, e->fp_round, e->experimental_fpvec, e->force_generic,
+                      e->timing};
   h = fnv(h, opts, sizeof opts);
   h = fnv(h, &e->fp_sub_bytes, sizeof e->fp_sub_bytes);
   // XofHmacSha256Aes128 keys enter the kernels as HMAC midstates: one engine per launch; an
@@ -3732,28 +3401,10 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
     int* field;
   } ints[] = {{"force_slow_path", &e->force_slow}, {"chunks", &e->chunks},
               {"leader_fast", &e->leader_fast},    {"fuse_acc", &e->fuse_acc},
-              {"qh_regs", &e->qh_regs},            {"qh_occ", &e->qh_occ},
-              {"slow_rpl", &e->slow_rpl},          {"qwide32", &e->qwide32},
-              {"msg_cmp", &e->msg_cmp},            {"qsum", &e->qsum},
-              {"qsum_occ", &e->qsum_occ},          {"fuse_q", &e->fuse_q},
-              {"fp_round", &e->fp_round},          {"qrows", &e->qrows},
-              {"slow_defer", &e->slow_defer},      {"prep_fused", &e->prep_fused},
-              {"qh_prefetch", &e->qh_prefetch},    {"split_xof", &e->split_xof},
-              {"qpair", &e->qpair},                {"timing", &e->timing},
+              {"fp_round", &e->fp_round},          {"timing", &e->timing},
               {"coalesce", &e->coalesce},          {"experimental_fpvec", &e->experimental_fpvec},
-              {"xof_pair", &e->xof_pair},          {"qwide", &e->qwide},
-              {"trunc_xof", &e->trunc_xof},        {"fp_wide", &e->fp_wide},
-              {"leader_fuse_acc", &e->leader_fuse_acc}};
-  if (!strcmp(key, "fp_wgs")) {
-    if (value < 2 || value > 4) return PRIO3_EINVAL;
-    e->fp_wgs = (int)value;
-    return PRIO3_OK;
-  }
-  if (!strcmp(key, "qw_gs")) {
-    if (value < 2 || value > 4) return PRIO3_EINVAL;
-    e->qw_gs = (int)value;
-    return PRIO3_OK;
-  }
+              {"leader_fuse_acc", &e->leader_fuse_acc},
+              {"force_generic_query", &e->force_generic}};
   for (auto& o : ints)
     if (!strcmp(key, o.name)) {
       *o.field = (int)value;
@@ -3762,15 +3413,6 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
   if (!strcmp(key, "fp_sub_bytes")) {  // FPVec scratch budget per sub-batch (0 = auto)
     if (value < 0) return PRIO3_EINVAL;
     e->fp_sub_bytes = value;
-    return PRIO3_OK;
-  }
-  if (!strcmp(key, "fp_overlap")) {
-    e->fp_overlap = value ? 1 : 0;
-    return PRIO3_OK;
-  }
-  if (!strcmp(key, "fp_gs")) {
-    if (value != 4 && value != 8 && value != 16) return PRIO3_EINVAL;
-    e->fp_gs = (int)value;
     return PRIO3_OK;
   }
   return PRIO3_EINVAL;

@@ -568,36 +568,18 @@ bool fpvec_query_wide_takes(const DevParams& p) {
          p.glen == 2 * p.P - 1 && p.arity == 2 * p.chunk;
 }
 
-// GS = chunk columns per pass: each pass re-reads beta_k and L_(k+1) for all K0 calls, and
-// its GS independent meas loads are the lane's memory-level parallelism (one wave per SIMD at
-// 10^4 entries, so latency, not occupancy, is what GS buys back)
+// The eight-lane k_query_fpw (three gadget-0 columns per lane and sweep: 268 K/s against 261 K/s
+// at two and 240 K/s at four, r02m), helper or leader role; the one-lane k_query_fp (eight chunk
+// columns per pass) where the eight-lane kernel does not apply.
 void launch_fpvec_query(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
-                        int gs) {
-  if (gs < -10) {  // the eight-lane kernel in its leader role: -12, -13, -14
+                        bool wide, bool leader) {
+  if (wide) {
     const uint32_t b = (p.n + 31) / 32;
-    if (gs == -14)
-      k_query_fpw<4, 1><<<b, 256, 0, st>>>(p, in, sc, out);
-    else if (gs == -12)
-      k_query_fpw<2, 1><<<b, 256, 0, st>>>(p, in, sc, out);
-    else
+    if (leader)
       k_query_fpw<3, 1><<<b, 256, 0, st>>>(p, in, sc, out);
-    return;
-  }
-  if (gs < 0) {  // the eight-lane kernel: -2, -3, -4 = its column group width
-    const uint32_t b = (p.n + 31) / 32;
-    if (gs == -4)
-      k_query_fpw<4><<<b, 256, 0, st>>>(p, in, sc, out);
-    else if (gs == -2)
-      k_query_fpw<2><<<b, 256, 0, st>>>(p, in, sc, out);
     else
       k_query_fpw<3><<<b, 256, 0, st>>>(p, in, sc, out);
     return;
   }
-  const uint32_t b = (p.n + 255) / 256;
-  if (gs >= 16)
-    k_query_fp<16><<<b, 256, 0, st>>>(p, in, sc, out);
-  else if (gs >= 8)
-    k_query_fp<8><<<b, 256, 0, st>>>(p, in, sc, out);
-  else
-    k_query_fp<4><<<b, 256, 0, st>>>(p, in, sc, out);
+  k_query_fp<8><<<(p.n + 255) / 256, 256, 0, st>>>(p, in, sc, out);
 }

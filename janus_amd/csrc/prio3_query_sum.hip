@@ -43,15 +43,13 @@ bool query_sum_takes(const DevParams& p) {
 }
 
 bool launch_query_sum(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
-                      int occ, bool leader) {
+                      bool leader) {
   if (!query_sum_takes(p) || p.n == 0) return false;
   const uint32_t blocks = (p.n + 255) / 256;
 #define QS(N)                                                             \
   do {                                                                    \
     if (leader)                                                           \
       k_query_sum<N, 3, 1><<<blocks, 256, 0, st>>>(p, in, sc, out);       \
-    else if (occ == 2)                                                    \
-      k_query_sum<N, 2><<<blocks, 256, 0, st>>>(p, in, sc, out);          \
     else                                                                  \
       k_query_sum<N, 3><<<blocks, 256, 0, st>>>(p, in, sc, out);          \
     return true;                                                          \

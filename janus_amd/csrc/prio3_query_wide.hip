@@ -52,31 +52,13 @@ bool query_wide_takes(const DevParams& p) {
   return p.calls + 1 <= p.P && p.glen == 2 * p.P - 1 && p.arity == 2 * p.chunk;
 }
 
-bool launch_query_wide(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
-                       int gs) {
-  if (!query_wide_takes(p) || p.n == 0) return false;
+// three wire columns per lane and sweep (within 5 % of two and four; the width without spills)
+bool launch_query_wide(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st) {
+  if (!query_wide_takes(p) || p.n == 0 || p.P == 32) return false;
   const uint32_t blocks = (p.n + 31) / 32;
-  if (p.P == 128) {
-    if (gs == 2)
-      k_query_w<16, 4, 2><<<blocks, 256, 0, st>>>(p, in, sc, out);
-    else if (gs == 3)
-      k_query_w<16, 4, 3><<<blocks, 256, 0, st>>>(p, in, sc, out);
-    else
-      k_query_w<16, 4, 4><<<blocks, 256, 0, st>>>(p, in, sc, out);
-    return true;
-  }
-  if (p.P == 32) {  // Prio3Histogram(256, 16): two columns per lane, one sweep
-    k_query_w<4, 2, 2><<<blocks, 256, 0, st>>>(p, in, sc, out);
-    return true;
-  }
-  if (p.P == 64) {
-    if (gs == 2)
-      k_query_w<8, 3, 2><<<blocks, 256, 0, st>>>(p, in, sc, out);
-    else if (gs == 3)
-      k_query_w<8, 3, 3><<<blocks, 256, 0, st>>>(p, in, sc, out);
-    else
-      k_query_w<8, 3, 4><<<blocks, 256, 0, st>>>(p, in, sc, out);
-    return true;
-  }
-  return false;
+  if (p.P == 128)
+    k_query_w<16, 4, 3><<<blocks, 256, 0, st>>>(p, in, sc, out);
+  else
+    k_query_w<8, 3, 3><<<blocks, 256, 0, st>>>(p, in, sc, out);
+  return true;
 }

@@ -44,7 +44,7 @@ CONFIGS = {
     "sumvec_32x20_c7": dict(kind="sumvec", bits=32, length=20, chunk_length=7),
     "hist_500_c8": dict(kind="histogram", length=500, chunk_length=8),
     "hist_1000_c10": dict(kind="histogram", length=1000, chunk_length=10),
-    # P = 32 on eight lanes (option qwide32): 20 and 25 gadget calls
+    # P = 32 with 20 and 25 gadget calls (k_prep_h with partially filled wire domains)
     "sumvec_2x100_c10": dict(kind="sumvec", bits=2, length=100, chunk_length=10),
     "hist_100_c4": dict(kind="histogram", length=100, chunk_length=4),
 }

@@ -345,23 +345,15 @@ def test_gpu_fpvec_c5_full_size():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("overlap", [1, 0])
-def test_gpu_fpvec_stream_overlapped_sub_batches(overlap):
-    """1300 reports with the whole batch's scratch: fp_overlap splits it into two column sets
-    of 512 and runs sub-batches 512 + 512 + 276 on alternating side streams; every sub-batch's
-    shares, statuses and the aggregate must equal the restatement's either way."""
+def test_gpu_fpvec_three_sub_batches():
+    """1300 reports through a scratch budget of 512 columns: sub-batches 512 + 512 + 276, each
+    one's shares, statuses and the aggregate equal to the restatement's."""
     v = _vdaf(6)
+    t = v.t
     reps = _reports(v, 1300, seed=21, distinct=130)
     _tamper(v, reps, 0.05, seed=4)
-    from janus_amd import prio3 as J
-    t = v.t
-    eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(t.length, t.bits), VK, allow_unpinned=True)
-    eng.set_option("fp_overlap", overlap)
-    A = lambda k: np.array([list(r[k]) for r in reps], np.uint8)
-    msgs, status, batch = eng.prepare_batch(A("nonce"), A("pub"), A("helper"), A("lps"))
-    outs = batch.output_shares()
-    agg, cnt = batch.accumulate()
-    _check(v, reps, (msgs, status, outs, agg, cnt))
+    per = 16 * (t.meas_len + t.proof_len + 2 + 2 + 2 * (t.P0 + t.P1) + t.K0) + 33
+    _check(v, reps, _run(v, reps, sub_bytes=per * 512 + 1, opts={"fp_round": 0}))
 
 
 @pytest.mark.gpu
@@ -402,19 +394,15 @@ def test_gpu_fpvec_requires_explicit_opt_in():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("trunc_xof", [1, 0])
-@pytest.mark.parametrize("xof_pair", [0, 1])
-def test_gpu_fpvec_xof_lane_pairs(xof_pair, trunc_xof):
-    """The FPVec share phase with and without the lane-pair XOF (the FPVec default), with the
-    entry decode (output share) done by the XOF as it squeezes or by the query, across two
-    sub-batches."""
+def test_gpu_fpvec_xof_lane_pairs():
+    """The FPVec share phase on the lane-pair XOF (k_xof_pair, the entries decoded as the share
+    is squeezed) across two sub-batches."""
     v = _vdaf(24)
     reps = _reports(v, 300, seed=23, distinct=60)
     _tamper(v, reps, 0.05, seed=6)
     t = v.t
     per = 16 * (t.meas_len + t.proof_len + 2 + 2 + 2 * (t.P0 + t.P1) + t.K0) + 33
-    _check(v, reps, _run(v, reps, sub_bytes=per * 256 + 1,
-                         opts={"xof_pair": xof_pair, "trunc_xof": trunc_xof}))
+    _check(v, reps, _run(v, reps, sub_bytes=per * 256 + 1))
 
 
 @pytest.mark.gpu
@@ -430,13 +418,13 @@ def test_gpu_fpvec_slow_path_decodes_entries(bits):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("length,opts", [
-    (24, {"fp_wide": 0}), (24, {"fp_wgs": 2}), (24, {"fp_wgs": 4}),
-    (24, {"fp_wgs": 3, "trunc_xof": 0}), (200, {"fp_wgs": 3}), (1000, {"fp_wgs": 4, "trunc_xof": 0}),
+    (24, {}), (24, {"force_generic_query": 1}), (200, {}), (1000, {}),
 ])
 def test_gpu_fpvec_query_variants(length, opts):
-    """The eight-lane FPVec query (k_query_fpw, default) at each column-group width, with the
-    entries decoded by the XOF or by the query, against the one-lane k_query_fp (fp_wide=0) and
-    the restatement; 1000 entries exercises the two-level Lagrange split (P0 = 128 -> 8 x 16)."""
+    """The eight-lane FPVec query (k_query_fpw) against the restatement, and the one-lane
+    k_query_fp that takes the domains beyond its four-step split (test hook
+    force_generic_query); 1000 entries exercises the two-level Lagrange split
+    (P0 = 128 -> 8 x 16)."""
     v = _vdaf(length)
     n = 130 if length >= 1000 else 200
     reps = _reports(v, n, seed=43 + length, distinct=5 if length >= 1000 else 40)

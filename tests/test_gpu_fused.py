@@ -92,16 +92,13 @@ def test_fused_ragged_tail_and_small_histogram():
     _run(CONFIGS["hist_100_c10"], 131, seed=6)
 
 
-@pytest.mark.parametrize("slow_defer", [1, 0])
-def test_fused_slow_path_flags(slow_defer):
-    """Every report flagged: the slow path deferred to the end of the run (slow_defer=1, the
-    default: the query skips flagged reports, k_xof_slow + a redo query after the last chunk) or
-    a k_xof_slow launch per chunk (slow_defer=0), with 2 chunks so both streams carry flags, on
-    the fused XOF + query kernel and on the two-kernel chain."""
-    for pf in (1, 0):
-        o = {"slow_defer": slow_defer, "prep_fused": pf}
-        _run(CONFIGS["hist_256_c16"], 192, seed=7, force_slow=True, opts=o)
-        _run(CONFIGS["hist_256_c16"], 700, seed=8, force_slow=True, chunks=2, opts=o)
+@pytest.mark.parametrize("chunks", [None, 2])
+def test_fused_slow_path_flags(chunks):
+    """Every report flagged: the query skips flagged reports and the run ends with one deferred
+    redo launch (k_slow_redo: the byte-level XOF, then the query); with 2 chunks both side
+    streams carry flags."""
+    _run(CONFIGS["hist_256_c16"], 192 if chunks is None else 700, seed=7 + (chunks or 0),
+         force_slow=True, chunks=chunks)
 
 
 @pytest.mark.parametrize("name", ["count", "sum8", "sumvec_8x10_c9"])
@@ -115,31 +112,22 @@ def test_fused_off_matches():
 
 
 @pytest.mark.parametrize("case", ["runs", "random", "slow", "chunks", "tampered_masked"])
-def test_fused_accumulate_in_query(case):
-    """Option fuse_q: the fused accumulate rides on k_query_h instead of k_xofd (wave pairs of
-    elements reduced as the sweeps load them) -- every fix-up path of the fused aggregate."""
-    o = {"fuse_q": 1}
+def test_fused_accumulate_fixups(case):
+    """Every fix-up path of the fused aggregate (wave partials taken in the XOF, k_agg_fix /
+    k_agg_final): segment runs inside waves, random segments (no wave fuses), the slow path,
+    stream-overlapped chunks with out-of-range segment ids, tampered and host-masked reports."""
     cfg = CONFIGS["hist_256_c16"]
     if case == "runs":
-        _run(cfg, 1500, seed=81, n_segments=7, seg_mode="runs", opts=o)
+        _run(cfg, 1500, seed=81, n_segments=7, seg_mode="runs")
     elif case == "random":
-        _run(cfg, 600, seed=82, n_segments=4, seg_mode="random", opts=o)
+        _run(cfg, 600, seed=82, n_segments=4, seg_mode="random")
     elif case == "slow":
-        _run(cfg, 192, seed=83, force_slow=True, opts=o)
+        _run(cfg, 192, seed=83, force_slow=True)
     elif case == "chunks":
-        _run(cfg, 1500, seed=84, n_segments=5, chunks=3, opts=o, oob_frac=0.02)
+        _run(cfg, 1500, seed=84, n_segments=5, chunks=3, oob_frac=0.02)
     else:
-        st = _run(cfg, 1000, seed=85, accept_frac=0.8, opts=o)
+        st = _run(cfg, 1000, seed=85, accept_frac=0.8)
         assert (st != 0).any()
-
-
-@pytest.mark.parametrize("chunks", [1, 3])
-def test_fused_wide_query_p32(chunks):
-    """The fused path with the eight-lane P = 32 query (option qwide32): tampered reports,
-    segment runs inside waves, stream-overlapped chunks, the slow path."""
-    _run(CONFIGS["hist_256_c16"], 1500, seed=60 + chunks, n_segments=5, chunks=chunks,
-         opts={"qwide32": 1})
-    _run(CONFIGS["hist_256_c16"], 192, seed=62, force_slow=True, opts={"qwide32": 1})
 
 
 @pytest.mark.parametrize("chunks", [2, 3, 5])
@@ -161,10 +149,10 @@ def test_out_of_range_segment_ids_are_excluded(name, fuse):
     _run(CONFIGS[name], 900, seed=31, n_segments=3, oob_frac=0.05, fuse=fuse)
 
 
-@pytest.mark.parametrize("opts", [{}, {"chunks": 3}, {"prep_fused": 0}])
+@pytest.mark.parametrize("opts", [{}, {"chunks": 3}])
 def test_fused_accumulate_on_fused_prepare_variants(opts):
-    """The fused accumulate (wave partials in the XOF) under the fused XOF + query kernel (one
-    launch or three stream-overlapped chunks) and the two-kernel chain: segment runs inside
-    waves, tampered reports, the host mask, every report on the deferred slow path."""
+    """The fused accumulate (wave partials in the XOF) under the fused XOF + query kernel, in one
+    launch or three stream-overlapped chunks: segment runs inside waves, tampered reports, the
+    host mask, every report on the deferred slow path."""
     _run(CONFIGS["hist_256_c16"], 3000, seed=91, n_segments=4, opts=opts)
     _run(CONFIGS["hist_256_c16"], 256, seed=92, force_slow=True, opts=opts)

@@ -100,14 +100,11 @@ def test_slow_path_parity(name):
     _check_against_oracle(CONFIGS[name], 130, seed=5, force_slow=True)
 
 
-@pytest.mark.parametrize("opts", [{"slow_defer": 0}, {"qrows": 1}, {"prep_fused": 0},
-                                  {"chunks": 3}])
 @pytest.mark.parametrize("name", ["hist_256_c16", "hist_10_c3"])
-def test_slow_path_launch_variants(name, opts):
-    """The slow path as a k_xof_slow launch between the XOF and the query (slow_defer=0, or under
-    k_query_rows), deferred after the two-kernel chain (prep_fused=0) or after stream-overlapped
-    chunks, besides the default (deferred after the fused XOF + query kernel)."""
-    _check_against_oracle(CONFIGS[name], 130, seed=6, force_slow=True, opts=opts)
+def test_slow_path_over_chunks(name):
+    """Every report on the slow path with the batch cut into three stream-overlapped chunks: the
+    deferred redo launch runs once after the last chunk."""
+    _check_against_oracle(CONFIGS[name], 130, seed=6, force_slow=True, opts={"chunks": 3})
 
 
 @pytest.mark.parametrize("name", ["count", "hist_256_c16", "sumvec_8x10_c9"])
@@ -218,82 +215,35 @@ def test_full_size_histogram_unshard_property():
     assert tot == exp
 
 
-@pytest.mark.parametrize("name", ["sumvec_8x10_c9", "hist_256_c16", "sum32", "sumvec_8x1000_c63"])
-@pytest.mark.parametrize("force_slow", [False, True])
-def test_xof_pair_parity(name, force_slow):
-    """The two-lanes-per-report XOF (k_xof_pair: share squeeze and joint-rand-part absorb in the
-    two lanes of a pair, DPP-linked) forced on for short shares too, with ragged tails."""
-    n = 70 if "1000" in name else 301
-    _check_against_oracle(CONFIGS[name], n, seed=13, force_slow=force_slow, opts={"xof_pair": 1})
-
-
-@pytest.mark.parametrize("name", ["hist_256_c16", "hist_100_c10", "sumvec_8x10_c9"])
-def test_query_pair_parity(name):
-    """The lane-pair query (k_query_pair, option qpair) stays bit-exact (off by default)."""
-    _check_against_oracle(CONFIGS[name], 333, seed=17, opts={"qpair": 1})
-
-
 WIDE = ["sumvec_8x1000_c63", "sumvec_4x100_c10", "sumvec_32x20_c7", "hist_500_c8",
         "hist_1000_c10"]
 
 
-@pytest.mark.parametrize("gs", [2, 3, 4])
 @pytest.mark.parametrize("name", WIDE)
-def test_query_wide_parity(name, gs):
-    """P = 64/128 ParallelSum query on eight lanes per report (k_query_w): every column-group
-    width, tampered reports, a batch that is not a multiple of the 32 reports of a block."""
+def test_query_wide_parity(name):
+    """P = 64/128 ParallelSum query on eight lanes per report (k_query_w, three columns per lane
+    and sweep): tampered reports, a batch that is not a multiple of the 32 reports of a block;
+    then every report through the slow path (the rejection-sampling XOF feeds k_query_w)."""
     n = 101 if "1000" in name else 333
-    _check_against_oracle(CONFIGS[name], n, seed=19 + gs, opts={"qwide": 1, "qw_gs": gs})
+    _check_against_oracle(CONFIGS[name], n, seed=21, opts={})
+    _check_against_oracle(CONFIGS[name], 70 if "1000" in name else 200, seed=29, force_slow=True)
 
 
-@pytest.mark.parametrize("opts", [{"msg_cmp": 1}, {"msg_cmp": 1, "qwide32": 1},
-                                  {"msg_cmp": 1, "chunks": 3, "coalesce": 0}])
-@pytest.mark.parametrize("name", ["hist_256_c16", "sumvec_8x1000_c63", "hist_500_c8"])
-def test_prepare_message_by_part_comparison(name, opts):
-    """Option msg_cmp: the prepare message is the corrected seed when the leader's joint-rand
-    part in its prep share equals the public share's (prep_msg_check), the same bytes and
-    statuses as re-hashing the parts, tampered parts and public shares included."""
-    n = 101 if "1000" in name else 700
-    _check_against_oracle(CONFIGS[name], n, seed=59, opts=opts)
-
-
-@pytest.mark.parametrize("occ", [3, 2])
 @pytest.mark.parametrize("name", ["sum8", "sum15", "sum17", "sum32", "sum50", "sum64"])
-def test_query_sum_parity(name, occ):
+def test_query_sum_parity(name):
     """Prio3Sum on k_query_sum (P = 16..128 as NPH phases of an in-register DFT16; the
-    validity weights with 16 | bits applied per phase, else per element): tampered reports,
-    the slow path, and the generic k_query it replaces."""
-    _check_against_oracle(CONFIGS[name], 700, seed=61, opts={"qsum_occ": occ})
-    if occ == 3:
-        _check_against_oracle(CONFIGS[name], 130, seed=67, force_slow=True)
-        _check_against_oracle(CONFIGS[name], 300, seed=71, opts={"qsum": 0})
-
-
-@pytest.mark.parametrize("name", ["hist_256_c16", "sumvec_2x100_c10", "hist_100_c4"])
-def test_query_wide_p32_parity(name):
-    """P = 32 on eight lanes (option qwide32, k_query_w<4, 2, 2>): two columns per lane in one
-    sweep; the headline Histogram(256, 16) instance, fused and unfused, with the slow path."""
-    _check_against_oracle(CONFIGS[name], 333, seed=43, opts={"qwide32": 1})
-    _check_against_oracle(CONFIGS[name], 97, seed=47, opts={"qwide32": 1}, force_slow=True)
-    _check_against_oracle(CONFIGS[name], 300, seed=53, opts={"qwide32": 1, "fuse_acc": 0})
-
-
-@pytest.mark.parametrize("name", ["sumvec_8x1000_c63", "hist_500_c8"])
-def test_query_wide_off_and_slow_path(name):
-    """The one-lane k_query_ps stays selectable; the rejection-sampling XOF feeds k_query_w."""
-    n = 70 if "1000" in name else 200
-    _check_against_oracle(CONFIGS[name], n, seed=23, opts={"qwide": 0})
-    _check_against_oracle(CONFIGS[name], n, seed=29, force_slow=True)
-    _check_against_oracle(CONFIGS[name], n, seed=31, opts={"trunc_xof": 0})
+    validity weights with 16 | bits applied per phase, else per element): tampered reports and
+    the slow path."""
+    _check_against_oracle(CONFIGS[name], 700, seed=61)
+    _check_against_oracle(CONFIGS[name], 130, seed=67, force_slow=True)
 
 
 @pytest.mark.parametrize("name", ["sumvec_8x1000_c63", "sumvec_32x20_c7"])
-def test_truncate_in_xof_chunked_and_paired(name):
+def test_truncate_in_xof_chunked(name):
     """SumVec under k_query_w truncates inside the XOF: over stream-overlapped chunks (the
-    output-share columns of every chunk) and on the lane-pair XOF."""
+    output-share columns of every chunk)."""
     n = 600 if "1000" in name else 1500
     _check_against_oracle(CONFIGS[name], n, seed=37, opts={"coalesce": 0, "chunks": 3})
-    _check_against_oracle(CONFIGS[name], n // 3, seed=41, opts={"xof_pair": 1})
 
 
 HIST_ROWS = {"hist_256_c16": CONFIGS["hist_256_c16"],
@@ -303,58 +253,58 @@ HIST_ROWS = {"hist_256_c16": CONFIGS["hist_256_c16"],
 
 @pytest.mark.parametrize("n", [1, 127, 700])
 @pytest.mark.parametrize("name", list(HIST_ROWS))
-def test_query_rows_parity(name, n):
-    """Histogram with 16 calls of chunk 16 (P = 32) on row-split lane pairs (k_query_rows, the
-    default): tampered reports (decide, decode, joint-rand and public-share failures), a share
-    shorter than K x C (masked rows), odd and sub-block batch sizes; then the same batch on the
-    one-lane k_query_h (qrows=0)."""
-    cfg = HIST_ROWS[name]
-    _check_against_oracle(cfg, n, seed=71 + n, tamper=n > 100, opts={"qrows": 1})
-    _check_against_oracle(cfg, n, seed=71 + n, tamper=n > 100, opts={"qrows": 0})
+def test_query_h_shapes(name, n):
+    """Histogram with 16 calls of chunk 16 (P = 32) on k_prep_h: tampered reports (decide,
+    decode, joint-rand and public-share failures), a share shorter than K x C (masked rows),
+    odd and sub-block batch sizes."""
+    _check_against_oracle(HIST_ROWS[name], n, seed=71 + n, tamper=n > 100)
 
 
-@pytest.mark.parametrize("opts", [{"qrows": 1, "chunks": 3}, {"qrows": 1, "msg_cmp": 1}])
-def test_query_rows_with_options(opts):
-    """k_query_rows under stream-overlapped chunks and the prepare message by comparison."""
-    _check_against_oracle(CONFIGS["hist_256_c16"], 900, seed=77, opts=opts)
-
-
-@pytest.mark.parametrize("opts", [{"prep_fused": 1}, {"prep_fused": 1, "chunks": 3},
-                                  {"prep_fused": 0}, {"prep_fused": 0, "slow_defer": 0}])
+@pytest.mark.parametrize("opts", [{}, {"chunks": 3}])
 @pytest.mark.parametrize("name", ["hist_256_c16", "sumvec_2x100_c10", "hist_100_c4"])
 def test_fused_prepare_kernel_parity(name, opts):
     """P = 32 ParallelSum(Mul) (Histogram with 16 and 25 calls, SumVec with 20): the XOF and the
-    query in one launch (k_prep_h, the default; one chunk or three stream-overlapped ones) and
-    the two-kernel chain with the slow path deferred or per chunk, on tampered ragged batches."""
+    query in one launch (k_prep_h; one chunk or three stream-overlapped ones), on tampered ragged
+    batches, with and without the fused accumulate, and every report on the deferred slow path."""
     _check_against_oracle(CONFIGS[name], 777, seed=83, opts=opts)
+    _check_against_oracle(CONFIGS[name], 300, seed=53, opts=dict(opts, fuse_acc=0))
+    _check_against_oracle(CONFIGS[name], 97, seed=47, force_slow=True, opts=opts)
 
 
-
-
-@pytest.mark.parametrize("opts", [{}, {"prep_fused": 0}, {"chunks": 3}])
 @pytest.mark.parametrize("name", ["sum8", "sum15", "sum32", "sum50", "sum64"])
-def test_fused_sum_prepare_parity(name, opts):
-    """Prio3Sum (P = 16..128) with the XOF and k_query_sum's body in one launch (k_prep_sum, the
-    default; one chunk or three), and the two-kernel chain, on tampered ragged batches; every
-    report through the deferred slow path (k_slow_redo_sum)."""
-    _check_against_oracle(CONFIGS[name], 555, seed=89, opts=opts)
-    _check_against_oracle(CONFIGS[name], 130, seed=90, force_slow=True, opts=opts)
+def test_fused_sum_prepare_chunked(name):
+    """Prio3Sum (P = 16..128; k_prep_sum from 19 bits, where the share spans two joint-rand
+    blocks) in three stream-overlapped chunks, on tampered ragged batches; every report through
+    the deferred slow path (k_slow_redo_sum) once after the last chunk."""
+    _check_against_oracle(CONFIGS[name], 555, seed=89, opts={"chunks": 3})
+    _check_against_oracle(CONFIGS[name], 130, seed=90, force_slow=True, opts={"chunks": 3})
 
 
-@pytest.mark.parametrize("opts", [{}, {"prep_fused": 0}, {"chunks": 3}])
 @pytest.mark.parametrize("name", ["sumvec_8x1000_c63", "sumvec_4x100_c10", "sumvec_32x20_c7"])
-def test_sumvec_wide_prepare_options_parity(name, opts):
+def test_sumvec_wide_prepare_chunked(name):
     """SumVec on the eight-lane query (P = 64 / 128): the two-kernel chain (its XOF truncating on
-    the fly), under every launch option, with every report through the slow path."""
+    the fly) in three chunks, with every report through the slow path."""
     n = 101 if "1000" in name else 333
-    _check_against_oracle(CONFIGS[name], n, seed=93, opts=opts)
-    _check_against_oracle(CONFIGS[name], 70, seed=94, force_slow=True, opts=opts)
+    _check_against_oracle(CONFIGS[name], n, seed=93, opts={"chunks": 3})
+    _check_against_oracle(CONFIGS[name], 70, seed=94, force_slow=True, opts={"chunks": 3})
 
 
-@pytest.mark.parametrize("opts", [{}, {"prep_fused": 0}, {"chunks": 3}, {"slow_rpl": 2}])
+@pytest.mark.parametrize("opts", [{}, {"chunks": 3}])
 def test_fused_count_prepare_parity(opts):
-    """Prio3Count (Field64) with the generic XOF and query in one launch (k_prep_gen, the default)
-    and on two kernels, on a tampered ragged batch and with every report on the slow path (its
-    redo in one k_slow_redo_gen launch, or, slow_rpl = 2, as k_xof_slow + k_query)."""
+    """Prio3Count (Field64) with the generic XOF and query in one launch (k_prep_gen) on a
+    tampered ragged batch and with every report on the slow path (its redo in one
+    k_slow_redo_gen launch)."""
     _check_against_oracle(CONFIGS["count"], 999, seed=95, opts=opts)
     _check_against_oracle(CONFIGS["count"], 130, seed=96, force_slow=True, opts=opts)
+
+
+@pytest.mark.parametrize("name", ["hist_256_c16", "hist_10_c3", "sum32", "sum8",
+                                  "sumvec_4x100_c10", "sumvec_8x1000_c63"])
+def test_generic_fallback_queries(name):
+    """The one-lane fallback queries (k_query_ps for ParallelSum at any P, the generic k_query for
+    Prio3Sum) that take the shapes the specialised kernels do not, forced on through the test
+    hook force_generic_query: tampered ragged batches and every report on the slow path."""
+    n = 70 if "1000" in name else 300
+    _check_against_oracle(CONFIGS[name], n, seed=97, opts={"force_generic_query": 1})
+    _check_against_oracle(CONFIGS[name], 64, seed=98, force_slow=True,
+                          opts={"force_generic_query": 1})
