@@ -63,6 +63,7 @@ def lib():
         L.orc_agg_merge.argtypes = [P(OrcParams), u8p, u8p]
         L.orc_gen_reports.argtypes = [P(OrcParams), u8p, C.c_uint32, C.c_uint64, C.c_int,
                                       u8p, u8p, u8p, u8p, P(C.c_uint64), u8p]
+        L.orc_prim_bench.argtypes = [P(C.c_double), P(C.c_double)]
         _lib = L
     return _lib
 
@@ -218,6 +219,13 @@ class Oracle:
         if p.public_share_len == 0:
             d["public_shares"] = np.zeros((n, 0), np.uint8)
         return d
+
+
+def prim_bench():
+    """(ns per Keccak-p[1600,12] permutation, ns per Field128 multiply) on one core."""
+    a, b = C.c_double(), C.c_double()
+    lib().orc_prim_bench(C.byref(a), C.byref(b))
+    return a.value, b.value
 
 
 def field_modulus(kind: str) -> int:

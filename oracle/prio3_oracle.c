@@ -13,10 +13,12 @@
 #include "prio3_oracle.h"
 
 #include <openssl/evp.h>
+#include <malloc.h>
 #include <pthread.h>
 #include <stdatomic.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 typedef unsigned __int128 u128;
 
@@ -87,10 +89,17 @@ static void sp_init(sponge* t, int rounds) {
   t->rounds = rounds;
 }
 static inline uint8_t* sp_bytes(sponge* t) { return (uint8_t*)t->s; } /* little-endian host */
+/* Absorb and squeeze a block's worth of bytes at a time (the rate region is XORed / copied as one
+ * run), as the sha3 crate's sponge does, not byte by byte. */
 static void sp_absorb(sponge* t, const uint8_t* d, size_t n) {
   uint8_t* b = sp_bytes(t);
-  while (n--) {
-    b[t->pos++] ^= *d++;
+  while (n) {
+    size_t k = TS_RATE - t->pos;
+    if (k > n) k = n;
+    for (size_t i = 0; i < k; i++) b[t->pos + i] ^= d[i];
+    t->pos += (uint32_t)k;
+    d += k;
+    n -= k;
     if (t->pos == TS_RATE) {
       orc_keccak_p1600(t->s, t->rounds);
       t->pos = 0;
@@ -105,13 +114,18 @@ static void sp_finalize(sponge* t, uint8_t domain) {
   t->pos = 0;
 }
 static void sp_squeeze(sponge* t, uint8_t* out, size_t n) {
-  uint8_t* b = sp_bytes(t);
-  while (n--) {
+  const uint8_t* b = sp_bytes(t);
+  while (n) {
     if (t->pos == TS_RATE) {
       orc_keccak_p1600(t->s, t->rounds);
       t->pos = 0;
     }
-    *out++ = b[t->pos++];
+    size_t k = TS_RATE - t->pos;
+    if (k > n) k = n;
+    memcpy(out, b + t->pos, k);
+    t->pos += (uint32_t)k;
+    out += k;
+    n -= k;
   }
 }
 
@@ -734,19 +748,49 @@ static int fpvec_query(const fld* F, const orc_params* p, const fe* meas, const 
   memset(fold, 0, sizeof(fe) * (P0 > P1 ? P0 : P1));
   for (uint32_t i = 0; i < G1; i++) fold[i % P1] = f_add(F, fold[i % P1], c1[i]);
   dft(F, pr1, fold, P1, P1);
-  /* valid(): wire values of each call recorded (row 0 = the proof's seeds) */
-  fe* w0 = (fe*)calloc((size_t)A0 * (K0 + 1), sizeof(fe));
-  fe* w1 = (fe*)calloc((size_t)C1 * (K1 + 1), sizeof(fe));
-  for (uint32_t w = 0; w < A0; w++) w0[(size_t)w * (K0 + 1)] = s0[w];
-  for (uint32_t w = 0; w < C1; w++) w1[(size_t)w * (K1 + 1)] = s1[w];
+  /* Lagrange basis at t: L_c(t) = alpha^c (t^P - 1) / (P (t - alpha^c)), c = 0..K, with one
+   * field inversion per gadget (batch inversion of the t - alpha^c) */
+  const uint32_t KM = K0 > K1 ? K0 : K1;
+  fe* L0 = (fe*)malloc(sizeof(fe) * (KM + 1) * 3);
+  fe *Lg = L0, *pre = L0 + (KM + 1), *den = L0 + 2 * (KM + 1);
+  fe* Lb1 = (fe*)malloc(sizeof(fe) * (K1 + 1));
+  for (int g = 0; g < 2; g++) {
+    const uint32_t P = g ? P1 : P0, K = g ? K1 : K0;
+    const fe t = g ? t1 : t0;
+    fe* L = g ? Lb1 : Lg;
+    const fe num = f_mul(F, f_sub(F, f_pow(F, t, P), 1), f_inv(F, P)), a = f_root(F, (int)log2u(P));
+    fe ac = 1, acc = 1;
+    for (uint32_t c = 0; c <= K; c++) {
+      den[c] = f_sub(F, t, ac);
+      pre[c] = acc;  /* product of den[0..c-1] */
+      acc = f_mul(F, acc, den[c]);
+      L[c] = ac;
+      ac = f_mul(F, ac, a);
+    }
+    fe inv = f_inv(F, acc);  /* 1 / prod den */
+    for (uint32_t c = K + 1; c-- > 0;) {
+      const fe ic = f_mul(F, inv, pre[c]);  /* 1 / den[c] */
+      inv = f_mul(F, inv, den[c]);
+      L[c] = f_mul(F, f_mul(F, L[c], ic), num);
+    }
+  }
+  /* valid() with each gadget call's wire values folded straight into the wire polynomials at t
+   * (f_w(t) = sum_c L_c(t) w[c], row c = 0 the proof's seeds): gadget 0's wires 2j, 2j+1 carry
+   * r^(i+1) m_i and m_i - 1/2 (i = k C0 + j, m = 0 past the share), gadget 1's wire j the
+   * decoded entry k C1 + j (0 past the last) */
+  fe* out0 = ver + 1;
+  fe* out1 = ver + 2 + A0;
+  for (uint32_t w = 0; w < A0; w++) out0[w] = f_mul(F, Lg[0], s0[w]);
+  for (uint32_t w = 0; w < C1; w++) out1[w] = f_mul(F, Lb1[0], s1[w]);
   const fe sinv = f_inv(F, 2);
   fe rng = 0, rp = jr[0];
   for (uint32_t k = 0; k < K0; k++) {
+    const fe Lk = Lg[k + 1];
     for (uint32_t j = 0; j < C0; j++) {
       const uint32_t i = k * C0 + j;
       const fe m = i < M ? meas[i] : 0;
-      w0[(size_t)(2 * j) * (K0 + 1) + k + 1] = f_mul(F, rp, m);
-      w0[(size_t)(2 * j + 1) * (K0 + 1) + k + 1] = f_sub(F, m, sinv);
+      out0[2 * j] = f_add(F, out0[2 * j], f_mul(F, Lk, f_mul(F, rp, m)));
+      out0[2 * j + 1] = f_add(F, out0[2 * j + 1], f_mul(F, Lk, f_sub(F, m, sinv)));
       rp = f_mul(F, rp, jr[0]);
     }
     rng = f_add(F, rng, pr0[k + 1]);
@@ -758,7 +802,7 @@ static int fpvec_query(const fld* F, const orc_params* p, const fe* meas, const 
       fe y = 0;
       if (e < E)
         for (uint32_t b = n; b-- > 0;) y = f_add(F, f_add(F, y, y), meas[n * e + b]);
-      w1[(size_t)j * (K1 + 1) + k + 1] = y;
+      out1[j] = f_add(F, out1[j], f_mul(F, Lb1[k + 1], y));
     }
     norm = f_add(F, norm, pr1[k + 1]);
   }
@@ -767,33 +811,13 @@ static int fpvec_query(const fld* F, const orc_params* p, const fe* meas, const 
   for (uint32_t b = 2 * n - 2; b-- > 0;) claimed = f_add(F, f_add(F, claimed, claimed), meas[n * E + b]);
   ver[0] = f_add(F, f_mul(F, jr[1], rng),
                  f_mul(F, f_mul(F, jr[1], jr[1]), f_sub(F, norm, claimed)));
-  /* wire polynomials at t: sum_c L_c(t) w[c], L_c(t) = alpha^c (t^P - 1) / (P (t - alpha^c)) */
-  for (int g = 0; g < 2; g++) {
-    const uint32_t P = g ? P1 : P0, K = g ? K1 : K0, A = g ? C1 : A0;
-    const fe t = g ? t1 : t0;
-    const fe* w = g ? w1 : w0;
-    fe* L = (fe*)malloc(sizeof(fe) * (K + 1));
-    const fe num = f_mul(F, f_sub(F, f_pow(F, t, P), 1), f_inv(F, P)), a = f_root(F, (int)log2u(P));
-    fe ac = 1;
-    for (uint32_t c = 0; c <= K; c++) {
-      L[c] = f_mul(F, f_mul(F, ac, f_inv(F, f_sub(F, t, ac))), num);
-      ac = f_mul(F, ac, a);
-    }
-    fe* out = ver + (g ? 2 + A0 : 1);
-    for (uint32_t x = 0; x < A; x++) {
-      fe acc = 0;
-      for (uint32_t c = 0; c <= K; c++) acc = f_add(F, acc, f_mul(F, L[c], w[(size_t)x * (K + 1) + c]));
-      out[x] = acc;
-    }
-    free(L);
-  }
+  free(L0);
+  free(Lb1);
   ver[1 + A0] = poly_eval(F, c0, G0, t0);
   ver[2 + A0 + C1] = poly_eval(F, c1, G1, t1);
   free(fold);
   free(pr0);
   free(pr1);
-  free(w0);
-  free(w1);
   return 0;
 }
 
@@ -1271,12 +1295,23 @@ static void* batch_worker(void* arg) {
   return NULL;
 }
 
+/* The per-report buffers of the long instances (FPVec: a 2.56 MB measurement share and its
+ * encoding) come from the heap arenas and are reused, not mmap'ed and unmapped per report: with
+ * several worker threads each munmap's TLB shootdown stalls every thread (8 threads ran 4.4x
+ * slower per report than one). */
+static pthread_once_t malloc_once = PTHREAD_ONCE_INIT;
+static void malloc_setup(void) {
+  mallopt(M_MMAP_THRESHOLD, 256 << 20);
+  mallopt(M_TRIM_THRESHOLD, 1 << 30);
+}
+
 int orc_helper_batch(const orc_params* p, const uint8_t* vk, uint32_t n,
                      const uint8_t* nonces, const uint8_t* public_shares,
                      const uint8_t* helper_shares, const uint8_t* leader_prep_shares,
                      const uint32_t* segment_ids, const uint8_t* accept_mask,
                      uint32_t n_segments, uint8_t* prep_msgs_out, uint8_t* status_out,
                      uint8_t* agg_out, uint64_t* count_out, int n_threads, int job_size) {
+  pthread_once(&malloc_once, malloc_setup);
   if (n_threads < 1) n_threads = 1;
   if (job_size < 1) job_size = 500;
   if (n_segments < 1) n_segments = 1;
@@ -1508,4 +1543,25 @@ int orc_gen_reports(const orc_params* p, const uint8_t vk[16], uint32_t n, uint6
   for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
   free(th);
   return 0;
+}
+
+/* Single-core cost of the two primitives the CPU baseline's per-report time is made of (bench.py
+ * reports the op-count estimate beside the measured time): one Keccak-p[1600, 12] permutation
+ * and one Field128 multiply, in ns. */
+void orc_prim_bench(double* ns_perm, double* ns_mul) {
+  struct timespec a, b;
+  uint64_t st[25] = {1, 2, 3};
+  const int NP = 200000, NM = 4000000;
+  clock_gettime(CLOCK_MONOTONIC, &a);
+  for (int i = 0; i < NP; i++) orc_keccak_p1600(st, 12);
+  clock_gettime(CLOCK_MONOTONIC, &b);
+  *ns_perm = ((b.tv_sec - a.tv_sec) * 1e9 + (b.tv_nsec - a.tv_nsec)) / NP;
+  volatile u128 sink;
+  u128 x = ((u128)st[0] << 64 | st[1]) % P128, y = ((u128)st[2] << 64 | st[3]) % P128;
+  clock_gettime(CLOCK_MONOTONIC, &a);
+  for (int i = 0; i < NM; i++) x = f128_mul(x, y);  /* a dependent chain, like Horner / MACs */
+  clock_gettime(CLOCK_MONOTONIC, &b);
+  sink = x;
+  (void)sink;
+  *ns_mul = ((b.tv_sec - a.tv_sec) * 1e9 + (b.tv_nsec - a.tv_nsec)) / NM;
 }

@@ -130,6 +130,9 @@ int orc_gen_reports(const orc_params* p, const uint8_t vk[16], uint32_t n, uint6
 /* Mod-p element-wise sum of agg shares (AggregateShare::merge). */
 void orc_agg_merge(const orc_params* p, uint8_t* acc, const uint8_t* other);
 
+/* ns per Keccak-p[1600, 12] permutation and per Field128 multiply on one core */
+void orc_prim_bench(double* ns_perm, double* ns_mul);
+
 #ifdef __cplusplus
 }
 #endif
