@@ -173,6 +173,9 @@ def main():
                     help="--role jobs: host worker threads (Janus's rayon pool)")
     ap.add_argument("--job-size", type=int, default=500,
                     help="--role jobs: reports per aggregation job (aggregation_job_creator.rs:63-64)")
+    ap.add_argument("--jobs-call", choices=["combined", "two"], default="combined",
+                    help="--role jobs: prio3_helper_prepare_aggregate_batch per job (one round "
+                         "trip) or prio3_helper_prepare_batch + prio3_accumulate (two)")
     ap.add_argument("--tasks", type=int, default=4,
                     help="--role jobs: tasks (verify keys) of the VDAF instance the jobs rotate over")
     ap.add_argument("--opt", action="append", default=[],
@@ -430,19 +433,20 @@ def jobs_main(args):
     lib.janus_jobs_run.restype = C.c_double
     vp = C.c_void_p
     lib.janus_jobs_run.argtypes = [C.POINTER(vp), C.c_int, vp, C.c_int, C.c_int, C.c_int,
-                                   C.c_uint32, vp, vp, vp, vp, vp, vp, vp]
+                                   C.c_uint32, vp, vp, vp, vp, vp, vp, vp, C.c_int]
     eng_arr = (vp * K)(*[e.handle.value for e in engines])
     status = np.zeros(n_jobs * js, np.uint8)
     counts = np.zeros(n_jobs, np.uint64)
-    agg = np.zeros(sz.agg_share_len, np.uint8)
+    agg = np.zeros((n_jobs, sz.agg_share_len), np.uint8)
     P = lambda a: a.ctypes.data_as(vp)
+    combined = args.jobs_call == "combined"
 
     def run(jobs):
         status[:] = 0xFF
         return lib.janus_jobs_run(eng_arr, K, C.cast(C.pointer(sz), vp), T, jobs, js, pool,
                                   P(host["nonces"]), P(host["public_shares"]),
                                   P(host["helper_shares"]), P(host["leader_prep_shares"]),
-                                  P(status), P(counts), P(agg))
+                                  P(status), P(counts), P(agg), int(combined))
 
     run(max(K, min(n_jobs, 8 * T)))  # warmup: pools, pinned staging, streams
     for e in engines:
@@ -454,16 +458,26 @@ def jobs_main(args):
     # the prepare launches: the fused XOF + query (k_prep_h) or, on the two-kernel chain, k_xofd
     launches = sum(e.timing().get(k, (0, 0))[1] for e in engines for k in ("k_prep_h", "k_xofd"))
     value = n_jobs * js / dt
-    # spot check: the last job's aggregate against the restatement
+    # every job against the restatement: per task, the jobs' report windows concatenated with
+    # segment id = the job, so each segment of the oracle's batch is one job's aggregate
     from oracle.oracle import Oracle
     o = Oracle("histogram", length=256, chunk_length=16)
-    j = n_jobs - 1
-    t = j % K
-    r0 = t * pool + ((j // K) * js) % (pool - js + 1)
-    sl = slice(r0, r0 + js)
-    _, rst, ragg, rcnt = o.helper_batch(vks[t], host["nonces"][sl], host["public_shares"][sl],
-                                        host["helper_shares"][sl],
-                                        host["leader_prep_shares"][sl], n_threads=cpu_threads())
+    t_chk = time.perf_counter()
+    jobs_ok = True
+    statuses_ok = True
+    for t in range(K):
+        jl = list(range(t, n_jobs, K))
+        r0s = [t * pool + ((j // K) * js) % (pool - js + 1) for j in jl]
+        idx = np.concatenate([np.arange(r, r + js) for r in r0s])
+        seg = np.repeat(np.arange(len(jl), dtype=np.uint32), js)
+        _, rst, ragg, rcnt = o.helper_batch(
+            vks[t], host["nonces"][idx], host["public_shares"][idx], host["helper_shares"][idx],
+            host["leader_prep_shares"][idx], segment_ids=seg, n_segments=len(jl),
+            n_threads=cpu_threads())
+        jobs_ok &= bool(np.array_equal(agg[jl], ragg) and
+                        np.array_equal(counts[jl], rcnt.astype(np.uint64)))
+        statuses_ok &= bool(np.array_equal(status.reshape(n_jobs, js)[jl], rst.reshape(-1, js)))
+    t_chk = time.perf_counter() - t_chk
     # the CPU reference path on this host: the restatement at the same job structure on all
     # cores, and its single-core per-report latency
     cores = cpu_threads()
@@ -500,10 +514,12 @@ def jobs_main(args):
                          roof_note="PCIe Gen5 x16 ~63 GB/s (MI355X_MICROARCH.md)"),
                coalescing=dict(launches=launches, jobs=n_jobs,
                                mean_reports_per_launch=n_jobs * js / max(launches, 1)),
+               call=("prio3_helper_prepare_aggregate_batch (one coalesced launch per group)"
+                     if combined else "prio3_helper_prepare_batch + prio3_accumulate"),
                checks=dict(all_finished=bool((status == 0).all()),
                            counts_ok=bool((counts == js).all()),
-                           last_job_matches_cpu=bool(np.array_equal(agg, ragg[0]) and
-                                                     int(rcnt[0]) == js and not rst.any())),
+                           every_job_matches_cpu=jobs_ok, statuses_match_cpu=statuses_ok,
+                           check_seconds=t_chk),
                cpu_baseline=cpu,
                speedup_vs_cpu=(value / cpu["value"]) if cpu else None)
     print(json.dumps(out), flush=True)
@@ -995,19 +1011,42 @@ def fpvec_main(args):
         th = cpu_threads()
         hostd = {k: g[k][idx] for k in ("nonce", "pub", "helper", "lps")}
 
-        def crun(m):
+        # Janus's jobs hold up to 500 reports; a bounded sample of a few thousand 20-50 ms
+        # reports must still give every worker thread jobs, so the jobs here are m / threads
+        # reports (r02's 500-report jobs put a sub-500 sample on ONE thread)
+        def crun(m, threads=th):
+            js = max(1, min(500, m // threads))
             t1 = time.perf_counter()
             r = o.helper_batch(vk, hostd["nonce"][:m], hostd["pub"][:m], hostd["helper"][:m],
-                               hostd["lps"][:m], n_threads=th, job_size=500)
+                               hostd["lps"][:m], n_threads=threads, job_size=js)
             return time.perf_counter() - t1, r
 
+        dt1, _ = crun(4, 1)  # single core, per report
         probe = min(n, 2 * th)
         dt, _ = crun(probe)
         m = int(min(n, max(probe, probe * args.cpu_seconds / max(dt, 1e-6))))
         dt, (cm, cs, cagg, ccnt) = crun(m)
+        # op count of one report on one core: the Keccak-p[1600,12] permutations (share
+        # expansion, the joint-rand part over the encoded share, prio's re-expansion in
+        # prepare_next, proofs, seeds) and the Field128 multiplies of the query (3 per gadget-0
+        # element, 1 per gadget-1 entry), priced at this host's measured single-core rates
+        from oracle.oracle import prim_bench
+        ns_perm, ns_mul = prim_bench()
+        M = o.meas_len
+        perms = 2 * -(-16 * M // 168) + (42 + 16 * M) // 168 + 1 + -(-16 * o.proof_len // 168) + 4
+        muls = 3 * o.calls * (o.arity // 2) + o.fp_K1 * o.fp_C1
+        model_ms = (perms * ns_perm + muls * ns_mul) / 1e6
         cpu = dict(value=m / dt, unit="reports/s", cores=th, kind="port",
                    sample=f"{m} of the tiled fixture reports through the C restatement "
-                          f"(oracle/prio3_oracle.c, ORC_FPVEC), {th} threads, {dt:.1f}s wall")
+                          f"(oracle/prio3_oracle.c, ORC_FPVEC), {th} threads, jobs of "
+                          f"{max(1, min(500, m // th))}, {dt:.1f}s wall",
+                   single_core_ms_per_report=dt1 / 4 * 1e3,
+                   op_count=dict(keccak_p12_perms=perms, f128_muls=muls, ns_per_perm=ns_perm,
+                                 ns_per_f128_mul=ns_mul, model_ms_per_report=model_ms,
+                                 note="perms x ns + muls x ns on one core; the rest of the "
+                                      "measured single-core time is the element decode / "
+                                      "encode passes over the 2.56 MB measurement share"),
+                   cpu_model=cpu_model())
         accept = torch.zeros(n, dtype=torch.uint8, device=dev)
         accept[:m] = 1
         agg_s = torch.zeros_like(agg)

@@ -131,6 +131,21 @@ int prio3_helper_prepare_batch(prio3_engine* engine, uint32_t n, const uint8_t* 
 int prio3_accumulate(prio3_batch* batch, const uint32_t* segment_ids, const uint8_t* accept_mask,
                      uint32_t n_segments, uint8_t* agg_shares_out, uint64_t* counts_out);
 
+/* prio3_helper_prepare_batch followed by prio3_accumulate of the same reports, in ONE coalesced
+ * launch: the job's reports are accumulated into its n_segments aggregations in the group
+ * launch that prepares them (no batch handle, no second round trip through the executor).
+ * For callers whose accept mask is known before preparation (the host-side exclusions of the
+ * aggregation job writer, aggregation_job_writer.rs:591-695); the output shares are not kept.
+ * Same arguments and results as the two calls. */
+int prio3_helper_prepare_aggregate_batch(prio3_engine* engine, uint32_t n, const uint8_t* nonces,
+                                         const uint8_t* public_shares,
+                                         const uint8_t* helper_shares,
+                                         const uint8_t* leader_prep_shares,
+                                         const uint32_t* segment_ids, const uint8_t* accept_mask,
+                                         uint32_t n_segments, uint8_t* prep_msgs_out,
+                                         uint8_t* status_out, uint8_t* agg_shares_out,
+                                         uint64_t* counts_out);
+
 /* Parity-only: copies the n output shares (n x agg_share_len). */
 int prio3_debug_output_shares(prio3_batch* batch, uint8_t* out);
 void prio3_batch_free(prio3_batch* batch);

@@ -614,6 +614,10 @@ struct Run {
   bool lfused = false;     // leader init summed the wave partials (segment 0; leader_fuse_acc)
   uint32_t nseg = 0;
   const uint32_t* seg = nullptr;
+  // executor groups with aggregating jobs (RUN_AGG_IO): group segment ids, accept bytes, the
+  // per-segment aggregate shares and counts
+  uint32_t* gseg = nullptr;
+  uint8_t *gaccept = nullptr, *gagg = nullptr, *gcnt = nullptr;
   std::atomic<int> refs{1};
   hipStream_t last = nullptr;  // stream of the latest work on the run (its release point)
 };

@@ -39,6 +39,9 @@
 #ifndef XOFD_OCC
 #define XOFD_OCC 3
 #endif
+#ifndef QH_PFD
+#define QH_PFD 1  // k_query_h: calls of measurement / coefficient loads in flight ahead
+#endif
 template <class F>
 __device__ __forceinline__ void xof_body(const DevParams& p, const InPtrs& in, const Scratch& sc,
                                          const uint32_t r) {
@@ -1420,6 +1423,33 @@ __device__ __forceinline__ void query_h_body(const DevParams& p, const InPtrs& i
     // measurement elements, one iteration ahead (they come from L2/MALL, and loading them at
     // their use left the waves parked on s_waitcnt).
     T be = ldf<F>(sc.beta, 0, ld, r), Lk = ldf<F>(sc.Lbuf, 1, ld, r);
+#if QH_PFD == 2  // A/B build: two calls ahead
+    T m1[GS];
+    fetch(1, m1);
+    T be1 = ldf<F>(sc.beta, K > 1 ? 1 : 0, ld, r), L1 = ldf<F>(sc.Lbuf, K > 1 ? 2 : 1, ld, r);
+#pragma unroll 1
+    for (uint32_t k = 0; k < K; k++) {
+      T mn[GS];
+      fetch(k + 2, mn);
+      const uint32_t kn = k + 2 < K ? k + 2 : K - 1;
+      const T be_n = ldf<F>(sc.beta, kn, ld, r), L_n = ldf<F>(sc.Lbuf, kn + 1, ld, r);
+#pragma unroll
+      for (int q = 0; q < GS; q++) {
+        mac_add(Aa[q], be, mc[q]);
+        mac_add(Bb[q], Lk, mc[q]);
+        sum_add(Ssum, mc[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < GS; q++) {
+        mc[q] = m1[q];
+        m1[q] = mn[q];
+      }
+      be = be1;
+      Lk = L1;
+      be1 = be_n;
+      L1 = L_n;
+    }
+#else
 #pragma unroll 1
     for (uint32_t k = 0; k < K; k++) {
       T mn[GS];
@@ -1437,6 +1467,7 @@ __device__ __forceinline__ void query_h_body(const DevParams& p, const InPtrs& i
       be = be_n;
       Lk = L_n;
     }
+#endif
     // Wire values at t, lazily reduced: f1 = seed_(2j+1) L0 + B_j - L/2 folds the seed term into
     // B's accumulator, f0 = seed_2j L0 + r^(j+1) A_j is one two-product MAC, and the gadget
     // products of the group are summed in one MAC before a single reduction.
@@ -1523,7 +1554,9 @@ __global__ __launch_bounds__(256, 3) void k_prep_h(DevParams p, InPtrs in, Scrat
                                                    OutPtrs out) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   xofd_body<FUSE, false>(p, in, sc, r);
+#ifndef JANUS_AB_XOF_ONLY  // A/B build: the fused kernel's XOF half alone
   query_h_body<2, 32>(p, in, sc, out, r);
+#endif
 }
 
 // k_prep_sum<NPH>: the same for Prio3Sum (P = 16 NPH): the dual-state XOF and k_query_sum's body
@@ -2432,6 +2465,7 @@ enum : unsigned {
   RUN_VK = 4,       // per-report verify-key slots + key table (coalesced launches)
   RUN_LINPUT = 8,   // leader input shares (host-buffer leader entry point)
   RUN_FUSED = 16,   // fused-accumulate partials (prio3_device_prepare_aggregate, Histogram)
+  RUN_AGG_IO = 32,  // group segment ids, accept bytes, aggregate shares + counts (executor)
 };
 
 // FPVec per-report scratch bytes of one sub-batch column: every buffer indexed [row][column]
@@ -2545,6 +2579,13 @@ static size_t run_carve(Run* R, unsigned flags, uint32_t n_keys, uint8_t* base) 
   if (flags & RUN_VK) {
     take(&R->vk_slot, 2 * n);
     take(&R->vk_tab, 16 * (size_t)(n_keys ? n_keys : 1));
+  }
+  if (flags & RUN_AGG_IO) {
+    const size_t S = R->nseg ? R->nseg : 1;
+    take(&R->gseg, 4 * n);
+    take(&R->gaccept, n);
+    take(&R->gagg, (size_t)d.out_len * es * S);
+    take(&R->gcnt, 8 * S);
   }
   if (flags & RUN_FUSED) {
     const size_t waves = (n + 63) / 64, M = d.meas_len, chunks = (waves + WCH_HOST - 1) / WCH_HOST;
@@ -3133,8 +3174,26 @@ void engine_io_layout(const prio3_engine* e, uint32_t cap, IoLayout* L) {
   off += L->msg_len * cap;
   L->status_off = off;
   off += cap;
+  // aggregating jobs (prio3_helper_prepare_aggregate_batch): group segment ids, accept bytes,
+  // and up to max_seg aggregate shares (at most 16 MiB of them) + counts
+  off = (off + 15) & ~(size_t)15;
+  L->seg_off = off;
+  off += (4 * (size_t)cap + 15) & ~(size_t)15;
+  L->accept_off = off;
+  off += (cap + 15) & ~(size_t)15;
+  L->agg_len = (size_t)d.out_len * d.es;
+  L->max_seg = (uint32_t)std::max<size_t>(1, std::min<size_t>(EXEC_MAX_SEGS,
+                                                                ((size_t)16 << 20) / L->agg_len));
+  L->agg_off = off;
+  off += (L->agg_len * L->max_seg + 15) & ~(size_t)15;
+  L->cnt_off = off;
+  off += 8 * (size_t)L->max_seg;
   L->bytes = off;
 }
+
+static int fused_finish(prio3_engine* e, Run* R, const uint8_t* d_status, const uint32_t* seg,
+                        const uint32_t* fix_seg, const uint8_t* d_accept_mask, uint32_t S,
+                        uint8_t* d_agg_shares, uint64_t* d_counts, hipStream_t st);
 
 int engine_run_group(prio3_engine* lead, const GroupView& g, Run** run_out) {
   *run_out = nullptr;
@@ -3143,9 +3202,16 @@ int engine_run_group(prio3_engine* lead, const GroupView& g, Run** run_out) {
   hipStream_t st = ps.s;
   if (!st) return PRIO3_EDEVICE;
   const bool mp = lead->dp.kind == PRIO3_SUMVEC_F64_MP;
+  // aggregating jobs: the group's reports are accumulated per job segment in this launch (the
+  // wave partials of the XOF where the instance fuses; waves that straddle two jobs and the
+  // excluded reports go through the fix-up list)
+  const bool agg = g.nseg > 0;
+  const bool fuse = agg && fusable(lead);
   int rc = PRIO3_OK;
-  Run* R = run_create(lead, g.n, RUN_SCRATCH | RUN_IO | (mp ? 0u : (unsigned)RUN_VK), 0,
-                      g.n_keys, st, &rc);
+  Run* R = run_create(lead, g.n,
+                      RUN_SCRATCH | RUN_IO | (mp ? 0u : (unsigned)RUN_VK) |
+                          (agg ? (unsigned)RUN_AGG_IO : 0u) | (fuse ? (unsigned)RUN_FUSED : 0u),
+                      agg ? g.nseg : 0, g.n_keys, st, &rc);
   if (!R) return rc;
   IoLayout L;
   engine_io_layout(lead, g.cap, &L);
@@ -3169,9 +3235,29 @@ int engine_run_group(prio3_engine* lead, const GroupView& g, Run** run_out) {
     in.vk_slot = R->vk_slot;
     in.vk_tab = R->vk_tab;
   }
+  if (agg) {
+    if (hipMemcpyAsync(R->gseg, g.stg + L.seg_off, 4 * (size_t)g.n, hipMemcpyHostToDevice, st) !=
+            hipSuccess ||
+        hipMemcpyAsync(R->gaccept, g.stg + L.accept_off, g.n, hipMemcpyHostToDevice, st) !=
+            hipSuccess)
+      return fail(PRIO3_EDEVICE);
+    R->seg = R->gseg;
+  }
   OutPtrs out{R->msgs, R->status};
-  rc = prepare_run(lead, R, in, out, st, false, false);
+  rc = prepare_run(lead, R, in, out, st, fuse, false);
   if (rc) return fail(rc);
+  if (agg) {
+    rc = fuse ? fused_finish(lead, R, R->status, R->gseg, R->gseg, R->gaccept, g.nseg, R->gagg,
+                             (uint64_t*)R->gcnt, st)
+              : run_accumulate(lead, R, 0, g.n, R->status, R->gseg, R->gaccept, g.nseg, R->gagg,
+                               (uint64_t*)R->gcnt, st);
+    if (rc) return fail(rc);
+    if (hipMemcpyAsync(g.stg + L.agg_off, R->gagg, L.agg_len * g.nseg, hipMemcpyDeviceToHost,
+                       st) != hipSuccess ||
+        hipMemcpyAsync(g.stg + L.cnt_off, R->gcnt, 8 * (size_t)g.nseg, hipMemcpyDeviceToHost,
+                       st) != hipSuccess)
+      return fail(PRIO3_EDEVICE);
+  }
   if ((L.msg_len && hipMemcpyAsync(g.stg + L.msg_off, R->msgs, L.msg_len * g.n,
                                    hipMemcpyDeviceToHost, st) != hipSuccess) ||
       hipMemcpyAsync(g.stg + L.status_off, R->status, g.n, hipMemcpyDeviceToHost, st) !=
@@ -3704,6 +3790,59 @@ int prio3_helper_prepare_batch(prio3_engine* e, uint32_t n, const uint8_t* nonce
     *batch_out = new prio3_batch{e, job.run, job.c0, n};
   else
     run_release(job.run, nullptr, false);
+  return PRIO3_OK;
+}
+
+int prio3_helper_prepare_aggregate_batch(prio3_engine* e, uint32_t n, const uint8_t* nonces,
+                                         const uint8_t* public_shares,
+                                         const uint8_t* helper_shares,
+                                         const uint8_t* leader_prep_shares,
+                                         const uint32_t* segment_ids, const uint8_t* accept_mask,
+                                         uint32_t n_segments, uint8_t* prep_msgs_out,
+                                         uint8_t* status_out, uint8_t* agg_shares_out,
+                                         uint64_t* counts_out) {
+  TraceSpan span_("handle_aggregate_init_generic threadpool task");
+  if (!e || n_segments == 0 || !agg_shares_out || !counts_out ||
+      (n && (!nonces || !helper_shares || !leader_prep_shares || !status_out)))
+    return PRIO3_EINVAL;
+  if (e->dp.kind == PRIO3_FPVEC_BOUNDED_L2 && !e->experimental_fpvec)
+    return PRIO3_EUNSUPPORTED;  // unpinned reconstruction: explicit opt-in only
+  const DevParams& d = e->dp;
+  if (n && d.jr_len && (!public_shares || !prep_msgs_out)) return PRIO3_EINVAL;
+  const size_t agg_len = (size_t)d.out_len * d.es;
+  IoLayout L1;
+  engine_io_layout(e, 1, &L1);
+  if (n == 0 || !e->coalesce || n_segments > L1.max_seg) {
+    // not coalescable (or empty): the two calls, as the caller would make them
+    prio3_batch* b = nullptr;
+    int rc = prio3_helper_prepare_batch(e, n, nonces, public_shares, helper_shares,
+                                        leader_prep_shares, prep_msgs_out, status_out, &b);
+    if (rc == PRIO3_OK) rc = prio3_accumulate(b, segment_ids, accept_mask, n_segments,
+                                              agg_shares_out, counts_out);
+    prio3_batch_free(b);
+    if (rc == PRIO3_OK && n == 0) {
+      memset(agg_shares_out, 0, agg_len * n_segments);
+      memset(counts_out, 0, 8 * (size_t)n_segments);
+    }
+    return rc;
+  }
+  ExecJob job;
+  job.e = e;
+  job.n = n;
+  job.nonces = nonces;
+  job.pub = d.jr_len ? public_shares : nullptr;
+  job.helper = helper_shares;
+  job.leader = leader_prep_shares;
+  job.msgs_out = prep_msgs_out;
+  job.status_out = status_out;
+  job.seg = segment_ids;
+  job.accept = accept_mask;
+  job.nseg = n_segments;
+  job.agg_out = agg_shares_out;
+  job.counts_out = counts_out;
+  const int rc = exec_submit(&job);
+  if (rc) return rc;
+  run_release(job.run, nullptr, false);  // no batch handle: the output shares are not kept
   return PRIO3_OK;
 }
 

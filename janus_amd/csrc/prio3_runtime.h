@@ -53,11 +53,20 @@ struct ExecJob {
   uint32_t n;
   const uint8_t *nonces, *pub, *helper, *leader;  // host inputs (packed per report)
   uint8_t *msgs_out, *status_out;                 // host outputs
+  // prepare + aggregate in the same launch (prio3_helper_prepare_aggregate_batch): the job's
+  // reports are accumulated into its n_segments batch aggregations in the group's launch, with
+  // no batch handle and no second round trip (nseg == 0: prepare only)
+  const uint32_t* seg = nullptr;   // host segment ids [n] (nullable: segment 0)
+  const uint8_t* accept = nullptr;  // host accept mask [n] (nullable: all)
+  uint32_t nseg = 0;
+  uint8_t* agg_out = nullptr;      // host [nseg][agg_share_len]
+  uint64_t* counts_out = nullptr;  // host [nseg]
   // results
   int rc = 0;
   Run* run = nullptr;  // holds one reference for this job
   uint32_t c0 = 0;     // the job's first column in the run
   uint32_t slot = 0;   // the job's verify-key slot in its group
+  uint32_t seg0 = 0;   // the job's first segment among the group's
 };
 // Blocks until the job's reports are prepared (alone or coalesced with concurrent jobs of
 // engines with the same VDAF instance on the same GPU).
@@ -68,9 +77,14 @@ int exec_submit(ExecJob* job);
 // fields [cap][len] (nonces, public shares, helper shares, leader prep shares), the per-report
 // verify-key slot (u16), the verify-key table [exec_max_keys()][16], then the outputs: prepare
 // messages [cap][msg_len] and statuses [cap].
+// Groups with aggregating jobs also stage per-report group segment ids (u32) and accept bytes,
+// and receive [max_seg][agg_len] aggregate shares + [max_seg] u64 counts.
 struct IoLayout {
   size_t len[4], off[4];
-  size_t slot_off, tab_off, msg_off, status_off, msg_len, bytes;
+  size_t slot_off, tab_off, msg_off, status_off, msg_len;
+  size_t seg_off, accept_off, agg_off, cnt_off, agg_len;
+  uint32_t max_seg;
+  size_t bytes;
 };
 void engine_io_layout(const prio3_engine* e, uint32_t cap, IoLayout* L);
 struct GroupView {
@@ -78,7 +92,10 @@ struct GroupView {
   uint8_t* stg;     // pinned staging (IoLayout for cap)
   uint32_t n_keys;  // verify keys in the table
   int jobs;         // references the run must carry (one per job)
+  uint32_t nseg;    // segments of the aggregating jobs (0: no job aggregates)
 };
+// segments one group can aggregate (its aggregating jobs' n_segments summed)
+constexpr uint32_t EXEC_MAX_SEGS = 1024;
 int engine_device(const prio3_engine* e);
 uint64_t engine_group_key(const prio3_engine* e);  // equal keys may share one launch
 void engine_vk(const prio3_engine* e, uint8_t out[16]);

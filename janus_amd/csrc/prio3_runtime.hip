@@ -367,7 +367,7 @@ struct PrepPolicy {
   struct State {
     prio3_engine* lead = nullptr;
     std::vector<const prio3_engine*> keys;  // verify-key table, slot = index
-    uint32_t n = 0, cap = 0, jobs = 0;
+    uint32_t n = 0, cap = 0, jobs = 0, nseg = 0;
     IoLayout L;
     Run* run = nullptr;
   };
@@ -388,11 +388,13 @@ struct PrepPolicy {
     uint32_t k = 0;
     while (k < s.keys.size() && s.keys[k] != j->e) k++;
     if (k == s.keys.size() && s.keys.size() >= exec_max_keys()) return false;
-    if (s.n + j->n > s.cap) return false;
+    if (s.n + j->n > s.cap || s.nseg + j->nseg > s.L.max_seg) return false;
     if (k == s.keys.size()) s.keys.push_back(j->e);
     j->c0 = s.n;
     j->slot = k;
+    j->seg0 = s.nseg;
     s.n += j->n;
+    s.nseg += j->nseg;
     s.jobs++;
     return true;
   }
@@ -405,6 +407,23 @@ struct PrepPolicy {
     uint16_t* slots = (uint16_t*)(g.p + L.slot_off) + j->c0;
     for (uint32_t i = 0; i < j->n; i++) slots[i] = (uint16_t)j->slot;
     engine_vk(j->e, g.p + L.tab_off + 16 * (size_t)j->slot);
+    // group segment ids: the job's own ids shifted to its segment range (an id >= its n_segments
+    // stays out of every aggregate: 0xFFFFFFFF); a prepare-only job's reports are out
+    uint32_t* sg = (uint32_t*)(g.p + L.seg_off) + j->c0;
+    uint8_t* ac = g.p + L.accept_off + j->c0;
+    if (j->nseg == 0) {
+      for (uint32_t i = 0; i < j->n; i++) sg[i] = 0xFFFFFFFFu;
+      memset(ac, 0, j->n);
+    } else {
+      for (uint32_t i = 0; i < j->n; i++) {
+        const uint32_t x = j->seg ? j->seg[i] : 0u;
+        sg[i] = x < j->nseg ? j->seg0 + x : 0xFFFFFFFFu;
+      }
+      if (j->accept)
+        memcpy(ac, j->accept, j->n);
+      else
+        memset(ac, 1, j->n);
+    }
   }
   static int launch(int device, State& s, Staging& g) {
     (void)device;
@@ -414,6 +433,7 @@ struct PrepPolicy {
     v.stg = g.p;
     v.n_keys = (uint32_t)s.keys.size();
     v.jobs = (int)s.jobs;
+    v.nseg = s.nseg;
     return engine_run_group(s.lead, v, &s.run);
   }
   static void unstage(State& s, Staging& g, Job* j) {
@@ -421,6 +441,10 @@ struct PrepPolicy {
     if (L.msg_len && j->msgs_out)
       memcpy(j->msgs_out, g.p + L.msg_off + L.msg_len * j->c0, L.msg_len * j->n);
     if (j->status_out) memcpy(j->status_out, g.p + L.status_off + j->c0, j->n);
+    if (j->nseg) {
+      memcpy(j->agg_out, g.p + L.agg_off + L.agg_len * j->seg0, L.agg_len * j->nseg);
+      memcpy(j->counts_out, g.p + L.cnt_off + 8 * (size_t)j->seg0, 8 * (size_t)j->nseg);
+    }
     j->run = s.run;  // one reference per job (engine_run_group sets refs = jobs)
   }
 };

@@ -74,6 +74,7 @@ class Prio3Sizes(C.Structure):
 #: Every symbol include/janus_prio3.h declares.
 EXPORTED_SYMBOLS = (
     "prio3_sizes", "prio3_engine_create", "prio3_engine_destroy", "prio3_helper_prepare_batch",
+    "prio3_helper_prepare_aggregate_batch",
     "prio3_accumulate", "prio3_debug_output_shares", "prio3_batch_free", "prio3_device_prepare",
     "prio3_device_accumulate", "prio3_device_output_shares", "prio3_device_combine",
     "prio3_engine_set_option", "prio3_engine_timing", "prio3_engine_timing_reset",
@@ -118,6 +119,8 @@ def load_library() -> C.CDLL:
     L.prio3_engine_destroy.restype = None
     L.prio3_helper_prepare_batch.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, vp, vp, P(vp)]
     L.prio3_accumulate.argtypes = [vp, vp, vp, C.c_uint32, vp, vp]
+    L.prio3_helper_prepare_aggregate_batch.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, vp, vp,
+                                                       C.c_uint32, vp, vp, vp, vp]
     L.prio3_debug_output_shares.argtypes = [vp, vp]
     L.prio3_batch_free.argtypes = [vp]
     L.prio3_batch_free.restype = None
@@ -355,6 +358,38 @@ class HelperEngine:
         if rc:
             raise RuntimeError(f"prio3_helper_prepare_batch failed (rc={rc})")
         return msgs[:, :sz.prep_msg_len], status, PreparedBatch(self, bh, n)
+
+    def prepare_aggregate_batch(self, nonces, public_shares, helper_shares, leader_prep_shares,
+                                segment_ids=None, accept_mask=None, n_segments: int = 1):
+        """prepare_batch + accumulate of the same reports in one coalesced launch
+        (prio3_helper_prepare_aggregate_batch).  Returns (prep_msgs, status, agg [S, agg_len],
+        counts [S])."""
+        sz = self.sz
+        nonces = np.ascontiguousarray(nonces, np.uint8)
+        n = nonces.shape[0]
+        helper_shares = np.ascontiguousarray(helper_shares, np.uint8)
+        leader_prep_shares = np.ascontiguousarray(leader_prep_shares, np.uint8)
+        if helper_shares.shape != (n, sz.helper_share_len) or \
+                leader_prep_shares.shape != (n, sz.prep_share_len):
+            raise ValueError("input share shapes do not match the VDAF instance")
+        pub = None
+        if sz.public_share_len:
+            pub = np.ascontiguousarray(public_shares, np.uint8)
+            if pub.shape != (n, sz.public_share_len):
+                raise ValueError("public share shape does not match the VDAF instance")
+        seg = None if segment_ids is None else np.ascontiguousarray(segment_ids, np.uint32)
+        acc = None if accept_mask is None else np.ascontiguousarray(accept_mask, np.uint8)
+        msgs = np.zeros((n, max(sz.prep_msg_len, 1)), np.uint8)
+        status = np.zeros(n, np.uint8)
+        agg = np.zeros((n_segments, sz.agg_share_len), np.uint8)
+        cnt = np.zeros(n_segments, np.uint64)
+        rc = load_library().prio3_helper_prepare_aggregate_batch(
+            self.handle, n, _np_ptr(nonces), _np_ptr(pub), _np_ptr(helper_shares),
+            _np_ptr(leader_prep_shares), _np_ptr(seg), _np_ptr(acc), n_segments, _np_ptr(msgs),
+            _np_ptr(status), _np_ptr(agg), _np_ptr(cnt))
+        if rc:
+            raise RuntimeError(f"prio3_helper_prepare_aggregate_batch failed (rc={rc})")
+        return msgs[:, :sz.prep_msg_len], status, agg, cnt
 
     # ---- leader side (same instance, agg_id 0) -----------------------------------
     def leader_prepare_init_batch(self, nonces, public_shares, leader_input_shares):

@@ -130,6 +130,91 @@ def test_concurrent_jobs_of_several_tasks_are_coalesced(name):
     assert 0 < launches < 24, launches
 
 
+@pytest.mark.parametrize("name", ["hist_256_c16", "sumvec_8x10_c9", "count", "sum32"])
+def test_combined_prepare_aggregate_jobs(name):
+    """prio3_helper_prepare_aggregate_batch from 8 threads at once: 32 jobs of 100-500 reports
+    for 4 tasks, each with its own segments (1-4, ids past n_segments included) and accept
+    mask, some tampered, and every fourth job a plain prepare_batch + accumulate in the same
+    groups.  Each job's messages, statuses, per-segment aggregates and counts equal the
+    restatement's, and the groups mixed jobs into fewer launches than jobs."""
+    from oracle.oracle import Oracle
+    cfg = CONFIGS[name]
+    o = Oracle(**cfg)
+    vks = [bytes([k]) * 16 for k in (0x41, 0x42, 0x43, 0x44)]
+    engines = [_engine(cfg, vk) for vk in vks]
+    for e in engines:
+        e.set_option("timing", 1)
+        e.timing_reset()
+    rng = np.random.default_rng(19)
+    jobs = []
+    for j in range(32):
+        t = j % 4
+        n = int(rng.integers(100, 501))
+        d = o.gen_reports(vks[t], n, seed=300 + j, n_threads=4)
+        if j % 3 == 1:
+            d = _tamper(o, d, rng)
+        S = int(rng.integers(1, 5))
+        seg = rng.integers(0, S + 1, n).astype(np.uint32)  # id S: out of range, excluded
+        acc = (rng.random(n) < 0.9).astype(np.uint8)
+        jobs.append((t, d, S, seg, acc))
+    start = threading.Barrier(8)
+
+    def run(j):
+        t, d, S, seg, acc = jobs[j]
+        if j < 8:
+            start.wait()
+        args = (d["nonces"], d["public_shares"], d["helper_shares"], d["leader_prep_shares"])
+        if j % 4 == 3:
+            msgs, status, batch = engines[t].prepare_batch(*args)
+            agg, cnt = batch.accumulate(seg, acc, S)
+            batch.free()
+            return msgs, status, agg, cnt
+        return engines[t].prepare_aggregate_batch(*args, segment_ids=seg, accept_mask=acc,
+                                                  n_segments=S)
+
+    with ThreadPoolExecutor(8) as ex:
+        got = list(ex.map(run, range(32)))
+    for (t, d, S, seg, acc), (msgs, status, agg, cnt) in zip(jobs, got):
+        ref_seg = np.where(seg < S, seg, 0).astype(np.uint32)
+        ref_acc = np.where(seg < S, acc, 0).astype(np.uint8)
+        rm, rs, ra, rc = _ref(o, vks[t], d, ref_seg, ref_acc, S)
+        np.testing.assert_array_equal(status, rs)
+        np.testing.assert_array_equal(msgs, rm)
+        np.testing.assert_array_equal(agg, ra)
+        np.testing.assert_array_equal(cnt, rc)
+    kern = {"count": "k_prep_gen", "hist_256_c16": "k_prep_h", "sum32": "k_prep_sum"}.get(
+        name, "k_xofd")
+    launches = sum(e.timing().get(kern, (0, 0))[1] for e in engines)
+    assert 0 < launches < 32, launches
+
+
+def test_combined_prepare_aggregate_single_job_and_empty():
+    """One combined call alone (the executor launches a lone job at once), with coalescing off
+    (the two-call fallback), and an empty job."""
+    from oracle.oracle import Oracle
+    cfg = CONFIGS["hist_256_c16"]
+    vk = bytes(range(0x50, 0x60))
+    o = Oracle(**cfg)
+    eng = _engine(cfg, vk)
+    d = _tamper(o, o.gen_reports(vk, 777, seed=8, n_threads=4), np.random.default_rng(8))
+    seg = (np.arange(777) % 3).astype(np.uint32)
+    rm, rs, ra, rc = _ref(o, vk, d, seg, None, 3)
+    for coalesce in (1, 0):
+        eng.set_option("coalesce", coalesce)
+        msgs, status, agg, cnt = eng.prepare_aggregate_batch(
+            d["nonces"], d["public_shares"], d["helper_shares"], d["leader_prep_shares"],
+            segment_ids=seg, n_segments=3)
+        np.testing.assert_array_equal(status, rs)
+        np.testing.assert_array_equal(msgs, rm)
+        np.testing.assert_array_equal(agg, ra)
+        np.testing.assert_array_equal(cnt, rc)
+    z = lambda k: np.zeros((0, k), np.uint8)
+    sz = eng.sz
+    msgs, status, agg, cnt = eng.prepare_aggregate_batch(
+        z(16), z(sz.public_share_len), z(sz.helper_share_len), z(sz.prep_share_len), n_segments=2)
+    assert status.shape == (0,) and cnt.tolist() == [0, 0] and not agg.any()
+
+
 def test_coalescing_off_matches():
     from oracle.oracle import Oracle
     cfg = CONFIGS["hist_10_c3"]
