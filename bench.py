@@ -80,13 +80,14 @@ def valu_model(kernel: str, length=256, chunk=16) -> float:
         squeezed = length + proof_len + 2 + 1
         return perms * perm + squeezed * PRIM["lt_p"] + jr_blocks * 42  # + funnel shifts
     if kernel in ("k_query_h", "k_query_pair", "k_query_rows"):
-        logP = P.bit_length() - 1
-        half = P // 2
-        # two DFTs of P/2 points (radix 2: (P/4) log2(P/2) butterflies, the w = 1 ones free)
-        bfly = (half // 2) * (logP - 1)
-        triv = sum(half // (1 << l) for l in range(1, logP))
-        muls = (logP + 4) + P + 2 * (bfly - triv)  # t powers, geometric sequences, twiddles
-        adds = 2 * 2 * bfly + calls
+        # Lagrange basis at t: four 8-point DFTs of geometric sequences (P = 32; radix 2, 12
+        # butterflies each, 5 with a non-trivial twiddle): t^8/t^16/t^32, the four phase sums G_ph
+        # (3 muls), the start values and ratios, 4 x 7 sequence steps, 4 x 5 twiddle products
+        nph, pts = 4, P // 4
+        bfly = (pts // 2) * 3
+        twid = 5
+        muls = 5 + 3 + nph + (nph - 1) + nph * (pts - 1) + nph * twid
+        adds = nph * 2 * bfly + 6 + calls
         muls += (glen - 1) + chunk.bit_length() + 2 * calls  # Horner, r^C, beta
         macs = (glen - 1) + 2 * length + 4 * chunk            # range, A/B sums, finalize
         reduces = 1 + 3 * chunk + chunk // 2                 # range, A/B/f0 per wire, gadget groups
@@ -178,6 +179,13 @@ def main():
                          "trip) or prio3_helper_prepare_batch + prio3_accumulate (two)")
     ap.add_argument("--tasks", type=int, default=4,
                     help="--role jobs: tasks (verify keys) of the VDAF instance the jobs rotate over")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="N>1: nccl (RCCL over xGMI, the measured path) or gloo with the combine's "
+                         "all-gather staged through host memory (lets N ranks share one GPU in a "
+                         "test; never a measurement)")
+    ap.add_argument("--check-combined", action="store_true",
+                    help="N>1: rank 0 regenerates every rank's shard and checks the combined "
+                         "aggregate, count, checksum and interval against the CPU restatement")
     ap.add_argument("--opt", action="append", default=[],
                     help="engine option key=value (e.g. chunks=3, force_generic_query=1), for A/B runs")
     args = ap.parse_args()
@@ -200,10 +208,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    if world > 1 and args.dist_backend == "gloo":
+        # ranks may outnumber GPUs here (a one-GPU test of this step): device = local rank mod count
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -227,9 +241,11 @@ def main():
     agg = torch.zeros((1, sz.agg_share_len), dtype=torch.uint8, device=dev)
     cnt = torch.zeros(1, dtype=torch.int64, device=dev)
     # report timestamps (seconds) inside one hour-long batch interval, seeded
-    g = torch.Generator(device=dev).manual_seed(0x4A414E55 + rank)
-    report_times = 1_700_000_000 + torch.randint(0, 3600, (n,), generator=g, device=dev,
-                                          dtype=torch.int64)
+    def times_of(r):
+        g = torch.Generator(device=dev).manual_seed(0x4A414E55 + r)
+        return 1_700_000_000 + torch.randint(0, 3600, (n,), generator=g, device=dev,
+                                             dtype=torch.int64)
+    report_times = times_of(rank)
     cks = torch.zeros((1, 32), dtype=torch.uint8, device=dev)
     ivs = torch.zeros((1, 2), dtype=torch.int64, device=dev)
     combiner = None
@@ -241,7 +257,8 @@ def main():
             lambda k, ga, gc, oa, oc: eng.combine_device(k, 1, ga, gc, oa, oc, stream=cur()),
             cks, ivs,
             lambda k, gk, gi, ok, oi: eng.combine_metadata_device(k, 1, gk, gi, ok, oi,
-                                                                  stream=cur()))
+                                                                  stream=cur()),
+            stage_device="cpu" if args.dist_backend == "gloo" else None)
 
     def step():
         # SURVEY 8(a) a3-a11 + a14: prepare, decide, prepare message, and the per-segment batch
@@ -359,6 +376,13 @@ def main():
                roofline=roofline, kernels=per_kernel,
                kernels_timed_region={k: dict(ms_total=v[0], launches=v[1]) for k, v in step_times.items()},
                checks=dict(finished=ok, generator_flags=flags, agg_count=final_cnt))
+    if world > 1:
+        out["dist_backend"] = args.dist_backend
+        if args.dist_backend == "gloo":
+            out["note"] = "gloo: all-gather staged through host memory (a correctness run, not RCCL)"
+    if world > 1 and args.check_combined and rank == 0:
+        out["checks"]["combined_matches_oracle"] = check_combined(eng, args, world, n, times_of,
+                                                                  combiner)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb, (msgs, cst, cagg, ccnt) = cpu_baseline(eng, data, min(n, 1 << 20), args.cpu_seconds)
         m = cb.pop("n")
@@ -390,6 +414,33 @@ def main():
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def check_combined(eng, args, world, n, times_of, combiner) -> bool:
+    """Rank 0, N>1: every rank's shard regenerated here (same seed and report indices), the CPU
+    restatement's helper batch over all world x n reports, and the combined aggregate share,
+    count, ReportIdChecksum and interval compared with it (aggregate_share.rs:55-96)."""
+    from oracle.oracle import Oracle, batch_metadata
+    o = Oracle("histogram", length=256, chunk_length=16)
+    cols = {k: [] for k in ("nonces", "public_shares", "helper_shares", "leader_prep_shares")}
+    times = []
+    for r in range(world):
+        d = eng.generate_reports_device(n, seed=0x4A414E5553000001, first_index=r * n)
+        for k in cols:
+            cols[k].append(d[k].cpu().numpy())
+        times.append(times_of(r).cpu().numpy())
+    host = {k: np.concatenate(v) for k, v in cols.items()}
+    _, st, agg, cnt = o.helper_batch(VK, host["nonces"], host["public_shares"],
+                                     host["helper_shares"], host["leader_prep_shares"],
+                                     n_threads=cpu_threads(), job_size=500)
+    ck, iv = batch_metadata(host["nonces"], np.concatenate(times), st, None,
+                            None, 1)
+    torch.cuda.synchronize()
+    return bool(
+        np.array_equal(combiner.out_agg.cpu().numpy().reshape(-1), np.asarray(agg).reshape(-1)) and
+        int(combiner.out_cnt[0].item()) == int(np.asarray(cnt).reshape(-1)[0]) and
+        np.array_equal(combiner.out_checksums.cpu().numpy(), ck) and
+        np.array_equal(combiner.out_intervals.cpu().numpy().view(np.uint64), iv))
 
 
 def cpu_model() -> str:

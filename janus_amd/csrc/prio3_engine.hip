@@ -246,11 +246,10 @@ __device__ __forceinline__ void xofd_body(const DevParams& p, const InPtrs& in, 
   }
   if (r >= p.n) return;
   uint32_t flag = p.force_slow;
-  uint32_t nonce[4], km[4], kp[4], kb[4];
+  uint32_t nonce[4], km[4], kb[4];
   load16(in.nonces + 16 * (size_t)r, nonce);
   const uint8_t* hs = in.helper + (size_t)r * p.helper_share_len;
   load16(hs, km);
-  load16(hs + 16, kp);
   load16(hs + 32, kb);
   {  // query randomness
     KState s;
@@ -287,7 +286,6 @@ __device__ __forceinline__ void xofd_body(const DevParams& p, const InPtrs& in, 
     msg_byte(m, 25, 1);
     msg_absorb_final(ms, m, 26);
   }
-  uint32_t tail[11];
   uint32_t pend0 = 0, pend1 = 0;
   TruncSink ts(p, sc.out, r);
   const int Mi = (int)M;
@@ -323,6 +321,25 @@ __device__ __forceinline__ void xofd_body(const DevParams& p, const InPtrs& in, 
                               : z);
     }
   };
+  // Joint-rand block b holds the last 42 bytes of share block b-1 (words 0..10, a 16-bit funnel
+  // shift) and the first 126 bytes of share block b (words 10..41).  The first part is XORed into
+  // js as soon as js has been permuted for block b-1 and before ms moves on, so no share words
+  // are carried across a permutation (the 11-word tail buffer spilled at 168 VGPRs).
+  auto wmask = [&](int j) __attribute__((always_inline)) {  // bytes of word j below rem
+    const uint32_t lo = 4u * (uint32_t)j;
+    return (lo + 4 <= rem) ? 0xffffffffu : (lo >= rem ? 0u : ((1u << (8 * (rem - lo))) - 1u));
+  };
+  auto carry_tail = [&](bool last) __attribute__((always_inline)) {  // last: block B is next
+#pragma unroll
+    for (int j = 0; j < 10; j++) {
+      uint32_t x = __builtin_amdgcn_alignbit(kword(ms, 32 + j), kword(ms, 31 + j), 16);
+      if (last) x &= wmask(j);
+      kxor_word(js, j, x);
+    }
+    uint32_t x = kword(ms, 41) >> 16;
+    if (last) x &= wmask(10);
+    kxor_word(js, 10, x);
+  };
   // block 0: prefix (42 bytes) + the first 126 bytes of the share
   {
     if (FUSE && fuse) fuse_block(0, 0, 0);
@@ -339,29 +356,21 @@ __device__ __forceinline__ void xofd_body(const DevParams& p, const InPtrs& in, 
 #pragma unroll
     for (int j = 11; j < 42; j++)
       kxor_word(js, j, __builtin_amdgcn_alignbit(kword(ms, j - 10), kword(ms, j - 11), 16));
-#pragma unroll
-    for (int t = 0; t < 11; t++) tail[t] = kword(ms, 31 + t);
     keccak_p12(js);
+    carry_tail(B == 1);
     keccak_p12(ms);
   }
-  // full joint-rand blocks 1 .. B-1 (share blocks b-1 tail + block b head)
+  // full joint-rand blocks 1 .. B-1 (B <= K, so share block b exists for every b < B)
 #pragma unroll 1
   for (uint32_t b = 1; b < B; b++) {
-    const bool hasW = b < K;  // wave-uniform
-    if (FUSE && fuse && hasW) fuse_block(b, pend0, pend1);
-    if (hasW) squeeze_meas<TR>(p, ms, b, M, pend0, pend1, sc.meas, r, flag, ts);
+    if (FUSE && fuse) fuse_block(b, pend0, pend1);
+    squeeze_meas<TR>(p, ms, b, M, pend0, pend1, sc.meas, r, flag, ts);
+    kxor_word(js, 10, kword(ms, 0) << 16);
 #pragma unroll
-    for (int j = 0; j < 10; j++)
-      kxor_word(js, j, __builtin_amdgcn_alignbit(tail[j + 1], tail[j], 16));
-    kxor_word(js, 10, __builtin_amdgcn_alignbit(hasW ? kword(ms, 0) : 0u, tail[10], 16));
-    if (hasW) {
-#pragma unroll
-      for (int j = 11; j < 42; j++)
-        kxor_word(js, j, __builtin_amdgcn_alignbit(kword(ms, j - 10), kword(ms, j - 11), 16));
-#pragma unroll
-      for (int t = 0; t < 11; t++) tail[t] = kword(ms, 31 + t);
-    }
+    for (int j = 11; j < 42; j++)
+      kxor_word(js, j, __builtin_amdgcn_alignbit(kword(ms, j - 10), kword(ms, j - 11), 16));
     keccak_p12(js);
+    carry_tail(b + 1 == B);
     if (b + 1 < K) keccak_p12(ms);
   }
   // final joint-rand block B: remaining share bytes, padding
@@ -372,14 +381,11 @@ __device__ __forceinline__ void xofd_body(const DevParams& p, const InPtrs& in, 
     if (hasW) squeeze_meas<TR>(p, ms, B, M, pend0, pend1, sc.meas, r, flag, ts);
 #pragma unroll
     for (int j = 0; j < 42; j++) {
-      uint32_t x;
-      if (j < 10) x = __builtin_amdgcn_alignbit(tail[j + 1], tail[j], 16);
-      else if (j == 10) x = __builtin_amdgcn_alignbit(hasW ? kword(ms, 0) : 0u, tail[10], 16);
-      else x = hasW ? __builtin_amdgcn_alignbit(kword(ms, j - 10), kword(ms, j - 11), 16) : 0u;
-      const uint32_t lo = 4 * j;
-      const uint32_t mask = (lo + 4 <= rem) ? 0xffffffffu
-                                            : (lo >= rem ? 0u : ((1u << (8 * (rem - lo))) - 1u));
-      x &= mask;
+      uint32_t x = 0;
+      if (j == 10) x = hasW ? kword(ms, 0) << 16 : 0u;
+      else if (j > 10)
+        x = hasW ? __builtin_amdgcn_alignbit(kword(ms, j - 10), kword(ms, j - 11), 16) : 0u;
+      x &= wmask(j);
       if ((uint32_t)j == (rem >> 2)) x ^= 1u << (8 * (rem & 3));
       if (j == 41) x ^= 0x80000000u;
       kxor_word(js, j, x);
@@ -391,6 +397,8 @@ __device__ __forceinline__ void xofd_body(const DevParams& p, const InPtrs& in, 
     part[3] = kword(js, 3);
   }
   {  // proofs share
+    uint32_t kp[4];  // loaded here: it was live across the share loop
+    load16(hs + 16, kp);
     KState s;
     kzero(s);
     Msg m;
@@ -1306,27 +1314,33 @@ __device__ __forceinline__ void query_h_body(const DevParams& p, const InPtrs& i
     for (int k = 0; k < PP; k++) store_L(k, x[k]);
   } else {
     static_assert(PP == 32, "PP must be <= 32");
-    T t16 = t;
+    // Four phases of an 8-point DFT: X[4k + ph] = DFT8(y^ph)[k] with y^ph_n = (G_ph / P)(t w^ph)^n,
+    // w = w32 and G_ph = sum_(i<4) (t^8 w4^ph)^i, so only 8 values (32 VGPRs) are live at a time
+    // (two 16-point phases held 64 and spilled at 168 VGPRs).
+    T t8 = t;
 #pragma unroll
-    for (int i = 0; i < 4; i++) t16 = F::mul(t16, t16);
+    for (int i = 0; i < 3; i++) t8 = F::mul(t8, t8);
+    const T t16 = F::mul(t8, t8);
     const T t32 = F::mul(t16, t16);
     if (F::eq(t32, F::one())) status = PRIO3_STATUS_PREP_INIT;
     const T ip = FC<F>::invP(p);
-    const T gy = F::mul(ip, F::add(F::one(), t16)), gz = F::mul(ip, F::sub(F::one(), t16));
-    const T tw = F::mul(t, F::from_words(p.tw128[1]));  // t * w32
+    const T a = F::add(F::one(), t16), b = F::sub(F::one(), t16);
+    const T c = F::mul(t8, a), wd = F::mul(F::mul(t8, b), F::from_words(p.tw128[8]));  // w4 = w32^8
 #pragma unroll
-    for (int ph = 0; ph < 2; ph++) {
-      T x[16];
-      T pw = F::sel(ph == 0, gy, gz);
-      const T ratio = F::sel(ph == 0, t, tw);
+    for (int ph = 0; ph < 4; ph++) {
+      const T g = ph == 0 ? F::add(a, c) : ph == 1 ? F::add(b, wd) : ph == 2 ? F::sub(a, c)
+                                                                              : F::sub(b, wd);
+      T x[8];
+      T pw = F::mul(ip, g);
+      const T ratio = ph == 0 ? t : F::mul(t, F::from_words(p.tw128[ph]));
 #pragma unroll
-      for (int e = 0; e < 16; e++) {
-        x[__builtin_bitreverse32(e) >> 28] = pw;
-        pw = F::mul(pw, ratio);
+      for (int e = 0; e < 8; e++) {
+        x[__builtin_bitreverse32(e) >> 29] = pw;
+        if (e + 1 < 8) pw = F::mul(pw, ratio);
       }
-      dft_reg<16, 4>(p, x, 2);
+      dft_reg<8, 3>(p, x, 4);
 #pragma unroll
-      for (int k = 0; k < 16; k++) store_L(2 * k + ph, x[k]);
+      for (int k = 0; k < 8; k++) store_L(4 * k + ph, x[k]);
     }
   }
   // p(t) (Horner) and range = sum_c p(alpha^c) = sum_e coef_e sigma_(e mod P)

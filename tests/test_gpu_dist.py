@@ -9,6 +9,10 @@
   the partials (staged through host memory for gloo) and combines them with the HIP kernels;
   the result must equal the CPU restatement's aggregate of the whole batch
   (aggregate_share.rs:55-96 merges per-shard batch aggregations the same way).
+* bench.py's own N > 1 step: two ranks under torch.distributed.run on the one
+  GPU of the box, gloo with the all-gather staged through host memory, and rank 0 checks the
+  combined aggregate, count, checksum and interval of both shards against the CPU restatement.
+  The RCCL (nccl) backend of the same step is only exercised by the driver's 8-GPU run.
 The ranks are child processes started with subprocess (the pytest process may already hold the
 GPU; nothing is exec'ed in place).  8-GPU RCCL runs are the driver's (SCALE_rNN.json).
 """
@@ -170,3 +174,25 @@ def test_two_rank_gloo_partials_from_the_hip_engine(tmp_path):
     np.testing.assert_array_equal(got["ck"], ck)
     np.testing.assert_array_equal(got["iv"].view(np.uint64), iv)
     assert int(cnt.sum()) < N  # the tampered reports are out
+
+
+def test_bench_step_two_ranks_gloo():
+    """bench.py --gpus 2 over gloo on one GPU: the timed step, the AggregateCombiner and the HIP
+    combine kernels, with the combined result checked against the oracle on rank 0."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--dist-backend", "gloo", "--reports", "16384", "--steps", "2",
+           "--warmup", "1", "--no-cpu-baseline", "--check-combined"]
+    p = subprocess.run(cmd, cwd=ROOT, env=dict(os.environ, PYTHONPATH=ROOT), capture_output=True,
+                       timeout=300)
+    out = p.stdout.decode(errors="replace")
+    assert p.returncode == 0, out + p.stderr.decode(errors="replace")[-4000:]
+    line = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["dist_backend"] == "gloo"
+    assert line["config"]["global_batch"] == 2 * 16384
+    assert line["checks"]["combined_matches_oracle"] is True
+    assert line["checks"]["agg_count"] == 2 * 16384  # honest reports: every one counted
