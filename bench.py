@@ -25,6 +25,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from janus_amd import prio3 as J  # noqa: E402
+import roofline_model as RM  # noqa: E402
 
 METRIC = "reports prepared+aggregated/sec (helper, Prio3Histogram len=256) at 1/2/4/8 GPUs"
 VK = bytes.fromhex("4a414e55532d414d442d42454e434821")
@@ -109,6 +110,33 @@ def valu_model(kernel: str, length=256, chunk=16) -> float:
 PEAK_VALU_NOMINAL = 256 * 4 * 32 * 2.4e9  # 78.6e12 lane-instr/s
 MEASURED_ISSUE_T = 64.5
 PEAK_HBM = 8.0e12
+
+
+ISSUED_PATH = os.path.join(ROOT, "profiles", "issued_per_report.json")
+
+
+def model_roofline(line: str, model: dict, n: int, steps: int, elapsed: float,
+                   note: str = "") -> dict:
+    """Roofline of a whole step from roofline_model: achieved = the frozen
+    minimum-instruction model per report x reports/s; peak = the guide's 78.6 T VALU issue rate.
+    issued_over_model: PMC SQ_INSTS_VALU x 64 per report of the same step (committed table
+    profiles/issued_per_report.json, tools/pmc_issued.py) over the model."""
+    peak_T = PEAK_VALU_NOMINAL / 1e12
+    ach = model["total"] * n * steps / elapsed / 1e12
+    r = dict(bound="valu", achieved=ach, peak=peak_T,
+             unit="T lane-instr/s (achieved = roofline_model.py minimum-instruction model x "
+                  "reports/s over the whole step; peak = guide vector rate)",
+             frac=ach / peak_T, frac_of_measured_issue=ach / MEASURED_ISSUE_T,
+             model_instr_per_report=model["total"],
+             model_parts={k: v for k, v in model.items() if k != "total"}, traffic=None)
+    if note:
+        r["note"] = note
+    issued = json.load(open(ISSUED_PATH)) if os.path.exists(ISSUED_PATH) else {}
+    if line in issued:
+        r["issued_instr_per_report"] = issued[line]["issued_instr_per_report"]
+        r["issued_over_model"] = issued[line]["issued_instr_per_report"] / model["total"]
+        r["issued_source"] = issued[line]["source"]
+    return r
 
 
 def cpu_threads() -> int:
@@ -636,6 +664,9 @@ def leader_main(args):
                                      "Prio3Sum bits=32") + " leader prepare_init+prepare_next+"
                                     "aggregate", reports_per_gpu=n),
                kernels=per_kernel,
+               roofline=model_roofline(f"leader_{args.leader_vdaf}", RM.leader_model(
+                   RM.instance("histogram", sz, length=256, chunk=16) if hist else
+                   RM.instance("sum", sz, bits=32)), n, args.steps, elapsed),
                checks=dict(helper_finished=helper_ok,
                            leader_finished=int((lstatus == 0).sum().item()),
                            leader_prep_shares_equal_generator=same, agg_count=int(cnt[0].item())),
@@ -721,17 +752,9 @@ def hpke_main(args):
     op.set_timing(False)
     value = n * args.steps / elapsed
     ms_avg = ms_total / max(launches, 1)
-    counts = json.load(open(COUNTS_PATH)) if os.path.exists(COUNTS_PATH) else dict(kernels={})
-    kc = counts["kernels"].get("k_hpke_open", {})
-    roofline = None
-    if "valu_instr_per_item" in kc and aead == 1 and kem == H.KEM_X25519:  # counts: that kernel
-        ach = kc["valu_instr_per_item"] * n / (ms_avg / 1e3) / 1e12
-        roofline = dict(bound="valu", achieved=ach, peak=PEAK_VALU_NOMINAL / 1e12,
-                        unit="T lane-instr/s (32-bit VALU issue; peak = guide vector rate)",
-                        frac=ach / (PEAK_VALU_NOMINAL / 1e12),
-                        frac_of_measured_issue=ach / MEASURED_ISSUE_T, traffic=kc.get("bytes"),
-                        kernel="k_hpke_open", ms_avg=ms_avg,
-                        valu_instr_per_report=kc["valu_instr_per_item"])
+    roofline = model_roofline(f"hpke_{args.hpke_kem}_aead{aead}",
+                              RM.hpke_model(args.hpke_kem, aead), n, args.steps, elapsed)
+    roofline.update(kernel="k_hpke_open", ms_avg=ms_avg)
     ok = int((status == 0).sum().item())
     out = dict(metric=f"helper input shares HPKE-opened+decoded/sec ({kem_name}-HKDF-SHA256, "
                       f"{aead_name})", value=value, unit="reports/s", n_gpus=1, steps=args.steps,
@@ -860,6 +883,7 @@ def pipeline_main(args):
                config=dict(workload="DAP-09 AggregationJobInitializeReq -> AggregationJobResp, "
                                     "helper, Prio3Histogram(256,16), X25519-HKDF-SHA256/"
                                     "AES-128-GCM", reports=n, request_bytes=len(body)),
+               roofline=model_roofline("pipeline", _pipeline_model(eng.sz), n, args.steps, elapsed),
                checks=dict(finished=ok, unpack_mismatch=int(res["mism"][0]),
                            response_bytes=resp_len,
                            response_len_expected=4 + ok * 42 + (n - ok) * 18))
@@ -885,6 +909,15 @@ def pipeline_main(args):
             np.array_equal(st[:m].cpu().numpy(), cs) and
             np.array_equal(msgs[:m].cpu().numpy(), cm))
     print(json.dumps(out), flush=True)
+
+
+def _pipeline_model(sz) -> dict:
+    """HPKE open (X25519, AES-128-GCM) + the Histogram(256,16) helper step + the ReportIdChecksum
+    (one SHA-256 compression per report id); the DAP codec is byte movement (HBM), not VALU."""
+    h = RM.hpke_model("x25519", 1)
+    p = RM.helper_model(RM.instance("histogram", sz, length=256, chunk=16))
+    parts = dict(hpke=h["total"], prepare=p["total"], checksum=RM.PRIM["sha256_compress"])
+    return dict(parts, total=sum(parts.values()))
 
 
 def _mp64_reports(args):
@@ -959,6 +992,8 @@ def mp64_main(args):
                            chunk_length=16, reports=n),
                kernels={k: dict(ms_total=v[0], launches=v[1], ms_avg=v[0] / max(v[1], 1))
                         for k, v in times.items()},
+               roofline=model_roofline("mp64", RM.mp64_model(eng.sz, cfg[1], cfg[2], cfg[3], cfg[0]),
+                                       n, args.steps, elapsed),
                checks=dict(finished=int((status == 0).sum().item()), agg_count=int(cnt[0])),
                cpu_baseline=None)
     if not args.no_cpu_baseline:
@@ -1121,6 +1156,8 @@ def fpvec_main(args):
                                     "prepare+aggregate (configs[4], C5)", length=10000, bits=16,
                            reports=n),
                kernels=kern,
+               roofline=model_roofline("fpvec", RM.helper_model(RM.instance(
+                   "fpvec", eng.sz, bits=16, length=10000)), n, args.steps, elapsed),
                checks=dict(finished=int((status == 0).sum().item()), agg_count=int(cnt[0]),
                            prep_msgs_match=ok_msgs, agg_sample_match=bool(ok_agg),
                            cpu_gpu_parity_on_sample=cpu_parity if cpu else None),
@@ -1215,6 +1252,9 @@ def config_main(args):
                            reports=n, **{k: v for k, v in okw.items() if k != "kind"}),
                kernels={k: dict(ms_total=v[0], launches=v[1], ms_avg=v[0] / max(v[1], 1))
                         for k, v in times.items()},
+               roofline=model_roofline(f"config_{args.vdaf}", RM.helper_model(RM.instance(
+                   okw["kind"], sz, bits=okw.get("bits", 0), length=okw.get("length", 0),
+                   chunk=okw.get("chunk_length", 0))), n, args.steps, elapsed),
                checks=dict(finished=int((status == 0).sum().item()), agg_count=int(cnt[0]),
                            generator_flags=flags, cpu_gpu_parity_on_sample=parity),
                cpu_baseline=cpu, speedup_vs_cpu=(value / cpu["value"]) if cpu else None)

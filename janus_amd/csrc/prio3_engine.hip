@@ -2763,6 +2763,9 @@ static int ensure_side_streams(prio3_engine* e) {
 // in one launch; the conditions under which launch_prepare would launch exactly those two).
 static bool prep_fused_takes(const prio3_engine* e, const DevParams& dp, bool fuse) {
   if (e->force_generic) return false;
+#ifdef JANUS_AB_NO_PREP_FUSED  // A/B build: the two-kernel chain (k_xofd + k_query_h)
+  if (dp.kind != PRIO3_SUM) return false;
+#endif
   const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
   const bool dual = dp.es == 16 && dp.jr_len && (42 + dp.meas_len * 16) / 168 >= 2;
   if (dp.kind == PRIO3_SUM) return dual && !fuse && query_sum_takes(dp);  // k_prep_sum
