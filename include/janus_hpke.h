@@ -110,6 +110,13 @@ int janus_hpke_open(janus_hpke_opener* opener, uint32_t n, const uint8_t* enc, c
 int janus_hpke_set_timing(janus_hpke_opener* opener, int on);
 int janus_hpke_timing(janus_hpke_opener* opener, double* ms_total, uint32_t* launches);
 
+/* Test-only: one GF(p256) operation of the P-256 KEM's device field code over n host operand
+ * pairs (8 x 32-bit LE limbs each, loosely reduced in [0, 2^256)) -- op 0 a*b, 1 a^2, 2 a+b,
+ * 3 a-b, 4 3a, 5 8a, 6 a^(p-2); results loosely reduced.  Pins the generated asm
+ * (tools/gen_p256_asm.py) against Python integers. */
+int janus_hpke_selftest_p256(int op, uint32_t n, const uint32_t* a, const uint32_t* b,
+                             uint32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

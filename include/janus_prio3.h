@@ -269,7 +269,8 @@ int prio3_client_generate_device(prio3_engine* engine, uint32_t n, uint64_t seed
  * launch variants prio3_engine.hip's prio3_engine_set_option lists. */
 int prio3_engine_set_option(prio3_engine* engine, const char* key, int64_t value);
 /* Per-kernel device time (ms) accumulated since the last reset, measured with HIP events
- * on the launch stream when option "timing" is 1.  names: comma-separated kernel names. */
+ * on the launch stream when option "timing" is 1 (2: launches counted, no events or times).
+ * names: comma-separated kernel names. */
 int prio3_engine_timing(prio3_engine* engine, char* names, size_t names_cap, double* ms,
                         uint64_t* launches, int cap);
 void prio3_engine_timing_reset(prio3_engine* engine);

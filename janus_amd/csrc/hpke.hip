@@ -620,8 +620,11 @@ DEV void load_words(const uint8_t* p, uint32_t* w, int n16) {
 // 65-byte uncompressed point)
 // The AEAD is a kernel argument (P.aead, wave-uniform): one instance per (MODE, PUB, KEM) keeps
 // the X25519 / P-256 ladders to six copies.
+#ifndef HPKE_WAVES  // A/B builds: e.g. -DHPKE_WAVES='__attribute__((amdgpu_waves_per_eu(3, 3)))'
+#define HPKE_WAVES
+#endif
 template <int MODE, int PUB, int KEM>
-__global__ __launch_bounds__(256) void k_hpke_open(HpkeParams P, OpenArgs a) {
+__global__ __launch_bounds__(256) HPKE_WAVES void k_hpke_open(HpkeParams P, OpenArgs a) {
   static_assert(KEM == 0x20 || KEM == 0x10, "KEM id");
   const uint32_t AEAD = P.aead;
   const uint32_t NK = AEAD == 1 ? 16 : 32;  // Nk: AEAD key bytes
@@ -813,7 +816,11 @@ __global__ __launch_bounds__(256) void k_hpke_open(HpkeParams P, OpenArgs a) {
 #pragma unroll
     for (int b = 0; b < (AW + 3) / 4; b++) ghash_block(y, aw + 4 * b, H);
   } else {
-    aad_len = a.aad_len[r];
+    // a per-report length past the row stride would authenticate the next rows (or read past
+    // the buffer): such a report fails to open, and only its own row is read
+    const uint32_t al = a.aad_len[r];
+    ok = ok && al <= a.aad_stride;
+    aad_len = al <= a.aad_stride ? al : a.aad_stride;
     const uint8_t* ap = a.aad + (size_t)a.aad_stride * r;
     for (uint32_t off = 0; off < aad_len; off += 16) {
       uint32_t xw[4];
@@ -914,7 +921,11 @@ __global__ __launch_bounds__(256) void k_hpke_open(HpkeParams P, OpenArgs a) {
 #pragma unroll
     for (int b = 0; b < (AW + 3) / 4; b++) poly_block(mac, aw + 4 * b);
   } else {
-    aad_len = a.aad_len[r];
+    // a per-report length past the row stride would authenticate the next rows (or read past
+    // the buffer): such a report fails to open, and only its own row is read
+    const uint32_t al = a.aad_len[r];
+    ok = ok && al <= a.aad_stride;
+    aad_len = al <= a.aad_stride ? al : a.aad_stride;
     const uint8_t* ap = a.aad + (size_t)a.aad_stride * r;
     for (uint32_t off = 0; off < aad_len; off += 16) {
       uint32_t xw[4];
@@ -1369,6 +1380,30 @@ int up(DevBuf& b, const void* h, size_t bytes, hipStream_t st) {
 }
 }  // namespace
 
+// Test-only (janus_hpke_selftest_p256): one GF(p256) operation of p256_device.h per element.
+__global__ __launch_bounds__(256) void k_selftest_p256(int op, uint32_t n, const uint32_t* a,
+                                                       const uint32_t* b, uint32_t* out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  p256::fp x, y, r;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    x.v[k] = a[8 * (size_t)i + k];
+    y.v[k] = b[8 * (size_t)i + k];
+  }
+  switch (op) {
+    case 0: r = p256::mul(x, y); break;
+    case 1: r = p256::sqr(x); break;
+    case 2: r = p256::add(x, y); break;
+    case 3: r = p256::sub(x, y); break;
+    case 4: r = p256::mul_small(x, 3); break;
+    case 5: r = p256::mul_small(x, 8); break;
+    default: r = p256::inv(x); break;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; k++) out[8 * (size_t)i + k] = r.v[k];
+}
+
 extern "C" {
 
 int janus_hpke_open_input_shares(janus_hpke_opener* o, uint32_t n, const uint8_t task_id[32],
@@ -1401,6 +1436,29 @@ int janus_hpke_open_input_shares(janus_hpke_opener* o, uint32_t n, const uint8_t
   HCHK(hipMemcpyAsync(status, dst.p, n, hipMemcpyDeviceToHost, o->stream));
   HCHK(hipStreamSynchronize(o->stream));
   return JANUS_HPKE_SUCCESS;
+}
+
+int janus_hpke_selftest_p256(int op, uint32_t n, const uint32_t* a, const uint32_t* b,
+                             uint32_t* out) {
+  if (op < 0 || op > 6) return JANUS_HPKE_EINVAL;
+  if (n == 0) return JANUS_HPKE_OK;
+  const size_t m = (size_t)n * 32;
+  void *da = nullptr, *db = nullptr, *dout = nullptr;
+  int rc = JANUS_HPKE_OK;
+  if (hipMalloc(&da, m) != hipSuccess || hipMalloc(&db, m) != hipSuccess ||
+      hipMalloc(&dout, m) != hipSuccess || hipMemcpy(da, a, m, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(db, b, m, hipMemcpyHostToDevice) != hipSuccess) {
+    rc = JANUS_HPKE_EDEVICE;
+  } else {
+    k_selftest_p256<<<(n + 255) / 256, 256>>>(op, n, (const uint32_t*)da, (const uint32_t*)db,
+                                              (uint32_t*)dout);
+    if (hipGetLastError() != hipSuccess || hipMemcpy(out, dout, m, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = JANUS_HPKE_EDEVICE;
+  }
+  (void)hipFree(da);
+  (void)hipFree(db);
+  (void)hipFree(dout);
+  return rc;
 }
 
 int janus_hpke_open(janus_hpke_opener* o, uint32_t n, const uint8_t* enc, const uint8_t* ct,

@@ -16,18 +16,21 @@
 #ifndef DEV
 #define DEV __device__ __forceinline__
 #endif
+#ifndef P256_TAB_MEM
+#define P256_TAB_MEM 0  // 1: the window table in private memory instead of registers (A/B)
+#endif
 #ifndef P256_ASM
 #define P256_ASM 1  // 1: the generated single-asm-statement products (p256_asm.h)
 #endif
-#if P256_ASM
-#include "p256_asm.h"  // mul512 / sqr512 (generated: tools/gen_p256_asm.py)
-#endif
-
 namespace p256 {
 
 struct fp {
   uint32_t v[8];
 };
+
+#if P256_ASM
+#include "p256_asm.h"  // p256_mul / sqr / add / sub / mul_small (generated: tools/gen_p256_asm.py)
+#endif
 
 // carry-propagate signed word sums t[0..7] (each |t| < 2^40) into [0, 2^256), folding the
 // carry out of 2^256 twice (the second carry is in {-1, 0, 1}, the third always 0)
@@ -54,6 +57,13 @@ DEV fp fold(int64_t t[8]) {
   return r;
 }
 
+#if P256_ASM
+DEV fp add(const fp& a, const fp& b) { return p256_add(a, b); }
+DEV fp sub(const fp& a, const fp& b) { return p256_sub(a, b); }
+DEV fp mul_small(const fp& a, uint32_t k) { return p256_mul_small(a, k); }  // k <= 8
+DEV fp mul(const fp& a, const fp& b) { return p256_mul(a, b); }
+DEV fp sqr(const fp& a) { return p256_sqr(a); }
+#else
 DEV fp add(const fp& a, const fp& b) {
   int64_t t[8];
 #pragma unroll
@@ -88,12 +98,8 @@ DEV fp reduce(const uint32_t c[16]) {
   return fold(t);
 }
 
-// out of line: ~20 call sites in the point formulas (compile time, code size)
 __device__ __noinline__ fp mul(const fp& a, const fp& b) {
   uint32_t c[16];
-#if P256_ASM
-  mul512(a.v, b.v, c);
-#else
 #pragma unroll
   for (int i = 0; i < 16; i++) c[i] = 0;
 #pragma unroll
@@ -107,47 +113,10 @@ __device__ __noinline__ fp mul(const fp& a, const fp& b) {
     }
     c[i + 8] = (uint32_t)carry;
   }
-#endif
   return reduce(c);
 }
-
-// a^2 with 36 word products instead of 64: the 28 cross products once, doubled by a one-bit
-// shift, plus the 8 squares on the diagonal
-__device__ __noinline__ fp sqr(const fp& a) {
-  uint32_t c[16];
-#if P256_ASM
-  sqr512(a.v, c);
-#else
-#pragma unroll
-  for (int i = 0; i < 16; i++) c[i] = 0;
-#pragma unroll
-  for (int i = 0; i < 7; i++) {
-    uint64_t carry = 0;
-#pragma unroll
-    for (int j = i + 1; j < 8; j++) {
-      const uint64_t x = (uint64_t)a.v[i] * a.v[j] + c[i + j] + carry;
-      c[i + j] = (uint32_t)x;
-      carry = x >> 32;
-    }
-    c[i + 8] = (uint32_t)carry;
-  }
-  uint32_t top = 0;  // the bit shifted out of the previous word pair
-  uint64_t cy = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const uint32_t e = c[2 * i], o = c[2 * i + 1];
-    const uint32_t d0 = e << 1 | top, d1 = o << 1 | e >> 31;
-    top = o >> 31;
-    const uint64_t sq = (uint64_t)a.v[i] * a.v[i];
-    const uint64_t t0 = (uint64_t)d0 + (uint32_t)sq + cy;
-    const uint64_t t1 = (uint64_t)d1 + (sq >> 32) + (t0 >> 32);
-    c[2 * i] = (uint32_t)t0;
-    c[2 * i + 1] = (uint32_t)t1;
-    cy = t1 >> 32;
-  }
-#endif
-  return reduce(c);
-}
+__device__ __noinline__ fp sqr(const fp& a) { return mul(a, a); }
+#endif  // P256_ASM
 
 // canonical representative in [0, p)
 DEV fp freeze(const fp& a) {
@@ -181,16 +150,27 @@ DEV bool is_zero(const fp& a) {
   return d == 0;
 }
 
-// a^(p - 2): p - 2 = ffffffff 00000001 00000000 00000000 00000000 ffffffff ffffffff fffffffd
-DEV fp inv(const fp& a) {
-  constexpr uint32_t E[8] = {0xfffffffdu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u, 1u, 0xffffffffu};
-  fp r = a;  // the top bit of E is set
+// a^(p - 2) by an addition chain: p - 2 = [32 ones][31 zeros][1][96 zeros][94 ones][0][1]
+// (MSB first); x_k = a^(2^k - 1).  255 squarings + 12 multiplies (the bit loop took 128).
+DEV fp sqr_n(fp x, int n) {
 #pragma unroll 1
-  for (int i = 254; i >= 0; i--) {
-    r = sqr(r);
-    if ((E[i >> 5] >> (i & 31)) & 1u) r = mul(r, a);
-  }
-  return r;
+  for (int i = 0; i < n; i++) x = sqr(x);
+  return x;
+}
+DEV fp inv(const fp& a) {
+  const fp x2 = mul(sqr(a), a);
+  const fp x3 = mul(sqr(x2), a);
+  const fp x6 = mul(sqr_n(x3, 3), x3);
+  const fp x12 = mul(sqr_n(x6, 6), x6);
+  const fp x15 = mul(sqr_n(x12, 3), x3);
+  const fp x30 = mul(sqr_n(x15, 15), x15);
+  const fp x32 = mul(sqr_n(x30, 2), x2);
+  fp t = mul(sqr_n(x32, 32), a);   // [32 ones][31 zeros][1]
+  t = sqr_n(t, 96);                // [96 zeros]
+  t = mul(sqr_n(t, 32), x32);      // [32 ones]
+  t = mul(sqr_n(t, 32), x32);      // [32 ones]
+  t = mul(sqr_n(t, 30), x30);      // [30 ones]
+  return mul(sqr_n(t, 2), a);      // [0][1]
 }
 
 // 32 big-endian bytes -> limbs; false if the value is >= p (a non-canonical coordinate)
@@ -284,6 +264,18 @@ DEV bool ecdh(const int8_t* dig, const uint8_t* enc, uint32_t dh_be[8]) {
     const jac P4 = dbl(P2);
     to_affine3(madd(P2, x, y), madd(P4, x, y), madd(dbl(P4), x, neg(y)), x3, y3, x5, y5, x7, y7);
   }
+#if P256_TAB_MEM
+  // the table in the lane's private memory (indexed by the wave-uniform digit: one 64-byte read
+  // per window, L1/L2-resident), so the ladder's registers fit three waves per SIMD
+  fp tab[4][2] = {{x, y}, {x3, y3}, {x5, y5}, {x7, y7}};
+  auto pick = [&](int d, fp& tx, fp& ty) {
+    const int a = (d < 0 ? -d : d) >> 1;
+    tx = tab[a][0];
+    ty = tab[a][1];
+    const fp ny = neg(ty);
+    if (d < 0) ty = ny;
+  };
+#else
   auto pick = [&](int d, fp& tx, fp& ty) {
     const int a = d < 0 ? -d : d;
 #pragma unroll
@@ -294,17 +286,22 @@ DEV bool ecdh(const int8_t* dig, const uint8_t* enc, uint32_t dh_be[8]) {
     const fp ny = neg(ty);
     if (d < 0) ty = ny;
   };
+#endif
   jac R;
   pick(dig[kDigits - 1], R.X, R.Y);
   R.Z = ONE;
+  // one doubling and one addition in the loop body (the inlined asm field operations make each
+  // ~3k instructions; three unrolled doublings would not fit the instruction cache)
 #pragma unroll 1
   for (int i = kDigits - 2; i >= 1; i--) {
-    R = dbl(dbl(dbl(R)));
+#pragma unroll 1
+    for (int j = 0; j < 3; j++) R = dbl(R);
     fp tx, ty;
     pick(dig[i], tx, ty);
     R = madd(R, tx, ty);
   }
-  R = dbl(dbl(dbl(R)));
+#pragma unroll 1
+  for (int j = 0; j < 3; j++) R = dbl(R);
   {
     fp tx, ty;
     pick(dig[0], tx, ty);

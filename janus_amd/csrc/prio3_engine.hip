@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <type_traits>
@@ -234,14 +235,19 @@ __device__ __forceinline__ void xofd_body(const DevParams& p, const InPtrs& in, 
                                           const uint32_t r) {  // r & 63 == this lane
   typedef Fp128 F;
   const uint32_t lane = threadIdx.x & 63u;
-  bool fuse = false;
+  bool fuse = false, oor = false, haspad = false;
   uint32_t s0 = 0;
   if constexpr (FUSE) {
     const bool valid = r < p.n;
     const uint32_t sg = valid ? (sc.seg ? sc.seg[r] : 0u) : 0xffffffffu;
-    s0 = (uint32_t)__shfl((int)sg, 0);
-    // a segment id >= n_segments excludes the report from every aggregate (never fused)
-    fuse = __all(valid && sg == s0 && sg < p.nseg);
+    // A segment id >= n_segments puts the report in no aggregate.  Such lanes (the executor's
+    // pad columns between jobs, excluded reports) are masked out of the wave partials, so they
+    // do not keep the wave's other 63 reports from fusing; k_agg_fix knows them (oor_masked).
+    const uint64_t inr = __ballot(valid && sg < p.nseg);
+    s0 = inr ? (uint32_t)__shfl((int)sg, __ffsll((long long)inr) - 1) : 0xffffffffu;
+    oor = valid && sg >= p.nseg;
+    fuse = inr != 0 && __all(valid && (sg == s0 || sg >= p.nseg));
+    haspad = __any(oor);
     if (lane == 0 && (r - lane) < p.n && !fuse) sc.wseg[r >> 6] = 0xffffffffu;
   }
   if (r >= p.n) return;
@@ -290,8 +296,12 @@ __device__ __forceinline__ void xofd_body(const DevParams& p, const InPtrs& in, 
   TruncSink ts(p, sc.out, r);
   const int Mi = (int)M;
   // wave totals of share elements e0, e0+1 (zero outside [0, M)), slot lane of lanes 0..15
-  auto fused_pair = [&](int e0, const f128& a, const f128& b2) __attribute__((always_inline)) {
+  auto fused_pair = [&](int e0, f128 a, f128 b2) __attribute__((always_inline)) {
     if (e0 >= Mi) return;  // wave-uniform
+    if (haspad && oor) {   // wave-uniform test; the masked lanes add nothing
+      a = zero128();
+      b2 = zero128();
+    }
     const uint32_t tot = wave_halfsum2(a, b2, lane);
     const int e = e0 + (int)((lane >> 3) & 1u);
     if (lane < 16 && e < Mi)
@@ -1569,7 +1579,10 @@ __global__ __launch_bounds__(256, 3) void k_prep_h(DevParams p, InPtrs in, Scrat
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   xofd_body<FUSE, false>(p, in, sc, r);
 #ifndef JANUS_AB_XOF_ONLY  // A/B build: the fused kernel's XOF half alone
-  query_h_body<2, 32>(p, in, sc, out, r);
+#ifndef QH_GS
+#define QH_GS 2  // wires per sweep of the fused kernel's query (A/B builds: 3, 4)
+#endif
+  query_h_body<QH_GS, 32>(p, in, sc, out, r);
 #endif
 }
 
@@ -1809,33 +1822,59 @@ __global__ __launch_bounds__(256) void k_agg_waves(uint32_t nwaves, uint32_t M,
     o[0] = a0, o[1] = a1, o[2] = a2, o[3] = a3;
     return;
   }
-  for (uint32_t k = 0; k < 4; k++) {
-    unsigned long long acc = 0;
-    uint32_t cur = 0xffffffffu;
-    for (uint32_t w = w0; w < w1; w++) {
-      const uint32_t sg = wseg[w];
+  // segment runs inside the chunk (e.g. the executor's jobs of a few waves each): the loads in
+  // batches of 8 waves, unconditional (clamped, masked), the run boundaries read from `my` by
+  // shuffle (wave-uniform), one 64-bit atomic per run and slot
+  unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+  uint32_t cur = 0xffffffffu;
+  auto flush = [&]() {
+    if (cur == 0xffffffffu) return;
+    unsigned long long* o = agg64 + (size_t)cur * row + slot;
+    if (a0) atomicAdd(o, a0);
+    if (a1) atomicAdd(o + 1, a1);
+    if (a2) atomicAdd(o + 2, a2);
+    if (a3) atomicAdd(o + 3, a3);
+  };
+#pragma unroll 1
+  for (uint32_t b = 0; b < WCH; b += 8) {
+    uint4 v[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 8; j++)
+      v[j] = *(const uint4*)(wpart + (size_t)min(w0 + b + j, w1 - 1) * row + slot);
+#pragma unroll
+    for (uint32_t j = 0; j < 8; j++) {
+      // v_readlane ignores EXEC: `my` was written with every lane active (lanes past the last
+      // slot have returned by now); ~0 = absent or unfused
+      const uint32_t sg = (uint32_t)__builtin_amdgcn_readlane((int)my, (int)(b + j));
       if (sg == 0xffffffffu) continue;
       if (sg != cur) {
-        if (cur != 0xffffffffu && acc) atomicAdd(&agg64[(size_t)cur * row + slot + k], acc);
+        flush();
         cur = sg;
-        acc = 0;
+        a0 = a1 = a2 = a3 = 0;
       }
-      acc += wpart[(size_t)w * row + slot + k];
+      a0 += v[j].x, a1 += v[j].y, a2 += v[j].z, a3 += v[j].w;
     }
-    if (cur != 0xffffffffu && acc) atomicAdd(&agg64[(size_t)cur * row + slot + k], acc);
   }
+  flush();
 }
 
 // Counts the reports the aggregate must contain (status FINISHED and accepted by the host
 // mask) per segment and lists every report whose fused inclusion differs (entry = r, or
 // r | 0x80000000 when it must be subtracted).  A block covers FIX_R consecutive reports and
 // keeps its counts in a small LDS table keyed by segment, flushed with one atomic per entry.
-constexpr uint32_t FIX_R = 4096, FIX_T = 64;
+// per: reports per block (4096 for large runs; 512 for the executor's 20-60k-report groups,
+// whose 4096-report blocks left most of the chip idle)
+constexpr uint32_t FIX_T = 64;
+static uint32_t fix_per(uint32_t n) { return n >= (1u << 18) ? 4096u : 512u; }
+// oor_masked: the fused kernel masked lanes with an out-of-range segment id out of its wave
+// partials (xofd_body); they are then not part of a fused wave's sum.  0: the wave partials
+// include them (the fused leader unpack), so they are subtracted like any excluded report.
 __global__ __launch_bounds__(256) void k_agg_fix(uint32_t n, const uint8_t* status,
                                                  const uint32_t* seg, const uint8_t* accept,
                                                  const uint32_t* wseg, uint32_t* fix,
                                                  uint32_t fix_cap, uint32_t nseg,
-                                                 unsigned long long* counts) {
+                                                 unsigned long long* counts, uint32_t oor_masked,
+                                                 uint32_t per) {
   __shared__ uint32_t tseg[FIX_T];
   __shared__ unsigned int tcnt[FIX_T];
   if (threadIdx.x < FIX_T) {
@@ -1843,7 +1882,7 @@ __global__ __launch_bounds__(256) void k_agg_fix(uint32_t n, const uint8_t* stat
     tcnt[threadIdx.x] = 0;
   }
   __syncthreads();
-  const uint32_t lo = blockIdx.x * FIX_R, hi = min(n, lo + FIX_R);
+  const uint32_t lo = blockIdx.x * per, hi = min(n, lo + per);
   for (uint32_t base = lo; base < hi; base += 256) {
     const uint32_t r = base + threadIdx.x;
     const bool valid = r < hi;
@@ -1851,7 +1890,7 @@ __global__ __launch_bounds__(256) void k_agg_fix(uint32_t n, const uint8_t* stat
     // out-of-range segment ids are excluded everywhere (as k_mask and k_meta do)
     const bool inc = valid && sg < nseg && status[r] == PRIO3_STATUS_FINISHED &&
                      (!accept || accept[r]);
-    const bool fused = valid && wseg[r >> 6] != 0xffffffffu;
+    const bool fused = valid && wseg[r >> 6] != 0xffffffffu && (!oor_masked || sg < nseg);
     const uint32_t s0 = (uint32_t)__shfl((int)sg, 0);
     const bool uni = __all(!valid || sg == s0);
     const unsigned long long b = __ballot(inc);
@@ -1875,6 +1914,9 @@ __global__ __launch_bounds__(256) void k_agg_fix(uint32_t n, const uint8_t* stat
   if (threadIdx.x < FIX_T && tseg[threadIdx.x] != 0xffffffffu && tcnt[threadIdx.x])
     atomicAdd(&counts[tseg[threadIdx.x]], (unsigned long long)tcnt[threadIdx.x]);
 }
+
+DEV f128 fold_halves_impl(const unsigned long long (&Hs)[8]);
+DEV f128 fold_halves(const unsigned long long (&Hs)[8]) { return fold_halves_impl(Hs); }
 
 // One block per (segment, element): thread (half h = tid & 7, lane cl = tid >> 3) sums the chunk
 // partials of its segment for chunks cl, cl+32, ...; then the fix-up list is applied by all
@@ -1920,9 +1962,67 @@ __global__ __launch_bounds__(256) void k_agg_final(uint32_t M, size_t ld,
     __syncthreads();
   }
   if (tid != 0) return;
+  unsigned long long Hs[8];
+  for (int hh = 0; hh < 8; hh++) Hs[hh] = red[hh] + agg64[(size_t)idx * 8 + hh];
+  Fp128::store(agg, idx, sub128(add128(fold_halves(Hs), fadd[0]), fsub[0]));
+}
+
+// Runs with few chunks and many segments (the executor's groups: one segment per job, 2-8 waves
+// each): one block per (segment, 32 elements), thread (element tid / 8, half h = tid % 8), so a
+// block does not reduce 256 threads through LDS for one element; the fix-up list (empty when
+// every wave fused) is split over the 8 halves and summed by shuffles.
+__global__ __launch_bounds__(256) void k_agg_final_s(uint32_t M, size_t ld,
+                                                     const unsigned long long* agg64,
+                                                     uint32_t nchunks,
+                                                     const unsigned long long* cpart,
+                                                     const uint32_t* cseg, const uint32_t* fix,
+                                                     const uint32_t* seg, const void* meas,
+                                                     uint8_t* agg) {
+  const uint32_t s = blockIdx.y, tid = threadIdx.x, h = tid & 7u, lane = tid & 63u;
+  const uint32_t e = blockIdx.x * 32u + (tid >> 3);
+  const bool live = e < M;
+  const uint32_t ec = live ? e : 0u;
+  unsigned long long H = agg64[((size_t)s * M + ec) * 8 + h];
+  for (uint32_t c = 0; c < nchunks; c++)
+    if (cseg[c] == s) H += cpart[((size_t)c * M + ec) * 8 + h];
+  f128 ad = zero128(), sb = zero128();
+  const uint32_t nfix = fix[0];
+  for (uint32_t i = h; i < nfix; i += 8) {
+    const uint32_t ent = fix[1 + i], r = ent & 0x7fffffffu;
+    if ((seg ? seg[r] : 0u) != s) continue;
+    const f128 x = Fp128::load(meas, (size_t)ec * ld + r);
+    if (ent & 0x80000000u) sb = add128(sb, x);
+    else ad = add128(ad, x);
+  }
+  if (nfix) {  // block-uniform
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) {
+      f128 xa, xs;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        xa.w[k] = (uint32_t)__shfl_xor((int)ad.w[k], m);
+        xs.w[k] = (uint32_t)__shfl_xor((int)sb.w[k], m);
+      }
+      ad = add128(ad, xa);
+      sb = add128(sb, xs);
+    }
+  }
+  unsigned long long Hs[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const int src = (int)((lane & ~7u) + (uint32_t)k);
+    Hs[k] = ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(H >> 32), src) << 32) |
+            (uint32_t)__shfl((int)(uint32_t)H, src);
+  }
+  if (h != 0 || !live) return;
+  Fp128::store(agg, (size_t)s * M + e, sub128(add128(fold_halves(Hs), ad), sb));
+}
+
+// X = sum_h H_h 2^(16h) (H_h < 2^48) mod p
+DEV f128 fold_halves_impl(const unsigned long long (&Hs)[8]) {
   uint32_t w[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   for (int hh = 0; hh < 8; hh++) {
-    const unsigned long long H = red[hh] + agg64[(size_t)idx * 8 + hh];
+    const unsigned long long H = Hs[hh];
     const int sh = 16 * hh, wi = sh >> 5, bi = sh & 31;
     const unsigned long long lo = bi ? (H << 16) & 0xffffffffull : H & 0xffffffffull;
     const unsigned long long mid = bi ? (H >> 16) & 0xffffffffull : H >> 32;
@@ -1938,9 +2038,7 @@ __global__ __launch_bounds__(256) void k_agg_final(uint32_t M, size_t ld,
       w[k] = (uint32_t)c;
     }
   }
-  f128 v = red288(w, w[8]);
-  v = sub128(add128(v, fadd[0]), fsub[0]);
-  Fp128::store(agg, idx, v);
+  return red288(w, w[8]);
 }
 
 // sum of k partial aggregates (multi-GPU combine)
@@ -2435,10 +2533,17 @@ static size_t time_slot(prio3_engine* e, const char* name) {
   e->times.push_back(KTime{name, 0, 0});
   return e->times.size() - 1;
 }
+// timing 2: launches are counted only (no events: the host-buffer executor's launch path stays
+// as in production, bench.py --role jobs)
+static void count_launch(prio3_engine* e, const char* name) {
+  const size_t i = time_slot(e, name);
+  std::lock_guard<std::mutex> lk(e->tmu);
+  e->times[i].launches += 1;
+}
 #define TIMED(e, st, name, launch)                                   \
   do {                                                               \
     hipEvent_t _a = nullptr, _b = nullptr;                           \
-    const bool _t = (e)->timing && hipEventCreate(&_a) == hipSuccess && \
+    const bool _t = (e)->timing == 1 && hipEventCreate(&_a) == hipSuccess && \
                     hipEventCreate(&_b) == hipSuccess;               \
     if (_t) (void)hipEventRecord(_a, st);                            \
     launch;                                                          \
@@ -2446,6 +2551,8 @@ static size_t time_slot(prio3_engine* e, const char* name) {
     if (_t) {                                                        \
       (void)hipEventRecord(_b, st);                                  \
       pending().push_back(Pending{(e), time_slot(e, name), _a, _b}); \
+    } else if ((e)->timing == 2) {                                   \
+      count_launch((e), name);                                       \
     }                                                                \
   } while (0)
 
@@ -2776,9 +2883,14 @@ static bool prep_fused_takes(const prio3_engine* e, const DevParams& dp, bool fu
 enum : int { DEFER_NONE = 0, DEFER_QH = 1, DEFER_SUM = 2, DEFER_GEN64 = 3 };
 // *deferred: set when a query kernel of this chain skipped flagged reports (slow_defer); the
 // caller then ends the run with launch_slow_redo
+// lready (nullable): the leader prep shares (in.leader) are not on the device yet; the chain is
+// the two-kernel one (splits_at_query), and lready(st) is called between the XOF launch and the
+// query launch -- it starts their copy on another stream and makes st wait for it, so the copy
+// runs under the XOF (and a host-blocking copy call does not hold back the XOF launch).
+typedef std::function<int(hipStream_t)> LeaderReady;
 static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, uint32_t n,
                           InPtrs in, OutPtrs out, Scratch sc, hipStream_t st, bool fuse,
-                          int* deferred) {
+                          int* deferred, const LeaderReady* lready = nullptr) {
   DevParams dp = base;
   dp.n = n;
   dp.force_slow = (uint32_t)e->force_slow;
@@ -2861,7 +2973,7 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
     dp.trunc_xof = dp.kind == PRIO3_SUMVEC && wide && dual && !fuse ? 1u : 0u;
     // XOF + query in one launch: Prio3Sum (k_prep_sum) and Histogram / SumVec with P = 32
     // (k_prep_h); the slow path of both is deferred to the run's redo launch
-    if (prep_fused_takes(e, dp, fuse)) {
+    if (!lready && prep_fused_takes(e, dp, fuse)) {
       dp.slow_defer = 1u;
       if (dp.kind == PRIO3_SUM) {
         if (deferred) *deferred = DEFER_SUM;
@@ -2897,6 +3009,10 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
     // read the shares the k_xof_slow launch rewrote
     const bool qh_path =
         ps && !e->force_generic && !wide && (dp.P == 32 || dp.P == 16 || dp.P == 8);
+    if (lready) {
+      const int rc = (*lready)(st);
+      if (rc) return rc;
+    }
     dp.slow_defer = qh_path ? 1u : 0u;
     if (qh_path && deferred) *deferred = DEFER_QH;
     if (!qh_path) TIMED(e, st, "k_xof_slow", launch_xof_slow<Fp128>(e, dp, in, sc, st));
@@ -2993,9 +3109,24 @@ static int launch_slow_redo(prio3_engine* e, const DevParams& base, uint32_t n, 
 // before and after), so one chunk's memory-bound query overlaps the next chunk's VALU-bound
 // Keccak.  Side streams are per engine: callers that may overlap (the executor's concurrent
 // groups) pass allow_chunks = false.
+// The chains that read the leader prep shares only from the query on (the XOF reads the
+// per-report seeds): Histogram / SumVec with P = 32 on k_xofd + k_query_h.
+static bool splits_at_query(const prio3_engine* e, const DevParams& dp) {
+  return !e->force_generic && (dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC) &&
+         dp.es == 16 && dp.jr_len && (42 + dp.meas_len * 16) / 168 >= 2 && dp.P == 32;
+}
+
+// lready (nullable): makes in.leader hold the leader prep shares (see launch_prepare); the chains
+// that split at the query (splits_at_query) call it after their XOF launch, the others first.
 static int prepare_run(prio3_engine* e, Run* R, InPtrs in, OutPtrs out, hipStream_t st, bool fuse,
-                       bool allow_chunks) {
+                       bool allow_chunks, const LeaderReady* lready = nullptr) {
   const uint32_t n = R->n;
+  if (lready && !splits_at_query(e, R->dp)) {
+    const int rc = (*lready)(st);
+    if (rc) return rc;
+    lready = nullptr;
+  }
+  if (lready) allow_chunks = false;
   Scratch sc = R->sc;
   sc.seg = R->seg;
   sc.wpart = R->wpart;
@@ -3009,7 +3140,7 @@ static int prepare_run(prio3_engine* e, Run* R, InPtrs in, OutPtrs out, hipStrea
   const uint32_t csz = ((n + K - 1) / K + 255) & ~255u;
   int deferred = DEFER_NONE;
   if (!allow_chunks || K == 1 || n <= csz || R->dp.kind == PRIO3_FPVEC_BOUNDED_L2) {
-    const int rc = launch_prepare(e, R->dp, 0, n, in, out, sc, st, fuse, &deferred);
+    const int rc = launch_prepare(e, R->dp, 0, n, in, out, sc, st, fuse, &deferred, lready);
     if (rc == PRIO3_OK && deferred)
       return launch_slow_redo(e, R->dp, n, in, out, sc, st, deferred);
     return rc;
@@ -3150,6 +3281,10 @@ static uint64_t fnv(uint64_t h, const void* p, size_t n) {
   return h;
 }
 
+// aggregating jobs start at a wave boundary where the XOF fuses the accumulate (their waves then
+// hold one job's reports and fuse; the pad columns carry an out-of-range segment id)
+uint32_t engine_job_align(const prio3_engine* e) { return fusable(e) ? 64u : 1u; }
+
 uint64_t engine_group_key(const prio3_engine* e) {
   uint64_t h = 1469598103934665603ull;
   h = fnv(h, &e->params, sizeof e->params);
@@ -3212,12 +3347,24 @@ static int fused_finish(prio3_engine* e, Run* R, const uint8_t* d_status, const 
                         const uint32_t* fix_seg, const uint8_t* d_accept_mask, uint32_t S,
                         uint8_t* d_agg_shares, uint64_t* d_counts, hipStream_t st);
 
+// Host-pull group launch: the kernels read each report's nonce, public share, helper share and
+// verify-key slot straight from the pinned staging (mapped; 96-112 B per report at the start of
+// the XOF), while one copy on a second stream moves the leader prep shares (560 B per report for
+// Histogram(256,16)) and the segment ids / accept bytes into the run; a chain that splits at the
+// query (splits_at_query) runs its XOF under that copy and waits on it only before the query.
+// One pinned-staging H2D copy per field on the launch stream instead (the r02 form) left the
+// PCIe transfer and the prepare in series (profiles/r03/r03e_jobs128_*.json).
 int engine_run_group(prio3_engine* lead, const GroupView& g, Run** run_out) {
   *run_out = nullptr;
   HIPCHK(hipSetDevice(lead->device));
-  PooledStream ps(lead->device);
-  hipStream_t st = ps.s;
-  if (!st) return PRIO3_EDEVICE;
+  PooledStream ps(lead->device), pc(lead->device);
+  hipStream_t st = ps.s, cs = pc.s;
+  if (!st || !cs) return PRIO3_EDEVICE;
+  static thread_local hipEvent_t evs[64][2] = {};
+  if (lead->device >= 64) return PRIO3_EINVAL;
+  hipEvent_t* ev = evs[lead->device];
+  for (int i = 0; i < 2; i++)
+    if (!ev[i]) HIPCHK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
   const bool mp = lead->dp.kind == PRIO3_SUMVEC_F64_MP;
   // aggregating jobs: the group's reports are accumulated per job segment in this launch (the
   // wave partials of the XOF where the instance fuses; waves that straddle two jobs and the
@@ -3232,36 +3379,38 @@ int engine_run_group(prio3_engine* lead, const GroupView& g, Run** run_out) {
   if (!R) return rc;
   IoLayout L;
   engine_io_layout(lead, g.cap, &L);
-  uint8_t* dst[4] = {R->nonces, R->pub, R->helper, R->leader};
   auto fail = [&](int code) {
+    (void)hipStreamSynchronize(cs);
     run_release(R, st, true);
     return code;
   };
-  for (int f = 0; f < 4; f++)
-    if (L.len[f] &&
-        hipMemcpyAsync(dst[f], g.stg + L.off[f], L.len[f] * g.n, hipMemcpyHostToDevice, st) !=
-            hipSuccess)
-      return fail(PRIO3_EDEVICE);
-  InPtrs in{R->nonces, L.len[1] ? R->pub : nullptr, R->helper, R->leader};
-  if (!mp) {
-    if (hipMemcpyAsync(R->vk_slot, g.stg + L.slot_off, 2 * (size_t)g.n, hipMemcpyHostToDevice,
-                       st) != hipSuccess ||
-        hipMemcpyAsync(R->vk_tab, g.stg + L.tab_off, 16 * (size_t)g.n_keys,
-                       hipMemcpyHostToDevice, st) != hipSuccess)
-      return fail(PRIO3_EDEVICE);
-    in.vk_slot = R->vk_slot;
-    in.vk_tab = R->vk_tab;
+  const uint8_t* hd = g.stg_dev;
+  InPtrs in{hd + L.off[0], L.len[1] ? hd + L.off[1] : nullptr, hd + L.off[2], R->leader};
+  if (!mp) {  // the slots and the key table are read from the staging by the XOF
+    in.vk_slot = (const uint16_t*)(hd + L.slot_off);
+    in.vk_tab = (const uint4*)(hd + L.tab_off);
   }
-  if (agg) {
-    if (hipMemcpyAsync(R->gseg, g.stg + L.seg_off, 4 * (size_t)g.n, hipMemcpyHostToDevice, st) !=
-            hipSuccess ||
-        hipMemcpyAsync(R->gaccept, g.stg + L.accept_off, g.n, hipMemcpyHostToDevice, st) !=
-            hipSuccess)
-      return fail(PRIO3_EDEVICE);
-    R->seg = R->gseg;
-  }
+  if (agg) R->seg = (const uint32_t*)(hd + L.seg_off);  // the fused XOF's segment check
+  // the leader prep shares (and the segment ids / accept bytes of the fix-up pass) on the copy
+  // stream, which starts after the run's slab is free (ws_acquire ordered that on st)
+  if (hipEventRecord(ev[0], st) != hipSuccess || hipStreamWaitEvent(cs, ev[0], 0) != hipSuccess)
+    return fail(PRIO3_EDEVICE);
+  const LeaderReady copy_in = [&](hipStream_t s) -> int {
+    if (L.len[3] && hipMemcpyAsync(R->leader, g.stg + L.off[3], L.len[3] * g.n,
+                                   hipMemcpyHostToDevice, cs) != hipSuccess)
+      return PRIO3_EDEVICE;
+    if (agg && (hipMemcpyAsync(R->gseg, g.stg + L.seg_off, 4 * (size_t)g.n,
+                               hipMemcpyHostToDevice, cs) != hipSuccess ||
+                hipMemcpyAsync(R->gaccept, g.stg + L.accept_off, g.n, hipMemcpyHostToDevice,
+                               cs) != hipSuccess))
+      return PRIO3_EDEVICE;
+    if (hipEventRecord(ev[1], cs) != hipSuccess || hipStreamWaitEvent(s, ev[1], 0) != hipSuccess)
+      return PRIO3_EDEVICE;
+    return PRIO3_OK;
+  };
   OutPtrs out{R->msgs, R->status};
-  rc = prepare_run(lead, R, in, out, st, fuse, false);
+  rc = prepare_run(lead, R, in, out, st, fuse, false, &copy_in);
+  if (agg) R->seg = R->gseg;
   if (rc) return fail(rc);
   if (agg) {
     rc = fuse ? fused_finish(lead, R, R->status, R->gseg, R->gseg, R->gaccept, g.nseg, R->gagg,
@@ -3570,12 +3719,18 @@ static int fused_finish(prio3_engine* e, Run* R, const uint8_t* d_status, const 
         (k_agg_waves<<<g1, 256, 0, st>>>(nwaves, M, R->wpart, R->wseg, R->cpart, R->cseg,
                                          R->agg64)));
   TIMED(e, st, "k_agg_fix",
-        (k_agg_fix<<<(n + FIX_R - 1) / FIX_R, 256, 0, st>>>(
+        (k_agg_fix<<<(n + fix_per(n) - 1) / fix_per(n), 256, 0, st>>>(
             n, d_status, seg, d_accept_mask, R->wseg, R->fix, (uint32_t)(R->fix_cap - 1), S,
-            (unsigned long long*)d_counts)));
-  TIMED(e, st, "k_agg_final",
-        (k_agg_final<<<S * M, 256, 0, st>>>(M, R->dp.ld, R->agg64, nchunks, R->cpart, R->cseg,
-                                             R->fix, fix_seg, R->sc.meas, d_agg_shares)));
+            (unsigned long long*)d_counts, fix_seg ? 1u : 0u, fix_per(n))));
+  if (nchunks <= 64 && S > 1)
+    TIMED(e, st, "k_agg_final",
+          (k_agg_final_s<<<dim3((M + 31) / 32, S), 256, 0, st>>>(
+              M, R->dp.ld, R->agg64, nchunks, R->cpart, R->cseg, R->fix, fix_seg, R->sc.meas,
+              d_agg_shares)));
+  else
+    TIMED(e, st, "k_agg_final",
+          (k_agg_final<<<S * M, 256, 0, st>>>(M, R->dp.ld, R->agg64, nchunks, R->cpart, R->cseg,
+                                               R->fix, fix_seg, R->sc.meas, d_agg_shares)));
   return PRIO3_OK;
 }
 

@@ -67,6 +67,7 @@ struct ExecJob {
   uint32_t c0 = 0;     // the job's first column in the run
   uint32_t slot = 0;   // the job's verify-key slot in its group
   uint32_t seg0 = 0;   // the job's first segment among the group's
+  uint32_t pad0 = 0;   // pad columns [pad0, c0) before the job (aligned aggregating jobs)
 };
 // Blocks until the job's reports are prepared (alone or coalesced with concurrent jobs of
 // engines with the same VDAF instance on the same GPU).
@@ -90,6 +91,7 @@ void engine_io_layout(const prio3_engine* e, uint32_t cap, IoLayout* L);
 struct GroupView {
   uint32_t n, cap;  // reports staged, staging capacity
   uint8_t* stg;     // pinned staging (IoLayout for cap)
+  uint8_t* stg_dev;  // the staging as the device addresses it (mapped pinned memory)
   uint32_t n_keys;  // verify keys in the table
   int jobs;         // references the run must carry (one per job)
   uint32_t nseg;    // segments of the aggregating jobs (0: no job aggregates)
@@ -98,6 +100,7 @@ struct GroupView {
 constexpr uint32_t EXEC_MAX_SEGS = 1024;
 int engine_device(const prio3_engine* e);
 uint64_t engine_group_key(const prio3_engine* e);  // equal keys may share one launch
+uint32_t engine_job_align(const prio3_engine* e);  // column alignment of aggregating jobs
 void engine_vk(const prio3_engine* e, uint8_t out[16]);
 int engine_run_group(prio3_engine* lead, const GroupView& g, Run** run_out);
 uint32_t exec_max_keys();

@@ -208,6 +208,8 @@ namespace {
 
 struct Staging {
   uint8_t* p = nullptr;
+  uint8_t* dev = nullptr;  // the same pinned bytes as the device addresses them (kernels read
+                           // per-report inputs straight from here: engine_run_group)
   size_t bytes = 0;
 };
 
@@ -233,9 +235,11 @@ Staging staging_get(int dev, size_t bytes) {
   Staging s;
   s.bytes = std::max(bytes, STAGING_TARGET);
   if (hipSetDevice(dev) != hipSuccess ||
-      hipHostMalloc((void**)&s.p, s.bytes, hipHostMallocDefault) != hipSuccess) {
+      hipHostMalloc((void**)&s.p, s.bytes, hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&s.dev, s.p, 0) != hipSuccess) {
     (void)hipGetLastError();
-    s.p = nullptr;
+    if (s.p) (void)hipHostFree(s.p);
+    s.p = s.dev = nullptr;
     s.bytes = 0;
   }
   return s;
@@ -367,7 +371,7 @@ struct PrepPolicy {
   struct State {
     prio3_engine* lead = nullptr;
     std::vector<const prio3_engine*> keys;  // verify-key table, slot = index
-    uint32_t n = 0, cap = 0, jobs = 0, nseg = 0;
+    uint32_t n = 0, cap = 0, jobs = 0, nseg = 0, align = 1;
     IoLayout L;
     Run* run = nullptr;
   };
@@ -379,7 +383,9 @@ struct PrepPolicy {
     engine_io_layout(j->e, 2, &l2);
     const size_t per = l2.bytes - l1.bytes + 1;
     const uint32_t cap_b = (uint32_t)std::max<size_t>(1, STAGING_TARGET / per);
+    s.align = engine_job_align(j->e);
     s.cap = std::max(j->n, std::min(max_group_reports(), cap_b));
+    s.cap = (s.cap + 63) & ~63u;  // room for the tail pad of a wave-aligned group
     engine_io_layout(j->e, s.cap, &s.L);
     *bytes = s.L.bytes;
     return true;
@@ -388,18 +394,32 @@ struct PrepPolicy {
     uint32_t k = 0;
     while (k < s.keys.size() && s.keys[k] != j->e) k++;
     if (k == s.keys.size() && s.keys.size() >= exec_max_keys()) return false;
-    if (s.n + j->n > s.cap || s.nseg + j->nseg > s.L.max_seg) return false;
+    const uint32_t al = j->nseg ? s.align : 1u;
+    const uint32_t c0 = (s.n + al - 1) / al * al;
+    if (c0 + j->n > s.cap || ((c0 + j->n + 63) & ~63u) > s.cap ||
+        s.nseg + j->nseg > s.L.max_seg)
+      return false;
     if (k == s.keys.size()) s.keys.push_back(j->e);
-    j->c0 = s.n;
+    j->pad0 = s.n;
+    j->c0 = c0;
     j->slot = k;
     j->seg0 = s.nseg;
-    s.n += j->n;
+    s.n = c0 + j->n;
     s.nseg += j->nseg;
     s.jobs++;
     return true;
   }
+  // pad columns [a, b): verify-key slot 0, an out-of-range segment id, not accepted (their
+  // prepare runs on whatever bytes the staging holds and is never returned)
+  static void pad(const IoLayout& L, Staging& g, uint32_t a, uint32_t b) {
+    if (a >= b) return;
+    memset(g.p + L.slot_off + 2 * (size_t)a, 0, 2 * (size_t)(b - a));
+    memset(g.p + L.seg_off + 4 * (size_t)a, 0xff, 4 * (size_t)(b - a));
+    memset(g.p + L.accept_off + a, 0, b - a);
+  }
   static void stage(State& s, Staging& g, Job* j) {
     const IoLayout& L = s.L;
+    pad(L, g, j->pad0, j->c0);
     const uint8_t* src[4] = {j->nonces, j->pub, j->helper, j->leader};
     for (int f = 0; f < 4; f++)
       if (L.len[f] && src[f])
@@ -428,9 +448,15 @@ struct PrepPolicy {
   static int launch(int device, State& s, Staging& g) {
     (void)device;
     GroupView v;
+    if (s.nseg && s.align > 1) {  // whole waves: the group's tail padded like the gaps
+      const uint32_t n1 = (s.n + s.align - 1) / s.align * s.align;
+      pad(s.L, g, s.n, n1);
+      s.n = n1;
+    }
     v.n = s.n;
     v.cap = s.cap;
     v.stg = g.p;
+    v.stg_dev = g.dev;
     v.n_keys = (uint32_t)s.keys.size();
     v.jobs = (int)s.jobs;
     v.nseg = s.nseg;

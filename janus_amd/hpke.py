@@ -43,6 +43,7 @@ def _lib():
         L.janus_hpke_open.argtypes = [vp, u32, vp, vp, vp, u32, vp, vp, u32, vp, vp]
         L.janus_hpke_set_timing.argtypes = [vp, C.c_int]
         L.janus_hpke_timing.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]
+        L.janus_hpke_selftest_p256.argtypes = [C.c_int, u32, vp, vp, vp]
         _bound = True
     return L
 

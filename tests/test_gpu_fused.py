@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(cfg, n, seed, n_segments=1, seg_mode="runs", tamper=True, accept_frac=0.9,
-         force_slow=False, fuse=True, chunks=None, oob_frac=0.0, opts=None):
+         force_slow=False, fuse=True, chunks=None, oob_frac=0.0, opts=None, oob_waves=()):
     import torch
     o = _oracle(cfg)
     eng = _engine(cfg)
@@ -43,6 +43,8 @@ def _run(cfg, n, seed, n_segments=1, seg_mode="runs", tamper=True, accept_frac=0
     # segment ids >= n_segments: the report is excluded from every aggregate and count, as if
     # its accept-mask byte were 0 (include/janus_prio3.h); the oracle sees exactly that
     oob = rng.random(n) < oob_frac
+    for w in oob_waves:  # every report of these waves out of range (no lane left to fuse)
+        oob[64 * w:64 * w + 64] = True
     dev_seg = np.where(oob, n_segments + 5 + (np.arange(n) % 3), seg).astype(np.uint32)
     ref_seg = np.where(oob, 0, seg).astype(np.uint32)
     ref_accept = np.where(oob, 0, accept).astype(np.uint8)
@@ -147,6 +149,16 @@ def test_out_of_range_segment_ids_are_excluded(name, fuse):
     """a segment id >= n_segments never reaches the aggregate or the counts (fused
     Histogram path, its unfused fallback, and the deferred masked reduction alike)."""
     _run(CONFIGS[name], 900, seed=31, n_segments=3, oob_frac=0.05, fuse=fuse)
+
+
+@pytest.mark.parametrize("n_segments,oob_frac", [(1, 0.3), (3, 0.1), (1, 0.9)])
+def test_out_of_range_lanes_fuse_with_their_wave(n_segments, oob_frac):
+    """Lanes with a segment id >= n_segments (the executor's pad columns, excluded reports) are
+    masked out of the fused XOF's wave partials, so the wave's other reports still fuse; a wave
+    with no in-range lane is not fused.  Tampered reports, the host mask and segment runs inside
+    waves on top."""
+    _run(CONFIGS["hist_256_c16"], 2048, seed=41 + n_segments, n_segments=n_segments,
+         oob_frac=oob_frac, oob_waves=(3, 17))
 
 
 @pytest.mark.parametrize("opts", [{}, {"chunks": 3}])

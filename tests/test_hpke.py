@@ -83,6 +83,36 @@ def test_gpu_rfc9180_vector():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("aead", [1, 3])
+def test_gpu_aad_length_past_stride_fails_that_report_only(aead):
+    """a per-report AAD length larger than the AAD row stride must not authenticate
+    the next rows' bytes (nor read past the buffer): that report fails, its neighbours open."""
+    import ctypes as C
+    from janus_amd import hpke as G
+    gold = GOLD if aead == 1 else GOLD_AEAD[aead]
+    op = G.HpkeOpener(b(gold["skRm"]), b(gold["pkRm"]), info=b(gold["info"]), aead_id=aead)
+    e = gold["encryptions"][0]
+    ct, aad = b(e["ct"]), b(e["aad"])
+    n, cs = 3, -(-len(ct) // 16) * 16
+    stride = -(-len(aad) // 16) * 16
+    encs = np.tile(np.frombuffer(b(gold["enc"]), np.uint8), (n, 1))
+    cts = np.zeros((n, cs), np.uint8)
+    cts[:, :len(ct)] = np.frombuffer(ct, np.uint8)
+    aads = np.zeros((n, stride), np.uint8)
+    aads[:, :len(aad)] = np.frombuffer(aad, np.uint8)
+    cl = np.full(n, len(ct), np.uint32)
+    al = np.array([len(aad), stride + 16, len(aad)], np.uint32)  # row 1: past its stride
+    pt = np.zeros((n, cs), np.uint8)
+    st = np.zeros(n, np.uint8)
+    P = lambda a: a.ctypes.data_as(C.c_void_p)
+    rc = G._lib().janus_hpke_open(op.handle, n, P(encs), P(cts), P(cl), cs, P(aads), P(al),
+                                  stride, P(pt), P(st))
+    assert rc == 0
+    assert st[1] != 0 and st[0] == 0 and st[2] == 0
+    assert pt[0, :len(ct) - 16].tobytes() == b(e["pt"])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n,pub,share_len,ext,tamper", [
     (1, 32, 48, (), False), (300, 32, 48, (), True), (257, 0, 32, (), True),
     (200, 32, 48, ((0xFF00, b""),), False)])
@@ -318,3 +348,36 @@ def test_gpu_p256_edge_private_keys(sk):
                                   d["times"], d["pubs"], 48)
     np.testing.assert_array_equal(st, ref_st)
     np.testing.assert_array_equal(sh, ref_sh)
+
+
+P256 = 2**256 - 2**224 + 2**192 + 2**96 - 1
+P256_EDGE = [0, 1, 2, P256 - 1, P256 - 2, P256, P256 + 1, 2**256 - 1, 2**256 - 2, 2**224,
+             2**256 - P256, 2**256 - P256 - 1, 2**255, 2**192, 2**96 - 1, (P256 - 1) // 2]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("op", range(7))
+def test_gpu_p256_field_ops_match_python(op):
+    """The generated GF(p256) asm (tools/gen_p256_asm.py: product + NIST reduction, add/sub with
+    two carry folds, small multiples) and the addition-chain inverse, on loose operands in
+    [0, 2^256) including [p, 2^256) and the carry-fold edge values, against Python integers:
+    every result is in [0, 2^256) and congruent mod p."""
+    import ctypes as C
+    import random
+    from janus_amd import hpke as G
+    rnd = random.Random(op)
+    n = 4096 if op == 6 else 1 << 16
+    a = [rnd.choice(P256_EDGE) if rnd.random() < 0.2 else rnd.randrange(2**256) for _ in range(n)]
+    b = [rnd.choice(P256_EDGE) if rnd.random() < 0.2 else rnd.randrange(2**256) for _ in range(n)]
+    a[:len(P256_EDGE)] = P256_EDGE
+    b[:len(P256_EDGE)] = P256_EDGE[::-1]
+    enc = lambda xs: np.frombuffer(b"".join(x.to_bytes(32, "little") for x in xs), np.uint32).copy()
+    A, B = enc(a), enc(b)
+    out = np.zeros_like(A)
+    P = lambda x: x.ctypes.data_as(C.c_void_p)
+    assert G._lib().janus_hpke_selftest_p256(op, n, P(A), P(B), P(out)) == 0
+    got = [int.from_bytes(out[8 * i:8 * i + 8].tobytes(), "little") for i in range(n)]
+    fn = [lambda x, y: x * y, lambda x, y: x * x, lambda x, y: x + y, lambda x, y: x - y,
+          lambda x, y: 3 * x, lambda x, y: 8 * x, lambda x, y: pow(x, P256 - 2, P256)][op]
+    bad = [i for i in range(n) if got[i] >= 2**256 or (got[i] - fn(a[i], b[i])) % P256]
+    assert not bad, f"op {op}: {len(bad)} wrong, first {bad[0]}: a={a[bad[0]]:x} b={b[bad[0]]:x}"
