@@ -89,6 +89,7 @@ HPKE_EXPORTED_SYMBOLS = (
     "janus_hpke_opener_create", "janus_hpke_opener_destroy",
     "janus_hpke_open_input_shares_device", "janus_hpke_open_input_shares",
     "janus_hpke_open_device", "janus_hpke_open", "janus_hpke_set_timing", "janus_hpke_timing",
+    "janus_hpke_selftest_p256",
 )
 
 _lib = None
