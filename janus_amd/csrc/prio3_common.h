@@ -75,6 +75,14 @@ struct InPtrs {
   // engine's own key, DevParams::vk)
   const uint16_t* vk_slot = nullptr;
   const uint4* vk_tab = nullptr;
+  // executor groups (xofd_body<.., PULL>): the lane's leader prep share is copied from here (the
+  // mapped host staging) into `leader` during its XOF, and its segment id / accept byte from
+  // seg_src / accept_src into seg_dst / accept_dst (nullable)
+  const uint8_t* leader_src = nullptr;
+  const uint32_t* seg_src = nullptr;
+  uint32_t* seg_dst = nullptr;
+  const uint8_t* accept_src = nullptr;
+  uint8_t* accept_dst = nullptr;
 };
 
 // the verify key of report r (query randomness: XOF(vk, dst(5), [PROOFS] || nonce))

@@ -25,6 +25,7 @@
 #include <functional>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -230,7 +231,11 @@ __global__ __launch_bounds__(256, XOFD_OCC) void k_xof(DevParams p, InPtrs in, S
 // flagged for the slow path is un-fused at the end (its partials are ignored, its reports go
 // through the fix-up list with their corrected shares).
 // TR: the measurement share is also truncated into sc.out on the fly (DevParams::trunc_xof).
-template <bool FUSE, bool TR = false>
+// PULL (executor groups): the lane's leader prep share is copied from the mapped host staging
+// (in.leader_src) into in.leader in 16-byte pieces spread over the share loop -- each load issued
+// before the iteration's two permutations and stored after them, so the PCIe latency hides under
+// the Keccak work and the transfer runs at the XOF's pace -- plus its segment id and accept byte.
+template <bool FUSE, bool TR = false, bool PULL = false>
 __device__ __forceinline__ void xofd_body(const DevParams& p, const InPtrs& in, const Scratch& sc,
                                           const uint32_t r) {  // r & 63 == this lane
   typedef Fp128 F;
@@ -370,9 +375,25 @@ __device__ __forceinline__ void xofd_body(const DevParams& p, const InPtrs& in, 
     carry_tail(B == 1);
     keccak_p12(ms);
   }
+  if constexpr (PULL) {
+    if (in.seg_dst) in.seg_dst[r] = in.seg_src[r];
+    if (in.accept_dst) in.accept_dst[r] = in.accept_src[r];
+  }
+  // PULL: pieces [Q (b-1) / (B-1), Q b / (B-1)) of the Q 16-byte pieces in iteration b (1 or 2)
+  const uint32_t Q = PULL ? p.prep_share_len / 16 : 0u;
+  const uint4* lsrc = PULL ? (const uint4*)(in.leader_src + (size_t)r * p.prep_share_len) : nullptr;
+  uint4* ldst = PULL ? (uint4*)(in.leader + (size_t)r * p.prep_share_len) : nullptr;
   // full joint-rand blocks 1 .. B-1 (B <= K, so share block b exists for every b < B)
 #pragma unroll 1
   for (uint32_t b = 1; b < B; b++) {
+    uint4 pc0, pc1;
+    uint32_t q0 = 0, q1 = 0;
+    if constexpr (PULL) {
+      q0 = Q * (b - 1) / (B - 1);
+      q1 = Q * b / (B - 1);
+      if (q0 < q1) pc0 = lsrc[q0];
+      if (q0 + 1 < q1) pc1 = lsrc[q0 + 1];
+    }
     if (FUSE && fuse) fuse_block(b, pend0, pend1);
     squeeze_meas<TR>(p, ms, b, M, pend0, pend1, sc.meas, r, flag, ts);
     kxor_word(js, 10, kword(ms, 0) << 16);
@@ -382,6 +403,10 @@ __device__ __forceinline__ void xofd_body(const DevParams& p, const InPtrs& in, 
     keccak_p12(js);
     carry_tail(b + 1 == B);
     if (b + 1 < K) keccak_p12(ms);
+    if constexpr (PULL) {
+      if (q0 < q1) ldst[q0] = pc0;
+      if (q0 + 1 < q1) ldst[q0 + 1] = pc1;
+    }
   }
   // final joint-rand block B: remaining share bytes, padding
   uint32_t part[4];
@@ -462,6 +487,30 @@ template <bool FUSE, bool TR = false>
 __global__ __launch_bounds__(256, XOFD_OCC) void k_xofd(DevParams p, InPtrs in, Scratch sc) {
   xofd_body<FUSE, TR>(p, in, sc, blockIdx.x * blockDim.x + threadIdx.x);
 }
+
+// Host -> device copy by the shader cores from mapped pinned memory (up to 3 ranges; 16-byte
+// loads, the byte tails by lane).  On MI355X this reads PCIe at ~55 GB/s where the SDMA copy of
+// the same staging ran at ~32 GB/s beside the XOF's own host reads (profiles/r03/r03l trace).
+struct PullRanges {
+  const uint8_t* src[3];
+  uint8_t* dst[3];
+  size_t bytes[3];
+};
+DEV void pull_body(const PullRanges& pr, size_t tid, size_t nth) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const size_t n16 = pr.bytes[k] / 16;
+    const uint4* s16 = (const uint4*)pr.src[k];
+    uint4* d16 = (uint4*)pr.dst[k];
+    for (size_t i = tid; i < n16; i += nth) d16[i] = s16[i];
+    const size_t t = 16 * n16 + tid;
+    if (t < pr.bytes[k] && tid < 16) pr.dst[k][t] = pr.src[k][t];
+  }
+}
+__global__ __launch_bounds__(256) void k_pull(PullRanges pr) {
+  pull_body(pr, (size_t)blockIdx.x * blockDim.x + threadIdx.x, (size_t)gridDim.x * blockDim.x);
+}
+
 
 // ------------------------------------------------------------------------------------
 // Split XOF path (one Keccak state live per kernel, for occupancy):
@@ -1573,11 +1622,11 @@ __global__ __launch_bounds__(256, 3) void k_query_h(DevParams p, InPtrs in, Scra
 // SIMD drift apart, so one wave's memory-bound query runs beside other waves' issue-bound Keccak
 // without a kernel boundary, a second stream or the k_xof_slow launch between them.  The query
 // reads the scratch rows its own lane has just written.
-template <bool FUSE>
+template <bool FUSE, bool PULL = false>
 __global__ __launch_bounds__(256, 3) void k_prep_h(DevParams p, InPtrs in, Scratch sc,
                                                    OutPtrs out) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  xofd_body<FUSE, false>(p, in, sc, r);
+  xofd_body<FUSE, false, PULL>(p, in, sc, r);
 #ifndef JANUS_AB_XOF_ONLY  // A/B build: the fused kernel's XOF half alone
 #ifndef QH_GS
 #define QH_GS 2  // wires per sweep of the fused kernel's query (A/B builds: 3, 4)
@@ -2883,14 +2932,11 @@ static bool prep_fused_takes(const prio3_engine* e, const DevParams& dp, bool fu
 enum : int { DEFER_NONE = 0, DEFER_QH = 1, DEFER_SUM = 2, DEFER_GEN64 = 3 };
 // *deferred: set when a query kernel of this chain skipped flagged reports (slow_defer); the
 // caller then ends the run with launch_slow_redo
-// lready (nullable): the leader prep shares (in.leader) are not on the device yet; the chain is
-// the two-kernel one (splits_at_query), and lready(st) is called between the XOF launch and the
-// query launch -- it starts their copy on another stream and makes st wait for it, so the copy
-// runs under the XOF (and a host-blocking copy call does not hold back the XOF launch).
-typedef std::function<int(hipStream_t)> LeaderReady;
+// in.leader_src (executor groups, pulls_in_xof): the leader prep shares are still in the mapped
+// host staging and the fused k_prep_h<.., PULL> copies them lane by lane during its XOF.
 static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, uint32_t n,
                           InPtrs in, OutPtrs out, Scratch sc, hipStream_t st, bool fuse,
-                          int* deferred, const LeaderReady* lready = nullptr) {
+                          int* deferred) {
   DevParams dp = base;
   dp.n = n;
   dp.force_slow = (uint32_t)e->force_slow;
@@ -2973,7 +3019,7 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
     dp.trunc_xof = dp.kind == PRIO3_SUMVEC && wide && dual && !fuse ? 1u : 0u;
     // XOF + query in one launch: Prio3Sum (k_prep_sum) and Histogram / SumVec with P = 32
     // (k_prep_h); the slow path of both is deferred to the run's redo launch
-    if (!lready && prep_fused_takes(e, dp, fuse)) {
+    if (prep_fused_takes(e, dp, fuse)) {
       dp.slow_defer = 1u;
       if (dp.kind == PRIO3_SUM) {
         if (deferred) *deferred = DEFER_SUM;
@@ -2985,8 +3031,13 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
         }
       } else {
         if (deferred) *deferred = DEFER_QH;
-        if (fuse)
+        const bool pl = in.leader_src != nullptr;
+        if (fuse && pl)
+          TIMED(e, st, "k_prep_h", (k_prep_h<true, true><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+        else if (fuse)
           TIMED(e, st, "k_prep_h", (k_prep_h<true><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
+        else if (pl)
+          TIMED(e, st, "k_prep_h", (k_prep_h<false, true><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
         else
           TIMED(e, st, "k_prep_h", (k_prep_h<false><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
       }
@@ -3009,10 +3060,6 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
     // read the shares the k_xof_slow launch rewrote
     const bool qh_path =
         ps && !e->force_generic && !wide && (dp.P == 32 || dp.P == 16 || dp.P == 8);
-    if (lready) {
-      const int rc = (*lready)(st);
-      if (rc) return rc;
-    }
     dp.slow_defer = qh_path ? 1u : 0u;
     if (qh_path && deferred) *deferred = DEFER_QH;
     if (!qh_path) TIMED(e, st, "k_xof_slow", launch_xof_slow<Fp128>(e, dp, in, sc, st));
@@ -3109,24 +3156,31 @@ static int launch_slow_redo(prio3_engine* e, const DevParams& base, uint32_t n, 
 // before and after), so one chunk's memory-bound query overlaps the next chunk's VALU-bound
 // Keccak.  Side streams are per engine: callers that may overlap (the executor's concurrent
 // groups) pass allow_chunks = false.
-// The chains that read the leader prep shares only from the query on (the XOF reads the
-// per-report seeds): Histogram / SumVec with P = 32 on k_xofd + k_query_h.
-static bool splits_at_query(const prio3_engine* e, const DevParams& dp) {
-  return !e->force_generic && (dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC) &&
-         dp.es == 16 && dp.jr_len && (42 + dp.meas_len * 16) / 168 >= 2 && dp.P == 32;
+// The chains whose XOF can pull the leader prep shares (the fused k_prep_h: the query reads them
+// only after the same lane's XOF); the share is copied in 16-byte pieces over the share loop.
+static bool pulls_in_xof(const prio3_engine* e, const DevParams& dp, bool fuse) {
+  const uint32_t B = (42 + dp.meas_len * 16) / 168;  // share-loop iterations: B - 1
+  return prep_fused_takes(e, dp, fuse) && dp.kind != PRIO3_SUM && dp.prep_share_len % 16 == 0 &&
+         B >= 2 && dp.prep_share_len / 16 <= 2 * (B - 1);
 }
 
-// lready (nullable): makes in.leader hold the leader prep shares (see launch_prepare); the chains
-// that split at the query (splits_at_query) call it after their XOF launch, the others first.
+// pull (nullable; executor groups): copies the leader prep shares (and the fix-up inputs) from
+// the mapped host staging into the run -- inside the fused XOF + query launch where the chain is
+// k_prep_h (pulls_in_xof), else by one copy launch ahead of the chain.
 static int prepare_run(prio3_engine* e, Run* R, InPtrs in, OutPtrs out, hipStream_t st, bool fuse,
-                       bool allow_chunks, const LeaderReady* lready = nullptr) {
+                       bool allow_chunks, const PullRanges* pull = nullptr) {
   const uint32_t n = R->n;
-  if (lready && !splits_at_query(e, R->dp)) {
-    const int rc = (*lready)(st);
-    if (rc) return rc;
-    lready = nullptr;
+  if (pull && pulls_in_xof(e, R->dp, fuse)) {
+    in.leader_src = pull->src[0];
+    in.seg_src = (const uint32_t*)pull->src[1];
+    in.seg_dst = (uint32_t*)pull->dst[1];
+    in.accept_src = pull->src[2];
+    in.accept_dst = pull->dst[2];
+    allow_chunks = false;
+  } else if (pull) {
+    k_pull<<<256, 256, 0, st>>>(*pull);
+    HIPCHK(hipGetLastError());
   }
-  if (lready) allow_chunks = false;
   Scratch sc = R->sc;
   sc.seg = R->seg;
   sc.wpart = R->wpart;
@@ -3140,7 +3194,7 @@ static int prepare_run(prio3_engine* e, Run* R, InPtrs in, OutPtrs out, hipStrea
   const uint32_t csz = ((n + K - 1) / K + 255) & ~255u;
   int deferred = DEFER_NONE;
   if (!allow_chunks || K == 1 || n <= csz || R->dp.kind == PRIO3_FPVEC_BOUNDED_L2) {
-    const int rc = launch_prepare(e, R->dp, 0, n, in, out, sc, st, fuse, &deferred, lready);
+    const int rc = launch_prepare(e, R->dp, 0, n, in, out, sc, st, fuse, &deferred);
     if (rc == PRIO3_OK && deferred)
       return launch_slow_redo(e, R->dp, n, in, out, sc, st, deferred);
     return rc;
@@ -3349,22 +3403,17 @@ static int fused_finish(prio3_engine* e, Run* R, const uint8_t* d_status, const 
 
 // Host-pull group launch: the kernels read each report's nonce, public share, helper share and
 // verify-key slot straight from the pinned staging (mapped; 96-112 B per report at the start of
-// the XOF), while one copy on a second stream moves the leader prep shares (560 B per report for
-// Histogram(256,16)) and the segment ids / accept bytes into the run; a chain that splits at the
-// query (splits_at_query) runs its XOF under that copy and waits on it only before the query.
-// One pinned-staging H2D copy per field on the launch stream instead (the r02 form) left the
-// PCIe transfer and the prepare in series (profiles/r03/r03e_jobs128_*.json).
+// the XOF), and each lane of the fused XOF + query launch copies its own leader prep share (560 B
+// for Histogram(256,16)), segment id and accept byte into the run during its XOF (xofd_body
+// PULL), so the PCIe transfer runs under the Keccak work.  One pinned-staging H2D copy
+// per field ahead of the prepare (the r02 form) left transfer and prepare in series
+// (profiles/r03/r03e_jobs128_*.json: 21.5 M reports/s at 128 threads).
 int engine_run_group(prio3_engine* lead, const GroupView& g, Run** run_out) {
   *run_out = nullptr;
   HIPCHK(hipSetDevice(lead->device));
-  PooledStream ps(lead->device), pc(lead->device);
-  hipStream_t st = ps.s, cs = pc.s;
-  if (!st || !cs) return PRIO3_EDEVICE;
-  static thread_local hipEvent_t evs[64][2] = {};
-  if (lead->device >= 64) return PRIO3_EINVAL;
-  hipEvent_t* ev = evs[lead->device];
-  for (int i = 0; i < 2; i++)
-    if (!ev[i]) HIPCHK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+  PooledStream ps(lead->device);
+  hipStream_t st = ps.s;
+  if (!st) return PRIO3_EDEVICE;
   const bool mp = lead->dp.kind == PRIO3_SUMVEC_F64_MP;
   // aggregating jobs: the group's reports are accumulated per job segment in this launch (the
   // wave partials of the XOF where the instance fuses; waves that straddle two jobs and the
@@ -3380,7 +3429,6 @@ int engine_run_group(prio3_engine* lead, const GroupView& g, Run** run_out) {
   IoLayout L;
   engine_io_layout(lead, g.cap, &L);
   auto fail = [&](int code) {
-    (void)hipStreamSynchronize(cs);
     run_release(R, st, true);
     return code;
   };
@@ -3393,23 +3441,20 @@ int engine_run_group(prio3_engine* lead, const GroupView& g, Run** run_out) {
   if (agg) R->seg = (const uint32_t*)(hd + L.seg_off);  // the fused XOF's segment check
   // the leader prep shares (and the segment ids / accept bytes of the fix-up pass) on the copy
   // stream, which starts after the run's slab is free (ws_acquire ordered that on st)
-  if (hipEventRecord(ev[0], st) != hipSuccess || hipStreamWaitEvent(cs, ev[0], 0) != hipSuccess)
-    return fail(PRIO3_EDEVICE);
-  const LeaderReady copy_in = [&](hipStream_t s) -> int {
-    if (L.len[3] && hipMemcpyAsync(R->leader, g.stg + L.off[3], L.len[3] * g.n,
-                                   hipMemcpyHostToDevice, cs) != hipSuccess)
-      return PRIO3_EDEVICE;
-    if (agg && (hipMemcpyAsync(R->gseg, g.stg + L.seg_off, 4 * (size_t)g.n,
-                               hipMemcpyHostToDevice, cs) != hipSuccess ||
-                hipMemcpyAsync(R->gaccept, g.stg + L.accept_off, g.n, hipMemcpyHostToDevice,
-                               cs) != hipSuccess))
-      return PRIO3_EDEVICE;
-    if (hipEventRecord(ev[1], cs) != hipSuccess || hipStreamWaitEvent(s, ev[1], 0) != hipSuccess)
-      return PRIO3_EDEVICE;
-    return PRIO3_OK;
-  };
+  PullRanges pr{};
+  pr.src[0] = hd + L.off[3];
+  pr.dst[0] = R->leader;
+  pr.bytes[0] = L.len[3] * g.n;
+  if (agg) {
+    pr.src[1] = hd + L.seg_off;
+    pr.dst[1] = (uint8_t*)R->gseg;
+    pr.bytes[1] = 4 * (size_t)g.n;
+    pr.src[2] = hd + L.accept_off;
+    pr.dst[2] = R->gaccept;
+    pr.bytes[2] = g.n;
+  }
   OutPtrs out{R->msgs, R->status};
-  rc = prepare_run(lead, R, in, out, st, fuse, false, &copy_in);
+  rc = prepare_run(lead, R, in, out, st, fuse, false, &pr);
   if (agg) R->seg = R->gseg;
   if (rc) return fail(rc);
   if (agg) {
@@ -3427,9 +3472,13 @@ int engine_run_group(prio3_engine* lead, const GroupView& g, Run** run_out) {
   if ((L.msg_len && hipMemcpyAsync(g.stg + L.msg_off, R->msgs, L.msg_len * g.n,
                                    hipMemcpyDeviceToHost, st) != hipSuccess) ||
       hipMemcpyAsync(g.stg + L.status_off, R->status, g.n, hipMemcpyDeviceToHost, st) !=
-          hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess)
+          hipSuccess)
     return fail(PRIO3_EDEVICE);
+  // the launcher polls instead of sleeping in hipStreamSynchronize: the group's jobs are woken
+  // as soon as their outputs land (the blocking wait added ~0.1 ms per group)
+  hipError_t q;
+  while ((q = hipStreamQuery(st)) == hipErrorNotReady) std::this_thread::yield();
+  if (q != hipSuccess) return fail(PRIO3_EDEVICE);
   if (lead->timing) collect_times(lead);
   R->refs.store(g.jobs);
   *run_out = R;
