@@ -379,10 +379,14 @@ __device__ __forceinline__ void xofd_body(const DevParams& p, const InPtrs& in, 
     if (in.seg_dst) in.seg_dst[r] = in.seg_src[r];
     if (in.accept_dst) in.accept_dst[r] = in.accept_src[r];
   }
-  // PULL: pieces [Q (b-1) / (B-1), Q b / (B-1)) of the Q 16-byte pieces in iteration b (1 or 2)
+  // PULL: the wave's 64 leader shares are one contiguous run of 64 Q 16-byte pieces; iteration b
+  // copies rows [Q (b-1) / (B-1), Q b / (B-1)) (1 or 2) of 64 pieces, lane l taking piece
+  // 64 row + l, so every load instruction reads 1 KiB of consecutive host bytes (one 16-byte
+  // piece per report per lane made the PCIe reads scattered: 18.5 GB/s, profiles/r03/r03o)
   const uint32_t Q = PULL ? p.prep_share_len / 16 : 0u;
-  const uint4* lsrc = PULL ? (const uint4*)(in.leader_src + (size_t)r * p.prep_share_len) : nullptr;
-  uint4* ldst = PULL ? (uint4*)(in.leader + (size_t)r * p.prep_share_len) : nullptr;
+  const size_t wbase = PULL ? (size_t)(r - lane) * (p.prep_share_len / 16) + lane : 0;
+  const uint4* lsrc = PULL ? (const uint4*)in.leader_src + wbase : nullptr;
+  uint4* ldst = PULL ? (uint4*)in.leader + wbase : nullptr;
   // full joint-rand blocks 1 .. B-1 (B <= K, so share block b exists for every b < B)
 #pragma unroll 1
   for (uint32_t b = 1; b < B; b++) {
@@ -391,8 +395,8 @@ __device__ __forceinline__ void xofd_body(const DevParams& p, const InPtrs& in, 
     if constexpr (PULL) {
       q0 = Q * (b - 1) / (B - 1);
       q1 = Q * b / (B - 1);
-      if (q0 < q1) pc0 = lsrc[q0];
-      if (q0 + 1 < q1) pc1 = lsrc[q0 + 1];
+      if (q0 < q1) pc0 = lsrc[64 * (size_t)q0];
+      if (q0 + 1 < q1) pc1 = lsrc[64 * (size_t)(q0 + 1)];
     }
     if (FUSE && fuse) fuse_block(b, pend0, pend1);
     squeeze_meas<TR>(p, ms, b, M, pend0, pend1, sc.meas, r, flag, ts);
@@ -404,8 +408,8 @@ __device__ __forceinline__ void xofd_body(const DevParams& p, const InPtrs& in, 
     carry_tail(b + 1 == B);
     if (b + 1 < K) keccak_p12(ms);
     if constexpr (PULL) {
-      if (q0 < q1) ldst[q0] = pc0;
-      if (q0 + 1 < q1) ldst[q0 + 1] = pc1;
+      if (q0 < q1) ldst[64 * (size_t)q0] = pc0;
+      if (q0 + 1 < q1) ldst[64 * (size_t)(q0 + 1)] = pc1;
     }
   }
   // final joint-rand block B: remaining share bytes, padding
@@ -3158,10 +3162,11 @@ static int launch_slow_redo(prio3_engine* e, const DevParams& base, uint32_t n, 
 // groups) pass allow_chunks = false.
 // The chains whose XOF can pull the leader prep shares (the fused k_prep_h: the query reads them
 // only after the same lane's XOF); the share is copied in 16-byte pieces over the share loop.
-static bool pulls_in_xof(const prio3_engine* e, const DevParams& dp, bool fuse) {
+// Every wave must be whole (the executor pads its groups to 64 columns for these instances).
+static bool pulls_in_xof(const prio3_engine* e, const DevParams& dp, bool fuse, uint32_t n) {
   const uint32_t B = (42 + dp.meas_len * 16) / 168;  // share-loop iterations: B - 1
   return prep_fused_takes(e, dp, fuse) && dp.kind != PRIO3_SUM && dp.prep_share_len % 16 == 0 &&
-         B >= 2 && dp.prep_share_len / 16 <= 2 * (B - 1);
+         B >= 2 && dp.prep_share_len / 16 <= 2 * (B - 1) && n % 64 == 0;
 }
 
 // pull (nullable; executor groups): copies the leader prep shares (and the fix-up inputs) from
@@ -3170,7 +3175,7 @@ static bool pulls_in_xof(const prio3_engine* e, const DevParams& dp, bool fuse) 
 static int prepare_run(prio3_engine* e, Run* R, InPtrs in, OutPtrs out, hipStream_t st, bool fuse,
                        bool allow_chunks, const PullRanges* pull = nullptr) {
   const uint32_t n = R->n;
-  if (pull && pulls_in_xof(e, R->dp, fuse)) {
+  if (pull && pulls_in_xof(e, R->dp, fuse, n)) {
     in.leader_src = pull->src[0];
     in.seg_src = (const uint32_t*)pull->src[1];
     in.seg_dst = (uint32_t*)pull->dst[1];

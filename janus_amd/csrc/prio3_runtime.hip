@@ -448,7 +448,7 @@ struct PrepPolicy {
   static int launch(int device, State& s, Staging& g) {
     (void)device;
     GroupView v;
-    if (s.nseg && s.align > 1) {  // whole waves: the group's tail padded like the gaps
+    if (s.align > 1) {  // whole waves: the group's tail padded like the gaps
       const uint32_t n1 = (s.n + s.align - 1) / s.align * s.align;
       pad(s.L, g, s.n, n1);
       s.n = n1;

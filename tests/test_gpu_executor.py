@@ -125,8 +125,7 @@ def test_concurrent_jobs_of_several_tasks_are_coalesced(name):
         np.testing.assert_array_equal(agg, ra)
         np.testing.assert_array_equal(cnt, rc)
     # Histogram(256, 16) (P = 32) and Count run their XOF and query in one launch
-    # Histogram groups run the XOF under the leader-share copy (k_xofd, then k_query_h)
-    kern = {"count": "k_prep_gen", "hist_256_c16": "k_xofd"}.get(name, "k_xofd")
+    kern = {"count": "k_prep_gen", "hist_256_c16": "k_prep_h"}.get(name, "k_xofd")
     launches = sum(e.timing().get(kern, (0, 0))[1] for e in engines)
     assert 0 < launches < 24, launches
 
@@ -183,7 +182,7 @@ def test_combined_prepare_aggregate_jobs(name):
         np.testing.assert_array_equal(msgs, rm)
         np.testing.assert_array_equal(agg, ra)
         np.testing.assert_array_equal(cnt, rc)
-    kern = {"count": "k_prep_gen", "hist_256_c16": "k_xofd", "sum32": "k_prep_sum"}.get(
+    kern = {"count": "k_prep_gen", "hist_256_c16": "k_prep_h", "sum32": "k_prep_sum"}.get(
         name, "k_xofd")
     launches = sum(e.timing().get(kern, (0, 0))[1] for e in engines)
     assert 0 < launches < 32, launches
