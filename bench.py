@@ -591,6 +591,13 @@ def jobs_main(args):
                          h2d_GBps=value * per_report_h2d / 1e9,
                          roof_reports_per_s=63e9 / per_report_h2d,
                          roof_note="PCIe Gen5 x16 ~63 GB/s (MI355X_MICROARCH.md)"),
+               roofline=dict(bound="pcie", achieved=value * per_report_h2d / 1e9, peak=63.0,
+                             unit="GB/s host->device (the report bytes each job hands over)",
+                             frac=value * per_report_h2d / 63e9,
+                             frac_of_measured_link=value * per_report_h2d / 57e9,
+                             note="measured link: 55-57 GB/s for 16-64 MB pinned copies and kernel "
+                                  "reads of mapped host memory (tools/ubench_h2d.hip, "
+                                  "profiles/r03/r03i_h2d.txt)", traffic=None),
                coalescing=dict(launches=launches, jobs=n_jobs,
                                mean_reports_per_launch=n_jobs * js / max(launches, 1)),
                call=("prio3_helper_prepare_aggregate_batch (one coalesced launch per group)"
