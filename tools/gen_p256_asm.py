@@ -7,9 +7,9 @@ p = 2^256 - 2^224 + 2^192 + 2^96 - 1; values are 8 little-endian 32-bit limbs, l
   p256_mul / p256_sqr  the 512-bit product (tools/gen_fe25519_asm.py's column-MAC and
                        normalisation emitters and its scratch layout v40-v82), then the NIST fast
                        reduction (FIPS 186-4 D.2.3, s1 + 2 s2 + 2 s3 + s4 + s5 - s6 - s7 - s8 - s9)
-                       as nine add / subtract chains over the 16 product words, started from
-                       5p (so the running top word never goes negative), and two folds of the top
-                       word through 2^256 = C (mod p);
+                       as ten add / subtract chains over the 16 product words, started from 5p (so
+                       the running top word t never goes negative), then t * C added as one
+                       non-negative 8-word value and its carry folded as C once more;
   p256_add / p256_sub  one 8-word carry (borrow) chain, then the carry (borrow) folded twice as
                        +C (-C): a loose result never needs a third;
   p256_mul_small       a x k for a small constant k (8 v_mad_u64_u32), the top word folded as in
@@ -63,25 +63,22 @@ def chain(sign, words, top):
 
 
 def fold_top(top):
-    """OUT + top * 2^256 (0 <= top < 2^31) -> [0, 2^256): add top * C as +top at words 0 and 7,
-    -top at words 3 and 6 (net carry U in {-1, 0, 1}), then U * C once more"""
-    out = chain(+1, [top, None, None, None, None, None, None, top], None)
-    out.append(f"v_cndmask_b32_e64 {TU}, 0, 1, vcc")
-    out += chain(-1, [None, None, None, top, None, None, top, None], TU)
-    out += fold_unit(TU)
-    return out
-
-
-def fold_unit(u, tt=None, tm=None, tw=None):
-    """OUT += u * C for u in {-1, 0, 1} (never carries or borrows out again)"""
-    tt, tm, tw = tt or TT, tm or TM, tw or TW
-    out = []
-    for want, sign in ((1, +1), (-1, -1)):
-        out.append(f"v_cmp_eq_u32 vcc, {lit(want % 2**32)}, {u}")
-        out.append(f"v_cndmask_b32_e64 {tt}, 0, 1, vcc")   # a in {0, 1}
-        out.append(f"v_sub_u32 {tm}, 0, {tt}")              # -a: words 3-5 of a * C
-        out.append(f"v_and_b32 {tw}, {lit(0xFFFFFFFE)}, {tm}")  # word 6
-        out += chain(sign, [tt, None, None, tm, tm, tm, tw, None], None)
+    """OUT + top * 2^256 (0 <= top < 2^31) -> [0, 2^256).  top * C < 2^228 as one non-negative
+    8-word addend: [t, 0, 0, -t, m, m, -t-1, t-1] (m = ~0 if t else 0; the -t words borrow from
+    their neighbours), so one chain; its carry u in {0, 1} is folded as u * C once more."""
+    T, U, M, A, W6, W7 = top, TU, TM, TW, "v50", "v51"
+    out = [f"v_cmp_ne_u32 vcc, 0, {T}",
+           f"v_cndmask_b32_e64 {M}, 0, -1, vcc",
+           f"v_sub_u32 {A}, 0, {T}",
+           f"v_add_u32 {W6}, -1, {A}",
+           f"v_and_b32 {W6}, {M}, {W6}",
+           f"v_add_u32 {W7}, -1, {T}",
+           f"v_and_b32 {W7}, {M}, {W7}"]
+    out += chain(+1, [T, None, None, A, M, M, W6, W7], None)
+    out.append(f"v_cndmask_b32_e64 {U}, 0, 1, vcc")
+    out.append(f"v_sub_u32 {M}, 0, {U}")
+    out.append(f"v_and_b32 {A}, {lit(0xFFFFFFFE)}, {M}")
+    out += chain(+1, [U, None, None, M, M, M, A, None], None)
     return out
 
 

@@ -139,9 +139,20 @@ def main():
                 "attributed to k_prep_h in kernel_counts.json\n")
         with open(os.path.join(ROOT, "profiles", f"{tag}_rocprof_summary.txt"), "w") as f:
             f.write(txt)
-    with open(os.path.join(ROOT, "profiles", "kernel_counts.json"), "w") as f:
-        json.dump(dict(tag=tag, source=f"profiles/{tag}_rocprof_summary.txt", kernels=kernels), f,
-                  indent=1)
+    # kernels this pass did not run (e.g. SKIP_HPKE) keep their earlier entry and its source
+    path = os.path.join(ROOT, "profiles", "kernel_counts.json")
+    src = f"profiles/{tag}_rocprof_summary.txt"
+    merged = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            old = json.load(f)
+        for k, v in old.get("kernels", {}).items():
+            if k not in kernels:
+                merged[k] = dict(v, source=v.get("source", old.get("source")))
+    for k, v in kernels.items():
+        merged[k] = dict(v, source=src)
+    with open(path, "w") as f:
+        json.dump(dict(tag=tag, source=src, kernels=merged), f, indent=1)
     print(txt)
 
 
