@@ -1098,9 +1098,9 @@ uint32_t le32(const uint8_t* p) {
 
 }  // namespace
 
-// Regular signed window recoding (w = 3) of a P-256 private key for p256::ecdh: k' = sk when sk
-// is odd, else n - sk (same x-coordinate of k'P), then 85 digits d = (k' mod 16) - 8 (odd, in
-// [-7, 7]) with k' <- (k' - d) / 8, which stays odd, and the remaining k' in {1, 3} on top.
+// Regular signed window recoding (w = 4) of a P-256 private key for p256::ecdh: k' = sk when sk
+// is odd, else n - sk (same x-coordinate of k'P), then 63 digits d = (k' mod 32) - 16 (odd, in
+// [-15, 15]) with k' <- (k' - d) / 16, which stays odd, and the remaining odd k' < 16 on top.
 static void p256_recode(const uint32_t sk[8], int8_t dig[88]) {
   uint32_t k[8];
   memcpy(k, sk, sizeof(k));
@@ -1113,8 +1113,8 @@ static void p256_recode(const uint32_t sk[8], int8_t dig[88]) {
       br = t >> 32;
     }
   }
-  for (int i = 0; i < 85; i++) {
-    const int d = (int)(k[0] & 15u) - 8;
+  for (int i = 0; i < p256::kDigits - 1; i++) {
+    const int d = (int)(k[0] & 31u) - 16;
     dig[i] = (int8_t)d;
     int64_t c = -(int64_t)d;  // k -= d
     for (int j = 0; j < 8; j++) {
@@ -1122,10 +1122,10 @@ static void p256_recode(const uint32_t sk[8], int8_t dig[88]) {
       k[j] = (uint32_t)t;
       c = t >> 32;
     }
-    for (int j = 0; j < 8; j++) k[j] = k[j] >> 3 | (j < 7 ? k[j + 1] << 29 : 0u);
+    for (int j = 0; j < 8; j++) k[j] = k[j] >> 4 | (j < 7 ? k[j + 1] << 28 : 0u);
   }
-  dig[85] = (int8_t)k[0];
-  dig[86] = dig[87] = 0;
+  dig[p256::kDigits - 1] = (int8_t)k[0];
+  for (int i = p256::kDigits; i < 88; i++) dig[i] = 0;
 }
 
 struct janus_hpke_opener {

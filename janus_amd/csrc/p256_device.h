@@ -7,7 +7,7 @@
 // NIST fast reduction (FIPS 186-4 D.2.3: s1 + 2 s2 + 2 s3 + s4 + s5 - s6 - s7 - s8 - s9) in
 // signed 64-bit word sums, whose carry out of 2^256 folds back as 2^256 = 2^224 - 2^192 - 2^96 + 1
 // (mod p); three carry passes always leave [0, 2^256).
-// The scalar is the server's private key, the same in every lane: a fixed signed window (w = 3)
+// The scalar is the server's private key, the same in every lane: a fixed signed window (w = 4)
 // over its host-side recoding, so every key runs the same instruction stream (see ecdh).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -15,9 +15,6 @@
 
 #ifndef DEV
 #define DEV __device__ __forceinline__
-#endif
-#ifndef P256_TAB_MEM
-#define P256_TAB_MEM 0  // 1: the window table in private memory instead of registers (A/B)
 #endif
 #ifndef P256_ASM
 #define P256_ASM 1  // 1: the generated single-asm-statement products (p256_asm.h)
@@ -191,62 +188,57 @@ struct jac {
   fp X, Y, Z;
 };
 
-// dbl-2001-b (a = -3): delta = Z^2, gamma = Y^2, beta = X gamma, alpha = 3 (X - delta)(X + delta)
+// dbl-2001-b (a = -3): delta = Z^2, gamma = Y^2, beta = X gamma, alpha = 3 (X - delta)(X + delta);
+// Z3 = 2 Y Z (one multiply and one add instead of (Y + Z)^2 - gamma - delta: 284 instructions
+// against 314 with the generated field routines) and 8 beta = 4 beta + 4 beta
 DEV jac dbl(const jac& P) {
   const fp delta = sqr(P.Z), gamma = sqr(P.Y), beta = mul(P.X, gamma);
   const fp alpha = mul_small(mul(sub(P.X, delta), add(P.X, delta)), 3);
+  const fp b4 = mul_small(beta, 4);
   jac R;
-  R.X = sub(sqr(alpha), mul_small(beta, 8));
-  R.Z = sub(sub(sqr(add(P.Y, P.Z)), gamma), delta);
-  R.Y = sub(mul(alpha, sub(mul_small(beta, 4), R.X)), mul_small(sqr(gamma), 8));
+  R.X = sub(sqr(alpha), add(b4, b4));
+  const fp yz = mul(P.Y, P.Z);
+  R.Z = add(yz, yz);
+  R.Y = sub(mul(alpha, sub(b4, R.X)), mul_small(sqr(gamma), 8));
   return R;
 }
 
-// madd-2007-bl: P (Jacobian) + (x2, y2) (affine), P != +-(x2, y2), P not at infinity
+// madd-2007-bl: P (Jacobian) + (x2, y2) (affine), P != +-(x2, y2), P not at infinity; doublings
+// as additions and Z3 = 2 Z1 H (as in dbl)
 DEV jac madd(const jac& P, const fp& x2, const fp& y2) {
   const fp Z1Z1 = sqr(P.Z);
   const fp U2 = mul(x2, Z1Z1), S2 = mul(y2, mul(P.Z, Z1Z1));
   const fp H = sub(U2, P.X), HH = sqr(H);
   const fp I = mul_small(HH, 4), J = mul(H, I);
-  const fp rr = mul_small(sub(S2, P.Y), 2), V = mul(P.X, I);
+  const fp s = sub(S2, P.Y), rr = add(s, s), V = mul(P.X, I);
   jac R;
-  R.X = sub(sub(sqr(rr), J), mul_small(V, 2));
-  R.Y = sub(mul(rr, sub(V, R.X)), mul_small(mul(P.Y, J), 2));
-  R.Z = sub(sub(sqr(add(P.Z, H)), Z1Z1), HH);
+  R.X = sub(sub(sqr(rr), J), add(V, V));
+  const fp yj = mul(P.Y, J);
+  R.Y = sub(mul(rr, sub(V, R.X)), add(yj, yj));
+  const fp zh = mul(P.Z, H);
+  R.Z = add(zh, zh);
   return R;
 }
 
 DEV fp neg(const fp& a) { return sub(fp{{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}}, a); }
 
-// Jacobian -> affine for three points with one inversion (Montgomery's trick)
-DEV void to_affine3(const jac& A, const jac& B, const jac& C, fp& ax, fp& ay, fp& bx, fp& by,
-                    fp& cx, fp& cy) {
-  const fp ab = mul(A.Z, B.Z), abc = mul(ab, C.Z), i = inv(abc);
-  const fp ic = mul(i, ab), iab = mul(i, C.Z), ia = mul(iab, B.Z), ib = mul(iab, A.Z);
-  const fp ia2 = sqr(ia), ib2 = sqr(ib), ic2 = sqr(ic);
-  ax = mul(A.X, ia2);
-  ay = mul(A.Y, mul(ia2, ia));
-  bx = mul(B.X, ib2);
-  by = mul(B.Y, mul(ib2, ib));
-  cx = mul(C.X, ic2);
-  cy = mul(C.Y, mul(ic2, ic));
-}
-
-// Digits of the regular signed window recoding (w = 3) of the private key, computed on the host
+// Digits of the regular signed window recoding (w = 4) of the private key, computed on the host
 // (hpke.hip p256_recode): k' = sk if sk is odd, else n - sk (x(k'P) = x(-sk P) = x(sk P)), and
-// k' = sum_i d_i 8^i with every d_i odd in [-7, 7], d_85 in {1, 3}.
-constexpr int kDigits = 86;
+// k' = sum_i d_i 16^i with every d_i odd in [-15, 15], d_63 odd in [1, 15].
+constexpr int kDigits = 64;
 
 // DH(sk, pkE) for an uncompressed SEC1 point enc = 0x04 || X || Y (65 bytes): validates the
 // point (prefix, canonical coordinates, y^2 = x^3 - 3x + b) and writes the shared x-coordinate
 // as 8 big-endian words (its 32-byte encoding, RFC 9180 7.1.1).
-// Fixed window over the recoded key: a table of P, 3P, 5P, 7P (affine, one shared inversion),
-// then 85 x (three doublings + one mixed addition of +-table[|d|]).  The digits are the same in
-// every lane (one server key), and every key runs the same instruction stream: 85 windows, the
-// table entry picked by selects, not by an indexed load.
-// The additions never meet the doubling case R = +-T except, for k' in {n - 2, n - 6, n - 10,
-// n - 14}, at the last window (8 k_1 = k' - d_0 = d_0 mod n); there madd returns Z = 0 and the
-// doubled R, computed beside it for every key, is the sum.
+// Fixed window over the recoded key: a table of P, 3P, .., 15P (affine, one shared inversion by
+// Montgomery's trick), then 63 x (four doublings + one mixed addition of +-table[|d|]): 252
+// doublings and 63 additions, where w = 3 took 255 and 85 (r03: -4.5 % of the kernel's
+// instructions for 23 more operations in the table).  The digits are the same in every lane
+// (one server key), so every key runs the same instruction stream and the table is read at a
+// wave-uniform index from the lane's private memory (64 bytes per window).
+// The additions never meet the doubling case R = +-T except, for k' in {n - 2, n - 6, .., n - 30},
+// at the last window (16 k_1 = k' - d_0 = d_0 mod n); there madd returns Z = 0 and the doubled R,
+// computed beside it for every key, is the sum.
 DEV bool ecdh(const int8_t* dig, const uint8_t* enc, uint32_t dh_be[8]) {
   constexpr fp B = {{0x27d2604bu, 0x3bce3c3eu, 0xcc53b0f6u, 0x651d06b0u, 0x769886bcu, 0xb3ebbd55u,
                      0xaa3a93e7u, 0x5ac635d8u}};
@@ -257,17 +249,56 @@ DEV bool ecdh(const int8_t* dig, const uint8_t* enc, uint32_t dh_be[8]) {
   ok = from_be(enc + 33, y) && ok;
   const fp rhs = add(sub(mul(sqr(x), x), mul_small(x, 3)), B);
   ok = ok && eq(sqr(y), rhs);
-  // odd multiples: 3P = 2P + P, 5P = 4P + P, 7P = 8P - P
-  fp x3, y3, x5, y5, x7, y7;
+  // odd multiples (2i+1)P, i = 1..7, in Jacobian coordinates: 6 doublings and 7 mixed additions
+  //   3P = 2P + P, 5P = 4P + P, 7P = 8P - P, 9P = 8P + P, 11P = 12P - P, 13P = 12P + P,
+  //   15P = 16P - P, with 4P = 2(2P), 8P = 2(4P), 12P = 2(2(3P)), 16P = 2(8P).
+  // tab / zz / pz are indexed by runtime values below, so they live in the lane's private memory
+  // and the points leave registers as soon as they are made.
+  fp tab[8][2];  // affine (x, y) of (2i+1)P; Jacobian X, Y until the inversion
+  fp zz[8], pz[8];  // Z of (2i+1)P; prefix products Z_1 .. Z_i
+  tab[0][0] = x;
+  tab[0][1] = y;
   {
+    const fp ny = neg(y);
+    auto put = [&](int k, const jac& T) {
+      tab[k][0] = T.X;
+      tab[k][1] = T.Y;
+      zz[k] = T.Z;
+    };
     const jac P2 = dbl(jac{x, y, ONE});
+    const jac P3 = madd(P2, x, y);
+    put(1, P3);
+    const jac P12 = dbl(dbl(P3));
+    put(5, madd(P12, x, ny));  // 11P
+    put(6, madd(P12, x, y));   // 13P
     const jac P4 = dbl(P2);
-    to_affine3(madd(P2, x, y), madd(P4, x, y), madd(dbl(P4), x, neg(y)), x3, y3, x5, y5, x7, y7);
+    put(2, madd(P4, x, y));    // 5P
+    const jac P8 = dbl(P4);
+    put(3, madd(P8, x, ny));   // 7P
+    put(4, madd(P8, x, y));    // 9P
+    put(7, madd(dbl(P8), x, ny));  // 15P
   }
-#if P256_TAB_MEM
-  // the table in the lane's private memory (indexed by the wave-uniform digit: one 64-byte read
-  // per window, L1/L2-resident), so the ladder's registers fit three waves per SIMD
-  fp tab[4][2] = {{x, y}, {x3, y3}, {x5, y5}, {x7, y7}};
+  {  // Montgomery's trick: one inversion for the seven Z
+    fp acc = zz[1];
+    pz[1] = acc;
+#pragma unroll 1
+    for (int k = 2; k < 8; k++) {
+      acc = mul(acc, zz[k]);
+      pz[k] = acc;
+    }
+    fp ia = inv(acc);  // 1 / (Z_1 .. Z_k) for the k of the next step
+#pragma unroll 1
+    for (int k = 7; k >= 1; k--) {
+      fp zi = ia;  // 1 / Z_k
+      if (k > 1) {  // wave-uniform
+        zi = mul(ia, pz[k - 1]);
+        ia = mul(ia, zz[k]);
+      }
+      const fp zi2 = sqr(zi);
+      tab[k][0] = mul(tab[k][0], zi2);
+      tab[k][1] = mul(tab[k][1], mul(zi2, zi));
+    }
+  }
   auto pick = [&](int d, fp& tx, fp& ty) {
     const int a = (d < 0 ? -d : d) >> 1;
     tx = tab[a][0];
@@ -275,33 +306,21 @@ DEV bool ecdh(const int8_t* dig, const uint8_t* enc, uint32_t dh_be[8]) {
     const fp ny = neg(ty);
     if (d < 0) ty = ny;
   };
-#else
-  auto pick = [&](int d, fp& tx, fp& ty) {
-    const int a = d < 0 ? -d : d;
-#pragma unroll
-    for (int w = 0; w < 8; w++) {
-      tx.v[w] = a == 1 ? x.v[w] : a == 3 ? x3.v[w] : a == 5 ? x5.v[w] : x7.v[w];
-      ty.v[w] = a == 1 ? y.v[w] : a == 3 ? y3.v[w] : a == 5 ? y5.v[w] : y7.v[w];
-    }
-    const fp ny = neg(ty);
-    if (d < 0) ty = ny;
-  };
-#endif
   jac R;
   pick(dig[kDigits - 1], R.X, R.Y);
   R.Z = ONE;
   // one doubling and one addition in the loop body (the inlined asm field operations make each
-  // ~3k instructions; three unrolled doublings would not fit the instruction cache)
+  // ~3k instructions; four unrolled doublings would not fit the instruction cache)
 #pragma unroll 1
   for (int i = kDigits - 2; i >= 1; i--) {
 #pragma unroll 1
-    for (int j = 0; j < 3; j++) R = dbl(R);
+    for (int j = 0; j < 4; j++) R = dbl(R);
     fp tx, ty;
     pick(dig[i], tx, ty);
     R = madd(R, tx, ty);
   }
 #pragma unroll 1
-  for (int j = 0; j < 3; j++) R = dbl(R);
+  for (int j = 0; j < 4; j++) R = dbl(R);
   {
     fp tx, ty;
     pick(dig[0], tx, ty);

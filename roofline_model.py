@@ -213,12 +213,15 @@ def hpke_model(kem: str, aead: int, pt_len: int = 48 + 8 + 32 + 16, aad_len: int
         compress = 19
     else:
         M, S, A = PRIM["p256_mul"], PRIM["p256_sqr"], PRIM["p256_add"]
-        dbl = 3 * M + 5 * S + 17 * A           # dbl-2001-b (a = -3)
-        madd = 7 * M + 4 * S + 13 * A          # madd-2007-bl
-        inv = 255 * S + 13 * M                 # p - 2 addition chain
-        table = 3 * dbl + 3 * madd + inv + 15 * M + 6 * S   # 3P, 5P, 7P affine (shared inverse)
+        # the w = 4 window of p256_device.h (r03; a small multiple counted as two adds)
+        dbl = 4 * M + 4 * S + 13 * A           # dbl-2001-b (a = -3), Z3 = 2 Y Z
+        madd = 8 * M + 3 * S + 12 * A          # madd-2007-bl, Z3 = 2 Z1 H
+        inv = 255 * S + 12 * M                 # p - 2 addition chain
+        # 3P .. 15P: 6 doublings, 7 mixed additions, then affine by Montgomery's trick
+        table = 6 * dbl + 7 * madd + inv + 39 * M + 7 * S + A
         check = 3 * M + 2 * S + 4 * A          # y^2 = x^3 - 3x + b
-        dh = check + table + 85 * (3 * dbl + madd) + 3 * dbl + madd + inv + 2 * M
+        # 63 windows of 4 doublings + 1 addition (the last one also doubles, for the R = T case)
+        dh = check + table + 63 * (4 * dbl + madd) + dbl + inv + M + S
         compress = 21  # kem_context = enc || pkR is 130 bytes (three-block HMAC message)
     ct_blocks = -(-pt_len // 16)
     if aead == 3:
