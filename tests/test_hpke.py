@@ -330,12 +330,14 @@ P256_N = 0xffffffff00000000ffffffffffffffffbce6faada7179e84f3b9cac2fc632551
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("sk", [1, 2, 3, 6, 14, P256_N - 1, P256_N - 2, P256_N - 6, P256_N - 14,
-                                P256_N - 15, 2 ** 255, 0x1234567 << 200])
+@pytest.mark.parametrize("sk", [1, 2, 3, 6, 14, 15, 16, 18, 30, P256_N - 1, P256_N - 2, P256_N - 6,
+                                P256_N - 14, P256_N - 15, P256_N - 18, P256_N - 30, P256_N - 31,
+                                2 ** 255, 0x1234567 << 200])
 def test_gpu_p256_edge_private_keys(sk):
-    """The fixed signed window (p256_device.h ecdh) over the host recoding of the server key:
-    even keys (run as n - sk), the keys whose last window meets the doubling case (n - 2, n - 6,
-    n - 10, n - 14 and the even 2, 6, 10, 14), tiny and near-n keys, against the OpenSSL oracle."""
+    """The fixed signed window (w = 4, p256_device.h ecdh) over the host recoding of the server
+    key: even keys (run as n - sk), the keys whose last window meets the doubling case (n - 2,
+    n - 6, .., n - 30 and the even 2, 6, .., 30), tiny and near-n keys, against the OpenSSL
+    oracle."""
     from janus_amd import hpke as G
     skR = sk.to_bytes(32, "big")
     d = H.make_batch(8, 48, 32, seed=sk % 997, skR=skR, kem=H.KEM_P256)
