@@ -41,9 +41,6 @@
 #ifndef XOFD_OCC
 #define XOFD_OCC 3
 #endif
-#ifndef QH_PFD
-#define QH_PFD 1  // k_query_h: calls of measurement / coefficient loads in flight ahead
-#endif
 template <class F>
 __device__ __forceinline__ void xof_body(const DevParams& p, const InPtrs& in, const Scratch& sc,
                                          const uint32_t r) {
@@ -492,17 +489,19 @@ __global__ __launch_bounds__(256, XOFD_OCC) void k_xofd(DevParams p, InPtrs in, 
   xofd_body<FUSE, TR>(p, in, sc, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
-// Host -> device copy by the shader cores from mapped pinned memory (up to 3 ranges; 16-byte
-// loads, the byte tails by lane).  On MI355X this reads PCIe at ~55 GB/s where the SDMA copy of
-// the same staging ran at ~32 GB/s beside the XOF's own host reads (profiles/r03/r03l trace).
+// Copies by the shader cores between device memory and mapped pinned memory (up to 4 ranges,
+// 16-byte aligned; 16-byte accesses, the byte tails by lane).  Host -> device, this reads PCIe at
+// ~55 GB/s where the SDMA copy of the same staging ran at ~32 GB/s beside the XOF's own host
+// reads (profiles/r03/r03l trace); device -> host, one launch returns a group's four outputs
+// where four SDMA copies each paid their own setup.
 struct PullRanges {
-  const uint8_t* src[3];
-  uint8_t* dst[3];
-  size_t bytes[3];
+  const uint8_t* src[4];
+  uint8_t* dst[4];
+  size_t bytes[4];
 };
 DEV void pull_body(const PullRanges& pr, size_t tid, size_t nth) {
 #pragma unroll
-  for (int k = 0; k < 3; k++) {
+  for (int k = 0; k < 4; k++) {
     const size_t n16 = pr.bytes[k] / 16;
     const uint4* s16 = (const uint4*)pr.src[k];
     uint4* d16 = (uint4*)pr.dst[k];
@@ -1500,33 +1499,6 @@ __device__ __forceinline__ void query_h_body(const DevParams& p, const InPtrs& i
     // measurement elements, one iteration ahead (they come from L2/MALL, and loading them at
     // their use left the waves parked on s_waitcnt).
     T be = ldf<F>(sc.beta, 0, ld, r), Lk = ldf<F>(sc.Lbuf, 1, ld, r);
-#if QH_PFD == 2  // A/B build: two calls ahead
-    T m1[GS];
-    fetch(1, m1);
-    T be1 = ldf<F>(sc.beta, K > 1 ? 1 : 0, ld, r), L1 = ldf<F>(sc.Lbuf, K > 1 ? 2 : 1, ld, r);
-#pragma unroll 1
-    for (uint32_t k = 0; k < K; k++) {
-      T mn[GS];
-      fetch(k + 2, mn);
-      const uint32_t kn = k + 2 < K ? k + 2 : K - 1;
-      const T be_n = ldf<F>(sc.beta, kn, ld, r), L_n = ldf<F>(sc.Lbuf, kn + 1, ld, r);
-#pragma unroll
-      for (int q = 0; q < GS; q++) {
-        mac_add(Aa[q], be, mc[q]);
-        mac_add(Bb[q], Lk, mc[q]);
-        sum_add(Ssum, mc[q]);
-      }
-#pragma unroll
-      for (int q = 0; q < GS; q++) {
-        mc[q] = m1[q];
-        m1[q] = mn[q];
-      }
-      be = be1;
-      Lk = L1;
-      be1 = be_n;
-      L1 = L_n;
-    }
-#else
 #pragma unroll 1
     for (uint32_t k = 0; k < K; k++) {
       T mn[GS];
@@ -1544,7 +1516,6 @@ __device__ __forceinline__ void query_h_body(const DevParams& p, const InPtrs& i
       be = be_n;
       Lk = L_n;
     }
-#endif
     // Wire values at t, lazily reduced: f1 = seed_(2j+1) L0 + B_j - L/2 folds the seed term into
     // B's accumulator, f0 = seed_2j L0 + r^(j+1) A_j is one two-product MAC, and the gadget
     // products of the group are summed in one MAC before a single reduction.
@@ -3468,17 +3439,31 @@ int engine_run_group(prio3_engine* lead, const GroupView& g, Run** run_out) {
               : run_accumulate(lead, R, 0, g.n, R->status, R->gseg, R->gaccept, g.nseg, R->gagg,
                                (uint64_t*)R->gcnt, st);
     if (rc) return fail(rc);
-    if (hipMemcpyAsync(g.stg + L.agg_off, R->gagg, L.agg_len * g.nseg, hipMemcpyDeviceToHost,
-                       st) != hipSuccess ||
-        hipMemcpyAsync(g.stg + L.cnt_off, R->gcnt, 8 * (size_t)g.nseg, hipMemcpyDeviceToHost,
-                       st) != hipSuccess)
-      return fail(PRIO3_EDEVICE);
   }
-  if ((L.msg_len && hipMemcpyAsync(g.stg + L.msg_off, R->msgs, L.msg_len * g.n,
-                                   hipMemcpyDeviceToHost, st) != hipSuccess) ||
-      hipMemcpyAsync(g.stg + L.status_off, R->status, g.n, hipMemcpyDeviceToHost, st) !=
-          hipSuccess)
-    return fail(PRIO3_EDEVICE);
+  {  // the outputs go back by one copy launch writing the mapped staging
+    uint8_t* sd = g.stg_dev;
+    PullRanges o{};
+    o.src[0] = R->status;
+    o.dst[0] = sd + L.status_off;
+    o.bytes[0] = g.n;
+    if (L.msg_len) {
+      o.src[1] = R->msgs;
+      o.dst[1] = sd + L.msg_off;
+      o.bytes[1] = L.msg_len * g.n;
+    }
+    if (agg) {
+      o.src[2] = R->gagg;
+      o.dst[2] = sd + L.agg_off;
+      o.bytes[2] = L.agg_len * g.nseg;
+      o.src[3] = (const uint8_t*)R->gcnt;
+      o.dst[3] = sd + L.cnt_off;
+      o.bytes[3] = 8 * (size_t)g.nseg;
+    }
+    const size_t tot = o.bytes[0] + o.bytes[1] + o.bytes[2] + o.bytes[3];
+    const unsigned blocks = (unsigned)std::min<size_t>(256, (tot / 16 + 255) / 256 + 1);
+    k_pull<<<blocks, 256, 0, st>>>(o);
+    if (hipGetLastError() != hipSuccess) return fail(PRIO3_EDEVICE);
+  }
   // the launcher polls instead of sleeping in hipStreamSynchronize: the group's jobs are woken
   // as soon as their outputs land (the blocking wait added ~0.1 ms per group)
   hipError_t q;
