@@ -3384,11 +3384,12 @@ static int fused_finish(prio3_engine* e, Run* R, const uint8_t* d_status, const 
 // PULL), so the PCIe transfer runs under the Keccak work.  One pinned-staging H2D copy
 // per field ahead of the prepare (the r02 form) left transfer and prepare in series
 // (profiles/r03/r03e_jobs128_*.json: 21.5 M reports/s at 128 threads).
-int engine_run_group(prio3_engine* lead, const GroupView& g, Run** run_out) {
-  *run_out = nullptr;
+int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr) {
+  *gr = GroupRun();
+  gr->lead = lead;
+  gr->jobs = g.jobs;
   HIPCHK(hipSetDevice(lead->device));
-  PooledStream ps(lead->device);
-  hipStream_t st = ps.s;
+  hipStream_t st = ws_stream_get(lead->device);
   if (!st) return PRIO3_EDEVICE;
   const bool mp = lead->dp.kind == PRIO3_SUMVEC_F64_MP;
   // aggregating jobs: the group's reports are accumulated per job segment in this launch (the
@@ -3401,11 +3402,17 @@ int engine_run_group(prio3_engine* lead, const GroupView& g, Run** run_out) {
                       RUN_SCRATCH | RUN_IO | (mp ? 0u : (unsigned)RUN_VK) |
                           (agg ? (unsigned)RUN_AGG_IO : 0u) | (fuse ? (unsigned)RUN_FUSED : 0u),
                       agg ? g.nseg : 0, g.n_keys, st, &rc);
-  if (!R) return rc;
+  if (!R) {
+    ws_stream_put(lead->device, st);
+    return rc;
+  }
   IoLayout L;
   engine_io_layout(lead, g.cap, &L);
   auto fail = [&](int code) {
     run_release(R, st, true);
+    if (gr->prep) (void)hipEventDestroy(gr->prep);
+    gr->prep = nullptr;
+    ws_stream_put(lead->device, st);
     return code;
   };
   const uint8_t* hd = g.stg_dev;
@@ -3433,6 +3440,13 @@ int engine_run_group(prio3_engine* lead, const GroupView& g, Run** run_out) {
   rc = prepare_run(lead, R, in, out, st, fuse, false, &pr);
   if (agg) R->seg = R->gseg;
   if (rc) return fail(rc);
+  // the executor may issue its next group once this group's prepare kernels are done
+  if (hipEventCreateWithFlags(&gr->prep, hipEventDisableTiming) != hipSuccess ||
+      hipEventRecord(gr->prep, st) != hipSuccess) {
+    (void)hipGetLastError();
+    if (gr->prep) (void)hipEventDestroy(gr->prep);
+    gr->prep = nullptr;
+  }
   if (agg) {
     rc = fuse ? fused_finish(lead, R, R->status, R->gseg, R->gseg, R->gaccept, g.nseg, R->gagg,
                              (uint64_t*)R->gcnt, st)
@@ -3464,14 +3478,35 @@ int engine_run_group(prio3_engine* lead, const GroupView& g, Run** run_out) {
     k_pull<<<blocks, 256, 0, st>>>(o);
     if (hipGetLastError() != hipSuccess) return fail(PRIO3_EDEVICE);
   }
-  // the launcher polls instead of sleeping in hipStreamSynchronize: the group's jobs are woken
-  // as soon as their outputs land (the blocking wait added ~0.1 ms per group)
-  hipError_t q;
-  while ((q = hipStreamQuery(st)) == hipErrorNotReady) std::this_thread::yield();
-  if (q != hipSuccess) return fail(PRIO3_EDEVICE);
-  if (lead->timing) collect_times(lead);
-  R->refs.store(g.jobs);
-  *run_out = R;
+  gr->st = st;
+  gr->R = R;
+  return PRIO3_OK;
+}
+
+// the launcher polls these instead of sleeping in hipStreamSynchronize: the group's jobs are woken
+// as soon as their outputs land (the blocking wait added ~0.1 ms per group)
+bool engine_group_prepared(const GroupRun& gr) {
+  return gr.prep && hipEventQuery(gr.prep) == hipSuccess;
+}
+bool engine_group_done(const GroupRun& gr) { return hipStreamQuery(gr.st) != hipErrorNotReady; }
+
+int engine_group_finish(GroupRun* gr, Run** run_out) {
+  *run_out = nullptr;
+  hipError_t q = hipStreamQuery(gr->st);
+  if (q == hipErrorNotReady) q = hipStreamSynchronize(gr->st);
+  if (gr->prep) (void)hipEventDestroy(gr->prep);
+  gr->prep = nullptr;
+  const int dev = gr->lead->device;
+  if (q != hipSuccess) {
+    (void)hipGetLastError();
+    run_release(gr->R, gr->st, true);
+    ws_stream_put(dev, gr->st);
+    return PRIO3_EDEVICE;
+  }
+  if (gr->lead->timing) collect_times(gr->lead);
+  gr->R->refs.store(gr->jobs);
+  *run_out = gr->R;
+  ws_stream_put(dev, gr->st);
   return PRIO3_OK;
 }
 

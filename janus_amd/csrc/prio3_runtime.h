@@ -102,7 +102,19 @@ int engine_device(const prio3_engine* e);
 uint64_t engine_group_key(const prio3_engine* e);  // equal keys may share one launch
 uint32_t engine_job_align(const prio3_engine* e);  // column alignment of aggregating jobs
 void engine_vk(const prio3_engine* e, uint8_t out[16]);
-int engine_run_group(prio3_engine* lead, const GroupView& g, Run** run_out);
+// A group launch in two halves: issue enqueues the whole group (prepare, aggregate, outputs back
+// into the staging) on a pooled stream; finish (after done) hands the run to the group's jobs.
+struct GroupRun {
+  prio3_engine* lead = nullptr;
+  hipStream_t st = nullptr;
+  Run* R = nullptr;
+  hipEvent_t prep = nullptr;  // recorded after the prepare kernels
+  int jobs = 0;
+};
+int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr);
+bool engine_group_prepared(const GroupRun& gr);  // the prepare kernels are done
+bool engine_group_done(const GroupRun& gr);      // everything is done (non-blocking)
+int engine_group_finish(GroupRun* gr, Run** run_out);
 uint32_t exec_max_keys();
 
 // ---- coalesced accumulate (prio3_accumulate of concurrent jobs) ----------------------------
