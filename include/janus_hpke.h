@@ -10,14 +10,19 @@
  * duplicate / taskprov extension checks and the helper input share decode -- writing the decoded
  * helper input shares straight into the layout prio3_device_prepare[_aggregate] reads.
  *
- * Suites: mode_base, DHKEM(X25519, HKDF-SHA256) (0x0020) or DHKEM(P-256, HKDF-SHA256) (0x0010),
- * HKDF-SHA256 (0x0001), with any of the three AEADs of messages/src/lib.rs:844-853 (HpkeAeadId):
- * AES-128-GCM (0x0001; X25519 + AES-128-GCM is the configuration Janus generates by default,
- * hpke.rs:260-300), AES-256-GCM (0x0002) and ChaCha20Poly1305 (0x0003).  Key and enc sizes
- * follow the KEM: X25519 private / public key 32 / 32 bytes and enc[n][32]; P-256 private key
- * 32 bytes (big-endian scalar, 1 <= sk < n), public key and enc[n][65] (uncompressed SEC1
- * points).  The other KEMs (P-384, P-521, X448) and KDFs (HKDF-SHA384 / -SHA512) return
- * JANUS_HPKE_EUNSUPPORTED at creation; the host keeps its CPU path for them.
+ * Suites: mode_base with any KEM x KDF x AEAD of messages/src/lib.rs:770-853 except P-384:
+ *   KEM  DHKEM(X25519, HKDF-SHA256) 0x0020, DHKEM(P-256, HKDF-SHA256) 0x0010 -- the two Janus's
+ *        hpke crate implements (core/src/hpke.rs:414-466, 520-525) -- and DHKEM(X448,
+ *        HKDF-SHA512) 0x0021, DHKEM(P-521, HKDF-SHA512) 0x0012 (pinned by the RFC 9180 vectors
+ *        of core/src/test-vectors.json, which Janus's own test skips);
+ *   KDF  HKDF-SHA256 0x0001, HKDF-SHA384 0x0002, HKDF-SHA512 0x0003 (the key schedule's);
+ *   AEAD AES-128-GCM 0x0001 (X25519 + AES-128-GCM is the configuration Janus generates by
+ *        default, hpke.rs:260-300), AES-256-GCM 0x0002, ChaCha20Poly1305 0x0003.
+ * Key and enc sizes follow the KEM (RFC 9180 7.1): private key 32 / 32 / 56 / 66 bytes (the NIST
+ * curves' a big-endian scalar, 1 <= sk < n), public key = enc[n][Nenc] with Nenc 32 / 65 / 56 /
+ * 133 (the NIST curves' uncompressed SEC1 points).  DHKEM(P-384, HKDF-SHA384) (0x0011; no RFC
+ * 9180 vector in the reference) returns JANUS_HPKE_EUNSUPPORTED at creation; the host keeps its
+ * CPU path for it.
  *
  * Conventions as in janus_prio3.h: plain pointers and sizes, caller-owned buffers, device
  * pointers (d_*) stream-ordered on a hipStream_t (NULL = the null stream), per-report failures
@@ -35,7 +40,11 @@ extern "C" {
 enum {
   JANUS_HPKE_KEM_X25519_HKDF_SHA256 = 0x0020,
   JANUS_HPKE_KEM_P256_HKDF_SHA256 = 0x0010,
+  JANUS_HPKE_KEM_X448_HKDF_SHA512 = 0x0021,
+  JANUS_HPKE_KEM_P521_HKDF_SHA512 = 0x0012,
   JANUS_HPKE_KDF_HKDF_SHA256 = 0x0001,
+  JANUS_HPKE_KDF_HKDF_SHA384 = 0x0002,
+  JANUS_HPKE_KDF_HKDF_SHA512 = 0x0003,
   JANUS_HPKE_AEAD_AES_128_GCM = 0x0001,
   JANUS_HPKE_AEAD_AES_256_GCM = 0x0002,
   JANUS_HPKE_AEAD_CHACHA20_POLY1305 = 0x0003,
@@ -61,8 +70,8 @@ enum {
 typedef struct janus_hpke_opener janus_hpke_opener;
 
 /* One opener per (HPKE keypair, application info), bound to one GPU: Janus's HpkeKeypair
- * (hpke.rs:283-305) -- private_key is the 32-byte X25519 SerializePrivateKey, public_key the
- * 32-byte pkRm -- and HpkeApplicationInfo (hpke.rs:70-85; for helper input shares
+ * (hpke.rs:283-305) -- private_key is the KEM's SerializePrivateKey, public_key its pkRm -- and
+ * HpkeApplicationInfo (hpke.rs:70-85; for helper input shares
  * "dap-09 input share" || 0x01 || 0x03). */
 int janus_hpke_opener_create(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id,
                              const uint8_t* private_key, size_t private_key_len,
@@ -72,7 +81,7 @@ int janus_hpke_opener_create(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id,
 void janus_hpke_opener_destroy(janus_hpke_opener* opener);
 
 /* Helper input shares of one task.  Per report r:
- *   d_enc[r][Nenc]                    HpkeCiphertext.encapsulated_key (Nenc = 32 X25519, 65 P-256)
+ *   d_enc[r][Nenc]                    HpkeCiphertext.encapsulated_key (Nenc of the KEM, above)
  *   d_ct[r][ct_stride], d_ct_len[r]   HpkeCiphertext.payload (ciphertext || 16-byte tag)
  *   d_report_ids[r][16], d_times[r]   ReportMetadata (report ID, time in seconds)
  *   d_public_shares[r][public_share_len]
@@ -116,6 +125,12 @@ int janus_hpke_timing(janus_hpke_opener* opener, double* ms_total, uint32_t* lau
  * (tools/gen_p256_asm.py) against Python integers. */
 int janus_hpke_selftest_p256(int op, uint32_t n, const uint32_t* a, const uint32_t* b,
                              uint32_t* out);
+/* Test-only: the same for GF(2^448 - 2^224 - 1) (field 1, the X448 KEM; 14 words) and
+ * GF(2^521 - 1) (field 2, the P-521 KEM; 17 words), operands canonical LE words below 2^448 /
+ * 2^521 -- op 0 a*b, 1 a^2, 2 a+b, 3 a-b, 4 a*39081 (X448) or 8a (P-521), 5 a^(p-2); results
+ * canonical (fully reduced). */
+int janus_hpke_selftest_field(int field, int op, uint32_t n, const uint32_t* a, const uint32_t* b,
+                              uint32_t* out);
 
 #ifdef __cplusplus
 }

@@ -127,6 +127,8 @@ int prio3_helper_prepare_batch(prio3_engine* engine, uint32_t n, const uint8_t* 
 /* Accumulates the finished reports whose accept_mask byte is non-zero (NULL = all) into
  * per-segment aggregate shares (segment = batch identifier, query_type.rs:72-82).  A segment id
  * >= n_segments excludes the report from every aggregate and count (all accumulate paths).
+ * segment_ids (NULL = all segment 0) and accept_mask, when given, must each hold exactly n
+ * entries (n = the batch's report count); n_segments >= 1.
  * agg_shares_out[n_segments][agg_share_len] (LE field elements, mod-p sums), counts_out. */
 int prio3_accumulate(prio3_batch* batch, const uint32_t* segment_ids, const uint8_t* accept_mask,
                      uint32_t n_segments, uint8_t* agg_shares_out, uint64_t* counts_out);

@@ -24,6 +24,10 @@
 #include "sha256_device.h"
 #include "aes_device.h"
 #include "p256_device.h"
+#include "p521_device.h"
+#include "ecdh_a3.h"
+#include "x448_device.h"
+#include "sha512_device.h"
 #include "sha256_host.h"
 
 // -------------------------------------------------------------------------------------
@@ -582,14 +586,28 @@ DEV void poly_finish(Poly1305& P, uint32_t tag[4]) {
 struct HpkeParams {
   uint32_t sk[8];        // clamped X25519 scalar, LE words
   uint32_t pk[8];        // pkRm bytes, LE-packed words
-  uint32_t ksc[17];      // key_schedule_context (65 bytes) as BE words, zero padded
+  uint32_t ksc[17];      // key_schedule_context (65 bytes) as BE words, zero padded (KDF 0x0001)
   uint32_t task[8];      // task ID (input-share AAD), BE words
-  uint32_t ipad0[8], opad0[8];  // HMAC midstates of the empty key
-  uint32_t aead;                // AEAD id (1, 2, 3): selects the kernel instance
-  uint32_t kem;                 // KEM id (0x20 X25519, 0x10 P-256)
+  uint32_t ipad0[8], opad0[8];  // HMAC-SHA256 midstates of the empty key
+  uint32_t aead;                // AEAD id (1, 2, 3), wave-uniform
+  uint32_t kem;                 // KEM id (0x20 X25519, 0x10 P-256, 0x21 X448, 0x12 P-521)
+  uint32_t kdf;                 // key-schedule KDF id (1 HKDF-SHA256, 2 -SHA384, 3 -SHA512)
   uint8_t pk65[68];             // P-256: pkRm, the 65-byte uncompressed point (kem_context)
   int8_t p256_dig[88];          // P-256: signed window digits of the private key (p256_recode)
+  uint64_t ksc64[17];           // key_schedule_context (97 / 129 bytes) as BE 64-bit words (KDF 2, 3)
+  uint64_t ipad0_64[8], opad0_64[8];  // HMAC-SHA512 midstates of the empty key (X448, P-521 KEMs)
+  uint32_t sk448[14];           // X448: clamped scalar, LE words
+  uint8_t pkraw[136];           // X448 / P-521: pkRm bytes (56 / 133)
+  int8_t p521_dig[136];         // P-521: signed window digits of the private key (recode_w4)
 };
+
+// KEM constants (RFC 9180 7.1): Nenc (= Npk) and Nsecret, i.e. the Nh of the KEM's own KDF
+template <int KEM>
+struct KemC {
+  static constexpr int NENC = KEM == 0x20 ? 32 : KEM == 0x10 ? 65 : KEM == 0x21 ? 56 : 133;
+  static constexpr int NSS_W = (KEM == 0x20 || KEM == 0x10) ? 8 : 16;  // shared secret, 32-bit words
+};
+constexpr int P521_DIGITS = 131;  // w = 4 digits of a 521-bit key (130 windows + the top digit)
 
 struct OpenArgs {
   uint32_t n, ct_stride, aad_stride, share_len;
@@ -613,29 +631,193 @@ DEV void load_words(const uint8_t* p, uint32_t* w, int n16) {
   for (int i = 0; i < n16; i++) load16(p + 16 * i, w + 4 * i);
 }
 
+// suite_id = "HPKE" || kem || kdf || aead at byte pos of a SHA-256 / SHA-512 message
+template <class M>
+DEV void msuite(M& m, int pos, uint32_t kem, uint32_t kdf, uint32_t aead) {
+  mstr(m, pos, "HPKE");
+  mbyte(m, pos + 4, 0x00);
+  mbyte(m, pos + 5, kem);
+  mbyte(m, pos + 6, 0x00);
+  mbyte(m, pos + 7, kdf);
+  mbyte(m, pos + 8, 0x00);
+  mbyte(m, pos + 9, aead);
+}
+
+// RFC 9180 5.1 KeySchedule(mode_base) with HKDF-SHA256 (KDF 0x0001): shared secret (NSS 32-bit
+// BE words) -> AEAD key (BE words) and base_nonce (3 BE words).  key_schedule_context is
+// constant per opener (P.ksc, host-computed).
+template <int NSS>
+__device__ __noinline__ void key_schedule_sha256(const HpkeParams& P, uint32_t kem, const uint32_t* ss,
+                             uint32_t keyw[8], uint32_t noncew[3]) {
+  const uint32_t AEAD = P.aead, NK = AEAD == 1 ? 16 : 32;
+  uint32_t secret[8];
+  {  // secret = LabeledExtract(shared_secret, "secret", "")
+    Msg32<16> m;
+    mz(m);
+    mstr(m, 0, "HPKE-v1");
+    msuite(m, 7, kem, 1, AEAD);
+    mstr(m, 17, "secret");
+    HmacKey k;
+    hmac_keyw<NSS>(k, ss);
+    hmac(k, m, 23, secret);
+  }
+  // key / base_nonce = LabeledExpand(secret, "key" | "base_nonce", ksc, Nk | 12)
+  HmacKey k;
+  hmac_key32(k, secret);
+  Msg32<32> m;
+  mz(m);
+  mbyte(m, 0, 0);
+  mbyte(m, 1, NK);
+  mstr(m, 2, "HPKE-v1");
+  msuite(m, 9, kem, 1, AEAD);
+  mstr(m, 19, "key");
+  mwords_be(m, 22, P.ksc, 17);  // 65 bytes + 3 zero padding bytes
+  mbyte(m, 87, 0x01);
+  hmac(k, m, 88, keyw);
+  Msg32<32> n2;
+  mz(n2);
+  mbyte(n2, 0, 0);
+  mbyte(n2, 1, 12);
+  mstr(n2, 2, "HPKE-v1");
+  msuite(n2, 9, kem, 1, AEAD);
+  mstr(n2, 19, "base_nonce");
+  mwords_be(n2, 29, P.ksc, 17);
+  mbyte(n2, 94, 0x01);
+  uint32_t nw[8];
+  hmac(k, n2, 95, nw);
+  noncew[0] = nw[0], noncew[1] = nw[1], noncew[2] = nw[2];
+}
+
+// The same with HKDF-SHA384 (S384, KDF 0x0002) or HKDF-SHA512 (KDF 0x0003): Nh = 48 / 64, so
+// key_schedule_context is 97 / 129 bytes (P.ksc64) and the expand messages take two blocks.
+template <int NSS, bool S384>
+__device__ __noinline__ void key_schedule_sha512(const HpkeParams& P, uint32_t kem, const uint32_t* ss,
+                             uint32_t keyw[8], uint32_t noncew[3]) {
+  constexpr int NH = S384 ? 48 : 64, KSC = 1 + 2 * NH;
+  constexpr uint32_t KDF = S384 ? 2 : 3;
+  const uint32_t AEAD = P.aead, NK = AEAD == 1 ? 16 : 32;
+  uint64_t secret[8];
+  {  // secret = LabeledExtract(shared_secret, "secret", "")
+    uint64_t key[NSS / 2];
+#pragma unroll
+    for (int i = 0; i < NSS / 2; i++) key[i] = (uint64_t)ss[2 * i] << 32 | ss[2 * i + 1];
+    HmacKey64 k;
+    hmac64_key(k, key, NSS / 2, S384);
+    Msg64<16> m;
+    mz(m);
+    mstr(m, 0, "HPKE-v1");
+    msuite(m, 7, kem, KDF, AEAD);
+    mstr(m, 17, "secret");
+    hmac64(k, m, 23, secret);
+  }
+  HmacKey64 k;
+  hmac64_key(k, secret, NH / 8, S384);
+  uint64_t o[8];
+  {  // key = LabeledExpand(secret, "key", ksc, Nk)
+    Msg64<32> m;
+    mz(m);
+    mbyte(m, 0, 0);
+    mbyte(m, 1, NK);
+    mstr(m, 2, "HPKE-v1");
+    msuite(m, 9, kem, KDF, AEAD);
+    mstr(m, 19, "key");
+    mwords64(m, 22, P.ksc64, 17);  // KSC bytes + zero padding
+    mbyte(m, 22 + KSC, 0x01);
+    hmac64(k, m, 23 + KSC, o);
+#pragma unroll
+    for (int i = 0; i < 4; i++) keyw[2 * i] = (uint32_t)(o[i] >> 32), keyw[2 * i + 1] = (uint32_t)o[i];
+  }
+  {  // base_nonce = LabeledExpand(secret, "base_nonce", ksc, 12)
+    Msg64<32> m;
+    mz(m);
+    mbyte(m, 0, 0);
+    mbyte(m, 1, 12);
+    mstr(m, 2, "HPKE-v1");
+    msuite(m, 9, kem, KDF, AEAD);
+    mstr(m, 19, "base_nonce");
+    mwords64(m, 29, P.ksc64, 17);
+    mbyte(m, 29 + KSC, 0x01);
+    hmac64(k, m, 30 + KSC, o);
+    noncew[0] = (uint32_t)(o[0] >> 32), noncew[1] = (uint32_t)o[0], noncew[2] = (uint32_t)(o[1] >> 32);
+  }
+}
+
+// DHKEM ExtractAndExpand with HKDF-SHA512 (the X448 and P-521 KEMs): dh (NDH bytes, a byte
+// accessor) and kem_context = enc || pkRm (NENC bytes each) -> shared_secret (16 BE words)
+template <int KEM, int NDH, class DhByte, class EncByte>
+DEV void eae_sha512(const HpkeParams& P, DhByte dh, EncByte enc, uint32_t ss[16]) {
+  constexpr int NENC = KemC<KEM>::NENC;
+  uint64_t prk[8];
+  {  // eae_prk = LabeledExtract("", "eae_prk", dh)
+    HmacKey64 k0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) k0.ist[i] = P.ipad0_64[i], k0.ost[i] = P.opad0_64[i];
+    k0.out_words = 8;
+    Msg64<(19 + NDH + 17 + 127) / 128 * 16> m;
+    mz(m);
+    mstr(m, 0, "HPKE-v1");
+    mstr(m, 7, "KEM");
+    mbyte(m, 10, 0x00);
+    mbyte(m, 11, KEM);
+    mstr(m, 12, "eae_prk");
+#pragma unroll
+    for (int i = 0; i < NDH; i++) mbyte(m, 19 + i, dh(i));
+    hmac64(k0, m, 19 + NDH, prk);
+  }
+  // shared_secret = LabeledExpand(eae_prk, "shared_secret", enc || pkRm, 64)
+  HmacKey64 k;
+  hmac64_key(k, prk, 8, false);
+  constexpr int LEN = 27 + 2 * NENC + 1;
+  Msg64<(LEN + 17 + 127) / 128 * 16> m;
+  mz(m);
+  mbyte(m, 0, 0);
+  mbyte(m, 1, 64);
+  mstr(m, 2, "HPKE-v1");
+  mstr(m, 9, "KEM");
+  mbyte(m, 12, 0x00);
+  mbyte(m, 13, KEM);
+  mstr(m, 14, "shared_secret");
+#pragma unroll
+  for (int i = 0; i < NENC; i++) mbyte(m, 27 + i, enc(i));
+#pragma unroll
+  for (int i = 0; i < NENC; i++) mbyte(m, 27 + NENC + i, P.pkraw[i]);
+  mbyte(m, LEN - 1, 0x01);
+  uint64_t o[8];
+  hmac64(k, m, LEN, o);
+#pragma unroll
+  for (int i = 0; i < 8; i++) ss[2 * i] = (uint32_t)(o[i] >> 32), ss[2 * i + 1] = (uint32_t)o[i];
+}
+
+// the P-521 ECDH, out of line (one copy for the three kernel instances of the KEM)
+__device__ __noinline__ bool p521_dh(const int8_t* dig, const uint8_t* enc, uint8_t* dh) {
+  return ecdh_a3::ecdh<p521::Field, P521_DIGITS>(dig, enc, dh);
+}
+
 // MODE 0: explicit AAD, plaintext out.  MODE 1: DAP helper input share with PUB bytes of
 // public share (InputShareAad built here), decoded helper share out.
 // AEAD (P.aead): 1 AES-128-GCM, 2 AES-256-GCM, 3 ChaCha20Poly1305 (RFC 9180 7.3 ids).
 // KEM: 0x20 DHKEM(X25519, HKDF-SHA256) (enc: 32 bytes), 0x10 DHKEM(P-256, HKDF-SHA256) (enc: the
-// 65-byte uncompressed point)
-// The AEAD is a kernel argument (P.aead, wave-uniform): one instance per (MODE, PUB, KEM) keeps
-// the X25519 / P-256 ladders to six copies.
+// 65-byte uncompressed point), 0x21 DHKEM(X448, HKDF-SHA512) (56 bytes), 0x12 DHKEM(P-521,
+// HKDF-SHA512) (133 bytes).  The key-schedule KDF (P.kdf: HKDF-SHA256 / -384 / -512) and the AEAD
+// are kernel arguments (wave-uniform): one instance per (MODE, PUB, KEM).
 #ifndef HPKE_WAVES  // A/B builds: e.g. -DHPKE_WAVES='__attribute__((amdgpu_waves_per_eu(3, 3)))'
 #define HPKE_WAVES
 #endif
 template <int MODE, int PUB, int KEM>
 __global__ __launch_bounds__(256) HPKE_WAVES void k_hpke_open(HpkeParams P, OpenArgs a) {
-  static_assert(KEM == 0x20 || KEM == 0x10, "KEM id");
+  static_assert(KEM == 0x20 || KEM == 0x10 || KEM == 0x21 || KEM == 0x12, "KEM id");
   const uint32_t AEAD = P.aead;
-  const uint32_t NK = AEAD == 1 ? 16 : 32;  // Nk: AEAD key bytes
   __shared__ AesT T;
   aes_tables_init(T);
   __syncthreads();
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= a.n) return;
   // ---- DHKEM Decap (RFC 9180 4.1): dh, then ExtractAndExpand(dh, enc || pkRm) -------------
-  uint32_t prk[8], ss[8], secret[8], keyw[8], noncew[8];
+  constexpr int NSS = KemC<KEM>::NSS_W;
+  uint32_t ss[NSS], keyw[8], noncew[3];
   bool ok;
+  if constexpr (KEM == 0x20 || KEM == 0x10) {
+  uint32_t prk[8];
   HmacKey k0;  // the empty-key HMAC midstates (eae_prk extraction)
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -716,58 +898,39 @@ __global__ __launch_bounds__(256) HPKE_WAVES void k_hpke_open(HpkeParams P, Open
       hmac(k, m, 158, ss);
     }
   }
-  {  // secret = LabeledExtract(shared_secret, "secret", "")
-    Msg32<16> m;
-    mz(m);
-    mstr(m, 0, "HPKE-v1");
-    mstr(m, 7, "HPKE");
-    mbyte(m, 11, 0x00);
-    mbyte(m, 12, KEM);
-    mbyte(m, 13, 0x00);
-    mbyte(m, 14, 0x01);
-    mbyte(m, 15, 0x00);
-    mbyte(m, 16, AEAD);
-    mstr(m, 17, "secret");
-    HmacKey k;
-    hmac_key32(k, ss);
-    hmac(k, m, 23, secret);
+  } else if constexpr (KEM == 0x21) {
+    // X448 (RFC 7748): enc is the 56-byte u-coordinate; rows are 8-byte aligned
+    uint32_t encw[14], dh[14];
+    const uint2* ep = (const uint2*)(a.enc + 56 * (size_t)r);
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+      const uint2 v = ep[i];
+      encw[2 * i] = v.x, encw[2 * i + 1] = v.y;
+    }
+    x448::ladder(P.sk448, encw, dh);
+    uint32_t nz = 0;
+#pragma unroll
+    for (int i = 0; i < 14; i++) nz |= dh[i];
+    ok = nz != 0;  // all-zero shared secret: ValidationError
+    auto byte_of = [](const uint32_t* w) {
+      return [w](int i) { return (w[i >> 2] >> (8 * (i & 3))) & 0xffu; };
+    };
+    eae_sha512<KEM, 56>(P, byte_of(dh), byte_of(encw), ss);
+  } else {
+    // P-521 (SEC 1): enc is the 133-byte uncompressed point
+    const uint8_t* ep = a.enc + 133 * (size_t)r;
+    uint8_t dh[66];
+    ok = p521_dh(P.p521_dig, ep, dh);
+    eae_sha512<KEM, 66>(P, [&](int i) { return (uint32_t)dh[i]; },
+                        [&](int i) { return (uint32_t)ep[i]; }, ss);
   }
-  {  // key / base_nonce = LabeledExpand(secret, "key" | "base_nonce", ksc, Nk | 12)
-    HmacKey k;
-    hmac_key32(k, secret);
-    Msg32<32> m;
-    mz(m);
-    mbyte(m, 0, 0);
-    mbyte(m, 1, NK);
-    mstr(m, 2, "HPKE-v1");
-    mstr(m, 9, "HPKE");
-    mbyte(m, 13, 0x00);
-    mbyte(m, 14, KEM);
-    mbyte(m, 15, 0x00);
-    mbyte(m, 16, 0x01);
-    mbyte(m, 17, 0x00);
-    mbyte(m, 18, AEAD);
-    mstr(m, 19, "key");
-    mwords_be(m, 22, P.ksc, 17);  // 65 bytes + 3 zero padding bytes
-    mbyte(m, 87, 0x01);
-    hmac(k, m, 88, keyw);
-    Msg32<32> n2;
-    mz(n2);
-    mbyte(n2, 0, 0);
-    mbyte(n2, 1, 12);
-    mstr(n2, 2, "HPKE-v1");
-    mstr(n2, 9, "HPKE");
-    mbyte(n2, 13, 0x00);
-    mbyte(n2, 14, KEM);
-    mbyte(n2, 15, 0x00);
-    mbyte(n2, 16, 0x01);
-    mbyte(n2, 17, 0x00);
-    mbyte(n2, 18, AEAD);
-    mstr(n2, 19, "base_nonce");
-    mwords_be(n2, 29, P.ksc, 17);
-    mbyte(n2, 94, 0x01);
-    hmac(k, n2, 95, noncew);
-  }
+  // ---- KeySchedule(mode_base) with the suite's KDF -----------------------------------------
+  if (P.kdf == 1)
+    key_schedule_sha256<NSS>(P, KEM, ss, keyw, noncew);
+  else if (P.kdf == 2)
+    key_schedule_sha512<NSS, true>(P, KEM, ss, keyw, noncew);
+  else
+    key_schedule_sha512<NSS, false>(P, KEM, ss, keyw, noncew);
   uint32_t aad_len, pt_len;
   uint8_t* pp;
   auto gcm_open = [&](auto nr_tag) {  // NR = 10 (AES-128-GCM) or 14 (AES-256-GCM)
@@ -1072,6 +1235,40 @@ void hmac_host(const uint8_t* key, size_t klen, const std::vector<uint8_t>& msg,
   sha256_host(outer, out);
 }
 
+// SHA-512 / SHA-384 and their HMAC on the host (key_schedule_context of KDFs 0x0002 / 0x0003)
+void sha512_host(const std::vector<uint8_t>& msg, bool s384, uint8_t* out) {
+  uint64_t st[8];
+  for (int i = 0; i < 8; i++) st[i] = s384 ? sha512d::IV384[i] : sha512d::IV512[i];
+  std::vector<uint8_t> m = msg;
+  const uint64_t bits = (uint64_t)msg.size() * 8;
+  m.push_back(0x80);
+  while (m.size() % 128 != 112) m.push_back(0);
+  for (int i = 0; i < 8; i++) m.push_back(0);
+  for (int i = 7; i >= 0; i--) m.push_back((uint8_t)(bits >> (8 * i)));
+  for (size_t o = 0; o < m.size(); o += 128) {
+    uint64_t w[16];
+    for (int i = 0; i < 16; i++) {
+      w[i] = 0;
+      for (int j = 0; j < 8; j++) w[i] = w[i] << 8 | m[o + 8 * i + j];
+    }
+    sha512d::compress(st, w);
+  }
+  for (int i = 0; i < (s384 ? 6 : 8); i++)
+    for (int j = 0; j < 8; j++) out[8 * i + j] = (uint8_t)(st[i] >> (56 - 8 * j));
+}
+void hmac512_host(const uint8_t* key, size_t klen, const std::vector<uint8_t>& msg, bool s384,
+                  uint8_t* out) {
+  uint8_t k[128] = {0};
+  memcpy(k, key, klen);  // klen <= 128 here
+  std::vector<uint8_t> in(128), outer(128);
+  for (int i = 0; i < 128; i++) in[i] = k[i] ^ 0x36, outer[i] = k[i] ^ 0x5c;
+  in.insert(in.end(), msg.begin(), msg.end());
+  uint8_t ih[64];
+  sha512_host(in, s384, ih);
+  outer.insert(outer.end(), ih, ih + (s384 ? 48 : 64));
+  sha512_host(outer, s384, out);
+}
+
 std::vector<uint8_t> cat(std::initializer_list<std::vector<uint8_t>> parts) {
   std::vector<uint8_t> r;
   for (auto& p : parts) r.insert(r.end(), p.begin(), p.end());
@@ -1080,9 +1277,32 @@ std::vector<uint8_t> cat(std::initializer_list<std::vector<uint8_t>> parts) {
 std::vector<uint8_t> bytes(const char* s) { return std::vector<uint8_t>(s, s + strlen(s)); }
 
 // suite_id = "HPKE" || kem_id || kdf_id || aead_id (RFC 9180 5.1)
-std::vector<uint8_t> hpke_suite(uint16_t kem, uint16_t aead) {
-  return {'H',         'P',           'K',  'E', (uint8_t)(kem >> 8), (uint8_t)kem, 0x00, 0x01,
+std::vector<uint8_t> hpke_suite(uint16_t kem, uint16_t kdf, uint16_t aead) {
+  return {'H', 'P', 'K', 'E', (uint8_t)(kem >> 8), (uint8_t)kem, (uint8_t)(kdf >> 8), (uint8_t)kdf,
           (uint8_t)(aead >> 8), (uint8_t)aead};
+}
+// P-521 group order n (SEC 2), big-endian
+const uint8_t kP521N[66] = {
+    0x01, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+    0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+    0xff, 0xff, 0xff, 0xff, 0xff, 0xfa, 0x51, 0x86, 0x87, 0x83, 0xbf, 0x2f, 0x96, 0x6b,
+    0x7f, 0xcc, 0x01, 0x48, 0xf7, 0x09, 0xa5, 0xd0, 0x3b, 0xb5, 0xc9, 0xb8, 0x89, 0x9c,
+    0x47, 0xae, 0xbb, 0x6f, 0xb7, 0x1e, 0x91, 0x38, 0x64, 0x09};
+// 1 <= sk < n for a big-endian scalar of the group order's length
+bool scalar_in_range(const uint8_t* sk, const uint8_t* n, size_t len) {
+  bool zero = true, below = false, decided = false;
+  for (size_t i = 0; i < len; i++) {
+    zero = zero && sk[i] == 0;
+    if (!decided && sk[i] != n[i]) below = sk[i] < n[i], decided = true;
+  }
+  return !zero && below;
+}
+// KEM sizes (RFC 9180 7.1): private key, Nenc (= Npk); 0 = not a KEM this opener implements
+size_t kem_nsk(uint16_t kem) {
+  return kem == 0x20 || kem == 0x10 ? 32 : kem == 0x21 ? 56 : kem == 0x12 ? 66 : 0;
+}
+size_t kem_nenc(uint16_t kem) {
+  return kem == 0x20 ? 32 : kem == 0x10 ? 65 : kem == 0x21 ? 56 : kem == 0x12 ? 133 : 0;
 }
 // P-256 group order n (SEC 2), big-endian
 const uint8_t kP256N[32] = {0xff, 0xff, 0xff, 0xff, 0x00, 0x00, 0x00, 0x00, 0xff, 0xff, 0xff,
@@ -1128,6 +1348,32 @@ static void p256_recode(const uint32_t sk[8], int8_t dig[88]) {
   for (int i = p256::kDigits; i < 88; i++) dig[i] = 0;
 }
 
+// The same recoding for a key of nw little-endian words against the group order n (nw words):
+// ndig - 1 digits of four bits, then the odd top digit (P-521: 131 digits for 521 bits).
+static void recode_w4(const uint32_t* sk, const uint32_t* n, int nw, int ndig, int8_t* dig) {
+  std::vector<uint32_t> k(sk, sk + nw);
+  if (!(k[0] & 1u)) {
+    int64_t br = 0;
+    for (int i = 0; i < nw; i++) {
+      const int64_t t = (int64_t)n[i] - k[i] + br;
+      k[i] = (uint32_t)t;
+      br = t >> 32;
+    }
+  }
+  for (int i = 0; i < ndig - 1; i++) {
+    const int d = (int)(k[0] & 31u) - 16;
+    dig[i] = (int8_t)d;
+    int64_t c = -(int64_t)d;
+    for (int j = 0; j < nw; j++) {
+      const int64_t t = (int64_t)k[j] + c;
+      k[j] = (uint32_t)t;
+      c = t >> 32;
+    }
+    for (int j = 0; j < nw; j++) k[j] = k[j] >> 4 | (j < nw - 1 ? k[j + 1] << 28 : 0u);
+  }
+  dig[ndig - 1] = (int8_t)k[0];
+}
+
 struct janus_hpke_opener {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -1160,47 +1406,78 @@ int janus_hpke_opener_create(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id,
                              janus_hpke_opener** out) {
   if (!out || !private_key || !public_key || (info_len && !info)) return JANUS_HPKE_EINVAL;
   *out = nullptr;
-  const bool x25519 = kem_id == JANUS_HPKE_KEM_X25519_HKDF_SHA256,
-             p256 = kem_id == JANUS_HPKE_KEM_P256_HKDF_SHA256;
-  if ((!x25519 && !p256) || kdf_id != JANUS_HPKE_KDF_HKDF_SHA256 ||
+  if (!kem_nsk(kem_id) || kdf_id < JANUS_HPKE_KDF_HKDF_SHA256 ||
+      kdf_id > JANUS_HPKE_KDF_HKDF_SHA512 ||
       (aead_id != JANUS_HPKE_AEAD_AES_128_GCM && aead_id != JANUS_HPKE_AEAD_AES_256_GCM &&
        aead_id != JANUS_HPKE_AEAD_CHACHA20_POLY1305))
     return JANUS_HPKE_EUNSUPPORTED;
-  if (private_key_len != 32 || public_key_len != (x25519 ? 32u : 65u)) return JANUS_HPKE_EINVAL;
-  if (p256) {  // DeserializePrivateKey: 1 <= sk < n; pkRm an uncompressed point
-    bool zero = true, below = false, decided = false;
-    for (int i = 0; i < 32; i++) {
-      zero = zero && private_key[i] == 0;
-      if (!decided && private_key[i] != kP256N[i]) below = private_key[i] < kP256N[i], decided = true;
-    }
-    if (zero || !below || public_key[0] != 0x04) return JANUS_HPKE_EINVAL;
-  }
+  if (private_key_len != kem_nsk(kem_id) || public_key_len != kem_nenc(kem_id))
+    return JANUS_HPKE_EINVAL;
+  // DeserializePrivateKey (RFC 9180 7.1.2): the NIST curves need 1 <= sk < n; pkRm uncompressed
+  if (kem_id == JANUS_HPKE_KEM_P256_HKDF_SHA256 &&
+      (!scalar_in_range(private_key, kP256N, 32) || public_key[0] != 0x04))
+    return JANUS_HPKE_EINVAL;
+  if (kem_id == JANUS_HPKE_KEM_P521_HKDF_SHA512 &&
+      (!scalar_in_range(private_key, kP521N, 66) || public_key[0] != 0x04))
+    return JANUS_HPKE_EINVAL;
   auto* o = new janus_hpke_opener();
   o->device = device;
   memset(&o->P, 0, sizeof(o->P));
   o->P.kem = kem_id;
-  if (x25519) {
+  o->P.kdf = kdf_id;
+  o->P.aead = aead_id;
+  if (kem_id == JANUS_HPKE_KEM_X25519_HKDF_SHA256) {
     uint8_t k[32];
     memcpy(k, private_key, 32);
     k[0] &= 248;  // decodeScalar25519 (RFC 7748 section 5)
     k[31] &= 127;
     k[31] |= 64;
     for (int i = 0; i < 8; i++) o->P.sk[i] = le32(k + 4 * i), o->P.pk[i] = le32(public_key + 4 * i);
-  } else {
+  } else if (kem_id == JANUS_HPKE_KEM_P256_HKDF_SHA256) {
     for (int i = 0; i < 8; i++) o->P.sk[i] = be32(private_key + 4 * (7 - i));  // LE limbs
     memcpy(o->P.pk65, public_key, 65);
     p256_recode(o->P.sk, o->P.p256_dig);
+  } else if (kem_id == JANUS_HPKE_KEM_X448_HKDF_SHA512) {
+    uint8_t k[56];
+    memcpy(k, private_key, 56);
+    k[0] &= 252;  // decodeScalar448 (RFC 7748 section 5)
+    k[55] |= 128;
+    for (int i = 0; i < 14; i++) o->P.sk448[i] = le32(k + 4 * i);
+    memcpy(o->P.pkraw, public_key, 56);
+  } else {  // P-521: the 66-byte big-endian scalar as 17 LE words, recoded against n
+    uint8_t kb[68] = {0}, nb[68] = {0};
+    memcpy(kb + 2, private_key, 66);
+    memcpy(nb + 2, kP521N, 66);
+    uint32_t kw[17], nw[17];
+    for (int i = 0; i < 17; i++) kw[i] = be32(kb + 4 * (16 - i)), nw[i] = be32(nb + 4 * (16 - i));
+    recode_w4(kw, nw, 17, P521_DIGITS, o->P.p521_dig);
+    memcpy(o->P.pkraw, public_key, 133);
   }
   // key_schedule_context = mode_base || LabeledExtract("", "psk_id_hash", "") ||
   //                        LabeledExtract("", "info_hash", info)        (RFC 9180 5.1)
-  uint8_t ksc[68] = {0};
   std::vector<uint8_t> inf(info, info + info_len);
-  const std::vector<uint8_t> suite = hpke_suite(kem_id, aead_id);
-  hmac_host(nullptr, 0, cat({bytes("HPKE-v1"), suite, bytes("psk_id_hash")}), ksc + 1);
-  hmac_host(nullptr, 0, cat({bytes("HPKE-v1"), suite, bytes("info_hash"), inf}), ksc + 33);
-  o->P.aead = aead_id;
-  for (int i = 0; i < 17; i++) o->P.ksc[i] = be32(ksc + 4 * i);
-  // HMAC midstates of the empty key (eae_prk extraction)
+  const std::vector<uint8_t> suite = hpke_suite(kem_id, kdf_id, aead_id);
+  const std::vector<uint8_t> psk_msg = cat({bytes("HPKE-v1"), suite, bytes("psk_id_hash")}),
+                             info_msg = cat({bytes("HPKE-v1"), suite, bytes("info_hash"), inf});
+  if (kdf_id == JANUS_HPKE_KDF_HKDF_SHA256) {
+    uint8_t ksc[68] = {0};
+    hmac_host(nullptr, 0, psk_msg, ksc + 1);
+    hmac_host(nullptr, 0, info_msg, ksc + 33);
+    for (int i = 0; i < 17; i++) o->P.ksc[i] = be32(ksc + 4 * i);
+  } else {
+    const bool s384 = kdf_id == JANUS_HPKE_KDF_HKDF_SHA384;
+    const size_t nh = s384 ? 48 : 64;
+    uint8_t ksc[136] = {0};
+    hmac512_host(nullptr, 0, psk_msg, s384, ksc + 1);
+    hmac512_host(nullptr, 0, info_msg, s384, ksc + 1 + nh);
+    for (int i = 0; i < 17; i++) {
+      uint64_t w = 0;
+      for (int j = 0; j < 8; j++) w = w << 8 | ksc[8 * i + j];
+      o->P.ksc64[i] = w;
+    }
+  }
+  // HMAC midstates of the empty key: SHA-256 (eae_prk of the X25519 / P-256 KEMs) and SHA-512
+  // (eae_prk of the X448 / P-521 KEMs, whose KDF is HKDF-SHA512 whatever the key schedule's)
   uint32_t iv[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                     0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
   uint8_t b36[64], b5c[64];
@@ -1210,6 +1487,12 @@ int janus_hpke_opener_create(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id,
   memcpy(o->P.opad0, iv, 32);
   sha256_compress_host(o->P.ipad0, b36);
   sha256_compress_host(o->P.opad0, b5c);
+  {
+    HmacKey64 k0;
+    hmac64_key(k0, nullptr, 0, false);
+    memcpy(o->P.ipad0_64, k0.ist, 64);
+    memcpy(o->P.opad0_64, k0.ost, 64);
+  }
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&o->stream, hipStreamNonBlocking) != hipSuccess) {
     delete o;
@@ -1279,6 +1562,10 @@ static int launch_open(janus_hpke_opener* o, int mode, int pub, const OpenArgs& 
     k_hpke_open<1, 0, KE><<<blocks, 256, 0, st>>>(o->P, a);
   if (o->P.kem == JANUS_HPKE_KEM_P256_HKDF_SHA256) {
     JANUS_HPKE_LAUNCH(0x10)
+  } else if (o->P.kem == JANUS_HPKE_KEM_X448_HKDF_SHA512) {
+    JANUS_HPKE_LAUNCH(0x21)
+  } else if (o->P.kem == JANUS_HPKE_KEM_P521_HKDF_SHA512) {
+    JANUS_HPKE_LAUNCH(0x12)
   } else {
     JANUS_HPKE_LAUNCH(0x20)
   }
@@ -1404,7 +1691,96 @@ __global__ __launch_bounds__(256) void k_selftest_p256(int op, uint32_t n, const
   for (int k = 0; k < 8; k++) out[8 * (size_t)i + k] = r.v[k];
 }
 
+// Test-only (janus_hpke_selftest_field): one operation of the X448 (field 1) or P-521 (field 2)
+// field code per element; operands and results as canonical little-endian 32-bit words (14 / 17)
+__device__ p521::fp p521_from_words(const uint32_t* w) {
+  p521::fp r;
+#pragma unroll
+  for (int k = 0; k < p521::NL; k++) {
+    const int bit = 29 * k, q = bit >> 5, o = bit & 31;
+    uint32_t x = w[q] >> o;
+    if (o > 3 && q + 1 < 17) x |= w[q + 1] << (32 - o);
+    r.v[k] = x & (k == p521::NL - 1 ? p521::M28 : p521::M29);
+  }
+  return r;
+}
+__device__ void p521_to_words(const p521::fp& a, uint32_t* w) {
+  const p521::fp f = p521::freeze(a);
+#pragma unroll
+  for (int q = 0; q < 17; q++) w[q] = 0;
+#pragma unroll
+  for (int k = 0; k < p521::NL; k++) {
+    const int bit = 29 * k, q = bit >> 5, o = bit & 31;
+    w[q] |= f.v[k] << o;
+    if (o > 3 && q + 1 < 17) w[q + 1] |= f.v[k] >> (32 - o);
+  }
+}
+__global__ __launch_bounds__(256) void k_selftest_field(int field, int op, uint32_t n,
+                                                        const uint32_t* a, const uint32_t* b,
+                                                        uint32_t* out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (field == 1) {
+    uint32_t wa[14], wb[14], wr[14];
+#pragma unroll
+    for (int k = 0; k < 14; k++) wa[k] = a[14 * (size_t)i + k], wb[k] = b[14 * (size_t)i + k];
+    const x448::fe x = x448::from_words(wa), y = x448::from_words(wb);
+    x448::fe r;
+    switch (op) {
+      case 0: r = x448::mul(x, y); break;
+      case 1: r = x448::sqr(x); break;
+      case 2: r = x448::add(x, y); break;
+      case 3: r = x448::sub(x, y); break;
+      case 4: r = x448::mul_small(x, 39081); break;
+      default: r = x448::inv(x); break;
+    }
+    x448::to_words(r, wr);
+#pragma unroll
+    for (int k = 0; k < 14; k++) out[14 * (size_t)i + k] = wr[k];
+  } else {
+    uint32_t wa[17], wb[17], wr[17];
+#pragma unroll
+    for (int k = 0; k < 17; k++) wa[k] = a[17 * (size_t)i + k], wb[k] = b[17 * (size_t)i + k];
+    const p521::fp x = p521_from_words(wa), y = p521_from_words(wb);
+    p521::fp r;
+    switch (op) {
+      case 0: r = p521::mul(x, y); break;
+      case 1: r = p521::sqr(x); break;
+      case 2: r = p521::add(x, y); break;
+      case 3: r = p521::sub(x, y); break;
+      case 4: r = p521::mul_small(x, 8); break;
+      default: r = p521::inv(x); break;
+    }
+    p521_to_words(r, wr);
+#pragma unroll
+    for (int k = 0; k < 17; k++) out[17 * (size_t)i + k] = wr[k];
+  }
+}
+
 extern "C" {
+
+int janus_hpke_selftest_field(int field, int op, uint32_t n, const uint32_t* a, const uint32_t* b,
+                              uint32_t* out) {
+  if ((field != 1 && field != 2) || op < 0 || op > 5) return JANUS_HPKE_EINVAL;
+  if (n == 0) return JANUS_HPKE_OK;
+  const size_t m = (size_t)n * (field == 1 ? 14 : 17) * 4;
+  void *da = nullptr, *db = nullptr, *dout = nullptr;
+  int rc = JANUS_HPKE_OK;
+  if (hipMalloc(&da, m) != hipSuccess || hipMalloc(&db, m) != hipSuccess ||
+      hipMalloc(&dout, m) != hipSuccess || hipMemcpy(da, a, m, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(db, b, m, hipMemcpyHostToDevice) != hipSuccess) {
+    rc = JANUS_HPKE_EDEVICE;
+  } else {
+    k_selftest_field<<<(n + 255) / 256, 256>>>(field, op, n, (const uint32_t*)da,
+                                               (const uint32_t*)db, (uint32_t*)dout);
+    if (hipGetLastError() != hipSuccess || hipMemcpy(out, dout, m, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = JANUS_HPKE_EDEVICE;
+  }
+  (void)hipFree(da);
+  (void)hipFree(db);
+  (void)hipFree(dout);
+  return rc;
+}
 
 int janus_hpke_open_input_shares(janus_hpke_opener* o, uint32_t n, const uint8_t task_id[32],
                                  const uint8_t* enc, const uint8_t* ct, const uint32_t* ct_len,
@@ -1417,7 +1793,7 @@ int janus_hpke_open_input_shares(janus_hpke_opener* o, uint32_t n, const uint8_t
   HCHK(hipSetDevice(o->device));
   DevBuf de, dc, dl, di, dt, dp, ds, dst;
   int rc;
-  const size_t nenc = o->P.kem == JANUS_HPKE_KEM_P256_HKDF_SHA256 ? 65 : 32;
+  const size_t nenc = kem_nenc((uint16_t)o->P.kem);
   if ((rc = up(de, enc, nenc * n, o->stream)) || (rc = up(dc, ct, (size_t)ct_stride * n, o->stream)) ||
       (rc = up(dl, ct_len, 4 * (size_t)n, o->stream)) ||
       (rc = up(di, report_ids, 16 * (size_t)n, o->stream)) ||
@@ -1469,7 +1845,7 @@ int janus_hpke_open(janus_hpke_opener* o, uint32_t n, const uint8_t* enc, const 
   HCHK(hipSetDevice(o->device));
   DevBuf de, dc, dl, da, dal, dpt, dst;
   int rc;
-  const size_t nenc = o->P.kem == JANUS_HPKE_KEM_P256_HKDF_SHA256 ? 65 : 32;
+  const size_t nenc = kem_nenc((uint16_t)o->P.kem);
   if ((rc = up(de, enc, nenc * n, o->stream)) || (rc = up(dc, ct, (size_t)ct_stride * n, o->stream)) ||
       (rc = up(dl, ct_len, 4 * (size_t)n, o->stream)) ||
       (rc = up(da, aad, (size_t)aad_stride * n, o->stream)) ||

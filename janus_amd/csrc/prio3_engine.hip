@@ -1602,12 +1602,8 @@ __global__ __launch_bounds__(256, 3) void k_prep_h(DevParams p, InPtrs in, Scrat
                                                    OutPtrs out) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   xofd_body<FUSE, false, PULL>(p, in, sc, r);
-#ifndef JANUS_AB_XOF_ONLY  // A/B build: the fused kernel's XOF half alone
-#ifndef QH_GS
-#define QH_GS 2  // wires per sweep of the fused kernel's query (A/B builds: 3, 4)
-#endif
-  query_h_body<QH_GS, 32>(p, in, sc, out, r);
-#endif
+  // two wires per sweep: 3 and 4 spill inside the wire loop
+  query_h_body<2, 32>(p, in, sc, out, r);
 }
 
 // k_prep_sum<NPH>: the same for Prio3Sum (P = 16 NPH): the dual-state XOF and k_query_sum's body
@@ -1830,9 +1826,14 @@ __global__ __launch_bounds__(256) void k_agg_waves(uint32_t nwaves, uint32_t M,
   const uint32_t s0 = fused ? (uint32_t)__shfl((int)my, __ffsll((long long)fused) - 1) : 0xffffffffu;
   const bool mixed = __any(my != 0xffffffffu && my != s0);
   if (slot == 0 && blockIdx.x == 0) cseg[c] = mixed ? 0xffffffffu : s0;
-  if (slot >= M * 8 || s0 == 0xffffffffu) return;  // M * 8 is a multiple of 4
+  if (s0 == 0xffffffffu) return;  // wave-uniform: no fused wave in the chunk
+  // Lanes past the last slot (M * 8 is a multiple of 4, not of 256) stay alive through the mixed
+  // path's readlane of `my` below: their loads are clamped to slot 0 and their atomics masked.
+  const bool act = slot < M * 8;
+  const uint32_t ls = act ? slot : 0u;
   const size_t row = (size_t)M * 8;
   if (!mixed) {
+    if (!act) return;
     // all WCH loads independent and unconditional (clamped to the last wave, masked by bit)
     unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
 #pragma unroll
@@ -1852,7 +1853,7 @@ __global__ __launch_bounds__(256) void k_agg_waves(uint32_t nwaves, uint32_t M,
   unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
   uint32_t cur = 0xffffffffu;
   auto flush = [&]() {
-    if (cur == 0xffffffffu) return;
+    if (cur == 0xffffffffu || !act) return;
     unsigned long long* o = agg64 + (size_t)cur * row + slot;
     if (a0) atomicAdd(o, a0);
     if (a1) atomicAdd(o + 1, a1);
@@ -1864,11 +1865,11 @@ __global__ __launch_bounds__(256) void k_agg_waves(uint32_t nwaves, uint32_t M,
     uint4 v[8];
 #pragma unroll
     for (uint32_t j = 0; j < 8; j++)
-      v[j] = *(const uint4*)(wpart + (size_t)min(w0 + b + j, w1 - 1) * row + slot);
+      v[j] = *(const uint4*)(wpart + (size_t)min(w0 + b + j, w1 - 1) * row + ls);
 #pragma unroll
     for (uint32_t j = 0; j < 8; j++) {
-      // v_readlane ignores EXEC: `my` was written with every lane active (lanes past the last
-      // slot have returned by now); ~0 = absent or unfused
+      // every lane of the wave is still active here (no early return above), so reading lane
+      // b + j of `my` is well defined; ~0 = absent or unfused
       const uint32_t sg = (uint32_t)__builtin_amdgcn_readlane((int)my, (int)(b + j));
       if (sg == 0xffffffffu) continue;
       if (sg != cur) {
@@ -2580,12 +2581,14 @@ static void count_launch(prio3_engine* e, const char* name) {
     }                                                                \
   } while (0)
 
-// folds this thread's finished timing events of engine e into e->times
-static void collect_times(prio3_engine* e) {
+// folds this thread's finished timing events of engine e into e->times.  wait = false (the
+// executor's group finish): events still pending -- those of the group issued ahead behind the
+// finishing one -- are left for a later call instead of blocking the launcher on them
+static void collect_times(prio3_engine* e, bool wait = true) {
   auto& v = pending();
   std::vector<Pending> keep;
   for (auto& pd : v) {
-    if (pd.e != e) {
+    if (pd.e != e || (!wait && hipEventQuery(pd.b) == hipErrorNotReady)) {
       keep.push_back(pd);
       continue;
     }
@@ -3503,7 +3506,7 @@ int engine_group_finish(GroupRun* gr, Run** run_out) {
     ws_stream_put(dev, gr->st);
     return PRIO3_EDEVICE;
   }
-  if (gr->lead->timing) collect_times(gr->lead);
+  if (gr->lead->timing) collect_times(gr->lead, false);
   gr->R->refs.store(gr->jobs);
   *run_out = gr->R;
   ws_stream_put(dev, gr->st);

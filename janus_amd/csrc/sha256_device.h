@@ -130,12 +130,14 @@ DEV void sha_final(uint32_t st[8], Msg32<NW>& m, int len, int prefix) {
 struct HmacKey {
   uint32_t ist[8], ost[8];
 };
-// HMAC key of 32 bytes (big-endian words): the ipad / opad midstates
-DEV void hmac_key32(HmacKey& k, const uint32_t key[8]) {
+// HMAC key of 4 NW bytes (NW <= 16 big-endian words): the ipad / opad midstates
+template <int NW>
+DEV void hmac_keyw(HmacKey& k, const uint32_t* key) {
+  static_assert(NW <= 16, "HMAC-SHA256 keys up to the 64-byte block");
   uint32_t bi[16], bo[16];
 #pragma unroll
   for (int i = 0; i < 16; i++) {
-    const uint32_t x = i < 8 ? key[i] : 0u;
+    const uint32_t x = i < NW ? key[i] : 0u;
     bi[i] = x ^ 0x36363636u;
     bo[i] = x ^ 0x5c5c5c5cu;
   }
@@ -144,6 +146,7 @@ DEV void hmac_key32(HmacKey& k, const uint32_t key[8]) {
   sha256d::compress(k.ist, bi);
   sha256d::compress(k.ost, bo);
 }
+DEV void hmac_key32(HmacKey& k, const uint32_t key[8]) { hmac_keyw<8>(k, key); }
 template <int NW>
 DEV void hmac(const HmacKey& k, Msg32<NW>& m, int len, uint32_t out[8]) {
   uint32_t st[8];

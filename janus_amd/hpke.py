@@ -16,7 +16,14 @@ from .prio3 import _np_ptr, _stream, _tptr, load_library
 
 KEM_X25519_HKDF_SHA256 = 0x0020
 KEM_P256_HKDF_SHA256 = 0x0010
+KEM_X448_HKDF_SHA512 = 0x0021
+KEM_P521_HKDF_SHA512 = 0x0012
 KDF_HKDF_SHA256 = 0x0001
+KDF_HKDF_SHA384 = 0x0002
+KDF_HKDF_SHA512 = 0x0003
+# Nenc (= Npk) per KEM (RFC 9180 7.1)
+NENC = {KEM_X25519_HKDF_SHA256: 32, KEM_P256_HKDF_SHA256: 65, KEM_X448_HKDF_SHA512: 56,
+        KEM_P521_HKDF_SHA512: 133}
 AEAD_AES_128_GCM = 0x0001
 AEAD_AES_256_GCM = 0x0002
 AEAD_CHACHA20_POLY1305 = 0x0003
@@ -44,6 +51,7 @@ def _lib():
         L.janus_hpke_set_timing.argtypes = [vp, C.c_int]
         L.janus_hpke_timing.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]
         L.janus_hpke_selftest_p256.argtypes = [C.c_int, u32, vp, vp, vp]
+        L.janus_hpke_selftest_field.argtypes = [C.c_int, C.c_int, u32, vp, vp, vp]
         _bound = True
     return L
 
@@ -57,7 +65,7 @@ class HpkeOpener:
                  device: int = 0, kem_id=KEM_X25519_HKDF_SHA256, kdf_id=KDF_HKDF_SHA256,
                  aead_id=AEAD_AES_128_GCM):
         self.device = device
-        self.nenc = 65 if kem_id == KEM_P256_HKDF_SHA256 else 32  # enc bytes per report
+        self.nenc = NENC.get(kem_id, 0)  # enc bytes per report
         self._keep = (bytes(private_key), bytes(public_key), bytes(info))
         h = C.c_void_p()
         rc = _lib().janus_hpke_opener_create(kem_id, kdf_id, aead_id, _b(private_key),

@@ -89,7 +89,7 @@ HPKE_EXPORTED_SYMBOLS = (
     "janus_hpke_opener_create", "janus_hpke_opener_destroy",
     "janus_hpke_open_input_shares_device", "janus_hpke_open_input_shares",
     "janus_hpke_open_device", "janus_hpke_open", "janus_hpke_set_timing", "janus_hpke_timing",
-    "janus_hpke_selftest_p256",
+    "janus_hpke_selftest_p256", "janus_hpke_selftest_field",
 )
 
 _lib = None
@@ -239,6 +239,20 @@ def _stream(stream, device):
     return C.c_void_p(torch.cuda.current_stream(device).cuda_stream or None)
 
 
+def _seg_accept(n, segment_ids, accept_mask, n_segments):
+    """The C ABI reads n segment ids and n accept bytes (janus_prio3.h): a shorter array would be
+    a host over-read inside the library, so the length contract is checked here."""
+    seg = None if segment_ids is None else np.ascontiguousarray(segment_ids, np.uint32)
+    acc = None if accept_mask is None else np.ascontiguousarray(accept_mask, np.uint8)
+    if seg is not None and seg.shape != (n,):
+        raise ValueError(f"segment_ids must have shape ({n},), got {seg.shape}")
+    if acc is not None and acc.shape != (n,):
+        raise ValueError(f"accept_mask must have shape ({n},), got {acc.shape}")
+    if n_segments < 1:
+        raise ValueError("n_segments must be >= 1")
+    return seg, acc
+
+
 class PreparedBatch:
     """Device-resident output shares of one ``prepare_batch`` call (prio3_batch*)."""
 
@@ -249,8 +263,7 @@ class PreparedBatch:
         sz = self.engine.sz
         agg = np.zeros((n_segments, sz.agg_share_len), np.uint8)
         cnt = np.zeros(n_segments, np.uint64)
-        seg = None if segment_ids is None else np.ascontiguousarray(segment_ids, np.uint32)
-        acc = None if accept_mask is None else np.ascontiguousarray(accept_mask, np.uint8)
+        seg, acc = _seg_accept(self.n, segment_ids, accept_mask, n_segments)
         rc = load_library().prio3_accumulate(self.handle, _np_ptr(seg), _np_ptr(acc), n_segments,
                                              _np_ptr(agg), _np_ptr(cnt))
         if rc:
@@ -378,8 +391,7 @@ class HelperEngine:
             pub = np.ascontiguousarray(public_shares, np.uint8)
             if pub.shape != (n, sz.public_share_len):
                 raise ValueError("public share shape does not match the VDAF instance")
-        seg = None if segment_ids is None else np.ascontiguousarray(segment_ids, np.uint32)
-        acc = None if accept_mask is None else np.ascontiguousarray(accept_mask, np.uint8)
+        seg, acc = _seg_accept(n, segment_ids, accept_mask, n_segments)
         msgs = np.zeros((n, max(sz.prep_msg_len, 1)), np.uint8)
         status = np.zeros(n, np.uint8)
         agg = np.zeros((n_segments, sz.agg_share_len), np.uint8)

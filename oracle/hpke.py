@@ -1,8 +1,8 @@
 """ctypes binding of oracle/hpke_oracle.c -- TEST INFRASTRUCTURE (checker + CPU baseline).
 
-HPKE base mode, DHKEM(X25519, HKDF-SHA256) / HKDF-SHA256 / AES-128-GCM, AES-256-GCM or
-ChaCha20Poly1305 (RFC 9180) composed over
-OpenSSL 3.0 primitives, plus Janus's helper input-share layer (aggregator.rs:1796-1990).
+HPKE base mode (RFC 9180) with KEM DHKEM(X25519 / P-256, HKDF-SHA256) or DHKEM(X448 / P-521,
+HKDF-SHA512), KDF HKDF-SHA256 / -SHA384 / -SHA512 and AEAD AES-128-GCM, AES-256-GCM or
+ChaCha20Poly1305, composed over OpenSSL 3.0 primitives, plus Janus's helper input-share layer (aggregator.rs:1796-1990).
 """
 from __future__ import annotations
 
@@ -53,6 +53,14 @@ def lib():
         _lib.hpke_seal_kem.argtypes = [u16] + _lib.hpke_seal_ex.argtypes
         _lib.hpke_open_input_shares_kem.argtypes = [u16] + _lib.hpke_open_input_shares_ex.argtypes
         _lib.hpke_make_input_shares_kem.argtypes = [u16] + _lib.hpke_make_input_shares_ex.argtypes
+        # and the suite forms (kem, kdf, aead): every KEM of KEMS, KDF 1 / 2 / 3
+        _lib.hpke_kem_public.argtypes = [u16, vp, vp]
+        _lib.hpke_open_suite.argtypes = [u16, u16, u16] + _lib.hpke_open.argtypes
+        _lib.hpke_seal_suite.argtypes = [u16, u16, u16] + _lib.hpke_seal.argtypes
+        _lib.hpke_open_input_shares_suite.argtypes = [u16, u16, u16] + \
+            _lib.hpke_open_input_shares.argtypes
+        _lib.hpke_make_input_shares_suite.argtypes = [u16, u16, u16] + \
+            _lib.hpke_make_input_shares.argtypes
     return _lib
 
 
@@ -64,49 +72,52 @@ def _p(b):
     return C.cast(C.c_char_p(bytes(b)), C.c_void_p)
 
 
-KEM_X25519, KEM_P256 = 0x20, 0x10
+KEM_X25519, KEM_P256, KEM_X448, KEM_P521 = 0x20, 0x10, 0x21, 0x12
+KDF_SHA256, KDF_SHA384, KDF_SHA512 = 1, 2, 3
+# RFC 9180 7.1: Nsk, Nenc (= Npk; the NIST curves' uncompressed points)
+NSK = {KEM_X25519: 32, KEM_P256: 32, KEM_X448: 56, KEM_P521: 66}
+NENC = {KEM_X25519: 32, KEM_P256: 65, KEM_X448: 56, KEM_P521: 133}
 
 
 def nenc(kem: int) -> int:
-    """Nenc = Npk: 32 (X25519) or 65 (P-256, uncompressed point)."""
-    return 65 if kem == KEM_P256 else 32
+    """Nenc = Npk of the KEM."""
+    return NENC[kem]
 
 
 def x25519_public(sk: bytes) -> bytes:
-    out = C.create_string_buffer(32)
-    assert lib().hpke_x25519_public(_p(sk), out) == 0
-    return out.raw
+    return kem_public(sk, KEM_X25519)
 
 
 def kem_public(sk: bytes, kem=KEM_X25519) -> bytes:
-    if kem == KEM_X25519:
-        return x25519_public(sk)
-    out = C.create_string_buffer(65)
-    assert lib().hpke_p256_public(_p(sk), out) == 0
+    out = C.create_string_buffer(NENC[kem])
+    assert lib().hpke_kem_public(kem, _p(sk), out) == 0
     return out.raw
 
 
 def kem_private(rng, kem=KEM_X25519) -> bytes:
-    """A random private key (P-256: below 2^255, hence below the group order)."""
-    sk = bytearray(rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+    """A random private key (P-256: below 2^255, P-521: below 2^520, hence below the order)."""
+    sk = bytearray(rng.integers(0, 256, NSK[kem], dtype=np.uint8).tobytes())
     if kem == KEM_P256:
         sk[0] &= 0x7F
+    if kem == KEM_P521:
+        sk[0] = 0
     return bytes(sk)
 
 
 def open_(skR: bytes, pkR: bytes, enc: bytes, info: bytes, aad: bytes, ct: bytes, aead=1,
-          kem=KEM_X25519):
+          kem=KEM_X25519, kdf=KDF_SHA256):
     pt = C.create_string_buffer(max(len(ct), 1))
-    n = lib().hpke_open_kem(kem, aead, _p(skR), _p(pkR), _p(enc), _p(info), len(info), _p(aad),
-                            len(aad), _p(ct), len(ct), pt)
+    n = lib().hpke_open_suite(kem, kdf, aead, _p(skR), _p(pkR), _p(enc), _p(info), len(info),
+                              _p(aad), len(aad), _p(ct), len(ct), pt)
     return None if n < 0 else pt.raw[:n]
 
 
-def seal(pkR: bytes, skE: bytes, info: bytes, aad: bytes, pt: bytes, aead=1, kem=KEM_X25519):
+def seal(pkR: bytes, skE: bytes, info: bytes, aad: bytes, pt: bytes, aead=1, kem=KEM_X25519,
+         kdf=KDF_SHA256):
     enc = C.create_string_buffer(nenc(kem))
     ct = C.create_string_buffer(len(pt) + 16)
-    assert lib().hpke_seal_kem(kem, aead, _p(pkR), _p(skE), _p(info), len(info), _p(aad),
-                               len(aad), _p(pt), len(pt), enc, ct) == 0
+    assert lib().hpke_seal_suite(kem, kdf, aead, _p(pkR), _p(skE), _p(info), len(info), _p(aad),
+                                 len(aad), _p(pt), len(pt), enc, ct) == 0
     return enc.raw, ct.raw
 
 
@@ -124,7 +135,7 @@ def plaintext_input_share(payload: bytes, extensions=()) -> bytes:
 
 
 def open_input_shares(skR, pkR, task_id, enc, ct, ct_len, report_ids, times, pubs, share_len,
-                      require_taskprov=False, n_threads=8, aead=1, kem=KEM_X25519):
+                      require_taskprov=False, n_threads=8, aead=1, kem=KEM_X25519, kdf=KDF_SHA256):
     """Batched helper input-share open: (shares [n, share_len], status [n] in {0, 4, 8})."""
     n = enc.shape[0]
     enc = np.ascontiguousarray(enc, np.uint8)
@@ -136,15 +147,15 @@ def open_input_shares(skR, pkR, task_id, enc, ct, ct_len, report_ids, times, pub
     pubs = None if pubs is None else np.ascontiguousarray(pubs, np.uint8)
     shares = np.zeros((n, share_len), np.uint8)
     status = np.zeros(n, np.uint8)
-    lib().hpke_open_input_shares_kem(kem, aead, _p(skR), _p(pkR), _p(task_id), n, _p(enc),
-                                     _p(ct), _p(ct_len), ct.shape[1], _p(ids), _p(times),
-                                     _p(pubs), publen, share_len, int(require_taskprov),
-                                     _p(shares), _p(status), n_threads)
+    lib().hpke_open_input_shares_suite(kem, kdf, aead, _p(skR), _p(pkR), _p(task_id), n, _p(enc),
+                                       _p(ct), _p(ct_len), ct.shape[1], _p(ids), _p(times),
+                                       _p(pubs), publen, share_len, int(require_taskprov),
+                                       _p(shares), _p(status), n_threads)
     return shares, status
 
 
 def make_batch(n, share_len, pub_len, seed=1, skR=None, extensions=(), tamper=0.0, aead=1,
-               kem=KEM_X25519):
+               kem=KEM_X25519, kdf=KDF_SHA256):
     """Synthetic Janus-shaped encrypted helper input shares (test/bench data), sealed by the
     oracle with deterministic ephemeral keys.  Returns a dict of numpy arrays."""
     rng = np.random.default_rng(seed)
@@ -165,7 +176,8 @@ def make_batch(n, share_len, pub_len, seed=1, skR=None, extensions=(), tamper=0.
                               b"" if pubs is None else pubs[r].tobytes())
         skE = kem_private(rng, kem)
         e, c = seal(pkR, skE, INFO_INPUT_SHARE_HELPER, aad,
-                    plaintext_input_share(shares[r].tobytes(), extensions), aead=aead, kem=kem)
+                    plaintext_input_share(shares[r].tobytes(), extensions), aead=aead, kem=kem,
+                    kdf=kdf)
         enc[r] = np.frombuffer(e, np.uint8)
         ct[r] = np.frombuffer(c, np.uint8)
     return dict(skR=skR, pkR=pkR, task_id=task_id, report_ids=ids, times=times, pubs=pubs,
@@ -173,7 +185,7 @@ def make_batch(n, share_len, pub_len, seed=1, skR=None, extensions=(), tamper=0.
 
 
 def make_batch_fast(n, share_len, pub_len, seed=1, taskprov=False, n_threads=8, skR=None, aead=1,
-                    kem=KEM_X25519):
+                    kem=KEM_X25519, kdf=KDF_SHA256):
     """make_batch in C with threads (bench-size batches); every report distinct."""
     rng = np.random.default_rng(seed)
     skR = kem_private(rng, kem) if skR is None else skR
@@ -187,10 +199,10 @@ def make_batch_fast(n, share_len, pub_len, seed=1, taskprov=False, n_threads=8, 
     times = np.zeros(n, np.uint64)
     pubs = np.zeros((n, pub_len), np.uint8) if pub_len else None
     shares = np.zeros((n, share_len), np.uint8)
-    rc = lib().hpke_make_input_shares_kem(kem, aead, _p(pkR), _p(task_id), n, seed, share_len,
-                                          pub_len, int(taskprov), stride, _p(enc), _p(ct),
-                                          _p(ct_len), _p(ids), _p(times), _p(pubs), _p(shares),
-                                          n_threads)
+    rc = lib().hpke_make_input_shares_suite(kem, kdf, aead, _p(pkR), _p(task_id), n, seed,
+                                            share_len, pub_len, int(taskprov), stride, _p(enc),
+                                            _p(ct), _p(ct_len), _p(ids), _p(times), _p(pubs),
+                                            _p(shares), n_threads)
     assert rc == 0
     return dict(skR=skR, pkR=pkR, task_id=task_id, report_ids=ids, times=times, pubs=pubs,
                 shares=shares, enc=enc, ct=ct, ct_len=ct_len)

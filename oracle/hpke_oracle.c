@@ -3,8 +3,10 @@
  * TEST INFRASTRUCTURE ONLY: the checker for tests/ and bench.py's cpu_baseline leg.
  *
  * HPKE base mode (RFC 9180 §5.1, §5.2) with DHKEM(X25519, HKDF-SHA256) (§4.1, §7.1),
- * HKDF-SHA256 and AES-128-GCM -- the suite Janus generates by default -- or AES-256-GCM /
- * ChaCha20Poly1305 (pinned by the RFC 9180 vectors for kem 0x20 / kdf 1 / aead 2 and 3)
+ * HKDF-SHA256 and AES-128-GCM -- the suite Janus generates by default -- or any other suite of
+ * KEM {X25519, P-256, X448, P-521} x KDF {HKDF-SHA256, -SHA384, -SHA512} x AEAD {AES-128-GCM,
+ * AES-256-GCM, ChaCha20Poly1305} (pinned by the 24 RFC 9180 base-mode vectors of
+ * core/src/test-vectors.json; the HKDF-SHA384 suites have none there and rest on OpenSSL)
  * (/root/reference/core/src/hpke.rs:260-280, generate_test_hpke_config_and_private_key), whose
  * Rust implementation (hpke-dispatch -> hpke crate) is not in /root/reference.  The RFC 9180
  * composition (labels, suite ids, key schedule) is restated here over OpenSSL 3.0 primitives
@@ -32,47 +34,67 @@
 
 enum { HPKE_OK = 0, HPKE_DECRYPT_ERROR = 4, HPKE_INVALID_MESSAGE = 8 };
 
-/* KEM 0x0020 DHKEM(X25519, HKDF-SHA256) (Nenc = Npk = 32) or 0x0010 DHKEM(P-256, HKDF-SHA256)
- * (Nenc = Npk = 65, uncompressed points) */
+/* KEMs (RFC 9180 7.1): 0x0020 DHKEM(X25519, HKDF-SHA256), 0x0010 DHKEM(P-256, HKDF-SHA256),
+ * 0x0021 DHKEM(X448, HKDF-SHA512), 0x0012 DHKEM(P-521, HKDF-SHA512) (messages/src/lib.rs:770-784);
+ * Nsk, Nenc (= Npk, the NIST curves' uncompressed points), Ndh, and the KEM's own KDF. */
+typedef struct {
+  uint16_t id;
+  size_t nsk, nenc, ndh;
+  int kdf; /* 1 HKDF-SHA256, 3 HKDF-SHA512 */
+} Kem;
+static const Kem KEMS[] = {{0x20, 32, 32, 32, 1}, {0x10, 32, 65, 32, 1},
+                           {0x21, 56, 56, 56, 3}, {0x12, 66, 133, 66, 3}};
+static const Kem* kem_of(uint16_t kem) {
+  for (size_t i = 0; i < sizeof(KEMS) / sizeof(KEMS[0]); i++)
+    if (KEMS[i].id == kem) return &KEMS[i];
+  return NULL;
+}
+static size_t kem_nenc(uint16_t kem) { return kem_of(kem) ? kem_of(kem)->nenc : 0; }
+/* KDFs (RFC 9180 7.2, lib.rs:809-815): 1 HKDF-SHA256, 2 HKDF-SHA384, 3 HKDF-SHA512 */
+static const EVP_MD* kdf_md(int kdf) {
+  return kdf == 1 ? EVP_sha256() : kdf == 2 ? EVP_sha384() : kdf == 3 ? EVP_sha512() : NULL;
+}
+static size_t kdf_nh(int kdf) { return kdf == 1 ? 32 : kdf == 2 ? 48 : 64; }
+
 static void kem_suite(uint16_t kem, uint8_t s[5]) {
   s[0] = 'K', s[1] = 'E', s[2] = 'M', s[3] = (uint8_t)(kem >> 8), s[4] = (uint8_t)kem;
 }
-static size_t kem_nenc(uint16_t kem) { return kem == 0x10 ? 65 : 32; }
 /* suite_id = "HPKE" || kem || kdf || aead (RFC 9180 5.1); aead 1 AES-128-GCM, 2 AES-256-GCM,
  * 3 ChaCha20Poly1305 (messages/src/lib.rs:844-853) */
-static void hpke_suite(uint16_t kem, uint16_t aead, uint8_t s[10]) {
+static void hpke_suite(uint16_t kem, uint16_t kdf, uint16_t aead, uint8_t s[10]) {
   s[0] = 'H', s[1] = 'P', s[2] = 'K', s[3] = 'E';
-  s[4] = (uint8_t)(kem >> 8), s[5] = (uint8_t)kem, s[6] = 0x00, s[7] = 0x01;
+  s[4] = (uint8_t)(kem >> 8), s[5] = (uint8_t)kem, s[6] = (uint8_t)(kdf >> 8), s[7] = (uint8_t)kdf;
   s[8] = (uint8_t)(aead >> 8);
   s[9] = (uint8_t)aead;
 }
 static size_t aead_nk(uint16_t aead) { return aead == 1 ? 16 : 32; }
 
-static void hmac256(const uint8_t* key, size_t klen, const uint8_t* msg, size_t mlen,
-                    uint8_t out[32]) {
-  unsigned int ol = 32;
+static void hmac_md(int kdf, const uint8_t* key, size_t klen, const uint8_t* msg, size_t mlen,
+                    uint8_t* out) {
+  unsigned int ol = 64;
   static const uint8_t zero = 0;
-  HMAC(EVP_sha256(), klen ? key : &zero, (int)klen, msg, mlen, out, &ol);
+  HMAC(kdf_md(kdf), klen ? key : &zero, (int)klen, msg, mlen, out, &ol);
 }
 
 /* LabeledExtract(salt, label, ikm) = HKDF-Extract(salt, "HPKE-v1" || suite_id || label || ikm) */
-static void labeled_extract(const uint8_t* suite, size_t slen, const uint8_t* salt, size_t saltlen,
-                            const char* label, const uint8_t* ikm, size_t ikmlen, uint8_t out[32]) {
-  uint8_t buf[256];
+static void labeled_extract(int kdf, const uint8_t* suite, size_t slen, const uint8_t* salt,
+                            size_t saltlen, const char* label, const uint8_t* ikm, size_t ikmlen,
+                            uint8_t* out) {
+  uint8_t buf[512];
   size_t l = 0, ll = strlen(label);
   memcpy(buf + l, "HPKE-v1", 7), l += 7;
   memcpy(buf + l, suite, slen), l += slen;
   memcpy(buf + l, label, ll), l += ll;
   memcpy(buf + l, ikm, ikmlen), l += ikmlen;
-  hmac256(salt, saltlen, buf, l, out);
+  hmac_md(kdf, salt, saltlen, buf, l, out);
 }
 
-/* LabeledExpand(prk, label, info, L <= 32) = HKDF-Expand(prk, I2OSP(L, 2) || "HPKE-v1" ||
+/* LabeledExpand(prk, label, info, L <= Nh) = HKDF-Expand(prk, I2OSP(L, 2) || "HPKE-v1" ||
  * suite_id || label || info, L): one HMAC block T(1) = HMAC(prk, labeled_info || 0x01) */
-static void labeled_expand(const uint8_t* suite, size_t slen, const uint8_t prk[32],
+static void labeled_expand(int kdf, const uint8_t* suite, size_t slen, const uint8_t* prk,
                            const char* label, const uint8_t* info, size_t infolen, size_t L,
                            uint8_t* out) {
-  uint8_t buf[256], t[32];
+  uint8_t buf[512], t[64];
   size_t l = 0, ll = strlen(label);
   buf[l++] = (uint8_t)(L >> 8);
   buf[l++] = (uint8_t)L;
@@ -81,93 +103,114 @@ static void labeled_expand(const uint8_t* suite, size_t slen, const uint8_t prk[
   memcpy(buf + l, label, ll), l += ll;
   memcpy(buf + l, info, infolen), l += infolen;
   buf[l++] = 0x01;
-  hmac256(prk, 32, buf, l, t);
+  hmac_md(kdf, prk, kdf_nh(kdf), buf, l, t);
   memcpy(out, t, L);
 }
 
-static int x25519(const uint8_t sk[32], const uint8_t pk[32], uint8_t out[32]) {
-  EVP_PKEY* k = EVP_PKEY_new_raw_private_key(EVP_PKEY_X25519, NULL, sk, 32);
-  EVP_PKEY* p = EVP_PKEY_new_raw_public_key(EVP_PKEY_X25519, NULL, pk, 32);
+/* X25519 / X448 (RFC 7748) through OpenSSL's raw keys */
+static int xdh(int type, size_t len, const uint8_t* sk, const uint8_t* pk, uint8_t* out) {
+  EVP_PKEY* k = EVP_PKEY_new_raw_private_key(type, NULL, sk, len);
+  EVP_PKEY* p = EVP_PKEY_new_raw_public_key(type, NULL, pk, len);
   EVP_PKEY_CTX* c = k ? EVP_PKEY_CTX_new(k, NULL) : NULL;
-  size_t ol = 32;
+  size_t ol = len;
   int ok = c && p && EVP_PKEY_derive_init(c) == 1 && EVP_PKEY_derive_set_peer(c, p) == 1 &&
-           EVP_PKEY_derive(c, out, &ol) == 1 && ol == 32;
+           EVP_PKEY_derive(c, out, &ol) == 1 && ol == len;
   EVP_PKEY_CTX_free(c);
   EVP_PKEY_free(k);
   EVP_PKEY_free(p);
   return ok ? 0 : -1;
 }
-
-/* P-256 ECDH (SEC 1): the x-coordinate of sk * pk, pk an uncompressed point (validated) */
-static int p256_dh(const uint8_t sk[32], const uint8_t pk[65], uint8_t out[32]) {
-  EC_KEY* k = EC_KEY_new_by_curve_name(NID_X9_62_prime256v1);
-  const EC_GROUP* g = k ? EC_KEY_get0_group(k) : NULL;
-  BIGNUM* d = BN_bin2bn(sk, 32, NULL);
-  EC_POINT* q = g ? EC_POINT_new(g) : NULL;
-  int ok = k && d && q && EC_KEY_set_private_key(k, d) == 1 &&
-           EC_POINT_oct2point(g, q, pk, 65, NULL) == 1 && EC_POINT_is_on_curve(g, q, NULL) == 1 &&
-           ECDH_compute_key(out, 32, q, k, NULL) == 32;
-  EC_POINT_free(q);
-  BN_free(d);
-  EC_KEY_free(k);
-  return ok ? 0 : -1;
-}
-
-int hpke_p256_public(const uint8_t sk[32], uint8_t pk[65]) {
-  EC_KEY* k = EC_KEY_new_by_curve_name(NID_X9_62_prime256v1);
-  const EC_GROUP* g = k ? EC_KEY_get0_group(k) : NULL;
-  BIGNUM* d = BN_bin2bn(sk, 32, NULL);
-  EC_POINT* q = g ? EC_POINT_new(g) : NULL;
-  int ok = k && d && q && EC_POINT_mul(g, q, d, NULL, NULL, NULL) == 1 &&
-           EC_POINT_point2oct(g, q, POINT_CONVERSION_UNCOMPRESSED, pk, 65, NULL) == 65;
-  EC_POINT_free(q);
-  BN_free(d);
-  EC_KEY_free(k);
-  return ok ? 0 : -1;
-}
-
-static int kem_dh(uint16_t kem, const uint8_t sk[32], const uint8_t* pk, uint8_t out[32]) {
-  return kem == 0x10 ? p256_dh(sk, pk, out) : x25519(sk, pk, out);
-}
-static int kem_public(uint16_t kem, const uint8_t sk[32], uint8_t* pk);
-
-int hpke_x25519_public(const uint8_t sk[32], uint8_t pk[32]) {
-  EVP_PKEY* k = EVP_PKEY_new_raw_private_key(EVP_PKEY_X25519, NULL, sk, 32);
-  size_t ol = 32;
-  int ok = k && EVP_PKEY_get_raw_public_key(k, pk, &ol) == 1 && ol == 32;
+static int xdh_public(int type, size_t len, const uint8_t* sk, uint8_t* pk) {
+  EVP_PKEY* k = EVP_PKEY_new_raw_private_key(type, NULL, sk, len);
+  size_t ol = len;
+  int ok = k && EVP_PKEY_get_raw_public_key(k, pk, &ol) == 1 && ol == len;
   EVP_PKEY_free(k);
   return ok ? 0 : -1;
 }
-static int kem_public(uint16_t kem, const uint8_t sk[32], uint8_t* pk) {
-  return kem == 0x10 ? hpke_p256_public(sk, pk) : hpke_x25519_public(sk, pk);
+
+/* NIST-curve ECDH (SEC 1): the x-coordinate of sk * pk, pk an uncompressed point (validated) */
+static int ec_dh(int nid, size_t n, const uint8_t* sk, const uint8_t* pk, uint8_t* out) {
+  EC_KEY* k = EC_KEY_new_by_curve_name(nid);
+  const EC_GROUP* g = k ? EC_KEY_get0_group(k) : NULL;
+  BIGNUM* d = BN_bin2bn(sk, (int)n, NULL);
+  EC_POINT* q = g ? EC_POINT_new(g) : NULL;
+  int ok = k && d && q && EC_KEY_set_private_key(k, d) == 1 &&
+           EC_POINT_oct2point(g, q, pk, 2 * n + 1, NULL) == 1 &&
+           EC_POINT_is_on_curve(g, q, NULL) == 1 && ECDH_compute_key(out, n, q, k, NULL) == (int)n;
+  EC_POINT_free(q);
+  BN_free(d);
+  EC_KEY_free(k);
+  return ok ? 0 : -1;
+}
+static int ec_public(int nid, size_t n, const uint8_t* sk, uint8_t* pk) {
+  EC_KEY* k = EC_KEY_new_by_curve_name(nid);
+  const EC_GROUP* g = k ? EC_KEY_get0_group(k) : NULL;
+  BIGNUM* d = BN_bin2bn(sk, (int)n, NULL);
+  EC_POINT* q = g ? EC_POINT_new(g) : NULL;
+  int ok = k && d && q && EC_POINT_mul(g, q, d, NULL, NULL, NULL) == 1 &&
+           EC_POINT_point2oct(g, q, POINT_CONVERSION_UNCOMPRESSED, pk, 2 * n + 1, NULL) == 2 * n + 1;
+  EC_POINT_free(q);
+  BN_free(d);
+  EC_KEY_free(k);
+  return ok ? 0 : -1;
 }
 
+static int kem_dh(uint16_t kem, const uint8_t* sk, const uint8_t* pk, uint8_t* out) {
+  switch (kem) {
+    case 0x20: return xdh(EVP_PKEY_X25519, 32, sk, pk, out);
+    case 0x21: return xdh(EVP_PKEY_X448, 56, sk, pk, out);
+    case 0x10: return ec_dh(NID_X9_62_prime256v1, 32, sk, pk, out);
+    case 0x12: return ec_dh(NID_secp521r1, 66, sk, pk, out);
+  }
+  return -1;
+}
+/* SerializePublicKey(DerivePublicKey(sk)) for any of the KEMs */
+int hpke_kem_public(uint16_t kem, const uint8_t* sk, uint8_t* pk) {
+  switch (kem) {
+    case 0x20: return xdh_public(EVP_PKEY_X25519, 32, sk, pk);
+    case 0x21: return xdh_public(EVP_PKEY_X448, 56, sk, pk);
+    case 0x10: return ec_public(NID_X9_62_prime256v1, 32, sk, pk);
+    case 0x12: return ec_public(NID_secp521r1, 66, sk, pk);
+  }
+  return -1;
+}
+int hpke_p256_public(const uint8_t sk[32], uint8_t pk[65]) { return hpke_kem_public(0x10, sk, pk); }
+int hpke_x25519_public(const uint8_t sk[32], uint8_t pk[32]) { return hpke_kem_public(0x20, sk, pk); }
+
 /* KeySchedule(mode_base, shared_secret, info) -> key (Nk), base_nonce (12)  [RFC 9180 §5.1] */
-static void key_schedule(uint16_t kem, uint16_t aead, const uint8_t ss[32], const uint8_t* info,
-                         size_t infolen, uint8_t key[32], uint8_t nonce[12]) {
-  uint8_t ksc[65], secret[32], su[10];
-  hpke_suite(kem, aead, su);
-  ksc[0] = 0x00;  /* mode_base */
-  labeled_extract(su, 10, NULL, 0, "psk_id_hash", NULL, 0, ksc + 1);
-  labeled_extract(su, 10, NULL, 0, "info_hash", info, infolen, ksc + 33);
-  labeled_extract(su, 10, ss, 32, "secret", NULL, 0, secret);
-  labeled_expand(su, 10, secret, "key", ksc, 65, aead_nk(aead), key);
-  labeled_expand(su, 10, secret, "base_nonce", ksc, 65, 12, nonce);
+static void key_schedule(uint16_t kem, int kdf, uint16_t aead, const uint8_t* ss, size_t nss,
+                         const uint8_t* info, size_t infolen, uint8_t key[32], uint8_t nonce[12]) {
+  uint8_t ksc[129], secret[64], su[10];
+  const size_t nh = kdf_nh(kdf);
+  hpke_suite(kem, (uint16_t)kdf, aead, su);
+  ksc[0] = 0x00; /* mode_base */
+  labeled_extract(kdf, su, 10, NULL, 0, "psk_id_hash", NULL, 0, ksc + 1);
+  labeled_extract(kdf, su, 10, NULL, 0, "info_hash", info, infolen, ksc + 1 + nh);
+  labeled_extract(kdf, su, 10, ss, nss, "secret", NULL, 0, secret);
+  labeled_expand(kdf, su, 10, secret, "key", ksc, 1 + 2 * nh, aead_nk(aead), key);
+  labeled_expand(kdf, su, 10, secret, "base_nonce", ksc, 1 + 2 * nh, 12, nonce);
+}
+
+/* ExtractAndExpand(dh, enc || pkRm) with the KEM's KDF -> shared_secret (Nsecret = its Nh) */
+static void extract_and_expand(const Kem* K, const uint8_t* dh, const uint8_t* enc,
+                               const uint8_t* pkR, uint8_t* ss) {
+  uint8_t prk[64], kc[266], ks[5];
+  kem_suite(K->id, ks);
+  labeled_extract(K->kdf, ks, 5, NULL, 0, "eae_prk", dh, K->ndh, prk);
+  memcpy(kc, enc, K->nenc);
+  memcpy(kc + K->nenc, pkR, K->nenc);
+  labeled_expand(K->kdf, ks, 5, prk, "shared_secret", kc, 2 * K->nenc, kdf_nh(K->kdf), ss);
 }
 
 /* Decap (§4.1): dh = DH(skR, enc); shared_secret = ExtractAndExpand(dh, enc || pkRm) */
-static int decap(uint16_t kem, const uint8_t* enc, const uint8_t skR[32], const uint8_t* pkR,
-                 uint8_t ss[32]) {
-  uint8_t dh[32], prk[32], kc[130], ks[5];
-  const size_t ne = kem_nenc(kem);
-  if (kem_dh(kem, skR, enc, dh)) return -1;
-  static const uint8_t zero32[32];
-  if (kem != 0x10 && !memcmp(dh, zero32, 32)) return -1; /* X25519 all-zero: ValidationError */
-  kem_suite(kem, ks);
-  labeled_extract(ks, 5, NULL, 0, "eae_prk", dh, 32, prk);
-  memcpy(kc, enc, ne);
-  memcpy(kc + ne, pkR, ne);
-  labeled_expand(ks, 5, prk, "shared_secret", kc, 2 * ne, 32, ss);
+static int decap(const Kem* K, const uint8_t* enc, const uint8_t* skR, const uint8_t* pkR,
+                 uint8_t* ss) {
+  uint8_t dh[66];
+  static const uint8_t zero[66];
+  if (kem_dh(K->id, skR, enc, dh)) return -1;
+  /* X25519 / X448 all-zero output: ValidationError */
+  if ((K->id == 0x20 || K->id == 0x21) && !memcmp(dh, zero, K->ndh)) return -1;
+  extract_and_expand(K, dh, enc, pkR, ss);
   return 0;
 }
 
@@ -196,16 +239,23 @@ static int aead_crypt(uint16_t aead, int decrypt, const uint8_t* key, const uint
   return ok ? 0 : -1;
 }
 
-/* base-mode single-shot open (sequence number 0); returns the plaintext length or -1 */
-int hpke_open_kem(uint16_t kem, uint16_t aead, const uint8_t skR[32], const uint8_t* pkR,
-                  const uint8_t* enc, const uint8_t* info, size_t infolen, const uint8_t* aad,
-                  size_t aadlen, const uint8_t* ct, size_t ctlen, uint8_t* pt) {
-  uint8_t ss[32], key[32], nonce[12], tag[16];
-  if (ctlen < 16 || decap(kem, enc, skR, pkR, ss)) return -1;
-  key_schedule(kem, aead, ss, info, infolen, key, nonce);
+/* base-mode single-shot open (sequence number 0) of any suite; the plaintext length or -1 */
+int hpke_open_suite(uint16_t kem, uint16_t kdf, uint16_t aead, const uint8_t* skR,
+                    const uint8_t* pkR, const uint8_t* enc, const uint8_t* info, size_t infolen,
+                    const uint8_t* aad, size_t aadlen, const uint8_t* ct, size_t ctlen,
+                    uint8_t* pt) {
+  uint8_t ss[64], key[32], nonce[12], tag[16];
+  const Kem* K = kem_of(kem);
+  if (!K || !kdf_md(kdf) || ctlen < 16 || decap(K, enc, skR, pkR, ss)) return -1;
+  key_schedule(kem, kdf, aead, ss, kdf_nh(K->kdf), info, infolen, key, nonce);
   memcpy(tag, ct + ctlen - 16, 16);
   if (aead_crypt(aead, 1, key, nonce, aad, aadlen, ct, ctlen - 16, pt, tag)) return -1;
   return (int)(ctlen - 16);
+}
+int hpke_open_kem(uint16_t kem, uint16_t aead, const uint8_t skR[32], const uint8_t* pkR,
+                  const uint8_t* enc, const uint8_t* info, size_t infolen, const uint8_t* aad,
+                  size_t aadlen, const uint8_t* ct, size_t ctlen, uint8_t* pt) {
+  return hpke_open_suite(kem, 1, aead, skR, pkR, enc, info, infolen, aad, aadlen, ct, ctlen, pt);
 }
 int hpke_open_ex(uint16_t aead, const uint8_t skR[32], const uint8_t pkR[32],
                  const uint8_t enc[32], const uint8_t* info, size_t infolen, const uint8_t* aad,
@@ -219,20 +269,21 @@ int hpke_open(const uint8_t skR[32], const uint8_t pkR[32], const uint8_t enc[32
 }
 
 /* base-mode seal with the ephemeral key skE (Encap with a given ephemeral key, as the RFC 9180
- * test vectors do); writes enc[32] and ct[ptlen + 16] */
+ * test vectors do); writes enc[Nenc] and ct[ptlen + 16] */
+int hpke_seal_suite(uint16_t kem, uint16_t kdf, uint16_t aead, const uint8_t* pkR,
+                    const uint8_t* skE, const uint8_t* info, size_t infolen, const uint8_t* aad,
+                    size_t aadlen, const uint8_t* pt, size_t ptlen, uint8_t* enc, uint8_t* ct) {
+  uint8_t dh[66], ss[64], key[32], nonce[12];
+  const Kem* K = kem_of(kem);
+  if (!K || !kdf_md(kdf) || hpke_kem_public(kem, skE, enc) || kem_dh(kem, skE, pkR, dh)) return -1;
+  extract_and_expand(K, dh, enc, pkR, ss);
+  key_schedule(kem, kdf, aead, ss, kdf_nh(K->kdf), info, infolen, key, nonce);
+  return aead_crypt(aead, 0, key, nonce, aad, aadlen, pt, ptlen, ct, ct + ptlen);
+}
 int hpke_seal_kem(uint16_t kem, uint16_t aead, const uint8_t* pkR, const uint8_t skE[32],
                   const uint8_t* info, size_t infolen, const uint8_t* aad, size_t aadlen,
                   const uint8_t* pt, size_t ptlen, uint8_t* enc, uint8_t* ct) {
-  uint8_t dh[32], prk[32], kc[130], ss[32], key[32], nonce[12], ks[5];
-  const size_t ne = kem_nenc(kem);
-  if (kem_public(kem, skE, enc) || kem_dh(kem, skE, pkR, dh)) return -1;
-  kem_suite(kem, ks);
-  labeled_extract(ks, 5, NULL, 0, "eae_prk", dh, 32, prk);
-  memcpy(kc, enc, ne);
-  memcpy(kc + ne, pkR, ne);
-  labeled_expand(ks, 5, prk, "shared_secret", kc, 2 * ne, 32, ss);
-  key_schedule(kem, aead, ss, info, infolen, key, nonce);
-  return aead_crypt(aead, 0, key, nonce, aad, aadlen, pt, ptlen, ct, ct + ptlen);
+  return hpke_seal_suite(kem, 1, aead, pkR, skE, info, infolen, aad, aadlen, pt, ptlen, enc, ct);
 }
 int hpke_seal_ex(uint16_t aead, const uint8_t pkR[32], const uint8_t skE[32],
                  const uint8_t* info, size_t infolen, const uint8_t* aad, size_t aadlen,
@@ -305,7 +356,7 @@ typedef struct {
   int require_taskprov;
   uint8_t *shares, *status;
   uint32_t lo, hi;
-  uint16_t aead, kem;
+  uint16_t aead, kem, kdf;
 } Job;
 
 static const uint8_t INFO[20] = {'d', 'a', 'p', '-', '0', '9', ' ', 'i', 'n', 'p',
@@ -320,9 +371,9 @@ static void* run(void* arg) {
                                      aad);
     uint32_t cl = j->ct_len[r];
     int ptl = cl <= sizeof(pt) + 16
-                  ? hpke_open_kem(j->kem, j->aead, j->skR, j->pkR,
-                                  j->enc + kem_nenc(j->kem) * (size_t)r, INFO, sizeof(INFO), aad,
-                                  al, j->ct + (size_t)j->ct_stride * r, cl, pt)
+                  ? hpke_open_suite(j->kem, j->kdf, j->aead, j->skR, j->pkR,
+                                    j->enc + kem_nenc(j->kem) * (size_t)r, INFO, sizeof(INFO), aad,
+                                    al, j->ct + (size_t)j->ct_stride * r, cl, pt)
                   : -1;
     uint8_t* so = j->shares + (size_t)j->share_len * r;
     memset(so, 0, j->share_len);
@@ -336,6 +387,34 @@ static void* run(void* arg) {
 
 /* Batched helper input-share open: status[r] = 0 (helper share written), 4 (HpkeDecryptError)
  * or 8 (InvalidMessage), the PrepareError codes of messages/src/lib.rs. */
+int hpke_open_input_shares_suite(uint16_t kem, uint16_t kdf, uint16_t aead, const uint8_t* skR,
+                                 const uint8_t* pkR, const uint8_t task_id[32], uint32_t n,
+                                 const uint8_t* enc, const uint8_t* ct, const uint32_t* ct_len,
+                                 uint32_t ct_stride, const uint8_t* report_ids,
+                                 const uint64_t* times, const uint8_t* pubs, uint32_t publen,
+                                 uint32_t share_len, int require_taskprov, uint8_t* shares,
+                                 uint8_t* status, int n_threads);
+int hpke_open_input_shares_suite(uint16_t kem, uint16_t kdf, uint16_t aead, const uint8_t* skR,
+                                 const uint8_t* pkR, const uint8_t task_id[32], uint32_t n,
+                                 const uint8_t* enc, const uint8_t* ct, const uint32_t* ct_len,
+                                 uint32_t ct_stride, const uint8_t* report_ids,
+                                 const uint64_t* times, const uint8_t* pubs, uint32_t publen,
+                                 uint32_t share_len, int require_taskprov, uint8_t* shares,
+                                 uint8_t* status, int n_threads) {
+  if (n_threads < 1) n_threads = 1;
+  pthread_t th[256];
+  Job jobs[256];
+  if (n_threads > 256) n_threads = 256;
+  for (int t = 0; t < n_threads; t++) {
+    jobs[t] = (Job){skR, pkR, task_id, enc, ct, report_ids, pubs, ct_len, times, n, ct_stride,
+                    publen, share_len, require_taskprov, shares, status,
+                    (uint32_t)((uint64_t)n * t / n_threads),
+                    (uint32_t)((uint64_t)n * (t + 1) / n_threads), aead, kem, kdf};
+    pthread_create(&th[t], NULL, run, &jobs[t]);
+  }
+  for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+  return 0;
+}
 int hpke_open_input_shares_kem(uint16_t kem, uint16_t aead, const uint8_t skR[32],
                                const uint8_t* pkR, const uint8_t task_id[32], uint32_t n,
                                const uint8_t* enc, const uint8_t* ct, const uint32_t* ct_len,
@@ -350,19 +429,9 @@ int hpke_open_input_shares_kem(uint16_t kem, uint16_t aead, const uint8_t skR[32
                                const uint64_t* times, const uint8_t* pubs, uint32_t publen,
                                uint32_t share_len, int require_taskprov, uint8_t* shares,
                                uint8_t* status, int n_threads) {
-  if (n_threads < 1) n_threads = 1;
-  pthread_t th[256];
-  Job jobs[256];
-  if (n_threads > 256) n_threads = 256;
-  for (int t = 0; t < n_threads; t++) {
-    jobs[t] = (Job){skR, pkR, task_id, enc, ct, report_ids, pubs, ct_len, times, n, ct_stride,
-                    publen, share_len, require_taskprov, shares, status,
-                    (uint32_t)((uint64_t)n * t / n_threads),
-                    (uint32_t)((uint64_t)n * (t + 1) / n_threads), aead, kem};
-    pthread_create(&th[t], NULL, run, &jobs[t]);
-  }
-  for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
-  return 0;
+  return hpke_open_input_shares_suite(kem, 1, aead, skR, pkR, task_id, n, enc, ct, ct_len,
+                                      ct_stride, report_ids, times, pubs, publen, share_len,
+                                      require_taskprov, shares, status, n_threads);
 }
 int hpke_open_input_shares_ex(uint16_t aead, const uint8_t skR[32], const uint8_t pkR[32],
                               const uint8_t task_id[32], uint32_t n, const uint8_t* enc,
@@ -397,7 +466,7 @@ typedef struct {
   uint8_t *enc, *ct, *ids, *pubs, *shares;
   uint32_t* ct_len;
   uint64_t* times;
-  uint16_t aead, kem;
+  uint16_t aead, kem, kdf;
 } GenJob;
 
 static void prf(uint64_t seed, uint32_t r, uint8_t purpose, uint8_t* out, size_t len) {
@@ -414,7 +483,8 @@ static void prf(uint64_t seed, uint32_t r, uint8_t purpose, uint8_t* out, size_t
 
 static void* gen_run(void* arg) {
   GenJob* j = (GenJob*)arg;
-  uint8_t pt[4096], aad[256], skE[32];
+  uint8_t pt[4096], aad[256], skE[66];
+  const Kem* K = kem_of(j->kem);
   for (uint32_t r = j->lo; r < j->hi; r++) {
     uint8_t* id = j->ids + 16 * (size_t)r;
     uint8_t* share = j->shares + (size_t)j->share_len * r;
@@ -422,7 +492,7 @@ static void* gen_run(void* arg) {
     prf(j->seed, r, 1, id, 16);
     prf(j->seed, r, 2, share, j->share_len);
     if (pub) prf(j->seed, r, 3, pub, j->publen);
-    prf(j->seed, r, 4, skE, 32);
+    prf(j->seed, r, 4, skE, K->nsk);
     uint8_t t8[8];
     prf(j->seed, r, 5, t8, 8);
     j->times[r] = 1700000000ull + (t8[0] | (uint32_t)t8[1] << 8) % 3600u;
@@ -440,19 +510,21 @@ static void* gen_run(void* arg) {
     uint8_t* ct = j->ct + (size_t)j->stride * r;
     memset(ct, 0, j->stride);
     if (j->kem == 0x10) skE[0] &= 0x7f; /* a P-256 scalar below the group order */
-    hpke_seal_kem(j->kem, j->aead, j->pkR, skE, INFO, sizeof(INFO), aad, al, pt, l,
-                  j->enc + kem_nenc(j->kem) * (size_t)r, ct);
+    if (j->kem == 0x12) skE[0] = 0;     /* a P-521 scalar below the group order */
+    hpke_seal_suite(j->kem, j->kdf, j->aead, j->pkR, skE, INFO, sizeof(INFO), aad, al, pt, l,
+                    j->enc + kem_nenc(j->kem) * (size_t)r, ct);
     j->ct_len[r] = (uint32_t)(l + 16);
   }
   return NULL;
 }
 
-int hpke_make_input_shares_kem(uint16_t kem, uint16_t aead, const uint8_t* pkR,
-                               const uint8_t task_id[32], uint32_t n, uint64_t seed,
-                               uint32_t share_len, uint32_t publen, int taskprov, uint32_t stride,
-                               uint8_t* enc, uint8_t* ct, uint32_t* ct_len, uint8_t* ids,
-                               uint64_t* times, uint8_t* pubs, uint8_t* shares, int n_threads) {
-  if ((taskprov ? 10u : 6u) + share_len + 16 > stride) return -1;
+int hpke_make_input_shares_suite(uint16_t kem, uint16_t kdf, uint16_t aead, const uint8_t* pkR,
+                                 const uint8_t task_id[32], uint32_t n, uint64_t seed,
+                                 uint32_t share_len, uint32_t publen, int taskprov,
+                                 uint32_t stride, uint8_t* enc, uint8_t* ct, uint32_t* ct_len,
+                                 uint8_t* ids, uint64_t* times, uint8_t* pubs, uint8_t* shares,
+                                 int n_threads) {
+  if ((taskprov ? 10u : 6u) + share_len + 16 > stride || !kem_of(kem)) return -1;
   if (n_threads < 1) n_threads = 1;
   if (n_threads > 256) n_threads = 256;
   pthread_t th[256];
@@ -461,11 +533,20 @@ int hpke_make_input_shares_kem(uint16_t kem, uint16_t aead, const uint8_t* pkR,
     jobs[t] = (GenJob){pkR, task_id, seed, share_len, publen, stride,
                        (uint32_t)((uint64_t)n * t / n_threads),
                        (uint32_t)((uint64_t)n * (t + 1) / n_threads), taskprov, enc, ct, ids, pubs,
-                       shares, ct_len, times, aead, kem};
+                       shares, ct_len, times, aead, kem, kdf};
     pthread_create(&th[t], NULL, gen_run, &jobs[t]);
   }
   for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
   return 0;
+}
+int hpke_make_input_shares_kem(uint16_t kem, uint16_t aead, const uint8_t* pkR,
+                               const uint8_t task_id[32], uint32_t n, uint64_t seed,
+                               uint32_t share_len, uint32_t publen, int taskprov, uint32_t stride,
+                               uint8_t* enc, uint8_t* ct, uint32_t* ct_len, uint8_t* ids,
+                               uint64_t* times, uint8_t* pubs, uint8_t* shares, int n_threads) {
+  return hpke_make_input_shares_suite(kem, 1, aead, pkR, task_id, n, seed, share_len, publen,
+                                      taskprov, stride, enc, ct, ct_len, ids, times, pubs, shares,
+                                      n_threads);
 }
 int hpke_make_input_shares_ex(uint16_t aead, const uint8_t pkR[32], const uint8_t task_id[32],
                               uint32_t n, uint64_t seed, uint32_t share_len, uint32_t publen,

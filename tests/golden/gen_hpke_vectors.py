@@ -20,6 +20,7 @@ OUTS = {(32, 1): OUT,
         (16, 1): os.path.join(_D, "hpke_rfc9180_p256_aes128gcm.json"),
         (16, 2): os.path.join(_D, "hpke_rfc9180_p256_aes256gcm.json"),
         (16, 3): os.path.join(_D, "hpke_rfc9180_p256_chacha20poly1305.json")}
+ALL_OUT = os.path.join(_D, "hpke_rfc9180_all.json")
 
 
 def main():
@@ -37,6 +38,23 @@ def main():
                          "hpke.rs decrypt_test_vectors)")
         json.dump(out, open(path, "w"), indent=1)
         print("wrote", path)
+    # every base-mode vector of the file: 4 KEMs (X25519, P-256, X448, P-521)
+    # x 2 KDFs (HKDF-SHA256, HKDF-SHA512) x 3 AEADs = 24, each with its base_nonce encryption
+    allv = []
+    for v in vecs:
+        if v["mode"] != 0:
+            continue
+        e = [x for x in v["encryptions"] if x["nonce"] == v["base_nonce"]]
+        out = {k: v[k] for k in ("mode", "kem_id", "kdf_id", "aead_id", "info", "enc", "pkRm",
+                                 "skRm", "base_nonce")}
+        out["encryptions"] = e[:1]
+        allv.append(out)
+    if len(allv) != 24:
+        sys.exit(f"expected 24 base-mode vectors, found {len(allv)}")
+    json.dump({"source": "RFC 9180 test-vector set, core/src/test-vectors.json (read by Janus's "
+                         "hpke.rs decrypt_test_vectors)", "vectors": allv},
+              open(ALL_OUT, "w"), indent=1)
+    print("wrote", ALL_OUT)
 
 
 if __name__ == "__main__":

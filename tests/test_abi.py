@@ -47,17 +47,22 @@ def test_dap_header_declares_the_exported_set():
 
 
 def test_hpke_unsupported_suite_is_refused():
-    """P-384 / P-521 / X448 and HKDF-SHA384/512 stay on the host path: creation says
-    EUNSUPPORTED before any GPU call; a P-256 key outside [1, n) is EINVAL (no GPU call)."""
+    """P-384 (no RFC 9180 vector in the reference) and unknown KDF / AEAD ids stay on the host
+    path: creation says EUNSUPPORTED before any GPU call; a NIST-curve key outside [1, n) or a
+    key of the wrong length is EINVAL (no GPU call)."""
     from janus_amd import hpke as H
     with pytest.raises(NotImplementedError):
         H.HpkeOpener(bytes(48), bytes(97), kem_id=0x0011)   # P-384
     with pytest.raises(NotImplementedError):
-        H.HpkeOpener(bytes(56), bytes(56), kem_id=0x0021)   # X448
+        H.HpkeOpener(bytes(32), bytes(32), kdf_id=0x0004)   # no such KDF
     with pytest.raises(NotImplementedError):
-        H.HpkeOpener(bytes(32), bytes(32), kdf_id=0x0003)   # HKDF-SHA512
+        H.HpkeOpener(bytes(32), bytes(32), aead_id=0xFFFF)  # export-only
     with pytest.raises(RuntimeError, match="rc=-1"):
         H.HpkeOpener(bytes(32), b"\x04" + bytes(64), kem_id=0x0010)  # sk = 0
+    with pytest.raises(RuntimeError, match="rc=-1"):
+        H.HpkeOpener(b"\xff" * 66, b"\x04" + bytes(132), kem_id=0x0012)  # P-521 sk >= n
+    with pytest.raises(RuntimeError, match="rc=-1"):
+        H.HpkeOpener(bytes(32), bytes(32), kem_id=0x0021)   # X448 takes 56-byte keys
     with pytest.raises(RuntimeError, match="rc=-1"):
         H.HpkeOpener(b"\xff" * 32, b"\x04" + bytes(64), kem_id=0x0010)  # sk >= n
 

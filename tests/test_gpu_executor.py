@@ -130,7 +130,8 @@ def test_concurrent_jobs_of_several_tasks_are_coalesced(name):
     assert 0 < launches < 24, launches
 
 
-@pytest.mark.parametrize("name", ["hist_256_c16", "sumvec_8x10_c9", "count", "sum32"])
+@pytest.mark.parametrize("name", ["hist_256_c16", "hist_100_c10", "sumvec_8x10_c9", "count",
+                                  "sum32"])
 def test_combined_prepare_aggregate_jobs(name):
     """prio3_helper_prepare_aggregate_batch from 8 threads at once: 32 jobs of 100-500 reports
     for 4 tasks, each with its own segments (1-4, ids past n_segments included) and accept

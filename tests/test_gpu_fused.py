@@ -168,3 +168,12 @@ def test_fused_accumulate_on_fused_prepare_variants(opts):
     host mask, every report on the deferred slow path."""
     _run(CONFIGS["hist_256_c16"], 3000, seed=91, n_segments=4, opts=opts)
     _run(CONFIGS["hist_256_c16"], 256, seed=92, force_slow=True, opts=opts)
+
+
+@pytest.mark.parametrize("name", ["hist_100_c10", "hist_10_c3"])
+def test_fused_segment_runs_partial_waves(name):
+    """for M % 32 != 0 the last k_agg_waves wave has lanes past the slot
+    range; with many segment runs per 32-wave chunk (the mixed path, as the executor's one
+    segment per job) those lanes must stay alive through the readlane of the wave segments."""
+    _run(CONFIGS[name], 4100, seed=51, n_segments=9, seg_mode="runs", accept_frac=0.95)
+    _run(CONFIGS[name], 2600, seed=52, n_segments=5, seg_mode="runs", oob_frac=0.03)

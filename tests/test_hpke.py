@@ -383,3 +383,106 @@ def test_gpu_p256_field_ops_match_python(op):
           lambda x, y: 3 * x, lambda x, y: 8 * x, lambda x, y: pow(x, P256 - 2, P256)][op]
     bad = [i for i in range(n) if got[i] >= 2**256 or (got[i] - fn(a[i], b[i])) % P256]
     assert not bad, f"op {op}: {len(bad)} wrong, first {bad[0]}: a={a[bad[0]]:x} b={b[bad[0]]:x}"
+
+
+# ---- every base-mode suite of the reference's vector file ------------------
+# core/src/test-vectors.json holds 24 base-mode vectors: KEM X25519 / P-256 / X448 / P-521 x KDF
+# HKDF-SHA256 / HKDF-SHA512 x the three AEADs (Janus's own test opens the 12 of its two KEMs,
+# hpke.rs:520-525).  tests/golden/hpke_rfc9180_all.json is extracted from it as data.
+ALL = json.load(open(os.path.join(_GDIR, "hpke_rfc9180_all.json")))["vectors"]
+_ID = lambda v: f"kem{v['kem_id']:#x}-kdf{v['kdf_id']}-aead{v['aead_id']}"
+
+
+def test_all_vectors_present():
+    suites = {(v["kem_id"], v["kdf_id"], v["aead_id"]) for v in ALL}
+    assert suites == {(k, f, a) for k in (0x20, 0x10, 0x21, 0x12) for f in (1, 3) for a in (1, 2, 3)}
+
+
+@pytest.mark.parametrize("v", ALL, ids=_ID)
+def test_oracle_rfc9180_all_vectors(v):
+    """The oracle (RFC 9180 over OpenSSL) against each vector: pkRm from skRm, and the open."""
+    assert H.kem_public(b(v["skRm"]), v["kem_id"]) == b(v["pkRm"])
+    e = v["encryptions"][0]
+    assert H.open_(b(v["skRm"]), b(v["pkRm"]), b(v["enc"]), b(v["info"]), b(e["aad"]), b(e["ct"]),
+                   aead=v["aead_id"], kem=v["kem_id"], kdf=v["kdf_id"]) == b(e["pt"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("v", ALL, ids=_ID)
+def test_gpu_rfc9180_all_vectors(v):
+    """The GPU opener on each of the 24 vectors: the plaintext, and a failed open for a wrong
+    tag, a wrong AAD and a corrupted enc."""
+    from janus_amd import hpke as G
+    op = G.HpkeOpener(b(v["skRm"]), b(v["pkRm"]), info=b(v["info"]), kem_id=v["kem_id"],
+                      kdf_id=v["kdf_id"], aead_id=v["aead_id"])
+    e = v["encryptions"][0]
+    bad = bytearray(b(e["ct"]))
+    bad[-1] ^= 1
+    enc2 = bytearray(b(v["enc"]))
+    enc2[len(enc2) // 3] ^= 4
+    got = op.open([b(v["enc"]), b(v["enc"]), b(v["enc"]), bytes(enc2)],
+                  [b(e["ct"]), bytes(bad), b(e["ct"]), b(e["ct"])],
+                  [b(e["aad"]), b(e["aad"]), b"wrong aad", b(e["aad"])])
+    assert got[0] == b(e["pt"])
+    assert got[1:] == [None] * 3
+    op.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kem,kdf,aead", [(0x20, 2, 1), (0x20, 3, 3), (0x10, 2, 2), (0x10, 3, 1),
+                                          (0x21, 1, 1), (0x21, 2, 3), (0x21, 3, 2),
+                                          (0x12, 3, 1), (0x12, 1, 3), (0x12, 2, 2)])
+def test_gpu_suite_input_shares_match_oracle(kem, kdf, aead):
+    """Janus-shaped helper input shares under every KEM and key-schedule KDF (HKDF-SHA384 has
+    no RFC vector: the OpenSSL-composed oracle is its pin), tampered reports included."""
+    from janus_amd import hpke as G
+    n = 70 if kem in (0x21, 0x12) else 130
+    rng = np.random.default_rng(kem * 7 + kdf * 3 + aead)
+    d = H.make_batch(n, 48, 32, seed=kem + kdf + aead, aead=aead, kem=kem, kdf=kdf)
+    d, exp = _tamper(d, rng)
+    ref_sh, ref_st = H.open_input_shares(d["skR"], d["pkR"], d["task_id"], d["enc"], d["ct"],
+                                         d["ct_len"], d["report_ids"], d["times"], d["pubs"], 48,
+                                         aead=aead, kem=kem, kdf=kdf)
+    np.testing.assert_array_equal(ref_st, exp)
+    op = G.HpkeOpener(d["skR"], d["pkR"], kem_id=kem, kdf_id=kdf, aead_id=aead)
+    sh, st = op.open_input_shares(d["task_id"], d["enc"], d["ct"], d["ct_len"], d["report_ids"],
+                                  d["times"], d["pubs"], 48)
+    np.testing.assert_array_equal(st, ref_st)
+    np.testing.assert_array_equal(sh, ref_sh)
+
+
+P448 = 2**448 - 2**224 - 1
+P521 = 2**521 - 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("field", [1, 2])
+@pytest.mark.parametrize("op", range(6))
+def test_gpu_x448_p521_field_ops_match_python(field, op):
+    """GF(2^448 - 2^224 - 1) (28-bit limbs) and GF(2^521 - 1) (29-bit limbs), unsaturated column
+    products with the Solinas / Mersenne folds, on operands below 2^448 / 2^521 (so also in
+    [p, 2^bits)) and edge values, against Python integers: results canonical."""
+    import ctypes as C
+    import random
+    from janus_amd import hpke as G
+    P, bits, nw = (P448, 448, 14) if field == 1 else (P521, 521, 17)
+    edge = [0, 1, 2, P - 1, P - 2, P, P + 1, 2**bits - 1, 2**bits - 2, (P - 1) // 2, 2**(bits - 1),
+            2**224 if field == 1 else 2**260, 2**224 - 1 if field == 1 else 2**29 - 1]
+    rnd = random.Random(100 * field + op)
+    n = 2048 if op == 5 else 1 << 15
+    a = [rnd.choice(edge) if rnd.random() < 0.2 else rnd.randrange(2**bits) for _ in range(n)]
+    bb = [rnd.choice(edge) if rnd.random() < 0.2 else rnd.randrange(2**bits) for _ in range(n)]
+    a[:len(edge)] = edge
+    bb[:len(edge)] = edge[::-1]
+    enc = lambda xs: np.frombuffer(b"".join(x.to_bytes(4 * nw, "little") for x in xs),
+                                   np.uint32).copy()
+    A, B = enc(a), enc(bb)
+    out = np.zeros_like(A)
+    Pp = lambda x: x.ctypes.data_as(C.c_void_p)
+    assert G._lib().janus_hpke_selftest_field(field, op, n, Pp(A), Pp(B), Pp(out)) == 0
+    got = [int.from_bytes(out[nw * i:nw * i + nw].tobytes(), "little") for i in range(n)]
+    small = 39081 if field == 1 else 8
+    fn = [lambda x, y: x * y, lambda x, y: x * x, lambda x, y: x + y, lambda x, y: x - y,
+          lambda x, y: small * x, lambda x, y: pow(x, P - 2, P)][op]
+    bad = [i for i in range(n) if got[i] != fn(a[i], bb[i]) % P]
+    assert not bad, f"field {field} op {op}: {len(bad)} wrong, first a={a[bad[0]]:x} b={bb[bad[0]]:x}"
