@@ -270,6 +270,14 @@ DEV void put_elem(const DevParams& p, void* base, uint32_t idx, uint32_t r, cons
   typename F::T x = F::from_words(w);
   if (!F::lt_p(x)) flag = 1;
   DCHECK(r < p.ld);
+#ifdef JANUS_NT_XOF  // A/B: squeezed elements stored non-temporally (re-read once, much later)
+  if constexpr (F::ES == 16) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u v = {x.w[0], x.w[1], x.w[2], x.w[3]};
+    __builtin_nontemporal_store(v, (v4u*)base + (size_t)idx * p.ld + r);
+    return;
+  }
+#endif
   F::store(base, (size_t)idx * p.ld + r, x);
 }
 
@@ -585,6 +593,10 @@ int launch_mp64_leader_next(uint32_t n, const uint8_t* d_prep_msgs, Scratch sc, 
                             hipStream_t st);
 // long-share helper XOF on lane pairs (prio3_xof_pair.hip); false if the instance is not one it takes
 bool launch_xof_pair(const DevParams& p, InPtrs in, Scratch sc, hipStream_t st);
+// prio3_prep_pair.hip: Histogram (P = 32) prepare on lane pairs (k_prep_hp); true if launched
+bool prep_pair_takes(const DevParams& p, bool pull);
+bool launch_prep_pair(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st,
+                      bool fuse, bool pull);
 // P = 64 / 128 ParallelSum(Mul) helper query, eight lanes per report (prio3_query_wide.hip);
 // false if the instance is not one it takes
 bool launch_query_wide(const DevParams& p, InPtrs in, Scratch sc, OutPtrs out, hipStream_t st);
@@ -620,6 +632,8 @@ struct Run {
   bool fused = false;
   bool aggregate = false;  // made by prio3_device_prepare_aggregate (finish may follow)
   bool lfused = false;     // leader init summed the wave partials (segment 0; leader_fuse_acc)
+  // reports per wave of the fused partials: 2^6 (one lane per report), 2^5 (k_prep_hp's pairs)
+  uint32_t wshift = 6;
   uint32_t nseg = 0;
   const uint32_t* seg = nullptr;
   // executor groups with aggregating jobs (RUN_AGG_IO): group segment ids, accept bytes, the
@@ -653,6 +667,9 @@ struct prio3_engine {
                           // k_query_fp) that take the shapes the specialised kernels do not
   int n_cu = 256;    // compute units of the engine's GPU
   int fp_round = 1;  // FPVec sub-batches rounded to whole query rounds (fp_sub_sizes)
+  // option: Histogram (P = 32) prepares of at most this many reports run on lane pairs
+  // (k_prep_hp; 0 = never): below ~3 waves per SIMD the one-lane k_prep_h leaves SIMDs idle
+  int pair_max = 196608;
   int timing = 0;
   Mp64Params mp{};  // PRIO3_SUMVEC_F64_MP only
   uint64_t* d_sigma64 = nullptr;

@@ -695,12 +695,17 @@ DEV void msg_absorb_final(KState& s, Msg& m, int len) {
 
 // -------------------------------------------------------------------------------------
 // Cross-lane aggregation for the fused accumulate: the 64 lanes' copies of two Field128
-// elements, split into 16-bit half-limbs (16 values per lane), are reduce-scattered over the
-// wave with a 4-stage DPP butterfly inside each row of 16 (row_mirror = xor 15,
-// row_half_mirror = xor 7, quad_perm xor 2, xor 1 -- each stage keeps the half of the vector
-// selected by one lane-id bit and adds the partner's matching half) and two cross-row adds
-// (ds_swizzle xor 16, ds_bpermute xor 32).  Lane l returns the wave total of slot l & 15:
-// element (l >> 3) & 1, half-limb l & 7 (weight 2^(16 (l & 7))); each total is < 2^22.
+// elements, split into 16-bit half-limbs (16 values per lane, slot s = element s >> 3,
+// half-limb s & 7), are reduce-scattered over the wave:
+//   - across the wave halves with v_permlane32_swap (8 swaps + 8 adds: lanes 0-31 keep slots
+//     0-7, lanes 32-63 slots 8-15) and across row pairs with v_permlane16_swap (4 + 4), so the
+//     two cross-row stages need no lane-select masks and no LDS (they were ds_swizzle and
+//     ds_bpermute after the in-row stages, r03);
+//   - inside each row of 16 by two DPP butterfly stages (row_mirror = xor 15, row_half_mirror
+//     = xor 7: keep the half selected by lane bit 3 / 2, add the partner's matching half);
+//   - the four lanes of a quad, which then hold the same slot, summed by two DPP adds.
+// Lane l returns the wave total of slot l >> 2 (element (l >> 5) & 1, half-limb (l >> 2) & 7,
+// weight 2^(16 ((l >> 2) & 7))); each total is < 2^22.
 // -------------------------------------------------------------------------------------
 template <int N, int CTRL, int BIT>
 DEV void halfsum_stage(uint32_t (&v)[16], uint32_t lane) {
@@ -721,12 +726,22 @@ DEV uint32_t wave_halfsum2(const f128& x0, const f128& x1, uint32_t lane) {
     v[8 + 2 * w] = x1.w[w] & 0xffffu;
     v[8 + 2 * w + 1] = x1.w[w] >> 16;
   }
-  halfsum_stage<16, 0x140, 3>(v, lane);  // row_mirror
-  halfsum_stage<8, 0x141, 2>(v, lane);   // row_half_mirror
-  halfsum_stage<4, 0x4E, 1>(v, lane);    // quad_perm [2,3,0,1]
-  halfsum_stage<2, 0xB1, 0>(v, lane);    // quad_perm [1,0,3,2]
+  // lanes 32-63 of v[i] <-> lanes 0-31 of v[i + 8]: the sum is slot i on lanes 0-31, i + 8 above
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v[i], v[i + 8], false, false);
+    v[i] = r[0] + r[1];
+  }
+  // odd rows of v[i] <-> even rows of v[i + 4]: slot i + 4 (lane bit 4) + 8 (lane bit 5)
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v[i], v[i + 4], false, false);
+    v[i] = r[0] + r[1];
+  }
+  halfsum_stage<4, 0x140, 3>(v, lane);  // row_mirror: slot bit 1 = lane bit 3
+  halfsum_stage<2, 0x141, 2>(v, lane);  // row_half_mirror: slot bit 0 = lane bit 2
   uint32_t x = v[0];
-  x += (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);                 // xor 16
-  x += (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane ^ 32u) << 2), (int)x);  // xor 32
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xf, 0xf, false);  // quad xor 1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xf, 0xf, false);  // quad xor 2
   return x;
 }

@@ -304,10 +304,10 @@ __device__ __forceinline__ void xofd_body(const DevParams& p, const InPtrs& in, 
       a = zero128();
       b2 = zero128();
     }
-    const uint32_t tot = wave_halfsum2(a, b2, lane);
-    const int e = e0 + (int)((lane >> 3) & 1u);
-    if (lane < 16 && e < Mi)
-      sc.wpart[((size_t)(r >> 6) * M + (uint32_t)e) * 8u + (lane & 7u)] = tot;
+    const uint32_t tot = wave_halfsum2(a, b2, lane);  // slot lane >> 2 on each lane of a quad
+    const int e = e0 + (int)(lane >> 5);
+    if ((lane & 3u) == 0 && e < Mi)
+      sc.wpart[((size_t)(r >> 6) * M + (uint32_t)e) * 8u + ((lane >> 2) & 7u)] = tot;
   };
   // the elements squeezed from share block b (state ms, pend = carried half element)
   auto fuse_block = [&](uint32_t b, uint32_t q0, uint32_t q1) __attribute__((always_inline)) {
@@ -489,6 +489,27 @@ __global__ __launch_bounds__(256, XOFD_OCC) void k_xofd(DevParams p, InPtrs in, 
   xofd_body<FUSE, TR>(p, in, sc, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
+// Zero-fills up to 4 ranges in one launch (4-byte aligned lengths and pointers: 16-byte stores
+// for the aligned body, 4-byte stores at the ends)
+struct ZeroRanges {
+  uint8_t* dst[4];
+  size_t bytes[4];
+};
+__global__ __launch_bounds__(256) void k_zero(ZeroRanges z) {
+  const size_t tid = blockIdx.x * (size_t)blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint8_t* d = z.dst[k];
+    const size_t n = z.bytes[k];
+    if (!d || !n) continue;
+    const size_t head = std::min(n, (size_t)((16 - ((uintptr_t)d & 15)) & 15));
+    const size_t n16 = (n - head) / 16;
+    for (size_t i = tid; i < n16; i += nth) ((uint4*)(d + head))[i] = make_uint4(0, 0, 0, 0);
+    for (size_t i = tid * 4; i < head; i += nth * 4) *(uint32_t*)(d + i) = 0u;
+    for (size_t i = head + 16 * n16 + tid * 4; i < n; i += nth * 4) *(uint32_t*)(d + i) = 0u;
+  }
+}
+
 // Copies by the shader cores between device memory and mapped pinned memory (up to 4 ranges,
 // 16-byte aligned; 16-byte accesses, the byte tails by lane).  Host -> device, this reads PCIe at
 // ~55 GB/s where the SDMA copy of the same staging ran at ~32 GB/s beside the XOF's own host
@@ -649,9 +670,9 @@ __global__ __launch_bounds__(256, JR_OCC) void k_jrpart(DevParams p, InPtrs in, 
   auto fused_pair = [&](int e0, const uint4& a, const uint4& b) {
     if (e0 + 1 < 0 || e0 >= M) return;  // wave-uniform
     const uint32_t tot = wave_halfsum2(mk128(a.x, a.y, a.z, a.w), mk128(b.x, b.y, b.z, b.w), lane);
-    const int e = e0 + (int)((lane >> 3) & 1u);
-    if (lane < 16 && e >= 0 && e < M)
-      sc.wpart[((size_t)(r >> 6) * (uint32_t)M + (uint32_t)e) * 8u + (lane & 7u)] = tot;
+    const int e = e0 + (int)(lane >> 5);  // slot lane >> 2 on each lane of a quad
+    if ((lane & 3u) == 0 && e >= 0 && e < M)
+      sc.wpart[((size_t)(r >> 6) * (uint32_t)M + (uint32_t)e) * 8u + ((lane >> 2) & 7u)] = tot;
   };
   const uint32_t L = 42 + (uint32_t)M * 16;
   const uint32_t B = L / 168, rem = L % 168;
@@ -1490,7 +1511,13 @@ __device__ __forceinline__ void query_h_body(const DevParams& p, const InPtrs& i
         const uint32_t i = k * C + jg + q;
         const bool valid = (k < K) && (jg + q < C) && (i < M);
         const uint32_t msk = valid ? 0xffffffffu : 0u;
+#ifdef JANUS_NT_Q  // A/B: the share read once, not kept in L2 (beta / L stay there)
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        const v4u vv = __builtin_nontemporal_load((const v4u*)sc.meas + (size_t)(valid ? i : 0) * ld + r);
+        const uint4 v = make_uint4(vv.x, vv.y, vv.z, vv.w);
+#else
         const uint4 v = ((const uint4*)sc.meas)[(size_t)(valid ? i : 0) * ld + r];
+#endif
         dst[q] = mk128(v.x & msk, v.y & msk, v.z & msk, v.w & msk);
       }
     };
@@ -1899,7 +1926,7 @@ __global__ __launch_bounds__(256) void k_agg_fix(uint32_t n, const uint8_t* stat
                                                  const uint32_t* wseg, uint32_t* fix,
                                                  uint32_t fix_cap, uint32_t nseg,
                                                  unsigned long long* counts, uint32_t oor_masked,
-                                                 uint32_t per) {
+                                                 uint32_t per, uint32_t wshift) {
   __shared__ uint32_t tseg[FIX_T];
   __shared__ unsigned int tcnt[FIX_T];
   if (threadIdx.x < FIX_T) {
@@ -1915,7 +1942,7 @@ __global__ __launch_bounds__(256) void k_agg_fix(uint32_t n, const uint8_t* stat
     // out-of-range segment ids are excluded everywhere (as k_mask and k_meta do)
     const bool inc = valid && sg < nseg && status[r] == PRIO3_STATUS_FINISHED &&
                      (!accept || accept[r]);
-    const bool fused = valid && wseg[r >> 6] != 0xffffffffu && (!oor_masked || sg < nseg);
+    const bool fused = valid && wseg[r >> wshift] != 0xffffffffu && (!oor_masked || sg < nseg);
     const uint32_t s0 = (uint32_t)__shfl((int)sg, 0);
     const bool uni = __all(!valid || sg == s0);
     const unsigned long long b = __ballot(inc);
@@ -2736,7 +2763,8 @@ static size_t run_carve(Run* R, unsigned flags, uint32_t n_keys, uint8_t* base) 
     take(&R->gcnt, 8 * S);
   }
   if (flags & RUN_FUSED) {
-    const size_t waves = (n + 63) / 64, M = d.meas_len, chunks = (waves + WCH_HOST - 1) / WCH_HOST;
+    // sized for 32-report waves (k_prep_hp); the one-lane kernels use the first half
+    const size_t waves = (n + 31) / 32, M = d.meas_len, chunks = (waves + WCH_HOST - 1) / WCH_HOST;
     take(&R->wpart, waves * M * 8 * sizeof(uint32_t));
     take(&R->wseg, waves * sizeof(uint32_t));
     take(&R->cpart, chunks * M * 8 * 8);
@@ -2912,9 +2940,10 @@ enum : int { DEFER_NONE = 0, DEFER_QH = 1, DEFER_SUM = 2, DEFER_GEN64 = 3 };
 // caller then ends the run with launch_slow_redo
 // in.leader_src (executor groups, pulls_in_xof): the leader prep shares are still in the mapped
 // host staging and the fused k_prep_h<.., PULL> copies them lane by lane during its XOF.
+// pair: Histogram on lane pairs (k_prep_hp, prio3_prep_pair.hip) instead of k_prep_h
 static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, uint32_t n,
                           InPtrs in, OutPtrs out, Scratch sc, hipStream_t st, bool fuse,
-                          int* deferred) {
+                          int* deferred, bool pair = false) {
   DevParams dp = base;
   dp.n = n;
   dp.force_slow = (uint32_t)e->force_slow;
@@ -3010,7 +3039,11 @@ static int launch_prepare(prio3_engine* e, const DevParams& base, uint32_t c0, u
       } else {
         if (deferred) *deferred = DEFER_QH;
         const bool pl = in.leader_src != nullptr;
-        if (fuse && pl)
+        bool paired = false;
+        if (pair)
+          TIMED(e, st, "k_prep_hp", (paired = launch_prep_pair(dp, in, sc, out, st, fuse, pl)));
+        if (paired) {
+        } else if (fuse && pl)
           TIMED(e, st, "k_prep_h", (k_prep_h<true, true><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
         else if (fuse)
           TIMED(e, st, "k_prep_h", (k_prep_h<true><<<blocks, 256, 0, st>>>(dp, in, sc, out)));
@@ -3143,6 +3176,16 @@ static bool pulls_in_xof(const prio3_engine* e, const DevParams& dp, bool fuse, 
          B >= 2 && dp.prep_share_len / 16 <= 2 * (B - 1) && n % 64 == 0;
 }
 
+// Histogram (P = 32) runs of at most pair_max reports on lane pairs (k_prep_hp)
+static bool pair_takes(const prio3_engine* e, const DevParams& base, uint32_t n, bool fuse,
+                       bool pulling) {
+  if (e->pair_max <= 0 || n == 0 || n > (uint32_t)e->pair_max || !prep_fused_takes(e, base, fuse))
+    return false;
+  DevParams d = base;
+  d.n = n;
+  return prep_pair_takes(d, pulling);
+}
+
 // pull (nullable; executor groups): copies the leader prep shares (and the fix-up inputs) from
 // the mapped host staging into the run -- inside the fused XOF + query launch where the chain is
 // k_prep_h (pulls_in_xof), else by one copy launch ahead of the chain.
@@ -3165,6 +3208,9 @@ static int prepare_run(prio3_engine* e, Run* R, InPtrs in, OutPtrs out, hipStrea
   sc.wpart = R->wpart;
   sc.wseg = R->wseg;
   R->last = st;
+  // small Histogram runs (the executor's groups) on lane pairs: twice the waves, half the work each
+  const bool pair = pair_takes(e, R->dp, n, fuse, in.leader_src != nullptr);
+  R->wshift = pair ? 5u : 6u;
   // auto: one chunk per 128Ki reports on the two-kernel chain; one launch for the fused k_prep_h
   // (A/B on MI355X, 1 Mi reports: 169.9 M/s at 1 chunk vs 163.2 M/s at 8)
   const uint32_t K = e->chunks > 0                       ? (uint32_t)e->chunks
@@ -3172,8 +3218,8 @@ static int prepare_run(prio3_engine* e, Run* R, InPtrs in, OutPtrs out, hipStrea
                                                         : std::max(1u, (n + (1u << 16)) >> 17);
   const uint32_t csz = ((n + K - 1) / K + 255) & ~255u;
   int deferred = DEFER_NONE;
-  if (!allow_chunks || K == 1 || n <= csz || R->dp.kind == PRIO3_FPVEC_BOUNDED_L2) {
-    const int rc = launch_prepare(e, R->dp, 0, n, in, out, sc, st, fuse, &deferred);
+  if (pair || !allow_chunks || K == 1 || n <= csz || R->dp.kind == PRIO3_FPVEC_BOUNDED_L2) {
+    const int rc = launch_prepare(e, R->dp, 0, n, in, out, sc, st, fuse, &deferred, pair);
     if (rc == PRIO3_OK && deferred)
       return launch_slow_redo(e, R->dp, n, in, out, sc, st, deferred);
     return rc;
@@ -3326,7 +3372,7 @@ uint64_t engine_group_key(const prio3_engine* e) {
   // engine must not silently run with the lead engine's options)
   const int opts[] = {e->force_slow, e->chunks, e->fuse_acc,           e->leader_fast,
                       e->leader_fuse_acc, e->fp_round, e->experimental_fpvec, e->force_generic,
-                      e->timing};
+                      e->timing, e->pair_max};
   h = fnv(h, opts, sizeof opts);
   h = fnv(h, &e->fp_sub_bytes, sizeof e->fp_sub_bytes);
   // XofHmacSha256Aes128 keys enter the kernels as HMAC midstates: one engine per launch; an
@@ -3733,7 +3779,7 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
               {"fp_round", &e->fp_round},          {"timing", &e->timing},
               {"coalesce", &e->coalesce},          {"experimental_fpvec", &e->experimental_fpvec},
               {"leader_fuse_acc", &e->leader_fuse_acc},
-              {"force_generic_query", &e->force_generic}};
+              {"force_generic_query", &e->force_generic}, {"pair_max", &e->pair_max}};
   for (auto& o : ints)
     if (!strcmp(key, o.name)) {
       *o.field = (int)value;
@@ -3785,11 +3831,18 @@ int prio3_device_prepare(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
 static int fused_finish(prio3_engine* e, Run* R, const uint8_t* d_status, const uint32_t* seg,
                         const uint32_t* fix_seg, const uint8_t* d_accept_mask, uint32_t S,
                         uint8_t* d_agg_shares, uint64_t* d_counts, hipStream_t st) {
-  const uint32_t n = R->n, M = R->dp.meas_len;
-  const uint32_t nwaves = (n + 63) / 64;
-  HIPCHK(hipMemsetAsync(R->agg64, 0, (size_t)S * M * 8 * 8, st));
-  HIPCHK(hipMemsetAsync(R->fix, 0, sizeof(uint32_t), st));
-  HIPCHK(hipMemsetAsync(d_counts, 0, 8 * (size_t)S, st));
+  const uint32_t n = R->n, M = R->dp.meas_len, ws = R->wshift;
+  const uint32_t nwaves = (n + (1u << ws) - 1) >> ws;
+  {  // one zeroing launch for the three accumulators (three memsets were ~15 us per group, r03ag)
+    ZeroRanges z{};
+    z.dst[0] = (uint8_t*)R->agg64;
+    z.bytes[0] = (size_t)S * M * 8 * 8;
+    z.dst[1] = (uint8_t*)R->fix;
+    z.bytes[1] = sizeof(uint32_t);
+    z.dst[2] = (uint8_t*)d_counts;
+    z.bytes[2] = 8 * (size_t)S;
+    TIMED(e, st, "k_zero", (k_zero<<<std::min<uint32_t>(256, (uint32_t)((z.bytes[0] / 16 + 255) / 256) + 1), 256, 0, st>>>(z)));
+  }
   const uint32_t nchunks = (nwaves + WCH - 1) / WCH;
   dim3 g1((M * 8 / 4 + 255) / 256, nchunks);  // 4 slots per thread (k_agg_waves)
   TIMED(e, st, "k_agg_waves",
@@ -3798,7 +3851,7 @@ static int fused_finish(prio3_engine* e, Run* R, const uint8_t* d_status, const 
   TIMED(e, st, "k_agg_fix",
         (k_agg_fix<<<(n + fix_per(n) - 1) / fix_per(n), 256, 0, st>>>(
             n, d_status, seg, d_accept_mask, R->wseg, R->fix, (uint32_t)(R->fix_cap - 1), S,
-            (unsigned long long*)d_counts, fix_seg ? 1u : 0u, fix_per(n))));
+            (unsigned long long*)d_counts, fix_seg ? 1u : 0u, fix_per(n), ws)));
   if (nchunks <= 64 && S > 1)
     TIMED(e, st, "k_agg_final",
           (k_agg_final_s<<<dim3((M + 31) / 32, S), 256, 0, st>>>(

@@ -125,13 +125,15 @@ def test_concurrent_jobs_of_several_tasks_are_coalesced(name):
         np.testing.assert_array_equal(agg, ra)
         np.testing.assert_array_equal(cnt, rc)
     # Histogram(256, 16) (P = 32) and Count run their XOF and query in one launch
-    kern = {"count": "k_prep_gen", "hist_256_c16": "k_prep_h"}.get(name, "k_xofd")
-    launches = sum(e.timing().get(kern, (0, 0))[1] for e in engines)
+    # (small groups on the lane-pair k_prep_hp)
+    kern = {"count": ("k_prep_gen",), "hist_256_c16": ("k_prep_h", "k_prep_hp")}.get(
+        name, ("k_xofd",))
+    launches = sum(e.timing().get(k, (0, 0))[1] for e in engines for k in kern)
     assert 0 < launches < 24, launches
 
 
 @pytest.mark.parametrize("name", ["hist_256_c16", "hist_100_c10", "sumvec_8x10_c9", "count",
-                                  "sum32"])
+                                  "sum32", "hist_256_c16/one_lane"])
 def test_combined_prepare_aggregate_jobs(name):
     """prio3_helper_prepare_aggregate_batch from 8 threads at once: 32 jobs of 100-500 reports
     for 4 tasks, each with its own segments (1-4, ids past n_segments included) and accept
@@ -139,12 +141,15 @@ def test_combined_prepare_aggregate_jobs(name):
     groups.  Each job's messages, statuses, per-segment aggregates and counts equal the
     restatement's, and the groups mixed jobs into fewer launches than jobs."""
     from oracle.oracle import Oracle
+    name, _, variant = name.partition("/")
     cfg = CONFIGS[name]
     o = Oracle(**cfg)
     vks = [bytes([k]) * 16 for k in (0x41, 0x42, 0x43, 0x44)]
     engines = [_engine(cfg, vk) for vk in vks]
     for e in engines:
         e.set_option("timing", 1)
+        if variant == "one_lane":  # groups on the one-lane k_prep_h instead of k_prep_hp
+            e.set_option("pair_max", 0)
         e.timing_reset()
     rng = np.random.default_rng(19)
     jobs = []
@@ -183,9 +188,9 @@ def test_combined_prepare_aggregate_jobs(name):
         np.testing.assert_array_equal(msgs, rm)
         np.testing.assert_array_equal(agg, ra)
         np.testing.assert_array_equal(cnt, rc)
-    kern = {"count": "k_prep_gen", "hist_256_c16": "k_prep_h", "sum32": "k_prep_sum"}.get(
-        name, "k_xofd")
-    launches = sum(e.timing().get(kern, (0, 0))[1] for e in engines)
+    kern = {"count": ("k_prep_gen",), "hist_256_c16": ("k_prep_h", "k_prep_hp"),
+            "sum32": ("k_prep_sum",), "hist_100_c10": ("k_xofd", "k_prep_h")}.get(name, ("k_xofd",))
+    launches = sum(e.timing().get(k, (0, 0))[1] for e in engines for k in kern)
     assert 0 < launches < 32, launches
 
 

@@ -177,3 +177,23 @@ def test_fused_segment_runs_partial_waves(name):
     segment per job) those lanes must stay alive through the readlane of the wave segments."""
     _run(CONFIGS[name], 4100, seed=51, n_segments=9, seg_mode="runs", accept_frac=0.95)
     _run(CONFIGS[name], 2600, seed=52, n_segments=5, seg_mode="runs", oob_frac=0.03)
+
+
+@pytest.mark.parametrize("pair_max", [196608, 0])
+@pytest.mark.parametrize("case", ["runs", "oob", "slow", "masked"])
+def test_fused_accumulate_pair_and_one_lane(case, pair_max):
+    """The fused accumulate on both Histogram(256, 16) kernels: the lane-pair k_prep_hp (32-report
+    waves, wshift 5 in k_agg_fix) and the one-lane k_prep_h (64-report waves): segment runs inside
+    waves, out-of-range lanes and whole out-of-range waves, the forced slow path, tampered and
+    host-masked reports."""
+    cfg = CONFIGS["hist_256_c16"]
+    o = {"pair_max": pair_max}
+    if case == "runs":
+        _run(cfg, 2500, seed=61, n_segments=9, seg_mode="runs", opts=o)
+    elif case == "oob":
+        _run(cfg, 2048, seed=62, n_segments=3, oob_frac=0.2, oob_waves=(1, 6, 21), opts=o)
+    elif case == "slow":
+        _run(cfg, 200, seed=63, force_slow=True, n_segments=2, opts=o)
+    else:
+        st = _run(cfg, 1100, seed=64, accept_frac=0.7, opts=o)
+        assert (st != 0).any()

@@ -251,16 +251,19 @@ HIST_ROWS = {"hist_256_c16": CONFIGS["hist_256_c16"],
              "hist_241_c16": dict(kind="histogram", length=241, chunk_length=16)}
 
 
+@pytest.mark.parametrize("pair_max", [196608, 0])
 @pytest.mark.parametrize("n", [1, 127, 700])
 @pytest.mark.parametrize("name", list(HIST_ROWS))
-def test_query_h_shapes(name, n):
-    """Histogram with 16 calls of chunk 16 (P = 32) on k_prep_h: tampered reports (decide,
+def test_query_h_shapes(name, n, pair_max):
+    """Histogram with 16 calls of chunk 16 (P = 32) on the lane-pair k_prep_hp (runs of at most
+    pair_max reports) and on the one-lane k_prep_h (pair_max 0): tampered reports (decide,
     decode, joint-rand and public-share failures), a share shorter than K x C (masked rows),
     odd and sub-block batch sizes."""
-    _check_against_oracle(HIST_ROWS[name], n, seed=71 + n, tamper=n > 100)
+    _check_against_oracle(HIST_ROWS[name], n, seed=71 + n, tamper=n > 100,
+                          opts={"pair_max": pair_max})
 
 
-@pytest.mark.parametrize("opts", [{}, {"chunks": 3}])
+@pytest.mark.parametrize("opts", [{}, {"chunks": 3}, {"pair_max": 0}])
 @pytest.mark.parametrize("name", ["hist_256_c16", "sumvec_2x100_c10", "hist_100_c4"])
 def test_fused_prepare_kernel_parity(name, opts):
     """P = 32 ParallelSum(Mul) (Histogram with 16 and 25 calls, SumVec with 20): the XOF and the

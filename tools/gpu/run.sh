@@ -2,12 +2,15 @@
 # The one GPU-box driver script (replaces the per-experiment one-offs of rounds 1-3).
 #   OUT=gpurun_out/<tag> bash tools/gpu/run.sh STEP [STEP ...]
 # Steps run in order, each under its own time limit; the first failure ends the script.
-#   tests[:K]             pytest -m gpu (optionally -k K)              -> $OUT/tests.log
+#   tests[:K]             pytest -m gpu -x (optionally -k K)           -> $OUT/tests.log
+#   testsall[:K]          the same without -x
 #   smoke                 __graft_entry__.smoke()                      -> $OUT/smoke.log
 #   bench:NAME[:ARGS]     python bench.py ARGS (',' separates args)    -> $OUT/NAME.json
 #   lines                 every bench line (helper, configs, fpvec, leader, jobs, hpke, pipeline, mp64)
 #   prof:NAME[:ARGS]      rocprofv3 --kernel-trace --stats of bench.py ARGS -> $OUT/prof_NAME/
 #   pmc:NAME:CTRS[:ARGS]  one rocprofv3 --pmc pass (CTRS ','-separated) -> $OUT/pmc_NAME/
+#   lib:TAG               later steps load janus_amd/variants/libjanus_prio3_TAG.so (tools/
+#                         build_variant.sh; lib:base = the in-tree library again)
 # e.g.  OUT=gpurun_out/r04a bash tools/gpu/run.sh tests smoke bench:c2 prof:c2:--steps,5
 set -e
 OUT=${OUT:-gpurun_out/run}
@@ -34,9 +37,10 @@ bench() {  # NAME ARGS...
 for step in "$@"; do
   IFS=: read -r kind a1 a2 a3 <<< "$step"
   case $kind in
-  tests)
+  tests|testsall)  # testsall: no -x, every selected test runs (a failure still ends the script)
     K=(); [ -n "$a1" ] && K=(-k "$a1")
-    timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread "${K[@]}" > "$OUT/tests.log" 2>&1 || { tail -40 "$OUT/tests.log"; exit 1; }
+    X=(-x); [ "$kind" = testsall ] && X=()
+    timeout -k 10 900 python3 -u -m pytest tests -m gpu "${X[@]}" -v --timeout 180 --timeout-method thread "${K[@]}" > "$OUT/tests.log" 2>&1 || { grep -E "FAILED|passed|failed" "$OUT/tests.log" | tail -30; exit 1; }
     tail -1 "$OUT/tests.log" ;;
   smoke)
     timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$OUT/smoke.log" 2>&1 || { tail -20 "$OUT/smoke.log"; exit 1; }
@@ -62,6 +66,9 @@ for step in "$@"; do
   pmc)
     timeout -s KILL 120 rocprofv3 --pmc $(args "$a2") -d "$OUT/pmc_$a1" -o run -- python3 bench.py --no-cpu-baseline --warmup 1 --steps 2 $(args "$a3") > "$OUT/pmc_$a1.json" 2> "$OUT/pmc_$a1.err" || { tail -20 "$OUT/pmc_$a1.err"; exit 1; }
     echo "pmc $a1 done" ;;
+  lib)
+    if [ "$a1" = base ]; then unset JANUS_PRIO3_LIB; else export JANUS_PRIO3_LIB=$PWD/janus_amd/variants/libjanus_prio3_$a1.so; fi
+    echo "lib $a1" ;;
   *) echo "unknown step $step"; exit 2 ;;
   esac
 done
