@@ -343,6 +343,18 @@ struct Exec {
   // A sleep that overshoots (the group was already prepared at the first poll) tells only an
   // upper bound, so it shrinks the estimate instead of feeding it (r04a: feeding it made the
   // estimate hold itself up, 5.4 M reports/s).
+  // JANUS_PRIO3_ISSUE_FRAC = f < 1: the next group may also be issued once the running one has
+  // run for f of its predicted prepare time (its kernels then share the GPU with the running
+  // group's, and its leader-share pull overlaps the running group's query); 1 = only when the
+  // running group's prepare kernels are done.
+  static double issue_frac() {
+    static const double v = [] {
+      const char* s = getenv("JANUS_PRIO3_ISSUE_FRAC");
+      const double x = s ? atof(s) : 1.0;
+      return x > 0 ? std::min(x, 1.0) : 1.0;
+    }();
+    return v;
+  }
   struct Pred {
     double ns_per_report = 0;
     int seen = 0;
@@ -352,11 +364,13 @@ struct Exec {
     std::unique_lock<std::mutex> lk(mu);
     Group* cur = nullptr;
     typename P::Handle hc{};
+    auto t0 = std::chrono::steady_clock::now();  // when cur was issued
     for (;;) {
       if (!cur) {
         while (order.empty()) cv.wait(lk);
         Group* g = take_locked(lk);
         lk.unlock();
+        t0 = std::chrono::steady_clock::now();
         const int rc = P::issue(device, g->st, g->stg, &hc);
         lk.lock();
         if (rc != PRIO3_OK) {
@@ -370,18 +384,31 @@ struct Exec {
       typename P::Handle hn{};
       int rcn = PRIO3_OK;
       bool looked = false, tried_sleep = false, just_slept = false;
-      const auto t0 = std::chrono::steady_clock::now();
+      auto tn = t0;  // when nxt was issued
       const uint32_t nrep = P::reports(cur->st);
       Pred& pr = preds[cur->key];
+      const double frac = issue_frac(), pred_ns = pr.ns_per_report * nrep;
       while (!P::done(hc)) {
         if (!tried_sleep) {
           tried_sleep = true;
-          // sleep to 70 % of the predicted prepare time, less the timer slack (~60 us), at most 2 ms
-          const double ns = std::min(2e6, 0.7 * pr.ns_per_report * nrep - 60e3);
+          // sleep to 70 % (or the early-issue point) of the predicted prepare time, less the
+          // timer slack (~60 us), at most 2 ms
+          const double ns = std::min(2e6, std::min(0.7, frac) * pred_ns - 60e3 -
+                                              std::chrono::duration<double, std::nano>(
+                                                  std::chrono::steady_clock::now() - t0).count());
           if (pr.seen >= 2 && ns > 20e3) {
             std::this_thread::sleep_for(std::chrono::nanoseconds((int64_t)ns));
             just_slept = true;
           }
+        }
+        if (!nxt && frac < 1.0 && pr.seen >= 2 &&
+            std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - t0)
+                    .count() >= frac * pred_ns) {
+          lk.lock();
+          if (!order.empty() && order.front()->writers == 0) nxt = take_locked(lk);
+          lk.unlock();
+          tn = std::chrono::steady_clock::now();
+          if (nxt) rcn = P::issue(device, nxt->st, nxt->stg, &hn);
         }
         if (!looked && P::prepared(hc)) {
           looked = true;
@@ -394,10 +421,13 @@ struct Exec {
             pr.ns_per_report = pr.seen ? std::min(x, 0.8 * pr.ns_per_report + 0.2 * x) : x;
             pr.seen++;
           }
-          lk.lock();
-          if (!order.empty() && order.front()->writers == 0) nxt = take_locked(lk);
-          lk.unlock();
-          if (nxt) rcn = P::issue(device, nxt->st, nxt->stg, &hn);
+          if (!nxt) {
+            lk.lock();
+            if (!order.empty() && order.front()->writers == 0) nxt = take_locked(lk);
+            lk.unlock();
+            tn = std::chrono::steady_clock::now();
+            if (nxt) rcn = P::issue(device, nxt->st, nxt->stg, &hn);
+          }
         }
         just_slept = false;
         std::this_thread::yield();
@@ -416,6 +446,7 @@ struct Exec {
         } else {
           cur = nxt;
           hc = hn;
+          t0 = tn;
         }
       }
     }
