@@ -216,6 +216,11 @@ def main():
                          "aggregate, count, checksum and interval against the CPU restatement")
     ap.add_argument("--opt", action="append", default=[],
                     help="engine option key=value (e.g. chunks=3, force_generic_query=1), for A/B runs")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="helper role, N=1: skip the secondary lines (C1/C3/C4 configs and a short "
+                         "jobs line) that the default run adds as extra keys")
+    ap.add_argument("--secondary-cpu-seconds", type=float, default=1.5,
+                    help="CPU restatement sample size (seconds) for each secondary config line")
     args = ap.parse_args()
     if args.role == "leader":
         return leader_main(args)
@@ -438,10 +443,62 @@ def main():
             np.array_equal(ivs.cpu().numpy().view(np.uint64), eiv))
         out["cpu_baseline"] = cb
         out["speedup_vs_cpu"] = value / cb["value"]
+    if rank == 0 and world == 1 and not args.no_secondary:
+        del data, prep_msgs, status, seg, report_times
+        eng.close()
+        torch.cuda.empty_cache()
+        out.update(secondary_lines(args))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def _summary(d: dict) -> dict:
+    """The fields of a secondary line the default bench keeps (the full line is what --role
+    config / --role jobs print)."""
+    rf = d.get("roofline") or {}
+    cb = d.get("cpu_baseline") or {}
+    ck = d.get("checks") or {}
+    return dict(metric=d["metric"], value=d["value"], unit=d["unit"], ms_per_step=d["ms_per_step"],
+                steps=d.get("steps"), config=d.get("config"),
+                roofline=dict(bound=rf.get("bound"), kernel=rf.get("kernel"), frac=rf.get("frac"),
+                              achieved=rf.get("achieved"), peak=rf.get("peak"), unit=rf.get("unit")),
+                checks=ck, cpu_baseline=dict(value=cb.get("value"), unit=cb.get("unit"),
+                                             cores=cb.get("cores"), sample=cb.get("sample"))
+                if cb else None)
+
+
+def secondary_lines(args) -> dict:
+    """the other BASELINE.json configs on this GPU (C1 Count 100k, C3
+    SumVec 8x1000 and C4 Sum(32) at one GPU's 1/8 shard), each with its roofline frac and the
+    GPU-vs-restatement parity of a bounded CPU sample, and a short host-buffer jobs line
+    (2048 jobs x 500 reports at 128 threads and 512 jobs at 16 threads, every job checked).  Extra keys of the headline line;
+    its `value` stays the C2 helper rate."""
+    out = {}
+    t0 = time.perf_counter()
+    for key, vdaf, steps in (("secondary_c1_count", "count", 20),
+                             ("secondary_c3_sumvec", "sumvec", 5),
+                             ("secondary_c4_sum32", "sum32", 10)):
+        try:
+            out[key] = _summary(config_line(vdaf, CONFIGS[vdaf][2], steps, 2,
+                                            args.secondary_cpu_seconds))
+        except Exception as ex:  # a secondary line never hides the headline
+            out[key] = dict(error=f"{type(ex).__name__}: {ex}")
+        torch.cuda.empty_cache()
+    for key, threads, n_jobs in (("secondary_jobs", 128, 2048), ("secondary_jobs_16t", 16, 512)):
+        try:
+            j = jobs_line(threads, 500, n_jobs, 4, with_cpu=False)
+            out[key] = dict(metric=j["metric"], value=j["value"], unit=j["unit"],
+                            ms_per_step=j["ms_per_step"], config=j["config"],
+                            coalescing=j["coalescing"],
+                            roofline={k: j["roofline"][k] for k in ("bound", "achieved", "peak",
+                                                                    "unit", "frac")},
+                            checks=j["checks"])
+        except Exception as ex:
+            out[key] = dict(error=f"{type(ex).__name__}: {ex}")
+    out["secondary_seconds"] = time.perf_counter() - t0
+    return out
 
 
 def check_combined(eng, args, world, n, times_of, combiner) -> bool:
@@ -490,15 +547,23 @@ def jobs_main(args):
     Concurrent jobs are coalesced by the engine's executor.  The harness is native
     (janus_amd/libjanus_jobs.so, C++ threads), so Python is not on the timed path.  Reported
     against the PCIe H2D roof and next to the CPU restatement's single-core latency."""
+    n_jobs = max(args.tasks, (args.reports if args.reports != 1 << 20 else 1 << 21) // args.job_size)
+    out = jobs_line(args.threads, args.job_size, n_jobs, args.tasks, args.opt,
+                    args.jobs_call == "combined", not args.no_cpu_baseline)
+    print(json.dumps(out), flush=True)
+
+
+def jobs_line(T, js, n_jobs, K, opts=(), combined=True, with_cpu=True, check_tasks=None):
+    """jobs_main's measurement (see there); check_tasks: check the jobs of only the first
+    check_tasks tasks against the restatement (None: all)."""
     import ctypes as C
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
-    K, js, T = args.tasks, args.job_size, args.threads
-    n_jobs = max(K, (args.reports if args.reports != 1 << 20 else 1 << 21) // js)
+    n_jobs = max(K, n_jobs)
     pool = 1 << 16
     vks = [bytes([0x51 + t]) * 16 for t in range(K)]
     engines = [J.HelperEngine(J.Prio3Histogram(256, 16), vk, device=0) for vk in vks]
-    for kv in args.opt:
+    for kv in opts:
         k, v = kv.split("=")
         for e in engines:
             e.set_option(k, int(v))
@@ -518,7 +583,6 @@ def jobs_main(args):
     counts = np.zeros(n_jobs, np.uint64)
     agg = np.zeros((n_jobs, sz.agg_share_len), np.uint8)
     P = lambda a: a.ctypes.data_as(vp)
-    combined = args.jobs_call == "combined"
 
     def run(jobs):
         status[:] = 0xFF
@@ -534,8 +598,10 @@ def jobs_main(args):
     dt = run(n_jobs)
     if dt < 0:
         raise RuntimeError("janus_jobs_run: a C-ABI call failed")
-    # the prepare launches: the fused XOF + query (k_prep_h) or, on the two-kernel chain, k_xofd
-    launches = sum(e.timing().get(k, (0, 0))[1] for e in engines for k in ("k_prep_h", "k_xofd"))
+    # the prepare launches: the fused XOF + query (k_prep_h, or k_prep_hp on lane pairs for small
+    # groups) or, on the two-kernel chain, k_xofd
+    launches = sum(e.timing().get(k, (0, 0))[1] for e in engines
+                   for k in ("k_prep_h", "k_prep_hp", "k_xofd"))
     value = n_jobs * js / dt
     # every job against the restatement: per task, the jobs' report windows concatenated with
     # segment id = the job, so each segment of the oracle's batch is one job's aggregate
@@ -544,7 +610,7 @@ def jobs_main(args):
     t_chk = time.perf_counter()
     jobs_ok = True
     statuses_ok = True
-    for t in range(K):
+    for t in range(K if check_tasks is None else min(K, check_tasks)):
         jl = list(range(t, n_jobs, K))
         r0s = [t * pool + ((j // K) * js) % (pool - js + 1) for j in jl]
         idx = np.concatenate([np.arange(r, r + js) for r in r0s])
@@ -561,7 +627,7 @@ def jobs_main(args):
     # cores, and its single-core per-report latency
     cores = cpu_threads()
     cpu = None
-    if not args.no_cpu_baseline:
+    if with_cpu:
         m = min(4000 * cores, len(host["nonces"]))
         t0 = time.perf_counter()
         o.helper_batch(vks[0], host["nonces"][:m], host["public_shares"][:m],
@@ -578,7 +644,7 @@ def jobs_main(args):
                    sample=f"{m} reports, jobs of {js}, one job per worker thread, {dta:.1f}s",
                    single_core_us_per_report=dt1 / m1 * 1e6, cpu_model=cpu_model())
     per_report_h2d = 16 + sz.public_share_len + sz.helper_share_len + sz.prep_share_len
-    out = dict(metric="reports prepared+aggregated/sec through the host-buffer C ABI "
+    return dict(metric="reports prepared+aggregated/sec through the host-buffer C ABI "
                       "(helper, Prio3Histogram len=256, concurrent aggregation jobs)",
                value=value, unit="reports/s", n_gpus=1, steps=1, warmup=1,
                ms_per_step=dt * 1e3, higher_is_better=True, scaling="weak", vs_baseline=None,
@@ -605,10 +671,11 @@ def jobs_main(args):
                checks=dict(all_finished=bool((status == 0).all()),
                            counts_ok=bool((counts == js).all()),
                            every_job_matches_cpu=jobs_ok, statuses_match_cpu=statuses_ok,
+                           jobs_checked=sum(len(range(t, n_jobs, K)) for t in
+                                            range(K if check_tasks is None else min(K, check_tasks))),
                            check_seconds=t_chk),
                cpu_baseline=cpu,
                speedup_vs_cpu=(value / cpu["value"]) if cpu else None)
-    print(json.dumps(out), flush=True)
 
 
 def leader_main(args):
@@ -1187,17 +1254,68 @@ def config_main(args):
     their 8-GPU totals).  Same step as the headline (prio3_device_prepare_aggregate +
     aggregate_finish over resident device-generated reports); cpu_baseline = the C
     restatement on a bounded sample of the same reports, Janus job structure."""
+    n = args.reports if args.reports != 1 << 20 else CONFIGS[args.vdaf][2]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        if args.dist_backend == "gloo":
+            local = local % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(local)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+    out = config_line(args.vdaf, n, args.steps, args.warmup, args.cpu_seconds, args.opt,
+                      not args.no_cpu_baseline and rank == 0, dist=dist, local=local,
+                      gloo=args.dist_backend == "gloo")
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def _leader_sum(eng, shares, n, dev):
+    """Mod-p sum of n leader output shares on the device: the combine kernel in two levels
+    (k1 rows of k2 "segments", then the k2 partial sums), so no work-item loops over millions
+    of rows."""
+    sz = eng.sz
+    k1 = next(k for k in (1000, 512, 500, 100, 64, 10, 8, 1) if n % k == 0)
+    k2 = n // k1
+    part = torch.zeros((k2, sz.agg_share_len), dtype=torch.uint8, device=dev)
+    pcnt = torch.zeros(k2, dtype=torch.int64, device=dev)
+    eng.combine_device(k1, k2, shares, torch.zeros(n, dtype=torch.int64, device=dev), part, pcnt)
+    lagg = torch.zeros((1, sz.agg_share_len), dtype=torch.uint8, device=dev)
+    lcnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    eng.combine_device(k2, 1, part, pcnt, lagg, lcnt)
+    return lagg
+
+
+def config_line(vdaf, n, steps, warmup, cpu_seconds, opts=(), with_cpu=True, dist=None, local=0,
+                gloo=False):
+    """One config's helper step on this GPU (n reports); with `dist` (N ranks, one shard of n
+    reports each, report indices rank*n + i) the step ends in the AggregateCombiner as the
+    headline's does, elapsed is the max over ranks and value counts every rank's reports.
+    Checks: every honest report finishes; unshard -- the (combined) helper aggregate plus the
+    leader aggregate summed from the on-device client's leader output shares equals the plain
+    sum of all measurements (integration_tests/tests/integration/common.rs:332-554,
+    aggregate_share.rs:55-96); and on rank 0 the restatement's statuses, prepare messages,
+    aggregate share and count over a bounded sample of its shard."""
     from oracle.oracle import Oracle, build
-    mk, okw, n_def = CONFIGS[args.vdaf]
-    n = args.reports if args.reports != 1 << 20 else n_def
-    dev = torch.device("cuda", 0)
-    torch.cuda.set_device(0)
-    eng = J.HelperEngine(mk(), VK, device=0)
-    for kv in args.opt:
+    mk, okw, _ = CONFIGS[vdaf]
+    world = dist.get_world_size() if dist else 1
+    rank = dist.get_rank() if dist else 0
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(local)
+    eng = J.HelperEngine(mk(), VK, device=local)
+    for kv in opts:
         k, v = kv.split("=")
         eng.set_option(k, int(v))
     sz = eng.sz
-    d = eng.generate_reports_device(n, seed=0x4A414E5553000001, with_checks=True)
+    d = eng.generate_reports_device(n, seed=0x4A414E5553000001, first_index=rank * n,
+                                    with_checks=True)
     torch.cuda.synchronize()
     flags = int(d["flags"].sum().item())
     msgs = torch.empty((n, max(sz.prep_msg_len, 1)), dtype=torch.uint8, device=dev)
@@ -1206,28 +1324,69 @@ def config_main(args):
     agg = torch.zeros((1, sz.agg_share_len), dtype=torch.uint8, device=dev)
     cnt = torch.zeros(1, dtype=torch.int64, device=dev)
     pub = d["public_shares"] if sz.public_share_len else None
+    cur = lambda: torch.cuda.current_stream().cuda_stream
+    combiner = lcombiner = None
+    if dist:
+        from janus_amd.dist import AggregateCombiner
+        comb = lambda k, ga, gc, oa, oc: eng.combine_device(k, 1, ga, gc, oa, oc, stream=cur())
+        combiner = AggregateCombiner(dist, agg, cnt, comb, stage_device="cpu" if gloo else None)
+        lcombiner = AggregateCombiner(dist, agg, cnt, comb, stage_device="cpu" if gloo else None)
 
     def step():
-        s = torch.cuda.current_stream().cuda_stream
+        s = cur()
         eng.prepare_aggregate_device(d["nonces"], pub, d["helper_shares"],
                                      d["leader_prep_shares"], seg, 1, msgs, status, stream=s)
         eng.aggregate_finish_device(status, None, agg, cnt, stream=s)
+        if combiner is not None:
+            combiner(agg, cnt)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     eng.set_option("timing", 1)
     eng.timing_reset()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
     elapsed = time.perf_counter() - t0
     times = eng.timing()
     eng.set_option("timing", 0)
-    value = n * args.steps / elapsed
-    cpu, parity = None, None
-    if not args.no_cpu_baseline:
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if gloo else dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = world * n * steps / elapsed
+
+    # unshard: helper (combined) + leader (combined) aggregate == sum of every measurement
+    lagg = _leader_sum(eng, d["leader_out_shares"], n, dev)
+    msum = d["measurements"].sum(dim=0)
+    if dist:
+        lagg, _ = lcombiner(lagg, torch.full_like(cnt, n))
+        msum = msum.cpu() if gloo else msum
+        dist.all_reduce(msum)
+        hagg, hcnt = combiner.out_agg, combiner.out_cnt
+    else:
+        hagg, hcnt = agg, cnt
+    torch.cuda.synchronize()
+    es = 8 if okw["kind"] == "count" else 16
+    P = 2**64 - 2**32 + 1 if es == 8 else 2**128 - 28 * 2**64 + 1
+    hb = hagg.cpu().numpy().reshape(-1, es)
+    lb = lagg.cpu().numpy().reshape(-1, es)
+    ms = [int(x) for x in msum.cpu().numpy().reshape(-1)]
+    unshard = len(ms) == hb.shape[0] and all(
+        (int.from_bytes(hb[e].tobytes(), "little") + int.from_bytes(lb[e].tobytes(), "little"))
+        % P == ms[e] for e in range(len(ms)))
+    total_cnt = int(hcnt[0].item())
+    del lagg, msum
+
+    cpu, parity, m = None, None, 0
+    if with_cpu:
         build()
         o = Oracle(**okw)
         th = cpu_threads()
@@ -1243,29 +1402,52 @@ def config_main(args):
 
         probe = min(n, 500 * th)
         dt, _ = run(probe)
-        m = int(min(n, max(probe, probe * args.cpu_seconds / max(dt, 1e-6))))
-        dt, (cm, cs, _, _) = run(m)
+        m = int(min(n, max(probe, probe * cpu_seconds / max(dt, 1e-6))))
+        dt, (cm, cs, ca, cc) = run(m)
+        # the GPU aggregate share and count of the same sample: the last step's statuses
+        # finished again with an accept mask selecting the first m reports
+        accept = torch.zeros(n, dtype=torch.uint8, device=dev)
+        accept[:m] = 1
+        agg_s = torch.zeros_like(agg)
+        cnt_s = torch.zeros_like(cnt)
+        eng.aggregate_finish_device(status, accept, agg_s, cnt_s)
+        torch.cuda.synchronize()
         parity = bool(np.array_equal(status[:m].cpu().numpy(), cs) and
-                      np.array_equal(msgs[:m, :cm.shape[1]].cpu().numpy(), cm))
+                      np.array_equal(msgs[:m, :cm.shape[1]].cpu().numpy(), cm) and
+                      np.array_equal(agg_s.cpu().numpy().reshape(-1), np.asarray(ca).reshape(-1))
+                      and int(cnt_s[0].item()) == int(np.asarray(cc).reshape(-1)[0]))
         cpu = dict(value=m / dt, unit="reports/s", cores=th, kind="port",
                    sample=f"{m} of the benchmark's GPU-generated reports, jobs of 500 reports, "
                           f"one job per worker thread (aggregator.rs:1794,2100), {dt:.1f}s wall")
-    out = dict(metric=f"reports prepared+aggregated/sec (helper, {args.vdaf})", value=value,
-               unit="reports/s", n_gpus=1, steps=args.steps, warmup=args.warmup,
-               ms_per_step=elapsed / args.steps * 1e3, higher_is_better=True, scaling="weak",
+    out = dict(metric=f"reports prepared+aggregated/sec (helper, {vdaf})", value=value,
+               unit="reports/s", n_gpus=world, steps=steps, warmup=warmup,
+               ms_per_step=elapsed / steps * 1e3, higher_is_better=True, scaling="weak",
                vs_baseline=None, dtype="u32 limbs (mod-p integer arithmetic)",
                data="synthetic: distinct honest reports generated on-device from a seed",
-               config=dict(workload=f"{args.vdaf} helper prepare+aggregate, 1 segment",
-                           reports=n, **{k: v for k, v in okw.items() if k != "kind"}),
+               config=dict(workload=f"{vdaf} helper prepare+aggregate, 1 segment",
+                           reports=n, reports_per_rank=n, global_batch=world * n,
+                           **{k: v for k, v in okw.items() if k != "kind"}),
                kernels={k: dict(ms_total=v[0], launches=v[1], ms_avg=v[0] / max(v[1], 1))
                         for k, v in times.items()},
-               roofline=model_roofline(f"config_{args.vdaf}", RM.helper_model(RM.instance(
+               roofline=model_roofline(f"config_{vdaf}", RM.helper_model(RM.instance(
                    okw["kind"], sz, bits=okw.get("bits", 0), length=okw.get("length", 0),
-                   chunk=okw.get("chunk_length", 0))), n, args.steps, elapsed),
-               checks=dict(finished=int((status == 0).sum().item()), agg_count=int(cnt[0]),
-                           generator_flags=flags, cpu_gpu_parity_on_sample=parity),
+                   chunk=okw.get("chunk_length", 0))), n, steps, elapsed),
+               checks=dict(finished=int((status == 0).sum().item()), agg_count=total_cnt,
+                           all_counted=total_cnt == world * n, generator_flags=flags,
+                           unshard_equals_measurement_sum=unshard,
+                           cpu_gpu_parity_on_sample=parity,
+                           cpu_gpu_parity_covers=(f"statuses, prepare messages, aggregate share "
+                                                  f"and count of rank 0's first {m} reports")
+                           if with_cpu else None),
                cpu_baseline=cpu, speedup_vs_cpu=(value / cpu["value"]) if cpu else None)
-    print(json.dumps(out), flush=True)
+    if dist:
+        out["dist_backend"] = "gloo" if gloo else "nccl"
+        out["config"]["parallelism"] = f"dp{world} (report shards; all-gather + mod-p combine)"
+        if gloo:
+            out["note"] = ("gloo, ranks sharing the box's GPUs: a correctness run of the sharded "
+                           "step (all-gather staged through host memory), unmeasured on "
+                           "hardware -- the RCCL scaling curve is the driver's")
+    return out
 
 
 if __name__ == "__main__":

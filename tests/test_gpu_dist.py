@@ -196,3 +196,32 @@ def test_bench_step_two_ranks_gloo():
     assert line["config"]["global_batch"] == 2 * 16384
     assert line["checks"]["combined_matches_oracle"] is True
     assert line["checks"]["agg_count"] == 2 * 16384  # honest reports: every one counted
+
+
+def test_config_sumvec_eight_ranks_gloo_one_gpu():
+    """`bench.py --role config --vdaf sumvec` as 8 ranks x 125k reports (C3's
+    whole 1M) on the one GPU of the box over gloo: the combined helper aggregate plus the
+    combined leader aggregate unshards to the sum of all 1M measurements, every report is
+    counted, and rank 0's first reports match the CPU restatement (statuses, prepare messages,
+    aggregate share, count).  A correctness run of the sharded step -- unmeasured on hardware;
+    the RCCL scaling curve is the driver's 8-GPU run."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--role", "config", "--vdaf", "sumvec", "--reports", "125000", "--steps", "1",
+           "--warmup", "1", "--dist-backend", "gloo", "--cpu-seconds", "2"]
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, timeout=600)
+    out = p.stdout.decode(errors="replace")
+    assert p.returncode == 0, out + p.stderr.decode(errors="replace")[-4000:]
+    line = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 8 and line["dist_backend"] == "gloo"
+    assert line["config"]["global_batch"] == 1_000_000
+    ck = line["checks"]
+    assert ck["generator_flags"] == 0 and ck["finished"] == 125000
+    assert ck["all_counted"] is True and ck["agg_count"] == 1_000_000
+    assert ck["unshard_equals_measurement_sum"] is True
+    assert ck["cpu_gpu_parity_on_sample"] is True

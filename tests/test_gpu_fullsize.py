@@ -9,6 +9,9 @@ sum of the measurements.  Bit-exactness at small sizes is test_gpu_parity.py's j
   C1 Prio3Count, 100k reports                       (configs[0], plumbing size)
   C3 Prio3SumVec bits=8 length=1000, 1M/8 reports   (configs[2], one GPU's shard)
   C4 Prio3Sum bits=32, 10M/8 reports                 (configs[3], one GPU's shard)
+  C3 at its whole 1M and C4 at its whole 10M on ONE GPU: the 8-GPU totals
+  fit one MI355X's HBM (C3's leader output shares are 16 GB), so the same properties hold
+  over the whole configured workload, not only a shard
 """
 import numpy as np
 import pytest
@@ -41,11 +44,17 @@ def _run(vdaf, n, field_p, es):
                                  seg, 1, msgs, status)
     eng.aggregate_finish_device(status, None, agg, cnt)
     # leader aggregate: mod-p sum of the n leader output shares (the multi-GPU combine kernel
-    # with one "rank" per report)
+    # with one "rank" per report), in two levels so no work-item loops over millions of rows:
+    # k1 rows of k2 "segments", then the k2 partial sums
+    k1 = next(k for k in (1000, 500, 100, 10, 1) if n % k == 0)
+    k2 = n // k1
+    part = torch.zeros((k2, sz.agg_share_len), dtype=torch.uint8, device=dev)
+    pcnt = torch.zeros(k2, dtype=torch.int64, device=dev)
+    eng.combine_device(k1, k2, d["leader_out_shares"],
+                       torch.zeros(n, dtype=torch.int64, device=dev), part, pcnt)
     lagg = torch.zeros((1, sz.agg_share_len), dtype=torch.uint8, device=dev)
     lcnt = torch.zeros(1, dtype=torch.int64, device=dev)
-    eng.combine_device(n, 1, d["leader_out_shares"], torch.zeros(n, dtype=torch.int64, device=dev),
-                       lagg, lcnt)
+    eng.combine_device(k2, 1, part, pcnt, lagg, lcnt)
     meas_sum = d["measurements"].sum(dim=0).cpu().numpy()
     torch.cuda.synchronize()
     assert int((status != 0).sum()) == 0
@@ -71,4 +80,18 @@ def test_c4_sum32_shard_of_10m():
 def test_c3_sumvec_8x1000_shard_of_1m():
     from janus_amd import prio3 as J
     tot, exp = _run(J.Prio3SumVec(8, 1000, 63), 1_000_000 // 8, 2**128 - 28 * 2**64 + 1, 16)
+    assert tot == exp
+
+
+def test_c4_sum32_whole_10m_one_gpu():
+    from janus_amd import prio3 as J
+    tot, exp = _run(J.Prio3Sum(32), 10_000_000, 2**128 - 28 * 2**64 + 1, 16)
+    assert tot == exp
+
+
+def test_c3_sumvec_8x1000_whole_1m_one_gpu():
+    import torch
+    from janus_amd import prio3 as J
+    tot, exp = _run(J.Prio3SumVec(8, 1000, 63), 1_000_000, 2**128 - 28 * 2**64 + 1, 16)
+    torch.cuda.empty_cache()
     assert tot == exp

@@ -27,11 +27,20 @@ ck = d.get("checks") or {}
 print(sys.argv[1].split("/")[-1], round(d["value"] / 1e6, 3), "M", d.get("unit"), "ms",
       round(d.get("ms_per_step") or 0, 4), "frac", rf.get("frac"), "cpu", cb.get("value"),
       {k: v for k, v in ck.items() if isinstance(v, bool)})
+for k, v in d.items():
+    if k.startswith("secondary_") and isinstance(v, dict):
+        print(" ", k, round((v.get("value") or 0) / 1e6, 3), "M ms", round(v.get("ms_per_step") or 0, 4),
+              "frac", (v.get("roofline") or {}).get("frac"), v.get("error", ""),
+              {c: x for c, x in (v.get("checks") or {}).items() if isinstance(x, bool)})
+if "secondary_seconds" in d:
+    print("  secondary_seconds", round(d["secondary_seconds"], 1))
 PY
 }
 bench() {  # NAME ARGS...
   local name=$1; shift
+  local t0=$SECONDS
   timeout -k 10 600 python3 bench.py "$@" > "$OUT/$name.json" 2> "$OUT/$name.err" || { tail -20 "$OUT/$name.err"; exit 1; }
+  echo "$name wall $((SECONDS - t0)) s"
   summ "$OUT/$name.json"
 }
 for step in "$@"; do
@@ -61,10 +70,10 @@ for step in "$@"; do
     bench pipeline --role pipeline --reports 1048576
     bench mp64 --role mp64 --reports 1000000 ;;
   prof)
-    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$a1" -o run -- python3 bench.py --no-cpu-baseline $(args "$a2") > "$OUT/prof_$a1.json" 2> "$OUT/prof_$a1.err" || { tail -20 "$OUT/prof_$a1.err"; exit 1; }
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$a1" -o run -- python3 bench.py --no-cpu-baseline --no-secondary $(args "$a2") > "$OUT/prof_$a1.json" 2> "$OUT/prof_$a1.err" || { tail -20 "$OUT/prof_$a1.err"; exit 1; }
     summ "$OUT/prof_$a1.json" ;;
   pmc)
-    timeout -s KILL 120 rocprofv3 --pmc $(args "$a2") -d "$OUT/pmc_$a1" -o run -- python3 bench.py --no-cpu-baseline --warmup 1 --steps 2 $(args "$a3") > "$OUT/pmc_$a1.json" 2> "$OUT/pmc_$a1.err" || { tail -20 "$OUT/pmc_$a1.err"; exit 1; }
+    timeout -s KILL 120 rocprofv3 --pmc $(args "$a2") -d "$OUT/pmc_$a1" -o run -- python3 bench.py --no-cpu-baseline --no-secondary --warmup 1 --steps 2 $(args "$a3") > "$OUT/pmc_$a1.json" 2> "$OUT/pmc_$a1.err" || { tail -20 "$OUT/pmc_$a1.err"; exit 1; }
     echo "pmc $a1 done" ;;
   lib)
     if [ "$a1" = base ]; then unset JANUS_PRIO3_LIB; else export JANUS_PRIO3_LIB=$PWD/janus_amd/variants/libjanus_prio3_$a1.so; fi
