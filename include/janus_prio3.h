@@ -267,8 +267,11 @@ int prio3_client_generate_device(prio3_engine* engine, uint32_t n, uint64_t seed
 
 /* ---- Test / measurement knobs ---- */
 /* force_slow_path=1 routes every report through the general rejection-sampling kernel;
- * leader_fuse_acc=0 turns off the fused device-leader accumulate (A/B); the other keys are the
- * launch variants prio3_engine.hip's prio3_engine_set_option lists. */
+ * leader_fuse_acc=0 turns off the fused device-leader accumulate (A/B); pair_max=N runs
+ * Histogram(P = 32) prepares of at most N reports on lane pairs (0: never); group_dma=N sends
+ * the host-buffer executor's groups of at most N reports to the device by DMA on a copy stream
+ * instead of the kernels pulling them from pinned staging (0: never, the default; -1: always);
+ * the other keys are the launch variants prio3_engine.hip's prio3_engine_set_option lists. */
 int prio3_engine_set_option(prio3_engine* engine, const char* key, int64_t value);
 /* Per-kernel device time (ms) accumulated since the last reset, measured with HIP events
  * on the launch stream when option "timing" is 1 (2: launches counted, no events or times).

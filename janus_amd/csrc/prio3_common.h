@@ -270,14 +270,6 @@ DEV void put_elem(const DevParams& p, void* base, uint32_t idx, uint32_t r, cons
   typename F::T x = F::from_words(w);
   if (!F::lt_p(x)) flag = 1;
   DCHECK(r < p.ld);
-#ifdef JANUS_NT_XOF  // A/B: squeezed elements stored non-temporally (re-read once, much later)
-  if constexpr (F::ES == 16) {
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    const v4u v = {x.w[0], x.w[1], x.w[2], x.w[3]};
-    __builtin_nontemporal_store(v, (v4u*)base + (size_t)idx * p.ld + r);
-    return;
-  }
-#endif
   F::store(base, (size_t)idx * p.ld + r, x);
 }
 
@@ -670,6 +662,10 @@ struct prio3_engine {
   // option: Histogram (P = 32) prepares of at most this many reports run on lane pairs
   // (k_prep_hp; 0 = never): below ~3 waves per SIMD the one-lane k_prep_h leaves SIMDs idle
   int pair_max = 196608;
+  // executor groups of at most group_dma reports send their inputs to the device by DMA on a copy
+  // stream, issued while the previous group computes; larger groups are pulled from the mapped
+  // staging by their kernels (0: never DMA, the default -- DESIGN.md 11; -1: always)
+  int group_dma = 0;
   int timing = 0;
   Mp64Params mp{};  // PRIO3_SUMVEC_F64_MP only
   uint64_t* d_sigma64 = nullptr;

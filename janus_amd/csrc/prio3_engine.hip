@@ -1511,13 +1511,7 @@ __device__ __forceinline__ void query_h_body(const DevParams& p, const InPtrs& i
         const uint32_t i = k * C + jg + q;
         const bool valid = (k < K) && (jg + q < C) && (i < M);
         const uint32_t msk = valid ? 0xffffffffu : 0u;
-#ifdef JANUS_NT_Q  // A/B: the share read once, not kept in L2 (beta / L stay there)
-        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-        const v4u vv = __builtin_nontemporal_load((const v4u*)sc.meas + (size_t)(valid ? i : 0) * ld + r);
-        const uint4 v = make_uint4(vv.x, vv.y, vv.z, vv.w);
-#else
         const uint4 v = ((const uint4*)sc.meas)[(size_t)(valid ? i : 0) * ld + r];
-#endif
         dst[q] = mk128(v.x & msk, v.y & msk, v.z & msk, v.w & msk);
       }
     };
@@ -2707,9 +2701,6 @@ constexpr uint32_t WCH_HOST = 32;  // waves per fused-partial chunk (k_agg_waves
 template <class F>
 static void launch_xof_slow(const prio3_engine* e, const DevParams& p, const InPtrs& in,
                             const Scratch& sc, hipStream_t st) {
-#ifdef JANUS_AB_SKIP_SLOW  // A/B build only (tools/build_variant.sh): the cost of the launch
-  return;
-#endif
   (void)e;
   k_xof_slow<F><<<slow_blocks(p.n), 64, 0, st>>>(p, in, sc);
 }
@@ -2925,9 +2916,6 @@ static int ensure_side_streams(prio3_engine* e) {
 // in one launch; the conditions under which launch_prepare would launch exactly those two).
 static bool prep_fused_takes(const prio3_engine* e, const DevParams& dp, bool fuse) {
   if (e->force_generic) return false;
-#ifdef JANUS_AB_NO_PREP_FUSED  // A/B build: the two-kernel chain (k_xofd + k_query_h)
-  if (dp.kind != PRIO3_SUM) return false;
-#endif
   const bool ps = dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC;
   const bool dual = dp.es == 16 && dp.jr_len && (42 + dp.meas_len * 16) / 168 >= 2;
   if (dp.kind == PRIO3_SUM) return dual && !fuse && query_sum_takes(dp);  // k_prep_sum
@@ -3372,7 +3360,7 @@ uint64_t engine_group_key(const prio3_engine* e) {
   // engine must not silently run with the lead engine's options)
   const int opts[] = {e->force_slow, e->chunks, e->fuse_acc,           e->leader_fast,
                       e->leader_fuse_acc, e->fp_round, e->experimental_fpvec, e->force_generic,
-                      e->timing, e->pair_max};
+                      e->timing, e->pair_max, e->group_dma};
   h = fnv(h, opts, sizeof opts);
   h = fnv(h, &e->fp_sub_bytes, sizeof e->fp_sub_bytes);
   // XofHmacSha256Aes128 keys enter the kernels as HMAC midstates: one engine per launch; an
@@ -3426,14 +3414,25 @@ static int fused_finish(prio3_engine* e, Run* R, const uint8_t* d_status, const 
                         const uint32_t* fix_seg, const uint8_t* d_accept_mask, uint32_t S,
                         uint8_t* d_agg_shares, uint64_t* d_counts, hipStream_t st);
 
-// Host-pull group launch: the kernels read each report's nonce, public share, helper share and
-// verify-key slot straight from the pinned staging (mapped; 96-112 B per report at the start of
-// the XOF), and each lane of the fused XOF + query launch copies its own leader prep share (560 B
-// for Histogram(256,16)), segment id and accept byte into the run during its XOF (xofd_body
-// PULL), so the PCIe transfer runs under the Keccak work.  One pinned-staging H2D copy
-// per field ahead of the prepare (the r02 form) left transfer and prepare in series
-// (profiles/r03/r03e_jobs128_*.json: 21.5 M reports/s at 128 threads).
-int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr) {
+// Group launch.  DMA (option group_dma: groups of at most that many reports; off by default, as
+// it measured no better than the pull on the jobs line): the staged inputs -- nonce, public share,
+// helper share, leader prep share, verify-key slot and table, segment id, accept byte -- go to the
+// run's device buffers by hipMemcpyAsync on a copy stream of their own (the SDMA engines at the
+// link's ~55 GB/s), and the kernels, on the group's stream, wait for those copies and for the
+// prepare kernels of the group before (`after`).  The executor issues a group while the one
+// before it still computes, so the transfer of group i+1 runs under the compute of group i and
+// the kernels read HBM.  Host pull (group_dma 0, the r03 form): the kernels read each report's
+// nonce, public share, helper share and verify-key slot straight from the pinned staging
+// (mapped) and each lane of the fused XOF + query launch copies its own leader prep share,
+// segment id and accept byte into the run during its XOF (xofd_body PULL), so the transfer runs
+// under that group's own Keccak work at the rate the lanes pull (~35 GB/s, profiles/r04).  One
+// pinned-staging H2D copy per field ahead of the prepare, without the overlap (the r02 form),
+// left transfer and prepare in series (profiles/r03/r03e_jobs128_*.json: 21.5 M reports/s).
+bool engine_group_dma(const prio3_engine* e, uint32_t n) {
+  return e->group_dma < 0 || (e->group_dma > 0 && n <= (uint32_t)e->group_dma);
+}
+
+int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr, const GroupRun* after) {
   *gr = GroupRun();
   gr->lead = lead;
   gr->jobs = g.jobs;
@@ -3441,6 +3440,7 @@ int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr) {
   hipStream_t st = ws_stream_get(lead->device);
   if (!st) return PRIO3_EDEVICE;
   const bool mp = lead->dp.kind == PRIO3_SUMVEC_F64_MP;
+  const bool dma = engine_group_dma(lead, g.n);
   // aggregating jobs: the group's reports are accumulated per job segment in this launch (the
   // wave partials of the XOF where the instance fuses; waves that straddle two jobs and the
   // excluded reports go through the fix-up list)
@@ -3458,35 +3458,82 @@ int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr) {
   IoLayout L;
   engine_io_layout(lead, g.cap, &L);
   auto fail = [&](int code) {
+    (void)hipStreamSynchronize(st);
+    if (gr->cs) {
+      (void)hipStreamSynchronize(gr->cs);
+      ws_stream_put(lead->device, gr->cs);
+    }
+    for (auto& ev : gr->ev)
+      if (ev) (void)hipEventDestroy(ev);
     run_release(R, st, true);
     if (gr->prep) (void)hipEventDestroy(gr->prep);
-    gr->prep = nullptr;
+    *gr = GroupRun();
     ws_stream_put(lead->device, st);
     return code;
   };
-  const uint8_t* hd = g.stg_dev;
-  InPtrs in{hd + L.off[0], L.len[1] ? hd + L.off[1] : nullptr, hd + L.off[2], R->leader};
-  if (!mp) {  // the slots and the key table are read from the staging by the XOF
-    in.vk_slot = (const uint16_t*)(hd + L.slot_off);
-    in.vk_tab = (const uint4*)(hd + L.tab_off);
-  }
-  if (agg) R->seg = (const uint32_t*)(hd + L.seg_off);  // the fused XOF's segment check
-  // the leader prep shares (and the segment ids / accept bytes of the fix-up pass) on the copy
-  // stream, which starts after the run's slab is free (ws_acquire ordered that on st)
+  InPtrs in{};
   PullRanges pr{};
-  pr.src[0] = hd + L.off[3];
-  pr.dst[0] = R->leader;
-  pr.bytes[0] = L.len[3] * g.n;
-  if (agg) {
-    pr.src[1] = hd + L.seg_off;
-    pr.dst[1] = (uint8_t*)R->gseg;
-    pr.bytes[1] = 4 * (size_t)g.n;
-    pr.src[2] = hd + L.accept_off;
-    pr.dst[2] = R->gaccept;
-    pr.bytes[2] = g.n;
+  const PullRanges* pull = nullptr;
+  if (dma) {
+    gr->cs = ws_stream_get(lead->device);
+    if (!gr->cs) return fail(PRIO3_EDEVICE);
+    for (auto& ev : gr->ev)
+      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return fail(PRIO3_EDEVICE);
+    // the copies start once the run's slab is free (ws_acquire ordered that on st)
+    if (hipEventRecord(gr->ev[0], st) != hipSuccess ||
+        hipStreamWaitEvent(gr->cs, gr->ev[0], 0) != hipSuccess)
+      return fail(PRIO3_EDEVICE);
+    const uint8_t* hs = g.stg;
+    struct Cp {
+      void* dst;
+      size_t off, bytes;
+    } cps[] = {{R->nonces, L.off[0], L.len[0] * (size_t)g.n},
+               {R->pub, L.off[1], L.len[1] * (size_t)g.n},
+               {R->helper, L.off[2], L.len[2] * (size_t)g.n},
+               {R->leader, L.off[3], L.len[3] * (size_t)g.n},
+               {mp ? nullptr : R->vk_slot, L.slot_off, 2 * (size_t)g.n},
+               {mp ? nullptr : R->vk_tab, L.tab_off, 16 * (size_t)g.n_keys},
+               {agg ? R->gseg : nullptr, L.seg_off, 4 * (size_t)g.n},
+               {agg ? R->gaccept : nullptr, L.accept_off, (size_t)g.n}};
+    for (const Cp& c : cps)
+      if (c.dst && c.bytes &&
+          hipMemcpyAsync(c.dst, hs + c.off, c.bytes, hipMemcpyHostToDevice, gr->cs) != hipSuccess)
+        return fail(PRIO3_EDEVICE);
+    if (hipEventRecord(gr->ev[1], gr->cs) != hipSuccess ||
+        hipStreamWaitEvent(st, gr->ev[1], 0) != hipSuccess)
+      return fail(PRIO3_EDEVICE);
+    if (after && after->prep && hipStreamWaitEvent(st, after->prep, 0) != hipSuccess)
+      return fail(PRIO3_EDEVICE);
+    in = InPtrs{R->nonces, L.len[1] ? R->pub : nullptr, R->helper, R->leader};
+    if (!mp) {
+      in.vk_slot = (const uint16_t*)R->vk_slot;
+      in.vk_tab = (const uint4*)R->vk_tab;
+    }
+    if (agg) R->seg = R->gseg;
+  } else {
+    const uint8_t* hd = g.stg_dev;
+    in = InPtrs{hd + L.off[0], L.len[1] ? hd + L.off[1] : nullptr, hd + L.off[2], R->leader};
+    if (!mp) {  // the slots and the key table are read from the staging by the XOF
+      in.vk_slot = (const uint16_t*)(hd + L.slot_off);
+      in.vk_tab = (const uint4*)(hd + L.tab_off);
+    }
+    if (agg) R->seg = (const uint32_t*)(hd + L.seg_off);  // the fused XOF's segment check
+    // the leader prep shares (and the segment ids / accept bytes of the fix-up pass)
+    pr.src[0] = hd + L.off[3];
+    pr.dst[0] = R->leader;
+    pr.bytes[0] = L.len[3] * g.n;
+    if (agg) {
+      pr.src[1] = hd + L.seg_off;
+      pr.dst[1] = (uint8_t*)R->gseg;
+      pr.bytes[1] = 4 * (size_t)g.n;
+      pr.src[2] = hd + L.accept_off;
+      pr.dst[2] = R->gaccept;
+      pr.bytes[2] = g.n;
+    }
+    pull = &pr;
   }
   OutPtrs out{R->msgs, R->status};
-  rc = prepare_run(lead, R, in, out, st, fuse, false, &pr);
+  rc = prepare_run(lead, R, in, out, st, fuse, false, pull);
   if (agg) R->seg = R->gseg;
   if (rc) return fail(rc);
   // the executor may issue its next group once this group's prepare kernels are done
@@ -3546,6 +3593,11 @@ int engine_group_finish(GroupRun* gr, Run** run_out) {
   if (gr->prep) (void)hipEventDestroy(gr->prep);
   gr->prep = nullptr;
   const int dev = gr->lead->device;
+  // the copy stream's work is ordered before st's kernels (ev[1]), so it is done too
+  for (auto& ev : gr->ev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (gr->cs) ws_stream_put(dev, gr->cs);
+  gr->cs = nullptr;
   if (q != hipSuccess) {
     (void)hipGetLastError();
     run_release(gr->R, gr->st, true);
@@ -3779,7 +3831,8 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
               {"fp_round", &e->fp_round},          {"timing", &e->timing},
               {"coalesce", &e->coalesce},          {"experimental_fpvec", &e->experimental_fpvec},
               {"leader_fuse_acc", &e->leader_fuse_acc},
-              {"force_generic_query", &e->force_generic}, {"pair_max", &e->pair_max}};
+              {"force_generic_query", &e->force_generic}, {"pair_max", &e->pair_max},
+              {"group_dma", &e->group_dma}};
   for (auto& o : ints)
     if (!strcmp(key, o.name)) {
       *o.field = (int)value;

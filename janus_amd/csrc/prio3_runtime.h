@@ -107,11 +107,18 @@ void engine_vk(const prio3_engine* e, uint8_t out[16]);
 struct GroupRun {
   prio3_engine* lead = nullptr;
   hipStream_t st = nullptr;
+  hipStream_t cs = nullptr;   // copy stream of a DMA group (group_dma), returned at finish
+  hipEvent_t ev[2] = {nullptr, nullptr};  // DMA group: slab ready on st, inputs on the device
   Run* R = nullptr;
   hipEvent_t prep = nullptr;  // recorded after the prepare kernels
   int jobs = 0;
 };
-int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr);
+// after (nullable): the group running before this one; a DMA group's kernels wait for its
+// prepare kernels (the copies do not)
+int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr,
+                       const GroupRun* after = nullptr);
+// a group of n reports goes to the device by DMA (option group_dma; the executor issues it early)
+bool engine_group_dma(const prio3_engine* e, uint32_t n);
 bool engine_group_prepared(const GroupRun& gr);  // the prepare kernels are done
 bool engine_group_done(const GroupRun& gr);      // everything is done (non-blocking)
 int engine_group_finish(GroupRun* gr, Run** run_out);

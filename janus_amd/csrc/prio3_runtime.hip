@@ -347,13 +347,18 @@ struct Exec {
   // run for f of its predicted prepare time (its kernels then share the GPU with the running
   // group's, and its leader-share pull overlaps the running group's query); 1 = only when the
   // running group's prepare kernels are done.
-  static double issue_frac() {
-    static const double v = [] {
-      const char* s = getenv("JANUS_PRIO3_ISSUE_FRAC");
-      const double x = s ? atof(s) : 1.0;
-      return x > 0 ? std::min(x, 1.0) : 1.0;
-    }();
-    return v;
+  // A DMA group (engine_group_issue) is issued at JANUS_PRIO3_DMA_FRAC (default 0.3) of the
+  // running group's predicted prepare time: its input copies then run under the running group's
+  // compute, and its kernels wait for that group's prepare kernels (engine_group_issue's `after`).
+  static double env_frac(const char* name, double dflt) {
+    const char* s = getenv(name);
+    const double x = s ? atof(s) : dflt;
+    return x > 0 ? std::min(x, 1.0) : dflt;
+  }
+  static double issue_frac(bool dma) {
+    static const double pull = env_frac("JANUS_PRIO3_ISSUE_FRAC", 1.0);
+    static const double d = env_frac("JANUS_PRIO3_DMA_FRAC", 0.3);
+    return dma ? d : pull;
   }
   struct Pred {
     double ns_per_report = 0;
@@ -371,7 +376,7 @@ struct Exec {
         Group* g = take_locked(lk);
         lk.unlock();
         t0 = std::chrono::steady_clock::now();
-        const int rc = P::issue(device, g->st, g->stg, &hc);
+        const int rc = P::issue(device, g->st, g->stg, &hc, nullptr);
         lk.lock();
         if (rc != PRIO3_OK) {
           finish_locked(g, rc);
@@ -385,9 +390,14 @@ struct Exec {
       int rcn = PRIO3_OK;
       bool looked = false, tried_sleep = false, just_slept = false;
       auto tn = t0;  // when nxt was issued
+      auto tp = t0;  // when cur was seen prepared (an early-issued nxt's kernels start then)
       const uint32_t nrep = P::reports(cur->st);
       Pred& pr = preds[cur->key];
-      const double frac = issue_frac(), pred_ns = pr.ns_per_report * nrep;
+      // the next group goes early when it will be a DMA group (its copies overlap cur)
+      lk.lock();
+      const bool nxt_dma = !order.empty() && P::early(order.front()->st);
+      lk.unlock();
+      const double frac = issue_frac(nxt_dma), pred_ns = pr.ns_per_report * nrep;
       while (!P::done(hc)) {
         if (!tried_sleep) {
           tried_sleep = true;
@@ -408,12 +418,12 @@ struct Exec {
           if (!order.empty() && order.front()->writers == 0) nxt = take_locked(lk);
           lk.unlock();
           tn = std::chrono::steady_clock::now();
-          if (nxt) rcn = P::issue(device, nxt->st, nxt->stg, &hn);
+          if (nxt) rcn = P::issue(device, nxt->st, nxt->stg, &hn, &hc);
         }
         if (!looked && P::prepared(hc)) {
           looked = true;
-          const double el = std::chrono::duration<double, std::nano>(
-                                std::chrono::steady_clock::now() - t0).count();
+          tp = std::chrono::steady_clock::now();
+          const double el = std::chrono::duration<double, std::nano>(tp - t0).count();
           const double x = nrep ? el / nrep : 0;
           if (just_slept) {
             pr.ns_per_report *= 0.8;  // overslept: el is only an upper bound
@@ -426,7 +436,7 @@ struct Exec {
             if (!order.empty() && order.front()->writers == 0) nxt = take_locked(lk);
             lk.unlock();
             tn = std::chrono::steady_clock::now();
-            if (nxt) rcn = P::issue(device, nxt->st, nxt->stg, &hn);
+            if (nxt) rcn = P::issue(device, nxt->st, nxt->stg, &hn, nullptr);
           }
         }
         just_slept = false;
@@ -446,7 +456,9 @@ struct Exec {
         } else {
           cur = nxt;
           hc = hn;
-          t0 = tn;
+          // its prepare time counts from when its kernels could start: an early-issued group
+          // waited for cur's prepare kernels
+          t0 = looked ? std::max(tn, tp) : tn;
         }
       }
     }
@@ -616,7 +628,8 @@ struct PrepPolicy {
     GroupRun gr;
     State* s = nullptr;
   };
-  static int issue(int device, State& s, Staging& g, Handle* h) {
+  static bool early(const State& s) { return engine_group_dma(s.lead, s.n); }
+  static int issue(int device, State& s, Staging& g, Handle* h, const Handle* prev) {
     (void)device;
     GroupView v;
     if (s.align > 1) {  // whole waves: the group's tail padded like the gaps
@@ -632,7 +645,7 @@ struct PrepPolicy {
     v.jobs = (int)s.jobs;
     v.nseg = s.nseg;
     h->s = &s;
-    return engine_group_issue(s.lead, v, &h->gr);
+    return engine_group_issue(s.lead, v, &h->gr, prev ? &prev->gr : nullptr);
   }
   static bool prepared(const Handle& h) { return engine_group_prepared(h.gr); }
   static bool done(const Handle& h) { return engine_group_done(h.gr); }
@@ -684,7 +697,8 @@ struct AccPolicy {
   }
   static void stage(State& s, Staging& g, Job* j) { engine_acc_stage(j, g.p, s.L); }
   struct Handle {};  // the accumulate group runs to completion inside issue
-  static int issue(int device, State& s, Staging& g, Handle*) {
+  static bool early(const State&) { return false; }
+  static int issue(int device, State& s, Staging& g, Handle*, const Handle*) {
     return engine_acc_group(device, s.es, g.p, s.L, s.jobs, s.out);
   }
   static bool prepared(const Handle&) { return true; }

@@ -133,13 +133,18 @@ def test_concurrent_jobs_of_several_tasks_are_coalesced(name):
 
 
 @pytest.mark.parametrize("name", ["hist_256_c16", "hist_100_c10", "sumvec_8x10_c9", "count",
-                                  "sum32", "hist_256_c16/one_lane"])
+                                  "sum32", "hist_256_c16/one_lane", "hist_256_c16/dma",
+                                  "hist_256_c16/one_lane_dma", "sumvec_8x10_c9/dma",
+                                  "count/dma", "hist_100_c10/dma", "sum32/dma"])
 def test_combined_prepare_aggregate_jobs(name):
     """prio3_helper_prepare_aggregate_batch from 8 threads at once: 32 jobs of 100-500 reports
     for 4 tasks, each with its own segments (1-4, ids past n_segments included) and accept
     mask, some tampered, and every fourth job a plain prepare_batch + accumulate in the same
     groups.  Each job's messages, statuses, per-segment aggregates and counts equal the
-    restatement's, and the groups mixed jobs into fewer launches than jobs."""
+    restatement's, and the groups mixed jobs into fewer launches than jobs.  Variants: /dma sends
+    every group's inputs to the device by DMA on a copy stream, issued under the running group
+    (option group_dma -1), instead of the kernels pulling them over PCIe; /one_lane runs the
+    groups on the one-lane k_prep_h."""
     from oracle.oracle import Oracle
     name, _, variant = name.partition("/")
     cfg = CONFIGS[name]
@@ -148,8 +153,10 @@ def test_combined_prepare_aggregate_jobs(name):
     engines = [_engine(cfg, vk) for vk in vks]
     for e in engines:
         e.set_option("timing", 1)
-        if variant == "one_lane":  # groups on the one-lane k_prep_h instead of k_prep_hp
+        if variant.startswith("one_lane"):  # groups on the one-lane k_prep_h, not k_prep_hp
             e.set_option("pair_max", 0)
+        if variant.endswith("dma"):  # every group's inputs by DMA (option group_dma -1)
+            e.set_option("group_dma", -1)
         e.timing_reset()
     rng = np.random.default_rng(19)
     jobs = []
