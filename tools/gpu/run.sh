@@ -73,7 +73,7 @@ for step in "$@"; do
     timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$a1" -o run -- python3 bench.py --no-cpu-baseline --no-secondary $(args "$a2") > "$OUT/prof_$a1.json" 2> "$OUT/prof_$a1.err" || { tail -20 "$OUT/prof_$a1.err"; exit 1; }
     summ "$OUT/prof_$a1.json" ;;
   pmc)
-    timeout -s KILL 120 rocprofv3 --pmc $(args "$a2") -d "$OUT/pmc_$a1" -o run -- python3 bench.py --no-cpu-baseline --no-secondary --warmup 1 --steps 2 $(args "$a3") > "$OUT/pmc_$a1.json" 2> "$OUT/pmc_$a1.err" || { tail -20 "$OUT/pmc_$a1.err"; exit 1; }
+    timeout -s KILL 120 rocprofv3 --pmc $(args "$a2") --output-format csv -d "$OUT/pmc_$a1" -o run -- python3 bench.py --no-cpu-baseline --no-secondary --warmup 1 --steps 2 $(args "$a3") > "$OUT/pmc_$a1.json" 2> "$OUT/pmc_$a1.err" || { tail -20 "$OUT/pmc_$a1.err"; exit 1; }
     echo "pmc $a1 done" ;;
   lib)
     if [ "$a1" = base ]; then unset JANUS_PRIO3_LIB; else export JANUS_PRIO3_LIB=$PWD/janus_amd/variants/libjanus_prio3_$a1.so; fi
