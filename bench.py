@@ -900,7 +900,9 @@ def pipeline_main(args):
         o += part.shape[1]
     body = (be(0, 4).tobytes() + b"\x01" + be(n * rec, 4).tobytes() + R.tobytes())
     gen_s = time.perf_counter() - t0
-    lay = DJ.scan(body)
+    # the task's expected lengths (VDAF public share, X25519 Nenc, leader prep share): every record
+    # is checked against them, as the handler knows them from the task
+    lay = DJ.scan(body, public_share_len=32, enc_len=32, prep_share_len=L)
     assert lay.uniform and lay.n == n
     d_body = torch.zeros(len(body) + 8, dtype=torch.uint8, device=dev)
     d_body[:len(body)] = torch.frombuffer(bytearray(body), dtype=torch.uint8).to(dev)
