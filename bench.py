@@ -193,8 +193,11 @@ def main():
                          "(1M/8 per GPU), C4 Prio3Sum 32 (10M/8 per GPU)")
     ap.add_argument("--hpke-aead", type=int, choices=[1, 2, 3], default=1,
                     help="--role hpke: AEAD id (1 AES-128-GCM, 2 AES-256-GCM, 3 ChaCha20Poly1305)")
-    ap.add_argument("--hpke-kem", choices=["x25519", "p256"], default="x25519",
-                    help="--role hpke: DHKEM(X25519, HKDF-SHA256) or DHKEM(P-256, HKDF-SHA256)")
+    ap.add_argument("--hpke-kem", choices=["x25519", "p256", "x448", "p521"], default="x25519",
+                    help="--role hpke: DHKEM(X25519, HKDF-SHA256), DHKEM(P-256, HKDF-SHA256), "
+                         "DHKEM(X448, HKDF-SHA512) or DHKEM(P-521, HKDF-SHA512); the key "
+                         "schedule's KDF follows the KEM's (RFC 9180 suites of the reference's "
+                         "test vectors)")
     ap.add_argument("--leader-vdaf", choices=["hist", "sum32"], default="hist",
                     help="--role leader: Prio3Histogram(256,16) at 1Mi (default) or Prio3Sum(32) "
                          "at C4's 1.25M per GPU")
@@ -796,10 +799,13 @@ def hpke_main(args):
     t0 = time.perf_counter()
     aead = args.hpke_aead
     aead_name = {1: "AES-128-GCM", 2: "AES-256-GCM", 3: "ChaCha20Poly1305"}[aead]
-    kem = H.KEM_P256 if args.hpke_kem == "p256" else H.KEM_X25519
-    kem_name = "P256" if kem == H.KEM_P256 else "X25519"
+    kem = dict(x25519=H.KEM_X25519, p256=H.KEM_P256, x448=H.KEM_X448,
+               p521=H.KEM_P521)[args.hpke_kem]
+    kem_name = dict(x25519="X25519", p256="P256", x448="X448", p521="P521")[args.hpke_kem]
+    kdf = H.KDF_SHA512 if args.hpke_kem in ("x448", "p521") else H.KDF_SHA256
+    kdf_name = "HKDF-SHA512" if kdf == H.KDF_SHA512 else "HKDF-SHA256"
     d = H.make_batch_fast(uniq, 48, 32, seed=0x4A414E55, n_threads=cpu_threads(), aead=aead,
-                          kem=kem)
+                          kem=kem, kdf=kdf)
     gen_s = time.perf_counter() - t0
     reps = -(-n // uniq)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(np.concatenate([a] * reps)[:n])).to(dev)
@@ -807,7 +813,7 @@ def hpke_main(args):
     ids, times, pubs = T(d["report_ids"]), T(d["times"].view(np.int64)), T(d["pubs"])
     shares = torch.empty((n, 48), dtype=torch.uint8, device=dev)
     status = torch.empty(n, dtype=torch.uint8, device=dev)
-    op = G.HpkeOpener(d["skR"], d["pkR"], device=0, aead_id=aead, kem_id=kem)
+    op = G.HpkeOpener(d["skR"], d["pkR"], device=0, aead_id=aead, kem_id=kem, kdf_id=kdf)
 
     def step():
         op.open_input_shares_device(d["task_id"], enc, ct, ct_len, ids, times, pubs, shares,
@@ -830,10 +836,10 @@ def hpke_main(args):
                               RM.hpke_model(args.hpke_kem, aead), n, args.steps, elapsed)
     roofline.update(kernel="k_hpke_open", ms_avg=ms_avg)
     ok = int((status == 0).sum().item())
-    out = dict(metric=f"helper input shares HPKE-opened+decoded/sec ({kem_name}-HKDF-SHA256, "
+    out = dict(metric=f"helper input shares HPKE-opened+decoded/sec ({kem_name}-{kdf_name}, "
                       f"{aead_name})", value=value, unit="reports/s", n_gpus=1, steps=args.steps,
                warmup=args.warmup, ms_per_step=elapsed / args.steps * 1e3, higher_is_better=True,
-               scaling="weak", vs_baseline=None, dtype="u32 limbs (GF(2^255-19), GF(2^128), bytes)",
+               scaling="weak", vs_baseline=None, dtype="u32 limbs (the KEM field, GF(2^128), bytes)",
                data=f"synthetic: {uniq} distinct sealed input shares (oracle/OpenSSL, seeded) "
                     f"tiled x{reps}; generation {gen_s:.1f}s, not timed",
                config=dict(workload=f"DAP helper input share open: {kem_name} decap + HPKE key "
@@ -847,11 +853,11 @@ def hpke_main(args):
         csh, cst = H.open_input_shares(d["skR"], d["pkR"], d["task_id"], d["enc"][:m],
                                        d["ct"][:m], d["ct_len"][:m], d["report_ids"][:m],
                                        d["times"][:m], d["pubs"][:m], 48, n_threads=th,
-                                       aead=aead, kem=kem)
+                                       aead=aead, kem=kem, kdf=kdf)
         dt = time.perf_counter() - t0
         out["cpu_baseline"] = dict(value=m / dt, unit="reports/s", cores=th, kind="port",
                                    sample=f"{m} of the sealed input shares, OpenSSL 3.0 {kem_name} / "
-                                          f"HMAC-SHA256 / {aead_name}, {th} threads, {dt:.1f}s")
+                                          f"{kdf_name} / {aead_name}, {th} threads, {dt:.1f}s")
         out["speedup_vs_cpu"] = value / (m / dt)
         out["checks"]["cpu_gpu_parity_on_sample"] = bool(
             np.array_equal(shares[:m].cpu().numpy(), csh) and

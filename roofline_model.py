@@ -39,6 +39,13 @@ PRIM = dict(
     # GF(p256): 64 (36 for squares) v_mad_u64_u32 + as many carries, the column normalisation
     # (~30) and the NIST fast reduction as nine 8-word add/sub chains (~90)
     p256_mul=250, p256_sqr=200, p256_add=24,
+    # GF(2^448 - 2^224 - 1) in 16 x 28-bit limbs (x448_device.h): 256 (136 for squares)
+    # v_mad_u64_u32 into 64-bit columns, the 31-column carry (~95) and the 2^448 = 2^224 + 1 fold
+    fe448_mul=380, fe448_sqr=260, fe448_add=34, fe448_mul_small=50,
+    # GF(2^521 - 1) in 18 x 29-bit limbs (p521_device.h): 324 (171 + 18 doublings for squares)
+    # v_mad_u64_u32, the 35-column carry (~105), the 2^522 = 2 fold and a limb carry (~90)
+    p521_mul=520, p521_sqr=385, p521_add=72,
+    sha512_compress=4000,  # 80 rounds x ~33 (64-bit words on 32-bit halves) + 64 x ~22 schedule
     aes_round=36,      # T-table round: 16 byte extracts + 16 XORs + 4 key XORs (lookups are LDS)
     ghash_block=320,   # 4-bit table (Shoup) GF(2^128) multiply: 32 nibble steps x ~10
     chacha_block=960,  # 20 rounds x 4 quarter rounds x 12 (add, xor, v_alignbit rotate)
@@ -211,6 +218,21 @@ def hpke_model(kem: str, aead: int, pt_len: int = 48 + 8 + 32 + 16, aad_len: int
         inv = 254 * PRIM["fe25519_sqr"] + 11 * PRIM["fe25519_mul"]
         dh = 255 * step + inv + PRIM["fe25519_mul"] + 24
         compress = 19
+    elif kem == "x448":
+        # RFC 7748 ladder over 448 bits + the p - 2 inversion; HKDF-SHA512 (kem_context 112 B)
+        step = (5 * PRIM["fe448_mul"] + 4 * PRIM["fe448_sqr"] + PRIM["fe448_mul_small"] +
+                8 * PRIM["fe448_add"] + 64)
+        dh = 448 * step + 446 * PRIM["fe448_sqr"] + 14 * PRIM["fe448_mul"] + 40
+        compress = 21
+    elif kem == "p521":
+        M, S, A = PRIM["p521_mul"], PRIM["p521_sqr"], PRIM["p521_add"]
+        # ecdh_a3.h: a = -3 Jacobian formulas, fixed signed w = 4 window over the host-recoded
+        # key (131 digits), table 1P..8P by doublings and additions, affine output
+        dbl = 4 * M + 4 * S + 13 * A
+        add = 12 * M + 4 * S + 12 * A
+        inv = 520 * S + 13 * M
+        dh = 3 * M + 2 * S + 4 * A + 7 * add + 131 * (4 * dbl + add) + inv + M + S
+        compress = 23  # kem_context = enc || pkR is 266 bytes
     else:
         M, S, A = PRIM["p256_mul"], PRIM["p256_sqr"], PRIM["p256_add"]
         # the w = 4 window of p256_device.h (r03; a small multiple counted as two adds)
@@ -231,7 +253,7 @@ def hpke_model(kem: str, aead: int, pt_len: int = 48 + 8 + 32 + 16, aad_len: int
         rounds = 10 if aead == 1 else 14
         aead_ops = (ct_blocks + 2) * rounds * PRIM["aes_round"] + rounds * 20 + \
             (ct_blocks + -(-aad_len // 16) + 1) * PRIM["ghash_block"]
-    kdf = compress * PRIM["sha256_compress"]
+    kdf = compress * PRIM["sha512_compress" if kem in ("x448", "p521") else "sha256_compress"]
     return dict(dh=dh, kdf=kdf, aead=aead_ops, total=dh + kdf + aead_ops)
 
 
