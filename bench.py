@@ -1114,27 +1114,30 @@ def mp64_main(args):
 
 def fpvec_main(args):
     """Prio3FixedPointBoundedL2VecSum(length=10000, BitSize16) helper prepare+aggregate line
-    (BASELINE.json configs[4], C5: 100k reports; not the headline metric).  Inputs are the two
-    honest full-size reports of tests/golden/fpvec_l10000.npz (Python restatement,
-    tests/golden/gen_fpvec_l10000.py; ~35 s of CPU per report to generate) tiled to --reports
-    (default here 100k) and resident in HBM.  One step = prepare (k_xof, k_xof_slow, k_query_fp
+    (BASELINE.json configs[4], C5: 100k reports; not the headline metric).  Inputs are --reports
+    (default here 100k) distinct honest reports from the engine's device client
+    (prio3_client_generate_device: entries, shares, the two-gadget proof and the leader's
+    prepare_init on the GPU, pinned to oracle/fpvec_py.py gen_report by
+    tests/test_fpvec_client.py), resident in HBM.  One step = prepare (the XOF and query kernels
     per scratch sub-batch) + masked mod-p accumulate of the 10000-entry output shares.
     cpu_baseline: the compiled C restatement (oracle/prio3_oracle.c ORC_FPVEC) on a bounded
     sample of the same reports, every host thread; it also cross-checks the GPU on the sample."""
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
-    g = np.load(os.path.join(ROOT, "tests", "golden", "fpvec_l10000.npz"))
-    vk = bytes(g["verify_key"])
+    vk = bytes(range(0x70, 0x80))
     n = args.reports if args.reports != 1 << 20 else 100_000
-    honest = np.flatnonzero(g["status"] == 0)
-    idx = honest[np.arange(n) % len(honest)]
-    T = lambda a: torch.from_numpy(np.ascontiguousarray(a[idx])).to(dev)
-    nonces, pub, helper, lps = T(g["nonce"]), T(g["pub"]), T(g["helper"]), T(g["lps"])
     eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(10000, 16), vk, device=0,
                          allow_unpinned=True)
     for kv in args.opt:
         k, v = kv.split("=")
         eng.set_option(k, int(v))
+    t0 = time.perf_counter()
+    gen = eng.generate_reports_device(n, seed=0x4A414E5553000007, with_checks=True)
+    torch.cuda.synchronize()
+    gen_s = time.perf_counter() - t0
+    nonces, pub, helper, lps = (gen["nonces"], gen["public_shares"], gen["helper_shares"],
+                                gen["leader_prep_shares"])
+    gen_flags = int(gen["flags"].sum().item())
     msgs = torch.empty((n, 16), dtype=torch.uint8, device=dev)
     status = torch.empty(n, dtype=torch.uint8, device=dev)
     seg = torch.zeros(n, dtype=torch.int32, device=dev)
@@ -1158,16 +1161,22 @@ def fpvec_main(args):
     elapsed = time.perf_counter() - t0
     times = eng.timing()
     eng.set_option("timing", 0)
-    # checks: prepare messages and every step's aggregate against the fixtures
+    # check: the step's aggregate plus the leader's (the generator's leader output shares,
+    # summed by the combine kernel in two levels) unshards to the sum of all n entry vectors
     P128 = (1 << 128) - 28 * (1 << 64) + 1
-    ok_msgs = bool(np.array_equal(msgs.cpu().numpy(), g["prep_msg"][idx]))
-    outs = [np.frombuffer(g["out_shares"][k].tobytes(), dtype="<u8").reshape(-1, 2) for k in honest]
-    cnts = [int((idx == k).sum()) for k in honest]  # accumulate overwrites: one step's sum
-    a = agg.cpu().numpy()[0].tobytes()
-    ok_agg = True
-    for e in range(0, 10000, 997):  # sampled entries (full check lives in tests/test_fpvec.py)
-        want = sum(c * (int(o[e, 0]) | int(o[e, 1]) << 64) for c, o in zip(cnts, outs)) % P128
-        ok_agg &= int.from_bytes(a[16 * e:16 * e + 16], "little") == want
+    k1 = next(k for k in (1000, 500, 100, 10, 1) if n % k == 0)
+    part = torch.zeros((n // k1, eng.sz.agg_share_len), dtype=torch.uint8, device=dev)
+    pc = torch.zeros(n // k1, dtype=torch.int64, device=dev)
+    eng.combine_device(k1, n // k1, gen["leader_out_shares"],
+                       torch.zeros(n, dtype=torch.int64, device=dev), part, pc)
+    lagg = torch.zeros_like(agg)
+    eng.combine_device(n // k1, 1, part, pc, lagg, torch.zeros_like(cnt))
+    esum = gen["measurements"].sum(dim=0).cpu().tolist()
+    del part, gen["leader_out_shares"]
+    a, la = agg.cpu().numpy()[0].tobytes(), lagg.cpu().numpy()[0].tobytes()
+    dec = lambda b, e: int.from_bytes(b[16 * e:16 * e + 16], "little")
+    ok_unshard = all((dec(a, e) + dec(la, e)) % P128 == esum[e] + n * (1 << 15)
+                     for e in range(10000))
     cpu = None
     if not args.no_cpu_baseline:
         # the compiled C restatement (oracle/prio3_oracle.c ORC_FPVEC, pinned to the Python one
@@ -1177,7 +1186,9 @@ def fpvec_main(args):
         build()
         o = Oracle("fpvec", bits=16, length=10000)
         th = cpu_threads()
-        hostd = {k: g[k][idx] for k in ("nonce", "pub", "helper", "lps")}
+        mh = min(n, 8192)
+        hostd = dict(nonce=nonces[:mh].cpu().numpy(), pub=pub[:mh].cpu().numpy(),
+                     helper=helper[:mh].cpu().numpy(), lps=lps[:mh].cpu().numpy())
 
         # Janus's jobs hold up to 500 reports; a bounded sample of a few thousand 20-50 ms
         # reports must still give every worker thread jobs, so the jobs here are m / threads
@@ -1192,7 +1203,7 @@ def fpvec_main(args):
         dt1, _ = crun(4, 1)  # single core, per report
         probe = min(n, 2 * th)
         dt, _ = crun(probe)
-        m = int(min(n, max(probe, probe * args.cpu_seconds / max(dt, 1e-6))))
+        m = int(min(mh, max(probe, probe * args.cpu_seconds / max(dt, 1e-6))))
         dt, (cm, cs, cagg, ccnt) = crun(m)
         # op count of one report on one core: the Keccak-p[1600,12] permutations (share
         # expansion, the joint-rand part over the encoded share, prio's re-expansion in
@@ -1205,7 +1216,7 @@ def fpvec_main(args):
         muls = 3 * o.calls * (o.arity // 2) + o.fp_K1 * o.fp_C1
         model_ms = (perms * ns_perm + muls * ns_mul) / 1e6
         cpu = dict(value=m / dt, unit="reports/s", cores=th, kind="port",
-                   sample=f"{m} of the tiled fixture reports through the C restatement "
+                   sample=f"{m} of the device-generated reports through the C restatement "
                           f"(oracle/prio3_oracle.c, ORC_FPVEC), {th} threads, jobs of "
                           f"{max(1, min(500, m // th))}, {dt:.1f}s wall",
                    single_core_ms_per_report=dt1 / 4 * 1e3,
@@ -1232,8 +1243,8 @@ def fpvec_main(args):
                       "length=10000)", value=value, unit="reports/s", n_gpus=1, steps=args.steps,
                warmup=args.warmup, ms_per_step=elapsed / args.steps * 1e3, higher_is_better=True,
                scaling="weak", vs_baseline=None, dtype="u32 limbs (Field128 mod-p integer arithmetic)",
-               data=f"synthetic: {len(honest)} honest full-size reports (tests/golden/"
-                    f"fpvec_l10000.npz) tiled to {n}",
+               data=f"synthetic: {n} distinct honest reports from the device client (seeded; "
+                    f"generation {gen_s:.1f}s, not timed)",
                config=dict(workload="Prio3FixedPointBoundedL2VecSum length=10000 BitSize16 helper "
                                     "prepare+aggregate (configs[4], C5)", length=10000, bits=16,
                            reports=n),
@@ -1241,7 +1252,7 @@ def fpvec_main(args):
                roofline=model_roofline("fpvec", RM.helper_model(RM.instance(
                    "fpvec", eng.sz, bits=16, length=10000)), n, args.steps, elapsed),
                checks=dict(finished=int((status == 0).sum().item()), agg_count=int(cnt[0]),
-                           prep_msgs_match=ok_msgs, agg_sample_match=bool(ok_agg),
+                           generator_flags=gen_flags, unshard_equals_entry_sum=bool(ok_unshard),
                            cpu_gpu_parity_on_sample=cpu_parity if cpu else None),
                cpu_baseline=cpu,
                speedup_vs_cpu=(value / cpu["value"]) if cpu else None)

@@ -12,6 +12,8 @@
 // (prio FlpGeneric::prove, ProveShimGadget).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -48,28 +50,22 @@ DEV void expand_to(const DevParams& p, const uint32_t* dst2, const uint32_t* see
   }
 }
 
-// joint_rand_part = XOF(blind, dst(7), [agg_id] || nonce || enc(share)) -> 16 bytes, with the
-// share read back from an SoA scratch column set.
-template <class F>
-DEV void jr_part_scratch(const DevParams& p, const uint32_t* blind, uint32_t agg_id,
-                         const uint32_t* nonce, const void* src, uint32_t r, uint32_t* part) {
-  constexpr uint32_t WPE = F::ES / 4;  // words per element
-  const uint32_t nwords = p.meas_len * WPE;
-  auto Sw = [&](uint32_t u) -> uint32_t {
-    if (u >= nwords) return 0u;
-    const uint32_t e = u / WPE, k = u % WPE;
-    return ((const uint32_t*)src)[((size_t)e * p.ld + r) * WPE + k];
-  };
+// joint_rand_part = XOF(blind, dst(7), [agg_id] || nonce || enc(share)) -> 16 bytes; Sw(u) is
+// word u of the encoded share (0 past its end), asked for in increasing u.
+template <class Get>
+DEV void jr_part_words(const DevParams& p, const uint32_t* blind, uint32_t agg_id,
+                       const uint32_t* nonce, uint32_t share_bytes, Get&& Sw, uint32_t* part) {
   Msg pm;
   msg_zero(pm);
   msg_dst(pm, p.dst[7]);
   msg_bytes16(pm, 9, blind);
   msg_byte(pm, 25, agg_id);
   msg_bytes16(pm, 26, nonce);
-  const uint32_t L = 42 + p.meas_len * F::ES;
+  const uint32_t L = 42 + share_bytes;
   const uint32_t B = L / 168, rem = L % 168;
   KState s;
   kzero(s);
+  uint32_t prev = 0;  // word u - 1 of the share (the 16-bit funnel shift's low half)
   for (uint32_t b = 0; b <= B; b++) {
     uint32_t x[42];
 #pragma unroll
@@ -78,10 +74,13 @@ DEV void jr_part_scratch(const DevParams& p, const uint32_t* blind, uint32_t agg
       if (b == 0 && j < 10) {
         v = pm.w[j];
       } else if (b == 0 && j == 10) {
-        v = (pm.w[10] & 0xffffu) | (Sw(0) << 16);
+        prev = Sw(0);
+        v = (pm.w[10] & 0xffffu) | (prev << 16);
       } else {
         const uint32_t u = 42 * b + j - 11;
-        v = __builtin_amdgcn_alignbit(Sw(u + 1), Sw(u), 16);
+        const uint32_t nx = Sw(u + 1);
+        v = __builtin_amdgcn_alignbit(nx, prev, 16);
+        prev = nx;
       }
       if (b == B) {
         const uint32_t lo = 4 * j;
@@ -98,6 +97,19 @@ DEV void jr_part_scratch(const DevParams& p, const uint32_t* blind, uint32_t agg
     keccak_p12(s);
   }
   for (int k = 0; k < 4; k++) part[k] = kword(s, k);
+}
+
+// the same with the share read back from an SoA scratch column set
+template <class F>
+DEV void jr_part_scratch(const DevParams& p, const uint32_t* blind, uint32_t agg_id,
+                         const uint32_t* nonce, const void* src, uint32_t r, uint32_t* part) {
+  constexpr uint32_t WPE = F::ES / 4;  // words per element
+  const uint32_t nwords = p.meas_len * WPE;
+  jr_part_words(p, blind, agg_id, nonce, p.meas_len * F::ES, [&](uint32_t u) -> uint32_t {
+    if (u >= nwords) return 0u;
+    const uint32_t e = u / WPE, k = u % WPE;
+    return ((const uint32_t*)src)[((size_t)e * p.ld + r) * WPE + k];
+  }, part);
 }
 
 template <class F>
@@ -363,6 +375,394 @@ __global__ __launch_bounds__(64) void k_gen(DevParams p, uint64_t seed, uint64_t
 }
 
 // ====================================================================================
+// Prio3FixedPointBoundedL2VecSum client.  Report i of (seed, i): the stream
+// TurboSHAKE128("janus-amd-gen" || seed || i, D = 1) as for the other kinds gives the nonce and
+// the five seeds (helper measurement, helper proofs, helper blind, leader blind, prove rand);
+// entry e is the signed byte at stream offset 96 + e shifted right by gsh (the host picks the
+// smallest gsh with length * 2^(14 - 2 gsh) < 2^(2 bits - 2), so the claimed squared norm always
+// fits: |x| <= 2^(7 - gsh) / 2^(bits - 1)).  oracle/fpvec_py.py gen_report is the same in Python.
+// Three launches per chunk: k_fg_shares (lane per report: entries, the measurement share, both
+// joint-rand parts, joint and prove randomness), k_fg_prove (one 256-thread workgroup per report:
+// both gadget polynomials by NTTs in LDS) and k_fg_finish (lane per report: the leader's proofs
+// share); then the engine's own device leader prepare_init on the explicit leader shares.
+// ====================================================================================
+struct FgBufs {
+  int16_t* X;        // [m][length] entries
+  uint64_t* norm;    // [m] claimed squared norm (sum of X^2)
+  uint8_t* lin;      // [m][leader_share_len] leader input shares being built
+  void* jr;          // SoA [2][ld] joint randomness
+  void* pr;          // SoA [arity + chunk1][ld] prove randomness
+  uint8_t* proof;    // [m][proof_len] 16-byte elements
+  uint32_t gsh;
+};
+// Field128 tables of one gadget's NTTs (host-computed, device memory): w[i] = omega_P^i (i < P),
+// tw[m] = psi^m / P and ipsi[m] = psi^-m (m < P) for psi a primitive 2P-th root
+struct FgGadget {
+  const f128 *w, *tw, *ipsi;
+  f128 c2P;  // 1 / (2P)
+};
+
+// the report's stream word wi (non-decreasing), 168-byte blocks
+struct GenStream {
+  KState st;
+  uint32_t blk = 0;
+  DEV uint32_t word(uint32_t wi) {
+    while (wi >= 42 * (blk + 1)) {
+      keccak_p12(st);
+      blk++;
+    }
+    const uint32_t w = wi - 42 * blk;
+    uint32_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 42; q++)
+      if ((uint32_t)q == w) v = kword(st, q);
+    return v;
+  }
+};
+
+DEV void gen_stream_init(KState& st, uint64_t seed, uint64_t idx) {
+  kzero(st);
+  Msg m;
+  msg_zero(m);
+  const char tag[13] = {'j', 'a', 'n', 'u', 's', '-', 'a', 'm', 'd', '-', 'g', 'e', 'n'};
+  for (int i = 0; i < 13; i++) msg_byte(m, i, (uint8_t)tag[i]);
+  for (int i = 0; i < 8; i++) msg_byte(m, 13 + i, (uint32_t)(seed >> (8 * i)));
+  for (int i = 0; i < 8; i++) msg_byte(m, 21 + i, (uint32_t)(idx >> (8 * i)));
+  msg_absorb_final(st, m, 29);
+}
+
+// measurement bit i of the encoding (entry bits y_e = X_e + 2^(bits-1), little-endian, then the
+// claimed norm's 2 bits - 2 bits); cur / ce cache the current entry
+DEV uint32_t fg_mbit(const DevParams& p, const int16_t* X, uint64_t N, uint32_t i) {
+  const uint32_t nb = p.bits, nl = nb * p.length;
+  if (i >= nl) return (uint32_t)(N >> (i - nl)) & 1u;
+  const uint32_t y = (uint32_t)(int32_t)X[i / nb] + (1u << (nb - 1));
+  return (y >> (i % nb)) & 1u;
+}
+
+__global__ __launch_bounds__(64) void k_fg_shares(DevParams p, uint64_t seed, uint64_t first,
+                                                  GenOut go, FgBufs fb) {
+  typedef Fp128 F;
+  typedef f128 T;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= p.n) return;
+  const uint32_t M = p.meas_len, Ln = p.length, nb = p.bits;
+  uint32_t flag = 0;
+  GenStream gst;
+  gen_stream_init(gst.st, seed, first + r);
+  uint32_t nonce[4], k_hm[4], k_hp[4], k_hb[4], k_lb[4], k_pr[4];
+  for (int k = 0; k < 4; k++) {
+    nonce[k] = kword(gst.st, k);
+    k_hm[k] = kword(gst.st, 4 + k);
+    k_hp[k] = kword(gst.st, 8 + k);
+    k_hb[k] = kword(gst.st, 12 + k);
+    k_lb[k] = kword(gst.st, 16 + k);
+    k_pr[k] = kword(gst.st, 20 + k);
+  }
+  // entries: signed bytes from stream offset 96
+  int16_t* X = fb.X + (size_t)r * Ln;
+  uint64_t N = 0;
+  for (uint32_t e = 0; e < Ln; e++) {
+    const uint32_t B = 96 + e;
+    const int32_t v = (int32_t)(int8_t)(gst.word(B >> 2) >> (8 * (B & 3))) >> fb.gsh;
+    X[e] = (int16_t)v;
+    N += (uint64_t)((int64_t)v * v);
+    if (go.meas) go.meas[(size_t)r * Ln + e] = (uint64_t)(int64_t)v;
+  }
+  fb.norm[r] = N;
+  // helper measurement share hm = XOF(k_hm, dst(1), [1]) and the leader's lm = meas - hm,
+  // written encoded into the leader input share; the leader output share (the decoded entries
+  // of lm) on the way
+  uint8_t* lin = fb.lin + (size_t)r * p.leader_share_len;
+  {
+    KState s;
+    kzero(s);
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[1]);
+    msg_bytes16(m, 9, k_hm);
+    msg_byte(m, 25, 1);
+    msg_absorb_final(s, m, 26);
+    const uint32_t K = (M * 16 + 167) / 168;
+    uint32_t q0 = 0, q1 = 0;
+    T acc = F::zero(), pw = F::one();
+    for (uint32_t b = 0; b < K; b++) {
+      squeeze_block_with<F>(s, b, M, q0, q1, [&](uint32_t i, const uint32_t* w) {
+        const T h = F::from_words(w);
+        if (!F::lt_p(h)) flag = 1;
+        const T l = F::sub(F::from_u32(fg_mbit(p, X, N, i)), h);
+        F::store(lin, i, l);
+        if (i < nb * Ln) {
+          const uint32_t bt = i % nb;
+          if (bt == 0) {
+            acc = F::zero();
+            pw = F::one();
+          }
+          acc = F::add(acc, F::mul(l, pw));
+          pw = F::add(pw, pw);
+          if (bt == nb - 1 && go.leader_out) F::store(go.leader_out + (size_t)r * Ln * 16, i / nb, acc);
+        }
+      });
+      if (b + 1 < K) keccak_p12(s);
+    }
+  }
+  // joint-rand parts: the helper's over enc(hm) (the hm stream squeezed again word by word),
+  // the leader's over enc(lm) (read back from the leader share)
+  uint32_t part0[4], part1[4], jseed[4];
+  {
+    GenStream hs;
+    kzero(hs.st);
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[1]);
+    msg_bytes16(m, 9, k_hm);
+    msg_byte(m, 25, 1);
+    msg_absorb_final(hs.st, m, 26);
+    const uint32_t nw = M * 4;
+    jr_part_words(p, k_hb, 1, nonce, M * 16, [&](uint32_t u) -> uint32_t {
+      return u < nw ? hs.word(u) : 0u;
+    }, part1);
+    const uint32_t* lw = (const uint32_t*)lin;
+    jr_part_words(p, k_lb, 0, nonce, M * 16, [&](uint32_t u) -> uint32_t {
+      return u < nw ? lw[u] : 0u;
+    }, part0);
+  }
+  const uint32_t zero[4] = {0, 0, 0, 0};
+  seed_of<F>(p, 6, zero, part0, part1, jseed);
+  const uint8_t b1[1] = {1};
+  expand_to<F>(p, p.dst[3], jseed, b1, 1, p.jr_len, fb.jr, r, flag);
+  expand_to<F>(p, p.dst[4], k_pr, b1, 1, p.arity + p.chunk1, fb.pr, r, flag);
+  // public outputs; the leader share's blind goes after its proofs share (k_fg_finish)
+  *(uint4*)(go.nonces + 16 * (size_t)r) = make_uint4(nonce[0], nonce[1], nonce[2], nonce[3]);
+  uint8_t* hsh = go.helper + (size_t)r * p.helper_share_len;
+  *(uint4*)hsh = make_uint4(k_hm[0], k_hm[1], k_hm[2], k_hm[3]);
+  *(uint4*)(hsh + 16) = make_uint4(k_hp[0], k_hp[1], k_hp[2], k_hp[3]);
+  *(uint4*)(hsh + 32) = make_uint4(k_hb[0], k_hb[1], k_hb[2], k_hb[3]);
+  uint8_t* pb = go.pub + (size_t)r * p.public_share_len;
+  *(uint4*)pb = make_uint4(part0[0], part0[1], part0[2], part0[3]);
+  *(uint4*)(pb + 16) = make_uint4(part1[0], part1[1], part1[2], part1[3]);
+  *(uint4*)(lin + (size_t)(M + p.proof_len) * 16) = make_uint4(k_lb[0], k_lb[1], k_lb[2], k_lb[3]);
+  if (go.flags) go.flags[r] = (uint8_t)flag;
+}
+
+// In-place transforms of the two LDS vectors V0, V1 of P elements by the 256 threads.
+// DIF with omega^-1: natural order in, P x the inverse DFT out in bit-reversed order.
+DEV void fg_dif_inv(f128* V0, f128* V1, uint32_t P, const f128* w, uint32_t t) {
+  typedef Fp128 F;
+  for (uint32_t len = P >> 1; len >= 1; len >>= 1) {
+    for (uint32_t bf = t; bf < (P >> 1); bf += 256) {
+      const uint32_t j = bf % len, i0 = (bf / len) * 2 * len + j, i1 = i0 + len;
+      const uint32_t e = j * (P / (2 * len));
+      const f128 tw = w[e ? P - e : 0];
+      f128 u = V0[i0], v = V0[i1];
+      V0[i0] = F::add(u, v);
+      V0[i1] = F::mul(F::sub(u, v), tw);
+      u = V1[i0];
+      v = V1[i1];
+      V1[i0] = F::add(u, v);
+      V1[i1] = F::mul(F::sub(u, v), tw);
+    }
+    __syncthreads();
+  }
+}
+// DIT with omega: bit-reversed order in, the DFT out in natural order
+DEV void fg_dit_fwd(f128* V0, f128* V1, uint32_t P, const f128* w, uint32_t t) {
+  typedef Fp128 F;
+  for (uint32_t len = 1; len < P; len <<= 1) {
+    for (uint32_t bf = t; bf < (P >> 1); bf += 256) {
+      const uint32_t j = bf % len, i0 = (bf / len) * 2 * len + j, i1 = i0 + len;
+      const f128 tw = w[j * (P / (2 * len))];
+      f128 u = V0[i0], v = F::mul(V0[i1], tw);
+      V0[i0] = F::add(u, v);
+      V0[i1] = F::sub(u, v);
+      u = V1[i0];
+      v = F::mul(V1[i1], tw);
+      V1[i0] = F::add(u, v);
+      V1[i1] = F::sub(u, v);
+    }
+    __syncthreads();
+  }
+}
+
+// One gadget's polynomial, FlpGeneric::prove (VDAF-08 7.3.3.1) on P-point wire polynomials:
+// G(psi^(2k)) = the gadget of the wire values at omega^k (computed directly), G(psi^(2k+1)) =
+// the gadget of the wires' coset evaluations DFT(psi^m c_m) with c = IDFT(wire values); then the
+// 2P - 1 coefficients g_m = (e_m + psi^-m o_m) / 2, g_(m+P) = (e_m - psi^-m o_m) / 2 from
+// e = IDFT(even values), o = IDFT(odd values).  val(j, k, a, b) fills wire pair j at point k
+// (gadget 1 takes its wires two at a time, j and j + 1); gad(acc, a, b) adds the gadget term of
+// one point.  PPT = points per thread (P <= 256 PPT).
+template <int PPT, class Val, class Gad>
+DEV void fg_gadget(uint32_t P, uint32_t logP, uint32_t npairs, const FgGadget& G, f128* V0,
+                   f128* V1, uint32_t t, Val&& val, Gad&& gad, f128* coef_out, uint32_t glen) {
+  typedef Fp128 F;
+  mac128 PE[PPT], PO[PPT];
+#pragma unroll
+  for (int q = 0; q < PPT; q++) {
+    mac_zero(PE[q]);
+    mac_zero(PO[q]);
+  }
+  for (uint32_t j = 0; j < npairs; j++) {
+#pragma unroll
+    for (int q = 0; q < PPT; q++) {
+      const uint32_t k = t + 256 * q;
+      if (k < P) {
+        f128 a, b;
+        val(j, k, q, a, b);
+        V0[k] = a;
+        V1[k] = b;
+        gad(PE[q], a, b);
+      }
+    }
+    __syncthreads();
+    fg_dif_inv(V0, V1, P, G.w, t);
+    for (uint32_t s = t; s < P; s += 256) {  // coset twist psi^m / P of coefficient m
+      const f128 tw = G.tw[bitrev(s, logP)];
+      V0[s] = F::mul(V0[s], tw);
+      V1[s] = F::mul(V1[s], tw);
+    }
+    __syncthreads();
+    fg_dit_fwd(V0, V1, P, G.w, t);
+#pragma unroll
+    for (int q = 0; q < PPT; q++) {
+      const uint32_t k = t + 256 * q;
+      if (k < P) gad(PO[q], V0[k], V1[k]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < PPT; q++) {
+    const uint32_t k = t + 256 * q;
+    if (k < P) {
+      V0[k] = mac_reduce_f(PE[q]);
+      V1[k] = mac_reduce_f(PO[q]);
+    }
+  }
+  __syncthreads();
+  fg_dif_inv(V0, V1, P, G.w, t);
+  for (uint32_t m = t; m < P; m += 256) {
+    const f128 e = V0[bitrev(m, logP)], o = F::mul(V1[bitrev(m, logP)], G.ipsi[m]);
+    coef_out[m] = F::mul(F::add(e, o), G.c2P);
+    if (m + P < glen) coef_out[m + P] = F::mul(F::sub(e, o), G.c2P);
+  }
+  __syncthreads();
+}
+
+template <int PPT>
+__global__ __launch_bounds__(256) void k_fg_prove(DevParams p, FgBufs fb, FgGadget G0,
+                                                  FgGadget G1, f128 twon) {
+  typedef Fp128 F;
+  typedef f128 T;
+  extern __shared__ f128 lds[];
+  const uint32_t r = blockIdx.x, t = threadIdx.x;
+  const uint32_t Pm = p.P > p.P1 ? p.P : p.P1;
+  f128* V0 = lds;
+  f128* V1 = lds + Pm;
+  const size_t ld = p.ld;
+  const uint32_t M = p.meas_len, Ln = p.length, nb = p.bits;
+  const uint32_t C0 = p.chunk, K0 = p.calls, A0 = p.arity, C1 = p.chunk1, K1 = p.calls1;
+  const int16_t* X = fb.X + (size_t)r * Ln;
+  const uint64_t N = fb.norm[r];
+  f128* proof = (f128*)(fb.proof + (size_t)r * p.proof_len * 16);
+  auto prv = [&](uint32_t w) { return F::load(fb.pr, (size_t)w * ld + r); };
+  const T r0 = F::load(fb.jr, r);
+  const T neg1 = F::sub(F::zero(), F::one());
+  // gadget 0: ParallelSum(Mul, C0) over the range-check wires; rp[q] = r0^(c C0 + j + 1) for
+  // call c = k - 1 of this thread's point k (valid(): the power advances per element)
+  T rp[PPT];
+  {
+    T rc = F::one(), sq = r0;
+    for (uint32_t e = C0; e; e >>= 1) {
+      if (e & 1) rc = F::mul(rc, sq);
+      if (e > 1) sq = F::mul(sq, sq);
+    }
+#pragma unroll
+    for (int q = 0; q < PPT; q++) {
+      const uint32_t k = t + 256 * q;
+      T x = r0, b = rc;
+      for (uint32_t e = k ? k - 1 : 0; e; e >>= 1) {
+        if (e & 1) x = F::mul(x, b);
+        if (e > 1) b = F::mul(b, b);
+      }
+      rp[q] = x;
+    }
+  }
+  for (uint32_t w = t; w < A0; w += 256) proof[w] = prv(w);
+  fg_gadget<PPT>(
+      p.P, p.logP, C0, G0, V0, V1, t,
+      [&](uint32_t j, uint32_t k, int q, T& a, T& b) {
+        if (k == 0) {
+          a = prv(2 * j);
+          b = prv(2 * j + 1);
+        } else if (k <= K0) {
+          const uint32_t i = (k - 1) * C0 + j;
+          const uint32_t mi = i < M ? fg_mbit(p, X, N, i) : 0u;
+          a = mi ? rp[q] : F::zero();
+          b = mi ? F::zero() : neg1;
+          rp[q] = F::mul(rp[q], r0);
+        } else {
+          a = F::zero();
+          b = F::zero();
+        }
+      },
+      [&](mac128& acc, const T& a, const T& b) { mac_add(acc, a, b); }, proof + A0, p.glen);
+  // gadget 1: ParallelSum(PolyEval(y^2 - 2^n y), C1) over the decoded entries, two wires
+  // (j, j + 1) per pass; a missing wire is zero and adds q(0) = 0
+  const uint32_t o1 = A0 + p.glen;
+  for (uint32_t w = t; w < C1; w += 256) proof[o1 + w] = prv(A0 + w);
+  const uint32_t half = 1u << (nb - 1);
+  auto wire1 = [&](uint32_t j, uint32_t k) -> T {
+    if (j >= C1) return F::zero();
+    if (k == 0) return prv(A0 + j);
+    if (k > K1) return F::zero();
+    const uint32_t idx = (k - 1) * C1 + j;
+    return idx < Ln ? F::from_u32((uint32_t)(int32_t)X[idx] + half) : F::zero();
+  };
+  fg_gadget<PPT>(
+      p.P1, p.logP1, (C1 + 1) / 2, G1, V0, V1, t,
+      [&](uint32_t j, uint32_t k, int, T& a, T& b) {
+        a = wire1(2 * j, k);
+        b = wire1(2 * j + 1, k);
+      },
+      [&](mac128& acc, const T& a, const T& b) {
+        mac_add(acc, a, F::sub(a, twon));
+        mac_add(acc, b, F::sub(b, twon));
+      },
+      proof + o1 + C1, p.glen1);
+}
+
+// the leader's proofs share = proof - XOF(k_hp, dst(2), [1, 1]), after lm in the leader share
+__global__ __launch_bounds__(64) void k_fg_finish(DevParams p, GenOut go, FgBufs fb) {
+  typedef Fp128 F;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= p.n) return;
+  uint32_t flag = go.flags ? go.flags[r] : 0u;
+  uint32_t k_hp[4];
+  load16(go.helper + (size_t)r * p.helper_share_len + 16, k_hp);
+  const uint8_t* prf = fb.proof + (size_t)r * p.proof_len * 16;
+  uint8_t* lp = fb.lin + (size_t)r * p.leader_share_len + (size_t)p.meas_len * 16;
+  KState s;
+  kzero(s);
+  Msg m;
+  msg_zero(m);
+  msg_dst(m, p.dst[2]);
+  msg_bytes16(m, 9, k_hp);
+  msg_byte(m, 25, 1);
+  msg_byte(m, 26, 1);
+  msg_absorb_final(s, m, 27);
+  const uint32_t PL = p.proof_len, K = (PL * 16 + 167) / 168;
+  uint32_t q0 = 0, q1 = 0;
+  for (uint32_t b = 0; b < K; b++) {
+    squeeze_block_with<F>(s, b, PL, q0, q1, [&](uint32_t i, const uint32_t* w) {
+      const f128 h = F::from_words(w);
+      if (!F::lt_p(h)) flag = 1;
+      F::store(lp, i, F::sub(F::load(prf, i), h));
+    });
+    if (b + 1 < K) keccak_p12(s);
+  }
+  if (go.flags) go.flags[r] = (uint8_t)flag;
+}
+
+// ====================================================================================
 // Host ABI
 // ====================================================================================
 #define GCHK(x)                                                                       \
@@ -498,6 +898,12 @@ __global__ __launch_bounds__(256) void k_leader_next(DevParams p, const uint8_t*
   }
 }
 
+// a leader prepare_init that did not finish marks the generated report unusable
+__global__ void k_fg_status(const uint8_t* status, uint8_t* flags, uint32_t n) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < n && status[r] != PRIO3_STATUS_FINISHED) flags[r] |= 2;
+}
+
 extern "C" int launch_leader_init(const DevParams& dp, const uint8_t* d_nonces, const uint8_t* d_pub,
                        const uint8_t* d_lshares, const Scratch& sc, uint8_t* d_prep_shares,
                        uint8_t* d_status, hipStream_t st) {
@@ -521,10 +927,152 @@ extern "C" int launch_leader_next(const DevParams& dp, const uint8_t* d_prep_msg
   return hipGetLastError() == hipSuccess ? PRIO3_OK : PRIO3_EDEVICE;
 }
 
+static f128 h128x(u128 x) {
+  f128 r;
+  for (int k = 0; k < 4; k++) r.w[k] = (uint32_t)(x >> (32 * k));
+  return r;
+}
 static f128 h128(const uint32_t* w) {
   f128 r;
   for (int k = 0; k < 4; k++) r.w[k] = w[k];
   return r;
+}
+
+// FPVec generator (k_fg_*): chunks of reports through the three kernels, then the engine's device
+// leader prepare_init on the chunk's leader input shares (so e->mu is not held here: that entry
+// point takes it).  Needs the engine's experimental_fpvec opt-in like every FPVec entry point.
+static int gen_fpvec(prio3_engine* e, uint32_t n, uint64_t seed, uint64_t first_index,
+                     uint8_t* d_nonces, uint8_t* d_pub, uint8_t* d_helper, uint8_t* d_lps,
+                     uint64_t* d_meas, uint8_t* d_lout, uint8_t* d_flags, uint8_t* d_lin,
+                     hipStream_t st) {
+  DevParams p = e->dp;
+  if (!d_pub) return PRIO3_EINVAL;
+  const uint32_t Pm = std::max(p.P, p.P1);
+  if (Pm > 1024 || p.logP + 1 > MAX_ROOTS || p.logP1 + 1 > MAX_ROOTS) return PRIO3_EUNSUPPORTED;
+  if (hipSetDevice(e->device) != hipSuccess) return PRIO3_EDEVICE;
+  // entries are signed bytes >> gsh, |X| <= 2^(7 - gsh): the claimed norm must stay below
+  // 2^(2 bits - 2) (FixedPointBoundedL2VecSum's bound, ||x|| < 1)
+  uint32_t gsh = 0;
+  while (gsh < 7 && std::ldexp((double)p.length, 14 - 2 * (int)gsh) >= std::ldexp(1.0, 2 * (int)p.bits - 2))
+    gsh++;
+  // NTT tables of both gadgets (one device buffer)
+  auto word4 = [](u128 x, uint32_t* w) {
+    for (int k = 0; k < 4; k++) w[k] = (uint32_t)(x >> (32 * k));
+  };
+  auto rootof = [&](uint32_t l) {
+    u128 x = 0;
+    for (int k = 0; k < 4; k++) x |= (u128)p.roots128[l][k] << (32 * k);
+    return x;
+  };
+  std::vector<uint32_t> tab;
+  struct Off { size_t w, tw, ipsi; u128 c2P; } offs[2];
+  for (int g = 0; g < 2; g++) {
+    const uint32_t P = g ? p.P1 : p.P, lg = g ? p.logP1 : p.logP;
+    const u128 om = rootof(lg), psi = rootof(lg + 1), ipsi = hpow(psi, HP128 - 2, HP128);
+    const u128 iP = hpow(P, HP128 - 2, HP128);
+    offs[g].c2P = hpow(2 * (u128)P, HP128 - 2, HP128);
+    uint32_t w4[4];
+    offs[g].w = tab.size() / 4;
+    u128 x = 1;
+    for (uint32_t i = 0; i < P; i++, x = hmul(x, om, HP128)) {
+      word4(x, w4);
+      tab.insert(tab.end(), w4, w4 + 4);
+    }
+    offs[g].tw = tab.size() / 4;
+    x = iP;
+    for (uint32_t i = 0; i < P; i++, x = hmul(x, psi, HP128)) {
+      word4(x, w4);
+      tab.insert(tab.end(), w4, w4 + 4);
+    }
+    offs[g].ipsi = tab.size() / 4;
+    x = 1;
+    for (uint32_t i = 0; i < P; i++, x = hmul(x, ipsi, HP128)) {
+      word4(x, w4);
+      tab.insert(tab.end(), w4, w4 + 4);
+    }
+  }
+  // chunk: at most 40 % of free HBM for the per-report buffers (the leader prepare's own
+  // sub-batched scratch takes what is left)
+  const size_t A = p.arity + p.chunk1;
+  const size_t per = 2 * (size_t)p.length + 8 + p.leader_share_len + 16 * (size_t)p.jr_len +
+                     16 * A + 16 * (size_t)p.proof_len + 1 + 64;
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) return PRIO3_EDEVICE;
+  size_t chunk = std::min<size_t>({(size_t)n, (size_t)16384, std::max<size_t>(64, (size_t)(0.4 * (double)fr) / per)});
+  chunk = (chunk + 63) & ~(size_t)63;
+  std::vector<void*> bufs;
+  int rc = PRIO3_OK;
+  auto alloc = [&](size_t bytes) -> void* {
+    void* b = nullptr;
+    if (hipMalloc(&b, std::max<size_t>(bytes, 256)) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    bufs.push_back(b);
+    return b;
+  };
+  FgBufs fb;
+  fb.gsh = gsh;
+  fb.X = (int16_t*)alloc(2 * (size_t)p.length * chunk);
+  fb.norm = (uint64_t*)alloc(8 * chunk);
+  fb.lin = (uint8_t*)alloc((size_t)p.leader_share_len * chunk);
+  fb.jr = alloc(16 * (size_t)p.jr_len * chunk);
+  fb.pr = alloc(16 * A * chunk);
+  fb.proof = (uint8_t*)alloc(16 * (size_t)p.proof_len * chunk);
+  uint8_t* stat = (uint8_t*)alloc(chunk);
+  f128* dtab = (f128*)alloc(4 * tab.size());
+  if (!fb.X || !fb.norm || !fb.lin || !fb.jr || !fb.pr || !fb.proof || !stat || !dtab) {
+    rc = PRIO3_EDEVICE;  // out of device memory
+  } else if (hipMemcpyAsync(dtab, tab.data(), 4 * tab.size(), hipMemcpyHostToDevice, st) !=
+             hipSuccess) {
+    rc = PRIO3_EDEVICE;
+  }
+  FgGadget G[2];
+  for (int g = 0; g < 2 && rc == PRIO3_OK; g++) {
+    G[g].w = dtab + offs[g].w;
+    G[g].tw = dtab + offs[g].tw;
+    G[g].ipsi = dtab + offs[g].ipsi;
+    G[g].c2P = h128x(offs[g].c2P);
+  }
+  const f128 twon = h128x((u128)1 << p.bits);
+  const uint32_t ppt = (Pm + 255) / 256;
+  const size_t lds = 2 * (size_t)Pm * 16;
+  for (uint64_t off = 0; off < n && rc == PRIO3_OK; off += chunk) {
+    const uint32_t m = (uint32_t)std::min<uint64_t>(chunk, n - off);
+    DevParams q = p;
+    q.n = m;
+    q.ld = (uint32_t)chunk;
+    GenOut go{};
+    go.nonces = d_nonces + 16 * off;
+    go.pub = d_pub + (size_t)p.public_share_len * off;
+    go.helper = d_helper + (size_t)p.helper_share_len * off;
+    go.leader_out = d_lout ? d_lout + (size_t)p.out_len * 16 * off : nullptr;
+    go.meas = d_meas ? d_meas + (size_t)p.length * off : nullptr;
+    go.flags = d_flags ? d_flags + off : nullptr;
+    k_fg_shares<<<(m + 63) / 64, 64, 0, st>>>(q, seed, first_index + off, go, fb);
+    if (ppt == 1)
+      k_fg_prove<1><<<m, 256, lds, st>>>(q, fb, G[0], G[1], twon);
+    else if (ppt == 2)
+      k_fg_prove<2><<<m, 256, lds, st>>>(q, fb, G[0], G[1], twon);
+    else
+      k_fg_prove<4><<<m, 256, lds, st>>>(q, fb, G[0], G[1], twon);
+    k_fg_finish<<<(m + 63) / 64, 64, 0, st>>>(q, go, fb);
+    if (hipGetLastError() != hipSuccess) {
+      rc = PRIO3_EDEVICE;
+      break;
+    }
+    rc = prio3_device_leader_prepare_init(e, m, go.nonces, go.pub, fb.lin,
+                                          d_lps + (size_t)p.prep_share_len * off, stat, st);
+    if (rc != PRIO3_OK) break;
+    if (d_flags) k_fg_status<<<(m + 255) / 256, 256, 0, st>>>(stat, d_flags + off, m);
+    if (d_lin && hipMemcpyAsync(d_lin + (size_t)p.leader_share_len * off, fb.lin,
+                                (size_t)p.leader_share_len * m, hipMemcpyDeviceToDevice,
+                                st) != hipSuccess)
+      rc = PRIO3_EDEVICE;
+  }
+  if (hipStreamSynchronize(st) != hipSuccess && rc == PRIO3_OK) rc = PRIO3_EDEVICE;
+  for (auto b : bufs) (void)hipFree(b);
+  return rc;
 }
 
 extern "C" int prio3_client_generate_device(prio3_engine* e, uint32_t n, uint64_t seed,
@@ -534,10 +1082,13 @@ extern "C" int prio3_client_generate_device(prio3_engine* e, uint32_t n, uint64_
                                             uint64_t* d_measurements,
                                             uint8_t* d_leader_out_shares, uint8_t* d_flags,
                                             uint8_t* d_leader_input_shares, void* stream) {
-  if (e && (e->dp.kind == PRIO3_SUMVEC_F64_MP || e->dp.kind == PRIO3_FPVEC_BOUNDED_L2))
-    return PRIO3_EUNSUPPORTED;  // TurboSHAKE single-gadget clients only
+  if (e && e->dp.kind == PRIO3_SUMVEC_F64_MP) return PRIO3_EUNSUPPORTED;  // not a TurboSHAKE client
   if (!e || !d_nonces || !d_helper_shares || !d_leader_prep_shares) return PRIO3_EINVAL;
   if (n == 0) return PRIO3_OK;
+  if (e->dp.kind == PRIO3_FPVEC_BOUNDED_L2)
+    return gen_fpvec(e, n, seed, first_index, d_nonces, d_public_shares, d_helper_shares,
+                     d_leader_prep_shares, d_measurements, d_leader_out_shares, d_flags,
+                     d_leader_input_shares, (hipStream_t)stream);
   std::lock_guard<std::mutex> lk(e->mu);
   if (hipSetDevice(e->device) != hipSuccess) return PRIO3_EDEVICE;
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)

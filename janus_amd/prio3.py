@@ -542,7 +542,10 @@ class HelperEngine:
         """Honest synthetic reports generated on the GPU (shard + leader prepare_init).
 
         Returns torch uint8 tensors on this engine's device (plus measurements / leader
-        output shares / flags when ``with_checks``)."""
+        output shares / flags when ``with_checks``).  Every TurboSHAKE instance, including
+        FixedPointBoundedL2VecSum (its prover runs on the device too; the engine needs the
+        allow_unpinned opt-in); not the HMAC-SHA256/AES-128 multiproof VDAF.  Report i is
+        derived from (seed, first_index + i) exactly as oracle's generators derive it."""
         import torch
         sz = self.sz
         dev = torch.device("cuda", self.device)
@@ -552,7 +555,9 @@ class HelperEngine:
                    helper_shares=torch.empty((n, sz.helper_share_len), **u8),
                    leader_prep_shares=torch.empty((n, sz.prep_share_len), **u8))
         if with_checks:
-            mstride = self.vdaf.length if self.vdaf.kind == PRIO3_SUMVEC else 1
+            # SumVec: the entries; FPVec: the signed fixed-point entries X (x = X / 2^(bits-1))
+            mstride = (self.vdaf.length if self.vdaf.kind in (PRIO3_SUMVEC, PRIO3_FPVEC_BOUNDED_L2)
+                       else 1)
             out["measurements"] = torch.empty((n, mstride), dtype=torch.int64, device=dev)
             out["leader_out_shares"] = torch.empty((n, sz.agg_share_len), **u8)
             out["flags"] = torch.zeros(n, **u8)

@@ -280,3 +280,34 @@ class FpVecType:
         f1 = verifier[2 + self.A0:2 + self.A0 + self.A1]
         p1 = verifier[2 + self.A0 + self.A1]
         return self.gadget0(f0) == p0 and self.gadget1(f1) == p1
+
+
+def gen_gsh(length: int, bits: int) -> int:
+    """The generator's entry shift: entries are signed bytes >> gsh, so |X| <= 2^(7 - gsh); the
+    smallest gsh with length * 2^(14 - 2 gsh) < 2^(2 bits - 2) keeps the squared norm in range."""
+    s = 0
+    while s < 7 and length * 2 ** (14 - 2 * s) >= 2 ** (2 * bits - 2):
+        s += 1
+    return s
+
+
+def gen_report(vk: bytes, length: int, bits: int, seed: int, idx: int) -> dict:
+    """Report idx of the synthetic client's seeded stream, as the device generator derives it
+    (janus_amd/csrc/prio3_client.hip k_fg_*): stream = TurboSHAKE128("janus-amd-gen" || seed ||
+    idx, D = 1) gives the nonce (16 bytes), the five shard seeds (80 bytes: helper measurement,
+    helper proofs, helper blind, leader blind, prove randomness) and one signed byte per entry
+    (>> gen_gsh) from offset 96; then Prio3 shard and the leader's prepare_init (agg_id 0).
+    Pure Python: seconds per report at length 100, about a minute at 10000."""
+    from oracle.prio3_py import Prio3, turboshake128
+    typ = FpVecType(length, bits)
+    P = Prio3(typ)
+    msg = b"janus-amd-gen" + seed.to_bytes(8, "little") + idx.to_bytes(8, "little")
+    stream = turboshake128(msg, 1, 96 + length)
+    nonce, rand = stream[:16], stream[16:96]
+    sh = gen_gsh(length, bits)
+    X = [((b - 256) if b >= 128 else b) >> sh for b in stream[96:96 + length]]
+    public, leader, helper = P.shard(X, nonce, rand)
+    _, lps, trace = P.prepare_init(vk, 0, nonce, public, leader)
+    out = typ.truncate(trace["meas"])
+    return dict(nonce=nonce, public=public, helper=helper, leader=leader, lps=lps, X=X,
+                leader_out=b"".join(P.F.enc(x) for x in out))

@@ -15,8 +15,9 @@ transcript tests compare with prio (core/src/test_util/mod.rs:86-232).
   C3 Prio3SumVec(8, 1000, 63), 125k (one GPU's 1/8)  oracle parity on an 8,192-report subset;
                                                      the whole batch by unshard (test_gpu_fullsize)
   C4 Prio3Sum(32), 1.25M (one GPU's 1/8)             full oracle parity
-  C5 FixedPointBoundedL2VecSum(10000), 100k          the fixture reports tiled to 100k: every
-                                                     prepare message and the whole aggregate
+  C5 FixedPointBoundedL2VecSum(10000), 100k          tests/test_fpvec_client.py: 100k distinct
+                                                     device-generated reports, unshard over all
+                                                     of them and the C restatement on a subset
 """
 import os
 
@@ -181,43 +182,3 @@ def test_c3_sumvec_shard_subset_vs_oracle():
     assert int(cnt_s[0]) == int(rc[0])
     # the whole batch: every untampered report finishes
     assert int(cnt[0]) == int((status == 0).sum())
-
-
-def test_c5_fpvec_100k_tiled_fixture():
-    """configs[4] at its size: the committed full-size fixture reports (tests/golden/
-    fpvec_l10000.npz, the restatement's bytes) tiled to 100k, every prepare message and the
-    whole 10,000-entry aggregate share against the fixture's output shares."""
-    import torch
-    from janus_amd import prio3 as J
-    root = os.path.dirname(os.path.abspath(__file__))
-    g = np.load(os.path.join(root, "golden", "fpvec_l10000.npz"))
-    vk = bytes(g["verify_key"])
-    n = 100_000
-    k = len(g["status"])
-    idx = np.arange(n) % k
-    dev = torch.device("cuda", 0)
-    T = lambda a: torch.from_numpy(np.ascontiguousarray(a[idx])).to(dev)
-    nonces, pub, helper, lps = T(g["nonce"]), T(g["pub"]), T(g["helper"]), T(g["lps"])
-    eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(10000, 16), vk, device=0,
-                         allow_unpinned=True)
-    msgs = torch.empty((n, 16), dtype=torch.uint8, device=dev)
-    status = torch.empty(n, dtype=torch.uint8, device=dev)
-    seg = torch.zeros(n, dtype=torch.int32, device=dev)
-    agg = torch.zeros((1, eng.sz.agg_share_len), dtype=torch.uint8, device=dev)
-    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
-    eng.prepare_device(nonces, pub, helper, lps, msgs, status)
-    eng.accumulate_device(n, status, seg, None, 1, agg, cnt)
-    torch.cuda.synchronize()
-    np.testing.assert_array_equal(status.cpu().numpy(), g["status"][idx])
-    ok = g["status"] == 0
-    np.testing.assert_array_equal(msgs.cpu().numpy()[ok[idx]], g["prep_msg"][idx][ok[idx]])
-    P = 2**128 - 28 * 2**64 + 1
-    want = [0] * 10000
-    for r in np.flatnonzero(ok):
-        c = int((idx == r).sum())
-        o = np.frombuffer(g["out_shares"][r].tobytes(), dtype="<u8").reshape(-1, 2)
-        for e in range(10000):
-            want[e] = (want[e] + c * (int(o[e, 0]) | int(o[e, 1]) << 64)) % P
-    got = agg.cpu().numpy()[0].tobytes()
-    assert [int.from_bytes(got[16 * e:16 * e + 16], "little") for e in range(10000)] == want
-    assert int(cnt[0]) == int(ok[idx].sum())
