@@ -1002,42 +1002,27 @@ def _pipeline_model(sz) -> dict:
     return dict(parts, total=sum(parts.values()))
 
 
-def _mp64_reports(args):
-    from oracle import prio3_py as P
-    i, cfg, vk = args
-    v = P.Prio3(P.Prio3Type("sumvec_f64_mp", bits=cfg[1], length=cfg[2], chunk_length=cfg[3],
-                            num_proofs=cfg[0]))
-    rng = np.random.default_rng(1000 + i)
-    m = [int(x) for x in rng.integers(0, 2 ** cfg[1], cfg[2])]
-    nonce = bytes(rng.integers(0, 256, 16, dtype=np.uint8))
-    pub, leader, helper = v.shard(m, nonce, bytes(rng.integers(0, 256, 160, dtype=np.uint8)))
-    _, lps, _ = v.prepare_init(vk, 0, nonce, pub, leader)
-    return nonce, pub, helper, lps
-
-
 def mp64_main(args):
     """Prio3SumVecField64MultiproofHmacSha256Aes128 helper prepare+aggregate line (not the
     BASELINE metric) at the reference's own end-to-end configuration
-    (proofs 2, bits 16, length 15, chunk 16: integration_tests janus.rs:387-392).  Reports come
-    from the Python restatement (distinct ones tiled).  cpu_baseline: the compiled C restatement
+    (proofs 2, bits 16, length 15, chunk 16: integration_tests janus.rs:387-392).  Reports are
+    distinct and generated on the device by the engine's client (prio3_client_generate_device,
+    pinned to oracle/prio3_py.py gen_report_mp64 by tests/test_mp64_client.py).  cpu_baseline: the compiled C restatement
     (oracle/prio3_oracle.c ORC_SUMVEC_F64_MP, OpenSSL SHA-256 / AES-128) in 500-report jobs on
     every host thread, on a bounded sample of the same reports, cross-checking the GPU there."""
-    import multiprocessing as mp_
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
     cfg = (2, 16, 15, 16)
     vk = bytes(range(0x40, 0x60))
     n = args.reports
-    uniq = min(n, 2048)
-    t0 = time.perf_counter()
-    with mp_.get_context("spawn").Pool(min(16, cpu_threads())) as pool:
-        reps = pool.map(_mp64_reports, [(i, cfg, vk) for i in range(uniq)])
-    gen_s = time.perf_counter() - t0
-    reps_n = -(-n // uniq)
-    A = lambda k: torch.from_numpy(np.ascontiguousarray(np.tile(
-        np.array([list(r[k]) for r in reps], np.uint8), (reps_n, 1))[:n])).to(dev)
-    nonces, pub, helper, lps = A(0), A(1), A(2), A(3)
     eng = J.HelperEngine(J.Prio3SumVecField64MultiproofHmacSha256Aes128(*cfg), vk, device=0)
+    t0 = time.perf_counter()
+    gen = eng.generate_reports_device(n, seed=0x4A414E5553000008, with_checks=True)
+    torch.cuda.synchronize()
+    gen_s = time.perf_counter() - t0
+    nonces, pub, helper, lps = (gen["nonces"], gen["public_shares"], gen["helper_shares"],
+                                gen["leader_prep_shares"])
+    gen_flags = int(gen["flags"].sum().item())
     msgs = torch.empty((n, 32), dtype=torch.uint8, device=dev)
     status = torch.empty(n, dtype=torch.uint8, device=dev)
     seg = torch.zeros(n, dtype=torch.int32, device=dev)
@@ -1067,8 +1052,8 @@ def mp64_main(args):
                unit="reports/s", n_gpus=1, steps=args.steps, warmup=args.warmup,
                ms_per_step=elapsed / args.steps * 1e3, higher_is_better=True, scaling="weak",
                vs_baseline=None, dtype="u64 (Field64), bytes",
-               data=f"synthetic: {uniq} distinct reports from the Python restatement tiled "
-                    f"x{reps_n}; generation {gen_s:.1f}s, not timed",
+               data=f"synthetic: {n} distinct reports from the device client (seeded); "
+                    f"generation {gen_s:.1f}s, not timed",
                config=dict(workload="Prio3SumVecField64MultiproofHmacSha256Aes128 helper "
                                     "prepare+aggregate", proofs=2, bits=16, length=15,
                            chunk_length=16, reports=n),
@@ -1076,7 +1061,8 @@ def mp64_main(args):
                         for k, v in times.items()},
                roofline=model_roofline("mp64", RM.mp64_model(eng.sz, cfg[1], cfg[2], cfg[3], cfg[0]),
                                        n, args.steps, elapsed),
-               checks=dict(finished=int((status == 0).sum().item()), agg_count=int(cnt[0])),
+               checks=dict(finished=int((status == 0).sum().item()), agg_count=int(cnt[0]),
+                           generator_flags=gen_flags),
                cpu_baseline=None)
     if not args.no_cpu_baseline:
         from oracle.oracle import Oracle, build
@@ -1084,16 +1070,17 @@ def mp64_main(args):
         o = Oracle("sumvec_f64_mp", bits=cfg[1], length=cfg[2], chunk_length=cfg[3],
                    num_proofs=cfg[0])
         th = cpu_threads()
-        host = [t.cpu().numpy() for t in (nonces, pub, helper, lps)]
+        mh = min(n, 1 << 20)
+        host = [t[:mh].cpu().numpy() for t in (nonces, pub, helper, lps)]
 
         def crun(m):
             t1 = time.perf_counter()
             r = o.helper_batch(vk, *(h[:m] for h in host), n_threads=th, job_size=500)
             return time.perf_counter() - t1, r
 
-        probe = min(n, 500 * th)
+        probe = min(mh, 500 * th)
         dt, _ = crun(probe)
-        m = int(min(n, max(probe, probe * args.cpu_seconds / max(dt, 1e-6))))
+        m = int(min(mh, max(probe, probe * args.cpu_seconds / max(dt, 1e-6))))
         dt, (cm, cs, cagg, ccnt) = crun(m)
         out["cpu_baseline"] = dict(value=m / dt, unit="reports/s", cores=th, kind="port",
                                    sample=f"{m} of the same reports through the C restatement "

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "prio3_common.h"
+#include "prio3_mp64_xof.h"
 
 struct GenScratch {
   void *meas, *hm, *lm, *wires, *evals, *g, *tmp, *proof, *hp, *prand, *jr, *qr, *L, *PV, *acc;
@@ -163,6 +164,64 @@ DEV typename F::T gadget_eval_lane(const DevParams& p, const void* ev, uint32_t 
   return s;
 }
 
+// FlpGeneric::prove (VDAF-08 7.3.3.1, num_shares = 1) of the single-gadget circuits -- Count,
+// Sum, and the ParallelSum(Mul) range check of SumVec / Histogram -- on one lane: the wire values
+// of every gadget call recorded (seed = prand[w] at point 0), each wire polynomial evaluated on
+// the 2P-th roots (size-P inverse DFT, size-2P DFT), the gadget applied pointwise and the gadget
+// polynomial's coefficients back by a size-2P inverse DFT.  meas / prand / jr / proof: SoA
+// column sets (the first jr element is the circuit's joint randomness); proof = prand || coeffs.
+template <class F>
+DEV void prove_lane(const DevParams& p, const GenScratch& gs, const void* meas, const void* prand,
+                    const void* jr, void* proof, uint32_t r, typename F::T invP,
+                    typename F::T inv2P) {
+  typedef typename F::T T;
+  const size_t ld = p.ld;
+  const uint32_t M = p.meas_len, A = p.arity, P = p.P, P2 = 2 * P;
+  for (uint32_t w = 0; w < A; w++) {
+    F::store(gs.wires, ((size_t)w * P) * ld + r, F::load(prand, (size_t)w * ld + r));
+    for (uint32_t c = 1; c < P; c++) F::store(gs.wires, ((size_t)w * P + c) * ld + r, F::zero());
+  }
+  auto wset = [&](uint32_t w, uint32_t c, const T& x) {
+    F::store(gs.wires, ((size_t)w * P + c) * ld + r, x);
+  };
+  if (p.kind == PRIO3_COUNT) {
+    T m = F::load(meas, r);
+    wset(0, 1, m);
+    wset(1, 1, m);
+  } else if (p.kind == PRIO3_SUM) {
+    for (uint32_t i = 0; i < M; i++) wset(0, i + 1, F::load(meas, (size_t)i * ld + r));
+  } else {
+    const T r0 = F::load(jr, r);
+    T rp = r0;
+    for (uint32_t k = 0; k < p.calls; k++)
+      for (uint32_t j = 0; j < p.chunk; j++) {
+        const uint32_t i = k * p.chunk + j;
+        const T m = i < M ? F::load(meas, (size_t)i * ld + r) : F::zero();
+        wset(2 * j, k + 1, F::mul(rp, m));
+        wset(2 * j + 1, k + 1, F::sub(m, F::one()));
+        rp = F::mul(rp, r0);
+      }
+  }
+  // ---- wire polys -> evaluations on the 2P-th roots ----
+  for (uint32_t w = 0; w < A; w++) {
+    void* wcol = (uint8_t*)gs.wires + (size_t)w * P * ld * F::ES;
+    idft_lane<F>(p, wcol, P, gs.tmp, P, p.logP, r, invP);  // coefficients in tmp[0..P)
+    void* ecol = (uint8_t*)gs.evals + (size_t)w * P2 * ld * F::ES;
+    for (uint32_t e = 0; e < P2; e++)
+      F::store(ecol, (size_t)bitrev(e, p.logP + 1) * ld + r,
+               e < P ? F::load(gs.tmp, (size_t)e * ld + r) : F::zero());
+    dft_lane<F>(p, ecol, r, P2, p.logP + 1);
+  }
+  for (uint32_t k = 0; k < P2; k++)
+    F::store(gs.g, (size_t)k * ld + r, gadget_eval_lane<F>(p, gs.evals, k, P2, r));
+  idft_lane<F>(p, gs.g, P2, gs.tmp, P2, p.logP + 1, r, inv2P);  // gadget poly coefficients
+  // proof = prove_rand || coeffs[0..glen)
+  for (uint32_t w = 0; w < A; w++)
+    F::store(proof, (size_t)w * ld + r, F::load(prand, (size_t)w * ld + r));
+  for (uint32_t e = 0; e < p.glen; e++)
+    F::store(proof, (size_t)(A + e) * ld + r, F::load(gs.tmp, (size_t)e * ld + r));
+}
+
 template <class F>
 __global__ __launch_bounds__(64) void k_gen(DevParams p, uint64_t seed, uint64_t first,
                                             GenScratch gs, GenOut go, typename F::T invP,
@@ -172,7 +231,7 @@ __global__ __launch_bounds__(64) void k_gen(DevParams p, uint64_t seed, uint64_t
   if (r >= p.n) return;
   const size_t ld = p.ld;
   const uint64_t idx = first + r;
-  const uint32_t M = p.meas_len, A = p.arity, P = p.P, P2 = 2 * P, PL = p.proof_len;
+  const uint32_t M = p.meas_len, A = p.arity, PL = p.proof_len;
   const bool JR = p.jr_len > 0;
   const uint32_t mstride = p.kind == PRIO3_SUMVEC ? p.length : 1;
   uint32_t flag = 0;
@@ -262,49 +321,7 @@ __global__ __launch_bounds__(64) void k_gen(DevParams p, uint64_t seed, uint64_t
     const uint8_t b1[1] = {1};
     expand_to<F>(p, p.dst[4], k_pr, b1, 1, A, gs.prand, r, flag);
   }
-  // ---- prove: record wires (num_shares = 1) ----
-  for (uint32_t w = 0; w < A; w++) {
-    F::store(gs.wires, ((size_t)w * P) * ld + r, F::load(gs.prand, (size_t)w * ld + r));
-    for (uint32_t c = 1; c < P; c++) F::store(gs.wires, ((size_t)w * P + c) * ld + r, F::zero());
-  }
-  auto wset = [&](uint32_t w, uint32_t c, const T& x) {
-    F::store(gs.wires, ((size_t)w * P + c) * ld + r, x);
-  };
-  if (p.kind == PRIO3_COUNT) {
-    T m = F::load(gs.meas, r);
-    wset(0, 1, m);
-    wset(1, 1, m);
-  } else if (p.kind == PRIO3_SUM) {
-    for (uint32_t i = 0; i < M; i++) wset(0, i + 1, F::load(gs.meas, (size_t)i * ld + r));
-  } else {
-    const T r0 = F::load(gs.jr, r);
-    T rp = r0;
-    for (uint32_t k = 0; k < p.calls; k++)
-      for (uint32_t j = 0; j < p.chunk; j++) {
-        const uint32_t i = k * p.chunk + j;
-        const T m = i < M ? F::load(gs.meas, (size_t)i * ld + r) : F::zero();
-        wset(2 * j, k + 1, F::mul(rp, m));
-        wset(2 * j + 1, k + 1, F::sub(m, F::one()));
-        rp = F::mul(rp, r0);
-      }
-  }
-  // ---- wire polys -> evaluations on the 2P-th roots ----
-  for (uint32_t w = 0; w < A; w++) {
-    void* wcol = (uint8_t*)gs.wires + (size_t)w * P * ld * F::ES;
-    idft_lane<F>(p, wcol, P, gs.tmp, P, p.logP, r, invP);  // coefficients in tmp[0..P)
-    void* ecol = (uint8_t*)gs.evals + (size_t)w * P2 * ld * F::ES;
-    for (uint32_t e = 0; e < P2; e++)
-      F::store(ecol, (size_t)bitrev(e, p.logP + 1) * ld + r,
-               e < P ? F::load(gs.tmp, (size_t)e * ld + r) : F::zero());
-    dft_lane<F>(p, ecol, r, P2, p.logP + 1);
-  }
-  for (uint32_t k = 0; k < P2; k++)
-    F::store(gs.g, (size_t)k * ld + r, gadget_eval_lane<F>(p, gs.evals, k, P2, r));
-  idft_lane<F>(p, gs.g, P2, gs.tmp, P2, p.logP + 1, r, inv2P);  // gadget poly coefficients
-  // proof = prove_rand || coeffs[0..glen)
-  for (uint32_t w = 0; w < A; w++) F::store(gs.proof, (size_t)w * ld + r, F::load(gs.prand, (size_t)w * ld + r));
-  for (uint32_t e = 0; e < p.glen; e++)
-    F::store(gs.proof, (size_t)(A + e) * ld + r, F::load(gs.tmp, (size_t)e * ld + r));
+  prove_lane<F>(p, gs, gs.meas, gs.prand, gs.jr, gs.proof, r, invP, inv2P);
   // leader proofs share = proof - helper proofs share
   {
     const uint8_t b2[2] = {1, 1};
@@ -402,7 +419,7 @@ struct FgGadget {
   f128 c2P;  // 1 / (2P)
 };
 
-// the report's stream word wi (non-decreasing), 168-byte blocks
+// the report's stream word wi, 168-byte blocks; wi never below the current block's first word
 struct GenStream {
   KState st;
   uint32_t blk = 0;
@@ -763,6 +780,156 @@ __global__ __launch_bounds__(64) void k_fg_finish(DevParams p, GenOut go, FgBufs
 }
 
 // ====================================================================================
+// Prio3SumVecField64MultiproofHmacSha256Aes128 client: the same seeded
+// stream, 32-byte seeds (nonce at bytes 0..15, then helper measurement, helper proofs, helper
+// blind, leader blind and prove-rand seeds, 32 bytes each, entries 8 bytes each from byte 176,
+// masked to `bits`), the shares and num_proofs proofs of the SumVec circuit over Field64 with
+// XofHmacSha256Aes128 (prio3_mp64_xof.h), one report per lane; then the engine's device leader
+// prepare_init on the leader input shares.  oracle/prio3_py.py is the same in Python
+// (tests/test_mp64_client.py).
+// ====================================================================================
+// joint_rand_part = XOF(k_blind, dst(7), [agg_id] || nonce || enc(share)) -> 32 bytes
+DEV void mp_jr_part(const AesT& A, const Mp64Params& P, const uint32_t kblind[8], uint32_t agg_id,
+                    const uint32_t nonce[4], const uint64_t* share, size_t ld, uint32_t r,
+                    uint32_t part[8]) {
+  HmacKey k;
+  hmac_key_ni(kblind, k.ist, k.ost);
+  Msg32<8> pm;
+  mz(pm);
+  msg_dst(pm, P, 7);
+  mbyte(pm, 9, agg_id);
+  mwords_le(pm, 10, nonce, 4);
+  const uint32_t M = P.meas_len, L = 26 + 8 * M, nblk = (L + 9 + 63) / 64;
+  uint32_t st[8];
+  for (int i = 0; i < 8; i++) st[i] = k.ist[i];
+  for (uint32_t b = 0; b < nblk; b++) {
+    uint32_t w[16];
+    for (int i = 0; i < 16; i++) w[i] = jr_word(16 * b + i, pm.w, share, ld, r, M, L, 16 * nblk);
+    compress_ni(st, w);
+  }
+  uint32_t o[16] = {st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], 0x80000000u,
+                    0, 0, 0, 0, 0, 0, (64 + 32) * 8};
+  uint32_t tag[8];
+  for (int i = 0; i < 8; i++) tag[i] = k.ost[i];
+  compress_ni(tag, o);
+  Stream s;
+  stream_init(A, s, tag);
+  derive32(A, s, part);
+}
+
+// XOF(seed, dst(usage), binder) -> n elements into SoA rows of base (rejection sampling)
+DEV void mp_expand(const AesT& A, const Mp64Params& P, const uint32_t seed[8], int usage,
+                   const uint8_t* binder, int blen, uint64_t* base, size_t ld, uint32_t r,
+                   uint32_t n) {
+  Msg32<16> m;
+  mz(m);
+  msg_dst(m, P, usage);
+  for (int i = 0; i < blen; i++) mbyte(m, 9 + i, binder[i]);
+  uint32_t tag[8];
+  xof_tag(seed, m, 9 + blen, tag);
+  Stream s;
+  stream_init(A, s, tag);
+  (void)expand_soa(A, s, base, ld, r, n);
+}
+
+__global__ __launch_bounds__(64) void k_gen_mp64(DevParams p, Mp64Params P, uint64_t seed,
+                                                 uint64_t first, GenScratch gs, GenOut go,
+                                                 uint8_t* lin, uint64_t invP, uint64_t inv2P) {
+  __shared__ AesT A;
+  aes_tables_init(A);
+  __syncthreads();
+  typedef Fp64 F;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= p.n) return;
+  const size_t ld = p.ld;
+  // DevParams::proof_len counts every proof here; Mp64Params::proof_len is one proof's
+  const uint32_t M = p.meas_len, np = P.np, Ar = p.arity, PL = P.proof_len, Ln = p.length;
+  GenStream gst;
+  gen_stream_init(gst.st, seed, first + r);
+  uint32_t nonce[4], k_hm[8], k_hp[8], k_hb[8], k_lb[8], k_pr[8];
+  // stream words in increasing order (GenStream moves forward only; words 42, 43 of the last
+  // seed are in the second block)
+  for (int k = 0; k < 4; k++) nonce[k] = gst.word(k);
+  for (int k = 0; k < 8; k++) k_hm[k] = gst.word(4 + k);
+  for (int k = 0; k < 8; k++) k_hp[k] = gst.word(12 + k);
+  for (int k = 0; k < 8; k++) k_hb[k] = gst.word(20 + k);
+  for (int k = 0; k < 8; k++) k_lb[k] = gst.word(28 + k);
+  for (int k = 0; k < 8; k++) k_pr[k] = gst.word(36 + k);
+  uint64_t* meas = (uint64_t*)gs.meas;
+  const uint64_t mask = p.bits < 64 ? (1ull << p.bits) - 1 : ~0ull;
+  for (uint32_t e = 0; e < Ln; e++) {
+    uint64_t v = (uint64_t)gst.word(44 + 2 * e);
+    v |= (uint64_t)gst.word(45 + 2 * e) << 32;
+    v &= mask;
+    if (go.meas) go.meas[(size_t)r * Ln + e] = v;
+    for (uint32_t b = 0; b < p.bits; b++) meas[(size_t)(e * p.bits + b) * ld + r] = (v >> b) & 1;
+  }
+  // shares and joint-rand parts
+  uint64_t* hm = (uint64_t*)gs.hm;
+  uint64_t* lm = (uint64_t*)gs.lm;
+  const uint8_t b1[1] = {1};
+  mp_expand(A, P, k_hm, 1, b1, 1, hm, ld, r, M);
+  for (uint32_t i = 0; i < M; i++)
+    lm[(size_t)i * ld + r] = F::sub(meas[(size_t)i * ld + r], hm[(size_t)i * ld + r]);
+  uint32_t part0[8], part1[8], jseed[8];
+  mp_jr_part(A, P, k_hb, 1, nonce, hm, ld, r, part1);
+  mp_jr_part(A, P, k_lb, 0, nonce, lm, ld, r, part0);
+  {
+    Msg32<32> m;
+    mz(m);
+    msg_dst(m, P, 6);
+    mwords_le(m, 9, part0, 8);
+    mwords_le(m, 41, part1, 8);
+    uint32_t tag[8];
+    hmac_ni(P.z_ist, P.z_ost, m.w, 73, tag);
+    Stream s;
+    stream_init(A, s, tag);
+    derive32(A, s, jseed);
+  }
+  const uint8_t bnp[2] = {(uint8_t)np, 1};
+  mp_expand(A, P, jseed, 3, bnp, 1, (uint64_t*)gs.jr, ld, r, np);           // one per proof
+  mp_expand(A, P, k_pr, 4, bnp, 1, (uint64_t*)gs.prand, ld, r, Ar * np);
+  // the num_proofs proofs (proof k: prove rand rows k A .., joint rand row k)
+  for (uint32_t k = 0; k < np; k++)
+    prove_lane<F>(p, gs, gs.meas, (const uint64_t*)gs.prand + (size_t)k * Ar * ld,
+                  (const uint64_t*)gs.jr + (size_t)k * ld, (uint64_t*)gs.proof + (size_t)k * PL * ld,
+                  r, invP, inv2P);
+  // leader input share = enc(lm) || enc(proofs - helper proofs share) || k_blind
+  uint64_t* hp = (uint64_t*)gs.hp;
+  mp_expand(A, P, k_hp, 2, bnp, 2, hp, ld, r, PL * np);
+  uint64_t* li = (uint64_t*)(lin + (size_t)r * p.leader_share_len);
+  for (uint32_t i = 0; i < M; i++) li[i] = lm[(size_t)i * ld + r];
+  const uint64_t* prf = (const uint64_t*)gs.proof;
+  for (uint32_t i = 0; i < PL * np; i++)
+    li[M + i] = F::sub(prf[(size_t)i * ld + r], hp[(size_t)i * ld + r]);
+  uint32_t* lt = (uint32_t*)(li + M + PL * np);
+  for (int k = 0; k < 8; k++) lt[k] = k_lb[k];
+  // public outputs
+  *(uint4*)(go.nonces + 16 * (size_t)r) = make_uint4(nonce[0], nonce[1], nonce[2], nonce[3]);
+  uint32_t* hs = (uint32_t*)(go.helper + (size_t)r * p.helper_share_len);
+  uint32_t* pb = (uint32_t*)(go.pub + (size_t)r * p.public_share_len);
+  for (int k = 0; k < 8; k++) {
+    hs[k] = k_hm[k];
+    hs[8 + k] = k_hp[k];
+    hs[16 + k] = k_hb[k];
+    pb[k] = part0[k];
+    pb[8 + k] = part1[k];
+  }
+  if (go.leader_out) {  // truncate(lm): entry e = sum_b 2^b lm[e bits + b]
+    uint64_t* lo = (uint64_t*)(go.leader_out + (size_t)r * p.out_len * 8);
+    for (uint32_t e = 0; e < p.out_len; e++) {
+      uint64_t acc = 0, pw = 1;
+      for (uint32_t b = 0; b < p.bits; b++) {
+        acc = F::add(acc, F::mul(pw, lm[(size_t)(e * p.bits + b) * ld + r]));
+        pw = F::add(pw, pw);
+      }
+      lo[e] = acc;
+    }
+  }
+  if (go.flags) go.flags[r] = 0;
+}
+
+// ====================================================================================
 // Host ABI
 // ====================================================================================
 #define GCHK(x)                                                                       \
@@ -1075,6 +1242,77 @@ static int gen_fpvec(prio3_engine* e, uint32_t n, uint64_t seed, uint64_t first_
   return rc;
 }
 
+// multiproof generator: chunks through k_gen_mp64, then the device leader prepare_init
+static int gen_mp64(prio3_engine* e, uint32_t n, uint64_t seed, uint64_t first_index,
+                    uint8_t* d_nonces, uint8_t* d_pub, uint8_t* d_helper, uint8_t* d_lps,
+                    uint64_t* d_meas, uint8_t* d_lout, uint8_t* d_flags, uint8_t* d_lin,
+                    hipStream_t st) {
+  DevParams p = e->dp;
+  const Mp64Params& P = e->mp;
+  if (!d_pub) return PRIO3_EINVAL;
+  if (hipSetDevice(e->device) != hipSuccess) return PRIO3_EDEVICE;
+  const uint32_t A = p.arity, np = P.np, PP = p.P;
+  const size_t chunk = std::min<size_t>(((size_t)n + 63) & ~(size_t)63, 65536);
+  std::vector<void*> bufs;
+  int rc = PRIO3_OK;
+  auto alloc = [&](size_t bytes) -> void* {
+    void* b = nullptr;
+    if (hipMalloc(&b, std::max<size_t>(bytes, 256)) != hipSuccess) {
+      (void)hipGetLastError();
+      rc = PRIO3_EDEVICE;
+      return nullptr;
+    }
+    bufs.push_back(b);
+    return b;
+  };
+  GenScratch gs{};
+  const size_t es = 8;
+  gs.meas = alloc(es * p.meas_len * chunk);
+  gs.hm = alloc(es * p.meas_len * chunk);
+  gs.lm = alloc(es * p.meas_len * chunk);
+  gs.wires = alloc(es * A * PP * chunk);
+  gs.evals = alloc(es * A * 2 * PP * chunk);
+  gs.g = alloc(es * 2 * PP * chunk);
+  gs.tmp = alloc(es * 2 * PP * chunk);
+  gs.proof = alloc(es * (size_t)P.proof_len * np * chunk);
+  gs.hp = alloc(es * (size_t)P.proof_len * np * chunk);
+  gs.prand = alloc(es * A * np * chunk);
+  gs.jr = alloc(es * np * chunk);
+  uint8_t* lin = (uint8_t*)alloc((size_t)p.leader_share_len * chunk);
+  uint8_t* stat = (uint8_t*)alloc(chunk);
+  const uint64_t invP = (uint64_t)hpow(PP, HP64 - 2, HP64), inv2P = (uint64_t)hpow(2 * PP, HP64 - 2, HP64);
+  for (uint64_t off = 0; off < n && rc == PRIO3_OK; off += chunk) {
+    const uint32_t m = (uint32_t)std::min<uint64_t>(chunk, n - off);
+    DevParams q = p;
+    q.n = m;
+    q.ld = (uint32_t)chunk;
+    GenOut go{};
+    go.nonces = d_nonces + 16 * off;
+    go.pub = d_pub + (size_t)p.public_share_len * off;
+    go.helper = d_helper + (size_t)p.helper_share_len * off;
+    go.leader_out = d_lout ? d_lout + (size_t)p.out_len * 8 * off : nullptr;
+    go.meas = d_meas ? d_meas + (size_t)p.length * off : nullptr;
+    go.flags = d_flags ? d_flags + off : nullptr;
+    k_gen_mp64<<<(m + 63) / 64, 64, 0, st>>>(q, P, seed, first_index + off, gs, go, lin, invP,
+                                              inv2P);
+    if (hipGetLastError() != hipSuccess) {
+      rc = PRIO3_EDEVICE;
+      break;
+    }
+    rc = prio3_device_leader_prepare_init(e, m, go.nonces, go.pub, lin,
+                                          d_lps + (size_t)p.prep_share_len * off, stat, st);
+    if (rc != PRIO3_OK) break;
+    if (d_flags) k_fg_status<<<(m + 255) / 256, 256, 0, st>>>(stat, d_flags + off, m);
+    if (d_lin && hipMemcpyAsync(d_lin + (size_t)p.leader_share_len * off, lin,
+                                (size_t)p.leader_share_len * m, hipMemcpyDeviceToDevice,
+                                st) != hipSuccess)
+      rc = PRIO3_EDEVICE;
+  }
+  if (hipStreamSynchronize(st) != hipSuccess && rc == PRIO3_OK) rc = PRIO3_EDEVICE;
+  for (auto b : bufs) (void)hipFree(b);
+  return rc;
+}
+
 extern "C" int prio3_client_generate_device(prio3_engine* e, uint32_t n, uint64_t seed,
                                             uint64_t first_index, uint8_t* d_nonces,
                                             uint8_t* d_public_shares, uint8_t* d_helper_shares,
@@ -1082,9 +1320,12 @@ extern "C" int prio3_client_generate_device(prio3_engine* e, uint32_t n, uint64_
                                             uint64_t* d_measurements,
                                             uint8_t* d_leader_out_shares, uint8_t* d_flags,
                                             uint8_t* d_leader_input_shares, void* stream) {
-  if (e && e->dp.kind == PRIO3_SUMVEC_F64_MP) return PRIO3_EUNSUPPORTED;  // not a TurboSHAKE client
   if (!e || !d_nonces || !d_helper_shares || !d_leader_prep_shares) return PRIO3_EINVAL;
   if (n == 0) return PRIO3_OK;
+  if (e->dp.kind == PRIO3_SUMVEC_F64_MP)
+    return gen_mp64(e, n, seed, first_index, d_nonces, d_public_shares, d_helper_shares,
+                    d_leader_prep_shares, d_measurements, d_leader_out_shares, d_flags,
+                    d_leader_input_shares, (hipStream_t)stream);
   if (e->dp.kind == PRIO3_FPVEC_BOUNDED_L2)
     return gen_fpvec(e, n, seed, first_index, d_nonces, d_public_shares, d_helper_shares,
                      d_leader_prep_shares, d_measurements, d_leader_out_shares, d_flags,

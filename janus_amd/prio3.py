@@ -544,7 +544,7 @@ class HelperEngine:
         Returns torch uint8 tensors on this engine's device (plus measurements / leader
         output shares / flags when ``with_checks``).  Every TurboSHAKE instance, including
         FixedPointBoundedL2VecSum (its prover runs on the device too; the engine needs the
-        allow_unpinned opt-in); not the HMAC-SHA256/AES-128 multiproof VDAF.  Report i is
+        allow_unpinned opt-in), and the HMAC-SHA256/AES-128 multiproof VDAF.  Report i is
         derived from (seed, first_index + i) exactly as oracle's generators derive it."""
         import torch
         sz = self.sz
@@ -556,8 +556,8 @@ class HelperEngine:
                    leader_prep_shares=torch.empty((n, sz.prep_share_len), **u8))
         if with_checks:
             # SumVec: the entries; FPVec: the signed fixed-point entries X (x = X / 2^(bits-1))
-            mstride = (self.vdaf.length if self.vdaf.kind in (PRIO3_SUMVEC, PRIO3_FPVEC_BOUNDED_L2)
-                       else 1)
+            mstride = (self.vdaf.length if self.vdaf.kind in (PRIO3_SUMVEC, PRIO3_FPVEC_BOUNDED_L2,
+                                                              PRIO3_SUMVEC_F64_MP) else 1)
             out["measurements"] = torch.empty((n, mstride), dtype=torch.int64, device=dev)
             out["leader_out_shares"] = torch.empty((n, sz.agg_share_len), **u8)
             out["flags"] = torch.zeros(n, **u8)

@@ -596,3 +596,26 @@ class Prio3:
 
     def unshard(self, agg_shares) -> object:
         return self.t.decode_agg(self.aggregate(agg_shares))
+
+
+def gen_report_mp64(vk: bytes, bits: int, length: int, chunk: int, proofs: int, seed: int,
+                    idx: int) -> dict:
+    """Report idx of the synthetic client's seeded stream for the Field64 multiproof VDAF, as the
+    device generator derives it (janus_amd/csrc/prio3_client.hip k_gen_mp64): stream =
+    TurboSHAKE128("janus-amd-gen" || seed || idx, D = 1) gives the nonce (16 bytes), the five
+    32-byte shard seeds (helper measurement, helper proofs, helper blind, leader blind, prove
+    randomness) and one 8-byte little-endian entry per element from byte 176, masked to `bits`;
+    then shard and the leader's prepare_init (agg_id 0).  TEST INFRASTRUCTURE ONLY."""
+    typ = Prio3Type("sumvec_f64_mp", bits=bits, length=length, chunk_length=chunk,
+                    num_proofs=proofs)
+    P = Prio3(typ)
+    msg = b"janus-amd-gen" + seed.to_bytes(8, "little") + idx.to_bytes(8, "little")
+    stream = turboshake128(msg, 1, 176 + 8 * length)
+    nonce, rand = stream[:16], stream[16:176]
+    m = [int.from_bytes(stream[176 + 8 * e:184 + 8 * e], "little") & ((1 << bits) - 1)
+         for e in range(length)]
+    public, leader, helper = P.shard(m, nonce, rand)
+    _, lps, trace = P.prepare_init(vk, 0, nonce, public, leader)
+    out = typ.truncate(trace["meas"])
+    return dict(nonce=nonce, public=public, helper=helper, leader=leader, lps=lps, m=m,
+                leader_out=b"".join(P.F.enc(x) for x in out))
