@@ -464,11 +464,85 @@ struct Exec {
     }
   }
 
+  // JANUS_PRIO3_PIPE=1: a pipeline of up to JANUS_PRIO3_PIPE_DEPTH (default 3) groups whose
+  // kernels run concurrently (no group waits for another's prepare): a group is issued as soon as
+  // it is staged and holds at least JANUS_PRIO3_PIPE_MIN reports (default 16384), or the
+  // pipeline is empty, or the oldest group in it has prepared; any finished group is completed.
+  // Polls with yields (no prepare-time prediction).  An experiment against launcher() above.
+  static bool pipe_mode() {
+    static const bool v = [] {
+      const char* s = getenv("JANUS_PRIO3_PIPE");
+      return s && atoi(s) != 0;
+    }();
+    return v;
+  }
+  static int env_int(const char* name, int dflt) {
+    const char* s = getenv(name);
+    return s ? atoi(s) : dflt;
+  }
+  void launcher_pipe() {
+    struct Slot {
+      Group* g;
+      typename P::Handle h;
+      bool prepared;
+    };
+    static const size_t depth = (size_t)std::max(1, std::min(16, env_int("JANUS_PRIO3_PIPE_DEPTH", 3)));
+    static const uint32_t min_n = (uint32_t)std::max(1, env_int("JANUS_PRIO3_PIPE_MIN", 16384));
+    std::deque<Slot> q;
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      while (!order.empty()) {
+        Group* g = order.front();
+        if (!q.empty()) {
+          if (g->writers > 0 || q.size() >= depth) break;
+          if (P::reports(g->st) < min_n && !q.front().prepared) break;
+        }
+        take_locked(lk);
+        lk.unlock();
+        Slot sl{g, typename P::Handle{}, false};
+        const int rc = P::issue(device, g->st, g->stg, &sl.h, nullptr);
+        lk.lock();
+        if (rc != PRIO3_OK) {
+          finish_locked(g, rc);
+          continue;
+        }
+        q.push_back(sl);
+      }
+      if (q.empty()) {
+        while (order.empty()) cv.wait(lk);
+        continue;
+      }
+      lk.unlock();
+      for (auto& sl : q)
+        if (!sl.prepared && P::prepared(sl.h)) sl.prepared = true;
+      bool any = false;
+      for (size_t i = 0; i < q.size();) {
+        if (P::done(q[i].h)) {
+          Slot sl = q[i];
+          q.erase(q.begin() + (long)i);
+          const int rc = P::finish(&sl.h);
+          if (FILE* f = exec_trace())
+            fprintf(f, "%.1f %.1f %.1f %.1f %d %u\n", exec_us(sl.g->created),
+                    exec_us(sl.g->t_take), exec_us(sl.g->t_staged),
+                    exec_us(std::chrono::steady_clock::now()), sl.g->njobs, P::reports(sl.g->st));
+          std::lock_guard<std::mutex> lg(mu);
+          finish_locked(sl.g, rc);
+          any = true;
+        } else {
+          i++;
+        }
+      }
+      if (!any) std::this_thread::yield();
+      lk.lock();
+    }
+  }
+
   int submit(typename P::Job* job) {
     std::unique_lock<std::mutex> lk(mu);
     if (!started) {
       started = true;
-      for (int i = 0; i < max_inflight(); i++) std::thread([this] { launcher(); }).detach();
+      for (int i = 0; i < max_inflight(); i++)
+        std::thread([this] { pipe_mode() ? launcher_pipe() : launcher(); }).detach();
     }
     const uint64_t key = P::key(job);
     Group* g = nullptr;
