@@ -364,14 +364,26 @@ struct Exec {
     double ns_per_report = 0;
     int seen = 0;
   };
+  std::map<uint64_t, Pred> preds;  // launcher()'s prepare-time table (kept across mode switches)
+  // heavy load: the reports inside submit at which launcher() takes over from launcher_pipe()
+  static uint64_t heavy() {
+    static const uint64_t v = (uint64_t)std::max(1, env_int("JANUS_PRIO3_PIPE_HEAVY", 32768));
+    return v;
+  }
+  // caller holds mu; hysteresis: launcher_pipe() hands over at heavy(), launcher() hands back only
+  // below a third of it (between two cohorts the callers of the finished group leave submit for
+  // a moment, and a handover there cost the 128-thread line 10 %, r04z6)
+  bool light() const { return pipe_mode() && active < heavy(); }
+  bool lighter() const { return pipe_mode() && active < heavy() / 3; }
+  // Returns (with nothing in flight) when the load turns light, to launcher_pipe().
   void launcher() {
-    std::map<uint64_t, Pred> preds;
     std::unique_lock<std::mutex> lk(mu);
     Group* cur = nullptr;
     typename P::Handle hc{};
     auto t0 = std::chrono::steady_clock::now();  // when cur was issued
     for (;;) {
       if (!cur) {
+        if (lighter()) return;
         while (order.empty()) cv.wait(lk);
         Group* g = take_locked(lk);
         lk.unlock();
@@ -415,7 +427,7 @@ struct Exec {
             std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - t0)
                     .count() >= frac * pred_ns) {
           lk.lock();
-          if (!order.empty() && order.front()->writers == 0) nxt = take_locked(lk);
+          if (!order.empty() && order.front()->writers == 0 && !lighter()) nxt = take_locked(lk);
           lk.unlock();
           tn = std::chrono::steady_clock::now();
           if (nxt) rcn = P::issue(device, nxt->st, nxt->stg, &hn, &hc);
@@ -433,7 +445,7 @@ struct Exec {
           }
           if (!nxt) {
             lk.lock();
-            if (!order.empty() && order.front()->writers == 0) nxt = take_locked(lk);
+            if (!order.empty() && order.front()->writers == 0 && !lighter()) nxt = take_locked(lk);
             lk.unlock();
             tn = std::chrono::steady_clock::now();
             if (nxt) rcn = P::issue(device, nxt->st, nxt->stg, &hn, nullptr);
@@ -464,15 +476,20 @@ struct Exec {
     }
   }
 
-  // JANUS_PRIO3_PIPE=1: a pipeline of up to JANUS_PRIO3_PIPE_DEPTH (default 3) groups whose
-  // kernels run concurrently (no group waits for another's prepare): a group is issued as soon as
-  // it is staged and holds at least JANUS_PRIO3_PIPE_MIN reports (default 16384), or the
-  // pipeline is empty, or the oldest group in it has prepared; any finished group is completed.
-  // Polls with yields (no prepare-time prediction).  An experiment against launcher() above.
+  // Under light load (fewer than JANUS_PRIO3_PIPE_HEAVY = 32 Ki reports inside submit: the box's
+  // 16 rayon threads make groups of a few jobs, each a latency-bound kernel at well under a wave
+  // per SIMD) the launcher runs this pipeline instead of launcher(): up to four groups whose
+  // kernels run concurrently (no group waits for another's prepare), each issued as soon as it is
+  // staged and holds >= 2 Ki reports (smaller ones wait for an empty pipeline), any finished group
+  // completed at once: 10-15 M reports/s at 16 threads against 5.6-7.6 M/s for launcher() on the
+  // same boxes (r04z).  Under heavy load (the 128-thread line) launcher()'s two-cohort rhythm
+  // stays ahead (38.6-39.6 M/s against 28-35 M/s for this pipeline, r04z2-4).
+  // JANUS_PRIO3_PIPE=0: launcher() only.  The pipeline yields between polls (a sleep's timer
+  // slack would be a fifth of a small group's time).
   static bool pipe_mode() {
     static const bool v = [] {
       const char* s = getenv("JANUS_PRIO3_PIPE");
-      return s && atoi(s) != 0;
+      return !s || atoi(s) != 0;
     }();
     return v;
   }
@@ -486,16 +503,16 @@ struct Exec {
       typename P::Handle h;
       bool prepared;
     };
-    static const size_t depth = (size_t)std::max(1, std::min(16, env_int("JANUS_PRIO3_PIPE_DEPTH", 3)));
-    static const uint32_t min_n = (uint32_t)std::max(1, env_int("JANUS_PRIO3_PIPE_MIN", 16384));
     std::deque<Slot> q;
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
+      if (q.empty() && !light()) return;  // heavy load: launcher() from here
       while (!order.empty()) {
         Group* g = order.front();
         if (!q.empty()) {
-          if (g->writers > 0 || q.size() >= depth) break;
-          if (P::reports(g->st) < min_n && !q.front().prepared) break;
+          // heavy load: let the pipeline drain (one bubble) and hand over to launcher()
+          if (g->writers > 0 || !light() || q.size() >= 4) break;
+          if (P::reports(g->st) < 2048u) break;  // a small group waits for a drained pipeline
         }
         take_locked(lk);
         lk.unlock();
@@ -537,12 +554,24 @@ struct Exec {
     }
   }
 
+  uint64_t active = 0;  // reports of the jobs inside submit (the callers' load; under mu)
   int submit(typename P::Job* job) {
     std::unique_lock<std::mutex> lk(mu);
+    active += job->n;
+    struct Done {  // runs with mu held: every return below holds lk
+      uint64_t& a;
+      uint32_t n;
+      ~Done() { a -= n; }
+    } done_{active, job->n};
     if (!started) {
       started = true;
       for (int i = 0; i < max_inflight(); i++)
-        std::thread([this] { pipe_mode() ? launcher_pipe() : launcher(); }).detach();
+        std::thread([this] {
+          for (;;) {  // launcher() under heavy load, launcher_pipe() under light load
+            launcher();
+            launcher_pipe();
+          }
+        }).detach();
     }
     const uint64_t key = P::key(job);
     Group* g = nullptr;
