@@ -216,7 +216,9 @@ def test_config_sumvec_eight_ranks_gloo_one_gpu():
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, timeout=600)
     out = p.stdout.decode(errors="replace")
-    assert p.returncode == 0, out + p.stderr.decode(errors="replace")[-4000:]
+    err = p.stderr.decode(errors="replace")
+    tb = [ln for ln in err.splitlines() if "Error" in ln or "error" in ln or "Traceback" in ln]
+    assert p.returncode == 0, out[-2000:] + "\n".join(tb[:40]) + err[:6000]
     line = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 8 and line["dist_backend"] == "gloo"
     assert line["config"]["global_batch"] == 1_000_000
