@@ -265,6 +265,11 @@ int prio3_client_generate_device(prio3_engine* engine, uint32_t n, uint64_t seed
                                  uint8_t* d_leader_out_shares, uint8_t* d_flags,
                                  uint8_t* d_leader_input_shares, void* stream);
 
+/* Frees the idle scratch slabs the device's pool keeps for later calls (up to 1/8 of HBM, shared
+ * by every engine on the GPU; a run an engine or a batch handle still references stays).  For a
+ * process that hands the GPU's memory to something else between batches. */
+int prio3_device_trim(int device);
+
 /* ---- Test / measurement knobs ---- */
 /* force_slow_path=1 routes every report through the general rejection-sampling kernel;
  * leader_fuse_acc=0 turns off the fused device-leader accumulate (A/B); pair_max=N runs

@@ -175,6 +175,15 @@ size_t ws_pool_bytes(int device, size_t* idle_bytes) {
   return p.total_bytes;
 }
 
+// frees every idle scratch slab of the device's pool (the C ABI's prio3_device_trim)
+extern "C" int prio3_device_trim(int device) {
+  if (device < 0 || device >= MAX_DEVICES) return PRIO3_EINVAL;
+  Pool& p = g_pools[device];
+  std::lock_guard<std::mutex> lk(p.mu);
+  trim_locked(p, 0);
+  return PRIO3_OK;
+}
+
 hipStream_t ws_stream_get(int device) {
   if (device < 0 || device >= MAX_DEVICES) return nullptr;
   StreamPool& sp = g_streams[device];

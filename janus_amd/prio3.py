@@ -79,6 +79,7 @@ EXPORTED_SYMBOLS = (
     "prio3_device_accumulate", "prio3_device_output_shares", "prio3_device_combine",
     "prio3_engine_set_option", "prio3_engine_timing", "prio3_engine_timing_reset",
     "prio3_client_generate_device", "prio3_selftest_field", "prio3_trace_enabled", "prio3_device_prepare_aggregate",
+    "prio3_device_trim",
     "prio3_device_aggregate_finish", "prio3_leader_prepare_init_batch",
     "prio3_leader_prepare_next_batch", "prio3_device_leader_prepare_init",
     "prio3_device_leader_prepare_next", "prio3_device_batch_metadata", "prio3_batch_metadata",
@@ -138,6 +139,7 @@ def load_library() -> C.CDLL:
     L.prio3_engine_timing_reset.restype = None
     L.prio3_selftest_field.argtypes = [C.c_int, C.c_uint32, vp, vp, vp]
     L.prio3_trace_enabled.argtypes = []
+    L.prio3_device_trim.argtypes = [C.c_int]
     L.prio3_device_prepare_aggregate.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, vp, C.c_uint32,
                                                  vp, vp, vp]
     L.prio3_device_aggregate_finish.argtypes = [vp, vp, vp, vp, vp, vp]
@@ -151,6 +153,13 @@ def load_library() -> C.CDLL:
     L.prio3_device_combine_metadata.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp]
     _lib = L
     return L
+
+
+def trim_device_pool(device: int = 0) -> None:
+    """Free the idle scratch slabs the engine keeps on `device` (prio3_device_trim)."""
+    rc = load_library().prio3_device_trim(device)
+    if rc:
+        raise RuntimeError(f"prio3_device_trim failed (rc={rc})")
 
 
 def selftest_field(op: int, a: np.ndarray, b: np.ndarray) -> np.ndarray:
