@@ -225,6 +225,9 @@ def main():
     ap.add_argument("--secondary-cpu-seconds", type=float, default=1.5,
                     help="CPU restatement sample size (seconds) for each secondary config line")
     args = ap.parse_args()
+    if os.environ.get("JANUS_BENCH_STACKDUMP"):  # tests: every thread's stack after N s, to stderr
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["JANUS_BENCH_STACKDUMP"]), exit=False)
     if args.role == "leader":
         return leader_main(args)
     if args.role == "hpke":
