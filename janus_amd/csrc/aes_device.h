@@ -116,3 +116,76 @@ DEV void aes128_encrypt(const AesT& T, const uint32_t rk[44], const uint32_t in[
   aes_encrypt<10>(T, rk, in, out);
 }
 
+// -------------------------------------------------------------------------------------
+// The same cipher on a bank-replicated T0 (32 KiB of LDS): entry x of copy c at word 32x + c,
+// and lane l reads copy l mod 32, so each 32-lane group of a ds_read_b32 touches 32 distinct
+// banks whatever the indices (with 4 KiB tables the 32 random indices of a group collide on a
+// bank 3-4 deep).  T1..T3 are T0 rotated (v_alignbit); the S-box is byte 1 of T0.
+// -------------------------------------------------------------------------------------
+struct AesR {
+  uint32_t t[256 * 32];
+};
+
+DEV void aesr_init(AesR& T) {
+  for (uint32_t i = threadIdx.x; i < 256 * 32; i += blockDim.x) {
+    const uint32_t s = c_sbox[i >> 5];
+    const uint32_t s2 = ((s << 1) ^ ((s >> 7) * 0x1bu)) & 0xffu, s3 = s2 ^ s;
+    T.t[i] = s2 | (s << 8) | (s << 16) | (s3 << 24);
+  }
+}
+
+struct AesRLane {
+  const uint32_t* base;  // &T.t[lane mod 32]
+  DEV uint32_t t0(uint32_t x) const { return base[x << 5]; }
+};
+
+DEV AesRLane aesr_lane(const AesR& T) { return AesRLane{T.t + (threadIdx.x & 31u)}; }
+
+DEV uint32_t rotl8(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 24); }
+DEV uint32_t rotl16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
+DEV uint32_t rotl24(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 8); }
+
+// S-box bytes of x's four bytes, in place
+DEV uint32_t aesr_sub_word(const AesRLane& L, uint32_t x) {
+  return ((L.t0(b0(x)) >> 8) & 0xffu) | (L.t0(b1(x)) & 0xff00u) | (L.t0(b2(x)) & 0xff0000u) |
+         ((L.t0(b3(x)) << 8) & 0xff000000u);
+}
+
+DEV void aesr128_expand(const AesRLane& L, const uint32_t key[4], uint32_t rk[44]) {
+  constexpr uint8_t RC[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1b, 0x36};
+#pragma unroll
+  for (int i = 0; i < 4; i++) rk[i] = key[i];
+#pragma unroll
+  for (int i = 4; i < 44; i++) {
+    uint32_t t = rk[i - 1];
+    if ((i & 3) == 0) t = aesr_sub_word(L, __builtin_amdgcn_alignbit(t, t, 8)) ^ RC[i / 4 - 1];
+    rk[i] = rk[i - 4] ^ t;
+  }
+}
+
+DEV void aesr128_encrypt(const AesRLane& L, const uint32_t rk[44], const uint32_t in[4],
+                         uint32_t out[4]) {
+  uint32_t s0 = in[0] ^ rk[0], s1 = in[1] ^ rk[1], s2 = in[2] ^ rk[2], s3 = in[3] ^ rk[3];
+#pragma unroll
+  for (int r = 1; r < 10; r++) {
+    const uint32_t t0 = L.t0(b0(s0)) ^ rotl8(L.t0(b1(s1))) ^ rotl16(L.t0(b2(s2))) ^
+                        rotl24(L.t0(b3(s3))) ^ rk[4 * r];
+    const uint32_t t1 = L.t0(b0(s1)) ^ rotl8(L.t0(b1(s2))) ^ rotl16(L.t0(b2(s3))) ^
+                        rotl24(L.t0(b3(s0))) ^ rk[4 * r + 1];
+    const uint32_t t2 = L.t0(b0(s2)) ^ rotl8(L.t0(b1(s3))) ^ rotl16(L.t0(b2(s0))) ^
+                        rotl24(L.t0(b3(s1))) ^ rk[4 * r + 2];
+    const uint32_t t3 = L.t0(b0(s3)) ^ rotl8(L.t0(b1(s0))) ^ rotl16(L.t0(b2(s1))) ^
+                        rotl24(L.t0(b3(s2))) ^ rk[4 * r + 3];
+    s0 = t0;
+    s1 = t1;
+    s2 = t2;
+    s3 = t3;
+  }
+  const uint32_t x[4] = {s0, s1, s2, s3};
+#pragma unroll
+  for (int c = 0; c < 4; c++)
+    out[c] = (((L.t0(b0(x[c])) >> 8) & 0xffu) | (L.t0(b1(x[(c + 1) & 3])) & 0xff00u) |
+              (L.t0(b2(x[(c + 2) & 3])) & 0xff0000u) |
+              ((L.t0(b3(x[(c + 3) & 3])) << 8) & 0xff000000u)) ^ rk[40 + c];
+}
+

@@ -8,7 +8,8 @@
 // low half (Ctr64BE<Aes128>).  Field64 elements are 8-byte LE chunks, rejected if >= p.
 //
 // One report per lane (k_mp64_prepare), everything in one launch: measurement and proofs
-// shares expanded to SoA scratch, the joint-rand part HMAC streamed over the encoded
+// shares expanded to SoA scratch (one inlined keystream loop with the round keys in registers
+// and a bank-replicated T-table, expand_soa_inl), the joint-rand part HMAC streamed over the encoded
 // measurement share as a 32-bit-word stream (the 26-byte prefix leaves every word a 16-bit
 // funnel shift of two elements), corrected seed, joint and query randomness, then per proof
 // the FLP query (Lagrange basis at t by one batch inversion over the P roots, wire sums, p(t) by
@@ -40,8 +41,11 @@ __global__ __launch_bounds__(256) void k_mp64_prepare(Mp64Params P, uint32_t n, 
                                                       InPtrs in, Scratch sc, OutPtrs out,
                                                       uint32_t force_slow) {
   __shared__ AesT A;
+  __shared__ AesR AR;  // bank-replicated T0 for the two share expansions (expand_soa_inl)
   aes_tables_init(A);
+  if (!LEADER) aesr_init(AR);
   __syncthreads();
+  const AesRLane AL = aesr_lane(AR);
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
   (void)force_slow;
@@ -91,30 +95,22 @@ __global__ __launch_bounds__(256) void k_mp64_prepare(Mp64Params P, uint32_t n, 
     }
     if (!ok) status = PRIO3_STATUS_INPUT_SHARE_DECODE;
   }
-  // 1. measurement share: XOF(k_meas, dst(1), [1])
+  // 1. measurement share: XOF(k_meas, dst(1), [1]); 2. proofs share: XOF(k_proofs, dst(2),
+  //    [np, 1]) -- one loop, so the unrolled keystream (expand_soa_inl) is inlined once
   if (!LEADER) {
-    Msg32<16> m;
-    mz(m);
-    msg_dst(m, P, 1);
-    mbyte(m, 9, 1);
-    uint32_t tag[8];
-    xof_tag(kmeas, m, 10, tag);
-    Stream s;
-    stream_init(A, s, tag);
-    rej += expand_soa(A, s, meas, ld, r, M);
-  }
-  // 2. proofs share: XOF(k_proofs, dst(2), [np, 1])
-  if (!LEADER) {
-    Msg32<16> m;
-    mz(m);
-    msg_dst(m, P, 2);
-    mbyte(m, 9, np);
-    mbyte(m, 10, 1);
-    uint32_t tag[8];
-    xof_tag(kproofs, m, 11, tag);
-    Stream s;
-    stream_init(A, s, tag);
-    rej += expand_soa(A, s, proofs, ld, r, PL * np);
+#pragma nounroll
+    for (int sh = 0; sh < 2; sh++) {
+      Msg32<16> m;
+      mz(m);
+      msg_dst(m, P, 1 + sh);
+      mbyte(m, 9, sh ? np : 1);
+      if (sh) mbyte(m, 10, 1);
+      uint32_t seed[8], tag[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) seed[i] = sh ? kproofs[i] : kmeas[i];
+      xof_tag(seed, m, 10 + sh, tag);
+      rej += expand_soa_inl(AL, tag, sh ? proofs : meas, ld, r, sh ? PL * np : M);
+    }
   }
   // 3. joint-rand part: XOF(k_blind, dst(7), [1] || nonce || enc(meas)) -> 32 bytes
   uint32_t part[8];
@@ -131,13 +127,7 @@ __global__ __launch_bounds__(256) void k_mp64_prepare(Mp64Params P, uint32_t n, 
     uint32_t st[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) st[i] = k.ist[i];
-    for (uint32_t b = 0; b < nblk; b++) {
-      uint32_t w[16];
-#pragma unroll
-      for (int i = 0; i < 16; i++)
-        w[i] = jr_word(16 * b + i, pm.w, meas, ld, r, M, L, 16 * nblk);
-      compress_ni(st, w);
-    }
+    jr_inner_inl(st, pm.w, meas, ld, r, M, L, nblk);
     uint32_t o[16] = {st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], 0x80000000u,
                       0, 0, 0, 0, 0, 0, (64 + 32) * 8};
     uint32_t tag[8];

@@ -15,8 +15,10 @@
 
 namespace {
 
-// This path favours code size over peak issue: the SHA-256 / AES / HMAC building blocks are
-// out-of-line calls (inlined ~40 times they would not fit the register file).
+// The SHA-256 / AES / HMAC building blocks of the short XOF instances are out-of-line calls
+// (inlined ~40 times they would not fit the register file; their arrays pass through the scratch
+// stack).  The two long ones -- the share expansions and the joint-rand part's hash over the
+// measurement share, ~95 % of the blocks -- are inlined once each (expand_soa_inl, jr_inner_inl).
 #define NI __device__ __attribute__((noinline))
 
 NI void compress_ni(uint32_t st[8], uint32_t w[16]) { sha256d::compress(st, w); }
@@ -129,6 +131,59 @@ DEV uint32_t expand_soa(const AesT& A, Stream& s, uint64_t* base, size_t ld, uin
   return rej;
 }
 
+// expand_soa at one inlined call site of the prepare kernel: the key schedule and the
+// encryptions unrolled, so the 44 round-key words stay in registers (the out-of-line
+// aes_enc_ni takes them from the scratch stack, 176 B per block).  Same stream, same rejection.
+DEV void aes_expand_any(const AesT& A, const uint32_t key[4], uint32_t rk[44]) {
+  aes128_expand(A, key, rk);
+}
+DEV void aes_expand_any(const AesRLane& A, const uint32_t key[4], uint32_t rk[44]) {
+  aesr128_expand(A, key, rk);
+}
+DEV void aes_encrypt_any(const AesT& A, const uint32_t rk[44], const uint32_t in[4],
+                         uint32_t out[4]) {
+  aes128_encrypt(A, rk, in, out);
+}
+DEV void aes_encrypt_any(const AesRLane& A, const uint32_t rk[44], const uint32_t in[4],
+                         uint32_t out[4]) {
+  aesr128_encrypt(A, rk, in, out);
+}
+
+template <class TB>
+DEV uint32_t expand_soa_inl(const TB& A, const uint32_t tag[8], uint64_t* base, size_t ld,
+                            uint32_t r, uint32_t n) {
+  uint32_t key[4], rk[44];
+#pragma unroll
+  for (int i = 0; i < 4; i++) key[i] = __builtin_bswap32(tag[i]);
+  aes_expand_any(A, key, rk);
+  const uint32_t iv0 = __builtin_bswap32(tag[4]), iv1 = __builtin_bswap32(tag[5]);
+  uint64_t ctr = ((uint64_t)tag[6] << 32) | tag[7];
+  uint32_t k = 0, rej = 0;
+  while (k < n) {
+    const uint32_t in[4] = {iv0, iv1, __builtin_bswap32((uint32_t)(ctr >> 32)),
+                            __builtin_bswap32((uint32_t)ctr)};
+    uint32_t w[4];
+    aes_encrypt_any(A, rk, in, w);
+    ctr++;
+    const uint64_t c0 = ((uint64_t)w[1] << 32) | w[0], c1 = ((uint64_t)w[3] << 32) | w[2];
+    if (c0 < P64) {
+      base[(size_t)k * ld + r] = c0;
+      k++;
+    } else {
+      rej++;
+    }
+    if (k < n) {
+      if (c1 < P64) {
+        base[(size_t)k * ld + r] = c1;
+        k++;
+      } else {
+        rej++;
+      }
+    }
+  }
+  return rej;
+}
+
 // first 32 bytes of the stream (derive_seed) as LE words
 DEV void derive32(const AesT& A, Stream& s, uint32_t out[8]) {
   stream_block(A, s, out);
@@ -189,6 +244,58 @@ NI uint32_t jr_word(uint32_t t, const uint32_t pre[7], const uint64_t* meas, siz
   uint32_t be = __builtin_bswap32(w);
   if (t == lw) be = (be & 0xffff0000u) | 0x8000u;  // 2 data bytes, then 0x80
   return be;
+}
+
+// The joint-rand part's HMAC inner hash (st = the key's ipad midstate on entry) over the
+// message jr_word describes, with the compression inlined at this one site.  Block b's data
+// bytes 64b - 26 .. 64b + 37 lie in elements 8b - 4 .. 8b + 4: the nine are loaded once, and
+// word i of the block is a 16-bit funnel shift of element 8b - 4 + (floor((4i - 26) / 8) + 4)
+// (odd i: its bytes 2..5) or of it and the next (even i: bytes 6, 7, 0', 1').  The first block
+// (the prefix) and the tail blocks (0x80, zero fill, length) take jr_word's cases.
+DEV void jr_inner_inl(uint32_t st[8], const uint32_t pre[7], const uint64_t* meas, size_t ld,
+                      uint32_t r, uint32_t M, uint32_t L, uint32_t nblk) {
+  const uint32_t lw = L >> 2, nw = 16 * nblk;
+#pragma nounroll
+  for (uint32_t b = 0; b < nblk; b++) {
+    uint64_t v[9];
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+      const int e = (int)(8 * b) - 4 + j;
+      v[j] = (e >= 0 && (uint32_t)e < M) ? ld64(meas, ld, (uint32_t)e, r) : 0ull;
+    }
+    const bool interior = b > 0 && 16 * b + 15 < lw;
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int rel = ((4 * i - 26) >> 3) + 4;  // arithmetic shift: floor
+      const uint64_t x = v[rel];
+      uint32_t dw;
+      if (i & 1) {
+        dw = __builtin_amdgcn_alignbit((uint32_t)(x >> 32), (uint32_t)x, 16);
+      } else {
+        dw = __builtin_amdgcn_alignbit((uint32_t)v[rel + 1], (uint32_t)(x >> 32), 16);
+      }
+      uint32_t be = __builtin_bswap32(dw);
+      if (!interior) {
+        const uint32_t t = 16 * b + i;
+        if (t + 1 == nw) {
+          be = (uint32_t)((64ull + L) * 8);
+        } else if (t + 2 == nw) {
+          be = (uint32_t)(((64ull + L) * 8) >> 32);
+        } else if (t > lw) {
+          be = 0;
+        } else if (t < 6) {
+          be = pre[t];
+        } else if (t == 6) {
+          be = (pre[6] & 0xffff0000u) | (be & 0xffffu);
+        } else if (t == lw) {
+          be = (be & 0xffff0000u) | 0x8000u;
+        }
+      }
+      w[i] = be;
+    }
+    sha256d::compress(st, w);
+  }
 }
 
 }  // namespace
