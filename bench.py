@@ -1019,6 +1019,9 @@ def mp64_main(args):
     vk = bytes(range(0x40, 0x60))
     n = args.reports
     eng = J.HelperEngine(J.Prio3SumVecField64MultiproofHmacSha256Aes128(*cfg), vk, device=0)
+    for kv in args.opt:
+        k, v = kv.split("=")
+        eng.set_option(k, int(v))
     t0 = time.perf_counter()
     gen = eng.generate_reports_device(n, seed=0x4A414E5553000008, with_checks=True)
     torch.cuda.synchronize()

@@ -3200,10 +3200,12 @@ static int prepare_run(prio3_engine* e, Run* R, InPtrs in, OutPtrs out, hipStrea
   const bool pair = pair_takes(e, R->dp, n, fuse, in.leader_src != nullptr);
   R->wshift = pair ? 5u : 6u;
   // auto: one chunk per 128Ki reports on the two-kernel chain; one launch for the fused k_prep_h
-  // (A/B on MI355X, 1 Mi reports: 169.9 M/s at 1 chunk vs 163.2 M/s at 8)
-  const uint32_t K = e->chunks > 0                       ? (uint32_t)e->chunks
-                     : prep_fused_takes(e, R->dp, fuse) ? 1u
-                                                        : std::max(1u, (n + (1u << 16)) >> 17);
+  // (A/B on MI355X, 1 Mi reports: 169.9 M/s at 1 chunk vs 163.2 M/s at 8) and for the one-kernel
+  // multiproof prepare (1 M reports: 93.1-93.3 M/s at 1 chunk vs 89.0-91.5 at 8, r04e2)
+  const uint32_t K = e->chunks > 0 ? (uint32_t)e->chunks
+                     : (prep_fused_takes(e, R->dp, fuse) || R->dp.kind == PRIO3_SUMVEC_F64_MP)
+                         ? 1u
+                         : std::max(1u, (n + (1u << 16)) >> 17);
   const uint32_t csz = ((n + K - 1) / K + 255) & ~255u;
   int deferred = DEFER_NONE;
   if (pair || !allow_chunks || K == 1 || n <= csz || R->dp.kind == PRIO3_FPVEC_BOUNDED_L2) {
