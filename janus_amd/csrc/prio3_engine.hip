@@ -3499,7 +3499,7 @@ int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr, con
                {agg ? R->gaccept : nullptr, L.accept_off, (size_t)g.n}};
     for (const Cp& c : cps)
       if (c.dst && c.bytes &&
-          hipMemcpyAsync(c.dst, hs + c.off, c.bytes, hipMemcpyHostToDevice, gr->cs) != hipSuccess)
+          hipMemcpyAsync(c.dst, hs + c.off, c.bytes, hipMemcpyDefault, gr->cs) != hipSuccess)
         return fail(PRIO3_EDEVICE);
     if (hipEventRecord(gr->ev[1], gr->cs) != hipSuccess ||
         hipStreamWaitEvent(st, gr->ev[1], 0) != hipSuccess)
@@ -3553,7 +3553,7 @@ int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr, con
     if (rc) return fail(rc);
   }
   {  // the outputs go back by one copy launch writing the mapped staging
-    uint8_t* sd = g.stg_dev;
+    uint8_t* sd = g.out_dev;
     PullRanges o{};
     o.src[0] = R->status;
     o.dst[0] = sd + L.status_off;

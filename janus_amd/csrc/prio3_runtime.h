@@ -90,8 +90,10 @@ struct IoLayout {
 void engine_io_layout(const prio3_engine* e, uint32_t cap, IoLayout* L);
 struct GroupView {
   uint32_t n, cap;  // reports staged, staging capacity
-  uint8_t* stg;     // pinned staging (IoLayout for cap)
-  uint8_t* stg_dev;  // the staging as the device addresses it (mapped pinned memory)
+  uint8_t* stg;     // the staged inputs as the job threads write them (IoLayout for cap)
+  uint8_t* stg_dev;  // the same inputs as the device addresses them
+  uint8_t* out;      // pinned output area (same IoLayout; = stg unless the inputs are in VRAM)
+  uint8_t* out_dev;  // the output area as the device addresses it (mapped pinned memory)
   uint32_t n_keys;  // verify keys in the table
   int jobs;         // references the run must carry (one per job)
   uint32_t nseg;    // segments of the aggregating jobs (0: no job aggregates)

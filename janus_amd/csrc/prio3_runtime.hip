@@ -218,11 +218,36 @@ void ws_stream_put(int device, hipStream_t s) {
 namespace {
 
 struct Staging {
-  uint8_t* p = nullptr;
-  uint8_t* dev = nullptr;  // the same pinned bytes as the device addresses them (kernels read
-                           // per-report inputs straight from here: engine_group_issue)
+  uint8_t* p = nullptr;    // inputs, as the job threads write them
+  uint8_t* dev = nullptr;  // the same bytes as the device addresses them (kernels read per-report
+                           // inputs straight from here: engine_group_issue)
+  uint8_t* out = nullptr;  // outputs (pinned, mapped): = p unless the inputs live in VRAM
+  uint8_t* out_dev = nullptr;
   size_t bytes = 0;
+  bool vram = false;  // inputs in fine-grained device memory, written through the PCIe BAR
 };
+
+// JANUS_PRIO3_VRAM_STAGING=1: a prepare group's inputs are staged in fine-grained HBM that the job
+// threads write through the BAR (~42 GB/s from 4-32 host threads, tools/ubench_h2vram.cpp), so
+// the group's kernels read HBM instead of pulling the shares over PCIe inside k_prep_h; the
+// outputs stay in pinned host memory.
+bool vram_staging() {
+  static const bool v = [] {
+    const char* s = getenv("JANUS_PRIO3_VRAM_STAGING");
+    return s && atoi(s) > 0;
+  }();
+  return v;
+}
+
+void staging_free(Staging& s) {
+  if (s.vram) {
+    if (s.p) (void)hipFree(s.p);
+    if (s.out) (void)hipHostFree(s.out);
+  } else if (s.p) {
+    (void)hipHostFree(s.p);
+  }
+  s = Staging();
+}
 
 constexpr size_t STAGING_TARGET = (size_t)96 << 20;  // pinned bytes per group (grows to fit)
 
@@ -232,12 +257,12 @@ struct StagingPool {
 };
 StagingPool* g_staging = new StagingPool[MAX_DEVICES];  // never destroyed (see Exec)
 
-Staging staging_get(int dev, size_t bytes) {
+Staging staging_get(int dev, size_t bytes, bool vram) {
   {
     std::lock_guard<std::mutex> lk(g_staging[dev].mu);
     auto& v = g_staging[dev].idle;
     for (size_t i = 0; i < v.size(); i++)
-      if (v[i].bytes >= bytes) {
+      if (v[i].bytes >= bytes && v[i].vram == vram) {
         Staging s = v[i];
         v.erase(v.begin() + (long)i);
         return s;
@@ -245,13 +270,22 @@ Staging staging_get(int dev, size_t bytes) {
   }
   Staging s;
   s.bytes = std::max(bytes, STAGING_TARGET);
-  if (hipSetDevice(dev) != hipSuccess ||
-      hipHostMalloc((void**)&s.p, s.bytes, hipHostMallocMapped) != hipSuccess ||
-      hipHostGetDevicePointer((void**)&s.dev, s.p, 0) != hipSuccess) {
+  s.vram = vram;
+  bool ok = hipSetDevice(dev) == hipSuccess;
+  if (ok && vram) {
+    ok = hipExtMallocWithFlags((void**)&s.p, s.bytes, hipDeviceMallocFinegrained) == hipSuccess &&
+         hipHostMalloc((void**)&s.out, s.bytes, hipHostMallocMapped) == hipSuccess &&
+         hipHostGetDevicePointer((void**)&s.out_dev, s.out, 0) == hipSuccess;
+    s.dev = s.p;
+  } else if (ok) {
+    ok = hipHostMalloc((void**)&s.p, s.bytes, hipHostMallocMapped) == hipSuccess &&
+         hipHostGetDevicePointer((void**)&s.dev, s.p, 0) == hipSuccess;
+    s.out = s.p;
+    s.out_dev = s.dev;
+  }
+  if (!ok) {
     (void)hipGetLastError();
-    if (s.p) (void)hipHostFree(s.p);
-    s.p = s.dev = nullptr;
-    s.bytes = 0;
+    staging_free(s);
   }
   return s;
 }
@@ -262,7 +296,7 @@ void staging_put(int dev, Staging s) {
   auto& v = g_staging[dev].idle;
   v.push_back(s);
   if (v.size() > 8) {  // keep a few
-    (void)hipHostFree(v.front().p);
+    staging_free(v.front());
     v.erase(v.begin());
   }
 }
@@ -599,7 +633,7 @@ struct Exec {
         delete g;
         return PRIO3_EINVAL;
       }
-      g->stg = staging_get(device, bytes);
+      g->stg = staging_get(device, bytes, P::vram_inputs());
       if (!g->stg.p) {
         delete g;
         return PRIO3_EDEVICE;
@@ -668,6 +702,7 @@ struct PrepPolicy {
   };
   static uint64_t key(Job* j) { return engine_group_key(j->e); }
   static uint32_t reports(const State& s) { return s.n; }
+  static bool vram_inputs() { return vram_staging(); }
   static bool create(State& s, Job* j, size_t* bytes) {
     s.lead = j->e;
     IoLayout l1, l2;
@@ -753,6 +788,8 @@ struct PrepPolicy {
     v.cap = s.cap;
     v.stg = g.p;
     v.stg_dev = g.dev;
+    v.out = g.out;
+    v.out_dev = g.out_dev;
     v.n_keys = (uint32_t)s.keys.size();
     v.jobs = (int)s.jobs;
     v.nseg = s.nseg;
@@ -765,11 +802,11 @@ struct PrepPolicy {
   static void unstage(State& s, Staging& g, Job* j) {
     const IoLayout& L = s.L;
     if (L.msg_len && j->msgs_out)
-      memcpy(j->msgs_out, g.p + L.msg_off + L.msg_len * j->c0, L.msg_len * j->n);
-    if (j->status_out) memcpy(j->status_out, g.p + L.status_off + j->c0, j->n);
+      memcpy(j->msgs_out, g.out + L.msg_off + L.msg_len * j->c0, L.msg_len * j->n);
+    if (j->status_out) memcpy(j->status_out, g.out + L.status_off + j->c0, j->n);
     if (j->nseg) {
-      memcpy(j->agg_out, g.p + L.agg_off + L.agg_len * j->seg0, L.agg_len * j->nseg);
-      memcpy(j->counts_out, g.p + L.cnt_off + 8 * (size_t)j->seg0, 8 * (size_t)j->nseg);
+      memcpy(j->agg_out, g.out + L.agg_off + L.agg_len * j->seg0, L.agg_len * j->nseg);
+      memcpy(j->counts_out, g.out + L.cnt_off + 8 * (size_t)j->seg0, 8 * (size_t)j->nseg);
     }
     j->run = s.run;  // one reference per job (engine_group_finish sets refs = jobs)
   }
@@ -788,6 +825,7 @@ struct AccPolicy {
   };
   static uint64_t key(Job* j) { return (uint64_t)engine_acc_key(j); }
   static uint32_t reports(const State& s) { return s.reps; }
+  static bool vram_inputs() { return false; }  // its host side reads the staging back
   static bool create(State& s, Job* j, size_t* bytes) {
     s.es = (int)engine_acc_key(j);
     const uint32_t reps = std::max(MAX_REPS, j->n);
