@@ -222,9 +222,25 @@ __global__ __launch_bounds__(256) void k_mp64_prepare(Mp64Params P, uint32_t n, 
     const T L0 = Lb[r];
     const uint64_t* pf = proofs + (size_t)k * PL * ld;
     // wire sums at t; r^(idx+1) on the even wires, (m - 1/2) on the odd ones (zero-padded
-    // measurement elements count as 0, VDAF-08 SumVec.eval)
+    // measurement elements count as 0, VDAF-08 SumVec.eval).  With rC = r^C, call kk of column
+    // jj weighs m_(kk C + jj) by r^(jj+1) rC^kk L_(kk+1) on the even wire and by L_(kk+1) on the
+    // odd one, so per column f0 = r^(jj+1) sum_kk m G_kk and f1 = sum_kk m L_(kk+1) - (1/2) SL
+    // with G_kk = rC^kk L_(kk+1) (kept in sc.beta) and SL = sum_kk L_(kk+1): two products per
+    // call instead of four
     T rC = 1;
     for (uint32_t i = 0; i < C; i++) rC = F::mul(rC, rr);
+    uint64_t* Gb = (uint64_t*)sc.beta;
+    T hSL = 0;
+    {
+      T g = 1;
+      for (uint32_t kk = 0; kk < K; kk++) {
+        const T Lk = Lb[(size_t)(kk + 1) * ld + r];
+        Gb[(size_t)kk * ld + r] = F::mul(g, Lk);
+        hSL = F::add(hSL, Lk);
+        g = F::mul(g, rC);
+      }
+      hSL = F::mul(hSL, half);
+    }
     T G = 0, rj = rr;
     const uint8_t* lv = LEADER ? nullptr : lps + (size_t)k * P.vlen * 8;
     T* vo = LEADER ? (T*)(lout + (size_t)k * P.vlen * 8) : nullptr;
@@ -234,16 +250,16 @@ __global__ __launch_bounds__(256) void k_mp64_prepare(Mp64Params P, uint32_t n, 
       return x;
     };
     for (uint32_t jj = 0; jj < C; jj++) {
-      T f0 = F::mul(ld64(pf, ld, 2 * jj, r), L0), f1 = F::mul(ld64(pf, ld, 2 * jj + 1, r), L0);
-      T rp = rj;
+      T s0 = 0, s1 = 0;
       for (uint32_t kk = 0; kk < K; kk++) {
         const uint32_t idx = kk * C + jj;
-        const T Lk = Lb[(size_t)(kk + 1) * ld + r];
-        const T m = idx < M ? ld64(meas, ld, idx, r) : 0;
-        f0 = F::add(f0, F::mul(F::mul(rp, m), Lk));
-        f1 = F::add(f1, F::mul(F::sub(m, half), Lk));
-        rp = F::mul(rp, rC);
+        if (idx >= M) break;  // zero-padded elements add nothing to s0 / s1
+        const T m = ld64(meas, ld, idx, r);
+        s0 = F::add(s0, F::mul(m, Gb[(size_t)kk * ld + r]));
+        s1 = F::add(s1, F::mul(m, Lb[(size_t)(kk + 1) * ld + r]));
       }
+      const T f0 = F::add(F::mul(ld64(pf, ld, 2 * jj, r), L0), F::mul(rj, s0));
+      const T f1 = F::sub(F::add(F::mul(ld64(pf, ld, 2 * jj + 1, r), L0), s1), hSL);
       if (LEADER) {
         vo[1 + 2 * jj] = f0;
         vo[2 + 2 * jj] = f1;
