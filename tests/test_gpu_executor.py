@@ -205,7 +205,9 @@ def test_combined_prepare_aggregate_jobs(name):
     kern = {"count": ("k_prep_gen",), "hist_256_c16": ("k_prep_h", "k_prep_hp"),
             "sum32": ("k_prep_sum",), "hist_100_c10": ("k_xofd", "k_prep_h")}.get(name, ("k_xofd",))
     launches = sum(e.timing().get(k, (0, 0))[1] for e in engines for k in kern)
-    assert 0 < launches < 32, launches
+    # fewer launches than jobs where a launch outlasts a Python caller's way into the C ABI
+    # (see test_concurrent_jobs_of_several_tasks_are_coalesced)
+    assert 0 < launches < 32 if name == "hist_256_c16" else 0 < launches <= 32, launches
 
 
 def test_combined_prepare_aggregate_single_job_and_empty():
