@@ -36,8 +36,11 @@ typedef uint64_t T;
 // k_blind): the shares are decoded (non-canonical -> INPUT_SHARE_DECODE) instead of expanded,
 // the verifier share || joint-rand part is written to out.prep_msgs (stride prep_share_len), and
 // the corrected seed is kept for prepare_next (words 0-3 in sc.corrected, 4-7 in sc.part).
+// 4 waves per SIMD (120 VGPRs, a few more spilled bytes in the short XOF calls; 37 KiB of LDS per
+// block still fits four blocks per CU): 100.9-101.2 against 96.8-97.0 M reports/s at the
+// default's 132 VGPRs / 3 waves (r04p, interleaved)
 template <int LEADER>
-__global__ __launch_bounds__(256) void k_mp64_prepare(Mp64Params P, uint32_t n, size_t ld,
+__global__ __launch_bounds__(256, 4) void k_mp64_prepare(Mp64Params P, uint32_t n, size_t ld,
                                                       InPtrs in, Scratch sc, OutPtrs out,
                                                       uint32_t force_slow) {
   __shared__ AesT A;
