@@ -96,7 +96,11 @@ int janus_hpke_open_input_shares_device(janus_hpke_opener* opener, uint32_t n,
                                         uint32_t public_share_len, uint32_t helper_share_len,
                                         int require_taskprov, uint8_t* d_helper_shares,
                                         uint8_t* d_status, void* stream);
-/* Host-buffer form (blocking). */
+/* Host-buffer form (blocking).  Concurrent calls -- the helper opens each job's reports on the
+ * job's own rayon worker (/root/reference/aggregator/src/aggregator.rs:1847-1890) -- are coalesced
+ * by the GPU's HPKE executor into shared launches: every opener's jobs with the same ct_stride,
+ * share lengths and taskprov flag, whatever their task IDs (each report carries its task's slot in
+ * the group's task-ID table for the AAD). */
 int janus_hpke_open_input_shares(janus_hpke_opener* opener, uint32_t n, const uint8_t task_id[32],
                                  const uint8_t* enc, const uint8_t* ct, const uint32_t* ct_len,
                                  uint32_t ct_stride, const uint8_t* report_ids,
@@ -114,6 +118,15 @@ int janus_hpke_open_device(janus_hpke_opener* opener, uint32_t n, const uint8_t*
 int janus_hpke_open(janus_hpke_opener* opener, uint32_t n, const uint8_t* enc, const uint8_t* ct,
                     const uint32_t* ct_len, uint32_t ct_stride, const uint8_t* aad,
                     const uint32_t* aad_len, uint32_t aad_stride, uint8_t* pt, uint8_t* status);
+
+/* The GPU's HPKE executor (shared by every opener on the GPU): counters, and control -- "hold"
+ * 1/0 (tests queue jobs behind it), "heavy" N (as prio3_executor_control), "coalesce" 0/1 (this
+ * opener's host-buffer opens launch alone / through the executor, the default). */
+typedef struct {
+  uint64_t jobs, reports, groups, active_jobs, active_reports;
+} janus_hpke_executor_stats;
+int janus_hpke_executor_stats_get(const janus_hpke_opener* opener, janus_hpke_executor_stats* out);
+int janus_hpke_executor_control(janus_hpke_opener* opener, const char* key, int64_t value);
 
 /* Per-kernel HIP-event timing of the opener's launches (as prio3_engine_timing). */
 int janus_hpke_set_timing(janus_hpke_opener* opener, int on);

@@ -105,6 +105,50 @@ int prio3_engine_create_ex(const prio3_params* params, const uint8_t* verify_key
                            size_t verify_key_len, int device, prio3_engine** out);
 void prio3_engine_destroy(prio3_engine* engine);
 
+/* One engine over several GPUs of the node: the `device_mask` form of SURVEY.md 8(b)'s
+ * prio3_engine_create.  A Janus helper process that owns the node's GPUs creates each task's
+ * engine over all of them (bit d = GPU d).  Host-buffer jobs (prio3_helper_prepare_batch,
+ * prio3_helper_prepare_aggregate_batch, prio3_leader_prepare_init_batch) go whole to the GPU
+ * whose executor holds the fewest reports -- the jobs of every engine of the same VDAF instance
+ * counted, equally loaded GPUs taken in turn -- and are coalesced there with the other engines'
+ * concurrent jobs.  No collective: a job's outputs (prepare messages, statuses, aggregate shares,
+ * batch handle) come back whole from the GPU that ran it, and Janus already merges per-job
+ * aggregations at collection (aggregation_job_writer.rs:510 writes a random `ord` shard per job;
+ * aggregate_share.rs:55-96 sums them).  Device-resident entry points act on the lowest GPU of the
+ * mask.  Options set on the engine apply to every GPU's part. */
+int prio3_engine_create_mask(const prio3_params* params, const uint8_t* verify_key,
+                             size_t verify_key_len, int device_mask, prio3_engine** out);
+/* The same over an explicit device list; a GPU named k times gets k executors of its own (lanes
+ * 0..k-1, at most 8), which lets a one-GPU box rehearse the placement (tests). */
+int prio3_engine_create_devices(const prio3_params* params, const uint8_t* verify_key,
+                                size_t verify_key_len, const int* devices, uint32_t n_devices,
+                                prio3_engine** out);
+typedef struct {
+  int32_t device;        /* the member's GPU */
+  uint32_t lane;         /* its executor on that GPU (0 unless the device list repeats the GPU) */
+  uint64_t jobs;         /* host-buffer jobs this engine placed on the member */
+  uint64_t reports;      /* their reports */
+  uint64_t exec_jobs;    /* jobs the member's helper executor took (every engine sharing it) */
+  uint64_t exec_groups;  /* group launches of that executor */
+} prio3_member_info;
+/* Fills out[0 .. min(cap, members)) and returns the member count (1 for a one-GPU engine). */
+int prio3_engine_members(const prio3_engine* engine, prio3_member_info* out, uint32_t cap);
+/* Counters of one executor a member's jobs use (shared with every engine of the same instance on
+ * that GPU): kind 0 helper prepare, 1 accumulate, 2 leader prepare_init, 3 leader prepare_next. */
+typedef struct {
+  uint64_t jobs, reports;  /* submitted since the process started */
+  uint64_t groups;         /* launches */
+  uint64_t active_jobs, active_reports;  /* inside the executor now */
+} prio3_executor_stats;
+int prio3_executor_stats_get(const prio3_engine* engine, uint32_t member, int kind,
+                             prio3_executor_stats* out);
+/* Executor control on the executors of `kind` (as above; -1: every kind) that the engine's jobs
+ * use (shared with the other engines of the same GPUs): "hold" = 1 -- launch nothing until
+ * "hold" = 0 (tests queue jobs behind it to pin coalescing); "heavy" = N -- reports inside the
+ * executor at which it switches from its light-load pipeline to the heavy-load launcher
+ * (0: the default 32768; 1: always the heavy-load one). */
+int prio3_executor_control(prio3_engine* engine, int kind, const char* key, int64_t value);
+
 /* ---- Host-buffer entry points (what the Rust FFI calls from inside rayon::spawn) ---- */
 
 /* Prepares n reports.  Inputs are packed per report:
@@ -273,10 +317,8 @@ int prio3_device_trim(int device);
 /* ---- Test / measurement knobs ---- */
 /* force_slow_path=1 routes every report through the general rejection-sampling kernel;
  * leader_fuse_acc=0 turns off the fused device-leader accumulate (A/B); pair_max=N runs
- * Histogram(P = 32) prepares of at most N reports on lane pairs (0: never); group_dma=N sends
- * the host-buffer executor's groups of at most N reports to the device by DMA on a copy stream
- * instead of the kernels pulling them from pinned staging (0: never, the default; -1: always);
- * the other keys are the launch variants prio3_engine.hip's prio3_engine_set_option lists. */
+ * Histogram(P = 32) prepares of at most N reports on lane pairs (0: never); the other keys are
+ * the launch variants prio3_engine.hip's prio3_engine_set_option lists. */
 int prio3_engine_set_option(prio3_engine* engine, const char* key, int64_t value);
 /* Per-kernel device time (ms) accumulated since the last reset, measured with HIP events
  * on the launch stream when option "timing" is 1 (2: launches counted, no events or times).

@@ -29,6 +29,7 @@
 #include "x448_device.h"
 #include "sha512_device.h"
 #include "sha256_host.h"
+#include "prio3_runtime.h"
 
 // -------------------------------------------------------------------------------------
 // GF(2^255 - 19), values in [0, 2^256) (loosely reduced), 8 little-endian 32-bit limbs
@@ -616,7 +617,16 @@ struct OpenArgs {
   const uint32_t *ct_len, *aad_len;
   const uint64_t* times;
   uint8_t *pt, *shares, *status;
+  // coalesced groups of several tasks (the executor): per-report slot into task_tab[slot][8]
+  // (BE words, like HpkeParams::task); nullable: HpkeParams::task
+  const uint16_t* task_slot;
+  const uint32_t* task_tab;
 };
+
+// word i of report r's task ID (input-share AAD), BE
+DEV uint32_t task_word(const HpkeParams& P, const OpenArgs& a, uint32_t r, int i) {
+  return a.task_slot ? a.task_tab[8 * (size_t)a.task_slot[r] + i] : P.task[i];
+}
 
 DEV void load16(const uint8_t* p, uint32_t* w) {
   const uint4 v = *(const uint4*)p;
@@ -959,7 +969,7 @@ __global__ __launch_bounds__(256) HPKE_WAVES void k_hpke_open(HpkeParams P, Open
 #pragma unroll
     for (int i = 0; i < ((AW + 3) / 4) * 4; i++) aw[i] = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) aw[i] = P.task[i];
+    for (int i = 0; i < 8; i++) aw[i] = task_word(P, a, r, i);
     uint32_t idw[4];
     load16(a.ids + 16 * (size_t)r, idw);
 #pragma unroll
@@ -1064,7 +1074,7 @@ __global__ __launch_bounds__(256) HPKE_WAVES void k_hpke_open(HpkeParams P, Open
 #pragma unroll
     for (int i = 0; i < ((AW + 3) / 4) * 4; i++) aw[i] = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) aw[i] = __builtin_bswap32(P.task[i]);
+    for (int i = 0; i < 8; i++) aw[i] = __builtin_bswap32(task_word(P, a, r, i));
     uint32_t idw[4];
     load16(a.ids + 16 * (size_t)r, idw);
 #pragma unroll
@@ -1376,6 +1386,7 @@ static void recode_w4(const uint32_t* sk, const uint32_t* n, int nw, int ndig, i
 
 struct janus_hpke_opener {
   int device = 0;
+  int coalesce = 1;  // host-buffer opens through the executor (janus_hpke_executor_control)
   hipStream_t stream = nullptr;
   HpkeParams P;
   uint8_t* d_pt = nullptr;
@@ -1587,6 +1598,114 @@ static int ensure_pt(janus_hpke_opener* o, size_t bytes) {
   return JANUS_HPKE_SUCCESS;
 }
 
+// ---- executor hooks (prio3_runtime.h) ----
+int hpke_opener_device(const janus_hpke_opener* o) { return o->device; }
+
+uint64_t hpke_group_key(const HpkeJob* j) {
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
+  mix((uint64_t)(uintptr_t)j->o);
+  mix(j->ct_stride);
+  mix(j->pub_len);
+  mix(j->share_len);
+  mix((uint64_t)j->require_taskprov);
+  mix((uint64_t)j->o->timing);
+  return h;
+}
+
+void hpke_layout(const HpkeJob* j, uint32_t cap, HpkeLayout* L) {
+  auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  L->nenc = (uint32_t)kem_nenc((uint16_t)j->o->P.kem);
+  size_t off = 0;
+  L->off_enc = off;
+  off += up((size_t)L->nenc * cap);
+  L->off_ct = off;
+  off += up((size_t)j->ct_stride * cap);
+  L->off_len = off;
+  off += up(4 * (size_t)cap);
+  L->off_ids = off;
+  off += up(16 * (size_t)cap);
+  L->off_times = off;
+  off += up(8 * (size_t)cap);
+  L->off_pub = off;
+  off += up((size_t)j->pub_len * cap);
+  L->slot_off = off;
+  off += up(2 * (size_t)cap);
+  L->tab_off = off;
+  off += up(32 * (size_t)HPKE_MAX_TASKS);
+  L->shares_off = off;
+  off += up((size_t)j->share_len * cap + 1);
+  L->status_off = off;
+  off += up(cap);
+  L->pt_off = off;
+  off += up((size_t)j->ct_stride * cap);
+  L->bytes = off;
+}
+
+// The group's per-field inputs to a device mirror (pinned-memory DMA), the open kernel (its AAD
+// task IDs from the group's table), the helper shares and statuses back into the staging.
+int hpke_group_issue(const HpkeJob& pj, const HpkeLayout& L, const uint8_t* stg, uint8_t* out,
+                     uint32_t n, hipStream_t* st_out, Slab** slab_out) {
+  janus_hpke_opener* o = pj.o;
+  *st_out = nullptr;
+  *slab_out = nullptr;
+  HCHK(hipSetDevice(o->device));
+  hipStream_t st = ws_stream_get(o->device);
+  if (!st) return JANUS_HPKE_EDEVICE;
+  int rc = JANUS_HPKE_SUCCESS;
+  Slab* sl = ws_acquire(o->device, L.bytes, st, &rc);
+  if (!sl) {
+    ws_stream_put(o->device, st);
+    return rc;
+  }
+  uint8_t* b = sl->base;
+  const struct {
+    size_t off, bytes;
+  } f[] = {{L.off_enc, (size_t)L.nenc * n},    {L.off_ct, (size_t)pj.ct_stride * n},
+           {L.off_len, 4 * (size_t)n},         {L.off_ids, 16 * (size_t)n},
+           {L.off_times, 8 * (size_t)n},       {L.off_pub, (size_t)pj.pub_len * n},
+           {L.slot_off, 2 * (size_t)n},        {L.tab_off, 32 * (size_t)HPKE_MAX_TASKS}};
+  for (auto& x : f)
+    if (rc == JANUS_HPKE_SUCCESS && x.bytes &&
+        hipMemcpyAsync(b + x.off, stg + x.off, x.bytes, hipMemcpyHostToDevice, st) != hipSuccess)
+      rc = JANUS_HPKE_EDEVICE;
+  if (rc == JANUS_HPKE_SUCCESS) {
+    OpenArgs a{};
+    a.n = n;
+    a.ct_stride = pj.ct_stride;
+    a.share_len = pj.share_len;
+    a.require_taskprov = pj.require_taskprov;
+    a.enc = b + L.off_enc;
+    a.ct = b + L.off_ct;
+    a.ct_len = (const uint32_t*)(b + L.off_len);
+    a.ids = b + L.off_ids;
+    a.times = (const uint64_t*)(b + L.off_times);
+    a.pubs = pj.pub_len ? b + L.off_pub : nullptr;
+    a.pt = b + L.pt_off;
+    a.shares = b + L.shares_off;
+    a.status = b + L.status_off;
+    a.task_slot = (const uint16_t*)(b + L.slot_off);
+    a.task_tab = (const uint32_t*)(b + L.tab_off);
+    std::lock_guard<std::mutex> lk(o->mu);  // o->P and the timing list
+    rc = launch_open(o, 1, (int)pj.pub_len, a, st);
+  }
+  if (rc == JANUS_HPKE_SUCCESS &&
+      (hipMemcpyAsync(out + L.shares_off, b + L.shares_off, (size_t)pj.share_len * n,
+                      hipMemcpyDeviceToHost, st) != hipSuccess ||
+       hipMemcpyAsync(out + L.status_off, b + L.status_off, n, hipMemcpyDeviceToHost, st) !=
+           hipSuccess))
+    rc = JANUS_HPKE_EDEVICE;
+  if (rc != JANUS_HPKE_SUCCESS) {
+    (void)hipStreamSynchronize(st);
+    ws_release(sl, st);
+    ws_stream_put(o->device, st);
+    return rc;
+  }
+  *st_out = st;
+  *slab_out = sl;
+  return JANUS_HPKE_SUCCESS;
+}
+
 extern "C" {
 
 int janus_hpke_open_input_shares_device(janus_hpke_opener* o, uint32_t n,
@@ -1788,8 +1907,31 @@ int janus_hpke_open_input_shares(janus_hpke_opener* o, uint32_t n, const uint8_t
                                  const uint64_t* times, const uint8_t* public_shares,
                                  uint32_t public_share_len, uint32_t helper_share_len,
                                  int require_taskprov, uint8_t* helper_shares, uint8_t* status) {
-  if (!o) return JANUS_HPKE_EINVAL;
+  if (!o || !task_id) return JANUS_HPKE_EINVAL;
   if (n == 0) return JANUS_HPKE_SUCCESS;
+  if (!enc || !ct || !ct_len || !report_ids || !times || !helper_shares || !status ||
+      ct_stride == 0 || ct_stride % 16 != 0 || (public_share_len != 0 && public_share_len != 32) ||
+      (public_share_len && !public_shares))
+    return JANUS_HPKE_EINVAL;
+  if (o->coalesce) {  // concurrent jobs of every task on this keypair: one launch (exec_hpke)
+    HpkeJob j;
+    j.o = o;
+    j.n = n;
+    j.task_id = task_id;
+    j.enc = enc;
+    j.ct = ct;
+    j.ct_len = ct_len;
+    j.ct_stride = ct_stride;
+    j.ids = report_ids;
+    j.times = times;
+    j.pubs = public_shares;
+    j.pub_len = public_share_len;
+    j.share_len = helper_share_len;
+    j.require_taskprov = require_taskprov;
+    j.shares_out = helper_shares;
+    j.status_out = status;
+    return exec_hpke(&j);
+  }
   HCHK(hipSetDevice(o->device));
   DevBuf de, dc, dl, di, dt, dp, ds, dst;
   int rc;
@@ -1812,6 +1954,28 @@ int janus_hpke_open_input_shares(janus_hpke_opener* o, uint32_t n, const uint8_t
   HCHK(hipMemcpyAsync(status, dst.p, n, hipMemcpyDeviceToHost, o->stream));
   HCHK(hipStreamSynchronize(o->stream));
   return JANUS_HPKE_SUCCESS;
+}
+
+int janus_hpke_executor_stats_get(const janus_hpke_opener* o, janus_hpke_executor_stats* out) {
+  if (!o || !out) return JANUS_HPKE_EINVAL;
+  ExecStats st;
+  const int rc = exec_stats(EXEC_HPKE, o->device * EXEC_LANES, &st);
+  if (rc) return rc;
+  out->jobs = st.jobs;
+  out->reports = st.reports;
+  out->groups = st.groups;
+  out->active_jobs = st.active_jobs;
+  out->active_reports = st.active_reports;
+  return JANUS_HPKE_SUCCESS;
+}
+
+int janus_hpke_executor_control(janus_hpke_opener* o, const char* key, int64_t value) {
+  if (!o || !key) return JANUS_HPKE_EINVAL;
+  if (!strcmp(key, "coalesce")) {
+    o->coalesce = value != 0;
+    return JANUS_HPKE_SUCCESS;
+  }
+  return exec_control(EXEC_HPKE, o->device * EXEC_LANES, key, value);
 }
 
 int janus_hpke_selftest_p256(int op, uint32_t n, const uint32_t* a, const uint32_t* b,

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "prio3_common.h"
+#include "prio3_runtime.h"
 #include "prio3_mp64_xof.h"
 
 struct GenScratch {
@@ -956,7 +957,7 @@ template <class F>
 __global__ __launch_bounds__(64) void k_leader_init(DevParams p, const uint8_t* nonces,
                                                     const uint8_t* pub, const uint8_t* lshares,
                                                     Scratch sc, uint8_t* prep_shares,
-                                                    uint8_t* status) {
+                                                    uint8_t* status, InPtrs keys) {
   typedef typename F::T T;
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= p.n) return;
@@ -984,7 +985,8 @@ __global__ __launch_bounds__(64) void k_leader_init(DevParams p, const uint8_t* 
   // query randomness
   {
     const uint8_t b1[1] = {1};
-    uint32_t vk[4] = {p.vk[0], p.vk[1], p.vk[2], p.vk[3]};
+    uint32_t vk[4];
+    load_vk(p, keys, r, vk);  // coalesced groups of several tasks: the report's own key
     KState s;
     kzero(s);
     Msg m;
@@ -1010,7 +1012,8 @@ __global__ __launch_bounds__(64) void k_leader_init(DevParams p, const uint8_t* 
     sc.corrected[r] = make_uint4(cor[0], cor[1], cor[2], cor[3]);
   }
   if (flag) {  // a rejection-sampling event: redo the expansions with the byte-level sponge
-    uint32_t vk[4] = {p.vk[0], p.vk[1], p.vk[2], p.vk[3]};
+    uint32_t vk[4];
+    load_vk(p, keys, r, vk);
     uint8_t b[17];
     b[0] = 1;
     for (int i = 0; i < 16; i++) b[1 + i] = (uint8_t)(nonce[i >> 2] >> (8 * (i & 3)));
@@ -1065,6 +1068,53 @@ __global__ __launch_bounds__(256) void k_leader_next(DevParams p, const uint8_t*
   }
 }
 
+// prepare_next of many jobs' leader batches (of different runs) in one launch: block row y is
+// job y (its descriptor, prepare messages and statuses in the executor's mapped staging); the
+// verdict goes back to the staging and to the run's device statuses (which prio3_accumulate
+// reads).  Same per-report work as k_leader_next.
+template <class F>
+__global__ __launch_bounds__(256) void k_leader_next_multi(const LNextDesc* descs,
+                                                           const uint8_t* msgs, uint8_t* status) {
+  typedef typename F::T T;
+  __shared__ LNextDesc D;
+  if (threadIdx.x == 0) D = descs[blockIdx.y];
+  __syncthreads();
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= D.n) return;
+  const size_t g = (size_t)D.rep_off + r, ld = D.ld;
+  uint8_t st = status[g];
+  if (st == PRIO3_STATUS_FINISHED && D.jr) {
+    uint32_t m[4];
+    load16(msgs + 16 * g, m);
+    const uint4 c = D.corrected[r];
+    if (m[0] != c.x || m[1] != c.y || m[2] != c.z || m[3] != c.w) st = PRIO3_STATUS_PREP_NEXT;
+  }
+  status[g] = st;
+  D.dstatus[r] = st;
+  if (D.kind == PRIO3_SUM || D.kind == PRIO3_SUMVEC) {
+    const uint32_t outs = D.kind == PRIO3_SUM ? 1 : D.out_len;
+    for (uint32_t e = 0; e < outs; e++) {
+      T acc = F::zero(), pw = F::one();
+      for (uint32_t b = 0; b < D.bits; b++) {
+        acc = F::add(acc, F::mul(pw, F::load(D.meas, (size_t)(e * D.bits + b) * ld + r)));
+        pw = F::add(pw, pw);
+      }
+      F::store(D.out, (size_t)e * ld + r, acc);
+    }
+  }
+}
+
+extern "C" int launch_leader_next_multi(uint32_t es, const LNextDesc* d_desc, const uint8_t* d_msgs,
+                                        uint8_t* d_status, uint32_t n_jobs, uint32_t max_n,
+                                        hipStream_t st) {
+  const dim3 grid((max_n + 255) / 256, n_jobs);
+  if (es == 16)
+    k_leader_next_multi<Fp128><<<grid, 256, 0, st>>>(d_desc, d_msgs, d_status);
+  else
+    k_leader_next_multi<Fp64><<<grid, 256, 0, st>>>(d_desc, d_msgs, d_status);
+  return hipGetLastError() == hipSuccess ? PRIO3_OK : PRIO3_EDEVICE;
+}
+
 // a leader prepare_init that did not finish marks the generated report unusable
 __global__ void k_fg_status(const uint8_t* status, uint8_t* flags, uint32_t n) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1073,14 +1123,18 @@ __global__ void k_fg_status(const uint8_t* status, uint8_t* flags, uint32_t n) {
 
 extern "C" int launch_leader_init(const DevParams& dp, const uint8_t* d_nonces, const uint8_t* d_pub,
                        const uint8_t* d_lshares, const Scratch& sc, uint8_t* d_prep_shares,
-                       uint8_t* d_status, hipStream_t st) {
+                       uint8_t* d_status, hipStream_t st, const uint16_t* vk_slot,
+                       const uint4* vk_tab) {
   const uint32_t blocks = (dp.n + 63) / 64;
+  InPtrs keys{};
+  keys.vk_slot = vk_slot;
+  keys.vk_tab = vk_tab;
   if (dp.es == 16)
     k_leader_init<Fp128><<<blocks, 64, 0, st>>>(dp, d_nonces, d_pub, d_lshares, sc,
-                                                d_prep_shares, d_status);
+                                                d_prep_shares, d_status, keys);
   else
     k_leader_init<Fp64><<<blocks, 64, 0, st>>>(dp, d_nonces, d_pub, d_lshares, sc,
-                                               d_prep_shares, d_status);
+                                               d_prep_shares, d_status, keys);
   return hipGetLastError() == hipSuccess ? PRIO3_OK : PRIO3_EDEVICE;
 }
 

@@ -662,10 +662,6 @@ struct prio3_engine {
   // option: Histogram (P = 32) prepares of at most this many reports run on lane pairs
   // (k_prep_hp; 0 = never): below ~3 waves per SIMD the one-lane k_prep_h leaves SIMDs idle
   int pair_max = 196608;
-  // executor groups of at most group_dma reports send their inputs to the device by DMA on a copy
-  // stream, issued while the previous group computes; larger groups are pulled from the mapped
-  // staging by their kernels (0: never DMA, the default -- DESIGN.md 11; -1: always)
-  int group_dma = 0;
   int timing = 0;
   Mp64Params mp{};  // PRIO3_SUMVEC_F64_MP only
   uint64_t* d_sigma64 = nullptr;
@@ -674,5 +670,15 @@ struct prio3_engine {
   std::vector<hipEvent_t> ev_pool;
   std::mutex tmu;  // timing bookkeeping (launches may come from several executor threads)
   std::mutex mu;   // device-resident calls, `cur`, side streams
+  // ---- one engine over several GPUs (prio3_engine_create_devices / _mask) ----
+  // lane: this engine's executor on its GPU (0 unless a device list names the GPU again)
+  int lane = 0;
+  // members[0] is the engine itself; the others are engines of the same instance and verify key
+  // on the other listed GPUs (owned by it).  Host-buffer jobs go to the least-loaded member;
+  // device-resident calls act on members[0].
+  std::vector<prio3_engine*> members;
+  prio3_engine* owner = nullptr;   // the engine whose member this is (nullptr: itself)
+  std::atomic<uint32_t> rr{0};     // round-robin start among equally loaded members
+  std::atomic<uint64_t> placed_jobs{0}, placed_reports{0};  // host-buffer jobs placed here
 };
 

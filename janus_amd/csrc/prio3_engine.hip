@@ -838,7 +838,11 @@ __global__ __launch_bounds__(256) void k_leader_unpack(DevParams p, InPtrs in, S
   Msg m;
   msg_zero(m);
   msg_dst(m, p.dst[5]);
-  msg_bytes16(m, 9, p.vk);
+  {
+    uint32_t vk[4];
+    load_vk(p, in, r, vk);  // coalesced groups of several tasks: the report's own key
+    msg_bytes16(m, 9, vk);
+  }
   msg_byte(m, 25, 1);
   msg_bytes16(m, 26, nonce);
   msg_absorb_final(s, m, 42);
@@ -867,7 +871,8 @@ __global__ __launch_bounds__(64) void k_leader_slowfix(DevParams p, InPtrs in, S
   uint8_t b[17];
   b[0] = 1;
   for (int i = 0; i < 16; i++) b[1 + i] = (uint8_t)(nonce[i >> 2] >> (8 * (i & 3)));
-  uint32_t vk[4] = {p.vk[0], p.vk[1], p.vk[2], p.vk[3]};
+  uint32_t vk[4];
+  load_vk(p, in, r, vk);
   bx_expand<F>(p.dst[5], vk, b, 17, p.qr_len, sc.qr, p.ld, r);
   const uint4 c = sc.corrected[r];
   const uint32_t cor[4] = {c.x, c.y, c.z, c.w};
@@ -3235,7 +3240,8 @@ static int prepare_run(prio3_engine* e, Run* R, InPtrs in, OutPtrs out, hipStrea
 // the leader's prepare_init (agg_id 0) over the run
 extern "C" int launch_leader_init(const DevParams& dp, const uint8_t* d_nonces, const uint8_t* d_pub,
                                   const uint8_t* d_lshares, const Scratch& sc,
-                                  uint8_t* d_prep_shares, uint8_t* d_status, hipStream_t st);
+                                  uint8_t* d_prep_shares, uint8_t* d_status, hipStream_t st,
+                                  const uint16_t* vk_slot, const uint4* vk_tab);
 extern "C" int launch_leader_next(const DevParams& dp, const uint8_t* d_prep_msgs, const Scratch& sc,
                        uint8_t* d_status, hipStream_t st);
 
@@ -3277,9 +3283,11 @@ static int leader_init_fpvec(prio3_engine* e, Run* R, const uint8_t* d_nonces,
   return PRIO3_OK;
 }
 
+// vk_slot / vk_tab (nullable): per-report verify keys of a coalesced group of several tasks
 static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
                            const uint8_t* d_public_shares, const uint8_t* d_leader_input_shares,
-                           uint8_t* d_prep_shares, uint8_t* d_status, hipStream_t st) {
+                           uint8_t* d_prep_shares, uint8_t* d_status, hipStream_t st,
+                           const uint16_t* vk_slot = nullptr, const uint4* vk_tab = nullptr) {
   DevParams dp = R->dp;
   dp.force_slow = (uint32_t)e->force_slow;
   const uint32_t n = R->n;
@@ -3299,6 +3307,8 @@ static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
   if (ps && dp.jr_len && (dp.P == 32 || dp.P == 16 || dp.P == 8) && e->leader_fast) {
     // the helper kernels in their leader role
     InPtrs in{d_nonces, d_public_shares, d_leader_input_shares, nullptr};
+    in.vk_slot = vk_slot;
+    in.vk_tab = vk_tab;
     OutPtrs out{d_prep_shares, d_status};
     const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
     // R->lfused: the wave partials of the share for segment 0, fixed up at accumulate
@@ -3320,6 +3330,8 @@ static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
   if (dp.kind == PRIO3_SUM && e->leader_fast && query_sum_takes(dp)) {
     // Prio3Sum: the same unpack / joint-rand kernels, then k_query_sum in its leader role
     InPtrs in{d_nonces, d_public_shares, d_leader_input_shares, nullptr};
+    in.vk_slot = vk_slot;
+    in.vk_tab = vk_tab;
     OutPtrs out{d_prep_shares, d_status};
     const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
     TIMED(e, st, "k_leader_unpack",
@@ -3335,12 +3347,39 @@ static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
   int rc2 = PRIO3_OK;
   TIMED(e, st, "k_leader_init",
         rc2 = launch_leader_init(dp, d_nonces, d_public_shares, d_leader_input_shares, R->sc,
-                                 d_prep_shares, d_status, st));
+                                 d_prep_shares, d_status, st, vk_slot, vk_tab));
   return rc2;
 }
 
 // ---- executor hooks (prio3_runtime.h) ----
 int engine_device(const prio3_engine* e) { return e->device; }
+int engine_exec_id(const prio3_engine* e) { return e->device * EXEC_LANES + e->lane; }
+
+// Host-buffer jobs of a multi-GPU engine go whole to the member whose executor holds the fewest
+// reports (all engines' jobs counted: tasks of one instance share the executors), equally loaded
+// members taken round-robin.  No collective: each job's outputs come back from the GPU that ran
+// it, and Janus merges the per-job aggregations at collection
+// (/root/reference/aggregator/src/aggregator/aggregation_job_writer.rs:510 writes a random `ord`
+// shard per job; aggregate_share.rs:55-96 sums the shards).
+static prio3_engine* place(prio3_engine* e, uint32_t n) {
+  prio3_engine* best = e;
+  const size_t k = e->members.size();
+  if (k > 1) {
+    const uint32_t s0 = e->rr.fetch_add(1, std::memory_order_relaxed);
+    uint64_t bl = UINT64_MAX;
+    for (size_t i = 0; i < k; i++) {
+      prio3_engine* m = e->members[(s0 + i) % k];
+      const uint64_t l = exec_load(engine_exec_id(m));
+      if (l < bl) {
+        bl = l;
+        best = m;
+      }
+    }
+  }
+  best->placed_jobs.fetch_add(1, std::memory_order_relaxed);
+  best->placed_reports.fetch_add(n, std::memory_order_relaxed);
+  return best;
+}
 
 void engine_vk(const prio3_engine* e, uint8_t out[16]) { memcpy(out, e->dp.vk, 16); }
 
@@ -3362,7 +3401,7 @@ uint64_t engine_group_key(const prio3_engine* e) {
   // engine must not silently run with the lead engine's options)
   const int opts[] = {e->force_slow, e->chunks, e->fuse_acc,           e->leader_fast,
                       e->leader_fuse_acc, e->fp_round, e->experimental_fpvec, e->force_generic,
-                      e->timing, e->pair_max, e->group_dma};
+                      e->timing, e->pair_max};
   h = fnv(h, opts, sizeof opts);
   h = fnv(h, &e->fp_sub_bytes, sizeof e->fp_sub_bytes);
   // XofHmacSha256Aes128 keys enter the kernels as HMAC midstates: one engine per launch; an
@@ -3416,25 +3455,16 @@ static int fused_finish(prio3_engine* e, Run* R, const uint8_t* d_status, const 
                         const uint32_t* fix_seg, const uint8_t* d_accept_mask, uint32_t S,
                         uint8_t* d_agg_shares, uint64_t* d_counts, hipStream_t st);
 
-// Group launch.  DMA (option group_dma: groups of at most that many reports; off by default, as
-// it measured no better than the pull on the jobs line): the staged inputs -- nonce, public share,
-// helper share, leader prep share, verify-key slot and table, segment id, accept byte -- go to the
-// run's device buffers by hipMemcpyAsync on a copy stream of their own (the SDMA engines at the
-// link's ~55 GB/s), and the kernels, on the group's stream, wait for those copies and for the
-// prepare kernels of the group before (`after`).  The executor issues a group while the one
-// before it still computes, so the transfer of group i+1 runs under the compute of group i and
-// the kernels read HBM.  Host pull (group_dma 0, the r03 form): the kernels read each report's
-// nonce, public share, helper share and verify-key slot straight from the pinned staging
-// (mapped) and each lane of the fused XOF + query launch copies its own leader prep share,
-// segment id and accept byte into the run during its XOF (xofd_body PULL), so the transfer runs
-// under that group's own Keccak work at the rate the lanes pull (~35 GB/s, profiles/r04).  One
-// pinned-staging H2D copy per field ahead of the prepare, without the overlap (the r02 form),
-// left transfer and prepare in series (profiles/r03/r03e_jobs128_*.json: 21.5 M reports/s).
-bool engine_group_dma(const prio3_engine* e, uint32_t n) {
-  return e->group_dma < 0 || (e->group_dma > 0 && n <= (uint32_t)e->group_dma);
-}
-
-int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr, const GroupRun* after) {
+// Group launch (host pull, the r03 form).  The kernels read each report's nonce, public share,
+// helper share and verify-key slot straight from the pinned staging (mapped), and each lane of the
+// fused XOF + query launch copies its own leader prep share, segment id and accept byte into the
+// run during its XOF (xofd_body PULL), so the transfer runs under that group's own Keccak work at
+// the rate the lanes pull (~35 GB/s, profiles/r04).  One pinned-staging H2D copy per field ahead
+// of the prepare, without the overlap (the r02 form), left transfer and prepare in series
+// (profiles/r03/r03e_jobs128_*.json: 21.5 M reports/s); SDMA copies of each group issued under the
+// previous group's compute (r04 option group_dma) measured 19.5-30.8 against 32-40 M/s for the
+// pull and were removed in r05.
+int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr) {
   *gr = GroupRun();
   gr->lead = lead;
   gr->jobs = g.jobs;
@@ -3442,7 +3472,6 @@ int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr, con
   hipStream_t st = ws_stream_get(lead->device);
   if (!st) return PRIO3_EDEVICE;
   const bool mp = lead->dp.kind == PRIO3_SUMVEC_F64_MP;
-  const bool dma = engine_group_dma(lead, g.n);
   // aggregating jobs: the group's reports are accumulated per job segment in this launch (the
   // wave partials of the XOF where the instance fuses; waves that straddle two jobs and the
   // excluded reports go through the fix-up list)
@@ -3450,8 +3479,8 @@ int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr, con
   const bool fuse = agg && fusable(lead);
   int rc = PRIO3_OK;
   Run* R = run_create(lead, g.n,
-                      RUN_SCRATCH | RUN_IO | (mp ? 0u : (unsigned)RUN_VK) |
-                          (agg ? (unsigned)RUN_AGG_IO : 0u) | (fuse ? (unsigned)RUN_FUSED : 0u),
+                      RUN_SCRATCH | RUN_IO | (agg ? (unsigned)RUN_AGG_IO : 0u) |
+                          (fuse ? (unsigned)RUN_FUSED : 0u),
                       agg ? g.nseg : 0, g.n_keys, st, &rc);
   if (!R) {
     ws_stream_put(lead->device, st);
@@ -3461,81 +3490,34 @@ int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr, con
   engine_io_layout(lead, g.cap, &L);
   auto fail = [&](int code) {
     (void)hipStreamSynchronize(st);
-    if (gr->cs) {
-      (void)hipStreamSynchronize(gr->cs);
-      ws_stream_put(lead->device, gr->cs);
-    }
-    for (auto& ev : gr->ev)
-      if (ev) (void)hipEventDestroy(ev);
     run_release(R, st, true);
     if (gr->prep) (void)hipEventDestroy(gr->prep);
     *gr = GroupRun();
     ws_stream_put(lead->device, st);
     return code;
   };
-  InPtrs in{};
+  const uint8_t* hd = g.stg_dev;
+  InPtrs in{hd + L.off[0], L.len[1] ? hd + L.off[1] : nullptr, hd + L.off[2], R->leader};
+  if (!mp) {  // the slots and the key table are read from the staging by the XOF
+    in.vk_slot = (const uint16_t*)(hd + L.slot_off);
+    in.vk_tab = (const uint4*)(hd + L.tab_off);
+  }
+  if (agg) R->seg = (const uint32_t*)(hd + L.seg_off);  // the fused XOF's segment check
+  // the leader prep shares (and the segment ids / accept bytes of the fix-up pass)
   PullRanges pr{};
-  const PullRanges* pull = nullptr;
-  if (dma) {
-    gr->cs = ws_stream_get(lead->device);
-    if (!gr->cs) return fail(PRIO3_EDEVICE);
-    for (auto& ev : gr->ev)
-      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return fail(PRIO3_EDEVICE);
-    // the copies start once the run's slab is free (ws_acquire ordered that on st)
-    if (hipEventRecord(gr->ev[0], st) != hipSuccess ||
-        hipStreamWaitEvent(gr->cs, gr->ev[0], 0) != hipSuccess)
-      return fail(PRIO3_EDEVICE);
-    const uint8_t* hs = g.stg;
-    struct Cp {
-      void* dst;
-      size_t off, bytes;
-    } cps[] = {{R->nonces, L.off[0], L.len[0] * (size_t)g.n},
-               {R->pub, L.off[1], L.len[1] * (size_t)g.n},
-               {R->helper, L.off[2], L.len[2] * (size_t)g.n},
-               {R->leader, L.off[3], L.len[3] * (size_t)g.n},
-               {mp ? nullptr : R->vk_slot, L.slot_off, 2 * (size_t)g.n},
-               {mp ? nullptr : R->vk_tab, L.tab_off, 16 * (size_t)g.n_keys},
-               {agg ? R->gseg : nullptr, L.seg_off, 4 * (size_t)g.n},
-               {agg ? R->gaccept : nullptr, L.accept_off, (size_t)g.n}};
-    for (const Cp& c : cps)
-      if (c.dst && c.bytes &&
-          hipMemcpyAsync(c.dst, hs + c.off, c.bytes, hipMemcpyDefault, gr->cs) != hipSuccess)
-        return fail(PRIO3_EDEVICE);
-    if (hipEventRecord(gr->ev[1], gr->cs) != hipSuccess ||
-        hipStreamWaitEvent(st, gr->ev[1], 0) != hipSuccess)
-      return fail(PRIO3_EDEVICE);
-    if (after && after->prep && hipStreamWaitEvent(st, after->prep, 0) != hipSuccess)
-      return fail(PRIO3_EDEVICE);
-    in = InPtrs{R->nonces, L.len[1] ? R->pub : nullptr, R->helper, R->leader};
-    if (!mp) {
-      in.vk_slot = (const uint16_t*)R->vk_slot;
-      in.vk_tab = (const uint4*)R->vk_tab;
-    }
-    if (agg) R->seg = R->gseg;
-  } else {
-    const uint8_t* hd = g.stg_dev;
-    in = InPtrs{hd + L.off[0], L.len[1] ? hd + L.off[1] : nullptr, hd + L.off[2], R->leader};
-    if (!mp) {  // the slots and the key table are read from the staging by the XOF
-      in.vk_slot = (const uint16_t*)(hd + L.slot_off);
-      in.vk_tab = (const uint4*)(hd + L.tab_off);
-    }
-    if (agg) R->seg = (const uint32_t*)(hd + L.seg_off);  // the fused XOF's segment check
-    // the leader prep shares (and the segment ids / accept bytes of the fix-up pass)
-    pr.src[0] = hd + L.off[3];
-    pr.dst[0] = R->leader;
-    pr.bytes[0] = L.len[3] * g.n;
-    if (agg) {
-      pr.src[1] = hd + L.seg_off;
-      pr.dst[1] = (uint8_t*)R->gseg;
-      pr.bytes[1] = 4 * (size_t)g.n;
-      pr.src[2] = hd + L.accept_off;
-      pr.dst[2] = R->gaccept;
-      pr.bytes[2] = g.n;
-    }
-    pull = &pr;
+  pr.src[0] = hd + L.off[3];
+  pr.dst[0] = R->leader;
+  pr.bytes[0] = L.len[3] * g.n;
+  if (agg) {
+    pr.src[1] = hd + L.seg_off;
+    pr.dst[1] = (uint8_t*)R->gseg;
+    pr.bytes[1] = 4 * (size_t)g.n;
+    pr.src[2] = hd + L.accept_off;
+    pr.dst[2] = R->gaccept;
+    pr.bytes[2] = g.n;
   }
   OutPtrs out{R->msgs, R->status};
-  rc = prepare_run(lead, R, in, out, st, fuse, false, pull);
+  rc = prepare_run(lead, R, in, out, st, fuse, false, &pr);
   if (agg) R->seg = R->gseg;
   if (rc) return fail(rc);
   // the executor may issue its next group once this group's prepare kernels are done
@@ -3553,7 +3535,7 @@ int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr, con
     if (rc) return fail(rc);
   }
   {  // the outputs go back by one copy launch writing the mapped staging
-    uint8_t* sd = g.out_dev;
+    uint8_t* sd = g.stg_dev;
     PullRanges o{};
     o.src[0] = R->status;
     o.dst[0] = sd + L.status_off;
@@ -3595,11 +3577,6 @@ int engine_group_finish(GroupRun* gr, Run** run_out) {
   if (gr->prep) (void)hipEventDestroy(gr->prep);
   gr->prep = nullptr;
   const int dev = gr->lead->device;
-  // the copy stream's work is ordered before st's kernels (ev[1]), so it is done too
-  for (auto& ev : gr->ev)
-    if (ev) (void)hipEventDestroy(ev);
-  if (gr->cs) ws_stream_put(dev, gr->cs);
-  gr->cs = nullptr;
   if (q != hipSuccess) {
     (void)hipGetLastError();
     run_release(gr->R, gr->st, true);
@@ -3686,6 +3663,134 @@ int engine_acc_group(int device, int es, uint8_t* stg, const AccLayout& L, uint3
   }
   ws_release(sl, st);
   return rc;
+}
+
+// ---- leader-executor hooks (prio3_runtime.h) ----
+// The leader groups take the TurboSHAKE instances; FPVec (sub-batched runs) and the multiproof
+// instance (HMAC midstates per engine) keep one run per call.
+static bool leader_coalescable(const prio3_engine* e) {
+  return e->coalesce && e->dp.kind != PRIO3_FPVEC_BOUNDED_L2 && e->dp.kind != PRIO3_SUMVEC_F64_MP;
+}
+
+void engine_leader_layout(const prio3_engine* e, uint32_t cap, LeaderLayout* L) {
+  const DevParams& d = e->dp;
+  auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  L->len[0] = 16;
+  L->len[1] = d.public_share_len;
+  L->len[2] = d.leader_share_len;
+  size_t off = 0;
+  for (int f = 0; f < 3; f++) {
+    L->off[f] = off;
+    off += up(L->len[f] * cap);
+  }
+  L->slot_off = off;
+  off += up(2 * (size_t)cap);
+  L->tab_off = off;
+  off += up(16 * (size_t)exec_max_keys());
+  L->ps_len = d.prep_share_len;
+  L->ps_off = off;
+  off += up(L->ps_len * cap);
+  L->status_off = off;
+  off += up(cap);
+  L->bytes = off;
+}
+
+// A leader group: the explicit input shares (5.6 KB per Histogram(256) report) go to the run by
+// one DMA, the kernels read the nonces, public shares and verify-key slots from the mapped
+// staging, and one copy launch writes the prepare shares and statuses back into it.
+int engine_leader_issue(prio3_engine* lead, const LeaderLayout& L, uint8_t* stg_dev, uint32_t n,
+                        uint32_t n_keys, int jobs, GroupRun* gr) {
+  (void)n_keys;
+  *gr = GroupRun();
+  gr->lead = lead;
+  gr->jobs = jobs;
+  HIPCHK(hipSetDevice(lead->device));
+  hipStream_t st = ws_stream_get(lead->device);
+  if (!st) return PRIO3_EDEVICE;
+  int rc = PRIO3_OK;
+  Run* R = run_create(lead, n, RUN_SCRATCH | RUN_IO | RUN_LINPUT, 0, 0, st, &rc);
+  if (!R) {
+    ws_stream_put(lead->device, st);
+    return rc;
+  }
+  auto fail = [&](int code) {
+    (void)hipStreamSynchronize(st);
+    run_release(R, st, true);
+    if (gr->prep) (void)hipEventDestroy(gr->prep);
+    *gr = GroupRun();
+    ws_stream_put(lead->device, st);
+    return code;
+  };
+  if (hipMemcpyAsync(R->linput, stg_dev + L.off[2], L.len[2] * n, hipMemcpyDefault, st) !=
+      hipSuccess)
+    return fail(PRIO3_EDEVICE);
+  rc = leader_init_run(lead, R, stg_dev + L.off[0], L.len[1] ? stg_dev + L.off[1] : nullptr,
+                       R->linput, R->leader, R->status, st, (const uint16_t*)(stg_dev + L.slot_off),
+                       (const uint4*)(stg_dev + L.tab_off));
+  if (rc) return fail(rc);
+  if (hipEventCreateWithFlags(&gr->prep, hipEventDisableTiming) != hipSuccess ||
+      hipEventRecord(gr->prep, st) != hipSuccess) {
+    (void)hipGetLastError();
+    if (gr->prep) (void)hipEventDestroy(gr->prep);
+    gr->prep = nullptr;
+  }
+  PullRanges o{};
+  o.src[0] = R->status;
+  o.dst[0] = stg_dev + L.status_off;
+  o.bytes[0] = n;
+  o.src[1] = R->leader;
+  o.dst[1] = stg_dev + L.ps_off;
+  o.bytes[1] = L.ps_len * n;
+  const size_t tot = o.bytes[0] + o.bytes[1];
+  k_pull<<<(unsigned)std::min<size_t>(256, (tot / 16 + 255) / 256 + 1), 256, 0, st>>>(o);
+  if (hipGetLastError() != hipSuccess) return fail(PRIO3_EDEVICE);
+  gr->st = st;
+  gr->R = R;
+  return PRIO3_OK;
+}
+
+uint32_t engine_lnext_key(const LNextJob* j) { return j->run->dp.es; }
+
+void engine_lnext_stage(LNextJob* j, uint8_t* stg, const LNextLayout& L) {
+  const Run* R = j->run;
+  const DevParams& d = R->dp;
+  const size_t es = d.es;
+  LNextDesc& D = ((LNextDesc*)(stg + L.desc_off))[j->slot];
+  D.corrected = R->sc.corrected + j->c0;
+  D.meas = (const uint8_t*)R->sc.meas + es * j->c0;
+  D.out = own_out(d) ? (uint8_t*)R->sc.out + es * j->c0 : nullptr;
+  D.dstatus = R->status + j->c0;
+  D.ld = d.ld;
+  D.n = j->n;
+  D.rep_off = j->rep_off;
+  D.kind = d.kind;
+  D.bits = d.bits;
+  D.out_len = d.out_len;
+  D.jr = d.jr_len ? 1u : 0u;
+  if (D.jr && j->msgs) memcpy(stg + L.msg_off + 16 * (size_t)j->rep_off, j->msgs, 16 * (size_t)j->n);
+  memcpy(stg + L.status_off + j->rep_off, j->status, j->n);
+}
+
+extern "C" int launch_leader_next_multi(uint32_t es, const LNextDesc* d_desc, const uint8_t* d_msgs,
+                                        uint8_t* d_status, uint32_t n_jobs, uint32_t max_n,
+                                        hipStream_t st);
+
+int engine_lnext_issue(int device, uint32_t es, uint8_t* stg_dev, const LNextLayout& L,
+                       uint32_t n_jobs, uint32_t max_n, hipStream_t* st_out) {
+  *st_out = nullptr;
+  HIPCHK(hipSetDevice(device));
+  hipStream_t st = ws_stream_get(device);
+  if (!st) return PRIO3_EDEVICE;
+  const int rc = launch_leader_next_multi(es, (const LNextDesc*)(stg_dev + L.desc_off),
+                                          stg_dev + L.msg_off, stg_dev + L.status_off, n_jobs,
+                                          max_n, st);
+  if (rc != PRIO3_OK) {
+    (void)hipStreamSynchronize(st);
+    ws_stream_put(device, st);
+    return rc;
+  }
+  *st_out = st;
+  return PRIO3_OK;
 }
 
 extern "C" {
@@ -3805,8 +3910,104 @@ int prio3_engine_create(const prio3_params* params, const uint8_t verify_key[16]
   return prio3_engine_create_ex(params, verify_key, 16, device, out);
 }
 
+int prio3_engine_create_devices(const prio3_params* params, const uint8_t* verify_key,
+                                size_t verify_key_len, const int* devices, uint32_t n_devices,
+                                prio3_engine** out) {
+  if (!out || !devices || n_devices == 0 || n_devices > (uint32_t)EXEC_LANES * 64)
+    return PRIO3_EINVAL;
+  *out = nullptr;
+  std::vector<prio3_engine*> ms;
+  for (uint32_t i = 0; i < n_devices; i++) {
+    // the lane of a GPU named again: its own executor (a one-GPU rehearsal of the placement)
+    int lane = 0;
+    for (uint32_t j = 0; j < i; j++) lane += devices[j] == devices[i];
+    prio3_engine* m = nullptr;
+    const int rc = lane < EXEC_LANES
+                       ? prio3_engine_create_ex(params, verify_key, verify_key_len, devices[i], &m)
+                       : PRIO3_EINVAL;
+    if (rc != PRIO3_OK) {
+      for (auto x : ms) prio3_engine_destroy(x);
+      return rc;
+    }
+    m->lane = lane;
+    ms.push_back(m);
+  }
+  prio3_engine* e = ms[0];
+  if (ms.size() > 1) {
+    e->members = ms;
+    for (size_t i = 1; i < ms.size(); i++) ms[i]->owner = e;
+  }
+  *out = e;
+  return PRIO3_OK;
+}
+
+int prio3_engine_create_mask(const prio3_params* params, const uint8_t* verify_key,
+                             size_t verify_key_len, int device_mask, prio3_engine** out) {
+  std::vector<int> devs;
+  for (int d = 0; d < 31; d++)
+    if (device_mask & (1 << d)) devs.push_back(d);
+  if (device_mask <= 0 || devs.empty()) return PRIO3_EINVAL;
+  return prio3_engine_create_devices(params, verify_key, verify_key_len, devs.data(),
+                                     (uint32_t)devs.size(), out);
+}
+
+int prio3_engine_members(const prio3_engine* e, prio3_member_info* out, uint32_t cap) {
+  if (!e) return PRIO3_EINVAL;
+  const uint32_t k = e->members.empty() ? 1u : (uint32_t)e->members.size();
+  for (uint32_t i = 0; i < k && i < cap && out; i++) {
+    const prio3_engine* m = e->members.empty() ? e : e->members[i];
+    prio3_member_info& x = out[i];
+    x.device = m->device;
+    x.lane = (uint32_t)m->lane;
+    x.jobs = m->placed_jobs.load();
+    x.reports = m->placed_reports.load();
+    ExecStats st;
+    if (exec_stats(EXEC_PREP, engine_exec_id(m), &st) != PRIO3_OK) st = ExecStats();
+    x.exec_jobs = st.jobs;
+    x.exec_groups = st.groups;
+  }
+  return (int)k;
+}
+
+int prio3_executor_stats_get(const prio3_engine* e, uint32_t member, int kind,
+                             prio3_executor_stats* out) {
+  if (!e || !out || kind < 0 || kind >= EXEC_KINDS) return PRIO3_EINVAL;
+  const size_t k = e->members.empty() ? 1 : e->members.size();
+  if (member >= k) return PRIO3_EINVAL;
+  const prio3_engine* m = e->members.empty() ? e : e->members[member];
+  const bool per_gpu = kind == EXEC_ACC || kind == EXEC_LNEXT;
+  ExecStats st;
+  const int rc = exec_stats(kind, per_gpu ? m->device * EXEC_LANES : engine_exec_id(m), &st);
+  if (rc != PRIO3_OK) return rc;
+  out->jobs = st.jobs;
+  out->reports = st.reports;
+  out->groups = st.groups;
+  out->active_jobs = st.active_jobs;
+  out->active_reports = st.active_reports;
+  return PRIO3_OK;
+}
+
+int prio3_executor_control(prio3_engine* e, int which, const char* key, int64_t value) {
+  if (!e || !key || which < -1 || which >= EXEC_KINDS) return PRIO3_EINVAL;
+  const size_t k = e->members.empty() ? 1 : e->members.size();
+  for (size_t i = 0; i < k; i++) {
+    const prio3_engine* m = e->members.empty() ? e : e->members[i];
+    for (int kind : {(int)EXEC_PREP, (int)EXEC_ACC, (int)EXEC_LEADER, (int)EXEC_LNEXT}) {
+      if (which >= 0 && kind != which) continue;
+      // the accumulate and prepare_next executors are one per GPU (lane 0)
+      const bool per_gpu = kind == EXEC_ACC || kind == EXEC_LNEXT;
+      const int id = per_gpu ? m->device * EXEC_LANES : engine_exec_id(m);
+      const int rc = exec_control(kind, id, key, value);
+      if (rc != PRIO3_OK) return rc;
+    }
+  }
+  return PRIO3_OK;
+}
+
 void prio3_engine_destroy(prio3_engine* e) {
   if (!e) return;
+  for (size_t i = 1; i < e->members.size(); i++) prio3_engine_destroy(e->members[i]);
+  e->members.clear();
   (void)hipSetDevice(e->device);
   (void)hipDeviceSynchronize();
   {
@@ -3825,6 +4026,10 @@ void prio3_engine_destroy(prio3_engine* e) {
 
 int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
   if (!e || !key) return PRIO3_EINVAL;
+  for (size_t i = 1; i < e->members.size(); i++) {  // a multi-GPU engine: every member alike
+    const int rc = prio3_engine_set_option(e->members[i], key, value);
+    if (rc != PRIO3_OK) return rc;
+  }
   struct {
     const char* name;
     int* field;
@@ -3833,8 +4038,7 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
               {"fp_round", &e->fp_round},          {"timing", &e->timing},
               {"coalesce", &e->coalesce},          {"experimental_fpvec", &e->experimental_fpvec},
               {"leader_fuse_acc", &e->leader_fuse_acc},
-              {"force_generic_query", &e->force_generic}, {"pair_max", &e->pair_max},
-              {"group_dma", &e->group_dma}};
+              {"force_generic_query", &e->force_generic}, {"pair_max", &e->pair_max}};
   for (auto& o : ints)
     if (!strcmp(key, o.name)) {
       *o.field = (int)value;
@@ -4117,17 +4321,18 @@ int prio3_device_output_shares(prio3_engine* e, uint32_t n, uint8_t* out) {
 }
 
 // ---- host-buffer entry points (what the Rust FFI calls from inside rayon::spawn) ----
-int prio3_helper_prepare_batch(prio3_engine* e, uint32_t n, const uint8_t* nonces,
-                               const uint8_t* public_shares, const uint8_t* helper_shares,
-                               const uint8_t* leader_prep_shares, uint8_t* prep_msgs_out,
-                               uint8_t* status_out, prio3_batch** batch_out) {
-  TraceSpan span_("handle_aggregate_init_generic threadpool task");
+// (e: the member the job was placed on)
+static int helper_prepare_batch(prio3_engine* e, uint32_t n, const uint8_t* nonces,
+                                const uint8_t* public_shares, const uint8_t* helper_shares,
+                                const uint8_t* leader_prep_shares, uint8_t* prep_msgs_out,
+                                uint8_t* status_out, prio3_batch** batch_out, bool placed) {
   if (!e || (n && (!nonces || !helper_shares || !leader_prep_shares || !status_out)))
     return PRIO3_EINVAL;
   if (e->dp.kind == PRIO3_FPVEC_BOUNDED_L2 && !e->experimental_fpvec)
     return PRIO3_EUNSUPPORTED;  // unpinned reconstruction: explicit opt-in only
   const DevParams& d = e->dp;
   if (n && d.jr_len && (!public_shares || !prep_msgs_out)) return PRIO3_EINVAL;
+  if (n && !placed) e = place(e, n);
   if (n == 0) {
     if (batch_out) *batch_out = new prio3_batch{e, nullptr, 0, 0};
     return PRIO3_OK;
@@ -4150,6 +4355,15 @@ int prio3_helper_prepare_batch(prio3_engine* e, uint32_t n, const uint8_t* nonce
   return PRIO3_OK;
 }
 
+int prio3_helper_prepare_batch(prio3_engine* e, uint32_t n, const uint8_t* nonces,
+                               const uint8_t* public_shares, const uint8_t* helper_shares,
+                               const uint8_t* leader_prep_shares, uint8_t* prep_msgs_out,
+                               uint8_t* status_out, prio3_batch** batch_out) {
+  TraceSpan span_("handle_aggregate_init_generic threadpool task");
+  return helper_prepare_batch(e, n, nonces, public_shares, helper_shares, leader_prep_shares,
+                              prep_msgs_out, status_out, batch_out, false);
+}
+
 int prio3_helper_prepare_aggregate_batch(prio3_engine* e, uint32_t n, const uint8_t* nonces,
                                          const uint8_t* public_shares,
                                          const uint8_t* helper_shares,
@@ -4166,14 +4380,15 @@ int prio3_helper_prepare_aggregate_batch(prio3_engine* e, uint32_t n, const uint
     return PRIO3_EUNSUPPORTED;  // unpinned reconstruction: explicit opt-in only
   const DevParams& d = e->dp;
   if (n && d.jr_len && (!public_shares || !prep_msgs_out)) return PRIO3_EINVAL;
+  if (n) e = place(e, n);
   const size_t agg_len = (size_t)d.out_len * d.es;
   IoLayout L1;
   engine_io_layout(e, 1, &L1);
   if (n == 0 || !e->coalesce || n_segments > L1.max_seg) {
     // not coalescable (or empty): the two calls, as the caller would make them
     prio3_batch* b = nullptr;
-    int rc = prio3_helper_prepare_batch(e, n, nonces, public_shares, helper_shares,
-                                        leader_prep_shares, prep_msgs_out, status_out, &b);
+    int rc = helper_prepare_batch(e, n, nonces, public_shares, helper_shares,
+                                  leader_prep_shares, prep_msgs_out, status_out, &b, true);
     if (rc == PRIO3_OK) rc = prio3_accumulate(b, segment_ids, accept_mask, n_segments,
                                               agg_shares_out, counts_out);
     prio3_batch_free(b);
@@ -4280,12 +4495,25 @@ void prio3_batch_free(prio3_batch* b) {
 int prio3_engine_timing(prio3_engine* e, char* names, size_t cap_names, double* ms,
                         uint64_t* launches, int cap) {
   if (!e) return PRIO3_EINVAL;
-  (void)hipSetDevice(e->device);
-  collect_times(e);
-  std::lock_guard<std::mutex> lk(e->tmu);
+  // a multi-GPU engine: its members' times, summed per kernel name
+  std::vector<KTime> sum;
+  const size_t nm = e->members.empty() ? 1 : e->members.size();
+  for (size_t i = 0; i < nm; i++) {
+    prio3_engine* m = e->members.empty() ? e : e->members[i];
+    (void)hipSetDevice(m->device);
+    collect_times(m);
+    std::lock_guard<std::mutex> lk(m->tmu);
+    for (auto& t : m->times) {
+      size_t j = 0;
+      while (j < sum.size() && sum[j].name != t.name) j++;
+      if (j == sum.size()) sum.push_back(KTime{t.name, 0, 0});
+      sum[j].ms += t.ms;
+      sum[j].launches += t.launches;
+    }
+  }
   std::string all;
   int k = 0;
-  for (auto& t : e->times) {
+  for (auto& t : sum) {
     if (k < cap) {
       if (ms) ms[k] = t.ms;
       if (launches) launches[k] = t.launches;
@@ -4303,6 +4531,7 @@ int prio3_engine_timing(prio3_engine* e, char* names, size_t cap_names, double* 
 
 void prio3_engine_timing_reset(prio3_engine* e) {
   if (!e) return;
+  for (size_t i = 1; i < e->members.size(); i++) prio3_engine_timing_reset(e->members[i]);
   collect_times(e);
   std::lock_guard<std::mutex> lk(e->tmu);
   for (auto& t : e->times) {
@@ -4378,6 +4607,24 @@ int prio3_leader_prepare_init_batch(prio3_engine* e, uint32_t n, const uint8_t* 
     if (batch_out) *batch_out = new prio3_batch{e, nullptr, 0, 0};
     return PRIO3_OK;
   }
+  e = place(e, n);
+  if (leader_coalescable(e)) {  // concurrent jobs (of any task of the instance): one launch
+    LeaderJob job{};
+    job.e = e;
+    job.n = n;
+    job.nonces = nonces;
+    job.pub = d.jr_len ? public_shares : nullptr;
+    job.linput = leader_input_shares;
+    job.prep_out = prep_shares_out;
+    job.status_out = status_out;
+    const int rc = exec_leader(&job);
+    if (rc) return rc;
+    if (batch_out)
+      *batch_out = new prio3_batch{e, job.run, job.c0, n};
+    else
+      run_release(job.run, nullptr, false);
+    return PRIO3_OK;
+  }
   HIPCHK(hipSetDevice(e->device));
   PooledStream ps(e->device);
   hipStream_t st = ps.s;
@@ -4422,27 +4669,45 @@ int prio3_leader_prepare_next_batch(prio3_batch* b, const uint8_t* prep_msgs,
   if (n == 0 || !b->run) return PRIO3_OK;
   if (d.jr_len && !prep_msgs) return PRIO3_EINVAL;
   Run* R = b->run;
-  if (!R->msgs || b->c0 != 0) return PRIO3_EINVAL;  // a leader batch (its own run)
+  if (!R->msgs || !R->linput) return PRIO3_EINVAL;  // a leader batch
+  const uint32_t c0 = b->c0;
+  if (leader_coalescable(e) && n <= LNEXT_MAX_REPS) {
+    // concurrent jobs' prepare_next (of any runs of this GPU) in one launch
+    LNextJob job;
+    job.device = e->device;
+    job.run = R;
+    job.c0 = c0;
+    job.n = n;
+    job.msgs = d.jr_len ? prep_msgs : nullptr;
+    job.status = status_inout;
+    return exec_leader_next(&job);
+  }
   HIPCHK(hipSetDevice(e->device));
   PooledStream ps(e->device);
   hipStream_t st = ps.s;
   if (!st) return PRIO3_EDEVICE;
   if (d.jr_len)
-    HIPCHK(hipMemcpyAsync(R->msgs, prep_msgs, (size_t)e->sz.prep_msg_len * n,
+    HIPCHK(hipMemcpyAsync(R->msgs + 16 * (size_t)c0, prep_msgs, (size_t)e->sz.prep_msg_len * n,
                           hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(R->status, status_inout, n, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(R->status + c0, status_inout, n, hipMemcpyHostToDevice, st));
   DevParams dp = R->dp;
   dp.n = n;
   R->last = st;
   Scratch sc = R->sc;
   if (R->corr_all) sc.corrected = R->corr_all;  // FPVec: seeds of every sub-batch
+  if (c0) {  // the batch's columns of a shared run (FPVec and multiproof runs are whole: c0 = 0)
+    sc.corrected += c0;
+    sc.meas = (uint8_t*)sc.meas + (size_t)dp.es * c0;
+    sc.out = (uint8_t*)sc.out + (size_t)dp.es * c0;
+  }
   int rc2 = PRIO3_OK;
   if (dp.kind == PRIO3_SUMVEC_F64_MP)
     TIMED(e, st, "k_leader_next", rc2 = launch_mp64_leader_next(n, R->msgs, sc, R->status, st));
   else
-    TIMED(e, st, "k_leader_next", rc2 = launch_leader_next(dp, R->msgs, sc, R->status, st));
+    TIMED(e, st, "k_leader_next",
+          rc2 = launch_leader_next(dp, R->msgs + 16 * (size_t)c0, sc, R->status + c0, st));
   if (rc2) return rc2;
-  HIPCHK(hipMemcpyAsync(status_inout, R->status, n, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(status_inout, R->status + c0, n, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   if (e->timing) collect_times(e);
   return PRIO3_OK;

@@ -46,6 +46,10 @@ hipStream_t ws_stream_get(int device);  // nullptr on failure
 void ws_stream_put(int device, hipStream_t s);
 
 // ---- coalescing executor -------------------------------------------------------------------
+// One executor per (GPU, lane): lane 0 is the GPU's executor; a multi-GPU engine created over a
+// device list that names a GPU k times gets lanes 0..k-1 on it (prio3_engine_create_devices; a
+// test form of the node-wide placement that runs on a one-GPU box).
+constexpr int EXEC_LANES = 8;
 struct prio3_engine;
 struct Run;
 struct ExecJob {
@@ -70,14 +74,30 @@ struct ExecJob {
   uint32_t pad0 = 0;   // pad columns [pad0, c0) before the job (aligned aggregating jobs)
 };
 // Blocks until the job's reports are prepared (alone or coalesced with concurrent jobs of
-// engines with the same VDAF instance on the same GPU).
+// engines with the same VDAF instance on the same executor).
 int exec_submit(ExecJob* job);
 
+// Executor control and counters (prio3_executor_control / prio3_engine_members).
+struct ExecStats {
+  uint64_t jobs = 0, reports = 0, groups = 0;  // submitted jobs / their reports / launches
+  uint64_t active_jobs = 0, active_reports = 0;  // jobs inside submit now
+};
+// kinds: 0 helper prepare, 1 accumulate, 2 leader prepare_init, 3 leader prepare_next,
+// 4 HPKE open of input shares
+enum { EXEC_PREP = 0, EXEC_ACC = 1, EXEC_LEADER = 2, EXEC_LNEXT = 3, EXEC_HPKE = 4, EXEC_KINDS = 5 };
+int exec_stats(int kind, int exec_id, ExecStats* out);
+// hold = 1: the executor's launcher takes no group until hold = 0 (tests pre-queue jobs with
+// it); heavy = reports inside submit at which the launcher switches to its heavy-load form
+// (0 = the default 32 Ki)
+int exec_control(int kind, int exec_id, const char* key, int64_t value);
+// reports of the jobs inside the helper/leader executors of exec_id (placement: least loaded)
+uint64_t exec_load(int exec_id);
+
 // Engine hooks the executor calls (prio3_engine.hip).
-// Staging layout of a group with room for `cap` reports (pinned host buffer): the four input
-// fields [cap][len] (nonces, public shares, helper shares, leader prep shares), the per-report
-// verify-key slot (u16), the verify-key table [exec_max_keys()][16], then the outputs: prepare
-// messages [cap][msg_len] and statuses [cap].
+// Staging layout of a group with room for `cap` reports (pinned, device-mapped host buffer):
+// the four input fields [cap][len] (nonces, public shares, helper shares, leader prep shares),
+// the per-report verify-key slot (u16), the verify-key table [exec_max_keys()][16], then the
+// outputs: prepare messages [cap][msg_len] and statuses [cap].
 // Groups with aggregating jobs also stage per-report group segment ids (u32) and accept bytes,
 // and receive [max_seg][agg_len] aggregate shares + [max_seg] u64 counts.
 struct IoLayout {
@@ -89,18 +109,17 @@ struct IoLayout {
 };
 void engine_io_layout(const prio3_engine* e, uint32_t cap, IoLayout* L);
 struct GroupView {
-  uint32_t n, cap;  // reports staged, staging capacity
-  uint8_t* stg;     // the staged inputs as the job threads write them (IoLayout for cap)
-  uint8_t* stg_dev;  // the same inputs as the device addresses them
-  uint8_t* out;      // pinned output area (same IoLayout; = stg unless the inputs are in VRAM)
-  uint8_t* out_dev;  // the output area as the device addresses it (mapped pinned memory)
-  uint32_t n_keys;  // verify keys in the table
-  int jobs;         // references the run must carry (one per job)
-  uint32_t nseg;    // segments of the aggregating jobs (0: no job aggregates)
+  uint32_t n, cap;   // reports staged, staging capacity
+  uint8_t* stg;      // the staged inputs and outputs as the job threads see them (IoLayout)
+  uint8_t* stg_dev;  // the same bytes as the device addresses them (mapped pinned memory)
+  uint32_t n_keys;   // verify keys in the table
+  int jobs;          // references the run must carry (one per job)
+  uint32_t nseg;     // segments of the aggregating jobs (0: no job aggregates)
 };
 // segments one group can aggregate (its aggregating jobs' n_segments summed)
 constexpr uint32_t EXEC_MAX_SEGS = 1024;
 int engine_device(const prio3_engine* e);
+int engine_exec_id(const prio3_engine* e);  // device * EXEC_LANES + lane
 uint64_t engine_group_key(const prio3_engine* e);  // equal keys may share one launch
 uint32_t engine_job_align(const prio3_engine* e);  // column alignment of aggregating jobs
 void engine_vk(const prio3_engine* e, uint8_t out[16]);
@@ -109,18 +128,11 @@ void engine_vk(const prio3_engine* e, uint8_t out[16]);
 struct GroupRun {
   prio3_engine* lead = nullptr;
   hipStream_t st = nullptr;
-  hipStream_t cs = nullptr;   // copy stream of a DMA group (group_dma), returned at finish
-  hipEvent_t ev[2] = {nullptr, nullptr};  // DMA group: slab ready on st, inputs on the device
   Run* R = nullptr;
   hipEvent_t prep = nullptr;  // recorded after the prepare kernels
   int jobs = 0;
 };
-// after (nullable): the group running before this one; a DMA group's kernels wait for its
-// prepare kernels (the copies do not)
-int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr,
-                       const GroupRun* after = nullptr);
-// a group of n reports goes to the device by DMA (option group_dma; the executor issues it early)
-bool engine_group_dma(const prio3_engine* e, uint32_t n);
+int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr);
 bool engine_group_prepared(const GroupRun& gr);  // the prepare kernels are done
 bool engine_group_done(const GroupRun& gr);      // everything is done (non-blocking)
 int engine_group_finish(GroupRun* gr, Run** run_out);
@@ -162,3 +174,97 @@ void engine_acc_stage(AccJob* j, uint8_t* stg, const AccLayout& L);
 void engine_acc_unstage(AccJob* j, const uint8_t* stg, const AccLayout& L);
 int engine_acc_group(int device, int es, uint8_t* stg, const AccLayout& L, uint32_t n_jobs,
                      size_t out_bytes);
+
+// ---- coalesced leader prepare_init (prio3_leader_prepare_init_batch of concurrent jobs) -------
+// Janus's aggregation job driver steps every job's reports through leader_initialized on its
+// own rayon worker (/root/reference/aggregator/src/aggregator/aggregation_job_driver.rs:397-415,
+// spawned at :449-462): the same group commit as the helper prepare, keyed by VDAF instance,
+// with per-report verify-key slots.
+struct LeaderJob {
+  prio3_engine* e;
+  uint32_t n;
+  const uint8_t *nonces, *pub, *linput;  // host inputs [n][16], [n][pub_len], [n][leader_share_len]
+  uint8_t *prep_out, *status_out;        // host outputs [n][prep_share_len], [n]
+  Run* run = nullptr;  // results: one reference for this job, its columns [c0, c0 + n)
+  uint32_t c0 = 0, slot = 0;
+};
+// staging of a leader group with room for cap reports: inputs, key slots, key table, outputs
+struct LeaderLayout {
+  size_t len[3], off[3];  // nonces, public shares, leader input shares
+  size_t slot_off, tab_off, ps_len, ps_off, status_off, bytes;
+};
+void engine_leader_layout(const prio3_engine* e, uint32_t cap, LeaderLayout* L);
+// one DMA of the staged inputs into the run, the leader kernels, the outputs back into the staging
+int engine_leader_issue(prio3_engine* lead, const LeaderLayout& L, uint8_t* stg_dev, uint32_t n,
+                        uint32_t n_keys, int jobs, GroupRun* gr);
+int exec_leader(LeaderJob* job);
+
+// ---- coalesced leader prepare_next (prio3_leader_prepare_next_batch of concurrent jobs) -------
+// leader_continued on the helper's response (aggregation_job_driver.rs:677-691), per job: the
+// kernel compares each prepare message with the corrected joint-rand seed and truncates the
+// measurement share, for many jobs' batches (of different runs) in one launch.
+struct LNextJob {
+  int device = 0;
+  Run* run = nullptr;
+  uint32_t c0 = 0, n = 0;          // the batch's columns in its run
+  const uint8_t* msgs = nullptr;   // host [n][16] (nullable: no joint randomness)
+  uint8_t* status = nullptr;       // host [n], in/out
+  uint32_t slot = 0, rep_off = 0;  // placement in the group
+};
+// one per job of a prepare_next group (read by the kernel from the mapped staging)
+struct LNextDesc {
+  const uint4* corrected;  // the run's corrected seeds at the job's first column
+  const uint8_t* meas;     // its measurement-share SoA column 0 (element stride ld)
+  uint8_t* out;            // its output-share SoA (Sum / SumVec truncation)
+  uint8_t* dstatus;        // the run's device statuses at the job's first column
+  uint64_t ld;
+  uint32_t n, rep_off, kind, bits, out_len, jr;
+};
+constexpr uint32_t LNEXT_MAX_JOBS = 1024, LNEXT_MAX_REPS = 1u << 17;
+struct LNextLayout {
+  size_t desc_off, msg_off, status_off, bytes;
+};
+void lnext_layout(LNextLayout* L);
+uint32_t engine_lnext_key(const LNextJob* j);
+void engine_lnext_stage(LNextJob* j, uint8_t* stg, const LNextLayout& L);
+// launches the group's kernel on a pooled stream of `device` (reads and writes the staging)
+int engine_lnext_issue(int device, uint32_t es, uint8_t* stg_dev, const LNextLayout& L,
+                       uint32_t n_jobs, uint32_t max_n, hipStream_t* st_out);
+int exec_leader_next(LNextJob* job);
+
+// ---- coalesced HPKE open of helper input shares (janus_hpke_open_input_shares) -----------
+// The helper opens each report's input share inside its job's rayon task
+// (/root/reference/aggregator/src/aggregator.rs:1847-1890): concurrent jobs of every task that
+// uses the same HPKE keypair share one launch, each report carrying a slot into the group's
+// task-ID table (the AAD's task_id).
+struct janus_hpke_opener;
+struct HpkeJob {
+  janus_hpke_opener* o = nullptr;
+  uint32_t n = 0;
+  const uint8_t* task_id = nullptr;  // [32]
+  const uint8_t *enc = nullptr, *ct = nullptr;
+  const uint32_t* ct_len = nullptr;
+  uint32_t ct_stride = 0;
+  const uint8_t* ids = nullptr;
+  const uint64_t* times = nullptr;
+  const uint8_t* pubs = nullptr;
+  uint32_t pub_len = 0, share_len = 0;
+  int require_taskprov = 0;
+  uint8_t *shares_out = nullptr, *status_out = nullptr;
+  uint32_t c0 = 0, slot = 0;  // placement in the group
+};
+// staging of an HPKE group with room for cap reports (per-field arrays), the task table, outputs
+struct HpkeLayout {
+  size_t off_enc, off_ct, off_len, off_ids, off_times, off_pub, slot_off, tab_off;
+  size_t shares_off, status_off, pt_off, bytes;  // pt: device plaintext scratch (not staged)
+  uint32_t nenc;
+};
+constexpr uint32_t HPKE_MAX_TASKS = 256;
+int hpke_opener_device(const janus_hpke_opener* o);
+uint64_t hpke_group_key(const HpkeJob* j);
+void hpke_layout(const HpkeJob* j, uint32_t cap, HpkeLayout* L);
+// the group's inputs to a device mirror (one DMA per field), the open kernel, outputs back
+int hpke_group_issue(const HpkeJob& proto, const HpkeLayout& L, const uint8_t* stg, uint8_t* out,
+                     uint32_t n, hipStream_t* st_out, Slab** slab_out);
+int exec_hpke(HpkeJob* job);
+

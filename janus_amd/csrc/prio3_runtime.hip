@@ -7,20 +7,21 @@
 // prio3_helper_prepare_batch at once, possibly for different tasks (verify keys) of the same VDAF
 // instance.  One 500-report device launch is latency-bound, so concurrent jobs are merged:
 //   * a job reserves columns in the open group of its key (VDAF instance + options), copies its
-//     inputs into that group's pinned staging itself (the copies run in parallel on the callers'
-//     threads) and registers its verify key in the group's key table (one slot per report);
-//   * a group is launched by one of its callers as soon as a launch slot is free (at most
-//     `max_inflight` groups are in flight per GPU) and all of its writers are done -- so an idle
-//     GPU takes a lone job at once, and under load jobs pile into the next group while the
-//     previous one runs (adaptive batching, no timer);
-//   * the launch is one H2D copy of the staged inputs, the prepare kernels over all columns, one
-//     D2H copy of prepare messages + statuses; every caller then copies its own outputs back and
-//     gets a batch handle that references its column range of the shared device run.
+//     inputs into that group's pinned, device-mapped staging itself (the copies run in parallel on
+//     the callers' threads) and registers its verify key in the group's key table (one slot per
+//     report);
+//   * the executor's launcher thread takes a group as soon as the GPU can take it and all of its
+//     writers are done -- so an idle GPU takes a lone job at once, and under load jobs pile into
+//     the next group while the previous one runs (adaptive batching, no timer);
+//   * the launch's kernels read the staged inputs over PCIe and write the outputs back into the
+//     staging; every caller then copies its own outputs out and gets a batch handle that
+//     references its column range of the shared device run.
 #include "prio3_runtime.h"
 
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -210,42 +211,22 @@ void ws_stream_put(int device, hipStream_t s) {
 }
 
 // ---- executors -----------------------------------------------------------------------------
-// A generic group-commit executor, one per (GPU, work kind).  Callers reserve room in the open
-// group of their key and stage their inputs themselves (in parallel); `max_inflight` launcher
-// threads per executor take the oldest ready group -- or, when idle, the oldest open one -- wait
-// for its writers, launch it and wake exactly that group's callers.  An idle GPU therefore runs a
-// lone job at once, and under load jobs pile into the next group while launchers are busy.
+// A generic group-commit executor, one per (GPU, lane, work kind).  Callers reserve room in the
+// open group of their key and stage their inputs themselves (in parallel); the executor's one
+// launcher thread takes the oldest ready group -- or, when idle, the oldest open one -- waits for
+// its writers, launches it and wakes exactly that group's callers.  An idle GPU therefore runs a
+// lone job at once, and under load jobs pile into the next group while the launcher is busy.
 namespace {
 
 struct Staging {
-  uint8_t* p = nullptr;    // inputs, as the job threads write them
+  uint8_t* p = nullptr;    // inputs and outputs, as the job threads see them (pinned host memory)
   uint8_t* dev = nullptr;  // the same bytes as the device addresses them (kernels read per-report
-                           // inputs straight from here: engine_group_issue)
-  uint8_t* out = nullptr;  // outputs (pinned, mapped): = p unless the inputs live in VRAM
-  uint8_t* out_dev = nullptr;
+                           // inputs straight from here and write outputs back: engine_group_issue)
   size_t bytes = 0;
-  bool vram = false;  // inputs in fine-grained device memory, written through the PCIe BAR
 };
 
-// JANUS_PRIO3_VRAM_STAGING=1: a prepare group's inputs are staged in fine-grained HBM that the job
-// threads write through the BAR (~42 GB/s from 4-32 host threads, tools/ubench_h2vram.cpp), so
-// the group's kernels read HBM instead of pulling the shares over PCIe inside k_prep_h; the
-// outputs stay in pinned host memory.
-bool vram_staging() {
-  static const bool v = [] {
-    const char* s = getenv("JANUS_PRIO3_VRAM_STAGING");
-    return s && atoi(s) > 0;
-  }();
-  return v;
-}
-
 void staging_free(Staging& s) {
-  if (s.vram) {
-    if (s.p) (void)hipFree(s.p);
-    if (s.out) (void)hipHostFree(s.out);
-  } else if (s.p) {
-    (void)hipHostFree(s.p);
-  }
+  if (s.p) (void)hipHostFree(s.p);
   s = Staging();
 }
 
@@ -257,12 +238,12 @@ struct StagingPool {
 };
 StagingPool* g_staging = new StagingPool[MAX_DEVICES];  // never destroyed (see Exec)
 
-Staging staging_get(int dev, size_t bytes, bool vram) {
+Staging staging_get(int dev, size_t bytes) {
   {
     std::lock_guard<std::mutex> lk(g_staging[dev].mu);
     auto& v = g_staging[dev].idle;
     for (size_t i = 0; i < v.size(); i++)
-      if (v[i].bytes >= bytes && v[i].vram == vram) {
+      if (v[i].bytes >= bytes) {
         Staging s = v[i];
         v.erase(v.begin() + (long)i);
         return s;
@@ -270,19 +251,9 @@ Staging staging_get(int dev, size_t bytes, bool vram) {
   }
   Staging s;
   s.bytes = std::max(bytes, STAGING_TARGET);
-  s.vram = vram;
-  bool ok = hipSetDevice(dev) == hipSuccess;
-  if (ok && vram) {
-    ok = hipExtMallocWithFlags((void**)&s.p, s.bytes, hipDeviceMallocFinegrained) == hipSuccess &&
-         hipHostMalloc((void**)&s.out, s.bytes, hipHostMallocMapped) == hipSuccess &&
-         hipHostGetDevicePointer((void**)&s.out_dev, s.out, 0) == hipSuccess;
-    s.dev = s.p;
-  } else if (ok) {
-    ok = hipHostMalloc((void**)&s.p, s.bytes, hipHostMallocMapped) == hipSuccess &&
-         hipHostGetDevicePointer((void**)&s.dev, s.p, 0) == hipSuccess;
-    s.out = s.p;
-    s.out_dev = s.dev;
-  }
+  const bool ok = hipSetDevice(dev) == hipSuccess &&
+                  hipHostMalloc((void**)&s.p, s.bytes, hipHostMallocMapped) == hipSuccess &&
+                  hipHostGetDevicePointer((void**)&s.dev, s.p, 0) == hipSuccess;
   if (!ok) {
     (void)hipGetLastError();
     staging_free(s);
@@ -301,24 +272,12 @@ void staging_put(int dev, Staging s) {
   }
 }
 
-int max_inflight() {
-  static const int v = [] {
-    const char* s = getenv("JANUS_PRIO3_MAX_INFLIGHT");
-    const int x = s ? atoi(s) : 1;
-    return x < 1 ? 1 : x;
-  }();
-  return v;
-}
-uint32_t max_group_reports() {
-  static const uint32_t v = [] {
-    const char* s = getenv("JANUS_PRIO3_GROUP_REPORTS");
-    const long x = s ? atol(s) : (1L << 17);
-    return (uint32_t)std::max(1L, x);
-  }();
-  return v;
-}
+constexpr uint32_t MAX_GROUP_REPORTS = 1u << 17;  // reports per prepare group
+// reports inside submit at which the launcher leaves its light-load pipeline (the box's 16 rayon
+// threads keep ~8 Ki in flight, 128 threads ~64 Ki)
+constexpr uint64_t HEAVY_DEFAULT = 32768;
 
-// JANUS_EXEC_TRACE=<path>: one line per launched group (microseconds: created, taken by a
+// JANUS_EXEC_TRACE=<path>: one line per launched group (microseconds: created, taken by the
 // launcher, writers done, launch returned; jobs; reports), for tuning the executor
 // (profiles/r03/r03t .. r03ab)
 FILE* exec_trace() {
@@ -331,6 +290,9 @@ FILE* exec_trace() {
 double exec_us(std::chrono::steady_clock::time_point t) {
   static const auto t0 = std::chrono::steady_clock::now();
   return std::chrono::duration<double, std::micro>(t - t0).count();
+}
+double ns_since(std::chrono::steady_clock::time_point t) {
+  return std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - t).count();
 }
 
 template <class P>
@@ -346,18 +308,23 @@ struct Exec {
     int njobs = 0;
     std::condition_variable cv;
   };
-  int device = 0;
+  int device = 0, id = 0;
   std::mutex mu;
-  std::condition_variable cv;  // launchers
+  std::condition_variable cv;  // the launcher
   std::map<uint64_t, Group*> open;
-  std::deque<Group*> order;  // groups not yet taken by a launcher, oldest first
+  std::deque<Group*> order;  // groups not yet taken by the launcher, oldest first
   bool started = false;
+  // under mu:
+  bool hold = false;                  // exec_control "hold": take no group
+  uint64_t heavy_at = HEAVY_DEFAULT;  // exec_control "heavy"
+  ExecStats stats;
 
   void finish_locked(Group* g, int rc) {
     g->rc = rc;
     g->done = true;
     g->cv.notify_all();
   }
+  bool takeable() const { return !order.empty() && !hold; }
   // the oldest group, closed to later jobs, once its writers are done (caller holds mu)
   Group* take_locked(std::unique_lock<std::mutex>& lk) {
     Group* g = order.front();
@@ -372,185 +339,131 @@ struct Exec {
     g->t_staged = std::chrono::steady_clock::now();
     return g;
   }
+  // issues g with mu released; on failure its callers are woken with the error (returns false)
+  bool issue_unlocked(std::unique_lock<std::mutex>& lk, Group* g, typename P::Handle* h) {
+    lk.unlock();
+    const int rc = P::issue(device, g->st, g->stg, h);
+    lk.lock();
+    if (rc != PRIO3_OK) {
+      finish_locked(g, rc);
+      return false;
+    }
+    stats.groups++;
+    return true;
+  }
+  void trace(const Group* g) {
+    if (FILE* f = exec_trace())
+      fprintf(f, "%.1f %.1f %.1f %.1f %d %u\n", exec_us(g->created), exec_us(g->t_take),
+              exec_us(g->t_staged), exec_us(std::chrono::steady_clock::now()), g->njobs,
+              P::reports(g->st));
+  }
 
-  // One group on the GPU at a time per launcher.  While it runs, the launcher polls it; once its
+  // Light load vs heavy load (reports of the jobs inside submit): launcher_pipe() below
+  // heavy_at, launcher() from there; launcher() hands back only below a third of it (between two
+  // cohorts the callers of the finished group leave submit for a moment, and a handover there
+  // cost the 128-thread line 10 %, r04z6).
+  bool light() const { return stats.active_reports < heavy_at; }
+  bool lighter() const { return stats.active_reports < heavy_at / 3; }
+
+  // Heavy load: one group on the GPU at a time.  While it runs, the launcher polls it; once its
   // prepare kernels are done, the next group -- by then holding the callers released by the
   // group before, all staged -- is issued behind it on its own stream, so the GPU does not idle
   // while this group's completion is noticed and the next launch is set up (r03y trace: 124 us
-  // between groups).
-  // The launcher must notice a group's 'prepared' event within microseconds (the next issue
-  // waits on it), but spinning through the whole ~0.7 ms group kept a core busy beside the
-  // staging writers.  It learns the prepare time per report from groups it watched
-  // complete while spinning, and sleeps through the first part of each later group (per group
-  // key: instances of very different cost share the executor; one table per launcher thread).
-  // A sleep that overshoots (the group was already prepared at the first poll) tells only an
-  // upper bound, so it shrinks the estimate instead of feeding it (r04a: feeding it made the
-  // estimate hold itself up, 5.4 M reports/s).
-  // JANUS_PRIO3_ISSUE_FRAC = f < 1: the next group may also be issued once the running one has
-  // run for f of its predicted prepare time (its kernels then share the GPU with the running
-  // group's, and its leader-share pull overlaps the running group's query); 1 = only when the
-  // running group's prepare kernels are done.
-  // A DMA group (engine_group_issue) is issued at JANUS_PRIO3_DMA_FRAC (default 0.3) of the
-  // running group's predicted prepare time: its input copies then run under the running group's
-  // compute, and its kernels wait for that group's prepare kernels (engine_group_issue's `after`).
-  static double env_frac(const char* name, double dflt) {
-    const char* s = getenv(name);
-    const double x = s ? atof(s) : dflt;
-    return x > 0 ? std::min(x, 1.0) : dflt;
-  }
-  static double issue_frac(bool dma) {
-    static const double pull = env_frac("JANUS_PRIO3_ISSUE_FRAC", 1.0);
-    static const double d = env_frac("JANUS_PRIO3_DMA_FRAC", 0.3);
-    return dma ? d : pull;
-  }
+  // between groups).  The launcher must notice a group's 'prepared' event within microseconds,
+  // but spinning through the whole ~0.7 ms group kept a core busy beside the staging writers
+  // (ADVICE r3): it learns the prepare time per report from groups it watched complete while
+  // spinning, and sleeps through the first 70 % of each later group (per group key: instances
+  // of very different cost share the executor).  A sleep that overshoots (the group was already
+  // prepared at the first poll) tells only an upper bound, so it shrinks the estimate instead of
+  // feeding it (r04a: feeding it made the estimate hold itself up, 5.4 M reports/s).  `preds` is
+  // the launcher thread's own table.  Returns (with nothing in flight) when the load turns light.
   struct Pred {
     double ns_per_report = 0;
     int seen = 0;
   };
-  std::map<uint64_t, Pred> preds;  // launcher()'s prepare-time table (kept across mode switches)
-  // heavy load: the reports inside submit at which launcher() takes over from launcher_pipe()
-  static uint64_t heavy() {
-    static const uint64_t v = (uint64_t)std::max(1, env_int("JANUS_PRIO3_PIPE_HEAVY", 32768));
-    return v;
-  }
-  // caller holds mu; hysteresis: launcher_pipe() hands over at heavy(), launcher() hands back only
-  // below a third of it (between two cohorts the callers of the finished group leave submit for
-  // a moment, and a handover there cost the 128-thread line 10 %, r04z6)
-  bool light() const { return pipe_mode() && active < heavy(); }
-  bool lighter() const { return pipe_mode() && active < heavy() / 3; }
-  // Returns (with nothing in flight) when the load turns light, to launcher_pipe().
-  void launcher() {
+  void launcher(std::map<uint64_t, Pred>& preds) {
     std::unique_lock<std::mutex> lk(mu);
     Group* cur = nullptr;
     typename P::Handle hc{};
-    auto t0 = std::chrono::steady_clock::now();  // when cur was issued
+    auto t0 = std::chrono::steady_clock::now();  // when cur could start
     for (;;) {
       if (!cur) {
         if (lighter()) return;
-        while (order.empty()) cv.wait(lk);
+        while (!takeable()) cv.wait(lk);
         Group* g = take_locked(lk);
-        lk.unlock();
         t0 = std::chrono::steady_clock::now();
-        const int rc = P::issue(device, g->st, g->stg, &hc, nullptr);
-        lk.lock();
-        if (rc != PRIO3_OK) {
-          finish_locked(g, rc);
-          continue;
-        }
+        if (!issue_unlocked(lk, g, &hc)) continue;
         cur = g;
       }
       lk.unlock();
       Group* nxt = nullptr;
       typename P::Handle hn{};
-      int rcn = PRIO3_OK;
-      bool looked = false, tried_sleep = false, just_slept = false;
+      bool looked = false;
       auto tn = t0;  // when nxt was issued
-      auto tp = t0;  // when cur was seen prepared (an early-issued nxt's kernels start then)
+      auto tp = t0;  // when cur was seen prepared (nxt's kernels start then)
       const uint32_t nrep = P::reports(cur->st);
       Pred& pr = preds[cur->key];
-      // the next group goes early when it will be a DMA group (its copies overlap cur)
-      lk.lock();
-      const bool nxt_dma = !order.empty() && P::early(order.front()->st);
-      lk.unlock();
-      const double frac = issue_frac(nxt_dma), pred_ns = pr.ns_per_report * nrep;
+      bool just_slept = false;
+      {  // sleep to 70 % of the predicted prepare time, less the timer slack (~60 us), <= 2 ms
+        const double ns = std::min(2e6, 0.7 * pr.ns_per_report * nrep - 60e3 - ns_since(t0));
+        if (pr.seen >= 2 && ns > 20e3) {
+          std::this_thread::sleep_for(std::chrono::nanoseconds((int64_t)ns));
+          just_slept = true;
+        }
+      }
       while (!P::done(hc)) {
-        if (!tried_sleep) {
-          tried_sleep = true;
-          // sleep to 70 % (or the early-issue point) of the predicted prepare time, less the
-          // timer slack (~60 us), at most 2 ms
-          const double ns = std::min(2e6, std::min(0.7, frac) * pred_ns - 60e3 -
-                                              std::chrono::duration<double, std::nano>(
-                                                  std::chrono::steady_clock::now() - t0).count());
-          if (pr.seen >= 2 && ns > 20e3) {
-            std::this_thread::sleep_for(std::chrono::nanoseconds((int64_t)ns));
-            just_slept = true;
-          }
-        }
-        if (!nxt && frac < 1.0 && pr.seen >= 2 &&
-            std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - t0)
-                    .count() >= frac * pred_ns) {
-          lk.lock();
-          if (!order.empty() && order.front()->writers == 0 && !lighter()) nxt = take_locked(lk);
-          lk.unlock();
-          tn = std::chrono::steady_clock::now();
-          if (nxt) rcn = P::issue(device, nxt->st, nxt->stg, &hn, &hc);
-        }
         if (!looked && P::prepared(hc)) {
           looked = true;
           tp = std::chrono::steady_clock::now();
-          const double el = std::chrono::duration<double, std::nano>(tp - t0).count();
-          const double x = nrep ? el / nrep : 0;
+          const double x = nrep ? ns_since(t0) / nrep : 0;
           if (just_slept) {
-            pr.ns_per_report *= 0.8;  // overslept: el is only an upper bound
+            pr.ns_per_report *= 0.8;  // overslept: the elapsed time is only an upper bound
           } else {
             pr.ns_per_report = pr.seen ? std::min(x, 0.8 * pr.ns_per_report + 0.2 * x) : x;
             pr.seen++;
           }
-          if (!nxt) {
-            lk.lock();
-            if (!order.empty() && order.front()->writers == 0 && !lighter()) nxt = take_locked(lk);
-            lk.unlock();
+          lk.lock();
+          if (takeable() && order.front()->writers == 0 && !lighter()) {
+            nxt = take_locked(lk);
             tn = std::chrono::steady_clock::now();
-            if (nxt) rcn = P::issue(device, nxt->st, nxt->stg, &hn, nullptr);
+            if (!issue_unlocked(lk, nxt, &hn)) nxt = nullptr;
           }
+          lk.unlock();
         }
         just_slept = false;
         std::this_thread::yield();
       }
       const int rc = P::finish(&hc);
-      if (FILE* f = exec_trace())
-        fprintf(f, "%.1f %.1f %.1f %.1f %d %u\n", exec_us(cur->created), exec_us(cur->t_take),
-                exec_us(cur->t_staged), exec_us(std::chrono::steady_clock::now()), cur->njobs,
-                P::reports(cur->st));
+      trace(cur);
       lk.lock();
       finish_locked(cur, rc);
       cur = nullptr;
       if (nxt) {
-        if (rcn != PRIO3_OK) {
-          finish_locked(nxt, rcn);
-        } else {
-          cur = nxt;
-          hc = hn;
-          // its prepare time counts from when its kernels could start: an early-issued group
-          // waited for cur's prepare kernels
-          t0 = looked ? std::max(tn, tp) : tn;
-        }
+        cur = nxt;
+        hc = hn;
+        t0 = std::max(tn, tp);  // its prepare time counts from when its kernels could start
       }
     }
   }
 
-  // Under light load (fewer than JANUS_PRIO3_PIPE_HEAVY = 32 Ki reports inside submit: the box's
-  // 16 rayon threads make groups of a few jobs, each a latency-bound kernel at well under a wave
-  // per SIMD) the launcher runs this pipeline instead of launcher(): up to four groups whose
-  // kernels run concurrently (no group waits for another's prepare), each issued as soon as it is
-  // staged and holds >= 2 Ki reports (smaller ones wait for an empty pipeline), any finished group
-  // completed at once: 10-15 M reports/s at 16 threads against 5.6-7.6 M/s for launcher() on the
-  // same boxes (r04z).  Under heavy load (the 128-thread line) launcher()'s two-cohort rhythm
-  // stays ahead (38.6-39.6 M/s against 28-35 M/s for this pipeline, r04z2-4).
-  // JANUS_PRIO3_PIPE=0: launcher() only.  The pipeline yields between polls (a sleep's timer
-  // slack would be a fifth of a small group's time).
-  static bool pipe_mode() {
-    static const bool v = [] {
-      const char* s = getenv("JANUS_PRIO3_PIPE");
-      return !s || atoi(s) != 0;
-    }();
-    return v;
-  }
-  static int env_int(const char* name, int dflt) {
-    const char* s = getenv(name);
-    return s ? atoi(s) : dflt;
-  }
+  // Light load (the box's 16 rayon threads make groups of a few jobs, each a latency-bound kernel
+  // at well under a wave per SIMD): up to four groups whose kernels run concurrently (no group
+  // waits for another's prepare), each issued as soon as it is staged and holds >= 2 Ki reports
+  // (smaller ones wait for an empty pipeline), any finished group completed at once: 10-15 M
+  // reports/s at 16 threads against 5.6-7.6 M/s for launcher() on the same boxes (r04z).  Under
+  // heavy load (the 128-thread line) launcher()'s two-cohort rhythm stays ahead (38.6-39.6 M/s
+  // against 28-35 M/s for this pipeline, r04z2-4).  The pipeline yields between polls (a sleep's
+  // timer slack would be a fifth of a small group's time).
   void launcher_pipe() {
     struct Slot {
       Group* g;
       typename P::Handle h;
-      bool prepared;
     };
     std::deque<Slot> q;
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
       if (q.empty() && !light()) return;  // heavy load: launcher() from here
-      while (!order.empty()) {
+      while (takeable()) {
         Group* g = order.front();
         if (!q.empty()) {
           // heavy load: let the pipeline drain (one bubble) and hand over to launcher()
@@ -558,33 +471,21 @@ struct Exec {
           if (P::reports(g->st) < 2048u) break;  // a small group waits for a drained pipeline
         }
         take_locked(lk);
-        lk.unlock();
-        Slot sl{g, typename P::Handle{}, false};
-        const int rc = P::issue(device, g->st, g->stg, &sl.h, nullptr);
-        lk.lock();
-        if (rc != PRIO3_OK) {
-          finish_locked(g, rc);
-          continue;
-        }
-        q.push_back(sl);
+        Slot sl{g, typename P::Handle{}};
+        if (issue_unlocked(lk, g, &sl.h)) q.push_back(sl);
       }
       if (q.empty()) {
-        while (order.empty()) cv.wait(lk);
+        while (!takeable() && light()) cv.wait(lk);
         continue;
       }
       lk.unlock();
-      for (auto& sl : q)
-        if (!sl.prepared && P::prepared(sl.h)) sl.prepared = true;
       bool any = false;
       for (size_t i = 0; i < q.size();) {
         if (P::done(q[i].h)) {
           Slot sl = q[i];
           q.erase(q.begin() + (long)i);
           const int rc = P::finish(&sl.h);
-          if (FILE* f = exec_trace())
-            fprintf(f, "%.1f %.1f %.1f %.1f %d %u\n", exec_us(sl.g->created),
-                    exec_us(sl.g->t_take), exec_us(sl.g->t_staged),
-                    exec_us(std::chrono::steady_clock::now()), sl.g->njobs, P::reports(sl.g->st));
+          trace(sl.g);
           std::lock_guard<std::mutex> lg(mu);
           finish_locked(sl.g, rc);
           any = true;
@@ -597,32 +498,39 @@ struct Exec {
     }
   }
 
-  uint64_t active = 0;  // reports of the jobs inside submit (the callers' load; under mu)
   int submit(typename P::Job* job) {
     std::unique_lock<std::mutex> lk(mu);
-    active += job->n;
+    stats.jobs++;
+    stats.reports += job->n;
+    stats.active_jobs++;
+    stats.active_reports += job->n;
     struct Done {  // runs with mu held: every return below holds lk
-      uint64_t& a;
+      ExecStats& s;
       uint32_t n;
-      ~Done() { a -= n; }
-    } done_{active, job->n};
-    if (!started) {
+      ~Done() {
+        s.active_jobs--;
+        s.active_reports -= n;
+      }
+    } done_{stats, job->n};
+    if (!started) {  // one launcher thread per executor (never joined: see g_exec)
       started = true;
-      for (int i = 0; i < max_inflight(); i++)
-        std::thread([this] {
-          for (;;) {  // launcher() under heavy load, launcher_pipe() under light load
-            launcher();
-            launcher_pipe();
-          }
-        }).detach();
+      std::thread([this] {
+        std::map<uint64_t, Pred> preds;
+        for (;;) {  // launcher() under heavy load, launcher_pipe() under light load
+          launcher(preds);
+          launcher_pipe();
+        }
+      }).detach();
     }
+    // the load may have crossed heavy_at: a launcher waiting in light mode re-checks
+    cv.notify_one();
     const uint64_t key = P::key(job);
     Group* g = nullptr;
     for (;;) {
       auto it = open.find(key);
       g = it == open.end() ? nullptr : it->second;
       if (g && P::reserve(g->st, job)) break;
-      if (g) {  // full: it stays queued for a launcher as it is
+      if (g) {  // full: it stays queued for the launcher as it is
         g->closed = true;
         open.erase(it);
       }
@@ -633,7 +541,7 @@ struct Exec {
         delete g;
         return PRIO3_EINVAL;
       }
-      g->stg = staging_get(device, bytes, P::vram_inputs());
+      g->stg = staging_get(device, bytes);
       if (!g->stg.p) {
         delete g;
         return PRIO3_EDEVICE;
@@ -662,6 +570,23 @@ struct Exec {
       delete g;
     }
     return rc;
+  }
+
+  int control(const char* key, int64_t value) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!strcmp(key, "hold")) {
+      hold = value != 0;
+    } else if (!strcmp(key, "heavy")) {
+      heavy_at = value > 0 ? (uint64_t)value : HEAVY_DEFAULT;
+    } else {
+      return PRIO3_EINVAL;
+    }
+    cv.notify_all();
+    return PRIO3_OK;
+  }
+  ExecStats get_stats() {
+    std::lock_guard<std::mutex> lk(mu);
+    return stats;
   }
 };
 
@@ -702,7 +627,6 @@ struct PrepPolicy {
   };
   static uint64_t key(Job* j) { return engine_group_key(j->e); }
   static uint32_t reports(const State& s) { return s.n; }
-  static bool vram_inputs() { return vram_staging(); }
   static bool create(State& s, Job* j, size_t* bytes) {
     s.lead = j->e;
     IoLayout l1, l2;
@@ -711,7 +635,7 @@ struct PrepPolicy {
     const size_t per = l2.bytes - l1.bytes + 1;
     const uint32_t cap_b = (uint32_t)std::max<size_t>(1, STAGING_TARGET / per);
     s.align = engine_job_align(j->e);
-    s.cap = std::max(j->n, std::min(max_group_reports(), cap_b));
+    s.cap = std::max(j->n, std::min(MAX_GROUP_REPORTS, cap_b));
     s.cap = (s.cap + 63) & ~63u;  // room for the tail pad of a wave-aligned group
     engine_io_layout(j->e, s.cap, &s.L);
     *bytes = s.L.bytes;
@@ -775,8 +699,7 @@ struct PrepPolicy {
     GroupRun gr;
     State* s = nullptr;
   };
-  static bool early(const State& s) { return engine_group_dma(s.lead, s.n); }
-  static int issue(int device, State& s, Staging& g, Handle* h, const Handle* prev) {
+  static int issue(int device, State& s, Staging& g, Handle* h) {
     (void)device;
     GroupView v;
     if (s.align > 1) {  // whole waves: the group's tail padded like the gaps
@@ -788,13 +711,11 @@ struct PrepPolicy {
     v.cap = s.cap;
     v.stg = g.p;
     v.stg_dev = g.dev;
-    v.out = g.out;
-    v.out_dev = g.out_dev;
     v.n_keys = (uint32_t)s.keys.size();
     v.jobs = (int)s.jobs;
     v.nseg = s.nseg;
     h->s = &s;
-    return engine_group_issue(s.lead, v, &h->gr, prev ? &prev->gr : nullptr);
+    return engine_group_issue(s.lead, v, &h->gr);
   }
   static bool prepared(const Handle& h) { return engine_group_prepared(h.gr); }
   static bool done(const Handle& h) { return engine_group_done(h.gr); }
@@ -802,11 +723,11 @@ struct PrepPolicy {
   static void unstage(State& s, Staging& g, Job* j) {
     const IoLayout& L = s.L;
     if (L.msg_len && j->msgs_out)
-      memcpy(j->msgs_out, g.out + L.msg_off + L.msg_len * j->c0, L.msg_len * j->n);
-    if (j->status_out) memcpy(j->status_out, g.out + L.status_off + j->c0, j->n);
+      memcpy(j->msgs_out, g.p + L.msg_off + L.msg_len * j->c0, L.msg_len * j->n);
+    if (j->status_out) memcpy(j->status_out, g.p + L.status_off + j->c0, j->n);
     if (j->nseg) {
-      memcpy(j->agg_out, g.out + L.agg_off + L.agg_len * j->seg0, L.agg_len * j->nseg);
-      memcpy(j->counts_out, g.out + L.cnt_off + 8 * (size_t)j->seg0, 8 * (size_t)j->nseg);
+      memcpy(j->agg_out, g.p + L.agg_off + L.agg_len * j->seg0, L.agg_len * j->nseg);
+      memcpy(j->counts_out, g.p + L.cnt_off + 8 * (size_t)j->seg0, 8 * (size_t)j->nseg);
     }
     j->run = s.run;  // one reference per job (engine_group_finish sets refs = jobs)
   }
@@ -825,7 +746,6 @@ struct AccPolicy {
   };
   static uint64_t key(Job* j) { return (uint64_t)engine_acc_key(j); }
   static uint32_t reports(const State& s) { return s.reps; }
-  static bool vram_inputs() { return false; }  // its host side reads the staging back
   static bool create(State& s, Job* j, size_t* bytes) {
     s.es = (int)engine_acc_key(j);
     const uint32_t reps = std::max(MAX_REPS, j->n);
@@ -847,8 +767,7 @@ struct AccPolicy {
   }
   static void stage(State& s, Staging& g, Job* j) { engine_acc_stage(j, g.p, s.L); }
   struct Handle {};  // the accumulate group runs to completion inside issue
-  static bool early(const State&) { return false; }
-  static int issue(int device, State& s, Staging& g, Handle*, const Handle*) {
+  static int issue(int device, State& s, Staging& g, Handle*) {
     return engine_acc_group(device, s.es, g.p, s.L, s.jobs, s.out);
   }
   static bool prepared(const Handle&) { return true; }
@@ -857,16 +776,215 @@ struct AccPolicy {
   static void unstage(State& s, Staging& g, Job* j) { engine_acc_unstage(j, g.p, s.L); }
 };
 
-Exec<PrepPolicy>* g_prep = [] {  // never destroyed: launcher threads may wait on them at exit
-  auto* x = new Exec<PrepPolicy>[MAX_DEVICES];
-  for (int d = 0; d < MAX_DEVICES; d++) x[d].device = d;
+// ---- leader prepare_init groups ----
+struct LeaderPolicy {
+  typedef LeaderJob Job;
+  struct State {
+    prio3_engine* lead = nullptr;
+    std::vector<const prio3_engine*> keys;  // verify-key table, slot = index
+    uint32_t n = 0, cap = 0, jobs = 0;
+    LeaderLayout L;
+    Run* run = nullptr;
+  };
+  // a different key space from the helper's groups: the executors are separate
+  static uint64_t key(Job* j) { return engine_group_key(j->e); }
+  static uint32_t reports(const State& s) { return s.n; }
+  static bool create(State& s, Job* j, size_t* bytes) {
+    s.lead = j->e;
+    LeaderLayout l1, l2;
+    engine_leader_layout(j->e, 1, &l1);
+    engine_leader_layout(j->e, 2, &l2);
+    const size_t per = l2.bytes - l1.bytes + 1;
+    const uint32_t cap_b = (uint32_t)std::max<size_t>(1, STAGING_TARGET / per);
+    s.cap = std::max(j->n, std::min(MAX_GROUP_REPORTS, cap_b));
+    engine_leader_layout(j->e, s.cap, &s.L);
+    *bytes = s.L.bytes;
+    return true;
+  }
+  static bool reserve(State& s, Job* j) {
+    uint32_t k = 0;
+    while (k < s.keys.size() && s.keys[k] != j->e) k++;
+    if (k == s.keys.size() && s.keys.size() >= exec_max_keys()) return false;
+    if (s.n + j->n > s.cap) return false;
+    if (k == s.keys.size()) s.keys.push_back(j->e);
+    j->c0 = s.n;
+    j->slot = k;
+    s.n += j->n;
+    s.jobs++;
+    return true;
+  }
+  static void stage(State& s, Staging& g, Job* j) {
+    const LeaderLayout& L = s.L;
+    const uint8_t* src[3] = {j->nonces, j->pub, j->linput};
+    for (int f = 0; f < 3; f++)
+      if (L.len[f] && src[f]) stream_copy(g.p + L.off[f] + L.len[f] * j->c0, src[f], L.len[f] * j->n);
+    uint16_t* slots = (uint16_t*)(g.p + L.slot_off) + j->c0;
+    for (uint32_t i = 0; i < j->n; i++) slots[i] = (uint16_t)j->slot;
+    engine_vk(j->e, g.p + L.tab_off + 16 * (size_t)j->slot);
+  }
+  struct Handle {
+    GroupRun gr;
+    State* s = nullptr;
+  };
+  static int issue(int, State& s, Staging& g, Handle* h) {
+    h->s = &s;
+    return engine_leader_issue(s.lead, s.L, g.dev, s.n, (uint32_t)s.keys.size(), (int)s.jobs,
+                               &h->gr);
+  }
+  static bool prepared(const Handle& h) { return engine_group_prepared(h.gr); }
+  static bool done(const Handle& h) { return engine_group_done(h.gr); }
+  static int finish(Handle* h) { return engine_group_finish(&h->gr, &h->s->run); }
+  static void unstage(State& s, Staging& g, Job* j) {
+    const LeaderLayout& L = s.L;
+    memcpy(j->prep_out, g.p + L.ps_off + L.ps_len * j->c0, L.ps_len * j->n);
+    memcpy(j->status_out, g.p + L.status_off + j->c0, j->n);
+    j->run = s.run;  // one reference per job
+  }
+};
+
+// ---- leader prepare_next groups ----
+struct LNextPolicy {
+  typedef LNextJob Job;
+  struct State {
+    LNextLayout L;
+    uint32_t jobs = 0, reps = 0, max_n = 0, es = 16;
+  };
+  struct Handle {
+    int device = 0;
+    hipStream_t st = nullptr;
+  };
+  static uint64_t key(Job* j) { return engine_lnext_key(j); }
+  static uint32_t reports(const State& s) { return s.reps; }
+  static bool create(State& s, Job* j, size_t* bytes) {
+    if (j->n > LNEXT_MAX_REPS) return false;
+    s.es = engine_lnext_key(j);
+    lnext_layout(&s.L);
+    *bytes = s.L.bytes;
+    return true;
+  }
+  static bool reserve(State& s, Job* j) {
+    if (s.jobs + 1 > LNEXT_MAX_JOBS || s.reps + j->n > LNEXT_MAX_REPS) return false;
+    j->slot = s.jobs++;
+    j->rep_off = s.reps;
+    s.reps += j->n;
+    s.max_n = std::max(s.max_n, j->n);
+    return true;
+  }
+  static void stage(State& s, Staging& g, Job* j) { engine_lnext_stage(j, g.p, s.L); }
+  static int issue(int device, State& s, Staging& g, Handle* h) {
+    h->device = device;
+    return engine_lnext_issue(device, s.es, g.dev, s.L, s.jobs, s.max_n, &h->st);
+  }
+  static bool prepared(const Handle& h) { return done(h); }
+  static bool done(const Handle& h) { return hipStreamQuery(h.st) != hipErrorNotReady; }
+  static int finish(Handle* h) {
+    const hipError_t q = hipStreamSynchronize(h->st);
+    ws_stream_put(h->device, h->st);
+    return q == hipSuccess ? PRIO3_OK : PRIO3_EDEVICE;
+  }
+  static void unstage(State& s, Staging& g, Job* j) {
+    memcpy(j->status, g.p + s.L.status_off + j->rep_off, j->n);
+  }
+};
+
+// ---- HPKE open groups ----
+struct HpkePolicy {
+  typedef HpkeJob Job;
+  struct State {
+    HpkeJob proto;  // the group's opener and per-task constants (stride, share lengths)
+    std::vector<std::array<uint8_t, 32>> tasks;  // task-ID table, slot = index
+    uint32_t n = 0, cap = 0;
+    HpkeLayout L;
+  };
+  struct Handle {
+    int device = 0;
+    hipStream_t st = nullptr;
+    Slab* slab = nullptr;
+  };
+  static uint64_t key(Job* j) { return hpke_group_key(j); }
+  static uint32_t reports(const State& s) { return s.n; }
+  static bool create(State& s, Job* j, size_t* bytes) {
+    s.proto = *j;
+    HpkeLayout l1, l2;
+    hpke_layout(j, 1, &l1);
+    hpke_layout(j, 2, &l2);
+    const size_t per = l2.pt_off - l1.pt_off + 1;
+    const uint32_t cap_b = (uint32_t)std::max<size_t>(1, STAGING_TARGET / per);
+    s.cap = std::max(j->n, std::min(MAX_GROUP_REPORTS, cap_b));
+    hpke_layout(j, s.cap, &s.L);
+    *bytes = s.L.pt_off;  // the staging holds everything but the device plaintext scratch
+    return true;
+  }
+  static bool reserve(State& s, Job* j) {
+    uint32_t k = 0;
+    while (k < s.tasks.size() && memcmp(s.tasks[k].data(), j->task_id, 32)) k++;
+    if (k == s.tasks.size() && s.tasks.size() >= HPKE_MAX_TASKS) return false;
+    if (s.n + j->n > s.cap) return false;
+    if (k == s.tasks.size()) {
+      std::array<uint8_t, 32> t;
+      memcpy(t.data(), j->task_id, 32);
+      s.tasks.push_back(t);
+    }
+    j->c0 = s.n;
+    j->slot = k;
+    s.n += j->n;
+    return true;
+  }
+  static void stage(State& s, Staging& g, Job* j) {
+    const HpkeLayout& L = s.L;
+    const size_t c0 = j->c0, n = j->n;
+    stream_copy(g.p + L.off_enc + L.nenc * c0, j->enc, L.nenc * n);
+    stream_copy(g.p + L.off_ct + (size_t)j->ct_stride * c0, j->ct, (size_t)j->ct_stride * n);
+    memcpy(g.p + L.off_len + 4 * c0, j->ct_len, 4 * n);
+    memcpy(g.p + L.off_ids + 16 * c0, j->ids, 16 * n);
+    memcpy(g.p + L.off_times + 8 * c0, j->times, 8 * n);
+    if (j->pub_len) memcpy(g.p + L.off_pub + (size_t)j->pub_len * c0, j->pubs, (size_t)j->pub_len * n);
+    uint16_t* slots = (uint16_t*)(g.p + L.slot_off) + c0;
+    for (uint32_t i = 0; i < j->n; i++) slots[i] = (uint16_t)j->slot;
+    uint32_t* tab = (uint32_t*)(g.p + L.tab_off) + 8 * (size_t)j->slot;
+    for (int i = 0; i < 8; i++) {  // BE words, as the kernel's AAD takes them
+      const uint8_t* b = j->task_id + 4 * i;
+      tab[i] = (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3];
+    }
+  }
+  static int issue(int device, State& s, Staging& g, Handle* h) {
+    h->device = device;
+    return hpke_group_issue(s.proto, s.L, g.p, g.p, s.n, &h->st, &h->slab);
+  }
+  static bool prepared(const Handle& h) { return done(h); }
+  static bool done(const Handle& h) { return hipStreamQuery(h.st) != hipErrorNotReady; }
+  static int finish(Handle* h) {
+    const hipError_t q = hipStreamSynchronize(h->st);
+    ws_release(h->slab, h->st);
+    ws_stream_put(h->device, h->st);
+    return q == hipSuccess ? PRIO3_OK : PRIO3_EDEVICE;
+  }
+  static void unstage(State& s, Staging& g, Job* j) {
+    const HpkeLayout& L = s.L;
+    memcpy(j->shares_out, g.p + L.shares_off + (size_t)j->share_len * j->c0,
+           (size_t)j->share_len * j->n);
+    memcpy(j->status_out, g.p + L.status_off + j->c0, j->n);
+  }
+};
+
+constexpr int N_EXEC = MAX_DEVICES * EXEC_LANES;
+
+template <class P>
+Exec<P>* make_execs() {  // never destroyed: launcher threads may wait on them at exit
+  auto* x = new Exec<P>[N_EXEC];
+  for (int i = 0; i < N_EXEC; i++) {
+    x[i].id = i;
+    x[i].device = i / EXEC_LANES;
+  }
   return x;
-}();
-Exec<AccPolicy>* g_acc = [] {
-  auto* x = new Exec<AccPolicy>[MAX_DEVICES];
-  for (int d = 0; d < MAX_DEVICES; d++) x[d].device = d;
-  return x;
-}();
+}
+Exec<PrepPolicy>* g_prep = make_execs<PrepPolicy>();
+Exec<AccPolicy>* g_acc = make_execs<AccPolicy>();
+Exec<LeaderPolicy>* g_lead = make_execs<LeaderPolicy>();
+Exec<LNextPolicy>* g_lnext = make_execs<LNextPolicy>();
+Exec<HpkePolicy>* g_hpke = make_execs<HpkePolicy>();
+
+bool exec_id_ok(int id) { return id >= 0 && id < N_EXEC; }
 
 }  // namespace
 
@@ -885,14 +1003,68 @@ void acc_layout(uint32_t max_jobs, uint32_t max_reps, size_t out_cap, AccLayout*
 }
 
 int exec_submit(ExecJob* job) {
-  const int device = engine_device(job->e);
-  if (device < 0 || device >= MAX_DEVICES) return PRIO3_EINVAL;
-  return g_prep[device].submit(job);
+  const int id = engine_exec_id(job->e);
+  if (!exec_id_ok(id)) return PRIO3_EINVAL;
+  return g_prep[id].submit(job);
 }
 
 int exec_accumulate(AccJob* job) {
   if (job->device < 0 || job->device >= MAX_DEVICES) return PRIO3_EINVAL;
-  return g_acc[job->device].submit(job);
+  return g_acc[job->device * EXEC_LANES].submit(job);
+}
+
+int exec_leader(LeaderJob* job) {
+  const int id = engine_exec_id(job->e);
+  if (!exec_id_ok(id)) return PRIO3_EINVAL;
+  return g_lead[id].submit(job);
+}
+
+int exec_hpke(HpkeJob* job) {
+  const int d = hpke_opener_device(job->o);
+  if (d < 0 || d >= MAX_DEVICES) return PRIO3_EINVAL;
+  return g_hpke[d * EXEC_LANES].submit(job);
+}
+
+int exec_leader_next(LNextJob* job) {
+  if (job->device < 0 || job->device >= MAX_DEVICES) return PRIO3_EINVAL;
+  return g_lnext[job->device * EXEC_LANES].submit(job);
+}
+
+void lnext_layout(LNextLayout* L) {
+  auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  L->desc_off = 0;
+  L->msg_off = up(sizeof(LNextDesc) * (size_t)LNEXT_MAX_JOBS);
+  L->status_off = L->msg_off + up(16 * (size_t)LNEXT_MAX_REPS);
+  L->bytes = L->status_off + up((size_t)LNEXT_MAX_REPS);
+}
+
+int exec_stats(int kind, int id, ExecStats* out) {
+  if (!exec_id_ok(id) || !out) return PRIO3_EINVAL;
+  switch (kind) {
+    case EXEC_PREP: *out = g_prep[id].get_stats(); return PRIO3_OK;
+    case EXEC_ACC: *out = g_acc[id].get_stats(); return PRIO3_OK;
+    case EXEC_LEADER: *out = g_lead[id].get_stats(); return PRIO3_OK;
+    case EXEC_LNEXT: *out = g_lnext[id].get_stats(); return PRIO3_OK;
+    case EXEC_HPKE: *out = g_hpke[id].get_stats(); return PRIO3_OK;
+    default: return PRIO3_EINVAL;
+  }
+}
+
+int exec_control(int kind, int id, const char* key, int64_t value) {
+  if (!exec_id_ok(id) || !key) return PRIO3_EINVAL;
+  switch (kind) {
+    case EXEC_PREP: return g_prep[id].control(key, value);
+    case EXEC_ACC: return g_acc[id].control(key, value);
+    case EXEC_LEADER: return g_lead[id].control(key, value);
+    case EXEC_LNEXT: return g_lnext[id].control(key, value);
+    case EXEC_HPKE: return g_hpke[id].control(key, value);
+    default: return PRIO3_EINVAL;
+  }
+}
+
+uint64_t exec_load(int id) {
+  if (!exec_id_ok(id)) return 0;
+  return g_prep[id].get_stats().active_reports + g_lead[id].get_stats().active_reports;
 }
 
 // ---- tracing -------------------------------------------------------------------------------

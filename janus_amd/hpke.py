@@ -50,6 +50,8 @@ def _lib():
         L.janus_hpke_open.argtypes = [vp, u32, vp, vp, vp, u32, vp, vp, u32, vp, vp]
         L.janus_hpke_set_timing.argtypes = [vp, C.c_int]
         L.janus_hpke_timing.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]
+        L.janus_hpke_executor_stats_get.argtypes = [vp, C.POINTER(C.c_uint64 * 5)]
+        L.janus_hpke_executor_control.argtypes = [vp, C.c_char_p, C.c_int64]
         L.janus_hpke_selftest_p256.argtypes = [C.c_int, u32, vp, vp, vp]
         L.janus_hpke_selftest_field.argtypes = [C.c_int, C.c_int, u32, vp, vp, vp]
         _bound = True
@@ -149,6 +151,20 @@ class HpkeOpener:
         if rc:
             raise RuntimeError(f"janus_hpke_open failed (rc={rc})")
         return [None if st[i] else pt[i, :cl[i] - 16].tobytes() for i in range(n)]
+
+    def executor_stats(self) -> dict:
+        """Counters of the GPU's HPKE executor (janus_hpke_executor_stats_get)."""
+        v = (C.c_uint64 * 5)()
+        rc = _lib().janus_hpke_executor_stats_get(self.handle, C.byref(v))
+        if rc:
+            raise RuntimeError(f"janus_hpke_executor_stats_get failed (rc={rc})")
+        return dict(zip(("jobs", "reports", "groups", "active_jobs", "active_reports"), v))
+
+    def executor_control(self, key: str, value: int):
+        """janus_hpke_executor_control: "hold", "heavy", "coalesce"."""
+        rc = _lib().janus_hpke_executor_control(self.handle, key.encode(), int(value))
+        if rc:
+            raise ValueError(f"executor control {key} failed (rc={rc})")
 
     def set_timing(self, on: bool):
         _lib().janus_hpke_set_timing(self.handle, int(on))

@@ -64,6 +64,20 @@ class Prio3Params(C.Structure):
                 ("chunk_length", C.c_uint32), ("num_proofs", C.c_uint32)]
 
 
+class Prio3MemberInfo(C.Structure):
+    _fields_ = [("device", C.c_int32), ("lane", C.c_uint32), ("jobs", C.c_uint64),
+                ("reports", C.c_uint64), ("exec_jobs", C.c_uint64), ("exec_groups", C.c_uint64)]
+
+
+class Prio3ExecutorStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("jobs", "reports", "groups", "active_jobs",
+                                          "active_reports")]
+
+
+#: executor kinds of prio3_executor_stats_get
+EXEC_PREPARE, EXEC_ACCUMULATE, EXEC_LEADER_INIT, EXEC_LEADER_NEXT = 0, 1, 2, 3
+
+
 class Prio3Sizes(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in (
         "field_bytes", "meas_len", "out_len", "proof_len", "verifier_len", "joint_rand_len",
@@ -83,14 +97,17 @@ EXPORTED_SYMBOLS = (
     "prio3_device_aggregate_finish", "prio3_leader_prepare_init_batch",
     "prio3_leader_prepare_next_batch", "prio3_device_leader_prepare_init",
     "prio3_device_leader_prepare_next", "prio3_device_batch_metadata", "prio3_batch_metadata",
-    "prio3_device_combine_metadata", "prio3_engine_create_ex",
+    "prio3_device_combine_metadata", "prio3_engine_create_ex", "prio3_engine_create_mask",
+    "prio3_engine_create_devices", "prio3_engine_members", "prio3_executor_control",
+    "prio3_executor_stats_get",
 )
 # include/janus_hpke.h (the batched HPKE opener, janus_amd/hpke.py)
 HPKE_EXPORTED_SYMBOLS = (
     "janus_hpke_opener_create", "janus_hpke_opener_destroy",
     "janus_hpke_open_input_shares_device", "janus_hpke_open_input_shares",
     "janus_hpke_open_device", "janus_hpke_open", "janus_hpke_set_timing", "janus_hpke_timing",
-    "janus_hpke_selftest_p256", "janus_hpke_selftest_field",
+    "janus_hpke_selftest_p256", "janus_hpke_selftest_field", "janus_hpke_executor_stats_get",
+    "janus_hpke_executor_control",
 )
 
 _lib = None
@@ -117,6 +134,12 @@ def load_library() -> C.CDLL:
     L.prio3_sizes.argtypes = [P(Prio3Params), P(Prio3Sizes)]
     L.prio3_engine_create.argtypes = [P(Prio3Params), u8p, C.c_int, P(vp)]
     L.prio3_engine_create_ex.argtypes = [P(Prio3Params), u8p, C.c_size_t, C.c_int, P(vp)]
+    L.prio3_engine_create_mask.argtypes = [P(Prio3Params), u8p, C.c_size_t, C.c_int, P(vp)]
+    L.prio3_engine_create_devices.argtypes = [P(Prio3Params), u8p, C.c_size_t, P(C.c_int),
+                                              C.c_uint32, P(vp)]
+    L.prio3_engine_members.argtypes = [vp, P(Prio3MemberInfo), C.c_uint32]
+    L.prio3_executor_control.argtypes = [vp, C.c_int, C.c_char_p, C.c_int64]
+    L.prio3_executor_stats_get.argtypes = [vp, C.c_uint32, C.c_int, P(Prio3ExecutorStats)]
     L.prio3_engine_destroy.argtypes = [vp]
     L.prio3_engine_destroy.restype = None
     L.prio3_helper_prepare_batch.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, vp, vp, P(vp)]
@@ -314,11 +337,15 @@ class PreparedBatch:
 
 
 class HelperEngine:
-    """One engine per (Prio3 instance, verify key, GPU) -- created where Janus builds
-    ``VdafOps`` for a task (aggregator.rs:880-988)."""
+    """One engine per (Prio3 instance, verify key) -- created where Janus builds ``VdafOps`` for
+    a task (aggregator.rs:880-988) -- on one GPU (``device``), on the GPUs of ``device_mask``
+    (bit d = GPU d; jobs placed whole on the least-loaded GPU, prio3_engine_create_mask), or on
+    an explicit ``devices`` list (a GPU listed k times gets k executors: the one-GPU rehearsal
+    of that placement)."""
 
     def __init__(self, vdaf: Prio3, verify_key: bytes, device: int = 0,
-                 allow_unpinned: bool = False):
+                 allow_unpinned: bool = False, device_mask: Optional[int] = None,
+                 devices: Optional[list] = None):
         """allow_unpinned: required for Prio3FixedPointBoundedL2VecSum, whose circuit is a
         reconstruction with parity against prio unpinned (engine option experimental_fpvec)."""
         vk_len = 32 if vdaf.kind == PRIO3_SUMVEC_F64_MP else 16
@@ -326,11 +353,21 @@ class HelperEngine:
             raise ValueError(f"verify key must be {vk_len} bytes (VERIFY_KEY_LENGTH[_HMACSHA256_"
                              "AES128], core/src/vdaf.rs)")
         L = load_library()
-        self.vdaf, self.device = vdaf, device
         self.sz = vdaf.sizes()
         h = C.c_void_p()
         vk = (C.c_uint8 * vk_len).from_buffer_copy(verify_key)
-        rc = L.prio3_engine_create_ex(C.byref(vdaf.params()), vk, vk_len, device, C.byref(h))
+        if devices is not None:
+            arr = (C.c_int * len(devices))(*devices)
+            device = devices[0]
+            rc = L.prio3_engine_create_devices(C.byref(vdaf.params()), vk, vk_len, arr,
+                                               len(devices), C.byref(h))
+        elif device_mask is not None:
+            device = (device_mask & -device_mask).bit_length() - 1
+            rc = L.prio3_engine_create_mask(C.byref(vdaf.params()), vk, vk_len, device_mask,
+                                            C.byref(h))
+        else:
+            rc = L.prio3_engine_create_ex(C.byref(vdaf.params()), vk, vk_len, device, C.byref(h))
+        self.vdaf, self.device = vdaf, device
         if rc:
             raise RuntimeError(f"prio3_engine_create failed (rc={rc}); a GPU is required")
         self.handle = h
@@ -352,6 +389,32 @@ class HelperEngine:
         rc = load_library().prio3_engine_set_option(self.handle, key.encode(), int(value))
         if rc:
             raise ValueError(f"unknown option {key}")
+
+    def members(self) -> list:
+        """Per-GPU placement of this engine's host-buffer jobs (prio3_engine_members): one dict
+        per member with device, lane, jobs, reports, and its executor's exec_jobs / exec_groups."""
+        L = load_library()
+        k = L.prio3_engine_members(self.handle, None, 0)
+        if k < 0:
+            raise RuntimeError(f"prio3_engine_members failed (rc={k})")
+        arr = (Prio3MemberInfo * k)()
+        L.prio3_engine_members(self.handle, arr, k)
+        return [{f: getattr(m, f) for f, _ in Prio3MemberInfo._fields_} for m in arr]
+
+    def executor_stats(self, kind: int = EXEC_PREPARE, member: int = 0) -> dict:
+        """Counters of the executor of `kind` that member `member`'s jobs use."""
+        st = Prio3ExecutorStats()
+        rc = load_library().prio3_executor_stats_get(self.handle, member, kind, C.byref(st))
+        if rc:
+            raise RuntimeError(f"prio3_executor_stats_get failed (rc={rc})")
+        return {f: getattr(st, f) for f, _ in Prio3ExecutorStats._fields_}
+
+    def executor_control(self, key: str, value: int, kind: int = -1):
+        """prio3_executor_control on the executors of `kind` (-1: all): "hold" (tests queue jobs
+        behind it), "heavy" (load switch)."""
+        rc = load_library().prio3_executor_control(self.handle, kind, key.encode(), int(value))
+        if rc:
+            raise ValueError(f"executor control {key} failed (rc={rc})")
 
     # ---- host-buffer path -----------------------------------------------------------
     def prepare_batch(self, nonces, public_shares, helper_shares, leader_prep_shares):

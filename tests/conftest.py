@@ -10,14 +10,6 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")
-    config.addinivalue_line("markers", "gpu_first: run before any other test of the session "
-                            "(before this process holds GPU queues or memory)")
-
-
-def pytest_collection_modifyitems(config, items):
-    first = [it for it in items if it.get_closest_marker("gpu_first")]
-    if first:
-        items[:] = first + [it for it in items if not it.get_closest_marker("gpu_first")]
 
 
 @pytest.fixture(scope="session")

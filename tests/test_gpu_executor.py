@@ -81,11 +81,44 @@ def test_interleaved_batches_keep_their_own_outputs():
         b.free()
 
 
-@pytest.mark.parametrize("name", ["hist_256_c16", "sumvec_8x10_c9", "count"])
+class _Held:
+    """Holds the executors of `eng` (prio3_executor_control "hold") until `n` jobs have entered
+    them, then releases them: the jobs are queued before the launcher can take any, so whether
+    they are coalesced no longer depends on thread timing.  Always released on exit
+    -- the executors are process-wide."""
+
+    def __init__(self, eng, n, kind=0):
+        self.eng, self.n, self.kind = eng, n, kind
+
+    def _entered(self):
+        return sum(self.eng.executor_stats(self.kind, i)["jobs"]
+                   for i in range(len(self.eng.members())))
+
+    def __enter__(self):
+        self.base = self._entered()
+        self.eng.executor_control("hold", 1, self.kind)
+        return self
+
+    def wait(self, timeout=60.0):
+        import time
+        t0 = time.monotonic()
+        while self._entered() - self.base < self.n:
+            if time.monotonic() - t0 > timeout:
+                raise AssertionError(f"only {self._entered() - self.base} of {self.n} jobs queued")
+            time.sleep(0.005)
+        time.sleep(0.05)  # their staging copies (the launcher waits for writers anyway)
+        self.eng.executor_control("hold", 0, self.kind)
+
+    def __exit__(self, *exc):
+        self.eng.executor_control("hold", 0, self.kind)
+
+
+@pytest.mark.parametrize("name", ["hist_256_c16", "sumvec_8x10_c9", "count", "sum32"])
 def test_concurrent_jobs_of_several_tasks_are_coalesced(name):
-    """24 jobs of 100-500 reports for 4 tasks (verify keys) of one VDAF instance from 8 threads
-    at once: every job's prepare messages, statuses and aggregate equal the restatement's, and
-    (Histogram(256, 16)) the executor merged them into fewer launches than jobs."""
+    """24 jobs of 100-500 reports for 4 tasks (verify keys) of one VDAF instance, queued behind
+    the executor's hold from 24 threads and then released: every job's prepare messages,
+    statuses and aggregate equal the restatement's, and the executor merged them into fewer
+    launches than jobs (one group holds them all)."""
     from oracle.oracle import Oracle
     cfg = CONFIGS[name]
     o = Oracle(**cfg)
@@ -103,12 +136,9 @@ def test_concurrent_jobs_of_several_tasks_are_coalesced(name):
         if j % 3 == 0:
             d = _tamper(o, d, rng)
         jobs.append((t, d))
-    start = threading.Barrier(8)
 
     def run(j):
         t, d = jobs[j]
-        if j < 8:
-            start.wait()
         msgs, status, batch = engines[t].prepare_batch(d["nonces"], d["public_shares"],
                                                        d["helper_shares"],
                                                        d["leader_prep_shares"])
@@ -116,42 +146,37 @@ def test_concurrent_jobs_of_several_tasks_are_coalesced(name):
         batch.free()
         return msgs, status, agg, cnt
 
-    with ThreadPoolExecutor(8) as ex:
-        got = list(ex.map(run, range(24)))
+    with _Held(engines[0], 24) as held, ThreadPoolExecutor(24) as ex:
+        futs = [ex.submit(run, j) for j in range(24)]
+        held.wait()
+        got = [f.result(timeout=120) for f in futs]
     for (t, d), (msgs, status, agg, cnt) in zip(jobs, got):
         rm, rs, ra, rc = _ref(o, vks[t], d)
         np.testing.assert_array_equal(status, rs)
         np.testing.assert_array_equal(msgs, rm)
         np.testing.assert_array_equal(agg, ra)
         np.testing.assert_array_equal(cnt, rc)
-    # Histogram(256, 16) (P = 32) and Count run their XOF and query in one launch
-    # (small groups on the lane-pair k_prep_hp)
-    kern = {"count": ("k_prep_gen",), "hist_256_c16": ("k_prep_h", "k_prep_hp")}.get(
-        name, ("k_xofd",))
+    # the prepare launch of each instance (one kernel per group: the fused XOF + query, or the
+    # XOF of the two-kernel chains)
+    kern = {"count": ("k_prep_gen",), "hist_256_c16": ("k_prep_h", "k_prep_hp"),
+            "sum32": ("k_prep_sum",)}.get(name, ("k_xofd",))
     launches = sum(e.timing().get(k, (0, 0))[1] for e in engines for k in kern)
-    # A small instance's group launch (Count: ~30 us) can be shorter than one Python caller's
-    # way into the C ABI, so on an idle GPU each job may find the pipeline drained and launch
-    # alone (r04n: Count, 24 launches).  Coalescing is asserted where a launch outlasts that
-    # (Histogram(256, 16), the headline instance) and measured by the native jobs line.
-    if name == "hist_256_c16":
-        assert 0 < launches < 24, launches
-    else:
-        assert 0 < launches <= 24, launches
+    assert 0 < launches < 24, launches
 
 
 @pytest.mark.parametrize("name", ["hist_256_c16", "hist_100_c10", "sumvec_8x10_c9", "count",
-                                  "sum32", "hist_256_c16/one_lane", "hist_256_c16/dma",
-                                  "hist_256_c16/one_lane_dma", "sumvec_8x10_c9/dma",
-                                  "count/dma", "hist_100_c10/dma", "sum32/dma"])
+                                  "sum32", "hist_256_c16/one_lane", "hist_256_c16/heavy",
+                                  "count/heavy", "sumvec_8x10_c9/heavy", "hist_100_c10/heavy"])
 def test_combined_prepare_aggregate_jobs(name):
-    """prio3_helper_prepare_aggregate_batch from 8 threads at once: 32 jobs of 100-500 reports
-    for 4 tasks, each with its own segments (1-4, ids past n_segments included) and accept
-    mask, some tampered, and every fourth job a plain prepare_batch + accumulate in the same
-    groups.  Each job's messages, statuses, per-segment aggregates and counts equal the
-    restatement's, and the groups mixed jobs into fewer launches than jobs.  Variants: /dma sends
-    every group's inputs to the device by DMA on a copy stream, issued under the running group
-    (option group_dma -1), instead of the kernels pulling them over PCIe; /one_lane runs the
-    groups on the one-lane k_prep_h."""
+    """prio3_helper_prepare_aggregate_batch from 32 threads: 32 jobs of 100-500 reports for 4
+    tasks, each with its own segments (1-4, ids past n_segments included) and accept mask, some
+    tampered, and every fourth job a plain prepare_batch + accumulate in the same groups.  Each
+    job's messages, statuses, per-segment aggregates and counts equal the restatement's.
+    Default: the jobs are queued behind the executor's hold, so the groups mix them into fewer
+    launches than jobs.  /heavy: no hold, and the executor's heavy-load launcher from the first
+    job (prio3_executor_control "heavy" 1) -- its sleep predictor and its issue of the next group
+    behind the running one's prepare kernels, the path the 128-thread load runs on.
+    /one_lane runs the groups on the one-lane k_prep_h."""
     from oracle.oracle import Oracle
     name, _, variant = name.partition("/")
     cfg = CONFIGS[name]
@@ -160,10 +185,8 @@ def test_combined_prepare_aggregate_jobs(name):
     engines = [_engine(cfg, vk) for vk in vks]
     for e in engines:
         e.set_option("timing", 1)
-        if variant.startswith("one_lane"):  # groups on the one-lane k_prep_h, not k_prep_hp
+        if variant == "one_lane":  # groups on the one-lane k_prep_h, not k_prep_hp
             e.set_option("pair_max", 0)
-        if variant.endswith("dma"):  # every group's inputs by DMA (option group_dma -1)
-            e.set_option("group_dma", -1)
         e.timing_reset()
     rng = np.random.default_rng(19)
     jobs = []
@@ -177,12 +200,9 @@ def test_combined_prepare_aggregate_jobs(name):
         seg = rng.integers(0, S + 1, n).astype(np.uint32)  # id S: out of range, excluded
         acc = (rng.random(n) < 0.9).astype(np.uint8)
         jobs.append((t, d, S, seg, acc))
-    start = threading.Barrier(8)
 
     def run(j):
         t, d, S, seg, acc = jobs[j]
-        if j < 8:
-            start.wait()
         args = (d["nonces"], d["public_shares"], d["helper_shares"], d["leader_prep_shares"])
         if j % 4 == 3:
             msgs, status, batch = engines[t].prepare_batch(*args)
@@ -192,8 +212,25 @@ def test_combined_prepare_aggregate_jobs(name):
         return engines[t].prepare_aggregate_batch(*args, segment_ids=seg, accept_mask=acc,
                                                   n_segments=S)
 
-    with ThreadPoolExecutor(8) as ex:
-        got = list(ex.map(run, range(32)))
+    if variant == "heavy":
+        engines[0].executor_control("heavy", 1)
+        try:
+            start = threading.Barrier(8)
+
+            def run8(j):
+                if j < 8:
+                    start.wait()
+                return run(j)
+
+            with ThreadPoolExecutor(8) as ex:
+                got = list(ex.map(run8, range(32)))
+        finally:
+            engines[0].executor_control("heavy", 0)
+    else:
+        with _Held(engines[0], 32) as held, ThreadPoolExecutor(32) as ex:
+            futs = [ex.submit(run, j) for j in range(32)]
+            held.wait()
+            got = [f.result(timeout=120) for f in futs]
     for (t, d, S, seg, acc), (msgs, status, agg, cnt) in zip(jobs, got):
         ref_seg = np.where(seg < S, seg, 0).astype(np.uint32)
         ref_acc = np.where(seg < S, acc, 0).astype(np.uint8)
@@ -205,9 +242,10 @@ def test_combined_prepare_aggregate_jobs(name):
     kern = {"count": ("k_prep_gen",), "hist_256_c16": ("k_prep_h", "k_prep_hp"),
             "sum32": ("k_prep_sum",), "hist_100_c10": ("k_xofd", "k_prep_h")}.get(name, ("k_xofd",))
     launches = sum(e.timing().get(k, (0, 0))[1] for e in engines for k in kern)
-    # fewer launches than jobs where a launch outlasts a Python caller's way into the C ABI
-    # (see test_concurrent_jobs_of_several_tasks_are_coalesced)
-    assert 0 < launches < 32 if name == "hist_256_c16" else 0 < launches <= 32, launches
+    if variant == "heavy":
+        assert 0 < launches <= 32, launches
+    else:
+        assert 0 < launches < 32, launches
 
 
 def test_combined_prepare_aggregate_single_job_and_empty():
@@ -280,3 +318,135 @@ def test_roctx_ranges_on_request(tmp_path):
     r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True,
                        env=dict(os.environ, JANUS_ROCTX="1", PYTHONPATH=root), timeout=240)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_engine_over_two_executors_places_jobs_and_matches():
+    """VERDICT r4 item 1 on the one-GPU box: an engine over the device list [0, 0] has two
+    executors (lanes 0 and 1 of GPU 0) standing in for two GPUs of a node.  Jobs submitted one
+    at a time (equal load) alternate between them; concurrent jobs from 16 threads spread over
+    both by load; every job -- prepare_aggregate, prepare + accumulate, leader prepare_init +
+    prepare_next -- equals the restatement's bytes, whichever member ran it."""
+    from janus_amd import prio3 as J
+    from oracle.oracle import Oracle
+    cfg = CONFIGS["hist_256_c16"]
+    vk = bytes(range(0x60, 0x70))
+    o = Oracle(**cfg)
+    eng = J.HelperEngine(J.Prio3Histogram(256, 16), vk, devices=[0, 0])
+    m0 = eng.members()
+    assert [(m["device"], m["lane"]) for m in m0] == [(0, 0), (0, 1)]
+    rng = np.random.default_rng(23)
+    # sequential: equal load every time, so the members alternate
+    for j in range(6):
+        d = o.gen_reports(vk, 200 + j, seed=700 + j, n_threads=4)
+        msgs, status, agg, cnt = eng.prepare_aggregate_batch(
+            d["nonces"], d["public_shares"], d["helper_shares"], d["leader_prep_shares"])
+        rm, rs, ra, rc = _ref(o, vk, d)
+        np.testing.assert_array_equal(status, rs)
+        np.testing.assert_array_equal(msgs, rm)
+        np.testing.assert_array_equal(agg, ra)
+    m1 = eng.members()
+    assert [m["jobs"] - a["jobs"] for m, a in zip(m1, m0)] == [3, 3], m1
+    assert all(m["exec_groups"] > a["exec_groups"] for m, a in zip(m1, m0)), m1
+    # concurrent: 32 jobs from 16 threads, mixed entry points, every job checked
+    jobs = []
+    for j in range(32):
+        n = int(rng.integers(100, 501))
+        d = o.gen_reports(vk, n, seed=800 + j, n_threads=4)
+        if j % 3 == 0:
+            d = _tamper(o, d, rng)
+        S = int(rng.integers(1, 4))
+        seg = rng.integers(0, S, n).astype(np.uint32)
+        jobs.append((d, S, seg))
+
+    def run(j):
+        d, S, seg = jobs[j]
+        args = (d["nonces"], d["public_shares"], d["helper_shares"], d["leader_prep_shares"])
+        if j % 2:
+            msgs, status, b = eng.prepare_batch(*args)
+            agg, cnt = b.accumulate(seg, None, S)
+            b.free()
+            return msgs, status, agg, cnt
+        return eng.prepare_aggregate_batch(*args, segment_ids=seg, n_segments=S)
+
+    with ThreadPoolExecutor(16) as ex:
+        got = list(ex.map(run, range(32)))
+    for (d, S, seg), (msgs, status, agg, cnt) in zip(jobs, got):
+        rm, rs, ra, rc = _ref(o, vk, d, seg, None, S)
+        np.testing.assert_array_equal(status, rs)
+        np.testing.assert_array_equal(msgs, rm)
+        np.testing.assert_array_equal(agg, ra)
+        np.testing.assert_array_equal(cnt, rc)
+    m2 = eng.members()
+    placed = [m["jobs"] - a["jobs"] for m, a in zip(m2, m1)]
+    assert sum(placed) == 32 and min(placed) > 0, placed
+    # the leader role on the same engine: the batch handle stays with the member that ran it
+    gen = eng.generate_reports_device(300, seed=31, with_leader_inputs=True)
+    d = o.gen_reports(vk, 300, seed=31, n_threads=4)
+    for _ in range(2):
+        ps, lst, lb = eng.leader_prepare_init_batch(d["nonces"], d["public_shares"],
+                                                    gen["leader_input_shares"].cpu().numpy())
+        np.testing.assert_array_equal(ps, d["leader_prep_shares"])
+        rm, rs, ra, rc = _ref(o, vk, d)
+        st = lb.leader_prepare_next(rm, lst)
+        assert (st == 0).all()
+        lagg, lcnt = lb.accumulate()
+        assert int(lcnt[0]) == 300
+        lb.free()
+    eng.close()
+
+
+@pytest.mark.parametrize("name", ["hist_256_c16", "sum32", "count", "sumvec_8x10_c9"])
+def test_concurrent_leader_jobs_are_coalesced(name):
+    """the leader's prepare_init (leader_initialized,
+    aggregation_job_driver.rs:397-415) and prepare_next (leader_continued, :677-691) of 24
+    concurrent 100-500-report jobs of 4 tasks, each queued behind its executor's hold: one
+    prepare_init launch and one prepare_next launch serve them all, and every job's prepare
+    shares, statuses (one tampered prepare message per third job) and aggregate equal the
+    restatement's leader path (orc_leader_batch)."""
+    from janus_amd import prio3 as J
+    from oracle.oracle import Oracle
+    cfg = CONFIGS[name]
+    o = Oracle(**cfg)
+    vks = [bytes([k]) * 16 for k in (0x71, 0x72, 0x73, 0x74)]
+    engines = [_engine(cfg, vk) for vk in vks]
+    rng = np.random.default_rng(41)
+    jobs = []
+    for j in range(24):
+        t = j % 4
+        n = int(rng.integers(100, 501))
+        d = o.gen_reports(vks[t], n, seed=900 + j, n_threads=4)
+        lin = engines[t].generate_reports_device(n, seed=900 + j, with_leader_inputs=True)
+        lin = lin["leader_input_shares"].cpu().numpy()
+        msgs = _ref(o, vks[t], d)[0].copy()
+        if j % 3 == 0 and msgs.shape[1]:
+            msgs[int(rng.integers(0, n)), 0] ^= 1  # the leader's prepare_next rejects it
+        jobs.append((t, d, lin, msgs))
+    g0 = [engines[0].executor_stats(k)["groups"] for k in (J.EXEC_LEADER_INIT, J.EXEC_LEADER_NEXT)]
+    barrier = threading.Barrier(24)
+
+    def run(j):
+        t, d, lin, msgs = jobs[j]
+        ps, st, b = engines[t].leader_prepare_init_batch(d["nonces"], d["public_shares"], lin)
+        barrier.wait()  # every prepare_init is back before the first prepare_next is queued
+        st2 = b.leader_prepare_next(msgs, st)
+        agg, cnt = b.accumulate()
+        b.free()
+        return ps, st, st2, agg, cnt
+
+    with ThreadPoolExecutor(24) as ex, _Held(engines[0], 24, J.EXEC_LEADER_NEXT) as held_next:
+        with _Held(engines[0], 24, J.EXEC_LEADER_INIT) as held_init:
+            futs = [ex.submit(run, j) for j in range(24)]
+            held_init.wait()
+        held_next.wait()
+        got = [f.result(timeout=120) for f in futs]
+    for (t, d, lin, msgs), (ps, st, st2, agg, cnt) in zip(jobs, got):
+        rps, rst, ragg, rcnt = o.leader_batch(vks[t], d["nonces"], d["public_shares"], lin, msgs,
+                                              n_threads=4)
+        np.testing.assert_array_equal(ps, rps)
+        np.testing.assert_array_equal(ps, d["leader_prep_shares"])
+        assert (st == 0).all()
+        np.testing.assert_array_equal(st2, rst)
+        np.testing.assert_array_equal(agg, ragg)
+        np.testing.assert_array_equal(cnt, rcnt)
+    g1 = [engines[0].executor_stats(k)["groups"] for k in (J.EXEC_LEADER_INIT, J.EXEC_LEADER_NEXT)]
+    assert [b - a for a, b in zip(g0, g1)] == [1, 1], (g0, g1)

@@ -488,3 +488,61 @@ def test_gpu_x448_p521_field_ops_match_python(field, op):
           lambda x, y: small * x, lambda x, y: pow(x, P - 2, P)][op]
     bad = [i for i in range(n) if got[i] != fn(a[i], bb[i]) % P]
     assert not bad, f"field {field} op {op}: {len(bad)} wrong, first a={a[bad[0]]:x} b={bb[bad[0]]:x}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("coalesce", [1, 0])
+def test_gpu_concurrent_input_share_jobs_are_coalesced(coalesce):
+    """the helper opens each job's input shares on the job's own rayon worker
+    (aggregator.rs:1847-1890).  24 concurrent jobs of 100-400 reports, each of its own task (its
+    own AAD task ID) under one HPKE keypair, some tampered, queued behind the HPKE executor's hold
+    from 24 threads: one launch opens them all, and every job's helper shares and statuses equal
+    the restatement's.  coalesce 0: the same jobs, each its own launch."""
+    import threading
+    from concurrent.futures import ThreadPoolExecutor
+    from janus_amd import hpke as G
+    rng = np.random.default_rng(77)
+    skR = H.kem_private(rng)
+    jobs = []
+    for j in range(24):
+        n = int(rng.integers(100, 401))
+        d = H.make_batch_fast(n, 48, 32, seed=5000 + j, skR=skR, n_threads=4)
+        if j % 3 == 0:
+            d, _ = _tamper(d, rng)
+        ref = H.open_input_shares(d["skR"], d["pkR"], d["task_id"], d["enc"], d["ct"],
+                                  d["ct_len"], d["report_ids"], d["times"], d["pubs"], 48)
+        jobs.append((d, ref))
+    op = G.HpkeOpener(skR, H.kem_public(skR))
+    op.executor_control("coalesce", coalesce)
+
+    def run(j):
+        d, _ = jobs[j]
+        return op.open_input_shares(d["task_id"], d["enc"], d["ct"], d["ct_len"],
+                                    d["report_ids"], d["times"], d["pubs"], 48)
+
+    g0 = op.executor_stats()
+    if coalesce:
+        op.executor_control("hold", 1)
+        try:
+            with ThreadPoolExecutor(24) as ex:
+                futs = [ex.submit(run, j) for j in range(24)]
+                import time
+                t0 = time.monotonic()
+                while op.executor_stats()["jobs"] - g0["jobs"] < 24:
+                    assert time.monotonic() - t0 < 60, op.executor_stats()
+                    time.sleep(0.005)
+                time.sleep(0.05)
+                op.executor_control("hold", 0)
+                got = [f.result(timeout=120) for f in futs]
+        finally:
+            op.executor_control("hold", 0)
+    else:
+        with ThreadPoolExecutor(8) as ex:
+            got = list(ex.map(run, range(24)))
+    for (d, (ref_sh, ref_st)), (sh, st) in zip(jobs, got):
+        np.testing.assert_array_equal(st, ref_st)
+        np.testing.assert_array_equal(sh, ref_sh)
+    g1 = op.executor_stats()
+    assert g1["groups"] - g0["groups"] == (1 if coalesce else 0), (g0, g1)
+    assert any((ref_st != 0).any() for _, (_, ref_st) in jobs)
+    op.close()

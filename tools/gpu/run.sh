@@ -51,6 +51,13 @@ for step in "$@"; do
     X=(-x); [ "$kind" = testsall ] && X=()
     timeout -k 10 900 python3 -u -m pytest tests -m gpu "${X[@]}" -v --timeout 180 --timeout-method thread "${K[@]}" > "$OUT/tests.log" 2>&1 || { grep -E "FAILED|passed|failed" "$OUT/tests.log" | tail -30; exit 1; }
     tail -1 "$OUT/tests.log" ;;
+  probe)  # the driver's process / queue limits the 8-rank test depends on
+    { for f in hws_max_conc_proc sched_policy hws_gws_support mes cwsr_enable; do
+        echo "amdgpu.$f = $(cat /sys/module/amdgpu/parameters/$f 2>&1)"; done
+      for n in /sys/class/kfd/kfd/topology/nodes/*/properties; do
+        grep -E "^(simd_count|cpu_cores_count|num_cp_queues|num_sdma_engines|num_sdma_xgmi_engines|num_sdma_queues_per_engine|max_waves_per_simd|gfx_target_version|num_xcc)" "$n" | tr '\n' ' '; echo " <- $n"; done
+      ls -l /proc/self/fd 2>&1 | grep -c kfd || true
+    } > "$OUT/probe.txt" 2>&1; cat "$OUT/probe.txt" ;;
   smoke)
     timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$OUT/smoke.log" 2>&1 || { tail -20 "$OUT/smoke.log"; exit 1; }
     tail -1 "$OUT/smoke.log" ;;
