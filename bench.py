@@ -210,6 +210,14 @@ def main():
                          "trip) or prio3_helper_prepare_batch + prio3_accumulate (two)")
     ap.add_argument("--tasks", type=int, default=4,
                     help="--role jobs: tasks (verify keys) of the VDAF instance the jobs rotate over")
+    ap.add_argument("--jobs-role", choices=["helper", "leader", "hpke"], default="helper",
+                    help="--role jobs: the helper's prepare + aggregate per job (default), the "
+                         "leader's prepare_init + prepare_next + aggregate per job, or the "
+                         "helper's HPKE open of each job's input shares")
+    ap.add_argument("--devices", default=None,
+                    help="--role jobs: the engines' GPUs as a comma list (prio3_engine_create_"
+                         "devices; a GPU named twice gets two executors); default: every visible "
+                         "GPU as one device mask (prio3_engine_create_mask)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="N>1: nccl (RCCL over xGMI, the measured path) or gloo with the combine's "
                          "all-gather staged through host memory (lets N ranks share one GPU in a "
@@ -493,19 +501,27 @@ def secondary_lines(args) -> dict:
             out[key] = dict(error=f"{type(ex).__name__}: {ex}")
         torch.cuda.empty_cache()
     # the jobs lines at jobs_main's default size (2 Mi reports at 128 threads): with 2048 jobs the
-    # timed region was ~40 ms and read 27-33 M/s against 38-40 M/s for the same launcher
-    for key, threads, n_jobs in (("secondary_jobs", 128, (1 << 21) // 500),
-                                 ("secondary_jobs_16t", 16, 2048)):
+    # timed region was ~40 ms and read 27-33 M/s against 38-40 M/s for the same launcher; the
+    # leader and HPKE jobs lines at 1 Mi reports
+    cs = args.secondary_cpu_seconds
+    for key, fn in (("secondary_jobs", lambda: jobs_line(128, 500, (1 << 21) // 500, 4,
+                                                         cpu_seconds=cs)),
+                    ("secondary_jobs_16t", lambda: jobs_line(16, 500, 2048, 4, cpu_seconds=cs)),
+                    ("secondary_jobs_leader", lambda: leader_jobs_line(128, 500, 2048, 4,
+                                                                       cpu_seconds=cs)),
+                    ("secondary_jobs_hpke", lambda: hpke_jobs_line(128, 500, 2048, 4,
+                                                                   cpu_seconds=cs))):
         try:
-            j = jobs_line(threads, 500, n_jobs, 4, with_cpu=False)
+            j = fn()
             out[key] = dict(metric=j["metric"], value=j["value"], unit=j["unit"],
                             ms_per_step=j["ms_per_step"], config=j["config"],
-                            coalescing=j["coalescing"],
+                            coalescing=j["coalescing"], placement=j.get("placement"),
                             roofline={k: j["roofline"][k] for k in ("bound", "achieved", "peak",
                                                                     "unit", "frac")},
-                            checks=j["checks"])
+                            checks=j["checks"], cpu_baseline=j["cpu_baseline"])
         except Exception as ex:
             out[key] = dict(error=f"{type(ex).__name__}: {ex}")
+        torch.cuda.empty_cache()
     out["secondary_seconds"] = time.perf_counter() - t0
     return out
 
@@ -557,21 +573,67 @@ def jobs_main(args):
     (janus_amd/libjanus_jobs.so, C++ threads), so Python is not on the timed path.  Reported
     against the PCIe H2D roof and next to the CPU restatement's single-core latency."""
     n_jobs = max(args.tasks, (args.reports if args.reports != 1 << 20 else 1 << 21) // args.job_size)
-    out = jobs_line(args.threads, args.job_size, n_jobs, args.tasks, args.opt,
-                    args.jobs_call == "combined", not args.no_cpu_baseline)
+    devices = None if args.devices is None else [int(x) for x in args.devices.split(",")]
+    if args.jobs_role == "leader":
+        out = leader_jobs_line(args.threads, args.job_size, n_jobs, args.tasks, devices,
+                               not args.no_cpu_baseline, args.cpu_seconds)
+    elif args.jobs_role == "hpke":
+        out = hpke_jobs_line(args.threads, args.job_size, n_jobs, args.tasks,
+                             not args.no_cpu_baseline, args.cpu_seconds)
+    else:
+        out = jobs_line(args.threads, args.job_size, n_jobs, args.tasks, args.opt,
+                        args.jobs_call == "combined", not args.no_cpu_baseline,
+                        devices=devices, cpu_seconds=args.cpu_seconds)
     print(json.dumps(out), flush=True)
 
 
-def jobs_line(T, js, n_jobs, K, opts=(), combined=True, with_cpu=True, check_tasks=None):
+def _job_engines(vdaf, vks, devices):
+    """One engine per task over the node's GPUs: `devices` (a list, prio3_engine_create_devices)
+    or every visible GPU as a device mask (prio3_engine_create_mask)."""
+    if devices is not None:
+        return [J.HelperEngine(vdaf, vk, devices=devices) for vk in vks], devices
+    mask = (1 << max(torch.cuda.device_count(), 1)) - 1
+    return ([J.HelperEngine(vdaf, vk, device_mask=mask) for vk in vks],
+            [d for d in range(32) if mask >> d & 1])
+
+
+def _placement(engines, before=None):
+    """Jobs / reports each member GPU (lane) took over all the line's engines."""
+    tot = None
+    for e in engines:
+        ms = e.members()
+        if tot is None:
+            tot = [dict(device=m["device"], lane=m["lane"], jobs=0, reports=0) for m in ms]
+        for t, m in zip(tot, ms):
+            t["jobs"] += m["jobs"]
+            t["reports"] += m["reports"]
+    if before:
+        for t, b in zip(tot, before):
+            t["jobs"] -= b["jobs"]
+            t["reports"] -= b["reports"]
+    return tot
+
+
+def _job_windows(t, n_jobs, K, js, pool):
+    """The report indices (into the concatenated per-task pools) of task t's jobs, and the job
+    numbers, as the native drivers choose them (jobs_driver.cpp)."""
+    jl = list(range(t, n_jobs, K))
+    r0s = [t * pool + ((j // K) * js) % (pool - js + 1) for j in jl]
+    return jl, np.concatenate([np.arange(r, r + js) for r in r0s])
+
+
+def jobs_line(T, js, n_jobs, K, opts=(), combined=True, with_cpu=True, check_tasks=None,
+              devices=None, cpu_seconds=10.0):
     """jobs_main's measurement (see there); check_tasks: check the jobs of only the first
-    check_tasks tasks against the restatement (None: all)."""
+    check_tasks tasks against the restatement (None: all).  The engines span `devices` (or
+    every visible GPU): each job runs whole on the least-loaded one."""
     import ctypes as C
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
     n_jobs = max(K, n_jobs)
     pool = 1 << 16
     vks = [bytes([0x51 + t]) * 16 for t in range(K)]
-    engines = [J.HelperEngine(J.Prio3Histogram(256, 16), vk, device=0) for vk in vks]
+    engines, devs = _job_engines(J.Prio3Histogram(256, 16), vks, devices)
     for kv in opts:
         k, v = kv.split("=")
         for e in engines:
@@ -604,7 +666,9 @@ def jobs_line(T, js, n_jobs, K, opts=(), combined=True, with_cpu=True, check_tas
     for e in engines:  # launches counted, no timing events on the production launch path
         e.set_option("timing", 2)
         e.timing_reset()
+    pl0 = _placement(engines)
     dt = run(n_jobs)
+    placement = _placement(engines, pl0)
     if dt < 0:
         raise RuntimeError("janus_jobs_run: a C-ABI call failed")
     # the prepare launches: the fused XOF + query (k_prep_h, or k_prep_hp on lane pairs for small
@@ -620,9 +684,7 @@ def jobs_line(T, js, n_jobs, K, opts=(), combined=True, with_cpu=True, check_tas
     jobs_ok = True
     statuses_ok = True
     for t in range(K if check_tasks is None else min(K, check_tasks)):
-        jl = list(range(t, n_jobs, K))
-        r0s = [t * pool + ((j // K) * js) % (pool - js + 1) for j in jl]
-        idx = np.concatenate([np.arange(r, r + js) for r in r0s])
+        jl, idx = _job_windows(t, n_jobs, K, js, pool)
         seg = np.repeat(np.arange(len(jl), dtype=np.uint32), js)
         _, rst, ragg, rcnt = o.helper_batch(
             vks[t], host["nonces"][idx], host["public_shares"][idx], host["helper_shares"][idx],
@@ -637,7 +699,7 @@ def jobs_line(T, js, n_jobs, K, opts=(), combined=True, with_cpu=True, check_tas
     cores = cpu_threads()
     cpu = None
     if with_cpu:
-        m = min(4000 * cores, len(host["nonces"]))
+        m = min(max(500 * cores, int(400 * cores * cpu_seconds)), len(host["nonces"]))
         t0 = time.perf_counter()
         o.helper_batch(vks[0], host["nonces"][:m], host["public_shares"][:m],
                        host["helper_shares"][:m], host["leader_prep_shares"][:m],
@@ -661,7 +723,8 @@ def jobs_line(T, js, n_jobs, K, opts=(), combined=True, with_cpu=True, check_tas
                data=f"synthetic: {K} x {pool} on-device client reports copied to host memory",
                config=dict(workload="Prio3Histogram length=256 chunk_length=16 helper prepare + "
                                     "accumulate per aggregation job, host buffers (PCIe included)",
-                           job_size=js, jobs=n_jobs, threads=T, tasks=K),
+                           job_size=js, jobs=n_jobs, threads=T, tasks=K, devices=devs),
+               placement=placement,
                pcie=dict(h2d_bytes_per_report=per_report_h2d,
                          h2d_GBps=value * per_report_h2d / 1e9,
                          roof_reports_per_s=63e9 / per_report_h2d,
@@ -685,6 +748,211 @@ def jobs_line(T, js, n_jobs, K, opts=(), combined=True, with_cpu=True, check_tas
                            check_seconds=t_chk),
                cpu_baseline=cpu,
                speedup_vs_cpu=(value / cpu["value"]) if cpu else None)
+
+
+def leader_jobs_line(T, js, n_jobs, K, devices=None, with_cpu=True, cpu_seconds=10.0):
+    """the leader's production call shape.  T host threads, each a worker of
+    Janus's aggregation job driver stepping whole jobs (aggregation_job_driver.rs:397-415,
+    677-691, one spawn per job at :449-462): prio3_leader_prepare_init_batch on the job's explicit
+    leader input shares, prio3_leader_prepare_next_batch on the helper's prepare messages,
+    prio3_accumulate, prio3_batch_free -- host buffers, PCIe included, coalesced by the leader
+    executors.  Every job's prepare shares, statuses, aggregate and count are checked against
+    the restatement's leader path (orc_leader_batch_seg)."""
+    import ctypes as C
+    torch.cuda.set_device(0)
+    n_jobs = max(K, n_jobs)
+    pool = 1 << 15
+    vks = [bytes([0x61 + t]) * 16 for t in range(K)]
+    engines, devs = _job_engines(J.Prio3Histogram(256, 16), vks, devices)
+    sz = engines[0].sz
+    cols = {k: [] for k in ("nonces", "public_shares", "leader_input_shares", "msgs")}
+    for t, e in enumerate(engines):
+        p = e.generate_reports_device(pool, seed=0x4A414E5553000005 + t, with_leader_inputs=True)
+        msgs = torch.empty((pool, sz.prep_msg_len), dtype=torch.uint8, device=p["nonces"].device)
+        st = torch.empty(pool, dtype=torch.uint8, device=p["nonces"].device)
+        # the helper's prepare messages: the engine's own device helper prepare of the pool
+        e.prepare_device(p["nonces"], p["public_shares"], p["helper_shares"],
+                         p["leader_prep_shares"], msgs, st)
+        torch.cuda.synchronize()
+        assert int((st != 0).sum().item()) == 0
+        for k in ("nonces", "public_shares", "leader_input_shares"):
+            cols[k].append(p[k].cpu().numpy())
+        cols["msgs"].append(msgs.cpu().numpy())
+        del p, msgs, st
+    host = {k: np.ascontiguousarray(np.concatenate(v)) for k, v in cols.items()}
+    lib = C.CDLL(os.path.join(ROOT, "janus_amd", "libjanus_jobs.so"))
+    lib.janus_jobs_run_leader.restype = C.c_double
+    vp = C.c_void_p
+    lib.janus_jobs_run_leader.argtypes = [C.POINTER(vp), C.c_int, vp, C.c_int, C.c_int, C.c_int,
+                                          C.c_uint32, vp, vp, vp, vp, vp, vp, vp, vp]
+    eng_arr = (vp * K)(*[e.handle.value for e in engines])
+    ps = np.zeros((n_jobs * js, sz.prep_share_len), np.uint8)
+    status = np.zeros(n_jobs * js, np.uint8)
+    counts = np.zeros(n_jobs, np.uint64)
+    agg = np.zeros((n_jobs, sz.agg_share_len), np.uint8)
+    P = lambda a: a.ctypes.data_as(vp)
+
+    def run(jobs):
+        status[:] = 0xFF
+        return lib.janus_jobs_run_leader(eng_arr, K, C.cast(C.pointer(sz), vp), T, jobs, js, pool,
+                                         P(host["nonces"]), P(host["public_shares"]),
+                                         P(host["leader_input_shares"]), P(host["msgs"]), P(ps),
+                                         P(status), P(counts), P(agg))
+
+    run(max(K, min(n_jobs, 8 * T)))  # warmup
+    g0 = [engines[0].executor_stats(k)["groups"] for k in (J.EXEC_LEADER_INIT,
+                                                          J.EXEC_LEADER_NEXT)]
+    pl0 = _placement(engines)
+    dt = run(n_jobs)
+    if dt < 0:
+        raise RuntimeError("janus_jobs_run_leader: a C-ABI call failed")
+    placement = _placement(engines, pl0)
+    g1 = [engines[0].executor_stats(k)["groups"] for k in (J.EXEC_LEADER_INIT,
+                                                          J.EXEC_LEADER_NEXT)]
+    value = n_jobs * js / dt
+    from oracle.oracle import Oracle
+    o = Oracle("histogram", length=256, chunk_length=16)
+    t_chk = time.perf_counter()
+    jobs_ok = statuses_ok = ps_ok = True
+    for t in range(K):
+        jl, idx = _job_windows(t, n_jobs, K, js, pool)
+        seg = np.repeat(np.arange(len(jl), dtype=np.uint32), js)
+        rps, rst, ragg, rcnt = o.leader_batch(
+            vks[t], host["nonces"][idx], host["public_shares"][idx],
+            host["leader_input_shares"][idx], host["msgs"][idx], n_threads=cpu_threads(),
+            job_size=js, segment_ids=seg, n_segments=len(jl))
+        rows = np.concatenate([np.arange(j * js, (j + 1) * js) for j in jl])
+        ps_ok &= bool(np.array_equal(ps[rows], rps))
+        statuses_ok &= bool(np.array_equal(status[rows], rst))
+        jobs_ok &= bool(np.array_equal(agg[jl], ragg) and
+                        np.array_equal(counts[jl], rcnt.astype(np.uint64)))
+    t_chk = time.perf_counter() - t_chk
+    cores = cpu_threads()
+    cpu = None
+    if with_cpu:
+        m = min(max(500 * cores, int(300 * cores * cpu_seconds)), pool)
+        t0 = time.perf_counter()
+        o.leader_batch(vks[0], host["nonces"][:m], host["public_shares"][:m],
+                       host["leader_input_shares"][:m], host["msgs"][:m], n_threads=cores,
+                       job_size=js)
+        dta = time.perf_counter() - t0
+        cpu = dict(value=m / dta, unit="reports/s", cores=cores, kind="port",
+                   sample=f"{m} reports through the restatement's leader path (prepare_init "
+                          f"agg_id 0 + prepare_next + aggregate), jobs of {js}, {cores} threads, "
+                          f"{dta:.1f}s", cpu_model=cpu_model())
+    h2d = 16 + sz.public_share_len + sz.leader_input_share_len + sz.prep_msg_len
+    return dict(metric="leader reports prepared (init + next) + aggregated/sec through the "
+                       "host-buffer C ABI (Prio3Histogram len=256, concurrent aggregation jobs)",
+                value=value, unit="reports/s", n_gpus=len(set(devs)), steps=1, warmup=1,
+                ms_per_step=dt * 1e3, higher_is_better=True, scaling="weak", vs_baseline=None,
+                dtype="u32 limbs (Field128 mod-p integer arithmetic)",
+                data=f"synthetic: {K} x {pool} on-device client reports (leader input shares) "
+                     "and the helper's prepare messages, copied to host memory",
+                config=dict(workload="Prio3Histogram length=256 chunk_length=16 leader "
+                                     "prepare_init + prepare_next + accumulate per aggregation "
+                                     "job, host buffers (PCIe included)",
+                            job_size=js, jobs=n_jobs, threads=T, tasks=K, devices=devs),
+                placement=placement,
+                roofline=dict(bound="pcie", achieved=value * h2d / 1e9, peak=63.0,
+                              unit="GB/s host->device (leader input share, nonce, public share, "
+                                   "prepare message per report)",
+                              frac=value * h2d / 63e9, h2d_bytes_per_report=h2d, traffic=None),
+                coalescing=dict(init_launches=g1[0] - g0[0], next_launches=g1[1] - g0[1],
+                                jobs=n_jobs),
+                checks=dict(all_finished=bool((status == 0).all()),
+                            counts_ok=bool((counts == js).all()), prep_shares_match_cpu=ps_ok,
+                            statuses_match_cpu=statuses_ok, every_job_matches_cpu=jobs_ok,
+                            jobs_checked=n_jobs, check_seconds=t_chk),
+                cpu_baseline=cpu, speedup_vs_cpu=(value / cpu["value"]) if cpu else None)
+
+
+def hpke_jobs_line(T, js, n_jobs, K, with_cpu=True, cpu_seconds=10.0):
+    """the helper's input-share open at the production call shape -- T host
+    threads each opening whole jobs' input shares (aggregator.rs:1847-1890) through
+    janus_hpke_open_input_shares (host buffers, PCIe included), K tasks (their own AAD task IDs)
+    under one X25519 keypair, coalesced by the GPU's HPKE executor.  Every job's helper shares and
+    statuses are checked against the restatement (OpenSSL)."""
+    import ctypes as C
+    from janus_amd import hpke as G
+    from oracle import hpke as H
+    torch.cuda.set_device(0)
+    n_jobs = max(K, n_jobs)
+    pool = 1 << 15
+    rng = np.random.default_rng(0x4A414E55)
+    skR = H.kem_private(rng)
+    parts = [H.make_batch_fast(pool, 48, 32, seed=0x4A41 + t, skR=skR, n_threads=cpu_threads())
+             for t in range(K)]
+    host = {k: np.ascontiguousarray(np.concatenate([p[k] for p in parts]))
+            for k in ("enc", "ct", "ct_len", "report_ids", "times", "pubs")}
+    task_ids = np.frombuffer(b"".join(p["task_id"] for p in parts), np.uint8).copy()
+    stride = host["ct"].shape[1]
+    op = G.HpkeOpener(skR, H.kem_public(skR), device=0)
+    lib = C.CDLL(os.path.join(ROOT, "janus_amd", "libjanus_jobs.so"))
+    lib.janus_jobs_run_hpke.restype = C.c_double
+    vp, u32 = C.c_void_p, C.c_uint32
+    lib.janus_jobs_run_hpke.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, u32, u32, vp,
+                                        vp, vp, u32, vp, vp, vp, u32, u32, vp, vp]
+    shares = np.zeros((n_jobs * js, 48), np.uint8)
+    status = np.zeros(n_jobs * js, np.uint8)
+    P = lambda a: a.ctypes.data_as(vp)
+
+    def run(jobs):
+        status[:] = 0xFF
+        return lib.janus_jobs_run_hpke(op.handle, K, P(task_ids), T, jobs, js, pool, 32,
+                                       P(host["enc"]), P(host["ct"]), P(host["ct_len"]), stride,
+                                       P(host["report_ids"]), P(host["times"]), P(host["pubs"]),
+                                       32, 48, P(shares), P(status))
+
+    run(max(K, min(n_jobs, 8 * T)))  # warmup
+    g0 = op.executor_stats()["groups"]
+    dt = run(n_jobs)
+    if dt < 0:
+        raise RuntimeError("janus_jobs_run_hpke: a C-ABI call failed")
+    launches = op.executor_stats()["groups"] - g0
+    value = n_jobs * js / dt
+    t_chk = time.perf_counter()
+    ok = True
+    for t in range(K):
+        d = parts[t]
+        rsh, rst = H.open_input_shares(skR, d["pkR"], d["task_id"], d["enc"], d["ct"],
+                                       d["ct_len"], d["report_ids"], d["times"], d["pubs"], 48,
+                                       n_threads=cpu_threads())
+        jl, idx = _job_windows(t, n_jobs, K, js, pool)
+        rows = np.concatenate([np.arange(j * js, (j + 1) * js) for j in jl])
+        ok &= bool(np.array_equal(shares[rows], rsh[idx - t * pool]) and
+                   np.array_equal(status[rows], rst[idx - t * pool]))
+    t_chk = time.perf_counter() - t_chk
+    cores = cpu_threads()
+    cpu = None
+    if with_cpu:
+        m = min(max(1000 * cores, int(1500 * cores * cpu_seconds)), pool)
+        d = parts[0]
+        t0 = time.perf_counter()
+        H.open_input_shares(skR, d["pkR"], d["task_id"], d["enc"][:m], d["ct"][:m],
+                            d["ct_len"][:m], d["report_ids"][:m], d["times"][:m], d["pubs"][:m],
+                            48, n_threads=cores)
+        dta = time.perf_counter() - t0
+        cpu = dict(value=m / dta, unit="reports/s", cores=cores, kind="port",
+                   sample=f"{m} sealed input shares, OpenSSL 3.0 X25519 / HKDF-SHA256 / "
+                          f"AES-128-GCM, {cores} threads, {dta:.1f}s", cpu_model=cpu_model())
+    h2d = 32 + stride + 4 + 16 + 8 + 32
+    roofline = model_roofline("hpke_x25519_aead1", RM.hpke_model("x25519", 1), n_jobs * js, 1, dt)
+    roofline["pcie"] = dict(h2d_bytes_per_report=h2d, frac=value * h2d / 63e9)
+    return dict(metric="helper input shares HPKE-opened+decoded/sec through the host-buffer C ABI "
+                       "(X25519-HKDF-SHA256, AES-128-GCM, concurrent aggregation jobs)",
+                value=value, unit="reports/s", n_gpus=1, steps=1, warmup=1, ms_per_step=dt * 1e3,
+                higher_is_better=True, scaling="weak", vs_baseline=None,
+                dtype="u32 limbs (GF(2^255 - 19), GF(2^128), bytes)",
+                data=f"synthetic: {K} tasks x {pool} input shares sealed by the oracle (OpenSSL, "
+                     "seeded), host memory",
+                config=dict(workload="DAP helper input share open per aggregation job: X25519 "
+                                     "decap + HPKE key schedule + AES-128-GCM + PlaintextInputShare "
+                                     "decode, Prio3Histogram(256,16) shares, host buffers",
+                            job_size=js, jobs=n_jobs, threads=T, tasks=K),
+                roofline=roofline, coalescing=dict(launches=launches, jobs=n_jobs),
+                checks=dict(all_opened=bool((status == 0).all()), every_job_matches_cpu=ok,
+                            jobs_checked=n_jobs, check_seconds=t_chk),
+                cpu_baseline=cpu, speedup_vs_cpu=(value / cpu["value"]) if cpu else None)
 
 
 def leader_main(args):

@@ -3,7 +3,10 @@
 // (/root/reference/aggregator/src/aggregator.rs:2100-2123) of `job_size` reports
 // (binaries/aggregation_job_creator.rs:63-64, default 100-500), calling the C ABI exactly as the
 // FFI crate of INTEGRATION.md would: prio3_helper_prepare_batch (host buffers, PCIe included),
-// then prio3_accumulate into the job's batch aggregation, then prio3_batch_free.
+// then prio3_accumulate into the job's batch aggregation, then prio3_batch_free.  The leader and
+// HPKE forms do the same for the leader's prepare_init / prepare_next
+// (aggregation_job_driver.rs:397-415, 677-691, spawned per job at :449-462) and the helper's
+// input-share open (aggregator.rs:1847-1890).
 // Not part of the engine: a separate library (libjanus_jobs.so) that links libjanus_prio3.so.
 #include <atomic>
 #include <chrono>
@@ -12,7 +15,30 @@
 #include <thread>
 #include <vector>
 
+#include "../../include/janus_hpke.h"
 #include "../../include/janus_prio3.h"
+
+namespace {
+// `threads` workers taking jobs 0..jobs-1 in order; returns elapsed seconds (< 0: a call failed)
+template <class F>
+double run_pool(int threads, int jobs, F job) {
+  std::atomic<int> next{0};
+  std::atomic<int> failed{0};
+  auto worker = [&]() {
+    for (;;) {
+      const int j = next.fetch_add(1);
+      if (j >= jobs) return;
+      if (!job(j)) failed = 1;
+    }
+  };
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<std::thread> th;
+  for (int i = 0; i < threads; i++) th.emplace_back(worker);
+  for (auto& t : th) t.join();
+  const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return failed ? -1.0 : dt;
+}
+}  // namespace
 
 extern "C" {
 
@@ -69,6 +95,62 @@ double janus_jobs_run(prio3_engine** engines, int n_engines, const prio3_sizes_t
   for (auto& t : th) t.join();
   const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return failed ? -1.0 : dt;
+}
+
+
+// The leader's side of the same jobs: per job prio3_leader_prepare_init_batch on the explicit
+// leader input shares lin[..][leader_input_share_len], prio3_leader_prepare_next_batch on the
+// helper's prepare messages msgs[..][prep_msg_len], prio3_accumulate, prio3_batch_free.  Job j's
+// reports are chosen as in janus_jobs_run; ps_out[jobs * job_size][prep_share_len].
+double janus_jobs_run_leader(prio3_engine** engines, int n_engines, const prio3_sizes_t* szp,
+                             int threads, int jobs, int job_size, uint32_t pool,
+                             const uint8_t* nonces, const uint8_t* pub, const uint8_t* lin,
+                             const uint8_t* msgs, uint8_t* ps_out, uint8_t* status_out,
+                             uint64_t* counts_out, uint8_t* agg_out) {
+  const prio3_sizes_t sz = *szp;
+  const uint32_t span = pool - (uint32_t)job_size + 1;
+  return run_pool(threads, jobs, [&](int j) {
+    const uint32_t t = (uint32_t)(j % n_engines);
+    const uint32_t r0 = t * pool + (uint32_t)(((uint64_t)(j / n_engines) * job_size) % span);
+    const size_t o = (size_t)j * job_size;
+    prio3_batch* b = nullptr;
+    int rc = prio3_leader_prepare_init_batch(
+        engines[t], (uint32_t)job_size, nonces + 16 * (size_t)r0,
+        sz.public_share_len ? pub + (size_t)sz.public_share_len * r0 : nullptr,
+        lin + (size_t)sz.leader_input_share_len * r0, ps_out + (size_t)sz.prep_share_len * o,
+        status_out + o, &b);
+    if (rc == PRIO3_OK)
+      rc = prio3_leader_prepare_next_batch(
+          b, sz.prep_msg_len ? msgs + (size_t)sz.prep_msg_len * r0 : nullptr, status_out + o);
+    uint64_t cnt = 0;
+    if (rc == PRIO3_OK)
+      rc = prio3_accumulate(b, nullptr, nullptr, 1, agg_out + (size_t)sz.agg_share_len * j, &cnt);
+    prio3_batch_free(b);
+    counts_out[j] = cnt;
+    return rc == PRIO3_OK;
+  });
+}
+
+// The helper's input-share open per job: janus_hpke_open_input_shares over job j's reports of
+// task t = j % n_tasks (task_ids[t][32]; per-task report pools as above, per-report rows of
+// nenc / ct_stride / 4 / 16 / 8 / pub_len bytes).  shares_out[jobs * job_size][share_len].
+double janus_jobs_run_hpke(janus_hpke_opener* op, int n_tasks, const uint8_t* task_ids,
+                           int threads, int jobs, int job_size, uint32_t pool, uint32_t nenc,
+                           const uint8_t* enc, const uint8_t* ct, const uint32_t* ct_len,
+                           uint32_t ct_stride, const uint8_t* ids, const uint64_t* times,
+                           const uint8_t* pubs, uint32_t pub_len, uint32_t share_len,
+                           uint8_t* shares_out, uint8_t* status_out) {
+  const uint32_t span = pool - (uint32_t)job_size + 1;
+  return run_pool(threads, jobs, [&](int j) {
+    const uint32_t t = (uint32_t)(j % n_tasks);
+    const size_t r0 = t * (size_t)pool + (((uint64_t)(j / n_tasks) * job_size) % span);
+    const size_t o = (size_t)j * job_size;
+    return janus_hpke_open_input_shares(
+               op, (uint32_t)job_size, task_ids + 32 * (size_t)t, enc + nenc * r0,
+               ct + (size_t)ct_stride * r0, ct_len + r0, ct_stride, ids + 16 * r0, times + r0,
+               pub_len ? pubs + pub_len * r0 : nullptr, pub_len, share_len,
+               0, shares_out + (size_t)share_len * o, status_out + o) == JANUS_HPKE_SUCCESS;
+  });
 }
 
 }  // extern "C"

@@ -60,6 +60,9 @@ def lib():
                                        P(C.c_uint64), C.c_int, C.c_int]
         L.orc_leader_batch.argtypes = [P(OrcParams), u8p, C.c_uint32, u8p, u8p, u8p, u8p, u8p,
                                        u8p, u8p, P(C.c_uint64), C.c_int, C.c_int]
+        L.orc_leader_batch_seg.argtypes = [P(OrcParams), u8p, C.c_uint32, u8p, u8p, u8p, u8p,
+                                           P(C.c_uint32), C.c_uint32, u8p, u8p, u8p,
+                                           P(C.c_uint64), C.c_int, C.c_int]
         L.orc_agg_merge.argtypes = [P(OrcParams), u8p, u8p]
         L.orc_gen_reports.argtypes = [P(OrcParams), u8p, C.c_uint32, C.c_uint64, C.c_int,
                                       u8p, u8p, u8p, u8p, P(C.c_uint64), u8p]
@@ -184,22 +187,24 @@ class Oracle:
         return msgs[:, :p.prep_msg_len], status, agg, cnt
 
     def leader_batch(self, vk: bytes, nonces, public_shares, leader_shares, prep_msgs,
-                     n_threads=1, job_size=500):
-        """Batched leader prepare_init (agg_id 0) + prepare_next + aggregate (one segment):
-        returns (prep_shares, status, agg, count).  Status 1 = non-canonical leader share
-        element (the engine reports it as 6, InputShareDecode), 4 = VdafPrepareNext."""
+                     n_threads=1, job_size=500, segment_ids=None, n_segments=1):
+        """Batched leader prepare_init (agg_id 0) + prepare_next + aggregate per segment:
+        returns (prep_shares, status, agg [S, out], count [S]).  Status 1 = non-canonical leader
+        share element (the engine reports it as 6, InputShareDecode), 4 = VdafPrepareNext."""
         p = self.p
         n = nonces.shape[0]
         ps = np.zeros((n, p.prep_share_len), np.uint8)
         status = np.zeros(n, np.uint8)
-        agg = np.zeros((1, p.out_share_bytes), np.uint8)
-        cnt = np.zeros(1, np.uint64)
+        agg = np.zeros((n_segments, p.out_share_bytes), np.uint8)
+        cnt = np.zeros(n_segments, np.uint64)
         pub = None if p.public_share_len == 0 else np.ascontiguousarray(public_shares)
         msgs = None if p.prep_msg_len == 0 else np.ascontiguousarray(prep_msgs)
-        lib().orc_leader_batch(C.byref(p), _buf(vk), n, _ptr(np.ascontiguousarray(nonces)),
-                               _ptr(pub), _ptr(np.ascontiguousarray(leader_shares)), _ptr(msgs),
-                               _ptr(ps), _ptr(status), _ptr(agg), _ptr(cnt, C.c_uint64),
-                               n_threads, job_size)
+        seg = None if segment_ids is None else np.ascontiguousarray(segment_ids, np.uint32)
+        lib().orc_leader_batch_seg(C.byref(p), _buf(vk), n, _ptr(np.ascontiguousarray(nonces)),
+                                   _ptr(pub), _ptr(np.ascontiguousarray(leader_shares)),
+                                   _ptr(msgs), _ptr(seg, C.c_uint32), n_segments, _ptr(ps),
+                                   _ptr(status), _ptr(agg), _ptr(cnt, C.c_uint64), n_threads,
+                                   job_size)
         return ps, status, agg, cnt
 
     def gen_reports(self, vk: bytes, n: int, seed: int = 1, n_threads: int = 8):

@@ -1358,12 +1358,29 @@ typedef struct {
   uint32_t n;
   const uint8_t *nonces, *publics, *leaders, *msgs;
   uint8_t *prep_out, *status;
+  const uint32_t* seg;  /* segment of each report (NULL: all segment 0) */
+  uint32_t n_segments;
   int job_size;
   atomic_uint next_job;
   pthread_mutex_t mu;
-  fe* agg;
-  uint64_t* count;
+  fe* agg;          /* [n_segments][out_len] */
+  uint64_t* count;  /* [n_segments] */
 } leader_ctx;
+
+/* adds a worker's partial of segment s into the batch's (under the mutex) and clears it */
+static void leader_flush(leader_ctx* c, const fld* F, uint32_t s, fe* lagg, uint64_t* lcnt) {
+  const orc_params* p = c->p;
+  if (*lcnt == 0) return;
+  pthread_mutex_lock(&c->mu);
+  for (uint32_t k = 0; k < p->out_len; k++) {
+    fe* g = c->agg + (size_t)s * p->out_len + k;
+    *g = f_add(F, *g, lagg[k]);
+    lagg[k] = 0;
+  }
+  c->count[s] += *lcnt;
+  pthread_mutex_unlock(&c->mu);
+  *lcnt = 0;
+}
 
 static void* leader_worker(void* arg) {
   leader_ctx* c = (leader_ctx*)arg;
@@ -1376,6 +1393,7 @@ static void* leader_worker(void* arg) {
   fe* out = (fe*)malloc(sizeof(fe) * p->out_len);
   fe* lagg = (fe*)calloc(p->out_len, sizeof(fe));
   uint64_t lcnt = 0;
+  uint32_t lseg = 0;  /* the segment lagg / lcnt belong to */
   fe jr[64], qr[64];
   uint8_t part[32], corrected[32];
   for (;;) {
@@ -1385,6 +1403,7 @@ static void* leader_worker(void* arg) {
     uint64_t hi = lo + c->job_size;
     if (hi > c->n) hi = c->n;
     for (uint64_t i = lo; i < hi; i++) {
+      const uint32_t sg = c->seg ? c->seg[i] : 0;
       const uint8_t* pub = c->publics ? c->publics + i * p->public_share_len : NULL;
       uint8_t* o = c->prep_out + i * p->prep_share_len;
       int rc = prepare_init_core(p, &F, c->vk, 0, c->nonces + i * 16, pub,
@@ -1399,16 +1418,17 @@ static void* leader_worker(void* arg) {
         memset(o, 0, p->prep_share_len);
       }
       c->status[i] = (uint8_t)rc;
-      if (rc != ORC_OK) continue;
+      if (rc != ORC_OK || sg >= c->n_segments) continue;
+      if (sg != lseg) {
+        leader_flush(c, &F, lseg, lagg, &lcnt);
+        lseg = sg;
+      }
       truncate_share(p, &F, meas, out);
       for (uint32_t k = 0; k < p->out_len; k++) lagg[k] = f_add(&F, lagg[k], out[k]);
       lcnt++;
     }
   }
-  pthread_mutex_lock(&c->mu);
-  for (uint32_t k = 0; k < p->out_len; k++) c->agg[k] = f_add(&F, c->agg[k], lagg[k]);
-  *c->count += lcnt;
-  pthread_mutex_unlock(&c->mu);
+  leader_flush(c, &F, lseg, lagg, &lcnt);
   free(meas);
   free(proofs);
   free(ver);
@@ -1421,9 +1441,23 @@ int orc_leader_batch(const orc_params* p, const uint8_t* vk, uint32_t n, const u
                      const uint8_t* public_shares, const uint8_t* leader_shares,
                      const uint8_t* prep_msgs, uint8_t* prep_shares_out, uint8_t* status_out,
                      uint8_t* agg_out, uint64_t* count_out, int n_threads, int job_size) {
+  return orc_leader_batch_seg(p, vk, n, nonces, public_shares, leader_shares, prep_msgs, NULL, 1,
+                              prep_shares_out, status_out, agg_out, count_out, n_threads,
+                              job_size);
+}
+
+int orc_leader_batch_seg(const orc_params* p, const uint8_t* vk, uint32_t n,
+                         const uint8_t* nonces, const uint8_t* public_shares,
+                         const uint8_t* leader_shares, const uint8_t* prep_msgs,
+                         const uint32_t* segment_ids, uint32_t n_segments,
+                         uint8_t* prep_shares_out, uint8_t* status_out, uint8_t* agg_out,
+                         uint64_t* count_out, int n_threads, int job_size) {
   if (n_threads < 1) n_threads = 1;
   if (job_size < 1) job_size = 500;
+  if (n_segments < 1) n_segments = 1;
   leader_ctx c;
+  c.seg = segment_ids;
+  c.n_segments = n_segments;
   c.p = p;
   c.vk = vk;
   c.n = n;
@@ -1436,14 +1470,15 @@ int orc_leader_batch(const orc_params* p, const uint8_t* vk, uint32_t n, const u
   c.job_size = job_size;
   atomic_init(&c.next_job, 0);
   pthread_mutex_init(&c.mu, NULL);
-  c.agg = (fe*)calloc(p->out_len, sizeof(fe));
+  c.agg = (fe*)calloc((size_t)n_segments * p->out_len, sizeof(fe));
   c.count = count_out;
-  *count_out = 0;
+  memset(count_out, 0, 8 * (size_t)n_segments);
   pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * n_threads);
   for (int t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, leader_worker, &c);
   for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
   fld F = mkfld(p);
-  for (uint32_t k = 0; k < p->out_len; k++) enc_fe(&F, c.agg[k], agg_out + (size_t)k * p->es);
+  for (size_t k = 0; k < (size_t)n_segments * p->out_len; k++)
+    enc_fe(&F, c.agg[k], agg_out + k * p->es);
   free(th);
   free(c.agg);
   pthread_mutex_destroy(&c.mu);

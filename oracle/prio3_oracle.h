@@ -120,6 +120,14 @@ int orc_leader_batch(const orc_params* p, const uint8_t* vk, uint32_t n, const u
                      const uint8_t* public_shares, const uint8_t* leader_shares,
                      const uint8_t* prep_msgs, uint8_t* prep_shares_out, uint8_t* status_out,
                      uint8_t* agg_out, uint64_t* count_out, int n_threads, int job_size);
+/* orc_leader_batch with per-report segment ids (NULL: segment 0; ids >= n_segments are
+ * prepared but aggregated nowhere): agg_out[n_segments][out_len * es], count_out[n_segments]. */
+int orc_leader_batch_seg(const orc_params* p, const uint8_t* vk, uint32_t n,
+                         const uint8_t* nonces, const uint8_t* public_shares,
+                         const uint8_t* leader_shares, const uint8_t* prep_msgs,
+                         const uint32_t* segment_ids, uint32_t n_segments,
+                         uint8_t* prep_shares_out, uint8_t* status_out, uint8_t* agg_out,
+                         uint64_t* count_out, int n_threads, int job_size);
 
 /* Deterministic synthetic reports (client shard + leader prepare_init), multithreaded.
  * meas_out: n x (SumVec: length, else 1) u64; leader_out_shares: n x out_len*es (nullable). */
