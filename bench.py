@@ -215,7 +215,7 @@ def main():
                          "leader's prepare_init + prepare_next + aggregate per job, or the "
                          "helper's HPKE open of each job's input shares")
     ap.add_argument("--devices", default=None,
-                    help="--role jobs: the engines' GPUs as a comma list (prio3_engine_create_"
+                    help="--role jobs: the engines' GPUs as a comma (or +) list (prio3_engine_create_"
                          "devices; a GPU named twice gets two executors); default: every visible "
                          "GPU as one device mask (prio3_engine_create_mask)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
@@ -573,7 +573,7 @@ def jobs_main(args):
     (janus_amd/libjanus_jobs.so, C++ threads), so Python is not on the timed path.  Reported
     against the PCIe H2D roof and next to the CPU restatement's single-core latency."""
     n_jobs = max(args.tasks, (args.reports if args.reports != 1 << 20 else 1 << 21) // args.job_size)
-    devices = None if args.devices is None else [int(x) for x in args.devices.split(",")]
+    devices = None if args.devices is None else [int(x) for x in args.devices.replace("+", ",").split(",")]
     if args.jobs_role == "leader":
         out = leader_jobs_line(args.threads, args.job_size, n_jobs, args.tasks, devices,
                                not args.no_cpu_baseline, args.cpu_seconds)

@@ -1650,12 +1650,12 @@ int hpke_group_issue(const HpkeJob& pj, const HpkeLayout& L, const uint8_t* stg,
   *st_out = nullptr;
   *slab_out = nullptr;
   HCHK(hipSetDevice(o->device));
-  hipStream_t st = ws_stream_get(o->device);
+  hipStream_t st = ws_exec_stream_get(o->device);
   if (!st) return JANUS_HPKE_EDEVICE;
   int rc = JANUS_HPKE_SUCCESS;
   Slab* sl = ws_acquire(o->device, L.bytes, st, &rc);
   if (!sl) {
-    ws_stream_put(o->device, st);
+    ws_exec_stream_put(o->device, st);
     return rc;
   }
   uint8_t* b = sl->base;
@@ -1698,7 +1698,7 @@ int hpke_group_issue(const HpkeJob& pj, const HpkeLayout& L, const uint8_t* stg,
   if (rc != JANUS_HPKE_SUCCESS) {
     (void)hipStreamSynchronize(st);
     ws_release(sl, st);
-    ws_stream_put(o->device, st);
+    ws_exec_stream_put(o->device, st);
     return rc;
   }
   *st_out = st;

@@ -3469,7 +3469,7 @@ int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr) {
   gr->lead = lead;
   gr->jobs = g.jobs;
   HIPCHK(hipSetDevice(lead->device));
-  hipStream_t st = ws_stream_get(lead->device);
+  hipStream_t st = ws_exec_stream_get(lead->device);
   if (!st) return PRIO3_EDEVICE;
   const bool mp = lead->dp.kind == PRIO3_SUMVEC_F64_MP;
   // aggregating jobs: the group's reports are accumulated per job segment in this launch (the
@@ -3483,7 +3483,7 @@ int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr) {
                           (fuse ? (unsigned)RUN_FUSED : 0u),
                       agg ? g.nseg : 0, g.n_keys, st, &rc);
   if (!R) {
-    ws_stream_put(lead->device, st);
+    ws_exec_stream_put(lead->device, st);
     return rc;
   }
   IoLayout L;
@@ -3493,7 +3493,7 @@ int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr) {
     run_release(R, st, true);
     if (gr->prep) (void)hipEventDestroy(gr->prep);
     *gr = GroupRun();
-    ws_stream_put(lead->device, st);
+    ws_exec_stream_put(lead->device, st);
     return code;
   };
   const uint8_t* hd = g.stg_dev;
@@ -3580,13 +3580,13 @@ int engine_group_finish(GroupRun* gr, Run** run_out) {
   if (q != hipSuccess) {
     (void)hipGetLastError();
     run_release(gr->R, gr->st, true);
-    ws_stream_put(dev, gr->st);
+    ws_exec_stream_put(dev, gr->st);
     return PRIO3_EDEVICE;
   }
   if (gr->lead->timing) collect_times(gr->lead, false);
   gr->R->refs.store(gr->jobs);
   *run_out = gr->R;
-  ws_stream_put(dev, gr->st);
+  ws_exec_stream_put(dev, gr->st);
   return PRIO3_OK;
 }
 
@@ -3705,12 +3705,12 @@ int engine_leader_issue(prio3_engine* lead, const LeaderLayout& L, uint8_t* stg_
   gr->lead = lead;
   gr->jobs = jobs;
   HIPCHK(hipSetDevice(lead->device));
-  hipStream_t st = ws_stream_get(lead->device);
+  hipStream_t st = ws_exec_stream_get(lead->device);
   if (!st) return PRIO3_EDEVICE;
   int rc = PRIO3_OK;
   Run* R = run_create(lead, n, RUN_SCRATCH | RUN_IO | RUN_LINPUT, 0, 0, st, &rc);
   if (!R) {
-    ws_stream_put(lead->device, st);
+    ws_exec_stream_put(lead->device, st);
     return rc;
   }
   auto fail = [&](int code) {
@@ -3718,7 +3718,7 @@ int engine_leader_issue(prio3_engine* lead, const LeaderLayout& L, uint8_t* stg_
     run_release(R, st, true);
     if (gr->prep) (void)hipEventDestroy(gr->prep);
     *gr = GroupRun();
-    ws_stream_put(lead->device, st);
+    ws_exec_stream_put(lead->device, st);
     return code;
   };
   if (hipMemcpyAsync(R->linput, stg_dev + L.off[2], L.len[2] * n, hipMemcpyDefault, st) !=
@@ -3779,14 +3779,14 @@ int engine_lnext_issue(int device, uint32_t es, uint8_t* stg_dev, const LNextLay
                        uint32_t n_jobs, uint32_t max_n, hipStream_t* st_out) {
   *st_out = nullptr;
   HIPCHK(hipSetDevice(device));
-  hipStream_t st = ws_stream_get(device);
+  hipStream_t st = ws_exec_stream_get(device);
   if (!st) return PRIO3_EDEVICE;
   const int rc = launch_leader_next_multi(es, (const LNextDesc*)(stg_dev + L.desc_off),
                                           stg_dev + L.msg_off, stg_dev + L.status_off, n_jobs,
                                           max_n, st);
   if (rc != PRIO3_OK) {
     (void)hipStreamSynchronize(st);
-    ws_stream_put(device, st);
+    ws_exec_stream_put(device, st);
     return rc;
   }
   *st_out = st;

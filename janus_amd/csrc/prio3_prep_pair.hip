@@ -43,9 +43,19 @@ DEV T sel(bool c, const T& a, const T& b) { return F::sel(c, a, b); }
 
 // ---- the query of one report on its lane pair (h = 0 even, 1 odd); both lanes active --------
 // The one-lane form is query_h_body<2, 32> (prio3_engine.hip); this splits its work in halves.
+// PAIR_GS: wires per sweep of the wire loop (each sweep re-reads the 16 beta_k and L_k); 2 keeps
+// four lazy 128-bit MAC accumulators (21 VGPRs each) live.  PAIR_DIRECT_BETA: the beta_k are
+// formed and stored as the Lagrange phases produce their L values (r^C taken first), instead of
+// keeping this lane's eight L values in registers through the Horner / range pass.
+#ifndef PAIR_GS
+#define PAIR_GS 2
+#endif
+#ifndef PAIR_DIRECT_BETA
+#define PAIR_DIRECT_BETA 0
+#endif
 DEV void query_pair(const DevParams& p, const InPtrs& in, const Scratch& sc, const OutPtrs& out,
                     const uint32_t r, const uint32_t h) {
-  constexpr int PP = 32, GLEN = 2 * (PP - 1) + 1, GS = 2;
+  constexpr int PP = 32, GLEN = 2 * (PP - 1) + 1, GS = PAIR_GS;
   const size_t ld = p.ld;
   const uint32_t A = p.arity, C = p.chunk, M = p.meas_len, K = p.calls;
   uint8_t status = PRIO3_STATUS_FINISHED;
@@ -62,8 +72,22 @@ DEV void query_pair(const DevParams& p, const InPtrs& in, const Scratch& sc, con
   const T a = F::add(F::one(), t16), b = F::sub(F::one(), t16);
   const T c = F::mul(t8, a), wd = F::mul(F::mul(t8, b), F::from_words(p.tw128[8]));  // w4 = w32^8
   T L0 = F::zero(), sumL = F::zero();
+  const T r0 = ldf<F>(sc.jr, 0, ld, r);
+#if PAIR_DIRECT_BETA
+  // r^C, r^(2C), r^(4C): beta_k = L_(k+1) r^(C k) leaves each phase straight to scratch
+  T rC = F::one();
+  {
+    T sq = r0;
+    for (uint32_t e = C; e; e >>= 1) {
+      if (e & 1) rC = F::mul(rC, sq);
+      if (e > 1) sq = F::mul(sq, sq);
+    }
+  }
+  const T rC2 = F::mul(rC, rC), rC4 = F::mul(rC2, rC2);
+#else
   // the betas this lane can form from its own L values: k with (31 - k) & 3 in {2h, 2h + 1}
   T Lmine[8];
+#endif
 #pragma unroll
   for (int i = 0; i < 2; i++) {
     const T g = i == 0 ? sel(h, F::sub(a, c), F::add(a, c)) : sel(h, F::sub(b, wd), F::add(b, wd));
@@ -87,9 +111,22 @@ DEV void query_pair(const DevParams& p, const InPtrs& in, const Scratch& sc, con
         F::store(sc.Lbuf, (size_t)cc * ld + r, x[k]);
         sumL = F::add(sumL, x[k]);
       }
+#if !PAIR_DIRECT_BETA
       // c = k' + 1 for beta_k' (k' = 31 - idx): this lane owns the betas of its L values
       if (k >= 4) Lmine[2 * (k - 4) + i] = x[k];  // idx >= 16: c <= 16
+#endif
     }
+#if PAIR_DIRECT_BETA
+    // beta_k' for idx = 4 kx + 2h + i >= 16 (kx = 7 .. 4): k' = 31 - idx = 3 - 2h - i + 4 (7 - kx),
+    // r^(C k') from r^(C (3 - 2h - i)) by r^(4C) steps
+    T rk = i == 0 ? sel(h, rC, F::mul(rC2, rC)) : sel(h, F::one(), rC2);
+#pragma unroll
+    for (int kx = 7; kx >= 4; kx--) {
+      const uint32_t k = 31u - (4u * kx + 2u * h + (uint32_t)i);
+      if (k < K) F::store(sc.beta, (size_t)k * ld + r, F::mul(x[kx], rk));
+      if (kx > 4) rk = F::mul(rk, rC4);
+    }
+#endif
   }
   L0 = sel(h, pair_x(L0), L0);  // c = 0 is idx 0: the even lane's phase 0
   sumL = F::add(sumL, pair_x(sumL));
@@ -131,8 +168,8 @@ DEV void query_pair(const DevParams& p, const InPtrs& in, const Scratch& sc, con
     const T hi = sel(h, other, pt), lo = sel(h, pt, other);
     pt = F::add(F::mul(hi, t32), lo);
   }
+#if !PAIR_DIRECT_BETA
   // 3. beta_k = L_(k+1) r^(C k): this lane's eight k (k & 3 = 3 - (2h + i)), from its registers
-  const T r0 = ldf<F>(sc.jr, 0, ld, r);
   T rC = F::one();
   {
     T sq = r0;
@@ -156,6 +193,7 @@ DEV void query_pair(const DevParams& p, const InPtrs& in, const Scratch& sc, con
       rk0 = F::mul(rk0, rC4);
     }
   }
+#endif
   // the wire loop reads every beta_k and L_(k+1): the partner's stores must have landed
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // 4. the wires: lane h owns j in [8h, 8h + 8): four sweeps of two wires
@@ -267,8 +305,13 @@ DEV void query_pair(const DevParams& p, const InPtrs& in, const Scratch& sc, con
 
 // ---- the kernel: XOF (k_xof_pair's lane split, plus the fused accumulate and the leader-share
 //      pull of the executor groups), then query_pair on the same lanes ------------------------
+// PAIR_OCC: waves per SIMD the compiler must fit (0: its own choice, 188 VGPRs = 2 waves)
+#ifndef PAIR_OCC
+#define PAIR_OCC 0
+#endif
 template <bool FUSE, bool PULL>
-__global__ __launch_bounds__(256) void k_prep_hp(DevParams p, InPtrs in, Scratch sc, OutPtrs out) {
+__global__ __launch_bounds__(256, PAIR_OCC) void k_prep_hp(DevParams p, InPtrs in, Scratch sc,
+                                                           OutPtrs out) {
   const uint32_t tid = threadIdx.x, h = tid & 1u, lane = tid & 63u;
   const uint32_t r = blockIdx.x * 128 + (tid >> 1);
   const bool live = r < p.n;

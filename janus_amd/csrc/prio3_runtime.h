@@ -44,6 +44,15 @@ bool trace_enabled();
 // ---- stream pool ---------------------------------------------------------------------------
 hipStream_t ws_stream_get(int device);  // nullptr on failure
 void ws_stream_put(int device, hipStream_t s);
+// Launch streams of the executors' groups: the first EXEC_QUEUE_STREAMS per GPU are CU-masked
+// (all CUs), and the HIP runtime gives such a stream a hardware queue of its own, so groups in
+// flight together run concurrently.  Plain pooled streams share the process's GPU_MAX_HW_QUEUES
+// queues, and two groups' streams on one queue ran back to back (r05e: every launch on 'Queue 1',
+// the 16-thread jobs line at 10.2-10.5 instead of 15.4-15.6 M reports/s).  Past that count the
+// plain pool; put takes either kind back.
+constexpr int EXEC_QUEUE_STREAMS = 4;
+hipStream_t ws_exec_stream_get(int device);
+void ws_exec_stream_put(int device, hipStream_t s);
 
 // ---- coalescing executor -------------------------------------------------------------------
 // One executor per (GPU, lane): lane 0 is the GPU's executor; a multi-GPU engine created over a

@@ -210,6 +210,76 @@ void ws_stream_put(int device, hipStream_t s) {
   sp.free.push_back(s);
 }
 
+namespace {
+struct QueuePool {
+  std::mutex mu;
+  std::vector<hipStream_t> own, free;  // the CU-masked streams made so far / idle ones
+};
+QueuePool g_queues[MAX_DEVICES];
+// the CU-masked streams are destroyed at exit before the HIP runtime's own teardown (an exit
+// handler registered after the runtime's runs first): under rocprofv3 a process that left them
+// to the runtime crashed in __cxa_finalize (r05f)
+void destroy_queues() {
+  for (int d = 0; d < MAX_DEVICES; d++) {
+    QueuePool& qp = g_queues[d];
+    std::lock_guard<std::mutex> lk(qp.mu);
+    if (qp.own.empty()) continue;
+    (void)hipSetDevice(d);
+    for (hipStream_t s : qp.own) {
+      (void)hipStreamSynchronize(s);
+      (void)hipStreamDestroy(s);
+    }
+    qp.own.clear();
+    qp.free.clear();
+  }
+}
+}  // namespace
+
+hipStream_t ws_exec_stream_get(int device) {
+  if (device < 0 || device >= MAX_DEVICES) return nullptr;
+  QueuePool& qp = g_queues[device];
+  {
+    std::lock_guard<std::mutex> lk(qp.mu);
+    if (!qp.free.empty()) {
+      hipStream_t s = qp.free.back();
+      qp.free.pop_back();
+      return s;
+    }
+    if ((int)qp.own.size() < EXEC_QUEUE_STREAMS) {
+      int cus = 0;
+      hipStream_t s = nullptr;
+      if (hipSetDevice(device) == hipSuccess &&
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) ==
+              hipSuccess &&
+          cus > 0) {
+        std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xffffffffu);
+        if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
+        if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
+          static const int reg = std::atexit(destroy_queues);
+          (void)reg;
+          qp.own.push_back(s);
+          return s;
+        }
+      }
+      (void)hipGetLastError();
+    }
+  }
+  return ws_stream_get(device);
+}
+
+void ws_exec_stream_put(int device, hipStream_t s) {
+  if (!s) return;
+  QueuePool& qp = g_queues[device];
+  {
+    std::lock_guard<std::mutex> lk(qp.mu);
+    if (std::find(qp.own.begin(), qp.own.end(), s) != qp.own.end()) {
+      qp.free.push_back(s);
+      return;
+    }
+  }
+  ws_stream_put(device, s);
+}
+
 // ---- executors -----------------------------------------------------------------------------
 // A generic group-commit executor, one per (GPU, lane, work kind).  Callers reserve room in the
 // open group of their key and stage their inputs themselves (in parallel); the executor's one
@@ -879,7 +949,7 @@ struct LNextPolicy {
   static bool done(const Handle& h) { return hipStreamQuery(h.st) != hipErrorNotReady; }
   static int finish(Handle* h) {
     const hipError_t q = hipStreamSynchronize(h->st);
-    ws_stream_put(h->device, h->st);
+    ws_exec_stream_put(h->device, h->st);
     return q == hipSuccess ? PRIO3_OK : PRIO3_EDEVICE;
   }
   static void unstage(State& s, Staging& g, Job* j) {
@@ -956,7 +1026,7 @@ struct HpkePolicy {
   static int finish(Handle* h) {
     const hipError_t q = hipStreamSynchronize(h->st);
     ws_release(h->slab, h->st);
-    ws_stream_put(h->device, h->st);
+    ws_exec_stream_put(h->device, h->st);
     return q == hipSuccess ? PRIO3_OK : PRIO3_EDEVICE;
   }
   static void unstage(State& s, Staging& g, Job* j) {

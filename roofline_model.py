@@ -226,12 +226,17 @@ def hpke_model(kem: str, aead: int, pt_len: int = 48 + 8 + 32 + 16, aad_len: int
         compress = 21
     elif kem == "p521":
         M, S, A = PRIM["p521_mul"], PRIM["p521_sqr"], PRIM["p521_add"]
-        # ecdh_a3.h: a = -3 Jacobian formulas, fixed signed w = 4 window over the host-recoded
-        # key (131 digits), table 1P..8P by doublings and additions, affine output
-        dbl = 4 * M + 4 * S + 13 * A
-        add = 12 * M + 4 * S + 12 * A
-        inv = 520 * S + 13 * M
-        dh = 3 * M + 2 * S + 4 * A + 7 * add + 131 * (4 * dbl + add) + inv + M + S
+        # ecdh_a3.h, counted from its code (the r4 model charged a 12M + 4S
+        # general addition where the code runs the 8M + 3S mixed one): a = -3 Jacobian
+        # doublings (dbl-2001-b), mixed additions (madd-2007-bl), the odd multiples P..15P by 5
+        # doublings and 7 mixed additions made affine by Montgomery's trick, a fixed signed w = 4
+        # window over the 131 host-recoded digits, affine output
+        dbl = 4 * M + 4 * S + 13 * A           # three small multiples counted as two adds each
+        madd = 8 * M + 3 * S + 12 * A
+        inv = 520 * S + 13 * M                 # p - 2 addition chain
+        check = 3 * M + 2 * S + 4 * A          # y^2 = x^3 - 3x + b
+        table = 5 * dbl + 7 * madd + inv + 39 * M + 7 * S
+        dh = check + table + 129 * (4 * dbl + madd) + 5 * dbl + madd + inv + M + S
         compress = 23  # kem_context = enc || pkR is 266 bytes
     else:
         M, S, A = PRIM["p256_mul"], PRIM["p256_sqr"], PRIM["p256_add"]
