@@ -1645,12 +1645,12 @@ void hpke_layout(const HpkeJob* j, uint32_t cap, HpkeLayout* L) {
 // The group's per-field inputs to a device mirror (pinned-memory DMA), the open kernel (its AAD
 // task IDs from the group's table), the helper shares and statuses back into the staging.
 int hpke_group_issue(const HpkeJob& pj, const HpkeLayout& L, const uint8_t* stg, uint8_t* out,
-                     uint32_t n, hipStream_t* st_out, Slab** slab_out) {
+                     uint32_t n, hipStream_t* st_out, Slab** slab_out, bool own_queue) {
   janus_hpke_opener* o = pj.o;
   *st_out = nullptr;
   *slab_out = nullptr;
   HCHK(hipSetDevice(o->device));
-  hipStream_t st = ws_exec_stream_get(o->device);
+  hipStream_t st = own_queue ? ws_exec_stream_get(o->device) : ws_stream_get(o->device);
   if (!st) return JANUS_HPKE_EDEVICE;
   int rc = JANUS_HPKE_SUCCESS;
   Slab* sl = ws_acquire(o->device, L.bytes, st, &rc);

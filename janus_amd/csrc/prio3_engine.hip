@@ -3464,12 +3464,12 @@ static int fused_finish(prio3_engine* e, Run* R, const uint8_t* d_status, const 
 // (profiles/r03/r03e_jobs128_*.json: 21.5 M reports/s); SDMA copies of each group issued under the
 // previous group's compute (r04 option group_dma) measured 19.5-30.8 against 32-40 M/s for the
 // pull and were removed in r05.
-int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr) {
+int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr, bool own_queue) {
   *gr = GroupRun();
   gr->lead = lead;
   gr->jobs = g.jobs;
   HIPCHK(hipSetDevice(lead->device));
-  hipStream_t st = ws_exec_stream_get(lead->device);
+  hipStream_t st = own_queue ? ws_exec_stream_get(lead->device) : ws_stream_get(lead->device);
   if (!st) return PRIO3_EDEVICE;
   const bool mp = lead->dp.kind == PRIO3_SUMVEC_F64_MP;
   // aggregating jobs: the group's reports are accumulated per job segment in this launch (the
@@ -3699,13 +3699,13 @@ void engine_leader_layout(const prio3_engine* e, uint32_t cap, LeaderLayout* L) 
 // one DMA, the kernels read the nonces, public shares and verify-key slots from the mapped
 // staging, and one copy launch writes the prepare shares and statuses back into it.
 int engine_leader_issue(prio3_engine* lead, const LeaderLayout& L, uint8_t* stg_dev, uint32_t n,
-                        uint32_t n_keys, int jobs, GroupRun* gr) {
+                        uint32_t n_keys, int jobs, GroupRun* gr, bool own_queue) {
   (void)n_keys;
   *gr = GroupRun();
   gr->lead = lead;
   gr->jobs = jobs;
   HIPCHK(hipSetDevice(lead->device));
-  hipStream_t st = ws_exec_stream_get(lead->device);
+  hipStream_t st = own_queue ? ws_exec_stream_get(lead->device) : ws_stream_get(lead->device);
   if (!st) return PRIO3_EDEVICE;
   int rc = PRIO3_OK;
   Run* R = run_create(lead, n, RUN_SCRATCH | RUN_IO | RUN_LINPUT, 0, 0, st, &rc);
@@ -3776,10 +3776,10 @@ extern "C" int launch_leader_next_multi(uint32_t es, const LNextDesc* d_desc, co
                                         hipStream_t st);
 
 int engine_lnext_issue(int device, uint32_t es, uint8_t* stg_dev, const LNextLayout& L,
-                       uint32_t n_jobs, uint32_t max_n, hipStream_t* st_out) {
+                       uint32_t n_jobs, uint32_t max_n, hipStream_t* st_out, bool own_queue) {
   *st_out = nullptr;
   HIPCHK(hipSetDevice(device));
-  hipStream_t st = ws_exec_stream_get(device);
+  hipStream_t st = own_queue ? ws_exec_stream_get(device) : ws_stream_get(device);
   if (!st) return PRIO3_EDEVICE;
   const int rc = launch_leader_next_multi(es, (const LNextDesc*)(stg_dev + L.desc_off),
                                           stg_dev + L.msg_off, stg_dev + L.status_off, n_jobs,

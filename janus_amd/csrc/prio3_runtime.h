@@ -44,13 +44,16 @@ bool trace_enabled();
 // ---- stream pool ---------------------------------------------------------------------------
 hipStream_t ws_stream_get(int device);  // nullptr on failure
 void ws_stream_put(int device, hipStream_t s);
-// Launch streams of the executors' groups: the first EXEC_QUEUE_STREAMS per GPU are CU-masked
-// (all CUs), and the HIP runtime gives such a stream a hardware queue of its own, so groups in
-// flight together run concurrently.  Plain pooled streams share the process's GPU_MAX_HW_QUEUES
-// queues, and two groups' streams on one queue ran back to back (r05e: every launch on 'Queue 1',
-// the 16-thread jobs line at 10.2-10.5 instead of 15.4-15.6 M reports/s).  Past that count the
-// plain pool; put takes either kind back.
-constexpr int EXEC_QUEUE_STREAMS = 4;
+// Launch streams of the light-load pipeline's groups: the first EXEC_QUEUE_STREAMS per GPU are
+// CU-masked (all CUs), and the HIP runtime gives such a stream a hardware queue of its own, so
+// groups in flight together run concurrently.  Plain pooled streams share the process's
+// GPU_MAX_HW_QUEUES queues, and two groups' streams on one queue ran back to back (r05e: every
+// launch on 'Queue 1', the 16-thread jobs line at 10.2-10.5 instead of 15.4-15.6 M reports/s).
+// Past that count the plain pool; put takes either kind back.
+#ifndef JANUS_EXEC_QUEUE_STREAMS  // A/B builds (tools/build_variant.sh): 0 = the plain pool only
+#define JANUS_EXEC_QUEUE_STREAMS 4
+#endif
+constexpr int EXEC_QUEUE_STREAMS = JANUS_EXEC_QUEUE_STREAMS;
 hipStream_t ws_exec_stream_get(int device);
 void ws_exec_stream_put(int device, hipStream_t s);
 
@@ -141,7 +144,8 @@ struct GroupRun {
   hipEvent_t prep = nullptr;  // recorded after the prepare kernels
   int jobs = 0;
 };
-int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr);
+// own_queue: the group's stream from ws_exec_stream_get (else the plain pool)
+int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr, bool own_queue);
 bool engine_group_prepared(const GroupRun& gr);  // the prepare kernels are done
 bool engine_group_done(const GroupRun& gr);      // everything is done (non-blocking)
 int engine_group_finish(GroupRun* gr, Run** run_out);
@@ -205,7 +209,7 @@ struct LeaderLayout {
 void engine_leader_layout(const prio3_engine* e, uint32_t cap, LeaderLayout* L);
 // one DMA of the staged inputs into the run, the leader kernels, the outputs back into the staging
 int engine_leader_issue(prio3_engine* lead, const LeaderLayout& L, uint8_t* stg_dev, uint32_t n,
-                        uint32_t n_keys, int jobs, GroupRun* gr);
+                        uint32_t n_keys, int jobs, GroupRun* gr, bool own_queue);
 int exec_leader(LeaderJob* job);
 
 // ---- coalesced leader prepare_next (prio3_leader_prepare_next_batch of concurrent jobs) -------
@@ -238,7 +242,7 @@ uint32_t engine_lnext_key(const LNextJob* j);
 void engine_lnext_stage(LNextJob* j, uint8_t* stg, const LNextLayout& L);
 // launches the group's kernel on a pooled stream of `device` (reads and writes the staging)
 int engine_lnext_issue(int device, uint32_t es, uint8_t* stg_dev, const LNextLayout& L,
-                       uint32_t n_jobs, uint32_t max_n, hipStream_t* st_out);
+                       uint32_t n_jobs, uint32_t max_n, hipStream_t* st_out, bool own_queue);
 int exec_leader_next(LNextJob* job);
 
 // ---- coalesced HPKE open of helper input shares (janus_hpke_open_input_shares) -----------
@@ -274,6 +278,6 @@ uint64_t hpke_group_key(const HpkeJob* j);
 void hpke_layout(const HpkeJob* j, uint32_t cap, HpkeLayout* L);
 // the group's inputs to a device mirror (one DMA per field), the open kernel, outputs back
 int hpke_group_issue(const HpkeJob& proto, const HpkeLayout& L, const uint8_t* stg, uint8_t* out,
-                     uint32_t n, hipStream_t* st_out, Slab** slab_out);
+                     uint32_t n, hipStream_t* st_out, Slab** slab_out, bool own_queue);
 int exec_hpke(HpkeJob* job);
 

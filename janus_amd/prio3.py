@@ -129,7 +129,10 @@ def load_library() -> C.CDLL:
         import torch  # noqa: F401
     except ImportError:
         pass
-    L = C.CDLL(LIB_PATH)
+    # RTLD_GLOBAL: the native jobs harness (libjanus_jobs.so, linked against libjanus_prio3.so)
+    # then binds to this same copy, also when JANUS_PRIO3_LIB selects an A/B build -- one engine
+    # library (one set of executors) per process
+    L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
     P, u8p, vp = C.POINTER, C.POINTER(C.c_uint8), C.c_void_p
     L.prio3_sizes.argtypes = [P(Prio3Params), P(Prio3Sizes)]
     L.prio3_engine_create.argtypes = [P(Prio3Params), u8p, C.c_int, P(vp)]
