@@ -246,6 +246,17 @@ def test_config_sumvec_eight_ranks_gloo_one_gpu():
     ranks = min(8, limit - holders)
     assert ranks >= 2, f"{holders} processes already hold the GPU (limit {limit})"
     per_rank = -(-1_000_000 // ranks)
+    # the ranks need the GPU's memory (C3's 128 KB measurement shares: ~25 GB per 125k-report
+    # rank): this process's idle scratch slabs go back first -- after test_fpvec the pool keeps
+    # the last FPVec run's slab (hundreds of GB) for the next call (r05k: the ranks ran out of
+    # memory with 0.7 GB free)
+    if holders:
+        import torch
+        from janus_amd import prio3 as J
+        J.trim_device_pool(0)
+        torch.cuda.empty_cache()
+        free, total = torch.cuda.mem_get_info(0)
+        assert free > ranks * (28 << 30), f"{free / 2**30:.0f} of {total / 2**30:.0f} GiB free"
     import signal
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
