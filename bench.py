@@ -214,6 +214,10 @@ def main():
                     help="--role jobs: the helper's prepare + aggregate per job (default), the "
                          "leader's prepare_init + prepare_next + aggregate per job, or the "
                          "helper's HPKE open of each job's input shares")
+    ap.add_argument("--exec-heavy", type=int, default=0,
+                    help="--role jobs: the executors' light/heavy switch in reports inside them "
+                         "(prio3_executor_control / janus_hpke_executor_control \"heavy\"; 0: the "
+                         "default 32768), for A/B runs")
     ap.add_argument("--devices", default=None,
                     help="--role jobs: the engines' GPUs as a comma (or +) list (prio3_engine_create_"
                          "devices; a GPU named twice gets two executors); default: every visible "
@@ -576,14 +580,14 @@ def jobs_main(args):
     devices = None if args.devices is None else [int(x) for x in args.devices.replace("+", ",").split(",")]
     if args.jobs_role == "leader":
         out = leader_jobs_line(args.threads, args.job_size, n_jobs, args.tasks, devices,
-                               not args.no_cpu_baseline, args.cpu_seconds)
+                               not args.no_cpu_baseline, args.cpu_seconds, args.exec_heavy)
     elif args.jobs_role == "hpke":
         out = hpke_jobs_line(args.threads, args.job_size, n_jobs, args.tasks,
-                             not args.no_cpu_baseline, args.cpu_seconds)
+                             not args.no_cpu_baseline, args.cpu_seconds, args.exec_heavy)
     else:
         out = jobs_line(args.threads, args.job_size, n_jobs, args.tasks, args.opt,
                         args.jobs_call == "combined", not args.no_cpu_baseline,
-                        devices=devices, cpu_seconds=args.cpu_seconds)
+                        devices=devices, cpu_seconds=args.cpu_seconds, heavy=args.exec_heavy)
     print(json.dumps(out), flush=True)
 
 
@@ -623,7 +627,7 @@ def _job_windows(t, n_jobs, K, js, pool):
 
 
 def jobs_line(T, js, n_jobs, K, opts=(), combined=True, with_cpu=True, check_tasks=None,
-              devices=None, cpu_seconds=10.0):
+              devices=None, cpu_seconds=10.0, heavy=0):
     """jobs_main's measurement (see there); check_tasks: check the jobs of only the first
     check_tasks tasks against the restatement (None: all).  The engines span `devices` (or
     every visible GPU): each job runs whole on the least-loaded one."""
@@ -634,6 +638,7 @@ def jobs_line(T, js, n_jobs, K, opts=(), combined=True, with_cpu=True, check_tas
     pool = 1 << 16
     vks = [bytes([0x51 + t]) * 16 for t in range(K)]
     engines, devs = _job_engines(J.Prio3Histogram(256, 16), vks, devices)
+    engines[0].executor_control("heavy", heavy)  # the executors are process-wide: 0 resets
     for kv in opts:
         k, v = kv.split("=")
         for e in engines:
@@ -750,7 +755,7 @@ def jobs_line(T, js, n_jobs, K, opts=(), combined=True, with_cpu=True, check_tas
                speedup_vs_cpu=(value / cpu["value"]) if cpu else None)
 
 
-def leader_jobs_line(T, js, n_jobs, K, devices=None, with_cpu=True, cpu_seconds=10.0):
+def leader_jobs_line(T, js, n_jobs, K, devices=None, with_cpu=True, cpu_seconds=10.0, heavy=0):
     """the leader's production call shape.  T host threads, each a worker of
     Janus's aggregation job driver stepping whole jobs (aggregation_job_driver.rs:397-415,
     677-691, one spawn per job at :449-462): prio3_leader_prepare_init_batch on the job's explicit
@@ -764,6 +769,7 @@ def leader_jobs_line(T, js, n_jobs, K, devices=None, with_cpu=True, cpu_seconds=
     pool = 1 << 15
     vks = [bytes([0x61 + t]) * 16 for t in range(K)]
     engines, devs = _job_engines(J.Prio3Histogram(256, 16), vks, devices)
+    engines[0].executor_control("heavy", heavy)
     sz = engines[0].sz
     cols = {k: [] for k in ("nonces", "public_shares", "leader_input_shares", "msgs")}
     for t, e in enumerate(engines):
@@ -866,7 +872,7 @@ def leader_jobs_line(T, js, n_jobs, K, devices=None, with_cpu=True, cpu_seconds=
                 cpu_baseline=cpu, speedup_vs_cpu=(value / cpu["value"]) if cpu else None)
 
 
-def hpke_jobs_line(T, js, n_jobs, K, with_cpu=True, cpu_seconds=10.0):
+def hpke_jobs_line(T, js, n_jobs, K, with_cpu=True, cpu_seconds=10.0, heavy=0):
     """the helper's input-share open at the production call shape -- T host
     threads each opening whole jobs' input shares (aggregator.rs:1847-1890) through
     janus_hpke_open_input_shares (host buffers, PCIe included), K tasks (their own AAD task IDs)
@@ -887,6 +893,7 @@ def hpke_jobs_line(T, js, n_jobs, K, with_cpu=True, cpu_seconds=10.0):
     task_ids = np.frombuffer(b"".join(p["task_id"] for p in parts), np.uint8).copy()
     stride = host["ct"].shape[1]
     op = G.HpkeOpener(skR, H.kem_public(skR), device=0)
+    op.executor_control("heavy", heavy)
     lib = C.CDLL(os.path.join(ROOT, "janus_amd", "libjanus_jobs.so"))
     lib.janus_jobs_run_hpke.restype = C.c_double
     vp, u32 = C.c_void_p, C.c_uint32

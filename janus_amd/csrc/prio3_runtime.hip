@@ -385,8 +385,8 @@ struct Exec {
   std::deque<Group*> order;  // groups not yet taken by the launcher, oldest first
   bool started = false;
   // under mu:
-  bool hold = false;                  // exec_control "hold": take no group
-  uint64_t heavy_at = HEAVY_DEFAULT;  // exec_control "heavy"
+  bool hold = false;                     // exec_control "hold": take no group
+  uint64_t heavy_at = P::heavy_default();  // exec_control "heavy"
   ExecStats stats;
 
   void finish_locked(Group* g, int rc) {
@@ -652,7 +652,7 @@ struct Exec {
     if (!strcmp(key, "hold")) {
       hold = value != 0;
     } else if (!strcmp(key, "heavy")) {
-      heavy_at = value > 0 ? (uint64_t)value : HEAVY_DEFAULT;
+      heavy_at = value > 0 ? (uint64_t)value : P::heavy_default();
     } else {
       return PRIO3_EINVAL;
     }
@@ -693,6 +693,7 @@ void stream_copy(uint8_t* dst, const uint8_t* src, size_t n) {
 // ---- prepare groups ----
 struct PrepPolicy {
   typedef ExecJob Job;
+  static uint64_t heavy_default() { return HEAVY_DEFAULT; }
   struct State {
     prio3_engine* lead = nullptr;
     std::vector<const prio3_engine*> keys;  // verify-key table, slot = index
@@ -811,6 +812,7 @@ struct PrepPolicy {
 // ---- accumulate groups ----
 struct AccPolicy {
   typedef AccJob Job;
+  static uint64_t heavy_default() { return HEAVY_DEFAULT; }
   static constexpr uint32_t MAX_JOBS = 1024, MAX_REPS = 1u << 17;
   static constexpr size_t MAX_OUT = (size_t)32 << 20;
   struct State {
@@ -854,6 +856,7 @@ struct AccPolicy {
 // ---- leader prepare_init groups ----
 struct LeaderPolicy {
   typedef LeaderJob Job;
+  static uint64_t heavy_default() { return HEAVY_DEFAULT; }
   struct State {
     prio3_engine* lead = nullptr;
     std::vector<const prio3_engine*> keys;  // verify-key table, slot = index
@@ -920,6 +923,7 @@ struct LeaderPolicy {
 // ---- leader prepare_next groups ----
 struct LNextPolicy {
   typedef LNextJob Job;
+  static uint64_t heavy_default() { return HEAVY_DEFAULT; }
   struct State {
     LNextLayout L;
     uint32_t jobs = 0, reps = 0, max_n = 0, es = 16;
@@ -965,6 +969,11 @@ struct LNextPolicy {
 // ---- HPKE open groups ----
 struct HpkePolicy {
   typedef HpkeJob Job;
+  // never the heavy-load launcher: one wave's HPKE open is a long dependent chain, so a group
+  // takes about as long at 31k reports as at 62k, and the light-load pipeline's concurrent groups
+  // win (r05o, 128 threads: 20.6-23.4 against 13.8-13.9 M reports/s interleaved; the prepare and
+  // leader executors lose the other way, 19.4-21.4 against 34.3-40.0 and 4.0-4.8 against 5.9-6.8)
+  static uint64_t heavy_default() { return UINT64_MAX / 4; }
   struct State {
     HpkeJob proto;  // the group's opener and per-task constants (stride, share lengths)
     std::vector<std::array<uint8_t, 32>> tasks;  // task-ID table, slot = index
