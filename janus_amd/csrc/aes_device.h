@@ -48,6 +48,18 @@ DEV void aes_tables_init(AesT& T) {
   }
 }
 
+// Byte offset 4 (byte K of w) into a 1 KiB table as a full-rate shift and one v_bitop3_b32 AND
+// (LLVM otherwise forms v_bfe_u32 + v_lshl_add_u32, both half rate); an inlined table's LDS
+// address folds into the ds_read offset field.
+template <int K>
+DEV uint32_t boff(uint32_t w) {
+  const uint32_t sh = K == 0 ? w << 2 : w >> (8 * K - 2);
+  return __builtin_amdgcn_bitop3_b32(sh, 0x3FCu, 0u, 0xC0);
+}
+template <int K>
+DEV uint32_t tlook(const uint32_t* tab, uint32_t w) {
+  return *(const uint32_t*)((const char*)tab + boff<K>(w));
+}
 DEV uint32_t b0(uint32_t x) { return x & 0xffu; }
 DEV uint32_t b1(uint32_t x) { return (x >> 8) & 0xffu; }
 DEV uint32_t b2(uint32_t x) { return (x >> 16) & 0xffu; }
@@ -92,10 +104,17 @@ DEV void aes_encrypt(const AesT& T, const uint32_t* rk, const uint32_t in[4], ui
   uint32_t s0 = in[0] ^ rk[0], s1 = in[1] ^ rk[1], s2 = in[2] ^ rk[2], s3 = in[3] ^ rk[3];
 #pragma unroll
   for (int r = 1; r < NR; r++) {
-    const uint32_t t0 = T.t[0][b0(s0)] ^ T.t[1][b1(s1)] ^ T.t[2][b2(s2)] ^ T.t[3][b3(s3)] ^ rk[4 * r];
-    const uint32_t t1 = T.t[0][b0(s1)] ^ T.t[1][b1(s2)] ^ T.t[2][b2(s3)] ^ T.t[3][b3(s0)] ^ rk[4 * r + 1];
-    const uint32_t t2 = T.t[0][b0(s2)] ^ T.t[1][b1(s3)] ^ T.t[2][b2(s0)] ^ T.t[3][b3(s1)] ^ rk[4 * r + 2];
-    const uint32_t t3 = T.t[0][b0(s3)] ^ T.t[1][b1(s0)] ^ T.t[2][b2(s1)] ^ T.t[3][b3(s2)] ^ rk[4 * r + 3];
+    // five-way XORs as two v_bitop3_b32 (LLVM emits four v_xor)
+    auto col = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
+      return __builtin_amdgcn_bitop3_b32(
+          __builtin_amdgcn_bitop3_b32(tlook<0>(T.t[0], a), tlook<1>(T.t[1], b),
+                                      tlook<2>(T.t[2], c), 0x96),
+          tlook<3>(T.t[3], d), k, 0x96);
+    };
+    const uint32_t t0 = col(s0, s1, s2, s3, rk[4 * r]);
+    const uint32_t t1 = col(s1, s2, s3, s0, rk[4 * r + 1]);
+    const uint32_t t2 = col(s2, s3, s0, s1, rk[4 * r + 2]);
+    const uint32_t t3 = col(s3, s0, s1, s2, rk[4 * r + 3]);
     s0 = t0;
     s1 = t1;
     s2 = t2;
@@ -134,12 +153,28 @@ DEV void aesr_init(AesR& T) {
   }
 }
 
+// Entry x of this lane's copy is at byte offset 128 x + 4 (lane mod 32) from T.t.  The round
+// forms that offset for byte k of a state word as one shift and one v_bitop3_b32
+// ((w >> (8k - 7)) & 0x7F80 | 4 (lane mod 32), both full rate); the table's own LDS address is
+// a constant the compiler folds into the ds_read offset field.
 struct AesRLane {
-  const uint32_t* base;  // &T.t[lane mod 32]
-  DEV uint32_t t0(uint32_t x) const { return base[x << 5]; }
+  const char* base;  // (const char*)T.t
+  uint32_t lane4;    // 4 (lane mod 32)
+  DEV uint32_t t0(uint32_t x) const { return *(const uint32_t*)(base + (x << 7) + lane4); }
+  DEV uint32_t at(uint32_t off) const { return *(const uint32_t*)(base + off); }
+  template <int K>
+  DEV uint32_t off(uint32_t w) const {
+    const uint32_t sh = K == 0 ? w << 7 : w >> (8 * K - 7);
+    return __builtin_amdgcn_bitop3_b32(sh, 0x7F80u, lane4, 0xEA);  // (a & b) | c
+  }
 };
 
-DEV AesRLane aesr_lane(const AesR& T) { return AesRLane{T.t + (threadIdx.x & 31u)}; }
+DEV AesRLane aesr_lane(const AesR& T) {
+  return AesRLane{(const char*)T.t, (threadIdx.x & 31u) << 2};
+}
+DEV uint32_t aes_x3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
 
 DEV uint32_t rotl8(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 24); }
 DEV uint32_t rotl16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
@@ -168,14 +203,14 @@ DEV void aesr128_encrypt(const AesRLane& L, const uint32_t rk[44], const uint32_
   uint32_t s0 = in[0] ^ rk[0], s1 = in[1] ^ rk[1], s2 = in[2] ^ rk[2], s3 = in[3] ^ rk[3];
 #pragma unroll
   for (int r = 1; r < 10; r++) {
-    const uint32_t t0 = L.t0(b0(s0)) ^ rotl8(L.t0(b1(s1))) ^ rotl16(L.t0(b2(s2))) ^
-                        rotl24(L.t0(b3(s3))) ^ rk[4 * r];
-    const uint32_t t1 = L.t0(b0(s1)) ^ rotl8(L.t0(b1(s2))) ^ rotl16(L.t0(b2(s3))) ^
-                        rotl24(L.t0(b3(s0))) ^ rk[4 * r + 1];
-    const uint32_t t2 = L.t0(b0(s2)) ^ rotl8(L.t0(b1(s3))) ^ rotl16(L.t0(b2(s0))) ^
-                        rotl24(L.t0(b3(s1))) ^ rk[4 * r + 2];
-    const uint32_t t3 = L.t0(b0(s3)) ^ rotl8(L.t0(b1(s0))) ^ rotl16(L.t0(b2(s1))) ^
-                        rotl24(L.t0(b3(s2))) ^ rk[4 * r + 3];
+    auto col = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
+      return aes_x3(aes_x3(L.at(L.off<0>(a)), rotl8(L.at(L.off<1>(b))), rotl16(L.at(L.off<2>(c)))),
+                    rotl24(L.at(L.off<3>(d))), k);
+    };
+    const uint32_t t0 = col(s0, s1, s2, s3, rk[4 * r]);
+    const uint32_t t1 = col(s1, s2, s3, s0, rk[4 * r + 1]);
+    const uint32_t t2 = col(s2, s3, s0, s1, rk[4 * r + 2]);
+    const uint32_t t3 = col(s3, s0, s1, s2, rk[4 * r + 3]);
     s0 = t0;
     s1 = t1;
     s2 = t2;

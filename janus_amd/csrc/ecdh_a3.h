@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #ifndef DEV
 #define DEV __device__ __forceinline__
 #endif
@@ -52,13 +54,24 @@ DEV jac<F> madd(const jac<F>& P, const typename F::T& x2, const typename F::T& y
   return R;
 }
 
+// The four doublings of a window as one out-of-line call whose body inlines the field products
+// of FD (P-521: the 18-limb operands exceed the calling convention's argument registers, so
+// every out-of-line product passes them through scratch; here only R does, once per window)
+template <class FD>
+__device__ __noinline__ void dbl4(jac<FD>& R) {
+  jac<FD> Q = R;
+#pragma unroll 1
+  for (int j = 0; j < 4; j++) Q = dbl<FD>(Q);
+  R = Q;
+}
+
 // DH(sk, pkE) for an uncompressed SEC 1 point enc = 0x04 || X || Y (1 + 2 kBytes bytes): validates
 // the point (prefix, canonical coordinates, y^2 = x^3 - 3x + b) and writes the shared
 // x-coordinate's kBytes big-endian bytes.  dig: NDIG signed odd digits in [-15, 15] of the
 // recoded key k' (k' = sk or n - sk, whichever is odd; top digit in [1, 15]), low digit first.
 // As in p256_device.h, the additions meet the doubling case only at the last window (k' close
 // to n), where the doubled point, computed beside the addition for every key, is the sum.
-template <class F, int NDIG>
+template <class F, int NDIG, class FD = F>
 DEV bool ecdh(const int8_t* dig, const uint8_t* enc, uint8_t* dh_be) {
   typedef typename F::T T;
   constexpr int NB = F::kBytes;
@@ -122,16 +135,24 @@ DEV bool ecdh(const int8_t* dig, const uint8_t* enc, uint8_t* dh_be) {
   jac<F> R;
   pick(dig[NDIG - 1], R.X, R.Y);
   R.Z = F::one();
+  auto dbl_w = [&](jac<F>& Q) {
+    if constexpr (std::is_same<F, FD>::value) {
+#pragma unroll 1
+      for (int j = 0; j < 4; j++) Q = dbl<F>(Q);
+    } else {
+      jac<FD> q{Q.X, Q.Y, Q.Z};
+      dbl4<FD>(q);
+      Q = jac<F>{q.X, q.Y, q.Z};
+    }
+  };
 #pragma unroll 1
   for (int i = NDIG - 2; i >= 1; i--) {
-#pragma unroll 1
-    for (int j = 0; j < 4; j++) R = dbl<F>(R);
+    dbl_w(R);
     T tx, ty;
     pick(dig[i], tx, ty);
-    R = madd<F>(R, tx, ty);
+    R = madd<F>(R, tx, ty);  // products out of line (inlined: 256+ VGPRs, 5.99 vs 6.88 M/s)
   }
-#pragma unroll 1
-  for (int j = 0; j < 4; j++) R = dbl<F>(R);
+  dbl_w(R);
   {
     T tx, ty;
     pick(dig[0], tx, ty);

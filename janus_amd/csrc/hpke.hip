@@ -800,7 +800,7 @@ DEV void eae_sha512(const HpkeParams& P, DhByte dh, EncByte enc, uint32_t ss[16]
 
 // the P-521 ECDH, out of line (one copy for the three kernel instances of the KEM)
 __device__ __noinline__ bool p521_dh(const int8_t* dig, const uint8_t* enc, uint8_t* dh) {
-  return ecdh_a3::ecdh<p521::Field, P521_DIGITS>(dig, enc, dh);
+  return ecdh_a3::ecdh<p521::Field, P521_DIGITS, p521::FieldInl>(dig, enc, dh);
 }
 
 // MODE 0: explicit AAD, plaintext out.  MODE 1: DAP helper input share with PUB bytes of

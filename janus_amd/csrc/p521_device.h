@@ -89,34 +89,59 @@ DEV fp reduce(uint64_t c[2 * NL]) {
   return o;
 }
 
-// out of line: the curve formulas call it ~20 times per window step, inlined that is ~80 KB of
-// code per loop body (more than the instruction cache)
-__device__ __noinline__ fp mul(const fp& a, const fp& b) {
-  uint64_t c[2 * NL];
+// Product scanning: column k of the 1044-bit product is accumulated in one 64-bit register
+// (each limb product one v_mad_u64_u32 with the running sum as its addend), carried into the
+// next column at once, and leaves one 29-bit limb: 36 limbs + 2 64-bit registers live instead of
+// 35 64-bit columns, so the product can be inlined into the curve formulas (ecdh_a3.h's dbl4).
+// The high limbs fold with 2^522 = 2 (mod p).
+DEV fp fold(const uint32_t lo[NL], const uint32_t hi[NL], uint32_t top) {
+  // value = lo + 2^522 (hi + 2^522 top), limbs 29 bits; 2^522 = 2 (mod p)
+  fp o;
+  uint32_t c = 0;
 #pragma unroll
-  for (int k = 0; k < 2 * NL; k++) c[k] = 0;
-#pragma unroll
-  for (int i = 0; i < NL; i++)
-#pragma unroll
-    for (int j = 0; j < NL; j++) c[i + j] += (uint64_t)a.v[i] * b.v[j];
-  return reduce(c);
+  for (int k = 0; k < NL; k++) {
+    const uint32_t x = lo[k] + 2 * hi[k] + (k == 0 ? 4 * top : 0) + c;  // < 2^31
+    c = x >> (k == NL - 1 ? 28 : 29);
+    o.v[k] = x & (k == NL - 1 ? M28 : M29);
+  }
+  o.v[0] += c;  // 2^521 = 1
+  return o;
 }
-
-__device__ __noinline__ fp sqr(const fp& a) {
-  uint64_t c[2 * NL];
-  uint32_t d[NL];
+DEV fp mul_i(const fp& a, const fp& b) {
+  uint32_t lo[NL], hi[NL];
+  uint64_t acc = 0;
 #pragma unroll
-  for (int k = 0; k < 2 * NL; k++) c[k] = 0;
+  for (int k = 0; k < 2 * NL - 1; k++) {
+#pragma unroll
+    for (int i = (k < NL ? 0 : k - NL + 1); i <= (k < NL ? k : NL - 1); i++)
+      acc += (uint64_t)a.v[i] * b.v[k - i];
+    (k < NL ? lo[k] : hi[k - NL]) = (uint32_t)acc & M29;
+    acc >>= 29;
+  }
+  hi[NL - 1] = (uint32_t)acc & M29;
+  return fold(lo, hi, (uint32_t)(acc >> 29));
+}
+DEV fp sqr_i(const fp& a) {
+  uint32_t lo[NL], hi[NL], d[NL];
 #pragma unroll
   for (int i = 0; i < NL; i++) d[i] = 2 * a.v[i];
+  uint64_t acc = 0;
 #pragma unroll
-  for (int i = 0; i < NL; i++) {
-    c[2 * i] += (uint64_t)a.v[i] * a.v[i];
+  for (int k = 0; k < 2 * NL - 1; k++) {
 #pragma unroll
-    for (int j = i + 1; j < NL; j++) c[i + j] += (uint64_t)d[i] * a.v[j];
+    for (int i = (k < NL ? 0 : k - NL + 1); 2 * i < k; i++) acc += (uint64_t)d[i] * a.v[k - i];
+    if ((k & 1) == 0) acc += (uint64_t)a.v[k / 2] * a.v[k / 2];
+    (k < NL ? lo[k] : hi[k - NL]) = (uint32_t)acc & M29;
+    acc >>= 29;
   }
-  return reduce(c);
+  hi[NL - 1] = (uint32_t)acc & M29;
+  return fold(lo, hi, (uint32_t)(acc >> 29));
 }
+
+// out of line for the mixed additions, the table and the inversions (one copy each); the
+// doublings, 3/4 of the multiplies, inline them (dbl4)
+__device__ __noinline__ fp mul(const fp& a, const fp& b) { return mul_i(a, b); }
+__device__ __noinline__ fp sqr(const fp& a) { return sqr_i(a); }
 
 DEV fp mul_small(const fp& a, uint32_t k) {  // k <= 8
   uint64_t r[NL];
@@ -137,9 +162,15 @@ DEV fp mul_small(const fp& a, uint32_t k) {  // k <= 8
   return o;
 }
 
-DEV fp sqr_n(fp x, int n) {
+// x^(2^n): one out-of-line call around a loop of inlined squarings (the inversions' 520)
+__device__ __noinline__ void sqr_n_ool(fp& x, int n) {
+  fp y = x;
 #pragma unroll 1
-  for (int i = 0; i < n; i++) x = sqr(x);
+  for (int i = 0; i < n; i++) y = sqr_i(y);
+  x = y;
+}
+DEV fp sqr_n(fp x, int n) {
+  sqr_n_ool(x, n);
   return x;
 }
 
@@ -257,6 +288,11 @@ struct Field {
     return r;
   }
   DEV static T b() { return kB; }
+};
+// the same field with the products inlined (ecdh_a3.h's dbl4)
+struct FieldInl : Field {
+  DEV static T mul(const T& a, const T& b) { return p521::mul_i(a, b); }
+  DEV static T sqr(const T& a) { return p521::sqr_i(a); }
 };
 
 }  // namespace p521

@@ -465,16 +465,62 @@ DEV uint64_t sub64f(uint64_t a, uint64_t b) {
   uint64_t d = a - b;
   return a < b ? d + P64 : d;
 }
-DEV uint64_t mul64f(uint64_t a, uint64_t b) {
-  uint64_t lo = a * b, hi = __umul64hi(a, b);
-  uint64_t hh = hi >> 32, hl = hi & 0xffffffffull;
-  uint64_t t0 = lo - hh;
-  if (lo < hh) t0 -= 0xffffffffull;
-  uint64_t t1 = hl * 0xffffffffull;
+// (hi:lo) mod p, canonical: 2^64 = 2^32 - 1 and 2^96 = -1 (mod p), so with hi = x3:x2 the value
+// is lo + x2 (2^32 - 1) - x3.
+DEV uint64_t red128_64(uint64_t lo, uint64_t hi) {
+  const uint32_t x2 = (uint32_t)hi, x3 = (uint32_t)(hi >> 32);
+  uint64_t t0 = lo - x3;
+  if (lo < x3) t0 -= 0xffffffffull;  // borrow: -2^64 = -(2^32 - 1)
+  const uint64_t t1 = ((uint64_t)x2 << 32) - x2;
   uint64_t r = t0 + t1;
-  if (r < t0) r += 0xffffffffull;
+  if (r < t1) r += 0xffffffffull;  // carry: 2^64 = 2^32 - 1
   if (r >= P64) r -= P64;
   return r;
+}
+// The 128-bit product as four v_mad_u64_u32 (each partial sum fits 64 bits), then red128_64.
+DEV uint64_t mul64f(uint64_t a, uint64_t b) {
+  const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b,
+                 b1 = (uint32_t)(b >> 32);
+  const uint64_t p00 = (uint64_t)a0 * b0;
+  const uint64_t p01 = (uint64_t)a0 * b1 + (p00 >> 32);
+  const uint64_t p10 = (uint64_t)a1 * b0 + (uint32_t)p01;
+  const uint64_t hi = (uint64_t)a1 * b1 + (p01 >> 32) + (p10 >> 32);  // <= 2^64 - 1
+  return red128_64((p10 << 32) | (uint32_t)p00, hi);
+}
+
+// Lazily reduced Field64 multiply-accumulate: column k (weight 2^(32k)) = c_k + h_k 2^64; each
+// 32x32 limb product is one v_mad_u64_u32 with its carry-out counted by one v_addc (as
+// mac_add for Field128).  Up to 2^31 products; mac64_reduce folds once.
+struct mac64 {
+  uint64_t c0, c1, c2;
+  uint32_t h0, h1, h2;
+};
+DEV void mac64_zero(mac64& a) {
+  a.c0 = a.c1 = a.c2 = 0;
+  a.h0 = a.h1 = a.h2 = 0;
+}
+DEV void mac64_add(mac64& a, uint64_t x, uint64_t y) {
+  asm("v_mad_u64_u32 %0, vcc, %6, %8, %0\n\t"
+      "v_addc_co_u32 %3, vcc, 0, %3, vcc\n\t"
+      "v_mad_u64_u32 %1, vcc, %6, %9, %1\n\t"
+      "v_addc_co_u32 %4, vcc, 0, %4, vcc\n\t"
+      "v_mad_u64_u32 %1, vcc, %7, %8, %1\n\t"
+      "v_addc_co_u32 %4, vcc, 0, %4, vcc\n\t"
+      "v_mad_u64_u32 %2, vcc, %7, %9, %2\n\t"
+      "v_addc_co_u32 %5, vcc, 0, %5, vcc"
+      : "+v"(a.c0), "+v"(a.c1), "+v"(a.c2), "+v"(a.h0), "+v"(a.h1), "+v"(a.h2)
+      : "v"((uint32_t)x), "v"((uint32_t)(x >> 32)), "v"((uint32_t)y), "v"((uint32_t)(y >> 32))
+      : "vcc");
+}
+// value = c0 + c1 2^32 + (c2 + h0) 2^64 + h1 2^96 + h2 2^128 as 32-bit words w0..w4, then
+// w0..w3 by red128_64 and w4 2^128 = -w4 2^32 (mod p)
+DEV uint64_t mac64_reduce(const mac64& a) {
+  const uint64_t s1 = (a.c0 >> 32) + (uint32_t)a.c1;
+  const uint64_t s2 = (s1 >> 32) + (a.c1 >> 32) + (uint32_t)a.c2 + a.h0;
+  const uint64_t s3 = (s2 >> 32) + (a.c2 >> 32) + a.h1;
+  const uint32_t w4 = (uint32_t)(s3 >> 32) + a.h2;
+  const uint64_t r = red128_64((s1 << 32) | (uint32_t)a.c0, (s3 << 32) | (uint32_t)s2);
+  return sub64f(r, (uint64_t)w4 << 32);
 }
 
 // -------------------------------------------------------------------------------------

@@ -29,6 +29,25 @@ namespace {
 typedef Fp64 F;
 typedef uint64_t T;
 
+DEV T sqn64(T x, int n) {
+  for (int i = 0; i < n; i++) x = mul64f(x, x);
+  return x;
+}
+// x^(p-2), p - 2 = (2^32 - 2) 2^32 + (2^32 - 1): u = x^(2^32 - 2) = (x^(2^31 - 1))^2 by an
+// addition chain (31 squarings, 8 multiplies), then u^(2^32) u x -- 63 squarings and 9 multiplies
+// instead of the 64 + 62 of square-and-multiply
+DEV T inv64(T x) {
+  const T t2 = mul64f(sqn64(x, 1), x);      // 2^2 - 1
+  const T t3 = mul64f(sqn64(t2, 1), x);     // 2^3 - 1
+  const T t6 = mul64f(sqn64(t3, 3), t3);    // 2^6 - 1
+  const T t12 = mul64f(sqn64(t6, 6), t6);   // 2^12 - 1
+  const T t15 = mul64f(sqn64(t12, 3), t3);  // 2^15 - 1
+  const T t16 = mul64f(sqn64(t15, 1), x);   // 2^16 - 1
+  const T t31 = mul64f(sqn64(t16, 15), t15);  // 2^31 - 1
+  const T u = sqn64(t31, 1);                // 2^32 - 2
+  return mul64f(sqn64(u, 32), mul64f(u, x));  // (2^32 - 2) 2^32 + 2^32 - 1
+}
+
 }  // namespace
 
 // LEADER = 1: the leader's prepare_init (agg_id 0, aggregation_job_driver.rs:397-415) on its
@@ -202,19 +221,8 @@ __global__ __launch_bounds__(256, 4) void k_mp64_prepare(Mp64Params P, uint32_t 
       Lb[(size_t)i * ld + r] = pre;
       ai = F::mul(ai, P.alpha);
     }
-    T inv;
-    {  // pre^(p-2), p - 2 = 0xFFFFFFFEFFFFFFFF
-      T x = pre, acc = 1;
-      uint64_t e = 0xFFFFFFFEFFFFFFFFull;
-      while (e) {
-        if (e & 1) acc = F::mul(acc, x);
-        x = F::mul(x, x);
-        e >>= 1;
-      }
-      inv = acc;
-    }
-    T aback = 1;  // alpha^i, i = P-1 .. 0 (alpha^(P-1) = alpha^-1)
-    for (uint32_t i = 0; i < PP - 1; i++) aback = F::mul(aback, P.alpha);
+    T inv = inv64(pre);
+    T aback = P.alpha_inv;  // alpha^i, i = P-1 .. 0 (alpha^(P-1) = alpha^-1)
     for (uint32_t i = PP; i-- > 0;) {
       const T di = F::sub(t, aback);
       const T inv_i = i ? F::mul(inv, Lb[(size_t)(i - 1) * ld + r]) : inv;
@@ -253,14 +261,17 @@ __global__ __launch_bounds__(256, 4) void k_mp64_prepare(Mp64Params P, uint32_t 
       return x;
     };
     for (uint32_t jj = 0; jj < C; jj++) {
-      T s0 = 0, s1 = 0;
+      mac64 a0, a1;  // lazily reduced sums of the call products (one fold per column)
+      mac64_zero(a0);
+      mac64_zero(a1);
       for (uint32_t kk = 0; kk < K; kk++) {
         const uint32_t idx = kk * C + jj;
         if (idx >= M) break;  // zero-padded elements add nothing to s0 / s1
         const T m = ld64(meas, ld, idx, r);
-        s0 = F::add(s0, F::mul(m, Gb[(size_t)kk * ld + r]));
-        s1 = F::add(s1, F::mul(m, Lb[(size_t)(kk + 1) * ld + r]));
+        mac64_add(a0, m, Gb[(size_t)kk * ld + r]);
+        mac64_add(a1, m, Lb[(size_t)(kk + 1) * ld + r]);
       }
+      const T s0 = mac64_reduce(a0), s1 = mac64_reduce(a1);
       const T f0 = F::add(F::mul(ld64(pf, ld, 2 * jj, r), L0), F::mul(rj, s0));
       const T f1 = F::sub(F::add(F::mul(ld64(pf, ld, 2 * jj + 1, r), L0), s1), hSL);
       if (LEADER) {
@@ -272,13 +283,16 @@ __global__ __launch_bounds__(256, 4) void k_mp64_prepare(Mp64Params P, uint32_t 
       rj = F::mul(rj, rr);
     }
     // p(t) by Horner; v = sum_calls p(alpha^(c+1)) = sum_e coef_e sigma_(e mod P)
-    T pt = 0, v = 0;
+    T pt = 0;
+    mac64 va;
+    mac64_zero(va);
     for (uint32_t q = 0; q < P.glen; q++) {
       const uint32_t e = P.glen - 1 - q;
       const T c = ld64(pf, ld, P.arity + e, r);
       pt = F::add(F::mul(pt, t), c);
-      v = F::add(v, F::mul(c, P.sigma[e & (PP - 1)]));
+      mac64_add(va, c, P.sigma[e & (PP - 1)]);
     }
+    const T v = mac64_reduce(va);
     if (LEADER) {
       vo[0] = v;
       vo[P.arity + 1] = pt;
@@ -340,10 +354,23 @@ __global__ __launch_bounds__(256, 4) void k_mp64_prepare(Mp64Params P, uint32_t 
   // 8. output share: SumVec truncate (bit recomposition)
   uint64_t* o = (uint64_t*)sc.out;
   for (uint32_t e = 0; e < P.out_len; e++) {
-    T acc = 0, pw = 1;
-    for (uint32_t b = 0; b < P.bits; b++) {
-      acc = F::add(acc, F::mul(pw, ld64(meas, ld, e * P.bits + b, r)));
-      pw = F::add(pw, pw);
+    T acc;
+    if (P.bits <= 31) {  // sum of m_b 2^b as two 64-bit columns (no carries: < 2^63), one fold
+      uint64_t c0 = 0, c1 = 0;
+      for (uint32_t b = 0; b < P.bits; b++) {
+        const T m = ld64(meas, ld, e * P.bits + b, r);
+        c0 += (uint64_t)(uint32_t)m * (1u << b);
+        c1 += (uint64_t)(uint32_t)(m >> 32) * (1u << b);
+      }
+      const uint64_t s1 = (c0 >> 32) + (uint32_t)c1;
+      acc = red128_64((s1 << 32) | (uint32_t)c0, (s1 >> 32) + (c1 >> 32));
+    } else {
+      T pw = 1;
+      acc = 0;
+      for (uint32_t b = 0; b < P.bits; b++) {
+        acc = F::add(acc, F::mul(pw, ld64(meas, ld, e * P.bits + b, r)));
+        pw = F::add(pw, pw);
+      }
     }
     o[(size_t)e * ld + r] = acc;
   }

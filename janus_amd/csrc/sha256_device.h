@@ -12,6 +12,11 @@
 namespace sha256d {
 
 DEV uint32_t rotr(uint32_t x, uint32_t n) { return __builtin_amdgcn_alignbit(x, x, n); }
+// Three-input logic as one full-rate v_bitop3_b32 (truth table over src0 = 0xF0, src1 = 0xCC,
+// src2 = 0xAA): LLVM emits two v_xor for a ^ b ^ c and v_xor + v_and + v_bitop3 for Maj.
+DEV uint32_t x3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+DEV uint32_t maj(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8); }
+DEV uint32_t ch(uint32_t e, uint32_t f, uint32_t g) { return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA); }
 
 constexpr uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                             0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
@@ -38,15 +43,14 @@ DEV void compress(uint32_t st[8], uint32_t w[16]) {
       wt = w[t];
     } else {  // rolling 16-word schedule
       const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
-      const uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
-      const uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
+      const uint32_t s0 = x3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+      const uint32_t s1 = x3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
       wt = w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
     }
-    const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
-    const uint32_t ch = (e & f) ^ (~e & g);
-    const uint32_t t1 = h + S1 + ch + K[t] + wt;
-    const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
-    const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    const uint32_t S1 = x3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+    const uint32_t t1 = h + S1 + ch(e, f, g) + K[t] + wt;
+    const uint32_t S0 = x3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+    const uint32_t mj = maj(a, b, c);
     h = g;
     g = f;
     f = e;

@@ -14,7 +14,45 @@
 
 namespace sha512d {
 
-HD uint64_t rotr(uint64_t x, uint32_t n) { return (x >> n) | (x << (64 - n)); }
+// Rotations and shifts on the device as v_alignbit_b32 on the 32-bit halves (LLVM otherwise
+// builds them from 64-bit shifts and ORs)
+HD uint64_t rotr(uint64_t x, uint32_t n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  if (n < 32)
+    return (uint64_t)__builtin_amdgcn_alignbit(lo, hi, n) << 32 | __builtin_amdgcn_alignbit(hi, lo, n);
+  return (uint64_t)__builtin_amdgcn_alignbit(hi, lo, n - 32) << 32 |
+         __builtin_amdgcn_alignbit(lo, hi, n - 32);
+#else
+  return (x >> n) | (x << (64 - n));
+#endif
+}
+HD uint64_t shr(uint64_t x, uint32_t n) {  // n < 32
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return (uint64_t)(hi >> n) << 32 | __builtin_amdgcn_alignbit(hi, lo, n);
+#else
+  return x >> n;
+#endif
+}
+// Three-input logic on both 32-bit halves as v_bitop3_b32 (full rate) on the device; LLVM emits
+// two v_xor per half for a ^ b ^ c and v_xor + v_and + v_bitop3 for Maj.
+template <uint32_t TT>
+HD uint64_t bop3(uint64_t a, uint64_t b, uint64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, TT);
+  const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32),
+                                                  (uint32_t)(c >> 32), TT);
+  return (uint64_t)hi << 32 | lo;
+#else
+  uint64_t r = 0;  // the truth table bit by bit (src0 = 0xF0, src1 = 0xCC, src2 = 0xAA)
+  for (int i = 0; i < 8; i++)
+    if ((TT >> i) & 1) {
+      r |= ((i & 4) ? a : ~a) & ((i & 2) ? b : ~b) & ((i & 1) ? c : ~c);
+    }
+  return r;
+#endif
+}
 
 // IVs: SHA-512 (FIPS 180-4 5.3.5) and SHA-384 (5.3.4)
 constexpr uint64_t IV512[8] = {0x6a09e667f3bcc908ull, 0xbb67ae8584caa73bull, 0x3c6ef372fe94f82bull,
@@ -58,15 +96,15 @@ __host__ __device__ __noinline__ void compress(uint64_t st[8], uint64_t w[16]) {
       wt = w[t];
     } else {  // rolling 16-word schedule
       const uint64_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
-      const uint64_t s0 = rotr(w15, 1) ^ rotr(w15, 8) ^ (w15 >> 7);
-      const uint64_t s1 = rotr(w2, 19) ^ rotr(w2, 61) ^ (w2 >> 6);
+      const uint64_t s0 = bop3<0x96>(rotr(w15, 1), rotr(w15, 8), shr(w15, 7));
+      const uint64_t s1 = bop3<0x96>(rotr(w2, 19), rotr(w2, 61), shr(w2, 6));
       wt = w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
     }
-    const uint64_t S1 = rotr(e, 14) ^ rotr(e, 18) ^ rotr(e, 41);
-    const uint64_t ch = (e & f) ^ (~e & g);
+    const uint64_t S1 = bop3<0x96>(rotr(e, 14), rotr(e, 18), rotr(e, 41));
+    const uint64_t ch = bop3<0xCA>(e, f, g);
     const uint64_t t1 = h + S1 + ch + K[t] + wt;
-    const uint64_t S0 = rotr(a, 28) ^ rotr(a, 34) ^ rotr(a, 39);
-    const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
+    const uint64_t S0 = bop3<0x96>(rotr(a, 28), rotr(a, 34), rotr(a, 39));
+    const uint64_t mj = bop3<0xE8>(a, b, c);
     h = g;
     g = f;
     f = e;

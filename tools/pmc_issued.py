@@ -38,11 +38,17 @@ def main():
         for row in csv.DictReader(open(f)):
             if row["Counter_Name"] != "SQ_INSTS_VALU":
                 continue
-            m = re.search(r"\b(k_[A-Za-z_0-9]+)", row["Kernel_Name"])
-            if not m or m.group(1) not in per_step:
+            m = re.search(r"\b(k_[A-Za-z_0-9]+)(<[^>]*>)?", row["Kernel_Name"])
+            if not m:
                 continue
-            tot[m.group(1)] += float(row["Counter_Value"])
-            disp[m.group(1)].add(row["Dispatch_Id"])
+            # a --kernels entry may name one instantiation (k_mp64_prepare<0>)
+            name = m.group(1) + (m.group(2) or "")
+            if name not in per_step:
+                name = m.group(1)
+                if name not in per_step:
+                    continue
+            tot[name] += float(row["Counter_Value"])
+            disp[name].add(row["Dispatch_Id"])
     parts = {k: tot[k] / len(disp[k]) * per_step[k] * 64 / n for k in tot}
     table = json.load(open(TABLE)) if os.path.exists(TABLE) else {}
     table[key] = dict(issued_instr_per_report=sum(parts.values()),
