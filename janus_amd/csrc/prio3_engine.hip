@@ -860,6 +860,193 @@ __global__ __launch_bounds__(256) void k_leader_unpack(DevParams p, InPtrs in, S
   }
 }
 
+// ------------------------------------------------------------------------------------
+// k_leader_jr: k_leader_unpack + k_jrpart<false, true> in one launch.  Each lane absorbs its
+// own report's measurement share into the joint-rand sponge straight from the AoS input (the
+// 11-12 16-byte loads of a sponge block run back to back over the same 176-192 bytes of the
+// row), checks the encodings and writes the SoA measurement / proofs scratch the query reads;
+// the share is read from HBM once instead of twice.  Then the joint-rand part, corrected seed,
+// joint randomness (k_jrpart) and the query randomness (k_leader_unpack).  wpart / wseg as
+// k_leader_unpack's (the device leader's fused accumulate): the wave totals of each element by
+// wave_halfsum2, the wave marked fused when all 64 reports are present and canonical.
+// Interleaved on one box (profiles/r05/leader_jr/): 173.4-173.9 against 165.4-166.5 M reports/s
+// for the two kernels (k_leader_jr 3.76 ms against 2.32 + 1.70 ms per 1 Mi).  Staging each
+// sponge block's 64 x 11-12 elements through LDS with coalesced row segments instead (one wave
+// per block, 12 KiB, 3 waves per SIMD) took 4.12 ms.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256, JR_OCC) void k_leader_jr(DevParams p, InPtrs in, Scratch sc,
+                                                         uint8_t* status, uint32_t* wpart,
+                                                         uint32_t* wseg) {
+  typedef Fp128 F;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  const bool acc = wpart != nullptr && __all(r < p.n);  // wave-uniform
+  if (r >= p.n) return;
+  const size_t ld = p.ld;
+  const int M = (int)p.meas_len;
+  const uint32_t PL = p.proof_len;
+  const uint4* row = (const uint4*)(in.helper + (size_t)r * p.leader_share_len);
+  uint32_t bad = 0;
+  uint32_t nonce[4], kb[4];
+  load16(in.nonces + 16 * (size_t)r, nonce);
+  load16((const uint8_t*)(row + (M + PL)), kb);
+  uint32_t pre[11];
+  {
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[7]);
+    msg_bytes16(m, 9, kb);
+    msg_byte(m, 25, 0);
+    msg_bytes16(m, 26, nonce);
+#pragma unroll
+    for (int j = 0; j < 11; j++) pre[j] = m.w[j];
+  }
+  uint4* meas = (uint4*)sc.meas;
+  auto ldel = [&](int e) -> uint4 {
+    const bool ok = e >= 0 && e < M;
+    const uint4 v = row[ok ? e : 0];
+    return ok ? v : make_uint4(0, 0, 0, 0);
+  };
+  // element e (owned by this window): canonical check and the SoA copy
+  auto own = [&](int e, const uint4& v) {
+    if (e < 0 || e >= M) return;
+    if (!F::lt_p(mk128(v.x, v.y, v.z, v.w))) bad = 1;
+    meas[(size_t)e * ld + r] = v;
+  };
+  auto wsel = [](const uint4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; };
+  // wave totals of elements e0, e0 + 1 (the second only if below lim)
+  auto acc_pair = [&](int e0, const uint4& a, const uint4& b, int lim) {
+    if (e0 + 1 < 0 || e0 >= M) return;  // wave-uniform
+    const uint32_t tot = wave_halfsum2(mk128(a.x, a.y, a.z, a.w), mk128(b.x, b.y, b.z, b.w), lane);
+    const int e = e0 + (int)(lane >> 5);
+    if ((lane & 3u) == 0 && e >= 0 && e < M && e < lim)
+      wpart[((size_t)(r >> 6) * (uint32_t)M + (uint32_t)e) * 8u + ((lane >> 2) & 7u)] = tot;
+  };
+  const uint32_t L = 42 + (uint32_t)M * 16;
+  const uint32_t B = L / 168, rem = L % 168;
+  KState s;
+  kzero(s);
+  for (uint32_t b = 0; b <= B; b++) {
+    uint32_t x[42];
+    const int q21 = 21 * (int)(b >> 1);
+    if ((b & 1) == 0) {
+      // window q21-3 .. q21+7; this block owns q21-2 .. q21+7 (E[1..10])
+      uint4 E[11];
+#pragma unroll
+      for (int t = 0; t < 11; t++) E[t] = ldel(q21 - 3 + t);
+#pragma unroll
+      for (int t = 1; t < 11; t++) own(q21 - 3 + t, E[t]);
+      if (acc) {
+#pragma unroll
+        for (int t = 1; t < 11; t += 2) acc_pair(q21 - 3 + t, E[t], E[t + 1], q21 + 8);
+      }
+#pragma unroll
+      for (int j = 0; j < 42; j++) {
+        const int u0 = j - 11 + 12, u1 = j - 10 + 12;
+        const uint32_t w0 = wsel(E[u0 >> 2], u0 & 3), w1 = wsel(E[u1 >> 2], u1 & 3);
+        x[j] = __builtin_amdgcn_alignbit(w1, w0, 16);
+      }
+      if (b == 0) {
+#pragma unroll
+        for (int j = 0; j < 10; j++) x[j] = pre[j];
+        x[10] = (pre[10] & 0xffffu) | (wsel(E[3], 0) << 16);
+      }
+    } else {
+      // window q21+7 .. q21+18; this block owns q21+8 .. q21+18 (E[1..11])
+      uint4 E[12];
+#pragma unroll
+      for (int t = 0; t < 12; t++) E[t] = ldel(q21 + 7 + t);
+#pragma unroll
+      for (int t = 1; t < 12; t++) own(q21 + 7 + t, E[t]);
+      if (acc) {
+#pragma unroll
+        for (int t = 1; t < 12; t += 2)
+          acc_pair(q21 + 7 + t, E[t], t + 1 < 12 ? E[t + 1] : make_uint4(0, 0, 0, 0), q21 + 19);
+      }
+#pragma unroll
+      for (int j = 0; j < 42; j++) {
+        const int u0 = j + 3, u1 = j + 4;
+        const uint32_t w0 = wsel(E[u0 >> 2], u0 & 3), w1 = wsel(E[u1 >> 2], u1 & 3);
+        x[j] = __builtin_amdgcn_alignbit(w1, w0, 16);
+      }
+    }
+    if (b == B) {
+#pragma unroll
+      for (int j = 0; j < 42; j++) {
+        const uint32_t lo = 4 * j;
+        uint32_t mask = (lo + 4 <= rem) ? 0xffffffffu
+                                        : (lo >= rem ? 0u : ((1u << (8 * (rem - lo))) - 1u));
+        x[j] &= mask;
+        if ((uint32_t)j == (rem >> 2)) x[j] ^= 1u << (8 * (rem & 3));
+      }
+      x[41] ^= 0x80000000u;
+    }
+#pragma unroll
+    for (int j = 0; j < 42; j++) kxor_word(s, j, x[j]);
+    keccak_p12(s);
+  }
+  {  // the proofs share: canonical check and SoA copy
+    uint4* proofs = (uint4*)sc.proofs;
+    for (uint32_t e = 0; e < PL; e++) {
+      const uint4 v = row[M + e];
+      if (!F::lt_p(mk128(v.x, v.y, v.z, v.w))) bad = 1;
+      proofs[(size_t)e * ld + r] = v;
+    }
+  }
+  uint32_t flag = p.force_slow;
+  {  // query randomness (k_leader_unpack)
+    KState q;
+    kzero(q);
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[5]);
+    {
+      uint32_t vk[4];
+      load_vk(p, in, r, vk);
+      msg_bytes16(m, 9, vk);
+    }
+    msg_byte(m, 25, 1);
+    msg_bytes16(m, 26, nonce);
+    msg_absorb_final(q, m, 42);
+    uint32_t w[4] = {kword(q, 0), kword(q, 1), kword(q, 2), kword(q, 3)};
+    put_elem<F>(p, sc.qr, 0, r, w, flag);
+  }
+  uint32_t part[4] = {kword(s, 0), kword(s, 1), kword(s, 2), kword(s, 3)};
+  uint32_t pub0[4];
+  load16(in.pub + (size_t)r * p.public_share_len + 16, pub0);
+  KState c;
+  kzero(c);
+  {
+    Msg m;
+    msg_zero(m);
+    msg_dst(m, p.dst[6]);
+    msg_bytes16(m, 25, part);
+    msg_bytes16(m, 41, pub0);
+    msg_absorb_final(c, m, 57);
+  }
+  uint32_t cor[4] = {kword(c, 0), kword(c, 1), kword(c, 2), kword(c, 3)};
+  {
+    KState t;
+    kzero(t);
+    Msg m2;
+    msg_zero(m2);
+    msg_dst(m2, p.dst[3]);
+    msg_bytes16(m2, 9, cor);
+    msg_byte(m2, 25, 1);
+    msg_absorb_final(t, m2, 26);
+    uint32_t q0 = 0, q1 = 0;
+    squeeze_block<Fp128>(p, t, 0, p.jr_len, q0, q1, sc.jr, r, flag);
+  }
+  sc.part[r] = make_uint4(part[0], part[1], part[2], part[3]);
+  sc.corrected[r] = make_uint4(cor[0], cor[1], cor[2], cor[3]);
+  sc.flag[r] = (uint8_t)flag;
+  status[r] = bad ? PRIO3_STATUS_INPUT_SHARE_DECODE : PRIO3_STATUS_FINISHED;
+  if (wseg) {
+    const bool fuse = acc && __all(!bad);
+    if (lane == 0) wseg[r >> 6] = fuse ? 0u : 0xffffffffu;
+  }
+}
+
 // Leader slow path: reports whose query or joint-rand expansion hit a rejection-sampling
 // event (flagged by k_leader_unpack / k_jrpart) get both redone by the byte-level sponge.
 __global__ __launch_bounds__(64) void k_leader_slowfix(DevParams p, InPtrs in, Scratch sc) {
@@ -3358,11 +3545,10 @@ static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
     OutPtrs out{d_prep_shares, d_status};
     const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
     // R->lfused: the wave partials of the share for segment 0, fixed up at accumulate
-    TIMED(e, st, "k_leader_unpack",
-          (k_leader_unpack<<<(n + 63) / 64, 256, 0, st>>>(dp, in, R->sc, d_status,
-                                                         R->lfused ? R->wpart : nullptr,
-                                                         R->lfused ? R->wseg : nullptr)));
-    TIMED(e, st, "k_jrpart", (k_jrpart<false, true><<<blocks, 256, 0, st>>>(dp, in, R->sc)));
+    TIMED(e, st, "k_leader_jr",
+          (k_leader_jr<<<blocks, 256, 0, st>>>(dp, in, R->sc, d_status,
+                                               R->lfused ? R->wpart : nullptr,
+                                               R->lfused ? R->wseg : nullptr)));
     TIMED(e, st, "k_leader_slowfix",
           (k_leader_slowfix<<<blocks64, 64, 0, st>>>(dp, in, R->sc)));
     if (dp.P == 32)
@@ -3380,10 +3566,8 @@ static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
     in.vk_tab = vk_tab;
     OutPtrs out{d_prep_shares, d_status};
     const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
-    TIMED(e, st, "k_leader_unpack",
-          (k_leader_unpack<<<(n + 63) / 64, 256, 0, st>>>(dp, in, R->sc, d_status, nullptr,
-                                                         nullptr)));
-    TIMED(e, st, "k_jrpart", (k_jrpart<false, true><<<blocks, 256, 0, st>>>(dp, in, R->sc)));
+    TIMED(e, st, "k_leader_jr",
+          (k_leader_jr<<<blocks, 256, 0, st>>>(dp, in, R->sc, d_status, nullptr, nullptr)));
     TIMED(e, st, "k_leader_slowfix",
           (k_leader_slowfix<<<blocks64, 64, 0, st>>>(dp, in, R->sc)));
     bool ok = false;
@@ -4169,9 +4353,9 @@ static int fused_finish(prio3_engine* e, Run* R, const uint8_t* d_status, const 
   return PRIO3_OK;
 }
 
-// Device leader init with the accumulate fused into k_leader_unpack (option leader_fuse_acc):
+// Device leader init with the accumulate fused into k_leader_jr (option leader_fuse_acc):
 // Histogram on the helper kernels' leader role, whose output share is the measurement share
-// that the unpack stages through LDS anyway.
+// that k_leader_jr streams through anyway.
 static bool leader_fuse_takes(const prio3_engine* e) {
   const DevParams& d = e->dp;
   return e->leader_fuse_acc && e->leader_fast && d.jr_len && d.kind == PRIO3_HISTOGRAM &&
