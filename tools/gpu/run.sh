@@ -74,6 +74,8 @@ for step in "$@"; do
     bench jobs128 --role jobs
     bench hpke --role hpke --reports 1048576
     bench hpke_p256 --role hpke --hpke-kem p256 --reports 262144
+    bench hpke_x448 --role hpke --hpke-kem x448 --reports 262144
+    bench hpke_p521 --role hpke --hpke-kem p521 --reports 262144
     bench pipeline --role pipeline --reports 1048576
     bench mp64 --role mp64 --reports 1000000 ;;
   prof)
