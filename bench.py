@@ -193,7 +193,7 @@ def main():
                          "(1M/8 per GPU), C4 Prio3Sum 32 (10M/8 per GPU)")
     ap.add_argument("--hpke-aead", type=int, choices=[1, 2, 3], default=1,
                     help="--role hpke: AEAD id (1 AES-128-GCM, 2 AES-256-GCM, 3 ChaCha20Poly1305)")
-    ap.add_argument("--hpke-kem", choices=["x25519", "p256", "x448", "p521"], default="x25519",
+    ap.add_argument("--hpke-kem", choices=["x25519", "p256", "x448", "p521", "p384"], default="x25519",
                     help="--role hpke: DHKEM(X25519, HKDF-SHA256), DHKEM(P-256, HKDF-SHA256), "
                          "DHKEM(X448, HKDF-SHA512) or DHKEM(P-521, HKDF-SHA512); the key "
                          "schedule's KDF follows the KEM's (RFC 9180 suites of the reference's "
@@ -1080,11 +1080,15 @@ def hpke_main(args):
     t0 = time.perf_counter()
     aead = args.hpke_aead
     aead_name = {1: "AES-128-GCM", 2: "AES-256-GCM", 3: "ChaCha20Poly1305"}[aead]
-    kem = dict(x25519=H.KEM_X25519, p256=H.KEM_P256, x448=H.KEM_X448,
-               p521=H.KEM_P521)[args.hpke_kem]
-    kem_name = dict(x25519="X25519", p256="P256", x448="X448", p521="P521")[args.hpke_kem]
-    kdf = H.KDF_SHA512 if args.hpke_kem in ("x448", "p521") else H.KDF_SHA256
-    kdf_name = "HKDF-SHA512" if kdf == H.KDF_SHA512 else "HKDF-SHA256"
+    kem = dict(x25519=H.KEM_X25519, p256=H.KEM_P256, x448=H.KEM_X448, p521=H.KEM_P521,
+               p384=H.KEM_P384)[args.hpke_kem]
+    kem_name = dict(x25519="X25519", p256="P256", x448="X448", p521="P521",
+                    p384="P384")[args.hpke_kem]
+    # each KEM with its own KDF in the key schedule too (the suites of the RFC 9180 vectors)
+    kdf = {"x448": H.KDF_SHA512, "p521": H.KDF_SHA512, "p384": H.KDF_SHA384}.get(args.hpke_kem,
+                                                                             H.KDF_SHA256)
+    kdf_name = {H.KDF_SHA256: "HKDF-SHA256", H.KDF_SHA384: "HKDF-SHA384",
+                H.KDF_SHA512: "HKDF-SHA512"}[kdf]
     d = H.make_batch_fast(uniq, 48, 32, seed=0x4A414E55, n_threads=cpu_threads(), aead=aead,
                           kem=kem, kdf=kdf)
     gen_s = time.perf_counter() - t0

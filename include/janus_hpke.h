@@ -10,19 +10,18 @@
  * duplicate / taskprov extension checks and the helper input share decode -- writing the decoded
  * helper input shares straight into the layout prio3_device_prepare[_aggregate] reads.
  *
- * Suites: mode_base with any KEM x KDF x AEAD of messages/src/lib.rs:770-853 except P-384:
+ * Suites: mode_base with any KEM x KDF x AEAD of messages/src/lib.rs:770-853:
  *   KEM  DHKEM(X25519, HKDF-SHA256) 0x0020, DHKEM(P-256, HKDF-SHA256) 0x0010 -- the two Janus's
  *        hpke crate implements (core/src/hpke.rs:414-466, 520-525) -- and DHKEM(X448,
  *        HKDF-SHA512) 0x0021, DHKEM(P-521, HKDF-SHA512) 0x0012 (pinned by the RFC 9180 vectors
- *        of core/src/test-vectors.json, which Janus's own test skips);
+ *        of core/src/test-vectors.json, which Janus's own test skips), and DHKEM(P-384,
+ *        HKDF-SHA384) 0x0011 (no RFC 9180 vector: pinned to the OpenSSL-composed oracle only);
  *   KDF  HKDF-SHA256 0x0001, HKDF-SHA384 0x0002, HKDF-SHA512 0x0003 (the key schedule's);
  *   AEAD AES-128-GCM 0x0001 (X25519 + AES-128-GCM is the configuration Janus generates by
  *        default, hpke.rs:260-300), AES-256-GCM 0x0002, ChaCha20Poly1305 0x0003.
- * Key and enc sizes follow the KEM (RFC 9180 7.1): private key 32 / 32 / 56 / 66 bytes (the NIST
- * curves' a big-endian scalar, 1 <= sk < n), public key = enc[n][Nenc] with Nenc 32 / 65 / 56 /
- * 133 (the NIST curves' uncompressed SEC1 points).  DHKEM(P-384, HKDF-SHA384) (0x0011; no RFC
- * 9180 vector in the reference) returns JANUS_HPKE_EUNSUPPORTED at creation; the host keeps its
- * CPU path for it.
+ * Key and enc sizes follow the KEM (RFC 9180 7.1): private key 32 / 32 / 56 / 66 / 48 bytes (the
+ * NIST curves' a big-endian scalar, 1 <= sk < n), public key = enc[n][Nenc] with Nenc 32 / 65 /
+ * 56 / 133 / 97 (the NIST curves' uncompressed SEC1 points).
  *
  * Conventions as in janus_prio3.h: plain pointers and sizes, caller-owned buffers, device
  * pointers (d_*) stream-ordered on a hipStream_t (NULL = the null stream), per-report failures
@@ -42,6 +41,7 @@ enum {
   JANUS_HPKE_KEM_P256_HKDF_SHA256 = 0x0010,
   JANUS_HPKE_KEM_X448_HKDF_SHA512 = 0x0021,
   JANUS_HPKE_KEM_P521_HKDF_SHA512 = 0x0012,
+  JANUS_HPKE_KEM_P384_HKDF_SHA384 = 0x0011,
   JANUS_HPKE_KDF_HKDF_SHA256 = 0x0001,
   JANUS_HPKE_KDF_HKDF_SHA384 = 0x0002,
   JANUS_HPKE_KDF_HKDF_SHA512 = 0x0003,
@@ -140,9 +140,10 @@ int janus_hpke_timing(janus_hpke_opener* opener, double* ms_total, uint32_t* lau
  * (tools/gen_p256_asm.py) against Python integers. */
 int janus_hpke_selftest_p256(int op, uint32_t n, const uint32_t* a, const uint32_t* b,
                              uint32_t* out);
-/* Test-only: the same for GF(2^448 - 2^224 - 1) (field 1, the X448 KEM; 14 words) and
- * GF(2^521 - 1) (field 2, the P-521 KEM; 17 words), operands canonical LE words below 2^448 /
- * 2^521 -- op 0 a*b, 1 a^2, 2 a+b, 3 a-b, 4 a*39081 (X448) or 8a (P-521), 5 a^(p-2); results
+/* Test-only: the same for GF(2^448 - 2^224 - 1) (field 1, the X448 KEM; 14 words),
+ * GF(2^521 - 1) (field 2, the P-521 KEM; 17 words) and GF(p384) (field 3, the P-384 KEM; 12
+ * words, Montgomery form inside), operands canonical LE words below 2^448 / 2^521 / 2^384 --
+ * op 0 a*b, 1 a^2, 2 a+b, 3 a-b, 4 a*39081 (X448) or 8a (P-521, P-384), 5 a^(p-2); results
  * canonical (fully reduced). */
 int janus_hpke_selftest_field(int field, int op, uint32_t n, const uint32_t* a, const uint32_t* b,
                               uint32_t* out);

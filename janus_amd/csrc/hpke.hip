@@ -25,6 +25,7 @@
 #include "aes_device.h"
 #include "p256_device.h"
 #include "p521_device.h"
+#include "p384_device.h"
 #include "ecdh_a3.h"
 #include "x448_device.h"
 #include "sha512_device.h"
@@ -600,15 +601,20 @@ struct HpkeParams {
   uint32_t sk448[14];           // X448: clamped scalar, LE words
   uint8_t pkraw[136];           // X448 / P-521: pkRm bytes (56 / 133)
   int8_t p521_dig[136];         // P-521: signed window digits of the private key (recode_w4)
+  int8_t p384_dig[96];          // P-384: the same (recode_w4, 96 digits)
+  uint64_t ipad0_384[8], opad0_384[8];  // HMAC-SHA384 midstates of the empty key (P-384 KEM)
 };
 
 // KEM constants (RFC 9180 7.1): Nenc (= Npk) and Nsecret, i.e. the Nh of the KEM's own KDF
 template <int KEM>
 struct KemC {
-  static constexpr int NENC = KEM == 0x20 ? 32 : KEM == 0x10 ? 65 : KEM == 0x21 ? 56 : 133;
-  static constexpr int NSS_W = (KEM == 0x20 || KEM == 0x10) ? 8 : 16;  // shared secret, 32-bit words
+  static constexpr int NENC =
+      KEM == 0x20 ? 32 : KEM == 0x10 ? 65 : KEM == 0x21 ? 56 : KEM == 0x11 ? 97 : 133;
+  static constexpr int NSS_W =  // shared secret (the KEM KDF's Nh), 32-bit words
+      (KEM == 0x20 || KEM == 0x10) ? 8 : KEM == 0x11 ? 12 : 16;
 };
 constexpr int P521_DIGITS = 131;  // w = 4 digits of a 521-bit key (130 windows + the top digit)
+constexpr int P384_DIGITS = 96;   // 95 windows of a 384-bit key + the top digit
 
 struct OpenArgs {
   uint32_t n, ct_stride, aad_stride, share_len;
@@ -752,17 +758,21 @@ __device__ __noinline__ void key_schedule_sha512(const HpkeParams& P, uint32_t k
   }
 }
 
-// DHKEM ExtractAndExpand with HKDF-SHA512 (the X448 and P-521 KEMs): dh (NDH bytes, a byte
-// accessor) and kem_context = enc || pkRm (NENC bytes each) -> shared_secret (16 BE words)
-template <int KEM, int NDH, class DhByte, class EncByte>
-DEV void eae_sha512(const HpkeParams& P, DhByte dh, EncByte enc, uint32_t ss[16]) {
-  constexpr int NENC = KemC<KEM>::NENC;
+// DHKEM ExtractAndExpand with HKDF-SHA512 (the X448 and P-521 KEMs) or HKDF-SHA384 (S384: the
+// P-384 KEM): dh (NDH bytes, a byte accessor) and kem_context = enc || pkRm (NENC bytes each)
+// -> shared_secret (Nh = 64 / 48 bytes: 16 / 12 BE words)
+template <int KEM, int NDH, bool S384 = false, class DhByte, class EncByte>
+DEV void eae_sha512(const HpkeParams& P, DhByte dh, EncByte enc, uint32_t* ss) {
+  constexpr int NENC = KemC<KEM>::NENC, NHW = S384 ? 6 : 8;  // Nh in 64-bit words
   uint64_t prk[8];
   {  // eae_prk = LabeledExtract("", "eae_prk", dh)
     HmacKey64 k0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) k0.ist[i] = P.ipad0_64[i], k0.ost[i] = P.opad0_64[i];
-    k0.out_words = 8;
+    for (int i = 0; i < 8; i++) {
+      k0.ist[i] = S384 ? P.ipad0_384[i] : P.ipad0_64[i];
+      k0.ost[i] = S384 ? P.opad0_384[i] : P.opad0_64[i];
+    }
+    k0.out_words = NHW;
     Msg64<(19 + NDH + 17 + 127) / 128 * 16> m;
     mz(m);
     mstr(m, 0, "HPKE-v1");
@@ -774,14 +784,14 @@ DEV void eae_sha512(const HpkeParams& P, DhByte dh, EncByte enc, uint32_t ss[16]
     for (int i = 0; i < NDH; i++) mbyte(m, 19 + i, dh(i));
     hmac64(k0, m, 19 + NDH, prk);
   }
-  // shared_secret = LabeledExpand(eae_prk, "shared_secret", enc || pkRm, 64)
+  // shared_secret = LabeledExpand(eae_prk, "shared_secret", enc || pkRm, Nh)
   HmacKey64 k;
-  hmac64_key(k, prk, 8, false);
+  hmac64_key(k, prk, NHW, S384);
   constexpr int LEN = 27 + 2 * NENC + 1;
   Msg64<(LEN + 17 + 127) / 128 * 16> m;
   mz(m);
   mbyte(m, 0, 0);
-  mbyte(m, 1, 64);
+  mbyte(m, 1, 8 * NHW);
   mstr(m, 2, "HPKE-v1");
   mstr(m, 9, "KEM");
   mbyte(m, 12, 0x00);
@@ -795,12 +805,16 @@ DEV void eae_sha512(const HpkeParams& P, DhByte dh, EncByte enc, uint32_t ss[16]
   uint64_t o[8];
   hmac64(k, m, LEN, o);
 #pragma unroll
-  for (int i = 0; i < 8; i++) ss[2 * i] = (uint32_t)(o[i] >> 32), ss[2 * i + 1] = (uint32_t)o[i];
+  for (int i = 0; i < NHW; i++) ss[2 * i] = (uint32_t)(o[i] >> 32), ss[2 * i + 1] = (uint32_t)o[i];
 }
 
 // the P-521 ECDH, out of line (one copy for the three kernel instances of the KEM)
 __device__ __noinline__ bool p521_dh(const int8_t* dig, const uint8_t* enc, uint8_t* dh) {
   return ecdh_a3::ecdh<p521::Field, P521_DIGITS, p521::FieldInl>(dig, enc, dh);
+}
+// the P-384 ECDH, out of line (its field products are out-of-line calls with register operands)
+__device__ __noinline__ bool p384_dh(const int8_t* dig, const uint8_t* enc, uint8_t* dh) {
+  return ecdh_a3::ecdh<p384::Field, P384_DIGITS>(dig, enc, dh);
 }
 
 // MODE 0: explicit AAD, plaintext out.  MODE 1: DAP helper input share with PUB bytes of
@@ -808,14 +822,16 @@ __device__ __noinline__ bool p521_dh(const int8_t* dig, const uint8_t* enc, uint
 // AEAD (P.aead): 1 AES-128-GCM, 2 AES-256-GCM, 3 ChaCha20Poly1305 (RFC 9180 7.3 ids).
 // KEM: 0x20 DHKEM(X25519, HKDF-SHA256) (enc: 32 bytes), 0x10 DHKEM(P-256, HKDF-SHA256) (enc: the
 // 65-byte uncompressed point), 0x21 DHKEM(X448, HKDF-SHA512) (56 bytes), 0x12 DHKEM(P-521,
-// HKDF-SHA512) (133 bytes).  The key-schedule KDF (P.kdf: HKDF-SHA256 / -384 / -512) and the AEAD
+// HKDF-SHA512) (133 bytes), 0x11 DHKEM(P-384, HKDF-SHA384) (97 bytes).  The key-schedule KDF (P.kdf: HKDF-SHA256 / -384 / -512) and the AEAD
 // are kernel arguments (wave-uniform): one instance per (MODE, PUB, KEM).
+// (amdgpu_waves_per_eu(2), which caps the P-384 instance's 354 VGPRs + AGPRs at 256: 5.15 against
+// 5.16 M/s, X25519 / P-521 unchanged -- not kept)
 #ifndef HPKE_WAVES  // A/B builds: e.g. -DHPKE_WAVES='__attribute__((amdgpu_waves_per_eu(3, 3)))'
 #define HPKE_WAVES
 #endif
 template <int MODE, int PUB, int KEM>
 __global__ __launch_bounds__(256) HPKE_WAVES void k_hpke_open(HpkeParams P, OpenArgs a) {
-  static_assert(KEM == 0x20 || KEM == 0x10 || KEM == 0x21 || KEM == 0x12, "KEM id");
+  static_assert(KEM == 0x20 || KEM == 0x10 || KEM == 0x21 || KEM == 0x12 || KEM == 0x11, "KEM id");
   const uint32_t AEAD = P.aead;
   __shared__ AesT T;
   aes_tables_init(T);
@@ -926,6 +942,13 @@ __global__ __launch_bounds__(256) HPKE_WAVES void k_hpke_open(HpkeParams P, Open
       return [w](int i) { return (w[i >> 2] >> (8 * (i & 3))) & 0xffu; };
     };
     eae_sha512<KEM, 56>(P, byte_of(dh), byte_of(encw), ss);
+  } else if constexpr (KEM == 0x11) {
+    // P-384 (SEC 1): enc is the 97-byte uncompressed point; the KEM's KDF is HKDF-SHA384
+    const uint8_t* ep = a.enc + 97 * (size_t)r;
+    uint8_t dh[48];
+    ok = p384_dh(P.p384_dig, ep, dh);
+    eae_sha512<KEM, 48, true>(P, [&](int i) { return (uint32_t)dh[i]; },
+                              [&](int i) { return (uint32_t)ep[i]; }, ss);
   } else {
     // P-521 (SEC 1): enc is the 133-byte uncompressed point
     const uint8_t* ep = a.enc + 133 * (size_t)r;
@@ -1309,11 +1332,16 @@ bool scalar_in_range(const uint8_t* sk, const uint8_t* n, size_t len) {
 }
 // KEM sizes (RFC 9180 7.1): private key, Nenc (= Npk); 0 = not a KEM this opener implements
 size_t kem_nsk(uint16_t kem) {
-  return kem == 0x20 || kem == 0x10 ? 32 : kem == 0x21 ? 56 : kem == 0x12 ? 66 : 0;
+  return kem == 0x20 || kem == 0x10 ? 32 : kem == 0x21 ? 56 : kem == 0x12 ? 66 : kem == 0x11 ? 48 : 0;
 }
 size_t kem_nenc(uint16_t kem) {
-  return kem == 0x20 ? 32 : kem == 0x10 ? 65 : kem == 0x21 ? 56 : kem == 0x12 ? 133 : 0;
+  return kem == 0x20 ? 32 : kem == 0x10 ? 65 : kem == 0x21 ? 56 : kem == 0x12 ? 133 : kem == 0x11 ? 97 : 0;
 }
+// P-384 group order n (SEC 2 2.5.1), big-endian
+const uint8_t kP384N[48] = {
+    0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+    0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xc7, 0x63, 0x4d, 0x81, 0xf4, 0x37, 0x2d, 0xdf,
+    0x58, 0x1a, 0x0d, 0xb2, 0x48, 0xb0, 0xa7, 0x7a, 0xec, 0xec, 0x19, 0x6a, 0xcc, 0xc5, 0x29, 0x73};
 // P-256 group order n (SEC 2), big-endian
 const uint8_t kP256N[32] = {0xff, 0xff, 0xff, 0xff, 0x00, 0x00, 0x00, 0x00, 0xff, 0xff, 0xff,
                             0xff, 0xff, 0xff, 0xff, 0xff, 0xbc, 0xe6, 0xfa, 0xad, 0xa7, 0x17,
@@ -1431,6 +1459,9 @@ int janus_hpke_opener_create(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id,
   if (kem_id == JANUS_HPKE_KEM_P521_HKDF_SHA512 &&
       (!scalar_in_range(private_key, kP521N, 66) || public_key[0] != 0x04))
     return JANUS_HPKE_EINVAL;
+  if (kem_id == JANUS_HPKE_KEM_P384_HKDF_SHA384 &&
+      (!scalar_in_range(private_key, kP384N, 48) || public_key[0] != 0x04))
+    return JANUS_HPKE_EINVAL;
   auto* o = new janus_hpke_opener();
   o->device = device;
   memset(&o->P, 0, sizeof(o->P));
@@ -1455,6 +1486,12 @@ int janus_hpke_opener_create(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id,
     k[55] |= 128;
     for (int i = 0; i < 14; i++) o->P.sk448[i] = le32(k + 4 * i);
     memcpy(o->P.pkraw, public_key, 56);
+  } else if (kem_id == JANUS_HPKE_KEM_P384_HKDF_SHA384) {  // 12 LE words, recoded against n
+    uint32_t kw[12], nw[12];
+    for (int i = 0; i < 12; i++)
+      kw[i] = be32(private_key + 4 * (11 - i)), nw[i] = be32(kP384N + 4 * (11 - i));
+    recode_w4(kw, nw, 12, P384_DIGITS, o->P.p384_dig);
+    memcpy(o->P.pkraw, public_key, 97);
   } else {  // P-521: the 66-byte big-endian scalar as 17 LE words, recoded against n
     uint8_t kb[68] = {0}, nb[68] = {0};
     memcpy(kb + 2, private_key, 66);
@@ -1503,6 +1540,9 @@ int janus_hpke_opener_create(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id,
     hmac64_key(k0, nullptr, 0, false);
     memcpy(o->P.ipad0_64, k0.ist, 64);
     memcpy(o->P.opad0_64, k0.ost, 64);
+    hmac64_key(k0, nullptr, 0, true);  // HKDF-SHA384 (eae_prk of the P-384 KEM)
+    memcpy(o->P.ipad0_384, k0.ist, 64);
+    memcpy(o->P.opad0_384, k0.ost, 64);
   }
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&o->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -1577,6 +1617,8 @@ static int launch_open(janus_hpke_opener* o, int mode, int pub, const OpenArgs& 
     JANUS_HPKE_LAUNCH(0x21)
   } else if (o->P.kem == JANUS_HPKE_KEM_P521_HKDF_SHA512) {
     JANUS_HPKE_LAUNCH(0x12)
+  } else if (o->P.kem == JANUS_HPKE_KEM_P384_HKDF_SHA384) {
+    JANUS_HPKE_LAUNCH(0x11)
   } else {
     JANUS_HPKE_LAUNCH(0x20)
   }
@@ -1856,6 +1898,26 @@ __global__ __launch_bounds__(256) void k_selftest_field(int field, int op, uint3
     x448::to_words(r, wr);
 #pragma unroll
     for (int k = 0; k < 14; k++) out[14 * (size_t)i + k] = wr[k];
+  } else if (field == 3) {  // P-384: operands below 2^384, into / out of Montgomery form
+    p384::fp x, y, r;
+#pragma unroll
+    for (int k = 0; k < 12; k++) x.v[k] = a[12 * (size_t)i + k], y.v[k] = b[12 * (size_t)i + k];
+    x = p384::mul_i(x, p384::kR2);
+    y = p384::mul_i(y, p384::kR2);
+    switch (op) {
+      case 0: r = p384::mul(x, y); break;
+      case 1: r = p384::sqr(x); break;
+      case 2: r = p384::add(x, y); break;
+      case 3: r = p384::sub(x, y); break;
+      case 4: r = p384::mul_small(x, 8); break;
+      default: r = p384::inv(x); break;
+    }
+    p384::fp one;
+#pragma unroll
+    for (int k = 0; k < 12; k++) one.v[k] = k ? 0u : 1u;
+    r = p384::mul_i(r, one);
+#pragma unroll
+    for (int k = 0; k < 12; k++) out[12 * (size_t)i + k] = r.v[k];
   } else {
     uint32_t wa[17], wb[17], wr[17];
 #pragma unroll
@@ -1880,9 +1942,9 @@ extern "C" {
 
 int janus_hpke_selftest_field(int field, int op, uint32_t n, const uint32_t* a, const uint32_t* b,
                               uint32_t* out) {
-  if ((field != 1 && field != 2) || op < 0 || op > 5) return JANUS_HPKE_EINVAL;
+  if (field < 1 || field > 3 || op < 0 || op > 5) return JANUS_HPKE_EINVAL;
   if (n == 0) return JANUS_HPKE_OK;
-  const size_t m = (size_t)n * (field == 1 ? 14 : 17) * 4;
+  const size_t m = (size_t)n * (field == 1 ? 14 : field == 3 ? 12 : 17) * 4;
   void *da = nullptr, *db = nullptr, *dout = nullptr;
   int rc = JANUS_HPKE_OK;
   if (hipMalloc(&da, m) != hipSuccess || hipMalloc(&db, m) != hipSuccess ||

@@ -18,12 +18,13 @@ KEM_X25519_HKDF_SHA256 = 0x0020
 KEM_P256_HKDF_SHA256 = 0x0010
 KEM_X448_HKDF_SHA512 = 0x0021
 KEM_P521_HKDF_SHA512 = 0x0012
+KEM_P384_HKDF_SHA384 = 0x0011
 KDF_HKDF_SHA256 = 0x0001
 KDF_HKDF_SHA384 = 0x0002
 KDF_HKDF_SHA512 = 0x0003
 # Nenc (= Npk) per KEM (RFC 9180 7.1)
 NENC = {KEM_X25519_HKDF_SHA256: 32, KEM_P256_HKDF_SHA256: 65, KEM_X448_HKDF_SHA512: 56,
-        KEM_P521_HKDF_SHA512: 133}
+        KEM_P521_HKDF_SHA512: 133, KEM_P384_HKDF_SHA384: 97}
 AEAD_AES_128_GCM = 0x0001
 AEAD_AES_256_GCM = 0x0002
 AEAD_CHACHA20_POLY1305 = 0x0003

@@ -72,11 +72,11 @@ def _p(b):
     return C.cast(C.c_char_p(bytes(b)), C.c_void_p)
 
 
-KEM_X25519, KEM_P256, KEM_X448, KEM_P521 = 0x20, 0x10, 0x21, 0x12
+KEM_X25519, KEM_P256, KEM_X448, KEM_P521, KEM_P384 = 0x20, 0x10, 0x21, 0x12, 0x11
 KDF_SHA256, KDF_SHA384, KDF_SHA512 = 1, 2, 3
 # RFC 9180 7.1: Nsk, Nenc (= Npk; the NIST curves' uncompressed points)
-NSK = {KEM_X25519: 32, KEM_P256: 32, KEM_X448: 56, KEM_P521: 66}
-NENC = {KEM_X25519: 32, KEM_P256: 65, KEM_X448: 56, KEM_P521: 133}
+NSK = {KEM_X25519: 32, KEM_P256: 32, KEM_X448: 56, KEM_P521: 66, KEM_P384: 48}
+NENC = {KEM_X25519: 32, KEM_P256: 65, KEM_X448: 56, KEM_P521: 133, KEM_P384: 97}
 
 
 def nenc(kem: int) -> int:
@@ -95,9 +95,10 @@ def kem_public(sk: bytes, kem=KEM_X25519) -> bytes:
 
 
 def kem_private(rng, kem=KEM_X25519) -> bytes:
-    """A random private key (P-256: below 2^255, P-521: below 2^520, hence below the order)."""
+    """A random private key (P-256 / P-384: below 2^255 / 2^383, P-521: below 2^520, hence below
+    the order)."""
     sk = bytearray(rng.integers(0, 256, NSK[kem], dtype=np.uint8).tobytes())
-    if kem == KEM_P256:
+    if kem in (KEM_P256, KEM_P384):
         sk[0] &= 0x7F
     if kem == KEM_P521:
         sk[0] = 0

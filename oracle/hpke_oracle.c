@@ -4,7 +4,7 @@
  *
  * HPKE base mode (RFC 9180 §5.1, §5.2) with DHKEM(X25519, HKDF-SHA256) (§4.1, §7.1),
  * HKDF-SHA256 and AES-128-GCM -- the suite Janus generates by default -- or any other suite of
- * KEM {X25519, P-256, X448, P-521} x KDF {HKDF-SHA256, -SHA384, -SHA512} x AEAD {AES-128-GCM,
+ * KEM {X25519, P-256, X448, P-521, P-384} x KDF {HKDF-SHA256, -SHA384, -SHA512} x AEAD {AES-128-GCM,
  * AES-256-GCM, ChaCha20Poly1305} (pinned by the 24 RFC 9180 base-mode vectors of
  * core/src/test-vectors.json; the HKDF-SHA384 suites have none there and rest on OpenSSL)
  * (/root/reference/core/src/hpke.rs:260-280, generate_test_hpke_config_and_private_key), whose
@@ -35,15 +35,17 @@
 enum { HPKE_OK = 0, HPKE_DECRYPT_ERROR = 4, HPKE_INVALID_MESSAGE = 8 };
 
 /* KEMs (RFC 9180 7.1): 0x0020 DHKEM(X25519, HKDF-SHA256), 0x0010 DHKEM(P-256, HKDF-SHA256),
- * 0x0021 DHKEM(X448, HKDF-SHA512), 0x0012 DHKEM(P-521, HKDF-SHA512) (messages/src/lib.rs:770-784);
+ * 0x0021 DHKEM(X448, HKDF-SHA512), 0x0012 DHKEM(P-521, HKDF-SHA512), 0x0011 DHKEM(P-384,
+ * HKDF-SHA384) (messages/src/lib.rs:770-784; P-384 has no RFC 9180 vector: OpenSSL is its pin);
  * Nsk, Nenc (= Npk, the NIST curves' uncompressed points), Ndh, and the KEM's own KDF. */
 typedef struct {
   uint16_t id;
   size_t nsk, nenc, ndh;
-  int kdf; /* 1 HKDF-SHA256, 3 HKDF-SHA512 */
+  int kdf; /* 1 HKDF-SHA256, 2 HKDF-SHA384, 3 HKDF-SHA512 */
 } Kem;
 static const Kem KEMS[] = {{0x20, 32, 32, 32, 1}, {0x10, 32, 65, 32, 1},
-                           {0x21, 56, 56, 56, 3}, {0x12, 66, 133, 66, 3}};
+                           {0x21, 56, 56, 56, 3}, {0x12, 66, 133, 66, 3},
+                           {0x11, 48, 97, 48, 2}};
 static const Kem* kem_of(uint16_t kem) {
   for (size_t i = 0; i < sizeof(KEMS) / sizeof(KEMS[0]); i++)
     if (KEMS[i].id == kem) return &KEMS[i];
@@ -161,6 +163,7 @@ static int kem_dh(uint16_t kem, const uint8_t* sk, const uint8_t* pk, uint8_t* o
     case 0x21: return xdh(EVP_PKEY_X448, 56, sk, pk, out);
     case 0x10: return ec_dh(NID_X9_62_prime256v1, 32, sk, pk, out);
     case 0x12: return ec_dh(NID_secp521r1, 66, sk, pk, out);
+    case 0x11: return ec_dh(NID_secp384r1, 48, sk, pk, out);
   }
   return -1;
 }
@@ -171,6 +174,7 @@ int hpke_kem_public(uint16_t kem, const uint8_t* sk, uint8_t* pk) {
     case 0x21: return xdh_public(EVP_PKEY_X448, 56, sk, pk);
     case 0x10: return ec_public(NID_X9_62_prime256v1, 32, sk, pk);
     case 0x12: return ec_public(NID_secp521r1, 66, sk, pk);
+    case 0x11: return ec_public(NID_secp384r1, 48, sk, pk);
   }
   return -1;
 }
@@ -511,6 +515,7 @@ static void* gen_run(void* arg) {
     memset(ct, 0, j->stride);
     if (j->kem == 0x10) skE[0] &= 0x7f; /* a P-256 scalar below the group order */
     if (j->kem == 0x12) skE[0] = 0;     /* a P-521 scalar below the group order */
+    if (j->kem == 0x11) skE[0] &= 0x7f; /* a P-384 scalar below the group order */
     hpke_seal_suite(j->kem, j->kdf, j->aead, j->pkR, skE, INFO, sizeof(INFO), aad, al, pt, l,
                     j->enc + kem_nenc(j->kem) * (size_t)r, ct);
     j->ct_len[r] = (uint32_t)(l + 16);

@@ -45,6 +45,10 @@ PRIM = dict(
     # GF(2^521 - 1) in 18 x 29-bit limbs (p521_device.h): 324 (171 + 18 doublings for squares)
     # v_mad_u64_u32, the 35-column carry (~105), the 2^522 = 2 fold and a limb carry (~90)
     p521_mul=520, p521_sqr=385, p521_add=72,
+    # GF(p384) Montgomery (CIOS) in 12 saturated words: 144 + 130 v_mad_u64_u32 (the reduction
+    # skips p's two zero words) + one carry add each, the conditional subtract (~36); squares
+    # run as products.  An add / sub is a 12-word carry chain + the conditional correction
+    p384_mul=600, p384_add=48,
     sha512_compress=4000,  # 80 rounds x ~33 (64-bit words on 32-bit halves) + 64 x ~22 schedule
     aes_round=36,      # T-table round: 16 byte extracts + 16 XORs + 4 key XORs (lookups are LDS)
     ghash_block=320,   # 4-bit table (Shoup) GF(2^128) multiply: 32 nibble steps x ~10
@@ -224,6 +228,16 @@ def hpke_model(kem: str, aead: int, pt_len: int = 48 + 8 + 32 + 16, aad_len: int
                 8 * PRIM["fe448_add"] + 64)
         dh = 448 * step + 446 * PRIM["fe448_sqr"] + 14 * PRIM["fe448_mul"] + 40
         compress = 21
+    elif kem == "p384":
+        M, S, A = PRIM["p384_mul"], PRIM["p384_mul"], PRIM["p384_add"]
+        # ecdh_a3.h as for P-521 (Montgomery products, squares as products), 96 digits
+        dbl = 4 * M + 4 * S + 13 * A
+        madd = 8 * M + 3 * S + 12 * A
+        inv = 385 * S + 15 * M                 # p - 2 addition chain (p384_device.h inv)
+        check = 3 * M + 2 * S + 4 * A
+        table = 5 * dbl + 7 * madd + inv + 39 * M + 7 * S
+        dh = check + table + 94 * (4 * dbl + madd) + 5 * dbl + madd + inv + M + S + 2 * M
+        compress = 23  # HKDF-SHA384: kem_context = enc || pkR is 194 bytes
     elif kem == "p521":
         M, S, A = PRIM["p521_mul"], PRIM["p521_sqr"], PRIM["p521_add"]
         # ecdh_a3.h, counted from its code (the r4 model charged a 12M + 4S
@@ -258,7 +272,7 @@ def hpke_model(kem: str, aead: int, pt_len: int = 48 + 8 + 32 + 16, aad_len: int
         rounds = 10 if aead == 1 else 14
         aead_ops = (ct_blocks + 2) * rounds * PRIM["aes_round"] + rounds * 20 + \
             (ct_blocks + -(-aad_len // 16) + 1) * PRIM["ghash_block"]
-    kdf = compress * PRIM["sha512_compress" if kem in ("x448", "p521") else "sha256_compress"]
+    kdf = compress * PRIM["sha512_compress" if kem in ("x448", "p521", "p384") else "sha256_compress"]
     return dict(dh=dh, kdf=kdf, aead=aead_ops, total=dh + kdf + aead_ops)
 
 

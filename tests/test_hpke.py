@@ -431,12 +431,14 @@ def test_gpu_rfc9180_all_vectors(v):
 @pytest.mark.gpu
 @pytest.mark.parametrize("kem,kdf,aead", [(0x20, 2, 1), (0x20, 3, 3), (0x10, 2, 2), (0x10, 3, 1),
                                           (0x21, 1, 1), (0x21, 2, 3), (0x21, 3, 2),
-                                          (0x12, 3, 1), (0x12, 1, 3), (0x12, 2, 2)])
+                                          (0x12, 3, 1), (0x12, 1, 3), (0x12, 2, 2),
+                                          (0x11, 2, 1), (0x11, 1, 3), (0x11, 3, 2)])
 def test_gpu_suite_input_shares_match_oracle(kem, kdf, aead):
-    """Janus-shaped helper input shares under every KEM and key-schedule KDF (HKDF-SHA384 has
-    no RFC vector: the OpenSSL-composed oracle is its pin), tampered reports included."""
+    """Janus-shaped helper input shares under every KEM and key-schedule KDF (HKDF-SHA384 and
+    DHKEM(P-384, HKDF-SHA384) have no RFC vector: the OpenSSL-composed oracle is their pin),
+    tampered reports included."""
     from janus_amd import hpke as G
-    n = 70 if kem in (0x21, 0x12) else 130
+    n = 70 if kem in (0x21, 0x12, 0x11) else 130
     rng = np.random.default_rng(kem * 7 + kdf * 3 + aead)
     d = H.make_batch(n, 48, 32, seed=kem + kdf + aead, aead=aead, kem=kem, kdf=kdf)
     d, exp = _tamper(d, rng)
@@ -453,22 +455,25 @@ def test_gpu_suite_input_shares_match_oracle(kem, kdf, aead):
 
 P448 = 2**448 - 2**224 - 1
 P521 = 2**521 - 1
+P384 = 2**384 - 2**128 - 2**96 + 2**32 - 1
+P384_N = 0xffffffffffffffffffffffffffffffffffffffffffffffffc7634d81f4372ddf581a0db248b0a77aecec196accc52973
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("field", [1, 2])
+@pytest.mark.parametrize("field", [1, 2, 3])
 @pytest.mark.parametrize("op", range(6))
 def test_gpu_x448_p521_field_ops_match_python(field, op):
     """GF(2^448 - 2^224 - 1) (28-bit limbs) and GF(2^521 - 1) (29-bit limbs), unsaturated column
-    products with the Solinas / Mersenne folds, on operands below 2^448 / 2^521 (so also in
-    [p, 2^bits)) and edge values, against Python integers: results canonical."""
+    products with the Solinas / Mersenne folds, and GF(p384) (12 saturated words, Montgomery
+    form), on operands below 2^448 / 2^521 / 2^384 (so also in [p, 2^bits)) and edge values,
+    against Python integers: results canonical."""
     import ctypes as C
     import random
     from janus_amd import hpke as G
-    P, bits, nw = (P448, 448, 14) if field == 1 else (P521, 521, 17)
+    P, bits, nw = {1: (P448, 448, 14), 2: (P521, 521, 17), 3: (P384, 384, 12)}[field]
     edge = [0, 1, 2, P - 1, P - 2, P, 2**bits - 1, 2**bits - 2, (P - 1) // 2, 2**(bits - 1),
-            2**224 if field == 1 else 2**260, 2**224 - 1 if field == 1 else 2**29 - 1]
-    if field == 1:
+            {1: 2**224, 2: 2**260, 3: 2**128}[field], {1: 2**224 - 1, 2: 2**29 - 1, 3: 2**96}[field]]
+    if field != 2:
         edge.append(P + 1)  # (for P-521, P + 1 = 2^521 is past the operand range)
     rnd = random.Random(100 * field + op)
     n = 2048 if op == 5 else 1 << 15
@@ -484,10 +489,52 @@ def test_gpu_x448_p521_field_ops_match_python(field, op):
     assert G._lib().janus_hpke_selftest_field(field, op, n, Pp(A), Pp(B), Pp(out)) == 0
     got = [int.from_bytes(out[nw * i:nw * i + nw].tobytes(), "little") for i in range(n)]
     small = 39081 if field == 1 else 8
+    if field == 3 and op in (2, 3):  # P-384's add / sub take canonical operands (Montgomery form)
+        a = [x % P for x in a]
+        bb = [x % P for x in bb]
+        A, B = enc(a), enc(bb)
     fn = [lambda x, y: x * y, lambda x, y: x * x, lambda x, y: x + y, lambda x, y: x - y,
           lambda x, y: small * x, lambda x, y: pow(x, P - 2, P)][op]
     bad = [i for i in range(n) if got[i] != fn(a[i], bb[i]) % P]
     assert not bad, f"field {field} op {op}: {len(bad)} wrong, first a={a[bad[0]]:x} b={bb[bad[0]]:x}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sk", [1, 2, 3, 6, 15, 16, 30, P384_N - 1, P384_N - 2, P384_N - 6,
+                                P384_N - 30, P384_N - 31, 2 ** 383, 0x1234567 << 300])
+def test_gpu_p384_edge_private_keys(sk):
+    """DHKEM(P-384, HKDF-SHA384): the fixed signed window of ecdh_a3.h over the host recoding
+    (96 digits) for even keys (run as n - sk), keys whose last window meets the doubling case,
+    tiny and near-n keys, against the OpenSSL oracle (no RFC 9180 vector covers this KEM)."""
+    from janus_amd import hpke as G
+    skR = sk.to_bytes(48, "big")
+    d = H.make_batch(8, 48, 32, seed=sk % 991, skR=skR, kem=H.KEM_P384, kdf=2)
+    ref_sh, ref_st = H.open_input_shares(d["skR"], d["pkR"], d["task_id"], d["enc"], d["ct"],
+                                         d["ct_len"], d["report_ids"], d["times"], d["pubs"], 48,
+                                         kem=H.KEM_P384, kdf=2)
+    assert (ref_st == 0).all()
+    op = G.HpkeOpener(d["skR"], d["pkR"], kem_id=G.KEM_P384_HKDF_SHA384, kdf_id=2)
+    sh, st = op.open_input_shares(d["task_id"], d["enc"], d["ct"], d["ct_len"], d["report_ids"],
+                                  d["times"], d["pubs"], 48)
+    np.testing.assert_array_equal(st, ref_st)
+    np.testing.assert_array_equal(sh, ref_sh)
+
+
+def test_p384_opener_rejects_bad_keys():
+    """DeserializePrivateKey (1 <= sk < n) and the public key's SEC 1 prefix for the P-384 KEM:
+    creation fails with JANUS_HPKE_EINVAL before any device call (runs without a GPU)."""
+    import ctypes as C
+    from janus_amd import hpke as G
+    lib = G._lib()
+    out = C.c_void_p()
+    pk = b"\x04" + bytes(96)
+    for sk in (bytes(48), P384_N.to_bytes(48, "big"), (P384_N + 1).to_bytes(48, "big")):
+        assert lib.janus_hpke_opener_create(0x11, 2, 1, sk, 48, pk, 97, None, 0, 0,
+                                            C.byref(out)) == -1
+    assert lib.janus_hpke_opener_create(0x11, 2, 1, (5).to_bytes(48, "big"), 48,
+                                        b"\x02" + bytes(96), 97, None, 0, 0, C.byref(out)) == -1
+    assert lib.janus_hpke_opener_create(0x11, 2, 1, (5).to_bytes(48, "big"), 47, pk, 97, None,
+                                        0, 0, C.byref(out)) == -1
 
 
 @pytest.mark.gpu
