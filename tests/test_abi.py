@@ -47,12 +47,14 @@ def test_dap_header_declares_the_exported_set():
 
 
 def test_hpke_unsupported_suite_is_refused():
-    """P-384 (no RFC 9180 vector in the reference) and unknown KDF / AEAD ids stay on the host
-    path: creation says EUNSUPPORTED before any GPU call; a NIST-curve key outside [1, n) or a
-    key of the wrong length is EINVAL (no GPU call)."""
+    """Unknown KEM / KDF / AEAD ids stay on the host path: creation says EUNSUPPORTED before any
+    GPU call; a NIST-curve key outside [1, n) or a key of the wrong length is EINVAL (no GPU
+    call).  (P-384, 0x0011, opens on the device since r05: tests/test_hpke.py.)"""
     from janus_amd import hpke as H
     with pytest.raises(NotImplementedError):
-        H.HpkeOpener(bytes(48), bytes(97), kem_id=0x0011)   # P-384
+        H.HpkeOpener(bytes(48), bytes(97), kem_id=0x0013)   # no such KEM
+    with pytest.raises(RuntimeError, match="rc=-1"):
+        H.HpkeOpener(bytes(48), b"\x04" + bytes(96), kem_id=0x0011)  # P-384 sk = 0
     with pytest.raises(NotImplementedError):
         H.HpkeOpener(bytes(32), bytes(32), kdf_id=0x0004)   # no such KDF
     with pytest.raises(NotImplementedError):
