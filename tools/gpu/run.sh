@@ -76,6 +76,7 @@ for step in "$@"; do
     bench hpke_p256 --role hpke --hpke-kem p256 --reports 262144
     bench hpke_x448 --role hpke --hpke-kem x448 --reports 262144
     bench hpke_p521 --role hpke --hpke-kem p521 --reports 262144
+    bench hpke_p384 --role hpke --hpke-kem p384 --reports 65536
     bench pipeline --role pipeline --reports 1048576
     bench mp64 --role mp64 --reports 1000000 ;;
   prof)
