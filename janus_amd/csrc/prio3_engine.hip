@@ -874,11 +874,9 @@ __global__ __launch_bounds__(256) void k_leader_unpack(DevParams p, InPtrs in, S
 // sponge block's 64 x 11-12 elements through LDS with coalesced row segments instead (one wave
 // per block, 12 KiB, 3 waves per SIMD) took 4.12 ms.
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256, JR_OCC) void k_leader_jr(DevParams p, InPtrs in, Scratch sc,
-                                                         uint8_t* status, uint32_t* wpart,
-                                                         uint32_t* wseg) {
+DEV void leader_jr_body(const DevParams& p, const InPtrs& in, const Scratch& sc,
+                        uint8_t* status, uint32_t* wpart, uint32_t* wseg, const uint32_t r) {
   typedef Fp128 F;
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
   const bool acc = wpart != nullptr && __all(r < p.n);  // wave-uniform
   if (r >= p.n) return;
@@ -1045,6 +1043,11 @@ __global__ __launch_bounds__(256, JR_OCC) void k_leader_jr(DevParams p, InPtrs i
     const bool fuse = acc && __all(!bad);
     if (lane == 0) wseg[r >> 6] = fuse ? 0u : 0xffffffffu;
   }
+}
+__global__ __launch_bounds__(256, JR_OCC) void k_leader_jr(DevParams p, InPtrs in, Scratch sc,
+                                                         uint8_t* status, uint32_t* wpart,
+                                                         uint32_t* wseg) {
+  leader_jr_body(p, in, sc, status, wpart, wseg, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // Leader slow path: reports whose query or joint-rand expansion hit a rejection-sampling
@@ -1560,6 +1563,14 @@ __device__ __forceinline__ void query_h_body(const DevParams& p, const InPtrs& i
     } else if (p.slow_defer && sc.flag[r]) {
       return;
     }
+  } else {
+    // the fused leader kernel (k_leader_prep) defers a flagged report; k_leader_slowfix redoes
+    // its randomness and this query runs again for exactly those reports (p.redo)
+    if (p.redo) {
+      if (!sc.flag[r]) return;
+    } else if (p.slow_defer && sc.flag[r]) {
+      return;
+    }
   }
   const size_t ld = p.ld;
   const uint32_t A = p.arity, C = p.chunk, M = p.meas_len, K = p.calls;
@@ -1863,6 +1874,20 @@ __global__ __launch_bounds__(256, 3) void k_prep_h(DevParams p, InPtrs in, Scrat
   xofd_body<FUSE, false, PULL>(p, in, sc, r);
   // two wires per sweep: 3 and 4 spill inside the wire loop
   query_h_body<2, 32>(p, in, sc, out, r);
+}
+
+// k_leader_prep<PP>: the leader's prepare_init of Prio3Histogram / SumVec in one launch, as
+// k_prep_h is the helper's: leader_jr_body (the explicit share streamed once into the joint-rand
+// sponge and the SoA scratch) and then query_h_body<2, PP, 1> on the scratch rows the same lane
+// has just written, so one wave's memory-bound share streaming runs beside other waves' query.
+// Flagged reports are deferred to k_leader_slowfix + a k_query_h redo launch.
+template <int PP>
+__global__ __launch_bounds__(256, 3) void k_leader_prep(DevParams p, InPtrs in, Scratch sc,
+                                                        OutPtrs out, uint32_t* wpart,
+                                                        uint32_t* wseg) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  leader_jr_body(p, in, sc, out.status, wpart, wseg, r);
+  query_h_body<2, PP, 1>(p, in, sc, out, r);
 }
 
 // k_prep_sum<NPH>: the same for Prio3Sum (P = 16 NPH): the dual-state XOF and k_query_sum's body
@@ -3516,6 +3541,9 @@ static int leader_init_fpvec(prio3_engine* e, Run* R, const uint8_t* d_nonces,
   return PRIO3_OK;
 }
 
+#ifndef LEADER_FUSED
+#define LEADER_FUSED 1  // k_leader_prep (k_leader_jr + the query in one launch); 0: two kernels (A/B)
+#endif
 // vk_slot / vk_tab (nullable): per-report verify keys of a coalesced group of several tasks
 static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
                            const uint8_t* d_public_shares, const uint8_t* d_leader_input_shares,
@@ -3545,10 +3573,25 @@ static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
     OutPtrs out{d_prep_shares, d_status};
     const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
     // R->lfused: the wave partials of the share for segment 0, fixed up at accumulate
-    TIMED(e, st, "k_leader_jr",
-          (k_leader_jr<<<blocks, 256, 0, st>>>(dp, in, R->sc, d_status,
-                                               R->lfused ? R->wpart : nullptr,
-                                               R->lfused ? R->wseg : nullptr)));
+    uint32_t* wp = R->lfused ? R->wpart : nullptr;
+    uint32_t* wsg = R->lfused ? R->wseg : nullptr;
+    if (LEADER_FUSED) {  // one launch; flagged reports redone after k_leader_slowfix
+      DevParams d1 = dp;
+      d1.slow_defer = 1;
+      if (dp.P == 32)
+        TIMED(e, st, "k_leader_prep",
+              (k_leader_prep<32><<<blocks, 256, 0, st>>>(d1, in, R->sc, out, wp, wsg)));
+      else if (dp.P == 16)
+        TIMED(e, st, "k_leader_prep",
+              (k_leader_prep<16><<<blocks, 256, 0, st>>>(d1, in, R->sc, out, wp, wsg)));
+      else
+        TIMED(e, st, "k_leader_prep",
+              (k_leader_prep<8><<<blocks, 256, 0, st>>>(d1, in, R->sc, out, wp, wsg)));
+      dp.redo = 1;
+    } else {
+      TIMED(e, st, "k_leader_jr",
+            (k_leader_jr<<<blocks, 256, 0, st>>>(dp, in, R->sc, d_status, wp, wsg)));
+    }
     TIMED(e, st, "k_leader_slowfix",
           (k_leader_slowfix<<<blocks64, 64, 0, st>>>(dp, in, R->sc)));
     if (dp.P == 32)
