@@ -3609,8 +3609,12 @@ static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
     in.vk_tab = vk_tab;
     OutPtrs out{d_prep_shares, d_status};
     const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
-    TIMED(e, st, "k_leader_jr",
-          (k_leader_jr<<<blocks, 256, 0, st>>>(dp, in, R->sc, d_status, nullptr, nullptr)));
+    // (k_leader_jr's per-lane row streaming loses here: the short share leaves little Keccak
+    // to hide the 1.6 KB rows' uncoalesced reads -- 2.63 against 1.30 + 0.46 ms per 1.25 M)
+    TIMED(e, st, "k_leader_unpack",
+          (k_leader_unpack<<<(n + 63) / 64, 256, 0, st>>>(dp, in, R->sc, d_status, nullptr,
+                                                         nullptr)));
+    TIMED(e, st, "k_jrpart", (k_jrpart<false, true><<<blocks, 256, 0, st>>>(dp, in, R->sc)));
     TIMED(e, st, "k_leader_slowfix",
           (k_leader_slowfix<<<blocks64, 64, 0, st>>>(dp, in, R->sc)));
     bool ok = false;
