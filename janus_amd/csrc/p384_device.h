@@ -35,54 +35,38 @@ constexpr fp kBR = {{0x9d412dccu, 0x08118871u, 0x7a4c32ecu, 0xf729add8u, 0x19200
                      0x77f2209bu, 0x94938ae2u, 0xe3374beeu, 0x1f022094u, 0xb62b21f4u,
                      0x604fbff9u, 0xcd08114bu}};
 
-// s (NL words) + carry-out c -> s mod p, given s + c 2^384 < 2p
+// s (NL words) + carry-out c -> s mod p, given s + c 2^384 < 2p.  The carry chains are
+// __builtin_addc / __builtin_subc (one v_add_co / v_addc / v_sub_co / v_subb each; int64
+// arithmetic here compiled to 64-bit adds and moves, 155 instructions per add).
 DEV fp cond_sub(const uint32_t s[NL], uint32_t c) {
-  uint32_t t[NL];
-  int64_t br = 0;
+  uint32_t t[NL], br = 0;
 #pragma unroll
-  for (int i = 0; i < NL; i++) {
-    const int64_t d = (int64_t)s[i] - kP[i] + br;
-    t[i] = (uint32_t)d;
-    br = d >> 32;  // 0 or -1
-  }
-  const bool use_t = c != 0 || br == 0;
+  for (int i = 0; i < NL; i++) t[i] = __builtin_subc(s[i], kP[i], br, &br);
+  // s - p borrowed past the carry-out: keep s
+  const bool keep_s = br > c;
   fp r;
 #pragma unroll
-  for (int i = 0; i < NL; i++) r.v[i] = use_t ? t[i] : s[i];
+  for (int i = 0; i < NL; i++) r.v[i] = keep_s ? s[i] : t[i];
   return r;
 }
 
 DEV fp add(const fp& a, const fp& b) {
-  uint32_t s[NL];
-  uint64_t c = 0;
+  uint32_t s[NL], c = 0;
 #pragma unroll
-  for (int i = 0; i < NL; i++) {
-    c += (uint64_t)a.v[i] + b.v[i];
-    s[i] = (uint32_t)c;
-    c >>= 32;
-  }
-  return cond_sub(s, (uint32_t)c);
+  for (int i = 0; i < NL; i++) s[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
+  return cond_sub(s, c);
 }
 
 DEV fp sub(const fp& a, const fp& b) {
-  uint32_t d[NL];
-  int64_t br = 0;
+  uint32_t d[NL], br = 0;
 #pragma unroll
-  for (int i = 0; i < NL; i++) {
-    const int64_t x = (int64_t)a.v[i] - b.v[i] + br;
-    d[i] = (uint32_t)x;
-    br = x >> 32;
-  }
+  for (int i = 0; i < NL; i++) d[i] = __builtin_subc(a.v[i], b.v[i], br, &br);
   // borrow: add p back
-  const uint32_t m = br ? 0xffffffffu : 0u;
+  const uint32_t m = 0u - br;
   fp r;
-  uint64_t c = 0;
+  uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < NL; i++) {
-    c += (uint64_t)d[i] + (kP[i] & m);
-    r.v[i] = (uint32_t)c;
-    c >>= 32;
-  }
+  for (int i = 0; i < NL; i++) r.v[i] = __builtin_addc(d[i], kP[i] & m, c, &c);
   return r;
 }
 
