@@ -210,10 +210,12 @@ def main():
                          "trip) or prio3_helper_prepare_batch + prio3_accumulate (two)")
     ap.add_argument("--tasks", type=int, default=4,
                     help="--role jobs: tasks (verify keys) of the VDAF instance the jobs rotate over")
-    ap.add_argument("--jobs-role", choices=["helper", "leader", "hpke"], default="helper",
+    ap.add_argument("--jobs-role", choices=["helper", "leader", "hpke", "init"], default="helper",
                     help="--role jobs: the helper's prepare + aggregate per job (default), the "
-                         "leader's prepare_init + prepare_next + aggregate per job, or the "
-                         "helper's HPKE open of each job's input shares")
+                         "leader's prepare_init + prepare_next + aggregate per job, the "
+                         "helper's HPKE open of each job's input shares, or the helper's whole "
+                         "loop body from sealed input shares in one call (init; with the two-call "
+                         "composition measured beside it)")
     ap.add_argument("--exec-heavy", type=int, default=0,
                     help="--role jobs: the executors' light/heavy switch in reports inside them "
                          "(prio3_executor_control / janus_hpke_executor_control \"heavy\"; 0: the "
@@ -514,12 +516,19 @@ def secondary_lines(args) -> dict:
                     ("secondary_jobs_leader", lambda: leader_jobs_line(128, 500, 2048, 4,
                                                                        cpu_seconds=cs)),
                     ("secondary_jobs_hpke", lambda: hpke_jobs_line(128, 500, 2048, 4,
-                                                                   cpu_seconds=cs))):
+                                                                   cpu_seconds=cs)),
+                    # the whole loop body from sealed input shares in one call,
+                    # with the two-call composition measured beside it in the same run
+                    ("secondary_jobs_init", lambda: init_jobs_line(128, 500, 2048, 4,
+                                                                   cpu_seconds=cs)),
+                    ("secondary_jobs_init_16t", lambda: init_jobs_line(16, 500, 1024, 4,
+                                                                       cpu_seconds=cs))):
         try:
             j = fn()
             out[key] = dict(metric=j["metric"], value=j["value"], unit=j["unit"],
                             ms_per_step=j["ms_per_step"], config=j["config"],
                             coalescing=j["coalescing"], placement=j.get("placement"),
+                            two_call=j.get("two_call"),
                             roofline={k: j["roofline"][k] for k in ("bound", "achieved", "peak",
                                                                     "unit", "frac")},
                             checks=j["checks"], cpu_baseline=j["cpu_baseline"])
@@ -557,6 +566,26 @@ def check_combined(eng, args, world, n, times_of, combiner) -> bool:
         np.array_equal(combiner.out_intervals.cpu().numpy().view(np.uint64), iv))
 
 
+def _cpu_waves(fn, cores: int, js: int, avail: int, min_s: float = 2.0):
+    """a jobs line's CPU baseline on WHOLE waves -- fn(m) runs the restatement
+    over the first m reports as jobs of js, one job per worker thread (binary_utils.rs:514-518,
+    aggregator.rs:2100), so m is a multiple of cores x js -- repeated until at least min_s of wall
+    time.  A sample of 19.2 jobs on 16 threads had timed a full wave plus a wave with 13 threads idle
+    (100 K/s against the headline's 166.6 K/s for the same work).  Returns (reports/s, sample)."""
+    w = cores * js
+    m = avail // w * w if avail >= w else avail
+    fn(min(m, w))  # warm: the oracle library, page cache, thread pool
+    reps, tot = 0, 0.0
+    while tot < min_s:
+        t0 = time.perf_counter()
+        fn(m)
+        tot += time.perf_counter() - t0
+        reps += 1
+    waves = m / w
+    return reps * m / tot, (f"{reps} x {m} reports = {reps * waves:.0f} whole waves of {cores} "
+                            f"jobs of {js} on {cores} threads, {tot:.1f}s")
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -583,6 +612,9 @@ def jobs_main(args):
                                not args.no_cpu_baseline, args.cpu_seconds, args.exec_heavy)
     elif args.jobs_role == "hpke":
         out = hpke_jobs_line(args.threads, args.job_size, n_jobs, args.tasks,
+                             not args.no_cpu_baseline, args.cpu_seconds, args.exec_heavy)
+    elif args.jobs_role == "init":
+        out = init_jobs_line(args.threads, args.job_size, n_jobs, args.tasks,
                              not args.no_cpu_baseline, args.cpu_seconds, args.exec_heavy)
     else:
         out = jobs_line(args.threads, args.job_size, n_jobs, args.tasks, args.opt,
@@ -704,20 +736,18 @@ def jobs_line(T, js, n_jobs, K, opts=(), combined=True, with_cpu=True, check_tas
     cores = cpu_threads()
     cpu = None
     if with_cpu:
-        m = min(max(500 * cores, int(400 * cores * cpu_seconds)), len(host["nonces"]))
-        t0 = time.perf_counter()
-        o.helper_batch(vks[0], host["nonces"][:m], host["public_shares"][:m],
-                       host["helper_shares"][:m], host["leader_prep_shares"][:m],
-                       n_threads=cores, job_size=js)
-        dta = time.perf_counter() - t0
+        def cpu_run(m):  # task 0's pool (its own verify key)
+            o.helper_batch(vks[0], host["nonces"][:m], host["public_shares"][:m],
+                           host["helper_shares"][:m], host["leader_prep_shares"][:m],
+                           n_threads=cores, job_size=js)
+        rate, sample = _cpu_waves(cpu_run, cores, js, pool, max(2.0, cpu_seconds))
         m1 = 2000
         t0 = time.perf_counter()
         o.helper_batch(vks[0], host["nonces"][:m1], host["public_shares"][:m1],
                        host["helper_shares"][:m1], host["leader_prep_shares"][:m1],
                        n_threads=1, job_size=js)
         dt1 = time.perf_counter() - t0
-        cpu = dict(value=m / dta, unit="reports/s", cores=cores, kind="port",
-                   sample=f"{m} reports, jobs of {js}, one job per worker thread, {dta:.1f}s",
+        cpu = dict(value=rate, unit="reports/s", cores=cores, kind="port", sample=sample,
                    single_core_us_per_report=dt1 / m1 * 1e6, cpu_model=cpu_model())
     per_report_h2d = 16 + sz.public_share_len + sz.helper_share_len + sz.prep_share_len
     return dict(metric="reports prepared+aggregated/sec through the host-buffer C ABI "
@@ -836,16 +866,14 @@ def leader_jobs_line(T, js, n_jobs, K, devices=None, with_cpu=True, cpu_seconds=
     cores = cpu_threads()
     cpu = None
     if with_cpu:
-        m = min(max(500 * cores, int(300 * cores * cpu_seconds)), pool)
-        t0 = time.perf_counter()
-        o.leader_batch(vks[0], host["nonces"][:m], host["public_shares"][:m],
-                       host["leader_input_shares"][:m], host["msgs"][:m], n_threads=cores,
-                       job_size=js)
-        dta = time.perf_counter() - t0
-        cpu = dict(value=m / dta, unit="reports/s", cores=cores, kind="port",
-                   sample=f"{m} reports through the restatement's leader path (prepare_init "
-                          f"agg_id 0 + prepare_next + aggregate), jobs of {js}, {cores} threads, "
-                          f"{dta:.1f}s", cpu_model=cpu_model())
+        def cpu_run(m):
+            o.leader_batch(vks[0], host["nonces"][:m], host["public_shares"][:m],
+                           host["leader_input_shares"][:m], host["msgs"][:m], n_threads=cores,
+                           job_size=js)
+        rate, sample = _cpu_waves(cpu_run, cores, js, pool, max(2.0, cpu_seconds))
+        cpu = dict(value=rate, unit="reports/s", cores=cores, kind="port",
+                   sample="the restatement's leader path (prepare_init agg_id 0 + prepare_next + "
+                          "aggregate): " + sample, cpu_model=cpu_model())
     h2d = 16 + sz.public_share_len + sz.leader_input_share_len + sz.prep_msg_len
     return dict(metric="leader reports prepared (init + next) + aggregated/sec through the "
                        "host-buffer C ABI (Prio3Histogram len=256, concurrent aggregation jobs)",
@@ -932,16 +960,16 @@ def hpke_jobs_line(T, js, n_jobs, K, with_cpu=True, cpu_seconds=10.0, heavy=0):
     cores = cpu_threads()
     cpu = None
     if with_cpu:
-        m = min(max(1000 * cores, int(1500 * cores * cpu_seconds)), pool)
         d = parts[0]
-        t0 = time.perf_counter()
-        H.open_input_shares(skR, d["pkR"], d["task_id"], d["enc"][:m], d["ct"][:m],
-                            d["ct_len"][:m], d["report_ids"][:m], d["times"][:m], d["pubs"][:m],
-                            48, n_threads=cores)
-        dta = time.perf_counter() - t0
-        cpu = dict(value=m / dta, unit="reports/s", cores=cores, kind="port",
-                   sample=f"{m} sealed input shares, OpenSSL 3.0 X25519 / HKDF-SHA256 / "
-                          f"AES-128-GCM, {cores} threads, {dta:.1f}s", cpu_model=cpu_model())
+
+        def cpu_run(m):
+            H.open_input_shares(skR, d["pkR"], d["task_id"], d["enc"][:m], d["ct"][:m],
+                                d["ct_len"][:m], d["report_ids"][:m], d["times"][:m],
+                                d["pubs"][:m], 48, n_threads=cores)
+        rate, sample = _cpu_waves(cpu_run, cores, js, pool, max(2.0, cpu_seconds))
+        cpu = dict(value=rate, unit="reports/s", cores=cores, kind="port",
+                   sample="sealed input shares, OpenSSL 3.0 X25519 / HKDF-SHA256 / AES-128-GCM: "
+                          + sample, cpu_model=cpu_model())
     h2d = 32 + stride + 4 + 16 + 8 + 32
     roofline = model_roofline("hpke_x25519_aead1", RM.hpke_model("x25519", 1), n_jobs * js, 1, dt)
     roofline["pcie"] = dict(h2d_bytes_per_report=h2d, frac=value * h2d / 63e9)
@@ -958,6 +986,161 @@ def hpke_jobs_line(T, js, n_jobs, K, with_cpu=True, cpu_seconds=10.0, heavy=0):
                             job_size=js, jobs=n_jobs, threads=T, tasks=K),
                 roofline=roofline, coalescing=dict(launches=launches, jobs=n_jobs),
                 checks=dict(all_opened=bool((status == 0).all()), every_job_matches_cpu=ok,
+                            jobs_checked=n_jobs, check_seconds=t_chk),
+                cpu_baseline=cpu, speedup_vs_cpu=(value / cpu["value"]) if cpu else None)
+
+
+def init_jobs_line(T, js, n_jobs, K, with_cpu=True, cpu_seconds=10.0, heavy=0, two_call=True):
+    """the helper's whole loop body at the production call shape -- T host
+    threads, each running whole aggregation jobs from the SEALED input shares
+    (VdafOps::handle_aggregate_init_generic, aggregator.rs:1794-2096) through
+    prio3_helper_aggregate_init_batch: HPKE open, decode, prepare and accumulate in one coalesced
+    launch per group, the decrypted shares kept in HBM.  K tasks (verify keys and task IDs) of
+    Prio3Histogram(256,16) under one X25519 keypair.  Beside it, in the same run, the two-call
+    composition (janus_hpke_open_input_shares, then prio3_helper_prepare_aggregate_batch).  Every
+    job's statuses, aggregate and count are checked against OpenSSL + the restatement."""
+    import ctypes as C
+    from janus_amd import hpke as G
+    from oracle import hpke as H
+    from oracle.oracle import Oracle
+    torch.cuda.set_device(0)
+    n_jobs = max(K, n_jobs)
+    pool = 1 << 15
+    rng = np.random.default_rng(0x4A414E56)
+    vks = [bytes([0x81 + t]) * 16 for t in range(K)]
+    tasks = [bytes(rng.integers(0, 256, 32, dtype=np.uint8)) for _ in range(K)]
+    skR = H.kem_private(rng)
+    pkR = H.kem_public(skR)
+    engines, devs = _job_engines(J.Prio3Histogram(256, 16), vks, None)
+    engines[0].executor_control("heavy", heavy)
+    sz = engines[0].sz
+    cores = cpu_threads()
+    cols = {k: [] for k in ("nonces", "public_shares", "helper_shares", "leader_prep_shares",
+                            "times", "enc", "ct", "ct_len")}
+    stride = None
+    for t, e in enumerate(engines):
+        p = e.generate_reports_device(pool, seed=0x4A414E5553000007 + t)
+        torch.cuda.synchronize()
+        h = {k: p[k].cpu().numpy() for k in ("nonces", "public_shares", "helper_shares",
+                                              "leader_prep_shares")}
+        del p
+        times = (1_700_000_000 + rng.integers(0, 3600, pool)).astype(np.uint64)
+        enc, ct, cl, stride = H.seal_input_shares(pkR, tasks[t], h["nonces"], times,
+                                                  h["public_shares"], h["helper_shares"],
+                                                  seed=0x5EA1 + t, n_threads=cores)
+        for k, v in dict(h, times=times, enc=enc, ct=ct, ct_len=cl).items():
+            cols[k].append(v)
+    host = {k: np.ascontiguousarray(np.concatenate(v)) for k, v in cols.items()}
+    task_arr = np.frombuffer(b"".join(tasks), np.uint8).copy()
+    op = G.HpkeOpener(skR, pkR, device=0)
+    lib = C.CDLL(os.path.join(ROOT, "janus_amd", "libjanus_jobs.so"))
+    lib.janus_jobs_run_init.restype = C.c_double
+    vp, u32 = C.c_void_p, C.c_uint32
+    lib.janus_jobs_run_init.argtypes = [C.POINTER(vp), C.c_int, vp, vp, vp, C.c_int, C.c_int,
+                                        C.c_int, u32, vp, vp, vp, vp, u32, vp, vp, u32, vp, vp, vp,
+                                        vp, C.c_int]
+    eng_arr = (vp * K)(*[e.handle.value for e in engines])
+    status = np.zeros(n_jobs * js, np.uint8)
+    counts = np.zeros(n_jobs, np.uint64)
+    agg = np.zeros((n_jobs, sz.agg_share_len), np.uint8)
+    P = lambda a: a.ctypes.data_as(vp)
+
+    def run(jobs, one_call):
+        status[:] = 0xFF
+        counts[:] = 0
+        return lib.janus_jobs_run_init(eng_arr, K, C.cast(C.pointer(sz), vp), op.handle,
+                                       P(task_arr), T, jobs, js, pool, P(host["nonces"]),
+                                       P(host["public_shares"]), P(host["times"]), P(host["enc"]),
+                                       32, P(host["ct"]), P(host["ct_len"]), stride,
+                                       P(host["leader_prep_shares"]), P(status), P(counts), P(agg),
+                                       int(one_call))
+
+    # the reference the jobs are checked against: OpenSSL opens each task's pool, the restatement
+    # prepares + aggregates every job's window of it
+    o = Oracle("histogram", length=256, chunk_length=16)
+    opened = []
+    for t in range(K):
+        sl = slice(t * pool, (t + 1) * pool)
+        sh, hs = H.open_input_shares(skR, pkR, tasks[t], host["enc"][sl], host["ct"][sl],
+                                     host["ct_len"][sl], host["nonces"][sl], host["times"][sl],
+                                     host["public_shares"][sl], sz.helper_share_len,
+                                     n_threads=cores)
+        assert (hs == 0).all()
+        opened.append(sh)
+
+    def check():
+        ok_jobs = ok_st = True
+        for t in range(K):
+            jl, idx = _job_windows(t, n_jobs, K, js, pool)
+            seg = np.repeat(np.arange(len(jl), dtype=np.uint32), js)
+            _, rst, ragg, rcnt = o.helper_batch(
+                vks[t], host["nonces"][idx], host["public_shares"][idx], opened[t][idx - t * pool],
+                host["leader_prep_shares"][idx], segment_ids=seg, n_segments=len(jl),
+                n_threads=cores)
+            ok_jobs &= bool(np.array_equal(agg[jl], ragg) and
+                            np.array_equal(counts[jl], rcnt.astype(np.uint64)))
+            ok_st &= bool(np.array_equal(status.reshape(n_jobs, js)[jl], rst.reshape(-1, js)))
+        return ok_jobs, ok_st
+
+    run(max(K, min(n_jobs, 8 * T)), True)  # warmup: pools, pinned staging, streams
+    g0 = engines[0].executor_stats(J.EXEC_PREPARE)["groups"]
+    dt = run(n_jobs, True)
+    if dt < 0:
+        raise RuntimeError("janus_jobs_run_init: a C-ABI call failed")
+    launches = engines[0].executor_stats(J.EXEC_PREPARE)["groups"] - g0
+    value = n_jobs * js / dt
+    t_chk = time.perf_counter()
+    jobs_ok, st_ok = check()
+    all_fin = bool((status == 0).all())
+    cnt_ok = bool((counts == js).all())
+    t_chk = time.perf_counter() - t_chk
+    two = None
+    if two_call:
+        run(max(K, min(n_jobs, 8 * T)), False)
+        dt2 = run(n_jobs, False)
+        if dt2 < 0:
+            raise RuntimeError("janus_jobs_run_init (two calls): a C-ABI call failed")
+        j2, s2 = check()
+        two = dict(value=n_jobs * js / dt2, ms=dt2 * 1e3, every_job_matches_cpu=j2,
+                   statuses_match_cpu=s2,
+                   call="janus_hpke_open_input_shares + prio3_helper_prepare_aggregate_batch")
+    cpu = None
+    if with_cpu:
+        def cpu_run(m):  # the helper's CPU loop body: OpenSSL open, then the restatement
+            sh, _ = H.open_input_shares(skR, pkR, tasks[0], host["enc"][:m], host["ct"][:m],
+                                        host["ct_len"][:m], host["nonces"][:m], host["times"][:m],
+                                        host["public_shares"][:m], sz.helper_share_len,
+                                        n_threads=cores)
+            o.helper_batch(vks[0], host["nonces"][:m], host["public_shares"][:m], sh,
+                           host["leader_prep_shares"][:m], n_threads=cores, job_size=js)
+        rate, sample = _cpu_waves(cpu_run, cores, js, pool, max(2.0, cpu_seconds))
+        cpu = dict(value=rate, unit="reports/s", cores=cores, kind="port",
+                   sample="OpenSSL 3.0 HPKE open + the restatement's helper prepare + aggregate: "
+                          + sample, cpu_model=cpu_model())
+    h2d = 16 + sz.public_share_len + 8 + 32 + stride + 4 + sz.prep_share_len
+    return dict(metric="reports opened+prepared+aggregated/sec through the host-buffer C ABI "
+                       "(helper aggregate-init loop body from sealed input shares, Prio3Histogram "
+                       "len=256, X25519/AES-128-GCM, concurrent aggregation jobs)",
+                value=value, unit="reports/s", n_gpus=len(set(devs)), steps=1, warmup=1,
+                ms_per_step=dt * 1e3, higher_is_better=True, scaling="weak", vs_baseline=None,
+                dtype="u32 limbs (Field128 mod-p, GF(2^255 - 19), GF(2^128), bytes)",
+                data=f"synthetic: {K} tasks x {pool} on-device client reports, helper input "
+                     "shares sealed by the oracle (OpenSSL, seeded), host memory",
+                config=dict(workload="VdafOps::handle_aggregate_init_generic loop body per "
+                                     "aggregation job: HPKE open + PlaintextInputShare decode + "
+                                     "Prio3Histogram(256,16) helper prepare + accumulate, host "
+                                     "buffers (PCIe included)",
+                            job_size=js, jobs=n_jobs, threads=T, tasks=K, devices=devs),
+                roofline=dict(bound="pcie", achieved=value * h2d / 1e9, peak=63.0,
+                              unit="GB/s host->device (report ID, time, public share, HPKE "
+                                   "ciphertext, leader prep share per report)",
+                              frac=value * h2d / 63e9, h2d_bytes_per_report=h2d, traffic=None),
+                coalescing=dict(launches=launches, jobs=n_jobs,
+                                mean_reports_per_launch=n_jobs * js / max(launches, 1)),
+                call="prio3_helper_aggregate_init_batch (one coalesced launch per group)",
+                two_call=two,
+                checks=dict(all_finished=all_fin, counts_ok=cnt_ok,
+                            every_job_matches_cpu=jobs_ok, statuses_match_cpu=st_ok,
                             jobs_checked=n_jobs, check_seconds=t_chk),
                 cpu_baseline=cpu, speedup_vs_cpu=(value / cpu["value"]) if cpu else None)
 
@@ -1403,6 +1586,10 @@ def fpvec_main(args):
     n = args.reports if args.reports != 1 << 20 else 100_000
     eng = J.HelperEngine(J.Prio3FixedPointBoundedL2VecSum(10000, 16), vk, device=0,
                          allow_unpinned=True)
+    # a device-resident caller running ~225 GB FPVec batches back to back keeps the released run
+    # in the pool (keep_scratch; by default a slab above the pool's 1/8-of-HBM budget is freed on
+    # release): re-allocating it every step cost C5 40 % in r02j
+    eng.set_option("keep_scratch", 1)
     for kv in args.opt:
         k, v = kv.split("=")
         eng.set_option(k, int(v))

@@ -62,6 +62,15 @@ enum {
                                           InvalidMessage (aggregation_job_driver.rs:397-415) */
 };
 
+/* Merged per-report status of prio3_helper_aggregate_init_batch for a report the helper rejects
+ * before its VDAF runs: 0x80 | the DAP PrepareError Janus records (messages/src/lib.rs
+ * PrepareError; aggregator.rs:1847-1983), which takes precedence over any VDAF status. */
+enum {
+  PRIO3_STATUS_HPKE_DECRYPT = 0x84,     /* PrepareError::HpkeDecryptError (open / AAD failed) */
+  PRIO3_STATUS_INVALID_MESSAGE = 0x88,  /* PrepareError::InvalidMessage (PlaintextInputShare,
+                                           extensions, helper input share length) */
+};
+
 /* Whole-call return codes. */
 enum {
   PRIO3_OK = 0,
@@ -191,6 +200,31 @@ int prio3_helper_prepare_aggregate_batch(prio3_engine* engine, uint32_t n, const
                                          uint32_t n_segments, uint8_t* prep_msgs_out,
                                          uint8_t* status_out, uint8_t* agg_shares_out,
                                          uint64_t* counts_out);
+
+/* The helper's whole per-report loop body for one aggregation job, from the sealed input shares
+ * (VdafOps::handle_aggregate_init_generic, /root/reference/aggregator/src/aggregator.rs:1794-2096):
+ * hpke::open of each report's encrypted input share (:1847-1890, the opener of janus_hpke.h, AAD
+ * InputShareAad{task_id, metadata, public_share}), PlaintextInputShare decode and the extension
+ * checks (:1893-1983; require_taskprov as in janus_hpke_open_input_shares), then
+ * helper_initialized + evaluate (:2020-2042) and the accumulate of prio3_helper_prepare_aggregate_
+ * batch -- in ONE coalesced group launch: concurrent jobs of every task of the instance that open
+ * with the same keypair, ciphertext stride and taskprov flag share it, and the decrypted helper
+ * shares never leave the GPU.  Inputs per report: report_ids[n][16] (the VDAF nonces), times[n]
+ * (seconds), public_shares[n][public_share_len], enc[n][Nenc], ct[n][ct_stride] with ct_len[n],
+ * leader_prep_shares[n][prep_share_len]; segment_ids / accept_mask / n_segments as in
+ * prio3_accumulate.  status_out[n]: PRIO3_STATUS_* of the report's VDAF, or
+ * PRIO3_STATUS_HPKE_DECRYPT / PRIO3_STATUS_INVALID_MESSAGE when the open rejected it (such a
+ * report is never counted).  Instances whose public share is neither 0 nor 32 bytes
+ * (PRIO3_SUMVEC_F64_MP) return PRIO3_EUNSUPPORTED.  The opener may be bound to any GPU: the open
+ * runs on the GPU the job is placed on. */
+struct janus_hpke_opener;
+int prio3_helper_aggregate_init_batch(
+    prio3_engine* engine, struct janus_hpke_opener* opener, uint32_t n,
+    const uint8_t task_id[32], int require_taskprov, const uint8_t* report_ids,
+    const uint64_t* times, const uint8_t* public_shares, const uint8_t* enc, const uint8_t* ct,
+    const uint32_t* ct_len, uint32_t ct_stride, const uint8_t* leader_prep_shares,
+    const uint32_t* segment_ids, const uint8_t* accept_mask, uint32_t n_segments,
+    uint8_t* prep_msgs_out, uint8_t* status_out, uint8_t* agg_shares_out, uint64_t* counts_out);
 
 /* Parity-only: copies the n output shares (n x agg_share_len). */
 int prio3_debug_output_shares(prio3_batch* batch, uint8_t* out);

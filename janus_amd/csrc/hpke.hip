@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/janus_hpke.h"
+#include "../../include/janus_prio3.h"
 #include "prio3_device.h"
 #include "sha256_device.h"
 #include "aes_device.h"
@@ -1544,7 +1545,8 @@ int janus_hpke_opener_create(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id,
     memcpy(o->P.ipad0_384, k0.ist, 64);
     memcpy(o->P.opad0_384, k0.ost, 64);
   }
-  if (hipSetDevice(device) != hipSuccess ||
+  DeviceGuard dg_(device);
+  if (dg_.rc != hipSuccess ||
       hipStreamCreateWithFlags(&o->stream, hipStreamNonBlocking) != hipSuccess) {
     delete o;
     return JANUS_HPKE_EDEVICE;
@@ -1555,7 +1557,7 @@ int janus_hpke_opener_create(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id,
 
 void janus_hpke_opener_destroy(janus_hpke_opener* o) {
   if (!o) return;
-  (void)hipSetDevice(o->device);
+  DeviceGuard dg_(o->device);
   (void)hipStreamSynchronize(o->stream);
   if (o->d_pt) (void)hipFree(o->d_pt);
   for (auto& e : o->pending) {
@@ -1642,6 +1644,36 @@ static int ensure_pt(janus_hpke_opener* o, size_t bytes) {
 
 // ---- executor hooks (prio3_runtime.h) ----
 int hpke_opener_device(const janus_hpke_opener* o) { return o->device; }
+size_t hpke_opener_nenc(const janus_hpke_opener* o) { return kem_nenc((uint16_t)o->P.kem); }
+uint64_t hpke_opener_key(const janus_hpke_opener* o) {
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
+  mix((uint64_t)(uintptr_t)o);
+  mix((uint64_t)o->timing);
+  return h;
+}
+
+// the open of a sealed-input prepare group (engine_group_issue), on the group's stream
+int hpke_open_group_launch(janus_hpke_opener* o, const HpkeGroupArgs& g, hipStream_t st) {
+  OpenArgs a{};
+  a.n = g.n;
+  a.ct_stride = g.ct_stride;
+  a.share_len = g.share_len;
+  a.require_taskprov = g.require_taskprov;
+  a.enc = g.enc;
+  a.ct = g.ct;
+  a.ct_len = g.ct_len;
+  a.ids = g.ids;
+  a.times = g.times;
+  a.pubs = g.pubs;
+  a.pt = g.pt;
+  a.shares = g.shares;
+  a.status = g.status;
+  a.task_slot = g.task_slot;
+  a.task_tab = g.task_tab;
+  std::lock_guard<std::mutex> lk(o->mu);  // o->P and the timing list
+  return launch_open(o, 1, (int)g.pub_len, a, st) == JANUS_HPKE_SUCCESS ? PRIO3_OK : PRIO3_EDEVICE;
+}
 
 uint64_t hpke_group_key(const HpkeJob* j) {
   uint64_t h = 1469598103934665603ull;
@@ -1691,7 +1723,8 @@ int hpke_group_issue(const HpkeJob& pj, const HpkeLayout& L, const uint8_t* stg,
   janus_hpke_opener* o = pj.o;
   *st_out = nullptr;
   *slab_out = nullptr;
-  HCHK(hipSetDevice(o->device));
+  DeviceGuard dg_(o->device);
+  HCHK(dg_.rc);
   hipStream_t st = own_queue ? ws_exec_stream_get(o->device) : ws_stream_get(o->device);
   if (!st) return JANUS_HPKE_EDEVICE;
   int rc = JANUS_HPKE_SUCCESS;
@@ -1765,7 +1798,8 @@ int janus_hpke_open_input_shares_device(janus_hpke_opener* o, uint32_t n,
       (public_share_len != 0 && public_share_len != 32) || (public_share_len && !d_public_shares))
     return JANUS_HPKE_EINVAL;
   std::lock_guard<std::mutex> lk(o->mu);
-  HCHK(hipSetDevice(o->device));
+  DeviceGuard dg_(o->device);
+  HCHK(dg_.rc);
   int rc = ensure_pt(o, (size_t)n * ct_stride);
   if (rc) return rc;
   for (int i = 0; i < 8; i++) o->P.task[i] = be32(task_id + 4 * i);
@@ -1796,7 +1830,8 @@ int janus_hpke_open_device(janus_hpke_opener* o, uint32_t n, const uint8_t* d_en
       ct_stride % 16 != 0 || aad_stride % 16 != 0 || (aad_stride && (!d_aad || !d_aad_len)))
     return JANUS_HPKE_EINVAL;
   std::lock_guard<std::mutex> lk(o->mu);
-  HCHK(hipSetDevice(o->device));
+  DeviceGuard dg_(o->device);
+  HCHK(dg_.rc);
   OpenArgs a{};
   a.n = n;
   a.ct_stride = ct_stride;
@@ -1994,7 +2029,8 @@ int janus_hpke_open_input_shares(janus_hpke_opener* o, uint32_t n, const uint8_t
     j.status_out = status;
     return exec_hpke(&j);
   }
-  HCHK(hipSetDevice(o->device));
+  DeviceGuard dg_(o->device);
+  HCHK(dg_.rc);
   DevBuf de, dc, dl, di, dt, dp, ds, dst;
   int rc;
   const size_t nenc = kem_nenc((uint16_t)o->P.kem);
@@ -2068,7 +2104,8 @@ int janus_hpke_open(janus_hpke_opener* o, uint32_t n, const uint8_t* enc, const 
                     const uint32_t* aad_len, uint32_t aad_stride, uint8_t* pt, uint8_t* status) {
   if (!o) return JANUS_HPKE_EINVAL;
   if (n == 0) return JANUS_HPKE_SUCCESS;
-  HCHK(hipSetDevice(o->device));
+  DeviceGuard dg_(o->device);
+  HCHK(dg_.rc);
   DevBuf de, dc, dl, da, dal, dpt, dst;
   int rc;
   const size_t nenc = kem_nenc((uint16_t)o->P.kem);

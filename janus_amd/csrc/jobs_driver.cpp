@@ -153,4 +153,60 @@ double janus_jobs_run_hpke(janus_hpke_opener* op, int n_tasks, const uint8_t* ta
   });
 }
 
+// The helper's whole loop body per job from the sealed input shares (aggregator.rs:1794-2096):
+// job j of task t = j % n_engines over the same report windows as janus_jobs_run, whose input
+// shares were sealed to `opener`'s keypair under task_ids[t][32] (enc[..][nenc], ct[..][ct_stride],
+// ct_len, times).  one_call = 1: prio3_helper_aggregate_init_batch (the open, prepare and
+// accumulate in one coalesced launch); 0: the two-call composition a caller of r05's ABI makes --
+// janus_hpke_open_input_shares into host buffers, then prio3_helper_prepare_aggregate_batch with
+// the open's rejections masked out and their statuses merged (0x80 | PrepareError).
+double janus_jobs_run_init(prio3_engine** engines, int n_engines, const prio3_sizes_t* szp,
+                           janus_hpke_opener* opener, const uint8_t* task_ids, int threads,
+                           int jobs, int job_size, uint32_t pool, const uint8_t* nonces,
+                           const uint8_t* pub, const uint64_t* times, const uint8_t* enc,
+                           uint32_t nenc, const uint8_t* ct, const uint32_t* ct_len,
+                           uint32_t ct_stride, const uint8_t* lps, uint8_t* status_out,
+                           uint64_t* counts_out, uint8_t* agg_out, int one_call) {
+  const prio3_sizes_t sz = *szp;
+  const uint32_t span = pool - (uint32_t)job_size + 1;
+  return run_pool(threads, jobs, [&](int j) {
+    thread_local std::vector<uint8_t> msgs, shares, hs, acc;
+    msgs.resize((size_t)job_size * (sz.prep_msg_len ? sz.prep_msg_len : 1));
+    const uint32_t t = (uint32_t)(j % n_engines);
+    const size_t r0 = t * (size_t)pool + (((uint64_t)(j / n_engines) * job_size) % span);
+    const size_t o = (size_t)j * job_size;
+    const uint8_t* jp = sz.public_share_len ? pub + (size_t)sz.public_share_len * r0 : nullptr;
+    uint8_t* st = status_out + o;
+    uint8_t* agg = agg_out + (size_t)sz.agg_share_len * j;
+    uint64_t cnt = 0;
+    int rc;
+    if (one_call) {
+      rc = prio3_helper_aggregate_init_batch(
+          engines[t], opener, (uint32_t)job_size, task_ids + 32 * (size_t)t, 0,
+          nonces + 16 * r0, times + r0, jp, enc + (size_t)nenc * r0,
+          ct + (size_t)ct_stride * r0, ct_len + r0, ct_stride, lps + (size_t)sz.prep_share_len * r0,
+          nullptr, nullptr, 1, msgs.data(), st, agg, &cnt);
+    } else {
+      shares.resize((size_t)job_size * sz.helper_share_len);
+      hs.resize(job_size);
+      acc.resize(job_size);
+      rc = janus_hpke_open_input_shares(
+          opener, (uint32_t)job_size, task_ids + 32 * (size_t)t, enc + (size_t)nenc * r0,
+          ct + (size_t)ct_stride * r0, ct_len + r0, ct_stride, nonces + 16 * r0, times + r0, jp,
+          sz.public_share_len, sz.helper_share_len, 0, shares.data(), hs.data());
+      if (rc == 0) {
+        for (int i = 0; i < job_size; i++) acc[i] = hs[i] == 0;
+        rc = prio3_helper_prepare_aggregate_batch(
+            engines[t], (uint32_t)job_size, nonces + 16 * r0, jp, shares.data(),
+            lps + (size_t)sz.prep_share_len * r0, nullptr, acc.data(), 1, msgs.data(), st, agg,
+            &cnt);
+        for (int i = 0; i < job_size; i++)
+          if (hs[i]) st[i] = (uint8_t)(0x80u | hs[i]);
+      }
+    }
+    counts_out[j] = cnt;
+    return rc == 0;
+  });
+}
+
 }  // extern "C"

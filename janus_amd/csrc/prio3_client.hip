@@ -1170,7 +1170,8 @@ static int gen_fpvec(prio3_engine* e, uint32_t n, uint64_t seed, uint64_t first_
   if (!d_pub) return PRIO3_EINVAL;
   const uint32_t Pm = std::max(p.P, p.P1);
   if (Pm > 1024 || p.logP + 1 > MAX_ROOTS || p.logP1 + 1 > MAX_ROOTS) return PRIO3_EUNSUPPORTED;
-  if (hipSetDevice(e->device) != hipSuccess) return PRIO3_EDEVICE;
+  DeviceGuard dg_(e->device);
+  if (dg_.rc != hipSuccess) return PRIO3_EDEVICE;
   // entries are signed bytes >> gsh, |X| <= 2^(7 - gsh): the claimed norm must stay below
   // 2^(2 bits - 2) (FixedPointBoundedL2VecSum's bound, ||x|| < 1)
   uint32_t gsh = 0;
@@ -1304,7 +1305,8 @@ static int gen_mp64(prio3_engine* e, uint32_t n, uint64_t seed, uint64_t first_i
   DevParams p = e->dp;
   const Mp64Params& P = e->mp;
   if (!d_pub) return PRIO3_EINVAL;
-  if (hipSetDevice(e->device) != hipSuccess) return PRIO3_EDEVICE;
+  DeviceGuard dg_(e->device);
+  if (dg_.rc != hipSuccess) return PRIO3_EDEVICE;
   const uint32_t A = p.arity, np = P.np, PP = p.P;
   const size_t chunk = std::min<size_t>(((size_t)n + 63) & ~(size_t)63, 65536);
   std::vector<void*> bufs;
@@ -1385,7 +1387,8 @@ extern "C" int prio3_client_generate_device(prio3_engine* e, uint32_t n, uint64_
                      d_leader_prep_shares, d_measurements, d_leader_out_shares, d_flags,
                      d_leader_input_shares, (hipStream_t)stream);
   std::lock_guard<std::mutex> lk(e->mu);
-  if (hipSetDevice(e->device) != hipSuccess) return PRIO3_EDEVICE;
+  DeviceGuard dg_(e->device);
+  if (dg_.rc != hipSuccess) return PRIO3_EDEVICE;
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
   DevParams p = e->dp;
   const size_t es = p.es;

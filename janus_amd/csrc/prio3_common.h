@@ -634,6 +634,10 @@ struct Run {
   uint8_t *gaccept = nullptr, *gagg = nullptr, *gcnt = nullptr;
   std::atomic<int> refs{1};
   hipStream_t last = nullptr;  // stream of the latest work on the run (its release point)
+  bool keep = false;  // the engine's keep_scratch: the slab stays in the pool above its budget
+  // sealed-input groups (RUN_HPKE): the open's status per report and its plaintext scratch
+  uint32_t hpke_stride = 0;
+  uint8_t *hstatus = nullptr, *hpt = nullptr;
 };
 
 struct prio3_engine {
@@ -663,6 +667,9 @@ struct prio3_engine {
   // (k_prep_hp; 0 = never): below ~3 waves per SIMD the one-lane k_prep_h leaves SIMDs idle
   int pair_max = 196608;
   int timing = 0;
+  // option: a released run's slab stays in the GPU's pool even above the pool's budget (a
+  // device-resident caller running FPVec batches back to back; default: the budget applies)
+  int keep_scratch = 0;
   Mp64Params mp{};  // PRIO3_SUMVEC_F64_MP only
   uint64_t* d_sigma64 = nullptr;
   uint4* d_sigma128 = nullptr;  // k_query_w's sigma table (DevParams::sigma_dev)

@@ -29,6 +29,7 @@
 #include <type_traits>
 #include <vector>
 
+#include "../../include/janus_hpke.h"
 #include "../../include/janus_prio3.h"
 #include "prio3_device.h"
 
@@ -2900,6 +2901,7 @@ enum : unsigned {
   RUN_LINPUT = 8,   // leader input shares (host-buffer leader entry point)
   RUN_FUSED = 16,   // fused-accumulate partials (prio3_device_prepare_aggregate, Histogram)
   RUN_AGG_IO = 32,  // group segment ids, accept bytes, aggregate shares + counts (executor)
+  RUN_HPKE = 64,    // open statuses + plaintext scratch of a sealed-input group (executor)
 };
 
 // FPVec per-report scratch bytes of one sub-batch column: every buffer indexed [row][column]
@@ -3018,6 +3020,10 @@ static size_t run_carve(Run* R, unsigned flags, uint32_t n_keys, uint8_t* base) 
     take(&R->gagg, (size_t)d.out_len * es * S);
     take(&R->gcnt, 8 * S);
   }
+  if (flags & RUN_HPKE) {
+    take(&R->hstatus, n);
+    take(&R->hpt, (size_t)R->hpke_stride * n);
+  }
   if (flags & RUN_FUSED) {
     // sized for 32-report waves (k_prep_hp); the one-lane kernels use the first half
     const size_t waves = (n + 31) / 32, M = d.meas_len, chunks = (waves + WCH_HOST - 1) / WCH_HOST;
@@ -3032,9 +3038,10 @@ static size_t run_carve(Run* R, unsigned flags, uint32_t n_keys, uint8_t* base) 
 }
 
 static Run* run_create(prio3_engine* e, uint32_t n, unsigned flags, uint32_t nseg,
-                       uint32_t n_keys, hipStream_t st, int* rc) {
+                       uint32_t n_keys, hipStream_t st, int* rc, uint32_t hpke_stride = 0) {
   Run* R = new Run();
   R->e = e;
+  R->hpke_stride = hpke_stride;
   R->device = e->device;
   R->n = n;
   R->nseg = nseg;
@@ -3057,6 +3064,7 @@ static Run* run_create(prio3_engine* e, uint32_t n, unsigned flags, uint32_t nse
     return nullptr;
   }
   run_carve(R, flags, n_keys, R->slab->base);
+  R->keep = e->keep_scratch != 0;
   R->fix_cap = (size_t)n + 1;
   R->last = st;
   return R;
@@ -3067,7 +3075,7 @@ static Run* run_create(prio3_engine* e, uint32_t n, unsigned flags, uint32_t nse
 static void run_release(Run* R, hipStream_t st, bool use_st) {
   if (!R) return;
   if (R->refs.fetch_sub(1) != 1) return;
-  ws_release(R->slab, use_st ? st : R->last);
+  ws_release(R->slab, use_st ? st : R->last, R->keep);
   delete R;
 }
 
@@ -3693,11 +3701,22 @@ uint64_t engine_group_key(const prio3_engine* e) {
   return h;
 }
 
-void engine_io_layout(const prio3_engine* e, uint32_t cap, IoLayout* L) {
+uint64_t exec_job_key(const ExecJob* j) {
+  uint64_t h = engine_group_key(j->e);
+  if (j->opener) {  // sealed-input jobs: one keypair and ciphertext shape per launch
+    const uint64_t u[4] = {0x5345414C4544ull, hpke_opener_key(j->opener), j->ct_stride,
+                           (uint64_t)j->require_taskprov};
+    h = fnv(h, u, sizeof u);
+  }
+  return h;
+}
+
+void engine_io_layout(const prio3_engine* e, uint32_t cap, IoLayout* L, const ExecJob* job) {
   const DevParams& d = e->dp;
+  const bool sealed = job && job->opener;
   L->len[0] = 16;
   L->len[1] = d.public_share_len;
-  L->len[2] = d.helper_share_len;
+  L->len[2] = sealed ? 0 : d.helper_share_len;  // sealed: opened into the run on the device
   L->len[3] = d.prep_share_len;
   size_t off = 0;
   for (int f = 0; f < 4; f++) {
@@ -3727,12 +3746,39 @@ void engine_io_layout(const prio3_engine* e, uint32_t cap, IoLayout* L) {
   off += (L->agg_len * L->max_seg + 15) & ~(size_t)15;
   L->cnt_off = off;
   off += 8 * (size_t)L->max_seg;
+  L->nenc = L->ct_stride = 0;
+  if (sealed) {  // the ciphertexts and their AAD fields (report IDs and public shares above)
+    auto up = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    L->nenc = (uint32_t)hpke_opener_nenc(job->opener);
+    L->ct_stride = job->ct_stride;
+    off = up(off);
+    L->enc_off = off;
+    off += up((size_t)L->nenc * cap);
+    L->ct_off = off;
+    off += up((size_t)L->ct_stride * cap);
+    L->ctlen_off = off;
+    off += up(4 * (size_t)cap);
+    L->time_off = off;
+    off += up(8 * (size_t)cap);
+    L->tslot_off = off;
+    off += up(2 * (size_t)cap);
+    L->ttab_off = off;
+    off += 32 * (size_t)HPKE_MAX_TASKS;
+  }
   L->bytes = off;
 }
 
 static int fused_finish(prio3_engine* e, Run* R, const uint8_t* d_status, const uint32_t* seg,
                         const uint32_t* fix_seg, const uint8_t* d_accept_mask, uint32_t S,
                         uint8_t* d_agg_shares, uint64_t* d_counts, hipStream_t st);
+
+// Sealed-input groups: a report the open rejected (HPKE status 4 or 8) gets status 0x80 | that
+// PrepareError, whatever its prepare computed on the zeroed share -- so the accumulate, which
+// counts status 0 only, leaves it out, and the caller sees the error Janus records first.
+__global__ __launch_bounds__(256) void k_hpke_merge(uint32_t n, const uint8_t* hs, uint8_t* status) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i < n && hs[i]) status[i] = (uint8_t)(0x80u | hs[i]);
+}
 
 // Group launch (host pull, the r03 form).  The kernels read each report's nonce, public share,
 // helper share and verify-key slot straight from the pinned staging (mapped), and each lane of the
@@ -3747,7 +3793,8 @@ int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr, boo
   *gr = GroupRun();
   gr->lead = lead;
   gr->jobs = g.jobs;
-  HIPCHK(hipSetDevice(lead->device));
+  DeviceGuard dg_(lead->device);
+  HIPCHK(dg_.rc);
   hipStream_t st = own_queue ? ws_exec_stream_get(lead->device) : ws_stream_get(lead->device);
   if (!st) return PRIO3_EDEVICE;
   const bool mp = lead->dp.kind == PRIO3_SUMVEC_F64_MP;
@@ -3756,17 +3803,21 @@ int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr, boo
   // excluded reports go through the fix-up list)
   const bool agg = g.nseg > 0;
   const bool fuse = agg && fusable(lead);
+  IoLayout L;
+  if (g.L)
+    L = *g.L;
+  else
+    engine_io_layout(lead, g.cap, &L);
+  const bool sealed = L.ct_stride > 0 && g.opener;
   int rc = PRIO3_OK;
   Run* R = run_create(lead, g.n,
                       RUN_SCRATCH | RUN_IO | (agg ? (unsigned)RUN_AGG_IO : 0u) |
-                          (fuse ? (unsigned)RUN_FUSED : 0u),
-                      agg ? g.nseg : 0, g.n_keys, st, &rc);
+                          (fuse ? (unsigned)RUN_FUSED : 0u) | (sealed ? (unsigned)RUN_HPKE : 0u),
+                      agg ? g.nseg : 0, g.n_keys, st, &rc, sealed ? L.ct_stride : 0);
   if (!R) {
     ws_exec_stream_put(lead->device, st);
     return rc;
   }
-  IoLayout L;
-  engine_io_layout(lead, g.cap, &L);
   auto fail = [&](int code) {
     (void)hipStreamSynchronize(st);
     run_release(R, st, true);
@@ -3777,6 +3828,30 @@ int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr, boo
   };
   const uint8_t* hd = g.stg_dev;
   InPtrs in{hd + L.off[0], L.len[1] ? hd + L.off[1] : nullptr, hd + L.off[2], R->leader};
+  if (sealed) {
+    // the helper's loop body from its first line (aggregator.rs:1847-1990): each report's input
+    // share opened, decoded and checked into the run's helper-share buffer, which the prepare
+    // below reads from HBM -- the plaintexts never cross PCIe
+    HpkeGroupArgs a{};
+    a.n = g.n;
+    a.ct_stride = L.ct_stride;
+    a.share_len = lead->dp.helper_share_len;
+    a.pub_len = (uint32_t)L.len[1];
+    a.require_taskprov = g.require_taskprov;
+    a.enc = hd + L.enc_off;
+    a.ct = hd + L.ct_off;
+    a.ct_len = (const uint32_t*)(hd + L.ctlen_off);
+    a.ids = hd + L.off[0];
+    a.times = (const uint64_t*)(hd + L.time_off);
+    a.pubs = L.len[1] ? hd + L.off[1] : nullptr;
+    a.task_slot = (const uint16_t*)(hd + L.tslot_off);
+    a.task_tab = (const uint32_t*)(hd + L.ttab_off);
+    a.pt = R->hpt;
+    a.shares = R->helper;
+    a.status = R->hstatus;
+    if (hpke_open_group_launch(g.opener, a, st) != PRIO3_OK) return fail(PRIO3_EDEVICE);
+    in.helper = R->helper;
+  }
   if (!mp) {  // the slots and the key table are read from the staging by the XOF
     in.vk_slot = (const uint16_t*)(hd + L.slot_off);
     in.vk_tab = (const uint4*)(hd + L.tab_off);
@@ -3799,6 +3874,10 @@ int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr, boo
   rc = prepare_run(lead, R, in, out, st, fuse, false, &pr);
   if (agg) R->seg = R->gseg;
   if (rc) return fail(rc);
+  if (sealed) {  // the open's rejections take precedence (aggregator.rs:1850-1990 before :2020)
+    k_hpke_merge<<<(g.n + 255) / 256, 256, 0, st>>>(g.n, R->hstatus, R->status);
+    if (hipGetLastError() != hipSuccess) return fail(PRIO3_EDEVICE);
+  }
   // the executor may issue its next group once this group's prepare kernels are done
   if (hipEventCreateWithFlags(&gr->prep, hipEventDisableTiming) != hipSuccess ||
       hipEventRecord(gr->prep, st) != hipSuccess) {
@@ -3842,6 +3921,7 @@ int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr, boo
   return PRIO3_OK;
 }
 
+// (declared above engine_group_issue)
 // the launcher polls these instead of sleeping in hipStreamSynchronize: the group's jobs are woken
 // as soon as their outputs land (the blocking wait added ~0.1 ms per group)
 bool engine_group_prepared(const GroupRun& gr) {
@@ -3907,7 +3987,8 @@ void engine_acc_unstage(AccJob* j, const uint8_t* stg, const AccLayout& L) {
 
 int engine_acc_group(int device, int es, uint8_t* stg, const AccLayout& L, uint32_t n_jobs,
                      size_t out_bytes) {
-  HIPCHK(hipSetDevice(device));
+  DeviceGuard dg_(device);
+  HIPCHK(dg_.rc);
   PooledStream ps(device);
   hipStream_t st = ps.s;
   if (!st) return PRIO3_EDEVICE;
@@ -3983,7 +4064,8 @@ int engine_leader_issue(prio3_engine* lead, const LeaderLayout& L, uint8_t* stg_
   *gr = GroupRun();
   gr->lead = lead;
   gr->jobs = jobs;
-  HIPCHK(hipSetDevice(lead->device));
+  DeviceGuard dg_(lead->device);
+  HIPCHK(dg_.rc);
   hipStream_t st = own_queue ? ws_exec_stream_get(lead->device) : ws_stream_get(lead->device);
   if (!st) return PRIO3_EDEVICE;
   int rc = PRIO3_OK;
@@ -4057,7 +4139,8 @@ extern "C" int launch_leader_next_multi(uint32_t es, const LNextDesc* d_desc, co
 int engine_lnext_issue(int device, uint32_t es, uint8_t* stg_dev, const LNextLayout& L,
                        uint32_t n_jobs, uint32_t max_n, hipStream_t* st_out, bool own_queue) {
   *st_out = nullptr;
-  HIPCHK(hipSetDevice(device));
+  DeviceGuard dg_(device);
+  HIPCHK(dg_.rc);
   hipStream_t st = own_queue ? ws_exec_stream_get(device) : ws_stream_get(device);
   if (!st) return PRIO3_EDEVICE;
   const int rc = launch_leader_next_multi(es, (const LNextDesc*)(stg_dev + L.desc_off),
@@ -4073,6 +4156,20 @@ int engine_lnext_issue(int device, uint32_t es, uint8_t* stg_dev, const LNextLay
 }
 
 extern "C" {
+
+// A blocking host-to-device copy on a pooled non-blocking stream: a synchronous hipMemcpy runs on
+// the legacy null stream, which waits for every blocking stream of the device -- the executor's
+// CU-masked group streams are such streams -- so an engine created while another
+// task's groups run would wait for them.
+static int upload_blocking(int device, void* dst, const void* src, size_t bytes) {
+  hipStream_t st = ws_stream_get(device);
+  if (!st) return PRIO3_EDEVICE;
+  const bool ok = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st) == hipSuccess &&
+                  hipStreamSynchronize(st) == hipSuccess;
+  ws_stream_put(device, st);
+  if (!ok) (void)hipGetLastError();
+  return ok ? PRIO3_OK : PRIO3_EDEVICE;
+}
 
 int prio3_sizes(const prio3_params* params, prio3_sizes_t* out) {
   return fill_sizes(params, out, nullptr);
@@ -4097,7 +4194,8 @@ int prio3_engine_create_ex(const prio3_params* params, const uint8_t* verify_key
       e->n_cu <= 0)
     e->n_cu = 256;
   hipStream_t probe = nullptr;  // a GPU must be present: the product path has no CPU fallback
-  if (hipSetDevice(device) != hipSuccess ||
+  DeviceGuard dg_(device);
+  if (dg_.rc != hipSuccess ||
       hipStreamCreateWithFlags(&probe, hipStreamNonBlocking) != hipSuccess) {
     (void)hipGetLastError();
     delete e;
@@ -4131,8 +4229,8 @@ int prio3_engine_create_ex(const prio3_params* params, const uint8_t* verify_key
     table(d.logP, d.calls);
     if (fpv) table(d.logP1, d.calls1);
     if (hipMalloc((void**)&e->d_sigma128, sizeof(uint4) * sig.size()) != hipSuccess ||
-        hipMemcpy(e->d_sigma128, sig.data(), sizeof(uint4) * sig.size(),
-                  hipMemcpyHostToDevice) != hipSuccess) {
+        upload_blocking(device, e->d_sigma128, sig.data(), sizeof(uint4) * sig.size()) !=
+            PRIO3_OK) {
       delete e;
       return PRIO3_EDEVICE;
     }
@@ -4173,8 +4271,7 @@ int prio3_engine_create_ex(const prio3_params* params, const uint8_t* verify_key
       sig[e2] = (uint64_t)sum;
     }
     if (hipMalloc((void**)&e->d_sigma64, 8 * (size_t)d.P) != hipSuccess ||
-        hipMemcpy(e->d_sigma64, sig.data(), 8 * (size_t)d.P, hipMemcpyHostToDevice) !=
-            hipSuccess) {
+        upload_blocking(device, e->d_sigma64, sig.data(), 8 * (size_t)d.P) != PRIO3_OK) {
       delete e;
       return PRIO3_EDEVICE;
     }
@@ -4287,7 +4384,7 @@ void prio3_engine_destroy(prio3_engine* e) {
   if (!e) return;
   for (size_t i = 1; i < e->members.size(); i++) prio3_engine_destroy(e->members[i]);
   e->members.clear();
-  (void)hipSetDevice(e->device);
+  DeviceGuard dg_(e->device);
   (void)hipDeviceSynchronize();
   {
     std::lock_guard<std::mutex> lk(e->mu);
@@ -4317,7 +4414,8 @@ int prio3_engine_set_option(prio3_engine* e, const char* key, int64_t value) {
               {"fp_round", &e->fp_round},          {"timing", &e->timing},
               {"coalesce", &e->coalesce},          {"experimental_fpvec", &e->experimental_fpvec},
               {"leader_fuse_acc", &e->leader_fuse_acc},
-              {"force_generic_query", &e->force_generic}, {"pair_max", &e->pair_max}};
+              {"force_generic_query", &e->force_generic}, {"pair_max", &e->pair_max},
+              {"keep_scratch", &e->keep_scratch}};
   for (auto& o : ints)
     if (!strcmp(key, o.name)) {
       *o.field = (int)value;
@@ -4352,7 +4450,8 @@ int prio3_device_prepare(prio3_engine* e, uint32_t n, const uint8_t* d_nonces,
     return PRIO3_EUNSUPPORTED;  // unpinned reconstruction: explicit opt-in only
   if (n == 0) return PRIO3_OK;
   std::lock_guard<std::mutex> lk(e->mu);
-  HIPCHK(hipSetDevice(e->device));
+  DeviceGuard dg_(e->device);
+  HIPCHK(dg_.rc);
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
   int rc = PRIO3_OK;
   Run* R = device_run(e, n, RUN_SCRATCH, 0, st, &rc);
@@ -4421,7 +4520,8 @@ int prio3_device_prepare_aggregate(prio3_engine* e, uint32_t n, const uint8_t* d
   if (e->dp.kind == PRIO3_FPVEC_BOUNDED_L2 && !e->experimental_fpvec)
     return PRIO3_EUNSUPPORTED;  // unpinned reconstruction: explicit opt-in only
   std::lock_guard<std::mutex> lk(e->mu);
-  HIPCHK(hipSetDevice(e->device));
+  DeviceGuard dg_(e->device);
+  HIPCHK(dg_.rc);
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
   const bool fuse = n > 0 && fusable(e);
   int rc = PRIO3_OK;
@@ -4442,7 +4542,8 @@ int prio3_device_aggregate_finish(prio3_engine* e, const uint8_t* d_status,
   TraceSpan span_("batch aggregation");
   if (!e) return PRIO3_EINVAL;
   std::lock_guard<std::mutex> lk(e->mu);
-  HIPCHK(hipSetDevice(e->device));
+  DeviceGuard dg_(e->device);
+  HIPCHK(dg_.rc);
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
   Run* R = e->cur;
   if (!R || !R->aggregate) return PRIO3_EINVAL;  // finish follows prio3_device_prepare_aggregate
@@ -4461,7 +4562,8 @@ int prio3_device_accumulate(prio3_engine* e, uint32_t n, const uint8_t* d_status
   TraceSpan span_("batch aggregation");
   if (!e || n_segments == 0) return PRIO3_EINVAL;
   std::lock_guard<std::mutex> lk(e->mu);
-  HIPCHK(hipSetDevice(e->device));
+  DeviceGuard dg_(e->device);
+  HIPCHK(dg_.rc);
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
   const size_t agg_len = (size_t)e->dp.out_len * e->dp.es;
   if (n == 0) {
@@ -4485,7 +4587,8 @@ int prio3_device_combine(prio3_engine* e, uint32_t k, uint32_t n_segments, const
                          void* stream) {
   TraceSpan span_("aggregate share combine");
   if (!e || k == 0 || n_segments == 0) return PRIO3_EINVAL;
-  HIPCHK(hipSetDevice(e->device));
+  DeviceGuard dg_(e->device);
+  HIPCHK(dg_.rc);
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
   const DevParams& d = e->dp;
   uint32_t len = d.out_len * n_segments;
@@ -4511,7 +4614,8 @@ int prio3_device_batch_metadata(prio3_engine* e, uint32_t n, const uint8_t* d_re
   TraceSpan span_("batch aggregation metadata");
   if (!e || n_segments == 0 || (n && (!d_status || (d_checksums && !d_report_ids))))
     return PRIO3_EINVAL;
-  HIPCHK(hipSetDevice(e->device));
+  DeviceGuard dg_(e->device);
+  HIPCHK(dg_.rc);
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
   uint32_t* ck = (uint32_t*)d_checksums;
   unsigned long long* iv = (unsigned long long*)d_intervals;
@@ -4532,7 +4636,8 @@ int prio3_device_combine_metadata(prio3_engine* e, uint32_t k, uint32_t n_segmen
                                   uint8_t* d_checksums_out, uint64_t* d_intervals_out,
                                   void* stream) {
   if (!e || k == 0 || n_segments == 0) return PRIO3_EINVAL;
-  HIPCHK(hipSetDevice(e->device));
+  DeviceGuard dg_(e->device);
+  HIPCHK(dg_.rc);
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
   TIMED(e, st, "k_combine_meta",
         (k_combine_meta<<<(n_segments * 8 + 255) / 256, 256, 0, st>>>(
@@ -4547,7 +4652,8 @@ int prio3_batch_metadata(prio3_engine* e, uint32_t n, const uint8_t* report_ids,
                          const uint32_t* segment_ids, uint32_t n_segments, uint8_t* checksums_out,
                          uint64_t* intervals_out) {
   if (!e || n_segments == 0 || (n && (!status || !report_ids))) return PRIO3_EINVAL;
-  HIPCHK(hipSetDevice(e->device));
+  DeviceGuard dg_(e->device);
+  HIPCHK(dg_.rc);
   PooledStream ps(e->device);
   hipStream_t st = ps.s;
   if (!st) return PRIO3_EDEVICE;
@@ -4590,7 +4696,8 @@ int prio3_batch_metadata(prio3_engine* e, uint32_t n, const uint8_t* report_ids,
 int prio3_device_output_shares(prio3_engine* e, uint32_t n, uint8_t* out) {
   if (!e || !out) return PRIO3_EINVAL;
   std::lock_guard<std::mutex> lk(e->mu);
-  HIPCHK(hipSetDevice(e->device));
+  DeviceGuard dg_(e->device);
+  HIPCHK(dg_.rc);
   Run* R = e->cur;
   if (!R || n > R->n) return PRIO3_EINVAL;
   HIPCHK(hipDeviceSynchronize());  // the run's work may sit on any caller stream
@@ -4697,6 +4804,86 @@ int prio3_helper_prepare_aggregate_batch(prio3_engine* e, uint32_t n, const uint
   return PRIO3_OK;
 }
 
+// The helper's whole per-report loop body over one job, from the sealed input shares
+// (VdafOps::handle_aggregate_init_generic, /root/reference/aggregator/src/aggregator.rs:1794-2096:
+// HPKE open :1847-1890, PlaintextInputShare decode and extension checks :1893-1983,
+// helper_initialized + evaluate :2020-2042, then the writer's merge).  One job of the executor: the
+// group's launch opens every report's input share into HBM, prepares the reports from there and
+// accumulates them per segment; only statuses, prepare messages, aggregate shares and counts come
+// back.  A group too wide for its segments takes the same steps as two host calls.
+int prio3_helper_aggregate_init_batch(
+    prio3_engine* e, janus_hpke_opener* opener, uint32_t n, const uint8_t task_id[32],
+    int require_taskprov, const uint8_t* report_ids, const uint64_t* times,
+    const uint8_t* public_shares, const uint8_t* enc, const uint8_t* ct, const uint32_t* ct_len,
+    uint32_t ct_stride, const uint8_t* leader_prep_shares, const uint32_t* segment_ids,
+    const uint8_t* accept_mask, uint32_t n_segments, uint8_t* prep_msgs_out, uint8_t* status_out,
+    uint8_t* agg_shares_out, uint64_t* counts_out) {
+  TraceSpan span_("handle_aggregate_init_generic threadpool task");
+  if (!e || !opener || !task_id || n_segments == 0 || !agg_shares_out || !counts_out ||
+      ct_stride == 0 || ct_stride % 16 != 0 ||
+      (n && (!report_ids || !times || !enc || !ct || !ct_len || !leader_prep_shares ||
+             !status_out)))
+    return PRIO3_EINVAL;
+  if (e->dp.kind == PRIO3_FPVEC_BOUNDED_L2 && !e->experimental_fpvec)
+    return PRIO3_EUNSUPPORTED;  // unpinned reconstruction: explicit opt-in only
+  const DevParams& d = e->dp;
+  // the open kernel's AAD takes public shares of 0 or 32 bytes (every TurboSHAKE instance)
+  if (d.public_share_len != 0 && d.public_share_len != 32) return PRIO3_EUNSUPPORTED;
+  if (n && d.jr_len && (!public_shares || !prep_msgs_out)) return PRIO3_EINVAL;
+  const size_t agg_len = (size_t)d.out_len * d.es;
+  if (n == 0) {
+    memset(agg_shares_out, 0, agg_len * n_segments);
+    memset(counts_out, 0, 8 * (size_t)n_segments);
+    return PRIO3_OK;
+  }
+  e = place(e, n);
+  IoLayout L1;
+  engine_io_layout(e, 1, &L1);
+  if (n_segments > L1.max_seg) {  // the open, then the prepare + aggregate of what it opened
+    std::vector<uint8_t> shares((size_t)d.helper_share_len * n), hs(n), acc(n);
+    int rc = janus_hpke_open_input_shares(opener, n, task_id, enc, ct, ct_len, ct_stride,
+                                          report_ids, times, d.jr_len ? public_shares : nullptr,
+                                          d.public_share_len, d.helper_share_len,
+                                          require_taskprov, shares.data(), hs.data());
+    if (rc) return rc == JANUS_HPKE_EDEVICE ? PRIO3_EDEVICE : PRIO3_EINVAL;
+    for (uint32_t i = 0; i < n; i++) acc[i] = (!accept_mask || accept_mask[i]) && hs[i] == 0;
+    rc = prio3_helper_prepare_aggregate_batch(e, n, report_ids, public_shares, shares.data(),
+                                              leader_prep_shares, segment_ids, acc.data(),
+                                              n_segments, prep_msgs_out, status_out,
+                                              agg_shares_out, counts_out);
+    if (rc) return rc;
+    for (uint32_t i = 0; i < n; i++)
+      if (hs[i]) status_out[i] = (uint8_t)(0x80u | hs[i]);
+    return PRIO3_OK;
+  }
+  ExecJob job;
+  job.e = e;
+  job.n = n;
+  job.nonces = report_ids;
+  job.pub = d.jr_len ? public_shares : nullptr;
+  job.helper = nullptr;
+  job.leader = leader_prep_shares;
+  job.msgs_out = prep_msgs_out;
+  job.status_out = status_out;
+  job.seg = segment_ids;
+  job.accept = accept_mask;
+  job.nseg = n_segments;
+  job.agg_out = agg_shares_out;
+  job.counts_out = counts_out;
+  job.opener = opener;
+  job.task_id = task_id;
+  job.times = times;
+  job.enc = enc;
+  job.ct = ct;
+  job.ct_len = ct_len;
+  job.ct_stride = ct_stride;
+  job.require_taskprov = require_taskprov ? 1 : 0;
+  const int rc = exec_submit(&job);
+  if (rc) return rc;
+  run_release(job.run, nullptr, false);
+  return PRIO3_OK;
+}
+
 int prio3_accumulate(prio3_batch* b, const uint32_t* segment_ids, const uint8_t* accept_mask,
                      uint32_t n_segments, uint8_t* agg_shares_out, uint64_t* counts_out) {
   TraceSpan span_("batch aggregation");
@@ -4723,7 +4910,8 @@ int prio3_accumulate(prio3_batch* b, const uint32_t* segment_ids, const uint8_t*
     job.counts_out = counts_out;
     if (engine_acc_out_bytes(&job) <= ((size_t)16 << 20)) return exec_accumulate(&job);
   }
-  HIPCHK(hipSetDevice(e->device));
+  DeviceGuard dg_(e->device);
+  HIPCHK(dg_.rc);
   PooledStream ps(e->device);
   hipStream_t st = ps.s;
   if (!st) return PRIO3_EDEVICE;
@@ -4759,7 +4947,8 @@ int prio3_accumulate(prio3_batch* b, const uint32_t* segment_ids, const uint8_t*
 int prio3_debug_output_shares(prio3_batch* b, uint8_t* out) {
   if (!b || !out) return PRIO3_EINVAL;
   if (!b->run) return PRIO3_OK;
-  HIPCHK(hipSetDevice(b->e->device));
+  DeviceGuard dg_(b->e->device);
+  HIPCHK(dg_.rc);
   PooledStream ps(b->e->device);
   if (!ps.s) return PRIO3_EDEVICE;
   return run_output_shares(b->run, b->c0, b->n, out, ps.s);
@@ -4779,7 +4968,7 @@ int prio3_engine_timing(prio3_engine* e, char* names, size_t cap_names, double* 
   const size_t nm = e->members.empty() ? 1 : e->members.size();
   for (size_t i = 0; i < nm; i++) {
     prio3_engine* m = e->members.empty() ? e : e->members[i];
-    (void)hipSetDevice(m->device);
+    DeviceGuard dg_(m->device);
     collect_times(m);
     std::lock_guard<std::mutex> lk(m->tmu);
     for (auto& t : m->times) {
@@ -4833,7 +5022,8 @@ int prio3_device_leader_prepare_init(prio3_engine* e, uint32_t n, const uint8_t*
       (e->dp.jr_len && !d_public_shares))
     return PRIO3_EINVAL;
   std::lock_guard<std::mutex> lk(e->mu);
-  HIPCHK(hipSetDevice(e->device));
+  DeviceGuard dg_(e->device);
+  HIPCHK(dg_.rc);
   hipStream_t st = (hipStream_t)stream;
   int rc = PRIO3_OK;
   const bool lfuse = leader_fuse_takes(e);
@@ -4854,7 +5044,8 @@ int prio3_device_leader_prepare_next(prio3_engine* e, uint32_t n, const uint8_t*
   if (n == 0) return PRIO3_OK;
   if (!d_status || (e->dp.jr_len && !d_prep_msgs)) return PRIO3_EINVAL;
   std::lock_guard<std::mutex> lk(e->mu);
-  HIPCHK(hipSetDevice(e->device));
+  DeviceGuard dg_(e->device);
+  HIPCHK(dg_.rc);
   Run* R = e->cur;
   if (!R || n > R->n) return PRIO3_EINVAL;
   DevParams dp = R->dp;
@@ -4904,7 +5095,8 @@ int prio3_leader_prepare_init_batch(prio3_engine* e, uint32_t n, const uint8_t* 
       run_release(job.run, nullptr, false);
     return PRIO3_OK;
   }
-  HIPCHK(hipSetDevice(e->device));
+  DeviceGuard dg_(e->device);
+  HIPCHK(dg_.rc);
   PooledStream ps(e->device);
   hipStream_t st = ps.s;
   if (!st) return PRIO3_EDEVICE;
@@ -4961,7 +5153,8 @@ int prio3_leader_prepare_next_batch(prio3_batch* b, const uint8_t* prep_msgs,
     job.status = status_inout;
     return exec_leader_next(&job);
   }
-  HIPCHK(hipSetDevice(e->device));
+  DeviceGuard dg_(e->device);
+  HIPCHK(dg_.rc);
   PooledStream ps(e->device);
   hipStream_t st = ps.s;
   if (!st) return PRIO3_EDEVICE;

@@ -10,11 +10,48 @@
 #include <cstddef>
 #include <cstdint>
 
+// ---- the calling thread's current device -------------------------------------------------
+// Every C entry point (and every runtime helper that needs a device current) makes its GPU
+// current through this guard and gives the calling thread its own device back on return: a Janus
+// rayon worker whose job a multi-GPU engine placed on GPU k must not come back bound to GPU k
+// (VERDICT r5 weak item 5).  hipSetDevice appears nowhere else in the library
+// (tests/test_abi.py::test_set_device_only_inside_the_guard).
+struct DeviceGuard {
+  explicit DeviceGuard(int device) {
+    if (hipGetDevice(&prev) != hipSuccess) {
+      (void)hipGetLastError();
+      prev = -1;
+    }
+    rc = prev == device ? hipSuccess : hipSetDevice(device);
+    restore = rc == hipSuccess && prev >= 0 && prev != device;
+  }
+  ~DeviceGuard() {
+    if (restore) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+  int prev = -1;
+  hipError_t rc = hipSuccess;
+  bool restore = false;
+};
+
+// ---- NUMA placement ---------------------------------------------------------------------------
+// The NUMA node of a GPU (its PCI function's numa_node in sysfs; -1 when unknown), and the host
+// CPUs of that node this process may run on (empty when unknown or when they are every CPU the
+// process has).  An 8-GPU node has two sockets: each GPU's executor launcher runs on its GPU's
+// node, and its pinned staging comes from that node's memory (hipHostMalloc takes host memory
+// from the pool of the current device's nearest CPU agent).
+int gpu_numa_node(int device);
+// NUMA node of the page holding host address p (-1 unknown); tests
+int host_page_node(const void* p);
+
 // ---- device scratch slabs ----------------------------------------------------------------
 // A slab is one hipMalloc'ed byte range.  Released slabs return to the GPU's pool with an event
 // recorded on the releasing stream; the next acquirer's stream waits on that event, so reuse is
 // stream-ordered and no host synchronisation is needed.  Idle slabs beyond the pool's byte
-// budget are freed (oldest first).
+// budget (1/8 of HBM) are freed, oldest first -- the slab just released too when it alone exceeds
+// the budget (an FPVec run, ~225 GB at 10^4 entries), unless its releaser asked to keep it
+// (engine option keep_scratch: a device-resident caller that runs such batches back to back).
 struct Slab {
   uint8_t* base = nullptr;
   size_t bytes = 0;
@@ -24,7 +61,7 @@ struct Slab {
 };
 // returns nullptr (rc = PRIO3_EDEVICE) when the device cannot provide `bytes`
 Slab* ws_acquire(int device, size_t bytes, hipStream_t st, int* rc);
-void ws_release(Slab* s, hipStream_t st);
+void ws_release(Slab* s, hipStream_t st, bool keep = false);
 // bytes currently held by the GPU's pool (idle + in use), for tests
 size_t ws_pool_bytes(int device, size_t* idle_bytes);
 
@@ -49,7 +86,11 @@ void ws_stream_put(int device, hipStream_t s);
 // groups in flight together run concurrently.  Plain pooled streams share the process's
 // GPU_MAX_HW_QUEUES queues, and two groups' streams on one queue ran back to back (r05e: every
 // launch on 'Queue 1', the 16-thread jobs line at 10.2-10.5 instead of 15.4-15.6 M reports/s).
-// Past that count the plain pool; put takes either kind back.
+// Past that count the plain pool; put takes either kind back.  hipExtStreamCreateWithCUMask takes
+// no flags, so these are BLOCKING streams: work on the legacy null stream (a synchronous
+// hipMemcpy, torch's default stream) waits for their groups and they for it.  The library itself
+// issues nothing on the null stream; a caller that mixes null-stream work with
+// light-load jobs serialises the two.
 #ifndef JANUS_EXEC_QUEUE_STREAMS  // A/B builds (tools/build_variant.sh): 0 = the plain pool only
 #define JANUS_EXEC_QUEUE_STREAMS 4
 #endif
@@ -64,6 +105,7 @@ void ws_exec_stream_put(int device, hipStream_t s);
 constexpr int EXEC_LANES = 8;
 struct prio3_engine;
 struct Run;
+struct janus_hpke_opener;
 struct ExecJob {
   prio3_engine* e;
   uint32_t n;
@@ -77,11 +119,24 @@ struct ExecJob {
   uint32_t nseg = 0;
   uint8_t* agg_out = nullptr;      // host [nseg][agg_share_len]
   uint64_t* counts_out = nullptr;  // host [nseg]
+  // the helper's whole loop body (prio3_helper_aggregate_init_batch, aggregator.rs:1794-2096):
+  // the job hands over sealed input shares (helper == nullptr) and the group opens them on the
+  // device first -- HPKE open, PlaintextInputShare decode, extension checks -- into the run's
+  // helper-share buffer, which the prepare then reads; the decrypted shares never leave HBM.
+  // status_out then carries the merged status (0x80 | PrepareError for reports the open rejects).
+  janus_hpke_opener* opener = nullptr;
+  const uint8_t* task_id = nullptr;  // [32], the AAD's task ID
+  const uint64_t* times = nullptr;   // [n] report times (AAD)
+  const uint8_t *enc = nullptr, *ct = nullptr;  // [n][Nenc], [n][ct_stride]
+  const uint32_t* ct_len = nullptr;             // [n]
+  uint32_t ct_stride = 0;
+  int require_taskprov = 0;
   // results
   int rc = 0;
   Run* run = nullptr;  // holds one reference for this job
   uint32_t c0 = 0;     // the job's first column in the run
   uint32_t slot = 0;   // the job's verify-key slot in its group
+  uint32_t tslot = 0;  // the job's task slot in its group (sealed-input jobs)
   uint32_t seg0 = 0;   // the job's first segment among the group's
   uint32_t pad0 = 0;   // pad columns [pad0, c0) before the job (aligned aggregating jobs)
 };
@@ -112,14 +167,23 @@ uint64_t exec_load(int exec_id);
 // outputs: prepare messages [cap][msg_len] and statuses [cap].
 // Groups with aggregating jobs also stage per-report group segment ids (u32) and accept bytes,
 // and receive [max_seg][agg_len] aggregate shares + [max_seg] u64 counts.
+// Groups of sealed-input jobs (ExecJob::opener) stage no helper shares (len[2] = 0) but, per
+// report, the HPKE ciphertext: enc [cap][nenc], ct [cap][ct_stride], ct_len (u32), the report time
+// (u64) and the task slot (u16), plus the task-ID table [HPKE_MAX_TASKS][8] (BE words).
 struct IoLayout {
   size_t len[4], off[4];
   size_t slot_off, tab_off, msg_off, status_off, msg_len;
   size_t seg_off, accept_off, agg_off, cnt_off, agg_len;
   uint32_t max_seg;
+  uint32_t nenc = 0, ct_stride = 0;  // ct_stride > 0: a sealed-input group
+  size_t enc_off = 0, ct_off = 0, ctlen_off = 0, time_off = 0, tslot_off = 0, ttab_off = 0;
   size_t bytes;
 };
-void engine_io_layout(const prio3_engine* e, uint32_t cap, IoLayout* L);
+// job: the group's first job (its opener and ciphertext stride shape a sealed-input group)
+void engine_io_layout(const prio3_engine* e, uint32_t cap, IoLayout* L,
+                      const ExecJob* job = nullptr);
+// equal keys may share one launch: engine_group_key, and for sealed-input jobs their HPKE shape
+uint64_t exec_job_key(const ExecJob* job);
 struct GroupView {
   uint32_t n, cap;   // reports staged, staging capacity
   uint8_t* stg;      // the staged inputs and outputs as the job threads see them (IoLayout)
@@ -127,6 +191,9 @@ struct GroupView {
   uint32_t n_keys;   // verify keys in the table
   int jobs;          // references the run must carry (one per job)
   uint32_t nseg;     // segments of the aggregating jobs (0: no job aggregates)
+  const IoLayout* L = nullptr;  // the staging layout (engine_io_layout of the group's first job)
+  janus_hpke_opener* opener = nullptr;  // sealed-input group: the keypair its reports open with
+  int require_taskprov = 0;
 };
 // segments one group can aggregate (its aggregating jobs' n_segments summed)
 constexpr uint32_t EXEC_MAX_SEGS = 1024;
@@ -273,6 +340,21 @@ struct HpkeLayout {
   uint32_t nenc;
 };
 constexpr uint32_t HPKE_MAX_TASKS = 256;
+size_t hpke_opener_nenc(const janus_hpke_opener* o);
+uint64_t hpke_opener_key(const janus_hpke_opener* o);  // keypair + suite (+ timing option)
+// The open kernel over a sealed-input prepare group, on the group's stream: inputs from the mapped
+// staging, the helper shares (zeroed unless opened) and the open status into the run.
+struct HpkeGroupArgs {
+  uint32_t n, ct_stride, share_len, pub_len;
+  int require_taskprov;
+  const uint8_t *enc, *ct, *ids, *pubs;
+  const uint32_t* ct_len;
+  const uint64_t* times;
+  const uint16_t* task_slot;
+  const uint32_t* task_tab;
+  uint8_t *pt, *shares, *status;  // device: plaintext scratch [n][ct_stride], outputs
+};
+int hpke_open_group_launch(janus_hpke_opener* o, const HpkeGroupArgs& a, hipStream_t st);
 int hpke_opener_device(const janus_hpke_opener* o);
 uint64_t hpke_group_key(const HpkeJob* j);
 void hpke_layout(const HpkeJob* j, uint32_t cap, HpkeLayout* L);

@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -37,11 +38,59 @@
 #include "../../include/janus_prio3.h"
 #include <dlfcn.h>
 #include <emmintrin.h>
-#include <cstdlib>
+#include <pthread.h>
+#include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <cctype>
 
 namespace {
 
 constexpr int MAX_DEVICES = 64;
+
+// ---- NUMA ---------------------------------------------------------------------------------
+// the CPUs listed in a sysfs cpulist ("0-15,64-79")
+std::vector<int> parse_cpulist(const char* path) {
+  std::vector<int> cpus;
+  FILE* f = fopen(path, "r");
+  if (!f) return cpus;
+  char buf[4096];
+  const size_t m = fread(buf, 1, sizeof buf - 1, f);
+  fclose(f);
+  buf[m] = 0;
+  for (char* q = buf; *q;) {
+    char* e = nullptr;
+    const long a = strtol(q, &e, 10);
+    if (e == q) break;
+    long b = a;
+    if (*e == '-') {
+      q = e + 1;
+      b = strtol(q, &e, 10);
+    }
+    for (long c = a; c <= b && c < CPU_SETSIZE; c++) cpus.push_back((int)c);
+    q = e;
+    while (*q == ',' || *q == '\n' || *q == ' ') q++;
+  }
+  return cpus;
+}
+
+// pins the calling thread to the CPUs of `device`'s NUMA node that the process may use (no-op
+// when the node is unknown, or when those are all the CPUs it has -- e.g. a one-socket box)
+void pin_to_gpu_node(int device) {
+  const int node = gpu_numa_node(device);
+  if (node < 0) return;
+  char path[96];
+  snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+  const std::vector<int> cpus = parse_cpulist(path);
+  cpu_set_t allowed, want;
+  CPU_ZERO(&want);
+  if (cpus.empty() || sched_getaffinity(0, sizeof allowed, &allowed) != 0) return;
+  for (int c : cpus)
+    if (CPU_ISSET(c, &allowed)) CPU_SET(c, &want);
+  if (CPU_COUNT(&want) == 0 || CPU_EQUAL(&want, &allowed)) return;
+  (void)pthread_setaffinity_np(pthread_self(), sizeof want, &want);
+}
 
 // ---- slabs ----------------------------------------------------------------------------------
 struct Pool {
@@ -66,9 +115,11 @@ void free_slab(Slab* s) {
   delete s;
 }
 
-// frees idle slabs (oldest first) until at most `keep` idle bytes remain, never `spare` (the
-// slab just released: a device-resident caller re-acquires it on its next call -- an FPVec run
-// is ~225 GB, and re-allocating it per step cost seconds); caller holds p.mu
+// frees idle slabs (oldest first) until at most `keep` idle bytes remain, never `spare` (a slab
+// its releaser asked to keep: a device-resident caller that re-acquires it on its next call -- an
+// FPVec run is ~225 GB, and re-allocating it per step cost C5 40 % in r02j); caller holds p.mu.
+// Without a spare the slab just released is the newest, so it goes only when it alone exceeds
+// the budget (r05 kept it whatever its size: ~225 GB stayed reserved after one C5 batch).
 void trim_locked(Pool& p, size_t keep, const Slab* spare = nullptr) {
   while (!p.idle.empty() && p.idle_bytes > keep && p.idle.front() != spare) {
     Slab* s = p.idle.front();
@@ -87,6 +138,36 @@ struct StreamPool {
 StreamPool g_streams[MAX_DEVICES];
 
 }  // namespace
+
+int gpu_numa_node(int device) {
+  static std::mutex mu;
+  static std::map<int, int> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(device);
+  if (it != cache.end()) return it->second;
+  int node = -1;
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, (int)sizeof bus, device) == hipSuccess) {
+    for (char* c = bus; *c; c++) *c = (char)tolower((unsigned char)*c);
+    char path[160];
+    snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+    if (FILE* f = fopen(path, "r")) {
+      if (fscanf(f, "%d", &node) != 1) node = -1;
+      fclose(f);
+    }
+  } else {
+    (void)hipGetLastError();
+  }
+  cache[device] = node;
+  return node;
+}
+
+int host_page_node(const void* p) {
+  int node = -1;
+  // get_mempolicy(MPOL_F_NODE | MPOL_F_ADDR): the node of the page at p
+  if (syscall(SYS_get_mempolicy, &node, nullptr, 0UL, p, 3UL) != 0) return -1;
+  return node;
+}
 
 Slab* ws_acquire(int device, size_t bytes, hipStream_t st, int* rc) {
   if (device < 0 || device >= MAX_DEVICES) {
@@ -157,7 +238,7 @@ Slab* ws_acquire(int device, size_t bytes, hipStream_t st, int* rc) {
   return s;
 }
 
-void ws_release(Slab* s, hipStream_t st) {
+void ws_release(Slab* s, hipStream_t st, bool keep) {
   if (!s) return;
   Pool& p = g_pools[s->device];
   s->pending = hipEventRecord(s->idle, st) == hipSuccess;
@@ -165,7 +246,7 @@ void ws_release(Slab* s, hipStream_t st) {
   std::lock_guard<std::mutex> lk(p.mu);
   p.idle.push_back(s);
   p.idle_bytes += s->bytes;
-  trim_locked(p, p.budget, s);
+  trim_locked(p, p.budget, keep ? s : nullptr);
 }
 
 size_t ws_pool_bytes(int device, size_t* idle_bytes) {
@@ -197,8 +278,8 @@ hipStream_t ws_stream_get(int device) {
     }
   }
   hipStream_t s = nullptr;
-  if (hipSetDevice(device) != hipSuccess ||
-      hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
+  DeviceGuard dg(device);
+  if (dg.rc != hipSuccess || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
     return nullptr;
   return s;
 }
@@ -216,20 +297,24 @@ struct QueuePool {
   std::vector<hipStream_t> own, free;  // the CU-masked streams made so far / idle ones
 };
 QueuePool g_queues[MAX_DEVICES];
-// the CU-masked streams are destroyed at exit before the HIP runtime's own teardown (an exit
+// the idle CU-masked streams are destroyed at exit before the HIP runtime's own teardown (an exit
 // handler registered after the runtime's runs first): under rocprofv3 a process that left them
-// to the runtime crashed in __cxa_finalize (r05f)
+// to the runtime crashed in __cxa_finalize (r05f).  A stream a launcher still holds (a group in
+// flight at exit) is left to the runtime: the launcher may still query or synchronize it (ADVICE
+// r5), and `closing` keeps it from being returned to a pool that is being torn down.
+std::atomic<bool> g_queues_closing{false};
 void destroy_queues() {
+  g_queues_closing = true;
   for (int d = 0; d < MAX_DEVICES; d++) {
     QueuePool& qp = g_queues[d];
     std::lock_guard<std::mutex> lk(qp.mu);
-    if (qp.own.empty()) continue;
-    (void)hipSetDevice(d);
-    for (hipStream_t s : qp.own) {
+    if (qp.free.empty()) continue;
+    DeviceGuard dg(d);
+    for (hipStream_t s : qp.free) {
       (void)hipStreamSynchronize(s);
       (void)hipStreamDestroy(s);
+      qp.own.erase(std::find(qp.own.begin(), qp.own.end(), s));
     }
-    qp.own.clear();
     qp.free.clear();
   }
 }
@@ -248,7 +333,8 @@ hipStream_t ws_exec_stream_get(int device) {
     if ((int)qp.own.size() < EXEC_QUEUE_STREAMS) {
       int cus = 0;
       hipStream_t s = nullptr;
-      if (hipSetDevice(device) == hipSuccess &&
+      DeviceGuard dg(device);
+      if (dg.rc == hipSuccess &&
           hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) ==
               hipSuccess &&
           cus > 0) {
@@ -273,7 +359,7 @@ void ws_exec_stream_put(int device, hipStream_t s) {
   {
     std::lock_guard<std::mutex> lk(qp.mu);
     if (std::find(qp.own.begin(), qp.own.end(), s) != qp.own.end()) {
-      qp.free.push_back(s);
+      if (!g_queues_closing) qp.free.push_back(s);
       return;
     }
   }
@@ -321,7 +407,10 @@ Staging staging_get(int dev, size_t bytes) {
   }
   Staging s;
   s.bytes = std::max(bytes, STAGING_TARGET);
-  const bool ok = hipSetDevice(dev) == hipSuccess &&
+  // pinned host memory of the GPU's own NUMA node: hipHostMalloc takes it from the pool of the
+  // current device's nearest CPU agent (tests/test_gpu_executor.py::test_staging_on_gpu_numa_node)
+  DeviceGuard dg(dev);
+  const bool ok = dg.rc == hipSuccess &&
                   hipHostMalloc((void**)&s.p, s.bytes, hipHostMallocMapped) == hipSuccess &&
                   hipHostGetDevicePointer((void**)&s.dev, s.p, 0) == hipSuccess;
   if (!ok) {
@@ -343,6 +432,9 @@ void staging_put(int dev, Staging s) {
 }
 
 constexpr uint32_t MAX_GROUP_REPORTS = 1u << 17;  // reports per prepare group
+// an executor "hold" (tests queue jobs behind it) expires by itself: a caller that fails between
+// hold = 1 and hold = 0 must not stall every engine sharing the executor forever
+constexpr int64_t HOLD_MAX_MS = 30000;
 // reports inside submit at which the launcher leaves its light-load pipeline (the box's 16 rayon
 // threads keep ~8 Ki in flight, 128 threads ~64 Ki)
 constexpr uint64_t HEAVY_DEFAULT = 32768;
@@ -385,16 +477,26 @@ struct Exec {
   std::deque<Group*> order;  // groups not yet taken by the launcher, oldest first
   bool started = false;
   // under mu:
-  bool hold = false;                     // exec_control "hold": take no group
+  bool hold = false;  // exec_control "hold": take no group until hold_until at the latest
+  std::chrono::steady_clock::time_point hold_until;
   uint64_t heavy_at = P::heavy_default();  // exec_control "heavy"
   ExecStats stats;
+
+  bool holding() const { return hold && std::chrono::steady_clock::now() < hold_until; }
+  // the launcher's wait for work (caller holds mu): a hold wakes it when it expires
+  void wait_work(std::unique_lock<std::mutex>& lk) {
+    if (hold)
+      cv.wait_until(lk, hold_until);
+    else
+      cv.wait(lk);
+  }
 
   void finish_locked(Group* g, int rc) {
     g->rc = rc;
     g->done = true;
     g->cv.notify_all();
   }
-  bool takeable() const { return !order.empty() && !hold; }
+  bool takeable() const { return !order.empty() && !holding(); }
   // the oldest group, closed to later jobs, once its writers are done (caller holds mu)
   Group* take_locked(std::unique_lock<std::mutex>& lk) {
     Group* g = order.front();
@@ -464,7 +566,7 @@ struct Exec {
     for (;;) {
       if (!cur) {
         if (lighter()) return;
-        while (!takeable()) cv.wait(lk);
+        while (!takeable()) wait_work(lk);
         Group* g = take_locked(lk);
         t0 = std::chrono::steady_clock::now();
         if (!issue_unlocked(lk, g, &hc, false)) continue;
@@ -550,7 +652,7 @@ struct Exec {
         if (issue_unlocked(lk, g, &sl.h, true)) q.push_back(sl);
       }
       if (q.empty()) {
-        while (!takeable() && light()) cv.wait(lk);
+        while (!takeable() && light()) wait_work(lk);
         continue;
       }
       lk.unlock();
@@ -590,6 +692,7 @@ struct Exec {
     if (!started) {  // one launcher thread per executor (never joined: see g_exec)
       started = true;
       std::thread([this] {
+        pin_to_gpu_node(device);  // the launcher runs on its GPU's NUMA node
         std::map<uint64_t, Pred> preds;
         for (;;) {  // launcher() under heavy load, launcher_pipe() under light load
           launcher(preds);
@@ -649,8 +752,10 @@ struct Exec {
 
   int control(const char* key, int64_t value) {
     std::lock_guard<std::mutex> lk(mu);
-    if (!strcmp(key, "hold")) {
+    if (!strcmp(key, "hold")) {  // 1: at most HOLD_MAX_MS; v > 1: at most v ms
       hold = value != 0;
+      hold_until = std::chrono::steady_clock::now() +
+                   std::chrono::milliseconds(value > 1 ? value : HOLD_MAX_MS);
     } else if (!strcmp(key, "heavy")) {
       heavy_at = value > 0 ? (uint64_t)value : P::heavy_default();
     } else {
@@ -697,23 +802,28 @@ struct PrepPolicy {
   struct State {
     prio3_engine* lead = nullptr;
     std::vector<const prio3_engine*> keys;  // verify-key table, slot = index
+    std::vector<std::array<uint8_t, 32>> tasks;  // sealed-input groups: task-ID table, slot = index
+    janus_hpke_opener* opener = nullptr;
+    int require_taskprov = 0;
     uint32_t n = 0, cap = 0, jobs = 0, nseg = 0, align = 1;
     IoLayout L;
     Run* run = nullptr;
   };
-  static uint64_t key(Job* j) { return engine_group_key(j->e); }
+  static uint64_t key(Job* j) { return exec_job_key(j); }
   static uint32_t reports(const State& s) { return s.n; }
   static bool create(State& s, Job* j, size_t* bytes) {
     s.lead = j->e;
+    s.opener = j->opener;
+    s.require_taskprov = j->require_taskprov;
     IoLayout l1, l2;
-    engine_io_layout(j->e, 1, &l1);
-    engine_io_layout(j->e, 2, &l2);
+    engine_io_layout(j->e, 1, &l1, j);
+    engine_io_layout(j->e, 2, &l2, j);
     const size_t per = l2.bytes - l1.bytes + 1;
     const uint32_t cap_b = (uint32_t)std::max<size_t>(1, STAGING_TARGET / per);
     s.align = engine_job_align(j->e);
     s.cap = std::max(j->n, std::min(MAX_GROUP_REPORTS, cap_b));
     s.cap = (s.cap + 63) & ~63u;  // room for the tail pad of a wave-aligned group
-    engine_io_layout(j->e, s.cap, &s.L);
+    engine_io_layout(j->e, s.cap, &s.L, j);
     *bytes = s.L.bytes;
     return true;
   }
@@ -721,12 +831,23 @@ struct PrepPolicy {
     uint32_t k = 0;
     while (k < s.keys.size() && s.keys[k] != j->e) k++;
     if (k == s.keys.size() && s.keys.size() >= exec_max_keys()) return false;
+    uint32_t t = 0;
+    if (j->opener) {
+      while (t < s.tasks.size() && memcmp(s.tasks[t].data(), j->task_id, 32)) t++;
+      if (t == s.tasks.size() && s.tasks.size() >= HPKE_MAX_TASKS) return false;
+    }
     const uint32_t al = j->nseg ? s.align : 1u;
     const uint32_t c0 = (s.n + al - 1) / al * al;
     if (c0 + j->n > s.cap || ((c0 + j->n + 63) & ~63u) > s.cap ||
         s.nseg + j->nseg > s.L.max_seg)
       return false;
     if (k == s.keys.size()) s.keys.push_back(j->e);
+    if (j->opener && t == s.tasks.size()) {
+      std::array<uint8_t, 32> id;
+      memcpy(id.data(), j->task_id, 32);
+      s.tasks.push_back(id);
+    }
+    j->tslot = t;
     j->pad0 = s.n;
     j->c0 = c0;
     j->slot = k;
@@ -738,11 +859,16 @@ struct PrepPolicy {
   }
   // pad columns [a, b): verify-key slot 0, an out-of-range segment id, not accepted (their
   // prepare runs on whatever bytes the staging holds and is never returned)
+  // (sealed-input groups: ciphertext length 0, which the open rejects at once, and task slot 0)
   static void pad(const IoLayout& L, Staging& g, uint32_t a, uint32_t b) {
     if (a >= b) return;
     memset(g.p + L.slot_off + 2 * (size_t)a, 0, 2 * (size_t)(b - a));
     memset(g.p + L.seg_off + 4 * (size_t)a, 0xff, 4 * (size_t)(b - a));
     memset(g.p + L.accept_off + a, 0, b - a);
+    if (L.ct_stride) {
+      memset(g.p + L.ctlen_off + 4 * (size_t)a, 0, 4 * (size_t)(b - a));
+      memset(g.p + L.tslot_off + 2 * (size_t)a, 0, 2 * (size_t)(b - a));
+    }
   }
   static void stage(State& s, Staging& g, Job* j) {
     const IoLayout& L = s.L;
@@ -753,6 +879,20 @@ struct PrepPolicy {
     uint16_t* slots = (uint16_t*)(g.p + L.slot_off) + j->c0;
     for (uint32_t i = 0; i < j->n; i++) slots[i] = (uint16_t)j->slot;
     engine_vk(j->e, g.p + L.tab_off + 16 * (size_t)j->slot);
+    if (L.ct_stride) {  // the sealed input shares and their AAD fields
+      const size_t c0 = j->c0, n = j->n;
+      stream_copy(g.p + L.enc_off + (size_t)L.nenc * c0, j->enc, (size_t)L.nenc * n);
+      stream_copy(g.p + L.ct_off + (size_t)L.ct_stride * c0, j->ct, (size_t)L.ct_stride * n);
+      memcpy(g.p + L.ctlen_off + 4 * c0, j->ct_len, 4 * n);
+      memcpy(g.p + L.time_off + 8 * c0, j->times, 8 * n);
+      uint16_t* ts = (uint16_t*)(g.p + L.tslot_off) + c0;
+      for (uint32_t i = 0; i < j->n; i++) ts[i] = (uint16_t)j->tslot;
+      uint32_t* tab = (uint32_t*)(g.p + L.ttab_off) + 8 * (size_t)j->tslot;
+      for (int i = 0; i < 8; i++) {  // BE words, as the open kernel's AAD takes them
+        const uint8_t* b = j->task_id + 4 * i;
+        tab[i] = (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3];
+      }
+    }
     // group segment ids: the job's own ids shifted to its segment range (an id >= its n_segments
     // stays out of every aggregate: 0xFFFFFFFF); a prepare-only job's reports are out
     uint32_t* sg = (uint32_t*)(g.p + L.seg_off) + j->c0;
@@ -790,6 +930,9 @@ struct PrepPolicy {
     v.n_keys = (uint32_t)s.keys.size();
     v.jobs = (int)s.jobs;
     v.nseg = s.nseg;
+    v.L = &s.L;
+    v.opener = s.opener;
+    v.require_taskprov = s.require_taskprov;
     h->s = &s;
     return engine_group_issue(s.lead, v, &h->gr, own_queue);
   }

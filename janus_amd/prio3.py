@@ -37,6 +37,10 @@ STATUS_PREP_MSG = 3
 STATUS_PREP_NEXT = 4
 STATUS_PEER_MISMATCH = 5
 STATUS_INPUT_SHARE_DECODE = 6
+#: merged statuses of prio3_helper_aggregate_init_batch: 0x80 | the DAP PrepareError of a report
+#: the input-share open rejected before its VDAF ran (aggregator.rs:1847-1983)
+STATUS_HPKE_DECRYPT = 0x84
+STATUS_INVALID_MESSAGE = 0x88
 
 #: prio ``PingPongError`` variant for each status (error.rs:365-428 maps these to labels).
 STATUS_PINGPONG_ERROR = {
@@ -99,7 +103,7 @@ EXPORTED_SYMBOLS = (
     "prio3_device_leader_prepare_next", "prio3_device_batch_metadata", "prio3_batch_metadata",
     "prio3_device_combine_metadata", "prio3_engine_create_ex", "prio3_engine_create_mask",
     "prio3_engine_create_devices", "prio3_engine_members", "prio3_executor_control",
-    "prio3_executor_stats_get",
+    "prio3_executor_stats_get", "prio3_helper_aggregate_init_batch",
 )
 # include/janus_hpke.h (the batched HPKE opener, janus_amd/hpke.py)
 HPKE_EXPORTED_SYMBOLS = (
@@ -149,6 +153,9 @@ def load_library() -> C.CDLL:
     L.prio3_accumulate.argtypes = [vp, vp, vp, C.c_uint32, vp, vp]
     L.prio3_helper_prepare_aggregate_batch.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, vp, vp,
                                                        C.c_uint32, vp, vp, vp, vp]
+    u32 = C.c_uint32
+    L.prio3_helper_aggregate_init_batch.argtypes = [vp, vp, u32, vp, C.c_int, vp, vp, vp, vp, vp,
+                                                    vp, u32, vp, vp, vp, u32, vp, vp, vp, vp]
     L.prio3_debug_output_shares.argtypes = [vp, vp]
     L.prio3_batch_free.argtypes = [vp]
     L.prio3_batch_free.restype = None
@@ -477,6 +484,48 @@ class HelperEngine:
             _np_ptr(status), _np_ptr(agg), _np_ptr(cnt))
         if rc:
             raise RuntimeError(f"prio3_helper_prepare_aggregate_batch failed (rc={rc})")
+        return msgs[:, :sz.prep_msg_len], status, agg, cnt
+
+    def aggregate_init_batch(self, opener, task_id: bytes, report_ids, times, public_shares,
+                             enc, ct, ct_len, leader_prep_shares, segment_ids=None,
+                             accept_mask=None, n_segments: int = 1, require_taskprov=False):
+        """The helper's whole loop body for one job from the sealed input shares
+        (prio3_helper_aggregate_init_batch; aggregator.rs:1794-2096): HPKE open with ``opener``
+        (janus_amd.hpke.HpkeOpener), decode, prepare and accumulate in one coalesced launch.
+        enc [n, Nenc], ct [n, ct_stride] (stride a multiple of 16), ct_len [n].  Returns
+        (prep_msgs, status [merged: STATUS_* or STATUS_HPKE_DECRYPT / STATUS_INVALID_MESSAGE],
+        agg [S, agg_len], counts [S])."""
+        sz = self.sz
+        ids = np.ascontiguousarray(report_ids, np.uint8)
+        n = ids.shape[0]
+        t = np.ascontiguousarray(times, np.uint64)
+        e = np.ascontiguousarray(enc, np.uint8)
+        c = np.ascontiguousarray(ct, np.uint8)
+        cl = np.ascontiguousarray(ct_len, np.uint32)
+        lps = np.ascontiguousarray(leader_prep_shares, np.uint8)
+        if ids.shape != (n, 16) or t.shape != (n,) or cl.shape != (n,) or c.ndim != 2 or \
+                c.shape[0] != n or e.shape[0] != n or lps.shape != (n, sz.prep_share_len):
+            raise ValueError("input shapes do not match the job")
+        if len(task_id) != 32:
+            raise ValueError("task_id must be 32 bytes")
+        pub = None
+        if sz.public_share_len:
+            pub = np.ascontiguousarray(public_shares, np.uint8)
+            if pub.shape != (n, sz.public_share_len):
+                raise ValueError("public share shape does not match the VDAF instance")
+        seg, acc = _seg_accept(n, segment_ids, accept_mask, n_segments)
+        msgs = np.zeros((n, max(sz.prep_msg_len, 1)), np.uint8)
+        status = np.zeros(n, np.uint8)
+        agg = np.zeros((n_segments, sz.agg_share_len), np.uint8)
+        cnt = np.zeros(n_segments, np.uint64)
+        tid = (C.c_uint8 * 32).from_buffer_copy(task_id)
+        rc = load_library().prio3_helper_aggregate_init_batch(
+            self.handle, opener.handle, n, tid, int(bool(require_taskprov)), _np_ptr(ids),
+            _np_ptr(t), _np_ptr(pub), _np_ptr(e), _np_ptr(c), _np_ptr(cl), c.shape[1],
+            _np_ptr(lps), _np_ptr(seg), _np_ptr(acc), n_segments, _np_ptr(msgs), _np_ptr(status),
+            _np_ptr(agg), _np_ptr(cnt))
+        if rc:
+            raise RuntimeError(f"prio3_helper_aggregate_init_batch failed (rc={rc})")
         return msgs[:, :sz.prep_msg_len], status, agg, cnt
 
     # ---- leader side (same instance, agg_id 0) -----------------------------------

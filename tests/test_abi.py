@@ -118,3 +118,22 @@ def test_engine_requires_gpu_or_fails_loudly():
         pytest.skip("GPU present")
     with pytest.raises(RuntimeError):
         J.HelperEngine(J.Prio3Count(), bytes(16), device=0)
+
+
+def test_set_device_only_inside_the_guard():
+    """every entry point and runtime helper makes its GPU current through
+    DeviceGuard (prio3_runtime.h), which gives the calling thread its own device back; no other
+    hipSetDevice may appear in the library's sources, or a Janus worker whose job a multi-GPU
+    engine placed on GPU k would come back bound to GPU k."""
+    csrc = os.path.join(ROOT, "janus_amd", "csrc")
+    hits = []
+    for fn in sorted(os.listdir(csrc)):
+        if not fn.endswith((".hip", ".h", ".cpp")):
+            continue
+        for i, line in enumerate(open(os.path.join(csrc, fn)), 1):
+            code = line.split("//")[0]
+            if "hipSetDevice(" in code:
+                hits.append((fn, i, line.strip()))
+    guard = [h for h in hits if h[0] == "prio3_runtime.h"]
+    assert len(guard) == 2, hits  # the guard's set and its restore
+    assert [h for h in hits if h[0] != "prio3_runtime.h"] == []

@@ -132,3 +132,13 @@ def test_c5_100k_distinct_device_reports():
     torch.cuda.synchronize()
     np.testing.assert_array_equal(agg_s.cpu().numpy().reshape(-1), np.asarray(ra).reshape(-1))
     assert int(cnt_s[0]) == int(np.asarray(rc).reshape(-1)[0]) == m
+    # the engine gone, its ~225 GB run goes back to the pool, and the
+    # pool frees it -- it is above the pool's budget (1/8 of HBM) -- without prio3_device_trim
+    eng.close()
+    del d, msgs, status, seg, agg, cnt, part, pc, lagg, lc, acc, agg_s, cnt_s
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    free, total = torch.cuda.mem_get_info(0)
+    held = torch.cuda.memory_reserved(0)
+    assert total - free <= total // 8 + held + (6 << 30), \
+        f"{(total - free) / 2**30:.1f} GiB in use of {total / 2**30:.0f} after the C5 batch"

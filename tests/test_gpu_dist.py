@@ -210,13 +210,30 @@ def _kfd_process_limit():
     return v if v > 0 else 8
 
 
-def _kfd_holders():
-    """Our processes that hold /dev/kfd open, i.e. have a GPU context (this pytest process once
-    any earlier test touched the GPU)."""
-    n = 0
+def _own_pids():
+    """This process and its descendants (not every process on the box)."""
+    children = {}
     for pid in os.listdir("/proc"):
         if not pid.isdigit():
             continue
+        try:
+            ppid = int(open(f"/proc/{pid}/stat").read().rsplit(")", 1)[1].split()[1])
+        except (OSError, IndexError, ValueError):
+            continue
+        children.setdefault(ppid, []).append(int(pid))
+    out, todo = [], [os.getpid()]
+    while todo:
+        p = todo.pop()
+        out.append(p)
+        todo += children.get(p, [])
+    return out
+
+
+def _kfd_holders():
+    """Our processes (this one and its descendants) that hold /dev/kfd open, i.e. have a GPU
+    context (this pytest process once any earlier test touched the GPU)."""
+    n = 0
+    for pid in _own_pids():
         try:
             fds = os.listdir(f"/proc/{pid}/fd")
             if any(os.readlink(f"/proc/{pid}/fd/{fd}") == "/dev/kfd" for fd in fds):
@@ -226,7 +243,7 @@ def _kfd_holders():
     return n
 
 
-def test_config_sumvec_eight_ranks_gloo_one_gpu():
+def test_config_sumvec_kfd_limited_ranks_gloo_one_gpu():
     """`bench.py --role config --vdaf sumvec` as up to 8 gloo ranks sharing C3's
     whole 1M reports on the one GPU of the box: the combined helper aggregate plus the combined
     leader aggregate unshards to the sum of all measurements, every report is counted, and rank
@@ -244,16 +261,15 @@ def test_config_sumvec_eight_ranks_gloo_one_gpu():
     ranks still cover the whole 1M."""
     limit, holders = _kfd_process_limit(), _kfd_holders()
     ranks = min(8, limit - holders)
-    assert ranks >= 2, f"{holders} processes already hold the GPU (limit {limit})"
+    print(f"ranks = {ranks} (KFD process limit {limit}, {holders} of our processes on the GPU)")
+    if ranks < 2:
+        pytest.skip(f"{holders} of our processes already hold the GPU (limit {limit})")
     per_rank = -(-1_000_000 // ranks)
     # the ranks need the GPU's memory (C3's 128 KB measurement shares: ~25 GB per 125k-report
-    # rank): this process's idle scratch slabs go back first -- after test_fpvec the pool keeps
-    # the last FPVec run's slab (hundreds of GB) for the next call (r05k: the ranks ran out of
-    # memory with 0.7 GB free)
+    # rank).  Since r06 the pool frees a released slab above its budget by itself (r05 kept the
+    # last FPVec run's ~225 GB slab and this test had to call prio3_device_trim first)
     if holders:
         import torch
-        from janus_amd import prio3 as J
-        J.trim_device_pool(0)
         torch.cuda.empty_cache()
         free, total = torch.cuda.mem_get_info(0)
         assert free > ranks * (28 << 30), f"{free / 2**30:.0f} of {total / 2**30:.0f} GiB free"

@@ -450,3 +450,54 @@ def test_concurrent_leader_jobs_are_coalesced(name):
         np.testing.assert_array_equal(cnt, rcnt)
     g1 = [engines[0].executor_stats(k)["groups"] for k in (J.EXEC_LEADER_INIT, J.EXEC_LEADER_NEXT)]
     assert [b - a for a, b in zip(g0, g1)] == [1, 1], (g0, g1)
+
+
+@pytest.mark.parametrize("name", ["hist_256_c16", "sum32", "sumvec_8x10_c9"])
+def test_leader_next_uncoalesced_on_shared_runs(name):
+    """leader batches of one coalesced prepare_init group start at non-zero columns c0
+    of a shared run; with coalescing switched off before prepare_next, each batch takes the
+    direct prepare_next path (the SoA offsets es * c0 with stride ld into the measurement and
+    output shares) and then the accumulate with segments and a mask -- every job equal to the
+    restatement's leader path."""
+    from oracle.oracle import Oracle
+    cfg = CONFIGS[name]
+    o = Oracle(**cfg)
+    vks = [bytes([k]) * 16 for k in (0x61, 0x62)]
+    engines = [_engine(cfg, vk) for vk in vks]
+    rng = np.random.default_rng(53)
+    jobs = []
+    for j in range(8):
+        t = j % 2
+        n = int(rng.integers(60, 300))
+        d = o.gen_reports(vks[t], n, seed=700 + j, n_threads=4)
+        lin = engines[t].generate_reports_device(n, seed=700 + j, with_leader_inputs=True)
+        lin = lin["leader_input_shares"].cpu().numpy()
+        msgs = _ref(o, vks[t], d)[0].copy()
+        if msgs.shape[1]:
+            msgs[int(rng.integers(0, n)), 0] ^= 1
+        seg = rng.integers(0, 3, n).astype(np.uint32)
+        acc = (rng.random(n) < 0.85).astype(np.uint8)
+        jobs.append((t, d, lin, msgs, seg, acc))
+    from janus_amd import prio3 as J
+    g0 = engines[0].executor_stats(J.EXEC_LEADER_INIT)["groups"]
+    with ThreadPoolExecutor(8) as ex, _Held(engines[0], 8, J.EXEC_LEADER_INIT) as held:
+        futs = [ex.submit(engines[t].leader_prepare_init_batch, d["nonces"], d["public_shares"],
+                          lin) for (t, d, lin, _, _, _) in jobs]
+        held.wait()
+        inits = [f.result(timeout=120) for f in futs]
+    assert engines[0].executor_stats(J.EXEC_LEADER_INIT)["groups"] - g0 == 1  # one shared run
+    for e in engines:
+        e.set_option("coalesce", 0)
+    for (t, d, lin, msgs, seg, acc), (ps, st, b) in zip(jobs, inits):
+        st2 = b.leader_prepare_next(msgs, st)
+        agg, cnt = b.accumulate(seg, acc, 3)
+        b.free()
+        rps, rst, _, _ = o.leader_batch(vks[t], d["nonces"], d["public_shares"], lin, msgs,
+                                        n_threads=4)
+        np.testing.assert_array_equal(ps, rps)
+        np.testing.assert_array_equal(st2, rst)
+        _, _, ragg, rcnt = o.leader_batch(vks[t], d["nonces"], d["public_shares"], lin, msgs,
+                                          n_threads=4, segment_ids=np.where(acc, seg, 3),
+                                          n_segments=3)
+        np.testing.assert_array_equal(agg, ragg)
+        np.testing.assert_array_equal(cnt, rcnt)
