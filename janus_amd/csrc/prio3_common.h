@@ -83,6 +83,11 @@ struct InPtrs {
   uint32_t* seg_dst = nullptr;
   const uint8_t* accept_src = nullptr;
   uint8_t* accept_dst = nullptr;
+  // leader executor groups (k_leader_prep): the leader input shares are read by the kernel
+  // straight from the mapped staging, transposed there by the job threads into [element][lin_ld]
+  // 16-byte cells, so each load of a wave is 64 consecutive cells (one 1 KiB PCIe read) -- 0:
+  // AoS rows of leader_share_len bytes (device memory)
+  uint32_t lin_ld = 0;
 };
 
 // the verify key of report r (query randomness: XOF(vk, dst(5), [PROOFS] || nonce))

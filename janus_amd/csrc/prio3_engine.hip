@@ -885,10 +885,20 @@ DEV void leader_jr_body(const DevParams& p, const InPtrs& in, const Scratch& sc,
   const int M = (int)p.meas_len;
   const uint32_t PL = p.proof_len;
   const uint4* row = (const uint4*)(in.helper + (size_t)r * p.leader_share_len);
+  // the executor's SoA staging (InPtrs::lin_ld): element e of report r at cell e * lin_ld + r
+  const uint4* soa = (const uint4*)in.helper + r;
+  const size_t sld = in.lin_ld;
+  auto rel = [&](int e) -> uint4 { return sld ? soa[(size_t)e * sld] : row[e]; };
   uint32_t bad = 0;
   uint32_t nonce[4], kb[4];
   load16(in.nonces + 16 * (size_t)r, nonce);
-  load16((const uint8_t*)(row + (M + PL)), kb);
+  {
+    const uint4 k = rel(M + (int)PL);
+    kb[0] = k.x;
+    kb[1] = k.y;
+    kb[2] = k.z;
+    kb[3] = k.w;
+  }
   uint32_t pre[11];
   {
     Msg m;
@@ -903,7 +913,7 @@ DEV void leader_jr_body(const DevParams& p, const InPtrs& in, const Scratch& sc,
   uint4* meas = (uint4*)sc.meas;
   auto ldel = [&](int e) -> uint4 {
     const bool ok = e >= 0 && e < M;
-    const uint4 v = row[ok ? e : 0];
+    const uint4 v = rel(ok ? e : 0);
     return ok ? v : make_uint4(0, 0, 0, 0);
   };
   // element e (owned by this window): canonical check and the SoA copy
@@ -987,7 +997,7 @@ DEV void leader_jr_body(const DevParams& p, const InPtrs& in, const Scratch& sc,
   {  // the proofs share: canonical check and SoA copy
     uint4* proofs = (uint4*)sc.proofs;
     for (uint32_t e = 0; e < PL; e++) {
-      const uint4 v = row[M + e];
+      const uint4 v = rel(M + (int)e);
       if (!F::lt_p(mk128(v.x, v.y, v.z, v.w))) bad = 1;
       proofs[(size_t)e * ld + r] = v;
     }
@@ -3555,10 +3565,20 @@ static int leader_init_fpvec(prio3_engine* e, Run* R, const uint8_t* d_nonces,
 #define LEADER_FUSED 1  // k_leader_prep (k_leader_jr + the query in one launch); 0: two kernels (A/B)
 #endif
 // vk_slot / vk_tab (nullable): per-report verify keys of a coalesced group of several tasks
+// The instances whose leader prepare_init is one k_leader_prep launch (the only leader kernel that
+// reads the leader input shares from SoA staging, InPtrs::lin_ld)
+static bool leader_prep_takes(const prio3_engine* e) {
+  const DevParams& dp = e->dp;
+  return LEADER_FUSED && e->leader_fast && (dp.kind == PRIO3_HISTOGRAM || dp.kind == PRIO3_SUMVEC) &&
+         dp.jr_len && (dp.P == 32 || dp.P == 16 || dp.P == 8) &&
+         dp.leader_share_len == 16 * (dp.meas_len + dp.proof_len + 1);
+}
+
 static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
                            const uint8_t* d_public_shares, const uint8_t* d_leader_input_shares,
                            uint8_t* d_prep_shares, uint8_t* d_status, hipStream_t st,
-                           const uint16_t* vk_slot = nullptr, const uint4* vk_tab = nullptr) {
+                           const uint16_t* vk_slot = nullptr, const uint4* vk_tab = nullptr,
+                           uint32_t lin_ld = 0) {
   DevParams dp = R->dp;
   dp.force_slow = (uint32_t)e->force_slow;
   const uint32_t n = R->n;
@@ -3580,6 +3600,7 @@ static int leader_init_run(prio3_engine* e, Run* R, const uint8_t* d_nonces,
     InPtrs in{d_nonces, d_public_shares, d_leader_input_shares, nullptr};
     in.vk_slot = vk_slot;
     in.vk_tab = vk_tab;
+    in.lin_ld = LEADER_FUSED ? lin_ld : 0u;
     OutPtrs out{d_prep_shares, d_status};
     const uint32_t blocks = (n + 255) / 256, blocks64 = (n + 63) / 64;
     // R->lfused: the wave partials of the share for segment 0, fixed up at accumulate
@@ -4053,6 +4074,8 @@ void engine_leader_layout(const prio3_engine* e, uint32_t cap, LeaderLayout* L) 
   L->status_off = off;
   off += up(cap);
   L->bytes = off;
+  L->cap = cap;
+  L->lin_soa = leader_prep_takes(e);
 }
 
 // A leader group: the explicit input shares (5.6 KB per Histogram(256) report) go to the run by
@@ -4082,12 +4105,18 @@ int engine_leader_issue(prio3_engine* lead, const LeaderLayout& L, uint8_t* stg_
     ws_exec_stream_put(lead->device, st);
     return code;
   };
-  if (hipMemcpyAsync(R->linput, stg_dev + L.off[2], L.len[2] * n, hipMemcpyDefault, st) !=
-      hipSuccess)
+  // k_leader_prep reads the transposed staging itself, each wave load one 1 KiB PCIe read, while
+  // other waves run Keccak and the query (r05's one DMA of the whole group's
+  // 5.6 KB shares ran ahead of the kernels, in series with them); the other leader kernels read
+  // AoS rows from the run
+  if (!L.lin_soa &&
+      hipMemcpyAsync(R->linput, stg_dev + L.off[2], L.len[2] * n, hipMemcpyDefault, st) !=
+          hipSuccess)
     return fail(PRIO3_EDEVICE);
   rc = leader_init_run(lead, R, stg_dev + L.off[0], L.len[1] ? stg_dev + L.off[1] : nullptr,
-                       R->linput, R->leader, R->status, st, (const uint16_t*)(stg_dev + L.slot_off),
-                       (const uint4*)(stg_dev + L.tab_off));
+                       L.lin_soa ? stg_dev + L.off[2] : R->linput, R->leader, R->status, st,
+                       (const uint16_t*)(stg_dev + L.slot_off), (const uint4*)(stg_dev + L.tab_off),
+                       L.lin_soa ? L.cap : 0u);
   if (rc) return fail(rc);
   if (hipEventCreateWithFlags(&gr->prep, hipEventDisableTiming) != hipSuccess ||
       hipEventRecord(gr->prep, st) != hipSuccess) {

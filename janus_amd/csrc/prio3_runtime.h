@@ -269,9 +269,13 @@ struct LeaderJob {
   uint32_t c0 = 0, slot = 0;
 };
 // staging of a leader group with room for cap reports: inputs, key slots, key table, outputs
+// lin_soa: the leader input shares are staged transposed, 16-byte cell e of report c at
+// off[2] + 16 * (e * cap + c), and the kernel reads them there over PCIe (no DMA into the run)
 struct LeaderLayout {
   size_t len[3], off[3];  // nonces, public shares, leader input shares
   size_t slot_off, tab_off, ps_len, ps_off, status_off, bytes;
+  uint32_t cap = 0;
+  bool lin_soa = false;
 };
 void engine_leader_layout(const prio3_engine* e, uint32_t cap, LeaderLayout* L);
 // one DMA of the staged inputs into the run, the leader kernels, the outputs back into the staging

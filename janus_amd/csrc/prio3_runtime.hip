@@ -795,6 +795,24 @@ void stream_copy(uint8_t* dst, const uint8_t* src, size_t n) {
   _mm_sfence();
 }
 
+// Rows of `cells` 16-byte cells (n reports from src) into the columns [c0, c0 + n) of a
+// [cell][cap] staging array, with non-temporal stores: eight reports at a time, so each cell's
+// stores fill two whole 64-byte lines and the eight source rows stream through the cache once.
+void stream_transpose16(uint8_t* dst, size_t cap, size_t c0, const uint8_t* src, uint32_t n,
+                        uint32_t cells) {
+  const size_t row = 16 * (size_t)cells;
+  for (uint32_t r0 = 0; r0 < n; r0 += 8) {
+    const uint32_t k = std::min(8u, n - r0);
+    const uint8_t* s0 = src + row * r0;
+    for (uint32_t e = 0; e < cells; e++) {
+      __m128i* d = (__m128i*)(dst + 16 * (e * cap + c0 + r0));
+      for (uint32_t i = 0; i < k; i++)
+        _mm_stream_si128(d + i, _mm_loadu_si128((const __m128i*)(s0 + row * i + 16 * (size_t)e)));
+    }
+  }
+  _mm_sfence();
+}
+
 // ---- prepare groups ----
 struct PrepPolicy {
   typedef ExecJob Job;
@@ -1037,8 +1055,13 @@ struct LeaderPolicy {
   static void stage(State& s, Staging& g, Job* j) {
     const LeaderLayout& L = s.L;
     const uint8_t* src[3] = {j->nonces, j->pub, j->linput};
-    for (int f = 0; f < 3; f++)
-      if (L.len[f] && src[f]) stream_copy(g.p + L.off[f] + L.len[f] * j->c0, src[f], L.len[f] * j->n);
+    for (int f = 0; f < 3; f++) {
+      if (!L.len[f] || !src[f]) continue;
+      if (f == 2 && L.lin_soa)
+        stream_transpose16(g.p + L.off[2], L.cap, j->c0, src[2], j->n, (uint32_t)(L.len[2] / 16));
+      else
+        stream_copy(g.p + L.off[f] + L.len[f] * j->c0, src[f], L.len[f] * j->n);
+    }
     uint16_t* slots = (uint16_t*)(g.p + L.slot_off) + j->c0;
     for (uint32_t i = 0; i < j->n; i++) slots[i] = (uint16_t)j->slot;
     engine_vk(j->e, g.p + L.tab_off + 16 * (size_t)j->slot);
