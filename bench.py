@@ -207,7 +207,9 @@ def main():
                     help="--role jobs: reports per aggregation job (aggregation_job_creator.rs:63-64)")
     ap.add_argument("--jobs-call", choices=["combined", "two"], default="combined",
                     help="--role jobs: prio3_helper_prepare_aggregate_batch per job (one round "
-                         "trip) or prio3_helper_prepare_batch + prio3_accumulate (two)")
+                         "trip) or prio3_helper_prepare_batch + prio3_accumulate (two); the "
+                         "leader: prio3_leader_prepare_next_aggregate_batch after the init, or "
+                         "prio3_leader_prepare_next_batch + prio3_accumulate")
     ap.add_argument("--tasks", type=int, default=4,
                     help="--role jobs: tasks (verify keys) of the VDAF instance the jobs rotate over")
     ap.add_argument("--jobs-role", choices=["helper", "leader", "hpke", "init"], default="helper",
@@ -609,7 +611,8 @@ def jobs_main(args):
     devices = None if args.devices is None else [int(x) for x in args.devices.replace("+", ",").split(",")]
     if args.jobs_role == "leader":
         out = leader_jobs_line(args.threads, args.job_size, n_jobs, args.tasks, devices,
-                               not args.no_cpu_baseline, args.cpu_seconds, args.exec_heavy)
+                               not args.no_cpu_baseline, args.cpu_seconds, args.exec_heavy,
+                               combined=args.jobs_call == "combined")
     elif args.jobs_role == "hpke":
         out = hpke_jobs_line(args.threads, args.job_size, n_jobs, args.tasks,
                              not args.no_cpu_baseline, args.cpu_seconds, args.exec_heavy)
@@ -785,7 +788,8 @@ def jobs_line(T, js, n_jobs, K, opts=(), combined=True, with_cpu=True, check_tas
                speedup_vs_cpu=(value / cpu["value"]) if cpu else None)
 
 
-def leader_jobs_line(T, js, n_jobs, K, devices=None, with_cpu=True, cpu_seconds=10.0, heavy=0):
+def leader_jobs_line(T, js, n_jobs, K, devices=None, with_cpu=True, cpu_seconds=10.0, heavy=0,
+                     combined=True):
     """the leader's production call shape.  T host threads, each a worker of
     Janus's aggregation job driver stepping whole jobs (aggregation_job_driver.rs:397-415,
     677-691, one spawn per job at :449-462): prio3_leader_prepare_init_batch on the job's explicit
@@ -820,7 +824,7 @@ def leader_jobs_line(T, js, n_jobs, K, devices=None, with_cpu=True, cpu_seconds=
     lib.janus_jobs_run_leader.restype = C.c_double
     vp = C.c_void_p
     lib.janus_jobs_run_leader.argtypes = [C.POINTER(vp), C.c_int, vp, C.c_int, C.c_int, C.c_int,
-                                          C.c_uint32, vp, vp, vp, vp, vp, vp, vp, vp]
+                                          C.c_uint32, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int]
     eng_arr = (vp * K)(*[e.handle.value for e in engines])
     ps = np.zeros((n_jobs * js, sz.prep_share_len), np.uint8)
     status = np.zeros(n_jobs * js, np.uint8)
@@ -833,7 +837,7 @@ def leader_jobs_line(T, js, n_jobs, K, devices=None, with_cpu=True, cpu_seconds=
         return lib.janus_jobs_run_leader(eng_arr, K, C.cast(C.pointer(sz), vp), T, jobs, js, pool,
                                          P(host["nonces"]), P(host["public_shares"]),
                                          P(host["leader_input_shares"]), P(host["msgs"]), P(ps),
-                                         P(status), P(counts), P(agg))
+                                         P(status), P(counts), P(agg), int(combined))
 
     run(max(K, min(n_jobs, 8 * T)))  # warmup
     g0 = [engines[0].executor_stats(k)["groups"] for k in (J.EXEC_LEADER_INIT,
@@ -893,6 +897,9 @@ def leader_jobs_line(T, js, n_jobs, K, devices=None, with_cpu=True, cpu_seconds=
                               frac=value * h2d / 63e9, h2d_bytes_per_report=h2d, traffic=None),
                 coalescing=dict(init_launches=g1[0] - g0[0], next_launches=g1[1] - g0[1],
                                 jobs=n_jobs),
+                call=("prio3_leader_prepare_init_batch + prio3_leader_prepare_next_aggregate_batch"
+                      if combined else "prio3_leader_prepare_init_batch + "
+                      "prio3_leader_prepare_next_batch + prio3_accumulate"),
                 checks=dict(all_finished=bool((status == 0).all()),
                             counts_ok=bool((counts == js).all()), prep_shares_match_cpu=ps_ok,
                             statuses_match_cpu=statuses_ok, every_job_matches_cpu=jobs_ok,

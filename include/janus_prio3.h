@@ -315,6 +315,16 @@ int prio3_leader_prepare_init_batch(prio3_engine* engine, uint32_t n, const uint
                                     uint8_t* status_out, prio3_batch** batch_out);
 int prio3_leader_prepare_next_batch(prio3_batch* batch, const uint8_t* prep_msgs,
                                     uint8_t* status_inout);
+/* prio3_leader_prepare_next_batch followed by prio3_accumulate of the same batch, in ONE launch of
+ * the GPU's prepare_next executor (concurrent jobs' checks and merges together): for a leader that
+ * knows the job's batch identifiers and accept mask when the helper's response arrives
+ * (process_response_from_helper, aggregation_job_driver.rs:629-691, then the writer's merge,
+ * aggregation_job_writer.rs:591-695).  Same arguments and results as the two calls; the batch
+ * keeps its output shares (it may be accumulated again) until prio3_batch_free. */
+int prio3_leader_prepare_next_aggregate_batch(prio3_batch* batch, const uint8_t* prep_msgs,
+                                              uint8_t* status_inout, const uint32_t* segment_ids,
+                                              const uint8_t* accept_mask, uint32_t n_segments,
+                                              uint8_t* agg_shares_out, uint64_t* counts_out);
 int prio3_device_leader_prepare_init(prio3_engine* engine, uint32_t n, const uint8_t* d_nonces,
                                      const uint8_t* d_public_shares,
                                      const uint8_t* d_leader_input_shares, uint8_t* d_prep_shares,

@@ -1551,6 +1551,7 @@ int janus_hpke_opener_create(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id,
     delete o;
     return JANUS_HPKE_EDEVICE;
   }
+  ws_warm(device);  // the GPU's pooled streams, before any job runs
   *out = o;
   return JANUS_HPKE_SUCCESS;
 }

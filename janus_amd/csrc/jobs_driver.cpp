@@ -102,11 +102,12 @@ double janus_jobs_run(prio3_engine** engines, int n_engines, const prio3_sizes_t
 // leader input shares lin[..][leader_input_share_len], prio3_leader_prepare_next_batch on the
 // helper's prepare messages msgs[..][prep_msg_len], prio3_accumulate, prio3_batch_free.  Job j's
 // reports are chosen as in janus_jobs_run; ps_out[jobs * job_size][prep_share_len].
+// combined = 1: prio3_leader_prepare_next_aggregate_batch instead of the last two calls.
 double janus_jobs_run_leader(prio3_engine** engines, int n_engines, const prio3_sizes_t* szp,
                              int threads, int jobs, int job_size, uint32_t pool,
                              const uint8_t* nonces, const uint8_t* pub, const uint8_t* lin,
                              const uint8_t* msgs, uint8_t* ps_out, uint8_t* status_out,
-                             uint64_t* counts_out, uint8_t* agg_out) {
+                             uint64_t* counts_out, uint8_t* agg_out, int combined) {
   const prio3_sizes_t sz = *szp;
   const uint32_t span = pool - (uint32_t)job_size + 1;
   return run_pool(threads, jobs, [&](int j) {
@@ -119,12 +120,16 @@ double janus_jobs_run_leader(prio3_engine** engines, int n_engines, const prio3_
         sz.public_share_len ? pub + (size_t)sz.public_share_len * r0 : nullptr,
         lin + (size_t)sz.leader_input_share_len * r0, ps_out + (size_t)sz.prep_share_len * o,
         status_out + o, &b);
-    if (rc == PRIO3_OK)
-      rc = prio3_leader_prepare_next_batch(
-          b, sz.prep_msg_len ? msgs + (size_t)sz.prep_msg_len * r0 : nullptr, status_out + o);
+    const uint8_t* m = sz.prep_msg_len ? msgs + (size_t)sz.prep_msg_len * r0 : nullptr;
+    uint8_t* agg = agg_out + (size_t)sz.agg_share_len * j;
     uint64_t cnt = 0;
-    if (rc == PRIO3_OK)
-      rc = prio3_accumulate(b, nullptr, nullptr, 1, agg_out + (size_t)sz.agg_share_len * j, &cnt);
+    if (rc == PRIO3_OK && combined) {
+      rc = prio3_leader_prepare_next_aggregate_batch(b, m, status_out + o, nullptr, nullptr, 1,
+                                                     agg, &cnt);
+    } else if (rc == PRIO3_OK) {
+      rc = prio3_leader_prepare_next_batch(b, m, status_out + o);
+      if (rc == PRIO3_OK) rc = prio3_accumulate(b, nullptr, nullptr, 1, agg, &cnt);
+    }
     prio3_batch_free(b);
     counts_out[j] = cnt;
     return rc == PRIO3_OK;

@@ -4081,8 +4081,11 @@ void engine_leader_layout(const prio3_engine* e, uint32_t cap, LeaderLayout* L) 
 // A leader group: the explicit input shares (5.6 KB per Histogram(256) report) go to the run by
 // one DMA, the kernels read the nonces, public shares and verify-key slots from the mapped
 // staging, and one copy launch writes the prepare shares and statuses back into it.
-int engine_leader_issue(prio3_engine* lead, const LeaderLayout& L, uint8_t* stg_dev, uint32_t n,
-                        uint32_t n_keys, int jobs, GroupRun* gr, bool own_queue) {
+#ifndef LEADER_OUT_DMA  // A/B builds: 0 = the prepare shares back by the k_pull copy kernel
+#define LEADER_OUT_DMA 1
+#endif
+int engine_leader_issue(prio3_engine* lead, const LeaderLayout& L, uint8_t* stg, uint8_t* stg_dev,
+                        uint32_t n, uint32_t n_keys, int jobs, GroupRun* gr, bool own_queue) {
   (void)n_keys;
   *gr = GroupRun();
   gr->lead = lead;
@@ -4124,13 +4127,22 @@ int engine_leader_issue(prio3_engine* lead, const LeaderLayout& L, uint8_t* stg_
     if (gr->prep) (void)hipEventDestroy(gr->prep);
     gr->prep = nullptr;
   }
+  // the prepare shares (560 B per Histogram(256) report, 17 MB per 31k group) go back by the
+  // copy engine: written by k_pull into the mapped staging they took 0.88 ms per group (~20 GB/s,
+  // r06c kernel trace); the statuses by the copy kernel
   PullRanges o{};
   o.src[0] = R->status;
   o.dst[0] = stg_dev + L.status_off;
   o.bytes[0] = n;
-  o.src[1] = R->leader;
-  o.dst[1] = stg_dev + L.ps_off;
-  o.bytes[1] = L.ps_len * n;
+  if (LEADER_OUT_DMA) {
+    if (hipMemcpyAsync(stg + L.ps_off, R->leader, L.ps_len * n, hipMemcpyDeviceToHost, st) !=
+        hipSuccess)
+      return fail(PRIO3_EDEVICE);
+  } else {
+    o.src[1] = R->leader;
+    o.dst[1] = stg_dev + L.ps_off;
+    o.bytes[1] = L.ps_len * n;
+  }
   const size_t tot = o.bytes[0] + o.bytes[1];
   k_pull<<<(unsigned)std::min<size_t>(256, (tot / 16 + 255) / 256 + 1), 256, 0, st>>>(o);
   if (hipGetLastError() != hipSuccess) return fail(PRIO3_EDEVICE);
@@ -4159,28 +4171,102 @@ void engine_lnext_stage(LNextJob* j, uint8_t* stg, const LNextLayout& L) {
   D.jr = d.jr_len ? 1u : 0u;
   if (D.jr && j->msgs) memcpy(stg + L.msg_off + 16 * (size_t)j->rep_off, j->msgs, 16 * (size_t)j->n);
   memcpy(stg + L.status_off + j->rep_off, j->status, j->n);
+  if (j->nseg) {  // its accumulate descriptor (offsets from the accumulate area's base)
+    const AccLayout& A = L.acc;
+    uint8_t* base = stg + L.acc_base;
+    AccDesc& X = ((AccDesc*)(base + A.desc_off))[j->acc_slot];
+    X.src = (const uint8_t*)(own_out(d) ? R->sc.out : R->sc.meas) + es * j->c0;
+    X.status = R->status + j->c0;  // the device verdicts, after the check of the same launch
+    X.ld = d.ld_out;
+    X.n = j->n;
+    X.nseg = j->nseg;
+    X.out_len = d.out_len;
+    X.flags = (j->seg ? 1u : 0u) | (j->accept ? 2u : 0u);
+    X.seg_off = A.seg_off + 4 * (size_t)j->rep_off;
+    X.acc_off = A.acc_off + j->rep_off;
+    X.agg_off = A.out_off + j->out_off;
+    const size_t agg = (size_t)d.out_len * es * j->nseg;
+    X.cnt_off = X.agg_off + ((agg + 7) & ~(size_t)7);
+    if (j->seg) memcpy(base + X.seg_off, j->seg, 4 * (size_t)j->n);
+    if (j->accept) memcpy(base + X.acc_off, j->accept, j->n);
+  }
+}
+
+size_t engine_lnext_out_bytes(const LNextJob* j) {
+  if (!j->nseg) return 0;
+  const size_t agg = (size_t)j->run->dp.out_len * j->run->dp.es * j->nseg;
+  return ((agg + 7) & ~(size_t)7) + 8 * (size_t)j->nseg;
+}
+
+void engine_lnext_unstage(LNextJob* j, const uint8_t* stg, const LNextLayout& L) {
+  memcpy(j->status, stg + L.status_off + j->rep_off, j->n);
+  if (!j->nseg) return;
+  const DevParams& d = j->run->dp;
+  const uint8_t* base = stg + L.acc_base;
+  const AccDesc& X = ((const AccDesc*)(base + L.acc.desc_off))[j->acc_slot];
+  memcpy(j->agg_out, base + X.agg_off, (size_t)d.out_len * d.es * j->nseg);
+  memcpy(j->counts_out, base + X.cnt_off, 8 * (size_t)j->nseg);
 }
 
 extern "C" int launch_leader_next_multi(uint32_t es, const LNextDesc* d_desc, const uint8_t* d_msgs,
                                         uint8_t* d_status, uint32_t n_jobs, uint32_t max_n,
                                         hipStream_t st);
 
-int engine_lnext_issue(int device, uint32_t es, uint8_t* stg_dev, const LNextLayout& L,
-                       uint32_t n_jobs, uint32_t max_n, hipStream_t* st_out, bool own_queue) {
+int engine_lnext_issue(int device, uint32_t es, uint8_t* stg, uint8_t* stg_dev,
+                       const LNextLayout& L, uint32_t n_jobs, uint32_t max_n, uint32_t n_acc,
+                       size_t out_bytes, hipStream_t* st_out, Slab** slab_out, bool own_queue) {
   *st_out = nullptr;
+  *slab_out = nullptr;
   DeviceGuard dg_(device);
   HIPCHK(dg_.rc);
   hipStream_t st = own_queue ? ws_exec_stream_get(device) : ws_stream_get(device);
   if (!st) return PRIO3_EDEVICE;
-  const int rc = launch_leader_next_multi(es, (const LNextDesc*)(stg_dev + L.desc_off),
-                                          stg_dev + L.msg_off, stg_dev + L.status_off, n_jobs,
-                                          max_n, st);
+  int rc = launch_leader_next_multi(es, (const LNextDesc*)(stg_dev + L.desc_off),
+                                    stg_dev + L.msg_off, stg_dev + L.status_off, n_jobs, max_n, st);
+  Slab* sl = nullptr;
+  if (rc == PRIO3_OK && n_acc) {
+    // the aggregating jobs' accumulate (leader_continued's output shares merged by the writer,
+    // aggregation_job_writer.rs:591-695) on the same stream: descriptors, segment ids and accept
+    // bytes into a device area, k_acc_multi, the aggregate shares and counts back into the staging
+    const AccLayout& A = L.acc;
+    uint8_t* host = stg + L.acc_base;  // the accumulate area as the host sees it
+    const AccDesc* D = (const AccDesc*)(host + A.desc_off);
+    uint32_t reps = 0, max_len = 0;
+    for (uint32_t i = 0; i < n_acc; i++) {
+      reps = std::max(reps, (uint32_t)((D[i].acc_off - A.acc_off) + D[i].n));
+      max_len = std::max(max_len, D[i].out_len);
+    }
+    sl = ws_acquire(device, A.bytes, st, &rc);
+    if (sl) {
+      uint8_t* b = sl->base;
+      if (hipMemcpyAsync(b + A.desc_off, host + A.desc_off, sizeof(AccDesc) * n_acc,
+                         hipMemcpyHostToDevice, st) != hipSuccess ||
+          hipMemcpyAsync(b + A.seg_off, host + A.seg_off, 4 * (size_t)reps, hipMemcpyHostToDevice,
+                         st) != hipSuccess ||
+          hipMemcpyAsync(b + A.acc_off, host + A.acc_off, reps, hipMemcpyHostToDevice, st) !=
+              hipSuccess) {
+        rc = PRIO3_EDEVICE;
+      } else {
+        dim3 grid(max_len, n_acc);
+        if (es == 16)
+          k_acc_multi<Fp128><<<grid, 256, 0, st>>>((const AccDesc*)(b + A.desc_off), b);
+        else
+          k_acc_multi<Fp64><<<grid, 256, 0, st>>>((const AccDesc*)(b + A.desc_off), b);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(host + A.out_off, b + A.out_off, out_bytes, hipMemcpyDeviceToHost,
+                           st) != hipSuccess)
+          rc = PRIO3_EDEVICE;
+      }
+    }
+  }
   if (rc != PRIO3_OK) {
     (void)hipStreamSynchronize(st);
+    if (sl) ws_release(sl, st);
     ws_exec_stream_put(device, st);
     return rc;
   }
   *st_out = st;
+  *slab_out = sl;
   return PRIO3_OK;
 }
 
@@ -4231,6 +4317,7 @@ int prio3_engine_create_ex(const prio3_params* params, const uint8_t* verify_key
     return PRIO3_EDEVICE;
   }
   ws_stream_put(device, probe);  // the first member of the GPU's stream pool
+  ws_warm(device);               // the rest of it, before any job runs
   const bool fpv = e->dp.kind == PRIO3_FPVEC_BOUNDED_L2;
   if (((e->dp.kind == PRIO3_HISTOGRAM || e->dp.kind == PRIO3_SUMVEC) &&
        (e->dp.P == 32 || e->dp.P == 64 || e->dp.P == 128)) ||
@@ -5212,6 +5299,45 @@ int prio3_leader_prepare_next_batch(prio3_batch* b, const uint8_t* prep_msgs,
   HIPCHK(hipStreamSynchronize(st));
   if (e->timing) collect_times(e);
   return PRIO3_OK;
+}
+
+// leader_continued on the helper's messages and the writer's merge of the job's output shares
+// (/root/reference/aggregator/src/aggregator/aggregation_job_driver.rs:677-691, then
+// aggregation_job_writer.rs:591-695) in one launch of the prepare_next executor: the check of
+// each report, then the per-segment sum of the reports it kept, for many jobs at once.
+int prio3_leader_prepare_next_aggregate_batch(prio3_batch* b, const uint8_t* prep_msgs,
+                                              uint8_t* status_inout, const uint32_t* segment_ids,
+                                              const uint8_t* accept_mask, uint32_t n_segments,
+                                              uint8_t* agg_shares_out, uint64_t* counts_out) {
+  TraceSpan span_("leader VDAF preparation");
+  if (!b || !status_inout || n_segments == 0 || !agg_shares_out || !counts_out)
+    return PRIO3_EINVAL;
+  prio3_engine* e = b->e;
+  const uint32_t n = b->n;
+  const DevParams& d = e->dp;
+  Run* R = b->run;
+  const bool one = R && n && leader_coalescable(e) && n <= LNEXT_MAX_REPS && R->msgs &&
+                   R->linput;
+  LNextJob job;
+  job.device = e->device;
+  job.run = R;
+  job.nseg = n_segments;
+  if (one && engine_lnext_out_bytes(&job) <= LNEXT_MAX_OUT) {
+    if (d.jr_len && !prep_msgs) return PRIO3_EINVAL;
+    job.c0 = b->c0;
+    job.n = n;
+    job.msgs = d.jr_len ? prep_msgs : nullptr;
+    job.status = status_inout;
+    job.seg = segment_ids;
+    job.accept = accept_mask;
+    job.agg_out = agg_shares_out;
+    job.counts_out = counts_out;
+    return exec_leader_next(&job);
+  }
+  int rc = prio3_leader_prepare_next_batch(b, prep_msgs, status_inout);
+  if (rc == PRIO3_OK)
+    rc = prio3_accumulate(b, segment_ids, accept_mask, n_segments, agg_shares_out, counts_out);
+  return rc;
 }
 
 int prio3_trace_enabled(void) { return trace_enabled() ? 1 : 0; }

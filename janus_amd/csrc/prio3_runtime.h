@@ -97,6 +97,13 @@ void ws_stream_put(int device, hipStream_t s);
 constexpr int EXEC_QUEUE_STREAMS = JANUS_EXEC_QUEUE_STREAMS;
 hipStream_t ws_exec_stream_get(int device);
 void ws_exec_stream_put(int device, hipStream_t s);
+// Creates the GPU's pooled streams up front (WARM_STREAMS plain ones and the EXEC_QUEUE_STREAMS
+// CU-masked ones), once per GPU, at the first engine or opener creation: a stream created while
+// groups run maps a new hardware queue, and the GPU stalled for 7-13 ms each time the heavy-load
+// launcher met an empty pool inside the 128-thread jobs line's timed region (r06b: 29.8 against
+// 36.8 M reports/s, the two runs' kernel traces differing only in two new queues).
+constexpr int WARM_STREAMS = 6;
+void ws_warm(int device);
 
 // ---- coalescing executor -------------------------------------------------------------------
 // One executor per (GPU, lane): lane 0 is the GPU's executor; a multi-GPU engine created over a
@@ -279,8 +286,8 @@ struct LeaderLayout {
 };
 void engine_leader_layout(const prio3_engine* e, uint32_t cap, LeaderLayout* L);
 // one DMA of the staged inputs into the run, the leader kernels, the outputs back into the staging
-int engine_leader_issue(prio3_engine* lead, const LeaderLayout& L, uint8_t* stg_dev, uint32_t n,
-                        uint32_t n_keys, int jobs, GroupRun* gr, bool own_queue);
+int engine_leader_issue(prio3_engine* lead, const LeaderLayout& L, uint8_t* stg, uint8_t* stg_dev,
+                        uint32_t n, uint32_t n_keys, int jobs, GroupRun* gr, bool own_queue);
 int exec_leader(LeaderJob* job);
 
 // ---- coalesced leader prepare_next (prio3_leader_prepare_next_batch of concurrent jobs) -------
@@ -293,7 +300,17 @@ struct LNextJob {
   uint32_t c0 = 0, n = 0;          // the batch's columns in its run
   const uint8_t* msgs = nullptr;   // host [n][16] (nullable: no joint randomness)
   uint8_t* status = nullptr;       // host [n], in/out
+  // prepare_next + accumulate in the same launch (prio3_leader_prepare_next_aggregate_batch):
+  // the job's verdicts and output shares are summed into its n_segments aggregations right after
+  // the joint-rand check, with no second round trip (nseg == 0: prepare_next only)
+  const uint32_t* seg = nullptr;   // host [n] (nullable: segment 0)
+  const uint8_t* accept = nullptr;  // host [n] (nullable: all)
+  uint32_t nseg = 0;
+  uint8_t* agg_out = nullptr;      // host [nseg][agg_len]
+  uint64_t* counts_out = nullptr;  // host [nseg]
   uint32_t slot = 0, rep_off = 0;  // placement in the group
+  uint32_t acc_slot = 0;           // its accumulate descriptor (aggregating jobs)
+  size_t out_off = 0;              // its aggregate shares + counts in the accumulate area
 };
 // one per job of a prepare_next group (read by the kernel from the mapped staging)
 struct LNextDesc {
@@ -305,15 +322,25 @@ struct LNextDesc {
   uint32_t n, rep_off, kind, bits, out_len, jr;
 };
 constexpr uint32_t LNEXT_MAX_JOBS = 1024, LNEXT_MAX_REPS = 1u << 17;
+constexpr size_t LNEXT_MAX_OUT = (size_t)32 << 20;  // aggregate shares + counts per group
+// the staging of a prepare_next group: descriptors, messages, statuses, then (aggregating jobs)
+// an accumulate area laid out as an accumulate group's (acc_layout) from acc_base
 struct LNextLayout {
-  size_t desc_off, msg_off, status_off, bytes;
+  size_t desc_off, msg_off, status_off, acc_base, bytes;
+  AccLayout acc;
 };
 void lnext_layout(LNextLayout* L);
 uint32_t engine_lnext_key(const LNextJob* j);
 void engine_lnext_stage(LNextJob* j, uint8_t* stg, const LNextLayout& L);
 // launches the group's kernel on a pooled stream of `device` (reads and writes the staging)
-int engine_lnext_issue(int device, uint32_t es, uint8_t* stg_dev, const LNextLayout& L,
-                       uint32_t n_jobs, uint32_t max_n, hipStream_t* st_out, bool own_queue);
+// n_acc aggregating jobs (descriptors 0 .. n_acc - 1 of the accumulate area; out_bytes its used
+// output bytes) are accumulated after the check, in an area the call takes from the scratch pool
+// (*slab_out, released after the stream by the finish)
+int engine_lnext_issue(int device, uint32_t es, uint8_t* stg, uint8_t* stg_dev,
+                       const LNextLayout& L, uint32_t n_jobs, uint32_t max_n, uint32_t n_acc,
+                       size_t out_bytes, hipStream_t* st_out, Slab** slab_out, bool own_queue);
+size_t engine_lnext_out_bytes(const LNextJob* j);
+void engine_lnext_unstage(LNextJob* j, const uint8_t* stg, const LNextLayout& L);
 int exec_leader_next(LNextJob* job);
 
 // ---- coalesced HPKE open of helper input shares (janus_hpke_open_input_shares) -----------

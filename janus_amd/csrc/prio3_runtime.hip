@@ -366,6 +366,18 @@ void ws_exec_stream_put(int device, hipStream_t s) {
   ws_stream_put(device, s);
 }
 
+void ws_warm(int device) {
+  if (device < 0 || device >= MAX_DEVICES) return;
+  static std::once_flag once[MAX_DEVICES];
+  std::call_once(once[device], [device] {
+    hipStream_t s[WARM_STREAMS > EXEC_QUEUE_STREAMS ? WARM_STREAMS : EXEC_QUEUE_STREAMS] = {};
+    for (int i = 0; i < WARM_STREAMS; i++) s[i] = ws_stream_get(device);
+    for (int i = 0; i < WARM_STREAMS; i++) ws_stream_put(device, s[i]);
+    for (int i = 0; i < EXEC_QUEUE_STREAMS; i++) s[i] = ws_exec_stream_get(device);
+    for (int i = 0; i < EXEC_QUEUE_STREAMS; i++) ws_exec_stream_put(device, s[i]);
+  });
+}
+
 // ---- executors -----------------------------------------------------------------------------
 // A generic group-commit executor, one per (GPU, lane, work kind).  Callers reserve room in the
 // open group of their key and stage their inputs themselves (in parallel); the executor's one
@@ -438,6 +450,13 @@ constexpr int64_t HOLD_MAX_MS = 30000;
 // reports inside submit at which the launcher leaves its light-load pipeline (the box's 16 rayon
 // threads keep ~8 Ki in flight, 128 threads ~64 Ki)
 constexpr uint64_t HEAVY_DEFAULT = 32768;
+// the heavy-load launcher's streams: 0 the plain pool (r05i), 1 the light pipeline's CU-masked
+// streams, whose hardware queues are already active when the load crosses HEAVY_DEFAULT (the
+// first heavy groups on idle plain queues stalled 7-20 ms, r06b / r06c kernel traces)
+#ifndef JANUS_HEAVY_OWN_QUEUE
+#define JANUS_HEAVY_OWN_QUEUE 0
+#endif
+constexpr bool HEAVY_OWN_QUEUE = JANUS_HEAVY_OWN_QUEUE != 0;
 
 // JANUS_EXEC_TRACE=<path>: one line per launched group (microseconds: created, taken by the
 // launcher, writers done, launch returned; jobs; reports), for tuning the executor
@@ -569,7 +588,7 @@ struct Exec {
         while (!takeable()) wait_work(lk);
         Group* g = take_locked(lk);
         t0 = std::chrono::steady_clock::now();
-        if (!issue_unlocked(lk, g, &hc, false)) continue;
+        if (!issue_unlocked(lk, g, &hc, HEAVY_OWN_QUEUE)) continue;
         cur = g;
       }
       lk.unlock();
@@ -603,7 +622,7 @@ struct Exec {
           if (takeable() && order.front()->writers == 0 && !lighter()) {
             nxt = take_locked(lk);
             tn = std::chrono::steady_clock::now();
-            if (!issue_unlocked(lk, nxt, &hn, false)) nxt = nullptr;
+            if (!issue_unlocked(lk, nxt, &hn, HEAVY_OWN_QUEUE)) nxt = nullptr;
           }
           lk.unlock();
         }
@@ -1072,8 +1091,8 @@ struct LeaderPolicy {
   };
   static int issue(int, State& s, Staging& g, Handle* h, bool own_queue) {
     h->s = &s;
-    return engine_leader_issue(s.lead, s.L, g.dev, s.n, (uint32_t)s.keys.size(), (int)s.jobs,
-                               &h->gr, own_queue);
+    return engine_leader_issue(s.lead, s.L, g.p, g.dev, s.n, (uint32_t)s.keys.size(),
+                               (int)s.jobs, &h->gr, own_queue);
   }
   static bool prepared(const Handle& h) { return engine_group_prepared(h.gr); }
   static bool done(const Handle& h) { return engine_group_done(h.gr); }
@@ -1093,43 +1112,54 @@ struct LNextPolicy {
   struct State {
     LNextLayout L;
     uint32_t jobs = 0, reps = 0, max_n = 0, es = 16;
+    uint32_t acc_jobs = 0;  // aggregating jobs (next + accumulate)
+    size_t out = 0;
   };
   struct Handle {
     int device = 0;
     hipStream_t st = nullptr;
+    Slab* slab = nullptr;  // the accumulate area on the device (aggregating jobs)
   };
   static uint64_t key(Job* j) { return engine_lnext_key(j); }
   static uint32_t reports(const State& s) { return s.reps; }
   static bool create(State& s, Job* j, size_t* bytes) {
-    if (j->n > LNEXT_MAX_REPS) return false;
+    if (j->n > LNEXT_MAX_REPS || engine_lnext_out_bytes(j) > LNEXT_MAX_OUT) return false;
     s.es = engine_lnext_key(j);
     lnext_layout(&s.L);
     *bytes = s.L.bytes;
     return true;
   }
   static bool reserve(State& s, Job* j) {
-    if (s.jobs + 1 > LNEXT_MAX_JOBS || s.reps + j->n > LNEXT_MAX_REPS) return false;
+    const size_t ob = engine_lnext_out_bytes(j);
+    if (s.jobs + 1 > LNEXT_MAX_JOBS || s.reps + j->n > LNEXT_MAX_REPS ||
+        s.out + ob > LNEXT_MAX_OUT)
+      return false;
     j->slot = s.jobs++;
     j->rep_off = s.reps;
     s.reps += j->n;
     s.max_n = std::max(s.max_n, j->n);
+    if (j->nseg) {
+      j->acc_slot = s.acc_jobs++;
+      j->out_off = s.out;
+      s.out += ob;
+    }
     return true;
   }
   static void stage(State& s, Staging& g, Job* j) { engine_lnext_stage(j, g.p, s.L); }
   static int issue(int device, State& s, Staging& g, Handle* h, bool own_queue) {
     h->device = device;
-    return engine_lnext_issue(device, s.es, g.dev, s.L, s.jobs, s.max_n, &h->st, own_queue);
+    return engine_lnext_issue(device, s.es, g.p, g.dev, s.L, s.jobs, s.max_n, s.acc_jobs, s.out,
+                              &h->st, &h->slab, own_queue);
   }
   static bool prepared(const Handle& h) { return done(h); }
   static bool done(const Handle& h) { return hipStreamQuery(h.st) != hipErrorNotReady; }
   static int finish(Handle* h) {
     const hipError_t q = hipStreamSynchronize(h->st);
+    if (h->slab) ws_release(h->slab, h->st);
     ws_exec_stream_put(h->device, h->st);
     return q == hipSuccess ? PRIO3_OK : PRIO3_EDEVICE;
   }
-  static void unstage(State& s, Staging& g, Job* j) {
-    memcpy(j->status, g.p + s.L.status_off + j->rep_off, j->n);
-  }
+  static void unstage(State& s, Staging& g, Job* j) { engine_lnext_unstage(j, g.p, s.L); }
 };
 
 // ---- HPKE open groups ----
@@ -1285,7 +1315,9 @@ void lnext_layout(LNextLayout* L) {
   L->desc_off = 0;
   L->msg_off = up(sizeof(LNextDesc) * (size_t)LNEXT_MAX_JOBS);
   L->status_off = L->msg_off + up(16 * (size_t)LNEXT_MAX_REPS);
-  L->bytes = L->status_off + up((size_t)LNEXT_MAX_REPS);
+  L->acc_base = L->status_off + up((size_t)LNEXT_MAX_REPS);
+  acc_layout(LNEXT_MAX_JOBS, LNEXT_MAX_REPS, LNEXT_MAX_OUT, &L->acc);
+  L->bytes = L->acc_base + L->acc.bytes;
 }
 
 int exec_stats(int kind, int id, ExecStats* out) {

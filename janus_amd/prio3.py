@@ -104,6 +104,7 @@ EXPORTED_SYMBOLS = (
     "prio3_device_combine_metadata", "prio3_engine_create_ex", "prio3_engine_create_mask",
     "prio3_engine_create_devices", "prio3_engine_members", "prio3_executor_control",
     "prio3_executor_stats_get", "prio3_helper_aggregate_init_batch",
+    "prio3_leader_prepare_next_aggregate_batch",
 )
 # include/janus_hpke.h (the batched HPKE opener, janus_amd/hpke.py)
 HPKE_EXPORTED_SYMBOLS = (
@@ -178,6 +179,8 @@ def load_library() -> C.CDLL:
     L.prio3_device_aggregate_finish.argtypes = [vp, vp, vp, vp, vp, vp]
     L.prio3_leader_prepare_init_batch.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, vp, P(vp)]
     L.prio3_leader_prepare_next_batch.argtypes = [vp, vp, vp]
+    L.prio3_leader_prepare_next_aggregate_batch.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp,
+                                                            vp]
     L.prio3_device_leader_prepare_init.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, vp, vp]
     L.prio3_device_leader_prepare_next.argtypes = [vp, C.c_uint32, vp, vp, vp]
     L.prio3_device_batch_metadata.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, vp, C.c_uint32, vp,
@@ -326,6 +329,27 @@ class PreparedBatch:
         if rc:
             raise RuntimeError(f"prio3_leader_prepare_next_batch failed (rc={rc})")
         return st
+
+    def leader_prepare_next_aggregate(self, prep_msgs, status, segment_ids=None,
+                                      accept_mask=None, n_segments: int = 1):
+        """``leader_prepare_next`` + ``accumulate`` in one launch of the prepare_next executor
+        (prio3_leader_prepare_next_aggregate_batch).  Returns (status, agg [S, agg_len],
+        counts [S])."""
+        st = np.array(status, np.uint8, copy=True)
+        msgs = None
+        if self.engine.sz.prep_msg_len:
+            msgs = np.ascontiguousarray(prep_msgs, np.uint8)
+            if msgs.shape != (self.n, self.engine.sz.prep_msg_len):
+                raise ValueError("prepare message shape does not match the VDAF instance")
+        seg, acc = _seg_accept(self.n, segment_ids, accept_mask, n_segments)
+        agg = np.zeros((n_segments, self.engine.sz.agg_share_len), np.uint8)
+        cnt = np.zeros(n_segments, np.uint64)
+        rc = load_library().prio3_leader_prepare_next_aggregate_batch(
+            self.handle, _np_ptr(msgs), _np_ptr(st), _np_ptr(seg), _np_ptr(acc), n_segments,
+            _np_ptr(agg), _np_ptr(cnt))
+        if rc:
+            raise RuntimeError(f"prio3_leader_prepare_next_aggregate_batch failed (rc={rc})")
+        return st, agg, cnt
 
     def output_shares(self) -> np.ndarray:
         out = np.zeros((self.n, self.engine.sz.agg_share_len), np.uint8)

@@ -501,3 +501,52 @@ def test_leader_next_uncoalesced_on_shared_runs(name):
                                           n_segments=3)
         np.testing.assert_array_equal(agg, ragg)
         np.testing.assert_array_equal(cnt, rcnt)
+
+
+@pytest.mark.parametrize("name", ["hist_256_c16", "sumvec_8x10_c9", "sum32", "count"])
+def test_concurrent_leader_next_aggregate_jobs(name):
+    """prio3_leader_prepare_next_aggregate_batch: 16 jobs of 4 tasks queued behind the prepare_next
+    executor's hold share ONE launch that checks every job's prepare messages (a tampered message
+    per third job) and sums its kept output shares per segment under a mask; statuses,
+    aggregates and counts equal the restatement's leader path, and the batches can still be
+    accumulated again afterwards (the same aggregates)."""
+    from janus_amd import prio3 as J
+    from oracle.oracle import Oracle
+    cfg = CONFIGS[name]
+    o = Oracle(**cfg)
+    vks = [bytes([k]) * 16 for k in (0x91, 0x92, 0x93, 0x94)]
+    engines = [_engine(cfg, vk) for vk in vks]
+    rng = np.random.default_rng(59)
+    jobs = []
+    for j in range(16):
+        t = j % 4
+        n = int(rng.integers(80, 400))
+        d = o.gen_reports(vks[t], n, seed=1300 + j, n_threads=4)
+        lin = engines[t].generate_reports_device(n, seed=1300 + j, with_leader_inputs=True)
+        lin = lin["leader_input_shares"].cpu().numpy()
+        msgs = _ref(o, vks[t], d)[0].copy()
+        if j % 3 == 0 and msgs.shape[1]:
+            msgs[int(rng.integers(0, n)), 0] ^= 1
+        seg = rng.integers(0, 3, n).astype(np.uint32)
+        acc = (rng.random(n) < 0.9).astype(np.uint8)
+        jobs.append((t, d, lin, msgs, seg, acc))
+    inits = [engines[t].leader_prepare_init_batch(d["nonces"], d["public_shares"], lin)
+             for (t, d, lin, _, _, _) in jobs]
+    g0 = engines[0].executor_stats(J.EXEC_LEADER_NEXT)["groups"]
+    with ThreadPoolExecutor(16) as ex, _Held(engines[0], 16, J.EXEC_LEADER_NEXT) as held:
+        futs = [ex.submit(b.leader_prepare_next_aggregate, msgs, st, seg, acc, 3)
+                for (_, _, _, msgs, seg, acc), (_, st, b) in zip(jobs, inits)]
+        held.wait()
+        got = [f.result(timeout=120) for f in futs]
+    assert engines[0].executor_stats(J.EXEC_LEADER_NEXT)["groups"] - g0 == 1
+    for (t, d, lin, msgs, seg, acc), (ps, st, b), (st2, agg, cnt) in zip(jobs, inits, got):
+        _, rst, ragg, rcnt = o.leader_batch(vks[t], d["nonces"], d["public_shares"], lin, msgs,
+                                            n_threads=4, segment_ids=np.where(acc, seg, 3),
+                                            n_segments=3)
+        np.testing.assert_array_equal(st2, rst)
+        np.testing.assert_array_equal(agg, ragg)
+        np.testing.assert_array_equal(cnt, rcnt)
+        agg2, cnt2 = b.accumulate(seg, acc, 3)
+        np.testing.assert_array_equal(agg2, ragg)
+        np.testing.assert_array_equal(cnt2, rcnt)
+        b.free()

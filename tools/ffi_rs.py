@@ -2,6 +2,7 @@
 
   python tools/ffi_rs.py            prints the `janus_prio3_sys` declarations
   python tools/ffi_rs.py --check    exits 1 if INTEGRATION.md's block drifted from the headers
+  python tools/ffi_rs.py --write    rewrites that block from the headers (after a header change)
 
 parse_header() reads the C prototypes, typedef'd structs and enum constants of a header;
 rust_type() maps a C parameter type to the Rust FFI type the crate must declare (pointers keep
@@ -203,7 +204,17 @@ def diff(c: dict, r: dict) -> list:
     return out
 
 
+def write_integration(path=INTEGRATION) -> None:
+    """Replaces INTEGRATION.md's src/lib.rs block with gen_rust()."""
+    src = open(path).read()
+    m = re.search(r"(`src/lib\.rs`[^\n]*\n+```rust\n)(.*?)(```)", src, re.S)
+    open(path, "w").write(src[:m.start(2)] + gen_rust() + src[m.end(2):])
+
+
 if __name__ == "__main__":
+    if "--write" in sys.argv:
+        write_integration()
+        sys.argv.append("--check")
     if "--check" in sys.argv:
         d = diff(parse_headers(), parse_rust(integration_block()))
         print("\n".join(d) if d else "INTEGRATION.md src/lib.rs matches include/*.h")
