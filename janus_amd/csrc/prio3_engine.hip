@@ -3793,6 +3793,19 @@ static int fused_finish(prio3_engine* e, Run* R, const uint8_t* d_status, const 
                         const uint32_t* fix_seg, const uint8_t* d_accept_mask, uint32_t S,
                         uint8_t* d_agg_shares, uint64_t* d_counts, hipStream_t st);
 
+#ifndef SEALED_EARLY_NEXT  // A/B builds: 0 = a sealed group's next group waits for its prepare
+#define SEALED_EARLY_NEXT 1
+#endif
+// the group's "prepared" event (engine_group_prepared), recorded on its stream now
+static void record_prep(GroupRun* gr, hipStream_t st) {
+  if (hipEventCreateWithFlags(&gr->prep, hipEventDisableTiming) != hipSuccess ||
+      hipEventRecord(gr->prep, st) != hipSuccess) {
+    (void)hipGetLastError();
+    if (gr->prep) (void)hipEventDestroy(gr->prep);
+    gr->prep = nullptr;
+  }
+}
+
 // Sealed-input groups: a report the open rejected (HPKE status 4 or 8) gets status 0x80 | that
 // PrepareError, whatever its prepare computed on the zeroed share -- so the accumulate, which
 // counts status 0 only, leaves it out, and the caller sees the error Janus records first.
@@ -3872,6 +3885,10 @@ int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr, boo
     a.status = R->hstatus;
     if (hpke_open_group_launch(g.opener, a, st) != PRIO3_OK) return fail(PRIO3_EDEVICE);
     in.helper = R->helper;
+    // the executor may issue the next group as soon as this one's open is done: a group's open
+    // (one X25519 ladder per lane, ~1 wave per SIMD on half the SIMDs at 31k reports) then runs
+    // beside this group's prepare instead of after it
+    if (SEALED_EARLY_NEXT) record_prep(gr, st);
   }
   if (!mp) {  // the slots and the key table are read from the staging by the XOF
     in.vk_slot = (const uint16_t*)(hd + L.slot_off);
@@ -3900,12 +3917,7 @@ int engine_group_issue(prio3_engine* lead, const GroupView& g, GroupRun* gr, boo
     if (hipGetLastError() != hipSuccess) return fail(PRIO3_EDEVICE);
   }
   // the executor may issue its next group once this group's prepare kernels are done
-  if (hipEventCreateWithFlags(&gr->prep, hipEventDisableTiming) != hipSuccess ||
-      hipEventRecord(gr->prep, st) != hipSuccess) {
-    (void)hipGetLastError();
-    if (gr->prep) (void)hipEventDestroy(gr->prep);
-    gr->prep = nullptr;
-  }
+  if (!gr->prep) record_prep(gr, st);
   if (agg) {
     rc = fuse ? fused_finish(lead, R, R->status, R->gseg, R->gseg, R->gaccept, g.nseg, R->gagg,
                              (uint64_t*)R->gcnt, st)

@@ -452,9 +452,10 @@ constexpr int64_t HOLD_MAX_MS = 30000;
 constexpr uint64_t HEAVY_DEFAULT = 32768;
 // the heavy-load launcher's streams: 0 the plain pool (r05i), 1 the light pipeline's CU-masked
 // streams, whose hardware queues are already active when the load crosses HEAVY_DEFAULT (the
-// first heavy groups on idle plain queues stalled 7-20 ms, r06b / r06c kernel traces)
+// first heavy groups on idle plain queues stalled 7-20 ms, r06b / r06c kernel traces; interleaved
+// r06d: 35.5 / 35.7 / 36.2 against 34.5 / 35.7 / 33.6 M reports/s at 128 threads)
 #ifndef JANUS_HEAVY_OWN_QUEUE
-#define JANUS_HEAVY_OWN_QUEUE 0
+#define JANUS_HEAVY_OWN_QUEUE 1
 #endif
 constexpr bool HEAVY_OWN_QUEUE = JANUS_HEAVY_OWN_QUEUE != 0;
 
@@ -532,9 +533,9 @@ struct Exec {
   }
   // issues g with mu released; on failure its callers are woken with the error (returns false)
   // own_queue: the group's kernels on a hardware queue of their own (ws_exec_stream_get) -- the
-  // light-load pipeline, whose groups are meant to run concurrently; the heavy-load launcher
-  // runs one group at a time on the plain stream pool (r05i: 38.5-39.8 M/s at 128 threads
-  // against 30.2-36.0 with dedicated queues, interleaved)
+  // light-load pipeline, whose groups are meant to run concurrently, and since r06 the heavy-load
+  // launcher too (HEAVY_OWN_QUEUE; r05 had put it on the plain stream pool, r05i: 38.5-39.8 M/s
+  // at 128 threads against 30.2-36.0 with dedicated queues, interleaved)
   bool issue_unlocked(std::unique_lock<std::mutex>& lk, Group* g, typename P::Handle* h,
                       bool own_queue) {
     lk.unlock();
