@@ -521,7 +521,9 @@ def secondary_lines(args) -> dict:
                                                                    cpu_seconds=cs)),
                     # the whole loop body from sealed input shares in one call,
                     # with the two-call composition measured beside it in the same run
-                    ("secondary_jobs_init", lambda: init_jobs_line(128, 500, 2048, 4,
+                    # (at jobs_main's 2 Mi reports like secondary_jobs: with 1 Mi the ~80 ms timed
+                    # region is mostly the ramp from the light-load pipeline, r06f: 12.4 M/s)
+                    ("secondary_jobs_init", lambda: init_jobs_line(128, 500, (1 << 21) // 500, 4,
                                                                    cpu_seconds=cs)),
                     ("secondary_jobs_init_16t", lambda: init_jobs_line(16, 500, 1024, 4,
                                                                        cpu_seconds=cs))):
