@@ -120,10 +120,12 @@ int janus_hpke_open(janus_hpke_opener* opener, uint32_t n, const uint8_t* enc, c
                     const uint32_t* aad_len, uint32_t aad_stride, uint8_t* pt, uint8_t* status);
 
 /* The GPU's HPKE executor (shared by every opener on the GPU): counters, and control -- "hold"
- * 1/0 (tests queue jobs behind it), "heavy" N (as prio3_executor_control; 0 = this executor's
- * default, which never leaves the light-load pipeline: concurrent groups win for the latency-bound
- * open), "coalesce" 0/1 (this opener's host-buffer opens launch alone / through the executor, the
- * default). */
+ * 1/0 (tests queue jobs behind it; expires by itself after 30 s, or after N ms for hold = N > 1),
+ * "heavy" N (as prio3_executor_control; 0 = this executor's default, which never leaves the
+ * light-load pipeline: concurrent groups win for the latency-bound open), and two options of this
+ * opener: "coalesce" 0/1 (its host-buffer opens launch alone / through the executor, the
+ * default), "pair_max" N (X25519 opens of at most N reports run the ladder on lane pairs, default
+ * 65536; 0 = never). */
 typedef struct {
   uint64_t jobs, reports, groups, active_jobs, active_reports;
 } janus_hpke_executor_stats;

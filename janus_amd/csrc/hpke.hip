@@ -451,6 +451,65 @@ DEV fe x25519_ladder(const uint32_t* k, const fe& u) {
   return fe_freeze(fe_mul(x2, fe_inv(z2)));
 }
 
+// The same ladder on a lane pair (both lanes hold the whole state; `odd` = the pair's second lane):
+// per step each lane runs one square and one product of the first stage (lane 0: AA = A^2,
+// DA = D A; lane 1: BB = B^2, CB = C B), they swap them by DPP, then three products of the
+// second stage (lane 0: x2 = AA BB, z2 = E (AA + a24 E); lane 1: x3 = (DA + CB)^2,
+// t = (DA - CB)^2, z3 = x1 t) and swap again -- 1S + 4M per lane instead of 4S + 5M, so a small
+// group's open (one wave per SIMD, each lane's ladder a long dependent chain) runs on twice the
+// waves with a shorter chain per lane.  Both lanes end with the same result.
+DEV uint32_t pair_swap(uint32_t x) {  // the value of the other lane of the pair (quad_perm 1,0,3,2)
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+}
+DEV fe fe_pair_swap(const fe& a) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = pair_swap(a.v[i]);
+  return r;
+}
+DEV fe fe_sel(bool c, const fe& a, const fe& b) {  // c ? a : b
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = c ? a.v[i] : b.v[i];
+  return r;
+}
+DEV fe x25519_ladder_pair(const uint32_t* k, const fe& u, const bool odd) {
+  const fe x1 = u;
+  fe x2 = fe_set(1), z2 = fe_set(0), x3 = u, z3 = fe_set(1);
+  bool swap = false;
+#pragma unroll 1
+  for (int t = 254; t >= 0; t--) {
+    const bool kt = (k[t >> 5] >> (t & 31)) & 1u;
+    swap ^= kt;
+    fe_cswap(swap, x2, x3);
+    fe_cswap(swap, z2, z3);
+    swap = kt;
+    // stage 1: lane 0 (A, D), lane 1 (B, C); every choice is a select -- no branch, so the two
+    // lanes run one instruction stream
+    const fe A = fe_add(x2, z2), B = fe_sub(x2, z2), C = fe_add(x3, z3), D = fe_sub(x3, z3);
+    const fe X = fe_sel(odd, B, A), Y = fe_sel(odd, C, D);
+    const fe s1 = fe_sqr(X), m1 = fe_mul(Y, X);
+    const fe s1o = fe_pair_swap(s1), m1o = fe_pair_swap(m1);
+    const fe AA = fe_sel(odd, s1o, s1), BB = fe_sel(odd, s1, s1o);
+    const fe DA = fe_sel(odd, m1o, m1), CB = fe_sel(odd, m1, m1o);
+    // stage 2
+    const fe E = fe_sub(AA, BB);
+    const fe sp = fe_add(DA, CB), sm = fe_sub(DA, CB);
+    const fe G = fe_add(AA, fe_mul121665(E));
+    const fe r1 = fe_mul(fe_sel(odd, sp, AA), fe_sel(odd, sp, BB));  // x3 | x2
+    const fe r2 = fe_mul(fe_sel(odd, sm, E), fe_sel(odd, sm, G));    // t  | z2
+    const fe r3 = fe_mul(x1, r2);                                    // z3 | -
+    const fe r1o = fe_pair_swap(r1), r2o = fe_pair_swap(r2), r3o = fe_pair_swap(r3);
+    x2 = fe_sel(odd, r1o, r1);
+    z2 = fe_sel(odd, r2o, r2);
+    x3 = fe_sel(odd, r1, r1o);
+    z3 = fe_sel(odd, r3, r3o);
+  }
+  fe_cswap(swap, x2, x3);
+  fe_cswap(swap, z2, z3);
+  return fe_freeze(fe_mul(x2, fe_inv(z2)));
+}
+
 // GHASH step (SP 800-38D Algorithm 1): y = (y ^ x) * H in GF(2^128), big-endian words
 DEV void ghash_block(uint32_t y[4], const uint32_t x[4], const uint32_t H[4]) {
   uint32_t X[4] = {y[0] ^ x[0], y[1] ^ x[1], y[2] ^ x[2], y[3] ^ x[3]};
@@ -830,14 +889,17 @@ __device__ __noinline__ bool p384_dh(const int8_t* dig, const uint8_t* enc, uint
 #ifndef HPKE_WAVES  // A/B builds: e.g. -DHPKE_WAVES='__attribute__((amdgpu_waves_per_eu(3, 3)))'
 #define HPKE_WAVES
 #endif
-template <int MODE, int PUB, int KEM>
+template <int MODE, int PUB, int KEM, bool PAIR = false>
 __global__ __launch_bounds__(256) HPKE_WAVES void k_hpke_open(HpkeParams P, OpenArgs a) {
   static_assert(KEM == 0x20 || KEM == 0x10 || KEM == 0x21 || KEM == 0x12 || KEM == 0x11, "KEM id");
+  static_assert(!PAIR || KEM == 0x20, "the lane-pair ladder is X25519's");
   const uint32_t AEAD = P.aead;
   __shared__ AesT T;
   aes_tables_init(T);
   __syncthreads();
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  // PAIR: two lanes per report; they differ only inside the ladder and write the same bytes
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t r = PAIR ? gid >> 1 : gid;
   if (r >= a.n) return;
   // ---- DHKEM Decap (RFC 9180 4.1): dh, then ExtractAndExpand(dh, enc || pkRm) -------------
   constexpr int NSS = KemC<KEM>::NSS_W;
@@ -858,7 +920,7 @@ __global__ __launch_bounds__(256) HPKE_WAVES void k_hpke_open(HpkeParams P, Open
 #pragma unroll
     for (int i = 0; i < 8; i++) u.v[i] = encw[i];
     u.v[7] &= 0x7fffffffu;  // decodeUCoordinate masks bit 255
-    const fe dh = x25519_ladder(P.sk, u);
+    const fe dh = PAIR ? x25519_ladder_pair(P.sk, u, (threadIdx.x & 1u) != 0) : x25519_ladder(P.sk, u);
     uint32_t nz = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) nz |= dh.v[i];
@@ -1413,9 +1475,15 @@ static void recode_w4(const uint32_t* sk, const uint32_t* n, int nw, int ndig, i
   dig[ndig - 1] = (int8_t)k[0];
 }
 
+#ifndef JANUS_HPKE_PAIR_MAX  // A/B builds: 0 = never the lane-pair ladder
+#define JANUS_HPKE_PAIR_MAX 65536
+#endif
 struct janus_hpke_opener {
   int device = 0;
   int coalesce = 1;  // host-buffer opens through the executor (janus_hpke_executor_control)
+  // X25519 opens of at most this many reports run on lane pairs (x25519_ladder_pair): up to 2
+  // waves per SIMD at the kernel's 248 VGPRs, i.e. 2 x 1024 SIMDs x 64 lanes / 2 lanes per report
+  int pair_max = JANUS_HPKE_PAIR_MAX;
   hipStream_t stream = nullptr;
   HpkeParams P;
   uint8_t* d_pt = nullptr;
@@ -1614,7 +1682,17 @@ static int launch_open(janus_hpke_opener* o, int mode, int pub, const OpenArgs& 
     k_hpke_open<1, 32, KE><<<blocks, 256, 0, st>>>(o->P, a);     \
   else                                                           \
     k_hpke_open<1, 0, KE><<<blocks, 256, 0, st>>>(o->P, a);
-  if (o->P.kem == JANUS_HPKE_KEM_P256_HKDF_SHA256) {
+  // small X25519 batches (the executors' groups) on lane pairs: below ~2 waves per SIMD the
+  // one-lane open leaves SIMDs idle and each lane's ladder is a long dependent chain
+  const bool pair = o->P.kem == JANUS_HPKE_KEM_X25519_HKDF_SHA256 && mode == 1 &&
+                    a.n <= (uint32_t)o->pair_max;
+  if (pair) {
+    const uint32_t b2 = (2 * a.n + 255) / 256;
+    if (pub == 32)
+      k_hpke_open<1, 32, 0x20, true><<<b2, 256, 0, st>>>(o->P, a);
+    else
+      k_hpke_open<1, 0, 0x20, true><<<b2, 256, 0, st>>>(o->P, a);
+  } else if (o->P.kem == JANUS_HPKE_KEM_P256_HKDF_SHA256) {
     JANUS_HPKE_LAUNCH(0x10)
   } else if (o->P.kem == JANUS_HPKE_KEM_X448_HKDF_SHA512) {
     JANUS_HPKE_LAUNCH(0x21)
@@ -1651,6 +1729,7 @@ uint64_t hpke_opener_key(const janus_hpke_opener* o) {
   auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
   mix((uint64_t)(uintptr_t)o);
   mix((uint64_t)o->timing);
+  mix((uint64_t)o->pair_max);
   return h;
 }
 
@@ -1680,6 +1759,7 @@ uint64_t hpke_group_key(const HpkeJob* j) {
   uint64_t h = 1469598103934665603ull;
   auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
   mix((uint64_t)(uintptr_t)j->o);
+  mix((uint64_t)j->o->pair_max);
   mix(j->ct_stride);
   mix(j->pub_len);
   mix(j->share_len);
@@ -2072,6 +2152,12 @@ int janus_hpke_executor_control(janus_hpke_opener* o, const char* key, int64_t v
   if (!o || !key) return JANUS_HPKE_EINVAL;
   if (!strcmp(key, "coalesce")) {
     o->coalesce = value != 0;
+    return JANUS_HPKE_SUCCESS;
+  }
+  if (!strcmp(key, "pair_max")) {  // X25519 opens of at most this many reports on lane pairs
+    if (value < 0) return JANUS_HPKE_EINVAL;
+    std::lock_guard<std::mutex> lk(o->mu);
+    o->pair_max = (int)std::min<int64_t>(value, INT32_MAX);
     return JANUS_HPKE_SUCCESS;
   }
   return exec_control(EXEC_HPKE, o->device * EXEC_LANES, key, value);

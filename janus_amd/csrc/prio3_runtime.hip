@@ -399,6 +399,12 @@ void staging_free(Staging& s) {
 }
 
 constexpr size_t STAGING_TARGET = (size_t)96 << 20;  // pinned bytes per group (grows to fit)
+// a leader group stages 5.7 KB per Histogram(256) report: 96 MB caps it at ~16k reports, half the
+// helper's groups at the same load (A/B builds: JANUS_LEADER_STAGING_MB)
+#ifndef JANUS_LEADER_STAGING_MB
+#define JANUS_LEADER_STAGING_MB 96
+#endif
+constexpr size_t LEADER_STAGING_TARGET = (size_t)JANUS_LEADER_STAGING_MB << 20;
 
 struct StagingPool {
   std::mutex mu;
@@ -1054,7 +1060,7 @@ struct LeaderPolicy {
     engine_leader_layout(j->e, 1, &l1);
     engine_leader_layout(j->e, 2, &l2);
     const size_t per = l2.bytes - l1.bytes + 1;
-    const uint32_t cap_b = (uint32_t)std::max<size_t>(1, STAGING_TARGET / per);
+    const uint32_t cap_b = (uint32_t)std::max<size_t>(1, LEADER_STAGING_TARGET / per);
     s.cap = std::max(j->n, std::min(MAX_GROUP_REPORTS, cap_b));
     engine_leader_layout(j->e, s.cap, &s.L);
     *bytes = s.L.bytes;

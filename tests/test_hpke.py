@@ -113,10 +113,13 @@ def test_gpu_aad_length_past_stride_fails_that_report_only(aead):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pair_max", [65536, 0], ids=["lane_pair", "one_lane"])
 @pytest.mark.parametrize("n,pub,share_len,ext,tamper", [
     (1, 32, 48, (), False), (300, 32, 48, (), True), (257, 0, 32, (), True),
     (200, 32, 48, ((0xFF00, b""),), False)])
-def test_gpu_input_shares_match_oracle(n, pub, share_len, ext, tamper):
+def test_gpu_input_shares_match_oracle(n, pub, share_len, ext, tamper, pair_max):
+    """pair_max: the X25519 ladder on lane pairs (x25519_ladder_pair, the default for batches of
+    at most 65536 reports) or on one lane per report."""
     from janus_amd import hpke as G
     rng = np.random.default_rng(n + pub)
     d = H.make_batch(n, share_len, pub, seed=n * 7 + pub, extensions=ext)
@@ -130,6 +133,7 @@ def test_gpu_input_shares_match_oracle(n, pub, share_len, ext, tamper):
     if exp_status is not None:
         np.testing.assert_array_equal(ref_st, exp_status)
     op = G.HpkeOpener(d["skR"], d["pkR"])
+    op.executor_control("pair_max", pair_max)
     sh, st = op.open_input_shares(d["task_id"], d["enc"], d["ct"], d["ct_len"], d["report_ids"],
                                   d["times"], d["pubs"], share_len, require_taskprov=taskprov)
     np.testing.assert_array_equal(st, ref_st)
