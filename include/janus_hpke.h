@@ -125,7 +125,7 @@ int janus_hpke_open(janus_hpke_opener* opener, uint32_t n, const uint8_t* enc, c
  * light-load pipeline: concurrent groups win for the latency-bound open), and two options of this
  * opener: "coalesce" 0/1 (its host-buffer opens launch alone / through the executor, the
  * default), "pair_max" N (X25519 opens of at most N reports run the ladder on lane pairs, default
- * 65536; 0 = never). */
+ * 8192; 0 = never). */
 typedef struct {
   uint64_t jobs, reports, groups, active_jobs, active_reports;
 } janus_hpke_executor_stats;

@@ -1475,15 +1475,19 @@ static void recode_w4(const uint32_t* sk, const uint32_t* n, int nw, int ndig, i
   dig[ndig - 1] = (int8_t)k[0];
 }
 
-#ifndef JANUS_HPKE_PAIR_MAX  // A/B builds: 0 = never the lane-pair ladder
-#define JANUS_HPKE_PAIR_MAX 65536
+// X25519 opens of at most this many reports run the ladder on lane pairs (x25519_ladder_pair).
+// Interleaved (r06h, HPKE jobs lines, every job checked): at 16 threads (groups of ~3-7k
+// reports) 6.50 / 6.54 / 6.64 against 6.37 / 6.11 / 6.43 M/s one lane per report; at 128 threads
+// (~30k) the pair loses (19.2 / 21.3 / 19.0 against 21.0 / 24.7 / 24.3 M/s; the helper init line
+// 16.2-18.0 against 18.0-19.4) -- its second lane repeats the key schedule and the AEAD, and at two
+// waves per SIMD the one-lane ladder's chains already overlap.  A/B builds: 0 = never.
+#ifndef JANUS_HPKE_PAIR_MAX
+#define JANUS_HPKE_PAIR_MAX 8192
 #endif
 struct janus_hpke_opener {
   int device = 0;
   int coalesce = 1;  // host-buffer opens through the executor (janus_hpke_executor_control)
-  // X25519 opens of at most this many reports run on lane pairs (x25519_ladder_pair): up to 2
-  // waves per SIMD at the kernel's 248 VGPRs, i.e. 2 x 1024 SIMDs x 64 lanes / 2 lanes per report
-  int pair_max = JANUS_HPKE_PAIR_MAX;
+  int pair_max = JANUS_HPKE_PAIR_MAX;  // lane-pair ladder for opens of at most this many reports
   hipStream_t stream = nullptr;
   HpkeParams P;
   uint8_t* d_pt = nullptr;

@@ -119,7 +119,7 @@ def test_gpu_aad_length_past_stride_fails_that_report_only(aead):
     (200, 32, 48, ((0xFF00, b""),), False)])
 def test_gpu_input_shares_match_oracle(n, pub, share_len, ext, tamper, pair_max):
     """pair_max: the X25519 ladder on lane pairs (x25519_ladder_pair, the default for batches of
-    at most 65536 reports) or on one lane per report."""
+    at most 8192 reports) or on one lane per report."""
     from janus_amd import hpke as G
     rng = np.random.default_rng(n + pub)
     d = H.make_batch(n, share_len, pub, seed=n * 7 + pub, extensions=ext)
