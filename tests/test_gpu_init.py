@@ -211,3 +211,40 @@ def test_taskprov_task_and_wide_segment_fallback():
                                    d2["enc"], d2["ct"], d2["ct_len"], d2["leader_prep_shares"],
                                    seg, None, 1025)
     _check(got, _expected(o, vk, d2, skR, pkR, task, seg, None, 1025))
+
+
+def test_sealed_jobs_on_an_engine_over_two_executors():
+    """The one-call helper init on an engine over the device list [0, 0] (two executors standing
+    in for two GPUs, prio3_engine_create_devices): 16 concurrent sealed-input jobs are placed on
+    both members, each opens its input shares on the member that runs it (the opener is bound to
+    GPU 0 only for its own stream), and every job equals OpenSSL + the restatement."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from janus_amd import hpke as G
+    from janus_amd import prio3 as J
+    from oracle import hpke as H
+    from oracle.oracle import Oracle
+    cfg = CONFIGS["hist_256_c16"]
+    o = Oracle(**cfg)
+    rng = np.random.default_rng(61)
+    vk = bytes([0x3C]) * 16
+    skR = H.kem_private(rng)
+    pkR = H.kem_public(skR)
+    task = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+    eng = J.HelperEngine(J.Prio3Histogram(256, 16), vk, devices=[0, 0])
+    op = G.HpkeOpener(skR, pkR, device=0)
+    m0 = eng.members()
+    jobs = [_sealed_job(o, vk, int(rng.integers(100, 400)), 1500 + j, pkR, task, rng,
+                        tamper=j % 2 == 0) for j in range(16)]
+
+    def run(d):
+        return eng.aggregate_init_batch(op, task, d["nonces"], d["times"], d["public_shares"],
+                                        d["enc"], d["ct"], d["ct_len"], d["leader_prep_shares"])
+
+    with ThreadPoolExecutor(16) as ex:
+        got = list(ex.map(run, jobs))
+    m1 = eng.members()
+    placed = [m["jobs"] - a["jobs"] for m, a in zip(m1, m0)]
+    assert sum(placed) == 16 and min(placed) > 0, placed
+    for d, g in zip(jobs, got):
+        _check(g, _expected(o, vk, d, skR, pkR, task))
