@@ -532,6 +532,7 @@ def secondary_lines(args) -> dict:
             out[key] = dict(metric=j["metric"], value=j["value"], unit=j["unit"],
                             ms_per_step=j["ms_per_step"], config=j["config"],
                             coalescing=j["coalescing"], placement=j.get("placement"),
+                            host=j.get("host"),
                             two_call=j.get("two_call"),
                             roofline={k: j["roofline"][k] for k in ("bound", "achieved", "peak",
                                                                     "unit", "frac")},
@@ -655,6 +656,33 @@ def _placement(engines, before=None):
     return tot
 
 
+def _host_timed(fn):
+    """fn()'s elapsed seconds (as fn returns them) and the host side of it: CPU seconds of this
+    process over the call, and how often / how long the container's CPU quota (cgroup v2
+    cpu.stat) throttled it meanwhile -- on the GPU box a 16-CPU quota throttles the whole process
+    for up to the rest of a 100 ms period, which shows up as a 12-30 ms stall of a jobs line."""
+    import resource
+
+    def cg():
+        try:
+            d = dict(ln.split() for ln in open("/sys/fs/cgroup/cpu.stat"))
+            return int(d["nr_throttled"]), int(d["throttled_usec"])
+        except (OSError, KeyError, ValueError):
+            return None
+
+    def cpu():
+        r = resource.getrusage(resource.RUSAGE_SELF)
+        return r.ru_utime + r.ru_stime
+
+    c0, g0 = cpu(), cg()
+    dt = fn()
+    c1, g1 = cpu(), cg()
+    host = dict(cpu_seconds=c1 - c0, cpus_busy=(c1 - c0) / dt if dt > 0 else None)
+    if g0 and g1:
+        host.update(cgroup_throttled=g1[0] - g0[0], cgroup_throttled_ms=(g1[1] - g0[1]) / 1e3)
+    return dt, host
+
+
 def _job_windows(t, n_jobs, K, js, pool):
     """The report indices (into the concatenated per-task pools) of task t's jobs, and the job
     numbers, as the native drivers choose them (jobs_driver.cpp)."""
@@ -709,7 +737,7 @@ def jobs_line(T, js, n_jobs, K, opts=(), combined=True, with_cpu=True, check_tas
         e.set_option("timing", 2)
         e.timing_reset()
     pl0 = _placement(engines)
-    dt = run(n_jobs)
+    dt, host_side = _host_timed(lambda: run(n_jobs))
     placement = _placement(engines, pl0)
     if dt < 0:
         raise RuntimeError("janus_jobs_run: a C-ABI call failed")
@@ -776,6 +804,7 @@ def jobs_line(T, js, n_jobs, K, opts=(), combined=True, with_cpu=True, check_tas
                              note="measured link: 55-57 GB/s for 16-64 MB pinned copies and kernel "
                                   "reads of mapped host memory (tools/ubench_h2d.hip, "
                                   "profiles/r03/r03i_h2d.txt)", traffic=None),
+               host=host_side,
                coalescing=dict(launches=launches, jobs=n_jobs,
                                mean_reports_per_launch=n_jobs * js / max(launches, 1)),
                call=("prio3_helper_prepare_aggregate_batch (one coalesced launch per group)"
@@ -845,7 +874,7 @@ def leader_jobs_line(T, js, n_jobs, K, devices=None, with_cpu=True, cpu_seconds=
     g0 = [engines[0].executor_stats(k)["groups"] for k in (J.EXEC_LEADER_INIT,
                                                           J.EXEC_LEADER_NEXT)]
     pl0 = _placement(engines)
-    dt = run(n_jobs)
+    dt, host_side = _host_timed(lambda: run(n_jobs))
     if dt < 0:
         raise RuntimeError("janus_jobs_run_leader: a C-ABI call failed")
     placement = _placement(engines, pl0)
@@ -897,7 +926,8 @@ def leader_jobs_line(T, js, n_jobs, K, devices=None, with_cpu=True, cpu_seconds=
                               unit="GB/s host->device (leader input share, nonce, public share, "
                                    "prepare message per report)",
                               frac=value * h2d / 63e9, h2d_bytes_per_report=h2d, traffic=None),
-                coalescing=dict(init_launches=g1[0] - g0[0], next_launches=g1[1] - g0[1],
+                host=host_side,
+               coalescing=dict(init_launches=g1[0] - g0[0], next_launches=g1[1] - g0[1],
                                 jobs=n_jobs),
                 call=("prio3_leader_prepare_init_batch + prio3_leader_prepare_next_aggregate_batch"
                       if combined else "prio3_leader_prepare_init_batch + "
@@ -949,7 +979,7 @@ def hpke_jobs_line(T, js, n_jobs, K, with_cpu=True, cpu_seconds=10.0, heavy=0):
 
     run(max(K, min(n_jobs, 8 * T)))  # warmup
     g0 = op.executor_stats()["groups"]
-    dt = run(n_jobs)
+    dt, host_side = _host_timed(lambda: run(n_jobs))
     if dt < 0:
         raise RuntimeError("janus_jobs_run_hpke: a C-ABI call failed")
     launches = op.executor_stats()["groups"] - g0
@@ -993,7 +1023,8 @@ def hpke_jobs_line(T, js, n_jobs, K, with_cpu=True, cpu_seconds=10.0, heavy=0):
                                      "decap + HPKE key schedule + AES-128-GCM + PlaintextInputShare "
                                      "decode, Prio3Histogram(256,16) shares, host buffers",
                             job_size=js, jobs=n_jobs, threads=T, tasks=K),
-                roofline=roofline, coalescing=dict(launches=launches, jobs=n_jobs),
+                roofline=roofline, host=host_side,
+                coalescing=dict(launches=launches, jobs=n_jobs),
                 checks=dict(all_opened=bool((status == 0).all()), every_job_matches_cpu=ok,
                             jobs_checked=n_jobs, check_seconds=t_chk),
                 cpu_baseline=cpu, speedup_vs_cpu=(value / cpu["value"]) if cpu else None)
@@ -1093,7 +1124,7 @@ def init_jobs_line(T, js, n_jobs, K, with_cpu=True, cpu_seconds=10.0, heavy=0, t
 
     run(max(K, min(n_jobs, 8 * T)), True)  # warmup: pools, pinned staging, streams
     g0 = engines[0].executor_stats(J.EXEC_PREPARE)["groups"]
-    dt = run(n_jobs, True)
+    dt, host_side = _host_timed(lambda: run(n_jobs, True))
     if dt < 0:
         raise RuntimeError("janus_jobs_run_init: a C-ABI call failed")
     launches = engines[0].executor_stats(J.EXEC_PREPARE)["groups"] - g0
@@ -1144,7 +1175,8 @@ def init_jobs_line(T, js, n_jobs, K, with_cpu=True, cpu_seconds=10.0, heavy=0, t
                               unit="GB/s host->device (report ID, time, public share, HPKE "
                                    "ciphertext, leader prep share per report)",
                               frac=value * h2d / 63e9, h2d_bytes_per_report=h2d, traffic=None),
-                coalescing=dict(launches=launches, jobs=n_jobs,
+                host=host_side,
+               coalescing=dict(launches=launches, jobs=n_jobs,
                                 mean_reports_per_launch=n_jobs * js / max(launches, 1)),
                 call="prio3_helper_aggregate_init_batch (one coalesced launch per group)",
                 two_call=two,

@@ -409,20 +409,11 @@ constexpr size_t LEADER_STAGING_TARGET = (size_t)JANUS_LEADER_STAGING_MB << 20;
 struct StagingPool {
   std::mutex mu;
   std::vector<Staging> idle;
+  bool refilling = false;  // a spare is being allocated off the caller's path
 };
 StagingPool* g_staging = new StagingPool[MAX_DEVICES];  // never destroyed (see Exec)
 
-Staging staging_get(int dev, size_t bytes) {
-  {
-    std::lock_guard<std::mutex> lk(g_staging[dev].mu);
-    auto& v = g_staging[dev].idle;
-    for (size_t i = 0; i < v.size(); i++)
-      if (v[i].bytes >= bytes) {
-        Staging s = v[i];
-        v.erase(v.begin() + (long)i);
-        return s;
-      }
-  }
+Staging staging_alloc(int dev, size_t bytes) {
   Staging s;
   s.bytes = std::max(bytes, STAGING_TARGET);
   // pinned host memory of the GPU's own NUMA node: hipHostMalloc takes it from the pool of the
@@ -436,6 +427,57 @@ Staging staging_get(int dev, size_t bytes) {
     staging_free(s);
   }
   return s;
+}
+
+// Takes an idle staging of at least `bytes`, or allocates one.  The executor calls this with its
+// lock held when it opens a group, and a 96 MB hipHostMalloc takes ~13 ms: every job of the GPU
+// then waited for it (r06q: a 12.8 ms gap in the 128-thread line, 36.0 -> 28.8 M reports/s).  So
+// whenever the pool runs dry a spare of the same size is allocated on a thread of its own, and the
+// next group finds it ready.
+Staging staging_get(int dev, size_t bytes) {
+  Staging s;
+  size_t refill = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_staging[dev].mu);
+    auto& v = g_staging[dev].idle;
+    for (size_t i = 0; i < v.size(); i++)
+      if (v[i].bytes >= bytes) {
+        s = v[i];
+        v.erase(v.begin() + (long)i);
+        break;
+      }
+    if (v.empty() && !g_staging[dev].refilling && !g_queues_closing) {
+      g_staging[dev].refilling = true;
+      refill = std::max(bytes, STAGING_TARGET);
+    }
+  }
+  if (refill) {
+    // a process that exits right after a job waits for a spare still being allocated (at most
+    // 2 s), before the HIP runtime's own teardown (an exit handler registered after the runtime's
+    // runs first)
+    static std::once_flag once;
+    std::call_once(once, [] {
+      std::atexit([] {
+        for (int i = 0; i < 2000; i++) {
+          bool busy = false;
+          for (int d = 0; d < MAX_DEVICES; d++) {
+            std::lock_guard<std::mutex> lk(g_staging[d].mu);
+            busy |= g_staging[d].refilling;
+          }
+          if (!busy) return;
+          std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        }
+      });
+    });
+    std::thread([dev, refill] {
+      pin_to_gpu_node(dev);
+      Staging r = g_queues_closing ? Staging() : staging_alloc(dev, refill);
+      std::lock_guard<std::mutex> lk(g_staging[dev].mu);
+      if (r.p) g_staging[dev].idle.push_back(r);
+      g_staging[dev].refilling = false;
+    }).detach();
+  }
+  return s.p ? s : staging_alloc(dev, bytes);
 }
 
 void staging_put(int dev, Staging s) {
@@ -464,6 +506,14 @@ constexpr uint64_t HEAVY_DEFAULT = 32768;
 #define JANUS_HEAVY_OWN_QUEUE 1
 #endif
 constexpr bool HEAVY_OWN_QUEUE = JANUS_HEAVY_OWN_QUEUE != 0;
+// JANUS_COHORT_CAP=0 (A/B): no cap on a heavy-load group's share of the jobs (Exec::cohort_full)
+bool cohort_cap() {
+  static const bool v = [] {
+    const char* s = getenv("JANUS_COHORT_CAP");
+    return !(s && atoi(s) == 0);
+  }();
+  return v;
+}
 
 // JANUS_EXEC_TRACE=<path>: one line per launched group (microseconds: created, taken by the
 // launcher, writers done, launch returned; jobs; reports), for tuning the executor
@@ -566,6 +616,14 @@ struct Exec {
   // cohorts the callers of the finished group leave submit for a moment, and a handover there
   // cost the 128-thread line 10 %, r04z6).
   bool light() const { return stats.active_reports < heavy_at; }
+  // Heavy load runs two cohorts of callers in turn: while one group runs, the callers it released
+  // last fill the next.  Their sizes are whatever the start-up or a late caller made them, and they
+  // persist: 41 / 87 jobs of the 128-thread line ran at 33.5 M reports/s, 58 / 68 at 37.6 (r06r).
+  // A group open under heavy load takes at most about half the jobs inside submit, so a cohort
+  // that is too big spills into the next group, which the other cohort then joins.
+  bool cohort_full(const Group* g) const {
+    return cohort_cap() && !light() && 2 * (uint64_t)g->njobs >= stats.active_jobs + 4;
+  }
   bool lighter() const { return stats.active_reports < heavy_at / 3; }
 
   // Heavy load: one group on the GPU at a time.  While it runs, the launcher polls it; once its
@@ -733,7 +791,7 @@ struct Exec {
     for (;;) {
       auto it = open.find(key);
       g = it == open.end() ? nullptr : it->second;
-      if (g && P::reserve(g->st, job)) break;
+      if (g && !cohort_full(g) && P::reserve(g->st, job)) break;
       if (g) {  // full: it stays queued for the launcher as it is
         g->closed = true;
         open.erase(it);
