@@ -670,14 +670,13 @@ def _host_timed(fn):
         except (OSError, KeyError, ValueError):
             return None
 
-    def cpu():
-        r = resource.getrusage(resource.RUSAGE_SELF)
-        return r.ru_utime + r.ru_stime
-
-    c0, g0 = cpu(), cg()
+    r0, g0 = resource.getrusage(resource.RUSAGE_SELF), cg()
     dt = fn()
-    c1, g1 = cpu(), cg()
-    host = dict(cpu_seconds=c1 - c0, cpus_busy=(c1 - c0) / dt if dt > 0 else None)
+    r1, g1 = resource.getrusage(resource.RUSAGE_SELF), cg()
+    c = (r1.ru_utime - r0.ru_utime) + (r1.ru_stime - r0.ru_stime)
+    host = dict(cpu_seconds=c, sys_seconds=r1.ru_stime - r0.ru_stime,
+                cpus_busy=c / dt if dt > 0 else None,
+                ctx_switches=(r1.ru_nvcsw - r0.ru_nvcsw) + (r1.ru_nivcsw - r0.ru_nivcsw))
     if g0 and g1:
         host.update(cgroup_throttled=g1[0] - g0[0], cgroup_throttled_ms=(g1[1] - g0[1]) / 1e3)
     return dt, host

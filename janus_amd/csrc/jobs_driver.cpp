@@ -10,8 +10,10 @@
 // Not part of the engine: a separate library (libjanus_jobs.so) that links libjanus_prio3.so.
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -25,11 +27,18 @@ namespace {
 // creation and first scheduling of 128 threads (which added 4-9 ms to a ~55 ms region, r06o).
 template <class F>
 double run_pool(int threads, int jobs, F job) {
-  std::atomic<int> next{0}, failed{0}, ready{0};
-  std::atomic<bool> go{false};
+  std::atomic<int> next{0}, failed{0};
+  std::mutex mu;
+  std::condition_variable cv;
+  int ready = 0;
+  bool go = false;
   auto worker = [&]() {
-    ready.fetch_add(1);
-    while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+    {  // parked without spinning: 128 yielding threads burnt CPU quota (a 16-CPU cgroup on the
+       // GPU box throttles the whole process once it is used up)
+      std::unique_lock<std::mutex> lk(mu);
+      if (++ready == threads) cv.notify_all();
+      cv.wait(lk, [&] { return go; });
+    }
     for (;;) {
       const int j = next.fetch_add(1);
       if (j >= jobs) return;
@@ -38,9 +47,14 @@ double run_pool(int threads, int jobs, F job) {
   };
   std::vector<std::thread> th;
   for (int i = 0; i < threads; i++) th.emplace_back(worker);
-  while (ready.load() < threads) std::this_thread::yield();
-  const auto t0 = std::chrono::steady_clock::now();
-  go.store(true, std::memory_order_release);
+  std::chrono::steady_clock::time_point t0;
+  {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return ready == threads; });
+    go = true;
+    t0 = std::chrono::steady_clock::now();
+  }
+  cv.notify_all();
   for (auto& t : th) t.join();
   const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return failed ? -1.0 : dt;
