@@ -682,6 +682,16 @@ def _host_timed(fn):
     return dt, host
 
 
+def _warm(*arrays):
+    """Writes the jobs lines' output arrays once before the clock: np.zeros maps zero pages lazily,
+    so the first job to write each 4 KB page took a fault inside the timed region (the leader
+    line's 1.2 GB of prepare shares: 1.1-1.9 s of system time per run, which pushed the process
+    over the GPU box's 16-CPU quota), where a Janus worker writes into buffers its allocator has
+    long mapped."""
+    for a in arrays:
+        a.fill(0)
+
+
 def _job_windows(t, n_jobs, K, js, pool):
     """The report indices (into the concatenated per-task pools) of task t's jobs, and the job
     numbers, as the native drivers choose them (jobs_driver.cpp)."""
@@ -722,6 +732,7 @@ def jobs_line(T, js, n_jobs, K, opts=(), combined=True, with_cpu=True, check_tas
     status = np.zeros(n_jobs * js, np.uint8)
     counts = np.zeros(n_jobs, np.uint64)
     agg = np.zeros((n_jobs, sz.agg_share_len), np.uint8)
+    _warm(status, counts, agg)
     P = lambda a: a.ctypes.data_as(vp)
 
     def run(jobs):
@@ -860,6 +871,7 @@ def leader_jobs_line(T, js, n_jobs, K, devices=None, with_cpu=True, cpu_seconds=
     status = np.zeros(n_jobs * js, np.uint8)
     counts = np.zeros(n_jobs, np.uint64)
     agg = np.zeros((n_jobs, sz.agg_share_len), np.uint8)
+    _warm(ps, status, counts, agg)
     P = lambda a: a.ctypes.data_as(vp)
 
     def run(jobs):
@@ -967,6 +979,7 @@ def hpke_jobs_line(T, js, n_jobs, K, with_cpu=True, cpu_seconds=10.0, heavy=0):
                                         vp, vp, u32, vp, vp, vp, u32, u32, vp, vp]
     shares = np.zeros((n_jobs * js, 48), np.uint8)
     status = np.zeros(n_jobs * js, np.uint8)
+    _warm(shares, status)
     P = lambda a: a.ctypes.data_as(vp)
 
     def run(jobs):
@@ -1082,6 +1095,7 @@ def init_jobs_line(T, js, n_jobs, K, with_cpu=True, cpu_seconds=10.0, heavy=0, t
     status = np.zeros(n_jobs * js, np.uint8)
     counts = np.zeros(n_jobs, np.uint64)
     agg = np.zeros((n_jobs, sz.agg_share_len), np.uint8)
+    _warm(status, counts, agg)
     P = lambda a: a.ctypes.data_as(vp)
 
     def run(jobs, one_call):
