@@ -40,6 +40,7 @@
 #include <emmintrin.h>
 #include <pthread.h>
 #include <sched.h>
+#include <sys/mman.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -391,10 +392,17 @@ struct Staging {
   uint8_t* dev = nullptr;  // the same bytes as the device addresses them (kernels read per-report
                            // inputs straight from here and write outputs back: engine_group_issue)
   size_t bytes = 0;
+  void* map = nullptr;  // huge-page staging: the mapping (hipHostRegister'ed at p) and its length
+  size_t map_bytes = 0;
 };
 
 void staging_free(Staging& s) {
-  if (s.p) (void)hipHostFree(s.p);
+  if (s.map) {
+    (void)hipHostUnregister(s.p);
+    munmap(s.map, s.map_bytes);
+  } else if (s.p) {
+    (void)hipHostFree(s.p);
+  }
   s = Staging();
 }
 
@@ -413,7 +421,57 @@ struct StagingPool {
 };
 StagingPool* g_staging = new StagingPool[MAX_DEVICES];  // never destroyed (see Exec)
 
+// JANUS_STAGING_HUGE=0 (A/B): the staging from hipHostMalloc (4 KB pages) instead
+bool staging_huge() {
+  static const bool v = [] {
+    const char* e = getenv("JANUS_STAGING_HUGE");
+    return !(e && atoi(e) == 0);
+  }();
+  return v;
+}
+
+// Pinned staging on 2 MB pages: an anonymous mapping on 2 MB boundaries with MADV_HUGEPAGE, bound
+// to the GPU's NUMA node, faulted in, then registered with the GPU (mapped).  The leader's staging
+// writes each report's 5.6 KB share transposed into [cell][report] form, one 16-byte cell into
+// each of 352 rows ~1.5 MB apart: on 4 KB pages every cell is a TLB miss.  On the GPU box 16
+// threads transposed 97 GB/s into 2 MB pages against 50 GB/s into 4 KB ones, and copied 113
+// against 85 GB/s (tools/ubench_staging.cpp, profiles/r06/jobs/r06aa/).
+Staging staging_alloc_huge(int dev, size_t bytes) {
+  constexpr size_t H = (size_t)2 << 20;
+  Staging s;
+  s.bytes = (std::max(bytes, STAGING_TARGET) + H - 1) & ~(H - 1);
+  s.map_bytes = s.bytes + H;
+  void* m = mmap(nullptr, s.map_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (m == MAP_FAILED) return Staging();
+  s.map = m;
+  s.p = (uint8_t*)(((uintptr_t)m + H - 1) & ~(uintptr_t)(H - 1));
+  (void)madvise(s.p, s.bytes, MADV_HUGEPAGE);
+  const int node = gpu_numa_node(dev);
+  if (node >= 0 && node < 64) {  // MPOL_PREFERRED: the GPU's node first, any node if it is full
+    const unsigned long mask = 1UL << node;
+    (void)syscall(SYS_mbind, s.p, s.bytes, 1 /* MPOL_PREFERRED */, &mask, 64UL, 0U);
+  }
+  memset(s.p, 0, s.bytes);
+  DeviceGuard dg(dev);
+  const bool ok = dg.rc == hipSuccess &&
+                  hipHostRegister(s.p, s.bytes, hipHostRegisterMapped) == hipSuccess;
+  if (!ok) {
+    (void)hipGetLastError();
+    munmap(s.map, s.map_bytes);
+    return Staging();
+  }
+  if (hipHostGetDevicePointer((void**)&s.dev, s.p, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    staging_free(s);
+  }
+  return s;
+}
+
 Staging staging_alloc(int dev, size_t bytes) {
+  if (staging_huge()) {
+    Staging h = staging_alloc_huge(dev, bytes);
+    if (h.p) return h;
+  }
   Staging s;
   s.bytes = std::max(bytes, STAGING_TARGET);
   // pinned host memory of the GPU's own NUMA node: hipHostMalloc takes it from the pool of the
@@ -531,6 +589,36 @@ double exec_us(std::chrono::steady_clock::time_point t) {
 }
 double ns_since(std::chrono::steady_clock::time_point t) {
   return std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - t).count();
+}
+
+// JANUS_HOST_CPU=1: the job threads' CPU time in staging and unstaging per executor kind, printed
+// to stderr at exit (where the jobs lines' host CPU goes)
+bool host_cpu_on() {
+  static const bool v = getenv("JANUS_HOST_CPU") != nullptr;
+  return v;
+}
+double host_cpu_ns() {
+  if (!host_cpu_on()) return 0;
+  timespec t;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &t);
+  return t.tv_sec * 1e9 + t.tv_nsec;
+}
+std::atomic<uint64_t> g_host_cpu[8][3];  // per kind: stage ns, unstage ns, jobs
+void host_cpu_add(int kind, double stage_ns, double unstage_ns) {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    std::atexit([] {
+      static const char* names[] = {"prepare", "accumulate", "leader", "leader_next", "hpke"};
+      for (int k = 0; k < 5; k++)
+        if (const uint64_t n = g_host_cpu[k][2])
+          fprintf(stderr, "janus host cpu: %s jobs %lu stage %.3f s unstage %.3f s (%.1f / %.1f us per job)\n",
+                  names[k], (unsigned long)n, g_host_cpu[k][0] / 1e9, g_host_cpu[k][1] / 1e9,
+                  g_host_cpu[k][0] / 1e3 / n, g_host_cpu[k][1] / 1e3 / n);
+    });
+  });
+  g_host_cpu[kind][0] += (uint64_t)stage_ns;
+  g_host_cpu[kind][1] += (uint64_t)unstage_ns;
+  g_host_cpu[kind][2] += 1;
 }
 
 template <class P>
@@ -819,13 +907,17 @@ struct Exec {
     g->readers++;
     g->njobs++;
     lk.unlock();
+    const double c0 = host_cpu_ns();
     P::stage(g->st, g->stg, job);
+    const double c1 = host_cpu_ns();
     lk.lock();
     if (--g->writers == 0) g->cv.notify_all();
     while (!g->done) g->cv.wait(lk);
     const int rc = g->rc;
     lk.unlock();
+    const double c2 = host_cpu_ns();
     if (rc == PRIO3_OK) P::unstage(g->st, g->stg, job);
+    if (host_cpu_on()) host_cpu_add(P::kind, c1 - c0, host_cpu_ns() - c2);
     lk.lock();
     if (--g->readers == 0) {
       staging_put(device, g->stg);
@@ -899,6 +991,7 @@ void stream_transpose16(uint8_t* dst, size_t cap, size_t c0, const uint8_t* src,
 
 // ---- prepare groups ----
 struct PrepPolicy {
+  static constexpr int kind = 0;
   typedef ExecJob Job;
   static uint64_t heavy_default() { return HEAVY_DEFAULT; }
   struct State {
@@ -1056,6 +1149,7 @@ struct PrepPolicy {
 
 // ---- accumulate groups ----
 struct AccPolicy {
+  static constexpr int kind = 1;
   typedef AccJob Job;
   static uint64_t heavy_default() { return HEAVY_DEFAULT; }
   static constexpr uint32_t MAX_JOBS = 1024, MAX_REPS = 1u << 17;
@@ -1100,6 +1194,7 @@ struct AccPolicy {
 
 // ---- leader prepare_init groups ----
 struct LeaderPolicy {
+  static constexpr int kind = 2;
   typedef LeaderJob Job;
   static uint64_t heavy_default() { return HEAVY_DEFAULT; }
   struct State {
@@ -1172,6 +1267,7 @@ struct LeaderPolicy {
 
 // ---- leader prepare_next groups ----
 struct LNextPolicy {
+  static constexpr int kind = 3;
   typedef LNextJob Job;
   static uint64_t heavy_default() { return HEAVY_DEFAULT; }
   struct State {
@@ -1229,6 +1325,7 @@ struct LNextPolicy {
 
 // ---- HPKE open groups ----
 struct HpkePolicy {
+  static constexpr int kind = 4;
   typedef HpkeJob Job;
   // never the heavy-load launcher: one wave's HPKE open is a long dependent chain, so a group
   // takes about as long at 31k reports as at 62k, and the light-load pipeline's concurrent groups

@@ -10,6 +10,7 @@
 #include <thread>
 #include <pthread.h>
 #include <sched.h>
+#include <sys/mman.h>
 #include <vector>
 #include <algorithm>
 static void stream_copy(uint8_t* dst, const uint8_t* src, size_t n) {
@@ -79,11 +80,24 @@ __attribute__((target("avx512f"))) static void tr512(uint8_t* dst, size_t cap, s
                        _mm_loadu_si128((const __m128i*)(src + row * r + 16 * (size_t)e)));
   _mm_sfence();
 }
+// variant: plain (cached) 16-byte stores
+static void tr_cached(uint8_t* dst, size_t cap, size_t c0, const uint8_t* src, uint32_t n, uint32_t cells) {
+  const size_t row = 16 * (size_t)cells;
+  for (uint32_t r0 = 0; r0 < n; r0 += 8) {
+    const uint32_t k = std::min(8u, n - r0);
+    const uint8_t* s0 = src + row * r0;
+    for (uint32_t e = 0; e < cells; e++) {
+      __m128i* d = (__m128i*)(dst + 16 * (e * cap + c0 + r0));
+      for (uint32_t i = 0; i < k; i++) _mm_storeu_si128(d + i, _mm_loadu_si128((const __m128i*)(s0 + row * i + 16 * (size_t)e)));
+    }
+  }
+}
 int main(int argc, char** argv) {
   int mode = atoi(argv[1]), T = atoi(argv[2]);
   // PIN (argv[3]): 0 none; 1 main and workers on CPUs 0.. (one socket, where the data is touched);
   // 2 workers alternate between CPUs 0.. and 64.. (half of them on the other socket)
   const int pin = argc > 3 ? atoi(argv[3]) : 0;
+  const int huge = argc > 4 ? atoi(argv[4]) : 0;  // 1: destination on transparent 2 MB pages
   auto pin_to = [](int cpu) {
     cpu_set_t cs; CPU_ZERO(&cs); CPU_SET(cpu, &cs); pthread_setaffinity_np(pthread_self(), sizeof(cs), &cs);
   };
@@ -91,7 +105,12 @@ int main(int argc, char** argv) {
   const uint32_t cells = 352, js = 500, pool = 4 * 32768; const size_t row = 16 * cells;
   std::vector<uint8_t> src((size_t)pool * row); for (size_t i = 0; i < src.size(); i += 4096) src[i] = i;
   const uint32_t cap = 16384; std::vector<uint8_t*> dst(T);
-  for (int t = 0; t < T; t++) { dst[t] = (uint8_t*)aligned_alloc(4096, (size_t)cap * row); memset(dst[t], 0, (size_t)cap * row); }
+  for (int t = 0; t < T; t++) {
+    const size_t bytes = ((size_t)cap * row + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+    dst[t] = (uint8_t*)aligned_alloc(2u << 20, bytes);
+    if (huge) madvise(dst[t], bytes, MADV_HUGEPAGE);
+    memset(dst[t], 0, bytes);
+  }
   if (mode == 9) {  // tr512 against tr on odd shapes
     for (uint32_t n : {500u, 503u, 1u, 7u}) for (uint32_t cl : {352u, 351u, 5u}) {
       const size_t rw = 16 * (size_t)cl;
@@ -105,6 +124,12 @@ int main(int argc, char** argv) {
     return 0;
   }
   const int jobs_per_thread = 64;
+  if (FILE* f = fopen("/proc/self/smaps_rollup", "r")) {  // did the destination get 2 MB pages?
+    char ln[256];
+    while (fgets(ln, sizeof ln, f))
+      if (!strncmp(ln, "AnonHugePages", 13)) fprintf(stderr, "%s", ln);
+    fclose(f);
+  }
   auto t0 = std::chrono::steady_clock::now();
   std::vector<std::thread> th;
   for (int t = 0; t < T; t++) th.emplace_back([&, t] {
@@ -114,12 +139,13 @@ int main(int argc, char** argv) {
       if (mode == 0) stream_copy(dst[t] + (size_t)c0 * row, src.data() + r0 * row, (size_t)js * row);
       else if (mode == 1) tr(dst[t], cap, c0, src.data() + r0 * row, js, cells);
       else if (mode == 2) tr16(dst[t], cap, c0, src.data() + r0 * row, js, cells);
-      else tr512(dst[t], cap, c0, src.data() + r0 * row, js, cells);
+      else if (mode == 3) tr512(dst[t], cap, c0, src.data() + r0 * row, js, cells);
+      else tr_cached(dst[t], cap, c0, src.data() + r0 * row, js, cells);
     }
   });
   for (auto& x : th) x.join();
   double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   double gb = (double)T * jobs_per_thread * js * row / 1e9;
-  printf("pin %d mode %d T %d: %.2f GB in %.3f s = %.2f GB/s total, %.2f GB/s per thread\n", pin, mode, T, gb, dt, gb / dt, gb / dt / T);
+  printf("huge %d pin %d mode %d T %d: %.2f GB in %.3f s = %.2f GB/s total, %.2f GB/s per thread\n", huge, pin, mode, T, gb, dt, gb / dt, gb / dt / T);
   (void)pin;
 }
