@@ -515,8 +515,10 @@ def secondary_lines(args) -> dict:
     for key, fn in (("secondary_jobs", lambda: jobs_line(128, 500, (1 << 21) // 500, 4,
                                                          cpu_seconds=cs)),
                     ("secondary_jobs_16t", lambda: jobs_line(16, 500, 2048, 4, cpu_seconds=cs)),
-                    ("secondary_jobs_leader", lambda: leader_jobs_line(128, 500, 2048, 4,
-                                                                       cpu_seconds=cs)),
+                    # (the leader line at 2 Mi reports too: at 1 Mi its 66 groups are a third
+                    # ramp, r06ae: 5.7 against 5.8-7.5 M/s at 2 Mi)
+                    ("secondary_jobs_leader", lambda: leader_jobs_line(128, 500, (1 << 21) // 500,
+                                                                       4, cpu_seconds=cs)),
                     ("secondary_jobs_hpke", lambda: hpke_jobs_line(128, 500, 2048, 4,
                                                                    cpu_seconds=cs)),
                     # the whole loop body from sealed input shares in one call,
