@@ -248,6 +248,45 @@ def test_combined_prepare_aggregate_jobs(name):
         assert 0 < launches < 32, launches
 
 
+def test_heavy_load_group_takes_at_most_half_the_jobs():
+    """Under heavy load a group takes at most about half the jobs inside the executor
+    (Exec::cohort_full), so the two cohorts of a closed loop of callers stay balanced (DESIGN.md
+    11: 41 / 87 jobs of the 128-thread line ran at 33.5 M reports/s, 58 / 68 at 37.6).  32 jobs
+    queued behind the hold with the heavy-load launcher on from the first job land in at least two
+    groups -- one group would hold them all without the cap -- and every job matches the
+    restatement."""
+    from oracle.oracle import Oracle
+    cfg = CONFIGS["hist_256_c16"]
+    o = Oracle(**cfg)
+    vk = bytes([0x4d]) * 16
+    eng = _engine(cfg, vk)
+    eng.set_option("timing", 1)
+    eng.timing_reset()
+    jobs = [o.gen_reports(vk, 200, seed=700 + j, n_threads=4) for j in range(32)]
+
+    def run(j):
+        d = jobs[j]
+        return eng.prepare_aggregate_batch(d["nonces"], d["public_shares"], d["helper_shares"],
+                                           d["leader_prep_shares"])
+
+    eng.executor_control("heavy", 1)
+    try:
+        with _Held(eng, 32) as held, ThreadPoolExecutor(32) as ex:
+            futs = [ex.submit(run, j) for j in range(32)]
+            held.wait()
+            got = [f.result(timeout=120) for f in futs]
+    finally:
+        eng.executor_control("heavy", 0)
+    for d, (msgs, status, agg, cnt) in zip(jobs, got):
+        rm, rs, ra, rc = _ref(o, vk, d)
+        np.testing.assert_array_equal(status, rs)
+        np.testing.assert_array_equal(msgs, rm)
+        np.testing.assert_array_equal(agg, ra)
+        np.testing.assert_array_equal(cnt, rc)
+    launches = sum(eng.timing().get(k, (0, 0))[1] for k in ("k_prep_h", "k_prep_hp"))
+    assert 2 <= launches < 32, launches
+
+
 def test_combined_prepare_aggregate_single_job_and_empty():
     """One combined call alone (the executor launches a lone job at once), with coalescing off
     (the two-call fallback), and an empty job."""
