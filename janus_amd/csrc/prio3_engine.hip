@@ -4087,7 +4087,17 @@ void engine_leader_layout(const prio3_engine* e, uint32_t cap, LeaderLayout* L) 
   off += up(cap);
   L->bytes = off;
   L->cap = cap;
-  L->lin_soa = leader_prep_takes(e);
+  // The executor's leader groups stage the input shares as plain rows, one DMA copies them into
+  // the run, and the next group is issued as soon as that copy is done, so its copy runs under this
+  // group's kernels.  Interleaved on one box (r06ai): 9.24 / 8.57 / 8.76 M reports/s against
+  // 6.97 / 7.31 / 7.58 for the transposed staging read in-kernel (r06), whose
+  // host-side transpose (~870 us of CPU per 500-report job) ran the process into the box's 16-CPU
+  // quota.  JANUS_LEADER_SOA=1 (A/B): the transposed form.
+  static const bool soa = [] {
+    const char* v = getenv("JANUS_LEADER_SOA");
+    return v && atoi(v) != 0;
+  }();
+  L->lin_soa = leader_prep_takes(e) && soa;
 }
 
 // A leader group: the explicit input shares (5.6 KB per Histogram(256) report) go to the run by
@@ -4120,25 +4130,25 @@ int engine_leader_issue(prio3_engine* lead, const LeaderLayout& L, uint8_t* stg,
     ws_exec_stream_put(lead->device, st);
     return code;
   };
-  // k_leader_prep reads the transposed staging itself, each wave load one 1 KiB PCIe read, while
-  // other waves run Keccak and the query (r05's one DMA of the whole group's
-  // 5.6 KB shares ran ahead of the kernels, in series with them); the other leader kernels read
-  // AoS rows from the run
+  // The input shares (5.6 KB per Histogram(256) report) go to the run by one DMA, and the kernels
+  // read AoS rows from HBM.  r05 issued the next group only after this group's kernels, so copy
+  // and kernels ran in series; now the group's 'prepared' event follows the copy (below).  With
+  // lin_soa (A/B) k_leader_prep reads the transposed staging itself instead, each wave load one
+  // 1 KiB PCIe read, and the other leader kernels read AoS rows from the run.
   if (!L.lin_soa &&
       hipMemcpyAsync(R->linput, stg_dev + L.off[2], L.len[2] * n, hipMemcpyDefault, st) !=
           hipSuccess)
     return fail(PRIO3_EDEVICE);
+  // the DMA form: the executor may issue its next group once this group's shares are in HBM, so
+  // the next group's copy runs under this group's kernels (as a sealed group's next goes after
+  // its open)
+  if (!L.lin_soa) record_prep(gr, st);
   rc = leader_init_run(lead, R, stg_dev + L.off[0], L.len[1] ? stg_dev + L.off[1] : nullptr,
                        L.lin_soa ? stg_dev + L.off[2] : R->linput, R->leader, R->status, st,
                        (const uint16_t*)(stg_dev + L.slot_off), (const uint4*)(stg_dev + L.tab_off),
                        L.lin_soa ? L.cap : 0u);
   if (rc) return fail(rc);
-  if (hipEventCreateWithFlags(&gr->prep, hipEventDisableTiming) != hipSuccess ||
-      hipEventRecord(gr->prep, st) != hipSuccess) {
-    (void)hipGetLastError();
-    if (gr->prep) (void)hipEventDestroy(gr->prep);
-    gr->prep = nullptr;
-  }
+  if (!gr->prep) record_prep(gr, st);
   // the prepare shares (560 B per Histogram(256) report, 17 MB per 31k group) go back by the
   // copy engine: written by k_pull into the mapped staging they took 0.88 ms per group (~20 GB/s,
   // r06c kernel trace); the statuses by the copy kernel
