@@ -446,6 +446,9 @@ Staging staging_alloc_huge(int dev, size_t bytes) {
   s.map = m;
   s.p = (uint8_t*)(((uintptr_t)m + H - 1) & ~(uintptr_t)(H - 1));
   (void)madvise(s.p, s.bytes, MADV_HUGEPAGE);
+  // not inherited by a child (a subprocess started after the engine): a copy-on-write share of
+  // the registered pages would make the driver re-validate the mapping when this process writes
+  (void)madvise(s.p, s.bytes, MADV_DONTFORK);
   const int node = gpu_numa_node(dev);
   if (node >= 0 && node < 64) {  // MPOL_PREFERRED: the GPU's node first, any node if it is full
     const unsigned long mask = 1UL << node;

@@ -287,6 +287,31 @@ def test_heavy_load_group_takes_at_most_half_the_jobs():
     assert 2 <= launches < 32, launches
 
 
+def test_jobs_after_a_subprocess_still_match():
+    """The executor's pinned staging (2 MB pages registered with the GPU, MADV_DONTFORK) is not
+    shared copy-on-write with a child process: jobs before and after a subprocess started by
+    this process, on the same pooled staging, all match the restatement."""
+    import subprocess
+    from oracle.oracle import Oracle
+    cfg = CONFIGS["hist_256_c16"]
+    o = Oracle(**cfg)
+    vk = bytes([0x5a]) * 16
+    eng = _engine(cfg, vk)
+    for rnd in range(3):
+        d = o.gen_reports(vk, 300, seed=900 + rnd, n_threads=4)
+        with ThreadPoolExecutor(4) as ex:
+            got = list(ex.map(lambda _: eng.prepare_aggregate_batch(
+                d["nonces"], d["public_shares"], d["helper_shares"], d["leader_prep_shares"]),
+                range(4)))
+        rm, rs, ra, rc = _ref(o, vk, d)
+        for msgs, status, agg, cnt in got:
+            np.testing.assert_array_equal(status, rs)
+            np.testing.assert_array_equal(msgs, rm)
+            np.testing.assert_array_equal(agg, ra)
+            np.testing.assert_array_equal(cnt, rc)
+        subprocess.run(["true"], check=True)
+
+
 def test_combined_prepare_aggregate_single_job_and_empty():
     """One combined call alone (the executor launches a lone job at once), with coalescing off
     (the two-call fallback), and an empty job."""
