@@ -13,6 +13,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -21,42 +22,61 @@
 #include "../../include/janus_prio3.h"
 
 namespace {
-// `threads` workers taking jobs 0..jobs-1 in order; returns elapsed seconds (< 0: a call failed).
-// The workers are started and parked before the clock starts, as Janus's rayon pool exists before
-// any job arrives (aggregator/src/binary_utils.rs:514-518): the timed region is the jobs, not the
-// creation and first scheduling of 128 threads (which added 4-9 ms to a ~55 ms region, r06o).
+// A persistent pool, as Janus's rayon pool is (aggregator/src/binary_utils.rs:514-518): its
+// threads are created by the first call that needs them (the lines' warmup run) and parked on a
+// condition variable between calls, so a timed call neither creates threads nor pays each new
+// thread's first HIP calls.  r06 timed 128 fresh threads per call: their creation added 4-9 ms to
+// a ~55 ms region (r06o), and spinning while parked burnt CPU quota (r06v).
+struct Pool {
+  std::mutex mu;
+  std::condition_variable cv, done;
+  std::function<void()> work;
+  uint64_t gen = 0;
+  int threads = 0, want = 0, active = 0;
+};
+Pool& pool() {
+  static Pool* p = new Pool();  // never destroyed: its threads stay parked until exit
+  return *p;
+}
+
+// `threads` workers taking jobs 0..jobs-1 in order; returns elapsed seconds (< 0: a call failed)
 template <class F>
 double run_pool(int threads, int jobs, F job) {
+  Pool& P = pool();
   std::atomic<int> next{0}, failed{0};
-  std::mutex mu;
-  std::condition_variable cv;
-  int ready = 0;
-  bool go = false;
-  auto worker = [&]() {
-    {  // parked without spinning: 128 yielding threads burnt CPU quota (a 16-CPU cgroup on the
-       // GPU box throttles the whole process once it is used up)
-      std::unique_lock<std::mutex> lk(mu);
-      if (++ready == threads) cv.notify_all();
-      cv.wait(lk, [&] { return go; });
-    }
+  std::unique_lock<std::mutex> lk(P.mu);
+  while (P.threads < threads) {
+    const int idx = P.threads++;
+    std::thread([&P, idx] {
+      uint64_t seen = 0;
+      std::unique_lock<std::mutex> l(P.mu);
+      for (;;) {
+        P.cv.wait(l, [&] { return P.gen != seen; });
+        seen = P.gen;
+        if (idx >= P.want) continue;
+        const std::function<void()> w = P.work;
+        l.unlock();
+        w();
+        l.lock();
+        if (--P.active == 0) P.done.notify_all();
+      }
+    }).detach();
+  }
+  P.work = [&] {
     for (;;) {
       const int j = next.fetch_add(1);
       if (j >= jobs) return;
       if (!job(j)) failed = 1;
     }
   };
-  std::vector<std::thread> th;
-  for (int i = 0; i < threads; i++) th.emplace_back(worker);
-  std::chrono::steady_clock::time_point t0;
-  {
-    std::unique_lock<std::mutex> lk(mu);
-    cv.wait(lk, [&] { return ready == threads; });
-    go = true;
-    t0 = std::chrono::steady_clock::now();
-  }
-  cv.notify_all();
-  for (auto& t : th) t.join();
+  P.want = threads;
+  P.active = threads;
+  P.gen++;
+  const auto t0 = std::chrono::steady_clock::now();
+  P.cv.notify_all();
+  P.done.wait(lk, [&] { return P.active == 0; });
   const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  P.work = nullptr;
   return failed ? -1.0 : dt;
 }
 }  // namespace
